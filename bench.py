@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Headline benchmark: DiFacto FM (embedding dim 64) training throughput on
+Criteo-1TB-shaped sparse data, examples/sec over all GPUs (BASELINE.json).
+
+Config follows the reference's own Criteo DiFacto conf
+(learn/difacto/guide/criteo.conf: minibatch 100000, threshold 100, V lambda_l2
+1, lr_eta .01) with the embedding dim set to 64 as BASELINE.json names.  Data
+is synthetic (13 integer + 26 categorical fields, Criteo-1TB field
+cardinalities, power-law values) generated on the device every step; the
+model is random-initialised.  Every timed step is a full training step:
+generate -> localize -> key all-to-all -> count push (data pass 0) -> pull ->
+FM forward + loss + AUC -> FM backward -> push -> fused FTRL/AdaGrad update.
+
+Weak scaling: each GPU processes its own minibatch of --batch rows per step;
+the keys are sharded over all GPUs (ps-lite server group -> xGMI all-to-all).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model difacto|linear]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from wormhole_amd.config.schema import DifactoConfig, Embedding, LinearConfig  # noqa: E402
+from wormhole_amd.data.synthetic import CRITEO_TB_CARD  # noqa: E402
+from wormhole_amd.parallel.comm import Comm, env_local_rank  # noqa: E402
+
+LINEAR_REF_EX_PER_S = 1.85e6  # linear.dmlc FTRL, Criteo, CPU host
+
+
+def build(args, comm, device):
+    if args.model == "difacto":
+        from wormhole_amd.models.difacto import DifactoLearner
+        emb = Embedding(dim=args.dim, threshold=100, lambda_l2=1.0, lr_eta=0.01)
+        emb._set = {"dim", "threshold", "lambda_l2", "lr_eta"}
+        conf = DifactoConfig(minibatch=args.batch, lr_eta=0.01, embedding=[emb])
+        return DifactoLearner(conf, comm, device, cap=args.cap, vcap=args.vcap, seed=1)
+    from wormhole_amd.models.linear import LinearLearner
+    conf = LinearConfig(minibatch=args.batch, lambda_l1=4.0, lr_eta=0.1)
+    return LinearLearner(conf, comm, device, cap=args.cap, seed=1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="difacto", choices=["difacto", "linear"])
+    ap.add_argument("--batch", type=int, default=100000, help="rows per GPU per step")
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--cap", type=int, default=1 << 27, help="KV slots per GPU shard")
+    ap.add_argument("--vcap", type=int, default=1 << 24, help="embedding rows per shard")
+    args = ap.parse_args()
+
+    local = env_local_rank()
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    comm = Comm(device)
+    n = comm.size
+    learner = build(args, comm, device)
+    card = torch.tensor(CRITEO_TB_CARD, dtype=torch.int64, device=device)
+    from wormhole_amd import _native
+    hip = _native.hip()
+    seed = 1000 + comm.rank
+
+    def one(step):
+        keys, label, offset = hip.synth_criteo(args.batch, seed, step, card)
+        learner.process(keys, offset, None, label, 0, 0)
+
+    for s in range(args.warmup):
+        one(s)
+    torch.cuda.synchronize()
+    comm.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        one(args.warmup + s)
+    torch.cuda.synchronize()
+    comm.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    comm.allreduce(t, "max")
+    dt = float(t.item())
+    prog = learner.take_progress()
+    ex = args.batch * args.steps * n
+    value = ex / dt
+    if args.model == "difacto":
+        metric = "examples/sec, DiFacto FM on Criteo-1TB-shaped sparse at 1/2/4/8 MI355X"
+        vs = None
+        model = "difacto-fm-dim%d" % args.dim
+    else:
+        metric = "examples/sec, linear FTRL logistic regression on Criteo-shaped sparse"
+        vs = value / LINEAR_REF_EX_PER_S
+        model = "linear-ftrl"
+    if comm.rank == 0:
+        nex = max(prog[5], 1.0)
+        print(json.dumps({
+            "metric": metric, "value": value, "unit": "examples/s", "n_gpus": n,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * dt / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": vs, "dtype": "fp32",
+            "data": "synthetic (Criteo-1TB-shaped: 13 int + 26 cat fields, power-law, device-generated each step); random-init model",
+            "config": {"model": model, "global_batch": args.batch * n, "seq_len": 39,
+                       "parallelism": "dp%d+kvshard%d" % (n, n),
+                       "minibatch_per_gpu": args.batch, "threshold": 100, "nnz_per_example": 39},
+            "train_logloss": prog[0] / nex, "train_auc": prog[1] / max(prog[4], 1.0),
+        }), flush=True)
+    comm.finalize()
+
+
+if __name__ == "__main__":
+    main()

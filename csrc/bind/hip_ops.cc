@@ -1,0 +1,407 @@
+// torch / pybind11 binding layer for the gfx950 HIP kernels (module
+// wormhole_amd._hip). Host-only translation unit: validates tensors, sizes
+// outputs and launches on the current PyTorch HIP stream.
+#include <torch/extension.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "hip/wh_kernels.h"
+
+namespace {
+
+using torch::Tensor;
+
+inline hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONT(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype ", (t).scalar_type())
+#define CHECK_IN(t, dt) \
+  CHECK_DEV(t);         \
+  CHECK_CONT(t);        \
+  CHECK_DT(t, dt)
+
+template <typename T>
+T* ptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+
+template <typename T>
+const T* optptr(const c10::optional<Tensor>& t) {
+  return (t.has_value() && t->defined() && t->numel() > 0) ? reinterpret_cast<const T*>(t->data_ptr())
+                                                           : nullptr;
+}
+
+inline int64_t next_pow2(int64_t x) {
+  int64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// ------------------------------------------------------------------ scan
+Tensor scan_excl(const Tensor& in) {
+  CHECK_DEV(in); CHECK_CONT(in);
+  c10::DeviceGuard g(in.device());
+  const int64_t n = in.numel();
+  auto o = torch::empty({n + 1}, in.options().dtype(torch::kInt64));
+  auto tmp = torch::empty({wh::scan_tmp_elems(n)}, in.options().dtype(torch::kInt64));
+  if (in.scalar_type() == torch::kInt32)
+    wh::scan_i32(ptr<int32_t>(in), ptr<int64_t>(o), n, ptr<int64_t>(tmp), cur_stream(in));
+  else {
+    CHECK_DT(in, torch::kInt64);
+    wh::scan_i64(ptr<int64_t>(in), ptr<int64_t>(o), n, ptr<int64_t>(tmp), cur_stream(in));
+  }
+  return o;
+}
+
+// -------------------------------------------------------------- localize
+// Returns (uniq i64[U], ucnt i32[U], owner_cnt i64[P], lid i32[nnz],
+//          csc_off i64[U+1], csc_row i32[nnz], csc_val f32[nnz|0])
+std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
+                             const c10::optional<Tensor>& val, int64_t nshard) {
+  CHECK_IN(keys, torch::kInt64);
+  CHECK_IN(offset, torch::kInt64);
+  TORCH_CHECK(nshard >= 1 && nshard <= 1024, "nshard out of range");
+  c10::DeviceGuard g(keys.device());
+  auto s = cur_stream(keys);
+  const int64_t nnz = keys.numel();
+  const int64_t nrows = offset.numel() - 1;
+  TORCH_CHECK(nnz < (int64_t)INT32_MAX, "minibatch too large for int32 local ids");
+  const float* vp = optptr<float>(val);
+  if (vp) { CHECK_IN((*val), torch::kFloat32); TORCH_CHECK(val->numel() == nnz); }
+  auto i32 = keys.options().dtype(torch::kInt32);
+  auto i64 = keys.options().dtype(torch::kInt64);
+  const int64_t tsize = next_pow2(std::max<int64_t>(2 * nnz, 1024));
+  auto tkeys = torch::full({tsize}, -1, i64);
+  auto tcnt = torch::zeros({tsize}, i32);
+  auto slot_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
+  wh::loc_count(reinterpret_cast<const uint64_t*>(keys.data_ptr()), nnz,
+                reinterpret_cast<uint64_t*>(tkeys.data_ptr()), ptr<uint32_t>(tcnt), tsize,
+                ptr<int32_t>(slot_of), s);
+  auto owner_cnt = torch::zeros({nshard}, i64);
+  wh::loc_owner_hist(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
+                     ptr<int64_t>(owner_cnt), s);
+  // the number of unique keys sizes everything downstream: one host sync
+  auto owner_cnt_h = owner_cnt.to(torch::kCPU);
+  int64_t U = 0;
+  std::vector<int64_t> cursor_h(nshard);
+  for (int64_t p = 0; p < nshard; ++p) {
+    cursor_h[p] = U;
+    U += owner_cnt_h.data_ptr<int64_t>()[p];
+  }
+  auto cursor = torch::from_blob(cursor_h.data(), {nshard}, torch::kInt64).to(keys.device());
+  auto tlid = torch::empty({tsize}, i32);
+  auto uniq = torch::empty({U}, i64);
+  auto ucnt = torch::empty({U}, i32);
+  wh::loc_assign(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), ptr<uint32_t>(tcnt), tsize,
+                 (int)nshard, ptr<int64_t>(cursor), ptr<int32_t>(tlid),
+                 reinterpret_cast<uint64_t*>(uniq.data_ptr()), ptr<int32_t>(ucnt), s);
+  auto row_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
+  wh::row_of_nnz(ptr<int64_t>(offset), nrows, ptr<int32_t>(row_of), s);
+  auto csc_off = torch::empty({U + 1}, i64);
+  auto stmp = torch::empty({wh::scan_tmp_elems(U)}, i64);
+  wh::scan_i32(ptr<int32_t>(ucnt), ptr<int64_t>(csc_off), U, ptr<int64_t>(stmp), s);
+  auto csc_cursor = csc_off.clone();
+  auto lid = torch::empty({nnz}, i32);
+  auto csc_row = torch::empty({nnz}, i32);
+  auto csc_val = vp ? torch::empty({nnz}, keys.options().dtype(torch::kFloat32))
+                    : torch::empty({0}, keys.options().dtype(torch::kFloat32));
+  wh::loc_csc(ptr<int32_t>(slot_of), ptr<int32_t>(tlid), ptr<int32_t>(row_of), vp, nnz,
+              ptr<int64_t>(csc_cursor), ptr<int32_t>(lid), ptr<int32_t>(csc_row),
+              vp ? ptr<float>(csc_val) : nullptr, s);
+  return {uniq, ucnt, owner_cnt_h, lid, csc_off, csc_row, csc_val};
+}
+
+// --------------------------------------------------------------- KVStore
+class KVStore {
+ public:
+  KVStore(int64_t cap, int64_t vcap, int64_t dim, int64_t device) {
+    TORCH_CHECK(cap > 0 && (cap & (cap - 1)) == 0, "cap must be a power of two");
+    TORCH_CHECK(dim >= 0 && dim <= 256, "embedding dim must be in [0, 256]");
+    dim_ = dim;
+    vstride_ = dim == 0 ? 0 : (int)(4 * next_pow2((dim + 3) / 4));
+    auto dev = torch::Device(torch::kCUDA, device);
+    c10::DeviceGuard g(dev);
+    auto f32 = torch::TensorOptions().dtype(torch::kFloat32).device(dev);
+    keys_ = torch::full({cap}, -1, f32.dtype(torch::kInt64));
+    w_ = torch::zeros({cap}, f32);
+    z_ = torch::zeros({cap}, f32);
+    sq_ = torch::zeros({cap}, f32);
+    if (dim > 0) {
+      cnt_ = torch::zeros({cap}, f32.dtype(torch::kInt32));
+      vrow_ = torch::full({cap}, -1, f32.dtype(torch::kInt32));
+      V_ = torch::zeros({std::max<int64_t>(vcap, 1), vstride_}, f32);
+      VG_ = torch::zeros({std::max<int64_t>(vcap, 1), vstride_}, f32);
+    }
+    vnext_ = torch::zeros({1}, f32.dtype(torch::kInt32));
+    stats_ = torch::zeros({8}, f32.dtype(torch::kInt64));
+    cap_ = cap;
+    vcap_ = dim > 0 ? vcap : 0;
+  }
+
+  wh::KVTable table() const {
+    wh::KVTable t;
+    t.keys = reinterpret_cast<uint64_t*>(keys_.data_ptr());
+    t.w = ptr<float>(w_);
+    t.z = ptr<float>(z_);
+    t.sq = ptr<float>(sq_);
+    t.cnt = dim_ > 0 ? ptr<uint32_t>(cnt_) : nullptr;
+    t.vrow = dim_ > 0 ? ptr<int32_t>(vrow_) : nullptr;
+    t.V = dim_ > 0 ? ptr<float>(V_) : nullptr;
+    t.VG = dim_ > 0 ? ptr<float>(VG_) : nullptr;
+    t.vnext = ptr<int32_t>(vnext_);
+    t.stats = ptr<int64_t>(stats_);
+    t.cap = cap_;
+    t.vcap = vcap_;
+    t.vstride = vstride_;
+    t.dim = (int)dim_;
+    return t;
+  }
+
+  Tensor find(const Tensor& keys, bool insert) {
+    CHECK_IN(keys, torch::kInt64);
+    c10::DeviceGuard g(keys.device());
+    auto slot = torch::empty({keys.numel()}, keys.options().dtype(torch::kInt32));
+    wh::kv_find(table(), reinterpret_cast<const uint64_t*>(keys.data_ptr()), keys.numel(),
+                insert ? 1 : 0, ptr<int32_t>(slot), cur_stream(keys));
+    return slot;
+  }
+
+  Tensor occupied() {
+    c10::DeviceGuard g(keys_.device());
+    auto out = torch::empty({cap_}, keys_.options().dtype(torch::kInt32));
+    auto n = torch::zeros({1}, keys_.options());
+    wh::kv_occupied(table(), ptr<int32_t>(out), ptr<int64_t>(n), cur_stream(keys_));
+    return out.narrow(0, 0, n.item<int64_t>());
+  }
+
+  Tensor linear_pull(const Tensor& slot) {
+    CHECK_IN(slot, torch::kInt32);
+    c10::DeviceGuard g(slot.device());
+    auto out = torch::empty({slot.numel()}, slot.options().dtype(torch::kFloat32));
+    wh::linear_pull(table(), ptr<int32_t>(slot), slot.numel(), ptr<float>(out), cur_stream(slot));
+    return out;
+  }
+
+  void linear_push(const Tensor& slot, const Tensor& grad, int64_t algo, double alpha, double beta,
+                   double l1, double l2, double sgd_eta) {
+    CHECK_IN(slot, torch::kInt32);
+    CHECK_IN(grad, torch::kFloat32);
+    TORCH_CHECK(grad.numel() >= slot.numel());
+    c10::DeviceGuard g(slot.device());
+    wh::LinearHP hp{(int)algo, (float)alpha, (float)beta, (float)l1, (float)l2, (float)sgd_eta};
+    wh::linear_push(table(), ptr<int32_t>(slot), ptr<float>(grad), slot.numel(), hp,
+                    cur_stream(slot));
+  }
+
+  static wh::DifactoHP dhp(const std::vector<double>& h, int64_t threshold, bool l1_shrk,
+                           int64_t seed) {
+    TORCH_CHECK(h.size() == 8, "difacto hyper-parameter vector must have 8 entries");
+    wh::DifactoHP hp;
+    hp.alpha = (float)h[0]; hp.beta = (float)h[1]; hp.l1 = (float)h[2]; hp.l2 = (float)h[3];
+    hp.v_alpha = (float)h[4]; hp.v_beta = (float)h[5]; hp.v_l2 = (float)h[6];
+    hp.v_init = (float)h[7];
+    hp.threshold = (uint32_t)threshold;
+    hp.l1_shrk = l1_shrk ? 1 : 0;
+    hp.seed = (uint64_t)seed;
+    return hp;
+  }
+
+  void difacto_push_cnt(const Tensor& slot, const Tensor& cnt, const std::vector<double>& h,
+                        int64_t threshold, bool l1_shrk, int64_t seed) {
+    CHECK_IN(slot, torch::kInt32);
+    CHECK_IN(cnt, torch::kFloat32);
+    TORCH_CHECK(cnt.numel() >= slot.numel());
+    c10::DeviceGuard g(slot.device());
+    wh::difacto_push_cnt(table(), ptr<int32_t>(slot), ptr<float>(cnt), slot.numel(),
+                         dhp(h, threshold, l1_shrk, seed), cur_stream(slot));
+  }
+
+  Tensor difacto_pull(const Tensor& slot, bool l1_shrk) {
+    CHECK_IN(slot, torch::kInt32);
+    c10::DeviceGuard g(slot.device());
+    auto out = torch::empty({slot.numel(), vstride_ + 4}, slot.options().dtype(torch::kFloat32));
+    wh::difacto_pull(table(), ptr<int32_t>(slot), slot.numel(), l1_shrk ? 1 : 0, ptr<float>(out),
+                     cur_stream(slot));
+    return out;
+  }
+
+  void difacto_push(const Tensor& slot, const Tensor& grad, const std::vector<double>& h,
+                    int64_t threshold, bool l1_shrk, int64_t seed) {
+    CHECK_IN(slot, torch::kInt32);
+    CHECK_IN(grad, torch::kFloat32);
+    TORCH_CHECK(grad.numel() >= slot.numel() * (vstride_ + 4), "grad rows too short");
+    c10::DeviceGuard g(slot.device());
+    wh::difacto_push(table(), ptr<int32_t>(slot), ptr<float>(grad), slot.numel(),
+                     dhp(h, threshold, l1_shrk, seed), cur_stream(slot));
+  }
+
+  int64_t dim() const { return dim_; }
+  int64_t vstride() const { return vstride_; }
+  int64_t cap() const { return cap_; }
+  int64_t vcap() const { return vcap_; }
+
+  Tensor keys_, w_, z_, sq_, cnt_, vrow_, V_, VG_, vnext_, stats_;
+
+ private:
+  int64_t cap_ = 0, vcap_ = 0, dim_ = 0;
+  int vstride_ = 0;
+};
+
+// --------------------------------------------------------------------- FM
+std::vector<Tensor> fm_forward(const Tensor& offset, const Tensor& lid,
+                               const c10::optional<Tensor>& val, const Tensor& pulled,
+                               int64_t vstride, const Tensor& label, int64_t loss,
+                               const Tensor& met) {
+  CHECK_IN(offset, torch::kInt64);
+  CHECK_IN(lid, torch::kInt32);
+  CHECK_IN(pulled, torch::kFloat32);
+  CHECK_IN(label, torch::kFloat32);
+  CHECK_IN(met, torch::kFloat64);
+  TORCH_CHECK(vstride >= 0 && vstride <= 256 && vstride % 4 == 0, "bad vstride");
+  TORCH_CHECK(met.numel() >= 4, "met needs 4 doubles");
+  const int64_t nrows = offset.numel() - 1;
+  TORCH_CHECK(label.numel() == nrows, "label size mismatch");
+  const int64_t stride = vstride > 0 ? vstride + 4 : 1;
+  TORCH_CHECK(pulled.numel() % stride == 0, "pulled row stride mismatch");
+  const float* vp = optptr<float>(val);
+  c10::DeviceGuard g(offset.device());
+  auto f32 = offset.options().dtype(torch::kFloat32);
+  auto py = torch::empty({nrows}, f32);
+  auto dual = torch::empty({nrows}, f32);
+  auto xv = torch::empty({vstride > 0 ? nrows * vstride : 0}, f32);
+  wh::fm_forward(nrows, ptr<int64_t>(offset), ptr<int32_t>(lid), vp, ptr<float>(pulled),
+                 (int)vstride, ptr<float>(label), (int)loss, ptr<float>(py), ptr<float>(dual),
+                 vstride > 0 ? ptr<float>(xv) : nullptr, ptr<double>(met), cur_stream(offset));
+  return {py, dual, xv};
+}
+
+Tensor fm_backward(const Tensor& csc_off, const Tensor& csc_row, const c10::optional<Tensor>& csc_val,
+                   const Tensor& dual, const c10::optional<Tensor>& xv, const Tensor& pulled,
+                   int64_t vstride) {
+  CHECK_IN(csc_off, torch::kInt64);
+  CHECK_IN(csc_row, torch::kInt32);
+  CHECK_IN(dual, torch::kFloat32);
+  CHECK_IN(pulled, torch::kFloat32);
+  TORCH_CHECK(vstride >= 0 && vstride <= 256 && vstride % 4 == 0, "bad vstride");
+  c10::DeviceGuard g(csc_off.device());
+  auto s = cur_stream(csc_off);
+  const int64_t U = csc_off.numel() - 1;
+  const int64_t nnz = csc_row.numel();
+  const int64_t stride = vstride > 0 ? vstride + 4 : 1;
+  TORCH_CHECK(pulled.numel() == U * stride, "pulled must be [U, stride]");
+  auto f32 = csc_off.options().dtype(torch::kFloat32);
+  auto i32 = csc_off.options().dtype(torch::kInt32);
+  auto i64 = csc_off.options().dtype(torch::kInt64);
+  auto grad = torch::empty({U, stride}, f32);
+  const int64_t cap = wh::fm_bwd_chunks_bound(U, nnz);
+  auto chunk_key = torch::empty({cap}, i32);
+  auto chunk_beg = torch::empty({cap}, i32);
+  auto chunk_cnt = torch::empty({std::max<int64_t>(U, 1)}, i64);
+  auto chunk_off = torch::empty({U + 1}, i64);
+  auto stmp = torch::empty({wh::scan_tmp_elems(U)}, i64);
+  wh::fm_backward(U, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row), optptr<float>(csc_val),
+                  ptr<float>(dual), vstride > 0 ? optptr<float>(xv) : nullptr, ptr<float>(pulled),
+                  (int)vstride, ptr<float>(grad), ptr<int32_t>(chunk_key), ptr<int32_t>(chunk_beg),
+                  ptr<int64_t>(chunk_cnt), ptr<int64_t>(chunk_off), ptr<int64_t>(stmp), cap, s);
+  return grad;
+}
+
+void fm_grad_post(const Tensor& grad, int64_t vstride, int64_t dim, double clip, double dropout,
+                  int64_t seed, bool normalize) {
+  CHECK_IN(grad, torch::kFloat32);
+  if (vstride == 0) return;
+  c10::DeviceGuard g(grad.device());
+  auto s = cur_stream(grad);
+  const int64_t U = grad.numel() / (vstride + 4);
+  Tensor sumsq;
+  if (normalize) sumsq = torch::zeros({1}, grad.options().dtype(torch::kFloat64));
+  wh::fm_grad_post(U, ptr<float>(grad), (int)vstride, (int)dim, (float)clip, (float)dropout,
+                   (uint64_t)seed, normalize ? ptr<double>(sumsq) : nullptr, s);
+  if (normalize) wh::fm_grad_scale(U, ptr<float>(grad), (int)vstride, ptr<double>(sumsq), s);
+}
+
+// -------------------------------------------------------------- metrics
+Tensor auc(const Tensor& py, const Tensor& label) {
+  CHECK_IN(py, torch::kFloat32);
+  CHECK_IN(label, torch::kFloat32);
+  c10::DeviceGuard g(py.device());
+  const int64_t n = py.numel();
+  auto order = std::get<1>(py.sort(0, false));
+  auto lab = label.index_select(0, order).contiguous();
+  auto tmp = torch::empty({n / 2 + 1 + n + 1 + wh::scan_tmp_elems(n)},
+                          py.options().dtype(torch::kInt64));
+  auto out = torch::empty({2}, py.options().dtype(torch::kFloat64));
+  wh::auc_from_sorted(ptr<float>(lab), n, ptr<double>(out), ptr<int64_t>(tmp), cur_stream(py));
+  return out.narrow(0, 0, 1);
+}
+
+// ---------------------------------------------------------------- synth
+std::vector<Tensor> synth_criteo(int64_t nrows, int64_t seed, int64_t step, const Tensor& card) {
+  CHECK_IN(card, torch::kInt64);
+  c10::DeviceGuard g(card.device());
+  const int nfield = (int)card.numel();
+  auto keys = torch::empty({nrows * nfield}, card.options());
+  auto label = torch::empty({nrows}, card.options().dtype(torch::kFloat32));
+  auto offset = torch::empty({nrows + 1}, card.options());
+  wh::synth_criteo(nrows, (uint64_t)seed, (uint64_t)step, ptr<int64_t>(card), nfield,
+                   reinterpret_cast<uint64_t*>(keys.data_ptr()), ptr<float>(label),
+                   ptr<int64_t>(offset), cur_stream(card));
+  return {keys, label, offset};
+}
+
+Tensor gather_rows(const Tensor& in, const Tensor& idx) {
+  CHECK_IN(in, torch::kFloat32);
+  CHECK_IN(idx, torch::kInt32);
+  c10::DeviceGuard g(in.device());
+  const int64_t width = in.dim() > 1 ? in.numel() / in.size(0) : 1;
+  auto out = torch::empty({idx.numel(), width}, in.options());
+  wh::gather_rows(ptr<float>(in), ptr<int32_t>(idx), idx.numel(), (int)width, ptr<float>(out),
+                  cur_stream(in));
+  return in.dim() > 1 ? out : out.view({idx.numel()});
+}
+
+int64_t vstride_for(int64_t dim) { return dim == 0 ? 0 : 4 * next_pow2((dim + 3) / 4); }
+
+}  // namespace
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "wormhole_amd gfx950 HIP kernels";
+  m.def("scan_excl", &scan_excl);
+  m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
+        py::arg("nshard") = 1);
+  m.def("fm_forward", &fm_forward);
+  m.def("fm_backward", &fm_backward);
+  m.def("fm_grad_post", &fm_grad_post);
+  m.def("auc", &auc);
+  m.def("synth_criteo", &synth_criteo);
+  m.def("gather_rows", &gather_rows);
+  m.def("vstride_for", &vstride_for);
+  py::class_<KVStore>(m, "KVStore")
+      .def(py::init<int64_t, int64_t, int64_t, int64_t>(), py::arg("cap"), py::arg("vcap"),
+           py::arg("dim"), py::arg("device"))
+      .def("find", &KVStore::find)
+      .def("occupied", &KVStore::occupied)
+      .def("linear_pull", &KVStore::linear_pull)
+      .def("linear_push", &KVStore::linear_push)
+      .def("difacto_push_cnt", &KVStore::difacto_push_cnt)
+      .def("difacto_pull", &KVStore::difacto_pull)
+      .def("difacto_push", &KVStore::difacto_push)
+      .def_property_readonly("dim", &KVStore::dim)
+      .def_property_readonly("vstride", &KVStore::vstride)
+      .def_property_readonly("cap", &KVStore::cap)
+      .def_property_readonly("vcap", &KVStore::vcap)
+      .def_readonly("keys", &KVStore::keys_)
+      .def_readonly("w", &KVStore::w_)
+      .def_readonly("z", &KVStore::z_)
+      .def_readonly("sq", &KVStore::sq_)
+      .def_readonly("cnt", &KVStore::cnt_)
+      .def_readonly("vrow", &KVStore::vrow_)
+      .def_readonly("V", &KVStore::V_)
+      .def_readonly("VG", &KVStore::VG_)
+      .def_readonly("vnext", &KVStore::vnext_)
+      .def_readonly("stats", &KVStore::stats_);
+}

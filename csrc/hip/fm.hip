@@ -1,0 +1,392 @@
+// Fused factorization-machine / linear forward and backward on a localized
+// minibatch (K4-K10 in SURVEY §2.5).
+//
+// Reference math (learn/difacto/loss.h:53-158, learn/linear/loss.h:92-157):
+//   py   = X w + 0.5 * sum_d ((X V)_d^2 - ((X.*X)(V.*V))_d)
+//   p    = dual(py)                       (logit: -y / (1 + exp(y py)))
+//   gw   = X^T p
+//   gV   = X^T diag(p) X V - diag((X.*X)^T p) V
+// The reference does this with 2 SpMV + 4 SpMM passes and several
+// elementwise loops; here it is ONE forward kernel (a lane group of
+// G = vstride/4 lanes per row, float4 per lane: wave64 holds 64/G rows) that
+// also emits loss/objective/accuracy sums and the dual, and ONE backward
+// kernel that walks each key's occurrence list (the CSC produced by
+// localize) so gradients are segmented sums, not scattered atomics. Only
+// keys whose occurrence list is longer than one chunk (hot features) use
+// float atomics, one per chunk.
+#include "wh_common.h"
+#include "wh_kernels.h"
+
+namespace wh {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kChunk = 32;  // occurrences per backward work item
+
+struct LossOut {
+  float objv, dual;
+};
+
+__device__ __forceinline__ float softplus(float x) {  // log(1 + exp(x)), stable
+  return x > 0.f ? x + log1pf(__expf(-x)) : log1pf(__expf(x));
+}
+
+__device__ __forceinline__ LossOut eval_loss(int loss, float label, float py) {
+  LossOut o;
+  if (loss == 1) {  // square: 0.5 (p - y)^2
+    const float d = py - label;
+    o.objv = 0.5f * d * d;
+    o.dual = d;
+  } else if (loss == 4) {  // squared hinge: max(0, 1 - y p)^2
+    const float y = label > 0.f ? 1.f : -1.f;
+    const float t = fmaxf(1.f - y * py, 0.f);
+    o.objv = t * t;
+    o.dual = -2.f * y * t;
+  } else {  // logit
+    const float y = label > 0.f ? 1.f : -1.f;
+    o.objv = softplus(-y * py);
+    o.dual = -y / (1.f + __expf(y * py));
+  }
+  return o;
+}
+
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_t* __restrict__ off,
+                                                     const int32_t* __restrict__ lid,
+                                                     const float* __restrict__ val,
+                                                     const float* __restrict__ pulled, int vstride,
+                                                     const float* __restrict__ label, int loss,
+                                                     float* __restrict__ py_out,
+                                                     float* __restrict__ dual_out,
+                                                     float* __restrict__ xv, double* met) {
+  __shared__ double sh[kThreads / 64];
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
+  const int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
+  const int stride = vstride + 4;
+  double m_objv = 0, m_objw = 0, m_corr = 0, m_n = 0;
+  if (row < nrows) {
+    float wsum = 0.f;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+    const int64_t b = off[row], e = off[row + 1];
+    int64_t j = b;
+    for (; j + 1 < e; j += 2) {  // two independent gathers in flight
+      const int k0 = lid[j], k1 = lid[j + 1];
+      const float x0 = val ? val[j] : 1.f, x1 = val ? val[j + 1] : 1.f;
+      const float* r0 = pulled + (int64_t)k0 * stride;
+      const float* r1 = pulled + (int64_t)k1 * stride;
+      const float2 h0 = *reinterpret_cast<const float2*>(r0);
+      const float2 h1 = *reinterpret_cast<const float2*>(r1);
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
+      if (h0.y != 0.f) v0 = reinterpret_cast<const float4*>(r0 + 4)[gl];
+      if (h1.y != 0.f) v1 = reinterpret_cast<const float4*>(r1 + 4)[gl];
+      wsum += x0 * h0.x + x1 * h1.x;
+      s.x += x0 * v0.x + x1 * v1.x; s.y += x0 * v0.y + x1 * v1.y;
+      s.z += x0 * v0.z + x1 * v1.z; s.w += x0 * v0.w + x1 * v1.w;
+      const float xx0 = x0 * x0, xx1 = x1 * x1;
+      q.x += xx0 * v0.x * v0.x + xx1 * v1.x * v1.x; q.y += xx0 * v0.y * v0.y + xx1 * v1.y * v1.y;
+      q.z += xx0 * v0.z * v0.z + xx1 * v1.z * v1.z; q.w += xx0 * v0.w * v0.w + xx1 * v1.w * v1.w;
+    }
+    if (j < e) {
+      const int k0 = lid[j];
+      const float x0 = val ? val[j] : 1.f;
+      const float* r0 = pulled + (int64_t)k0 * stride;
+      const float2 h0 = *reinterpret_cast<const float2*>(r0);
+      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (h0.y != 0.f) v0 = reinterpret_cast<const float4*>(r0 + 4)[gl];
+      wsum += x0 * h0.x;
+      s.x += x0 * v0.x; s.y += x0 * v0.y; s.z += x0 * v0.z; s.w += x0 * v0.w;
+      const float xx0 = x0 * x0;
+      q.x += xx0 * v0.x * v0.x; q.y += xx0 * v0.y * v0.y;
+      q.z += xx0 * v0.z * v0.z; q.w += xx0 * v0.w * v0.w;
+    }
+    float part = (s.x * s.x - q.x) + (s.y * s.y - q.y) + (s.z * s.z - q.z) + (s.w * s.w - q.w);
+    part = group_sum<G>(part);
+    reinterpret_cast<float4*>(xv + row * vstride)[gl] = s;
+    if (gl == 0) {
+      const float p = wsum + 0.5f * part;
+      const float y = label[row];
+      const LossOut o = eval_loss(loss, y, p);
+      const LossOut ow = eval_loss(loss, y, wsum);
+      py_out[row] = p;
+      dual_out[row] = o.dual;
+      m_objv = o.objv;
+      m_objw = ow.objv;
+      m_corr = ((y > 0.f && p > 0.f) || (y <= 0.f && p <= 0.f)) ? 1.0 : 0.0;
+      m_n = 1.0;
+    }
+  } else {
+    // keep every lane in the group_sum shuffle pattern
+    group_sum<G>(0.f);
+  }
+  double r;
+  r = block_sum_d(m_objv, sh); if (threadIdx.x == 0) atomicAdd(met + 0, r); __syncthreads();
+  r = block_sum_d(m_objw, sh); if (threadIdx.x == 0) atomicAdd(met + 1, r); __syncthreads();
+  r = block_sum_d(m_corr, sh); if (threadIdx.x == 0) atomicAdd(met + 2, r); __syncthreads();
+  r = block_sum_d(m_n, sh); if (threadIdx.x == 0) atomicAdd(met + 3, r);
+}
+
+// linear model: G lanes stride over one row's non-zeros
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_lin_fwd(int64_t nrows, const int64_t* __restrict__ off,
+                                                      const int32_t* __restrict__ lid,
+                                                      const float* __restrict__ val,
+                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ label, int loss,
+                                                      float* __restrict__ py_out,
+                                                      float* __restrict__ dual_out, double* met) {
+  __shared__ double sh[kThreads / 64];
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
+  const int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
+  double m_objv = 0, m_corr = 0, m_n = 0;
+  float acc = 0.f;
+  if (row < nrows) {
+    const int64_t b = off[row], e = off[row + 1];
+    for (int64_t j = b + gl; j < e; j += G) acc += (val ? val[j] : 1.f) * w[lid[j]];
+  }
+  acc = group_sum<G>(acc);
+  if (row < nrows && gl == 0) {
+    const float y = label[row];
+    const LossOut o = eval_loss(loss, y, acc);
+    py_out[row] = acc;
+    dual_out[row] = o.dual;
+    m_objv = o.objv;
+    m_corr = ((y > 0.f && acc > 0.f) || (y <= 0.f && acc <= 0.f)) ? 1.0 : 0.0;
+    m_n = 1.0;
+  }
+  double r;
+  r = block_sum_d(m_objv, sh); if (threadIdx.x == 0) { atomicAdd(met + 0, r); atomicAdd(met + 1, r); }
+  __syncthreads();
+  r = block_sum_d(m_corr, sh); if (threadIdx.x == 0) atomicAdd(met + 2, r); __syncthreads();
+  r = block_sum_d(m_n, sh); if (threadIdx.x == 0) atomicAdd(met + 3, r);
+}
+
+// ---------------------------------------------------------------- backward
+__global__ void k_chunk_count(int64_t nuniq, const int64_t* csc_off, int64_t* chunk_cnt) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nuniq) {
+    const int64_t c = csc_off[k + 1] - csc_off[k];
+    chunk_cnt[k] = c > 0 ? (c + kChunk - 1) / kChunk : 0;
+  }
+}
+
+// writes the chunk table; zeroes the gradient rows of multi-chunk keys
+__global__ void k_chunk_fill(int64_t nuniq, const int64_t* csc_off, const int64_t* chunk_off,
+                             const float* pulled, int vstride, int32_t* chunk_key,
+                             int32_t* chunk_beg, float* grad) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nuniq) return;
+  const int64_t c0 = chunk_off[k], nc = chunk_off[k + 1] - c0;
+  for (int64_t c = 0; c < nc; ++c) {
+    chunk_key[c0 + c] = (int32_t)k;
+    chunk_beg[c0 + c] = (int32_t)(csc_off[k] + c * kChunk);
+  }
+  if (nc > 1) {
+    const int stride = vstride > 0 ? vstride + 4 : 1;
+    float* g = grad + k * stride;
+    if (vstride > 0) {
+      const float flag = pulled[k * stride + 1];
+      g[0] = 0.f; g[1] = flag; g[2] = 0.f; g[3] = 0.f;
+      if (flag != 0.f)
+        for (int d = 0; d < vstride; ++d) g[4 + d] = 0.f;
+    } else {
+      g[0] = 0.f;
+    }
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_fm_bwd(const int64_t* __restrict__ nchunk_p, const int32_t* __restrict__ chunk_key,
+                                                     const int32_t* __restrict__ chunk_beg,
+                                                     const int64_t* __restrict__ csc_off,
+                                                     const int32_t* __restrict__ csc_row,
+                                                     const float* __restrict__ csc_val,
+                                                     const float* __restrict__ dual,
+                                                     const float* __restrict__ xv,
+                                                     const float* __restrict__ pulled, int vstride,
+                                                     float* __restrict__ grad) {
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
+  const int64_t c = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
+  if (c >= *nchunk_p) return;
+  const int k = chunk_key[c];
+  const int64_t kb = csc_off[k], ke = csc_off[k + 1];
+  const int64_t b = chunk_beg[c];
+  const int64_t e = b + kChunk < ke ? b + kChunk : ke;
+  const bool multi = (ke - kb) > kChunk;
+  const int stride = vstride + 4;
+  const float* hdr = pulled + (int64_t)k * stride;
+  const bool flag = hdr[1] != 0.f;
+  float gw = 0.f, xxp = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (flag) {
+    int64_t p = b;
+    for (; p + 1 < e; p += 2) {
+      const int i0 = csc_row[p], i1 = csc_row[p + 1];
+      const float x0 = csc_val ? csc_val[p] : 1.f, x1 = csc_val ? csc_val[p + 1] : 1.f;
+      const float d0 = dual[i0] * x0, d1 = dual[i1] * x1;
+      const float4 a0 = reinterpret_cast<const float4*>(xv + (int64_t)i0 * vstride)[gl];
+      const float4 a1 = reinterpret_cast<const float4*>(xv + (int64_t)i1 * vstride)[gl];
+      gw += d0 + d1;
+      xxp += d0 * x0 + d1 * x1;
+      acc.x += d0 * a0.x + d1 * a1.x; acc.y += d0 * a0.y + d1 * a1.y;
+      acc.z += d0 * a0.z + d1 * a1.z; acc.w += d0 * a0.w + d1 * a1.w;
+    }
+    if (p < e) {
+      const int i0 = csc_row[p];
+      const float x0 = csc_val ? csc_val[p] : 1.f;
+      const float d0 = dual[i0] * x0;
+      const float4 a0 = reinterpret_cast<const float4*>(xv + (int64_t)i0 * vstride)[gl];
+      gw += d0;
+      xxp += d0 * x0;
+      acc.x += d0 * a0.x; acc.y += d0 * a0.y; acc.z += d0 * a0.z; acc.w += d0 * a0.w;
+    }
+    const float4 v = reinterpret_cast<const float4*>(hdr + 4)[gl];
+    acc.x -= xxp * v.x; acc.y -= xxp * v.y; acc.z -= xxp * v.z; acc.w -= xxp * v.w;
+  } else {
+    for (int64_t p = b + gl; p < e; p += G) {
+      const float x0 = csc_val ? csc_val[p] : 1.f;
+      gw += dual[csc_row[p]] * x0;
+    }
+    gw = group_sum<G>(gw);
+  }
+  float* g = grad + (int64_t)k * stride;
+  if (!multi) {
+    if (gl == 0) *reinterpret_cast<float4*>(g) = make_float4(gw, flag ? 1.f : 0.f, 0.f, 0.f);
+    if (flag) reinterpret_cast<float4*>(g + 4)[gl] = acc;
+  } else {
+    if (gl == 0) atomicAdd(g, gw);
+    if (flag) {
+      float* gv = g + 4 + gl * 4;
+      atomicAdd(gv + 0, acc.x); atomicAdd(gv + 1, acc.y);
+      atomicAdd(gv + 2, acc.z); atomicAdd(gv + 3, acc.w);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_lin_bwd(const int64_t* __restrict__ nchunk_p, const int32_t* __restrict__ chunk_key,
+                                                      const int32_t* __restrict__ chunk_beg,
+                                                      const int64_t* __restrict__ csc_off,
+                                                      const int32_t* __restrict__ csc_row,
+                                                      const float* __restrict__ csc_val,
+                                                      const float* __restrict__ dual,
+                                                      float* __restrict__ grad) {
+  const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (c >= *nchunk_p) return;
+  const int k = chunk_key[c];
+  const int64_t kb = csc_off[k], ke = csc_off[k + 1];
+  const int64_t b = chunk_beg[c];
+  const int64_t e = b + kChunk < ke ? b + kChunk : ke;
+  float gw = 0.f;
+  for (int64_t p = b; p < e; ++p) gw += dual[csc_row[p]] * (csc_val ? csc_val[p] : 1.f);
+  if ((ke - kb) > kChunk) atomicAdd(grad + k, gw);
+  else grad[k] = gw;
+}
+
+__global__ __launch_bounds__(kThreads) void k_grad_post(int64_t nuniq, float* grad, int vstride,
+                                                        int dim, float clip, float dropout,
+                                                        uint64_t seed, double* sumsq) {
+  __shared__ double sh[kThreads / 64];
+  const int stride = vstride + 4;
+  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t k = t / vstride;
+  const int d = (int)(t % vstride);
+  double ss = 0;
+  if (k < nuniq && d < dim) {
+    float* g = grad + k * stride;
+    if (g[1] != 0.f) {
+      float v = g[4 + d];
+      if (clip > 0.f) v = fminf(fmaxf(v, -clip), clip);
+      if (dropout > 0.f && uhash01(seed, (uint64_t)k, (uint64_t)d) > 1.f - dropout) v = 0.f;
+      g[4 + d] = v;
+      ss = (double)v * v;
+    }
+  }
+  if (sumsq) {
+    const double r = block_sum_d(ss, sh);
+    if (threadIdx.x == 0) atomicAdd(sumsq, r);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_grad_scale(int64_t nuniq, float* grad, int vstride,
+                                                         const double* sumsq) {
+  const int stride = vstride + 4;
+  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const int64_t k = t / vstride;
+  const int d = (int)(t % vstride);
+  const double n2 = *sumsq;
+  if (n2 < 1e-10 || k >= nuniq) return;
+  float* g = grad + k * stride;
+  if (g[1] != 0.f) g[4 + d] = (float)(g[4 + d] / sqrt(n2));
+}
+
+}  // namespace
+
+#define WH_DISPATCH_G(G, KERNEL, ...)                                            \
+  switch (G) {                                                                   \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                   \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                   \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                   \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                   \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                 \
+    case 32: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                 \
+    default: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                 \
+  }
+
+void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
+                const float* pulled, int vstride, const float* label, int loss, float* py,
+                float* dual, float* xv, double* met, hipStream_t s) {
+  if (nrows <= 0) return;
+  if (vstride == 0) {
+    constexpr int G = 8;
+    hipLaunchKernelGGL(k_lin_fwd<G>, dim3(grid_for(nrows * G, kThreads)), dim3(kThreads), 0, s,
+                       nrows, offset, lid, val, pulled, label, loss, py, dual, met);
+    return;
+  }
+  const int G = vstride / 4;  // vstride <= 256 enforced by the binding
+  const dim3 grid(grid_for(nrows * G, kThreads)), block(kThreads);
+  WH_DISPATCH_G(G, k_fm_fwd, grid, block, 0, s, nrows, offset, lid, val, pulled, vstride, label,
+                loss, py, dual, xv, met);
+}
+
+int64_t fm_bwd_chunks_bound(int64_t nuniq, int64_t nnz) { return nuniq + nnz / kChunk + 1; }
+
+void fm_backward(int64_t nuniq, const int64_t* csc_off, const int32_t* csc_row,
+                 const float* csc_val, const float* dual, const float* xv, const float* pulled,
+                 int vstride, float* grad, int32_t* chunk_key, int32_t* chunk_beg,
+                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, int64_t chunk_cap,
+                 hipStream_t s) {
+  if (nuniq <= 0) return;
+  hipLaunchKernelGGL(k_chunk_count, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
+                     csc_off, chunk_cnt);
+  scan_i64(chunk_cnt, chunk_off, nuniq, scan_tmp, s);
+  hipLaunchKernelGGL(k_chunk_fill, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
+                     csc_off, chunk_off, pulled, vstride, chunk_key, chunk_beg, grad);
+  // the chunk count is data dependent (device value chunk_off[nuniq]); launch
+  // over the host-side bound and let surplus work items exit, so the whole
+  // step stays free of host synchronisation.
+  const int64_t* nchunk_p = chunk_off + nuniq;
+  if (vstride == 0) {
+    hipLaunchKernelGGL(k_lin_bwd, dim3(grid_for(chunk_cap, kThreads)), dim3(kThreads), 0, s,
+                       nchunk_p, chunk_key, chunk_beg, csc_off, csc_row, csc_val, dual, grad);
+    return;
+  }
+  const int G = vstride / 4;
+  const dim3 grid(grid_for(chunk_cap * G, kThreads)), block(kThreads);
+  WH_DISPATCH_G(G, k_fm_bwd, grid, block, 0, s, nchunk_p, chunk_key, chunk_beg, csc_off,
+                csc_row, csc_val, dual, xv, pulled, vstride, grad);
+}
+
+void fm_grad_post(int64_t nuniq, float* grad, int vstride, int dim, float clip, float dropout,
+                  uint64_t seed, double* sumsq, hipStream_t s) {
+  if (nuniq <= 0 || vstride == 0) return;
+  hipLaunchKernelGGL(k_grad_post, dim3(grid_for(nuniq * vstride, kThreads)), dim3(kThreads), 0,
+                     s, nuniq, grad, vstride, dim, clip, dropout, seed, sumsq);
+}
+
+void fm_grad_scale(int64_t nuniq, float* grad, int vstride, const double* sumsq,
+                   hipStream_t s) {
+  if (nuniq <= 0 || vstride == 0) return;
+  hipLaunchKernelGGL(k_grad_scale, dim3(grid_for(nuniq * vstride, kThreads)), dim3(kThreads), 0,
+                     s, nuniq, grad, vstride, sumsq);
+}
+
+}  // namespace wh

@@ -1,0 +1,383 @@
+// Device-resident sharded parameter store and fused optimizer updates.
+//
+// Replaces the ps-lite OnlineServer/KVStore with per-GPU open-addressing
+// tables in HBM (keys + SoA value arrays + an embedding slab), and the
+// per-key server handles with fused kernels:
+//   * linear SGD / AdaGrad / FTRL + L1L2 proximal step
+//       (reference learn/linear/async_sgd.h:71-180, learn/linear/penalty.h:36-41)
+//   * DiFacto: feature-count push with lazy V allocation, FTRL on w,
+//     AdaGrad on V, variable-length pull
+//       (reference learn/difacto/async_sgd.h:214-296)
+// One lane group of G = vstride/4 lanes owns one key (float4 per lane), so a
+// 64-dim embedding row is one 256-byte coalesced access per 16 lanes.
+#include "wh_common.h"
+#include "wh_kernels.h"
+
+namespace wh {
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kThreads) void k_kv_find(const uint64_t* keys_in, int64_t n,
+                                                      uint64_t* tkeys, int64_t cap, int insert,
+                                                      int32_t* slot, int64_t* stats) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  bool created = false, failed = false;
+  if (i < n) {
+    const uint64_t k = keys_in[i];
+    const uint64_t mask = (uint64_t)cap - 1;
+    uint64_t h = mix64(k) & mask;
+    int64_t res = -1;
+    for (int64_t probe = 0; probe < cap; ++probe) {
+      uint64_t prev = ld_relaxed(tkeys + h);
+      if (prev == k) { res = (int64_t)h; break; }
+      if (prev == kEmptyKey) {
+        if (!insert) break;
+        uint64_t old = atomicCAS((unsigned long long*)(tkeys + h),
+                                 (unsigned long long)kEmptyKey, (unsigned long long)k);
+        if (old == kEmptyKey) { res = (int64_t)h; created = true; break; }
+        if (old == k) { res = (int64_t)h; break; }
+      }
+      h = (h + 1) & mask;
+    }
+    if (insert && res < 0) failed = true;
+    slot[i] = (int32_t)res;
+  }
+  const uint64_t bc = __ballot(created), bf = __ballot(failed);
+  if ((threadIdx.x & 63) == 0) {
+    if (bc) atomicAdd((unsigned long long*)(stats + 4), (unsigned long long)__popcll(bc));
+    if (bf) atomicAdd((unsigned long long*)(stats + 2), (unsigned long long)__popcll(bf));
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_kv_occupied(const uint64_t* tkeys, int64_t cap,
+                                                          int32_t* out, int64_t* out_n) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool occ = i < cap && tkeys[i] != kEmptyKey;
+  const uint64_t b = __ballot(occ);
+  const int lane = threadIdx.x & 63;
+  int64_t base = 0;
+  if (lane == 0 && b)
+    base = (int64_t)atomicAdd((unsigned long long*)out_n, (unsigned long long)__popcll(b));
+  base = __shfl(base, 0, 64);
+  if (occ) {
+    const int rank = __popcll(b & ((1ull << lane) - 1));
+    out[base + rank] = (int32_t)i;
+  }
+}
+
+__device__ __forceinline__ float l1l2_solve(float z, float eta, float l1, float l2) {
+  // argmin_x 0.5*eta*(x - z/eta)^2 + l1|x| + l2 x^2 (soft threshold)
+  if (z <= l1 && z >= -l1) return 0.f;
+  return (z > 0 ? z - l1 : z + l1) / (eta + l2);
+}
+
+__device__ __forceinline__ void count_nnz_delta(float oldw, float neww, int64_t* stats) {
+  const int d = (oldw == 0.f && neww != 0.f) ? 1 : ((oldw != 0.f && neww == 0.f) ? -1 : 0);
+  long long s = wave_sum_ll(d);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd((unsigned long long*)(stats + 0), (unsigned long long)s);
+}
+
+__global__ __launch_bounds__(kThreads) void k_linear_pull(const float* w, const int32_t* slot,
+                                                          int64_t n, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < n) {
+    const int32_t s = slot[i];
+    out[i] = s >= 0 ? w[s] : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_linear_push(KVTable t, const int32_t* slot,
+                                                          const float* grad, int64_t n,
+                                                          LinearHP hp) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  float oldw = 0.f, neww = 0.f;
+  if (i < n) {
+    const int32_t s = slot[i];
+    if (s >= 0) {
+      const float g = grad[i];
+      oldw = t.w[s];
+      if (hp.algo == 1) {  // SGD, eta = (beta + sqrt(t)) / alpha
+        neww = l1l2_solve(hp.sgd_eta * oldw - g, hp.sgd_eta, hp.l1, hp.l2);
+      } else if (hp.algo == 2) {  // AdaGrad
+        const float sq = sqrtf(t.sq[s] * t.sq[s] + g * g);
+        t.sq[s] = sq;
+        const float eta = (sq + hp.beta) / hp.alpha;
+        neww = l1l2_solve(eta * oldw - g, eta, hp.l1, hp.l2);
+      } else {  // FTRL
+        const float sq0 = t.sq[s];
+        const float sq = sqrtf(sq0 * sq0 + g * g);
+        t.sq[s] = sq;
+        const float sigma = (sq - sq0) / hp.alpha;
+        const float z = t.z[s] + g - sigma * oldw;
+        t.z[s] = z;
+        neww = l1l2_solve(-z, (hp.beta + sq) / hp.alpha, hp.l1, hp.l2);
+      }
+      t.w[s] = neww;
+    }
+  }
+  count_nnz_delta(oldw, neww, t.stats);
+}
+
+// ---------------------------------------------------------------- difacto
+// allocate + initialise the V row of slot s if the reference Resize rule
+// fires (learn/difacto/async_sgd.h:247-259). Called by ONE group; lane `gl`
+// of G lanes. Returns the row (or -1), identical in every lane of the group.
+template <int G>
+__device__ __forceinline__ int32_t maybe_alloc_v(const KVTable& t, int32_t s, bool want, int gl,
+                                                 int gbase, const DifactoHP& hp,
+                                                 long long* newv) {
+  int32_t row = -1;
+  if (gl == 0 && want) {
+    row = atomicAdd(t.vnext, 1);
+    if (row >= t.vcap) {
+      atomicAdd((unsigned long long*)(t.stats + 3), 1ull);
+      row = -1;
+    } else {
+      t.vrow[s] = row;
+      *newv += t.dim;
+    }
+  }
+  row = __shfl(row, gbase, 64);
+  if (row >= 0) {
+    const uint64_t key = t.keys[s];
+    float* V = t.V + (int64_t)row * t.vstride;
+    float* VG = t.VG + (int64_t)row * t.vstride;
+    for (int c = gl * 4; c < t.vstride; c += 4 * G) {
+      float4 v, zero = make_float4(0.f, 0.f, 0.f, 0.f);
+      float* pv = &v.x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int d = c + e;
+        pv[e] = d < t.dim ? (uhash01(hp.seed, key, (uint64_t)d) * 2.f - 1.f) * hp.v_init : 0.f;
+      }
+      *reinterpret_cast<float4*>(V + c) = v;
+      *reinterpret_cast<float4*>(VG + c) = zero;
+    }
+  }
+  return row;
+}
+
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const int32_t* slot,
+                                                               const float* cnt, int64_t n,
+                                                               DifactoHP hp) {
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane - gl;
+  const int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
+  long long newv = 0;
+  bool active = false;
+  int32_t s = -1;
+  bool want = false;
+  if (i < n) {
+    s = slot[i];
+    if (s >= 0) {
+      active = true;
+      if (gl == 0) {
+        const uint32_t c = t.cnt[s] + (uint32_t)cnt[i];
+        t.cnt[s] = c;
+        want = c > hp.threshold && t.vrow[s] < 0 && (!hp.l1_shrk || t.w[s] != 0.f);
+      }
+    }
+  }
+  // every lane of the wave must reach the shuffles inside maybe_alloc_v
+  if (t.vstride > 0) maybe_alloc_v<G>(t, active ? s : 0, want && active, gl, gbase, hp, &newv);
+  newv = wave_sum_ll(newv);
+  if (lane == 0 && newv) atomicAdd((unsigned long long*)(t.stats + 1), (unsigned long long)newv);
+}
+
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_difacto_pull(KVTable t, const int32_t* slot,
+                                                           int64_t n, int l1_shrk, float* out) {
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
+  const int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
+  if (i >= n) return;
+  const int32_t s = slot[i];
+  const int stride = t.vstride + 4;
+  float* o = out + i * stride;
+  float w = 0.f;
+  int32_t row = -1;
+  if (s >= 0) {
+    w = t.w[s];
+    row = t.vrow[s];
+    if (l1_shrk && w == 0.f) row = -1;
+  }
+  if (gl == 0) *reinterpret_cast<float4*>(o) = make_float4(w, row >= 0 ? 1.f : 0.f, 0.f, 0.f);
+  if (row >= 0) {
+    const float* V = t.V + (int64_t)row * t.vstride;
+    for (int c = gl * 4; c < t.vstride; c += 4 * G)
+      *reinterpret_cast<float4*>(o + 4 + c) = *reinterpret_cast<const float4*>(V + c);
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int32_t* slot,
+                                                           const float* grad, int64_t n,
+                                                           DifactoHP hp) {
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane - gl;
+  const int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
+  const int stride = t.vstride + 4;
+  long long newv = 0;
+  float oldw = 0.f, neww = 0.f;
+  bool want = false;
+  int32_t s = -1;
+  float gflag = 0.f;
+  if (i < n) {
+    s = slot[i];
+    const float* gr = grad + i * stride;
+    gflag = gr[1];
+    if (s >= 0 && gl == 0) {
+      // FTRL on w (reference UpdateW, learn/difacto/async_sgd.h:262-286)
+      float g = gr[0];
+      const float w = t.w[s];
+      g += hp.l2 * w;
+      const float cg = t.sq[s];
+      const float cg_new = sqrtf(cg * cg + g * g);
+      t.sq[s] = cg_new;
+      const float z = t.z[s] - (g - (cg_new - cg) / hp.alpha * w);
+      t.z[s] = z;
+      float nw;
+      if (z <= hp.l1 && z >= -hp.l1) {
+        nw = 0.f;
+      } else {
+        const float eta = (hp.beta + cg_new) / hp.alpha;
+        nw = (z > 0 ? z - hp.l1 : z + hp.l1) / eta;
+      }
+      t.w[s] = nw;
+      oldw = w;
+      neww = nw;
+      if (t.vstride > 0 && w == 0.f && nw != 0.f)
+        want = t.cnt[s] > hp.threshold && t.vrow[s] < 0;
+    }
+  }
+  if (t.vstride > 0) {
+    const bool act = i < n && s >= 0;
+    maybe_alloc_v<G>(t, act ? s : 0, want && act, gl, gbase, hp, &newv);
+    // AdaGrad on V (reference UpdateV, learn/difacto/async_sgd.h:289-296)
+    if (act && gflag != 0.f) {
+      const int32_t row = t.vrow[s];
+      if (row >= 0) {
+        float* V = t.V + (int64_t)row * t.vstride;
+        float* VG = t.VG + (int64_t)row * t.vstride;
+        const float* gv = grad + i * stride + 4;
+        for (int c = gl * 4; c < t.vstride; c += 4 * G) {
+          float4 v = *reinterpret_cast<float4*>(V + c);
+          float4 cg = *reinterpret_cast<float4*>(VG + c);
+          const float4 g = *reinterpret_cast<const float4*>(gv + c);
+          float* pv = &v.x;
+          float* pc = &cg.x;
+          const float* pg = &g.x;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gg = pg[e] + hp.v_l2 * pv[e];
+            pc[e] = sqrtf(pc[e] * pc[e] + gg * gg);
+            pv[e] -= hp.v_alpha / (pc[e] + hp.v_beta) * gg;
+          }
+          *reinterpret_cast<float4*>(V + c) = v;
+          *reinterpret_cast<float4*>(VG + c) = cg;
+        }
+      }
+    }
+  }
+  count_nnz_delta(oldw, neww, t.stats);
+  newv = wave_sum_ll(newv);
+  if (lane == 0 && newv) atomicAdd((unsigned long long*)(t.stats + 1), (unsigned long long)newv);
+}
+
+__global__ __launch_bounds__(kThreads) void k_gather_rows(const float* in, const int32_t* idx,
+                                                          int64_t n, int width, float* out) {
+  // width in floats; vectorised when width % 4 == 0
+  const int64_t tid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (width % 4 == 0) {
+    const int q = width / 4;
+    const int64_t r = tid / q, c = tid % q;
+    if (r >= n) return;
+    reinterpret_cast<float4*>(out + r * width)[c] =
+        reinterpret_cast<const float4*>(in + (int64_t)idx[r] * width)[c];
+  } else {
+    const int64_t r = tid / width, c = tid % width;
+    if (r >= n) return;
+    out[r * width + c] = in[(int64_t)idx[r] * width + c];
+  }
+}
+
+inline int lanes_per_key(int vstride) {
+  if (vstride <= 0) return 1;
+  int q = vstride / 4;
+  return q >= 64 ? 64 : q;
+}
+
+}  // namespace
+
+void kv_find(const KVTable& t, const uint64_t* keys, int64_t n, int insert, int32_t* slot,
+             hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_kv_find, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, keys, n,
+                     t.keys, t.cap, insert, slot, t.stats);
+}
+
+void kv_occupied(const KVTable& t, int32_t* out_slots, int64_t* out_n, hipStream_t s) {
+  hipLaunchKernelGGL(k_kv_occupied, dim3(grid_for(t.cap, kThreads)), dim3(kThreads), 0, s,
+                     t.keys, t.cap, out_slots, out_n);
+}
+
+void linear_pull(const KVTable& t, const int32_t* slot, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_linear_pull, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t.w,
+                     slot, n, out);
+}
+
+void linear_push(const KVTable& t, const int32_t* slot, const float* grad, int64_t n,
+                 LinearHP hp, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_linear_push, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t, slot,
+                     grad, n, hp);
+}
+
+#define WH_DISPATCH_G(G, KERNEL, ...)                                            \
+  switch (G) {                                                                   \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                   \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                   \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                   \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                   \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                 \
+    case 32: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                 \
+    default: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                 \
+  }
+
+void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt, int64_t n,
+                      DifactoHP hp, hipStream_t s) {
+  if (n <= 0) return;
+  const int G = lanes_per_key(t.vstride);
+  const dim3 grid(grid_for(n * G, kThreads)), block(kThreads);
+  WH_DISPATCH_G(G, k_difacto_push_cnt, grid, block, 0, s, t, slot, cnt, n, hp);
+}
+
+void difacto_pull(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk, float* out,
+                  hipStream_t s) {
+  if (n <= 0) return;
+  const int G = lanes_per_key(t.vstride);
+  const dim3 grid(grid_for(n * G, kThreads)), block(kThreads);
+  WH_DISPATCH_G(G, k_difacto_pull, grid, block, 0, s, t, slot, n, l1_shrk, out);
+}
+
+void difacto_push(const KVTable& t, const int32_t* slot, const float* grad, int64_t n,
+                  DifactoHP hp, hipStream_t s) {
+  if (n <= 0) return;
+  const int G = lanes_per_key(t.vstride);
+  const dim3 grid(grid_for(n * G, kThreads)), block(kThreads);
+  WH_DISPATCH_G(G, k_difacto_push, grid, block, 0, s, t, slot, grad, n, hp);
+}
+
+void gather_rows(const float* in, const int32_t* idx, int64_t n, int width, float* out,
+                 hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t work = (width % 4 == 0) ? n * (width / 4) : n * width;
+  hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((work + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, s, in, idx, n, width, out);
+}
+
+}  // namespace wh

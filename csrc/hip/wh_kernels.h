@@ -1,0 +1,141 @@
+// Host-side launcher API of the wormhole_amd HIP kernels.
+//
+// Every launcher takes raw device pointers plus the HIP stream to enqueue on;
+// none allocates, frees or synchronises, so every call is hipGraph-capturable.
+// The torch binding layer (csrc/bind/hip_ops.cc) validates shapes/dtypes and
+// passes the current PyTorch HIP stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace wh {
+
+// ---------------------------------------------------------------- scan.hip
+// exclusive prefix sum: out[i] = sum_{k<i} in[k], out[n] = total.
+// tmp must hold scan_tmp_elems(n) int64.
+int64_t scan_tmp_elems(int64_t n);
+void scan_i32(const int32_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t s);
+void scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t s);
+
+// ------------------------------------------------------------ localize.hip
+// Batch-local de-duplication of uint64 feature ids (reference Localizer,
+// learn/base/localizer.h:42-221) via a device open-addressing table of
+// `tsize` (power of two, >= 2*nnz) slots instead of a global sort.
+//   tkeys[tsize] (init ~0), tcnt[tsize] (init 0) are scratch.
+void loc_count(const uint64_t* keys, int64_t nnz, uint64_t* tkeys, uint32_t* tcnt,
+               int64_t tsize, int32_t* slot_of, hipStream_t s);
+// per-owner histogram of the occupied slots (owner = mix64b(key) % nshard)
+void loc_owner_hist(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* owner_cnt,
+                    hipStream_t s);
+// assign local ids grouped by owner; owner_cursor[p] must start at the
+// exclusive scan of owner_cnt. Writes tlid[slot], uniq[lid], ucnt[lid].
+void loc_assign(const uint64_t* tkeys, const uint32_t* tcnt, int64_t tsize, int nshard,
+                int64_t* owner_cursor, int32_t* tlid, uint64_t* uniq, int32_t* ucnt,
+                hipStream_t s);
+// CSR row id of every non-zero
+void row_of_nnz(const int64_t* offset, int64_t nrows, int32_t* row_of, hipStream_t s);
+// remap nnz -> local id, and fill the CSC (per-unique-key occurrence lists).
+// csc_cursor[lid] must start at the exclusive scan of ucnt.
+void loc_csc(const int32_t* slot_of, const int32_t* tlid, const int32_t* row_of,
+             const float* val, int64_t nnz, int64_t* csc_cursor, int32_t* lid,
+             int32_t* csc_row, float* csc_val, hipStream_t s);
+
+// ---------------------------------------------------------- kvstore.hip
+// Sharded parameter store (replaces the ps-lite server KVStore). Open
+// addressing, linear probing, 64-bit CAS insert.
+struct KVTable {
+  uint64_t* keys;     // [cap] ~0 == empty
+  float* w;           // [cap]
+  float* z;           // [cap]  FTRL z (linear sign convention per app)
+  float* sq;          // [cap]  sqrt of cumulative squared gradient
+  uint32_t* cnt;      // [cap]  feature count (difacto)
+  int32_t* vrow;      // [cap]  row into V slab, -1 = no embedding
+  float* V;           // [vcap * vstride]
+  float* VG;          // [vcap * vstride] AdaGrad accumulators of V
+  int32_t* vnext;     // [1] bump allocator for V rows
+  int64_t* stats;     // [8]  0:new_w 1:new_V 2:insert_fail 3:vslab_full 4:n_keys
+  int64_t cap;        // power of two
+  int64_t vcap;
+  int vstride;        // padded embedding stride (multiple of 4), 0 = linear
+  int dim;            // logical embedding dim
+};
+// find (insert=0) or find-or-insert (insert=1) each key; slot=-1 when absent
+void kv_find(const KVTable& t, const uint64_t* keys, int64_t n, int insert, int32_t* slot,
+             hipStream_t s);
+// dump: indices of occupied slots (compaction); out_n[0] receives the count
+void kv_occupied(const KVTable& t, int32_t* out_slots, int64_t* out_n, hipStream_t s);
+
+// ------------------------------------------------------------ linear optim
+// algo: 1 SGD, 2 AdaGrad, 3 FTRL (reference learn/linear/async_sgd.h:71-180)
+struct LinearHP {
+  int algo;
+  float alpha, beta, l1, l2;
+  float sgd_eta;  // SGD only: (beta + sqrt(t)) / alpha for this push
+};
+void linear_pull(const KVTable& t, const int32_t* slot, int64_t n, float* out, hipStream_t s);
+void linear_push(const KVTable& t, const int32_t* slot, const float* grad, int64_t n,
+                 LinearHP hp, hipStream_t s);
+
+// ----------------------------------------------------------- difacto optim
+struct DifactoHP {
+  float alpha, beta, l1, l2;       // FTRL on w
+  float v_alpha, v_beta, v_l2;     // AdaGrad on V
+  float v_init;                    // V ~ U[-v_init, v_init]
+  uint32_t threshold;              // allocate V once cnt > threshold
+  int l1_shrk;
+  uint64_t seed;
+};
+// add feature counts (reference AdaGradHandle::Push with kPushFeaCnt)
+void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt, int64_t n,
+                      DifactoHP hp, hipStream_t s);
+// pull rows [w, flag, 0, 0, V(vstride)] with row stride vstride+4
+void difacto_pull(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk, float* out,
+                  hipStream_t s);
+// push gradient rows in the same layout (flag!=0 => V gradient present)
+void difacto_push(const KVTable& t, const int32_t* slot, const float* grad, int64_t n,
+                  DifactoHP hp, hipStream_t s);
+
+// ---------------------------------------------------------------- fm.hip
+// Forward of FM / linear model on a localized minibatch.
+//   pulled rows: stride = vstride + 4 (difacto) or 1 (linear, vstride == 0)
+//   loss: 1 square, 2 logit, 4 squared hinge
+//   met[0..3] += {objv, objv_w, correct(threshold 0), n}  (double)
+void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
+                const float* pulled, int vstride, const float* label, int loss, float* py,
+                float* dual, float* xv, double* met, hipStream_t s);
+// Backward: gradient rows (same stride as pulled) for every local key.
+//   gw_k = sum_i dual_i x_ik
+//   gV_k = sum_i dual_i x_ik xv_i - (sum_i dual_i x_ik^2) V_k     (keys with flag)
+// work: chunk scratch, see fm_bwd_work_elems
+int64_t fm_bwd_chunks_bound(int64_t nuniq, int64_t nnz);
+void fm_backward(int64_t nuniq, const int64_t* csc_off, const int32_t* csc_row,
+                 const float* csc_val, const float* dual, const float* xv, const float* pulled,
+                 int vstride, float* grad, int32_t* chunk_key, int32_t* chunk_beg,
+                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, int64_t chunk_cap,
+                 hipStream_t s);
+// post-process V gradients: clip to [-c, c] (c>0), dropout with prob p (p>0)
+void fm_grad_post(int64_t nuniq, float* grad, int vstride, int dim, float clip, float dropout,
+                  uint64_t seed, double* sumsq, hipStream_t s);
+void fm_grad_scale(int64_t nuniq, float* grad, int vstride, const double* sumsq,
+                   hipStream_t s);
+
+// ------------------------------------------------------------ metrics.hip
+// exact per-minibatch AUC (reference BinClassEval::AUC) from predictions
+// sorted ascending: area = sum over negatives of #positives ranked below.
+void auc_from_sorted(const float* label_sorted, int64_t n, double* out, int64_t* tmp_i64,
+                     hipStream_t s);
+
+// ------------------------------------------------------------ synth.hip
+// Criteo-1TB-shaped synthetic minibatch: 13 integer + 26 categorical fields,
+// power-law value ranks per field, keys hashed as (h>>10)|(field<<54)
+// (reference learn/base/criteo_parser.h:64-86), labels from a hidden
+// logistic model so the learners have signal.
+void synth_criteo(int64_t nrows, uint64_t seed, uint64_t step, const int64_t* card,
+                  int nfield, uint64_t* keys, float* label, int64_t* offset, hipStream_t s);
+
+// -------------------------------------------------------------- exchange
+// gather rows: out[i, :] = in[idx[i], :]   (row width in floats)
+void gather_rows(const float* in, const int32_t* idx, int64_t n, int width, float* out,
+                 hipStream_t s);
+
+}  // namespace wh

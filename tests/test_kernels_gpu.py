@@ -1,0 +1,242 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references
+(wormhole_amd.ops.ref) and the host parameter store (kv.cpu_store)."""
+import numpy as np
+import pytest
+import torch
+
+from wormhole_amd.ops import ref
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def hip():
+    from wormhole_amd import _native
+    return _native.hip()
+
+
+def _rand_batch(nrows, nnz_per_row, nkeys, seed, with_val=False, skew=True):
+    g = torch.Generator().manual_seed(seed)
+    lens = torch.randint(1, 2 * nnz_per_row, (nrows,), generator=g)
+    off = torch.zeros(nrows + 1, dtype=torch.int64)
+    off[1:] = torch.cumsum(lens, 0)
+    nnz = int(off[-1])
+    if skew:
+        u = torch.rand(nnz, generator=g)
+        ids = (torch.exp(u * np.log(nkeys)) - 1).long()
+    else:
+        ids = torch.randint(0, nkeys, (nnz,), generator=g)
+    keys = ids * 0x9E3779B97F4A7C15 % (1 << 62) + 7
+    val = torch.rand(nnz, generator=g) + 0.5 if with_val else None
+    label = (torch.rand(nrows, generator=g) < 0.3).float()
+    return keys, off, val, label
+
+
+def test_scan(hip):
+    for n in [0, 1, 5, 2047, 2048, 2049, 100000, 3_000_001]:
+        x = torch.randint(0, 7, (n,), dtype=torch.int32, device=DEV)
+        o = hip.scan_excl(x)
+        exp = torch.zeros(n + 1, dtype=torch.int64, device=DEV)
+        exp[1:] = torch.cumsum(x.long(), 0)
+        assert torch.equal(o, exp), n
+
+
+@pytest.mark.parametrize("nshard", [1, 3, 8])
+@pytest.mark.parametrize("with_val", [False, True])
+def test_localize(hip, nshard, with_val):
+    keys, off, val, _ = _rand_batch(3000, 20, 5000, 1, with_val)
+    k, o = keys.to(DEV), off.to(DEV)
+    v = val.to(DEV) if val is not None else None
+    uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = hip.localize(k, o, v, nshard)
+    ru = torch.unique(keys)
+    assert uniq.numel() == ru.numel()
+    assert torch.equal(torch.sort(uniq.cpu()).values, ru)
+    # lid maps every non-zero back to its key
+    assert torch.equal(uniq[lid.long()].cpu(), keys)
+    # counts
+    cnt_ref = torch.bincount(lid.long().cpu(), minlength=uniq.numel())
+    assert torch.equal(ucnt.cpu().long(), cnt_ref)
+    # grouping by owner
+    own = ref.owner_of(uniq.cpu(), nshard)
+    assert torch.equal(torch.bincount(own, minlength=nshard), owner_cnt)
+    assert bool((own[1:] >= own[:-1]).all())
+    # CSC: occurrence rows of each key
+    rows = torch.repeat_interleave(torch.arange(3000), off[1:] - off[:-1])
+    assert torch.equal(csc_off.cpu()[1:] - csc_off.cpu()[:-1], cnt_ref)
+    cr = csc_row.cpu().long()
+    keyof = torch.repeat_interleave(torch.arange(uniq.numel()), cnt_ref)
+    pairs = torch.sort(keyof * 10_000 + cr).values
+    pairs_ref = torch.sort(lid.cpu().long() * 10_000 + rows).values
+    assert torch.equal(pairs, pairs_ref)
+    if with_val:
+        # values follow their non-zeros
+        got = torch.sort(keyof.double() * 1e4 + cr.double() + csc_val.cpu().double() / 10).values
+        exp = torch.sort(lid.cpu().double() * 1e4 + rows.double() + val.double() / 10).values
+        assert torch.allclose(got, exp)
+
+
+def _pulled(U, vstride, dim, seed, frac_v=0.6):
+    g = torch.Generator().manual_seed(seed)
+    p = torch.zeros(U, vstride + 4)
+    p[:, 0] = torch.randn(U, generator=g) * 0.3
+    flag = torch.rand(U, generator=g) < frac_v
+    p[:, 1] = flag.float()
+    V = torch.randn(U, vstride, generator=g) * 0.2
+    V[:, dim:] = 0
+    p[:, 4:] = V * flag[:, None]
+    return p
+
+
+@pytest.mark.parametrize("dim", [5, 16, 64])
+@pytest.mark.parametrize("with_val", [False, True])
+def test_fm_forward_backward(hip, dim, with_val):
+    vs = ref.vstride_for(dim)
+    keys, off, val, label = _rand_batch(2000, 15, 3000, 2, with_val)
+    uniq, ucnt, oc, lid, csc_off, csc_row, csc_val = hip.localize(
+        keys.to(DEV), off.to(DEV), val.to(DEV) if val is not None else None, 1)
+    U = uniq.numel()
+    pulled = _pulled(U, vs, dim, 3)
+    met = torch.zeros(4, dtype=torch.float64, device=DEV)
+    py, dual, xv = hip.fm_forward(off.to(DEV), lid, val.to(DEV) if val is not None else None,
+                                  pulled.to(DEV), vs, label.to(DEV), 2, met)
+    met_r = torch.zeros(4, dtype=torch.float64)
+    py_r, dual_r, xv_r = ref.fm_forward(off, lid.cpu(), val, pulled, vs, label, 2, met_r)
+    assert torch.allclose(py.cpu(), py_r, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(dual.cpu(), dual_r, atol=1e-5, rtol=1e-4)
+    assert torch.allclose(xv.cpu(), xv_r, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(met.cpu(), met_r, rtol=1e-5)
+    grad = hip.fm_backward(csc_off, csc_row, csc_val if with_val else None, dual, xv,
+                           pulled.to(DEV), vs)
+    grad_r = ref.fm_backward(csc_off.cpu(), csc_row.cpu(), csc_val.cpu() if with_val else None,
+                             dual.cpu(), xv.cpu(), pulled, vs)
+    gr = grad.cpu()
+    assert torch.allclose(gr[:, 0], grad_r[:, 0], atol=1e-4, rtol=1e-3)
+    assert torch.equal(gr[:, 1], grad_r[:, 1])
+    flag = grad_r[:, 1] != 0
+    assert torch.allclose(gr[flag][:, 4:], grad_r[flag][:, 4:], atol=1e-4, rtol=1e-3)
+
+
+@pytest.mark.parametrize("loss", [1, 2, 4])
+def test_linear_forward_backward(hip, loss):
+    keys, off, val, label = _rand_batch(5000, 30, 20000, 4, True)
+    uniq, ucnt, oc, lid, csc_off, csc_row, csc_val = hip.localize(
+        keys.to(DEV), off.to(DEV), val.to(DEV), 1)
+    w = torch.randn(uniq.numel()) * 0.1
+    met = torch.zeros(4, dtype=torch.float64, device=DEV)
+    py, dual, _ = hip.fm_forward(off.to(DEV), lid, val.to(DEV), w.to(DEV), 0, label.to(DEV),
+                                 loss, met)
+    met_r = torch.zeros(4, dtype=torch.float64)
+    py_r, dual_r, _ = ref.fm_forward(off, lid.cpu(), val, w, 0, label, loss, met_r)
+    assert torch.allclose(py.cpu(), py_r, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(dual.cpu(), dual_r, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(met.cpu(), met_r, rtol=1e-5)
+    g = hip.fm_backward(csc_off, csc_row, csc_val, dual, None, w.to(DEV), 0)
+    g_r = ref.fm_backward(csc_off.cpu(), csc_row.cpu(), csc_val.cpu(), dual.cpu(), None, w, 0)
+    assert torch.allclose(g.cpu(), g_r, atol=1e-3, rtol=1e-3)
+
+
+def test_auc(hip):
+    g = torch.Generator().manual_seed(5)
+    for n in [10, 1000, 100000]:
+        py = torch.randn(n, generator=g)
+        lab = (torch.rand(n, generator=g) < torch.sigmoid(py)).float()
+        a = hip.auc(py.to(DEV), lab.to(DEV)).cpu()
+        r = ref.auc(py, lab)
+        assert abs(float(a) - float(r)) < 1e-9
+    one = hip.auc(torch.randn(50, device=DEV), torch.ones(50, device=DEV))
+    assert float(one) == 1.0
+
+
+@pytest.mark.parametrize("algo", [1, 2, 3])
+def test_linear_store_updates(hip, algo):
+    from wormhole_amd.kv.cpu_store import CpuKVStore
+    gs = hip.KVStore(1 << 12, 0, 0, 0)
+    cs = CpuKVStore(1 << 12, 0, 0)
+    g = torch.Generator().manual_seed(algo)
+    keys = torch.randint(0, 1 << 40, (1000,), generator=g)
+    keys = torch.unique(keys)
+    for it in range(5):
+        sel = keys[torch.randperm(keys.numel(), generator=g)[:600]]
+        grad = torch.randn(sel.numel(), generator=g)
+        s_g = gs.find(sel.to(DEV), True)
+        s_c = cs.find(sel, True)
+        eta = (1.0 + (it + 1) ** 0.5) / 0.1
+        gs.linear_push(s_g, grad.to(DEV), algo, 0.1, 1.0, 0.3, 0.05, eta)
+        cs.linear_push(s_c, grad, algo, 0.1, 1.0, 0.3, 0.05, eta)
+    s_g = gs.find(keys.to(DEV), False)
+    s_c = cs.find(keys, False)
+    assert torch.allclose(gs.linear_pull(s_g).cpu(), cs.linear_pull(s_c), atol=1e-5, rtol=1e-4)
+    assert int(gs.stats[0]) == int(cs.stats[0])
+    assert int(gs.stats[4]) == keys.numel()
+
+
+@pytest.mark.parametrize("dim", [5, 64])
+def test_difacto_store_updates(hip, dim):
+    from wormhole_amd.kv.cpu_store import CpuKVStore
+    gs = hip.KVStore(1 << 12, 1 << 10, dim, 0)
+    cs = CpuKVStore(1 << 12, 1 << 10, dim)
+    vs = gs.vstride
+    hp = [0.05, 1.0, 0.01, 0.1, 0.02, 1.0, 0.5, 0.01]
+    g = torch.Generator().manual_seed(dim)
+    keys = torch.unique(torch.randint(0, 1 << 40, (800,), generator=g))
+    for it in range(6):
+        sel = keys[torch.randperm(keys.numel(), generator=g)[:500]]
+        cnt = torch.randint(1, 4, (sel.numel(),), generator=g).float()
+        s_g = gs.find(sel.to(DEV), True)
+        s_c = cs.find(sel, True)
+        gs.difacto_push_cnt(s_g, cnt.to(DEV), hp, 3, True, 42)
+        cs.difacto_push_cnt(s_c, cnt, hp, 3, True, 42)
+        p_g = gs.difacto_pull(s_g, True).cpu()
+        p_c = cs.difacto_pull(s_c, True)
+        assert torch.allclose(p_g[:, :2], p_c[:, :2], atol=1e-5, rtol=1e-4), it
+        fl = p_c[:, 1] != 0
+        assert torch.allclose(p_g[fl][:, 4:], p_c[fl][:, 4:], atol=1e-5, rtol=1e-4), it
+        grad = torch.randn(sel.numel(), vs + 4, generator=g) * 0.5
+        grad[:, 1] = p_c[:, 1]
+        grad[:, 2:4] = 0
+        gs.difacto_push(s_g, grad.to(DEV), hp, 3, True, 42)
+        cs.difacto_push(s_c, grad, hp, 3, True, 42)
+    s_g = gs.find(keys.to(DEV), False)
+    s_c = cs.find(keys, False)
+    p_g = gs.difacto_pull(s_g, False).cpu()
+    p_c = cs.difacto_pull(s_c, False)
+    assert torch.allclose(p_g[:, :2], p_c[:, :2], atol=1e-5, rtol=1e-4)
+    fl = p_c[:, 1] != 0
+    assert fl.any()
+    assert torch.allclose(p_g[fl][:, 4:], p_c[fl][:, 4:], atol=1e-5, rtol=1e-4)
+    assert int(gs.stats[0]) == int(cs.stats[0])
+    assert int(gs.stats[1]) == int(cs.stats[1])
+
+
+def test_synth_criteo(hip):
+    from wormhole_amd.data.synthetic import CRITEO_TB_CARD
+    card = torch.tensor(CRITEO_TB_CARD, dtype=torch.int64, device=DEV)
+    keys, label, off = hip.synth_criteo(10000, 1, 0, card)
+    assert keys.numel() == 390000 and off[-1].item() == 390000
+    f = (keys.cpu() >> 54) & 1023
+    assert torch.equal(f.view(10000, 39), torch.arange(39).expand(10000, 39))
+    ctr = float(label.mean())
+    assert 0.05 < ctr < 0.6
+    keys2, _, _ = hip.synth_criteo(10000, 1, 0, card)
+    assert torch.equal(keys, keys2)
+
+
+def test_difacto_learner_matches_cpu(hip):
+    """A few GPU training steps track the CPU reference path."""
+    from wormhole_amd.config.schema import DifactoConfig, Embedding
+    from wormhole_amd.models.difacto import DifactoLearner
+    from wormhole_amd.parallel.comm import Comm
+    emb = Embedding(dim=8, threshold=2)
+    conf = DifactoConfig(embedding=[emb], lambda_l1=0.01)
+    lg = DifactoLearner(conf, Comm(DEV, init=False), DEV, cap=1 << 14, vcap=1 << 12, seed=5)
+    lc = DifactoLearner(conf, Comm(torch.device("cpu"), init=False), "cpu", cap=1 << 14,
+                        vcap=1 << 12, seed=5)
+    for step in range(4):
+        keys, off, val, label = _rand_batch(400, 10, 800, 10 + step)
+        lg.process(keys.to(DEV), off.to(DEV), None, label.to(DEV), 0, 0)
+        lc.process(keys, off, None, label, 0, 0)
+    pg, pc = lg.take_progress(), lc.take_progress()
+    assert abs(pg[0] - pc[0]) / pc[0] < 1e-3
+    assert abs(pg[1] - pc[1]) < 1e-3
+    assert pg[6] == pc[6] and pg[7] == pc[7]

@@ -1,0 +1,94 @@
+"""Sharded key-value parameter store (the ps-lite server group, re-designed).
+
+Every GPU process owns one shard: keys with ``mix64b(key) % P == rank`` live
+in its HBM table (:class:`wormhole_amd._hip.KVStore`).  A minibatch's unique
+keys are already grouped by owner by ``localize``, so a pull is
+
+    all_to_all_v(keys) -> owner find/insert -> owner gather -> all_to_all_v(values)
+
+and a push sends only the values back along the same splits (the keys and
+owner-side slots are cached for the minibatch: ps-lite's KEY_CACHING filter).
+Owner-side updates are applied per source rank in rank order, so each
+worker's push is one atomic update like a ps-lite server request.
+"""
+import torch
+
+from .. import _native
+from .cpu_store import CpuKVStore
+
+
+def make_store(cap, vcap, dim, device):
+    device = torch.device(device)
+    if device.type == "cuda":
+        return _native.hip().KVStore(int(cap), int(vcap), int(dim), device.index or 0)
+    return CpuKVStore(cap, vcap, dim)
+
+
+class Session:
+    """Per-minibatch exchange state (keys sent once, splits reused)."""
+
+    __slots__ = ("send", "recv", "keys", "slots")
+
+    def __init__(self, send, recv, keys):
+        self.send = send
+        self.recv = recv
+        self.keys = keys
+        self.slots = None
+
+    def segments(self):
+        b = 0
+        for n in self.recv:
+            yield b, b + n
+            b += n
+
+
+class ShardedKV:
+    def __init__(self, store, comm):
+        self.store = store
+        self.comm = comm
+        self.nshard = comm.size
+        self.push_count = 0  # number of push requests applied (SGD's t)
+
+    def open(self, uniq, owner_cnt, insert):
+        send = [int(x) for x in (owner_cnt.tolist() if hasattr(owner_cnt, "tolist") else owner_cnt)]
+        if self.nshard == 1:
+            sess = Session(send, send, uniq)
+        else:
+            recv = self.comm.exchange_counts(send)
+            sess = Session(send, recv, self.comm.all_to_all_v(uniq, send, recv))
+        sess.slots = self.store.find(sess.keys, insert)
+        return sess
+
+    def _to_owner(self, sess, x):
+        return x if self.nshard == 1 else self.comm.all_to_all_v(x, sess.send, sess.recv)
+
+    def _to_worker(self, sess, x):
+        return x if self.nshard == 1 else self.comm.all_to_all_v(x, sess.recv, sess.send)
+
+    # ---------------------------------------------------------------- linear
+    def linear_pull(self, sess):
+        return self._to_worker(sess, self.store.linear_pull(sess.slots))
+
+    def linear_push(self, sess, grad, algo, alpha, beta, l1, l2):
+        g = self._to_owner(sess, grad.reshape(-1).contiguous())
+        for a, b in sess.segments():
+            self.push_count += 1
+            eta = (beta + float(self.push_count) ** 0.5) / alpha
+            if b > a:
+                self.store.linear_push(sess.slots[a:b], g[a:b], algo, alpha, beta, l1, l2, eta)
+
+    # --------------------------------------------------------------- difacto
+    def difacto_push_cnt(self, sess, cnt, hp, threshold, l1_shrk, seed):
+        c = self._to_owner(sess, cnt)
+        for a, b in sess.segments():
+            if b > a:
+                self.store.difacto_push_cnt(sess.slots[a:b], c[a:b], hp, threshold, l1_shrk, seed)
+
+    def difacto_pull(self, sess, l1_shrk):
+        return self._to_worker(sess, self.store.difacto_pull(sess.slots, l1_shrk))
+
+    def difacto_push(self, sess, grad, hp, threshold, l1_shrk, seed):
+        g = self._to_owner(sess, grad)
+        for a, b in sess.segments():
+            if b > a:
+                self.store.difacto_push(sess.slots[a:b], g[a:b], hp, threshold, l1_shrk, seed)

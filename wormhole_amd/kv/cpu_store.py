@@ -1,0 +1,276 @@
+"""Host (CPU) parameter store with the same interface and update math as the
+device store ``wormhole_amd._hip.KVStore``.
+
+Used for the GPU-free plumbing configuration and as the oracle of the fused
+update kernels in tests.  Update rules follow the reference handles:
+linear SGD/AdaGrad/FTRL (learn/linear/async_sgd.h:71-180) and DiFacto
+FTRL-w + AdaGrad-V with lazy V allocation (learn/difacto/async_sgd.h:214-296).
+"""
+import numpy as np
+import torch
+
+_M = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64(x):
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = x ^ (x >> np.uint64(30))
+        x = x * np.uint64(0xbf58476d1ce4e5b9)
+        x = x ^ (x >> np.uint64(27))
+        x = x * np.uint64(0x94d049bb133111eb)
+        x = x ^ (x >> np.uint64(31))
+    return x
+
+
+def uhash01(seed, a, b):
+    """Same counter-based uniform as wh::uhash01 (device)."""
+    a = np.asarray(a, dtype=np.uint64)
+    b = np.asarray(b, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        inner = _mix64(a * np.uint64(0x9e3779b97f4a7c15) + b)
+        h = _mix64(np.uint64(seed & 0xFFFFFFFFFFFFFFFF) ^ inner)
+    return (h >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+
+
+def _vstride(dim):
+    if dim == 0:
+        return 0
+    q, p = (dim + 3) // 4, 1
+    while p < q:
+        p <<= 1
+    return 4 * p
+
+
+class CpuKVStore:
+    def __init__(self, cap=1 << 16, vcap=1 << 14, dim=0, device=None):
+        self.dim = int(dim)
+        self.vstride = _vstride(self.dim)
+        self.cap = int(cap)
+        self.vcap = int(vcap) if dim > 0 else 0
+        self._index = {}
+        n = 0
+        self._keys = np.zeros(64, dtype=np.int64)
+        self._w = np.zeros(64, dtype=np.float32)
+        self._z = np.zeros(64, dtype=np.float32)
+        self._sq = np.zeros(64, dtype=np.float32)
+        self._cnt = np.zeros(64, dtype=np.uint32)
+        self._vrow = np.full(64, -1, dtype=np.int32)
+        self._V = np.zeros((16, max(self.vstride, 1)), dtype=np.float32)
+        self._VG = np.zeros((16, max(self.vstride, 1)), dtype=np.float32)
+        self._n = n
+        self._vnext = 0
+        self._stats = np.zeros(8, dtype=np.int64)
+
+    # ---------------------------------------------------------------- views
+    @property
+    def keys(self):
+        return torch.from_numpy(self._keys[: self._n].copy())
+
+    @property
+    def w(self):
+        return torch.from_numpy(self._w[: self._n].copy())
+
+    @property
+    def z(self):
+        return torch.from_numpy(self._z[: self._n].copy())
+
+    @property
+    def sq(self):
+        return torch.from_numpy(self._sq[: self._n].copy())
+
+    @property
+    def cnt(self):
+        return torch.from_numpy(self._cnt[: self._n].astype(np.int32))
+
+    @property
+    def vrow(self):
+        return torch.from_numpy(self._vrow[: self._n].copy())
+
+    @property
+    def V(self):
+        return torch.from_numpy(self._V[: self._vnext].copy())
+
+    @property
+    def VG(self):
+        return torch.from_numpy(self._VG[: self._vnext].copy())
+
+    @property
+    def vnext(self):
+        return torch.tensor([self._vnext], dtype=torch.int32)
+
+    @property
+    def stats(self):
+        return torch.from_numpy(self._stats)  # shares memory (like the device store)
+
+    def occupied(self):
+        return torch.arange(self._n, dtype=torch.int32)
+
+    # ---------------------------------------------------------------- index
+    def _grow(self, need):
+        cur = self._keys.shape[0]
+        if need <= cur:
+            return
+        new = max(need, cur * 2)
+        for name, fill in (("_keys", 0), ("_w", 0), ("_z", 0), ("_sq", 0), ("_cnt", 0),
+                           ("_vrow", -1)):
+            a = getattr(self, name)
+            b = np.full(new, fill, dtype=a.dtype)
+            b[:cur] = a
+            setattr(self, name, b)
+
+    def _grow_v(self, need):
+        cur = self._V.shape[0]
+        if need <= cur:
+            return
+        new = max(need, cur * 2)
+        for name in ("_V", "_VG"):
+            a = getattr(self, name)
+            b = np.zeros((new, a.shape[1]), dtype=np.float32)
+            b[:cur] = a
+            setattr(self, name, b)
+
+    def find(self, keys, insert):
+        ks = keys.cpu().numpy().astype(np.int64)
+        out = np.empty(ks.shape[0], dtype=np.int32)
+        idx = self._index
+        for i, k in enumerate(ks.tolist()):
+            s = idx.get(k)
+            if s is None:
+                if insert:
+                    if self._n >= self.cap:
+                        self._stats[2] += 1
+                        s = -1
+                    else:
+                        s = self._n
+                        self._grow(s + 1)
+                        self._keys[s] = k
+                        idx[k] = s
+                        self._n += 1
+                        self._stats[4] += 1
+                else:
+                    s = -1
+            out[i] = s
+        return torch.from_numpy(out)
+
+    # --------------------------------------------------------------- linear
+    @staticmethod
+    def _solve(z, eta, l1, l2):
+        out = (z - np.sign(z) * l1) / (eta + l2)
+        return np.where(np.abs(z) <= l1, 0.0, out).astype(np.float32)
+
+    def _count_delta(self, old, new):
+        self._stats[0] += int(((old == 0) & (new != 0)).sum()) - int(((old != 0) & (new == 0)).sum())
+
+    def linear_pull(self, slot):
+        s = slot.cpu().numpy()
+        out = np.where(s >= 0, self._w[np.maximum(s, 0)], 0.0).astype(np.float32)
+        return torch.from_numpy(out)
+
+    def linear_push(self, slot, grad, algo, alpha, beta, l1, l2, sgd_eta):
+        s = slot.cpu().numpy()
+        g = grad.cpu().numpy().reshape(-1)[: s.shape[0]].astype(np.float32)
+        m = s >= 0
+        s, g = s[m], g[m]
+        old = self._w[s].copy()
+        f32 = np.float32
+        if algo == 1:
+            new = self._solve(f32(sgd_eta) * old - g, f32(sgd_eta), f32(l1), f32(l2))
+        elif algo == 2:
+            sq = np.sqrt(self._sq[s] * self._sq[s] + g * g).astype(np.float32)
+            self._sq[s] = sq
+            eta = (sq + f32(beta)) / f32(alpha)
+            new = self._solve(eta * old - g, eta, f32(l1), f32(l2))
+        else:
+            sq0 = self._sq[s]
+            sq = np.sqrt(sq0 * sq0 + g * g).astype(np.float32)
+            self._sq[s] = sq
+            sigma = (sq - sq0) / f32(alpha)
+            z = self._z[s] + g - sigma * old
+            self._z[s] = z
+            new = self._solve(-z, (f32(beta) + sq) / f32(alpha), f32(l1), f32(l2))
+        self._w[s] = new
+        self._count_delta(old, new)
+
+    # -------------------------------------------------------------- difacto
+    def _alloc_v(self, s, seed, v_init):
+        row = self._vnext
+        self._vnext += 1
+        if row >= self.vcap:
+            self._stats[3] += 1
+            return -1
+        self._grow_v(row + 1)
+        self._vrow[s] = row
+        d = np.arange(self.vstride, dtype=np.uint64)
+        u = uhash01(seed, np.uint64(np.int64(self._keys[s]).view(np.uint64)), d)
+        v = ((u * np.float32(2) - np.float32(1)) * np.float32(v_init)).astype(np.float32)
+        v[self.dim:] = 0
+        self._V[row] = v
+        self._VG[row] = 0
+        self._stats[1] += self.dim
+        return row
+
+    def difacto_push_cnt(self, slot, cnt, h, threshold, l1_shrk, seed):
+        s_all = slot.cpu().numpy()
+        c_all = cnt.cpu().numpy()
+        for s, c in zip(s_all.tolist(), c_all.tolist()):
+            if s < 0:
+                continue
+            self._cnt[s] = np.uint32(int(self._cnt[s]) + int(c))
+            if (self.vstride > 0 and self._cnt[s] > threshold and self._vrow[s] < 0
+                    and (not l1_shrk or self._w[s] != 0)):
+                self._alloc_v(s, seed, h[7])
+
+    def difacto_pull(self, slot, l1_shrk):
+        s_all = slot.cpu().numpy()
+        st = self.vstride + 4
+        out = np.zeros((s_all.shape[0], st), dtype=np.float32)
+        for i, s in enumerate(s_all.tolist()):
+            if s < 0:
+                continue
+            w = self._w[s]
+            row = self._vrow[s]
+            if l1_shrk and w == 0:
+                row = -1
+            out[i, 0] = w
+            if row >= 0:
+                out[i, 1] = 1.0
+                out[i, 4:] = self._V[row]
+        return torch.from_numpy(out)
+
+    def difacto_push(self, slot, grad, h, threshold, l1_shrk, seed):
+        alpha, beta, l1, l2, v_alpha, v_beta, v_l2, v_init = [np.float32(x) for x in h]
+        s_all = slot.cpu().numpy()
+        g_all = grad.cpu().numpy().reshape(s_all.shape[0], -1)
+        for i, s in enumerate(s_all.tolist()):
+            if s < 0:
+                continue
+            gr = g_all[i]
+            g = np.float32(gr[0])
+            w = self._w[s]
+            g = np.float32(g + l2 * w)
+            cg = self._sq[s]
+            cg_new = np.float32(np.sqrt(cg * cg + g * g))
+            self._sq[s] = cg_new
+            z = np.float32(self._z[s] - (g - (cg_new - cg) / alpha * w))
+            self._z[s] = z
+            if -l1 <= z <= l1:
+                nw = np.float32(0)
+            else:
+                eta = (beta + cg_new) / alpha
+                nw = np.float32((z - l1 if z > 0 else z + l1) / eta)
+            self._w[s] = nw
+            if w == 0 and nw != 0:
+                self._stats[0] += 1
+                if self.vstride > 0 and self._cnt[s] > threshold and self._vrow[s] < 0:
+                    self._alloc_v(s, seed, v_init)
+            elif w != 0 and nw == 0:
+                self._stats[0] -= 1
+            if self.vstride > 0 and gr[1] != 0:
+                row = self._vrow[s]
+                if row >= 0:
+                    v = self._V[row]
+                    cgv = self._VG[row]
+                    gv = gr[4:].astype(np.float32) + v_l2 * v
+                    cgv[:] = np.sqrt(cgv * cgv + gv * gv)
+                    v -= v_alpha / (cgv + v_beta) * gv

@@ -1,0 +1,90 @@
+"""DiFacto: distributed factorization machines with frequency-adaptive
+embeddings (reference learn/difacto/).
+
+Per minibatch (reference AsyncWorker::ProcessMinibatch,
+learn/difacto/async_sgd.h:363-425), re-expressed on the GPU:
+
+  localize (device hash)  ->  key all-to-all  ->  [pass 0: push feature
+  counts; owner allocates V lazily for keys with cnt > threshold]  ->  pull
+  w / V (variable length: V only where allocated and, with l1_shrk, w != 0)
+  ->  fused FM forward + loss + metrics  ->  AUC  ->  fused FM backward
+  ->  gradient clip / dropout / normalisation  ->  push  ->  owner applies
+  FTRL on w and AdaGrad on V in one fused kernel.
+"""
+import torch
+
+from .. import ops
+from ..kv import ShardedKV, make_store
+
+TRAIN, VAL, PRED = 0, 1, 2
+
+
+class DifactoLearner:
+    def __init__(self, conf, comm, device, cap=1 << 22, vcap=1 << 20, seed=0):
+        self.conf = conf
+        self.comm = comm
+        self.device = torch.device(device)
+        emb = conf.embedding[0] if conf.embedding else None
+        self.dim = emb.dim if emb is not None else 0
+        self.emb = emb
+        self.vstride = ops.vstride_for(self.dim)
+        self.store = make_store(cap, vcap, self.dim, self.device)
+        self.kv = ShardedKV(self.store, comm)
+        self.seed = seed
+        self.l1_shrk = bool(conf.l1_shrk)
+        if emb is not None:
+            v_alpha = emb.lr_eta if emb.has("lr_eta") else conf.lr_eta
+            v_beta = emb.lr_beta if emb.has("lr_beta") else conf.lr_beta
+            self.hp = [conf.lr_eta, conf.lr_beta, conf.lambda_l1, conf.lambda_l2,
+                       v_alpha, v_beta, emb.lambda_l2, emb.init_scale]
+            self.threshold = int(emb.threshold)
+        else:
+            self.hp = [conf.lr_eta, conf.lr_beta, conf.lambda_l1, conf.lambda_l2,
+                       conf.lr_eta, conf.lr_beta, 0.0, 0.01]
+            self.threshold = 0
+        # device-side progress accumulators (read only when printing)
+        self.met = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self.auc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.n_mb = 0
+        self.step = 0
+
+    # ------------------------------------------------------------------ step
+    def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0):
+        """One minibatch. Returns predictions (py) for PRED, else None."""
+        train = wtype == TRAIN
+        uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = ops.localize(
+            keys, offset, val, self.kv.nshard)
+        sess = self.kv.open(uniq, owner_cnt, insert=train)
+        if train and data_pass == 0 and self.dim > 0:
+            self.kv.difacto_push_cnt(sess, ucnt.float(), self.hp, self.threshold,
+                                     self.l1_shrk, self.seed)
+        pulled = self.kv.difacto_pull(sess, self.l1_shrk)
+        py, dual, xv = ops.fm_forward(offset, lid, val, pulled, self.vstride, label,
+                                      ops.LOSS_LOGIT, self.met)
+        self.auc_sum += ops.auc(py, label)
+        self.n_mb += 1
+        if train:
+            grad = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, pulled, self.vstride)
+            if self.emb is not None:
+                ops.fm_grad_post(grad, self.vstride, self.dim, self.emb.grad_clipping,
+                                 self.emb.dropout, self.seed + 7919 * self.step + 1,
+                                 bool(self.emb.grad_normalization))
+            self.kv.difacto_push(sess, grad, self.hp, self.threshold, self.l1_shrk,
+                                 self.seed)
+        self.step += 1
+        return py if wtype == PRED else None
+
+    # -------------------------------------------------------------- progress
+    def take_progress(self):
+        """Progress vector in the reference layout (learn/difacto/progress.h):
+        [objv, auc, objv_w, copc, count, new_ex, new_w, new_V]; resets."""
+        m = self.met.tolist()
+        a = float(self.auc_sum.item())
+        st = self.store.stats
+        st_l = st.tolist()
+        prog = [m[0], a, m[1], 0.0, float(self.n_mb), m[3], float(st_l[0]), float(st_l[1])]
+        self.met.zero_()
+        self.auc_sum.zero_()
+        self.n_mb = 0
+        st[0:2].zero_()
+        return prog

@@ -1,0 +1,60 @@
+"""Linear models trained by asynchronous-style minibatch SGD / AdaGrad / FTRL
+with an L1/L2 proximal step (reference learn/linear/).
+
+Per minibatch (reference AsgdWorker::ProcessMinibatch,
+learn/linear/async_sgd.h:240-288): localize -> key all-to-all -> pull w ->
+fused SpMV forward + loss + dual + metrics -> AUC -> segmented SpMV^T
+backward -> push -> owner applies the fused proximal update.
+"""
+import torch
+
+from .. import ops
+from ..kv import ShardedKV, make_store
+
+TRAIN, VAL, PRED = 0, 1, 2
+
+
+class LinearLearner:
+    def __init__(self, conf, comm, device, cap=1 << 22, seed=0):
+        self.conf = conf
+        self.comm = comm
+        self.device = torch.device(device)
+        self.store = make_store(cap, 0, 0, self.device)
+        self.kv = ShardedKV(self.store, comm)
+        self.seed = seed
+        self.alpha = conf.lr_eta
+        self.beta = conf.lr_beta
+        self.met = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self.auc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.n_mb = 0
+
+    def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0):
+        train = wtype == TRAIN
+        uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = ops.localize(
+            keys, offset, val, self.kv.nshard)
+        sess = self.kv.open(uniq, owner_cnt, insert=train)
+        w = self.kv.linear_pull(sess)
+        py, dual, _ = ops.fm_forward(offset, lid, val, w, 0, label, self.conf.loss, self.met)
+        self.auc_sum += ops.auc(py, label)
+        self.n_mb += 1
+        if train:
+            grad = ops.fm_backward(csc_off, csc_row, csc_val, dual, None, w, 0)
+            self.kv.linear_push(sess, grad, self.conf.algo, self.alpha, self.beta,
+                                self.conf.lambda_l1, self.conf.lambda_l2)
+        return py if wtype == PRED else None
+
+    def take_progress(self):
+        """Reference layout (learn/linear/progress.h): [objv, acc, auc, count,
+        new_ex, new_w]; accuracy is the per-minibatch-mean convention."""
+        m = self.met.tolist()
+        a = float(self.auc_sum.item())
+        st = self.store.stats
+        new_w = float(st.tolist()[0])
+        st[0:1].zero_()
+        acc = m[2] / m[3] if m[3] else 0.0
+        acc = acc if acc > 0.5 else 1 - acc
+        prog = [m[0], acc * self.n_mb, a, float(self.n_mb), m[3], new_w]
+        self.met.zero_()
+        self.auc_sum.zero_()
+        self.n_mb = 0
+        return prog

@@ -1,0 +1,170 @@
+"""Plain-PyTorch reference implementations of every hot op.
+
+These are (a) the numerics oracle for the HIP kernel tests and (b) the
+execution path for CPU tensors (the reference's CPU plumbing configuration,
+e.g. ``dmlc_local.py -n 2 -s 1 bin/linear.dmlc demo.conf`` on a machine with
+no GPU).  They follow the reference formulas literally:
+
+* localize      learn/base/localizer.h:96-221
+* FM forward    learn/difacto/loss.h:53-94
+* FM backward   learn/difacto/loss.h:102-158
+* linear losses learn/linear/loss.h:92-157
+* AUC           learn/base/binary_class_evaluation.h:17-38
+"""
+import math
+
+import torch
+
+LOSS_SQUARE, LOSS_LOGIT, LOSS_SQUARE_HINGE = 1, 2, 4
+_M64 = (1 << 64) - 1
+
+
+def _u64(x):
+    return x & _M64
+
+
+def mix64b_int(x):
+    x = _u64(x)
+    x ^= x >> 33
+    x = _u64(x * 0xff51afd7ed558ccd)
+    x ^= x >> 33
+    x = _u64(x * 0xc4ceb9fe1a85ec53)
+    x ^= x >> 33
+    return x
+
+
+def owner_of(keys, nshard):
+    """Shard owner of each int64-encoded uint64 key (matches wh::owner_of)."""
+    if nshard <= 1:
+        return torch.zeros(keys.numel(), dtype=torch.int64, device=keys.device)
+    lst = keys.cpu().tolist()
+    own = [mix64b_int(k) % nshard for k in lst]
+    return torch.tensor(own, dtype=torch.int64, device=keys.device)
+
+
+def localize(keys, offset, val=None, nshard=1):
+    """Map feature ids to local ids grouped by owner; build the CSC.
+
+    Returns (uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val) with the
+    same meaning as the HIP ``_hip.localize``.  Within an owner bucket ids are
+    sorted by key (the HIP version uses table order; tests compare sets).
+    """
+    nnz = keys.numel()
+    dev = keys.device
+    uniq, inv, cnt = torch.unique(keys, sorted=True, return_inverse=True, return_counts=True)
+    own = owner_of(uniq, nshard)
+    order = torch.argsort(own * (1 << 0), stable=True)  # stable: keeps key order per owner
+    uniq = uniq[order]
+    cnt = cnt[order]
+    rank = torch.empty_like(order)
+    rank[order] = torch.arange(order.numel(), device=dev)
+    lid = rank[inv].to(torch.int32)
+    owner_cnt = torch.bincount(own, minlength=nshard).cpu()
+    nrows = offset.numel() - 1
+    rows = torch.repeat_interleave(torch.arange(nrows, device=dev), offset[1:] - offset[:-1])
+    perm = torch.argsort(lid.long(), stable=True)
+    csc_off = torch.zeros(uniq.numel() + 1, dtype=torch.int64, device=dev)
+    csc_off[1:] = torch.cumsum(cnt, 0)
+    csc_row = rows[perm].to(torch.int32)
+    csc_val = val[perm] if val is not None and val.numel() else torch.empty(0, device=dev)
+    return uniq, cnt.to(torch.int32), owner_cnt, lid, csc_off, csc_row, csc_val
+
+
+def _loss(loss, label, py):
+    if loss == LOSS_SQUARE:
+        d = py - label
+        return 0.5 * d * d, d
+    y = torch.where(label > 0, 1.0, -1.0).to(py.dtype)
+    if loss == LOSS_SQUARE_HINGE:
+        t = torch.clamp(1 - y * py, min=0)
+        return t * t, -2 * y * t
+    return torch.nn.functional.softplus(-y * py), -y / (1 + torch.exp(y * py))
+
+
+def fm_forward(offset, lid, val, pulled, vstride, label, loss, met):
+    """Returns (py, dual, xv); accumulates {objv, objv_w, correct, n} into met."""
+    nrows = offset.numel() - 1
+    dev = pulled.device
+    rows = torch.repeat_interleave(torch.arange(nrows, device=dev), offset[1:] - offset[:-1])
+    lid = lid.long()
+    x = val if (val is not None and val.numel()) else torch.ones(lid.numel(), device=dev)
+    if vstride == 0:
+        w = pulled.reshape(-1)
+        py = torch.zeros(nrows, device=dev).index_add_(0, rows, x * w[lid])
+        wsum = py
+        xv = torch.empty(0, device=dev)
+    else:
+        p = pulled.reshape(-1, vstride + 4)
+        w = p[:, 0]
+        flag = (p[:, 1] != 0).to(p.dtype)
+        V = p[:, 4:] * flag[:, None]
+        wsum = torch.zeros(nrows, device=dev).index_add_(0, rows, x * w[lid])
+        xv = torch.zeros(nrows, vstride, device=dev).index_add_(0, rows, x[:, None] * V[lid])
+        xxvv = torch.zeros(nrows, vstride, device=dev).index_add_(
+            0, rows, (x * x)[:, None] * V[lid] * V[lid])
+        py = wsum + 0.5 * (xv * xv - xxvv).sum(1)
+    objv, dual = _loss(loss, label, py)
+    objw, _ = _loss(loss, label, wsum)
+    correct = ((label > 0) & (py > 0)) | ((label <= 0) & (py <= 0))
+    met[0] += objv.double().sum().to(met.device)
+    met[1] += objw.double().sum().to(met.device)
+    met[2] += correct.double().sum().to(met.device)
+    met[3] += float(nrows)
+    return py, dual, xv.reshape(-1)
+
+
+def fm_backward(csc_off, csc_row, csc_val, dual, xv, pulled, vstride):
+    U = csc_off.numel() - 1
+    dev = dual.device
+    cnt = csc_off[1:] - csc_off[:-1]
+    key = torch.repeat_interleave(torch.arange(U, device=dev), cnt)
+    rows = csc_row.long()
+    x = csc_val if (csc_val is not None and csc_val.numel()) else torch.ones(rows.numel(), device=dev)
+    dx = dual[rows] * x
+    gw = torch.zeros(U, device=dev).index_add_(0, key, dx)
+    if vstride == 0:
+        return gw.reshape(U, 1)
+    p = pulled.reshape(U, vstride + 4)
+    flag = (p[:, 1] != 0)
+    V = p[:, 4:]
+    xvr = xv.reshape(-1, vstride)
+    acc = torch.zeros(U, vstride, device=dev).index_add_(0, key, dx[:, None] * xvr[rows])
+    xxp = torch.zeros(U, device=dev).index_add_(0, key, dx * x)
+    gV = acc - xxp[:, None] * V
+    grad = torch.zeros(U, vstride + 4, device=dev)
+    grad[:, 0] = gw
+    grad[:, 1] = flag.to(grad.dtype)
+    grad[:, 4:] = torch.where(flag[:, None], gV, torch.zeros_like(gV))
+    return grad
+
+
+def auc(py, label):
+    """Exact AUC with the reference's rank-sum convention (>= 0.5)."""
+    n = py.numel()
+    order = torch.argsort(py, stable=True)
+    lab = (label[order] > 0).double()
+    cum = torch.cumsum(lab, 0) - lab  # positives strictly before
+    tp = float(lab.sum())
+    if tp == 0 or tp == n:
+        return torch.ones(1, dtype=torch.float64, device=py.device)
+    area = float((cum * (1 - lab)).sum()) / (tp * (n - tp))
+    return torch.tensor([max(area, 1 - area)], dtype=torch.float64, device=py.device)
+
+
+def l1l2_solve(z, eta, l1, l2):
+    out = (z - torch.sign(z) * l1) / (eta + l2)
+    return torch.where(z.abs() <= l1, torch.zeros_like(z), out)
+
+
+def vstride_for(dim):
+    if dim == 0:
+        return 0
+    q = (dim + 3) // 4
+    p = 1
+    while p < q:
+        p <<= 1
+    return 4 * p
+
+
+def sigmoid(x):
+    return 1.0 / (1.0 + math.exp(-x))

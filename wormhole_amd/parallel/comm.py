@@ -1,0 +1,121 @@
+"""Collective communication: RCCL over xGMI on GPUs (torch.distributed backend
+"nccl" IS RCCL on ROCm), gloo on CPU.  One process per GPU.
+
+Replaces both of the reference's communication substrates:
+
+* rabit (BSP allreduce / broadcast; SURVEY §2.6 call sites) -> :meth:`allreduce`,
+  :meth:`broadcast`, :meth:`allgather_object`.
+* ps-lite KVWorker push/pull (ZPull/ZPush/ZVPull/ZVPush) -> :meth:`all_to_all_v`,
+  used by :class:`wormhole_amd.kv.ShardedKV` (keys sent once per minibatch,
+  values/gradients reuse the same splits = ps-lite's KEY_CACHING).
+"""
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank():
+    return int(os.environ.get("RANK", os.environ.get("DMLC_TASK_ID", "0")))
+
+
+def env_world():
+    return int(os.environ.get("WORLD_SIZE", os.environ.get("DMLC_NUM_WORKER", "1")))
+
+
+def env_local_rank():
+    return int(os.environ.get("LOCAL_RANK", "0"))
+
+
+class Comm:
+    """A process group handle.  ``size == 1`` needs no torch.distributed."""
+
+    def __init__(self, device=None, backend=None, init=True, timeout_s=600):
+        self.rank = env_rank()
+        self.size = env_world()
+        if device is None:
+            device = torch.device("cpu")
+        self.device = torch.device(device)
+        if backend is None:
+            backend = "nccl" if self.device.type == "cuda" else "gloo"
+        self.backend = backend
+        self.pg = None
+        if self.size > 1 and init:
+            if not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", "29500")
+                kw = dict(backend=backend, rank=self.rank, world_size=self.size,
+                          timeout=datetime.timedelta(seconds=timeout_s))
+                if backend == "nccl":
+                    kw["device_id"] = self.device
+                dist.init_process_group(**kw)
+            self.pg = dist.group.WORLD
+            self.rank = dist.get_rank()
+            self.size = dist.get_world_size()
+
+    # ----------------------------------------------------------- basics
+    def barrier(self):
+        if self.size > 1:
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device.index])
+            else:
+                dist.barrier()
+
+    def allreduce(self, t, op="sum"):
+        if self.size == 1:
+            return t
+        o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
+             "min": dist.ReduceOp.MIN}[op]
+        dist.all_reduce(t, op=o)
+        return t
+
+    def broadcast(self, t, root=0):
+        if self.size > 1:
+            dist.broadcast(t, src=root)
+        return t
+
+    def allgather_object(self, obj):
+        if self.size == 1:
+            return [obj]
+        out = [None] * self.size
+        dist.all_gather_object(out, obj)
+        return out
+
+    def allgather(self, t):
+        if self.size == 1:
+            return [t]
+        out = [torch.empty_like(t) for _ in range(self.size)]
+        dist.all_gather(out, t)
+        return out
+
+    # ----------------------------------------------------- all-to-all-v
+    def exchange_counts(self, send_counts):
+        """send_counts: python list (len size) -> recv_counts list."""
+        if self.size == 1:
+            return list(send_counts)
+        s = torch.tensor(send_counts, dtype=torch.int64, device=self.device)
+        r = torch.empty_like(s)
+        dist.all_to_all_single(r, s)
+        return r.tolist()
+
+    def all_to_all_v(self, x, send_rows, recv_rows):
+        """Row-wise all-to-all-v: rank p receives send_rows[p] rows of x from
+        this rank.  x may be 1-D or 2-D [rows, width]."""
+        if self.size == 1:
+            return x
+        width = x[0].numel() if x.dim() > 1 and x.shape[0] > 0 else (
+            x.shape[1] if x.dim() > 1 else 1)
+        shape = (sum(recv_rows),) + tuple(x.shape[1:])
+        out = torch.empty(shape, dtype=x.dtype, device=x.device)
+        if x.dim() == 1:
+            dist.all_to_all_single(out, x.contiguous(), recv_rows, send_rows)
+        else:
+            dist.all_to_all_single(out.view(-1), x.contiguous().view(-1),
+                                   [r * width for r in recv_rows],
+                                   [s * width for s in send_rows])
+        return out
+
+    def finalize(self):
+        if self.size > 1 and dist.is_initialized():
+            dist.destroy_process_group()
