@@ -59,48 +59,72 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
                                                      float* __restrict__ py_out,
                                                      float* __restrict__ dual_out,
                                                      float* __restrict__ xv, double* met) {
+  // G lanes own one row. Per round the group loads G of the row's non-zeros
+  // cooperatively (coalesced local ids, G independent header gathers), then
+  // walks the ones that carry an embedding four at a time, every lane
+  // gathering its float4 slice of each V row (four 16-byte loads in flight).
   __shared__ double sh[kThreads / 64];
-  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane - gl;
   const int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
   const int stride = vstride + 4;
+  const uint64_t gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << gbase);
   double m_objv = 0, m_objw = 0, m_corr = 0, m_n = 0;
-  if (row < nrows) {
-    float wsum = 0.f;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
-    const int64_t b = off[row], e = off[row + 1];
-    int64_t j = b;
-    for (; j + 1 < e; j += 2) {  // two independent gathers in flight
-      const int k0 = lid[j], k1 = lid[j + 1];
-      const float x0 = val ? val[j] : 1.f, x1 = val ? val[j + 1] : 1.f;
-      const float* r0 = pulled + (int64_t)k0 * stride;
-      const float* r1 = pulled + (int64_t)k1 * stride;
-      const float2 h0 = *reinterpret_cast<const float2*>(r0);
-      const float2 h1 = *reinterpret_cast<const float2*>(r1);
-      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-      if (h0.y != 0.f) v0 = reinterpret_cast<const float4*>(r0 + 4)[gl];
-      if (h1.y != 0.f) v1 = reinterpret_cast<const float4*>(r1 + 4)[gl];
-      wsum += x0 * h0.x + x1 * h1.x;
-      s.x += x0 * v0.x + x1 * v1.x; s.y += x0 * v0.y + x1 * v1.y;
-      s.z += x0 * v0.z + x1 * v1.z; s.w += x0 * v0.w + x1 * v1.w;
-      const float xx0 = x0 * x0, xx1 = x1 * x1;
-      q.x += xx0 * v0.x * v0.x + xx1 * v1.x * v1.x; q.y += xx0 * v0.y * v0.y + xx1 * v1.y * v1.y;
-      q.z += xx0 * v0.z * v0.z + xx1 * v1.z * v1.z; q.w += xx0 * v0.w * v0.w + xx1 * v1.w * v1.w;
+  const bool live = row < nrows;
+  float wl = 0.f;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  int64_t b = 0, e = 0;
+  if (live) {
+    b = off[row];
+    e = off[row + 1];
+  }
+  for (int64_t base = b; base < e; base += G) {
+    const int64_t j = base + gl;
+    const bool valid = j < e;
+    int k = 0;
+    float x = 0.f;
+    float2 h = make_float2(0.f, 0.f);
+    if (valid) {
+      k = lid[j];
+      x = val ? val[j] : 1.f;
+      h = *reinterpret_cast<const float2*>(pulled + (int64_t)k * stride);
     }
-    if (j < e) {
-      const int k0 = lid[j];
-      const float x0 = val ? val[j] : 1.f;
-      const float* r0 = pulled + (int64_t)k0 * stride;
-      const float2 h0 = *reinterpret_cast<const float2*>(r0);
-      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (h0.y != 0.f) v0 = reinterpret_cast<const float4*>(r0 + 4)[gl];
-      wsum += x0 * h0.x;
-      s.x += x0 * v0.x; s.y += x0 * v0.y; s.z += x0 * v0.z; s.w += x0 * v0.w;
-      const float xx0 = x0 * x0;
-      q.x += xx0 * v0.x * v0.x; q.y += xx0 * v0.y * v0.y;
-      q.z += xx0 * v0.z * v0.z; q.w += xx0 * v0.w * v0.w;
+    wl += x * h.x;
+    uint64_t mg = __ballot(valid && h.y != 0.f) & gmask;
+    while (mg) {
+      int t[4];
+      float keep[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (mg) {
+          t[u] = __ffsll((unsigned long long)mg) - 1;
+          mg &= mg - 1;
+          keep[u] = 1.f;
+        } else {
+          t[u] = t[0];
+          keep[u] = 0.f;
+        }
+      }
+      float4 v[4];
+      float xs[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ku = __shfl(k, t[u], 64);
+        xs[u] = __shfl(x, t[u], 64) * keep[u];
+        v[u] = reinterpret_cast<const float4*>(pulled + (int64_t)ku * stride + 4)[gl];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float xu = xs[u], xx = xu * xu;
+        s.x += xu * v[u].x; s.y += xu * v[u].y; s.z += xu * v[u].z; s.w += xu * v[u].w;
+        q.x += xx * v[u].x * v[u].x; q.y += xx * v[u].y * v[u].y;
+        q.z += xx * v[u].z * v[u].z; q.w += xx * v[u].w * v[u].w;
+      }
     }
-    float part = (s.x * s.x - q.x) + (s.y * s.y - q.y) + (s.z * s.z - q.z) + (s.w * s.w - q.w);
-    part = group_sum<G>(part);
+  }
+  const float wsum = group_sum<G>(wl);
+  float part = (s.x * s.x - q.x) + (s.y * s.y - q.y) + (s.z * s.z - q.z) + (s.w * s.w - q.w);
+  part = group_sum<G>(part);
+  if (live) {
     reinterpret_cast<float4*>(xv + row * vstride)[gl] = s;
     if (gl == 0) {
       const float p = wsum + 0.5f * part;
@@ -114,9 +138,6 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
       m_corr = ((y > 0.f && p > 0.f) || (y <= 0.f && p <= 0.f)) ? 1.0 : 0.0;
       m_n = 1.0;
     }
-  } else {
-    // keep every lane in the group_sum shuffle pattern
-    group_sum<G>(0.f);
   }
   double r;
   r = block_sum_d(m_objv, sh); if (threadIdx.x == 0) atomicAdd(met + 0, r); __syncthreads();
@@ -204,62 +225,90 @@ __global__ __launch_bounds__(kThreads) void k_fm_bwd(const int64_t* __restrict__
                                                      const float* __restrict__ xv,
                                                      const float* __restrict__ pulled, int vstride,
                                                      float* __restrict__ grad) {
-  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
-  const int64_t c = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
-  if (c >= *nchunk_p) return;
-  const int k = chunk_key[c];
-  const int64_t kb = csc_off[k], ke = csc_off[k + 1];
-  const int64_t b = chunk_beg[c];
-  const int64_t e = b + kChunk < ke ? b + kChunk : ke;
-  const bool multi = (ke - kb) > kChunk;
+  // ONE LANE PER CHUNK computes the scalar sums (gw, xxp) of its <= kChunk
+  // occurrences; the wave then runs the embedding-gradient jobs of the
+  // chunks whose key has V, G lanes per job (float4 slice of each xv row).
+  const int lane = threadIdx.x & 63;
+  const int64_t nch = *nchunk_p;
+  const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool live = c < nch;
   const int stride = vstride + 4;
-  const float* hdr = pulled + (int64_t)k * stride;
-  const bool flag = hdr[1] != 0.f;
+  int k = 0, b = 0, e = 0;
+  bool multi = false, flag = false;
   float gw = 0.f, xxp = 0.f;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (flag) {
-    int64_t p = b;
-    for (; p + 1 < e; p += 2) {
-      const int i0 = csc_row[p], i1 = csc_row[p + 1];
-      const float x0 = csc_val ? csc_val[p] : 1.f, x1 = csc_val ? csc_val[p + 1] : 1.f;
-      const float d0 = dual[i0] * x0, d1 = dual[i1] * x1;
-      const float4 a0 = reinterpret_cast<const float4*>(xv + (int64_t)i0 * vstride)[gl];
-      const float4 a1 = reinterpret_cast<const float4*>(xv + (int64_t)i1 * vstride)[gl];
-      gw += d0 + d1;
-      xxp += d0 * x0 + d1 * x1;
-      acc.x += d0 * a0.x + d1 * a1.x; acc.y += d0 * a0.y + d1 * a1.y;
-      acc.z += d0 * a0.z + d1 * a1.z; acc.w += d0 * a0.w + d1 * a1.w;
+  if (live) {
+    k = chunk_key[c];
+    const int kb = (int)csc_off[k], ke = (int)csc_off[k + 1];
+    b = chunk_beg[c];
+    e = b + kChunk < ke ? b + kChunk : ke;
+    multi = (ke - kb) > kChunk;
+    int p = b;
+    for (; p + 3 < e; p += 4) {  // 4 independent row->dual chains in flight
+      int i[4];
+      float x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        i[u] = csc_row[p + u];
+        x[u] = csc_val ? csc_val[p + u] : 1.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float d = dual[i[u]] * x[u];
+        gw += d;
+        xxp += d * x[u];
+      }
     }
-    if (p < e) {
-      const int i0 = csc_row[p];
-      const float x0 = csc_val ? csc_val[p] : 1.f;
-      const float d0 = dual[i0] * x0;
-      const float4 a0 = reinterpret_cast<const float4*>(xv + (int64_t)i0 * vstride)[gl];
-      gw += d0;
-      xxp += d0 * x0;
-      acc.x += d0 * a0.x; acc.y += d0 * a0.y; acc.z += d0 * a0.z; acc.w += d0 * a0.w;
+    for (; p < e; ++p) {
+      const float x = csc_val ? csc_val[p] : 1.f;
+      const float d = dual[csc_row[p]] * x;
+      gw += d;
+      xxp += d * x;
     }
-    const float4 v = reinterpret_cast<const float4*>(hdr + 4)[gl];
-    acc.x -= xxp * v.x; acc.y -= xxp * v.y; acc.z -= xxp * v.z; acc.w -= xxp * v.w;
-  } else {
-    for (int64_t p = b + gl; p < e; p += G) {
-      const float x0 = csc_val ? csc_val[p] : 1.f;
-      gw += dual[csc_row[p]] * x0;
-    }
-    gw = group_sum<G>(gw);
+    const float* hdr = pulled + (int64_t)k * stride;
+    flag = hdr[1] != 0.f;
+    float* g = grad + (int64_t)k * stride;
+    if (!multi) *reinterpret_cast<float4*>(g) = make_float4(gw, flag ? 1.f : 0.f, 0.f, 0.f);
+    else atomicAdd(g, gw);
   }
-  float* g = grad + (int64_t)k * stride;
-  if (!multi) {
-    if (gl == 0) *reinterpret_cast<float4*>(g) = make_float4(gw, flag ? 1.f : 0.f, 0.f, 0.f);
-    if (flag) reinterpret_cast<float4*>(g + 4)[gl] = acc;
-  } else {
-    if (gl == 0) atomicAdd(g, gw);
-    if (flag) {
-      float* gv = g + 4 + gl * 4;
+  for_each_row_job<G>(live && flag, [&](int src, int gl) {
+    const int sl = src >= 0 ? src : lane;
+    const int jk = __shfl(k, sl, 64), jb = __shfl(b, sl, 64), je = __shfl(e, sl, 64);
+    const float jx = __shfl(xxp, sl, 64);
+    const int jm = __shfl((int)multi, sl, 64);
+    if (src < 0) return;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int p = jb;
+    for (; p + 3 < je; p += 4) {
+      float d[4];
+      float4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = csc_row[p + u];
+        d[u] = dual[i] * (csc_val ? csc_val[p + u] : 1.f);
+        a[u] = reinterpret_cast<const float4*>(xv + (int64_t)i * vstride)[gl];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += d[u] * a[u].x; acc.y += d[u] * a[u].y;
+        acc.z += d[u] * a[u].z; acc.w += d[u] * a[u].w;
+      }
+    }
+    for (; p < je; ++p) {
+      const int i = csc_row[p];
+      const float d = dual[i] * (csc_val ? csc_val[p] : 1.f);
+      const float4 a = reinterpret_cast<const float4*>(xv + (int64_t)i * vstride)[gl];
+      acc.x += d * a.x; acc.y += d * a.y; acc.z += d * a.z; acc.w += d * a.w;
+    }
+    const float4 v = reinterpret_cast<const float4*>(pulled + (int64_t)jk * stride + 4)[gl];
+    acc.x -= jx * v.x; acc.y -= jx * v.y; acc.z -= jx * v.z; acc.w -= jx * v.w;
+    float* gv = grad + (int64_t)jk * stride + 4 + gl * 4;
+    if (!jm) {
+      *reinterpret_cast<float4*>(gv) = acc;
+    } else {
       atomicAdd(gv + 0, acc.x); atomicAdd(gv + 1, acc.y);
       atomicAdd(gv + 2, acc.z); atomicAdd(gv + 3, acc.w);
     }
-  }
+  });
 }
 
 __global__ __launch_bounds__(kThreads) void k_lin_bwd(const int64_t* __restrict__ nchunk_p, const int32_t* __restrict__ chunk_key,
@@ -370,7 +419,7 @@ void fm_backward(int64_t nuniq, const int64_t* csc_off, const int32_t* csc_row,
     return;
   }
   const int G = vstride / 4;
-  const dim3 grid(grid_for(chunk_cap * G, kThreads)), block(kThreads);
+  const dim3 grid(grid_for(chunk_cap, kThreads)), block(kThreads);  // lane per chunk
   WH_DISPATCH_G(G, k_fm_bwd, grid, block, 0, s, nchunk_p, chunk_key, chunk_beg, csc_off,
                 csc_row, csc_val, dual, xv, pulled, vstride, grad);
 }

@@ -123,68 +123,77 @@ __global__ __launch_bounds__(kThreads) void k_linear_push(KVTable t, const int32
   count_nnz_delta(oldw, neww, t.stats);
 }
 
+
 // ---------------------------------------------------------------- difacto
-// allocate + initialise the V row of slot s if the reference Resize rule
-// fires (learn/difacto/async_sgd.h:247-259). Called by ONE group; lane `gl`
-// of G lanes. Returns the row (or -1), identical in every lane of the group.
-template <int G>
-__device__ __forceinline__ int32_t maybe_alloc_v(const KVTable& t, int32_t s, bool want, int gl,
-                                                 int gbase, const DifactoHP& hp,
-                                                 long long* newv) {
-  int32_t row = -1;
-  if (gl == 0 && want) {
-    row = atomicAdd(t.vnext, 1);
-    if (row >= t.vcap) {
-      atomicAdd((unsigned long long*)(t.stats + 3), 1ull);
-      row = -1;
-    } else {
-      t.vrow[s] = row;
-      *newv += t.dim;
-    }
-  }
-  row = __shfl(row, gbase, 64);
-  if (row >= 0) {
-    const uint64_t key = t.keys[s];
-    float* V = t.V + (int64_t)row * t.vstride;
-    float* VG = t.VG + (int64_t)row * t.vstride;
-    for (int c = gl * 4; c < t.vstride; c += 4 * G) {
-      float4 v, zero = make_float4(0.f, 0.f, 0.f, 0.f);
-      float* pv = &v.x;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int d = c + e;
-        pv[e] = d < t.dim ? (uhash01(hp.seed, key, (uint64_t)d) * 2.f - 1.f) * hp.v_init : 0.f;
-      }
-      *reinterpret_cast<float4*>(V + c) = v;
-      *reinterpret_cast<float4*>(VG + c) = zero;
-    }
+// Layout of the work: ONE LANE PER KEY for everything scalar (count add,
+// FTRL on w, the allocation decision), then the wave cooperatively runs the
+// per-key embedding-row jobs (init a new V row / AdaGrad an existing one /
+// copy a row out) with G = vstride/4 lanes per row, 64/G rows at a time.
+// Most keys of a power-law minibatch have no V, so lane-per-key keeps all 64
+// lanes busy on the scalar part instead of 1 of every G.
+
+// wave-aggregated bump allocation of V rows; returns the row or -1
+__device__ __forceinline__ int32_t wave_alloc_rows(const KVTable& t, bool want) {
+  const uint64_t m = __ballot(want);
+  if (!m) return -1;
+  const int lane = threadIdx.x & 63;
+  int32_t base = 0;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  if (lane == leader) base = atomicAdd(t.vnext, (int)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (!want) return -1;
+  const int32_t row = base + (int32_t)__popcll(m & ((1ull << lane) - 1));
+  if (row >= t.vcap) {
+    atomicAdd((unsigned long long*)(t.stats + 3), 1ull);
+    return -1;
   }
   return row;
+}
+
+__device__ __forceinline__ void init_v_row(const KVTable& t, int32_t s, int32_t row, int gl, int G,
+                                           const DifactoHP& hp) {
+  const uint64_t key = t.keys[s];
+  float* V = t.V + (int64_t)row * t.vstride;
+  float* VG = t.VG + (int64_t)row * t.vstride;
+  for (int c = gl * 4; c < t.vstride; c += 4 * G) {
+    float4 v;
+    float* pv = &v.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int d = c + e;
+      pv[e] = d < t.dim ? (uhash01(hp.seed, key, (uint64_t)d) * 2.f - 1.f) * hp.v_init : 0.f;
+    }
+    *reinterpret_cast<float4*>(V + c) = v;
+    *reinterpret_cast<float4*>(VG + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
 }
 
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const int32_t* slot,
                                                                const float* cnt, int64_t n,
                                                                DifactoHP hp) {
-  const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane - gl;
-  const int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
-  long long newv = 0;
-  bool active = false;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   int32_t s = -1;
   bool want = false;
   if (i < n) {
     s = slot[i];
     if (s >= 0) {
-      active = true;
-      if (gl == 0) {
-        const uint32_t c = t.cnt[s] + (uint32_t)cnt[i];
-        t.cnt[s] = c;
-        want = c > hp.threshold && t.vrow[s] < 0 && (!hp.l1_shrk || t.w[s] != 0.f);
-      }
+      const uint32_t c = t.cnt[s] + (uint32_t)cnt[i];
+      t.cnt[s] = c;
+      want = t.vstride > 0 && c > hp.threshold && t.vrow[s] < 0 &&
+             (!hp.l1_shrk || t.w[s] != 0.f);
     }
   }
-  // every lane of the wave must reach the shuffles inside maybe_alloc_v
-  if (t.vstride > 0) maybe_alloc_v<G>(t, active ? s : 0, want && active, gl, gbase, hp, &newv);
+  if (t.vstride == 0) return;
+  const int32_t row = wave_alloc_rows(t, want);
+  if (row >= 0) t.vrow[s] = row;
+  long long newv = row >= 0 ? t.dim : 0;
+  for_each_row_job<G>(row >= 0, [&](int src, int gl) {
+    const int sl = src >= 0 ? src : lane;
+    const int32_t js = __shfl(s, sl, 64), jr = __shfl(row, sl, 64);
+    if (src >= 0) init_v_row(t, js, jr, gl, G, hp);
+  });
   newv = wave_sum_ll(newv);
   if (lane == 0 && newv) atomicAdd((unsigned long long*)(t.stats + 1), (unsigned long long)newv);
 }
@@ -192,48 +201,53 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const 
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_difacto_pull(KVTable t, const int32_t* slot,
                                                            int64_t n, int l1_shrk, float* out) {
-  const int lane = threadIdx.x & 63, gl = lane & (G - 1);
-  const int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
-  if (i >= n) return;
-  const int32_t s = slot[i];
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const int stride = t.vstride + 4;
-  float* o = out + i * stride;
-  float w = 0.f;
   int32_t row = -1;
-  if (s >= 0) {
-    w = t.w[s];
-    row = t.vrow[s];
-    if (l1_shrk && w == 0.f) row = -1;
+  if (i < n) {
+    const int32_t s = slot[i];
+    float w = 0.f;
+    if (s >= 0) {
+      w = t.w[s];
+      row = t.vstride > 0 ? t.vrow[s] : -1;
+      if (l1_shrk && w == 0.f) row = -1;
+    }
+    *reinterpret_cast<float4*>(out + i * stride) = make_float4(w, row >= 0 ? 1.f : 0.f, 0.f, 0.f);
   }
-  if (gl == 0) *reinterpret_cast<float4*>(o) = make_float4(w, row >= 0 ? 1.f : 0.f, 0.f, 0.f);
-  if (row >= 0) {
-    const float* V = t.V + (int64_t)row * t.vstride;
-    for (int c = gl * 4; c < t.vstride; c += 4 * G)
-      *reinterpret_cast<float4*>(o + 4 + c) = *reinterpret_cast<const float4*>(V + c);
-  }
+  if (t.vstride == 0) return;
+  for_each_row_job<G>(row >= 0, [&](int src, int gl) {
+    const int sl = src >= 0 ? src : lane;
+    const int32_t jr = __shfl(row, sl, 64);
+    const int64_t ji = (int64_t)blockIdx.x * kThreads + (threadIdx.x & ~63) + sl;
+    if (src >= 0) {
+      const float* V = t.V + (int64_t)jr * t.vstride;
+      float* o = out + ji * stride + 4;
+      for (int c = gl * 4; c < t.vstride; c += 4 * G)
+        *reinterpret_cast<float4*>(o + c) = *reinterpret_cast<const float4*>(V + c);
+    }
+  });
 }
 
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int32_t* slot,
                                                            const float* grad, int64_t n,
                                                            DifactoHP hp) {
-  const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane - gl;
-  const int64_t i = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const int stride = t.vstride + 4;
-  long long newv = 0;
   float oldw = 0.f, neww = 0.f;
   bool want = false;
-  int32_t s = -1;
+  int32_t s = -1, row = -1;
   float gflag = 0.f;
   if (i < n) {
     s = slot[i];
-    const float* gr = grad + i * stride;
-    gflag = gr[1];
-    if (s >= 0 && gl == 0) {
+    if (s >= 0) {
+      const float2 gr = *reinterpret_cast<const float2*>(grad + i * stride);
+      gflag = gr.y;
       // FTRL on w (reference UpdateW, learn/difacto/async_sgd.h:262-286)
-      float g = gr[0];
       const float w = t.w[s];
-      g += hp.l2 * w;
+      const float g = gr.x + hp.l2 * w;
       const float cg = t.sq[s];
       const float cg_new = sqrtf(cg * cg + g * g);
       t.sq[s] = cg_new;
@@ -249,40 +263,56 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int3
       t.w[s] = nw;
       oldw = w;
       neww = nw;
-      if (t.vstride > 0 && w == 0.f && nw != 0.f)
-        want = t.cnt[s] > hp.threshold && t.vrow[s] < 0;
-    }
-  }
-  if (t.vstride > 0) {
-    const bool act = i < n && s >= 0;
-    maybe_alloc_v<G>(t, act ? s : 0, want && act, gl, gbase, hp, &newv);
-    // AdaGrad on V (reference UpdateV, learn/difacto/async_sgd.h:289-296)
-    if (act && gflag != 0.f) {
-      const int32_t row = t.vrow[s];
-      if (row >= 0) {
-        float* V = t.V + (int64_t)row * t.vstride;
-        float* VG = t.VG + (int64_t)row * t.vstride;
-        const float* gv = grad + i * stride + 4;
-        for (int c = gl * 4; c < t.vstride; c += 4 * G) {
-          float4 v = *reinterpret_cast<float4*>(V + c);
-          float4 cg = *reinterpret_cast<float4*>(VG + c);
-          const float4 g = *reinterpret_cast<const float4*>(gv + c);
-          float* pv = &v.x;
-          float* pc = &cg.x;
-          const float* pg = &g.x;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float gg = pg[e] + hp.v_l2 * pv[e];
-            pc[e] = sqrtf(pc[e] * pc[e] + gg * gg);
-            pv[e] -= hp.v_alpha / (pc[e] + hp.v_beta) * gg;
-          }
-          *reinterpret_cast<float4*>(V + c) = v;
-          *reinterpret_cast<float4*>(VG + c) = cg;
-        }
+      if (t.vstride > 0) {
+        row = t.vrow[s];
+        if (w == 0.f && nw != 0.f) want = t.cnt[s] > hp.threshold && row < 0;
       }
     }
   }
   count_nnz_delta(oldw, neww, t.stats);
+  if (t.vstride == 0) return;
+  // job kinds: 1 = initialise a freshly allocated row, 2 = AdaGrad step
+  const int32_t nrow = wave_alloc_rows(t, want);
+  int kind = 0;
+  if (nrow >= 0) {
+    t.vrow[s] = nrow;
+    row = nrow;
+    kind = 1;
+  } else if (gflag != 0.f && row >= 0) {
+    kind = 2;
+  }
+  long long newv = kind == 1 ? t.dim : 0;
+  for_each_row_job<G>(kind != 0, [&](int src, int gl) {
+    const int sl = src >= 0 ? src : lane;
+    const int32_t js = __shfl(s, sl, 64), jr = __shfl(row, sl, 64);
+    const int jk = __shfl(kind, sl, 64);
+    const int64_t ji = (int64_t)blockIdx.x * kThreads + (threadIdx.x & ~63) + sl;
+    if (src < 0) return;
+    if (jk == 1) {
+      init_v_row(t, js, jr, gl, G, hp);
+      return;
+    }
+    // AdaGrad on V (reference UpdateV, learn/difacto/async_sgd.h:289-296)
+    float* V = t.V + (int64_t)jr * t.vstride;
+    float* VG = t.VG + (int64_t)jr * t.vstride;
+    const float* gv = grad + ji * stride + 4;
+    for (int c = gl * 4; c < t.vstride; c += 4 * G) {
+      float4 v = *reinterpret_cast<float4*>(V + c);
+      float4 cg = *reinterpret_cast<float4*>(VG + c);
+      const float4 g = *reinterpret_cast<const float4*>(gv + c);
+      float* pv = &v.x;
+      float* pc = &cg.x;
+      const float* pg = &g.x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float gg = pg[e] + hp.v_l2 * pv[e];
+        pc[e] = sqrtf(pc[e] * pc[e] + gg * gg);
+        pv[e] -= hp.v_alpha / (pc[e] + hp.v_beta) * gg;
+      }
+      *reinterpret_cast<float4*>(V + c) = v;
+      *reinterpret_cast<float4*>(VG + c) = cg;
+    }
+  });
   newv = wave_sum_ll(newv);
   if (lane == 0 && newv) atomicAdd((unsigned long long*)(t.stats + 1), (unsigned long long)newv);
 }
@@ -352,7 +382,7 @@ void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt, i
                       DifactoHP hp, hipStream_t s) {
   if (n <= 0) return;
   const int G = lanes_per_key(t.vstride);
-  const dim3 grid(grid_for(n * G, kThreads)), block(kThreads);
+  const dim3 grid(grid_for(n, kThreads)), block(kThreads);  // lane per key
   WH_DISPATCH_G(G, k_difacto_push_cnt, grid, block, 0, s, t, slot, cnt, n, hp);
 }
 
@@ -360,7 +390,7 @@ void difacto_pull(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk,
                   hipStream_t s) {
   if (n <= 0) return;
   const int G = lanes_per_key(t.vstride);
-  const dim3 grid(grid_for(n * G, kThreads)), block(kThreads);
+  const dim3 grid(grid_for(n, kThreads)), block(kThreads);  // lane per key
   WH_DISPATCH_G(G, k_difacto_pull, grid, block, 0, s, t, slot, n, l1_shrk, out);
 }
 
@@ -368,7 +398,7 @@ void difacto_push(const KVTable& t, const int32_t* slot, const float* grad, int6
                   DifactoHP hp, hipStream_t s) {
   if (n <= 0) return;
   const int G = lanes_per_key(t.vstride);
-  const dim3 grid(grid_for(n * G, kThreads)), block(kThreads);
+  const dim3 grid(grid_for(n, kThreads)), block(kThreads);  // lane per key
   WH_DISPATCH_G(G, k_difacto_push, grid, block, 0, s, t, slot, grad, n, hp);
 }
 

@@ -76,6 +76,27 @@ __device__ __forceinline__ long long wave_sum_ll(long long v) {
   return v;
 }
 
+// Runs job(src, gl) for every lane `src` whose `has` is set, G lanes per job.
+// job() is called by ALL lanes (src < 0: this group is idle this round) so it
+// may shuffle; it must read per-job data with __shfl(v, src >= 0 ? src : lane).
+template <int G, typename F>
+__device__ __forceinline__ void for_each_row_job(bool has, F&& job) {
+  const int lane = threadIdx.x & 63, grp = lane / G, gl = lane & (G - 1);
+  uint64_t m = __ballot(has);
+  while (m) {
+    int src = -1;
+#pragma unroll
+    for (int t = 0; t < 64 / G; ++t) {
+      if (m) {
+        const int b = __ffsll((unsigned long long)m) - 1;
+        if (t == grp) src = b;
+        m &= m - 1;
+      }
+    }
+    job(src, gl);
+  }
+}
+
 inline int grid_for(int64_t n, int threads, int max_blocks = 0x7fffffff) {
   int64_t b = (n + threads - 1) / threads;
   if (b < 1) b = 1;
