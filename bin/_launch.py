@@ -1,0 +1,7 @@
+"""Shared shim of the bin/*.dmlc entry scripts: puts the repo on sys.path."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)

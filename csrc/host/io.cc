@@ -1,0 +1,242 @@
+// File-system and split I/O (replaces the dmlc-core Stream / InputSplit /
+// FileSystem / RecordIO pieces wormhole uses; SURVEY §2.2 "dmlc-core I/O").
+//   * ListDirectory + MatchFile: reference learn/base/match_file.h:12-45
+//     (POSIX extended regex ".*<file part>", unanchored search)
+//   * InputSplit: part k of n of a file as a byte range snapped to record
+//     boundaries (text lines or RecordIO records)
+//   * RecordIO: dmlc-compatible framing (magic 0xced7230a, 29-bit length,
+//     3-bit continuation flag, 4-byte alignment)
+#include "io.h"
+
+#include <dirent.h>
+#include <regex.h>
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <cstring>
+
+namespace wh {
+namespace host {
+
+namespace {
+std::string strip_scheme(const std::string& p) {
+  if (p.rfind("file://", 0) == 0) return p.substr(7);
+  return p;
+}
+}  // namespace
+
+std::vector<std::string> ListDirectory(const std::string& dir_in) {
+  const std::string dir = strip_scheme(dir_in);
+  std::vector<std::string> out;
+  struct stat st;
+  if (stat(dir.c_str(), &st) != 0) return out;
+  if (!S_ISDIR(st.st_mode)) {
+    out.push_back(dir);
+    return out;
+  }
+  DIR* d = opendir(dir.c_str());
+  if (!d) return out;
+  while (struct dirent* e = readdir(d)) {
+    std::string name = e->d_name;
+    if (name == "." || name == "..") continue;
+    std::string full = dir;
+    if (!full.empty() && full.back() != '/') full += "/";
+    full += name;
+    struct stat fs;
+    if (stat(full.c_str(), &fs) == 0 && S_ISREG(fs.st_mode)) out.push_back(full);
+  }
+  closedir(d);
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+std::vector<std::string> MatchFile(const std::string& pattern_in) {
+  const std::string pattern = strip_scheme(pattern_in);
+  const size_t pos = pattern.find_last_of("/\\");
+  std::string path = "./";
+  if (pos != std::string::npos) path = pattern.substr(0, pos);
+  std::string file = pos == std::string::npos ? pattern : pattern.substr(pos + 1);
+  file = ".*" + file;
+  regex_t re;
+  int status = regcomp(&re, file.c_str(), REG_EXTENDED | REG_NEWLINE);
+  if (status != 0) {
+    char msg[512];
+    regerror(status, &re, msg, sizeof(msg));
+    throw std::runtime_error("error regex '" + pattern + "': " + msg);
+  }
+  std::vector<std::string> out;
+  for (const auto& f : ListDirectory(path)) {
+    std::string name = f;
+    if (pos == std::string::npos && name.rfind("./", 0) == 0) name = name.substr(2);
+    regmatch_t m[1];
+    if (regexec(&re, name.c_str(), 1, m, 0) == 0) out.push_back(name);
+  }
+  regfree(&re);
+  return out;
+}
+
+int64_t FileSize(const std::string& path) {
+  struct stat st;
+  if (stat(strip_scheme(path).c_str(), &st) != 0) return -1;
+  return (int64_t)st.st_size;
+}
+
+// ------------------------------------------------------------------ split
+InputSplit::InputSplit(const std::string& path, int part, int nparts, bool recordio)
+    : path_(strip_scheme(path)), recordio_(recordio) {
+  fp_ = std::fopen(path_.c_str(), "rb");
+  if (!fp_) throw std::runtime_error("cannot open " + path_);
+  const int64_t size = FileSize(path_);
+  WH_CHECK(nparts >= 1 && part >= 0 && part < nparts, "bad part index");
+  const int64_t nstep = (size + nparts - 1) / nparts;
+  int64_t b = std::min<int64_t>(size, nstep * part);
+  int64_t e = std::min<int64_t>(size, nstep * (part + 1));
+  begin_ = Align(b, size);
+  end_ = Align(e, size);
+  BeforeFirst();
+}
+
+InputSplit::~InputSplit() {
+  if (fp_) std::fclose(fp_);
+}
+
+int64_t InputSplit::Align(int64_t pos, int64_t size) {
+  if (pos <= 0) return 0;
+  if (pos >= size) return size;
+  if (!recordio_) {
+    // a line belongs to the part holding its first byte
+    std::fseek(fp_, pos - 1, SEEK_SET);
+    int c;
+    int64_t p = pos - 1;
+    while ((c = std::fgetc(fp_)) != EOF) {
+      ++p;
+      if (c == '\n' || c == '\r') {
+        // swallow a "\r\n" pair
+        int c2 = std::fgetc(fp_);
+        if (c2 != EOF && (c2 == '\n' || c2 == '\r') && c2 != c) ++p;
+        return p;
+      }
+    }
+    return size;
+  }
+  // recordio: first 4-aligned magic whose cflag is 0 (full) or 1 (start)
+  int64_t p = (pos + 3) & ~int64_t(3);
+  std::fseek(fp_, p, SEEK_SET);
+  uint32_t w[2];
+  while (p + 8 <= size) {
+    std::fseek(fp_, p, SEEK_SET);
+    if (std::fread(w, 4, 2, fp_) != 2) break;
+    if (w[0] == kRecordIOMagic) {
+      const uint32_t cflag = w[1] >> 29;
+      if (cflag == 0 || cflag == 1) return p;
+    }
+    p += 4;
+  }
+  return size;
+}
+
+void InputSplit::BeforeFirst() {
+  std::fseek(fp_, begin_, SEEK_SET);
+  pos_ = begin_;
+  carry_.clear();
+}
+
+bool InputSplit::NextChunk(std::string* out, size_t hint) {
+  out->clear();
+  if (recordio_) throw std::runtime_error("NextChunk on a recordio split");
+  if (pos_ >= end_ && carry_.empty()) return false;
+  const int64_t want = std::min<int64_t>((int64_t)hint, end_ - pos_);
+  std::string buf = carry_;
+  carry_.clear();
+  if (want > 0) {
+    const size_t old = buf.size();
+    buf.resize(old + want);
+    const size_t got = std::fread(&buf[old], 1, want, fp_);
+    buf.resize(old + got);
+    pos_ += got;
+  }
+  if (pos_ < end_) {
+    // keep the trailing partial line for the next chunk
+    size_t cut = buf.find_last_of("\n\r");
+    if (cut == std::string::npos) {
+      carry_ = buf;
+      return NextChunk(out, hint * 2);
+    }
+    carry_ = buf.substr(cut + 1);
+    buf.resize(cut + 1);
+  }
+  out->swap(buf);
+  return !out->empty() || pos_ < end_;
+}
+
+bool InputSplit::NextRecord(std::string* out) {
+  out->clear();
+  if (!recordio_) throw std::runtime_error("NextRecord on a text split");
+  while (true) {
+    if (pos_ >= end_) return false;
+    uint32_t hdr[2];
+    if (std::fread(hdr, 4, 2, fp_) != 2) return false;
+    WH_CHECK(hdr[0] == kRecordIOMagic, "invalid recordio stream in " + path_);
+    const uint32_t cflag = hdr[1] >> 29, len = hdr[1] & ((1u << 29) - 1);
+    const uint32_t padded = (len + 3u) & ~3u;
+    std::string data(padded, '\0');
+    if (padded && std::fread(&data[0], 1, padded, fp_) != padded)
+      throw std::runtime_error("truncated recordio record in " + path_);
+    pos_ += 8 + padded;
+    data.resize(len);
+    if (cflag == 0) {
+      *out = std::move(data);
+      return true;
+    }
+    if (cflag == 1) {
+      *out = std::move(data);
+      continue;
+    }
+    // 2 = middle, 3 = end: the writer split at an embedded magic word
+    const uint32_t m = kRecordIOMagic;
+    out->append(reinterpret_cast<const char*>(&m), 4);
+    out->append(data);
+    if (cflag == 3) return true;
+  }
+}
+
+// --------------------------------------------------------------- recordio
+RecordIOWriter::RecordIOWriter(const std::string& path) {
+  fp_ = std::fopen(path.c_str(), "wb");
+  if (!fp_) throw std::runtime_error("cannot open " + path + " for writing");
+}
+RecordIOWriter::~RecordIOWriter() { Close(); }
+void RecordIOWriter::Close() {
+  if (fp_) std::fclose(fp_);
+  fp_ = nullptr;
+}
+
+void RecordIOWriter::WriteRecord(const char* buf, size_t size) {
+  WH_CHECK(size < (1u << 29), "record too large");
+  const uint32_t magic = kRecordIOMagic;
+  const size_t lower = (size >> 2) << 2, upper = ((size + 3) >> 2) << 2;
+  size_t dptr = 0;
+  auto emit = [&](uint32_t cflag, size_t from, size_t len) {
+    const uint32_t lrec = (cflag << 29) | (uint32_t)len;
+    std::fwrite(&magic, 4, 1, fp_);
+    std::fwrite(&lrec, 4, 1, fp_);
+    if (len) std::fwrite(buf + from, 1, len, fp_);
+    bytes_ += 8 + len;
+  };
+  for (size_t i = 0; i < lower; i += 4) {
+    uint32_t w;
+    std::memcpy(&w, buf + i, 4);
+    if (w == magic) {
+      emit(dptr == 0 ? 1 : 2, dptr, i - dptr);
+      dptr = i + 4;
+    }
+  }
+  emit(dptr != 0 ? 3 : 0, dptr, size - dptr);
+  const size_t pad = upper - size;
+  static const char zeros[4] = {0, 0, 0, 0};
+  if (pad) std::fwrite(zeros, 1, pad, fp_);
+  bytes_ += pad;
+}
+
+}  // namespace host
+}  // namespace wh

@@ -1,0 +1,56 @@
+#pragma once
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+namespace wh {
+namespace host {
+
+constexpr uint32_t kRecordIOMagic = 0xced7230a;
+
+std::vector<std::string> ListDirectory(const std::string& dir);
+std::vector<std::string> MatchFile(const std::string& pattern);
+int64_t FileSize(const std::string& path);
+
+// Part `part` of `nparts` of one file, snapped to line (text) or record
+// (RecordIO) boundaries so every record belongs to exactly one part.
+class InputSplit {
+ public:
+  InputSplit(const std::string& path, int part, int nparts, bool recordio);
+  ~InputSplit();
+  void BeforeFirst();
+  // text: next chunk of whole lines (about `hint` bytes)
+  bool NextChunk(std::string* out, size_t hint = 4 << 20);
+  // recordio: next (re-assembled) record
+  bool NextRecord(std::string* out);
+  int64_t begin() const { return begin_; }
+  int64_t end() const { return end_; }
+  int64_t bytes_read() const { return pos_ - begin_; }
+
+ private:
+  int64_t Align(int64_t pos, int64_t size);
+  std::string path_;
+  bool recordio_;
+  std::FILE* fp_ = nullptr;
+  int64_t begin_ = 0, end_ = 0, pos_ = 0;
+  std::string carry_;
+};
+
+class RecordIOWriter {
+ public:
+  explicit RecordIOWriter(const std::string& path);
+  ~RecordIOWriter();
+  void WriteRecord(const char* buf, size_t size);
+  void WriteRecord(const std::string& s) { WriteRecord(s.data(), s.size()); }
+  size_t bytes_written() const { return bytes_; }
+  void Close();
+
+ private:
+  std::FILE* fp_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+}  // namespace host
+}  // namespace wh

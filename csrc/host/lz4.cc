@@ -1,0 +1,138 @@
+// LZ4 block format codec (compatible with LZ4_compress_default /
+// LZ4_decompress_safe as used by the reference CompressedRowBlock,
+// learn/base/compressed_row_block.h:77-105). Greedy single-probe hash
+// compressor; the decompressor accepts any conforming LZ4 block.
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+namespace wh {
+namespace host {
+namespace {
+
+constexpr int kMinMatch = 4;
+constexpr int kLastLiterals = 5;
+constexpr int kMfLimit = 12;
+constexpr int kHashLog = 16;
+
+inline uint32_t read32(const char* p) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return v;
+}
+inline uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - kHashLog); }
+
+inline void put_len(char*& op, int len) {
+  while (len >= 255) {
+    *op++ = (char)255;
+    len -= 255;
+  }
+  *op++ = (char)len;
+}
+
+}  // namespace
+
+int LZ4CompressBound(int n) { return n + n / 255 + 16; }
+
+int LZ4Compress(const char* src, char* dst, int n, int cap) {
+  if (cap < LZ4CompressBound(n)) return 0;
+  char* op = dst;
+  const char* anchor = src;
+  const char* const end = src + n;
+  if (n >= kMfLimit + 1) {
+    std::vector<int32_t> table(1 << kHashLog, -1);
+    const char* ip = src;
+    const char* const mflimit = end - kMfLimit;
+    const char* const matchlimit = end - kLastLiterals;
+    while (ip < mflimit) {
+      const uint32_t seq = read32(ip);
+      const uint32_t h = hash4(seq);
+      const int32_t cand = table[h];
+      table[h] = (int32_t)(ip - src);
+      if (cand < 0 || (ip - src) - cand > 65535 || read32(src + cand) != seq) {
+        ++ip;
+        continue;
+      }
+      const char* match = src + cand;
+      // extend backwards
+      while (ip > anchor && match > src && ip[-1] == match[-1]) {
+        --ip;
+        --match;
+      }
+      // forward
+      const char* p = ip + kMinMatch;
+      const char* m = match + kMinMatch;
+      while (p < matchlimit && *p == *m) {
+        ++p;
+        ++m;
+      }
+      const int litlen = (int)(ip - anchor);
+      const int mlen = (int)(p - ip) - kMinMatch;
+      char* token = op++;
+      *token = (char)(((litlen >= 15 ? 15 : litlen) << 4) | (mlen >= 15 ? 15 : mlen));
+      if (litlen >= 15) put_len(op, litlen - 15);
+      std::memcpy(op, anchor, litlen);
+      op += litlen;
+      const int off = (int)(ip - match);
+      *op++ = (char)(off & 0xff);
+      *op++ = (char)((off >> 8) & 0xff);
+      if (mlen >= 15) put_len(op, mlen - 15);
+      ip = p;
+      anchor = ip;
+      if (ip < mflimit) table[hash4(read32(ip - 2))] = (int32_t)(ip - 2 - src);
+    }
+  }
+  const int litlen = (int)(end - anchor);
+  *op++ = (char)((litlen >= 15 ? 15 : litlen) << 4);
+  if (litlen >= 15) put_len(op, litlen - 15);
+  std::memcpy(op, anchor, litlen);
+  op += litlen;
+  return (int)(op - dst);
+}
+
+int LZ4Decompress(const char* src, char* dst, int csize, int cap) {
+  const unsigned char* ip = (const unsigned char*)src;
+  const unsigned char* const iend = ip + csize;
+  char* op = dst;
+  char* const oend = dst + cap;
+  while (ip < iend) {
+    const unsigned token = *ip++;
+    size_t lit = token >> 4;
+    if (lit == 15) {
+      unsigned s;
+      do {
+        if (ip >= iend) return -1;
+        s = *ip++;
+        lit += s;
+      } while (s == 255);
+    }
+    if ((size_t)(iend - ip) < lit || (size_t)(oend - op) < lit) return -1;
+    std::memcpy(op, ip, lit);
+    op += lit;
+    ip += lit;
+    if (ip >= iend) break;  // last sequence
+    if (iend - ip < 2) return -1;
+    const size_t off = (size_t)ip[0] | ((size_t)ip[1] << 8);
+    ip += 2;
+    if (off == 0 || off > (size_t)(op - dst)) return -1;
+    size_t mlen = token & 15;
+    if (mlen == 15) {
+      unsigned s;
+      do {
+        if (ip >= iend) return -1;
+        s = *ip++;
+        mlen += s;
+      } while (s == 255);
+    }
+    mlen += kMinMatch;
+    if ((size_t)(oend - op) < mlen) return -1;
+    const char* m = op - off;
+    for (size_t i = 0; i < mlen; ++i) op[i] = m[i];  // overlap-safe
+    op += mlen;
+  }
+  return (int)(op - dst);
+}
+
+}  // namespace host
+}  // namespace wh

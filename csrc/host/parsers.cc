@@ -1,0 +1,343 @@
+// Text / binary row-block parsers (reference: dmlc LibSVMParser [ext],
+// learn/base/criteo_parser.h, learn/base/adfea_parser.h,
+// learn/base/compressed_row_block.h) and the threaded minibatch iterator
+// (learn/base/minibatch_iter.h: fixed-size minibatches of part k/n of a
+// file, optional shuffle buffer, negative down-sampling).
+#include "parsers.h"
+
+#include <algorithm>
+#include <cctype>
+#include <cstring>
+#include <numeric>
+
+namespace wh {
+namespace host {
+
+namespace {
+
+inline bool is_space(char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; }
+inline bool is_eol(char c) { return c == '\n' || c == '\r'; }
+
+}  // namespace
+
+// libsvm:  label[:weight] idx[:value] idx[:value] ...
+void ParseLibSVM(const char* p, const char* end, RowBlock* blk) {
+  blk->clear();
+  bool any_val = false;
+  while (p < end) {
+    while (p < end && is_space(*p)) ++p;
+    if (p >= end) break;
+    // label
+    char* q;
+    float label = std::strtof(p, &q);
+    if (q == p) throw std::runtime_error("libsvm: bad label");
+    p = q;
+    if (p < end && *p == ':') {
+      ++p;
+      float w = std::strtof(p, &q);
+      p = q;
+      blk->weight.resize(blk->label.size(), 1.f);
+      blk->weight.push_back(w);
+    } else if (!blk->weight.empty()) {
+      blk->weight.push_back(1.f);
+    }
+    blk->label.push_back(label);
+    while (p < end && !is_eol(*p)) {
+      while (p < end && (*p == ' ' || *p == '\t')) ++p;
+      if (p >= end || is_eol(*p)) break;
+      uint64_t idx = std::strtoull(p, &q, 10);
+      if (q == p) throw std::runtime_error("libsvm: bad feature index");
+      p = q;
+      float v = 1.f;
+      if (p < end && *p == ':') {
+        ++p;
+        v = std::strtof(p, &q);
+        p = q;
+      }
+      if (v != 1.f && !any_val) {
+        any_val = true;
+        blk->value.assign(blk->index.size(), 1.f);
+      }
+      blk->index.push_back(idx);
+      if (any_val) blk->value.push_back(v);
+    }
+    blk->offset.push_back((int64_t)blk->index.size());
+  }
+}
+
+// criteo TSV: [label] 13 integer fields, 26 categorical (8-char hex) fields
+void ParseCriteo(const char* p, const char* end, bool is_train, RowBlock* blk) {
+  blk->clear();
+  auto find = [&](const char* s, char c) {
+    while (s != end && *s != c && !is_eol(*s)) ++s;
+    return s;
+  };
+  while (p < end) {
+    while (p < end && is_eol(*p)) ++p;
+    if (p >= end) break;
+    const char* pp;
+    if (is_train) {
+      pp = find(p, '\t');
+      if (pp == p) throw std::runtime_error("criteo: no label, try criteo_test");
+      blk->label.push_back((float)std::atof(std::string(p, pp).c_str()));
+      p = pp < end ? pp + 1 : pp;
+    } else {
+      blk->label.push_back(0.f);
+    }
+    for (uint64_t i = 0; i < 13; ++i) {
+      pp = find(p, '\t');
+      if (pp > p)
+        blk->index.push_back((CityHash64(p, pp - p) >> 10) | (i << 54));
+      p = pp;
+      if (p < end && *p == '\t') ++p;
+    }
+    for (uint64_t i = 0; i < 26; ++i) {
+      if (p >= end || is_eol(*p)) break;
+      pp = find(p, '\t');
+      if (pp > p)
+        blk->index.push_back((CityHash64(p, pp - p) >> 10) | ((i + 13) << 54));
+      p = pp;
+      if (p < end && *p == '\t') ++p;
+    }
+    while (p < end && !is_eol(*p)) ++p;
+    blk->offset.push_back((int64_t)blk->index.size());
+  }
+}
+
+// adfea: "<lineid> <count> <label> idx:gid idx:gid ..." (learn/base/adfea_parser.h:43-79)
+void ParseAdfea(const char* p, const char* end, RowBlock* blk) {
+  blk->clear();
+  int i = 0;
+  while (p != end && std::isspace((unsigned char)*p)) ++p;
+  while (p != end) {
+    const char* head = p;
+    while (p != end && std::isdigit((unsigned char)*p)) ++p;
+    if (head == p) throw std::runtime_error("adfea: unexpected character");
+    if (p != end && *p == ':') {
+      ++p;
+      uint64_t idx = std::strtoull(head, nullptr, 10);
+      uint64_t gid = std::strtoull(p, nullptr, 10);
+      idx = (idx >> 10) | (gid << 54);
+      while (p != end && std::isdigit((unsigned char)*p)) ++p;
+      blk->index.push_back(idx);
+    } else {
+      if (i == 2) {
+        i = 0;
+        if (!blk->label.empty()) blk->offset.push_back((int64_t)blk->index.size());
+        blk->label.push_back(*head == '1' ? 1.f : 0.f);
+      } else {
+        ++i;
+      }
+    }
+    while (p != end && std::isspace((unsigned char)*p)) ++p;
+  }
+  if (!blk->label.empty()) blk->offset.push_back((int64_t)blk->index.size());
+}
+
+// ------------------------------------------------------------------- CRB
+namespace {
+constexpr int kCRBMagic = 1196140743;
+void put_int(std::string* s, int v) { s->append(reinterpret_cast<const char*>(&v), 4); }
+void put_section(std::string* s, const void* data, size_t bytes) {
+  if (!data || bytes == 0) {
+    put_int(s, 0);
+    return;
+  }
+  std::vector<char> dst(LZ4CompressBound((int)bytes));
+  const int n = LZ4Compress((const char*)data, dst.data(), (int)bytes, (int)dst.size());
+  WH_CHECK(n > 0, "lz4 compression failed");
+  put_int(s, n);
+  s->append(dst.data(), n);
+}
+}  // namespace
+
+std::string CRBEncode(const RowBlock& in) {
+  RowBlock b = in;
+  b.compact_binary();
+  const int nrows = (int)b.size();
+  const int nnz = (int)(b.offset.back() - b.offset.front());
+  std::string s;
+  put_int(&s, kCRBMagic);
+  put_int(&s, (int)sizeof(uint64_t));
+  put_int(&s, nrows);
+  std::vector<size_t> off(b.offset.begin(), b.offset.end());
+  put_section(&s, b.label.data(), nrows * sizeof(float));
+  put_section(&s, off.data(), (nrows + 1) * sizeof(size_t));
+  put_section(&s, b.index.data(), nnz * sizeof(uint64_t));
+  put_section(&s, b.value.empty() ? nullptr : b.value.data(), nnz * sizeof(float));
+  put_section(&s, b.weight.empty() ? nullptr : b.weight.data(), nrows * sizeof(float));
+  return s;
+}
+
+void CRBDecode(const char* data, size_t size, RowBlock* blk) {
+  blk->clear();
+  size_t cur = 0;
+  auto get_int = [&]() {
+    WH_CHECK(cur + 4 <= size, "truncated crb record");
+    int v;
+    std::memcpy(&v, data + cur, 4);
+    cur += 4;
+    return v;
+  };
+  auto section = [&](void* dst, size_t bytes) -> bool {
+    const int cp = get_int();
+    if (cp <= 0) return false;
+    WH_CHECK(cur + cp <= size, "truncated crb section");
+    const int got = LZ4Decompress(data + cur, (char*)dst, cp, (int)bytes);
+    WH_CHECK(got == (int)bytes, "crb section size mismatch");
+    cur += cp;
+    return true;
+  };
+  WH_CHECK(get_int() == kCRBMagic, "wrong data format (not a CRB record)");
+  const int isz = get_int();
+  WH_CHECK(isz == 8 || isz == 4, "unsupported crb index width");
+  const int nrows = get_int();
+  blk->label.resize(nrows);
+  if (!section(blk->label.data(), nrows * sizeof(float))) blk->label.assign(nrows, 0.f);
+  std::vector<size_t> off(nrows + 1);
+  section(off.data(), (nrows + 1) * sizeof(size_t));
+  blk->offset.assign(off.begin(), off.end());
+  const int64_t base = blk->offset[0];
+  for (auto& o : blk->offset) o -= base;
+  const int nnz = (int)blk->offset.back();
+  if (isz == 8) {
+    blk->index.resize(nnz);
+    section(blk->index.data(), nnz * sizeof(uint64_t));
+  } else {
+    std::vector<uint32_t> tmp(nnz);
+    section(tmp.data(), nnz * sizeof(uint32_t));
+    blk->index.assign(tmp.begin(), tmp.end());
+  }
+  blk->value.resize(nnz);
+  if (!section(blk->value.data(), nnz * sizeof(float))) blk->value.clear();
+  blk->weight.resize(nrows);
+  if (!section(blk->weight.data(), nrows * sizeof(float))) blk->weight.clear();
+}
+
+// --------------------------------------------------------------- parsing
+BlockReader::BlockReader(const std::string& path, int part, int nparts, const std::string& fmt)
+    : fmt_(fmt) {
+  if (fmt != "libsvm" && fmt != "criteo" && fmt != "criteo_test" && fmt != "adfea" &&
+      fmt != "crb")
+    throw std::runtime_error("unknown datatype " + fmt);
+  split_.reset(new InputSplit(path, part, nparts, fmt == "crb"));
+}
+
+bool BlockReader::Next(RowBlock* blk) {
+  std::string buf;
+  if (fmt_ == "crb") {
+    if (!split_->NextRecord(&buf)) return false;
+    CRBDecode(buf.data(), buf.size(), blk);
+    return true;
+  }
+  while (true) {
+    if (!split_->NextChunk(&buf)) return false;
+    const char* p = buf.data();
+    const char* e = p + buf.size();
+    if (fmt_ == "libsvm") ParseLibSVM(p, e, blk);
+    else if (fmt_ == "criteo") ParseCriteo(p, e, true, blk);
+    else if (fmt_ == "criteo_test") ParseCriteo(p, e, false, blk);
+    else ParseAdfea(p, e, blk);
+    if (blk->size() > 0) return true;
+  }
+}
+
+// ------------------------------------------------------ threaded parser
+ThreadedReader::ThreadedReader(const std::string& path, int part, int nparts,
+                               const std::string& fmt, size_t depth)
+    : reader_(path, part, nparts, fmt), depth_(depth) {
+  th_ = std::thread([this] { Run(); });
+}
+
+ThreadedReader::~ThreadedReader() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (th_.joinable()) th_.join();
+}
+
+void ThreadedReader::Run() {
+  try {
+    while (true) {
+      RowBlock b;
+      const bool ok = reader_.Next(&b);
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return stop_ || q_.size() < depth_; });
+      if (stop_) return;
+      if (!ok) {
+        done_ = true;
+        cv_.notify_all();
+        return;
+      }
+      q_.push_back(std::move(b));
+      cv_.notify_all();
+    }
+  } catch (const std::exception& e) {
+    std::lock_guard<std::mutex> lk(mu_);
+    err_ = e.what();
+    done_ = true;
+    cv_.notify_all();
+  }
+}
+
+bool ThreadedReader::Next(RowBlock* out) {
+  std::unique_lock<std::mutex> lk(mu_);
+  cv_.wait(lk, [&] { return !q_.empty() || done_; });
+  if (!err_.empty()) throw std::runtime_error(err_);
+  if (q_.empty()) return false;
+  *out = std::move(q_.front());
+  q_.pop_front();
+  cv_.notify_all();
+  return true;
+}
+
+// ------------------------------------------------------- minibatch iter
+MinibatchIter::MinibatchIter(const std::string& path, int part, int nparts,
+                             const std::string& fmt, size_t mb_size, size_t shuf_buf,
+                             float neg_sampling, uint64_t seed)
+    : mb_size_(mb_size), shuf_buf_(shuf_buf), neg_(neg_sampling), rng_(seed) {
+  WH_CHECK(mb_size > 0, "minibatch size must be positive");
+  if (shuf_buf) {
+    WH_CHECK(shuf_buf > mb_size, "shuffle buffer must exceed the minibatch size");
+    inner_.reset(new MinibatchIter(path, part, nparts, fmt, shuf_buf, 0, 1.f, seed + 1));
+  } else {
+    reader_.reset(new ThreadedReader(path, part, nparts, fmt));
+  }
+}
+
+bool MinibatchIter::Next() {
+  mb_.clear();
+  while (mb_.size() < mb_size_) {
+    if (start_ == end_) {
+      if (!inner_) {
+        if (!reader_->Next(&in_)) break;
+      } else {
+        if (!inner_->Next()) break;
+        in_ = inner_->Value();
+        perm_.resize(in_.size());
+        std::iota(perm_.begin(), perm_.end(), 0);
+        std::shuffle(perm_.begin(), perm_.end(), rng_);
+      }
+      start_ = 0;
+      end_ = in_.size();
+    }
+    const size_t len = std::min(end_ - start_, mb_size_ - mb_.size());
+    std::uniform_real_distribution<float> U(0.f, 1.f);
+    for (size_t i = start_; i < start_ + len; ++i) {
+      const size_t r = inner_ ? perm_[i] : i;
+      // negative down-sampling keeps a negative with probability neg_sampling
+      // (the reference drops with that probability, §2.9 item 7: fixed here
+      // to the documented "down sampling ratio" meaning)
+      if (inner_ && neg_ < 1.f && in_.label[r] <= 0.f && U(rng_) > neg_) continue;
+      mb_.push_row(in_, r);
+    }
+    start_ += len;
+  }
+  mb_.compact_binary();
+  return mb_.size() > 0;
+}
+
+}  // namespace host
+}  // namespace wh

@@ -1,4 +1,267 @@
+// pybind11 registration of the native host runtime (wormhole_amd._host).
 #include <torch/extension.h>
-namespace wh { namespace host {
-void register_all(pybind11::module& m) { (void)m; }
-} }
+
+#include <cstring>
+#include <memory>
+
+#include "common.h"
+#include "io.h"
+#include "localizer.h"
+#include "parsers.h"
+#include "van.h"
+#include "workload_pool.h"
+
+namespace wh {
+namespace host {
+
+
+namespace {
+
+using torch::Tensor;
+
+py::list conf_to_py(const std::vector<ConfItem>& items) {
+  py::list out;
+  for (const auto& it : items) {
+    if (it.kind == 'm')
+      out.append(py::make_tuple(it.key, std::string("m"), conf_to_py(it.children)));
+    else
+      out.append(py::make_tuple(it.key, std::string(1, it.kind), it.value));
+  }
+  return out;
+}
+
+template <typename T>
+Tensor vec_to_tensor(const std::vector<T>& v, torch::ScalarType dt) {
+  auto t = torch::empty({(int64_t)v.size()}, torch::TensorOptions().dtype(dt));
+  if (!v.empty()) std::memcpy(t.data_ptr(), v.data(), v.size() * sizeof(T));
+  return t;
+}
+
+py::tuple block_to_py(const RowBlock& b) {
+  py::object val = py::none(), wt = py::none();
+  if (!b.value.empty()) val = py::cast(vec_to_tensor(b.value, torch::kFloat32));
+  if (!b.weight.empty()) wt = py::cast(vec_to_tensor(b.weight, torch::kFloat32));
+  return py::make_tuple(vec_to_tensor(b.index, torch::kInt64), vec_to_tensor(b.offset, torch::kInt64),
+                        val, vec_to_tensor(b.label, torch::kFloat32), wt);
+}
+
+RowBlock py_to_block(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+                     const Tensor& label, const c10::optional<Tensor>& weight) {
+  RowBlock b;
+  auto k = keys.contiguous().to(torch::kInt64);
+  auto o = offset.contiguous().to(torch::kInt64);
+  auto l = label.contiguous().to(torch::kFloat32);
+  b.index.assign((const uint64_t*)k.data_ptr(), (const uint64_t*)k.data_ptr() + k.numel());
+  b.offset.assign(o.data_ptr<int64_t>(), o.data_ptr<int64_t>() + o.numel());
+  b.label.assign(l.data_ptr<float>(), l.data_ptr<float>() + l.numel());
+  if (val && val->defined() && val->numel()) {
+    auto v = val->contiguous().to(torch::kFloat32);
+    b.value.assign(v.data_ptr<float>(), v.data_ptr<float>() + v.numel());
+  }
+  if (weight && weight->defined() && weight->numel()) {
+    auto w = weight->contiguous().to(torch::kFloat32);
+    b.weight.assign(w.data_ptr<float>(), w.data_ptr<float>() + w.numel());
+  }
+  return b;
+}
+
+// whole split of a file as one block (for the BSP apps that keep their split resident)
+py::tuple load_split(const std::string& path, int part, int nparts, const std::string& fmt) {
+  py::gil_scoped_release nogil;
+  BlockReader r(path, part, nparts, fmt);
+  RowBlock all, b;
+  bool any_val = false;
+  while (r.Next(&b)) {
+    if (!b.value.empty() && !any_val) {
+      any_val = true;
+      all.value.assign(all.index.size(), 1.f);
+    }
+    const int64_t base = (int64_t)all.index.size();
+    all.label.insert(all.label.end(), b.label.begin(), b.label.end());
+    if (!b.weight.empty()) all.weight.insert(all.weight.end(), b.weight.begin(), b.weight.end());
+    for (size_t i = 1; i < b.offset.size(); ++i) all.offset.push_back(base + b.offset[i]);
+    all.index.insert(all.index.end(), b.index.begin(), b.index.end());
+    if (any_val) {
+      if (b.value.empty()) all.value.resize(all.index.size(), 1.f);
+      else all.value.insert(all.value.end(), b.value.begin(), b.value.end());
+    }
+  }
+  py::gil_scoped_acquire g;
+  return block_to_py(all);
+}
+
+class PyMinibatchIter {
+ public:
+  PyMinibatchIter(const std::string& path, int part, int nparts, const std::string& fmt,
+                  int64_t mb, int64_t shuf, double neg, int64_t seed)
+      : it_(path, part, nparts, fmt, (size_t)mb, (size_t)shuf, (float)neg, (uint64_t)seed) {}
+  py::object next() {
+    bool ok;
+    {
+      py::gil_scoped_release nogil;
+      ok = it_.Next();
+    }
+    if (!ok) return py::none();
+    return block_to_py(it_.Value());
+  }
+
+ private:
+  MinibatchIter it_;
+};
+
+py::tuple localize_cpu(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+                       int64_t nshard, int64_t nthreads) {
+  auto k = keys.contiguous();
+  auto o = offset.contiguous();
+  Tensor v;
+  const float* vp = nullptr;
+  if (val && val->defined() && val->numel()) {
+    v = val->contiguous();
+    vp = v.data_ptr<float>();
+  }
+  LocalizeResult r;
+  {
+    py::gil_scoped_release nogil;
+    LocalizeCPU((const uint64_t*)k.data_ptr(), (size_t)k.numel(), o.data_ptr<int64_t>(),
+                (size_t)o.numel() - 1, vp, (int)nshard, (int)nthreads, &r);
+  }
+  return py::make_tuple(vec_to_tensor(r.uniq, torch::kInt64), vec_to_tensor(r.ucnt, torch::kInt32),
+                        vec_to_tensor(r.owner_cnt, torch::kInt64), vec_to_tensor(r.lid, torch::kInt32),
+                        vec_to_tensor(r.csc_off, torch::kInt64), vec_to_tensor(r.csc_row, torch::kInt32),
+                        vec_to_tensor(r.csc_val, torch::kFloat32));
+}
+
+}  // namespace
+
+void register_all(py::module& m) {
+  m.def("parse_conf", [](const std::string& text) { return conf_to_py(ParseConf(text)); });
+  m.def("cityhash64", [](py::bytes b) {
+    std::string s = b;
+    return CityHash64(s.data(), s.size());
+  });
+  m.def("lz4_compress", [](py::bytes b) {
+    std::string s = b;
+    std::string out(LZ4CompressBound((int)s.size()), '\0');
+    int n = LZ4Compress(s.data(), &out[0], (int)s.size(), (int)out.size());
+    out.resize(n);
+    return py::bytes(out);
+  });
+  m.def("lz4_decompress", [](py::bytes b, int64_t size) {
+    std::string s = b;
+    std::string out(size, '\0');
+    int n = LZ4Decompress(s.data(), &out[0], (int)s.size(), (int)size);
+    if (n != size) throw std::runtime_error("lz4: corrupt input");
+    return py::bytes(out);
+  });
+  m.def("match_file", &MatchFile);
+  m.def("list_directory", &ListDirectory);
+  m.def("file_size", &FileSize);
+  m.def("load_split", &load_split, py::arg("path"), py::arg("part") = 0, py::arg("nparts") = 1,
+        py::arg("fmt") = "libsvm");
+  m.def("read_text_split", [](const std::string& path, int part, int nparts) {
+    InputSplit s(path, part, nparts, false);
+    std::string chunk, all;
+    while (s.NextChunk(&chunk)) all += chunk;
+    return py::bytes(all);
+  });
+  m.def("read_recordio", [](const std::string& path, int part, int nparts) {
+    InputSplit s(path, part, nparts, true);
+    std::string rec;
+    py::list out;
+    while (s.NextRecord(&rec)) out.append(py::bytes(rec));
+    return out;
+  });
+  m.def("crb_encode", [](const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+                         const Tensor& label, const c10::optional<Tensor>& weight) {
+    return py::bytes(CRBEncode(py_to_block(keys, offset, val, label, weight)));
+  }, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(), py::arg("label"),
+     py::arg("weight") = py::none());
+  m.def("crb_decode", [](py::bytes b) {
+    std::string s = b;
+    RowBlock blk;
+    CRBDecode(s.data(), s.size(), &blk);
+    return block_to_py(blk);
+  });
+  m.def("parse_text", [](py::bytes b, const std::string& fmt) {
+    std::string s = b;
+    RowBlock blk;
+    const char* p = s.data();
+    const char* e = p + s.size();
+    if (fmt == "libsvm") ParseLibSVM(p, e, &blk);
+    else if (fmt == "criteo") ParseCriteo(p, e, true, &blk);
+    else if (fmt == "criteo_test") ParseCriteo(p, e, false, &blk);
+    else if (fmt == "adfea") ParseAdfea(p, e, &blk);
+    else throw std::runtime_error("unknown text format " + fmt);
+    return block_to_py(blk);
+  });
+  m.def("localize_cpu", &localize_cpu, py::arg("keys"), py::arg("offset"),
+        py::arg("val") = py::none(), py::arg("nshard") = 1, py::arg("nthreads") = 4);
+
+  py::class_<RecordIOWriter>(m, "RecordIOWriter")
+      .def(py::init<const std::string&>())
+      .def("write", [](RecordIOWriter& w, py::bytes b) {
+        std::string s = b;
+        w.WriteRecord(s);
+      })
+      .def("close", &RecordIOWriter::Close)
+      .def_property_readonly("bytes_written", &RecordIOWriter::bytes_written);
+
+  py::class_<PyMinibatchIter>(m, "MinibatchIter")
+      .def(py::init<const std::string&, int, int, const std::string&, int64_t, int64_t, double,
+                    int64_t>(),
+           py::arg("path"), py::arg("part"), py::arg("nparts"), py::arg("fmt"),
+           py::arg("minibatch"), py::arg("shuffle_buf") = 0, py::arg("neg_sampling") = 1.0,
+           py::arg("seed") = 0)
+      .def("next", &PyMinibatchIter::next);
+
+  py::class_<WorkloadPool>(m, "WorkloadPool")
+      .def(py::init<bool, uint64_t, double, double, int, double>(), py::arg("shuffle") = false,
+           py::arg("seed") = 0, py::arg("straggler_factor") = 2.0,
+           py::arg("straggler_min_sec") = 5.0, py::arg("straggler_min_done") = 10,
+           py::arg("period") = 2.0)
+      .def("add", &WorkloadPool::Add, py::arg("files"), py::arg("npart"), py::arg("node") = "")
+      .def("clear", &WorkloadPool::Clear)
+      .def("get", [](WorkloadPool& p, const std::string& node) -> py::object {
+        Assignment a;
+        if (!p.Get(node, &a)) return py::none();
+        return py::make_tuple(a.filename, a.k, a.n);
+      })
+      .def("finish", &WorkloadPool::Finish)
+      .def("reset", &WorkloadPool::Reset)
+      .def("remove_straggler", &WorkloadPool::RemoveStraggler)
+      .def("is_finished", &WorkloadPool::IsFinished)
+      .def("set_verbose", &WorkloadPool::set_verbose)
+      .def_property_readonly("num_finished", &WorkloadPool::num_finished)
+      .def_property_readonly("num_assigned", &WorkloadPool::num_assigned)
+      .def_property_readonly("num_requeued", &WorkloadPool::num_requeued);
+
+  py::class_<Van>(m, "Van")
+      .def(py::init<>())
+      .def("listen", &Van::Listen)
+      .def("connect", &Van::Connect, py::arg("host"), py::arg("port"), py::arg("my_id"),
+           py::arg("timeout") = 60.0)
+      .def("send", [](Van& v, const std::string& to, py::bytes b) {
+        std::string s = b;
+        py::gil_scoped_release nogil;
+        return v.Send(to, s);
+      })
+      .def("recv", [](Van& v, double timeout) -> py::object {
+        std::string from, msg;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = v.Recv(timeout, &from, &msg);
+        }
+        if (!ok) return py::none();
+        return py::make_tuple(from, py::bytes(msg));
+      })
+      .def("peers", &Van::Peers)
+      .def("close", [](Van& v) {
+        py::gil_scoped_release nogil;
+        v.Close();
+      })
+      .def_property_readonly("port", &Van::port);
+}
+
+}  // namespace host
+}  // namespace wh

@@ -1,0 +1,126 @@
+"""Entry point of the parameter-server learners (bin/linear.dmlc,
+bin/difacto.dmlc): ``<bin> <conf|none> [key=value ...]``.
+
+Role comes from the launcher environment (tracker/dmlc_local.py):
+``DMLC_ROLE`` = scheduler | worker (servers are folded into the workers: each
+worker owns one parameter shard).  Without a launcher the binary runs a
+1-worker job in-process (scheduler thread + worker), which is what
+``dmlc_local.py -n 1 -s 1`` would do.
+"""
+import os
+import sys
+import threading
+
+import torch
+
+
+def _device():
+    want = os.environ.get("WH_DEVICE", "auto")
+    if want == "cpu":
+        return torch.device("cpu")
+    if want == "auto" and not torch.cuda.is_available():
+        return torch.device("cpu")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = torch.cuda.device_count()
+    idx = local % max(n, 1)
+    torch.cuda.set_device(idx)
+    return torch.device("cuda", idx)
+
+
+def _make(kind, conf):
+    from ..config import schema
+    if kind == "linear":
+        from ..models.progress import LinearProgress
+        return schema.LinearConfig, LinearProgress, None
+    from ..models.progress import DifactoProgress
+
+    def stop_fn(agg, train, state={"pre": 100.0}):
+        cur = agg[0] / agg[5] if agg[5] else 0.0
+        if train:
+            return conf.has("max_objv") and cur > conf.max_objv
+        diff = state["pre"] - cur
+        state["pre"] = cur
+        if conf.early_stop and diff < conf.min_objv_decr:
+            print("The decrease of validation objective is smaller than the minimal "
+                  "requirement: %g vs %g" % (diff, conf.min_objv_decr), flush=True)
+            return True
+        return False
+    return schema.DifactoConfig, DifactoProgress, stop_fn
+
+
+def _learner(kind, conf, comm, device, nshard):
+    cap = int(os.environ.get("WH_KV_CAP", 1 << (24 if device.type == "cuda" else 16)))
+    vcap = int(os.environ.get("WH_KV_VCAP", 1 << (20 if device.type == "cuda" else 14)))
+    if kind == "linear":
+        from ..models.linear import LinearLearner
+        return LinearLearner(conf, comm, device, cap=cap, nshard=nshard)
+    from ..models.difacto import DifactoLearner
+    return DifactoLearner(conf, comm, device, cap=cap, vcap=vcap, nshard=nshard)
+
+
+def main(kind, argv):
+    from .. import _native, config
+    from ..parallel.comm import Comm
+    from ..solver.ps import Scheduler, Worker
+
+    if len(argv) < 1:
+        print("usage: %s.dmlc <conf|none> [key=value ...]" % kind, file=sys.stderr)
+        return 1
+    cls, prog_cls, _ = _make(kind, None)
+    conf = config.load(cls, argv[0], argv[1:])
+    _, prog_cls, stop_fn = _make(kind, conf)
+    if kind == "difacto" and conf.early_stop and not conf.val_data:
+        raise SystemExit("early stop needs validation dataset")
+    role = os.environ.get("DMLC_ROLE")
+    nw = int(os.environ.get("DMLC_NUM_WORKER", "1"))
+    ns = int(os.environ.get("DMLC_NUM_SERVER", "1"))
+    nshard = max(1, min(ns, nw))
+    host = _native.host()
+    if role is None:
+        # standalone: scheduler in a thread, one worker here
+        van_s = host.Van()
+        port = van_s.listen(0)
+        sched = Scheduler(conf, kind, 1, 1, van=van_s, progress_cls=prog_cls, stop_fn=stop_fn)
+        err = []
+
+        def run_sched():
+            try:
+                sched.run()
+            except Exception as e:  # pragma: no cover - surfaced below
+                err.append(e)
+        th = threading.Thread(target=run_sched, daemon=True)
+        th.start()
+        os.environ.setdefault("WORLD_SIZE", "1")
+        os.environ.setdefault("RANK", "0")
+        dev = _device()
+        comm = Comm(dev)
+        van = host.Van()
+        van.connect("127.0.0.1", port, "worker-0")
+        Worker(conf, kind, _learner(kind, conf, comm, dev, 1), comm, van, 1, kind).serve()
+        th.join()
+        van.close()
+        van_s.close()
+        if err:
+            raise err[0]
+        return 0
+    uri = os.environ.get("DMLC_PS_ROOT_URI", "127.0.0.1")
+    port = int(os.environ["DMLC_PS_ROOT_PORT"])
+    if role == "scheduler":
+        van = host.Van()
+        van.listen(port)
+        Scheduler(conf, kind, nw, nshard, van=van, progress_cls=prog_cls, stop_fn=stop_fn).run()
+        van.close()
+        return 0
+    if role == "server":
+        # parameter shards live inside the workers; a server process has nothing to do
+        return 0
+    dev = _device()
+    comm = Comm(dev)
+    van = host.Van()
+    van.connect(uri, port, "worker-%d" % comm.rank)
+    try:
+        Worker(conf, kind, _learner(kind, conf, comm, dev, nshard), comm, van, nshard, kind).serve()
+    finally:
+        van.close()
+        comm.finalize()
+    return 0

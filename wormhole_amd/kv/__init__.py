@@ -43,15 +43,17 @@ class Session:
 
 
 class ShardedKV:
-    def __init__(self, store, comm):
+    def __init__(self, store, comm, nshard=None):
         self.store = store
         self.comm = comm
-        self.nshard = comm.size
+        # keys are owned by the first `nshard` ranks (the conf's -s S servers)
+        self.nshard = comm.size if nshard is None else max(1, min(int(nshard), comm.size))
         self.push_count = 0  # number of push requests applied (SGD's t)
 
     def open(self, uniq, owner_cnt, insert):
         send = [int(x) for x in (owner_cnt.tolist() if hasattr(owner_cnt, "tolist") else owner_cnt)]
-        if self.nshard == 1:
+        send += [0] * (self.comm.size - len(send))
+        if self.comm.size == 1:
             sess = Session(send, send, uniq)
         else:
             recv = self.comm.exchange_counts(send)
@@ -60,10 +62,10 @@ class ShardedKV:
         return sess
 
     def _to_owner(self, sess, x):
-        return x if self.nshard == 1 else self.comm.all_to_all_v(x, sess.send, sess.recv)
+        return x if self.comm.size == 1 else self.comm.all_to_all_v(x, sess.send, sess.recv)
 
     def _to_worker(self, sess, x):
-        return x if self.nshard == 1 else self.comm.all_to_all_v(x, sess.recv, sess.send)
+        return x if self.comm.size == 1 else self.comm.all_to_all_v(x, sess.recv, sess.send)
 
     # ---------------------------------------------------------------- linear
     def linear_pull(self, sess):

@@ -153,6 +153,26 @@ class CpuKVStore:
             out[i] = s
         return torch.from_numpy(out)
 
+    # ------------------------------------------------------------- loading
+    def load_entries(self, keys, cols):
+        s = self.find(keys, True).numpy()
+        if (s < 0).any():
+            raise RuntimeError("parameter table full while loading the model")
+        for name, val in cols.items():
+            getattr(self, "_" + name)[s] = val.numpy()
+
+    def load_v(self, keys, V, VG):
+        s = self.find(keys, True).numpy()
+        for i, slot in enumerate(s.tolist()):
+            row = self._vnext
+            self._vnext += 1
+            self._grow_v(row + 1)
+            self._vrow[slot] = row
+            self._V[row] = 0
+            self._V[row, : V.shape[1]] = V[i].numpy()
+            self._VG[row] = 0
+            self._VG[row, : VG.shape[1]] = VG[i].numpy()
+
     # --------------------------------------------------------------- linear
     @staticmethod
     def _solve(z, eta, l1, l2):

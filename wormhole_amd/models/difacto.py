@@ -20,7 +20,7 @@ TRAIN, VAL, PRED = 0, 1, 2
 
 
 class DifactoLearner:
-    def __init__(self, conf, comm, device, cap=1 << 22, vcap=1 << 20, seed=0):
+    def __init__(self, conf, comm, device, cap=1 << 22, vcap=1 << 20, seed=0, nshard=None):
         self.conf = conf
         self.comm = comm
         self.device = torch.device(device)
@@ -29,7 +29,7 @@ class DifactoLearner:
         self.emb = emb
         self.vstride = ops.vstride_for(self.dim)
         self.store = make_store(cap, vcap, self.dim, self.device)
-        self.kv = ShardedKV(self.store, comm)
+        self.kv = ShardedKV(self.store, comm, nshard)
         self.seed = seed
         self.l1_shrk = bool(conf.l1_shrk)
         if emb is not None:

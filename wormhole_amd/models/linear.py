@@ -15,12 +15,12 @@ TRAIN, VAL, PRED = 0, 1, 2
 
 
 class LinearLearner:
-    def __init__(self, conf, comm, device, cap=1 << 22, seed=0):
+    def __init__(self, conf, comm, device, cap=1 << 22, seed=0, nshard=None):
         self.conf = conf
         self.comm = comm
         self.device = torch.device(device)
         self.store = make_store(cap, 0, 0, self.device)
-        self.kv = ShardedKV(self.store, comm)
+        self.kv = ShardedKV(self.store, comm, nshard)
         self.seed = seed
         self.alpha = conf.lr_eta
         self.beta = conf.lr_beta

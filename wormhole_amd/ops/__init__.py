@@ -22,7 +22,7 @@ def localize(keys, offset, val=None, nshard=1):
     counts, the nnz->local-id map and the per-id occurrence lists (CSC)."""
     if _gpu(keys):
         return _native.hip().localize(keys, offset, val, nshard)
-    return ref.localize(keys, offset, val, nshard)
+    return _native.host().localize_cpu(keys, offset, val, nshard)
 
 
 def fm_forward(offset, lid, val, pulled, vstride, label, loss, met):

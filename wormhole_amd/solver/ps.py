@@ -1,0 +1,380 @@
+"""Parameter-server solver runtime: scheduler + workers.
+
+Reference layering (learn/solver/): DataParScheduler/Worker (dynamic
+workload dispatch, data_parallel.h) < IterScheduler/Server/Worker (model
+load/save, progress, prediction files, iter_solver.h) < MinibatchScheduler/
+Worker (epoch loop, minibatch streaming, minibatch_solver.h).
+
+MI355X design: one worker process per GPU; every worker also owns a shard of
+the parameter store (the ps-lite server group is folded into the workers and
+push/pull are all-to-all collectives over xGMI).  The scheduler is a separate
+CPU process that keeps the reference's control semantics: it matches files,
+splits them into ``num_parts_per_file`` virtual parts, hands them out one at
+a time from the native WorkloadPool, sum-merges progress and prints the
+reference progress table every ``print_sec``, and fans out load/save.
+
+Because collectives are group-synchronous, workers step in lockstep: a worker
+whose current part is exhausted asks for another; once the pool is empty it
+keeps joining the collectives with empty minibatches until an allreduce of
+"have data" flags is zero (SURVEY §7.5 hard part 1).  ``max_concurrency``
+bounds the minibatches in flight per worker exactly as before (the device
+queue depth), with zero staleness inside a step.
+"""
+import json
+import os
+import sys
+import time
+
+import torch
+
+from .. import _native
+from ..kv import checkpoint
+from ..models.progress import merge
+
+TRAIN, VAL, PRED = 0, 1, 2
+_TYPE_NAME = {TRAIN: "training", VAL: "validation", PRED: "prediction"}
+
+
+def _msg(**kw):
+    return json.dumps(kw).encode()
+
+
+def _log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# --------------------------------------------------------------------------
+# scheduler
+# --------------------------------------------------------------------------
+class Scheduler:
+    """MinibatchScheduler (learn/solver/minibatch_solver.h:10-195)."""
+
+    def __init__(self, conf, app, num_workers, num_servers, van=None, port=0,
+                 progress_cls=None, stop_fn=None):
+        self.conf = conf
+        self.app = app
+        self.nw = num_workers
+        self.ns = num_servers
+        self.host = _native.host()
+        self.van = van or self.host.Van()
+        self.port = self.van.port if van else self.van.listen(port)
+        self.progress_cls = progress_cls
+        self.stop_fn = stop_fn
+        self.workers = []
+        self.pool = None
+        self.dead = set()
+        self.start = time.time()
+
+    # ---------------------------------------------------------- plumbing
+    def wait_workers(self, timeout=600):
+        t0 = time.time()
+        while len(self.workers) < self.nw:
+            m = self.van.recv(1.0)
+            if m is None:
+                if time.time() - t0 > timeout:
+                    raise RuntimeError("only %d of %d workers connected" % (len(self.workers), self.nw))
+                continue
+            who, raw = m
+            d = json.loads(raw)
+            if d.get("msg") == "ready":
+                self.workers.append(who)
+        self.workers.sort(key=lambda w: int(w.split("-")[1]))
+
+    def broadcast(self, **kw):
+        for w in self.workers:
+            self.van.send(w, _msg(**kw))
+
+    def _recv(self, timeout=1.0):
+        m = self.van.recv(timeout)
+        if m is None:
+            return None, None
+        who, raw = m
+        if raw == b"__closed__":
+            return who, {"msg": "__closed__"}
+        return who, json.loads(raw)
+
+    def _on_dead(self, who):
+        if who in self.dead:
+            return
+        self.dead.add(who)
+        _log("[scheduler] node %s died" % who)
+        if self.pool is not None:
+            self.pool.reset(who)  # re-queue its workload (data_parallel.h:131-135)
+        raise RuntimeError("worker %s failed; its workload was re-queued, restart from the "
+                           "last saved model (model_in / load_iter)" % who)
+
+    def command(self, cmd, **kw):
+        """Send a command to all workers and wait for every ack."""
+        self.broadcast(cmd=cmd, **kw)
+        acks = 0
+        prog = None
+        while acks < len(self.workers):
+            who, d = self._recv()
+            if d is None:
+                continue
+            if d["msg"] == "__closed__":
+                self._on_dead(who)
+            elif d["msg"] == "ack":
+                acks += 1
+                if d.get("progress"):
+                    prog = merge(prog, d["progress"])
+        return prog
+
+    # ------------------------------------------------------------ epochs
+    def run(self):
+        c = self.conf
+        self.wait_workers()
+        print("Connected %d servers and %d workers" % (self.ns, self.nw), flush=True)
+        self.start = time.time()
+        is_pred = bool(c.predict_out)
+        if is_pred and not c.model_in:
+            raise RuntimeError("should provide model_in for predicting")
+        cur = 0
+        if c.model_in:
+            if c.load_iter > 0:
+                print("Loading model from iter = %d" % c.load_iter, flush=True)
+                cur = c.load_iter
+            else:
+                print("Loading the last model", flush=True)
+                cur = -1
+            self.command("load", file=c.model_in, iter=cur)
+            self.iterate(cur, PRED)
+            cur += 1
+        if is_pred:
+            print("Prediction is finished!", flush=True)
+            self.shutdown()
+            return True
+        while cur < c.max_data_pass:
+            if self.iterate(cur, TRAIN) or self.iterate(cur, VAL):
+                print("Hit stop critera", flush=True)
+                break
+            if cur == c.max_data_pass - 1:
+                print("Hit max number of data passes %d" % c.max_data_pass, flush=True)
+                break
+            if c.model_out and c.save_iter > 0 and (cur + 1) % c.save_iter == 0:
+                print("Saving model for iter = %d" % cur, flush=True)
+                self.command("save", file=c.model_out, iter=cur)
+            cur += 1
+        if c.model_out:
+            print("Saving the final model", flush=True)
+            self.command("save", file=c.model_out, iter=-1)
+        print("Training is finished!", flush=True)
+        self.shutdown()
+        return True
+
+    def shutdown(self):
+        self.broadcast(cmd="exit")
+        time.sleep(0.2)
+
+    def iterate(self, it, wtype):
+        """One data pass; returns True when the stop criterion fires."""
+        c = self.conf
+        train = wtype == TRAIN
+        if train:
+            data = c.train_data
+            print("Training: iter = %d" % it, flush=True)
+        else:
+            data = c.val_data
+            if wtype == PRED:
+                print("Predicting", flush=True)
+            else:
+                print("Validating: iter = %d" % it, flush=True)
+                if not data:
+                    return False
+        files = self.host.match_file(data)
+        if not files:
+            raise RuntimeError("no file matches '%s'" % data)
+        if c.num_parts_per_file * len(files) < self.nw:
+            _log("[scheduler] #parts (%d) < #workers (%d): some workers idle; increase "
+                 "num_parts_per_file" % (c.num_parts_per_file * len(files), self.nw))
+        self.pool = self.host.WorkloadPool(shuffle=train, seed=it + 1)
+        self.pool.add(files, int(c.num_parts_per_file))
+        prog_printer = self.progress_cls()
+        print("  sec %s" % prog_printer.head(), flush=True)
+        self.broadcast(cmd="iterate", type=wtype, data_pass=it, fmt=c.data_format)
+        done = 0
+        agg = None
+        stop = False
+        last = time.time()
+        while done < len(self.workers):
+            who, d = self._recv(0.05)
+            if d is not None:
+                m = d["msg"]
+                if m == "__closed__":
+                    self._on_dead(who)
+                elif m == "request":
+                    if d.get("finished"):
+                        self.pool.finish(who)
+                    if stop:
+                        self.van.send(who, _msg(cmd="workload", file=None))
+                        continue
+                    a = self.pool.get(who)
+                    if a is None:
+                        self.van.send(who, _msg(cmd="workload", file=None))
+                    else:
+                        self.van.send(who, _msg(cmd="workload", file=a[0], k=a[1], n=a[2]))
+                elif m == "progress":
+                    agg = merge(agg, d["data"])
+                elif m == "pass_done":
+                    done += 1
+                    if d.get("progress"):
+                        agg = merge(agg, d["progress"])
+            if train and time.time() - last >= c.print_sec:
+                last = time.time()
+                if agg is not None:
+                    s = self.show(prog_printer, agg, True)
+                    agg = None
+                    if s and not stop:
+                        stop = True
+                        self.pool.clear()  # reference StopDispatch
+        if agg is not None:
+            s = self.show(prog_printer, agg, train)
+            stop = stop or s
+        return stop
+
+    def show(self, printer, agg, train):
+        line = printer.line(agg)
+        if not line:
+            return False
+        print("%5.0f  %s" % (time.time() - self.start, line), flush=True)
+        return bool(self.stop_fn and self.stop_fn(agg, train))
+
+
+# --------------------------------------------------------------------------
+# worker
+# --------------------------------------------------------------------------
+class Worker:
+    """MinibatchWorker + IterServer of its shard (minibatch_solver.h:200-330,
+    iter_solver.h:77-167)."""
+
+    def __init__(self, conf, app, learner, comm, van, nshard, kind):
+        self.conf = conf
+        self.app = app
+        self.learner = learner
+        self.comm = comm
+        self.van = van
+        self.nshard = nshard
+        self.kind = kind  # "linear" | "difacto"
+        self.device = learner.device
+        self.host = _native.host()
+        self.report_sec = max(0.1, float(conf.print_sec) / 2)
+
+    def send(self, **kw):
+        self.van.send("scheduler", _msg(**kw))
+
+    def recv(self):
+        while True:
+            m = self.van.recv(1.0)
+            if m is None:
+                continue
+            _, raw = m
+            if raw == b"__closed__":
+                raise SystemExit("scheduler connection lost")
+            return json.loads(raw)
+
+    def serve(self):
+        self.send(msg="ready", rank=self.comm.rank)
+        while True:
+            d = self.recv()
+            cmd = d.get("cmd")
+            if cmd == "exit":
+                return
+            if cmd == "save":
+                if self.comm.rank < self.nshard:
+                    name = checkpoint.model_name(d["file"], d["iter"], self.comm.rank)
+                    fn = checkpoint.save_linear if self.kind == "linear" else checkpoint.save_difacto
+                    fn(self.learner.store, name)
+                self.comm.barrier()
+                self.send(msg="ack")
+            elif cmd == "load":
+                if self.comm.rank < self.nshard:
+                    name = checkpoint.model_name(d["file"], d["iter"], self.comm.rank)
+                    fn = checkpoint.load_linear if self.kind == "linear" else checkpoint.load_difacto
+                    fn(self.learner.store, name)
+                self.comm.barrier()
+                self.send(msg="ack")
+            elif cmd == "iterate":
+                self.run_pass(d["type"], d["data_pass"], d.get("fmt", self.conf.data_format))
+
+    # -------------------------------------------------------- one pass
+    def _empty_batch(self):
+        dev = self.device
+        return (torch.zeros(0, dtype=torch.int64, device=dev),
+                torch.zeros(1, dtype=torch.int64, device=dev), None,
+                torch.zeros(0, dtype=torch.float32, device=dev))
+
+    def _to_dev(self, b):
+        keys, off, val, label, _w = b
+        dev = self.device
+        nb = dev.type == "cuda"
+        keys = keys.to(dev, non_blocking=nb)
+        off = off.to(dev, non_blocking=nb)
+        label = label.to(dev, non_blocking=nb)
+        if val is not None:
+            val = val.to(dev, non_blocking=nb)
+        return keys, off, val, label
+
+    def run_pass(self, wtype, data_pass, fmt):
+        c = self.conf
+        train = wtype == TRAIN
+        mb = c.minibatch if train else 10_000_000 if wtype == PRED else 100_000
+        shuf = c.minibatch * c.rand_shuffle if (train and c.rand_shuffle > 0) else 0
+        neg = c.neg_sampling if train else 1.0
+        it = None
+        cur = None
+        finished_one = False
+        exhausted = False
+        pred_f = None
+        pred_name = None
+        last = time.time()
+        seed = 1000003 * (data_pass + 1) + self.comm.rank
+        while True:
+            batch = None
+            while it is None and not exhausted:
+                self.send(msg="request", finished=finished_one)
+                finished_one = False
+                d = self.recv()
+                if d.get("file") is None:
+                    exhausted = True
+                    break
+                cur = d
+                it = self.host.MinibatchIter(d["file"], d["k"], d["n"], fmt, int(mb), int(shuf),
+                                             float(neg), seed + d["k"])
+                if wtype == PRED:
+                    base = os.path.basename(d["file"])
+                    name = "%s%s_part-%d" % (c.predict_out, base, d["k"])
+                    if name != pred_name:
+                        if pred_f:
+                            pred_f.close()
+                        pred_f = open(name, "w")
+                        pred_name = name
+            if it is not None:
+                batch = it.next()
+                if batch is None:
+                    it = None
+                    finished_one = True
+                    continue
+            have = 1 if batch is not None else 0
+            if self.comm.size > 1:
+                flag = torch.tensor([have], dtype=torch.int32, device=self.comm.device)
+                self.comm.allreduce(flag)
+                if int(flag.item()) == 0:
+                    break
+            elif not have:
+                break
+            args = self._to_dev(batch) if batch is not None else self._empty_batch()
+            py = self.learner.process(*args, wtype=wtype, data_pass=data_pass)
+            if wtype == PRED and batch is not None:
+                p = py.float().cpu()
+                if c.prob_predict:
+                    p = torch.sigmoid(p)
+                pred_f.write("".join("%g\n" % v for v in p.tolist()))
+            if time.time() - last > self.report_sec:
+                last = time.time()
+                self.send(msg="progress", data=self.learner.take_progress())
+        if pred_f:
+            pred_f.close()
+        if finished_one:
+            self.send(msg="request", finished=True)
+            self.recv()  # the (empty) answer
+        self.send(msg="pass_done", progress=self.learner.take_progress())
