@@ -1,0 +1,151 @@
+"""Multi-process parameter-server jobs on CPU (gloo), launched through
+tracker/dmlc_local.py exactly like the reference:
+the demo confs train, save shards, and predict; the scheduler dispatches
+every virtual part exactly once (port of learn/test/data_parallel_test.cc);
+save/load fan-out uses the `_iter-i_part-r` naming (port of
+learn/test/iter_solver_test.cc); a killed worker fails the job cleanly."""
+import glob
+import json
+import os
+import re
+import subprocess
+import sys
+import threading
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TRACKER = os.path.join(ROOT, "tracker", "dmlc_local.py")
+
+
+def run(args, cwd, env_extra=None, timeout=300):
+    env = dict(os.environ)
+    env["WH_DEVICE"] = "cpu"
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, TRACKER] + args, cwd=cwd, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    return r
+
+
+@pytest.fixture()
+def work(tmp_path):
+    os.symlink(os.path.join(ROOT, "learn"), tmp_path / "learn")
+    return tmp_path
+
+
+def _table(stdout, header_word):
+    rows = []
+    for line in stdout.splitlines():
+        if re.match(r"^\s*\d+\s+\S", line) and "|" in line or re.match(r"^\s*\d+\s+[\d.e+]+\s", line):
+            rows.append(line)
+    return rows
+
+
+def test_linear_demo_two_workers(work):
+    r = run(["-n", "2", "-s", "1", os.path.join(ROOT, "bin", "linear.dmlc"),
+             "learn/linear/guide/demo.conf", "save_iter=1"], work)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = r.stdout
+    assert "Connected 1 servers and 2 workers" in out
+    assert "  sec   ttl #ex   inc #ex    |w|_0       logloss  accuracy     AUC" in out
+    assert "Hit max number of data passes 3" in out and "Training is finished!" in out
+    # per-pass save (iter_solver_test port): <model_out>_iter-<k>_part-<shard>
+    for k in range(2):
+        assert os.path.exists(work / ("agaricus_model_iter-%d_part-0" % k))
+    assert os.path.exists(work / "agaricus_model_part-0")
+    assert not os.path.exists(work / "agaricus_model_part-1")  # -s 1: one shard
+    vals = [float(l.split()[4]) for l in out.splitlines() if re.match(r"^\s+\d+\s+1\.61e\+03", l)]
+    assert len(vals) == 3 and vals[-1] < vals[0] and vals[-1] < 0.6  # validation logloss falls
+
+
+def test_difacto_train_save_predict(work):
+    r = run(["-n", "2", "-s", "2", os.path.join(ROOT, "bin", "difacto.dmlc"),
+             "learn/difacto/guide/demo.conf"], work)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "|   |V|_0    logloss    AUC" in r.stdout
+    last_val = [l for l in r.stdout.splitlines() if "1611" in l][-1]
+    assert os.path.exists(work / "agaricus_model_part-0")
+    assert os.path.exists(work / "agaricus_model_part-1")
+    r2 = run(["-n", "2", "-s", "2", os.path.join(ROOT, "bin", "difacto.dmlc"),
+              "learn/difacto/guide/demo.conf", "model_in=agaricus_model", "predict_out=pred_"], work)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    assert "Prediction is finished!" in r2.stdout
+    pred_line = [l for l in r2.stdout.splitlines() if "1611" in l][-1]
+    # the reloaded model reproduces the last validation logloss / AUC exactly
+    assert pred_line.split("|")[-1].split()[1:] == last_val.split("|")[-1].split()[1:]
+    preds = sorted(glob.glob(str(work / "pred_agaricus.txt.test_part-*")))
+    assert len(preds) == 10
+    vals = [float(x) for p in preds for x in open(p)]
+    assert len(vals) == 1611 and all(0 < v < 1 for v in vals)
+
+
+def test_standalone_single_process(work):
+    env = dict(os.environ, WH_DEVICE="cpu")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bin", "linear.dmlc"),
+                        "learn/linear/guide/demo.conf", "max_data_pass=1", "algo=ADAGRAD",
+                        'model_out=""'], cwd=work, env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Training is finished!" in r.stdout
+
+
+def test_scheduler_dispatches_every_part_once(work):
+    """Port of learn/test/data_parallel_test.cc with assertions: fake workers
+    request workloads from a real Scheduler; every (file, part) is handed out
+    exactly once and the pass ends when all report done."""
+    from wormhole_amd import _native
+    from wormhole_amd.config.schema import LinearConfig
+    from wormhole_amd.models.progress import LinearProgress
+    from wormhole_amd.solver.ps import Scheduler
+    host = _native.host()
+    data = work / "data"
+    data.mkdir()
+    for i in range(4):
+        (data / ("part-%d" % i)).write_text("1 1:1\n")
+    conf = LinearConfig(train_data=str(data / "part-.*"), num_parts_per_file=3,
+                        max_data_pass=1, print_sec=0.1)
+    van = host.Van()
+    port = van.listen(0)
+    sched = Scheduler(conf, "linear", 4, 2, van=van, progress_cls=LinearProgress)
+    got = []
+    lock = threading.Lock()
+
+    def fake_worker(i):
+        v = host.Van()
+        v.connect("127.0.0.1", port, "worker-%d" % i)
+        v.send("scheduler", json.dumps({"msg": "ready"}).encode())
+        while True:
+            m = v.recv(10.0)
+            d = json.loads(m[1])
+            if d["cmd"] == "exit":
+                break
+            if d["cmd"] == "iterate":
+                fin = False
+                while True:
+                    v.send("scheduler", json.dumps({"msg": "request", "finished": fin}).encode())
+                    w = json.loads(v.recv(10.0)[1])
+                    if w["file"] is None:
+                        break
+                    with lock:
+                        got.append((os.path.basename(w["file"]), w["k"], w["n"]))
+                    fin = True
+                v.send("scheduler", json.dumps({"msg": "pass_done",
+                                                "progress": [0, 0, 0, 0, 0, 0]}).encode())
+        v.close()
+
+    ths = [threading.Thread(target=fake_worker, args=(i,)) for i in range(4)]
+    for t in ths:
+        t.start()
+    sched.run()
+    for t in ths:
+        t.join(timeout=30)
+    van.close()
+    assert sorted(got) == sorted(("part-%d" % f, k, 3) for f in range(4) for k in range(3))
+
+
+def test_killed_worker_fails_the_job(work):
+    r = run(["-n", "2", "-s", "1", os.path.join(ROOT, "bin", "linear.dmlc"),
+             "learn/linear/guide/demo.conf", "minibatch=100"], work,
+            env_extra={"WH_FAULT": "kill:1:3"}, timeout=120)
+    assert r.returncode != 0
+    assert "WH_FAULT" in r.stderr

@@ -43,6 +43,17 @@ def _log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _parse_fault(spec, rank):
+    """WH_FAULT=kill:<rank>:<after_n_minibatches> | sleep:<rank>:<sec_per_minibatch>
+    (fault injection for the failure / straggler tests)."""
+    if not spec:
+        return None
+    kind, r, arg = spec.split(":")
+    if int(r) != rank:
+        return None
+    return kind, float(arg)
+
+
 # --------------------------------------------------------------------------
 # scheduler
 # --------------------------------------------------------------------------
@@ -258,6 +269,8 @@ class Worker:
         self.device = learner.device
         self.host = _native.host()
         self.report_sec = max(0.1, float(conf.print_sec) / 2)
+        self.n_done = 0
+        self.fault = _parse_fault(os.environ.get("WH_FAULT", ""), comm.rank)
 
     def send(self, **kw):
         self.van.send("scheduler", _msg(**kw))
@@ -295,6 +308,15 @@ class Worker:
                 self.send(msg="ack")
             elif cmd == "iterate":
                 self.run_pass(d["type"], d["data_pass"], d.get("fmt", self.conf.data_format))
+
+    def _inject_fault(self):
+        kind, arg = self.fault
+        if kind == "kill" and self.n_done >= arg:
+            _log("[worker %d] WH_FAULT: killing myself after %d minibatches" % (
+                self.comm.rank, self.n_done))
+            os._exit(17)
+        if kind == "sleep":
+            time.sleep(arg)
 
     # -------------------------------------------------------- one pass
     def _empty_batch(self):
@@ -363,7 +385,10 @@ class Worker:
             elif not have:
                 break
             args = self._to_dev(batch) if batch is not None else self._empty_batch()
+            if self.fault and batch is not None:
+                self._inject_fault()
             py = self.learner.process(*args, wtype=wtype, data_pass=data_pass)
+            self.n_done += 1
             if wtype == PRED and batch is not None:
                 p = py.float().cpu()
                 if c.prob_predict:
