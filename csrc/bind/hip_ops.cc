@@ -366,6 +366,32 @@ Tensor gather_rows(const Tensor& in, const Tensor& idx) {
 
 int64_t vstride_for(int64_t dim) { return dim == 0 ? 0 : 4 * next_pow2((dim + 3) / 4); }
 
+Tensor spmv(const Tensor& offset, const Tensor& col, const c10::optional<Tensor>& val,
+            const Tensor& x) {
+  CHECK_IN(offset, torch::kInt64);
+  CHECK_IN(col, torch::kInt32);
+  CHECK_IN(x, torch::kFloat32);
+  c10::DeviceGuard g(offset.device());
+  const int64_t nrows = offset.numel() - 1;
+  auto y = torch::empty({nrows}, x.options());
+  wh::spmv(nrows, ptr<int64_t>(offset), ptr<int32_t>(col), optptr<float>(val), ptr<float>(x),
+           ptr<float>(y), cur_stream(x));
+  return y;
+}
+
+Tensor spmv_t(const Tensor& csc_off, const Tensor& csc_row, const c10::optional<Tensor>& csc_val,
+              const Tensor& p) {
+  CHECK_IN(csc_off, torch::kInt64);
+  CHECK_IN(csc_row, torch::kInt32);
+  CHECK_IN(p, torch::kFloat32);
+  c10::DeviceGuard g(p.device());
+  const int64_t ncol = csc_off.numel() - 1;
+  auto y = torch::empty({ncol}, p.options());
+  wh::spmv_t(ncol, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row), optptr<float>(csc_val),
+             ptr<float>(p), ptr<float>(y), cur_stream(p));
+  return y;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_hip, m) {
@@ -380,6 +406,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("synth_criteo", &synth_criteo);
   m.def("gather_rows", &gather_rows);
   m.def("vstride_for", &vstride_for);
+  m.def("spmv", &spmv, py::arg("offset"), py::arg("col"), py::arg("val"), py::arg("x"));
+  m.def("spmv_t", &spmv_t, py::arg("csc_off"), py::arg("csc_row"), py::arg("csc_val"),
+        py::arg("p"));
   py::class_<KVStore>(m, "KVStore")
       .def(py::init<int64_t, int64_t, int64_t, int64_t>(), py::arg("cap"), py::arg("vcap"),
            py::arg("dim"), py::arg("device"))

@@ -1,0 +1,102 @@
+"""BSP (rabit-style) apps on CPU through tracker/dmlc_local.py: L-BFGS linear
+and FM, checkpoint-restart after an injected rank failure, and the solver's
+numerics against a plain PyTorch reference of the reference objective."""
+import os
+import re
+import struct
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TRACKER = os.path.join(ROOT, "tracker", "dmlc_local.py")
+TRAIN = os.path.join(ROOT, "learn", "data", "agaricus.txt.train")
+TEST = os.path.join(ROOT, "learn", "data", "agaricus.txt.test")
+
+
+def run(args, cwd, env_extra=None, timeout=300):
+    env = dict(os.environ, WH_DEVICE="cpu")
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, TRACKER] + args, cwd=cwd, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def objvals(out):
+    return [float(x) for x in re.findall(r"new_objval=([-\d.e+]+)", out)]
+
+
+def test_lbfgs_ranks_agree_and_predict(tmp_path):
+    r1 = run(["-n", "1", os.path.join(ROOT, "bin", "lbfgs.dmlc"), TRAIN, "reg_L1=1",
+              "max_lbfgs_iter=15", "model_out=m1"], tmp_path)
+    r2 = run(["-n", "2", os.path.join(ROOT, "bin", "lbfgs.dmlc"), TRAIN, "reg_L1=1",
+              "max_lbfgs_iter=15", "model_out=m2"], tmp_path)
+    assert r1.returncode == 0 and r2.returncode == 0, r2.stderr[-2000:]
+    o1, o2 = objvals(r1.stdout), objvals(r2.stdout)
+    assert len(o1) == len(o2) >= 10
+    for a, b in zip(o1, o2):
+        assert abs(a - b) <= 1e-3 * abs(a) + 1e-3
+    assert o1[-1] < o1[0]
+    raw = open(tmp_path / "m2", "rb").read()
+    assert raw[:4] == b"binf" and len(raw) == 4 + 88 + 4 * 127
+    bs, nf, lt = struct.unpack_from("<f4xQi", raw, 4)
+    assert nf == 126 and lt == 1 and abs(bs) < 1e-6  # logit(0.5) == 0
+    r3 = run(["-n", "1", os.path.join(ROOT, "bin", "lbfgs.dmlc"), TEST, "task=pred",
+              "model_in=m2", "name_pred=p.txt"], tmp_path)
+    assert r3.returncode == 0, r3.stderr[-2000:]
+    preds = [float(x) for x in open(tmp_path / "p.txt")]
+    labels = [float(l.split()[0]) for l in open(TEST)]
+    acc = sum((p > 0.5) == (y > 0.5) for p, y in zip(preds, labels)) / len(labels)
+    assert len(preds) == 1611 and acc > 0.95
+
+
+def test_lbfgs_restart_from_checkpoint_matches(tmp_path):
+    base = [os.path.join(ROOT, "bin", "lbfgs.dmlc"), TRAIN, "reg_L1=1", "max_lbfgs_iter=8"]
+    ref = run(["-n", "2"] + base, tmp_path, {"WH_CKPT_DIR": str(tmp_path / "ck0")})
+    rr = run(["-n", "2", "--max-restart", "1"] + base, tmp_path,
+             {"WH_CKPT_DIR": str(tmp_path / "ck1"), "WH_FAULT": "die:1:4"})
+    assert ref.returncode == 0 and rr.returncode == 0, rr.stderr[-2000:]
+    assert "restart from version=4" in rr.stdout
+    assert "WH_FAULT" in rr.stderr
+    a, b = objvals(ref.stdout), objvals(rr.stdout)
+    assert abs(a[-1] - b[-1]) <= 1e-4 * abs(a[-1])
+
+
+def test_fm_lbfgs_trains(tmp_path):
+    r = run(["-n", "2", os.path.join(ROOT, "bin", "fm.dmlc"), TRAIN, "nfactor=4",
+             "max_lbfgs_iter=12", "reg_L2=1", "model_out=fm.model"], tmp_path)
+    assert r.returncode == 0, r.stderr[-2000:]
+    o = objvals(r.stdout)
+    assert o[-1] < 0.5 * o[0]
+    size = os.path.getsize(tmp_path / "fm.model")
+    assert size == 4 + 88 + 4 * (126 * 5 + 1)
+
+
+def test_fm_objective_gradient_matches_autograd():
+    """FM objective + gradient (fused FM kernels' CPU path) against autograd
+    on the reference formula (learn/lbfgs-fm/fm.h:84-107)."""
+    from wormhole_amd import _native
+    from wormhole_amd.models.lbfgs_models import FMObjective, _SplitData, margin_to_loss
+    from wormhole_amd.parallel.bsp import BSP
+    keys, off, val, lab, _ = _native.host().load_split(TRAIN, 0, 8, "libsvm")
+    bsp = BSP(torch.device("cpu"))
+    obj = FMObjective(bsp, _SplitData(keys, off, val, lab, torch.device("cpu")), torch.device("cpu"))
+    obj.set_param("nfactor", "3")
+    obj.set_param("reg_L2", "0.5")
+    obj.set_param("reg_L2_V", "0.25")
+    n = obj.init_num_dim()
+    w = obj.init_model(n) * 10
+    F, k = obj.param.num_feature, 3
+    wt = w.clone().double().requires_grad_(True)
+    rows = torch.repeat_interleave(torch.arange(off.numel() - 1), off[1:] - off[:-1])
+    X = torch.zeros(off.numel() - 1, F, dtype=torch.float64)
+    X[rows, keys] = 1.0
+    V = wt[F:F * (k + 1)].view(F, k)
+    py = obj.param.base_score + wt[-1] + X @ wt[:F] + 0.5 * ((X @ V) ** 2 - (X * X) @ (V * V)).sum(1)
+    loss = margin_to_loss(1, lab.double(), py).sum() + 0.25 * (wt[:F] ** 2).sum() + \
+        0.125 * (wt[F:F * (k + 1)] ** 2).sum()
+    loss.backward()
+    assert abs(obj.eval(w) - float(loss)) < 1e-3 * float(loss)
+    g = obj.calc_grad(w)
+    assert torch.allclose(g.double(), wt.grad, atol=1e-3, rtol=1e-3)

@@ -59,6 +59,30 @@ def fm_grad_post(grad, vstride, dim, clip, dropout, seed, normalize):
             gv /= n2 ** 0.5
 
 
+def spmv(offset, col, val, x):
+    """y = X x for CSR X (columns are dense local ids; col < 0 skipped)."""
+    if _gpu(x):
+        return _native.hip().spmv(offset, col, val, x)
+    import torch
+    nrows = offset.numel() - 1
+    rows = torch.repeat_interleave(torch.arange(nrows), offset[1:] - offset[:-1])
+    c = col.long()
+    m = c >= 0
+    v = val if (val is not None and val.numel()) else torch.ones(c.numel())
+    return torch.zeros(nrows, dtype=x.dtype).index_add_(0, rows[m], v[m] * x[c[m]])
+
+
+def spmv_t(csc_off, csc_row, csc_val, p):
+    """y = X^T p using the per-column occurrence lists of `localize`."""
+    if _gpu(p):
+        return _native.hip().spmv_t(csc_off, csc_row, csc_val, p)
+    import torch
+    ncol = csc_off.numel() - 1
+    key = torch.repeat_interleave(torch.arange(ncol), csc_off[1:] - csc_off[:-1])
+    v = csc_val if (csc_val is not None and csc_val.numel()) else torch.ones(csc_row.numel())
+    return torch.zeros(ncol, dtype=p.dtype).index_add_(0, key, v * p[csc_row.long()])
+
+
 def auc(py, label):
     if _gpu(py):
         return _native.hip().auc(py, label)

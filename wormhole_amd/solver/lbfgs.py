@@ -1,0 +1,278 @@
+"""Distributed vector-free OWL-QN L-BFGS (reference learn/solver/lbfgs.h:56-663,
+SURVEY C22).
+
+The 2m+1 history vectors (m weight deltas s, m gradient deltas y, and the
+steepest-descent direction) are sharded by parameter range: each rank keeps
+only its ``[range_begin, range_end)`` slice in device memory (8-aligned,
+lbfgs.h:126-136).  Per iteration the ranks compute the <= 5n new partial dot
+products with ONE batched device reduction, allreduce them (<= 50 doubles),
+run the scalar two-loop recursion on the (2m+1)^2 dot basis, build their
+direction slice as one skinny GEMV (coef[2m+1] @ H[2m+1, nsub]) and
+all-gather the slices (the reference allreduces a zero-padded full vector).
+Backtracking Armijo line search; OWL-QN pseudo-gradient and sign fixing for
+L1.  State is checkpointed every iteration through :class:`BSP`.
+"""
+import math
+
+import torch
+
+
+class LBFGSSolver:
+    def __init__(self, bsp, obj):
+        self.bsp = bsp
+        self.obj = obj
+        self.device = obj.device
+        self.reg_L1 = 0.0
+        self.max_linesearch_iter = 100
+        self.linesearch_backoff = 0.5
+        self.linesearch_c1 = 1e-4
+        self.min_lbfgs_iter = 5
+        self.max_lbfgs_iter = 500
+        self.lbfgs_stop_tol = 1e-5
+        self.size_memory = 10
+        self.num_dim = 0
+        self.silent = False
+
+    def set_param(self, name, val):
+        conv = {"num_dim": int, "size_memory": int, "reg_L1": float, "lbfgs_stop_tol": float,
+                "linesearch_backoff": float, "max_linesearch_iter": int,
+                "max_lbfgs_iter": int, "min_lbfgs_iter": int, "linesearch_c1": float}
+        if name in conv:
+            setattr(self, name, conv[name](val))
+
+    # ----------------------------------------------------------- indexing
+    def _map(self, i):
+        m = self.size_memory
+        if i == 2 * m:
+            return i
+        if i < m:
+            return (i + self.offset) % m
+        return (i + self.offset) % m + m
+
+    def _dot_idx(self, i, j):
+        if i > j:
+            i, j = j, i
+        return self._map(i), self._map(j)
+
+    def dotbuf(self, i, j):
+        a, b = self._dot_idx(i, j)
+        return self.data[a, b]
+
+    def _set_dotbuf(self, i, j, v):
+        a, b = self._dot_idx(i, j)
+        self.data[a, b] = v
+
+    def H(self, i):
+        return self.hist[self._map(i)]
+
+    # --------------------------------------------------------------- init
+    def init(self):
+        bsp = self.bsp
+        version, g, loc = bsp.load_checkpoint()
+        if version == 0:
+            self.num_dim = int(self.obj.init_num_dim())
+        else:
+            print("restart from version=%d" % version, flush=True)
+            self.size_memory = int(g["size_memory"])
+            self.num_dim = int(g["num_dim"])
+        nproc, rank = bsp.world, bsp.rank
+        step = (self.num_dim + nproc - 1) // nproc
+        step = (step + 7) // 8 * 8
+        self.step = step
+        self.rb = min(rank * step, self.num_dim)
+        self.re = min((rank + 1) * step, self.num_dim)
+        self.nsub = self.re - self.rb
+        m = self.size_memory
+        dev = self.device
+        self.hist = torch.zeros(2 * m + 1, self.nsub, dtype=torch.float32, device=dev)
+        if version == 0:
+            self.num_iteration = 0
+            self.offset = 0
+            self.num_useful = 0
+            self.data = torch.zeros(2 * m + 1, 2 * m + 1, dtype=torch.float64)
+            self.weight = self.obj.init_model(self.num_dim).to(dev)
+            bsp.broadcast(self.weight, 0)
+            self.old_objval = self.eval(self.weight)
+            self.init_objval = self.old_objval
+            if not self.silent:
+                bsp.tracker_print(
+                    "L-BFGS solver starts, num_dim=%d, init_objval=%g, size_memory=%d, "
+                    "RAM-approx=%d" % (self.num_dim, self.init_objval, m,
+                                       4 * 3 * self.num_dim + 4 * (2 * m + 1) * self.nsub))
+        else:
+            self.num_iteration = int(g["num_iteration"])
+            self.init_objval = float(g["init_objval"])
+            self.old_objval = float(g["old_objval"])
+            self.offset = int(g["offset"])
+            self.data = g["data"].clone()
+            self.weight = g["weight"].to(dev)
+            self.obj.load_state(g["obj"])
+            self.num_useful = int(loc["num_useful"])
+            for i in range(self.num_useful):
+                self.H(i).copy_(loc["s"][i].to(dev))
+                self.H(i + m).copy_(loc["y"][i].to(dev))
+
+    def _state(self):
+        m = self.size_memory
+        g = {"size_memory": m, "num_iteration": self.num_iteration, "num_dim": self.num_dim,
+             "init_objval": self.init_objval, "old_objval": self.old_objval,
+             "offset": self.offset, "data": self.data.clone(),
+             "weight": self.weight.detach().cpu().clone(), "obj": self.obj.save_state()}
+        loc = {"num_useful": self.num_useful,
+               "s": torch.stack([self.H(i).cpu() for i in range(self.num_useful)])
+               if self.num_useful else torch.zeros(0),
+               "y": torch.stack([self.H(i + m).cpu() for i in range(self.num_useful)])
+               if self.num_useful else torch.zeros(0)}
+        return g, loc
+
+    # ---------------------------------------------------------- iteration
+    def eval(self, w):
+        val = self.bsp.allreduce_scalar(float(self.obj.eval(w)))
+        if self.reg_L1 != 0.0:
+            val += float(w.abs().sum(dtype=torch.float64)) * self.reg_L1
+        return val
+
+    def update_one_iter(self):
+        g = self.obj.calc_grad(self.weight)
+        self.bsp.allreduce(g)
+        d, vdot = self.find_change_direction(g, self.weight)
+        new_w, it = self.backtrack_line_search(d, self.weight, vdot)
+        if it >= self.max_linesearch_iter:
+            raise RuntimeError("line search failed")
+        self.weight = new_w
+        if self.num_iteration > self.min_lbfgs_iter:
+            if self.old_objval - self.new_objval < self.lbfgs_stop_tol * self.init_objval:
+                return True
+        if not self.silent:
+            self.bsp.tracker_print(
+                "[%d] L-BFGS: linesearch finishes in %d rounds, new_objval=%g, improvment=%g" % (
+                    self.num_iteration, it, self.new_objval, self.old_objval - self.new_objval))
+        self.old_objval = self.new_objval
+        gs, loc = self._state()
+        v = self.bsp.checkpoint(gs, loc)
+        from ..parallel.bsp import fault_point
+        fault_point(self.bsp.rank, v)
+        return False
+
+    def run(self):
+        self.init()
+        while self.num_iteration < self.max_lbfgs_iter:
+            if self.update_one_iter():
+                break
+        if not self.silent:
+            nz = int((self.weight != 0).sum())
+            self.bsp.tracker_print("L-BFGS: finishes at iteration %d, %d/%d active weights" % (
+                self.num_iteration, nz, self.num_dim))
+        return self.weight
+
+    # ------------------------------------------------------------ OWL-QN
+    def set_l1_dir(self, grad, weight):
+        l1 = self.reg_L1
+        if l1 == 0.0:
+            return -grad
+        d = torch.where(weight > 0, -grad - l1, torch.where(weight < 0, -grad + l1, torch.zeros_like(grad)))
+        zero = weight == 0
+        d = torch.where(zero & (grad < -l1), -grad - l1, d)
+        d = torch.where(zero & (grad > l1), -grad + l1, d)
+        return d
+
+    def fix_dir_l1_sign(self, d, steep):
+        if self.reg_L1 != 0.0:
+            d = torch.where(d * steep <= 0, torch.zeros_like(d), d)
+        return d
+
+    def fix_weight_l1_sign(self, new_w, w):
+        if self.reg_L1 != 0.0:
+            new_w = torch.where(new_w * w < 0, torch.zeros_like(new_w), new_w)
+        return new_w
+
+    def find_change_direction(self, grad, weight):
+        m = self.size_memory
+        n = self.num_useful
+        rb, re = self.rb, self.re
+        gsub = grad[rb:re]
+        if n != 0:
+            y_last = self.H(m + n - 1)
+            y_last.copy_(gsub - y_last)  # y_{n-1} = g_new - g_old
+            self.H(2 * m).copy_(self.set_l1_dir(gsub, weight[rb:re]))
+            idx = []
+            for j in range(n):
+                idx += [(j, 2 * m), (j, n - 1), (j, m + n - 1)]
+            for j in range(n):
+                idx += [(m + j, 2 * m), (m + j, m + n - 1)]
+            ia = torch.tensor([self._map(a) for a, _ in idx], device=self.device)
+            ib = torch.tensor([self._map(b) for _, b in idx], device=self.device)
+            # all new partial dots in ONE batched reduction, then one allreduce
+            tmp = (self.hist[ia] * self.hist[ib]).sum(1, dtype=torch.float64)
+            self.bsp.allreduce(tmp)
+            tmp = tmp.cpu()
+            for k, (a, b) in enumerate(idx):
+                self._set_dotbuf(a, b, float(tmp[k]))
+            # two-loop recursion on the dot basis (vector-free)
+            alpha = [0.0] * n
+            delta = [0.0] * (2 * m + 1)
+            delta[2 * m] = 1.0
+            D = self.dotbuf
+            for j in range(n - 1, -1, -1):
+                vsum = sum(delta[k] * D(k, j) for k in range(2 * m + 1))
+                alpha[j] = vsum / D(j, m + j)
+                delta[m + j] -= alpha[j]
+            scale = D(n - 1, m + n - 1) / D(m + n - 1, m + n - 1)
+            delta = [x * scale for x in delta]
+            for j in range(n):
+                vsum = sum(delta[k] * D(k, m + j) for k in range(2 * m + 1))
+                beta = vsum / D(j, m + j)
+                delta[j] += alpha[j] - beta
+            coef = torch.zeros(2 * m + 1, dtype=torch.float32)
+            for k in list(range(n)) + list(range(m, m + n)) + [2 * m]:
+                coef[self._map(k)] = delta[k]
+            dirsub = coef.to(self.device) @ self.hist  # skinny GEMV over the shard
+            steep = self.H(2 * m)
+            dirsub = self.fix_dir_l1_sign(dirsub, steep)
+            vdot = -float((dirsub * steep).sum(dtype=torch.float64))
+            d = self._allgather_dir(dirsub)
+            vdot = self.bsp.allreduce_scalar(vdot)
+        else:
+            d = self.set_l1_dir(grad, weight)
+            vdot = -float((d * d).sum(dtype=torch.float64))
+        if n < m:
+            n += 1
+        else:
+            self.offset = (self.offset + 1) % m
+        self.num_useful = n
+        self.H(m + n - 1).copy_(gsub)
+        return d, vdot
+
+    def _allgather_dir(self, dirsub):
+        if self.bsp.world == 1:
+            return dirsub.clone()
+        pad = torch.zeros(self.step, dtype=dirsub.dtype, device=dirsub.device)
+        pad[: dirsub.numel()] = dirsub
+        parts = self.bsp.comm.allgather(pad)
+        return torch.cat(parts)[: self.num_dim]
+
+    def backtrack_line_search(self, d, w, vdot):
+        if not vdot < 0.0:
+            raise RuntimeError("not a descent direction (dot=%g)" % vdot)
+        alpha = 1.0
+        backoff = self.linesearch_backoff
+        if self.num_iteration == 0:
+            alpha = 1.0 / math.sqrt(-vdot)
+            backoff = 0.1
+        it = 0
+        old_val = self.old_objval
+        c1 = self.linesearch_c1
+        new_w = None
+        while True:
+            it += 1
+            if it >= self.max_linesearch_iter:
+                return new_w, it
+            new_w = self.fix_weight_l1_sign(w + d * alpha, w)
+            new_val = self.eval(new_w)
+            if new_val - old_val <= c1 * vdot * alpha:
+                self.new_objval = new_val
+                break
+            alpha *= backoff
+        self.H(self.num_useful - 1).copy_(new_w[self.rb:self.re] - w[self.rb:self.re])
+        self.num_iteration += 1
+        return new_w, it
