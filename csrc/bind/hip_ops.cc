@@ -366,6 +366,57 @@ Tensor gather_rows(const Tensor& in, const Tensor& idx) {
 
 int64_t vstride_for(int64_t dim) { return dim == 0 ? 0 : 4 * next_pow2((dim + 3) / 4); }
 
+// ---------------------------------------------------------------- kmeans
+Tensor kmeans_pack_x(const Tensor& X) {
+  CHECK_IN(X, torch::kFloat32);
+  TORCH_CHECK(X.dim() == 2, "X must be [n, f]");
+  c10::DeviceGuard g(X.device());
+  const int64_t n = X.size(0);
+  const int f = (int)X.size(1);
+  const int ks = wh::kmeans_ks(f);
+  auto Xp = torch::empty({(n + 31) / 32 * ks * 64}, X.options());
+  wh::kmeans_pack_x(ptr<float>(X), n, f, ptr<float>(Xp), cur_stream(X));
+  return Xp;
+}
+
+Tensor kmeans_pack_c(const Tensor& C) {
+  CHECK_IN(C, torch::kFloat32);
+  TORCH_CHECK(C.dim() == 2, "C must be [k, f]");
+  c10::DeviceGuard g(C.device());
+  const int k = (int)C.size(0), f = (int)C.size(1);
+  const int ks = wh::kmeans_ks(f);
+  auto Cp = torch::empty({(int64_t)((k + 31) / 32) * ks * 64}, C.options());
+  wh::kmeans_pack_c(ptr<float>(C), k, f, ptr<float>(Cp), cur_stream(C));
+  return Cp;
+}
+
+std::vector<Tensor> kmeans_assign(const Tensor& Xp, int64_t n, int64_t f, const Tensor& Cp,
+                                  int64_t k) {
+  CHECK_IN(Xp, torch::kFloat32);
+  CHECK_IN(Cp, torch::kFloat32);
+  const int ks = wh::kmeans_ks((int)f);
+  TORCH_CHECK(Xp.numel() == (n + 31) / 32 * ks * 64, "packed X size mismatch");
+  TORCH_CHECK(Cp.numel() == (k + 31) / 32 * ks * 64, "packed C size mismatch");
+  c10::DeviceGuard g(Xp.device());
+  auto assign = torch::empty({n}, Xp.options().dtype(torch::kInt32));
+  auto score = torch::empty({n}, Xp.options());
+  wh::kmeans_assign(ptr<float>(Xp), n, (int)f, ptr<float>(Cp), (int)k, ptr<int32_t>(assign),
+                    ptr<float>(score), cur_stream(Xp));
+  return {assign, score};
+}
+
+Tensor kmeans_accum(const Tensor& X, const Tensor& assign, int64_t k) {
+  CHECK_IN(X, torch::kFloat32);
+  CHECK_IN(assign, torch::kInt32);
+  c10::DeviceGuard g(X.device());
+  const int64_t n = X.size(0);
+  const int f = (int)X.size(1);
+  TORCH_CHECK(assign.numel() == n);
+  auto sums = torch::zeros({k, f + 1}, X.options());
+  wh::kmeans_accum(ptr<float>(X), n, f, ptr<int32_t>(assign), ptr<float>(sums), cur_stream(X));
+  return sums;
+}
+
 Tensor spmv(const Tensor& offset, const Tensor& col, const c10::optional<Tensor>& val,
             const Tensor& x) {
   CHECK_IN(offset, torch::kInt64);
@@ -407,6 +458,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gather_rows", &gather_rows);
   m.def("vstride_for", &vstride_for);
   m.def("spmv", &spmv, py::arg("offset"), py::arg("col"), py::arg("val"), py::arg("x"));
+  m.def("kmeans_pack_x", &kmeans_pack_x);
+  m.def("kmeans_pack_c", &kmeans_pack_c);
+  m.def("kmeans_assign", &kmeans_assign);
+  m.def("kmeans_accum", &kmeans_accum);
   m.def("spmv_t", &spmv_t, py::arg("csc_off"), py::arg("csc_row"), py::arg("csc_val"),
         py::arg("p"));
   py::class_<KVStore>(m, "KVStore")

@@ -140,6 +140,15 @@ void auc_from_sorted(const float* label_sorted, int64_t n, double* out, int64_t*
 void synth_criteo(int64_t nrows, uint64_t seed, uint64_t step, const int64_t* card,
                   int nfield, uint64_t* keys, float* label, int64_t* offset, hipStream_t s);
 
+// ------------------------------------------------------------ kmeans.hip
+int kmeans_ks(int f);  // padded MFMA k-steps (2 features each)
+void kmeans_pack_x(const float* X, int64_t n, int f, float* Xp, hipStream_t s);
+void kmeans_pack_c(const float* C, int k, int f, float* Cp, hipStream_t s);
+void kmeans_assign(const float* Xp, int64_t n, int f, const float* Cp, int k, int32_t* assign,
+                   float* score, hipStream_t s);
+void kmeans_accum(const float* X, int64_t n, int f, const int32_t* assign, float* sums,
+                  hipStream_t s);
+
 // -------------------------------------------------------------- exchange
 // gather rows: out[i, :] = in[idx[i], :]   (row width in floats)
 void gather_rows(const float* in, const int32_t* idx, int64_t n, int width, float* out,

@@ -100,3 +100,34 @@ def test_fm_objective_gradient_matches_autograd():
     assert abs(obj.eval(w) - float(loss)) < 1e-3 * float(loss)
     g = obj.calc_grad(w)
     assert torch.allclose(g.double(), wt.grad, atol=1e-3, rtol=1e-3)
+
+
+def test_kmeans_app_and_restart(tmp_path):
+    base = [os.path.join(ROOT, "bin", "kmeans.dmlc"), TRAIN, "4", "6"]
+    r = run(["-n", "2"] + base + ["km.txt"], tmp_path, {"WH_CKPT_DIR": str(tmp_path / "c0")})
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Finish 5-th iteration" in r.stdout
+    rows = [list(map(float, l.split())) for l in open(tmp_path / "km.txt")]
+    assert len(rows) == 4 and all(len(x) == 126 for x in rows)  # feature ids 0..125
+    for x in rows:  # centroids are L2-normalised
+        assert abs(sum(v * v for v in x) - 1.0) < 1e-4
+    r2 = run(["-n", "2", "--max-restart", "1"] + base + ["km2.txt"], tmp_path,
+             {"WH_CKPT_DIR": str(tmp_path / "c1"), "WH_FAULT": "die:0:3"})
+    assert r2.returncode == 0, r2.stderr[-2000:]
+    rows2 = [list(map(float, l.split())) for l in open(tmp_path / "km2.txt")]
+    for a, b in zip(rows, rows2):
+        assert max(abs(x - y) for x, y in zip(a, b)) < 1e-4
+
+
+def test_kmeans_converges_on_separated_clusters():
+    from wormhole_amd.models.kmeans import KMeans
+    from wormhole_amd.parallel.bsp import BSP
+    g = torch.Generator().manual_seed(0)
+    centers = torch.nn.functional.normalize(torch.randn(5, 16, generator=g), dim=1) * 10
+    lab = torch.randint(0, 5, (2000,), generator=g)
+    X = centers[lab] + 0.1 * torch.randn(2000, 16, generator=g)
+    km = KMeans(BSP(torch.device("cpu")), X, 5)
+    km.init_centroids(3)
+    for _ in range(10):
+        a = km.step()
+    assert km.objective(a) > 0.99

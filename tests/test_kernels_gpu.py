@@ -240,3 +240,44 @@ def test_difacto_learner_matches_cpu(hip):
     assert abs(pg[0] - pc[0]) / pc[0] < 1e-3
     assert abs(pg[1] - pc[1]) < 1e-3
     assert pg[6] == pc[6] and pg[7] == pc[7]
+
+
+@pytest.mark.parametrize("n,f,k", [(1000, 5, 7), (4096, 64, 33), (5000, 127, 100),
+                                   (3000, 128, 1000), (777, 200, 40)])
+def test_kmeans_assign_accum(hip, n, f, k):
+    g = torch.Generator().manual_seed(n + f + k)
+    X = torch.randn(n, f, generator=g)
+    C = torch.nn.functional.normalize(torch.randn(k, f, generator=g), dim=1)
+    Xd = X.to(DEV)
+    Xp = hip.kmeans_pack_x(Xd)
+    Cp = hip.kmeans_pack_c(C.to(DEV))
+    a, score = hip.kmeans_assign(Xp, n, f, Cp, k)
+    S = X.double() @ C.double().t()
+    ref_a = S.argmax(1)
+    a = a.cpu().long()
+    # exact fp32 MFMA: any disagreement must be a numerical near-tie
+    best = S.gather(1, ref_a[:, None])[:, 0]
+    got = S.gather(1, a[:, None])[:, 0]
+    assert bool(((best - got) <= 1e-4 * best.abs().clamp_min(1)).all())
+    assert (a == ref_a).float().mean() > 0.999
+    assert torch.allclose(score.cpu().double(), got, atol=1e-3, rtol=1e-4)
+    sums = hip.kmeans_accum(Xd, a.to(torch.int32).to(DEV), k).cpu()
+    ref_s = torch.zeros(k, f + 1)
+    ref_s[:, :f].index_add_(0, a, X)
+    ref_s[:, f].index_add_(0, a, torch.ones(n))
+    assert torch.allclose(sums, ref_s, atol=1e-3, rtol=1e-4)
+
+
+def test_spmv_kernels(hip):
+    keys, off, val, label = _rand_batch(3000, 20, 5000, 9, True)
+    uniq, ucnt, oc, lid, csc_off, csc_row, csc_val = hip.localize(
+        keys.to(DEV), off.to(DEV), val.to(DEV), 1)
+    x = torch.randn(uniq.numel())
+    y = hip.spmv(off.to(DEV), lid, val.to(DEV), x.to(DEV)).cpu()
+    rows = torch.repeat_interleave(torch.arange(3000), off[1:] - off[:-1])
+    ref_y = torch.zeros(3000).index_add_(0, rows, val * x[lid.cpu().long()])
+    assert torch.allclose(y, ref_y, atol=1e-4, rtol=1e-4)
+    p = torch.randn(3000)
+    yt = hip.spmv_t(csc_off, csc_row, csc_val, p.to(DEV)).cpu()
+    ref_t = torch.zeros(uniq.numel()).index_add_(0, lid.cpu().long(), val * p[rows])
+    assert torch.allclose(yt, ref_t, atol=1e-4, rtol=1e-4)

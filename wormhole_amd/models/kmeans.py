@@ -1,0 +1,104 @@
+"""Distributed spherical k-means (reference learn/kmeans/kmeans.cc).
+
+Each rank keeps its data split resident in HBM (densified, plus the MFMA
+fragment-packed copy), so one iteration is: pack C -> fused MFMA X.C^T +
+row argmax -> per-cluster sum/count with row-contiguous atomics -> one
+allreduce of K x (F+1) floats (RCCL) -> mean + L2 normalise -> checkpoint.
+
+Deviations from the reference (fixed): a zero-norm
+centroid row is skipped instead of aborting the normalisation of the rest,
+and an empty cluster keeps its previous centroid (with a warning) instead of
+exit(-1).
+"""
+import torch
+
+from .. import _native
+
+
+def densify(keys, offset, val, nrows, ncol, device):
+    X = torch.zeros(nrows, ncol, dtype=torch.float32, device=device)
+    if keys.numel():
+        rows = torch.repeat_interleave(torch.arange(nrows, device=device),
+                                       (offset[1:] - offset[:-1]).to(device))
+        v = val.to(device) if val is not None else torch.ones(keys.numel(), device=device)
+        X.index_put_((rows, keys.to(device)), v, accumulate=True)
+    return X
+
+
+def normalize_rows(C):
+    n = C.double().norm(dim=1)
+    scale = torch.where(n < 1e-6, torch.ones_like(n), 1.0 / n).to(C.dtype)
+    return C * scale[:, None]
+
+
+class KMeans:
+    def __init__(self, bsp, X, k):
+        self.bsp = bsp
+        self.X = X.contiguous()
+        self.n, self.f = X.shape
+        self.k = int(k)
+        self.device = X.device
+        self.gpu = X.is_cuda
+        self.Xp = _native.hip().kmeans_pack_x(self.X) if self.gpu else None
+        self.C = None
+
+    def init_centroids(self, seed=0):
+        """Reference InitCentroids: every rank draws num_cluster random rows of
+        its data (same srand(0) sequence), centroid i comes from a random rank."""
+        g = torch.Generator().manual_seed(seed)
+        if self.n == 0:
+            raise RuntimeError("dataset is empty")
+        idx = torch.randint(0, self.n, (self.k,), generator=g)
+        cand = self.X[idx.to(self.device)].contiguous()
+        parts = self.bsp.comm.allgather(cand) if self.bsp.world > 1 else [cand]
+        proc = torch.randint(0, self.bsp.world, (self.k,), generator=g).tolist()
+        C = torch.stack([parts[p][i] for i, p in enumerate(proc)])
+        self.C = normalize_rows(C)
+
+    def assign(self):
+        if self.gpu:
+            hip = _native.hip()
+            Cp = hip.kmeans_pack_c(self.C.contiguous())
+            a, _ = hip.kmeans_assign(self.Xp, self.n, self.f, Cp, self.k)
+            return a
+        s = self.X.double() @ self.C.double().t()
+        return s.argmax(1).to(torch.int32)
+
+    def accumulate(self, a):
+        if self.gpu:
+            return _native.hip().kmeans_accum(self.X, a, self.k)
+        sums = torch.zeros(self.k, self.f + 1, dtype=torch.float32)
+        sums[:, : self.f].index_add_(0, a.long(), self.X)
+        sums[:, self.f].index_add_(0, a.long(), torch.ones(self.n))
+        return sums
+
+    def step(self):
+        a = self.assign()
+        sums = self.accumulate(a)
+        self.bsp.allreduce(sums)  # rabit::Allreduce<Sum>(temp, K*(F+1), lazy_fn)
+        cnt = sums[:, self.f]
+        empty = cnt == 0
+        if bool(empty.any()):
+            self.bsp.tracker_print("Warning: found %d zero size cluster(s), maybe too less number "
+                                   "of datapoints? keeping their previous centroids"
+                                   % int(empty.sum()))
+        newC = sums[:, : self.f] / torch.where(empty, torch.ones_like(cnt), cnt)[:, None]
+        newC = torch.where(empty[:, None], self.C, newC)
+        self.C = normalize_rows(newC)
+        return a
+
+    def objective(self, a=None):
+        """Mean cosine similarity of rows to their centroid (diagnostic)."""
+        if a is None:
+            a = self.assign()
+        xn = self.X.norm(dim=1).clamp_min(1e-12)
+        s = (self.X * self.C[a.long()]).sum(1) / xn
+        tot = torch.tensor([float(s.sum()), float(self.n)], dtype=torch.float64,
+                           device=self.bsp.comm.device)
+        self.bsp.allreduce(tot)
+        return float(tot[0] / tot[1])
+
+    def save_text(self, path):
+        with open(path, "w") as f:
+            for row in self.C.cpu().tolist():
+                f.write(" ".join("%g" % v for v in row) + "\n")
