@@ -366,6 +366,83 @@ Tensor gather_rows(const Tensor& in, const Tensor& idx) {
 
 int64_t vstride_for(int64_t dim) { return dim == 0 ? 0 : 4 * next_pow2((dim + 3) / 4); }
 
+// ------------------------------------------------------------------ gbdt
+Tensor gbdt_bin(const Tensor& X, const Tensor& cuts, const Tensor& cut_off) {
+  CHECK_IN(X, torch::kFloat32);
+  CHECK_IN(cuts, torch::kFloat32);
+  CHECK_IN(cut_off, torch::kInt32);
+  TORCH_CHECK(X.dim() == 2 && cut_off.numel() == X.size(1) + 1);
+  c10::DeviceGuard g(X.device());
+  auto B = torch::empty({X.size(0), X.size(1)}, X.options().dtype(torch::kUInt8));
+  wh::gbdt_bin(ptr<float>(X), X.size(0), (int)X.size(1), ptr<float>(cuts), ptr<int32_t>(cut_off),
+               ptr<uint8_t>(B), cur_stream(X));
+  return B;
+}
+
+void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& gpair,
+               const Tensor& tasks, int64_t max_fcnt, const Tensor& hist) {
+  CHECK_IN(B, torch::kUInt8);
+  CHECK_IN(ridx, torch::kInt32);
+  CHECK_IN(gpair, torch::kFloat32);
+  CHECK_IN(tasks, torch::kInt32);
+  CHECK_IN(hist, torch::kFloat64);
+  TORCH_CHECK(nbin >= 1 && nbin <= 255, "nbin must be in [1, 255]");
+  TORCH_CHECK(wh::gbdt_hist_lds((int)max_fcnt, (int)nbin) <= 64 * 1024, "feature group too wide");
+  TORCH_CHECK(tasks.dim() == 2 && tasks.size(1) == 5);
+  c10::DeviceGuard g(B.device());
+  wh::gbdt_hist(ptr<uint8_t>(B), (int)B.size(1), (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
+                ptr<int32_t>(tasks), (int)tasks.size(0), (int)max_fcnt, ptr<double>(hist),
+                cur_stream(B));
+}
+
+// partition the positions of the split nodes; returns the new ridx
+Tensor gbdt_partition(const Tensor& B, const Tensor& ridx, const Tensor& pos_node,
+                      const Tensor& node_feat, const Tensor& node_bin, const Tensor& node_defl,
+                      const Tensor& seg_beg, const Tensor& seg_end, Tensor nleft_out) {
+  CHECK_IN(B, torch::kUInt8);
+  CHECK_IN(ridx, torch::kInt32);
+  CHECK_IN(pos_node, torch::kInt32);
+  c10::DeviceGuard g(B.device());
+  auto s = cur_stream(B);
+  const int64_t n = ridx.numel();
+  auto left = torch::empty({n}, ridx.options());
+  wh::gbdt_goleft(ptr<uint8_t>(B), (int)B.size(1), ptr<int32_t>(ridx), n, ptr<int32_t>(pos_node),
+                  ptr<int32_t>(node_feat), ptr<int32_t>(node_bin), ptr<uint8_t>(node_defl),
+                  ptr<int32_t>(left), s);
+  auto lscan = torch::empty({n + 1}, ridx.options().dtype(torch::kInt64));
+  auto tmp = torch::empty({wh::scan_tmp_elems(n)}, lscan.options());
+  wh::scan_i32(ptr<int32_t>(left), ptr<int64_t>(lscan), n, ptr<int64_t>(tmp), s);
+  // nleft[node] = lscan[end] - lscan[beg]
+  auto nl = (lscan.index_select(0, seg_end.to(torch::kInt64)) -
+             lscan.index_select(0, seg_beg.to(torch::kInt64))).to(torch::kInt32);
+  nleft_out.copy_(nl);
+  auto out = torch::empty_like(ridx);
+  wh::gbdt_scatter(ptr<int32_t>(ridx), n, ptr<int32_t>(pos_node), ptr<int32_t>(node_feat),
+                   ptr<int32_t>(seg_beg), ptr<int32_t>(nleft_out), ptr<int32_t>(left),
+                   ptr<int64_t>(lscan), ptr<int32_t>(out), s);
+  return out;
+}
+
+void gbdt_leaf_add(const Tensor& ridx, const Tensor& pos_node, const Tensor& leaf,
+                   const Tensor& margin) {
+  CHECK_IN(ridx, torch::kInt32);
+  CHECK_IN(leaf, torch::kFloat32);
+  CHECK_IN(margin, torch::kFloat32);
+  c10::DeviceGuard g(ridx.device());
+  wh::gbdt_leaf_add(ptr<int32_t>(ridx), ridx.numel(), ptr<int32_t>(pos_node), ptr<float>(leaf),
+                    ptr<float>(margin), cur_stream(ridx));
+}
+
+void gbdt_predict(const Tensor& X, const Tensor& feat, const Tensor& thr, const Tensor& left,
+                  const Tensor& right, const Tensor& defl, const Tensor& leaf, const Tensor& margin) {
+  CHECK_IN(X, torch::kFloat32);
+  CHECK_IN(margin, torch::kFloat32);
+  c10::DeviceGuard g(X.device());
+  wh::gbdt_predict(ptr<float>(X), X.size(0), (int)X.size(1), ptr<int32_t>(feat), ptr<float>(thr),
+                   ptr<int32_t>(left), ptr<int32_t>(right), ptr<uint8_t>(defl), ptr<float>(leaf),
+                   ptr<float>(margin), cur_stream(X));
+}
+
 // ---------------------------------------------------------------- kmeans
 Tensor kmeans_pack_x(const Tensor& X) {
   CHECK_IN(X, torch::kFloat32);
@@ -458,6 +535,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gather_rows", &gather_rows);
   m.def("vstride_for", &vstride_for);
   m.def("spmv", &spmv, py::arg("offset"), py::arg("col"), py::arg("val"), py::arg("x"));
+  m.def("gbdt_bin", &gbdt_bin);
+  m.def("gbdt_hist", &gbdt_hist);
+  m.def("gbdt_partition", &gbdt_partition);
+  m.def("gbdt_leaf_add", &gbdt_leaf_add);
+  m.def("gbdt_predict", &gbdt_predict);
   m.def("kmeans_pack_x", &kmeans_pack_x);
   m.def("kmeans_pack_c", &kmeans_pack_c);
   m.def("kmeans_assign", &kmeans_assign);

@@ -149,6 +149,25 @@ void kmeans_assign(const float* Xp, int64_t n, int f, const float* Cp, int k, in
 void kmeans_accum(const float* X, int64_t n, int f, const int32_t* assign, float* sums,
                   hipStream_t s);
 
+// -------------------------------------------------------------- gbdt.hip
+void gbdt_bin(const float* X, int64_t n, int f, const float* cuts, const int32_t* cut_off,
+              uint8_t* B, hipStream_t s);
+size_t gbdt_hist_lds(int fcnt, int nbin);
+// tasks: int32 [ntask x 5] = {node slot, fbeg, fcnt, rbeg, rend}; hist fp64 [slots x f x nbin x 2]
+void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
+               const int32_t* tasks, int ntask, int max_fcnt, double* hist, hipStream_t s);
+void gbdt_goleft(const uint8_t* B, int f, const int32_t* ridx, int64_t n, const int32_t* pos_node,
+                 const int32_t* node_feat, const int32_t* node_bin, const uint8_t* node_defl,
+                 int32_t* left, hipStream_t s);
+void gbdt_scatter(const int32_t* ridx, int64_t n, const int32_t* pos_node, const int32_t* node_feat,
+                  const int32_t* seg_beg, const int32_t* nleft, const int32_t* left,
+                  const int64_t* lscan, int32_t* out, hipStream_t s);
+void gbdt_leaf_add(const int32_t* ridx, int64_t n, const int32_t* pos_node, const float* leaf,
+                   float* margin, hipStream_t s);
+void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const float* thr,
+                  const int32_t* left, const int32_t* right, const uint8_t* defl,
+                  const float* leaf, float* margin, hipStream_t s);
+
 // -------------------------------------------------------------- exchange
 // gather rows: out[i, :] = in[idx[i], :]   (row width in floats)
 void gather_rows(const float* in, const int32_t* idx, int64_t n, int width, float* out,

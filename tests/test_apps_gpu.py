@@ -59,6 +59,49 @@ def test_lbfgs_gpu(work, capsys, monkeypatch):
     assert fm[-1] < 0.5 * fm[0]
 
 
+def test_gbdt_kernels_match_cpu():
+    from wormhole_amd.models import gbdt as G
+    from wormhole_amd.parallel.bsp import BSP
+    g = torch.Generator().manual_seed(1)
+    n, f = 20000, 40
+    X = torch.randn(n, f, generator=g)
+    X[torch.rand(n, f, generator=g) < 0.1] = float("nan")
+    X[:, 3] = torch.randint(0, 3, (n,), generator=g).float()  # few distinct values
+    y = (torch.nan_to_num(X[:, 0]) + torch.nan_to_num(X[:, 5]) > 0).float()
+    bsp = BSP(torch.device("cpu"))
+    p = G.GBDTParam()
+    p.max_depth = 6
+    p.objective = "binary:logistic"
+    dmc = G.DMatrix.from_dense(X, y, torch.device("cpu"))
+    dmg = G.DMatrix.from_dense(X, y, torch.device("cuda", 0))
+    cuts = G.Cuts.build(dmc, 64, bsp)
+    Bc, Bg = cuts.bin(dmc), cuts.bin(dmg)
+    assert torch.equal(Bc, Bg.cpu())
+    obj = G.Objective("binary:logistic")
+    trees = []
+    for dm, B in ((dmc, Bc), (dmg, Bg)):
+        margin = torch.zeros(n, device=dm.device)
+        tb = G.TreeBuilder(p, bsp, dm, cuts, B)
+        out = []
+        for _ in range(3):
+            t = tb.build(obj.gpair(margin, dm.label, None), margin)
+            out.append(t.dump(with_stats=False))
+        trees.append((out, margin.cpu()))
+    assert trees[0][0] == trees[1][0]
+    assert torch.allclose(trees[0][1], trees[1][1], atol=1e-5)
+
+
+def test_xgboost_app_gpu(work, capsys, monkeypatch):
+    from wormhole_amd.apps.xgboost_app import main
+    monkeypatch.setenv("WH_DEVICE", "auto")
+    assert main(["learn/xgboost/mushroom.conf", "num_round=3", "model_out=g.model"]) == 0
+    gpu = [l for l in capsys.readouterr().out.splitlines() if l.startswith("[")]
+    monkeypatch.setenv("WH_DEVICE", "cpu")
+    assert main(["learn/xgboost/mushroom.conf", "num_round=3", "model_out=c.model"]) == 0
+    cpu = [l for l in capsys.readouterr().out.splitlines() if l.startswith("[")]
+    assert gpu == cpu and len(gpu) == 3
+
+
 def test_kmeans_gpu_matches_cpu(work, monkeypatch):
     from wormhole_amd.apps.kmeans_app import main
     monkeypatch.setenv("WH_DEVICE", "auto")

@@ -1,0 +1,720 @@
+"""Distributed histogram GBDT: the xgboost learner the
+reference wraps (bin/xgboost.dmlc, learn/xgboost/), built from scratch on
+HIP kernels + RCCL.
+
+Algorithm (xgboost "hist" semantics, row split ``dsplit=row``):
+
+* quantile cuts per feature from rank-local order statistics that are
+  all-gathered and merged (<= max_bin cuts; features with few distinct values
+  get one bin per value); values are binned once into a uint8 matrix
+  (255 = missing) that stays resident in HBM;
+* per level, LDS-privatised (g, h) histograms are built only for the smaller
+  child of every split (the sibling is parent - child), allreduced over the
+  ranks (RCCL), and scanned for the best split of every node: gain
+  G_L^2/(H_L+lambda) + G_R^2/(H_R+lambda) - G^2/(H+lambda) with L1 ``alpha``,
+  ``min_child_weight`` on both children, and both default directions for
+  missing values;
+* rows are stably partitioned per node on the device;
+* the grown tree is pruned bottom-up with ``gamma`` (xgboost's prune updater)
+  and leaves store eta * weight; training margins are updated from the final
+  leaf segments, other sets by a device tree walk.
+"""
+import math
+import struct
+
+import numpy as np
+import torch
+
+from .. import _native
+
+RT_EPS = 1e-6
+MISSING_BIN = 255
+
+
+# ------------------------------------------------------------------ params
+class GBDTParam:
+    ALIASES = {"learning_rate": "eta", "min_split_loss": "gamma", "reg_lambda": "lambda",
+               "reg_alpha": "alpha", "n_estimators": "num_round"}
+
+    def __init__(self):
+        self.booster = "gbtree"
+        self.objective = "reg:linear"
+        self.eta = 0.3
+        self.gamma = 0.0
+        self.min_child_weight = 1.0
+        self.max_depth = 6
+        self.reg_lambda = 1.0
+        self.alpha = 0.0
+        self.base_score = 0.5
+        self.max_bin = 256
+        self.subsample = 1.0
+        self.colsample_bytree = 1.0
+        self.seed = 0
+        self.eval_metric = []
+        self.silent = 0
+
+    def set(self, name, val):
+        name = self.ALIASES.get(name, name)
+        if name == "lambda":
+            self.reg_lambda = float(val)
+        elif name in ("eta", "gamma", "min_child_weight", "alpha", "base_score", "subsample",
+                      "colsample_bytree"):
+            setattr(self, name, float(val))
+        elif name in ("max_depth", "max_bin", "seed", "silent"):
+            setattr(self, name, int(val))
+        elif name in ("objective", "booster"):
+            setattr(self, name, val)
+        elif name == "eval_metric":
+            self.eval_metric.append(val)
+        else:
+            return False
+        return True
+
+    def calc_gain(self, G, H):
+        g = _threshold_l1(G, self.alpha)
+        out = g * g / (H + self.reg_lambda)
+        return torch.where(H < self.min_child_weight, torch.zeros_like(out), out)
+
+    def calc_weight(self, G, H):
+        if H < self.min_child_weight:
+            return 0.0
+        g = G
+        if self.alpha > 0:
+            g = G - self.alpha if G > self.alpha else (G + self.alpha if G < -self.alpha else 0.0)
+        return -g / (H + self.reg_lambda)
+
+
+def _threshold_l1(G, alpha):
+    if alpha == 0:
+        return G
+    return torch.where(G > alpha, G - alpha, torch.where(G < -alpha, G + alpha, torch.zeros_like(G)))
+
+
+# ---------------------------------------------------------------- objective
+class Objective:
+    def __init__(self, name):
+        if name not in ("binary:logistic", "reg:logistic", "reg:linear", "reg:squarederror",
+                        "binary:logitraw"):
+            raise ValueError("unknown objective " + name)
+        self.name = name
+        self.logistic = name in ("binary:logistic", "reg:logistic", "binary:logitraw")
+
+    def prob_to_margin(self, base):
+        if self.logistic:
+            if not 0.0 < base < 1.0:
+                raise ValueError("base_score must be in (0,1) for logistic loss")
+            return -math.log(1.0 / base - 1.0)
+        return base
+
+    def gpair(self, margin, label, weight):
+        if self.logistic:
+            p = torch.sigmoid(margin)
+            g = p - label
+            h = torch.clamp(p * (1.0 - p), min=1e-16)
+        else:
+            g = margin - label
+            h = torch.ones_like(margin)
+        if weight is not None:
+            g, h = g * weight, h * weight
+        return torch.stack([g, h], 1).float().contiguous()
+
+    def pred(self, margin):
+        if self.name in ("binary:logistic", "reg:logistic"):
+            return torch.sigmoid(margin)
+        return margin
+
+    def default_metric(self):
+        return "error" if self.name == "binary:logistic" else "rmse"
+
+
+def eval_metric(name, pred, label, weight, bsp):
+    """Globally reduced metric (xgboost CLI names)."""
+    w = weight if weight is not None else torch.ones_like(label)
+    if name == "error":
+        s = (((pred > 0.5).float() != (label > 0.5).float()).float() * w).sum()
+        v = torch.stack([s.double(), w.sum().double()])
+        bsp.allreduce(v)
+        return float(v[0] / v[1])
+    if name == "logloss":
+        p = pred.clamp(1e-16, 1 - 1e-16)
+        s = (-(label * torch.log(p) + (1 - label) * torch.log(1 - p)) * w).sum()
+        v = torch.stack([s.double(), w.sum().double()])
+        bsp.allreduce(v)
+        return float(v[0] / v[1])
+    if name == "rmse":
+        s = (((pred - label) ** 2) * w).sum()
+        v = torch.stack([s.double(), w.sum().double()])
+        bsp.allreduce(v)
+        return math.sqrt(float(v[0] / v[1]))
+    if name == "auc":
+        from .. import ops
+        parts = bsp.comm.allgather_object((pred.cpu(), label.cpu())) if bsp.world > 1 else [
+            (pred.cpu(), label.cpu())]
+        p = torch.cat([a for a, _ in parts])
+        lab = torch.cat([b for _, b in parts])
+        return float(ops.ref.auc(p, lab))
+    raise ValueError("unknown eval_metric " + name)
+
+
+# ------------------------------------------------------------------- data
+class DMatrix:
+    """A rank's rows as a dense device matrix with NaN = missing."""
+
+    def __init__(self, keys, offset, val, label, weight, ncol, device):
+        n = offset.numel() - 1
+        self.n = n
+        self.ncol = int(ncol)
+        self.device = device
+        X = torch.full((n, self.ncol), float("nan"), dtype=torch.float32, device=device)
+        if keys.numel():
+            rows = torch.repeat_interleave(torch.arange(n), offset[1:] - offset[:-1]).to(device)
+            k = keys.to(device)
+            m = k < self.ncol
+            v = val.to(device) if val is not None else torch.ones(keys.numel(), device=device)
+            X[rows[m], k[m]] = v[m]
+        self.X = X
+        self.label = label.to(device).float()
+        self.weight = weight.to(device).float() if weight is not None else None
+        self.B = None
+
+    @staticmethod
+    def from_dense(X, label, device):
+        d = DMatrix.__new__(DMatrix)
+        d.n, d.ncol = X.shape
+        d.device = device
+        d.X = X.to(device).float().contiguous()
+        d.label = label.to(device).float()
+        d.weight = None
+        d.B = None
+        return d
+
+
+class Cuts:
+    def __init__(self, values, offsets):
+        self.values = values  # float32 [total]
+        self.offsets = offsets  # int32 [F + 1]
+
+    @property
+    def nbin_max(self):
+        o = self.offsets.tolist()
+        return max(b - a for a, b in zip(o, o[1:])) if len(o) > 1 else 1
+
+    @staticmethod
+    def build(dm, max_bin, bsp, nsample=2048):
+        """Merge rank-local order statistics into <= max_bin cuts per feature."""
+        max_bin = min(int(max_bin), 255)
+        F = dm.ncol
+        samples = []
+        counts = []
+        X = dm.X
+        for j in range(F):
+            col = X[:, j]
+            col = col[~torch.isnan(col)]
+            c = col.numel()
+            if c == 0:
+                s = torch.zeros(0)
+            else:
+                col, _ = torch.sort(col)
+                if c > nsample:
+                    idx = torch.linspace(0, c - 1, nsample, device=col.device).round().long()
+                    col = col[idx]
+                s = col.float().cpu()
+            samples.append(s)
+            counts.append(c)
+        gathered = bsp.comm.allgather_object((samples, counts)) if bsp.world > 1 else [
+            (samples, counts)]
+        vals, offs = [], [0]
+        for j in range(F):
+            parts = [(g[0][j], g[1][j]) for g in gathered]
+            v = torch.cat([p for p, _ in parts]) if parts else torch.zeros(0)
+            w = torch.cat([torch.full((p.numel(),), c / max(p.numel(), 1), dtype=torch.float64)
+                           for p, c in parts]) if parts else torch.zeros(0, dtype=torch.float64)
+            cuts = Cuts._feature_cuts(v, w, max_bin)
+            vals.extend(cuts)
+            offs.append(len(vals))
+        return Cuts(torch.tensor(vals, dtype=torch.float32), torch.tensor(offs, dtype=torch.int32))
+
+    @staticmethod
+    def _feature_cuts(v, w, max_bin):
+        if v.numel() == 0:
+            return [float("inf")]
+        order = torch.argsort(v)
+        v, w = v[order].double(), w[order]
+        uniq, inv = torch.unique_consecutive(v, return_inverse=True)
+        uw = torch.zeros(uniq.numel(), dtype=torch.float64).index_add_(0, inv, w)
+        last = float(uniq[-1])
+        top = last + abs(last) + 1.0
+        if uniq.numel() <= max_bin:
+            cuts = uniq[1:].tolist() + [top]
+        else:
+            cw = torch.cumsum(uw, 0)
+            total = float(cw[-1])
+            cuts = []
+            for b in range(1, max_bin):
+                target = total * b / max_bin
+                i = int(torch.searchsorted(cw, torch.tensor([target], dtype=torch.float64)))
+                i = min(i + 1, uniq.numel() - 1)
+                c = float(uniq[i])
+                if not cuts or c > cuts[-1]:
+                    cuts.append(c)
+            cuts.append(top)
+        return [float(np.float32(c)) for c in cuts]
+
+    def bin(self, dm):
+        if dm.X.is_cuda:
+            return _native.hip().gbdt_bin(dm.X, self.values.to(dm.device),
+                                          self.offsets.to(dm.device))
+        out = torch.full(dm.X.shape, MISSING_BIN, dtype=torch.uint8)
+        o = self.offsets.tolist()
+        for j in range(dm.ncol):
+            c = self.values[o[j]:o[j + 1]]
+            col = dm.X[:, j]
+            ok = ~torch.isnan(col)
+            b = torch.searchsorted(c, col[ok], right=True).clamp(max=c.numel() - 1)
+            out[ok, j] = b.to(torch.uint8)
+        return out
+
+
+# ------------------------------------------------------------------- tree
+class RegTree:
+    def __init__(self):
+        self.feat, self.bin, self.cond, self.defl = [], [], [], []
+        self.left, self.right, self.parent = [], [], []
+        self.leaf, self.gain, self.cover, self.base_weight = [], [], [], []
+
+    def add(self, parent):
+        i = len(self.feat)
+        self.feat.append(-1), self.bin.append(0), self.cond.append(0.0), self.defl.append(0)
+        self.left.append(-1), self.right.append(-1), self.parent.append(parent)
+        self.leaf.append(0.0), self.gain.append(0.0), self.cover.append(0.0)
+        self.base_weight.append(0.0)
+        return i
+
+    def is_leaf(self, i):
+        return self.feat[i] < 0
+
+    def depth(self, i):
+        d = 0
+        while self.parent[i] >= 0:
+            i = self.parent[i]
+            d += 1
+        return d
+
+    def device_arrays(self, device):
+        f = torch.tensor(self.feat, dtype=torch.int32, device=device)
+        return (f, torch.tensor(self.cond, dtype=torch.float32, device=device),
+                torch.tensor(self.left, dtype=torch.int32, device=device),
+                torch.tensor(self.right, dtype=torch.int32, device=device),
+                torch.tensor(self.defl, dtype=torch.uint8, device=device),
+                torch.tensor(self.leaf, dtype=torch.float32, device=device))
+
+    def predict_margin(self, X, margin):
+        if X.is_cuda:
+            _native.hip().gbdt_predict(X, *self.device_arrays(X.device), margin)
+            return margin
+        node = torch.zeros(X.shape[0], dtype=torch.long)
+        feat = torch.tensor(self.feat)
+        cond = torch.tensor(self.cond)
+        left, right = torch.tensor(self.left), torch.tensor(self.right)
+        defl = torch.tensor(self.defl, dtype=torch.bool)
+        leaf = torch.tensor(self.leaf)
+        for _ in range(64):
+            f = feat[node]
+            active = f >= 0
+            if not bool(active.any()):
+                break
+            v = X[torch.arange(X.shape[0]), f.clamp(min=0)]
+            go_left = torch.where(torch.isnan(v), defl[node], v < cond[node])
+            nxt = torch.where(go_left, left[node], right[node])
+            node = torch.where(active, nxt, node)
+        margin += leaf[node]
+        return margin
+
+    # -------------------------------------------------------------- dump
+    def dump(self, fmap=None, with_stats=False):
+        out = []
+
+        def rec(i, depth):
+            pad = "\t" * depth
+            if self.is_leaf(i):
+                s = "%s%d:leaf=%s" % (pad, i, _fmt(self.leaf[i]))
+                if with_stats:
+                    s += ",cover=%s" % _fmt(self.cover[i])
+                out.append(s)
+                return
+            f = self.feat[i]
+            name, typ = (fmap[f] if fmap and f < len(fmap) else ("f%d" % f, "q"))
+            if typ == "i":
+                # indicator: "yes" is the branch a present feature (value 1) takes
+                yes, no = (self.left[i], self.right[i]) if 1.0 < self.cond[i] else (
+                    self.right[i], self.left[i])
+                s = "%s%d:[%s] yes=%d,no=%d" % (pad, i, name, yes, no)
+            elif typ == "int":
+                s = "%s%d:[%s<%d] yes=%d,no=%d" % (pad, i, name, int(math.ceil(self.cond[i])),
+                                                   self.left[i], self.right[i])
+            else:
+                s = "%s%d:[%s<%s] yes=%d,no=%d" % (pad, i, name, _fmt(self.cond[i]),
+                                                   self.left[i], self.right[i])
+            if typ != "i":
+                s += ",missing=%d" % (self.left[i] if self.defl[i] else self.right[i])
+            if with_stats:
+                s += ",gain=%s,cover=%s" % (_fmt(self.gain[i]), _fmt(self.cover[i]))
+            out.append(s)
+            rec(self.left[i], depth + 1)
+            rec(self.right[i], depth + 1)
+        rec(0, 0)
+        return "\n".join(out) + "\n"
+
+
+def _fmt(x):
+    return "%g" % x
+
+
+def load_fmap(path):
+    names = []
+    for line in open(path):
+        parts = line.rstrip("\n").split("\t")
+        if len(parts) < 3:
+            continue
+        fid = int(parts[0])
+        while len(names) <= fid:
+            names.append(("f%d" % len(names), "q"))
+        names[fid] = (parts[1], parts[2])
+    return names
+
+
+# ---------------------------------------------------------------- builder
+class TreeBuilder:
+    """Depth-wise histogram tree growth on one DMatrix split per rank."""
+
+    def __init__(self, param, bsp, dm, cuts, B):
+        self.p = param
+        self.bsp = bsp
+        self.dm = dm
+        self.cuts = cuts
+        self.B = B.contiguous()
+        self.F = dm.ncol
+        self.nbin = max(1, cuts.nbin_max)
+        self.gpu = B.is_cuda
+        self.device = B.device
+        fg = max(1, (64 * 1024) // (self.nbin * 8))  # features per LDS histogram block
+        self.fgroups = [(j, min(fg, self.F - j)) for j in range(0, self.F, fg)]
+        self.max_fcnt = max(c for _, c in self.fgroups) if self.fgroups else 1
+        self.chunk = 2048
+        o = cuts.offsets.tolist()
+        nb = torch.tensor([b - a for a, b in zip(o, o[1:])])
+        self.bin_mask = torch.arange(self.nbin)[None, :] < nb[:, None]  # [F, nbin]
+        self.valid_mask = self.bin_mask.clone()
+
+    def sample_features(self, gen):
+        """colsample_bytree: restrict this tree's candidate features."""
+        self.valid_mask = self.bin_mask.clone()
+        if self.p.colsample_bytree < 1.0 and self.F > 0:
+            k = max(1, int(round(self.p.colsample_bytree * self.F)))
+            keep = torch.randperm(self.F, generator=gen)[:k]
+            m = torch.zeros(self.F, dtype=torch.bool)
+            m[keep] = True
+            self.valid_mask &= m[:, None]
+
+    # ----------------------------------------------------------- histograms
+    def _build_hist(self, ridx, gpair, segs, slots, nslot):
+        """segs: list of (beg, end) local row ranges; slots: output slot of each."""
+        hist = torch.zeros(nslot, self.F, self.nbin, 2, dtype=torch.float64, device=self.device)
+        if self.gpu:
+            tasks = []
+            for (b, e), s in zip(segs, slots):
+                for r in range(b, e, self.chunk):
+                    for fb, fc in self.fgroups:
+                        tasks.append((s, fb, fc, r, min(e, r + self.chunk)))
+            if tasks:
+                t = torch.tensor(tasks, dtype=torch.int32).to(self.device)
+                _native.hip().gbdt_hist(self.B, self.nbin, ridx, gpair, t, self.max_fcnt, hist)
+        else:
+            for (b, e), s in zip(segs, slots):
+                if e <= b:
+                    continue
+                rows = ridx[b:e].long()
+                bins = self.B[rows].long()  # [r, F]
+                gh = gpair[rows].double()  # [r, 2]
+                ok = bins != MISSING_BIN
+                flat = (torch.arange(self.F)[None, :] * self.nbin + bins.clamp(max=self.nbin - 1))
+                for c in range(2):
+                    val = gh[:, c][:, None].expand_as(flat)[ok]
+                    hist[s].view(-1, 2)[:, c].index_add_(0, flat[ok], val)
+        return hist
+
+    # -------------------------------------------------------- split search
+    def _find_splits(self, hist, totals):
+        """hist [S, F, nbin, 2] (global); totals [S, 2] -> per slot best split."""
+        p = self.p
+        cum = hist.cumsum(2)
+        present = cum[:, :, -1, :]
+        tot = totals[:, None, None, :]
+        miss = (totals[:, None, :] - present)[:, :, None, :]
+        G, H = totals[:, 0], totals[:, 1]
+        parent_gain = p.calc_gain(G, H)[:, None, None]
+        best = []
+        cands = []
+        for defl in (0, 1):
+            L = cum + (miss if defl else 0.0)
+            R = tot - L
+            ok = (L[..., 1] >= p.min_child_weight) & (R[..., 1] >= p.min_child_weight)
+            gain = p.calc_gain(L[..., 0], L[..., 1]) + p.calc_gain(R[..., 0], R[..., 1]) - parent_gain
+            gain = torch.where(ok, gain, torch.full_like(gain, -float("inf")))
+            cands.append((gain, L))
+        gain = torch.stack([c[0] for c in cands], -1)  # [S, F, nbin, 2dir]
+        # thresholds past a feature's own bin count, and features dropped by
+        # colsample_bytree, are not candidates
+        gain = torch.where(self.valid_mask.to(gain.device)[None, :, :, None], gain,
+                           torch.full_like(gain, -float("inf")))
+        S = gain.shape[0]
+        flat = gain.reshape(S, -1)
+        arg = flat.argmax(1)
+        bg = flat.gather(1, arg[:, None])[:, 0]
+        d = arg % 2
+        rest = arg // 2
+        b = rest % self.nbin
+        f = rest // self.nbin
+        Ls = torch.stack([cands[int(di)][1][s, f[s], b[s]] for s, di in enumerate(d.tolist())]) \
+            if S else torch.zeros(0, 2, dtype=torch.float64)
+        return bg.cpu(), f.cpu(), b.cpu(), d.cpu(), Ls.cpu()
+
+    # ----------------------------------------------------------------- build
+    def build(self, gpair, margin):
+        p = self.p
+        n = self.dm.n
+        dev = self.device
+        tree = RegTree()
+        root = tree.add(-1)
+        ridx = torch.arange(n, dtype=torch.int32, device=dev)
+        tot = gpair.double().sum(0) if n else torch.zeros(2, dtype=torch.float64, device=dev)
+        self.bsp.allreduce(tot)
+        totals = {root: tot.cpu()}
+        seg = {root: (0, n)}
+        hist_root = self._build_hist(ridx, gpair, [seg[root]], [0], 1)
+        self.bsp.allreduce(hist_root)
+        hists = {root: hist_root[0]}
+        frontier = [root]
+        cuts_v = self.cuts.values.tolist()
+        cuts_o = self.cuts.offsets.tolist()
+        for depth in range(p.max_depth + 1):
+            if not frontier:
+                break
+            for nd in frontier:
+                G, H = float(totals[nd][0]), float(totals[nd][1])
+                tree.cover[nd] = H
+                tree.base_weight[nd] = p.calc_weight(G, H)
+                tree.leaf[nd] = p.eta * tree.base_weight[nd]
+            if depth == p.max_depth:
+                break
+            S = len(frontier)
+            H_all = torch.stack([hists[nd] for nd in frontier])
+            T_all = torch.stack([totals[nd] for nd in frontier]).to(H_all.device)
+            bg, bf, bb, bd, bL = self._find_splits(H_all, T_all)
+            split_nodes = []
+            for k, nd in enumerate(frontier):
+                if float(bg[k]) > RT_EPS:
+                    f, b = int(bf[k]), int(bb[k])
+                    tree.feat[nd] = f
+                    tree.bin[nd] = b
+                    tree.cond[nd] = cuts_v[cuts_o[f] + b]
+                    tree.defl[nd] = int(bd[k])
+                    tree.gain[nd] = float(bg[k])
+                    l, r = tree.add(nd), tree.add(nd)
+                    tree.left[nd], tree.right[nd] = l, r
+                    totals[l] = bL[k].double()
+                    totals[r] = (totals[nd] - bL[k]).double()
+                    split_nodes.append(nd)
+            if not split_nodes:
+                break
+            # ---- partition rows of the split nodes
+            nnode = len(tree.feat)
+            node_feat = torch.full((nnode,), -1, dtype=torch.int32)
+            node_bin = torch.zeros(nnode, dtype=torch.int32)
+            node_defl = torch.zeros(nnode, dtype=torch.uint8)
+            seg_beg = torch.zeros(nnode, dtype=torch.int32)
+            seg_end = torch.zeros(nnode, dtype=torch.int32)
+            for nd in split_nodes:
+                node_feat[nd] = tree.feat[nd]
+                node_bin[nd] = tree.bin[nd]
+                node_defl[nd] = tree.defl[nd]
+            for nd, (b, e) in seg.items():
+                seg_beg[nd], seg_end[nd] = b, e
+            pos_node = self._pos_node(seg, n)
+            ridx, nleft = self._partition(ridx, pos_node, node_feat, node_bin, node_defl,
+                                          seg_beg, seg_end)
+            nleft = nleft.tolist()
+            new_frontier = []
+            build_segs, build_slots, small, big = [], [], [], []
+            for nd in split_nodes:
+                b, e = seg.pop(nd)
+                l, r = tree.left[nd], tree.right[nd]
+                seg[l] = (b, b + nleft[nd])
+                seg[r] = (b + nleft[nd], e)
+                new_frontier += [l, r]
+                # build the child with the smaller GLOBAL hessian, derive the other
+                s_, g_ = (l, r) if float(totals[l][1]) <= float(totals[r][1]) else (r, l)
+                small.append(s_)
+                big.append(g_)
+                build_segs.append(seg[s_])
+                build_slots.append(len(build_slots))
+            for nd in frontier:
+                if nd not in split_nodes:
+                    seg.pop(nd, None)  # finished leaf: its rows are final
+            hsmall = self._build_hist(ridx, gpair, build_segs, build_slots, len(build_slots))
+            self.bsp.allreduce(hsmall)
+            for k, nd in enumerate(split_nodes):
+                hists[small[k]] = hsmall[k]
+                hists[big[k]] = hists[nd] - hsmall[k]
+                del hists[nd]
+            frontier = new_frontier
+        self._prune(tree)
+        # margins of the training rows from the final leaf segments
+        self._apply_leaves(tree, ridx, margin, n)
+        return tree
+
+    def _pos_node(self, seg, n):
+        pos = torch.full((n,), -1, dtype=torch.int32)
+        for nd, (b, e) in seg.items():
+            pos[b:e] = nd
+        return pos.to(self.device)
+
+    def _partition(self, ridx, pos_node, node_feat, node_bin, node_defl, seg_beg, seg_end):
+        dev = self.device
+        if self.gpu:
+            nleft = torch.zeros(node_feat.numel(), dtype=torch.int32, device=dev)
+            out = _native.hip().gbdt_partition(self.B, ridx, pos_node, node_feat.to(dev),
+                                               node_bin.to(dev), node_defl.to(dev),
+                                               seg_beg.to(dev), seg_end.to(dev), nleft)
+            return out, nleft.cpu()
+        out = ridx.clone()
+        nleft = torch.zeros(node_feat.numel(), dtype=torch.int32)
+        for nd in range(node_feat.numel()):
+            f = int(node_feat[nd])
+            if f < 0:
+                continue
+            b, e = int(seg_beg[nd]), int(seg_end[nd])
+            rows = ridx[b:e].long()
+            bins = self.B[rows, f].long()
+            left = torch.where(bins == MISSING_BIN, torch.full_like(bins, int(node_defl[nd])),
+                               (bins <= int(node_bin[nd])).long()).bool()
+            nl = int(left.sum())
+            out[b:b + nl] = ridx[b:e][left]
+            out[b + nl:e] = ridx[b:e][~left]
+            nleft[nd] = nl
+        return out, nleft
+
+    def _prune(self, tree):
+        """xgboost prune updater: collapse splits whose loss_chg < gamma."""
+        changed = True
+        while changed:
+            changed = False
+            for i in range(len(tree.feat)):
+                if tree.is_leaf(i):
+                    continue
+                l, r = tree.left[i], tree.right[i]
+                if tree.is_leaf(l) and tree.is_leaf(r) and tree.gain[i] < self.p.gamma:
+                    tree.feat[i] = -1
+                    tree.leaf[i] = self.p.eta * tree.base_weight[i]
+                    changed = True
+        self._compact(tree)
+
+    @staticmethod
+    def _compact(tree):
+        """Renumber reachable nodes in BFS order (like xgboost's node ids)."""
+        order = [0]
+        k = 0
+        while k < len(order):
+            i = order[k]
+            if not tree.is_leaf(i):
+                order += [tree.left[i], tree.right[i]]
+            k += 1
+        remap = {old: new for new, old in enumerate(order)}
+        t = RegTree()
+        for old in order:
+            t.add(remap.get(tree.parent[old], -1) if tree.parent[old] >= 0 else -1)
+        for old in order:
+            i = remap[old]
+            t.feat[i] = tree.feat[old]
+            t.bin[i], t.cond[i], t.defl[i] = tree.bin[old], tree.cond[old], tree.defl[old]
+            t.leaf[i], t.gain[i], t.cover[i] = tree.leaf[old], tree.gain[old], tree.cover[old]
+            t.base_weight[i] = tree.base_weight[old]
+            if not tree.is_leaf(old):
+                t.left[i], t.right[i] = remap[tree.left[old]], remap[tree.right[old]]
+        tree.__dict__.update(t.__dict__)
+        tree._remap = remap
+
+    def _apply_leaves(self, tree, ridx, margin, n):
+        # rows still sit in the segments of the (pre-prune) frontier leaves; a
+        # device tree walk on the binned values is simplest and exact
+        if n == 0:
+            return
+        tree.predict_margin(self.dm.X, margin)
+
+
+# ---------------------------------------------------------------- booster
+class Booster:
+    MAGIC = b"WHGB"
+
+    def __init__(self, param, num_feature):
+        self.param = param
+        self.num_feature = int(num_feature)
+        self.trees = []
+        self.obj = Objective(param.objective)
+        self.base_margin = self.obj.prob_to_margin(param.base_score)
+
+    def predict_margin(self, dm, ntree_limit=0):
+        margin = torch.full((dm.n,), self.base_margin, dtype=torch.float32, device=dm.device)
+        trees = self.trees[:ntree_limit] if ntree_limit else self.trees
+        for t in trees:
+            t.predict_margin(dm.X, margin)
+        return margin
+
+    def save(self, path):
+        p = self.param
+        with open(path, "wb") as f:
+            f.write(self.MAGIC)
+            hdr = ("%s|%g|%d|%d" % (p.objective, p.base_score, self.num_feature,
+                                     len(self.trees))).encode()
+            f.write(struct.pack("<I", len(hdr)) + hdr)
+            for t in self.trees:
+                n = len(t.feat)
+                f.write(struct.pack("<I", n))
+                arr = np.zeros(n, dtype=[("feat", "<i4"), ("cond", "<f4"), ("left", "<i4"),
+                                         ("right", "<i4"), ("defl", "<i4"), ("leaf", "<f4"),
+                                         ("gain", "<f4"), ("cover", "<f4")])
+                for k in ("feat", "cond", "left", "right", "defl", "leaf", "gain", "cover"):
+                    arr[k] = getattr(t, k)
+                f.write(arr.tobytes())
+
+    @staticmethod
+    def load(path, param):
+        with open(path, "rb") as f:
+            if f.read(4) != Booster.MAGIC:
+                raise ValueError("invalid model file " + path)
+            (ln,) = struct.unpack("<I", f.read(4))
+            objective, base, nf, ntree = f.read(ln).decode().split("|")
+            param.objective = objective
+            param.base_score = float(base)
+            b = Booster(param, int(nf))
+            for _ in range(int(ntree)):
+                (n,) = struct.unpack("<I", f.read(4))
+                arr = np.frombuffer(f.read(32 * n), dtype=[
+                    ("feat", "<i4"), ("cond", "<f4"), ("left", "<i4"), ("right", "<i4"),
+                    ("defl", "<i4"), ("leaf", "<f4"), ("gain", "<f4"), ("cover", "<f4")])
+                t = RegTree()
+                for k in ("feat", "cond", "left", "right", "defl", "leaf", "gain", "cover"):
+                    setattr(t, k, [x.item() for x in arr[k]])
+                t.parent = [-1] * n
+                for i in range(n):
+                    if t.feat[i] >= 0:
+                        t.parent[t.left[i]] = i
+                        t.parent[t.right[i]] = i
+                t.bin = [0] * n
+                t.base_weight = [0.0] * n
+                b.trees.append(t)
+        return b
+
+    def dump(self, fmap=None, with_stats=False):
+        return "".join("booster[%d]:\n%s" % (i, t.dump(fmap, with_stats))
+                       for i, t in enumerate(self.trees))
