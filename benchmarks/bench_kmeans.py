@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""k-means benchmark (BASELINE.json config: k=1000 on dense 10M x 128).
+
+Strong scaling: --rows is the TOTAL row count, split over the ranks.  Every
+timed iteration is a full reference iteration (assign + accumulate + RCCL
+allreduce of K x (F+1) + normalise).  Data: synthetic Gaussian mixture on
+the device.
+
+    python benchmarks/bench_kmeans.py [--rows 10000000] [--dim 128] [--k 1000] [--iters 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from wormhole_amd.models.kmeans import KMeans  # noqa: E402
+from wormhole_amd.parallel.bsp import BSP  # noqa: E402
+from wormhole_amd.parallel.comm import env_local_rank  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--k", type=int, default=1000)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    a = ap.parse_args()
+    torch.cuda.set_device(env_local_rank())
+    dev = torch.device("cuda", env_local_rank())
+    bsp = BSP(dev)
+    n = a.rows // bsp.world
+    g = torch.Generator(device=dev).manual_seed(1234 + bsp.rank)
+    centers = torch.randn(a.k, a.dim, device=dev, generator=g)
+    lab = torch.randint(0, a.k, (n,), device=dev, generator=g)
+    X = centers[lab] + 0.5 * torch.randn(n, a.dim, device=dev, generator=g)
+    del lab
+    km = KMeans(bsp, X, a.k)
+    km.init_centroids(0)
+    for _ in range(a.warmup):
+        km.step()
+    torch.cuda.synchronize()
+    bsp.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        km.step()
+    torch.cuda.synchronize()
+    bsp.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    bsp.allreduce(t, "max")
+    dt = float(t.item())
+    flops = 2.0 * a.rows * a.k * a.dim * a.iters
+    if bsp.rank == 0:
+        print(json.dumps({"metric": "k-means iterations/s (k=%d, dense %dx%d)" % (a.k, a.rows, a.dim),
+                          "value": a.iters / dt, "unit": "iter/s", "n_gpus": bsp.world,
+                          "ms_per_iter": 1000 * dt / a.iters, "rows_per_s": a.rows * a.iters / dt,
+                          "assign_tflops": flops / dt / 1e12, "scaling": "strong",
+                          "dtype": "fp32 (exact fp32 MFMA)", "data": "synthetic gaussian mixture"}),
+              flush=True)
+    bsp.finalize()
+
+
+if __name__ == "__main__":
+    main()

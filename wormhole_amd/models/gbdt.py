@@ -574,10 +574,21 @@ class TreeBuilder:
         return tree
 
     def _pos_node(self, seg, n):
-        pos = torch.full((n,), -1, dtype=torch.int32)
-        for nd, (b, e) in seg.items():
-            pos[b:e] = nd
-        return pos.to(self.device)
+        """Node id of every ridx position (-1 for rows of finished leaves),
+        expanded on the device from the segment list."""
+        ids, lens = [], []
+        cur = 0
+        for nd, (b, e) in sorted(seg.items(), key=lambda kv: kv[1][0]):
+            if b > cur:
+                ids.append(-1), lens.append(b - cur)
+            ids.append(nd), lens.append(e - b)
+            cur = e
+        if cur < n:
+            ids.append(-1), lens.append(n - cur)
+        dev = self.device
+        return torch.repeat_interleave(torch.tensor(ids, dtype=torch.int32, device=dev),
+                                       torch.tensor(lens, dtype=torch.int64, device=dev),
+                                       output_size=n)
 
     def _partition(self, ridx, pos_node, node_feat, node_bin, node_defl, seg_beg, seg_end):
         dev = self.device
