@@ -99,7 +99,10 @@ def main():
         vs = value / LINEAR_REF_EX_PER_S
         model = "linear-ftrl"
     if comm.rank == 0:
-        nex = max(prog[5], 1.0)
+        if args.model == "difacto":  # learn/difacto/progress.h layout
+            logloss, auc = prog[0] / max(prog[5], 1.0), prog[1] / max(prog[4], 1.0)
+        else:  # learn/linear/progress.h layout
+            logloss, auc = prog[0] / max(prog[4], 1.0), prog[2] / max(prog[3], 1.0)
         print(json.dumps({
             "metric": metric, "value": value, "unit": "examples/s", "n_gpus": n,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * dt / args.steps,
@@ -108,7 +111,7 @@ def main():
             "config": {"model": model, "global_batch": args.batch * n, "seq_len": 39,
                        "parallelism": "dp%d+kvshard%d" % (n, n),
                        "minibatch_per_gpu": args.batch, "threshold": 100, "nnz_per_example": 39},
-            "train_logloss": prog[0] / nex, "train_auc": prog[1] / max(prog[4], 1.0),
+            "train_logloss": logloss, "train_auc": auc,
         }), flush=True)
     comm.finalize()
 
