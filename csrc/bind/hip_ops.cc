@@ -220,23 +220,47 @@ class KVStore {
                          dhp(h, threshold, l1_shrk, seed), cur_stream(slot));
   }
 
-  Tensor difacto_pull(const Tensor& slot, bool l1_shrk) {
+  // Variable-length pull. Returns (hdr [n,2] f32 {w, vidx bits}, vc [mcap, vstride],
+  // vpos i64 [n+1]); m = vpos[n] stays on the device (vc is sized by the
+  // host-side bound mcap = n so the step needs no host synchronisation).
+  std::vector<Tensor> difacto_pull(const Tensor& slot, bool l1_shrk) {
     CHECK_IN(slot, torch::kInt32);
     c10::DeviceGuard g(slot.device());
-    auto out = torch::empty({slot.numel(), vstride_ + 4}, slot.options().dtype(torch::kFloat32));
-    wh::difacto_pull(table(), ptr<int32_t>(slot), slot.numel(), l1_shrk ? 1 : 0, ptr<float>(out),
-                     cur_stream(slot));
-    return out;
+    auto s = cur_stream(slot);
+    const int64_t n = slot.numel();
+    auto f32 = slot.options().dtype(torch::kFloat32);
+    auto hdr = torch::empty({n, 2}, f32);
+    auto vflag = torch::empty({std::max<int64_t>(n, 1)}, slot.options());
+    auto vpos = torch::zeros({n + 1}, slot.options().dtype(torch::kInt64));
+    const int64_t mcap = vstride_ > 0 ? n : 0;
+    auto vc = torch::empty({mcap, (int64_t)std::max(vstride_, 1)}, f32);
+    wh::difacto_pull_hdr(table(), ptr<int32_t>(slot), n, l1_shrk ? 1 : 0, ptr<float>(hdr),
+                         ptr<int32_t>(vflag), s);
+    if (vstride_ > 0 && n > 0) {
+      auto stmp = torch::empty({wh::scan_tmp_elems(n)}, vpos.options());
+      wh::scan_i32(ptr<int32_t>(vflag), ptr<int64_t>(vpos), n, ptr<int64_t>(stmp), s);
+      wh::difacto_pull_rows(table(), ptr<int32_t>(slot), n, ptr<int32_t>(vflag),
+                            ptr<int64_t>(vpos), ptr<float>(hdr), ptr<float>(vc), s);
+    }
+    return {hdr, vc, vpos};
   }
 
-  void difacto_push(const Tensor& slot, const Tensor& grad, const std::vector<double>& h,
-                    int64_t threshold, bool l1_shrk, int64_t seed) {
+  // hdr: this shard's pull header for the same keys (owner vidx numbering)
+  void difacto_push(const Tensor& slot, const Tensor& hdr, const Tensor& gw, const Tensor& gvc,
+                    const std::vector<double>& h, int64_t threshold, bool l1_shrk,
+                    int64_t seed) {
     CHECK_IN(slot, torch::kInt32);
-    CHECK_IN(grad, torch::kFloat32);
-    TORCH_CHECK(grad.numel() >= slot.numel() * (vstride_ + 4), "grad rows too short");
+    CHECK_IN(hdr, torch::kFloat32);
+    CHECK_IN(gw, torch::kFloat32);
+    CHECK_DEV(gvc); CHECK_CONT(gvc); CHECK_DT(gvc, torch::kFloat32);
+    const int64_t n = slot.numel();
+    TORCH_CHECK(hdr.numel() == 2 * n && gw.numel() == n, "push: hdr/gw size mismatch");
+    TORCH_CHECK(vstride_ == 0 || gvc.dim() == 2 && gvc.size(1) == vstride_,
+                "push: gvc must be [m, vstride]");
     c10::DeviceGuard g(slot.device());
-    wh::difacto_push(table(), ptr<int32_t>(slot), ptr<float>(grad), slot.numel(),
-                     dhp(h, threshold, l1_shrk, seed), cur_stream(slot));
+    wh::difacto_push(table(), ptr<int32_t>(slot), ptr<float>(hdr), ptr<float>(gw),
+                     gvc.numel() ? ptr<float>(gvc) : nullptr, n, dhp(h, threshold, l1_shrk, seed),
+                     cur_stream(slot));
   }
 
   int64_t dim() const { return dim_; }
@@ -252,51 +276,68 @@ class KVStore {
 };
 
 // --------------------------------------------------------------------- FM
+// difacto: w_or_hdr = hdr [U,2], vc = [m, vstride]; linear: w_or_hdr = w [U]
 std::vector<Tensor> fm_forward(const Tensor& offset, const Tensor& lid,
-                               const c10::optional<Tensor>& val, const Tensor& pulled,
-                               int64_t vstride, const Tensor& label, int64_t loss,
-                               const Tensor& met) {
+                               const c10::optional<Tensor>& val, const Tensor& w_or_hdr,
+                               const c10::optional<Tensor>& vc, int64_t vstride,
+                               const Tensor& label, int64_t loss, const Tensor& met) {
   CHECK_IN(offset, torch::kInt64);
   CHECK_IN(lid, torch::kInt32);
-  CHECK_IN(pulled, torch::kFloat32);
+  CHECK_IN(w_or_hdr, torch::kFloat32);
   CHECK_IN(label, torch::kFloat32);
   CHECK_IN(met, torch::kFloat64);
   TORCH_CHECK(vstride >= 0 && vstride <= 256 && vstride % 4 == 0, "bad vstride");
   TORCH_CHECK(met.numel() >= 4, "met needs 4 doubles");
   const int64_t nrows = offset.numel() - 1;
   TORCH_CHECK(label.numel() == nrows, "label size mismatch");
-  const int64_t stride = vstride > 0 ? vstride + 4 : 1;
-  TORCH_CHECK(pulled.numel() % stride == 0, "pulled row stride mismatch");
+  const float* vcp = nullptr;
+  if (vstride > 0) {
+    TORCH_CHECK(w_or_hdr.dim() == 2 && w_or_hdr.size(1) == 2, "hdr must be [U, 2]");
+    TORCH_CHECK(vc.has_value() && vc->defined(), "vc required");
+    CHECK_IN((*vc), torch::kFloat32);
+    TORCH_CHECK(vc->numel() == 0 || (vc->dim() == 2 && vc->size(1) == vstride), "vc must be [m, vstride]");
+    vcp = vc->numel() ? ptr<float>(*vc) : nullptr;
+  }
   const float* vp = optptr<float>(val);
   c10::DeviceGuard g(offset.device());
   auto f32 = offset.options().dtype(torch::kFloat32);
   auto py = torch::empty({nrows}, f32);
   auto dual = torch::empty({nrows}, f32);
   auto xv = torch::empty({vstride > 0 ? nrows * vstride : 0}, f32);
-  wh::fm_forward(nrows, ptr<int64_t>(offset), ptr<int32_t>(lid), vp, ptr<float>(pulled),
+  wh::fm_forward(nrows, ptr<int64_t>(offset), ptr<int32_t>(lid), vp, ptr<float>(w_or_hdr), vcp,
                  (int)vstride, ptr<float>(label), (int)loss, ptr<float>(py), ptr<float>(dual),
                  vstride > 0 ? ptr<float>(xv) : nullptr, ptr<double>(met), cur_stream(offset));
   return {py, dual, xv};
 }
 
-Tensor fm_backward(const Tensor& csc_off, const Tensor& csc_row, const c10::optional<Tensor>& csc_val,
-                   const Tensor& dual, const c10::optional<Tensor>& xv, const Tensor& pulled,
-                   int64_t vstride) {
+// returns (gw [U], gvc [like vc]) (linear: gvc is empty)
+std::vector<Tensor> fm_backward(const Tensor& csc_off, const Tensor& csc_row,
+                                const c10::optional<Tensor>& csc_val, const Tensor& dual,
+                                const c10::optional<Tensor>& xv, const Tensor& w_or_hdr,
+                                const c10::optional<Tensor>& vc, int64_t vstride) {
   CHECK_IN(csc_off, torch::kInt64);
   CHECK_IN(csc_row, torch::kInt32);
   CHECK_IN(dual, torch::kFloat32);
-  CHECK_IN(pulled, torch::kFloat32);
+  CHECK_IN(w_or_hdr, torch::kFloat32);
   TORCH_CHECK(vstride >= 0 && vstride <= 256 && vstride % 4 == 0, "bad vstride");
   c10::DeviceGuard g(csc_off.device());
   auto s = cur_stream(csc_off);
   const int64_t U = csc_off.numel() - 1;
   const int64_t nnz = csc_row.numel();
-  const int64_t stride = vstride > 0 ? vstride + 4 : 1;
-  TORCH_CHECK(pulled.numel() == U * stride, "pulled must be [U, stride]");
+  TORCH_CHECK(w_or_hdr.numel() == U * (vstride > 0 ? 2 : 1), "w/hdr must have U rows");
   auto f32 = csc_off.options().dtype(torch::kFloat32);
   auto i32 = csc_off.options().dtype(torch::kInt32);
   auto i64 = csc_off.options().dtype(torch::kInt64);
-  auto grad = torch::empty({U, stride}, f32);
+  auto gw = torch::empty({U}, f32);
+  Tensor gvc = torch::empty({0}, f32);
+  const float* vcp = nullptr;
+  if (vstride > 0) {
+    TORCH_CHECK(vc.has_value() && vc->defined() && xv.has_value() && xv->defined(), "vc/xv required");
+    CHECK_IN((*vc), torch::kFloat32);
+    CHECK_IN((*xv), torch::kFloat32);
+    gvc = torch::empty({vc->numel() ? vc->size(0) : 0, vstride}, f32);
+    vcp = vc->numel() ? ptr<float>(*vc) : nullptr;
+  }
   const int64_t cap = wh::fm_bwd_chunks_bound(U, nnz);
   auto chunk_key = torch::empty({cap}, i32);
   auto chunk_beg = torch::empty({cap}, i32);
@@ -304,24 +345,46 @@ Tensor fm_backward(const Tensor& csc_off, const Tensor& csc_row, const c10::opti
   auto chunk_off = torch::empty({U + 1}, i64);
   auto stmp = torch::empty({wh::scan_tmp_elems(U)}, i64);
   wh::fm_backward(U, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row), optptr<float>(csc_val),
-                  ptr<float>(dual), vstride > 0 ? optptr<float>(xv) : nullptr, ptr<float>(pulled),
-                  (int)vstride, ptr<float>(grad), ptr<int32_t>(chunk_key), ptr<int32_t>(chunk_beg),
-                  ptr<int64_t>(chunk_cnt), ptr<int64_t>(chunk_off), ptr<int64_t>(stmp), cap, s);
-  return grad;
+                  ptr<float>(dual), vstride > 0 ? optptr<float>(xv) : nullptr,
+                  ptr<float>(w_or_hdr), vcp, (int)vstride, ptr<float>(gw),
+                  gvc.numel() ? ptr<float>(gvc) : nullptr, ptr<int32_t>(chunk_key),
+                  ptr<int32_t>(chunk_beg), ptr<int64_t>(chunk_cnt), ptr<int64_t>(chunk_off),
+                  ptr<int64_t>(stmp), cap, s);
+  return {gw, gvc};
 }
 
-void fm_grad_post(const Tensor& grad, int64_t vstride, int64_t dim, double clip, double dropout,
+// gvc [mcap, vstride]; m: device int64 tensor holding the live row count
+void fm_grad_post(const Tensor& gvc, const Tensor& m, int64_t dim, double clip, double dropout,
                   int64_t seed, bool normalize) {
-  CHECK_IN(grad, torch::kFloat32);
-  if (vstride == 0) return;
-  c10::DeviceGuard g(grad.device());
-  auto s = cur_stream(grad);
-  const int64_t U = grad.numel() / (vstride + 4);
+  CHECK_IN(gvc, torch::kFloat32);
+  CHECK_IN(m, torch::kInt64);
+  if (gvc.numel() == 0) return;
+  TORCH_CHECK(gvc.dim() == 2, "gvc must be [m, vstride]");
+  const int64_t vstride = gvc.size(1);
+  c10::DeviceGuard g(gvc.device());
+  auto s = cur_stream(gvc);
   Tensor sumsq;
-  if (normalize) sumsq = torch::zeros({1}, grad.options().dtype(torch::kFloat64));
-  wh::fm_grad_post(U, ptr<float>(grad), (int)vstride, (int)dim, (float)clip, (float)dropout,
-                   (uint64_t)seed, normalize ? ptr<double>(sumsq) : nullptr, s);
-  if (normalize) wh::fm_grad_scale(U, ptr<float>(grad), (int)vstride, ptr<double>(sumsq), s);
+  if (normalize) sumsq = torch::zeros({1}, gvc.options().dtype(torch::kFloat64));
+  wh::fm_grad_post(ptr<int64_t>(m), gvc.size(0), ptr<float>(gvc), (int)vstride, (int)dim,
+                   (float)clip, (float)dropout, (uint64_t)seed,
+                   normalize ? ptr<double>(sumsq) : nullptr, s);
+  if (normalize)
+    wh::fm_grad_scale(ptr<int64_t>(m), gvc.size(0), ptr<float>(gvc), (int)vstride, (int)dim,
+                      ptr<double>(sumsq), s);
+}
+
+// worker side of a multi-shard pull: renumber hdr vidx into local compact
+// order; returns m as a device int64 [1] tensor
+Tensor vidx_renumber(const Tensor& hdr) {
+  CHECK_IN(hdr, torch::kFloat32);
+  c10::DeviceGuard g(hdr.device());
+  const int64_t n = hdr.numel() / 2;
+  auto flag = torch::empty({std::max<int64_t>(n, 1)}, hdr.options().dtype(torch::kInt32));
+  auto pos = torch::zeros({n + 1}, hdr.options().dtype(torch::kInt64));
+  auto stmp = torch::empty({wh::scan_tmp_elems(n)}, pos.options());
+  wh::vidx_renumber(ptr<float>(hdr), n, ptr<int32_t>(flag), ptr<int64_t>(pos), ptr<int64_t>(stmp),
+                    cur_stream(hdr));
+  return pos.narrow(0, n, 1);
 }
 
 // -------------------------------------------------------------- metrics
@@ -530,6 +593,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fm_forward", &fm_forward);
   m.def("fm_backward", &fm_backward);
   m.def("fm_grad_post", &fm_grad_post);
+  m.def("vidx_renumber", &vidx_renumber);
   m.def("auc", &auc);
   m.def("synth_criteo", &synth_criteo);
   m.def("gather_rows", &gather_rows);

@@ -14,6 +14,13 @@
 // localize) so gradients are segmented sums, not scattered atomics. Only
 // keys whose occurrence list is longer than one chunk (hot features) use
 // float atomics, one per chunk.
+//
+// Variable-length model layout (the ZVPull/ZVPush value layout of
+// learn/difacto/async_sgd.h:234-244, made dense): a pulled minibatch model is
+//   hdr[U]  float2 {w, vidx}   vidx = bit-cast int32 row in vc, or -1
+//   vc[m]   vstride floats     embedding rows of the keys that have one
+// and the gradient mirrors it: gw[U] + gvc[m] (same vidx numbering). Only the
+// m keys with an embedding move 256 bytes; the rest move 8 (pull) / 4 (push).
 #include "wh_common.h"
 #include "wh_kernels.h"
 
@@ -54,7 +61,8 @@ template <int G>
 __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_t* __restrict__ off,
                                                      const int32_t* __restrict__ lid,
                                                      const float* __restrict__ val,
-                                                     const float* __restrict__ pulled, int vstride,
+                                                     const float2* __restrict__ hdr,
+                                                     const float* __restrict__ vc, int vstride,
                                                      const float* __restrict__ label, int loss,
                                                      float* __restrict__ py_out,
                                                      float* __restrict__ dual_out,
@@ -66,7 +74,6 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
   __shared__ double sh[kThreads / 64];
   const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane - gl;
   const int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
-  const int stride = vstride + 4;
   const uint64_t gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << gbase);
   double m_objv = 0, m_objw = 0, m_corr = 0, m_n = 0;
   const bool live = row < nrows;
@@ -80,16 +87,17 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
   for (int64_t base = b; base < e; base += G) {
     const int64_t j = base + gl;
     const bool valid = j < e;
-    int k = 0;
+    int vid = -1;
     float x = 0.f;
     float2 h = make_float2(0.f, 0.f);
     if (valid) {
-      k = lid[j];
+      const int k = lid[j];
       x = val ? val[j] : 1.f;
-      h = *reinterpret_cast<const float2*>(pulled + (int64_t)k * stride);
+      h = hdr[k];
+      vid = __float_as_int(h.y);
     }
     wl += x * h.x;
-    uint64_t mg = __ballot(valid && h.y != 0.f) & gmask;
+    uint64_t mg = __ballot(valid && vid >= 0) & gmask;
     while (mg) {
       int t[4];
       float keep[4];
@@ -108,9 +116,9 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
       float xs[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int ku = __shfl(k, t[u], 64);
+        const int vu = __shfl(vid, t[u], 64);
         xs[u] = __shfl(x, t[u], 64) * keep[u];
-        v[u] = reinterpret_cast<const float4*>(pulled + (int64_t)ku * stride + 4)[gl];
+        v[u] = reinterpret_cast<const float4*>(vc + (int64_t)vu * vstride)[gl];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -190,27 +198,27 @@ __global__ void k_chunk_count(int64_t nuniq, const int64_t* csc_off, int64_t* ch
   }
 }
 
-// writes the chunk table; zeroes the gradient rows of multi-chunk keys
+// writes the chunk table; zeroes the gradients of multi-chunk keys (they
+// are accumulated with atomics)
 __global__ void k_chunk_fill(int64_t nuniq, const int64_t* csc_off, const int64_t* chunk_off,
-                             const float* pulled, int vstride, int32_t* chunk_key,
-                             int32_t* chunk_beg, float* grad) {
+                             const float2* hdr, int vstride, int32_t* chunk_key,
+                             int32_t* chunk_beg, float* gw, float* gvc) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nuniq) return;
   const int64_t c0 = chunk_off[k], nc = chunk_off[k + 1] - c0;
+  const int32_t b0 = (int32_t)csc_off[k];
   for (int64_t c = 0; c < nc; ++c) {
     chunk_key[c0 + c] = (int32_t)k;
-    chunk_beg[c0 + c] = (int32_t)(csc_off[k] + c * kChunk);
+    chunk_beg[c0 + c] = b0 + (int32_t)(c * kChunk);
   }
   if (nc > 1) {
-    const int stride = vstride > 0 ? vstride + 4 : 1;
-    float* g = grad + k * stride;
+    gw[k] = 0.f;
     if (vstride > 0) {
-      const float flag = pulled[k * stride + 1];
-      g[0] = 0.f; g[1] = flag; g[2] = 0.f; g[3] = 0.f;
-      if (flag != 0.f)
-        for (int d = 0; d < vstride; ++d) g[4 + d] = 0.f;
-    } else {
-      g[0] = 0.f;
+      const int vid = __float_as_int(hdr[k].y);
+      if (vid >= 0) {
+        float4* g = reinterpret_cast<float4*>(gvc + (int64_t)vid * vstride);
+        for (int d = 0; d < vstride / 4; ++d) g[d] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   }
 }
@@ -223,8 +231,10 @@ __global__ __launch_bounds__(kThreads) void k_fm_bwd(const int64_t* __restrict__
                                                      const float* __restrict__ csc_val,
                                                      const float* __restrict__ dual,
                                                      const float* __restrict__ xv,
-                                                     const float* __restrict__ pulled, int vstride,
-                                                     float* __restrict__ grad) {
+                                                     const float2* __restrict__ hdr,
+                                                     const float* __restrict__ vc, int vstride,
+                                                     float* __restrict__ gw_out,
+                                                     float* __restrict__ gvc) {
   // ONE LANE PER CHUNK computes the scalar sums (gw, xxp) of its <= kChunk
   // occurrences; the wave then runs the embedding-gradient jobs of the
   // chunks whose key has V, G lanes per job (float4 slice of each xv row).
@@ -232,9 +242,8 @@ __global__ __launch_bounds__(kThreads) void k_fm_bwd(const int64_t* __restrict__
   const int64_t nch = *nchunk_p;
   const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const bool live = c < nch;
-  const int stride = vstride + 4;
-  int k = 0, b = 0, e = 0;
-  bool multi = false, flag = false;
+  int k = 0, b = 0, e = 0, vid = -1;
+  bool multi = false;
   float gw = 0.f, xxp = 0.f;
   if (live) {
     k = chunk_key[c];
@@ -264,15 +273,13 @@ __global__ __launch_bounds__(kThreads) void k_fm_bwd(const int64_t* __restrict__
       gw += d;
       xxp += d * x;
     }
-    const float* hdr = pulled + (int64_t)k * stride;
-    flag = hdr[1] != 0.f;
-    float* g = grad + (int64_t)k * stride;
-    if (!multi) *reinterpret_cast<float4*>(g) = make_float4(gw, flag ? 1.f : 0.f, 0.f, 0.f);
-    else atomicAdd(g, gw);
+    vid = __float_as_int(hdr[k].y);
+    if (!multi) gw_out[k] = gw;
+    else atomicAdd(gw_out + k, gw);
   }
-  for_each_row_job<G>(live && flag, [&](int src, int gl) {
+  for_each_row_job<G>(live && vid >= 0, [&](int src, int gl) {
     const int sl = src >= 0 ? src : lane;
-    const int jk = __shfl(k, sl, 64), jb = __shfl(b, sl, 64), je = __shfl(e, sl, 64);
+    const int jv = __shfl(vid, sl, 64), jb = __shfl(b, sl, 64), je = __shfl(e, sl, 64);
     const float jx = __shfl(xxp, sl, 64);
     const int jm = __shfl((int)multi, sl, 64);
     if (src < 0) return;
@@ -299,9 +306,9 @@ __global__ __launch_bounds__(kThreads) void k_fm_bwd(const int64_t* __restrict__
       const float4 a = reinterpret_cast<const float4*>(xv + (int64_t)i * vstride)[gl];
       acc.x += d * a.x; acc.y += d * a.y; acc.z += d * a.z; acc.w += d * a.w;
     }
-    const float4 v = reinterpret_cast<const float4*>(pulled + (int64_t)jk * stride + 4)[gl];
+    const float4 v = reinterpret_cast<const float4*>(vc + (int64_t)jv * vstride)[gl];
     acc.x -= jx * v.x; acc.y -= jx * v.y; acc.z -= jx * v.z; acc.w -= jx * v.w;
-    float* gv = grad + (int64_t)jk * stride + 4 + gl * 4;
+    float* gv = gvc + (int64_t)jv * vstride + gl * 4;
     if (!jm) {
       *reinterpret_cast<float4*>(gv) = acc;
     } else {
@@ -330,41 +337,38 @@ __global__ __launch_bounds__(kThreads) void k_lin_bwd(const int64_t* __restrict_
   else grad[k] = gw;
 }
 
-__global__ __launch_bounds__(kThreads) void k_grad_post(int64_t nuniq, float* grad, int vstride,
-                                                        int dim, float clip, float dropout,
-                                                        uint64_t seed, double* sumsq) {
+// gradient clipping / dropout / normalisation on the m embedding-gradient
+// rows (reference learn/difacto/loss.h:131-155); m is a device count
+__global__ __launch_bounds__(kThreads) void k_grad_post(const int64_t* __restrict__ m_p,
+                                                        float* gvc, int vstride, int dim,
+                                                        float clip, float dropout, uint64_t seed,
+                                                        double* sumsq) {
   __shared__ double sh[kThreads / 64];
-  const int stride = vstride + 4;
   const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int64_t k = t / vstride;
+  const int64_t r = t / vstride;
   const int d = (int)(t % vstride);
+  const int64_t m = *m_p;
   double ss = 0;
-  if (k < nuniq && d < dim) {
-    float* g = grad + k * stride;
-    if (g[1] != 0.f) {
-      float v = g[4 + d];
-      if (clip > 0.f) v = fminf(fmaxf(v, -clip), clip);
-      if (dropout > 0.f && uhash01(seed, (uint64_t)k, (uint64_t)d) > 1.f - dropout) v = 0.f;
-      g[4 + d] = v;
-      ss = (double)v * v;
-    }
+  if (r < m && d < dim) {
+    float v = gvc[t];
+    if (clip > 0.f) v = fminf(fmaxf(v, -clip), clip);
+    if (dropout > 0.f && uhash01(seed, (uint64_t)r, (uint64_t)d) > 1.f - dropout) v = 0.f;
+    gvc[t] = v;
+    ss = (double)v * v;
   }
   if (sumsq) {
-    const double r = block_sum_d(ss, sh);
-    if (threadIdx.x == 0) atomicAdd(sumsq, r);
+    const double s = block_sum_d(ss, sh);
+    if (threadIdx.x == 0) atomicAdd(sumsq, s);
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_grad_scale(int64_t nuniq, float* grad, int vstride,
+__global__ __launch_bounds__(kThreads) void k_grad_scale(const int64_t* __restrict__ m_p,
+                                                         float* gvc, int vstride, int dim,
                                                          const double* sumsq) {
-  const int stride = vstride + 4;
   const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int64_t k = t / vstride;
-  const int d = (int)(t % vstride);
   const double n2 = *sumsq;
-  if (n2 < 1e-10 || k >= nuniq) return;
-  float* g = grad + k * stride;
-  if (g[1] != 0.f) g[4 + d] = (float)(g[4 + d] / sqrt(n2));
+  if (n2 < 1e-10 || t / vstride >= *m_p || (int)(t % vstride) >= dim) return;
+  gvc[t] = (float)(gvc[t] / sqrt(n2));
 }
 
 }  // namespace
@@ -381,61 +385,63 @@ __global__ __launch_bounds__(kThreads) void k_grad_scale(int64_t nuniq, float* g
   }
 
 void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
-                const float* pulled, int vstride, const float* label, int loss, float* py,
-                float* dual, float* xv, double* met, hipStream_t s) {
+                const float* w_or_hdr, const float* vc, int vstride, const float* label, int loss,
+                float* py, float* dual, float* xv, double* met, hipStream_t s) {
   if (nrows <= 0) return;
   if (vstride == 0) {
     constexpr int G = 8;
     hipLaunchKernelGGL(k_lin_fwd<G>, dim3(grid_for(nrows * G, kThreads)), dim3(kThreads), 0, s,
-                       nrows, offset, lid, val, pulled, label, loss, py, dual, met);
+                       nrows, offset, lid, val, w_or_hdr, label, loss, py, dual, met);
     return;
   }
   const int G = vstride / 4;  // vstride <= 256 enforced by the binding
+  const float2* hdr = reinterpret_cast<const float2*>(w_or_hdr);
   const dim3 grid(grid_for(nrows * G, kThreads)), block(kThreads);
-  WH_DISPATCH_G(G, k_fm_fwd, grid, block, 0, s, nrows, offset, lid, val, pulled, vstride, label,
+  WH_DISPATCH_G(G, k_fm_fwd, grid, block, 0, s, nrows, offset, lid, val, hdr, vc, vstride, label,
                 loss, py, dual, xv, met);
 }
 
 int64_t fm_bwd_chunks_bound(int64_t nuniq, int64_t nnz) { return nuniq + nnz / kChunk + 1; }
 
 void fm_backward(int64_t nuniq, const int64_t* csc_off, const int32_t* csc_row,
-                 const float* csc_val, const float* dual, const float* xv, const float* pulled,
-                 int vstride, float* grad, int32_t* chunk_key, int32_t* chunk_beg,
-                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, int64_t chunk_cap,
-                 hipStream_t s) {
+                 const float* csc_val, const float* dual, const float* xv, const float* hdr_f,
+                 const float* vc, int vstride, float* gw, float* gvc, int32_t* chunk_key,
+                 int32_t* chunk_beg, int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp,
+                 int64_t chunk_cap, hipStream_t s) {
   if (nuniq <= 0) return;
+  const float2* hdr = reinterpret_cast<const float2*>(hdr_f);
   hipLaunchKernelGGL(k_chunk_count, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
                      csc_off, chunk_cnt);
   scan_i64(chunk_cnt, chunk_off, nuniq, scan_tmp, s);
   hipLaunchKernelGGL(k_chunk_fill, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
-                     csc_off, chunk_off, pulled, vstride, chunk_key, chunk_beg, grad);
+                     csc_off, chunk_off, hdr, vstride, chunk_key, chunk_beg, gw, gvc);
   // the chunk count is data dependent (device value chunk_off[nuniq]); launch
   // over the host-side bound and let surplus work items exit, so the whole
   // step stays free of host synchronisation.
   const int64_t* nchunk_p = chunk_off + nuniq;
   if (vstride == 0) {
     hipLaunchKernelGGL(k_lin_bwd, dim3(grid_for(chunk_cap, kThreads)), dim3(kThreads), 0, s,
-                       nchunk_p, chunk_key, chunk_beg, csc_off, csc_row, csc_val, dual, grad);
+                       nchunk_p, chunk_key, chunk_beg, csc_off, csc_row, csc_val, dual, gw);
     return;
   }
   const int G = vstride / 4;
   const dim3 grid(grid_for(chunk_cap, kThreads)), block(kThreads);  // lane per chunk
   WH_DISPATCH_G(G, k_fm_bwd, grid, block, 0, s, nchunk_p, chunk_key, chunk_beg, csc_off,
-                csc_row, csc_val, dual, xv, pulled, vstride, grad);
+                csc_row, csc_val, dual, xv, hdr, vc, vstride, gw, gvc);
 }
 
-void fm_grad_post(int64_t nuniq, float* grad, int vstride, int dim, float clip, float dropout,
-                  uint64_t seed, double* sumsq, hipStream_t s) {
-  if (nuniq <= 0 || vstride == 0) return;
-  hipLaunchKernelGGL(k_grad_post, dim3(grid_for(nuniq * vstride, kThreads)), dim3(kThreads), 0,
-                     s, nuniq, grad, vstride, dim, clip, dropout, seed, sumsq);
+void fm_grad_post(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim, float clip,
+                  float dropout, uint64_t seed, double* sumsq, hipStream_t s) {
+  if (m_cap <= 0 || vstride == 0) return;
+  hipLaunchKernelGGL(k_grad_post, dim3(grid_for(m_cap * vstride, kThreads)), dim3(kThreads), 0,
+                     s, m, gvc, vstride, dim, clip, dropout, seed, sumsq);
 }
 
-void fm_grad_scale(int64_t nuniq, float* grad, int vstride, const double* sumsq,
-                   hipStream_t s) {
-  if (nuniq <= 0 || vstride == 0) return;
-  hipLaunchKernelGGL(k_grad_scale, dim3(grid_for(nuniq * vstride, kThreads)), dim3(kThreads), 0,
-                     s, nuniq, grad, vstride, sumsq);
+void fm_grad_scale(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim,
+                   const double* sumsq, hipStream_t s) {
+  if (m_cap <= 0 || vstride == 0) return;
+  hipLaunchKernelGGL(k_grad_scale, dim3(grid_for(m_cap * vstride, kThreads)), dim3(kThreads), 0,
+                     s, m, gvc, vstride, dim, sumsq);
 }
 
 }  // namespace wh

@@ -198,56 +198,80 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const 
   if (lane == 0 && newv) atomicAdd((unsigned long long*)(t.stats + 1), (unsigned long long)newv);
 }
 
+__global__ __launch_bounds__(kThreads) void k_difacto_pull_hdr(KVTable t, const int32_t* slot,
+                                                               int64_t n, int l1_shrk,
+                                                               float2* hdr, int32_t* vflag) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const int32_t s = slot[i];
+  float w = 0.f;
+  int32_t row = -1;
+  if (s >= 0) {
+    w = t.w[s];
+    row = t.vstride > 0 ? t.vrow[s] : -1;
+    if (l1_shrk && w == 0.f) row = -1;
+  }
+  hdr[i] = make_float2(w, __int_as_float(-1));
+  vflag[i] = row >= 0 ? 1 : 0;
+}
+
+// copy the V rows of flagged keys into their compact position
 template <int G>
-__global__ __launch_bounds__(kThreads) void k_difacto_pull(KVTable t, const int32_t* slot,
-                                                           int64_t n, int l1_shrk, float* out) {
+__global__ __launch_bounds__(kThreads) void k_difacto_pull_rows(KVTable t, const int32_t* slot,
+                                                                int64_t n,
+                                                                const int32_t* __restrict__ vflag,
+                                                                const int64_t* __restrict__ vpos,
+                                                                float2* hdr, float* vc) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int stride = t.vstride + 4;
-  int32_t row = -1;
-  if (i < n) {
-    const int32_t s = slot[i];
-    float w = 0.f;
-    if (s >= 0) {
-      w = t.w[s];
-      row = t.vstride > 0 ? t.vrow[s] : -1;
-      if (l1_shrk && w == 0.f) row = -1;
-    }
-    *reinterpret_cast<float4*>(out + i * stride) = make_float4(w, row >= 0 ? 1.f : 0.f, 0.f, 0.f);
+  int32_t row = -1, vp = -1;
+  if (i < n && vflag[i]) {
+    row = t.vrow[slot[i]];
+    vp = (int32_t)vpos[i];
+    hdr[i].y = __int_as_float(vp);
   }
-  if (t.vstride == 0) return;
   for_each_row_job<G>(row >= 0, [&](int src, int gl) {
     const int sl = src >= 0 ? src : lane;
-    const int32_t jr = __shfl(row, sl, 64);
-    const int64_t ji = (int64_t)blockIdx.x * kThreads + (threadIdx.x & ~63) + sl;
+    const int32_t jr = __shfl(row, sl, 64), jp = __shfl(vp, sl, 64);
     if (src >= 0) {
       const float* V = t.V + (int64_t)jr * t.vstride;
-      float* o = out + ji * stride + 4;
+      float* o = vc + (int64_t)jp * t.vstride;
       for (int c = gl * 4; c < t.vstride; c += 4 * G)
         *reinterpret_cast<float4*>(o + c) = *reinterpret_cast<const float4*>(V + c);
     }
   });
 }
 
+__global__ __launch_bounds__(kThreads) void k_vidx_flag(const float2* hdr, int64_t n,
+                                                        int32_t* flag) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < n) flag[i] = __float_as_int(hdr[i].y) >= 0 ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kThreads) void k_vidx_set(float2* hdr, int64_t n,
+                                                       const int32_t* flag, const int64_t* pos) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < n && flag[i]) hdr[i].y = __int_as_float((int32_t)pos[i]);
+}
+
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int32_t* slot,
-                                                           const float* grad, int64_t n,
-                                                           DifactoHP hp) {
+                                                           const float2* __restrict__ hdr,
+                                                           const float* __restrict__ gw,
+                                                           const float* __restrict__ gvc,
+                                                           int64_t n, DifactoHP hp) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int stride = t.vstride + 4;
   float oldw = 0.f, neww = 0.f;
   bool want = false;
-  int32_t s = -1, row = -1;
-  float gflag = 0.f;
+  int32_t s = -1, row = -1, gvid = -1;
   if (i < n) {
     s = slot[i];
     if (s >= 0) {
-      const float2 gr = *reinterpret_cast<const float2*>(grad + i * stride);
-      gflag = gr.y;
+      if (t.vstride > 0) gvid = __float_as_int(hdr[i].y);
       // FTRL on w (reference UpdateW, learn/difacto/async_sgd.h:262-286)
       const float w = t.w[s];
-      const float g = gr.x + hp.l2 * w;
+      const float g = gw[i] + hp.l2 * w;
       const float cg = t.sq[s];
       const float cg_new = sqrtf(cg * cg + g * g);
       t.sq[s] = cg_new;
@@ -278,15 +302,14 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int3
     t.vrow[s] = nrow;
     row = nrow;
     kind = 1;
-  } else if (gflag != 0.f && row >= 0) {
+  } else if (gvid >= 0 && row >= 0) {
     kind = 2;
   }
   long long newv = kind == 1 ? t.dim : 0;
   for_each_row_job<G>(kind != 0, [&](int src, int gl) {
     const int sl = src >= 0 ? src : lane;
     const int32_t js = __shfl(s, sl, 64), jr = __shfl(row, sl, 64);
-    const int jk = __shfl(kind, sl, 64);
-    const int64_t ji = (int64_t)blockIdx.x * kThreads + (threadIdx.x & ~63) + sl;
+    const int jk = __shfl(kind, sl, 64), jv = __shfl(gvid, sl, 64);
     if (src < 0) return;
     if (jk == 1) {
       init_v_row(t, js, jr, gl, G, hp);
@@ -295,7 +318,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int3
     // AdaGrad on V (reference UpdateV, learn/difacto/async_sgd.h:289-296)
     float* V = t.V + (int64_t)jr * t.vstride;
     float* VG = t.VG + (int64_t)jr * t.vstride;
-    const float* gv = grad + ji * stride + 4;
+    const float* gv = gvc + (int64_t)jv * t.vstride;
     for (int c = gl * 4; c < t.vstride; c += 4 * G) {
       float4 v = *reinterpret_cast<float4*>(V + c);
       float4 cg = *reinterpret_cast<float4*>(VG + c);
@@ -386,20 +409,40 @@ void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt, i
   WH_DISPATCH_G(G, k_difacto_push_cnt, grid, block, 0, s, t, slot, cnt, n, hp);
 }
 
-void difacto_pull(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk, float* out,
-                  hipStream_t s) {
+void difacto_pull_hdr(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk, float* hdr,
+                      int32_t* vflag, hipStream_t s) {
   if (n <= 0) return;
-  const int G = lanes_per_key(t.vstride);
-  const dim3 grid(grid_for(n, kThreads)), block(kThreads);  // lane per key
-  WH_DISPATCH_G(G, k_difacto_pull, grid, block, 0, s, t, slot, n, l1_shrk, out);
+  hipLaunchKernelGGL(k_difacto_pull_hdr, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t,
+                     slot, n, l1_shrk, reinterpret_cast<float2*>(hdr), vflag);
 }
 
-void difacto_push(const KVTable& t, const int32_t* slot, const float* grad, int64_t n,
-                  DifactoHP hp, hipStream_t s) {
+void difacto_pull_rows(const KVTable& t, const int32_t* slot, int64_t n, const int32_t* vflag,
+                       const int64_t* vpos, float* hdr, float* vc, hipStream_t s) {
+  if (n <= 0 || t.vstride == 0) return;
+  const int G = lanes_per_key(t.vstride);
+  const dim3 grid(grid_for(n, kThreads)), block(kThreads);  // lane per key
+  WH_DISPATCH_G(G, k_difacto_pull_rows, grid, block, 0, s, t, slot, n, vflag, vpos,
+                reinterpret_cast<float2*>(hdr), vc);
+}
+
+void difacto_push(const KVTable& t, const int32_t* slot, const float* hdr, const float* gw,
+                  const float* gvc, int64_t n, DifactoHP hp, hipStream_t s) {
   if (n <= 0) return;
   const int G = lanes_per_key(t.vstride);
   const dim3 grid(grid_for(n, kThreads)), block(kThreads);  // lane per key
-  WH_DISPATCH_G(G, k_difacto_push, grid, block, 0, s, t, slot, grad, n, hp);
+  WH_DISPATCH_G(G, k_difacto_push, grid, block, 0, s, t, slot,
+                reinterpret_cast<const float2*>(hdr), gw, gvc, n, hp);
+}
+
+void vidx_renumber(float* hdr, int64_t n, int32_t* flag_tmp, int64_t* pos_tmp, int64_t* scan_tmp,
+                   hipStream_t s) {
+  if (n <= 0) return;
+  float2* h = reinterpret_cast<float2*>(hdr);
+  hipLaunchKernelGGL(k_vidx_flag, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, h, n,
+                     flag_tmp);
+  scan_i32(flag_tmp, pos_tmp, n, scan_tmp, s);
+  hipLaunchKernelGGL(k_vidx_set, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, h, n,
+                     flag_tmp, pos_tmp);
 }
 
 void gather_rows(const float* in, const int32_t* idx, int64_t n, int width, float* out,

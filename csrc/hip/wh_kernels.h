@@ -88,36 +88,50 @@ struct DifactoHP {
 // add feature counts (reference AdaGradHandle::Push with kPushFeaCnt)
 void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt, int64_t n,
                       DifactoHP hp, hipStream_t s);
-// pull rows [w, flag, 0, 0, V(vstride)] with row stride vstride+4
-void difacto_pull(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk, float* out,
-                  hipStream_t s);
-// push gradient rows in the same layout (flag!=0 => V gradient present)
-void difacto_push(const KVTable& t, const int32_t* slot, const float* grad, int64_t n,
-                  DifactoHP hp, hipStream_t s);
+// Variable-length pull (reference ZVPull, learn/difacto/async_sgd.h:234-244):
+//   pass 1 (difacto_pull_hdr): hdr[i] = {w, -}, vflag[i] = key has a V row
+//          (and, with l1_shrk, w != 0)
+//   caller: vpos = exclusive scan of vflag (scan_i32), m = vpos[n]
+//   pass 2 (difacto_pull_rows): hdr[i].y = bit-cast vpos[i] (or -1) and
+//          vc[vpos[i]] = V row
+void difacto_pull_hdr(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk, float* hdr,
+                      int32_t* vflag, hipStream_t s);
+void difacto_pull_rows(const KVTable& t, const int32_t* slot, int64_t n, const int32_t* vflag,
+                       const int64_t* vpos, float* hdr, float* vc, hipStream_t s);
+// push: gw[i] for every key (FTRL on w), gvc[vidx_i] for keys whose pull
+// header (owner numbering) carried a V row (AdaGrad on V)
+void difacto_push(const KVTable& t, const int32_t* slot, const float* hdr, const float* gw,
+                  const float* gvc, int64_t n, DifactoHP hp, hipStream_t s);
+// worker side of a multi-shard pull: renumber hdr[i].y into the local
+// compact order (exclusive scan of hdr[i].y >= 0); tmp = n int32 +
+// scan_tmp_elems(n) int64; count[0] = m
+void vidx_renumber(float* hdr, int64_t n, int32_t* flag_tmp, int64_t* pos_tmp, int64_t* scan_tmp,
+                   hipStream_t s);
 
 // ---------------------------------------------------------------- fm.hip
 // Forward of FM / linear model on a localized minibatch.
-//   pulled rows: stride = vstride + 4 (difacto) or 1 (linear, vstride == 0)
+//   difacto: w_or_hdr = hdr[U] float2 {w, vidx}, vc = [m, vstride]
+//   linear (vstride == 0): w_or_hdr = w[U], vc unused
 //   loss: 1 square, 2 logit, 4 squared hinge
 //   met[0..3] += {objv, objv_w, correct(threshold 0), n}  (double)
 void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
-                const float* pulled, int vstride, const float* label, int loss, float* py,
-                float* dual, float* xv, double* met, hipStream_t s);
-// Backward: gradient rows (same stride as pulled) for every local key.
+                const float* w_or_hdr, const float* vc, int vstride, const float* label, int loss,
+                float* py, float* dual, float* xv, double* met, hipStream_t s);
+// Backward: gw[U] for every key, gvc[m] for the keys with an embedding row
 //   gw_k = sum_i dual_i x_ik
-//   gV_k = sum_i dual_i x_ik xv_i - (sum_i dual_i x_ik^2) V_k     (keys with flag)
-// work: chunk scratch, see fm_bwd_work_elems
+//   gV_k = sum_i dual_i x_ik xv_i - (sum_i dual_i x_ik^2) V_k
 int64_t fm_bwd_chunks_bound(int64_t nuniq, int64_t nnz);
 void fm_backward(int64_t nuniq, const int64_t* csc_off, const int32_t* csc_row,
-                 const float* csc_val, const float* dual, const float* xv, const float* pulled,
-                 int vstride, float* grad, int32_t* chunk_key, int32_t* chunk_beg,
-                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, int64_t chunk_cap,
-                 hipStream_t s);
-// post-process V gradients: clip to [-c, c] (c>0), dropout with prob p (p>0)
-void fm_grad_post(int64_t nuniq, float* grad, int vstride, int dim, float clip, float dropout,
-                  uint64_t seed, double* sumsq, hipStream_t s);
-void fm_grad_scale(int64_t nuniq, float* grad, int vstride, const double* sumsq,
-                   hipStream_t s);
+                 const float* csc_val, const float* dual, const float* xv, const float* hdr,
+                 const float* vc, int vstride, float* gw, float* gvc, int32_t* chunk_key,
+                 int32_t* chunk_beg, int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp,
+                 int64_t chunk_cap, hipStream_t s);
+// post-process the m (device count) V-gradient rows: clip to [-c, c] (c>0),
+// dropout with prob p (p>0); sumsq (optional) receives the squared norm
+void fm_grad_post(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim, float clip,
+                  float dropout, uint64_t seed, double* sumsq, hipStream_t s);
+void fm_grad_scale(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim,
+                   const double* sumsq, hipStream_t s);
 
 // --------------------------------------------------------------- spmv.hip
 // y = X x over CSR (col < 0 entries skipped); y = X^T p over the CSC of localize

@@ -77,15 +77,17 @@ def test_localize(hip, nshard, with_val):
 
 
 def _pulled(U, vstride, dim, seed, frac_v=0.6):
+    """A random variable-length pull: hdr {w, vidx} + compact V rows in a
+    shuffled (non-monotone) row order, with spare rows past m."""
     g = torch.Generator().manual_seed(seed)
-    p = torch.zeros(U, vstride + 4)
-    p[:, 0] = torch.randn(U, generator=g) * 0.3
+    w = torch.randn(U, generator=g) * 0.3
     flag = torch.rand(U, generator=g) < frac_v
-    p[:, 1] = flag.float()
-    V = torch.randn(U, vstride, generator=g) * 0.2
-    V[:, dim:] = 0
-    p[:, 4:] = V * flag[:, None]
-    return p
+    m = int(flag.sum())
+    vidx = torch.full((U,), -1, dtype=torch.int64)
+    vidx[flag] = torch.randperm(m, generator=g)
+    vc = torch.randn(m + 7, vstride, generator=g) * 0.2
+    vc[:, dim:] = 0
+    return ref.make_hdr(w, vidx), vc
 
 
 @pytest.mark.parametrize("dim", [5, 16, 64])
@@ -96,25 +98,45 @@ def test_fm_forward_backward(hip, dim, with_val):
     uniq, ucnt, oc, lid, csc_off, csc_row, csc_val = hip.localize(
         keys.to(DEV), off.to(DEV), val.to(DEV) if val is not None else None, 1)
     U = uniq.numel()
-    pulled = _pulled(U, vs, dim, 3)
+    hdr, vc = _pulled(U, vs, dim, 3)
     met = torch.zeros(4, dtype=torch.float64, device=DEV)
     py, dual, xv = hip.fm_forward(off.to(DEV), lid, val.to(DEV) if val is not None else None,
-                                  pulled.to(DEV), vs, label.to(DEV), 2, met)
+                                  hdr.to(DEV), vc.to(DEV), vs, label.to(DEV), 2, met)
     met_r = torch.zeros(4, dtype=torch.float64)
-    py_r, dual_r, xv_r = ref.fm_forward(off, lid.cpu(), val, pulled, vs, label, 2, met_r)
+    py_r, dual_r, xv_r = ref.fm_forward(off, lid.cpu(), val, hdr, vc, vs, label, 2, met_r)
     assert torch.allclose(py.cpu(), py_r, atol=1e-4, rtol=1e-4)
     assert torch.allclose(dual.cpu(), dual_r, atol=1e-5, rtol=1e-4)
     assert torch.allclose(xv.cpu(), xv_r, atol=1e-4, rtol=1e-4)
     assert torch.allclose(met.cpu(), met_r, rtol=1e-5)
-    grad = hip.fm_backward(csc_off, csc_row, csc_val if with_val else None, dual, xv,
-                           pulled.to(DEV), vs)
-    grad_r = ref.fm_backward(csc_off.cpu(), csc_row.cpu(), csc_val.cpu() if with_val else None,
-                             dual.cpu(), xv.cpu(), pulled, vs)
-    gr = grad.cpu()
-    assert torch.allclose(gr[:, 0], grad_r[:, 0], atol=1e-4, rtol=1e-3)
-    assert torch.equal(gr[:, 1], grad_r[:, 1])
-    flag = grad_r[:, 1] != 0
-    assert torch.allclose(gr[flag][:, 4:], grad_r[flag][:, 4:], atol=1e-4, rtol=1e-3)
+    gw, gvc = hip.fm_backward(csc_off, csc_row, csc_val if with_val else None, dual, xv,
+                              hdr.to(DEV), vc.to(DEV), vs)
+    gw_r, gvc_r = ref.fm_backward(csc_off.cpu(), csc_row.cpu(),
+                                  csc_val.cpu() if with_val else None, dual.cpu(), xv.cpu(),
+                                  hdr, vc, vs)
+    assert torch.allclose(gw.cpu(), gw_r, atol=1e-4, rtol=1e-3)
+    live = ref.hdr_vidx(hdr).long()
+    live = live[live >= 0]
+    assert torch.allclose(gvc.cpu()[live], gvc_r[live], atol=1e-4, rtol=1e-3)
+
+
+def test_grad_post_and_renumber(hip):
+    g = torch.Generator().manual_seed(8)
+    gvc = torch.randn(50, 16, generator=g) * 3
+    m = torch.tensor([40], dtype=torch.int64)
+    a = gvc.clone().to(DEV)
+    hip.fm_grad_post(a, m.to(DEV), 12, 1.0, 0.0, 1, True)
+    r = gvc.clone()
+    r[:40, :12].clamp_(-1, 1)
+    r[:40, :12] /= float((r[:40, :12].double() ** 2).sum()) ** 0.5
+    assert torch.allclose(a.cpu()[:40, :12], r[:40, :12], atol=1e-6)
+    assert torch.equal(a.cpu()[40:], gvc[40:]) and torch.equal(a.cpu()[:, 12:], gvc[:, 12:])
+    vidx = torch.tensor([5, -1, 9, 2, -1, -1, 7], dtype=torch.int64)
+    h = ref.make_hdr(torch.arange(7).float(), vidx)
+    hg = h.to(DEV)
+    mg = hip.vidx_renumber(hg)
+    assert int(mg) == 4
+    assert ref.hdr_vidx(hg.cpu()).tolist() == [0, -1, 1, 2, -1, -1, 3]
+    assert torch.equal(hg.cpu()[:, 0], h[:, 0])
 
 
 @pytest.mark.parametrize("loss", [1, 2, 4])
@@ -124,15 +146,16 @@ def test_linear_forward_backward(hip, loss):
         keys.to(DEV), off.to(DEV), val.to(DEV), 1)
     w = torch.randn(uniq.numel()) * 0.1
     met = torch.zeros(4, dtype=torch.float64, device=DEV)
-    py, dual, _ = hip.fm_forward(off.to(DEV), lid, val.to(DEV), w.to(DEV), 0, label.to(DEV),
-                                 loss, met)
+    py, dual, _ = hip.fm_forward(off.to(DEV), lid, val.to(DEV), w.to(DEV), None, 0,
+                                 label.to(DEV), loss, met)
     met_r = torch.zeros(4, dtype=torch.float64)
-    py_r, dual_r, _ = ref.fm_forward(off, lid.cpu(), val, w, 0, label, loss, met_r)
+    py_r, dual_r, _ = ref.fm_forward(off, lid.cpu(), val, w, None, 0, label, loss, met_r)
     assert torch.allclose(py.cpu(), py_r, atol=1e-4, rtol=1e-4)
     assert torch.allclose(dual.cpu(), dual_r, atol=1e-4, rtol=1e-4)
     assert torch.allclose(met.cpu(), met_r, rtol=1e-5)
-    g = hip.fm_backward(csc_off, csc_row, csc_val, dual, None, w.to(DEV), 0)
-    g_r = ref.fm_backward(csc_off.cpu(), csc_row.cpu(), csc_val.cpu(), dual.cpu(), None, w, 0)
+    g, _ = hip.fm_backward(csc_off, csc_row, csc_val, dual, None, w.to(DEV), None, 0)
+    g_r, _ = ref.fm_backward(csc_off.cpu(), csc_row.cpu(), csc_val.cpu(), dual.cpu(), None, w,
+                             None, 0)
     assert torch.allclose(g.cpu(), g_r, atol=1e-3, rtol=1e-3)
 
 
@@ -187,26 +210,31 @@ def test_difacto_store_updates(hip, dim):
         s_c = cs.find(sel, True)
         gs.difacto_push_cnt(s_g, cnt.to(DEV), hp, 3, True, 42)
         cs.difacto_push_cnt(s_c, cnt, hp, 3, True, 42)
-        p_g = gs.difacto_pull(s_g, True).cpu()
-        p_c = cs.difacto_pull(s_c, True)
-        assert torch.allclose(p_g[:, :2], p_c[:, :2], atol=1e-5, rtol=1e-4), it
-        fl = p_c[:, 1] != 0
-        assert torch.allclose(p_g[fl][:, 4:], p_c[fl][:, 4:], atol=1e-5, rtol=1e-4), it
-        grad = torch.randn(sel.numel(), vs + 4, generator=g) * 0.5
-        grad[:, 1] = p_c[:, 1]
-        grad[:, 2:4] = 0
-        gs.difacto_push(s_g, grad.to(DEV), hp, 3, True, 42)
-        cs.difacto_push(s_c, grad, hp, 3, True, 42)
+        hg, vg, _ = gs.difacto_pull(s_g, True)
+        hc, vcc, _ = cs.difacto_pull(s_c, True)
+        _same_pull(hg, vg, hc, vcc)
+        gw = torch.randn(sel.numel(), generator=g) * 0.5
+        m = vcc.shape[0]
+        gvc = torch.randn(m, vs, generator=g) * 0.5
+        # the GPU store numbers its rows by the same exclusive scan
+        gs.difacto_push(s_g, hg, gw.to(DEV), gvc.to(DEV), hp, 3, True, 42)
+        cs.difacto_push(s_c, hc, gw, gvc, hp, 3, True, 42)
     s_g = gs.find(keys.to(DEV), False)
     s_c = cs.find(keys, False)
-    p_g = gs.difacto_pull(s_g, False).cpu()
-    p_c = cs.difacto_pull(s_c, False)
-    assert torch.allclose(p_g[:, :2], p_c[:, :2], atol=1e-5, rtol=1e-4)
-    fl = p_c[:, 1] != 0
-    assert fl.any()
-    assert torch.allclose(p_g[fl][:, 4:], p_c[fl][:, 4:], atol=1e-5, rtol=1e-4)
+    hg, vg, _ = gs.difacto_pull(s_g, False)
+    hc, vcc, _ = cs.difacto_pull(s_c, False)
+    assert vcc.shape[0] > 0
+    _same_pull(hg, vg, hc, vcc)
     assert int(gs.stats[0]) == int(cs.stats[0])
     assert int(gs.stats[1]) == int(cs.stats[1])
+
+
+def _same_pull(hg, vg, hc, vcc):
+    hg = hg.cpu()
+    assert torch.allclose(hg[:, 0], hc[:, 0], atol=1e-5, rtol=1e-4)
+    assert torch.equal(ref.hdr_vidx(hg), ref.hdr_vidx(hc))
+    m = vcc.shape[0]
+    assert torch.allclose(vg.cpu()[:m], vcc, atol=1e-5, rtol=1e-4)
 
 
 def test_synth_criteo(hip):

@@ -1,0 +1,76 @@
+"""Sharded KV over a 2-rank gloo group (the ps-lite server group re-expressed
+as all-to-all-v): variable-length DiFacto pull/push exchange on CPU."""
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    from wormhole_amd import ops
+    from wormhole_amd.config.schema import DifactoConfig, Embedding
+    from wormhole_amd.data.synthetic import criteo_batch_cpu
+    from wormhole_amd.models.difacto import DifactoLearner
+    from wormhole_amd.parallel.comm import Comm
+    comm = Comm(torch.device("cpu"))
+    emb = Embedding(dim=8, threshold=3)
+    conf = DifactoConfig(embedding=[emb], lambda_l1=0.01, l1_shrk=False)
+    card = [50, 400, 3000, 20, 7]
+    lr = DifactoLearner(conf, comm, "cpu", cap=1 << 14, vcap=1 << 12, seed=5)
+    for step in range(4):
+        keys, label, off = criteo_batch_cpu(300, 17 + rank, step, card)
+        lr.process(keys, off, None, label, 0, 0)
+    # pull check: every worker sees exactly the owner's stored values
+    keys, label, off = criteo_batch_cpu(300, 99 + rank, 0, card)
+    uniq, ucnt, owner_cnt, lid, *_ = ops.localize(keys, off, None, comm.size)
+    sess = lr.kv.open(uniq, owner_cnt, insert=False)
+    hdr, vc = lr.kv.difacto_pull(sess, False)
+    st = lr.store
+    occ = st.occupied()
+    mine = {}
+    sk = st._keys if hasattr(st, "_keys") else None
+    for s in occ.tolist():
+        row = int(st._vrow[s])
+        mine[int(sk[s])] = (float(st._w[s]), None if row < 0 else st._V[row][:8].tolist())
+    allmaps = comm.allgather_object(mine)
+    owner = {}
+    for mp_ in allmaps:
+        owner.update(mp_)
+    vid = ops.hdr_vidx(hdr).tolist()
+    m = int(sess.m[0])
+    assert sorted(v for v in vid if v >= 0) == list(range(m))
+    nv = 0
+    for i, k in enumerate(uniq.tolist()):
+        w_o, v_o = owner.get(k, (0.0, None))
+        assert abs(float(hdr[i, 0]) - w_o) < 1e-7, (k, float(hdr[i, 0]), w_o)
+        if v_o is None:
+            assert vid[i] == -1
+        else:
+            nv += 1
+            assert vid[i] >= 0 and torch.allclose(vc[vid[i], :8], torch.tensor(v_o)), k
+    assert nv > 0
+    prog = lr.take_progress()
+    comm.barrier()
+    comm.finalize()
+    with open(os.path.join(out_dir, "r%d" % rank), "w") as f:
+        f.write("%r %d\n" % (prog[0] / prog[5], nv))
+
+
+def test_difacto_sharded_pull_push_two_ranks(tmp_path):
+    port = _free_port()
+    mp.spawn(_rank_main, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        ll, nv = open(tmp_path / ("r%d" % r)).read().split()
+        assert 0 < float(ll) < 1.0 and int(nv) > 0

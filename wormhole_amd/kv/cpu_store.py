@@ -242,31 +242,45 @@ class CpuKVStore:
                 self._alloc_v(s, seed, h[7])
 
     def difacto_pull(self, slot, l1_shrk):
+        """Variable-length pull: (hdr [n, 2] {w, vidx bits}, vc [m, vstride],
+        vpos int64 [n+1]) -- the layout of the HIP store (vc is exact here)."""
         s_all = slot.cpu().numpy()
-        st = self.vstride + 4
-        out = np.zeros((s_all.shape[0], st), dtype=np.float32)
+        n = s_all.shape[0]
+        w = np.zeros(n, dtype=np.float32)
+        vid = np.full(n, -1, dtype=np.int32)
+        rows = []
         for i, s in enumerate(s_all.tolist()):
             if s < 0:
                 continue
-            w = self._w[s]
-            row = self._vrow[s]
-            if l1_shrk and w == 0:
+            w[i] = self._w[s]
+            row = self._vrow[s] if self.vstride > 0 else -1
+            if l1_shrk and w[i] == 0:
                 row = -1
-            out[i, 0] = w
             if row >= 0:
-                out[i, 1] = 1.0
-                out[i, 4:] = self._V[row]
-        return torch.from_numpy(out)
+                vid[i] = len(rows)
+                rows.append(row)
+        hdr = np.zeros((n, 2), dtype=np.float32)
+        hdr[:, 0] = w
+        hdr.view(np.int32)[:, 1] = vid
+        vc = (self._V[np.array(rows, dtype=np.int64)] if rows
+              else np.zeros((0, max(self.vstride, 1)), dtype=np.float32))
+        flag = (vid >= 0).astype(np.int64)
+        vpos = np.zeros(n + 1, dtype=np.int64)
+        vpos[1:] = np.cumsum(flag)
+        return torch.from_numpy(hdr), torch.from_numpy(vc.copy()), torch.from_numpy(vpos)
 
-    def difacto_push(self, slot, grad, h, threshold, l1_shrk, seed):
+    def difacto_push(self, slot, hdr, gw, gvc, h, threshold, l1_shrk, seed):
+        """gw [n] for every key; gvc[vidx_i] for keys whose pull header
+        (this shard's numbering) had an embedding row."""
         alpha, beta, l1, l2, v_alpha, v_beta, v_l2, v_init = [np.float32(x) for x in h]
         s_all = slot.cpu().numpy()
-        g_all = grad.cpu().numpy().reshape(s_all.shape[0], -1)
+        gw_all = gw.cpu().numpy().reshape(-1)
+        vid_all = hdr.cpu().contiguous().numpy().view(np.int32).reshape(-1, 2)[:, 1]
+        gv_all = gvc.cpu().numpy().reshape(-1, max(self.vstride, 1)) if gvc.numel() else None
         for i, s in enumerate(s_all.tolist()):
             if s < 0:
                 continue
-            gr = g_all[i]
-            g = np.float32(gr[0])
+            g = np.float32(gw_all[i])
             w = self._w[s]
             g = np.float32(g + l2 * w)
             cg = self._sq[s]
@@ -286,11 +300,11 @@ class CpuKVStore:
                     self._alloc_v(s, seed, v_init)
             elif w != 0 and nw == 0:
                 self._stats[0] -= 1
-            if self.vstride > 0 and gr[1] != 0:
+            if self.vstride > 0 and vid_all[i] >= 0:
                 row = self._vrow[s]
                 if row >= 0:
                     v = self._V[row]
                     cgv = self._VG[row]
-                    gv = gr[4:].astype(np.float32) + v_l2 * v
+                    gv = gv_all[vid_all[i]].astype(np.float32) + v_l2 * v
                     cgv[:] = np.sqrt(cgv * cgv + gv * gv)
                     v -= v_alpha / (cgv + v_beta) * gv

@@ -58,18 +58,20 @@ class DifactoLearner:
         if train and data_pass == 0 and self.dim > 0:
             self.kv.difacto_push_cnt(sess, ucnt.float(), self.hp, self.threshold,
                                      self.l1_shrk, self.seed)
-        pulled = self.kv.difacto_pull(sess, self.l1_shrk)
-        py, dual, xv = ops.fm_forward(offset, lid, val, pulled, self.vstride, label,
+        hdr, vc = self.kv.difacto_pull(sess, self.l1_shrk)
+        if self.vstride == 0:  # no embedding: a plain linear model over w
+            hdr, vc = hdr[:, 0].contiguous(), None
+        py, dual, xv = ops.fm_forward(offset, lid, val, hdr, vc, self.vstride, label,
                                       ops.LOSS_LOGIT, self.met)
         self.auc_sum += ops.auc(py, label)
         self.n_mb += 1
         if train:
-            grad = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, pulled, self.vstride)
-            if self.emb is not None:
-                ops.fm_grad_post(grad, self.vstride, self.dim, self.emb.grad_clipping,
+            gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, hdr, vc, self.vstride)
+            if self.emb is not None and self.vstride > 0:
+                ops.fm_grad_post(gvc, sess.m, self.dim, self.emb.grad_clipping,
                                  self.emb.dropout, self.seed + 7919 * self.step + 1,
                                  bool(self.emb.grad_normalization))
-            self.kv.difacto_push(sess, grad, self.hp, self.threshold, self.l1_shrk,
+            self.kv.difacto_push(sess, gw, gvc, self.hp, self.threshold, self.l1_shrk,
                                  self.seed)
         self.step += 1
         return py if wtype == PRED else None

@@ -221,24 +221,27 @@ class FMObjective(LinearObjective):
         return self.loaded.clone()
 
     def _pulled(self, w):
+        """The FM weights in the variable-length pull layout of the fused FM
+        kernels: hdr {w, vidx} per local feature, vc = its V rows (vidx = i)."""
         F, k = self.param.num_feature, self.nfactor
         vs = ops.vstride_for(k)
         valid, idx = self._feat()
         U = idx.numel()
-        p = torch.zeros(U, vs + 4, dtype=torch.float32, device=w.device)
-        p[:, 0] = torch.where(valid, w[idx], torch.zeros((), device=w.device))
-        p[:, 1] = valid.float()
+        zero = torch.zeros((), device=w.device)
+        vidx = torch.where(valid, torch.arange(U, device=w.device), torch.full_like(idx, -1))
+        hdr = ops.make_hdr(torch.where(valid, w[idx], zero), vidx)
         V = w[F:F + F * k].view(F, k)
-        p[:, 4:4 + k] = torch.where(valid[:, None], V[idx], torch.zeros((), device=w.device))
-        return p, vs
+        vc = torch.zeros(U, vs, dtype=torch.float32, device=w.device)
+        vc[:, :k] = torch.where(valid[:, None], V[idx], zero)
+        return hdr, vc, vs
 
     def _forward(self, w):
-        p, vs = self._pulled(w)
+        hdr, vc, vs = self._pulled(w)
         met = torch.zeros(4, dtype=torch.float64, device=w.device)
-        py, _dual, xv = ops.fm_forward(self.d.offset, self.d.lid, self.d.val, p, vs,
+        py, _dual, xv = ops.fm_forward(self.d.offset, self.d.lid, self.d.val, hdr, vc, vs,
                                        self.d.label, 1, met)
         F, k = self.param.num_feature, self.nfactor
-        return py + (self.param.base_score + w[F * (k + 1)]), p, vs, xv
+        return py + (self.param.base_score + w[F * (k + 1)]), (hdr, vc), vs, xv
 
     def margin(self, w):
         return self._forward(w)[0]
@@ -258,15 +261,15 @@ class FMObjective(LinearObjective):
 
     def calc_grad(self, w):
         F, k = self.param.num_feature, self.nfactor
-        margin, p, vs, xv = self._forward(w)
+        margin, (hdr, vc), vs, xv = self._forward(w)
         g = (margin_to_pred(self.param.loss_type, margin) - self.d.label).contiguous()
-        grad_rows = ops.fm_backward(self.d.csc_off, self.d.csc_row, self.d.csc_val, g, xv, p, vs)
-        grad_rows = grad_rows.view(-1, vs + 4)
+        gw, gvc = ops.fm_backward(self.d.csc_off, self.d.csc_row, self.d.csc_val, g, xv, hdr, vc,
+                                  vs)
         valid, idx = self._feat()
         grad = torch.zeros_like(w)
-        grad.index_add_(0, idx[valid], grad_rows[valid, 0])
+        grad.index_add_(0, idx[valid], gw[valid])
         gV = grad[F:F + F * k].view(F, k)
-        gV.index_add_(0, idx[valid], grad_rows[valid, 4:4 + k])
+        gV.index_add_(0, idx[valid], gvc[valid][:, :k])
         grad[F * (k + 1)] = g.sum()
         if self.bsp.rank == 0:
             if self.reg_L2 != 0.0:

@@ -34,11 +34,11 @@ class LinearLearner:
             keys, offset, val, self.kv.nshard)
         sess = self.kv.open(uniq, owner_cnt, insert=train)
         w = self.kv.linear_pull(sess)
-        py, dual, _ = ops.fm_forward(offset, lid, val, w, 0, label, self.conf.loss, self.met)
+        py, dual, _ = ops.fm_forward(offset, lid, val, w, None, 0, label, self.conf.loss, self.met)
         self.auc_sum += ops.auc(py, label)
         self.n_mb += 1
         if train:
-            grad = ops.fm_backward(csc_off, csc_row, csc_val, dual, None, w, 0)
+            grad, _ = ops.fm_backward(csc_off, csc_row, csc_val, dual, None, w, None, 0)
             self.kv.linear_push(sess, grad, self.conf.algo, self.alpha, self.beta,
                                 self.conf.lambda_l1, self.conf.lambda_l2)
         return py if wtype == PRED else None

@@ -13,6 +13,10 @@ def _gpu(t):
     return t.is_cuda
 
 
+make_hdr = ref.make_hdr
+hdr_vidx = ref.hdr_vidx
+
+
 def vstride_for(dim):
     return ref.vstride_for(dim)
 
@@ -25,38 +29,54 @@ def localize(keys, offset, val=None, nshard=1):
     return _native.host().localize_cpu(keys, offset, val, nshard)
 
 
-def fm_forward(offset, lid, val, pulled, vstride, label, loss, met):
-    if _gpu(pulled):
-        return _native.hip().fm_forward(offset, lid, val, pulled, vstride, label, loss, met)
-    return ref.fm_forward(offset, lid, val, pulled, vstride, label, loss, met)
+def fm_forward(offset, lid, val, w_or_hdr, vc, vstride, label, loss, met):
+    """difacto: w_or_hdr = pull header [U, 2] {w, vidx}, vc = [m, vstride]
+    embedding rows; linear (vstride == 0): w_or_hdr = w [U], vc = None."""
+    if _gpu(w_or_hdr):
+        return _native.hip().fm_forward(offset, lid, val, w_or_hdr, vc, vstride, label, loss, met)
+    return ref.fm_forward(offset, lid, val, w_or_hdr, vc, vstride, label, loss, met)
 
 
-def fm_backward(csc_off, csc_row, csc_val, dual, xv, pulled, vstride):
+def fm_backward(csc_off, csc_row, csc_val, dual, xv, w_or_hdr, vc, vstride):
+    """Returns (gw [U], gvc [like vc])."""
     if _gpu(dual):
-        return _native.hip().fm_backward(csc_off, csc_row, csc_val, dual, xv, pulled, vstride)
-    return ref.fm_backward(csc_off, csc_row, csc_val, dual, xv, pulled, vstride)
+        return _native.hip().fm_backward(csc_off, csc_row, csc_val, dual, xv, w_or_hdr, vc,
+                                         vstride)
+    return ref.fm_backward(csc_off, csc_row, csc_val, dual, xv, w_or_hdr, vc, vstride)
 
 
-def fm_grad_post(grad, vstride, dim, clip, dropout, seed, normalize):
-    if vstride == 0 or (clip <= 0 and dropout <= 0 and not normalize):
+def fm_grad_post(gvc, m, dim, clip, dropout, seed, normalize):
+    """Clip / dropout / normalise the first m (device int64 [1]) rows of the
+    embedding gradient gvc [mcap, vstride] (learn/difacto/loss.h:131-155)."""
+    if gvc.numel() == 0 or (clip <= 0 and dropout <= 0 and not normalize):
         return
-    if _gpu(grad):
-        return _native.hip().fm_grad_post(grad, vstride, dim, clip, dropout, seed, normalize)
+    if _gpu(gvc):
+        return _native.hip().fm_grad_post(gvc, m, dim, clip, dropout, seed, normalize)
     import torch
-    g = grad.view(-1, vstride + 4)
-    flag = g[:, 1] != 0
-    gv = g[:, 4:4 + dim]
+    gv = gvc[:int(m.reshape(-1)[0]), :dim]
     if clip > 0:
         gv.clamp_(-clip, clip)
     if dropout > 0:
         gen = torch.Generator().manual_seed(int(seed) & 0x7fffffff)
         drop = torch.rand(gv.shape, generator=gen) > 1 - dropout
         gv[drop] = 0
-    gv[~flag] = 0
     if normalize:
         n2 = float((gv.double() ** 2).sum())
         if n2 >= 1e-10:
             gv /= n2 ** 0.5
+
+
+def vidx_renumber(hdr):
+    """Renumber a received pull header's vidx column into local compact order
+    (exclusive scan of vidx >= 0); returns m as an int64 [1] tensor."""
+    if _gpu(hdr):
+        return _native.hip().vidx_renumber(hdr)
+    import torch
+    v = ref.hdr_vidx(hdr)
+    has = v >= 0
+    pos = torch.cumsum(has.to(torch.int64), 0) - has.to(torch.int64)
+    hdr.view(torch.int32).view(-1, 2)[:, 1] = torch.where(has, pos, -1).to(torch.int32)
+    return has.sum().reshape(1).to(torch.int64)
 
 
 def spmv(offset, col, val, x):

@@ -81,23 +81,41 @@ def _loss(loss, label, py):
     return torch.nn.functional.softplus(-y * py), -y / (1 + torch.exp(y * py))
 
 
-def fm_forward(offset, lid, val, pulled, vstride, label, loss, met):
-    """Returns (py, dual, xv); accumulates {objv, objv_w, correct, n} into met."""
+def hdr_vidx(hdr):
+    """int32 view of the vidx column of a [U, 2] float32 pull header."""
+    return hdr.contiguous().view(torch.int32).view(-1, 2)[:, 1]
+
+
+def make_hdr(w, vidx):
+    """[U, 2] float32 pull header {w, bit-cast int32 vidx}."""
+    h = torch.empty(w.numel(), 2, dtype=torch.float32, device=w.device)
+    h[:, 0] = w
+    h.view(torch.int32)[:, 1] = vidx.to(torch.int32)
+    return h
+
+
+def fm_forward(offset, lid, val, w_or_hdr, vc, vstride, label, loss, met):
+    """Returns (py, dual, xv); accumulates {objv, objv_w, correct, n} into met.
+
+    difacto: w_or_hdr = hdr [U, 2] {w, vidx}, vc = [m, vstride] embedding rows
+    (vidx = -1: no embedding); linear (vstride == 0): w_or_hdr = w [U]."""
     nrows = offset.numel() - 1
-    dev = pulled.device
+    dev = w_or_hdr.device
     rows = torch.repeat_interleave(torch.arange(nrows, device=dev), offset[1:] - offset[:-1])
     lid = lid.long()
     x = val if (val is not None and val.numel()) else torch.ones(lid.numel(), device=dev)
     if vstride == 0:
-        w = pulled.reshape(-1)
+        w = w_or_hdr.reshape(-1)
         py = torch.zeros(nrows, device=dev).index_add_(0, rows, x * w[lid])
         wsum = py
         xv = torch.empty(0, device=dev)
     else:
-        p = pulled.reshape(-1, vstride + 4)
-        w = p[:, 0]
-        flag = (p[:, 1] != 0).to(p.dtype)
-        V = p[:, 4:] * flag[:, None]
+        w = w_or_hdr[:, 0]
+        vid = hdr_vidx(w_or_hdr).long()
+        has = vid >= 0
+        V = torch.zeros(w.numel(), vstride, device=dev)
+        if bool(has.any()):
+            V[has] = vc.reshape(-1, vstride)[vid[has]]
         wsum = torch.zeros(nrows, device=dev).index_add_(0, rows, x * w[lid])
         xv = torch.zeros(nrows, vstride, device=dev).index_add_(0, rows, x[:, None] * V[lid])
         xxvv = torch.zeros(nrows, vstride, device=dev).index_add_(
@@ -113,7 +131,8 @@ def fm_forward(offset, lid, val, pulled, vstride, label, loss, met):
     return py, dual, xv.reshape(-1)
 
 
-def fm_backward(csc_off, csc_row, csc_val, dual, xv, pulled, vstride):
+def fm_backward(csc_off, csc_row, csc_val, dual, xv, w_or_hdr, vc, vstride):
+    """Returns (gw [U], gvc [like vc]); gvc rows follow the header vidx."""
     U = csc_off.numel() - 1
     dev = dual.device
     cnt = csc_off[1:] - csc_off[:-1]
@@ -123,19 +142,18 @@ def fm_backward(csc_off, csc_row, csc_val, dual, xv, pulled, vstride):
     dx = dual[rows] * x
     gw = torch.zeros(U, device=dev).index_add_(0, key, dx)
     if vstride == 0:
-        return gw.reshape(U, 1)
-    p = pulled.reshape(U, vstride + 4)
-    flag = (p[:, 1] != 0)
-    V = p[:, 4:]
+        return gw, torch.empty(0, device=dev)
+    vid = hdr_vidx(w_or_hdr).long()
+    has = vid >= 0
+    vcr = vc.reshape(-1, vstride)
+    gvc = torch.zeros(vcr.shape[0], vstride, device=dev)
+    if not bool(has.any()):
+        return gw, gvc
     xvr = xv.reshape(-1, vstride)
     acc = torch.zeros(U, vstride, device=dev).index_add_(0, key, dx[:, None] * xvr[rows])
     xxp = torch.zeros(U, device=dev).index_add_(0, key, dx * x)
-    gV = acc - xxp[:, None] * V
-    grad = torch.zeros(U, vstride + 4, device=dev)
-    grad[:, 0] = gw
-    grad[:, 1] = flag.to(grad.dtype)
-    grad[:, 4:] = torch.where(flag[:, None], gV, torch.zeros_like(gV))
-    return grad
+    gvc[vid[has]] = acc[has] - xxp[has, None] * vcr[vid[has]]
+    return gw, gvc
 
 
 def auc(py, label):
