@@ -55,34 +55,53 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--cap", type=int, default=1 << 27, help="KV slots per GPU shard")
     ap.add_argument("--vcap", type=int, default=1 << 24, help="embedding rows per shard")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: gloo rehearsal of the distributed path (tiny batches only)")
     args = ap.parse_args()
 
     local = env_local_rank()
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    if args.device == "cuda":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+        args.cap, args.vcap = min(args.cap, 1 << 16), min(args.vcap, 1 << 14)
     comm = Comm(device)
     n = comm.size
     learner = build(args, comm, device)
-    card = torch.tensor(CRITEO_TB_CARD, dtype=torch.int64, device=device)
-    from wormhole_amd import _native
-    hip = _native.hip()
     seed = 1000 + comm.rank
+    if device.type == "cuda":
+        from wormhole_amd import _native
+        hip = _native.hip()
+        card = torch.tensor(CRITEO_TB_CARD, dtype=torch.int64, device=device)
+
+        def batch(step):
+            return hip.synth_criteo(args.batch, seed, step, card)
+    else:
+        from wormhole_amd.data.synthetic import criteo_batch_cpu
+
+        def batch(step):
+            return criteo_batch_cpu(args.batch, seed, step, CRITEO_TB_CARD)
 
     def one(step):
-        keys, label, offset = hip.synth_criteo(args.batch, seed, step, card)
+        keys, label, offset = batch(step)
         learner.process(keys, offset, None, label, 0, 0)
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
 
     for s in range(args.warmup):
         one(s)
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for s in range(args.steps):
         one(args.warmup + s)
-    torch.cuda.synchronize()
+    sync()
     comm.barrier()
-    torch.cuda.synchronize()
+    sync()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     comm.allreduce(t, "max")

@@ -1,0 +1,37 @@
+"""bench.py driver contract, rehearsed on CPU over gloo (the driver runs the
+same command line with RCCL on N GPUs): one JSON line from rank 0 with the
+BASELINE.json metric, whole-job value, N, steps, warmup."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_two_ranks_cpu():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--device", "cpu", "--batch", "500"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["global_batch"] == 1000
+    assert d["value"] > 0 and d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert abs(d["value"] - 1000 * 2 / (d["ms_per_step"] * 2 / 1000)) < 1e-6 * d["value"]

@@ -33,7 +33,7 @@ def make_store(cap, vcap, dim, device):
 class Session:
     """Per-minibatch exchange state (keys sent once, splits reused)."""
 
-    __slots__ = ("send", "recv", "keys", "slots", "hdr_own", "vsend", "vrecv", "m")
+    __slots__ = ("send", "recv", "keys", "slots", "hdr_own", "vsend", "vrecv", "m", "cnt")
 
     def __init__(self, send, recv, keys):
         self.send = send
@@ -44,6 +44,7 @@ class Session:
         self.vsend = None    # embedding rows this rank sent per peer in the pull
         self.vrecv = None    # ... and received per peer
         self.m = None        # device int64 [1]: embedding rows in the local model
+        self.cnt = None      # owner-side feature counts (DiFacto pass 0)
 
     def segments(self):
         b = 0
@@ -60,14 +61,24 @@ class ShardedKV:
         self.nshard = comm.size if nshard is None else max(1, min(int(nshard), comm.size))
         self.push_count = 0  # number of push requests applied (SGD's t)
 
-    def open(self, uniq, owner_cnt, insert):
+    def open(self, uniq, owner_cnt, insert, cnt=None):
+        """Send this minibatch's unique keys to their owners (plus, for the
+        DiFacto count push, their counts in the same exchange) and resolve
+        them to owner-side slots."""
         send = [int(x) for x in (owner_cnt.tolist() if hasattr(owner_cnt, "tolist") else owner_cnt)]
         send += [0] * (self.comm.size - len(send))
         if self.comm.size == 1:
             sess = Session(send, send, uniq)
+            sess.cnt = cnt
         else:
             recv = self.comm.exchange_counts(send)
-            sess = Session(send, recv, self.comm.all_to_all_v(uniq, send, recv))
+            if cnt is None:
+                keys = self.comm.all_to_all_v(uniq, send, recv)
+                sess = Session(send, recv, keys)
+            else:
+                keys, c = self.comm.all_to_all_v_multi([(uniq, send, recv), (cnt, send, recv)])
+                sess = Session(send, recv, keys)
+                sess.cnt = c
         sess.slots = self.store.find(sess.keys, insert)
         return sess
 
@@ -90,8 +101,10 @@ class ShardedKV:
                 self.store.linear_push(sess.slots[a:b], g[a:b], algo, alpha, beta, l1, l2, eta)
 
     # --------------------------------------------------------------- difacto
-    def difacto_push_cnt(self, sess, cnt, hp, threshold, l1_shrk, seed):
-        c = self._to_owner(sess, cnt)
+    def difacto_push_cnt(self, sess, hp, threshold, l1_shrk, seed):
+        """Feature-count push (kPushFeaCnt); the counts travelled with the
+        keys in :meth:`open`."""
+        c = sess.cnt.float() if sess.cnt.dtype != torch.float32 else sess.cnt
         for a, b in sess.segments():
             if b > a:
                 self.store.difacto_push_cnt(sess.slots[a:b], c[a:b], hp, threshold, l1_shrk, seed)
@@ -104,15 +117,20 @@ class ShardedKV:
         if self.comm.size == 1:
             sess.m = vpos[-1:]
             return hdr, vc
-        # per-peer embedding rows: vpos at the receive-segment boundaries
+        # embedding rows per peer = vpos at the receive-segment boundaries;
+        # exchanged on the device, then ONE host read for both directions
         bounds = [0]
         for n in sess.recv:
             bounds.append(bounds[-1] + n)
-        vb = vpos[torch.tensor(bounds, dtype=torch.int64, device=vpos.device)].tolist()
-        sess.vrecv = [vb[i + 1] - vb[i] for i in range(len(sess.recv))]  # owner -> worker
-        sess.vsend = self.comm.exchange_counts(sess.vrecv)
-        hdr_w = self.comm.all_to_all_v(hdr, sess.recv, sess.send)
-        vc_w = self.comm.all_to_all_v(vc[:vb[-1]], sess.vrecv, sess.vsend)
+        vb = vpos[torch.tensor(bounds, dtype=torch.int64, device=vpos.device)]
+        vrecv_d = (vb[1:] - vb[:-1]).contiguous()       # owner -> worker rows
+        vsend_d = self.comm.exchange_counts_dev(vrecv_d)  # worker <- owner rows
+        both = torch.cat([vrecv_d, vsend_d]).tolist()
+        P = self.comm.size
+        sess.vrecv, sess.vsend = both[:P], both[P:]
+        hdr_w, vc_w = self.comm.all_to_all_v_multi([
+            (hdr, sess.recv, sess.send),
+            (vc[:sum(sess.vrecv)], sess.vrecv, sess.vsend)])
         sess.m = ops.vidx_renumber(hdr_w)
         return hdr_w, vc_w
 
@@ -120,9 +138,9 @@ class ShardedKV:
         if self.comm.size == 1:
             g, gv = gw, gvc
         else:
-            g = self.comm.all_to_all_v(gw.contiguous(), sess.send, sess.recv)
-            gv = self.comm.all_to_all_v(gvc[:sum(sess.vsend)].contiguous(), sess.vsend,
-                                        sess.vrecv)
+            g, gv = self.comm.all_to_all_v_multi([
+                (gw, sess.send, sess.recv),
+                (gvc[:sum(sess.vsend)], sess.vsend, sess.vrecv)])
         for a, b in sess.segments():
             if b > a:
                 self.store.difacto_push(sess.slots[a:b], sess.hdr_own[a:b], g[a:b], gv, hp,

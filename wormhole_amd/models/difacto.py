@@ -54,10 +54,10 @@ class DifactoLearner:
         train = wtype == TRAIN
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = ops.localize(
             keys, offset, val, self.kv.nshard)
-        sess = self.kv.open(uniq, owner_cnt, insert=train)
-        if train and data_pass == 0 and self.dim > 0:
-            self.kv.difacto_push_cnt(sess, ucnt.float(), self.hp, self.threshold,
-                                     self.l1_shrk, self.seed)
+        push_cnt = train and data_pass == 0 and self.dim > 0
+        sess = self.kv.open(uniq, owner_cnt, insert=train, cnt=ucnt if push_cnt else None)
+        if push_cnt:
+            self.kv.difacto_push_cnt(sess, self.hp, self.threshold, self.l1_shrk, self.seed)
         hdr, vc = self.kv.difacto_pull(sess, self.l1_shrk)
         if self.vstride == 0:  # no embedding: a plain linear model over w
             hdr, vc = hdr[:, 0].contiguous(), None

@@ -116,6 +116,45 @@ class Comm:
                                    [s * width for s in send_rows])
         return out
 
+    def all_to_all_v_multi(self, items):
+        """Several row-wise all-to-all-v exchanges fused into ONE group of
+        point-to-point transfers (one RCCL group launch; on xGMI every peer
+        pair has its own link, so the transfers of all tensors to all peers
+        run concurrently).  items: [(x, send_rows, recv_rows), ...]."""
+        if self.size == 1:
+            return [x for x, _, _ in items]
+        outs, ops = [], []
+        for x, send, recv in items:
+            x = x.contiguous()
+            out = torch.empty((sum(recv),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+            so = ro = 0
+            for p in range(self.size):
+                sn, rn = send[p], recv[p]
+                if p == self.rank:
+                    if sn:
+                        out[ro:ro + rn].copy_(x[so:so + sn])
+                else:
+                    if sn:
+                        ops.append(dist.P2POp(dist.isend, x[so:so + sn], p))
+                    if rn:
+                        ops.append(dist.P2POp(dist.irecv, out[ro:ro + rn], p))
+                so += sn
+                ro += rn
+            outs.append(out)
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return outs
+
+    def exchange_counts_dev(self, send_dev):
+        """Device-side count exchange: send_dev int64 [size] -> recv int64
+        [size] on the device (no host synchronisation)."""
+        if self.size == 1:
+            return send_dev.clone()
+        r = torch.empty_like(send_dev)
+        dist.all_to_all_single(r, send_dev.contiguous())
+        return r
+
     def finalize(self):
         if self.size > 1 and dist.is_initialized():
             dist.destroy_process_group()
