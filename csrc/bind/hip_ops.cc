@@ -61,7 +61,7 @@ Tensor scan_excl(const Tensor& in) {
 // Returns (uniq i64[U], ucnt i32[U], owner_cnt i64[P], lid i32[nnz],
 //          csc_off i64[U+1], csc_row i32[nnz], csc_val f32[nnz|0])
 std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
-                             const c10::optional<Tensor>& val, int64_t nshard) {
+                             const c10::optional<Tensor>& val, int64_t nshard, int64_t hint) {
   CHECK_IN(keys, torch::kInt64);
   CHECK_IN(offset, torch::kInt64);
   TORCH_CHECK(nshard >= 1 && nshard <= 1024, "nshard out of range");
@@ -74,18 +74,30 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
   if (vp) { CHECK_IN((*val), torch::kFloat32); TORCH_CHECK(val->numel() == nnz); }
   auto i32 = keys.options().dtype(torch::kInt32);
   auto i64 = keys.options().dtype(torch::kInt64);
-  const int64_t tsize = next_pow2(std::max<int64_t>(2 * nnz, 1024));
-  auto tkeys = torch::full({tsize}, -1, i64);
-  auto tcnt = torch::zeros({tsize}, i32);
-  auto slot_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
-  wh::loc_count(reinterpret_cast<const uint64_t*>(keys.data_ptr()), nnz,
-                reinterpret_cast<uint64_t*>(tkeys.data_ptr()), ptr<uint32_t>(tcnt), tsize,
-                ptr<int32_t>(slot_of), s);
-  auto owner_cnt = torch::zeros({nshard}, i64);
-  wh::loc_owner_hist(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
-                     ptr<int64_t>(owner_cnt), s);
-  // the number of unique keys sizes everything downstream: one host sync
-  auto owner_cnt_h = owner_cnt.to(torch::kCPU);
+  // Table size: >= 2*nnz can never overflow; with a hint (the previous
+  // minibatch's unique count) use ~2.5x the hint instead, which keeps the
+  // scratch table small enough to stay cache resident, and fall back to the
+  // safe size if this minibatch overflowed it.
+  const int64_t safe = next_pow2(std::max<int64_t>(2 * nnz, 1024));
+  int64_t tsize = hint > 0 ? std::min(safe, next_pow2(std::max<int64_t>(hint * 5 / 2, 1024)))
+                           : safe;
+  Tensor tkeys, slot_of, owner_cnt, owner_cnt_h;
+  while (true) {
+    tkeys = torch::full({tsize}, -1, i64);
+    slot_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
+    owner_cnt = torch::zeros({nshard + 1}, i64);  // [nshard] = overflow count
+    wh::loc_insert(reinterpret_cast<const uint64_t*>(keys.data_ptr()), nnz,
+                   reinterpret_cast<uint64_t*>(tkeys.data_ptr()), tsize, ptr<int32_t>(slot_of),
+                   ptr<int64_t>(owner_cnt) + nshard, s);
+    wh::loc_owner_hist(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
+                       ptr<int64_t>(owner_cnt), s);
+    // the number of unique keys sizes everything downstream: one host sync
+    owner_cnt_h = owner_cnt.to(torch::kCPU);
+    if (owner_cnt_h.data_ptr<int64_t>()[nshard] == 0 || tsize >= safe) break;
+    tsize = safe;
+  }
+  TORCH_CHECK(owner_cnt_h.data_ptr<int64_t>()[nshard] == 0, "localize: table overflow");
+  owner_cnt_h = owner_cnt_h.narrow(0, 0, nshard).contiguous();
   int64_t U = 0;
   std::vector<int64_t> cursor_h(nshard);
   for (int64_t p = 0; p < nshard; ++p) {
@@ -95,22 +107,25 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
   auto cursor = torch::from_blob(cursor_h.data(), {nshard}, torch::kInt64).to(keys.device());
   auto tlid = torch::empty({tsize}, i32);
   auto uniq = torch::empty({U}, i64);
-  auto ucnt = torch::empty({U}, i32);
-  wh::loc_assign(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), ptr<uint32_t>(tcnt), tsize,
-                 (int)nshard, ptr<int64_t>(cursor), ptr<int32_t>(tlid),
-                 reinterpret_cast<uint64_t*>(uniq.data_ptr()), ptr<int32_t>(ucnt), s);
+  wh::loc_assign(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
+                 ptr<int64_t>(cursor), ptr<int32_t>(tlid),
+                 reinterpret_cast<uint64_t*>(uniq.data_ptr()), s);
   auto row_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
   wh::row_of_nnz(ptr<int64_t>(offset), nrows, ptr<int32_t>(row_of), s);
-  auto csc_off = torch::empty({U + 1}, i64);
-  auto stmp = torch::empty({wh::scan_tmp_elems(U)}, i64);
-  wh::scan_i32(ptr<int32_t>(ucnt), ptr<int64_t>(csc_off), U, ptr<int64_t>(stmp), s);
-  auto csc_cursor = csc_off.clone();
+  const int64_t n1 = std::max<int64_t>(nnz, 1);
   auto lid = torch::empty({nnz}, i32);
+  auto work = torch::empty({3 * n1}, i32);  // pos | sorted lid | sorted pos
+  const size_t sbytes = wh::loc_sort_tmp_bytes(nnz, U);
+  auto stmp = torch::empty({(int64_t)sbytes + 16}, keys.options().dtype(torch::kUInt8));
+  auto csc_off = torch::empty({U + 1}, i64);
+  auto ucnt = torch::empty({U}, i32);
   auto csc_row = torch::empty({nnz}, i32);
   auto csc_val = vp ? torch::empty({nnz}, keys.options().dtype(torch::kFloat32))
                     : torch::empty({0}, keys.options().dtype(torch::kFloat32));
-  wh::loc_csc(ptr<int32_t>(slot_of), ptr<int32_t>(tlid), ptr<int32_t>(row_of), vp, nnz,
-              ptr<int64_t>(csc_cursor), ptr<int32_t>(lid), ptr<int32_t>(csc_row),
+  int32_t* wp = ptr<int32_t>(work);
+  wh::loc_csc(ptr<int32_t>(slot_of), ptr<int32_t>(tlid), ptr<int32_t>(row_of), vp, nnz, U,
+              ptr<int32_t>(lid), wp, wp + n1, wp + 2 * n1, stmp.data_ptr(), sbytes,
+              ptr<int64_t>(csc_off), ptr<int32_t>(ucnt), ptr<int32_t>(csc_row),
               vp ? ptr<float>(csc_val) : nullptr, s);
   return {uniq, ucnt, owner_cnt_h, lid, csc_off, csc_row, csc_val};
 }
@@ -255,7 +270,7 @@ class KVStore {
     CHECK_DEV(gvc); CHECK_CONT(gvc); CHECK_DT(gvc, torch::kFloat32);
     const int64_t n = slot.numel();
     TORCH_CHECK(hdr.numel() == 2 * n && gw.numel() == n, "push: hdr/gw size mismatch");
-    TORCH_CHECK(vstride_ == 0 || gvc.dim() == 2 && gvc.size(1) == vstride_,
+    TORCH_CHECK(vstride_ == 0 || (gvc.dim() == 2 && gvc.size(1) == vstride_),
                 "push: gvc must be [m, vstride]");
     c10::DeviceGuard g(slot.device());
     wh::difacto_push(table(), ptr<int32_t>(slot), ptr<float>(hdr), ptr<float>(gw),
@@ -589,7 +604,7 @@ PYBIND11_MODULE(_hip, m) {
   m.doc() = "wormhole_amd gfx950 HIP kernels";
   m.def("scan_excl", &scan_excl);
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
-        py::arg("nshard") = 1);
+        py::arg("nshard") = 1, py::arg("hint") = 0);
   m.def("fm_forward", &fm_forward);
   m.def("fm_backward", &fm_backward);
   m.def("fm_grad_post", &fm_grad_post);

@@ -199,26 +199,48 @@ __global__ void k_chunk_count(int64_t nuniq, const int64_t* csc_off, int64_t* ch
 }
 
 // writes the chunk table; zeroes the gradients of multi-chunk keys (they
-// are accumulated with atomics)
-__global__ void k_chunk_fill(int64_t nuniq, const int64_t* csc_off, const int64_t* chunk_off,
-                             const float2* hdr, int vstride, int32_t* chunk_key,
-                             int32_t* chunk_beg, float* gw, float* gvc) {
+// are accumulated with atomics). Lane per key for the common single-chunk
+// key; a multi-chunk (hot) key is expanded by the whole wave, 64 chunks per
+// round, so the hottest key does not serialise on one lane.
+__global__ __launch_bounds__(kThreads) void k_chunk_fill(int64_t nuniq,
+                                                         const int64_t* __restrict__ csc_off,
+                                                         const int64_t* __restrict__ chunk_off,
+                                                         const float2* __restrict__ hdr,
+                                                         int vstride, int32_t* chunk_key,
+                                                         int32_t* chunk_beg, float* gw,
+                                                         float* gvc) {
+  const int lane = threadIdx.x & 63;
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nuniq) return;
-  const int64_t c0 = chunk_off[k], nc = chunk_off[k + 1] - c0;
-  const int32_t b0 = (int32_t)csc_off[k];
-  for (int64_t c = 0; c < nc; ++c) {
-    chunk_key[c0 + c] = (int32_t)k;
-    chunk_beg[c0 + c] = b0 + (int32_t)(c * kChunk);
+  int64_t c0 = 0, nc = 0;
+  int32_t b0 = 0;
+  if (k < nuniq) {
+    c0 = chunk_off[k];
+    nc = chunk_off[k + 1] - c0;
+    b0 = (int32_t)csc_off[k];
+    if (nc == 1) {
+      chunk_key[c0] = (int32_t)k;
+      chunk_beg[c0] = b0;
+    }
   }
-  if (nc > 1) {
-    gw[k] = 0.f;
+  uint64_t m = __ballot(nc > 1);
+  while (m) {
+    const int src = __ffsll((unsigned long long)m) - 1;
+    m &= m - 1;
+    const int32_t jk = (int32_t)__shfl((int)k, src, 64);
+    const int64_t jc0 = __shfl(c0, src, 64);
+    const int64_t jnc = __shfl(nc, src, 64);
+    const int32_t jb0 = __shfl(b0, src, 64);
+    for (int64_t c = lane; c < jnc; c += 64) {
+      chunk_key[jc0 + c] = jk;
+      chunk_beg[jc0 + c] = jb0 + (int32_t)(c * kChunk);
+    }
+    if (lane == 0) gw[jk] = 0.f;
     if (vstride > 0) {
-      const int vid = __float_as_int(hdr[k].y);
-      if (vid >= 0) {
-        float4* g = reinterpret_cast<float4*>(gvc + (int64_t)vid * vstride);
-        for (int d = 0; d < vstride / 4; ++d) g[d] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      const int vid = __float_as_int(hdr[jk].y);
+      if (vid >= 0)
+        for (int d = lane * 4; d < vstride; d += 256)
+          *reinterpret_cast<float4*>(gvc + (int64_t)vid * vstride + d) =
+              make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }

@@ -20,25 +20,29 @@ void scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStrea
 // ------------------------------------------------------------ localize.hip
 // Batch-local de-duplication of uint64 feature ids (reference Localizer,
 // learn/base/localizer.h:42-221) via a device open-addressing table of
-// `tsize` (power of two, >= 2*nnz) slots instead of a global sort.
-//   tkeys[tsize] (init ~0), tcnt[tsize] (init 0) are scratch.
-void loc_count(const uint64_t* keys, int64_t nnz, uint64_t* tkeys, uint32_t* tcnt,
-               int64_t tsize, int32_t* slot_of, hipStream_t s);
+// `tsize` (power of two) slots, then a radix sort of (local id, position)
+// pairs on ceil(log2 U) bits for the CSC. The host sizes the table from the
+// previous minibatch's unique count; if it fills up, inserts give up after a
+// full probe cycle and count into overflow[0] so the host retries with
+// tsize >= 2*nnz (which cannot overflow). tkeys[tsize] (init ~0) is scratch.
+void loc_insert(const uint64_t* keys, int64_t nnz, uint64_t* tkeys, int64_t tsize,
+                int32_t* slot_of, int64_t* overflow, hipStream_t s);
 // per-owner histogram of the occupied slots (owner = mix64b(key) % nshard)
 void loc_owner_hist(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* owner_cnt,
                     hipStream_t s);
 // assign local ids grouped by owner; owner_cursor[p] must start at the
-// exclusive scan of owner_cnt. Writes tlid[slot], uniq[lid], ucnt[lid].
-void loc_assign(const uint64_t* tkeys, const uint32_t* tcnt, int64_t tsize, int nshard,
-                int64_t* owner_cursor, int32_t* tlid, uint64_t* uniq, int32_t* ucnt,
-                hipStream_t s);
+// exclusive scan of owner_cnt. Writes tlid[slot], uniq[lid].
+void loc_assign(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* owner_cursor,
+                int32_t* tlid, uint64_t* uniq, hipStream_t s);
 // CSR row id of every non-zero
 void row_of_nnz(const int64_t* offset, int64_t nrows, int32_t* row_of, hipStream_t s);
-// remap nnz -> local id, and fill the CSC (per-unique-key occurrence lists).
-// csc_cursor[lid] must start at the exclusive scan of ucnt.
+// nnz -> local id map and the CSC (per-id occurrence lists, in row order)
+// plus per-id counts. Scratch: pos/slid/spos [nnz] int32, sort_tmp.
+size_t loc_sort_tmp_bytes(int64_t nnz, int64_t nuniq);
 void loc_csc(const int32_t* slot_of, const int32_t* tlid, const int32_t* row_of,
-             const float* val, int64_t nnz, int64_t* csc_cursor, int32_t* lid,
-             int32_t* csc_row, float* csc_val, hipStream_t s);
+             const float* val, int64_t nnz, int64_t nuniq, int32_t* lid, int32_t* pos,
+             int32_t* slid, int32_t* spos, void* sort_tmp, size_t sort_tmp_bytes,
+             int64_t* csc_off, int32_t* ucnt, int32_t* csc_row, float* csc_val, hipStream_t s);
 
 // ---------------------------------------------------------- kvstore.hip
 // Sharded parameter store (replaces the ps-lite server KVStore). Open

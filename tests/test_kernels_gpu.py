@@ -44,11 +44,12 @@ def test_scan(hip):
 
 @pytest.mark.parametrize("nshard", [1, 3, 8])
 @pytest.mark.parametrize("with_val", [False, True])
-def test_localize(hip, nshard, with_val):
+@pytest.mark.parametrize("hint", [0, 1, 2000])  # 1: table overflows -> safe-size retry
+def test_localize(hip, nshard, with_val, hint):
     keys, off, val, _ = _rand_batch(3000, 20, 5000, 1, with_val)
     k, o = keys.to(DEV), off.to(DEV)
     v = val.to(DEV) if val is not None else None
-    uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = hip.localize(k, o, v, nshard)
+    uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = hip.localize(k, o, v, nshard, hint)
     ru = torch.unique(keys)
     assert uniq.numel() == ru.numel()
     assert torch.equal(torch.sort(uniq.cpu()).values, ru)

@@ -46,6 +46,7 @@ class DifactoLearner:
         self.met = torch.zeros(4, dtype=torch.float64, device=self.device)
         self.auc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.n_mb = 0
+        self.uhint = 0  # unique ids of the previous minibatch (localize table size)
         self.step = 0
 
     # ------------------------------------------------------------------ step
@@ -53,7 +54,8 @@ class DifactoLearner:
         """One minibatch. Returns predictions (py) for PRED, else None."""
         train = wtype == TRAIN
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = ops.localize(
-            keys, offset, val, self.kv.nshard)
+            keys, offset, val, self.kv.nshard, self.uhint)
+        self.uhint = uniq.numel()
         push_cnt = train and data_pass == 0 and self.dim > 0
         sess = self.kv.open(uniq, owner_cnt, insert=train, cnt=ucnt if push_cnt else None)
         if push_cnt:

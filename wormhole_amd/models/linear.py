@@ -27,11 +27,13 @@ class LinearLearner:
         self.met = torch.zeros(4, dtype=torch.float64, device=self.device)
         self.auc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.n_mb = 0
+        self.uhint = 0  # unique ids of the previous minibatch (localize table size)
 
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0):
         train = wtype == TRAIN
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = ops.localize(
-            keys, offset, val, self.kv.nshard)
+            keys, offset, val, self.kv.nshard, self.uhint)
+        self.uhint = uniq.numel()
         sess = self.kv.open(uniq, owner_cnt, insert=train)
         w = self.kv.linear_pull(sess)
         py, dual, _ = ops.fm_forward(offset, lid, val, w, None, 0, label, self.conf.loss, self.met)

@@ -21,11 +21,13 @@ def vstride_for(dim):
     return ref.vstride_for(dim)
 
 
-def localize(keys, offset, val=None, nshard=1):
+def localize(keys, offset, val=None, nshard=1, hint=0):
     """Unique feature ids of a minibatch (grouped by owner shard), per-id
-    counts, the nnz->local-id map and the per-id occurrence lists (CSC)."""
+    counts, the nnz->local-id map and the per-id occurrence lists (CSC).
+    hint: expected number of unique ids (e.g. the previous minibatch's); it
+    sizes the GPU scratch table (a wrong hint costs a retry, never a result)."""
     if _gpu(keys):
-        return _native.hip().localize(keys, offset, val, nshard)
+        return _native.hip().localize(keys, offset, val, nshard, int(hint))
     return _native.host().localize_cpu(keys, offset, val, nshard)
 
 
