@@ -319,9 +319,11 @@ std::vector<Tensor> fm_forward(const Tensor& offset, const Tensor& lid,
   auto py = torch::empty({nrows}, f32);
   auto dual = torch::empty({nrows}, f32);
   auto xv = torch::empty({vstride > 0 ? nrows * vstride : 0}, f32);
+  auto part = torch::empty({wh::fm_fwd_partials()}, met.options());
   wh::fm_forward(nrows, ptr<int64_t>(offset), ptr<int32_t>(lid), vp, ptr<float>(w_or_hdr), vcp,
                  (int)vstride, ptr<float>(label), (int)loss, ptr<float>(py), ptr<float>(dual),
-                 vstride > 0 ? ptr<float>(xv) : nullptr, ptr<double>(met), cur_stream(offset));
+                 vstride > 0 ? ptr<float>(xv) : nullptr, ptr<double>(met), ptr<double>(part),
+                 cur_stream(offset));
   return {py, dual, xv};
 }
 
@@ -356,15 +358,15 @@ std::vector<Tensor> fm_backward(const Tensor& csc_off, const Tensor& csc_row,
   const int64_t cap = wh::fm_bwd_chunks_bound(U, nnz);
   auto chunk_key = torch::empty({cap}, i32);
   auto chunk_beg = torch::empty({cap}, i32);
-  auto chunk_cnt = torch::empty({std::max<int64_t>(U, 1)}, i64);
-  auto chunk_off = torch::empty({U + 1}, i64);
+  auto chunk_cnt = torch::empty({std::max<int64_t>(2 * U, 1)}, i64);
+  auto chunk_off = torch::empty({2 * (U + 1)}, i64);
   auto stmp = torch::empty({wh::scan_tmp_elems(U)}, i64);
-  wh::fm_backward(U, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row), optptr<float>(csc_val),
+  wh::fm_backward(U, nnz, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row), optptr<float>(csc_val),
                   ptr<float>(dual), vstride > 0 ? optptr<float>(xv) : nullptr,
                   ptr<float>(w_or_hdr), vcp, (int)vstride, ptr<float>(gw),
                   gvc.numel() ? ptr<float>(gvc) : nullptr, ptr<int32_t>(chunk_key),
                   ptr<int32_t>(chunk_beg), ptr<int64_t>(chunk_cnt), ptr<int64_t>(chunk_off),
-                  ptr<int64_t>(stmp), cap, s);
+                  ptr<int64_t>(stmp), s);
   return {gw, gvc};
 }
 

@@ -24,11 +24,26 @@
 #include "wh_common.h"
 #include "wh_kernels.h"
 
+#include <algorithm>
+
 namespace wh {
 namespace {
 
 constexpr int kThreads = 256;
 constexpr int kChunk = 32;  // occurrences per backward work item
+constexpr int kFwdBlocks = 2048;  // persistent forward grid: 8192 waves = 32 per CU
+
+// The four metric sums leave each block as plain stores into part[block][4]
+// (summed by k_partials_sum): one same-address float64 atomic per block costs
+// ~12 ns at the memory side, which at 25k blocks was a millisecond.
+__device__ __forceinline__ void block_partials(double* part, double* sh, double a, double b,
+                                               double c, double d) {
+  double r;
+  r = block_sum_d(a, sh); if (threadIdx.x == 0) part[blockIdx.x * 4 + 0] = r; __syncthreads();
+  r = block_sum_d(b, sh); if (threadIdx.x == 0) part[blockIdx.x * 4 + 1] = r; __syncthreads();
+  r = block_sum_d(c, sh); if (threadIdx.x == 0) part[blockIdx.x * 4 + 2] = r; __syncthreads();
+  r = block_sum_d(d, sh); if (threadIdx.x == 0) part[blockIdx.x * 4 + 3] = r;
+}
 
 struct LossOut {
   float objv, dual;
@@ -57,6 +72,22 @@ __device__ __forceinline__ LossOut eval_loss(int loss, float label, float py) {
   return o;
 }
 
+// Memory-level parallelism decides both FM kernels: every V / xv row is a
+// dependent gather (index load -> header -> row), and 256-byte rows only
+// reach the L2 / Infinity-Cache gather rates with many independent loads in
+// flight per wave. tools/microbench/fm_gather_bench.hip measured the forward's
+// 1 GB of row gathers per 100k-row minibatch at 189 us with G-lane groups
+// issuing 8 rows at a time vs 65 us with ONE WAVE PER ROW issuing all its rows
+// at once (15 TB/s), so both kernels use the wave-per-item shape:
+//   lanes = SUB sub-groups x G lanes (G = vstride/4, a float4 slice each);
+//   one wave-instruction gathers SUB rows; up to TI instructions in flight.
+template <int G>
+struct Shape {
+  static constexpr int SUB = 64 / G;             // rows per wave-instruction
+  static constexpr int NI = G;                   // instructions per 64 items
+  static constexpr int TI = G < 16 ? G : 16;     // instructions in flight
+};
+
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_t* __restrict__ off,
                                                      const int32_t* __restrict__ lid,
@@ -66,95 +97,85 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
                                                      const float* __restrict__ label, int loss,
                                                      float* __restrict__ py_out,
                                                      float* __restrict__ dual_out,
-                                                     float* __restrict__ xv, double* met) {
-  // G lanes own one row. Per round the group loads G of the row's non-zeros
-  // cooperatively (coalesced local ids, G independent header gathers), then
-  // walks the ones that carry an embedding four at a time, every lane
-  // gathering its float4 slice of each V row (four 16-byte loads in flight).
+                                                     float* __restrict__ xv, double* part) {
+  using S = Shape<G>;
   __shared__ double sh[kThreads / 64];
-  const int lane = threadIdx.x & 63, gl = lane & (G - 1), gbase = lane - gl;
-  const int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
-  const uint64_t gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << gbase);
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1), sub = lane / G;
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
   double m_objv = 0, m_objw = 0, m_corr = 0, m_n = 0;
-  const bool live = row < nrows;
+  // persistent: wave w handles rows w, w + nwaves, ...
+  for (int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6; row < nrows;
+       row += nwaves) {
+  const bool live = true;
   float wl = 0.f;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q = s;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q2 = s;
   int64_t b = 0, e = 0;
   if (live) {
     b = off[row];
     e = off[row + 1];
   }
-  for (int64_t base = b; base < e; base += G) {
-    const int64_t j = base + gl;
-    const bool valid = j < e;
-    int vid = -1;
-    float x = 0.f;
-    float2 h = make_float2(0.f, 0.f);
-    if (valid) {
-      const int k = lid[j];
-      x = val ? val[j] : 1.f;
-      h = hdr[k];
-      vid = __float_as_int(h.y);
-    }
+  for (int64_t pb = b; pb < e; pb += 64) {  // wave-uniform: one row per wave
+    const int n = (int)(e - pb < 64 ? e - pb : 64);
+    const bool ok = lane < n;
+    const int l = ok ? lid[pb + lane] : -1;
+    const float x = ok ? (val ? val[pb + lane] : 1.f) : 0.f;
+    const float2 h = l >= 0 ? hdr[l] : make_float2(0.f, __int_as_float(-1));
     wl += x * h.x;
-    uint64_t mg = __ballot(valid && vid >= 0) & gmask;
-    while (mg) {
-      int t[4];
-      float keep[4];
+    const int vid = __float_as_int(h.y);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (mg) {
-          t[u] = __ffsll((unsigned long long)mg) - 1;
-          mg &= mg - 1;
-          keep[u] = 1.f;
-        } else {
-          t[u] = t[0];
-          keep[u] = 0.f;
-        }
-      }
-      float4 v[4];
-      float xs[4];
+    for (int t0 = 0; t0 < S::NI; t0 += S::TI) {
+      if (t0 * S::SUB >= n) break;
+      float4 v[S::TI];
+      float xs[S::TI];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int vu = __shfl(vid, t[u], 64);
-        xs[u] = __shfl(x, t[u], 64) * keep[u];
-        v[u] = reinterpret_cast<const float4*>(vc + (int64_t)vu * vstride)[gl];
+      for (int t = 0; t < S::TI; ++t) {
+        const int idx = (t0 + t) * S::SUB + sub;
+        const int vu = __shfl(vid, idx, 64);
+        const float xu = __shfl(x, idx, 64);
+        xs[t] = vu >= 0 ? xu : 0.f;
+        v[t] = vu >= 0 ? reinterpret_cast<const float4*>(vc + (int64_t)vu * vstride)[gl]
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float xu = xs[u], xx = xu * xu;
-        s.x += xu * v[u].x; s.y += xu * v[u].y; s.z += xu * v[u].z; s.w += xu * v[u].w;
-        q.x += xx * v[u].x * v[u].x; q.y += xx * v[u].y * v[u].y;
-        q.z += xx * v[u].z * v[u].z; q.w += xx * v[u].w * v[u].w;
+      for (int t = 0; t < S::TI; ++t) {
+        const float xu = xs[t], xx = xu * xu;
+        s.x += xu * v[t].x; s.y += xu * v[t].y; s.z += xu * v[t].z; s.w += xu * v[t].w;
+        q2.x += xx * v[t].x * v[t].x; q2.y += xx * v[t].y * v[t].y;
+        q2.z += xx * v[t].z * v[t].z; q2.w += xx * v[t].w * v[t].w;
       }
     }
   }
-  const float wsum = group_sum<G>(wl);
-  float part = (s.x * s.x - q.x) + (s.y * s.y - q.y) + (s.z * s.z - q.z) + (s.w * s.w - q.w);
+  // sum the SUB partial rows: lanes gl, gl+G, gl+2G, ... hold the same dims
+#pragma unroll
+  for (int o = G; o < 64; o <<= 1) {
+    s.x += __shfl_xor(s.x, o, 64); s.y += __shfl_xor(s.y, o, 64);
+    s.z += __shfl_xor(s.z, o, 64); s.w += __shfl_xor(s.w, o, 64);
+    q2.x += __shfl_xor(q2.x, o, 64); q2.y += __shfl_xor(q2.y, o, 64);
+    q2.z += __shfl_xor(q2.z, o, 64); q2.w += __shfl_xor(q2.w, o, 64);
+  }
+  const float wsum = wave_sum(wl);
+  float part = (s.x * s.x - q2.x) + (s.y * s.y - q2.y) + (s.z * s.z - q2.z) + (s.w * s.w - q2.w);
   part = group_sum<G>(part);
   if (live) {
-    reinterpret_cast<float4*>(xv + row * vstride)[gl] = s;
-    if (gl == 0) {
+    if (sub == 0) reinterpret_cast<float4*>(xv + row * vstride)[gl] = s;
+    if (lane == 0) {
       const float p = wsum + 0.5f * part;
       const float y = label[row];
       const LossOut o = eval_loss(loss, y, p);
       const LossOut ow = eval_loss(loss, y, wsum);
       py_out[row] = p;
       dual_out[row] = o.dual;
-      m_objv = o.objv;
-      m_objw = ow.objv;
-      m_corr = ((y > 0.f && p > 0.f) || (y <= 0.f && p <= 0.f)) ? 1.0 : 0.0;
-      m_n = 1.0;
+      m_objv += o.objv;
+      m_objw += ow.objv;
+      m_corr += ((y > 0.f && p > 0.f) || (y <= 0.f && p <= 0.f)) ? 1.0 : 0.0;
+      m_n += 1.0;
     }
   }
-  double r;
-  r = block_sum_d(m_objv, sh); if (threadIdx.x == 0) atomicAdd(met + 0, r); __syncthreads();
-  r = block_sum_d(m_objw, sh); if (threadIdx.x == 0) atomicAdd(met + 1, r); __syncthreads();
-  r = block_sum_d(m_corr, sh); if (threadIdx.x == 0) atomicAdd(met + 2, r); __syncthreads();
-  r = block_sum_d(m_n, sh); if (threadIdx.x == 0) atomicAdd(met + 3, r);
+  }  // rows
+  block_partials(part, sh, m_objv, m_objw, m_corr, m_n);
 }
 
-// linear model: G lanes stride over one row's non-zeros
+// linear model: G lanes stride over one row's non-zeros; persistent over rows
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_lin_fwd(int64_t nrows, const int64_t* __restrict__ off,
                                                       const int32_t* __restrict__ lid,
@@ -162,64 +183,90 @@ __global__ __launch_bounds__(kThreads) void k_lin_fwd(int64_t nrows, const int64
                                                       const float* __restrict__ w,
                                                       const float* __restrict__ label, int loss,
                                                       float* __restrict__ py_out,
-                                                      float* __restrict__ dual_out, double* met) {
+                                                      float* __restrict__ dual_out, double* part) {
   __shared__ double sh[kThreads / 64];
   const int lane = threadIdx.x & 63, gl = lane & (G - 1);
-  const int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G;
+  const int64_t ngroups = (int64_t)gridDim.x * (kThreads / G);
   double m_objv = 0, m_corr = 0, m_n = 0;
-  float acc = 0.f;
-  if (row < nrows) {
+  for (int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) / G; row < nrows;
+       row += ngroups) {
+    float acc = 0.f;
     const int64_t b = off[row], e = off[row + 1];
     for (int64_t j = b + gl; j < e; j += G) acc += (val ? val[j] : 1.f) * w[lid[j]];
+    acc = group_sum<G>(acc);
+    if (gl == 0) {
+      const float y = label[row];
+      const LossOut o = eval_loss(loss, y, acc);
+      py_out[row] = acc;
+      dual_out[row] = o.dual;
+      m_objv += o.objv;
+      m_corr += ((y > 0.f && acc > 0.f) || (y <= 0.f && acc <= 0.f)) ? 1.0 : 0.0;
+      m_n += 1.0;
+    }
   }
-  acc = group_sum<G>(acc);
-  if (row < nrows && gl == 0) {
-    const float y = label[row];
-    const LossOut o = eval_loss(loss, y, acc);
-    py_out[row] = acc;
-    dual_out[row] = o.dual;
-    m_objv = o.objv;
-    m_corr = ((y > 0.f && acc > 0.f) || (y <= 0.f && acc <= 0.f)) ? 1.0 : 0.0;
-    m_n = 1.0;
+  (void)lane;
+  block_partials(part, sh, m_objv, m_objv, m_corr, m_n);
+}
+
+// met[i] += sum over blocks of part[b * 4 + i]
+__global__ __launch_bounds__(kThreads) void k_partials_sum(const double* __restrict__ part,
+                                                           int nblk, double* met) {
+  __shared__ double sh[kThreads / 64];
+  for (int i = 0; i < 4; ++i) {
+    double a = 0;
+    for (int bidx = threadIdx.x; bidx < nblk; bidx += kThreads) a += part[bidx * 4 + i];
+    const double r = block_sum_d(a, sh);
+    if (threadIdx.x == 0) met[i] += r;
+    __syncthreads();
   }
-  double r;
-  r = block_sum_d(m_objv, sh); if (threadIdx.x == 0) { atomicAdd(met + 0, r); atomicAdd(met + 1, r); }
-  __syncthreads();
-  r = block_sum_d(m_corr, sh); if (threadIdx.x == 0) atomicAdd(met + 2, r); __syncthreads();
-  r = block_sum_d(m_n, sh); if (threadIdx.x == 0) atomicAdd(met + 3, r);
 }
 
 // ---------------------------------------------------------------- backward
-__global__ void k_chunk_count(int64_t nuniq, const int64_t* csc_off, int64_t* chunk_cnt) {
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Two work lists over the CSC: keys WITHOUT an embedding are split into
+// "scalar" chunks of <= kChunkS occurrences summed by one lane each (gw
+// only); keys WITH an embedding into "V" chunks of <= kChunkV = 64
+// occurrences, one WAVE each (gw, xxp and the 64-float gV row). A key with
+// more than one chunk accumulates its chunks with float atomics.
+constexpr int kChunkV = 64;
+
+__global__ __launch_bounds__(kThreads) void k_chunk_count(int64_t nuniq,
+                                                          const int64_t* __restrict__ csc_off,
+                                                          const float2* __restrict__ hdr,
+                                                          int64_t* cnt_s, int64_t* cnt_v) {
+  const int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (k < nuniq) {
     const int64_t c = csc_off[k + 1] - csc_off[k];
-    chunk_cnt[k] = c > 0 ? (c + kChunk - 1) / kChunk : 0;
+    const bool has_v = hdr && __float_as_int(hdr[k].y) >= 0;
+    cnt_s[k] = has_v ? 0 : (c + kChunk - 1) / kChunk;
+    cnt_v[k] = has_v ? (c + kChunkV - 1) / kChunkV : 0;
   }
 }
 
-// writes the chunk table; zeroes the gradients of multi-chunk keys (they
-// are accumulated with atomics). Lane per key for the common single-chunk
-// key; a multi-chunk (hot) key is expanded by the whole wave, 64 chunks per
-// round, so the hottest key does not serialise on one lane.
+// writes both chunk tables; zeroes the gradients of multi-chunk keys. Lane
+// per key for single-chunk keys; a multi-chunk (hot) key is expanded by the
+// whole wave, 64 chunks per round, so the hottest key does not serialise.
 __global__ __launch_bounds__(kThreads) void k_chunk_fill(int64_t nuniq,
                                                          const int64_t* __restrict__ csc_off,
-                                                         const int64_t* __restrict__ chunk_off,
+                                                         const int64_t* __restrict__ off_s,
+                                                         const int64_t* __restrict__ off_v,
                                                          const float2* __restrict__ hdr,
-                                                         int vstride, int32_t* chunk_key,
-                                                         int32_t* chunk_beg, float* gw,
-                                                         float* gvc) {
+                                                         int vstride, int32_t* key_s,
+                                                         int32_t* beg_s, int32_t* key_v,
+                                                         int32_t* beg_v, float* gw, float* gvc) {
   const int lane = threadIdx.x & 63;
-  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   int64_t c0 = 0, nc = 0;
   int32_t b0 = 0;
+  int isv = 0;
   if (k < nuniq) {
-    c0 = chunk_off[k];
-    nc = chunk_off[k + 1] - c0;
+    const int64_t ns = off_s[k + 1] - off_s[k];
+    isv = ns == 0;
+    c0 = isv ? off_v[k] : off_s[k];
+    nc = isv ? off_v[k + 1] - c0 : ns;
     b0 = (int32_t)csc_off[k];
     if (nc == 1) {
-      chunk_key[c0] = (int32_t)k;
-      chunk_beg[c0] = b0;
+      (isv ? key_v : key_s)[c0] = (int32_t)k;
+      (isv ? beg_v : beg_s)[c0] = b0;
     }
   }
   uint64_t m = __ballot(nc > 1);
@@ -230,133 +277,129 @@ __global__ __launch_bounds__(kThreads) void k_chunk_fill(int64_t nuniq,
     const int64_t jc0 = __shfl(c0, src, 64);
     const int64_t jnc = __shfl(nc, src, 64);
     const int32_t jb0 = __shfl(b0, src, 64);
+    const int jv = __shfl(isv, src, 64);
+    const int csz = jv ? kChunkV : kChunk;
+    int32_t* kk = jv ? key_v : key_s;
+    int32_t* bb = jv ? beg_v : beg_s;
     for (int64_t c = lane; c < jnc; c += 64) {
-      chunk_key[jc0 + c] = jk;
-      chunk_beg[jc0 + c] = jb0 + (int32_t)(c * kChunk);
+      kk[jc0 + c] = jk;
+      bb[jc0 + c] = jb0 + (int32_t)(c * csz);
     }
     if (lane == 0) gw[jk] = 0.f;
-    if (vstride > 0) {
+    if (jv) {
       const int vid = __float_as_int(hdr[jk].y);
-      if (vid >= 0)
-        for (int d = lane * 4; d < vstride; d += 256)
-          *reinterpret_cast<float4*>(gvc + (int64_t)vid * vstride + d) =
-              make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int d = lane * 4; d < vstride; d += 256)
+        *reinterpret_cast<float4*>(gvc + (int64_t)vid * vstride + d) =
+            make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
 
-template <int G>
-__global__ __launch_bounds__(kThreads) void k_fm_bwd(const int64_t* __restrict__ nchunk_p, const int32_t* __restrict__ chunk_key,
-                                                     const int32_t* __restrict__ chunk_beg,
-                                                     const int64_t* __restrict__ csc_off,
-                                                     const int32_t* __restrict__ csc_row,
-                                                     const float* __restrict__ csc_val,
-                                                     const float* __restrict__ dual,
-                                                     const float* __restrict__ xv,
-                                                     const float2* __restrict__ hdr,
-                                                     const float* __restrict__ vc, int vstride,
-                                                     float* __restrict__ gw_out,
-                                                     float* __restrict__ gvc) {
-  // ONE LANE PER CHUNK computes the scalar sums (gw, xxp) of its <= kChunk
-  // occurrences; the wave then runs the embedding-gradient jobs of the
-  // chunks whose key has V, G lanes per job (float4 slice of each xv row).
-  const int lane = threadIdx.x & 63;
-  const int64_t nch = *nchunk_p;
-  const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const bool live = c < nch;
-  int k = 0, b = 0, e = 0, vid = -1;
-  bool multi = false;
-  float gw = 0.f, xxp = 0.f;
-  if (live) {
-    k = chunk_key[c];
-    const int kb = (int)csc_off[k], ke = (int)csc_off[k + 1];
-    b = chunk_beg[c];
-    e = b + kChunk < ke ? b + kChunk : ke;
-    multi = (ke - kb) > kChunk;
-    int p = b;
-    for (; p + 3 < e; p += 4) {  // 4 independent row->dual chains in flight
-      int i[4];
-      float x[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        i[u] = csc_row[p + u];
-        x[u] = csc_val ? csc_val[p + u] : 1.f;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float d = dual[i[u]] * x[u];
-        gw += d;
-        xxp += d * x[u];
-      }
-    }
-    for (; p < e; ++p) {
-      const float x = csc_val ? csc_val[p] : 1.f;
-      const float d = dual[csc_row[p]] * x;
-      gw += d;
-      xxp += d * x;
-    }
-    vid = __float_as_int(hdr[k].y);
-    if (!multi) gw_out[k] = gw;
-    else atomicAdd(gw_out + k, gw);
-  }
-  for_each_row_job<G>(live && vid >= 0, [&](int src, int gl) {
-    const int sl = src >= 0 ? src : lane;
-    const int jv = __shfl(vid, sl, 64), jb = __shfl(b, sl, 64), je = __shfl(e, sl, 64);
-    const float jx = __shfl(xxp, sl, 64);
-    const int jm = __shfl((int)multi, sl, 64);
-    if (src < 0) return;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    int p = jb;
-    for (; p + 3 < je; p += 4) {
-      float d[4];
-      float4 a[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = csc_row[p + u];
-        d[u] = dual[i] * (csc_val ? csc_val[p + u] : 1.f);
-        a[u] = reinterpret_cast<const float4*>(xv + (int64_t)i * vstride)[gl];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc.x += d[u] * a[u].x; acc.y += d[u] * a[u].y;
-        acc.z += d[u] * a[u].z; acc.w += d[u] * a[u].w;
-      }
-    }
-    for (; p < je; ++p) {
-      const int i = csc_row[p];
-      const float d = dual[i] * (csc_val ? csc_val[p] : 1.f);
-      const float4 a = reinterpret_cast<const float4*>(xv + (int64_t)i * vstride)[gl];
-      acc.x += d * a.x; acc.y += d * a.y; acc.z += d * a.z; acc.w += d * a.w;
-    }
-    const float4 v = reinterpret_cast<const float4*>(vc + (int64_t)jv * vstride)[gl];
-    acc.x -= jx * v.x; acc.y -= jx * v.y; acc.z -= jx * v.z; acc.w -= jx * v.w;
-    float* gv = gvc + (int64_t)jv * vstride + gl * 4;
-    if (!jm) {
-      *reinterpret_cast<float4*>(gv) = acc;
-    } else {
-      atomicAdd(gv + 0, acc.x); atomicAdd(gv + 1, acc.y);
-      atomicAdd(gv + 2, acc.z); atomicAdd(gv + 3, acc.w);
-    }
-  });
-}
-
-__global__ __launch_bounds__(kThreads) void k_lin_bwd(const int64_t* __restrict__ nchunk_p, const int32_t* __restrict__ chunk_key,
-                                                      const int32_t* __restrict__ chunk_beg,
-                                                      const int64_t* __restrict__ csc_off,
-                                                      const int32_t* __restrict__ csc_row,
-                                                      const float* __restrict__ csc_val,
-                                                      const float* __restrict__ dual,
-                                                      float* __restrict__ grad) {
+// scalar chunks: one lane sums dual_i * x_ik over <= kChunk occurrences
+__global__ __launch_bounds__(kThreads) void k_bwd_scalar(const int64_t* __restrict__ nchunk_p,
+                                                         const int32_t* __restrict__ chunk_key,
+                                                         const int32_t* __restrict__ chunk_beg,
+                                                         const int64_t* __restrict__ csc_off,
+                                                         const int32_t* __restrict__ csc_row,
+                                                         const float* __restrict__ csc_val,
+                                                         const float* __restrict__ dual,
+                                                         float* __restrict__ gw_out) {
   const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (c >= *nchunk_p) return;
   const int k = chunk_key[c];
-  const int64_t kb = csc_off[k], ke = csc_off[k + 1];
-  const int64_t b = chunk_beg[c];
-  const int64_t e = b + kChunk < ke ? b + kChunk : ke;
+  const int kb = (int)csc_off[k], ke = (int)csc_off[k + 1];
+  const int b = chunk_beg[c];
+  const int e = b + kChunk < ke ? b + kChunk : ke;
   float gw = 0.f;
-  for (int64_t p = b; p < e; ++p) gw += dual[csc_row[p]] * (csc_val ? csc_val[p] : 1.f);
-  if ((ke - kb) > kChunk) atomicAdd(grad + k, gw);
-  else grad[k] = gw;
+  int p = b;
+  for (; p + 3 < e; p += 4) {  // 4 independent row->dual chains in flight
+    int i[4];
+    float x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      i[u] = csc_row[p + u];
+      x[u] = csc_val ? csc_val[p + u] : 1.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) gw += dual[i[u]] * x[u];
+  }
+  for (; p < e; ++p) gw += dual[csc_row[p]] * (csc_val ? csc_val[p] : 1.f);
+  if (ke - kb > kChunk) atomicAdd(gw_out + k, gw);
+  else gw_out[k] = gw;
+}
+
+// V chunks: one wave per chunk, persistent over the (device-counted) list
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ nchunk_p,
+                                                    const int32_t* __restrict__ chunk_key,
+                                                    const int32_t* __restrict__ chunk_beg,
+                                                    const int64_t* __restrict__ csc_off,
+                                                    const int32_t* __restrict__ csc_row,
+                                                    const float* __restrict__ csc_val,
+                                                    const float* __restrict__ dual,
+                                                    const float* __restrict__ xv,
+                                                    const float2* __restrict__ hdr,
+                                                    const float* __restrict__ vc, int vstride,
+                                                    float* __restrict__ gw_out,
+                                                    float* __restrict__ gvc) {
+  using S = Shape<G>;
+  const int lane = threadIdx.x & 63, gl = lane & (G - 1), sub = lane / G;
+  const int64_t nch = *nchunk_p;
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+  for (int64_t c = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6; c < nch; c += nwaves) {
+    const int k = chunk_key[c];
+    const int kb = (int)csc_off[k], ke = (int)csc_off[k + 1];
+    const int b = chunk_beg[c];
+    const int n = b + kChunkV < ke ? kChunkV : ke - b;
+    const bool multi = ke - kb > kChunkV;
+    const int vid = __float_as_int(hdr[k].y);
+    const bool ok = lane < n;
+    const int r = ok ? csc_row[b + lane] : -1;
+    const float x = ok ? (csc_val ? csc_val[b + lane] : 1.f) : 0.f;
+    const float d = ok ? dual[r] * x : 0.f;
+    const float gw = wave_sum(d);
+    const float xxp = wave_sum(d * x);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int t0 = 0; t0 < S::NI; t0 += S::TI) {
+      if (t0 * S::SUB >= n) break;
+      float4 a[S::TI];
+      float du[S::TI];
+#pragma unroll
+      for (int t = 0; t < S::TI; ++t) {
+        const int idx = (t0 + t) * S::SUB + sub;
+        const int ru = __shfl(r, idx, 64);
+        du[t] = __shfl(d, idx, 64);
+        a[t] = ru >= 0 ? reinterpret_cast<const float4*>(xv + (int64_t)ru * vstride)[gl]
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int t = 0; t < S::TI; ++t) {
+        acc.x += du[t] * a[t].x; acc.y += du[t] * a[t].y;
+        acc.z += du[t] * a[t].z; acc.w += du[t] * a[t].w;
+      }
+    }
+#pragma unroll
+    for (int o = G; o < 64; o <<= 1) {
+      acc.x += __shfl_xor(acc.x, o, 64); acc.y += __shfl_xor(acc.y, o, 64);
+      acc.z += __shfl_xor(acc.z, o, 64); acc.w += __shfl_xor(acc.w, o, 64);
+    }
+    if (lane == 0) {
+      if (multi) atomicAdd(gw_out + k, gw);
+      else gw_out[k] = gw;
+    }
+    if (sub == 0) {
+      const float4 v = reinterpret_cast<const float4*>(vc + (int64_t)vid * vstride)[gl];
+      acc.x -= xxp * v.x; acc.y -= xxp * v.y; acc.z -= xxp * v.z; acc.w -= xxp * v.w;
+      float* gv = gvc + (int64_t)vid * vstride + gl * 4;
+      if (!multi) {
+        *reinterpret_cast<float4*>(gv) = acc;
+      } else {
+        atomicAdd(gv + 0, acc.x); atomicAdd(gv + 1, acc.y);
+        atomicAdd(gv + 2, acc.z); atomicAdd(gv + 3, acc.w);
+      }
+    }
+  }
 }
 
 // gradient clipping / dropout / normalisation on the m embedding-gradient
@@ -365,18 +408,20 @@ __global__ __launch_bounds__(kThreads) void k_grad_post(const int64_t* __restric
                                                         float* gvc, int vstride, int dim,
                                                         float clip, float dropout, uint64_t seed,
                                                         double* sumsq) {
+  // grid-stride (grid capped at 1024 blocks): one sumsq atomic per block
   __shared__ double sh[kThreads / 64];
-  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const int64_t r = t / vstride;
-  const int d = (int)(t % vstride);
-  const int64_t m = *m_p;
+  const int64_t total = *m_p * vstride;
   double ss = 0;
-  if (r < m && d < dim) {
+  for (int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * kThreads) {
+    const int64_t r = t / vstride;
+    const int d = (int)(t % vstride);
+    if (d >= dim) continue;
     float v = gvc[t];
     if (clip > 0.f) v = fminf(fmaxf(v, -clip), clip);
     if (dropout > 0.f && uhash01(seed, (uint64_t)r, (uint64_t)d) > 1.f - dropout) v = 0.f;
     gvc[t] = v;
-    ss = (double)v * v;
+    ss += (double)v * v;
   }
   if (sumsq) {
     const double s = block_sum_d(ss, sh);
@@ -406,57 +451,76 @@ __global__ __launch_bounds__(kThreads) void k_grad_scale(const int64_t* __restri
     default: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                 \
   }
 
+int64_t fm_fwd_partials() { return 4 * kFwdBlocks; }
+
 void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
                 const float* w_or_hdr, const float* vc, int vstride, const float* label, int loss,
-                float* py, float* dual, float* xv, double* met, hipStream_t s) {
+                float* py, float* dual, float* xv, double* met, double* part, hipStream_t s) {
   if (nrows <= 0) return;
+  int nblk;
   if (vstride == 0) {
     constexpr int G = 8;
-    hipLaunchKernelGGL(k_lin_fwd<G>, dim3(grid_for(nrows * G, kThreads)), dim3(kThreads), 0, s,
-                       nrows, offset, lid, val, w_or_hdr, label, loss, py, dual, met);
-    return;
+    nblk = grid_for(nrows * G, kThreads, kFwdBlocks);
+    hipLaunchKernelGGL(k_lin_fwd<G>, dim3(nblk), dim3(kThreads), 0, s, nrows, offset, lid, val,
+                       w_or_hdr, label, loss, py, dual, part);
+  } else {
+    const int G = vstride / 4;  // vstride <= 256 enforced by the binding
+    const float2* hdr = reinterpret_cast<const float2*>(w_or_hdr);
+    nblk = grid_for(nrows * 64, kThreads, kFwdBlocks);  // wave per row, persistent
+    const dim3 grid(nblk), block(kThreads);
+    WH_DISPATCH_G(G, k_fm_fwd, grid, block, 0, s, nrows, offset, lid, val, hdr, vc, vstride,
+                  label, loss, py, dual, xv, part);
   }
-  const int G = vstride / 4;  // vstride <= 256 enforced by the binding
-  const float2* hdr = reinterpret_cast<const float2*>(w_or_hdr);
-  const dim3 grid(grid_for(nrows * G, kThreads)), block(kThreads);
-  WH_DISPATCH_G(G, k_fm_fwd, grid, block, 0, s, nrows, offset, lid, val, hdr, vc, vstride, label,
-                loss, py, dual, xv, met);
+  hipLaunchKernelGGL(k_partials_sum, dim3(1), dim3(kThreads), 0, s, part, nblk, met);
 }
 
-int64_t fm_bwd_chunks_bound(int64_t nuniq, int64_t nnz) { return nuniq + nnz / kChunk + 1; }
+static int64_t scalar_cap(int64_t nuniq, int64_t nnz) { return nuniq + nnz / kChunk + 1; }
+static int64_t v_cap(int64_t nuniq, int64_t nnz) { return nuniq + nnz / kChunkV + 1; }
 
-void fm_backward(int64_t nuniq, const int64_t* csc_off, const int32_t* csc_row,
+int64_t fm_bwd_chunks_bound(int64_t nuniq, int64_t nnz) {
+  return scalar_cap(nuniq, nnz) + v_cap(nuniq, nnz);
+}
+
+void fm_backward(int64_t nuniq, int64_t nnz, const int64_t* csc_off, const int32_t* csc_row,
                  const float* csc_val, const float* dual, const float* xv, const float* hdr_f,
                  const float* vc, int vstride, float* gw, float* gvc, int32_t* chunk_key,
                  int32_t* chunk_beg, int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp,
-                 int64_t chunk_cap, hipStream_t s) {
+                 hipStream_t s) {
   if (nuniq <= 0) return;
-  const float2* hdr = reinterpret_cast<const float2*>(hdr_f);
+  const float2* hdr = vstride > 0 ? reinterpret_cast<const float2*>(hdr_f) : nullptr;
+  int64_t* cnt_s = chunk_cnt;
+  int64_t* cnt_v = chunk_cnt + nuniq;
+  int64_t* off_s = chunk_off;
+  int64_t* off_v = chunk_off + nuniq + 1;
+  const int64_t cap_s = scalar_cap(nuniq, nnz);
+  int32_t* key_s = chunk_key;
+  int32_t* beg_s = chunk_beg;
+  int32_t* key_v = chunk_key + cap_s;
+  int32_t* beg_v = chunk_beg + cap_s;
   hipLaunchKernelGGL(k_chunk_count, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
-                     csc_off, chunk_cnt);
-  scan_i64(chunk_cnt, chunk_off, nuniq, scan_tmp, s);
+                     csc_off, hdr, cnt_s, cnt_v);
+  scan_i64(cnt_s, off_s, nuniq, scan_tmp, s);
+  if (hdr) scan_i64(cnt_v, off_v, nuniq, scan_tmp, s);
   hipLaunchKernelGGL(k_chunk_fill, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
-                     csc_off, chunk_off, hdr, vstride, chunk_key, chunk_beg, gw, gvc);
-  // the chunk count is data dependent (device value chunk_off[nuniq]); launch
-  // over the host-side bound and let surplus work items exit, so the whole
-  // step stays free of host synchronisation.
-  const int64_t* nchunk_p = chunk_off + nuniq;
-  if (vstride == 0) {
-    hipLaunchKernelGGL(k_lin_bwd, dim3(grid_for(chunk_cap, kThreads)), dim3(kThreads), 0, s,
-                       nchunk_p, chunk_key, chunk_beg, csc_off, csc_row, csc_val, dual, gw);
-    return;
-  }
+                     csc_off, off_s, off_v, hdr, vstride, key_s, beg_s, key_v, beg_v, gw, gvc);
+  // chunk counts are device values (off[nuniq]); the scalar kernel launches
+  // over the host-side bound and surplus lanes exit; the V kernel is
+  // persistent. No host synchronisation in the step.
+  hipLaunchKernelGGL(k_bwd_scalar, dim3(grid_for(cap_s, kThreads)), dim3(kThreads), 0, s,
+                     off_s + nuniq, key_s, beg_s, csc_off, csc_row, csc_val, dual, gw);
+  if (!hdr) return;
   const int G = vstride / 4;
-  const dim3 grid(grid_for(chunk_cap, kThreads)), block(kThreads);  // lane per chunk
-  WH_DISPATCH_G(G, k_fm_bwd, grid, block, 0, s, nchunk_p, chunk_key, chunk_beg, csc_off,
-                csc_row, csc_val, dual, xv, hdr, vc, vstride, gw, gvc);
+  const int64_t vwaves = std::min<int64_t>(v_cap(nuniq, nnz), 8192);  // <= 32 waves per CU
+  const dim3 grid((unsigned)((vwaves + 3) / 4)), block(kThreads);
+  WH_DISPATCH_G(G, k_bwd_v, grid, block, 0, s, off_v + nuniq, key_v, beg_v, csc_off, csc_row,
+                csc_val, dual, xv, hdr, vc, vstride, gw, gvc);
 }
 
 void fm_grad_post(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim, float clip,
                   float dropout, uint64_t seed, double* sumsq, hipStream_t s) {
   if (m_cap <= 0 || vstride == 0) return;
-  hipLaunchKernelGGL(k_grad_post, dim3(grid_for(m_cap * vstride, kThreads)), dim3(kThreads), 0,
-                     s, m, gvc, vstride, dim, clip, dropout, seed, sumsq);
+  hipLaunchKernelGGL(k_grad_post, dim3(grid_for(m_cap * vstride, kThreads, 1024)), dim3(kThreads),
+                     0, s, m, gvc, vstride, dim, clip, dropout, seed, sumsq);
 }
 
 void fm_grad_scale(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim,

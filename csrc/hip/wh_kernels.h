@@ -118,18 +118,22 @@ void vidx_renumber(float* hdr, int64_t n, int32_t* flag_tmp, int64_t* pos_tmp, i
 //   linear (vstride == 0): w_or_hdr = w[U], vc unused
 //   loss: 1 square, 2 logit, 4 squared hinge
 //   met[0..3] += {objv, objv_w, correct(threshold 0), n}  (double)
+//   part: scratch of fm_fwd_partials() doubles (per-block metric partials)
+int64_t fm_fwd_partials();
 void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
                 const float* w_or_hdr, const float* vc, int vstride, const float* label, int loss,
-                float* py, float* dual, float* xv, double* met, hipStream_t s);
+                float* py, float* dual, float* xv, double* met, double* part, hipStream_t s);
 // Backward: gw[U] for every key, gvc[m] for the keys with an embedding row
 //   gw_k = sum_i dual_i x_ik
 //   gV_k = sum_i dual_i x_ik xv_i - (sum_i dual_i x_ik^2) V_k
 int64_t fm_bwd_chunks_bound(int64_t nuniq, int64_t nnz);
-void fm_backward(int64_t nuniq, const int64_t* csc_off, const int32_t* csc_row,
+// scratch: chunk_key/chunk_beg [fm_bwd_chunks_bound], chunk_cnt [2 nuniq],
+// chunk_off [2 (nuniq + 1)], scan_tmp [scan_tmp_elems(nuniq)]
+void fm_backward(int64_t nuniq, int64_t nnz, const int64_t* csc_off, const int32_t* csc_row,
                  const float* csc_val, const float* dual, const float* xv, const float* hdr,
                  const float* vc, int vstride, float* gw, float* gvc, int32_t* chunk_key,
                  int32_t* chunk_beg, int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp,
-                 int64_t chunk_cap, hipStream_t s);
+                 hipStream_t s);
 // post-process the m (device count) V-gradient rows: clip to [-c, c] (c>0),
 // dropout with prob p (p>0); sumsq (optional) receives the squared norm
 void fm_grad_post(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim, float clip,
