@@ -141,13 +141,20 @@ class KVStore {
     auto dev = torch::Device(torch::kCUDA, device);
     c10::DeviceGuard g(dev);
     auto f32 = torch::TensorOptions().dtype(torch::kFloat32).device(dev);
-    keys_ = torch::full({cap}, -1, f32.dtype(torch::kInt64));
-    w_ = torch::zeros({cap}, f32);
-    z_ = torch::zeros({cap}, f32);
-    sq_ = torch::zeros({cap}, f32);
+    // AoS slot table [cap, 8] x 4 bytes = wh::KVSlot; the per-field tensors
+    // below are strided views into it (shared storage, writable)
+    slots_ = torch::zeros({cap, 8}, f32.dtype(torch::kInt32));
+    auto as_i64 = slots_.view(torch::kInt64);   // [cap, 4]
+    auto as_f32 = slots_.view(torch::kFloat32); // [cap, 8]
+    keys_ = as_i64.select(1, 0);
+    keys_.fill_(-1);
+    w_ = as_f32.select(1, 2);
+    z_ = as_f32.select(1, 3);
+    sq_ = as_f32.select(1, 4);
+    cnt_ = slots_.select(1, 5);
+    vrow_ = slots_.select(1, 6);
+    vrow_.fill_(-1);
     if (dim > 0) {
-      cnt_ = torch::zeros({cap}, f32.dtype(torch::kInt32));
-      vrow_ = torch::full({cap}, -1, f32.dtype(torch::kInt32));
       V_ = torch::zeros({std::max<int64_t>(vcap, 1), vstride_}, f32);
       VG_ = torch::zeros({std::max<int64_t>(vcap, 1), vstride_}, f32);
     }
@@ -159,12 +166,7 @@ class KVStore {
 
   wh::KVTable table() const {
     wh::KVTable t;
-    t.keys = reinterpret_cast<uint64_t*>(keys_.data_ptr());
-    t.w = ptr<float>(w_);
-    t.z = ptr<float>(z_);
-    t.sq = ptr<float>(sq_);
-    t.cnt = dim_ > 0 ? ptr<uint32_t>(cnt_) : nullptr;
-    t.vrow = dim_ > 0 ? ptr<int32_t>(vrow_) : nullptr;
+    t.sl = reinterpret_cast<wh::KVSlot*>(slots_.data_ptr());
     t.V = dim_ > 0 ? ptr<float>(V_) : nullptr;
     t.VG = dim_ > 0 ? ptr<float>(VG_) : nullptr;
     t.vnext = ptr<int32_t>(vnext_);
@@ -283,7 +285,7 @@ class KVStore {
   int64_t cap() const { return cap_; }
   int64_t vcap() const { return vcap_; }
 
-  Tensor keys_, w_, z_, sq_, cnt_, vrow_, V_, VG_, vnext_, stats_;
+  Tensor slots_, keys_, w_, z_, sq_, cnt_, vrow_, V_, VG_, vnext_, stats_;
 
  private:
   int64_t cap_ = 0, vcap_ = 0, dim_ = 0;
@@ -410,8 +412,12 @@ Tensor auc(const Tensor& py, const Tensor& label) {
   CHECK_IN(label, torch::kFloat32);
   c10::DeviceGuard g(py.device());
   const int64_t n = py.numel();
-  auto order = std::get<1>(py.sort(0, false));
-  auto lab = label.index_select(0, order).contiguous();
+  auto pys = torch::empty_like(py);
+  auto lab = torch::empty_like(label);
+  const size_t sbytes = wh::auc_sort_tmp_bytes(n);
+  auto stmp = torch::empty({(int64_t)sbytes + 16}, py.options().dtype(torch::kUInt8));
+  wh::sort_by_score(ptr<float>(py), ptr<float>(label), n, ptr<float>(pys), ptr<float>(lab),
+                    stmp.data_ptr(), sbytes, cur_stream(py));
   auto tmp = torch::empty({n / 2 + 1 + n + 1 + wh::scan_tmp_elems(n)},
                           py.options().dtype(torch::kInt64));
   auto out = torch::empty({2}, py.options().dtype(torch::kFloat64));
@@ -641,6 +647,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("vstride", &KVStore::vstride)
       .def_property_readonly("cap", &KVStore::cap)
       .def_property_readonly("vcap", &KVStore::vcap)
+      .def_readonly("slots", &KVStore::slots_)
       .def_readonly("keys", &KVStore::keys_)
       .def_readonly("w", &KVStore::w_)
       .def_readonly("z", &KVStore::z_)

@@ -23,7 +23,7 @@ __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
 }
 
 __global__ __launch_bounds__(kThreads) void k_kv_find(const uint64_t* keys_in, int64_t n,
-                                                      uint64_t* tkeys, int64_t cap, int insert,
+                                                      KVSlot* tsl, int64_t cap, int insert,
                                                       int32_t* slot, int64_t* stats) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   bool created = false, failed = false;
@@ -33,11 +33,11 @@ __global__ __launch_bounds__(kThreads) void k_kv_find(const uint64_t* keys_in, i
     uint64_t h = mix64(k) & mask;
     int64_t res = -1;
     for (int64_t probe = 0; probe < cap; ++probe) {
-      uint64_t prev = ld_relaxed(tkeys + h);
+      uint64_t prev = ld_relaxed(&tsl[h].key);
       if (prev == k) { res = (int64_t)h; break; }
       if (prev == kEmptyKey) {
         if (!insert) break;
-        uint64_t old = atomicCAS((unsigned long long*)(tkeys + h),
+        uint64_t old = atomicCAS((unsigned long long*)(&tsl[h].key),
                                  (unsigned long long)kEmptyKey, (unsigned long long)k);
         if (old == kEmptyKey) { res = (int64_t)h; created = true; break; }
         if (old == k) { res = (int64_t)h; break; }
@@ -54,10 +54,10 @@ __global__ __launch_bounds__(kThreads) void k_kv_find(const uint64_t* keys_in, i
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_kv_occupied(const uint64_t* tkeys, int64_t cap,
+__global__ __launch_bounds__(kThreads) void k_kv_occupied(const KVSlot* tsl, int64_t cap,
                                                           int32_t* out, int64_t* out_n) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  const bool occ = i < cap && tkeys[i] != kEmptyKey;
+  const bool occ = i < cap && tsl[i].key != kEmptyKey;
   const uint64_t b = __ballot(occ);
   const int lane = threadIdx.x & 63;
   int64_t base = 0;
@@ -82,12 +82,12 @@ __device__ __forceinline__ void count_nnz_delta(float oldw, float neww, int64_t*
   if ((threadIdx.x & 63) == 0 && s) atomicAdd((unsigned long long*)(stats + 0), (unsigned long long)s);
 }
 
-__global__ __launch_bounds__(kThreads) void k_linear_pull(const float* w, const int32_t* slot,
+__global__ __launch_bounds__(kThreads) void k_linear_pull(const KVSlot* tsl, const int32_t* slot,
                                                           int64_t n, float* out) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i < n) {
     const int32_t s = slot[i];
-    out[i] = s >= 0 ? w[s] : 0.f;
+    out[i] = s >= 0 ? tsl[s].w : 0.f;
   }
 }
 
@@ -100,24 +100,24 @@ __global__ __launch_bounds__(kThreads) void k_linear_push(KVTable t, const int32
     const int32_t s = slot[i];
     if (s >= 0) {
       const float g = grad[i];
-      oldw = t.w[s];
+      oldw = t.sl[s].w;
       if (hp.algo == 1) {  // SGD, eta = (beta + sqrt(t)) / alpha
         neww = l1l2_solve(hp.sgd_eta * oldw - g, hp.sgd_eta, hp.l1, hp.l2);
       } else if (hp.algo == 2) {  // AdaGrad
-        const float sq = sqrtf(t.sq[s] * t.sq[s] + g * g);
-        t.sq[s] = sq;
+        const float sq = sqrtf(t.sl[s].sq * t.sl[s].sq + g * g);
+        t.sl[s].sq = sq;
         const float eta = (sq + hp.beta) / hp.alpha;
         neww = l1l2_solve(eta * oldw - g, eta, hp.l1, hp.l2);
       } else {  // FTRL
-        const float sq0 = t.sq[s];
+        const float sq0 = t.sl[s].sq;
         const float sq = sqrtf(sq0 * sq0 + g * g);
-        t.sq[s] = sq;
+        t.sl[s].sq = sq;
         const float sigma = (sq - sq0) / hp.alpha;
-        const float z = t.z[s] + g - sigma * oldw;
-        t.z[s] = z;
+        const float z = t.sl[s].z + g - sigma * oldw;
+        t.sl[s].z = z;
         neww = l1l2_solve(-z, (hp.beta + sq) / hp.alpha, hp.l1, hp.l2);
       }
-      t.w[s] = neww;
+      t.sl[s].w = neww;
     }
   }
   count_nnz_delta(oldw, neww, t.stats);
@@ -152,7 +152,7 @@ __device__ __forceinline__ int32_t wave_alloc_rows(const KVTable& t, bool want) 
 
 __device__ __forceinline__ void init_v_row(const KVTable& t, int32_t s, int32_t row, int gl, int G,
                                            const DifactoHP& hp) {
-  const uint64_t key = t.keys[s];
+  const uint64_t key = t.sl[s].key;
   float* V = t.V + (int64_t)row * t.vstride;
   float* VG = t.VG + (int64_t)row * t.vstride;
   for (int c = gl * 4; c < t.vstride; c += 4 * G) {
@@ -179,15 +179,15 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const 
   if (i < n) {
     s = slot[i];
     if (s >= 0) {
-      const uint32_t c = t.cnt[s] + (uint32_t)cnt[i];
-      t.cnt[s] = c;
-      want = t.vstride > 0 && c > hp.threshold && t.vrow[s] < 0 &&
-             (!hp.l1_shrk || t.w[s] != 0.f);
+      const uint32_t c = t.sl[s].cnt + (uint32_t)cnt[i];
+      t.sl[s].cnt = c;
+      want = t.vstride > 0 && c > hp.threshold && t.sl[s].vrow < 0 &&
+             (!hp.l1_shrk || t.sl[s].w != 0.f);
     }
   }
   if (t.vstride == 0) return;
   const int32_t row = wave_alloc_rows(t, want);
-  if (row >= 0) t.vrow[s] = row;
+  if (row >= 0) t.sl[s].vrow = row;
   long long newv = row >= 0 ? t.dim : 0;
   for_each_row_job<G>(row >= 0, [&](int src, int gl) {
     const int sl = src >= 0 ? src : lane;
@@ -207,8 +207,8 @@ __global__ __launch_bounds__(kThreads) void k_difacto_pull_hdr(KVTable t, const 
   float w = 0.f;
   int32_t row = -1;
   if (s >= 0) {
-    w = t.w[s];
-    row = t.vstride > 0 ? t.vrow[s] : -1;
+    w = t.sl[s].w;
+    row = t.vstride > 0 ? t.sl[s].vrow : -1;
     if (l1_shrk && w == 0.f) row = -1;
   }
   hdr[i] = make_float2(w, __int_as_float(-1));
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_pull_rows(KVTable t, const
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   int32_t row = -1, vp = -1;
   if (i < n && vflag[i]) {
-    row = t.vrow[slot[i]];
+    row = t.sl[slot[i]].vrow;
     vp = (int32_t)vpos[i];
     hdr[i].y = __int_as_float(vp);
   }
@@ -270,13 +270,13 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int3
     if (s >= 0) {
       if (t.vstride > 0) gvid = __float_as_int(hdr[i].y);
       // FTRL on w (reference UpdateW, learn/difacto/async_sgd.h:262-286)
-      const float w = t.w[s];
+      const float w = t.sl[s].w;
       const float g = gw[i] + hp.l2 * w;
-      const float cg = t.sq[s];
+      const float cg = t.sl[s].sq;
       const float cg_new = sqrtf(cg * cg + g * g);
-      t.sq[s] = cg_new;
-      const float z = t.z[s] - (g - (cg_new - cg) / hp.alpha * w);
-      t.z[s] = z;
+      t.sl[s].sq = cg_new;
+      const float z = t.sl[s].z - (g - (cg_new - cg) / hp.alpha * w);
+      t.sl[s].z = z;
       float nw;
       if (z <= hp.l1 && z >= -hp.l1) {
         nw = 0.f;
@@ -284,12 +284,12 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int3
         const float eta = (hp.beta + cg_new) / hp.alpha;
         nw = (z > 0 ? z - hp.l1 : z + hp.l1) / eta;
       }
-      t.w[s] = nw;
+      t.sl[s].w = nw;
       oldw = w;
       neww = nw;
       if (t.vstride > 0) {
-        row = t.vrow[s];
-        if (w == 0.f && nw != 0.f) want = t.cnt[s] > hp.threshold && row < 0;
+        row = t.sl[s].vrow;
+        if (w == 0.f && nw != 0.f) want = t.sl[s].cnt > hp.threshold && row < 0;
       }
     }
   }
@@ -299,7 +299,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int3
   const int32_t nrow = wave_alloc_rows(t, want);
   int kind = 0;
   if (nrow >= 0) {
-    t.vrow[s] = nrow;
+    t.sl[s].vrow = nrow;
     row = nrow;
     kind = 1;
   } else if (gvid >= 0 && row >= 0) {
@@ -369,17 +369,17 @@ void kv_find(const KVTable& t, const uint64_t* keys, int64_t n, int insert, int3
              hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(k_kv_find, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, keys, n,
-                     t.keys, t.cap, insert, slot, t.stats);
+                     t.sl, t.cap, insert, slot, t.stats);
 }
 
 void kv_occupied(const KVTable& t, int32_t* out_slots, int64_t* out_n, hipStream_t s) {
   hipLaunchKernelGGL(k_kv_occupied, dim3(grid_for(t.cap, kThreads)), dim3(kThreads), 0, s,
-                     t.keys, t.cap, out_slots, out_n);
+                     t.sl, t.cap, out_slots, out_n);
 }
 
 void linear_pull(const KVTable& t, const int32_t* slot, int64_t n, float* out, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_linear_pull, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t.w,
+  hipLaunchKernelGGL(k_linear_pull, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t.sl,
                      slot, n, out);
 }
 

@@ -1,8 +1,12 @@
 // Per-minibatch evaluation metrics (reference learn/base/binary_class_evaluation.h).
 // Loss / objective / accuracy sums are fused into the forward kernel (fm.hip);
 // this file holds the exact AUC rank-sum over predictions sorted ascending.
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "wh_common.h"
 #include "wh_kernels.h"
+
+#include <algorithm>
 
 namespace wh {
 namespace {
@@ -39,6 +43,22 @@ __global__ void k_auc_final(const int64_t* excl, int64_t n, double* out) {
 }
 
 }  // namespace
+
+size_t auc_sort_tmp_bytes(int64_t n) {
+  size_t bytes = 0;
+  WH_HIP_CHECK(rocprim::radix_sort_pairs(nullptr, bytes, (float*)nullptr, (float*)nullptr,
+                                         (float*)nullptr, (float*)nullptr,
+                                         (size_t)std::max<int64_t>(n, 1), 0, 32, (hipStream_t)0));
+  return bytes;
+}
+
+void sort_by_score(const float* py, const float* label, int64_t n, float* py_sorted,
+                   float* label_sorted, void* tmp, size_t tmp_bytes, hipStream_t s) {
+  if (n <= 0) return;
+  size_t bytes = tmp_bytes;
+  WH_HIP_CHECK(rocprim::radix_sort_pairs(tmp, bytes, py, py_sorted, label, label_sorted,
+                                         (size_t)n, 0, 32, s));
+}
 
 void auc_from_sorted(const float* label_sorted, int64_t n, double* out, int64_t* tmp_i64,
                      hipStream_t s) {

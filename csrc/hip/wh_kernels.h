@@ -47,13 +47,21 @@ void loc_csc(const int32_t* slot_of, const int32_t* tlid, const int32_t* row_of,
 // ---------------------------------------------------------- kvstore.hip
 // Sharded parameter store (replaces the ps-lite server KVStore). Open
 // addressing, linear probing, 64-bit CAS insert.
+// Array-of-structs slots: every scalar of a key (its id, w, FTRL/AdaGrad
+// state, count, embedding row) sits in ONE 32-byte sector, so find, pull and
+// push each cost one random HBM sector per key instead of one per field.
+struct alignas(32) KVSlot {
+  uint64_t key;    // ~0 == empty
+  float w;
+  float z;         // FTRL z (linear sign convention per app)
+  float sq;        // sqrt of cumulative squared gradient
+  uint32_t cnt;    // feature count (difacto)
+  int32_t vrow;    // row into the V slab, -1 = no embedding
+  float pad;
+};
+static_assert(sizeof(KVSlot) == 32, "KVSlot must be one 32-byte sector");
 struct KVTable {
-  uint64_t* keys;     // [cap] ~0 == empty
-  float* w;           // [cap]
-  float* z;           // [cap]  FTRL z (linear sign convention per app)
-  float* sq;          // [cap]  sqrt of cumulative squared gradient
-  uint32_t* cnt;      // [cap]  feature count (difacto)
-  int32_t* vrow;      // [cap]  row into V slab, -1 = no embedding
+  KVSlot* sl;         // [cap]
   float* V;           // [vcap * vstride]
   float* VG;          // [vcap * vstride] AdaGrad accumulators of V
   int32_t* vnext;     // [1] bump allocator for V rows
@@ -151,6 +159,10 @@ void spmv_t(int64_t ncol, const int64_t* csc_off, const int32_t* csc_row, const 
 // ------------------------------------------------------------ metrics.hip
 // exact per-minibatch AUC (reference BinClassEval::AUC) from predictions
 // sorted ascending: area = sum over negatives of #positives ranked below.
+// (py, label) pairs sorted ascending by py (rocPRIM radix sort, float keys)
+size_t auc_sort_tmp_bytes(int64_t n);
+void sort_by_score(const float* py, const float* label, int64_t n, float* py_sorted,
+                   float* label_sorted, void* tmp, size_t tmp_bytes, hipStream_t s);
 void auc_from_sorted(const float* label_sorted, int64_t n, double* out, int64_t* tmp_i64,
                      hipStream_t s);
 
