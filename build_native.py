@@ -8,6 +8,8 @@ Two shared objects are produced next to the Python sources:
   kernel file builds in seconds) plus the torch/pybind11 binding layer
   (``csrc/bind/*.cc``, host-only g++ compile that validates tensors and
   launches on the current HIP stream).
+* ``bin/native/{convert,text2crb}`` -- standalone C++ data conversion tools
+  (reference learn/tool/), wrapped by ``bin/convert.dmlc`` / ``bin/text2crb.dmlc``.
 * ``wormhole_amd/_host.so`` -- the native C++ runtime (``csrc/host/*.cc``):
   proto-text config parser, data parsers (libsvm / criteo / adfea / crb),
   CityHash64, LZ4 block codec, RecordIO, workload pool, control-plane
@@ -81,6 +83,14 @@ def gen_ninja():
         "rule link_host",
         "  command = $cxx -shared -fPIC -pthread $in -o $out %s" % tlibs,
         "  description = LINK $out",
+        "rule tool",
+        "  command = $cxx -O3 -std=c++17 -Wall -Wno-sign-compare -pthread -I%s/csrc -MD -MF $out.d -c $in -o $out" % ROOT,
+        "  depfile = $out.d",
+        "  deps = gcc",
+        "  description = CXX(tool) $in",
+        "rule link_tool",
+        "  command = $cxx -pthread $in -o $out",
+        "  description = LINK $out",
     ]
     hip_objs = []
     for src in sorted(glob.glob(os.path.join(ROOT, "csrc/hip/*.hip"))):
@@ -96,6 +106,20 @@ def gen_ninja():
         obj = os.path.join(BUILD, "host", os.path.basename(src) + ".o")
         lines.append("build %s: host %s" % (obj, src))
         host_objs.append(obj)
+    # standalone native tools (no torch): bin/native/{convert,text2crb}
+    core = []
+    for name in ("parsers", "io", "lz4", "cityhash"):
+        obj = os.path.join(BUILD, "tool", name + ".o")
+        lines.append("build %s: tool %s" % (obj, os.path.join(ROOT, "csrc/host/%s.cc" % name)))
+        core.append(obj)
+    lib = os.path.join(BUILD, "tool", "convert_lib.o")
+    lines.append("build %s: tool %s" % (lib, os.path.join(ROOT, "csrc/tools/convert_lib.cc")))
+    core.append(lib)
+    for tool in ("convert", "text2crb"):
+        obj = os.path.join(BUILD, "tool", tool + ".o")
+        lines.append("build %s: tool %s" % (obj, os.path.join(ROOT, "csrc/tools/%s.cc" % tool)))
+        lines.append("build %s: link_tool %s %s" % (os.path.join(ROOT, "bin", "native", tool), obj,
+                                                    " ".join(core)))
     lines.append("build %s: link_hip %s" % (os.path.join(PKG, "_hip.so"), " ".join(hip_objs)))
     lines.append("build %s: link_host %s" % (os.path.join(PKG, "_host.so"), " ".join(host_objs)))
     os.makedirs(BUILD, exist_ok=True)
