@@ -21,36 +21,19 @@ times (ranks resume from their last checkpoint).
 import argparse
 import os
 import signal
-import socket
 import subprocess
 import sys
 import time
 
-
-def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from tracker_common import job_env, normalize_cmd  # noqa: E402
 
 
 def launch_once(args, cmd, attempt):
     n, s = args.num_workers, args.num_servers
     base = dict(os.environ)
-    base.update({
-        "DMLC_NUM_WORKER": str(n),
-        "DMLC_NUM_SERVER": str(s),
-        "DMLC_PS_ROOT_URI": "127.0.0.1",
-        "DMLC_PS_ROOT_PORT": str(free_port()),
-        "DMLC_TRACKER_URI": "127.0.0.1",
-        "MASTER_ADDR": "127.0.0.1",
-        "MASTER_PORT": str(free_port()),
-        "WORLD_SIZE": str(n),
-        "LOCAL_WORLD_SIZE": str(n),
-        "WH_RESTART_ATTEMPT": str(attempt),
-    })
-    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    base.update(job_env(n, s, "127.0.0.1", attempt=attempt))
+    base["LOCAL_WORLD_SIZE"] = str(n)
     procs = []
 
     def spawn(role, rank):
@@ -115,9 +98,7 @@ def main(argv=None):
     args = ap.parse_args(argv)
     if not args.command:
         ap.error("missing the binary to run")
-    cmd = list(args.command)
-    if cmd[0].endswith(".dmlc") or cmd[0].endswith(".py"):
-        cmd = [sys.executable] + cmd
+    cmd = normalize_cmd(args.command)
     attempt = 0
     while True:
         rc = launch_once(args, cmd, attempt)

@@ -16,8 +16,22 @@ import torch
 import torch.distributed as dist
 
 
+# rank / local rank as set by the launchers (tracker/dmlc_*.py): torchrun and
+# dmlc_local/ssh set RANK / LOCAL_RANK; under dmlc_mpi the MPI launcher's own
+# variables name the rank; under dmlc_sge the (1-based) array task id does.
+_RANK_VARS = ("RANK", "DMLC_TASK_ID", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "PMIX_RANK",
+              "SLURM_PROCID")
+_LOCAL_VARS = ("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID",
+               "SLURM_LOCALID")
+
+
 def env_rank():
-    return int(os.environ.get("RANK", os.environ.get("DMLC_TASK_ID", "0")))
+    for v in _RANK_VARS:
+        if v in os.environ:
+            return int(os.environ[v])
+    if "SGE_TASK_ID" in os.environ and os.environ["SGE_TASK_ID"].isdigit():
+        return int(os.environ["SGE_TASK_ID"]) - 1
+    return 0
 
 
 def env_world():
@@ -25,7 +39,10 @@ def env_world():
 
 
 def env_local_rank():
-    return int(os.environ.get("LOCAL_RANK", "0"))
+    for v in _LOCAL_VARS:
+        if v in os.environ:
+            return int(os.environ[v])
+    return 0
 
 
 class Comm:
