@@ -149,3 +149,13 @@ def test_killed_worker_fails_the_job(work):
             env_extra={"WH_FAULT": "kill:1:3"}, timeout=120)
     assert r.returncode != 0
     assert "WH_FAULT" in r.stderr
+
+
+def test_linear_local_data(work):
+    """local_data: the workers match the files themselves (reference
+    DataParWorker local matching) and the job still covers the data."""
+    r = run(["-n", "2", "-s", "1", os.path.join(ROOT, "bin", "linear.dmlc"),
+             "learn/linear/guide/demo.conf", "local_data=true", "max_data_pass=1"], work)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rows = [l for l in r.stdout.splitlines() if re.match(r"^\s+\d+\s+\S+\s+\S+\s+", l)]
+    assert any("6.51e+03" in l for l in rows), r.stdout

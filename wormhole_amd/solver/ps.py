@@ -192,14 +192,22 @@ class Scheduler:
                 print("Validating: iter = %d" % it, flush=True)
                 if not data:
                     return False
-        files = self.host.match_file(data)
-        if not files:
-            raise RuntimeError("no file matches '%s'" % data)
-        if c.num_parts_per_file * len(files) < self.nw:
-            _log("[scheduler] #parts (%d) < #workers (%d): some workers idle; increase "
-                 "num_parts_per_file" % (c.num_parts_per_file * len(files), self.nw))
         self.pool = self.host.WorkloadPool(shuffle=train, seed=it + 1)
-        self.pool.add(files, int(c.num_parts_per_file))
+        if c.local_data:
+            # every worker matches the pattern on its own file system and its
+            # parts are preferably handed to it (reference StartDispatch with
+            # use_worker_local_data_, data_parallel.h:96-101 + node affinity)
+            nfiles = self.match_on_workers(data)
+            if nfiles == 0:
+                raise RuntimeError("no worker has a file matching '%s'" % data)
+        else:
+            files = self.host.match_file(data)
+            if not files:
+                raise RuntimeError("no file matches '%s'" % data)
+            if c.num_parts_per_file * len(files) < self.nw:
+                _log("[scheduler] #parts (%d) < #workers (%d): some workers idle; increase "
+                     "num_parts_per_file" % (c.num_parts_per_file * len(files), self.nw))
+            self.pool.add(files, int(c.num_parts_per_file))
         prog_printer = self.progress_cls()
         print("  sec %s" % prog_printer.head(), flush=True)
         self.broadcast(cmd="iterate", type=wtype, data_pass=it, fmt=c.data_format)
@@ -242,6 +250,22 @@ class Scheduler:
             s = self.show(prog_printer, agg, train)
             stop = stop or s
         return stop
+
+    def match_on_workers(self, pattern):
+        self.broadcast(cmd="match", data=pattern)
+        got, nfiles = 0, 0
+        while got < len(self.workers):
+            who, d = self._recv()
+            if d is None:
+                continue
+            if d["msg"] == "__closed__":
+                self._on_dead(who)
+            elif d["msg"] == "matched":
+                got += 1
+                if d["files"]:
+                    nfiles += len(d["files"])
+                    self.pool.add(d["files"], int(self.conf.num_parts_per_file), who)
+        return nfiles
 
     def show(self, printer, agg, train):
         line = printer.line(agg)
@@ -306,6 +330,8 @@ class Worker:
                     fn(self.learner.store, name)
                 self.comm.barrier()
                 self.send(msg="ack")
+            elif cmd == "match":
+                self.send(msg="matched", files=self.host.match_file(d["data"]))
             elif cmd == "iterate":
                 self.run_pass(d["type"], d["data_pass"], d.get("fmt", self.conf.data_format))
 
