@@ -68,7 +68,9 @@ def main(argv):
         elif k == "test:data":
             test_data = v
         elif k.startswith("eval[") and k.endswith("]"):
-            evals.append((k[5:-1], v))
+            # a later setting of the same eval set (command line after the
+            # conf) replaces the earlier one, like any other parameter
+            evals = [(n, p) for n, p in evals if n != k[5:-1]] + [(k[5:-1], v)]
         elif k == "model_in":
             model_in = None if v == "NULL" else v
         elif k == "model_out":
