@@ -360,14 +360,19 @@ std::vector<Tensor> fm_backward(const Tensor& csc_off, const Tensor& csc_row,
   const int64_t cap = wh::fm_bwd_chunks_bound(U, nnz);
   auto chunk_key = torch::empty({cap}, i32);
   auto chunk_beg = torch::empty({cap}, i32);
+  const int64_t nrows = dual.numel();
+  const int64_t mb = vstride > 0 ? wh::fm_bwd_meta_bound(U, nnz) : 1;
+  auto meta_v = torch::empty({2 * 4 * mb}, i32);
+  auto bucket_hist = torch::empty({wh::fm_bwd_bucket_scratch()}, i32);
   auto chunk_cnt = torch::empty({std::max<int64_t>(2 * U, 1)}, i64);
   auto chunk_off = torch::empty({2 * (U + 1)}, i64);
   auto stmp = torch::empty({wh::scan_tmp_elems(U)}, i64);
-  wh::fm_backward(U, nnz, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row), optptr<float>(csc_val),
-                  ptr<float>(dual), vstride > 0 ? optptr<float>(xv) : nullptr,
-                  ptr<float>(w_or_hdr), vcp, (int)vstride, ptr<float>(gw),
-                  gvc.numel() ? ptr<float>(gvc) : nullptr, ptr<int32_t>(chunk_key),
-                  ptr<int32_t>(chunk_beg), ptr<int64_t>(chunk_cnt), ptr<int64_t>(chunk_off),
+  wh::fm_backward(U, nnz, nrows, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row),
+                  optptr<float>(csc_val), ptr<float>(dual),
+                  vstride > 0 ? optptr<float>(xv) : nullptr, ptr<float>(w_or_hdr), vcp,
+                  (int)vstride, ptr<float>(gw), gvc.numel() ? ptr<float>(gvc) : nullptr,
+                  ptr<int32_t>(chunk_key), ptr<int32_t>(chunk_beg), ptr<int32_t>(meta_v),
+                  ptr<int32_t>(bucket_hist), ptr<int64_t>(chunk_cnt), ptr<int64_t>(chunk_off),
                   ptr<int64_t>(stmp), s);
   return {gw, gvc};
 }

@@ -86,7 +86,26 @@ struct Shape {
   static constexpr int SUB = 64 / G;             // rows per wave-instruction
   static constexpr int NI = G;                   // instructions per 64 items
   static constexpr int TI = G < 16 ? G : 16;     // instructions in flight
+  static constexpr int VS = 4 * G;               // row stride in floats (= vstride)
 };
+
+// A gather slot without a row reads this zero row instead of branching
+// around the load (a predicated load costs an exec-mask branch per gather).
+__device__ float kZeroRow[256];
+
+// Per-wave LDS staging of the 64 (row index, scalar) pairs of a pass, stored
+// transposed ([sub][t]) so that lane (sub, gl) reads the pairs of its
+// instructions t = 0.. as consecutive 8-byte entries (ds_read_b128 pairs,
+// broadcast across the G lanes of the sub-group) instead of two ds_bpermute
+// per gathered row.
+template <int G>
+__device__ __forceinline__ void stage_pairs(int2* st, int lane, int idx_val, float f) {
+  using S = Shape<G>;
+  st[(lane % S::SUB) * S::NI + lane / S::SUB] = make_int2(idx_val, __float_as_int(f));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_t* __restrict__ off,
@@ -98,30 +117,42 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
                                                      float* __restrict__ py_out,
                                                      float* __restrict__ dual_out,
                                                      float* __restrict__ xv, double* part) {
+  // Persistent waves, one example (row) at a time, software-pipelined over
+  // the wave's rows so each row exposes ~one memory round trip instead of
+  // four: while row i's embedding rows are gathered, the headers of row i+1,
+  // the ids of row i+2 and the CSR bounds of row i+3 are in flight. The
+  // gathers are issued first and the prefetches after them, so the in-order
+  // vmcnt wait before the accumulation covers the gathers only.
   using S = Shape<G>;
   __shared__ double sh[kThreads / 64];
+  __shared__ int2 stage[kThreads / 64][64];
   const int lane = threadIdx.x & 63, gl = lane & (G - 1), sub = lane / G;
-  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
+  const int64_t nw = (int64_t)gridDim.x * (kThreads / 64);
+  const int64_t w0 =
+      __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6));
   double m_objv = 0, m_objw = 0, m_corr = 0, m_n = 0;
-  // persistent: wave w handles rows w, w + nwaves, ...
-  for (int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6; row < nrows;
-       row += nwaves) {
-  const bool live = true;
-  float wl = 0.f;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q2 = s;
-  int64_t b = 0, e = 0;
-  if (live) {
-    b = off[row];
-    e = off[row + 1];
-  }
-  for (int64_t pb = b; pb < e; pb += 64) {  // wave-uniform: one row per wave
-    const int n = (int)(e - pb < 64 ? e - pb : 64);
-    const bool ok = lane < n;
-    const int l = ok ? lid[pb + lane] : -1;
-    const float x = ok ? (val ? val[pb + lane] : 1.f) : 0.f;
-    const float2 h = l >= 0 ? hdr[l] : make_float2(0.f, __int_as_float(-1));
-    wl += x * h.x;
-    const int vid = __float_as_int(h.y);
+  auto bounds = [&](int64_t r, int64_t& b, int64_t& e) {
+    if (r < nrows) {
+      b = off[r];
+      e = off[r + 1];
+    } else {
+      b = e = 0;
+    }
+  };
+  auto load_ids = [&](int64_t b, int64_t e, int& l, float& x) {
+    const bool ok = b + lane < e;
+    l = ok ? lid[b + lane] : -1;
+    x = ok ? (val ? val[b + lane] : 1.f) : 0.f;
+  };
+  auto load_hdr = [&](int l) {
+    return l >= 0 ? hdr[l] : make_float2(0.f, __int_as_float(-1));
+  };
+  // gather the embedding rows of one 64-id pass and accumulate them
+  int2* st = stage[threadIdx.x >> 6];
+  // gather the embedding rows of one 64-id pass and accumulate them
+  auto gather = [&](int n, int vid, float x, float4& s, float4& q2, bool prefetch_first,
+                    auto&& prefetch) {
+    stage_pairs<G>(st, lane, vid, x);
 #pragma unroll
     for (int t0 = 0; t0 < S::NI; t0 += S::TI) {
       if (t0 * S::SUB >= n) break;
@@ -129,13 +160,12 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
       float xs[S::TI];
 #pragma unroll
       for (int t = 0; t < S::TI; ++t) {
-        const int idx = (t0 + t) * S::SUB + sub;
-        const int vu = __shfl(vid, idx, 64);
-        const float xu = __shfl(x, idx, 64);
-        xs[t] = vu >= 0 ? xu : 0.f;
-        v[t] = vu >= 0 ? reinterpret_cast<const float4*>(vc + (int64_t)vu * vstride)[gl]
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int2 e = st[sub * S::NI + t0 + t];
+        xs[t] = __int_as_float(e.y);
+        const float* src = e.x >= 0 ? vc + (uint32_t)e.x * (uint32_t)S::VS : kZeroRow;
+        v[t] = reinterpret_cast<const float4*>(src)[gl];
       }
+      if (t0 == 0 && prefetch_first) prefetch();
 #pragma unroll
       for (int t = 0; t < S::TI; ++t) {
         const float xu = xs[t], xx = xu * xu;
@@ -144,34 +174,68 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
         q2.z += xx * v[t].z * v[t].z; q2.w += xx * v[t].w * v[t].w;
       }
     }
-  }
-  // sum the SUB partial rows: lanes gl, gl+G, gl+2G, ... hold the same dims
+  };
+  int64_t r = w0;
+  int64_t bc, ec, bn, en, b2, e2, b3 = 0, e3 = 0;
+  bounds(r, bc, ec);
+  bounds(r + nw, bn, en);
+  bounds(r + 2 * nw, b2, e2);
+  int lc, ln, l2 = -1;
+  float xc, xn, x2 = 0.f;
+  load_ids(bc, ec, lc, xc);
+  float2 hc = load_hdr(lc), hn = make_float2(0.f, 0.f);
+  load_ids(bn, en, ln, xn);
+  for (; r < nrows; r += nw) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f), q2 = s;
+    float wl = xc * hc.x;
+    const int nc = (int)(ec - bc < 64 ? ec - bc : 64);
+    bool fetched = false;
+    auto prefetch = [&]() {
+      hn = load_hdr(ln);
+      load_ids(b2, e2, l2, x2);
+      bounds(r + 3 * nw, b3, e3);
+      fetched = true;
+    };
+    gather(nc, __float_as_int(hc.y), xc, s, q2, true, prefetch);
+    if (!fetched) prefetch();  // empty row
+    for (int64_t pb = bc + 64; pb < ec; pb += 64) {  // rest of a long row, unpipelined
+      const int n = (int)(ec - pb < 64 ? ec - pb : 64);
+      int l;
+      float x;
+      load_ids(pb, ec, l, x);
+      const float2 h = load_hdr(l);
+      wl += x * h.x;
+      gather(n, __float_as_int(h.y), x, s, q2, false, prefetch);
+    }
+    // sum the SUB partial rows: lanes gl, gl+G, gl+2G, ... hold the same dims
 #pragma unroll
-  for (int o = G; o < 64; o <<= 1) {
-    s.x += __shfl_xor(s.x, o, 64); s.y += __shfl_xor(s.y, o, 64);
-    s.z += __shfl_xor(s.z, o, 64); s.w += __shfl_xor(s.w, o, 64);
-    q2.x += __shfl_xor(q2.x, o, 64); q2.y += __shfl_xor(q2.y, o, 64);
-    q2.z += __shfl_xor(q2.z, o, 64); q2.w += __shfl_xor(q2.w, o, 64);
-  }
-  const float wsum = wave_sum(wl);
-  float part = (s.x * s.x - q2.x) + (s.y * s.y - q2.y) + (s.z * s.z - q2.z) + (s.w * s.w - q2.w);
-  part = group_sum<G>(part);
-  if (live) {
-    if (sub == 0) reinterpret_cast<float4*>(xv + row * vstride)[gl] = s;
+    for (int o = G; o < 64; o <<= 1) {
+      s.x += __shfl_xor(s.x, o, 64); s.y += __shfl_xor(s.y, o, 64);
+      s.z += __shfl_xor(s.z, o, 64); s.w += __shfl_xor(s.w, o, 64);
+      q2.x += __shfl_xor(q2.x, o, 64); q2.y += __shfl_xor(q2.y, o, 64);
+      q2.z += __shfl_xor(q2.z, o, 64); q2.w += __shfl_xor(q2.w, o, 64);
+    }
+    const float wsum = wave_sum(wl);
+    float pt = (s.x * s.x - q2.x) + (s.y * s.y - q2.y) + (s.z * s.z - q2.z) + (s.w * s.w - q2.w);
+    pt = group_sum<G>(pt);
+    if (sub == 0) reinterpret_cast<float4*>(xv + r * vstride)[gl] = s;
     if (lane == 0) {
-      const float p = wsum + 0.5f * part;
-      const float y = label[row];
+      const float p = wsum + 0.5f * pt;
+      const float y = label[r];
       const LossOut o = eval_loss(loss, y, p);
       const LossOut ow = eval_loss(loss, y, wsum);
-      py_out[row] = p;
-      dual_out[row] = o.dual;
+      py_out[r] = p;
+      dual_out[r] = o.dual;
       m_objv += o.objv;
       m_objw += ow.objv;
       m_corr += ((y > 0.f && p > 0.f) || (y <= 0.f && p <= 0.f)) ? 1.0 : 0.0;
       m_n += 1.0;
     }
+    // rotate the pipeline
+    bc = bn; ec = en; xc = xn; hc = hn;
+    bn = b2; en = e2; ln = l2; xn = x2;
+    b2 = b3; e2 = e3;
   }
-  }  // rows
   block_partials(part, sh, m_objv, m_objw, m_corr, m_n);
 }
 
@@ -245,18 +309,20 @@ __global__ __launch_bounds__(kThreads) void k_chunk_count(int64_t nuniq,
 // writes both chunk tables; zeroes the gradients of multi-chunk keys. Lane
 // per key for single-chunk keys; a multi-chunk (hot) key is expanded by the
 // whole wave, 64 chunks per round, so the hottest key does not serialise.
+// V chunks get one packed int4 {key, csc begin, n | multi << 8, vidx} each,
+// so the backward wave fetches a chunk's description in one load.
 __global__ __launch_bounds__(kThreads) void k_chunk_fill(int64_t nuniq,
                                                          const int64_t* __restrict__ csc_off,
                                                          const int64_t* __restrict__ off_s,
                                                          const int64_t* __restrict__ off_v,
                                                          const float2* __restrict__ hdr,
                                                          int vstride, int32_t* key_s,
-                                                         int32_t* beg_s, int32_t* key_v,
-                                                         int32_t* beg_v, float* gw, float* gvc) {
+                                                         int32_t* beg_s, int4* meta_v, float* gw,
+                                                         float* gvc) {
   const int lane = threadIdx.x & 63;
   const int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   int64_t c0 = 0, nc = 0;
-  int32_t b0 = 0;
+  int32_t b0 = 0, cnt = 0, vid = -1;
   int isv = 0;
   if (k < nuniq) {
     const int64_t ns = off_s[k + 1] - off_s[k];
@@ -264,9 +330,15 @@ __global__ __launch_bounds__(kThreads) void k_chunk_fill(int64_t nuniq,
     c0 = isv ? off_v[k] : off_s[k];
     nc = isv ? off_v[k + 1] - c0 : ns;
     b0 = (int32_t)csc_off[k];
+    cnt = (int32_t)(csc_off[k + 1] - b0);
+    if (isv) vid = __float_as_int(hdr[k].y);
     if (nc == 1) {
-      (isv ? key_v : key_s)[c0] = (int32_t)k;
-      (isv ? beg_v : beg_s)[c0] = b0;
+      if (isv) {
+        meta_v[c0] = make_int4((int)k, b0, cnt, vid);
+      } else {
+        key_s[c0] = (int32_t)k;
+        beg_s[c0] = b0;
+      }
     }
   }
   uint64_t m = __ballot(nc > 1);
@@ -277,21 +349,103 @@ __global__ __launch_bounds__(kThreads) void k_chunk_fill(int64_t nuniq,
     const int64_t jc0 = __shfl(c0, src, 64);
     const int64_t jnc = __shfl(nc, src, 64);
     const int32_t jb0 = __shfl(b0, src, 64);
+    const int32_t jcnt = __shfl(cnt, src, 64);
+    const int32_t jvid = __shfl(vid, src, 64);
     const int jv = __shfl(isv, src, 64);
-    const int csz = jv ? kChunkV : kChunk;
-    int32_t* kk = jv ? key_v : key_s;
-    int32_t* bb = jv ? beg_v : beg_s;
     for (int64_t c = lane; c < jnc; c += 64) {
-      kk[jc0 + c] = jk;
-      bb[jc0 + c] = jb0 + (int32_t)(c * csz);
+      if (jv) {
+        const int32_t cb = (int32_t)(c * kChunkV);
+        const int32_t n = jcnt - cb < kChunkV ? jcnt - cb : kChunkV;
+        meta_v[jc0 + c] = make_int4(jk, jb0 + cb, n | (1 << 8), jvid);
+      } else {
+        key_s[jc0 + c] = jk;
+        beg_s[jc0 + c] = jb0 + (int32_t)(c * kChunk);
+      }
     }
     if (lane == 0) gw[jk] = 0.f;
     if (jv) {
-      const int vid = __float_as_int(hdr[jk].y);
       for (int d = lane * 4; d < vstride; d += 256)
-        *reinterpret_cast<float4*>(gvc + (int64_t)vid * vstride + d) =
+        *reinterpret_cast<float4*>(gvc + (int64_t)jvid * vstride + d) =
             make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  }
+}
+
+// V-chunk order: chunks bucketed by the first row they touch (256 row
+// windows of ~400 rows for a 100k minibatch), so the chunks in flight at any
+// moment cover a narrow window of rows and their xv gathers hit in L2. A
+// key-ordered list had every hot key's chunks sweep all rows concurrently:
+// 31% L2 hit rate and 248 us in rocprof, vs 144 us bucketed. A three-kernel
+// counting sort (block histograms -> bucket-major scan -> scatter); rocPRIM's
+// radix_sort_pairs picks a 10-pass merge sort at this size (124 us).
+constexpr int kBuckets = 256;
+constexpr int kBucketBlocks = 128;
+
+__device__ __forceinline__ int row_bucket(int row, int shift) {
+  const int b = row >> shift;
+  return b < kBuckets ? b : kBuckets - 1;
+}
+
+__global__ __launch_bounds__(kThreads) void k_vchunk_hist(const int64_t* __restrict__ nchunk_p,
+                                                          const int4* __restrict__ meta,
+                                                          const int32_t* __restrict__ csc_row,
+                                                          int shift, int32_t* hist) {
+  __shared__ int32_t h[kBuckets];
+  for (int i = threadIdx.x; i < kBuckets; i += kThreads) h[i] = 0;
+  __syncthreads();
+  const int64_t n = *nchunk_p;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t c0 = per * blockIdx.x, c1 = c0 + per < n ? c0 + per : n;
+  for (int64_t c = c0 + threadIdx.x; c < c1; c += kThreads)
+    atomicAdd(&h[row_bucket(csc_row[meta[c].y], shift)], 1);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kBuckets; i += kThreads) hist[blockIdx.x * kBuckets + i] = h[i];
+}
+
+// one block, thread per bucket: hist[block][bucket] -> bucket-major exclusive
+// offsets in place (reads coalesced across the bucket threads)
+__global__ __launch_bounds__(kBuckets) void k_vchunk_scan(int32_t* hist, int nblk) {
+  __shared__ int32_t tot[kBuckets];
+  const int b = threadIdx.x;
+  int32_t sum = 0;
+#pragma unroll 8
+  for (int i = 0; i < nblk; ++i) sum += hist[i * kBuckets + b];
+  tot[b] = sum;
+  __syncthreads();
+  if (b == 0) {
+    int32_t run = 0;
+    for (int i = 0; i < kBuckets; ++i) {
+      const int32_t t = tot[i];
+      tot[i] = run;
+      run += t;
+    }
+  }
+  __syncthreads();
+  int32_t run = tot[b];
+#pragma unroll 8
+  for (int i = 0; i < nblk; ++i) {
+    const int32_t t = hist[i * kBuckets + b];
+    hist[i * kBuckets + b] = run;
+    run += t;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_vchunk_scatter(const int64_t* __restrict__ nchunk_p,
+                                                             const int4* __restrict__ meta,
+                                                             const int32_t* __restrict__ csc_row,
+                                                             int shift,
+                                                             const int32_t* __restrict__ hist,
+                                                             int4* out) {
+  __shared__ int32_t base[kBuckets];
+  for (int i = threadIdx.x; i < kBuckets; i += kThreads) base[i] = hist[blockIdx.x * kBuckets + i];
+  __syncthreads();
+  const int64_t n = *nchunk_p;
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t c0 = per * blockIdx.x, c1 = c0 + per < n ? c0 + per : n;
+  for (int64_t c = c0 + threadIdx.x; c < c1; c += kThreads) {
+    const int4 m = meta[c];
+    const int pos = atomicAdd(&base[row_bucket(csc_row[m.y], shift)], 1);
+    out[pos] = m;
   }
 }
 
@@ -328,38 +482,51 @@ __global__ __launch_bounds__(kThreads) void k_bwd_scalar(const int64_t* __restri
   else gw_out[k] = gw;
 }
 
-// V chunks: one wave per chunk, persistent over the (device-counted) list
+// V chunks: one wave per chunk, persistent over the (device-counted) list,
+// software-pipelined like the forward: while chunk i's xv rows are gathered,
+// the duals of chunk i+1, the CSC rows of chunk i+2 and the description of
+// chunk i+3 are in flight.
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ nchunk_p,
-                                                    const int32_t* __restrict__ chunk_key,
-                                                    const int32_t* __restrict__ chunk_beg,
-                                                    const int64_t* __restrict__ csc_off,
+                                                    const int4* __restrict__ meta,
                                                     const int32_t* __restrict__ csc_row,
                                                     const float* __restrict__ csc_val,
                                                     const float* __restrict__ dual,
                                                     const float* __restrict__ xv,
-                                                    const float2* __restrict__ hdr,
                                                     const float* __restrict__ vc, int vstride,
                                                     float* __restrict__ gw_out,
                                                     float* __restrict__ gvc) {
   using S = Shape<G>;
+  __shared__ int2 stage[kThreads / 64][64];
+  int2* st = stage[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63, gl = lane & (G - 1), sub = lane / G;
   const int64_t nch = *nchunk_p;
-  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / 64);
-  for (int64_t c = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6; c < nch; c += nwaves) {
-    const int k = chunk_key[c];
-    const int kb = (int)csc_off[k], ke = (int)csc_off[k + 1];
-    const int b = chunk_beg[c];
-    const int n = b + kChunkV < ke ? kChunkV : ke - b;
-    const bool multi = ke - kb > kChunkV;
-    const int vid = __float_as_int(hdr[k].y);
-    const bool ok = lane < n;
-    const int r = ok ? csc_row[b + lane] : -1;
-    const float x = ok ? (csc_val ? csc_val[b + lane] : 1.f) : 0.f;
-    const float d = ok ? dual[r] * x : 0.f;
-    const float gw = wave_sum(d);
-    const float xxp = wave_sum(d * x);
+  const int64_t nw = (int64_t)gridDim.x * (kThreads / 64);
+  const int64_t w0 =
+      __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6));
+  auto get_meta = [&](int64_t c) {
+    return c < nch ? meta[c] : make_int4(0, 0, 0, -1);
+  };
+  auto load_rows = [&](const int4& mt, int& r, float& x) {
+    const bool ok = lane < (mt.z & 0xff);
+    r = ok ? csc_row[mt.y + lane] : -1;
+    x = ok ? (csc_val ? csc_val[mt.y + lane] : 1.f) : 0.f;
+  };
+  int64_t c = w0;
+  int4 mc = get_meta(c), mn = get_meta(c + nw), m2 = get_meta(c + 2 * nw),
+       m3 = make_int4(0, 0, 0, -1);
+  int rc, rn, r2 = -1;
+  float xc, xn, x2 = 0.f;
+  load_rows(mc, rc, xc);
+  float dc = rc >= 0 ? dual[rc] * xc : 0.f;
+  load_rows(mn, rn, xn);
+  float dn = 0.f;
+  for (; c < nch; c += nw) {
+    const int n = mc.z & 0xff;
+    const bool multi = (mc.z >> 8) != 0;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    stage_pairs<G>(st, lane, rc, dc);
 #pragma unroll
     for (int t0 = 0; t0 < S::NI; t0 += S::TI) {
       if (t0 * S::SUB >= n) break;
@@ -367,11 +534,17 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
       float du[S::TI];
 #pragma unroll
       for (int t = 0; t < S::TI; ++t) {
-        const int idx = (t0 + t) * S::SUB + sub;
-        const int ru = __shfl(r, idx, 64);
-        du[t] = __shfl(d, idx, 64);
-        a[t] = ru >= 0 ? reinterpret_cast<const float4*>(xv + (int64_t)ru * vstride)[gl]
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int2 e = st[sub * S::NI + t0 + t];
+        du[t] = __int_as_float(e.y);
+        const float* src = e.x >= 0 ? xv + (uint32_t)e.x * (uint32_t)S::VS : kZeroRow;
+        a[t] = reinterpret_cast<const float4*>(src)[gl];
+      }
+      if (t0 == 0) {
+        v = reinterpret_cast<const float4*>(vc + (uint32_t)mc.w * (uint32_t)S::VS)[gl];
+        // prefetch the next stages behind the gathers
+        dn = rn >= 0 ? dual[rn] * xn : 0.f;
+        load_rows(m2, r2, x2);
+        m3 = get_meta(c + 3 * nw);
       }
 #pragma unroll
       for (int t = 0; t < S::TI; ++t) {
@@ -379,19 +552,25 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
         acc.z += du[t] * a[t].z; acc.w += du[t] * a[t].w;
       }
     }
+    if (n == 0) {  // (chunks are never empty; keep the pipeline consistent anyway)
+      dn = rn >= 0 ? dual[rn] * xn : 0.f;
+      load_rows(m2, r2, x2);
+      m3 = get_meta(c + 3 * nw);
+    }
+    const float gw = wave_sum(dc);
+    const float xxp = wave_sum(dc * xc);
 #pragma unroll
     for (int o = G; o < 64; o <<= 1) {
       acc.x += __shfl_xor(acc.x, o, 64); acc.y += __shfl_xor(acc.y, o, 64);
       acc.z += __shfl_xor(acc.z, o, 64); acc.w += __shfl_xor(acc.w, o, 64);
     }
     if (lane == 0) {
-      if (multi) atomicAdd(gw_out + k, gw);
-      else gw_out[k] = gw;
+      if (multi) atomicAdd(gw_out + mc.x, gw);
+      else gw_out[mc.x] = gw;
     }
     if (sub == 0) {
-      const float4 v = reinterpret_cast<const float4*>(vc + (int64_t)vid * vstride)[gl];
       acc.x -= xxp * v.x; acc.y -= xxp * v.y; acc.z -= xxp * v.z; acc.w -= xxp * v.w;
-      float* gv = gvc + (int64_t)vid * vstride + gl * 4;
+      float* gv = gvc + (int64_t)mc.w * vstride + gl * 4;
       if (!multi) {
         *reinterpret_cast<float4*>(gv) = acc;
       } else {
@@ -399,6 +578,10 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
         atomicAdd(gv + 2, acc.z); atomicAdd(gv + 3, acc.w);
       }
     }
+    // rotate the pipeline
+    mc = mn; rc = rn; xc = xn; dc = dn;
+    mn = m2; rn = r2; xn = x2;
+    m2 = m3;
   }
 }
 
@@ -453,6 +636,29 @@ __global__ __launch_bounds__(kThreads) void k_grad_scale(const int64_t* __restri
 
 int64_t fm_fwd_partials() { return 4 * kFwdBlocks; }
 
+// Persistent grids are sized to what is actually resident: blocks per CU from
+// the occupancy API (register-limited kernels fit fewer than 8) x CU count,
+// so no block waits for a second round behind a full machine.
+template <typename K>
+static int resident_blocks(K kernel, int cap) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    WH_HIP_CHECK(hipGetDevice(&dev));
+    WH_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  int per_cu = 0;
+  WH_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0));
+  const int n = std::max(1, per_cu) * cus;
+  return n < cap ? n : cap;
+}
+
+#define WH_RESIDENT(G, KERNEL, CAP)                                              \
+  ((G) == 1 ? resident_blocks(KERNEL<1>, CAP) : (G) == 2 ? resident_blocks(KERNEL<2>, CAP) \
+   : (G) == 4 ? resident_blocks(KERNEL<4>, CAP) : (G) == 8 ? resident_blocks(KERNEL<8>, CAP) \
+   : (G) == 16 ? resident_blocks(KERNEL<16>, CAP) : (G) == 32 ? resident_blocks(KERNEL<32>, CAP) \
+   : resident_blocks(KERNEL<64>, CAP))
+
 void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
                 const float* w_or_hdr, const float* vc, int vstride, const float* label, int loss,
                 float* py, float* dual, float* xv, double* met, double* part, hipStream_t s) {
@@ -466,7 +672,7 @@ void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const 
   } else {
     const int G = vstride / 4;  // vstride <= 256 enforced by the binding
     const float2* hdr = reinterpret_cast<const float2*>(w_or_hdr);
-    nblk = grid_for(nrows * 64, kThreads, kFwdBlocks);  // wave per row, persistent
+    nblk = grid_for(nrows * 64, kThreads, WH_RESIDENT(G, k_fm_fwd, kFwdBlocks));
     const dim3 grid(nblk), block(kThreads);
     WH_DISPATCH_G(G, k_fm_fwd, grid, block, 0, s, nrows, offset, lid, val, hdr, vc, vstride,
                   label, loss, py, dual, xv, part);
@@ -481,11 +687,22 @@ int64_t fm_bwd_chunks_bound(int64_t nuniq, int64_t nnz) {
   return scalar_cap(nuniq, nnz) + v_cap(nuniq, nnz);
 }
 
-void fm_backward(int64_t nuniq, int64_t nnz, const int64_t* csc_off, const int32_t* csc_row,
-                 const float* csc_val, const float* dual, const float* xv, const float* hdr_f,
-                 const float* vc, int vstride, float* gw, float* gvc, int32_t* chunk_key,
-                 int32_t* chunk_beg, int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp,
-                 hipStream_t s) {
+int64_t fm_bwd_meta_bound(int64_t nuniq, int64_t nnz) { return v_cap(nuniq, nnz); }
+
+static int bucket_shift(int64_t nrows) {
+  int shift = 0;
+  while ((((nrows - 1) >> shift) >= kBuckets)) ++shift;
+  return shift;
+}
+
+int64_t fm_bwd_bucket_scratch() { return (int64_t)kBuckets * kBucketBlocks; }
+
+void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_off,
+                 const int32_t* csc_row, const float* csc_val, const float* dual, const float* xv,
+                 const float* hdr_f, const float* vc, int vstride, float* gw, float* gvc,
+                 int32_t* chunk_key, int32_t* chunk_beg, int32_t* meta_v_i32, int32_t* bucket_hist,
+                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, hipStream_t s) {
+  int4* meta_v = reinterpret_cast<int4*>(meta_v_i32);
   if (nuniq <= 0) return;
   const float2* hdr = vstride > 0 ? reinterpret_cast<const float2*>(hdr_f) : nullptr;
   int64_t* cnt_s = chunk_cnt;
@@ -495,25 +712,33 @@ void fm_backward(int64_t nuniq, int64_t nnz, const int64_t* csc_off, const int32
   const int64_t cap_s = scalar_cap(nuniq, nnz);
   int32_t* key_s = chunk_key;
   int32_t* beg_s = chunk_beg;
-  int32_t* key_v = chunk_key + cap_s;
-  int32_t* beg_v = chunk_beg + cap_s;
   hipLaunchKernelGGL(k_chunk_count, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
                      csc_off, hdr, cnt_s, cnt_v);
   scan_i64(cnt_s, off_s, nuniq, scan_tmp, s);
   if (hdr) scan_i64(cnt_v, off_v, nuniq, scan_tmp, s);
   hipLaunchKernelGGL(k_chunk_fill, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
-                     csc_off, off_s, off_v, hdr, vstride, key_s, beg_s, key_v, beg_v, gw, gvc);
+                     csc_off, off_s, off_v, hdr, vstride, key_s, beg_s, meta_v, gw, gvc);
   // chunk counts are device values (off[nuniq]); the scalar kernel launches
   // over the host-side bound and surplus lanes exit; the V kernel is
   // persistent. No host synchronisation in the step.
   hipLaunchKernelGGL(k_bwd_scalar, dim3(grid_for(cap_s, kThreads)), dim3(kThreads), 0, s,
                      off_s + nuniq, key_s, beg_s, csc_off, csc_row, csc_val, dual, gw);
   if (!hdr) return;
+  // order the V chunks by first-row bucket (meta_v[cap..2cap) receives the list)
+  const int64_t vcap = v_cap(nuniq, nnz);
+  int4* meta_sorted = meta_v + vcap;
+  const int shift = bucket_shift(std::max<int64_t>(nrows, 1));
+  hipLaunchKernelGGL(k_vchunk_hist, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
+                     meta_v, csc_row, shift, bucket_hist);
+  hipLaunchKernelGGL(k_vchunk_scan, dim3(1), dim3(kBuckets), 0, s, bucket_hist, kBucketBlocks);
+  hipLaunchKernelGGL(k_vchunk_scatter, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
+                     meta_v, csc_row, shift, bucket_hist, meta_sorted);
   const int G = vstride / 4;
-  const int64_t vwaves = std::min<int64_t>(v_cap(nuniq, nnz), 8192);  // <= 32 waves per CU
-  const dim3 grid((unsigned)((vwaves + 3) / 4)), block(kThreads);
-  WH_DISPATCH_G(G, k_bwd_v, grid, block, 0, s, off_v + nuniq, key_v, beg_v, csc_off, csc_row,
-                csc_val, dual, xv, hdr, vc, vstride, gw, gvc);
+  const int64_t vblk = std::min<int64_t>((v_cap(nuniq, nnz) + 3) / 4,
+                                         WH_RESIDENT(G, k_bwd_v, 2048));
+  const dim3 grid((unsigned)vblk), block(kThreads);
+  WH_DISPATCH_G(G, k_bwd_v, grid, block, 0, s, off_v + nuniq, meta_sorted, csc_row, csc_val,
+                dual, xv, vc, vstride, gw, gvc);
 }
 
 void fm_grad_post(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim, float clip,

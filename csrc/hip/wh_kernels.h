@@ -135,13 +135,16 @@ void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const 
 //   gw_k = sum_i dual_i x_ik
 //   gV_k = sum_i dual_i x_ik xv_i - (sum_i dual_i x_ik^2) V_k
 int64_t fm_bwd_chunks_bound(int64_t nuniq, int64_t nnz);
-// scratch: chunk_key/chunk_beg [fm_bwd_chunks_bound], chunk_cnt [2 nuniq],
-// chunk_off [2 (nuniq + 1)], scan_tmp [scan_tmp_elems(nuniq)]
-void fm_backward(int64_t nuniq, int64_t nnz, const int64_t* csc_off, const int32_t* csc_row,
-                 const float* csc_val, const float* dual, const float* xv, const float* hdr,
-                 const float* vc, int vstride, float* gw, float* gvc, int32_t* chunk_key,
-                 int32_t* chunk_beg, int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp,
-                 hipStream_t s);
+// scratch: chunk_key/chunk_beg [fm_bwd_chunks_bound], meta_v [2 x 4 fm_bwd_meta_bound]
+// int32 (16-byte aligned), bucket_hist [fm_bwd_bucket_scratch] int32,
+// chunk_cnt [2 nuniq], chunk_off [2 (nuniq + 1)], scan_tmp [scan_tmp_elems(nuniq)]
+int64_t fm_bwd_meta_bound(int64_t nuniq, int64_t nnz);
+int64_t fm_bwd_bucket_scratch();
+void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_off,
+                 const int32_t* csc_row, const float* csc_val, const float* dual, const float* xv,
+                 const float* hdr, const float* vc, int vstride, float* gw, float* gvc,
+                 int32_t* chunk_key, int32_t* chunk_beg, int32_t* meta_v, int32_t* bucket_hist,
+                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, hipStream_t s);
 // post-process the m (device count) V-gradient rows: clip to [-c, c] (c>0),
 // dropout with prob p (p>0); sumsq (optional) receives the squared norm
 void fm_grad_post(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim, float clip,

@@ -57,7 +57,19 @@ def load_linear(store, path):
     return len(raw)
 
 
+def _rec1():
+    return np.dtype([("k", "<u8"), ("size", "<i4"), ("w", "<f4"), ("pad", "<u4"),
+                     ("sq", "<f4"), ("z", "<f4")])
+
+
+def _recv(dim):
+    return np.dtype([("k", "<u8"), ("size", "<i4"), ("w", "<f4"), ("V", "<f4", (dim,)),
+                     ("sq", "<f4"), ("z", "<f4"), ("VG", "<f4", (dim,))])
+
+
 def save_difacto(store, path):
+    """Vectorised dump: all scalar (size 1) records, then all embedding
+    records -- a valid record stream in the reference layout."""
     slots = _occupied(store)
     keys = _arr(store.keys, slots).astype(np.uint64)
     w = _arr(store.w, slots).astype(np.float32)
@@ -65,43 +77,52 @@ def save_difacto(store, path):
     sq = _arr(store.sq, slots).astype(np.float32)
     dim = int(store.dim)
     has_v = np.zeros(len(keys), dtype=bool)
-    V = VG = None
-    if dim > 0:
-        vrow = _arr(store.vrow, slots).astype(np.int64)
-        has_v = vrow >= 0
-        if has_v.any():
-            rows = torch.from_numpy(vrow[has_v])
-            V = store.V[rows.to(store.V.device)].cpu().numpy()[:, :dim]
-            VG = store.VG[rows.to(store.VG.device)].cpu().numpy()[:, :dim]
-    out = bytearray()
-    vi = 0
-    n = 0
-    for i in range(len(keys)):
-        if not has_v[i]:
-            if w[i] == 0:
-                continue  # Empty(): w0 == 0 && size == 1
-            out += struct.pack("<Qi", int(keys[i]), 1)
-            out += struct.pack("<fIff", float(w[i]), 0, float(sq[i]), float(z[i]))
-        else:
-            size = dim + 1
-            out += struct.pack("<Qi", int(keys[i]), size)
-            out += np.concatenate([[w[i]], V[vi]]).astype("<f4").tobytes()
-            out += np.concatenate([[sq[i], z[i]], VG[vi]]).astype("<f4").tobytes()
-            vi += 1
-        n += 1
-    if dim > 0 and has_v.any():
-        assert vi == int(has_v.sum())
+    if dim > 0 and len(keys):
+        has_v = _arr(store.vrow, slots).astype(np.int64) >= 0
+    one = ~has_v & (w != 0)  # Empty(): w0 == 0 && size == 1
+    r1 = np.zeros(int(one.sum()), dtype=_rec1())
+    r1["k"], r1["size"], r1["w"], r1["sq"], r1["z"] = keys[one], 1, w[one], sq[one], z[one]
+    rv = np.zeros(int(has_v.sum()), dtype=_recv(max(dim, 1)))
+    if len(rv):
+        rows = torch.from_numpy(_arr(store.vrow, slots).astype(np.int64)[has_v])
+        rv["k"], rv["size"], rv["w"] = keys[has_v], dim + 1, w[has_v]
+        rv["sq"], rv["z"] = sq[has_v], z[has_v]
+        rv["V"] = store.V[rows.to(store.V.device)].cpu().numpy()[:, :dim]
+        rv["VG"] = store.VG[rows.to(store.VG.device)].cpu().numpy()[:, :dim]
     with open(path, "wb") as f:
-        f.write(bytes(out))
-    return n
+        f.write(r1.tobytes())
+        f.write(rv.tobytes())
+    return len(r1) + len(rv)
 
 
-def load_difacto(store, path):
-    data = open(path, "rb").read()
+def _parse_difacto(data, dim):
+    """(keys, w, z, sq, vkeys, V, VG). Fast path for files laid out as all
+    scalar records then all embedding records (what save_difacto writes);
+    interleaved files (e.g. written by the reference) take the record walk."""
+    d1, dv = _rec1(), _recv(max(dim, 1))
+    n = len(data)
+    # find the prefix of scalar records
+    n1 = 0
+    if n >= d1.itemsize:
+        cand = np.frombuffer(data[: (n // d1.itemsize) * d1.itemsize], dtype=d1)
+        bad = np.nonzero(cand["size"] != 1)[0]
+        n1 = int(bad[0]) if len(bad) else len(cand)
+    rest = n - n1 * d1.itemsize
+    if dim > 0 and rest % dv.itemsize == 0:
+        rv = np.frombuffer(data, dtype=dv, offset=n1 * d1.itemsize)
+        if bool((rv["size"] == dim + 1).all()):
+            r1 = np.frombuffer(data, dtype=d1, count=n1)
+            return (np.concatenate([r1["k"], rv["k"]]), np.concatenate([r1["w"], rv["w"]]),
+                    np.concatenate([r1["z"], rv["z"]]), np.concatenate([r1["sq"], rv["sq"]]),
+                    rv["k"], rv["V"], rv["VG"])
+    if rest == 0:
+        r1 = np.frombuffer(data, dtype=d1, count=n1)
+        e = np.zeros(0, dtype=np.float32)
+        return r1["k"], r1["w"], r1["z"], r1["sq"], np.zeros(0, np.uint64), e, e
+    # interleaved: walk the records
     pos = 0
     keys, w, z, sq, vk, vv, vg = [], [], [], [], [], [], []
-    dim = int(store.dim)
-    while pos < len(data):
+    while pos < n:
         k, size = struct.unpack_from("<Qi", data, pos)
         pos += 12
         if size == 1:
@@ -109,22 +130,36 @@ def load_difacto(store, path):
             pos += 16
             keys.append(k), w.append(w0), sq.append(s0), z.append(z0)
         else:
+            if size - 1 != dim:
+                raise ValueError("model embedding dim %d != configured dim %d" % (size - 1, dim))
             arr = np.frombuffer(data, dtype="<f4", count=size, offset=pos)
             pos += 4 * size
             acc = np.frombuffer(data, dtype="<f4", count=size + 1, offset=pos)
             pos += 4 * (size + 1)
-            if size - 1 != dim:
-                raise ValueError("model embedding dim %d != configured dim %d" % (size - 1, dim))
             keys.append(k), w.append(arr[0]), sq.append(acc[0]), z.append(acc[1])
             vk.append(k), vv.append(arr[1:]), vg.append(acc[2:])
-    kt = torch.tensor(np.array(keys, dtype=np.uint64).view(np.int64))
-    _put(store, kt, {"w": torch.tensor(w, dtype=torch.float32),
-                     "z": torch.tensor(z, dtype=torch.float32),
-                     "sq": torch.tensor(sq, dtype=torch.float32)})
-    if vk:
-        _put_v(store, torch.tensor(np.array(vk, dtype=np.uint64).view(np.int64)),
-               torch.tensor(np.stack(vv)), torch.tensor(np.stack(vg)))
-    store.stats[0] += int((torch.tensor(w) != 0).sum())
+    f32 = np.float32
+    return (np.array(keys, dtype=np.uint64), np.array(w, f32), np.array(z, f32),
+            np.array(sq, f32), np.array(vk, dtype=np.uint64),
+            np.stack(vv) if vv else np.zeros((0, dim), f32),
+            np.stack(vg) if vg else np.zeros((0, dim), f32))
+
+
+def load_difacto(store, path):
+    data = open(path, "rb").read()
+    dim = int(store.dim)
+    keys, w, z, sq, vk, V, VG = _parse_difacto(data, dim)
+    if len(vk) and V.shape[1] != dim:
+        raise ValueError("model embedding dim %d != configured dim %d" % (V.shape[1], dim))
+    kt = torch.from_numpy(np.ascontiguousarray(keys).view(np.int64).copy())
+    _put(store, kt, {"w": torch.from_numpy(np.array(w, dtype=np.float32)),
+                     "z": torch.from_numpy(np.array(z, dtype=np.float32)),
+                     "sq": torch.from_numpy(np.array(sq, dtype=np.float32))})
+    if len(vk):
+        _put_v(store, torch.from_numpy(np.ascontiguousarray(vk).view(np.int64).copy()),
+               torch.from_numpy(np.array(V, dtype=np.float32)),
+               torch.from_numpy(np.array(VG, dtype=np.float32)))
+    store.stats[0] += int((np.asarray(w) != 0).sum())
     store.stats[1] += len(vk) * dim
     return len(keys)
 
