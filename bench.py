@@ -93,12 +93,14 @@ def main():
 
     for s in range(args.warmup):
         one(s)
+    learner.flush()
     sync()
     comm.barrier()
     sync()
     t0 = time.perf_counter()
     for s in range(args.steps):
         one(args.warmup + s)
+    learner.flush()  # the last step's (deferred) push is part of the timed work
     sync()
     comm.barrier()
     sync()

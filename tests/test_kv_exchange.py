@@ -15,7 +15,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, out_dir):
+def _rank_main(rank, world, port, out_dir, defer=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     torch.set_num_threads(1)
@@ -29,6 +29,7 @@ def _rank_main(rank, world, port, out_dir):
     conf = DifactoConfig(embedding=[emb], lambda_l1=0.01, l1_shrk=False)
     card = [50, 400, 3000, 20, 7]
     lr = DifactoLearner(conf, comm, "cpu", cap=1 << 14, vcap=1 << 12, seed=5)
+    lr.defer_push = defer
     for step in range(4):
         keys, label, off = criteo_batch_cpu(300, 17 + rank, step, card)
         lr.process(keys, off, None, label, 0, 0)
@@ -66,6 +67,7 @@ def _rank_main(rank, world, port, out_dir):
     comm.finalize()
     with open(os.path.join(out_dir, "r%d" % rank), "w") as f:
         f.write("%r %d\n" % (prog[0] / prog[5], nv))
+    torch.save({k: v for k, v in sorted(mine.items())}, os.path.join(out_dir, "m%d" % rank))
 
 
 def test_difacto_sharded_pull_push_two_ranks(tmp_path):
@@ -74,3 +76,14 @@ def test_difacto_sharded_pull_push_two_ranks(tmp_path):
     for r in range(2):
         ll, nv = open(tmp_path / ("r%d" % r)).read().split()
         assert 0 < float(ll) < 1.0 and int(nv) > 0
+
+
+def test_deferred_push_is_exact(tmp_path):
+    """Overlapping a push with the next localize changes no result."""
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir(), b.mkdir()
+    mp.spawn(_rank_main, args=(2, _free_port(), str(a), True), nprocs=2, join=True)
+    mp.spawn(_rank_main, args=(2, _free_port(), str(b), False), nprocs=2, join=True)
+    for r in range(2):
+        assert open(a / ("r%d" % r)).read() == open(b / ("r%d" % r)).read()
+        assert torch.load(a / ("m%d" % r)) == torch.load(b / ("m%d" % r))

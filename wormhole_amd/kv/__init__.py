@@ -60,6 +60,15 @@ class ShardedKV:
         # keys are owned by the first `nshard` ranks (the conf's -s S servers)
         self.nshard = comm.size if nshard is None else max(1, min(int(nshard), comm.size))
         self.push_count = 0  # number of push requests applied (SGD's t)
+        self.pending = None  # a deferred push: (handle, apply)
+
+    def flush(self):
+        """Complete a deferred push (wait for its transfers, apply it)."""
+        if self.pending is not None:
+            handle, apply = self.pending
+            self.pending = None
+            handle.wait()
+            apply()
 
     def open(self, uniq, owner_cnt, insert, cnt=None):
         """Send this minibatch's unique keys to their owners (plus, for the
@@ -79,6 +88,7 @@ class ShardedKV:
                 keys, c = self.comm.all_to_all_v_multi([(uniq, send, recv), (cnt, send, recv)])
                 sess = Session(send, recv, keys)
                 sess.cnt = c
+        self.flush()  # a deferred push lands before this minibatch's lookups
         sess.slots = self.store.find(sess.keys, insert)
         return sess
 
@@ -92,13 +102,24 @@ class ShardedKV:
     def linear_pull(self, sess):
         return self._to_worker(sess, self.store.linear_pull(sess.slots))
 
-    def linear_push(self, sess, grad, algo, alpha, beta, l1, l2):
-        g = self._to_owner(sess, grad.reshape(-1).contiguous())
-        for a, b in sess.segments():
-            self.push_count += 1
-            eta = (beta + float(self.push_count) ** 0.5) / alpha
-            if b > a:
-                self.store.linear_push(sess.slots[a:b], g[a:b], algo, alpha, beta, l1, l2, eta)
+    def linear_push(self, sess, grad, algo, alpha, beta, l1, l2, defer=False):
+        self.flush()
+
+        def apply(g):
+            for a, b in sess.segments():
+                self.push_count += 1
+                eta = (beta + float(self.push_count) ** 0.5) / alpha
+                if b > a:
+                    self.store.linear_push(sess.slots[a:b], g[a:b], algo, alpha, beta, l1, l2,
+                                           eta)
+        if self.comm.size == 1:
+            apply(grad.reshape(-1))
+            return
+        (g,), handle = self.comm.all_to_all_v_multi(
+            [(grad.reshape(-1).contiguous(), sess.send, sess.recv)], async_op=True)
+        self.pending = (handle, lambda: apply(g))
+        if not defer:
+            self.flush()
 
     # --------------------------------------------------------------- difacto
     def difacto_push_cnt(self, sess, hp, threshold, l1_shrk, seed):
@@ -134,14 +155,25 @@ class ShardedKV:
         sess.m = ops.vidx_renumber(hdr_w)
         return hdr_w, vc_w
 
-    def difacto_push(self, sess, gw, gvc, hp, threshold, l1_shrk, seed):
+    def difacto_push(self, sess, gw, gvc, hp, threshold, l1_shrk, seed, defer=False):
+        """Send the gradients to their owners and apply them there.  With
+        defer=True (and more than one GPU) the transfer is only started: the
+        caller overlaps it with independent work (the next minibatch's
+        localize) and completes it with :meth:`flush` before the next pull,
+        so every pull still sees every earlier push."""
+        self.flush()
+
+        def apply(g, gv):
+            for a, b in sess.segments():
+                if b > a:
+                    self.store.difacto_push(sess.slots[a:b], sess.hdr_own[a:b], g[a:b], gv, hp,
+                                            threshold, l1_shrk, seed)
         if self.comm.size == 1:
-            g, gv = gw, gvc
-        else:
-            g, gv = self.comm.all_to_all_v_multi([
-                (gw, sess.send, sess.recv),
-                (gvc[:sum(sess.vsend)], sess.vsend, sess.vrecv)])
-        for a, b in sess.segments():
-            if b > a:
-                self.store.difacto_push(sess.slots[a:b], sess.hdr_own[a:b], g[a:b], gv, hp,
-                                        threshold, l1_shrk, seed)
+            apply(gw, gvc)
+            return
+        (g, gv), handle = self.comm.all_to_all_v_multi([
+            (gw, sess.send, sess.recv),
+            (gvc[:sum(sess.vsend)], sess.vsend, sess.vrecv)], async_op=True)
+        self.pending = (handle, lambda: apply(g, gv))
+        if not defer:
+            self.flush()

@@ -47,6 +47,9 @@ class DifactoLearner:
         self.auc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.n_mb = 0
         self.uhint = 0  # unique ids of the previous minibatch (localize table size)
+        # overlap each push's all-to-all with the next minibatch's localize
+        # (same semantics: the push is applied before the next lookup)
+        self.defer_push = True
         self.step = 0
 
     # ------------------------------------------------------------------ step
@@ -74,14 +77,20 @@ class DifactoLearner:
                                  self.emb.dropout, self.seed + 7919 * self.step + 1,
                                  bool(self.emb.grad_normalization))
             self.kv.difacto_push(sess, gw, gvc, self.hp, self.threshold, self.l1_shrk,
-                                 self.seed)
+                                 self.seed, defer=self.defer_push)
         self.step += 1
         return py if wtype == PRED else None
 
     # -------------------------------------------------------------- progress
+    def flush(self):
+        """Complete the last minibatch's deferred push (before reading the
+        model: progress counters, save, end of pass, end of a timed run)."""
+        self.kv.flush()
+
     def take_progress(self):
         """Progress vector in the reference layout (learn/difacto/progress.h):
         [objv, auc, objv_w, copc, count, new_ex, new_w, new_V]; resets."""
+        self.flush()
         m = self.met.tolist()
         a = float(self.auc_sum.item())
         st = self.store.stats

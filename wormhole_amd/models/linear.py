@@ -28,6 +28,9 @@ class LinearLearner:
         self.auc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.n_mb = 0
         self.uhint = 0  # unique ids of the previous minibatch (localize table size)
+        # overlap each push's all-to-all with the next minibatch's localize
+        # (same semantics: the push is applied before the next lookup)
+        self.defer_push = True
 
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0):
         train = wtype == TRAIN
@@ -42,12 +45,18 @@ class LinearLearner:
         if train:
             grad, _ = ops.fm_backward(csc_off, csc_row, csc_val, dual, None, w, None, 0)
             self.kv.linear_push(sess, grad, self.conf.algo, self.alpha, self.beta,
-                                self.conf.lambda_l1, self.conf.lambda_l2)
+                                self.conf.lambda_l1, self.conf.lambda_l2, defer=self.defer_push)
         return py if wtype == PRED else None
+
+    def flush(self):
+        """Complete the last minibatch's deferred push (before reading the
+        model: progress counters, save, end of pass, end of a timed run)."""
+        self.kv.flush()
 
     def take_progress(self):
         """Reference layout (learn/linear/progress.h): [objv, acc, auc, count,
         new_ex, new_w]; accuracy is the per-minibatch-mean convention."""
+        self.flush()
         m = self.met.tolist()
         a = float(self.auc_sum.item())
         st = self.store.stats

@@ -45,6 +45,24 @@ def env_local_rank():
     return 0
 
 
+class _Done:
+    def wait(self):
+        pass
+
+
+class _Reqs:
+    """Pending point-to-point group; keeps the send buffers alive."""
+
+    def __init__(self, reqs, keep):
+        self.reqs = reqs
+        self.keep = keep
+
+    def wait(self):
+        for r in self.reqs:
+            r.wait()
+        self.reqs, self.keep = [], None
+
+
 class Comm:
     """A process group handle.  ``size == 1`` needs no torch.distributed."""
 
@@ -133,13 +151,17 @@ class Comm:
                                    [s * width for s in send_rows])
         return out
 
-    def all_to_all_v_multi(self, items):
+    def all_to_all_v_multi(self, items, async_op=False):
         """Several row-wise all-to-all-v exchanges fused into ONE group of
         point-to-point transfers (one RCCL group launch; on xGMI every peer
         pair has its own link, so the transfers of all tensors to all peers
-        run concurrently).  items: [(x, send_rows, recv_rows), ...]."""
+        run concurrently).  items: [(x, send_rows, recv_rows), ...].
+        async_op: return (outputs, handle) and leave the wait to the caller
+        (handle.wait() orders the current stream after the transfers); the
+        inputs must stay alive until then."""
         if self.size == 1:
-            return [x for x, _, _ in items]
+            outs = [x for x, _, _ in items]
+            return (outs, _Done()) if async_op else outs
         outs, ops = [], []
         for x, send, recv in items:
             x = x.contiguous()
@@ -158,9 +180,11 @@ class Comm:
                 so += sn
                 ro += rn
             outs.append(out)
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+        if async_op:
+            return outs, _Reqs(reqs, [x for x, _, _ in items])
+        for req in reqs:
+            req.wait()
         return outs
 
     def exchange_counts_dev(self, send_dev):

@@ -316,6 +316,8 @@ class Worker:
             cmd = d.get("cmd")
             if cmd == "exit":
                 return
+            if cmd in ("save", "load"):
+                self.learner.flush()
             if cmd == "save":
                 if self.comm.rank < self.nshard:
                     name = checkpoint.model_name(d["file"], d["iter"], self.comm.rank)
