@@ -552,8 +552,7 @@ Tensor kmeans_pack_c(const Tensor& C) {
   TORCH_CHECK(C.dim() == 2, "C must be [k, f]");
   c10::DeviceGuard g(C.device());
   const int k = (int)C.size(0), f = (int)C.size(1);
-  const int ks = wh::kmeans_ks(f);
-  auto Cp = torch::empty({(int64_t)((k + 31) / 32) * ks * 64}, C.options());
+  auto Cp = torch::empty({wh::kmeans_cp_elems(k, f)}, C.options());
   wh::kmeans_pack_c(ptr<float>(C), k, f, ptr<float>(Cp), cur_stream(C));
   return Cp;
 }
@@ -564,7 +563,7 @@ std::vector<Tensor> kmeans_assign(const Tensor& Xp, int64_t n, int64_t f, const 
   CHECK_IN(Cp, torch::kFloat32);
   const int ks = wh::kmeans_ks((int)f);
   TORCH_CHECK(Xp.numel() == (n + 31) / 32 * ks * 64, "packed X size mismatch");
-  TORCH_CHECK(Cp.numel() == (k + 31) / 32 * ks * 64, "packed C size mismatch");
+  TORCH_CHECK(Cp.numel() == wh::kmeans_cp_elems((int)k, (int)f), "packed C size mismatch");
   c10::DeviceGuard g(Xp.device());
   auto assign = torch::empty({n}, Xp.options().dtype(torch::kInt32));
   auto score = torch::empty({n}, Xp.options());

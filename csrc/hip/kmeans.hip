@@ -19,6 +19,8 @@
 #include "wh_common.h"
 #include "wh_kernels.h"
 
+#include <cstdlib>
+
 namespace wh {
 namespace {
 
@@ -50,6 +52,130 @@ __global__ void k_pack_c(const float* __restrict__ C, int k, int f, int ks, int 
   const int cl = chunk * 32 + (lane & 31);
   const int col = 2 * s + (lane >> 5);
   Cp[t] = (cl < k && col < f) ? C[(int64_t)cl * f + col] : 0.f;
+}
+
+// Block-tiled assignment for F <= 128 (KS <= 64 k-steps). A workgroup of 4
+// waves owns 128 rows (each wave a 32-row tile, A fragments in VGPRs) and
+// sweeps the centroids in chunks of 128 (4 subtiles of 32) staged in LDS,
+// double-buffered: while the MFMAs consume chunk c from LDS, chunk c+1's
+// global loads are in flight in registers. One B read per k-step is a
+// ds_read_b128 holding the 4 subtiles' operands (LDS layout [s][lane][j]),
+// so each A fragment feeds 4 independent accumulators (4 x 32x32 outputs);
+// chunks arrive by LDS-DMA (no staging registers).
+// Replaces a per-wave kernel that streamed every B operand from L2 (rocprof:
+// 34 TF of the 157 TF fp32 MFMA peak at 10M x 128, k = 1000).
+__global__ void k_pack_cn(const float* __restrict__ C, int k, int f, int ks, int nchunk, int nsub,
+                          float* __restrict__ Cp) {
+  // Cp[((chunk*ks + s)*64 + lane)*nsub + j] = C[chunk*32nsub + j*32 + (lane&31)][2s + (lane>>5)]
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)nchunk * ks * 64 * nsub) return;
+  const int j = (int)(t % nsub);
+  const int lane = (int)((t / nsub) & 63);
+  const int64_t cs = t / nsub / 64;
+  const int s = (int)(cs % ks);
+  const int chunk = (int)(cs / ks);
+  const int cl = chunk * 32 * nsub + j * 32 + (lane & 31);
+  const int col = 2 * s + (lane >> 5);
+  Cp[t] = (cl < k && col < f) ? C[(int64_t)cl * f + col] : 0.f;
+}
+
+template <int NSUB>
+struct BVec;
+template <>
+struct BVec<4> { typedef float4 T; };
+template <>
+struct BVec<2> { typedef float2 T; };
+
+template <int KS, int NSUB>
+__global__ __launch_bounds__(256, 1) void k_assign_blk(const float* __restrict__ Xp, int64_t n,
+                                                       const float* __restrict__ Cp, int nchunk,
+                                                       int k, int32_t* __restrict__ assign,
+                                                       float* __restrict__ score) {
+  typedef typename BVec<NSUB>::T BT;
+  constexpr int CH = 32 * NSUB;               // centroids per chunk
+  constexpr int CF = KS * 64 * NSUB;          // floats per LDS chunk
+  constexpr int PER = CF / 4 / 256;           // 16-byte DMA pieces per thread per chunk
+  __shared__ float4 lds4[2 * CF / 4];         // 2 x KS*NSUB/4 KiB (128 KiB at KS 64, NSUB 4)
+  float4* buf0 = lds4;
+  float4* buf1 = lds4 + CF / 4;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t tile = (int64_t)blockIdx.x * 4 + wid;
+  const bool live = tile < ntiles;
+  float a[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) a[s] = live ? Xp[(tile * KS + s) * 64 + lane] : 0.f;
+  float bv[16];
+  int bk[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    bv[r] = -INFINITY;
+    bk[r] = 0x7fffffff;
+  }
+  const float4* cp4 = reinterpret_cast<const float4*>(Cp);
+  // chunk -> LDS with LDS-DMA (global_load_lds_dwordx4): the image is
+  // lane-linear ([s][lane][j] in both), so each wave-instruction writes 1 KiB
+  // at a wave-uniform base + lane * 16 B, with no staging registers
+  auto stage = [&](float4* dst, const float4* src) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      __builtin_amdgcn_global_load_lds(
+          src + i * 256 + threadIdx.x,
+          (__attribute__((address_space(3))) void*)(dst + i * 256 + wid * 64), 16, 0, 0);
+  };
+  stage(buf0, cp4);
+  __syncthreads();  // drains the DMA (vmcnt(0)) and publishes the chunk
+  for (int c = 0; c < nchunk; ++c) {
+    const float4* cur = (c & 1) ? buf1 : buf0;
+    float4* nxt = (c & 1) ? buf0 : buf1;
+    if (c + 1 < nchunk) stage(nxt, cp4 + (int64_t)(c + 1) * (CF / 4));
+    f32x16 acc[NSUB];
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) acc[j] = f32x16{0.f};
+    const BT* curb = reinterpret_cast<const BT*>(cur);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const BT b = curb[s * 64 + lane];
+      const float* bf = reinterpret_cast<const float*>(&b);
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bf[j], acc[j], 0, 0, 0);
+    }
+    const int col0 = c * CH + (lane & 31);
+    // subtiles in increasing column order; strict '>' keeps the lowest k on ties
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j)
+        if (col0 + 32 * j < k && acc[j][r] > bv[r]) {
+          bv[r] = acc[j][r];
+          bk[r] = col0 + 32 * j;
+        }
+    }
+    __syncthreads();  // next chunk landed; everyone is done with this one
+  }
+  if (!live) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = bv[r];
+    int kk = bk[r];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(v, o, 64);
+      const int ok = __shfl_xor(kk, o, 64);
+      if (ov > v || (ov == v && ok < kk)) {
+        v = ov;
+        kk = ok;
+      }
+    }
+    if ((lane & 31) == 0) {
+      const int64_t row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < n) {
+        assign[row] = kk == 0x7fffffff ? 0 : kk;
+        if (score) score[row] = v;
+      }
+    }
+  }
 }
 
 template <int KS>
@@ -156,32 +282,81 @@ void kmeans_pack_x(const float* X, int64_t n, int f, float* Xp, hipStream_t s) {
   hipLaunchKernelGGL(k_pack_x, dim3(grid_for(total, 256)), dim3(256), 0, s, X, n, f, ks, Xp);
 }
 
+// the block-tiled kernel handles F <= 128; wider rows use the streamed kernel.
+// NSUB = centroid subtiles of 32 per LDS chunk (WH_KMEANS_NSUB, default 4).
+static bool blocked(int f) { return kmeans_ks(f) <= 64; }
+static int nsub() {
+  static int v = 0;
+  if (v == 0) {
+    const char* e = getenv("WH_KMEANS_NSUB");
+    v = (e && atoi(e) == 2) ? 2 : 4;
+  }
+  return v;
+}
+
+int64_t kmeans_cp_elems(int k, int f) {
+  const int ks = kmeans_ks(f);
+  if (blocked(f)) {
+    const int ch = 32 * nsub();
+    return (int64_t)((k + ch - 1) / ch) * ks * 64 * nsub();
+  }
+  return (int64_t)((k + 31) / 32) * ks * 64;
+}
+
 void kmeans_pack_c(const float* C, int k, int f, float* Cp, hipStream_t s) {
   const int ks = kmeans_ks(f);
+  if (blocked(f)) {
+    const int ns = nsub(), nchunk = (k + 32 * ns - 1) / (32 * ns);
+    const int64_t total = (int64_t)nchunk * ks * 64 * ns;
+    hipLaunchKernelGGL(k_pack_cn, dim3(grid_for(total, 256)), dim3(256), 0, s, C, k, f, ks,
+                       nchunk, ns, Cp);
+    return;
+  }
   const int nchunk = (k + 31) / 32;
   const int64_t total = (int64_t)nchunk * ks * 64;
   hipLaunchKernelGGL(k_pack_c, dim3(grid_for(total, 256)), dim3(256), 0, s, C, k, f, ks, nchunk,
                      Cp);
 }
 
+template <int NS>
+static void launch_blk(int ks, dim3 grid, hipStream_t s, const float* Xp, int64_t n,
+                       const float* Cp, int nchunk, int k, int32_t* assign, float* score) {
+  const dim3 block(256);
+  switch (ks) {
+    case 8:
+      hipLaunchKernelGGL((k_assign_blk<8, NS>), grid, block, 0, s, Xp, n, Cp, nchunk, k, assign,
+                         score);
+      break;
+    case 16:
+      hipLaunchKernelGGL((k_assign_blk<16, NS>), grid, block, 0, s, Xp, n, Cp, nchunk, k, assign,
+                         score);
+      break;
+    case 32:
+      hipLaunchKernelGGL((k_assign_blk<32, NS>), grid, block, 0, s, Xp, n, Cp, nchunk, k, assign,
+                         score);
+      break;
+    default:
+      hipLaunchKernelGGL((k_assign_blk<64, NS>), grid, block, 0, s, Xp, n, Cp, nchunk, k, assign,
+                         score);
+      break;
+  }
+}
+
 void kmeans_assign(const float* Xp, int64_t n, int f, const float* Cp, int k, int32_t* assign,
                    float* score, hipStream_t s) {
   if (n <= 0) return;
   const int ks = kmeans_ks(f);
-  const int nchunk = (k + 31) / 32;
   const int64_t ntiles = (n + 31) / 32;
+  if (blocked(f)) {
+    const int ns = nsub(), nchunk = (k + 32 * ns - 1) / (32 * ns);
+    const dim3 grid((unsigned)((ntiles + 3) / 4));
+    if (ns == 2) launch_blk<2>(ks, grid, s, Xp, n, Cp, nchunk, k, assign, score);
+    else launch_blk<4>(ks, grid, s, Xp, n, Cp, nchunk, k, assign, score);
+    return;
+  }
+  const int nchunk = (k + 31) / 32;
   const dim3 grid(grid_for(ntiles * 64, 256)), block(256);
-  // register-resident A for the common widths, streamed A beyond
-  if (ks <= 8)
-    hipLaunchKernelGGL(k_assign<8>, grid, block, 0, s, Xp, n, ks, Cp, nchunk, k, assign, score);
-  else if (ks <= 16)
-    hipLaunchKernelGGL(k_assign<16>, grid, block, 0, s, Xp, n, ks, Cp, nchunk, k, assign, score);
-  else if (ks <= 32)
-    hipLaunchKernelGGL(k_assign<32>, grid, block, 0, s, Xp, n, ks, Cp, nchunk, k, assign, score);
-  else if (ks <= 64)
-    hipLaunchKernelGGL(k_assign<64>, grid, block, 0, s, Xp, n, ks, Cp, nchunk, k, assign, score);
-  else
-    hipLaunchKernelGGL(k_assign<0>, grid, block, 0, s, Xp, n, ks, Cp, nchunk, k, assign, score);
+  hipLaunchKernelGGL(k_assign<0>, grid, block, 0, s, Xp, n, ks, Cp, nchunk, k, assign, score);
 }
 
 void kmeans_accum(const float* X, int64_t n, int f, const int32_t* assign, float* sums,

@@ -180,6 +180,7 @@ void synth_criteo(int64_t nrows, uint64_t seed, uint64_t step, const int64_t* ca
 // ------------------------------------------------------------ kmeans.hip
 int kmeans_ks(int f);  // padded MFMA k-steps (2 features each)
 void kmeans_pack_x(const float* X, int64_t n, int f, float* Xp, hipStream_t s);
+int64_t kmeans_cp_elems(int k, int f);  // packed centroid floats
 void kmeans_pack_c(const float* C, int k, int f, float* Cp, hipStream_t s);
 void kmeans_assign(const float* Xp, int64_t n, int f, const float* Cp, int k, int32_t* assign,
                    float* score, hipStream_t s);
