@@ -470,20 +470,42 @@ Tensor gbdt_bin(const Tensor& X, const Tensor& cuts, const Tensor& cut_off) {
   return B;
 }
 
+// tasks [T, 5] (slot, fbeg, fcnt, rbeg, rend); red [R, 6] (slot, fbeg, fcnt,
+// t0, nt, tstride) sums the fp32 partials of tasks t0 + k * tstride into hist
 void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& gpair,
-               const Tensor& tasks, int64_t max_fcnt, const Tensor& hist) {
+               const Tensor& tasks, const Tensor& red, int64_t max_fcnt, const Tensor& hist) {
   CHECK_IN(B, torch::kUInt8);
   CHECK_IN(ridx, torch::kInt32);
   CHECK_IN(gpair, torch::kFloat32);
   CHECK_IN(tasks, torch::kInt32);
+  CHECK_IN(red, torch::kInt32);
   CHECK_IN(hist, torch::kFloat64);
   TORCH_CHECK(nbin >= 1 && nbin <= 255, "nbin must be in [1, 255]");
   TORCH_CHECK(wh::gbdt_hist_lds((int)max_fcnt, (int)nbin) <= 64 * 1024, "feature group too wide");
   TORCH_CHECK(tasks.dim() == 2 && tasks.size(1) == 5);
+  TORCH_CHECK(red.dim() == 2 && red.size(1) == 6);
+  const int f = (int)B.size(1);
+  TORCH_CHECK(hist.numel() % ((int64_t)f * nbin * 2) == 0, "hist must be [S, F, nbin, 2]");
+  // dword row loads need every group 4-aligned; the caller guarantees equal
+  // multiple-of-4 groups when f % 4 == 0 (checked again here on the host copy)
+  bool dw = f % 4 == 0 && max_fcnt % 4 == 0;
   c10::DeviceGuard g(B.device());
-  wh::gbdt_hist(ptr<uint8_t>(B), (int)B.size(1), (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
-                ptr<int32_t>(tasks), (int)tasks.size(0), (int)max_fcnt, ptr<double>(hist),
-                cur_stream(B));
+  auto part = torch::empty({tasks.size(0) * wh::gbdt_hist_pstride((int)max_fcnt, (int)nbin)},
+                           gpair.options());
+  wh::gbdt_hist(ptr<uint8_t>(B), f, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
+                ptr<int32_t>(tasks), (int)tasks.size(0), ptr<int32_t>(red), (int)red.size(0),
+                (int)max_fcnt, dw, ptr<float>(part), ptr<double>(hist), cur_stream(B));
+}
+
+Tensor gbdt_seg_fill(const Tensor& beg, const Tensor& node, int64_t n) {
+  CHECK_IN(beg, torch::kInt32);
+  CHECK_IN(node, torch::kInt32);
+  TORCH_CHECK(beg.numel() == node.numel() && beg.numel() > 0, "segment arrays mismatch");
+  c10::DeviceGuard g(beg.device());
+  auto out = torch::empty({n}, beg.options());
+  wh::gbdt_seg_fill(ptr<int32_t>(beg), ptr<int32_t>(node), (int)beg.numel(), n, ptr<int32_t>(out),
+                    cur_stream(beg));
+  return out;
 }
 
 // partition the positions of the split nodes; returns the new ridx
@@ -629,6 +651,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gbdt_bin", &gbdt_bin);
   m.def("gbdt_hist", &gbdt_hist);
   m.def("gbdt_partition", &gbdt_partition);
+  m.def("gbdt_seg_fill", &gbdt_seg_fill);
   m.def("gbdt_leaf_add", &gbdt_leaf_add);
   m.def("gbdt_predict", &gbdt_predict);
   m.def("kmeans_pack_x", &kmeans_pack_x);

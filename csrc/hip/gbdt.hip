@@ -3,8 +3,8 @@
 //   gbdt_bin       value -> quantile bin (uint8, 255 = missing) by binary
 //                  search in the feature's cut points
 //   gbdt_hist      per (node, feature-group, row-chunk) block: LDS-privatised
-//                  fp32 (g, h) histograms (ds_add_f32), flushed once per block
-//                  into the node's fp64 histogram with device-scope atomics
+//                  fp32 (g, h) histograms (ds_add_f32) stored as per-block
+//                  partials, then summed per (node, group) in fp64
 //   gbdt_goleft / gbdt_scatter   stable per-node row partition after a split
 //   gbdt_leaf_add  margin += leaf value for the rows of every leaf segment
 //   gbdt_predict   one lane per row walks a tree on raw values (NaN = missing)
@@ -49,36 +49,120 @@ struct HistTask {
   int32_t rend;
 };
 
-__global__ __launch_bounds__(256) void k_hist(const uint8_t* __restrict__ B, int f, int nbin,
-                                              const int32_t* __restrict__ ridx,
-                                              const float2* __restrict__ gpair,
-                                              const HistTask* __restrict__ tasks,
-                                              double* __restrict__ hist) {
+// Partial-sum reduction of the tasks of one (slot, feature group):
+// tasks t0, t0 + tstride, ... (nt of them).
+struct HistReduce {
+  int32_t node;
+  int32_t fbeg;
+  int32_t fcnt;
+  int32_t t0;
+  int32_t nt;
+  int32_t tstride;
+};
+
+constexpr int kHistThreads = 1024;  // 2 blocks (2 x <= 64 KB LDS) fill a CU's 32 wave slots
+
+__device__ __forceinline__ void hist_add(float* lds, int nbin, int fj, int b, float2 gh) {
+  if (b != kMissing) {
+    atomicAdd(&lds[2 * (fj * nbin + b)], gh.x);
+    atomicAdd(&lds[2 * (fj * nbin + b) + 1], gh.y);
+  }
+}
+
+// LDS-privatised histogram of one task, written (not atomically added) to the
+// task's fp32 partial slice; k_hist_reduce sums the slices in fp64.  Replacing
+// the per-block fp64 atomic flush (14 K memory-side atomics per block) by
+// plain coalesced stores is what makes small row chunks -- and so a full grid
+// at every tree level -- affordable.
+//
+// DW: the group's bytes of a row are 4-aligned (f % 4 == 0, fbeg % 4 == 0,
+// fcnt % 4 == 0): D = fcnt / 4 lanes share a row and each loads one dword
+// (4 bins), so a wave fetches floor(64 / D) rows with one load instruction
+// instead of one byte per lane per feature.  Four row batches are loaded
+// before any LDS atomic is issued, keeping 4 dependent gathers in flight per
+// wave.  Otherwise one thread per row walks the group's bytes.
+template <bool DW>
+__global__ __launch_bounds__(kHistThreads) void k_hist(const uint8_t* __restrict__ B, int f,
+                                                       int nbin, const int32_t* __restrict__ ridx,
+                                                       const float2* __restrict__ gpair,
+                                                       const HistTask* __restrict__ tasks,
+                                                       float* __restrict__ part, int64_t pstride) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const HistTask tk = tasks[blockIdx.x];
-  const int nl = tk.fcnt * nbin;
-  for (int i = threadIdx.x; i < 2 * nl; i += blockDim.x) lds[i] = 0.f;
+  const int nl2 = 2 * tk.fcnt * nbin;
+  for (int i = threadIdx.x; i < nl2; i += blockDim.x) lds[i] = 0.f;
   __syncthreads();
-  // threads sweep (row, feature) pairs of the chunk: consecutive lanes read
-  // consecutive feature bytes of a row
-  const int64_t pairs = (int64_t)(tk.rend - tk.rbeg) * tk.fcnt;
-  for (int64_t p = threadIdx.x; p < pairs; p += blockDim.x) {
-    const int r = tk.rbeg + (int)(p / tk.fcnt);
-    const int fj = (int)(p % tk.fcnt);
-    const int row = ridx[r];
-    const int b = B[(int64_t)row * f + tk.fbeg + fj];
-    if (b != kMissing) {
+  const int nrow = tk.rend - tk.rbeg;
+  const int32_t* rid = ridx + tk.rbeg;
+  if (DW) {
+    constexpr int U = 4;
+    const int D = tk.fcnt >> 2;
+    const int R = 64 / D;  // rows per wave batch
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int ri = lane / D, dj = lane - ri * D;
+    const bool act = ri < R;
+    const uint8_t* Bg = B + tk.fbeg + 4 * dj;
+    for (int base = wave * R; base < nrow; base += nw * R * U) {
+      uint32_t word[U];
+      float2 g[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int r = base + u * nw * R + ri;
+        const bool ok = act && r < nrow;
+        const int row = ok ? rid[r] : 0;
+        word[u] = ok ? *reinterpret_cast<const uint32_t*>(Bg + (int64_t)row * f) : 0xffffffffu;
+        g[u] = ok ? gpair[row] : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) hist_add(lds, nbin, 4 * dj + c, (word[u] >> (8 * c)) & 255, g[u]);
+    }
+  } else {
+    const int lane = threadIdx.x & 63;
+    for (int r = threadIdx.x; r < nrow; r += blockDim.x) {
+      const int row = rid[r];
       const float2 gh = gpair[row];
-      atomicAdd(&lds[2 * (fj * nbin + b)], gh.x);
-      atomicAdd(&lds[2 * (fj * nbin + b) + 1], gh.y);
+      const uint8_t* brow = B + (int64_t)row * f + tk.fbeg;
+      int fj = lane % tk.fcnt;  // lane-rotated feature order spreads the atomics
+      for (int q = 0; q < tk.fcnt; ++q) {
+        hist_add(lds, nbin, fj, brow[fj], gh);
+        fj = fj + 1 == tk.fcnt ? 0 : fj + 1;
+      }
     }
   }
   __syncthreads();
-  double* out = hist + ((int64_t)tk.node * f + tk.fbeg) * nbin * 2;
-  for (int i = threadIdx.x; i < 2 * nl; i += blockDim.x) {
-    const float v = lds[i];
-    if (v != 0.f) atomicAdd(out + i, (double)v);
+  float* out = part + (int64_t)blockIdx.x * pstride;
+  for (int i = threadIdx.x; i < nl2; i += blockDim.x) out[i] = lds[i];
+}
+
+__global__ __launch_bounds__(256) void k_hist_reduce(const float* __restrict__ part,
+                                                     int64_t pstride,
+                                                     const HistReduce* __restrict__ red, int f,
+                                                     int nbin, double* __restrict__ hist) {
+  const HistReduce rd = red[blockIdx.y];
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= 2 * rd.fcnt * nbin) return;
+  const float* p = part + (int64_t)rd.t0 * pstride + e;
+  double acc = 0.0;
+  for (int k = 0; k < rd.nt; ++k) acc += (double)p[(int64_t)k * rd.tstride * pstride];
+  hist[((int64_t)rd.node * f + rd.fbeg) * nbin * 2 + e] = acc;
+}
+
+// out[i] = node of the segment containing position i; segments sorted by
+// begin and tiling [0, n) (finished-leaf gaps carry node -1)
+__global__ __launch_bounds__(256) void k_seg_fill(const int32_t* __restrict__ beg,
+                                                  const int32_t* __restrict__ node, int nseg,
+                                                  int64_t n, int32_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int lo = 0, hi = nseg - 1;  // last segment with beg <= i
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (beg[mid] <= i) lo = mid;
+    else hi = mid - 1;
   }
+  out[i] = node[lo];
 }
 
 __global__ void k_goleft(const uint8_t* __restrict__ B, int f, const int32_t* __restrict__ ridx,
@@ -150,12 +234,32 @@ void gbdt_bin(const float* X, int64_t n, int f, const float* cuts, const int32_t
 
 size_t gbdt_hist_lds(int fcnt, int nbin) { return (size_t)fcnt * nbin * 2 * sizeof(float); }
 
+int64_t gbdt_hist_pstride(int max_fcnt, int nbin) { return ((int64_t)2 * max_fcnt * nbin + 63) & ~63; }
+
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
-               const int32_t* tasks, int ntask, int max_fcnt, double* hist, hipStream_t s) {
+               const int32_t* tasks, int ntask, const int32_t* red, int nred, int max_fcnt,
+               bool dword_rows, float* part, double* hist, hipStream_t s) {
   if (ntask <= 0) return;
-  hipLaunchKernelGGL(k_hist, dim3(ntask), dim3(256), gbdt_hist_lds(max_fcnt, nbin), s, B, f, nbin,
-                     ridx, reinterpret_cast<const float2*>(gpair),
-                     reinterpret_cast<const HistTask*>(tasks), hist);
+  const int64_t ps = gbdt_hist_pstride(max_fcnt, nbin);
+  const size_t lds = gbdt_hist_lds(max_fcnt, nbin);
+  const auto* tk = reinterpret_cast<const HistTask*>(tasks);
+  const auto* gp = reinterpret_cast<const float2*>(gpair);
+  if (dword_rows)
+    hipLaunchKernelGGL(k_hist<true>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx, gp,
+                       tk, part, ps);
+  else
+    hipLaunchKernelGGL(k_hist<false>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx,
+                       gp, tk, part, ps);
+  if (nred > 0)
+    hipLaunchKernelGGL(k_hist_reduce, dim3((unsigned)((2 * max_fcnt * nbin + 255) / 256), nred),
+                       dim3(256), 0, s, part, ps, reinterpret_cast<const HistReduce*>(red), f,
+                       nbin, hist);
+}
+
+void gbdt_seg_fill(const int32_t* beg, const int32_t* node, int nseg, int64_t n, int32_t* out,
+                   hipStream_t s) {
+  if (n <= 0 || nseg <= 0) return;
+  hipLaunchKernelGGL(k_seg_fill, dim3(grid_for(n, 256)), dim3(256), 0, s, beg, node, nseg, n, out);
 }
 
 void gbdt_goleft(const uint8_t* B, int f, const int32_t* ridx, int64_t n, const int32_t* pos_node,

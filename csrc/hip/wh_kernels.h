@@ -192,8 +192,13 @@ void gbdt_bin(const float* X, int64_t n, int f, const float* cuts, const int32_t
               uint8_t* B, hipStream_t s);
 size_t gbdt_hist_lds(int fcnt, int nbin);
 // tasks: int32 [ntask x 5] = {node slot, fbeg, fcnt, rbeg, rend}; hist fp64 [slots x f x nbin x 2]
+int64_t gbdt_hist_pstride(int max_fcnt, int nbin);
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
-               const int32_t* tasks, int ntask, int max_fcnt, double* hist, hipStream_t s);
+               const int32_t* tasks, int ntask, const int32_t* red, int nred, int max_fcnt,
+               bool dword_rows, float* part, double* hist, hipStream_t s);
+// position -> node id over sorted segments tiling [0, n)
+void gbdt_seg_fill(const int32_t* beg, const int32_t* node, int nseg, int64_t n, int32_t* out,
+                   hipStream_t s);
 void gbdt_goleft(const uint8_t* B, int f, const int32_t* ridx, int64_t n, const int32_t* pos_node,
                  const int32_t* node_feat, const int32_t* node_bin, const uint8_t* node_defl,
                  int32_t* left, hipStream_t s);

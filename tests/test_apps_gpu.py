@@ -101,6 +101,50 @@ def test_gbdt_kernels_match_cpu():
     assert abs(lc - lg) < 1e-3 * lc, (lc, lg)
 
 
+@pytest.mark.parametrize("f,nbin", [(40, 255), (40, 16), (13, 200)])
+def test_gbdt_hist_kernel(f, nbin):
+    """Per-segment histograms (dword-row and byte-row paths, one and several
+    feature groups, several row chunks per segment) vs an fp64 index_add."""
+    from wormhole_amd import _native
+    g = torch.Generator().manual_seed(f + nbin)
+    n = 300000
+    B = torch.randint(0, nbin, (n, f), generator=g, dtype=torch.uint8)
+    B[torch.rand(n, f, generator=g) < 0.05] = 255
+    gp = torch.randn(n, 2, generator=g)
+    ridx = torch.randperm(n, generator=g).to(torch.int32)
+    segs = [(0, 170000), (170000, 170000), (170000, 299000)]
+    fg = min(64, (64 * 1024) // (nbin * 8))
+    fg -= fg % 4
+    groups = [(j, min(fg, f - j)) for j in range(0, f, fg)]
+    chunk = 4096 * 3
+    tasks, red = [], []
+    for s, (b, e) in enumerate(segs):
+        if e <= b:
+            continue
+        t0, nch = len(tasks), 0
+        for r in range(b, e, chunk):
+            nch += 1
+            for fb, fc in groups:
+                tasks.append((s, fb, fc, r, min(e, r + chunk)))
+        for k, (fb, fc) in enumerate(groups):
+            red.append((s, fb, fc, t0 + k, nch, len(groups)))
+    dev = torch.device("cuda", 0)
+    hist = torch.zeros(len(segs), f, nbin, 2, dtype=torch.float64, device=dev)
+    _native.hip().gbdt_hist(B.to(dev), nbin, ridx.to(dev), gp.to(dev),
+                            torch.tensor(tasks, dtype=torch.int32, device=dev),
+                            torch.tensor(red, dtype=torch.int32, device=dev),
+                            max(c for _, c in groups), hist)
+    for s, (b, e) in enumerate(segs):
+        ref = torch.zeros(f * nbin, 2, dtype=torch.float64)
+        rows = ridx[b:e].long()
+        bins = B[rows].long()
+        ok = bins != 255
+        flat = (torch.arange(f)[None, :] * nbin + bins.clamp(max=nbin - 1))[ok]
+        for c in range(2):
+            ref[:, c].index_add_(0, flat, gp[rows, c].double()[:, None].expand(-1, f)[ok])
+        torch.testing.assert_close(hist[s].cpu().view(-1, 2), ref, rtol=1e-4, atol=1e-3)
+
+
 def test_xgboost_app_gpu(work, capsys, monkeypatch):
     from wormhole_amd.apps.xgboost_app import main
     monkeypatch.setenv("WH_DEVICE", "auto")

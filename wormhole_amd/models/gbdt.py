@@ -398,9 +398,11 @@ class TreeBuilder:
         self.gpu = B.is_cuda
         self.device = B.device
         fg = max(1, (64 * 1024) // (self.nbin * 8))  # features per LDS histogram block
+        fg = min(fg, 64)
+        if fg >= 4:
+            fg -= fg % 4  # 4-aligned groups let the kernel load 4 bins per dword
         self.fgroups = [(j, min(fg, self.F - j)) for j in range(0, self.F, fg)]
         self.max_fcnt = max(c for _, c in self.fgroups) if self.fgroups else 1
-        self.chunk = 2048
         o = cuts.offsets.tolist()
         nb = torch.tensor([b - a for a, b in zip(o, o[1:])])
         self.bin_mask = torch.arange(self.nbin)[None, :] < nb[:, None]  # [F, nbin]
@@ -421,14 +423,29 @@ class TreeBuilder:
         """segs: list of (beg, end) local row ranges; slots: output slot of each."""
         hist = torch.zeros(nslot, self.F, self.nbin, 2, dtype=torch.float64, device=self.device)
         if self.gpu:
-            tasks = []
+            # ~1024 row chunks per call (two rounds of the 512 resident
+            # 1024-thread blocks); partials are summed per (slot, group)
+            total = sum(max(0, e - b) for b, e in segs)
+            chunk = max(4096, -(-total // 1024))
+            G = len(self.fgroups)
+            tasks, red = [], []
             for (b, e), s in zip(segs, slots):
-                for r in range(b, e, self.chunk):
+                if e <= b:
+                    continue
+                t0, nch = len(tasks), 0
+                for r in range(b, e, chunk):
+                    nch += 1
                     for fb, fc in self.fgroups:
-                        tasks.append((s, fb, fc, r, min(e, r + self.chunk)))
+                        tasks.append((s, fb, fc, r, min(e, r + chunk)))
+                for g, (fb, fc) in enumerate(self.fgroups):
+                    red.append((s, fb, fc, t0 + g, nch, G))
             if tasks:
-                t = torch.tensor(tasks, dtype=torch.int32).to(self.device)
-                _native.hip().gbdt_hist(self.B, self.nbin, ridx, gpair, t, self.max_fcnt, hist)
+                both = torch.tensor(tasks, dtype=torch.int32).reshape(-1)
+                both = torch.cat([both, torch.tensor(red, dtype=torch.int32).reshape(-1)])
+                both = both.to(self.device)
+                t = both[:5 * len(tasks)].view(-1, 5)
+                rd = both[5 * len(tasks):].view(-1, 6)
+                _native.hip().gbdt_hist(self.B, self.nbin, ridx, gpair, t, rd, self.max_fcnt, hist)
         else:
             for (b, e), s in zip(segs, slots):
                 if e <= b:
@@ -493,7 +510,7 @@ class TreeBuilder:
         seg = {root: (0, n)}
         hist_root = self._build_hist(ridx, gpair, [seg[root]], [0], 1)
         self.bsp.allreduce(hist_root)
-        hists = {root: hist_root[0]}
+        H_front = hist_root  # [len(frontier), F, nbin, 2], frontier order
         frontier = [root]
         cuts_v = self.cuts.values.tolist()
         cuts_o = self.cuts.offsets.tolist()
@@ -508,7 +525,7 @@ class TreeBuilder:
             if depth == p.max_depth:
                 break
             S = len(frontier)
-            H_all = torch.stack([hists[nd] for nd in frontier])
+            H_all = H_front
             T_all = torch.stack([totals[nd] for nd in frontier]).to(H_all.device)
             bg, bf, bb, bd, bL = self._find_splits(H_all, T_all)
             split_nodes = []
@@ -563,10 +580,18 @@ class TreeBuilder:
                     seg.pop(nd, None)  # finished leaf: its rows are final
             hsmall = self._build_hist(ridx, gpair, build_segs, build_slots, len(build_slots))
             self.bsp.allreduce(hsmall)
-            for k, nd in enumerate(split_nodes):
-                hists[small[k]] = hsmall[k]
-                hists[big[k]] = hists[nd] - hsmall[k]
-                del hists[nd]
+            # sibling subtraction for every split node at once; the new
+            # frontier is [l, r] per split node, in split order
+            fpos = {nd: i for i, nd in enumerate(frontier)}
+            par = torch.tensor([fpos[nd] for nd in split_nodes], dtype=torch.int64,
+                               device=H_front.device)
+            hbig = H_front.index_select(0, par) - hsmall
+            small_is_left = torch.tensor([small[k] == tree.left[nd]
+                                          for k, nd in enumerate(split_nodes)],
+                                         device=H_front.device)
+            hl = torch.where(small_is_left[:, None, None, None], hsmall, hbig)
+            hr = torch.where(small_is_left[:, None, None, None], hbig, hsmall)
+            H_front = torch.stack([hl, hr], 1).reshape(-1, *H_front.shape[1:])
             frontier = new_frontier
         self._prune(tree)
         # margins of the training rows from the final leaf segments
@@ -586,6 +611,13 @@ class TreeBuilder:
         if cur < n:
             ids.append(-1), lens.append(n - cur)
         dev = self.device
+        if self.gpu and ids:
+            begs, acc = [], 0
+            for ln in lens:
+                begs.append(acc)
+                acc += ln
+            seg = torch.tensor([begs, ids], dtype=torch.int32).to(dev)
+            return _native.hip().gbdt_seg_fill(seg[0].contiguous(), seg[1].contiguous(), n)
         return torch.repeat_interleave(torch.tensor(ids, dtype=torch.int32, device=dev),
                                        torch.tensor(lens, dtype=torch.int64, device=dev),
                                        output_size=n)
