@@ -472,8 +472,10 @@ Tensor gbdt_bin(const Tensor& X, const Tensor& cuts, const Tensor& cut_off) {
 
 // tasks [T, 5] (slot, fbeg, fcnt, rbeg, rend); red [R, 6] (slot, fbeg, fcnt,
 // t0, nt, tstride) sums the fp32 partials of tasks t0 + k * tstride into hist
+// qscale [2] float32 = {2^eg, 2^eh}: fixed-point scales of g and h (see gbdt.hip)
 void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& gpair,
-               const Tensor& tasks, const Tensor& red, int64_t max_fcnt, const Tensor& hist) {
+               const Tensor& qscale, const Tensor& tasks, const Tensor& red, int64_t max_fcnt,
+               const Tensor& hist) {
   CHECK_IN(B, torch::kUInt8);
   CHECK_IN(ridx, torch::kInt32);
   CHECK_IN(gpair, torch::kFloat32);
@@ -481,7 +483,9 @@ void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& 
   CHECK_IN(red, torch::kInt32);
   CHECK_IN(hist, torch::kFloat64);
   TORCH_CHECK(nbin >= 1 && nbin <= 255, "nbin must be in [1, 255]");
-  TORCH_CHECK(wh::gbdt_hist_lds((int)max_fcnt, (int)nbin) <= 64 * 1024, "feature group too wide");
+  CHECK_IN(qscale, torch::kFloat32);
+  TORCH_CHECK(qscale.numel() == 2, "qscale must hold {scale_g, scale_h}");
+  TORCH_CHECK(wh::gbdt_hist_lds((int)max_fcnt, (int)nbin) <= 160 * 1024, "feature group too wide");
   TORCH_CHECK(tasks.dim() == 2 && tasks.size(1) == 5);
   TORCH_CHECK(red.dim() == 2 && red.size(1) == 6);
   const int f = (int)B.size(1);
@@ -491,10 +495,11 @@ void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& 
   bool dw = f % 4 == 0 && max_fcnt % 4 == 0;
   c10::DeviceGuard g(B.device());
   auto part = torch::empty({tasks.size(0) * wh::gbdt_hist_pstride((int)max_fcnt, (int)nbin)},
-                           gpair.options());
+                           gpair.options().dtype(torch::kInt64));
   wh::gbdt_hist(ptr<uint8_t>(B), f, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
-                ptr<int32_t>(tasks), (int)tasks.size(0), ptr<int32_t>(red), (int)red.size(0),
-                (int)max_fcnt, dw, ptr<float>(part), ptr<double>(hist), cur_stream(B));
+                ptr<float>(qscale), ptr<int32_t>(tasks), (int)tasks.size(0), ptr<int32_t>(red),
+                (int)red.size(0), (int)max_fcnt, dw, ptr<int64_t>(part), ptr<double>(hist),
+                cur_stream(B));
 }
 
 Tensor gbdt_seg_fill(const Tensor& beg, const Tensor& node, int64_t n) {

@@ -60,20 +60,28 @@ struct HistReduce {
   int32_t tstride;
 };
 
-constexpr int kHistThreads = 1024;  // 2 blocks (2 x <= 64 KB LDS) fill a CU's 32 wave slots
+constexpr int kHistThreads = 1024;
+constexpr int kHistLdsMax = 160 * 1024;  // one block per CU (<= 160 KB LDS) = 16 waves
 
-__device__ __forceinline__ void hist_add(float* lds, int nbin, int fj, int b, float2 gh) {
+// Histograms accumulate in 64-bit fixed point: ds_add_f32 on gfx950 runs ~20x
+// slower than ds_add_u32 / ~8x slower than ds_add_u64 (tools/microbench/
+// hist_bench.hip: 11M x 28 rows in 3.04 ms with f32 LDS atomics, 0.43 ms with
+// u64), and integer sums are exact, so a node's histogram no longer depends
+// on block scheduling.  qscale = {2^eg, 2^eh} is chosen by the caller so that
+// |sum of a node| * scale < 2^62 for every node (power-of-two: the scaling of
+// the fp32 gradient is exact; only its bits below 2^-e are rounded away).
+__device__ __forceinline__ void hist_add(unsigned long long* lds, int nbin, int fj, int b,
+                                         long long qg, long long qh) {
   if (b != kMissing) {
-    atomicAdd(&lds[2 * (fj * nbin + b)], gh.x);
-    atomicAdd(&lds[2 * (fj * nbin + b) + 1], gh.y);
+    atomicAdd(&lds[2 * (fj * nbin + b)], (unsigned long long)qg);
+    atomicAdd(&lds[2 * (fj * nbin + b) + 1], (unsigned long long)qh);
   }
 }
 
 // LDS-privatised histogram of one task, written (not atomically added) to the
-// task's fp32 partial slice; k_hist_reduce sums the slices in fp64.  Replacing
-// the per-block fp64 atomic flush (14 K memory-side atomics per block) by
-// plain coalesced stores is what makes small row chunks -- and so a full grid
-// at every tree level -- affordable.
+// task's int64 partial slice; k_hist_reduce sums the slices per (node, group).
+// Plain coalesced stores instead of a per-block atomic flush make small row
+// chunks -- and so a full grid at every tree level -- affordable.
 //
 // DW: the group's bytes of a row are 4-aligned (f % 4 == 0, fbeg % 4 == 0,
 // fcnt % 4 == 0): D = fcnt / 4 lanes share a row and each loads one dword
@@ -85,12 +93,15 @@ template <bool DW>
 __global__ __launch_bounds__(kHistThreads) void k_hist(const uint8_t* __restrict__ B, int f,
                                                        int nbin, const int32_t* __restrict__ ridx,
                                                        const float2* __restrict__ gpair,
+                                                       const float* __restrict__ qscale,
                                                        const HistTask* __restrict__ tasks,
-                                                       float* __restrict__ part, int64_t pstride) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
+                                                       long long* __restrict__ part,
+                                                       int64_t pstride) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
   const HistTask tk = tasks[blockIdx.x];
+  const float sg = qscale[0], sh = qscale[1];
   const int nl2 = 2 * tk.fcnt * nbin;
-  for (int i = threadIdx.x; i < nl2; i += blockDim.x) lds[i] = 0.f;
+  for (int i = threadIdx.x; i < nl2; i += blockDim.x) lds64[i] = 0ull;
   __syncthreads();
   const int nrow = tk.rend - tk.rbeg;
   const int32_t* rid = ridx + tk.rbeg;
@@ -114,39 +125,57 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(const uint8_t* __restrict
         g[u] = ok ? gpair[row] : make_float2(0.f, 0.f);
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u) {
+        const long long qg = __float2ll_rn(g[u].x * sg), qh = __float2ll_rn(g[u].y * sh);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) hist_add(lds, nbin, 4 * dj + c, (word[u] >> (8 * c)) & 255, g[u]);
+        for (int c = 0; c < 4; ++c)
+          hist_add(lds64, nbin, 4 * dj + c, (word[u] >> (8 * c)) & 255, qg, qh);
+      }
     }
   } else {
     const int lane = threadIdx.x & 63;
     for (int r = threadIdx.x; r < nrow; r += blockDim.x) {
       const int row = rid[r];
       const float2 gh = gpair[row];
+      const long long qg = __float2ll_rn(gh.x * sg), qh = __float2ll_rn(gh.y * sh);
       const uint8_t* brow = B + (int64_t)row * f + tk.fbeg;
       int fj = lane % tk.fcnt;  // lane-rotated feature order spreads the atomics
       for (int q = 0; q < tk.fcnt; ++q) {
-        hist_add(lds, nbin, fj, brow[fj], gh);
+        hist_add(lds64, nbin, fj, brow[fj], qg, qh);
         fj = fj + 1 == tk.fcnt ? 0 : fj + 1;
       }
     }
   }
   __syncthreads();
-  float* out = part + (int64_t)blockIdx.x * pstride;
-  for (int i = threadIdx.x; i < nl2; i += blockDim.x) out[i] = lds[i];
+  long long* out = part + (int64_t)blockIdx.x * pstride;
+  for (int i = threadIdx.x; i < nl2; i += blockDim.x) out[i] = (long long)lds64[i];
 }
 
-__global__ __launch_bounds__(256) void k_hist_reduce(const float* __restrict__ part,
-                                                     int64_t pstride,
-                                                     const HistReduce* __restrict__ red, int f,
-                                                     int nbin, double* __restrict__ hist) {
+// One block = 64 consecutive elements x 16 task slices: thread (e, k) sums
+// tasks k, k + 16, ... of its element (each 64-element row read is 512 B
+// contiguous), then the 16 slices are combined in LDS.
+constexpr int kRedE = 64, kRedK = 16;
+__global__ __launch_bounds__(kRedE * kRedK) void k_hist_reduce(
+    const long long* __restrict__ part, int64_t pstride, const HistReduce* __restrict__ red, int f,
+    int nbin, const float* __restrict__ qscale, double* __restrict__ hist) {
+  __shared__ unsigned long long acc_s[kRedK][kRedE];
   const HistReduce rd = red[blockIdx.y];
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= 2 * rd.fcnt * nbin) return;
-  const float* p = part + (int64_t)rd.t0 * pstride + e;
-  double acc = 0.0;
-  for (int k = 0; k < rd.nt; ++k) acc += (double)p[(int64_t)k * rd.tstride * pstride];
-  hist[((int64_t)rd.node * f + rd.fbeg) * nbin * 2 + e] = acc;
+  const int ei = threadIdx.x % kRedE, kj = threadIdx.x / kRedE;
+  const int e = blockIdx.x * kRedE + ei;
+  const int nl2 = 2 * rd.fcnt * nbin;
+  unsigned long long acc = 0;  // two's-complement sum: exact while |sum| < 2^63
+  if (e < nl2) {
+    const long long* p = part + (int64_t)rd.t0 * pstride + e;
+    for (int k = kj; k < rd.nt; k += kRedK) acc += (unsigned long long)p[(int64_t)k * rd.tstride * pstride];
+  }
+  acc_s[kj][ei] = acc;
+  __syncthreads();
+  if (kj == 0 && e < nl2) {
+#pragma unroll
+    for (int k = 1; k < kRedK; ++k) acc += acc_s[k][ei];
+    hist[((int64_t)rd.node * f + rd.fbeg) * nbin * 2 + e] =
+        (double)(long long)acc / (double)qscale[e & 1];
+  }
 }
 
 // out[i] = node of the segment containing position i; segments sorted by
@@ -232,28 +261,37 @@ void gbdt_bin(const float* X, int64_t n, int f, const float* cuts, const int32_t
   hipLaunchKernelGGL(k_bin, dim3(grid_for(n * f, 256)), dim3(256), 0, s, X, n, f, cuts, cut_off, B);
 }
 
-size_t gbdt_hist_lds(int fcnt, int nbin) { return (size_t)fcnt * nbin * 2 * sizeof(float); }
+size_t gbdt_hist_lds(int fcnt, int nbin) { return (size_t)fcnt * nbin * 2 * sizeof(int64_t); }
 
-int64_t gbdt_hist_pstride(int max_fcnt, int nbin) { return ((int64_t)2 * max_fcnt * nbin + 63) & ~63; }
+int64_t gbdt_hist_pstride(int max_fcnt, int nbin) { return ((int64_t)2 * max_fcnt * nbin + 31) & ~31; }
 
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
-               const int32_t* tasks, int ntask, const int32_t* red, int nred, int max_fcnt,
-               bool dword_rows, float* part, double* hist, hipStream_t s) {
+               const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
+               int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s) {
   if (ntask <= 0) return;
+  static bool attr = false;
+  if (!attr) {  // dynamic LDS above 64 KB must be opted into per kernel
+    WH_HIP_CHECK(hipFuncSetAttribute((const void*)k_hist<true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, kHistLdsMax));
+    WH_HIP_CHECK(hipFuncSetAttribute((const void*)k_hist<false>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, kHistLdsMax));
+    attr = true;
+  }
   const int64_t ps = gbdt_hist_pstride(max_fcnt, nbin);
   const size_t lds = gbdt_hist_lds(max_fcnt, nbin);
   const auto* tk = reinterpret_cast<const HistTask*>(tasks);
   const auto* gp = reinterpret_cast<const float2*>(gpair);
+  auto* pt = reinterpret_cast<long long*>(part);
   if (dword_rows)
     hipLaunchKernelGGL(k_hist<true>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx, gp,
-                       tk, part, ps);
+                       qscale, tk, pt, ps);
   else
     hipLaunchKernelGGL(k_hist<false>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx,
-                       gp, tk, part, ps);
+                       gp, qscale, tk, pt, ps);
   if (nred > 0)
-    hipLaunchKernelGGL(k_hist_reduce, dim3((unsigned)((2 * max_fcnt * nbin + 255) / 256), nred),
-                       dim3(256), 0, s, part, ps, reinterpret_cast<const HistReduce*>(red), f,
-                       nbin, hist);
+    hipLaunchKernelGGL(k_hist_reduce, dim3((unsigned)((2 * max_fcnt * nbin + kRedE - 1) / kRedE), nred),
+                       dim3(kRedE * kRedK), 0, s, pt, ps, reinterpret_cast<const HistReduce*>(red), f, nbin,
+                       qscale, hist);
 }
 
 void gbdt_seg_fill(const int32_t* beg, const int32_t* node, int nseg, int64_t n, int32_t* out,

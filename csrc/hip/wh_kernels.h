@@ -194,8 +194,8 @@ size_t gbdt_hist_lds(int fcnt, int nbin);
 // tasks: int32 [ntask x 5] = {node slot, fbeg, fcnt, rbeg, rend}; hist fp64 [slots x f x nbin x 2]
 int64_t gbdt_hist_pstride(int max_fcnt, int nbin);
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
-               const int32_t* tasks, int ntask, const int32_t* red, int nred, int max_fcnt,
-               bool dword_rows, float* part, double* hist, hipStream_t s);
+               const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
+               int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s);
 // position -> node id over sorted segments tiling [0, n)
 void gbdt_seg_fill(const int32_t* beg, const int32_t* node, int nseg, int64_t n, int32_t* out,
                    hipStream_t s);

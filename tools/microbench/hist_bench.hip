@@ -7,6 +7,9 @@
 //   3  like 2 with ds_add_u32 (fixed-point) instead of ds_add_f32
 //   4  production with planar g / h LDS arrays (bank = bin, not 2 * bin)
 //   5  like 4, 256-thread blocks
+//   6  LDS atomics only, ds_add_u64 (fixed point), hashed bins
+//   7  production with int32 fixed point (ds_add_u32)
+//   8  production with int64 fixed point (ds_add_u64, 2x LDS)
 // Build: hipcc -O3 --offload-arch=gfx950 -o /tmp/hb tools/microbench/hist_bench.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -26,7 +29,7 @@ template <int MODE>
 __global__ __launch_bounds__(1024) void k_hist(const uint8_t* B, const int* ridx, const float2* gp,
                                                int chunk, int n, float* out) {
   extern __shared__ float lds[];
-  const int nl2 = 2 * F * NBIN;
+  const int nl2 = 2 * F * NBIN * (MODE >= 6 && MODE != 7 ? 2 : 1);
   for (int i = threadIdx.x; i < nl2; i += blockDim.x) lds[i] = 0.f;
   __syncthreads();
   const int rbeg = blockIdx.x * chunk, nrow = min(chunk, n - rbeg);
@@ -41,7 +44,7 @@ __global__ __launch_bounds__(1024) void k_hist(const uint8_t* B, const int* ridx
     for (int u = 0; u < U; ++u) {
       const int r = base + u * nw * R + ri;
       const bool ok = act && r < nrow;
-      if (MODE == 2 || MODE == 3) {
+      if (MODE == 2 || MODE == 3 || MODE == 6) {
         word[u] = ok ? hash32(rbeg + r) : 0xffffffffu;
         g[u] = make_float2(1.f, 0.5f);
       } else {
@@ -59,7 +62,11 @@ __global__ __launch_bounds__(1024) void k_hist(const uint8_t* B, const int* ridx
         if (MODE == 1) {
           acc ^= b + __float_as_uint(g[u].x);
         } else if (b != 255) {
-          if (MODE == 3) {
+          if (MODE == 6 || MODE == 8) {
+            unsigned long long* l64 = reinterpret_cast<unsigned long long*>(lds);
+            atomicAdd(&l64[2 * (fj * NBIN + b)], (unsigned long long)(long long)(g[u].x * 1073741824.f));
+            atomicAdd(&l64[2 * (fj * NBIN + b) + 1], (unsigned long long)(long long)(g[u].y * 1073741824.f));
+          } else if (MODE == 3 || MODE == 7) {
             atomicAdd(reinterpret_cast<uint32_t*>(&lds[2 * (fj * NBIN + b)]), (uint32_t)(g[u].x * 1024));
             atomicAdd(reinterpret_cast<uint32_t*>(&lds[2 * (fj * NBIN + b) + 1]), (uint32_t)(g[u].y * 1024));
           } else if (MODE == 4 || MODE == 5) {
@@ -81,7 +88,8 @@ __global__ __launch_bounds__(1024) void k_hist(const uint8_t* B, const int* ridx
 template <int MODE>
 float run(int threads, const uint8_t* B, const int* ridx, const float2* gp, int n, float* out) {
   const int nblk = 1024, chunk = (n + nblk - 1) / nblk;
-  const size_t lds = 2 * F * NBIN * 4;
+  const size_t lds = 2 * F * NBIN * 4 * (MODE >= 6 && MODE != 7 ? 2 : 1);
+  CK(hipFuncSetAttribute((const void*)k_hist<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
@@ -110,7 +118,10 @@ int main() {
   CK(hipMalloc(&B, hB.size()));
   CK(hipMalloc(&ridx, n * 4));
   CK(hipMalloc(&gp, n * 8));
-  CK(hipMalloc(&out, (size_t)1024 * 2 * F * NBIN * 4));
+  CK(hipMalloc(&out, (size_t)1024 * 4 * F * NBIN * 4));
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, 0));
+  printf("sharedMemPerBlock %zu maxSharedMemoryPerMultiProcessor %zu\n", prop.sharedMemPerBlock, prop.maxSharedMemoryPerMultiProcessor);
   CK(hipMemcpy(B, hB.data(), hB.size(), hipMemcpyHostToDevice));
   CK(hipMemcpy(ridx, hr.data(), n * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(gp, hg.data(), n * 8, hipMemcpyHostToDevice));
@@ -120,5 +131,8 @@ int main() {
   printf("3 atomics only u32   %.3f ms\n", run<3>(1024, B, ridx, gp, n, out));
   printf("4 planar g/h         %.3f ms\n", run<4>(1024, B, ridx, gp, n, out));
   printf("5 planar, 256 thr    %.3f ms\n", run<5>(256, B, ridx, gp, n, out));
+  printf("6 atomics only u64   %.3f ms\n", run<6>(1024, B, ridx, gp, n, out));
+  printf("7 production u32     %.3f ms\n", run<7>(1024, B, ridx, gp, n, out));
+  printf("8 production u64     %.3f ms\n", run<8>(1024, B, ridx, gp, n, out));
   return 0;
 }

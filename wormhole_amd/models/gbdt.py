@@ -397,7 +397,8 @@ class TreeBuilder:
         self.nbin = max(1, cuts.nbin_max)
         self.gpu = B.is_cuda
         self.device = B.device
-        fg = max(1, (64 * 1024) // (self.nbin * 8))  # features per LDS histogram block
+        # features per LDS histogram block: int64 (g, h) per bin in <= 160 KB
+        fg = max(1, (160 * 1024) // (self.nbin * 16))
         fg = min(fg, 64)
         if fg >= 4:
             fg -= fg % 4  # 4-aligned groups let the kernel load 4 bins per dword
@@ -407,6 +408,19 @@ class TreeBuilder:
         nb = torch.tensor([b - a for a, b in zip(o, o[1:])])
         self.bin_mask = torch.arange(self.nbin)[None, :] < nb[:, None]  # [F, nbin]
         self.valid_mask = self.bin_mask.clone()
+        self._nglobal = None
+
+    def _hist_scale(self, gpair):
+        """Fixed-point scales {2^eg, 2^eh} of the GPU histograms: the largest
+        powers of two with (global rows) * max|g| * 2^eg <= 2^61, so no node's
+        int64 sum can overflow on any rank (see csrc/hip/gbdt.hip)."""
+        if self._nglobal is None:
+            self._nglobal = max(1, int(self.bsp.allreduce_scalar(self.dm.n)))
+        m = gpair.abs().amax(0) if self.dm.n else torch.zeros(2, device=self.device)
+        m = m.float().contiguous()
+        self.bsp.allreduce(m, op="max")
+        e = torch.floor(torch.log2(2.0 ** 61 / (self._nglobal * m.double().clamp_min(1e-30))))
+        return torch.pow(2.0, e.clamp(-60, 100)).float()
 
     def sample_features(self, gen):
         """colsample_bytree: restrict this tree's candidate features."""
@@ -423,10 +437,10 @@ class TreeBuilder:
         """segs: list of (beg, end) local row ranges; slots: output slot of each."""
         hist = torch.zeros(nslot, self.F, self.nbin, 2, dtype=torch.float64, device=self.device)
         if self.gpu:
-            # ~1024 row chunks per call (two rounds of the 512 resident
+            # ~512 row chunks per call (two rounds of the 256 resident
             # 1024-thread blocks); partials are summed per (slot, group)
             total = sum(max(0, e - b) for b, e in segs)
-            chunk = max(4096, -(-total // 1024))
+            chunk = max(8192, -(-total // 512))
             G = len(self.fgroups)
             tasks, red = [], []
             for (b, e), s in zip(segs, slots):
@@ -445,7 +459,8 @@ class TreeBuilder:
                 both = both.to(self.device)
                 t = both[:5 * len(tasks)].view(-1, 5)
                 rd = both[5 * len(tasks):].view(-1, 6)
-                _native.hip().gbdt_hist(self.B, self.nbin, ridx, gpair, t, rd, self.max_fcnt, hist)
+                _native.hip().gbdt_hist(self.B, self.nbin, ridx, gpair, self._qscale, t, rd,
+                                        self.max_fcnt, hist)
         else:
             for (b, e), s in zip(segs, slots):
                 if e <= b:
@@ -492,9 +507,12 @@ class TreeBuilder:
         rest = arg // 2
         b = rest % self.nbin
         f = rest // self.nbin
-        Ls = torch.stack([cands[int(di)][1][s, f[s], b[s]] for s, di in enumerate(d.tolist())]) \
-            if S else torch.zeros(0, 2, dtype=torch.float64)
-        return bg.cpu(), f.cpu(), b.cpu(), d.cpu(), Ls.cpu()
+        Lall = torch.stack([cands[0][1], cands[1][1]], 3)  # [S, F, nbin, 2dir, 2]
+        Ls = Lall[torch.arange(S, device=arg.device), f, b, d]  # [S, 2]
+        # one device->host transfer for the whole level
+        out = torch.cat([bg[:, None].double(), f[:, None].double(), b[:, None].double(),
+                         d[:, None].double(), Ls.double()], 1).cpu()
+        return out[:, 0], out[:, 1].long(), out[:, 2].long(), out[:, 3].long(), out[:, 4:6]
 
     # ----------------------------------------------------------------- build
     def build(self, gpair, margin):
@@ -508,6 +526,9 @@ class TreeBuilder:
         self.bsp.allreduce(tot)
         totals = {root: tot.cpu()}
         seg = {root: (0, n)}
+        done = {}  # finished leaves -> their final ridx segment
+        if self.gpu:
+            self._qscale = self._hist_scale(gpair)
         hist_root = self._build_hist(ridx, gpair, [seg[root]], [0], 1)
         self.bsp.allreduce(hist_root)
         H_front = hist_root  # [len(frontier), F, nbin, 2], frontier order
@@ -576,8 +597,8 @@ class TreeBuilder:
                 build_segs.append(seg[s_])
                 build_slots.append(len(build_slots))
             for nd in frontier:
-                if nd not in split_nodes:
-                    seg.pop(nd, None)  # finished leaf: its rows are final
+                if nd not in split_nodes and nd in seg:
+                    done[nd] = seg.pop(nd)  # finished leaf: its rows are final
             hsmall = self._build_hist(ridx, gpair, build_segs, build_slots, len(build_slots))
             self.bsp.allreduce(hsmall)
             # sibling subtraction for every split node at once; the new
@@ -595,7 +616,8 @@ class TreeBuilder:
             frontier = new_frontier
         self._prune(tree)
         # margins of the training rows from the final leaf segments
-        self._apply_leaves(tree, ridx, margin, n)
+        done.update(seg)
+        self._apply_leaves(tree, ridx, margin, n, done)
         return tree
 
     def _pos_node(self, seg, n):
@@ -626,9 +648,10 @@ class TreeBuilder:
         dev = self.device
         if self.gpu:
             nleft = torch.zeros(node_feat.numel(), dtype=torch.int32, device=dev)
-            out = _native.hip().gbdt_partition(self.B, ridx, pos_node, node_feat.to(dev),
-                                               node_bin.to(dev), node_defl.to(dev),
-                                               seg_beg.to(dev), seg_end.to(dev), nleft)
+            pk = torch.stack([node_feat, node_bin, node_defl.to(torch.int32), seg_beg,
+                              seg_end]).to(dev)  # one host->device copy
+            out = _native.hip().gbdt_partition(self.B, ridx, pos_node, pk[0], pk[1],
+                                               pk[2].to(torch.uint8), pk[3], pk[4], nleft)
             return out, nleft.cpu()
         out = ridx.clone()
         nleft = torch.zeros(node_feat.numel(), dtype=torch.int32)
@@ -687,12 +710,28 @@ class TreeBuilder:
         tree.__dict__.update(t.__dict__)
         tree._remap = remap
 
-    def _apply_leaves(self, tree, ridx, margin, n):
-        # rows still sit in the segments of the (pre-prune) frontier leaves; a
-        # device tree walk on the binned values is simplest and exact
+    def _apply_leaves(self, tree, ridx, margin, n, leaf_segs):
+        """margin[row] += leaf value, for the rows of every leaf segment.
+
+        Rows sit in the ridx segments of the (pre-prune) leaves; a pruned-away
+        subtree's rows take the value of its nearest ancestor that is a leaf
+        after pruning.  Same result as walking the tree on the raw values
+        (bin <= b <=> value < cut[b]; missing follows the default direction)."""
         if n == 0:
             return
-        tree.predict_margin(self.dm.X, margin)
+        if not self.gpu:
+            tree.predict_margin(self.dm.X, margin)
+            return
+        val = torch.zeros(len(tree.feat), dtype=torch.float32)
+        for nd in leaf_segs:
+            a, top = nd, nd
+            while tree.parent[a] >= 0:
+                a = tree.parent[a]
+                if tree.is_leaf(a):
+                    top = a
+            val[nd] = tree.leaf[top]
+        pos = self._pos_node(leaf_segs, n)
+        _native.hip().gbdt_leaf_add(ridx, pos, val.to(self.device), margin)
 
 
 # ---------------------------------------------------------------- booster
