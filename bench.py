@@ -60,6 +60,8 @@ def main():
     args = ap.parse_args()
 
     local = env_local_rank()
+    if os.environ.get("WH_BENCH_SAME_GPU") == "1":
+        local = 0  # rehearsal aid: every rank on GPU 0 (1-GPU box, multi-rank code path)
     if args.device == "cuda":
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
@@ -109,6 +111,9 @@ def main():
     comm.allreduce(t, "max")
     dt = float(t.item())
     prog = learner.take_progress()
+    sizes = getattr(learner, "last_sizes", None)
+    if sizes is not None:  # last minibatch: unique keys and embedding rows per GPU
+        sizes = [int(sizes[0]), int(sizes[1].reshape(-1)[0].item()) if torch.is_tensor(sizes[1]) else int(sizes[1])]
     ex = args.batch * args.steps * n
     value = ex / dt
     if args.model == "difacto":
@@ -133,6 +138,8 @@ def main():
                        "parallelism": "dp%d+kvshard%d" % (n, n),
                        "minibatch_per_gpu": args.batch, "threshold": 100, "nnz_per_example": 39},
             "train_logloss": logloss, "train_auc": auc,
+            "uniq_keys_per_gpu_step": sizes[0] if sizes else None,
+            "emb_rows_per_gpu_step": sizes[1] if sizes else None,
         }), flush=True)
     comm.finalize()
 

@@ -1,8 +1,12 @@
 """Sharded KV over a 2-rank gloo group (the ps-lite server group re-expressed
-as all-to-all-v): variable-length DiFacto pull/push exchange on CPU."""
+as all-to-all-v): variable-length DiFacto pull/push exchange on CPU, and the
+same multi-rank code path with the HIP kernels (2 ranks sharing the GPU,
+tensors staged through gloo)."""
 import os
 import socket
 
+import numpy as np
+import pytest
 import torch
 import torch.multiprocessing as mp
 
@@ -15,7 +19,7 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, out_dir, defer=True):
+def _rank_main(rank, world, port, out_dir, defer=True, device="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     torch.set_num_threads(1)
@@ -24,27 +28,35 @@ def _rank_main(rank, world, port, out_dir, defer=True):
     from wormhole_amd.data.synthetic import criteo_batch_cpu
     from wormhole_amd.models.difacto import DifactoLearner
     from wormhole_amd.parallel.comm import Comm
-    comm = Comm(torch.device("cpu"))
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(0)
+        comm = Comm(dev, backend="gloo")
+    else:
+        comm = Comm(dev)
     emb = Embedding(dim=8, threshold=3)
     conf = DifactoConfig(embedding=[emb], lambda_l1=0.01, l1_shrk=False)
     card = [50, 400, 3000, 20, 7]
-    lr = DifactoLearner(conf, comm, "cpu", cap=1 << 14, vcap=1 << 12, seed=5)
+    lr = DifactoLearner(conf, comm, device, cap=1 << 14, vcap=1 << 12, seed=5)
     lr.defer_push = defer
     for step in range(4):
-        keys, label, off = criteo_batch_cpu(300, 17 + rank, step, card)
+        keys, label, off = [t.to(dev) for t in criteo_batch_cpu(300, 17 + rank, step, card)]
         lr.process(keys, off, None, label, 0, 0)
     # pull check: every worker sees exactly the owner's stored values
-    keys, label, off = criteo_batch_cpu(300, 99 + rank, 0, card)
+    keys, label, off = [t.to(dev) for t in criteo_batch_cpu(300, 99 + rank, 0, card)]
     uniq, ucnt, owner_cnt, lid, *_ = ops.localize(keys, off, None, comm.size)
     sess = lr.kv.open(uniq, owner_cnt, insert=False)
     hdr, vc = lr.kv.difacto_pull(sess, False)
+    hdr, vc, uniq = hdr.cpu(), vc.cpu(), uniq.cpu()
     st = lr.store
-    occ = st.occupied()
+    occ = st.occupied().long()
+    sk = st.keys[occ.to(st.keys.device)].cpu().tolist()
+    sw = st.w[occ.to(st.w.device)].cpu().tolist()
+    sv = st.vrow[occ.to(st.vrow.device)].cpu().tolist()
+    V = st.V.cpu()
     mine = {}
-    sk = st._keys if hasattr(st, "_keys") else None
-    for s in occ.tolist():
-        row = int(st._vrow[s])
-        mine[int(sk[s])] = (float(st._w[s]), None if row < 0 else st._V[row][:8].tolist())
+    for k, w, row in zip(sk, sw, sv):
+        mine[int(np.int64(k))] = (float(w), None if row < 0 else V[row][:8].tolist())
     allmaps = comm.allgather_object(mine)
     owner = {}
     for mp_ in allmaps:
@@ -76,6 +88,26 @@ def test_difacto_sharded_pull_push_two_ranks(tmp_path):
     for r in range(2):
         ll, nv = open(tmp_path / ("r%d" % r)).read().split()
         assert 0 < float(ll) < 1.0 and int(nv) > 0
+
+
+@pytest.mark.gpu
+def test_difacto_sharded_two_ranks_gpu(tmp_path):
+    """The multi-rank path (owner-grouped localize, per-segment push, V-row
+    renumbering) with the HIP kernels; same numbers as the CPU path."""
+    g, c = tmp_path / "g", tmp_path / "c"
+    g.mkdir(), c.mkdir()
+    mp.spawn(_rank_main, args=(2, _free_port(), str(g), True, "cuda"), nprocs=2, join=True)
+    mp.spawn(_rank_main, args=(2, _free_port(), str(c), True, "cpu"), nprocs=2, join=True)
+    for r in range(2):
+        lg, nvg = open(g / ("r%d" % r)).read().split()
+        lc, nvc = open(c / ("r%d" % r)).read().split()
+        assert int(nvg) == int(nvc) > 0
+        assert abs(float(lg) - float(lc)) < 1e-4 * float(lc)
+        mg, mc = torch.load(g / ("m%d" % r)), torch.load(c / ("m%d" % r))
+        assert mg.keys() == mc.keys()
+        for k in mc:
+            assert abs(mg[k][0] - mc[k][0]) < 1e-4, k
+            assert (mg[k][1] is None) == (mc[k][1] is None), k
 
 
 def test_deferred_push_is_exact(tmp_path):

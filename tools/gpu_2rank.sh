@@ -1,0 +1,13 @@
+#!/bin/bash
+# Rehearse the multi-rank GPU code paths on a 1-GPU box: RCCL refuses two
+# ranks on one device, so the ranks share GPU 0 and exchange through gloo
+# (WH_COMM_BACKEND=gloo stages tensors through host memory; timings are NOT
+# representative of xGMI, correctness is).
+set -o pipefail
+OUT=gpurun_out/${1:-two}
+mkdir -p $OUT
+timeout -k 10 600 python -m pytest tests/test_kv_exchange.py -q -x -m gpu > $OUT/test.log 2>&1 || { tail -40 $OUT/test.log; exit 1; }
+tail -2 $OUT/test.log
+WH_BENCH_SAME_GPU=1 WH_COMM_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+  --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 5 --warmup 2 > $OUT/bench2.log 2>&1 || { tail -40 $OUT/bench2.log; exit 1; }
+tail -1 $OUT/bench2.log

@@ -64,6 +64,7 @@ class DifactoLearner:
         if push_cnt:
             self.kv.difacto_push_cnt(sess, self.hp, self.threshold, self.l1_shrk, self.seed)
         hdr, vc = self.kv.difacto_pull(sess, self.l1_shrk)
+        self.last_sizes = (uniq.numel(), sess.m)  # (unique keys, embedding rows; device)
         if self.vstride == 0:  # no embedding: a plain linear model over w
             hdr, vc = hdr[:, 0].contiguous(), None
         py, dual, xv = ops.fm_forward(offset, lid, val, hdr, vc, self.vstride, label,

@@ -73,8 +73,13 @@ class Comm:
             device = torch.device("cpu")
         self.device = torch.device(device)
         if backend is None:
-            backend = "nccl" if self.device.type == "cuda" else "gloo"
+            backend = os.environ.get("WH_COMM_BACKEND") or (
+                "nccl" if self.device.type == "cuda" else "gloo")
         self.backend = backend
+        # gloo with GPU tensors (a rehearsal of the multi-rank GPU code paths
+        # with several ranks sharing one GPU, which RCCL refuses): tensors are
+        # staged through host memory around every transfer
+        self.stage = backend == "gloo" and self.device.type == "cuda"
         self.pg = None
         if self.size > 1 and init:
             if not dist.is_initialized():
@@ -92,7 +97,7 @@ class Comm:
     # ----------------------------------------------------------- basics
     def barrier(self):
         if self.size > 1:
-            if self.backend == "nccl":
+            if self.backend == "nccl" and self.device.type == "cuda":
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
@@ -102,12 +107,22 @@ class Comm:
             return t
         o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX,
              "min": dist.ReduceOp.MIN}[op]
+        if self.stage and t.is_cuda:
+            h = t.cpu()
+            dist.all_reduce(h, op=o)
+            t.copy_(h)
+            return t
         dist.all_reduce(t, op=o)
         return t
 
     def broadcast(self, t, root=0):
         if self.size > 1:
-            dist.broadcast(t, src=root)
+            if self.stage and t.is_cuda:
+                h = t.cpu()
+                dist.broadcast(h, src=root)
+                t.copy_(h)
+            else:
+                dist.broadcast(t, src=root)
         return t
 
     def allgather_object(self, obj):
@@ -120,6 +135,11 @@ class Comm:
     def allgather(self, t):
         if self.size == 1:
             return [t]
+        if self.stage and t.is_cuda:
+            h = t.cpu()
+            out = [torch.empty_like(h) for _ in range(self.size)]
+            dist.all_gather(out, h)
+            return [o.to(t.device) for o in out]
         out = [torch.empty_like(t) for _ in range(self.size)]
         dist.all_gather(out, t)
         return out
@@ -129,7 +149,8 @@ class Comm:
         """send_counts: python list (len size) -> recv_counts list."""
         if self.size == 1:
             return list(send_counts)
-        s = torch.tensor(send_counts, dtype=torch.int64, device=self.device)
+        s = torch.tensor(send_counts, dtype=torch.int64,
+                         device="cpu" if self.stage else self.device)
         r = torch.empty_like(s)
         dist.all_to_all_single(r, s)
         return r.tolist()
@@ -139,6 +160,8 @@ class Comm:
         this rank.  x may be 1-D or 2-D [rows, width]."""
         if self.size == 1:
             return x
+        if self.stage and x.is_cuda:
+            return self.all_to_all_v(x.cpu(), send_rows, recv_rows).to(x.device)
         width = x[0].numel() if x.dim() > 1 and x.shape[0] > 0 else (
             x.shape[1] if x.dim() > 1 else 1)
         shape = (sum(recv_rows),) + tuple(x.shape[1:])
@@ -161,6 +184,11 @@ class Comm:
         inputs must stay alive until then."""
         if self.size == 1:
             outs = [x for x, _, _ in items]
+            return (outs, _Done()) if async_op else outs
+        if self.stage:
+            dev = [x.device for x, _, _ in items]
+            outs = self.all_to_all_v_multi([(x.cpu(), s, r) for x, s, r in items])
+            outs = [o.to(d) for o, d in zip(outs, dev)]
             return (outs, _Done()) if async_op else outs
         outs, ops = [], []
         for x, send, recv in items:
@@ -192,6 +220,8 @@ class Comm:
         [size] on the device (no host synchronisation)."""
         if self.size == 1:
             return send_dev.clone()
+        if self.stage and send_dev.is_cuda:
+            return self.exchange_counts_dev(send_dev.cpu()).to(send_dev.device)
         r = torch.empty_like(send_dev)
         dist.all_to_all_single(r, send_dev.contiguous())
         return r
