@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -64,6 +65,36 @@ struct ConfItem {
   std::vector<ConfItem> children;
 };
 std::vector<ConfItem> ParseConf(const std::string& text);
+std::string Arg2Proto(const std::string& text);
+
+// ---- debug strings (reference learn/base/debug.h:9-43) ---------------------
+// "[n]: a0 a1 ... " with the first and last m entries when n > 2m
+template <typename V>
+std::string DebugStr(const V* data, int64_t n, int m = 5) {
+  std::string s = "[" + std::to_string(n) + "]: ";
+  auto put = [&](int64_t i) {
+    std::ostringstream o;
+    o << data[i];
+    s += o.str() + " ";
+  };
+  if (n <= 2 * m) {
+    for (int64_t i = 0; i < n; ++i) put(i);
+  } else {
+    for (int64_t i = 0; i < m; ++i) put(i);
+    s += "... ";
+    for (int64_t i = n - m; i < n; ++i) put(i);
+  }
+  return s;
+}
+
+inline std::string DebugStr(const RowBlock& b) {
+  const int64_t n = (int64_t)b.size(), nnz = (int64_t)b.nnz();
+  std::string s = "label: " + DebugStr(b.label.data(), n) + "\n" +
+                  "offset: " + DebugStr(b.offset.data(), n + 1) + "\n" +
+                  "index: " + DebugStr(b.index.data(), nnz);
+  if (!b.value.empty()) s += "\nvalue: " + DebugStr(b.value.data(), nnz);
+  return s;
+}
 
 // ---- hashing / codecs ------------------------------------------------------
 uint64_t CityHash64(const char* s, size_t len);

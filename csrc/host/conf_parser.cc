@@ -132,5 +132,84 @@ std::vector<ConfItem> ParseConf(const std::string& text) {
   return items;
 }
 
+// dmlc::Config-format text ("key = value" per entry, '#' comments, quoted
+// values, repeated keys kept in order) -> protobuf text ("key: value", string
+// values re-quoted).  The reference's unused alternative front end
+// (learn/base/arg2proto.h:13-20: dmlc::Config(in, multi_value=true)
+// .ToProtoString() then TextFormat::ParseFromString).  Nested messages are
+// not part of that format; a line "name {" is passed through unchanged so
+// files in either syntax convert.
+std::string Arg2Proto(const std::string& text) {
+  std::string out;
+  size_t i = 0;
+  const size_t n = text.size();
+  auto quote = [](const std::string& v) {
+    std::string q = "\"";
+    for (char c : v) {
+      if (c == '"' || c == '\\') q += '\\';
+      if (c == '\n') { q += "\\n"; continue; }
+      q += c;
+    }
+    return q + "\"";
+  };
+  while (i < n) {
+    size_t e = text.find('\n', i);
+    if (e == std::string::npos) e = n;
+    std::string line = text.substr(i, e - i);
+    i = e + 1;
+    // strip comments outside quotes
+    bool inq = false;
+    char qc = 0;
+    for (size_t k = 0; k < line.size(); ++k) {
+      const char c = line[k];
+      if (inq) {
+        if (c == '\\') ++k;
+        else if (c == qc) inq = false;
+      } else if (c == '"' || c == '\'') {
+        inq = true;
+        qc = c;
+      } else if (c == '#') {
+        line.resize(k);
+        break;
+      }
+    }
+    auto trim = [](std::string s) {
+      size_t b = 0, t = s.size();
+      while (b < t && std::isspace((unsigned char)s[b])) ++b;
+      while (t > b && std::isspace((unsigned char)s[t - 1])) --t;
+      return s.substr(b, t - b);
+    };
+    line = trim(line);
+    if (line.empty()) continue;
+    size_t eq = std::string::npos;
+    for (size_t k = 0; k < line.size(); ++k)
+      if (line[k] == '=' || line[k] == ':') { eq = k; break; }
+    if (eq == std::string::npos) {  // "name {" / "}" of a nested message
+      out += line + "\n";
+      continue;
+    }
+    const std::string key = trim(line.substr(0, eq));
+    std::string val = trim(line.substr(eq + 1));
+    if (key.empty()) throw std::runtime_error("arg2proto: empty key in line: " + line);
+    if (val.size() >= 2 && (val[0] == '"' || val[0] == '\'') && val.back() == val[0]) {
+      std::string raw;
+      for (size_t k = 1; k + 1 < val.size(); ++k) {
+        if (val[k] == '\\' && k + 2 < val.size()) {
+          const char c = val[++k];
+          raw += c == 'n' ? '\n' : c == 't' ? '\t' : c;
+        } else {
+          raw += val[k];
+        }
+      }
+      out += key + ": " + quote(raw) + "\n";
+    } else if (val == "{") {
+      out += key + " {\n";
+    } else {
+      out += key + ": " + val + "\n";
+    }
+  }
+  return out;
+}
+
 }  // namespace host
 }  // namespace wh

@@ -135,6 +135,24 @@ py::tuple localize_cpu(const Tensor& keys, const Tensor& offset, const c10::opti
 
 void register_all(py::module& m) {
   m.def("parse_conf", [](const std::string& text) { return conf_to_py(ParseConf(text)); });
+  m.def("arg2proto", &Arg2Proto, "dmlc::Config-format text -> protobuf text format");
+  m.def("debug_str", [](const Tensor& t, int m) {
+    auto c = t.detach().cpu().contiguous().reshape({-1});
+    const int64_t n = c.numel();
+    switch (c.scalar_type()) {
+      case torch::kFloat32: return DebugStr(c.data_ptr<float>(), n, m);
+      case torch::kFloat64: return DebugStr(c.data_ptr<double>(), n, m);
+      case torch::kInt32: return DebugStr(c.data_ptr<int32_t>(), n, m);
+      case torch::kInt64: return DebugStr(c.data_ptr<int64_t>(), n, m);
+      default: return DebugStr(c.to(torch::kFloat64).data_ptr<double>(), n, m);
+    }
+  }, py::arg("t"), py::arg("m") = 5);
+  m.def("debug_str_block", [](const Tensor& keys, const Tensor& offset,
+                              const c10::optional<Tensor>& val, const Tensor& label) {
+    return DebugStr(py_to_block(keys.cpu(), offset.cpu(),
+                                val ? c10::optional<Tensor>(val->cpu()) : c10::nullopt,
+                                label.cpu(), c10::nullopt));
+  }, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(), py::arg("label"));
   m.def("cityhash64", [](py::bytes b) {
     std::string s = b;
     return CityHash64(s.data(), s.size());

@@ -64,6 +64,19 @@ def parse_text(cls, text, base=None):
     return _apply(obj, _native.host().parse_conf(text))
 
 
+def arg2proto(text):
+    """dmlc::Config-format text -> protobuf text (native; the reference's
+    alternative front end, learn/base/arg2proto.h:13-20)."""
+    return _native.host().arg2proto(text)
+
+
+def load_dmlc(cls, conf_path):
+    """Load a dmlc::Config-style conf (``key = value`` lines, repeated keys
+    allowed) into a schema object through :func:`arg2proto`."""
+    with open(conf_path) as f:
+        return parse_text(cls, arg2proto(f.read()))
+
+
 def load(cls, conf_path, argv=()):
     """Reference ArgParser: ReadFile(conf) then ReadArgs(argv) (later wins)."""
     obj = cls()
