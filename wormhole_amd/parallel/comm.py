@@ -185,7 +185,7 @@ class Comm:
         if self.size == 1:
             outs = [x for x, _, _ in items]
             return (outs, _Done()) if async_op else outs
-        if self.stage:
+        if self.stage and any(x.is_cuda for x, _, _ in items):
             dev = [x.device for x, _, _ in items]
             outs = self.all_to_all_v_multi([(x.cpu(), s, r) for x, s, r in items])
             outs = [o.to(d) for o, d in zip(outs, dev)]
