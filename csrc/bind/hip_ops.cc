@@ -59,9 +59,17 @@ Tensor scan_excl(const Tensor& in) {
 
 // -------------------------------------------------------------- localize
 // Returns (uniq i64[U], ucnt i32[U], owner_cnt i64[P], lid i32[nnz],
-//          csc_off i64[U+1], csc_row i32[nnz], csc_val f32[nnz|0])
+//          csc_off i64[U+1], csc_row i32[nnz], csc_val f32[nnz|0], recv i64[2W|0])
+//
+// exchange (multi-rank): a callable that takes the device owner counts
+// i64[nshard + 1] (last = table-overflow count) and returns the device i64
+// [2W] {count from rank q, overflow flag of rank q} of a count all-to-all.
+// It runs before the one host read, so the read returns both this rank's
+// counts and its peers' (one synchronisation per minibatch instead of two).
+// Every rank sees every rank's overflow flag, so all ranks retry together.
 std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
-                             const c10::optional<Tensor>& val, int64_t nshard, int64_t hint) {
+                             const c10::optional<Tensor>& val, int64_t nshard, int64_t hint,
+                             py::object exchange) {
   CHECK_IN(keys, torch::kInt64);
   CHECK_IN(offset, torch::kInt64);
   TORCH_CHECK(nshard >= 1 && nshard <= 1024, "nshard out of range");
@@ -81,7 +89,8 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
   const int64_t safe = next_pow2(std::max<int64_t>(2 * nnz, 1024));
   int64_t tsize = hint > 0 ? std::min(safe, next_pow2(std::max<int64_t>(hint * 5 / 2, 1024)))
                            : safe;
-  Tensor tkeys, slot_of, owner_cnt, owner_cnt_h;
+  Tensor tkeys, slot_of, owner_cnt, owner_cnt_h, recv_h;
+  const bool ex = !exchange.is_none();
   while (true) {
     tkeys = torch::full({tsize}, -1, i64);
     slot_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
@@ -92,8 +101,22 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
     wh::loc_owner_hist(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
                        ptr<int64_t>(owner_cnt), s);
     // the number of unique keys sizes everything downstream: one host sync
-    owner_cnt_h = owner_cnt.to(torch::kCPU);
-    if (owner_cnt_h.data_ptr<int64_t>()[nshard] == 0 || tsize >= safe) break;
+    if (ex) {
+      Tensor recv = exchange(owner_cnt).cast<Tensor>();
+      TORCH_CHECK(recv.scalar_type() == torch::kInt64 && recv.numel() % 2 == 0,
+                  "localize: exchange must return int64 [2 * world]");
+      auto both = torch::cat({owner_cnt, recv.reshape({-1})}).to(torch::kCPU);
+      owner_cnt_h = both.narrow(0, 0, nshard + 1);
+      recv_h = both.narrow(0, nshard + 1, recv.numel()).contiguous();
+      const bool own = owner_cnt_h.data_ptr<int64_t>()[nshard] != 0;
+      bool over = own;
+      for (int64_t q = 1; q < recv_h.numel(); q += 2) over |= recv_h.data_ptr<int64_t>()[q] != 0;
+      if (!over) break;
+      TORCH_CHECK(!(own && tsize >= safe), "localize: table overflow");
+    } else {
+      owner_cnt_h = owner_cnt.to(torch::kCPU);
+      if (owner_cnt_h.data_ptr<int64_t>()[nshard] == 0 || tsize >= safe) break;
+    }
     tsize = safe;
   }
   TORCH_CHECK(owner_cnt_h.data_ptr<int64_t>()[nshard] == 0, "localize: table overflow");
@@ -127,7 +150,8 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
               ptr<int32_t>(lid), wp, wp + n1, wp + 2 * n1, stmp.data_ptr(), sbytes,
               ptr<int64_t>(csc_off), ptr<int32_t>(ucnt), ptr<int32_t>(csc_row),
               vp ? ptr<float>(csc_val) : nullptr, s);
-  return {uniq, ucnt, owner_cnt_h, lid, csc_off, csc_row, csc_val};
+  if (!recv_h.defined()) recv_h = torch::empty({0}, torch::kInt64);
+  return {uniq, ucnt, owner_cnt_h, lid, csc_off, csc_row, csc_val, recv_h};
 }
 
 // --------------------------------------------------------------- KVStore
@@ -643,7 +667,7 @@ PYBIND11_MODULE(_hip, m) {
   m.doc() = "wormhole_amd gfx950 HIP kernels";
   m.def("scan_excl", &scan_excl);
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
-        py::arg("nshard") = 1, py::arg("hint") = 0);
+        py::arg("nshard") = 1, py::arg("hint") = 0, py::arg("exchange") = py::none());
   m.def("fm_forward", &fm_forward);
   m.def("fm_backward", &fm_backward);
   m.def("fm_grad_post", &fm_grad_post);

@@ -119,3 +119,41 @@ def test_deferred_push_is_exact(tmp_path):
     for r in range(2):
         assert open(a / ("r%d" % r)).read() == open(b / ("r%d" % r)).read()
         assert torch.load(a / ("m%d" % r)) == torch.load(b / ("m%d" % r))
+
+
+def _localize_ex_main(rank, world, port, device):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    from wormhole_amd import ops
+    from wormhole_amd.kv import ShardedKV, make_store
+    from wormhole_amd.parallel.comm import Comm
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(0)
+        comm = Comm(dev, backend="gloo")
+    else:
+        comm = Comm(dev)
+    kv = ShardedKV(make_store(1 << 12, 0, 0, dev), comm)
+    g = torch.Generator().manual_seed(rank)
+    nnz = 20000
+    keys = torch.randint(0, 1 << 40, (nnz,), generator=g).to(dev)
+    off = torch.arange(0, nnz + 1, 4, dtype=torch.int64).to(dev)
+    # rank 0 under-sizes its scratch table (hint 1): on the GPU it overflows
+    # and BOTH ranks must retry the fused count exchange together
+    hint = 1 if rank == 0 else 0
+    a = ops.localize(keys, off, None, comm.size, hint, exchange=kv.count_exchange())
+    b = ops.localize(keys, off, None, comm.size, 0)
+    # (the order of ids inside an owner group follows the GPU hash table,
+    # which concurrent inserts may permute; the key of every nnz may not change)
+    assert torch.equal(a[2].cpu(), b[2].cpu())
+    assert torch.equal(torch.sort(a[0].cpu())[0], torch.sort(b[0].cpu())[0])
+    assert torch.equal(a[0][a[3].long()].cpu(), keys.cpu())
+    assert a[7] == comm.exchange_counts([int(x) for x in b[2].tolist()])
+    comm.barrier()
+    comm.finalize()
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_localize_fused_count_exchange(device):
+    mp.spawn(_localize_ex_main, args=(2, _free_port(), device), nprocs=2, join=True)

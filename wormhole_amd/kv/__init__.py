@@ -70,17 +70,33 @@ class ShardedKV:
             handle.wait()
             apply()
 
-    def open(self, uniq, owner_cnt, insert, cnt=None):
+    def count_exchange(self):
+        """The per-minibatch key-count all-to-all, for ops.localize to run
+        before its host read (None on one rank).  Each rank sends every peer
+        {keys for that peer, own table-overflow flag}."""
+        if self.comm.size == 1:
+            return None
+        P, ns = self.comm.size, self.nshard
+
+        def ex(owner_cnt):
+            send = torch.zeros(2 * P, dtype=torch.int64, device=owner_cnt.device)
+            send[0:2 * ns:2] = owner_cnt[:ns]
+            send[1::2] = owner_cnt[ns]
+            return self.comm.exchange_counts_dev(send)
+        return ex
+
+    def open(self, uniq, owner_cnt, insert, cnt=None, recv=None):
         """Send this minibatch's unique keys to their owners (plus, for the
         DiFacto count push, their counts in the same exchange) and resolve
-        them to owner-side slots."""
+        them to owner-side slots.  recv: the per-rank receive counts when the
+        count exchange already ran inside localize."""
         send = [int(x) for x in (owner_cnt.tolist() if hasattr(owner_cnt, "tolist") else owner_cnt)]
         send += [0] * (self.comm.size - len(send))
         if self.comm.size == 1:
             sess = Session(send, send, uniq)
             sess.cnt = cnt
         else:
-            recv = self.comm.exchange_counts(send)
+            recv = self.comm.exchange_counts(send) if recv is None else [int(r) for r in recv]
             if cnt is None:
                 keys = self.comm.all_to_all_v(uniq, send, recv)
                 sess = Session(send, recv, keys)

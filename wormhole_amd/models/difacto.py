@@ -56,11 +56,13 @@ class DifactoLearner:
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0):
         """One minibatch. Returns predictions (py) for PRED, else None."""
         train = wtype == TRAIN
-        uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = ops.localize(
-            keys, offset, val, self.kv.nshard, self.uhint)
+        ex = self.kv.count_exchange()
+        loc = ops.localize(keys, offset, val, self.kv.nshard, self.uhint, exchange=ex)
+        uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
         self.uhint = uniq.numel()
         push_cnt = train and data_pass == 0 and self.dim > 0
-        sess = self.kv.open(uniq, owner_cnt, insert=train, cnt=ucnt if push_cnt else None)
+        sess = self.kv.open(uniq, owner_cnt, insert=train, cnt=ucnt if push_cnt else None,
+                            recv=loc[7] if ex is not None else None)
         if push_cnt:
             self.kv.difacto_push_cnt(sess, self.hp, self.threshold, self.l1_shrk, self.seed)
         hdr, vc = self.kv.difacto_pull(sess, self.l1_shrk)

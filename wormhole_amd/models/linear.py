@@ -34,10 +34,11 @@ class LinearLearner:
 
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0):
         train = wtype == TRAIN
-        uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = ops.localize(
-            keys, offset, val, self.kv.nshard, self.uhint)
+        ex = self.kv.count_exchange()
+        loc = ops.localize(keys, offset, val, self.kv.nshard, self.uhint, exchange=ex)
+        uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
         self.uhint = uniq.numel()
-        sess = self.kv.open(uniq, owner_cnt, insert=train)
+        sess = self.kv.open(uniq, owner_cnt, insert=train, recv=loc[7] if ex is not None else None)
         w = self.kv.linear_pull(sess)
         py, dual, _ = ops.fm_forward(offset, lid, val, w, None, 0, label, self.conf.loss, self.met)
         self.auc_sum += ops.auc(py, label)

@@ -3,6 +3,8 @@
 (:mod:`wormhole_amd.ops.ref`).  There is no silent fallback: a GPU tensor
 with the HIP extension missing raises.
 """
+import torch
+
 from .. import _native
 from . import ref
 
@@ -21,14 +23,27 @@ def vstride_for(dim):
     return ref.vstride_for(dim)
 
 
-def localize(keys, offset, val=None, nshard=1, hint=0):
+def localize(keys, offset, val=None, nshard=1, hint=0, exchange=None):
     """Unique feature ids of a minibatch (grouped by owner shard), per-id
     counts, the nnz->local-id map and the per-id occurrence lists (CSC).
     hint: expected number of unique ids (e.g. the previous minibatch's); it
-    sizes the GPU scratch table (a wrong hint costs a retry, never a result)."""
+    sizes the GPU scratch table (a wrong hint costs a retry, never a result).
+
+    exchange (multi-rank, see ShardedKV.count_exchange): the owner counts are
+    exchanged with the peers inside localize, before its one host read; then
+    an 8th result, the list of key counts received from each rank, is
+    returned."""
     if _gpu(keys):
-        return _native.hip().localize(keys, offset, val, nshard, int(hint))
-    return _native.host().localize_cpu(keys, offset, val, nshard)
+        out = _native.hip().localize(keys, offset, val, nshard, int(hint), exchange)
+        if exchange is None:
+            return tuple(out[:7])
+        return tuple(out[:7]) + (out[7][0::2].tolist(),)
+    out = tuple(_native.host().localize_cpu(keys, offset, val, nshard))
+    if exchange is None:
+        return out
+    oc = out[2]
+    dev = torch.cat([oc.to(torch.int64), torch.zeros(1, dtype=torch.int64)])
+    return out + (exchange(dev)[0::2].tolist(),)
 
 
 def fm_forward(offset, lid, val, w_or_hdr, vc, vstride, label, loss, met):
