@@ -89,7 +89,7 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
   const int64_t safe = next_pow2(std::max<int64_t>(2 * nnz, 1024));
   int64_t tsize = hint > 0 ? std::min(safe, next_pow2(std::max<int64_t>(hint * 5 / 2, 1024)))
                            : safe;
-  Tensor tkeys, slot_of, owner_cnt, owner_cnt_h, recv_h;
+  Tensor tkeys, slot_of, owner_cnt, owner_cnt_h, recv_h, blkoff;
   const bool ex = !exchange.is_none();
   while (true) {
     tkeys = torch::full({tsize}, -1, i64);
@@ -98,8 +98,9 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
     wh::loc_insert(reinterpret_cast<const uint64_t*>(keys.data_ptr()), nnz,
                    reinterpret_cast<uint64_t*>(tkeys.data_ptr()), tsize, ptr<int32_t>(slot_of),
                    ptr<int64_t>(owner_cnt) + nshard, s);
-    wh::loc_owner_hist(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
-                       ptr<int64_t>(owner_cnt), s);
+    blkoff = torch::empty({nshard * wh::loc_owner_blocks(tsize)}, i64);
+    wh::loc_owner_count(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
+                        ptr<int64_t>(blkoff), ptr<int64_t>(owner_cnt), s);
     // the number of unique keys sizes everything downstream: one host sync
     if (ex) {
       Tensor recv = exchange(owner_cnt).cast<Tensor>();
@@ -122,16 +123,11 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
   TORCH_CHECK(owner_cnt_h.data_ptr<int64_t>()[nshard] == 0, "localize: table overflow");
   owner_cnt_h = owner_cnt_h.narrow(0, 0, nshard).contiguous();
   int64_t U = 0;
-  std::vector<int64_t> cursor_h(nshard);
-  for (int64_t p = 0; p < nshard; ++p) {
-    cursor_h[p] = U;
-    U += owner_cnt_h.data_ptr<int64_t>()[p];
-  }
-  auto cursor = torch::from_blob(cursor_h.data(), {nshard}, torch::kInt64).to(keys.device());
+  for (int64_t p = 0; p < nshard; ++p) U += owner_cnt_h.data_ptr<int64_t>()[p];
   auto tlid = torch::empty({tsize}, i32);
   auto uniq = torch::empty({U}, i64);
   wh::loc_assign(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
-                 ptr<int64_t>(cursor), ptr<int32_t>(tlid),
+                 ptr<int64_t>(blkoff), ptr<int32_t>(tlid),
                  reinterpret_cast<uint64_t*>(uniq.data_ptr()), s);
   auto row_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
   wh::row_of_nnz(ptr<int64_t>(offset), nrows, ptr<int32_t>(row_of), s);
@@ -183,7 +179,7 @@ class KVStore {
       VG_ = torch::zeros({std::max<int64_t>(vcap, 1), vstride_}, f32);
     }
     vnext_ = torch::zeros({1}, f32.dtype(torch::kInt32));
-    stats_ = torch::zeros({8}, f32.dtype(torch::kInt64));
+    stats_ = torch::zeros({wh::kStatShards, wh::kStatStride}, f32.dtype(torch::kInt64));
     cap_ = cap;
     vcap_ = dim > 0 ? vcap : 0;
   }
@@ -713,5 +709,14 @@ PYBIND11_MODULE(_hip, m) {
       .def_readonly("V", &KVStore::V_)
       .def_readonly("VG", &KVStore::VG_)
       .def_readonly("vnext", &KVStore::vnext_)
-      .def_readonly("stats", &KVStore::stats_);
+      .def_property_readonly("stats", [](const KVStore& k) {
+        // counters summed over their shards: [8] int64 (a copy)
+        return k.stats_.narrow(1, 0, wh::kStatCount).sum(0);
+      })
+      .def("reset_stats", [](KVStore& k, int64_t i0, int64_t i1) {
+        k.stats_.narrow(1, i0, i1 - i0).zero_();
+      })
+      .def("add_stat", [](KVStore& k, int64_t i, int64_t v) {
+        k.stats_.select(1, i).narrow(0, 0, 1).add_(v);
+      });
 }

@@ -22,6 +22,13 @@ __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// counter `idx` of this wave's shard (see kStatShards)
+__device__ __forceinline__ unsigned long long* stat_ptr(int64_t* stats, int idx) {
+  const int shard =
+      (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kStatShards - 1));
+  return reinterpret_cast<unsigned long long*>(stats + shard * kStatStride + idx);
+}
+
 __global__ __launch_bounds__(kThreads) void k_kv_find(const uint64_t* keys_in, int64_t n,
                                                       KVSlot* tsl, int64_t cap, int insert,
                                                       int32_t* slot, int64_t* stats) {
@@ -49,8 +56,8 @@ __global__ __launch_bounds__(kThreads) void k_kv_find(const uint64_t* keys_in, i
   }
   const uint64_t bc = __ballot(created), bf = __ballot(failed);
   if ((threadIdx.x & 63) == 0) {
-    if (bc) atomicAdd((unsigned long long*)(stats + 4), (unsigned long long)__popcll(bc));
-    if (bf) atomicAdd((unsigned long long*)(stats + 2), (unsigned long long)__popcll(bf));
+    if (bc) atomicAdd(stat_ptr(stats, 4), (unsigned long long)__popcll(bc));
+    if (bf) atomicAdd(stat_ptr(stats, 2), (unsigned long long)__popcll(bf));
   }
 }
 
@@ -79,7 +86,7 @@ __device__ __forceinline__ float l1l2_solve(float z, float eta, float l1, float 
 __device__ __forceinline__ void count_nnz_delta(float oldw, float neww, int64_t* stats) {
   const int d = (oldw == 0.f && neww != 0.f) ? 1 : ((oldw != 0.f && neww == 0.f) ? -1 : 0);
   long long s = wave_sum_ll(d);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd((unsigned long long*)(stats + 0), (unsigned long long)s);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(stat_ptr(stats, 0), (unsigned long long)s);
 }
 
 __global__ __launch_bounds__(kThreads) void k_linear_pull(const KVSlot* tsl, const int32_t* slot,
@@ -144,7 +151,7 @@ __device__ __forceinline__ int32_t wave_alloc_rows(const KVTable& t, bool want) 
   if (!want) return -1;
   const int32_t row = base + (int32_t)__popcll(m & ((1ull << lane) - 1));
   if (row >= t.vcap) {
-    atomicAdd((unsigned long long*)(t.stats + 3), 1ull);
+    atomicAdd(stat_ptr(t.stats, 3), 1ull);
     return -1;
   }
   return row;
@@ -195,7 +202,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const 
     if (src >= 0) init_v_row(t, js, jr, gl, G, hp);
   });
   newv = wave_sum_ll(newv);
-  if (lane == 0 && newv) atomicAdd((unsigned long long*)(t.stats + 1), (unsigned long long)newv);
+  if (lane == 0 && newv) atomicAdd(stat_ptr(t.stats, 1), (unsigned long long)newv);
 }
 
 __global__ __launch_bounds__(kThreads) void k_difacto_pull_hdr(KVTable t, const int32_t* slot,
@@ -337,7 +344,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int3
     }
   });
   newv = wave_sum_ll(newv);
-  if (lane == 0 && newv) atomicAdd((unsigned long long*)(t.stats + 1), (unsigned long long)newv);
+  if (lane == 0 && newv) atomicAdd(stat_ptr(t.stats, 1), (unsigned long long)newv);
 }
 
 __global__ __launch_bounds__(kThreads) void k_gather_rows(const float* in, const int32_t* idx,

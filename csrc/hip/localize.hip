@@ -10,9 +10,10 @@
 //                 find-or-insert the tile's distinct ids into a batch hash
 //                 table (one CAS per NEW id; hot ids cost one plain load per
 //                 tile). Writes slot_of[nnz].
-//   loc_owner_hist / loc_assign : compact the occupied slots into local ids,
-//                 grouped by owning shard so the id order IS the send order
-//                 of the key exchange (no separate partition pass).
+//   loc_owner_count / loc_assign : compact the occupied slots into local
+//                 ids, grouped by owning shard so the id order IS the send
+//                 order of the key exchange (no separate partition pass);
+//                 per-block owner counts + one scan, no global atomics.
 //   loc_csc     : lid[j] = tlid[slot_of[j]] (the nnz -> local id map), then
 //                 a radix sort of (lid, j) pairs on ceil(log2 U) bits
 //                 (rocPRIM onesweep; stable, so every id's occurrence list
@@ -43,9 +44,9 @@ __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
 
 // returns the slot, or -1 once the probe sequence has visited every slot
 // (table full: the caller flags an overflow and the host retries larger)
-__device__ __forceinline__ int64_t table_insert(uint64_t* tkeys, uint64_t mask, uint64_t k) {
-  uint64_t h = mix64(k) & mask;
-  for (uint64_t probe = 0; probe <= mask; ++probe) {
+__device__ __forceinline__ int64_t table_insert_from(uint64_t* tkeys, uint64_t mask, uint64_t k,
+                                                     uint64_t h) {
+  for (uint64_t probe = 0; probe < mask; ++probe) {
     uint64_t prev = ld_relaxed(tkeys + h);
     if (prev == k) return (int64_t)h;
     if (prev == kEmptyKey) {
@@ -69,12 +70,17 @@ __global__ __launch_bounds__(kThreads) void k_loc_insert(const uint64_t* __restr
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * kTileItems;
   int ls[kPer];
+  uint64_t kin[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {  // all key loads in flight before the LDS work
+    const int64_t j = base + r * kThreads + threadIdx.x;
+    kin[r] = j < nnz ? keys[j] : kEmptyKey;
+  }
 #pragma unroll
   for (int r = 0; r < kPer; ++r) {
-    const int64_t j = base + r * kThreads + threadIdx.x;
+    const uint64_t k = kin[r];
     ls[r] = -1;
-    if (j < nnz) {
-      const uint64_t k = keys[j];
+    if (k != kEmptyKey) {
       int h = (int)(mix64(k) & (kLds - 1));
       while (true) {
         unsigned long long prev = __hip_atomic_load(&sk[h], __ATOMIC_RELAXED,
@@ -91,13 +97,34 @@ __global__ __launch_bounds__(kThreads) void k_loc_insert(const uint64_t* __restr
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kLds; i += kThreads) {
-    const uint64_t k = sk[i];
-    if (k != kEmptyKey) {
-      const int64_t g = table_insert(tkeys, tmask, k);
-      if (g < 0) atomicAdd((unsigned long long*)overflow, 1ull);
-      sg[i] = g >= 0 ? (int32_t)g : 0;
-    }
+  // Global find-or-insert of the tile's distinct ids, batched so that every
+  // thread has all its probes in flight at once: round 1 loads the home slot
+  // of each id, round 2 CASes the ids whose home slot was empty; only ids
+  // that met another id (load factor ~0.25: rare) walk the probe sequence.
+  constexpr int kSlotsPer = kLds / kThreads;
+  uint64_t gk[kSlotsPer], gh[kSlotsPer], gp[kSlotsPer];
+#pragma unroll
+  for (int q = 0; q < kSlotsPer; ++q) {
+    gk[q] = sk[q * kThreads + threadIdx.x];
+    gh[q] = mix64(gk[q]) & tmask;
+    gp[q] = gk[q] != kEmptyKey ? ld_relaxed(tkeys + gh[q]) : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < kSlotsPer; ++q) {
+    if (gk[q] != kEmptyKey && gp[q] == kEmptyKey)
+      gp[q] = atomicCAS((unsigned long long*)(tkeys + gh[q]), (unsigned long long)kEmptyKey,
+                        (unsigned long long)gk[q]);
+    // gp[q] is now kEmptyKey (we inserted), gk[q] (present) or another id
+  }
+#pragma unroll
+  for (int q = 0; q < kSlotsPer; ++q) {
+    const uint64_t k = gk[q];
+    if (k == kEmptyKey) continue;
+    int64_t g = (int64_t)gh[q];
+    if (gp[q] != kEmptyKey && gp[q] != k)
+      g = table_insert_from(tkeys, tmask, k, (gh[q] + 1) & tmask);
+    if (g < 0) atomicAdd((unsigned long long*)overflow, 1ull);
+    sg[q * kThreads + threadIdx.x] = g >= 0 ? (int32_t)g : 0;
   }
   __syncthreads();
 #pragma unroll
@@ -107,32 +134,84 @@ __global__ __launch_bounds__(kThreads) void k_loc_insert(const uint64_t* __restr
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_owner_hist(const uint64_t* __restrict__ tkeys,
-                                                         int64_t tsize, int nshard,
-                                                         int64_t* owner_cnt) {
+constexpr int kAssignPer = 16;
+constexpr int64_t kAssignItems = (int64_t)kThreads * kAssignPer;  // table slots per block
+
+// Per-block owner histogram of the occupied table slots, written owner-major
+// (blkcnt[owner * nblk + block]) so that one exclusive scan gives every
+// block's first local id in every owner group -- no same-address atomics
+// (each costs ~12 ns serialised; 2K blocks x 2 passes were ~45 us).
+__global__ __launch_bounds__(kThreads) void k_owner_count(const uint64_t* __restrict__ tkeys,
+                                                          int64_t tsize, int nshard,
+                                                          int64_t* __restrict__ blkcnt) {
   __shared__ int32_t h[kMaxShard];
   for (int i = threadIdx.x; i < nshard; i += kThreads) h[i] = 0;
   __syncthreads();
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < tsize;
-       i += (int64_t)gridDim.x * kThreads) {
-    const uint64_t k = tkeys[i];
-    if (k != kEmptyKey) atomicAdd(&h[owner_of(k, nshard)], 1);
+  const int64_t base = (int64_t)blockIdx.x * kAssignItems;
+#pragma unroll
+  for (int r = 0; r < kAssignPer; ++r) {
+    const int64_t i = base + (int64_t)r * kThreads + threadIdx.x;
+    if (i < tsize) {
+      const uint64_t k = tkeys[i];
+      if (k != kEmptyKey) {
+        if (nshard == 1) {
+          const uint64_t b = __ballot(1);
+          if ((threadIdx.x & 63) == __ffsll((unsigned long long)b) - 1)
+            atomicAdd(&h[0], (int)__popcll(b));
+        } else {
+          atomicAdd(&h[owner_of(k, nshard)], 1);
+        }
+      }
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < nshard; i += kThreads)
-    if (h[i]) atomicAdd((unsigned long long*)(owner_cnt + i), (unsigned long long)h[i]);
+    blkcnt[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
 }
 
-constexpr int kAssignPer = 16;
+// Single-block exclusive scan of n (<= a few 100K) int64 counts in place,
+// then owner totals: owner_cnt[o] = sum of blkcnt[o * nblk .. (o+1) * nblk).
+__global__ __launch_bounds__(1024) void k_owner_scan(int64_t* __restrict__ blk, int64_t nblk,
+                                                     int nshard, int64_t* __restrict__ owner_cnt) {
+  __shared__ int64_t part[1024];
+  const int64_t n = nblk * nshard;
+  const int64_t per = (n + 1023) / 1024;
+  const int64_t b = threadIdx.x * per, e = b + per < n ? b + per : n;
+  int64_t acc = 0;
+  for (int64_t i = b; i < e; ++i) acc += blk[i];
+  part[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    const int64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+  for (int64_t i = b; i < e; ++i) {
+    const int64_t c = blk[i];
+    blk[i] = run;
+    run += c;
+  }
+  __syncthreads();
+  const int64_t total = part[1023];
+  for (int o = threadIdx.x; o < nshard; o += 1024) {
+    const int64_t lo = blk[(int64_t)o * nblk];
+    const int64_t hi = o + 1 < nshard ? blk[(int64_t)(o + 1) * nblk] : total;
+    owner_cnt[o] = hi - lo;
+  }
+}
+
+// lid of every occupied slot: the block's scanned offset in its owner group
+// plus the slot's rank among the block's slots of that owner.
 __global__ __launch_bounds__(kThreads) void k_assign(const uint64_t* __restrict__ tkeys,
                                                      int64_t tsize, int nshard,
-                                                     int64_t* owner_cursor, int32_t* tlid,
-                                                     uint64_t* uniq) {
+                                                     const int64_t* __restrict__ blkoff,
+                                                     int32_t* tlid, uint64_t* uniq) {
   __shared__ int32_t lh[kMaxShard];
-  __shared__ int64_t lb[kMaxShard];
   for (int i = threadIdx.x; i < nshard; i += kThreads) lh[i] = 0;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kThreads * kAssignPer;
+  const int64_t base = (int64_t)blockIdx.x * kAssignItems;
   int own[kAssignPer], rk[kAssignPer];
 #pragma unroll
   for (int r = 0; r < kAssignPer; ++r) {
@@ -147,16 +226,11 @@ __global__ __launch_bounds__(kThreads) void k_assign(const uint64_t* __restrict_
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nshard; i += kThreads)
-    if (lh[i])
-      lb[i] = (int64_t)atomicAdd((unsigned long long*)(owner_cursor + i),
-                                 (unsigned long long)lh[i]);
-  __syncthreads();
 #pragma unroll
   for (int r = 0; r < kAssignPer; ++r) {
     if (own[r] >= 0) {
       const int64_t i = base + (int64_t)r * kThreads + threadIdx.x;
-      const int64_t lid = lb[own[r]] + rk[r];
+      const int64_t lid = blkoff[(int64_t)own[r] * gridDim.x + blockIdx.x] + rk[r];
       tlid[i] = (int32_t)lid;
       uniq[lid] = tkeys[i];
     }
@@ -178,7 +252,7 @@ __global__ __launch_bounds__(kThreads) void k_loc_lid(const int32_t* __restrict_
   const int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (j < nnz) {
     lid[j] = tlid[slot_of[j]];
-    pos[j] = (int32_t)j;
+    if (pos) pos[j] = (int32_t)j;
   }
 }
 
@@ -194,9 +268,11 @@ __global__ __launch_bounds__(kThreads) void k_loc_csc(const int32_t* __restrict_
     if (p == nnz) csc_off[nuniq] = nnz;
     return;
   }
-  const int32_t j = spos[p];
-  csc_row[p] = row_of[j];
-  if (val) csc_val[p] = val[j];
+  if (spos) {  // valued data: rows and values gathered through the sorted positions
+    const int32_t j = spos[p];
+    csc_row[p] = row_of[j];
+    csc_val[p] = val[j];
+  }  // (binary data: the sort carried the row ids straight into csc_row)
   const int32_t k = slid[p];
   if (p == 0 || slid[p - 1] != k) csc_off[k] = p;  // every id occurs at least once
 }
@@ -223,18 +299,21 @@ void loc_insert(const uint64_t* keys, int64_t nnz, uint64_t* tkeys, int64_t tsiz
                      (uint64_t)(tsize - 1), slot_of, overflow);
 }
 
-void loc_owner_hist(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* owner_cnt,
-                    hipStream_t s) {
-  hipLaunchKernelGGL(k_owner_hist, dim3(grid_for(tsize, kThreads, 2048)), dim3(kThreads), 0, s,
-                     tkeys, tsize, nshard, owner_cnt);
+int64_t loc_owner_blocks(int64_t tsize) { return (tsize + kAssignItems - 1) / kAssignItems; }
+
+void loc_owner_count(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* blkcnt,
+                     int64_t* owner_cnt, hipStream_t s) {
+  const int64_t nb = loc_owner_blocks(tsize);
+  hipLaunchKernelGGL(k_owner_count, dim3((unsigned)nb), dim3(kThreads), 0, s, tkeys, tsize,
+                     nshard, blkcnt);
+  hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, s, blkcnt, nb, nshard, owner_cnt);
 }
 
-void loc_assign(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* owner_cursor,
+void loc_assign(const uint64_t* tkeys, int64_t tsize, int nshard, const int64_t* blkoff,
                 int32_t* tlid, uint64_t* uniq, hipStream_t s) {
-  const int64_t per_block = (int64_t)kThreads * kAssignPer;
-  const int64_t nb = (tsize + per_block - 1) / per_block;
+  const int64_t nb = loc_owner_blocks(tsize);
   hipLaunchKernelGGL(k_assign, dim3((unsigned)nb), dim3(kThreads), 0, s, tkeys, tsize, nshard,
-                     owner_cursor, tlid, uniq);
+                     blkoff, tlid, uniq);
 }
 
 void row_of_nnz(const int64_t* offset, int64_t nrows, int32_t* row_of, hipStream_t s) {
@@ -262,13 +341,17 @@ void loc_csc(const int32_t* slot_of, const int32_t* tlid, const int32_t* row_of,
                        (int64_t)0, nuniq, csc_row, csc_val, csc_off);
     return;
   }
+  // binary data (no values): sort the row ids themselves as the payload,
+  // straight into csc_row; valued data: sort positions, then gather
+  int32_t* vin = val ? pos : const_cast<int32_t*>(row_of);
+  int32_t* vout = val ? spos : csc_row;
   hipLaunchKernelGGL(k_loc_lid, dim3(grid_for(nnz, kThreads)), dim3(kThreads), 0, s, slot_of,
-                     tlid, nnz, lid, pos);
+                     tlid, nnz, lid, val ? pos : nullptr);
   size_t bytes = sort_tmp_bytes;
-  WH_HIP_CHECK(rocprim::radix_sort_pairs(sort_tmp, bytes, lid, slid, pos, spos, (size_t)nnz, 0,
+  WH_HIP_CHECK(rocprim::radix_sort_pairs(sort_tmp, bytes, lid, slid, vin, vout, (size_t)nnz, 0,
                                          bits_for(nuniq), s));
   hipLaunchKernelGGL(k_loc_csc, dim3(grid_for(nnz + 1, kThreads)), dim3(kThreads), 0, s, slid,
-                     spos, row_of, val, nnz, nuniq, csc_row, csc_val, csc_off);
+                     val ? spos : nullptr, row_of, val, nnz, nuniq, csc_row, csc_val, csc_off);
   hipLaunchKernelGGL(k_ucnt, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, csc_off,
                      nuniq, ucnt);
 }

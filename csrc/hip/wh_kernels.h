@@ -27,12 +27,14 @@ void scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStrea
 // tsize >= 2*nnz (which cannot overflow). tkeys[tsize] (init ~0) is scratch.
 void loc_insert(const uint64_t* keys, int64_t nnz, uint64_t* tkeys, int64_t tsize,
                 int32_t* slot_of, int64_t* overflow, hipStream_t s);
-// per-owner histogram of the occupied slots (owner = mix64b(key) % nshard)
-void loc_owner_hist(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* owner_cnt,
-                    hipStream_t s);
-// assign local ids grouped by owner; owner_cursor[p] must start at the
-// exclusive scan of owner_cnt. Writes tlid[slot], uniq[lid].
-void loc_assign(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* owner_cursor,
+// per-owner counts of the occupied slots (owner = mix64b(key) % nshard):
+// blkcnt [nshard * loc_owner_blocks(tsize)] becomes the owner-major exclusive
+// scan of the per-block counts (= blkoff for loc_assign); owner_cnt[0..nshard)
+int64_t loc_owner_blocks(int64_t tsize);
+void loc_owner_count(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* blkcnt,
+                     int64_t* owner_cnt, hipStream_t s);
+// assign local ids grouped by owner. Writes tlid[slot], uniq[lid].
+void loc_assign(const uint64_t* tkeys, int64_t tsize, int nshard, const int64_t* blkoff,
                 int32_t* tlid, uint64_t* uniq, hipStream_t s);
 // CSR row id of every non-zero
 void row_of_nnz(const int64_t* offset, int64_t nrows, int32_t* row_of, hipStream_t s);
@@ -60,12 +62,17 @@ struct alignas(32) KVSlot {
   float pad;
 };
 static_assert(sizeof(KVSlot) == 32, "KVSlot must be one 32-byte sector");
+// Event counters are sharded over 64 cache lines: one counter word takes
+// ~12 ns per same-address atomic, and a kernel over 515K keys issues one per
+// wave (8K waves -> ~100 us serialised); sharded, the adds run in parallel.
+constexpr int kStatShards = 64, kStatStride = 16, kStatCount = 8;
 struct KVTable {
   KVSlot* sl;         // [cap]
   float* V;           // [vcap * vstride]
   float* VG;          // [vcap * vstride] AdaGrad accumulators of V
   int32_t* vnext;     // [1] bump allocator for V rows
-  int64_t* stats;     // [8]  0:new_w 1:new_V 2:insert_fail 3:vslab_full 4:n_keys
+  int64_t* stats;     // [kStatShards][kStatStride]  0:new_w 1:new_V 2:insert_fail
+                      //   3:vslab_full 4:n_keys (sum the shards to read)
   int64_t cap;        // power of two
   int64_t vcap;
   int vstride;        // padded embedding stride (multiple of 4), 0 = linear

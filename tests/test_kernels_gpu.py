@@ -49,7 +49,7 @@ def test_localize(hip, nshard, with_val, hint):
     keys, off, val, _ = _rand_batch(3000, 20, 5000, 1, with_val)
     k, o = keys.to(DEV), off.to(DEV)
     v = val.to(DEV) if val is not None else None
-    uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = hip.localize(k, o, v, nshard, hint)
+    uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = hip.localize(k, o, v, nshard, hint)[:7]
     ru = torch.unique(keys)
     assert uniq.numel() == ru.numel()
     assert torch.equal(torch.sort(uniq.cpu()).values, ru)
@@ -97,7 +97,7 @@ def test_fm_forward_backward(hip, dim, with_val):
     vs = ref.vstride_for(dim)
     keys, off, val, label = _rand_batch(2000, 15, 3000, 2, with_val)
     uniq, ucnt, oc, lid, csc_off, csc_row, csc_val = hip.localize(
-        keys.to(DEV), off.to(DEV), val.to(DEV) if val is not None else None, 1)
+        keys.to(DEV), off.to(DEV), val.to(DEV) if val is not None else None, 1)[:7]
     U = uniq.numel()
     hdr, vc = _pulled(U, vs, dim, 3)
     met = torch.zeros(4, dtype=torch.float64, device=DEV)
@@ -144,7 +144,7 @@ def test_grad_post_and_renumber(hip):
 def test_linear_forward_backward(hip, loss):
     keys, off, val, label = _rand_batch(5000, 30, 20000, 4, True)
     uniq, ucnt, oc, lid, csc_off, csc_row, csc_val = hip.localize(
-        keys.to(DEV), off.to(DEV), val.to(DEV), 1)
+        keys.to(DEV), off.to(DEV), val.to(DEV), 1)[:7]
     w = torch.randn(uniq.numel()) * 0.1
     met = torch.zeros(4, dtype=torch.float64, device=DEV)
     py, dual, _ = hip.fm_forward(off.to(DEV), lid, val.to(DEV), w.to(DEV), None, 0,
@@ -300,7 +300,7 @@ def test_kmeans_assign_accum(hip, n, f, k):
 def test_spmv_kernels(hip):
     keys, off, val, label = _rand_batch(3000, 20, 5000, 9, True)
     uniq, ucnt, oc, lid, csc_off, csc_row, csc_val = hip.localize(
-        keys.to(DEV), off.to(DEV), val.to(DEV), 1)
+        keys.to(DEV), off.to(DEV), val.to(DEV), 1)[:7]
     x = torch.randn(uniq.numel())
     y = hip.spmv(off.to(DEV), lid, val.to(DEV), x.to(DEV)).cpu()
     rows = torch.repeat_interleave(torch.arange(3000), off[1:] - off[:-1])

@@ -53,7 +53,7 @@ def load_linear(store, path):
     w = torch.from_numpy(raw["w"].copy())
     _put(store, keys, {"w": w})
     nnz = int((w != 0).sum())
-    store.stats[0] += nnz
+    store.add_stat(0, nnz)
     return len(raw)
 
 
@@ -159,8 +159,8 @@ def load_difacto(store, path):
         _put_v(store, torch.from_numpy(np.ascontiguousarray(vk).view(np.int64).copy()),
                torch.from_numpy(np.array(V, dtype=np.float32)),
                torch.from_numpy(np.array(VG, dtype=np.float32)))
-    store.stats[0] += int((np.asarray(w) != 0).sum())
-    store.stats[1] += len(vk) * dim
+    store.add_stat(0, int((np.asarray(w) != 0).sum()))
+    store.add_stat(1, len(vk) * dim)
     return len(keys)
 
 

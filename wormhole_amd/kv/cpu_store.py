@@ -101,7 +101,13 @@ class CpuKVStore:
 
     @property
     def stats(self):
-        return torch.from_numpy(self._stats)  # shares memory (like the device store)
+        return torch.from_numpy(self._stats.copy())  # a copy (like the device store)
+
+    def reset_stats(self, i0, i1):
+        self._stats[i0:i1] = 0
+
+    def add_stat(self, i, v):
+        self._stats[i] += int(v)
 
     def occupied(self):
         return torch.arange(self._n, dtype=torch.int32)

@@ -102,5 +102,5 @@ class DifactoLearner:
         self.met.zero_()
         self.auc_sum.zero_()
         self.n_mb = 0
-        st[0:2].zero_()
+        self.store.reset_stats(0, 2)
         return prog

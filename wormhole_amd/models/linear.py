@@ -62,7 +62,7 @@ class LinearLearner:
         a = float(self.auc_sum.item())
         st = self.store.stats
         new_w = float(st.tolist()[0])
-        st[0:1].zero_()
+        self.store.reset_stats(0, 1)
         acc = m[2] / m[3] if m[3] else 0.0
         acc = acc if acc > 0.5 else 1 - acc
         prog = [m[0], acc * self.n_mb, a, float(self.n_mb), m[3], new_w]
