@@ -48,8 +48,8 @@ def build(args, comm, device):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="difacto", choices=["difacto", "linear"])
     ap.add_argument("--batch", type=int, default=100000, help="rows per GPU per step")
     ap.add_argument("--dim", type=int, default=64)

@@ -41,6 +41,40 @@ inline int64_t next_pow2(int64_t x) {
   return p;
 }
 
+// Per-device persistent workspaces (allocated once, zero-initialised; the
+// kernels that use them leave them in that state). Intentionally leaked: they
+// must outlive every stream-ordered use and the process exit order.
+struct DevWs {
+  Tensor lb;          // look-back scan granules + ticket (wh_lookback.h)
+  Tensor auc;         // AUC bucket counters / min-max / area / ticket
+  Tensor fwd_ticket;  // arrival counter of the forward's last-block reduction
+  Tensor loc_tab;     // localize hash table (all ~0 between minibatches)
+  Tensor loc_ovf;     // localize overflow counter (0 between minibatches)
+  bool loc_dirty = false;
+};
+
+DevWs& dev_ws(const torch::Device& d) {
+  static std::vector<DevWs*> ws(64, nullptr);
+  const int i = d.index() < 0 ? 0 : d.index();
+  TORCH_CHECK(i < 64, "device index out of range");
+  if (!ws[i]) {
+    auto o = torch::TensorOptions().device(d);
+    auto* w = new DevWs();
+    w->lb = torch::zeros({wh::lookback_ws_words()}, o.dtype(torch::kInt64));
+    w->auc = torch::zeros({wh::auc_ws_persistent_bytes() / 8}, o.dtype(torch::kInt64));
+    w->auc.select(0, wh::auc_ws_lohi_offset() / 8).fill_(-1);
+    w->fwd_ticket = torch::zeros({4}, o.dtype(torch::kInt32));
+    w->loc_tab = torch::full({1024}, -1, o.dtype(torch::kInt64));
+    w->loc_ovf = torch::zeros({1}, o.dtype(torch::kInt64));
+    ws[i] = w;
+  }
+  return *ws[i];
+}
+
+inline wh::Lookback lookback(const torch::Device& d) {
+  return wh::lookback_bind(dev_ws(d).lb.data_ptr());
+}
+
 // ------------------------------------------------------------------ scan
 Tensor scan_excl(const Tensor& in) {
   CHECK_DEV(in); CHECK_CONT(in);
@@ -91,16 +125,30 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
                            : safe;
   Tensor tkeys, slot_of, owner_cnt, owner_cnt_h, recv_h, blkoff;
   const bool ex = !exchange.is_none();
+  // The table is a persistent per-device slab that loc_assign leaves empty,
+  // so a minibatch costs no clearing pass; it is re-filled only after an
+  // overflow retry or an aborted call (loc_dirty).
+  DevWs& ws = dev_ws(keys.device());
   while (true) {
-    tkeys = torch::full({tsize}, -1, i64);
+    if (ws.loc_tab.numel() < tsize) {
+      ws.loc_tab = torch::full({safe}, -1, i64);
+      ws.loc_dirty = false;
+    } else if (ws.loc_dirty) {
+      ws.loc_tab.fill_(-1);
+      ws.loc_ovf.zero_();
+      ws.loc_dirty = false;
+    }
+    tkeys = ws.loc_tab.narrow(0, 0, tsize);
+    ws.loc_dirty = true;
     slot_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
-    owner_cnt = torch::zeros({nshard + 1}, i64);  // [nshard] = overflow count
+    owner_cnt = torch::empty({nshard + 1}, i64);  // [nshard] = overflow count
     wh::loc_insert(reinterpret_cast<const uint64_t*>(keys.data_ptr()), nnz,
                    reinterpret_cast<uint64_t*>(tkeys.data_ptr()), tsize, ptr<int32_t>(slot_of),
-                   ptr<int64_t>(owner_cnt) + nshard, s);
+                   ptr<int64_t>(ws.loc_ovf), s);
     blkoff = torch::empty({nshard * wh::loc_owner_blocks(tsize)}, i64);
     wh::loc_owner_count(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
-                        ptr<int64_t>(blkoff), ptr<int64_t>(owner_cnt), s);
+                        ptr<int64_t>(blkoff), ptr<int64_t>(owner_cnt), ptr<int64_t>(ws.loc_ovf),
+                        s);
     // the number of unique keys sizes everything downstream: one host sync
     if (ex) {
       Tensor recv = exchange(owner_cnt).cast<Tensor>();
@@ -126,9 +174,10 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
   for (int64_t p = 0; p < nshard; ++p) U += owner_cnt_h.data_ptr<int64_t>()[p];
   auto tlid = torch::empty({tsize}, i32);
   auto uniq = torch::empty({U}, i64);
-  wh::loc_assign(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
+  wh::loc_assign(reinterpret_cast<uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
                  ptr<int64_t>(blkoff), ptr<int32_t>(tlid),
                  reinterpret_cast<uint64_t*>(uniq.data_ptr()), s);
+  ws.loc_dirty = false;
   auto row_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
   wh::row_of_nnz(ptr<int64_t>(offset), nrows, ptr<int32_t>(row_of), s);
   const int64_t n1 = std::max<int64_t>(nnz, 1);
@@ -250,10 +299,14 @@ class KVStore {
   void difacto_push_cnt(const Tensor& slot, const Tensor& cnt, const std::vector<double>& h,
                         int64_t threshold, bool l1_shrk, int64_t seed) {
     CHECK_IN(slot, torch::kInt32);
-    CHECK_IN(cnt, torch::kFloat32);
+    CHECK_DEV(cnt); CHECK_CONT(cnt);
+    TORCH_CHECK(cnt.scalar_type() == torch::kFloat32 || cnt.scalar_type() == torch::kInt32,
+                "counts must be float32 or int32");
     TORCH_CHECK(cnt.numel() >= slot.numel());
     c10::DeviceGuard g(slot.device());
-    wh::difacto_push_cnt(table(), ptr<int32_t>(slot), ptr<float>(cnt), slot.numel(),
+    const bool f = cnt.scalar_type() == torch::kFloat32;
+    wh::difacto_push_cnt(table(), ptr<int32_t>(slot), f ? ptr<float>(cnt) : nullptr,
+                         f ? nullptr : ptr<int32_t>(cnt), slot.numel(),
                          dhp(h, threshold, l1_shrk, seed), cur_stream(slot));
   }
 
@@ -267,10 +320,17 @@ class KVStore {
     const int64_t n = slot.numel();
     auto f32 = slot.options().dtype(torch::kFloat32);
     auto hdr = torch::empty({n, 2}, f32);
-    auto vflag = torch::empty({std::max<int64_t>(n, 1)}, slot.options());
-    auto vpos = torch::zeros({n + 1}, slot.options().dtype(torch::kInt64));
     const int64_t mcap = vstride_ > 0 ? n : 0;
     auto vc = torch::empty({mcap, (int64_t)std::max(vstride_, 1)}, f32);
+    if (n > 0) {
+      auto vpos = torch::empty({n + 1}, slot.options().dtype(torch::kInt64));
+      if (wh::difacto_pull_fused(table(), ptr<int32_t>(slot), n, l1_shrk ? 1 : 0,
+                                 lookback(slot.device()), ptr<float>(hdr), ptr<int64_t>(vpos),
+                                 ptr<float>(vc), s))
+        return {hdr, vc, vpos};
+    }
+    auto vflag = torch::empty({std::max<int64_t>(n, 1)}, slot.options());
+    auto vpos = torch::zeros({n + 1}, slot.options().dtype(torch::kInt64));
     wh::difacto_pull_hdr(table(), ptr<int32_t>(slot), n, l1_shrk ? 1 : 0, ptr<float>(hdr),
                          ptr<int32_t>(vflag), s);
     if (vstride_ > 0 && n > 0) {
@@ -345,7 +405,7 @@ std::vector<Tensor> fm_forward(const Tensor& offset, const Tensor& lid,
   wh::fm_forward(nrows, ptr<int64_t>(offset), ptr<int32_t>(lid), vp, ptr<float>(w_or_hdr), vcp,
                  (int)vstride, ptr<float>(label), (int)loss, ptr<float>(py), ptr<float>(dual),
                  vstride > 0 ? ptr<float>(xv) : nullptr, ptr<double>(met), ptr<double>(part),
-                 cur_stream(offset));
+                 ptr<unsigned int>(dev_ws(offset.device()).fwd_ticket), cur_stream(offset));
   return {py, dual, xv};
 }
 
@@ -387,13 +447,14 @@ std::vector<Tensor> fm_backward(const Tensor& csc_off, const Tensor& csc_row,
   auto chunk_cnt = torch::empty({std::max<int64_t>(2 * U, 1)}, i64);
   auto chunk_off = torch::empty({2 * (U + 1)}, i64);
   auto stmp = torch::empty({wh::scan_tmp_elems(U)}, i64);
+  const wh::Lookback lb = lookback(csc_off.device());
   wh::fm_backward(U, nnz, nrows, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row),
                   optptr<float>(csc_val), ptr<float>(dual),
                   vstride > 0 ? optptr<float>(xv) : nullptr, ptr<float>(w_or_hdr), vcp,
                   (int)vstride, ptr<float>(gw), gvc.numel() ? ptr<float>(gvc) : nullptr,
                   ptr<int32_t>(chunk_key), ptr<int32_t>(chunk_beg), ptr<int32_t>(meta_v),
                   ptr<int32_t>(bucket_hist), ptr<int64_t>(chunk_cnt), ptr<int64_t>(chunk_off),
-                  ptr<int64_t>(stmp), s);
+                  ptr<int64_t>(stmp), &lb, s);
   return {gw, gvc};
 }
 
@@ -423,6 +484,12 @@ Tensor vidx_renumber(const Tensor& hdr) {
   CHECK_IN(hdr, torch::kFloat32);
   c10::DeviceGuard g(hdr.device());
   const int64_t n = hdr.numel() / 2;
+  if (n > 0) {
+    auto cnt = torch::empty({1}, hdr.options().dtype(torch::kInt64));
+    if (wh::vidx_renumber_fused(ptr<float>(hdr), n, lookback(hdr.device()), ptr<int64_t>(cnt),
+                                cur_stream(hdr)))
+      return cnt;
+  }
   auto flag = torch::empty({std::max<int64_t>(n, 1)}, hdr.options().dtype(torch::kInt32));
   auto pos = torch::zeros({n + 1}, hdr.options().dtype(torch::kInt64));
   auto stmp = torch::empty({wh::scan_tmp_elems(n)}, pos.options());
@@ -432,7 +499,28 @@ Tensor vidx_renumber(const Tensor& hdr) {
 }
 
 // -------------------------------------------------------------- metrics
+// auc_sum[0] += exact AUC of (py, label) (sort-free bucketed rank sum)
+void auc_acc(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
+  CHECK_IN(py, torch::kFloat32);
+  CHECK_IN(label, torch::kFloat32);
+  CHECK_IN(auc_sum, torch::kFloat64);
+  TORCH_CHECK(py.numel() == label.numel(), "auc: py/label size mismatch");
+  TORCH_CHECK(py.numel() < (int64_t)1 << 30, "auc: at most 2^30 examples per call");
+  c10::DeviceGuard g(py.device());
+  const int64_t n = py.numel();
+  auto scratch = torch::empty({wh::auc_ws_bytes(n)}, py.options().dtype(torch::kUInt8));
+  wh::auc_accumulate(ptr<float>(py), ptr<float>(label), n, dev_ws(py.device()).auc.data_ptr(),
+                     scratch.data_ptr(), ptr<double>(auc_sum), cur_stream(py));
+}
+
 Tensor auc(const Tensor& py, const Tensor& label) {
+  auto out = torch::zeros({1}, py.options().dtype(torch::kFloat64));
+  auc_acc(py, label, out);
+  return out;
+}
+
+// reference path: rocPRIM radix sort + rank-sum (kept as a cross-check)
+Tensor auc_sorted(const Tensor& py, const Tensor& label) {
   CHECK_IN(py, torch::kFloat32);
   CHECK_IN(label, torch::kFloat32);
   c10::DeviceGuard g(py.device());
@@ -669,6 +757,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fm_grad_post", &fm_grad_post);
   m.def("vidx_renumber", &vidx_renumber);
   m.def("auc", &auc);
+  m.def("auc_acc", &auc_acc);
+  m.def("auc_sorted", &auc_sorted);
   m.def("synth_criteo", &synth_criteo);
   m.def("gather_rows", &gather_rows);
   m.def("vstride_for", &vstride_for);

@@ -23,6 +23,7 @@
 // m keys with an embedding move 256 bytes; the rest move 8 (pull) / 4 (push).
 #include "wh_common.h"
 #include "wh_kernels.h"
+#include "wh_lookback.h"
 
 #include <algorithm>
 
@@ -33,16 +34,43 @@ constexpr int kThreads = 256;
 constexpr int kChunk = 32;  // occurrences per backward work item
 constexpr int kFwdBlocks = 2048;  // persistent forward grid: 8192 waves = 32 per CU
 
-// The four metric sums leave each block as plain stores into part[block][4]
-// (summed by k_partials_sum): one same-address float64 atomic per block costs
+// The four metric sums leave each block as stores into part[block][4]
+// (summed by the last block): one same-address float64 atomic per block costs
 // ~12 ns at the memory side, which at 25k blocks was a millisecond.
+// The LAST block to finish (arrival ticket) sums the partials into met, so
+// the forward is one launch: partials are stored write-through (agent-scope
+// atomic stores) and drained before the ticket add, and read back with
+// agent-scope loads (wh_lookback.h: no fences needed in this form).
 __device__ __forceinline__ void block_partials(double* part, double* sh, double a, double b,
-                                               double c, double d) {
-  double r;
-  r = block_sum_d(a, sh); if (threadIdx.x == 0) part[blockIdx.x * 4 + 0] = r; __syncthreads();
-  r = block_sum_d(b, sh); if (threadIdx.x == 0) part[blockIdx.x * 4 + 1] = r; __syncthreads();
-  r = block_sum_d(c, sh); if (threadIdx.x == 0) part[blockIdx.x * 4 + 2] = r; __syncthreads();
-  r = block_sum_d(d, sh); if (threadIdx.x == 0) part[blockIdx.x * 4 + 3] = r;
+                                               double c, double d, double* met,
+                                               unsigned int* ticket) {
+  __shared__ int last;
+  double v[4] = {a, b, c, d};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double r = block_sum_d(v[i], sh);
+    if (threadIdx.x == 0)
+      lb_store(reinterpret_cast<unsigned long long*>(part) + blockIdx.x * 4 + i,
+               (unsigned long long)__double_as_longlong(r));
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = atomicAdd(ticket, 1u);
+    last = t == gridDim.x - 1;
+    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(part);
+  for (int i = 0; i < 4; ++i) {
+    double s = 0;
+    for (int bidx = threadIdx.x; bidx < (int)gridDim.x; bidx += blockDim.x)
+      s += __longlong_as_double((long long)lb_load(pp + bidx * 4 + i));
+    const double r = block_sum_d(s, sh);
+    if (threadIdx.x == 0) met[i] += r;
+    __syncthreads();
+  }
 }
 
 struct LossOut {
@@ -116,7 +144,8 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
                                                      const float* __restrict__ label, int loss,
                                                      float* __restrict__ py_out,
                                                      float* __restrict__ dual_out,
-                                                     float* __restrict__ xv, double* part) {
+                                                     float* __restrict__ xv, double* part,
+                                                     double* met, unsigned int* ticket) {
   // Persistent waves, one example (row) at a time, software-pipelined over
   // the wave's rows so each row exposes ~one memory round trip instead of
   // four: while row i's embedding rows are gathered, the headers of row i+1,
@@ -236,7 +265,7 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
     bn = b2; en = e2; ln = l2; xn = x2;
     b2 = b3; e2 = e3;
   }
-  block_partials(part, sh, m_objv, m_objw, m_corr, m_n);
+  block_partials(part, sh, m_objv, m_objw, m_corr, m_n, met, ticket);
 }
 
 // linear model: G lanes stride over one row's non-zeros; persistent over rows
@@ -247,7 +276,8 @@ __global__ __launch_bounds__(kThreads) void k_lin_fwd(int64_t nrows, const int64
                                                       const float* __restrict__ w,
                                                       const float* __restrict__ label, int loss,
                                                       float* __restrict__ py_out,
-                                                      float* __restrict__ dual_out, double* part) {
+                                                      float* __restrict__ dual_out, double* part,
+                                                      double* met, unsigned int* ticket) {
   __shared__ double sh[kThreads / 64];
   const int lane = threadIdx.x & 63, gl = lane & (G - 1);
   const int64_t ngroups = (int64_t)gridDim.x * (kThreads / G);
@@ -269,20 +299,7 @@ __global__ __launch_bounds__(kThreads) void k_lin_fwd(int64_t nrows, const int64
     }
   }
   (void)lane;
-  block_partials(part, sh, m_objv, m_objv, m_corr, m_n);
-}
-
-// met[i] += sum over blocks of part[b * 4 + i]
-__global__ __launch_bounds__(kThreads) void k_partials_sum(const double* __restrict__ part,
-                                                           int nblk, double* met) {
-  __shared__ double sh[kThreads / 64];
-  for (int i = 0; i < 4; ++i) {
-    double a = 0;
-    for (int bidx = threadIdx.x; bidx < nblk; bidx += kThreads) a += part[bidx * 4 + i];
-    const double r = block_sum_d(a, sh);
-    if (threadIdx.x == 0) met[i] += r;
-    __syncthreads();
-  }
+  block_partials(part, sh, m_objv, m_objv, m_corr, m_n, met, ticket);
 }
 
 // ---------------------------------------------------------------- backward
@@ -367,6 +384,98 @@ __global__ __launch_bounds__(kThreads) void k_chunk_fill(int64_t nuniq,
       for (int d = lane * 4; d < vstride; d += 256)
         *reinterpret_cast<float4*>(gvc + (int64_t)jvid * vstride + d) =
             make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+// Single-pass version of k_chunk_count -> 2 scans -> k_chunk_fill: each tile
+// of 1024 keys (4 per thread) counts its chunks, learns its chunk offsets
+// (both lists) by decoupled look-back (wh_lookback.h) and fills its chunks
+// in the same launch; the last tile writes the chunk totals to
+// off_s[nuniq] / off_v[nuniq].
+constexpr int kPlanPer = 4;
+constexpr int kPlanTile = kThreads * kPlanPer;
+
+__global__ __launch_bounds__(kThreads) void k_chunk_plan(int64_t nuniq,
+                                                         const int64_t* __restrict__ csc_off,
+                                                         const float2* __restrict__ hdr,
+                                                         int vstride, Lookback lb, int ntiles,
+                                                         int64_t* off_s_tot, int64_t* off_v_tot,
+                                                         int32_t* key_s, int32_t* beg_s,
+                                                         int4* meta_v, float* gw, float* gvc) {
+  __shared__ uint32_t shs[16];
+  __shared__ int sht;
+  const int tile = lb_tile(lb, ntiles, &sht);
+  const int lane = threadIdx.x & 63;
+  const int64_t k0 = (int64_t)tile * kPlanTile + threadIdx.x * kPlanPer;
+  int64_t co[kPlanPer + 1];
+#pragma unroll
+  for (int r = 0; r <= kPlanPer; ++r) co[r] = k0 + r <= nuniq ? csc_off[k0 + r] : 0;
+  int32_t vid[kPlanPer];
+#pragma unroll
+  for (int r = 0; r < kPlanPer; ++r)
+    vid[r] = (hdr && k0 + r < nuniq) ? __float_as_int(hdr[k0 + r].y) : -1;
+  uint32_t c[2] = {0u, 0u};
+  uint32_t nc[kPlanPer];
+#pragma unroll
+  for (int r = 0; r < kPlanPer; ++r) {
+    nc[r] = 0;
+    if (k0 + r < nuniq) {
+      const int64_t cnt = co[r + 1] - co[r];
+      nc[r] = vid[r] >= 0 ? (uint32_t)((cnt + kChunkV - 1) / kChunkV)
+                          : (uint32_t)((cnt + kChunk - 1) / kChunk);
+      c[vid[r] >= 0 ? 1 : 0] += nc[r];
+    }
+  }
+  uint32_t ex[2], tot[2];
+  lb_block_scan<2>(lb, tile, c, ex, tot, shs);
+  if (tile == ntiles - 1 && threadIdx.x == 0) {
+    *off_s_tot = tot[0];
+    *off_v_tot = tot[1];
+  }
+#pragma unroll
+  for (int r = 0; r < kPlanPer; ++r) {
+    const int64_t k = k0 + r;
+    const int isv = vid[r] >= 0;
+    const int64_t c0 = isv ? ex[1] : ex[0];
+    ex[isv ? 1 : 0] += nc[r];
+    const int32_t b0 = (int32_t)co[r];
+    const int32_t cnt = (int32_t)(co[r + 1] - co[r]);
+    if (nc[r] == 1) {
+      if (isv) {
+        meta_v[c0] = make_int4((int)k, b0, cnt, vid[r]);
+      } else {
+        key_s[c0] = (int32_t)k;
+        beg_s[c0] = b0;
+      }
+    }
+    uint64_t m = __ballot(nc[r] > 1);
+    while (m) {  // hot keys: the whole wave expands one key's chunk list
+      const int src = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      const int32_t jk = (int32_t)__shfl((int)k, src, 64);
+      const int64_t jc0 = __shfl(c0, src, 64);
+      const int64_t jnc = __shfl((int)nc[r], src, 64);
+      const int32_t jb0 = __shfl(b0, src, 64);
+      const int32_t jcnt = __shfl(cnt, src, 64);
+      const int32_t jvid = __shfl(vid[r], src, 64);
+      const int jv = __shfl(isv, src, 64);
+      for (int64_t q = lane; q < jnc; q += 64) {
+        if (jv) {
+          const int32_t cb = (int32_t)(q * kChunkV);
+          const int32_t n = jcnt - cb < kChunkV ? jcnt - cb : kChunkV;
+          meta_v[jc0 + q] = make_int4(jk, jb0 + cb, n | (1 << 8), jvid);
+        } else {
+          key_s[jc0 + q] = jk;
+          beg_s[jc0 + q] = jb0 + (int32_t)(q * kChunk);
+        }
+      }
+      if (lane == 0) gw[jk] = 0.f;
+      if (jv) {
+        for (int d = lane * 4; d < vstride; d += 256)
+          *reinterpret_cast<float4*>(gvc + (int64_t)jvid * vstride + d) =
+              make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   }
 }
@@ -661,23 +770,23 @@ static int resident_blocks(K kernel, int cap) {
 
 void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
                 const float* w_or_hdr, const float* vc, int vstride, const float* label, int loss,
-                float* py, float* dual, float* xv, double* met, double* part, hipStream_t s) {
+                float* py, float* dual, float* xv, double* met, double* part,
+                unsigned int* ticket, hipStream_t s) {
   if (nrows <= 0) return;
   int nblk;
   if (vstride == 0) {
     constexpr int G = 8;
     nblk = grid_for(nrows * G, kThreads, kFwdBlocks);
     hipLaunchKernelGGL(k_lin_fwd<G>, dim3(nblk), dim3(kThreads), 0, s, nrows, offset, lid, val,
-                       w_or_hdr, label, loss, py, dual, part);
+                       w_or_hdr, label, loss, py, dual, part, met, ticket);
   } else {
     const int G = vstride / 4;  // vstride <= 256 enforced by the binding
     const float2* hdr = reinterpret_cast<const float2*>(w_or_hdr);
     nblk = grid_for(nrows * 64, kThreads, WH_RESIDENT(G, k_fm_fwd, kFwdBlocks));
     const dim3 grid(nblk), block(kThreads);
     WH_DISPATCH_G(G, k_fm_fwd, grid, block, 0, s, nrows, offset, lid, val, hdr, vc, vstride,
-                  label, loss, py, dual, xv, part);
+                  label, loss, py, dual, xv, part, met, ticket);
   }
-  hipLaunchKernelGGL(k_partials_sum, dim3(1), dim3(kThreads), 0, s, part, nblk, met);
 }
 
 static int64_t scalar_cap(int64_t nuniq, int64_t nnz) { return nuniq + nnz / kChunk + 1; }
@@ -701,7 +810,8 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
                  const int32_t* csc_row, const float* csc_val, const float* dual, const float* xv,
                  const float* hdr_f, const float* vc, int vstride, float* gw, float* gvc,
                  int32_t* chunk_key, int32_t* chunk_beg, int32_t* meta_v_i32, int32_t* bucket_hist,
-                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, hipStream_t s) {
+                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, const Lookback* lb,
+                 hipStream_t s) {
   int4* meta_v = reinterpret_cast<int4*>(meta_v_i32);
   if (nuniq <= 0) return;
   const float2* hdr = vstride > 0 ? reinterpret_cast<const float2*>(hdr_f) : nullptr;
@@ -712,12 +822,19 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
   const int64_t cap_s = scalar_cap(nuniq, nnz);
   int32_t* key_s = chunk_key;
   int32_t* beg_s = chunk_beg;
-  hipLaunchKernelGGL(k_chunk_count, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
-                     csc_off, hdr, cnt_s, cnt_v);
-  scan_i64(cnt_s, off_s, nuniq, scan_tmp, s);
-  if (hdr) scan_i64(cnt_v, off_v, nuniq, scan_tmp, s);
-  hipLaunchKernelGGL(k_chunk_fill, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, nuniq,
-                     csc_off, off_s, off_v, hdr, vstride, key_s, beg_s, meta_v, gw, gvc);
+  const int64_t ntiles = (nuniq + kPlanTile - 1) / kPlanTile;
+  if (lb && ntiles <= kLbMaxTiles) {  // one launch
+    hipLaunchKernelGGL(k_chunk_plan, dim3((unsigned)ntiles), dim3(kThreads), 0, s, nuniq, csc_off,
+                       hdr, vstride, *lb, (int)ntiles, off_s + nuniq, off_v + nuniq, key_s, beg_s,
+                       meta_v, gw, gvc);
+  } else {
+    hipLaunchKernelGGL(k_chunk_count, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s,
+                       nuniq, csc_off, hdr, cnt_s, cnt_v);
+    scan_i64(cnt_s, off_s, nuniq, scan_tmp, s);
+    if (hdr) scan_i64(cnt_v, off_v, nuniq, scan_tmp, s);
+    hipLaunchKernelGGL(k_chunk_fill, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s,
+                       nuniq, csc_off, off_s, off_v, hdr, vstride, key_s, beg_s, meta_v, gw, gvc);
+  }
   // chunk counts are device values (off[nuniq]); the scalar kernel launches
   // over the host-side bound and surplus lanes exit; the V kernel is
   // persistent. No host synchronisation in the step.

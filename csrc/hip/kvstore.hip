@@ -12,6 +12,7 @@
 // 64-dim embedding row is one 256-byte coalesced access per 16 lanes.
 #include "wh_common.h"
 #include "wh_kernels.h"
+#include "wh_lookback.h"
 
 namespace wh {
 namespace {
@@ -177,7 +178,8 @@ __device__ __forceinline__ void init_v_row(const KVTable& t, int32_t s, int32_t 
 
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const int32_t* slot,
-                                                               const float* cnt, int64_t n,
+                                                               const float* cnt,
+                                                               const int32_t* cnti, int64_t n,
                                                                DifactoHP hp) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const 
   if (i < n) {
     s = slot[i];
     if (s >= 0) {
-      const uint32_t c = t.sl[s].cnt + (uint32_t)cnt[i];
+      const uint32_t c = t.sl[s].cnt + (cnt ? (uint32_t)cnt[i] : (uint32_t)cnti[i]);
       t.sl[s].cnt = c;
       want = t.vstride > 0 && c > hp.threshold && t.sl[s].vrow < 0 &&
              (!hp.l1_shrk || t.sl[s].w != 0.f);
@@ -247,6 +249,88 @@ __global__ __launch_bounds__(kThreads) void k_difacto_pull_rows(KVTable t, const
         *reinterpret_cast<float4*>(o + c) = *reinterpret_cast<const float4*>(V + c);
     }
   });
+}
+
+// Fused variable-length pull: header, V-flag scan (decoupled look-back)
+// and row copy in ONE launch (was: header kernel, 3-launch scan, row kernel).
+// A tile is 1024 consecutive keys, 4 per thread (vector loads of the slot
+// ids, 32-byte header stores), so a 515k-key minibatch is ~500 tiles and the
+// look-back finishes in ~2 windows.
+constexpr int kPullPer = 4;
+constexpr int kPullTile = kThreads * kPullPer;
+
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_difacto_pull(KVTable t, const int32_t* slot,
+                                                           int64_t n, int l1_shrk, Lookback lb,
+                                                           int ntiles, float2* hdr, int64_t* vpos,
+                                                           float* vc) {
+  __shared__ uint32_t shs[16];
+  __shared__ int sht;
+  const int tile = lb_tile(lb, ntiles, &sht);
+  const int lane = threadIdx.x & 63;
+  const int64_t i0 = (int64_t)tile * kPullTile + threadIdx.x * kPullPer;
+  int32_t sl[kPullPer];
+  if (i0 + kPullPer <= n && (reinterpret_cast<uintptr_t>(slot) & 15) == 0) {
+    const int4 q = *reinterpret_cast<const int4*>(slot + i0);
+    sl[0] = q.x; sl[1] = q.y; sl[2] = q.z; sl[3] = q.w;
+  } else {
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r) sl[r] = i0 + r < n ? slot[i0 + r] : -1;
+  }
+  float w[kPullPer];
+  int32_t row[kPullPer];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {  // all slot loads in flight together
+    w[r] = sl[r] >= 0 ? t.sl[sl[r]].w : 0.f;
+    row[r] = (sl[r] >= 0 && t.vstride > 0) ? t.sl[sl[r]].vrow : -1;
+  }
+  uint32_t f[1] = {0u}, ex[1], tot[1];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    if (l1_shrk && w[r] == 0.f) row[r] = -1;
+    f[0] += row[r] >= 0 ? 1u : 0u;
+  }
+  lb_block_scan<1>(lb, tile, f, ex, tot, shs);
+  int32_t vp[kPullPer];
+  uint32_t run = ex[0];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    vp[r] = row[r] >= 0 ? (int32_t)run : -1;
+    if (i0 + r < n) {
+      hdr[i0 + r] = make_float2(w[r], __int_as_float(vp[r]));
+      vpos[i0 + r] = run;
+    }
+    run += row[r] >= 0 ? 1u : 0u;
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) vpos[n] = tot[0];
+  if (t.vstride == 0) return;
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    for_each_row_job<G>(row[r] >= 0, [&](int src, int gl) {
+      const int sl2 = src >= 0 ? src : lane;
+      const int32_t jr = __shfl(row[r], sl2, 64), jp = __shfl(vp[r], sl2, 64);
+      if (src >= 0) {
+        const float* V = t.V + (int64_t)jr * t.vstride;
+        float* o = vc + (int64_t)jp * t.vstride;
+        for (int c = gl * 4; c < t.vstride; c += 4 * G)
+          *reinterpret_cast<float4*>(o + c) = *reinterpret_cast<const float4*>(V + c);
+      }
+    });
+  }
+}
+
+// worker side of a multi-shard pull, fused: flag -> scan -> renumber
+__global__ __launch_bounds__(kThreads) void k_vidx_renumber(float2* hdr, int64_t n, Lookback lb,
+                                                            int ntiles, int64_t* count) {
+  __shared__ uint32_t shs[16];
+  __shared__ int sht;
+  const int tile = lb_tile(lb, ntiles, &sht);
+  const int64_t i = (int64_t)tile * kThreads + threadIdx.x;
+  const bool has = i < n && __float_as_int(hdr[i].y) >= 0;
+  uint32_t f[1] = {has ? 1u : 0u}, ex[1], tot[1];
+  lb_block_scan<1>(lb, tile, f, ex, tot, shs);
+  if (has) hdr[i].y = __int_as_float((int32_t)ex[0]);
+  if (tile == ntiles - 1 && threadIdx.x == 0) *count = tot[0];
 }
 
 __global__ __launch_bounds__(kThreads) void k_vidx_flag(const float2* hdr, int64_t n,
@@ -408,12 +492,12 @@ void linear_push(const KVTable& t, const int32_t* slot, const float* grad, int64
     default: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                 \
   }
 
-void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt, int64_t n,
-                      DifactoHP hp, hipStream_t s) {
+void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt,
+                      const int32_t* cnti, int64_t n, DifactoHP hp, hipStream_t s) {
   if (n <= 0) return;
   const int G = lanes_per_key(t.vstride);
   const dim3 grid(grid_for(n, kThreads)), block(kThreads);  // lane per key
-  WH_DISPATCH_G(G, k_difacto_push_cnt, grid, block, 0, s, t, slot, cnt, n, hp);
+  WH_DISPATCH_G(G, k_difacto_push_cnt, grid, block, 0, s, t, slot, cnt, cnti, n, hp);
 }
 
 void difacto_pull_hdr(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk, float* hdr,
@@ -458,6 +542,30 @@ void gather_rows(const float* in, const int32_t* idx, int64_t n, int width, floa
   const int64_t work = (width % 4 == 0) ? n * (width / 4) : n * width;
   hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((work + kThreads - 1) / kThreads)),
                      dim3(kThreads), 0, s, in, idx, n, width, out);
+}
+
+}  // namespace wh
+
+namespace wh {
+
+bool difacto_pull_fused(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk,
+                        const Lookback& lb, float* hdr, int64_t* vpos, float* vc, hipStream_t s) {
+  const int64_t ntiles = (n + kPullTile - 1) / kPullTile;
+  if (n <= 0 || ntiles > kLbMaxTiles) return false;
+  const int G = lanes_per_key(t.vstride);
+  const dim3 grid((unsigned)ntiles), block(kThreads);
+  WH_DISPATCH_G(G, k_difacto_pull, grid, block, 0, s, t, slot, n, l1_shrk, lb, (int)ntiles,
+                reinterpret_cast<float2*>(hdr), vpos, vc);
+  return true;
+}
+
+bool vidx_renumber_fused(float* hdr, int64_t n, const Lookback& lb, int64_t* count,
+                         hipStream_t s) {
+  const int64_t ntiles = (n + kThreads - 1) / kThreads;
+  if (n <= 0 || ntiles > kLbMaxTiles) return false;
+  hipLaunchKernelGGL(k_vidx_renumber, dim3((unsigned)ntiles), dim3(kThreads), 0, s,
+                     reinterpret_cast<float2*>(hdr), n, lb, (int)ntiles, count);
+  return true;
 }
 
 }  // namespace wh

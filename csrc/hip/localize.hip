@@ -172,7 +172,14 @@ __global__ __launch_bounds__(kThreads) void k_owner_count(const uint64_t* __rest
 // Single-block exclusive scan of n (<= a few 100K) int64 counts in place,
 // then owner totals: owner_cnt[o] = sum of blkcnt[o * nblk .. (o+1) * nblk).
 __global__ __launch_bounds__(1024) void k_owner_scan(int64_t* __restrict__ blk, int64_t nblk,
-                                                     int nshard, int64_t* __restrict__ owner_cnt) {
+                                                     int nshard, int64_t* __restrict__ owner_cnt,
+                                                     int64_t* __restrict__ ovf) {
+  // the insert's overflow count travels with the owner counts (one host
+  // read) and the persistent counter is re-armed for the next minibatch
+  if (threadIdx.x == 0) {
+    owner_cnt[nshard] = *ovf;
+    *ovf = 0;
+  }
   __shared__ int64_t part[1024];
   const int64_t n = nblk * nshard;
   const int64_t per = (n + 1023) / 1024;
@@ -204,7 +211,7 @@ __global__ __launch_bounds__(1024) void k_owner_scan(int64_t* __restrict__ blk, 
 
 // lid of every occupied slot: the block's scanned offset in its owner group
 // plus the slot's rank among the block's slots of that owner.
-__global__ __launch_bounds__(kThreads) void k_assign(const uint64_t* __restrict__ tkeys,
+__global__ __launch_bounds__(kThreads) void k_assign(uint64_t* __restrict__ tkeys,
                                                      int64_t tsize, int nshard,
                                                      const int64_t* __restrict__ blkoff,
                                                      int32_t* tlid, uint64_t* uniq) {
@@ -233,6 +240,7 @@ __global__ __launch_bounds__(kThreads) void k_assign(const uint64_t* __restrict_
       const int64_t lid = blkoff[(int64_t)own[r] * gridDim.x + blockIdx.x] + rk[r];
       tlid[i] = (int32_t)lid;
       uniq[lid] = tkeys[i];
+      tkeys[i] = kEmptyKey;  // leave the persistent scratch table empty
     }
   }
 }
@@ -302,14 +310,15 @@ void loc_insert(const uint64_t* keys, int64_t nnz, uint64_t* tkeys, int64_t tsiz
 int64_t loc_owner_blocks(int64_t tsize) { return (tsize + kAssignItems - 1) / kAssignItems; }
 
 void loc_owner_count(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* blkcnt,
-                     int64_t* owner_cnt, hipStream_t s) {
+                     int64_t* owner_cnt, int64_t* overflow, hipStream_t s) {
   const int64_t nb = loc_owner_blocks(tsize);
   hipLaunchKernelGGL(k_owner_count, dim3((unsigned)nb), dim3(kThreads), 0, s, tkeys, tsize,
                      nshard, blkcnt);
-  hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, s, blkcnt, nb, nshard, owner_cnt);
+  hipLaunchKernelGGL(k_owner_scan, dim3(1), dim3(1024), 0, s, blkcnt, nb, nshard, owner_cnt,
+                     overflow);
 }
 
-void loc_assign(const uint64_t* tkeys, int64_t tsize, int nshard, const int64_t* blkoff,
+void loc_assign(uint64_t* tkeys, int64_t tsize, int nshard, const int64_t* blkoff,
                 int32_t* tlid, uint64_t* uniq, hipStream_t s) {
   const int64_t nb = loc_owner_blocks(tsize);
   hipLaunchKernelGGL(k_assign, dim3((unsigned)nb), dim3(kThreads), 0, s, tkeys, tsize, nshard,

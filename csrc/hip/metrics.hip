@@ -42,6 +42,226 @@ __global__ void k_auc_final(const int64_t* excl, int64_t n, double* out) {
   out[0] = auc;
 }
 
+// ---------------------------------------------------------------------------
+// Exact AUC without a full sort (5 short launches instead of a 10-launch
+// radix sort + flag/scan/area passes).
+//
+// Every prediction gets a unique 64-bit key  ord(py) << 32 | i << 1 | pos
+// (ord = order-preserving bits of the float, i = the example index, so ties
+// are broken by index exactly like the stable sort of the reference path).
+// Keys are bucketed linearly over [min, max] into kAucBuckets buckets; a
+// negative's rank-sum term is  (#positives in lower buckets) + (#positives
+// in its own bucket with a smaller key). Buckets hold a few keys each, and
+// all-equal predictions (e.g. a zero model) spread evenly because the index
+// is part of the key. Every count is an integer, so the result does not
+// depend on atomic ordering. The bucket counters are left zeroed by the
+// scan kernel and the min/max / area words by the last kernel, so the
+// persistent workspace never needs a clearing launch.
+constexpr int kAucBuckets = 16384;
+constexpr int kAucScanThreads = 1024;
+
+__device__ __forceinline__ uint64_t auc_key(float py, int64_t i, bool pos) {
+  uint32_t u = __float_as_uint(py == 0.f ? 0.f : py);  // -0 ties with +0
+  u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((uint64_t)u << 32) | ((uint64_t)i << 1) | (pos ? 1u : 0u);
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long t = __shfl_xor(v, o, 64);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+
+// min / max key: one pair of atomics per BLOCK (same-address atomics
+// serialise at ~12 ns each, so per-wave atomics from 1000 waves cost 25 us)
+__global__ __launch_bounds__(1024) void k_auc_minmax(const float* __restrict__ py,
+                                                     const float* __restrict__ lab, int64_t n,
+                                                     unsigned long long* lohi) {
+  __shared__ unsigned long long slo[16], shi[16];
+  unsigned long long lo = ~0ull, hi = 0ull;
+  for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * 1024) {
+    const unsigned long long k = auc_key(py[i], i, lab[i] > 0.f) >> 32;
+    lo = k < lo ? k : lo;
+    hi = k > hi ? k : hi;
+  }
+  lo = wave_min_u64(lo);
+  hi = wave_max_u64(hi);
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    slo[wid] = lo;
+    shi[wid] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; ++w) {
+      lo = slo[w] < lo ? slo[w] : lo;
+      hi = shi[w] > hi ? shi[w] : hi;
+    }
+    atomicMin(lohi, lo);
+    atomicMax(lohi + 1, hi);
+  }
+}
+
+// Bucket of example i: linear in the prediction VALUE between the minibatch's
+// min and max (double arithmetic: monotone non-decreasing in py, which is
+// all the exact count needs); all-equal predictions bucket by index (also
+// monotone in the key, whose high half is then constant). lo/hi are the
+// order-preserving keys of the min / max prediction.
+__device__ __forceinline__ float auc_unord(uint64_t k) {
+  const uint32_t u = (uint32_t)k;
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+__device__ __forceinline__ int auc_bucket(float py, int64_t i, int64_t n, uint64_t lo,
+                                          uint64_t hi) {
+  if (lo == hi) return (int)((i * kAucBuckets) / (n > 0 ? n : 1));
+  const double flo = auc_unord(lo), fhi = auc_unord(hi);
+  const double t = ((double)py - flo) * ((double)kAucBuckets / (fhi - flo));
+  if (!(t >= 0.0)) return 0;
+  return t < (double)(kAucBuckets - 1) ? (int)t : kAucBuckets - 1;
+}
+
+__global__ __launch_bounds__(kThreads) void k_auc_bucket(const float* __restrict__ py,
+                                                         const float* __restrict__ lab, int64_t n,
+                                                         const unsigned long long* lohi,
+                                                         uint32_t* cnt, uint32_t* pcnt,
+                                                         int2* br) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const bool pos = lab[i] > 0.f;
+  const int b = auc_bucket(py[i], i, n, lohi[0], lohi[1]);
+  const int r = (int)atomicAdd(cnt + b, 1u);
+  if (pos) atomicAdd(pcnt + b, 1u);
+  br[i] = make_int2(b, r);
+}
+
+// one block: exclusive scans of the bucket counts and positive counts
+// (8 consecutive buckets per thread, 16-byte loads); leaves the counters
+// zeroed, saves {lo, hi} and re-arms the min/max words
+__global__ __launch_bounds__(kAucScanThreads) void k_auc_scan(uint32_t* cnt, uint32_t* pcnt,
+                                                              unsigned long long* lohi,
+                                                              uint32_t* off, uint32_t* poff,
+                                                              unsigned long long* lw) {
+  constexpr int kPer = kAucBuckets / kAucScanThreads;
+  static_assert(kPer == 16, "scan assumes 16 buckets per thread");
+  __shared__ uint32_t wa[16], wp[16];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  constexpr int kV = kPer / 4;  // uint4 per thread per array
+  uint4* c4 = reinterpret_cast<uint4*>(cnt) + kV * t;
+  uint4* p4 = reinterpret_cast<uint4*>(pcnt) + kV * t;
+  uint32_t a[kPer], p[kPer];
+#pragma unroll
+  for (int v = 0; v < kV; ++v) {
+    const uint4 x = c4[v], y = p4[v];
+    a[4 * v] = x.x; a[4 * v + 1] = x.y; a[4 * v + 2] = x.z; a[4 * v + 3] = x.w;
+    p[4 * v] = y.x; p[4 * v + 1] = y.y; p[4 * v + 2] = y.z; p[4 * v + 3] = y.w;
+  }
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int v = 0; v < kV; ++v) { c4[v] = z; p4[v] = z; }
+  uint32_t sa = 0, sp = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) { sa += a[j]; sp += p[j]; }
+  uint32_t ia = sa, ip = sp;  // wave inclusive scans
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t xa = __shfl_up(ia, o, 64), xp = __shfl_up(ip, o, 64);
+    if (lane >= o) { ia += xa; ip += xp; }
+  }
+  if (lane == 63) { wa[wid] = ia; wp[wid] = ip; }
+  __syncthreads();
+  uint32_t ba = 0, bp = 0;
+  for (int w = 0; w < wid; ++w) { ba += wa[w]; bp += wp[w]; }
+  uint32_t ra = ba + ia - sa, rp = bp + ip - sp;
+  uint32_t oa[kPer], op[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    oa[j] = ra; op[j] = rp;
+    ra += a[j]; rp += p[j];
+  }
+#pragma unroll
+  for (int v = 0; v < kV; ++v) {
+    reinterpret_cast<uint4*>(off)[kV * t + v] =
+        make_uint4(oa[4 * v], oa[4 * v + 1], oa[4 * v + 2], oa[4 * v + 3]);
+    reinterpret_cast<uint4*>(poff)[kV * t + v] =
+        make_uint4(op[4 * v], op[4 * v + 1], op[4 * v + 2], op[4 * v + 3]);
+  }
+  if (t == kAucScanThreads - 1) {
+    off[kAucBuckets] = ra;
+    poff[kAucBuckets] = rp;
+    lw[0] = lohi[0];
+    lw[1] = lohi[1];
+    lohi[0] = ~0ull;
+    lohi[1] = 0ull;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_auc_place(const float* __restrict__ py,
+                                                        const float* __restrict__ lab, int64_t n,
+                                                        const int2* __restrict__ br,
+                                                        const uint32_t* __restrict__ off,
+                                                        unsigned long long* sorted) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const int2 q = br[i];
+  sorted[off[q.x] + q.y] = auc_key(py[i], i, lab[i] > 0.f);
+}
+
+__global__ __launch_bounds__(kThreads) void k_auc_count(const unsigned long long* __restrict__ sorted,
+                                                        int64_t n, const uint32_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ poff,
+                                                        const unsigned long long* __restrict__ lw,
+                                                        unsigned long long* area,
+                                                        unsigned int* ticket, double* auc_sum) {
+  __shared__ int last;
+  const int64_t q = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  unsigned long long a = 0;
+  if (q < n) {
+    const uint64_t k = sorted[q];
+    if (!(k & 1)) {
+      const int b = auc_bucket(auc_unord(k >> 32), (int64_t)((k & 0xffffffffull) >> 1), n, lw[0],
+                               lw[1]);
+      a = poff[b];
+      const uint32_t e = off[b + 1];
+      for (uint32_t j = off[b]; j < e; ++j) {
+        const uint64_t o = sorted[j];
+        a += (o & 1) && o < k;
+      }
+    }
+  }
+  a = wave_sum_ll((long long)a);
+  if ((threadIdx.x & 63) == 0 && a) atomicAdd(area, a);
+  // the area adds must be performed before this block's ticket add
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = atomicAdd(ticket, 1u);
+    last = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double tot = (double)atomicExch(area, 0ull);
+  const double tp = (double)poff[kAucBuckets];
+  double auc = 1.0;
+  if (tp != 0 && tp != (double)n) {
+    const double r = tot / (tp * ((double)n - tp));
+    auc = r < 0.5 ? 1 - r : r;
+  }
+  auc_sum[0] += auc;
+}
+
 }  // namespace
 
 size_t auc_sort_tmp_bytes(int64_t n) {
@@ -77,6 +297,47 @@ void auc_from_sorted(const float* label_sorted, int64_t n, double* out, int64_t*
   hipLaunchKernelGGL(k_auc_area, dim3(grid_for(n, kThreads, 1024)), dim3(kThreads), 0, s,
                      label_sorted, excl, n, out);
   hipLaunchKernelGGL(k_auc_final, dim3(1), dim3(1), 0, s, excl, n, out);
+}
+
+}  // namespace wh
+
+namespace wh {
+
+// persistent (zeroed once; lohi[0] = ~0): cnt, pcnt [NB] u32, lohi [2] u64,
+// area u64, ticket u32 (+pad).  scratch: off, poff [NB + 1] u32, {lo, width},
+// per-example (bucket, rank) and the bucket-ordered keys.
+int64_t auc_ws_bytes(int64_t n) {
+  return 2 * ((int64_t)kAucBuckets + 4) * 4 + 16 + 2 * 8 + 8 * n + 8 * n + 64;
+}
+int64_t auc_ws_persistent_bytes() { return 2 * (int64_t)kAucBuckets * 4 + 4 * 8; }
+int64_t auc_ws_lohi_offset() { return 2 * (int64_t)kAucBuckets * 4; }
+
+void auc_accumulate(const float* py, const float* label, int64_t n, void* persist, void* scratch,
+                    double* auc_sum, hipStream_t s) {
+  if (n <= 0) return;
+  char* base = static_cast<char*>(persist);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(base);
+  uint32_t* pcnt = cnt + kAucBuckets;
+  unsigned long long* lohi = reinterpret_cast<unsigned long long*>(pcnt + kAucBuckets);
+  unsigned long long* area = lohi + 2;
+  unsigned int* ticket = reinterpret_cast<unsigned int*>(lohi + 3);
+  char* sc = static_cast<char*>(scratch);
+  uint32_t* off = reinterpret_cast<uint32_t*>(sc);
+  uint32_t* poff = off + kAucBuckets + 4;  // 16-byte aligned for the vector stores
+  unsigned long long* lw = reinterpret_cast<unsigned long long*>(
+      (reinterpret_cast<uintptr_t>(poff + kAucBuckets + 4) + 15) & ~(uintptr_t)15);
+  int2* br = reinterpret_cast<int2*>(lw + 2);
+  unsigned long long* sorted = reinterpret_cast<unsigned long long*>(br + n);
+  const int g = grid_for(n, kThreads);
+  hipLaunchKernelGGL(k_auc_minmax, dim3(grid_for(n, 1024, 64)), dim3(1024), 0, s, py, label, n,
+                     lohi);
+  hipLaunchKernelGGL(k_auc_bucket, dim3(g), dim3(kThreads), 0, s, py, label, n, lohi, cnt, pcnt,
+                     br);
+  hipLaunchKernelGGL(k_auc_scan, dim3(1), dim3(kAucScanThreads), 0, s, cnt, pcnt, lohi, off, poff,
+                     lw);
+  hipLaunchKernelGGL(k_auc_place, dim3(g), dim3(kThreads), 0, s, py, label, n, br, off, sorted);
+  hipLaunchKernelGGL(k_auc_count, dim3(g), dim3(kThreads), 0, s, sorted, n, off, poff, lw, area,
+                     ticket, auc_sum);
 }
 
 }  // namespace wh

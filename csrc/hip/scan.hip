@@ -107,6 +107,21 @@ void scan_impl(const T* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t s
 
 }  // namespace
 
+int64_t lookback_ws_words() { return (int64_t)kLbChannels * kLbMaxTiles + 2; }
+
+Lookback lookback_bind(void* ws) {
+  static unsigned int epoch = 0;  // 30-bit, never 0
+  epoch = (epoch + 1) & ((1u << 30) - 1);
+  if (epoch == 0) epoch = 1;
+  Lookback lb;
+  lb.gran = static_cast<unsigned long long*>(ws);
+  unsigned int* tail = reinterpret_cast<unsigned int*>(lb.gran + (size_t)kLbChannels * kLbMaxTiles);
+  lb.ticket = tail;
+  lb.err = tail + 1;
+  lb.epoch = epoch;
+  return lb;
+}
+
 int64_t scan_tmp_elems(int64_t n) { return (n + kTile - 1) / kTile + 1; }
 
 void scan_i32(const int32_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t s) {

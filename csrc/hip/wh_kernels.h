@@ -16,6 +16,20 @@ namespace wh {
 int64_t scan_tmp_elems(int64_t n);
 void scan_i32(const int32_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t s);
 void scan_i64(const int64_t* in, int64_t* out, int64_t n, int64_t* tmp, hipStream_t s);
+// Decoupled look-back state (device side in wh_lookback.h).
+constexpr int kLbMaxTiles = 1 << 16;
+constexpr int kLbChannels = 2;
+struct Lookback {
+  unsigned long long* gran;  // [kLbChannels][kLbMaxTiles] {tag, value} granules
+  unsigned int* ticket;      // [1], zero between launches
+  unsigned int* err;         // [1], sticky spin-timeout flag
+  unsigned int epoch;        // 1 .. 2^30-1, new per launch
+};
+// Workspace of the single-pass look-back scans (wh_lookback.h): ONE per
+// device, zero-initialised once, shared by every fused-scan kernel on the
+// device's compute stream. lookback_bind hands out a fresh epoch per launch.
+int64_t lookback_ws_words();  // uint64 words
+Lookback lookback_bind(void* ws);
 
 // ------------------------------------------------------------ localize.hip
 // Batch-local de-duplication of uint64 feature ids (reference Localizer,
@@ -30,11 +44,13 @@ void loc_insert(const uint64_t* keys, int64_t nnz, uint64_t* tkeys, int64_t tsiz
 // per-owner counts of the occupied slots (owner = mix64b(key) % nshard):
 // blkcnt [nshard * loc_owner_blocks(tsize)] becomes the owner-major exclusive
 // scan of the per-block counts (= blkoff for loc_assign); owner_cnt[0..nshard)
+// and owner_cnt[nshard] = *overflow, which is reset to 0.
 int64_t loc_owner_blocks(int64_t tsize);
 void loc_owner_count(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* blkcnt,
-                     int64_t* owner_cnt, hipStream_t s);
-// assign local ids grouped by owner. Writes tlid[slot], uniq[lid].
-void loc_assign(const uint64_t* tkeys, int64_t tsize, int nshard, const int64_t* blkoff,
+                     int64_t* owner_cnt, int64_t* overflow, hipStream_t s);
+// assign local ids grouped by owner. Writes tlid[slot], uniq[lid] and
+// empties every slot it read, so a persistent table needs no clearing pass.
+void loc_assign(uint64_t* tkeys, int64_t tsize, int nshard, const int64_t* blkoff,
                 int32_t* tlid, uint64_t* uniq, hipStream_t s);
 // CSR row id of every non-zero
 void row_of_nnz(const int64_t* offset, int64_t nrows, int32_t* row_of, hipStream_t s);
@@ -105,8 +121,9 @@ struct DifactoHP {
   uint64_t seed;
 };
 // add feature counts (reference AdaGradHandle::Push with kPushFeaCnt)
-void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt, int64_t n,
-                      DifactoHP hp, hipStream_t s);
+// (counts as float cnt OR int32 cnti; the other is null)
+void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt,
+                      const int32_t* cnti, int64_t n, DifactoHP hp, hipStream_t s);
 // Variable-length pull (reference ZVPull, learn/difacto/async_sgd.h:234-244):
 //   pass 1 (difacto_pull_hdr): hdr[i] = {w, -}, vflag[i] = key has a V row
 //          (and, with l1_shrk, w != 0)
@@ -126,6 +143,14 @@ void difacto_push(const KVTable& t, const int32_t* slot, const float* hdr, const
 // scan_tmp_elems(n) int64; count[0] = m
 void vidx_renumber(float* hdr, int64_t n, int32_t* flag_tmp, int64_t* pos_tmp, int64_t* scan_tmp,
                    hipStream_t s);
+// single-launch versions (return false when n is beyond the look-back tile
+// limit; the caller then uses the multi-launch path above). The fused pull
+// writes hdr {w, vidx}, vpos[n + 1] (exclusive scan of the V flags, vpos[n]
+// = m) and the V rows.
+bool difacto_pull_fused(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk,
+                        const Lookback& lb, float* hdr, int64_t* vpos, float* vc, hipStream_t s);
+bool vidx_renumber_fused(float* hdr, int64_t n, const Lookback& lb, int64_t* count,
+                         hipStream_t s);
 
 // ---------------------------------------------------------------- fm.hip
 // Forward of FM / linear model on a localized minibatch.
@@ -137,7 +162,8 @@ void vidx_renumber(float* hdr, int64_t n, int32_t* flag_tmp, int64_t* pos_tmp, i
 int64_t fm_fwd_partials();
 void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
                 const float* w_or_hdr, const float* vc, int vstride, const float* label, int loss,
-                float* py, float* dual, float* xv, double* met, double* part, hipStream_t s);
+                float* py, float* dual, float* xv, double* met, double* part,
+                unsigned int* ticket, hipStream_t s);
 // Backward: gw[U] for every key, gvc[m] for the keys with an embedding row
 //   gw_k = sum_i dual_i x_ik
 //   gV_k = sum_i dual_i x_ik xv_i - (sum_i dual_i x_ik^2) V_k
@@ -151,7 +177,8 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
                  const int32_t* csc_row, const float* csc_val, const float* dual, const float* xv,
                  const float* hdr, const float* vc, int vstride, float* gw, float* gvc,
                  int32_t* chunk_key, int32_t* chunk_beg, int32_t* meta_v, int32_t* bucket_hist,
-                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, hipStream_t s);
+                 int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, const Lookback* lb,
+                 hipStream_t s);
 // post-process the m (device count) V-gradient rows: clip to [-c, c] (c>0),
 // dropout with prob p (p>0); sumsq (optional) receives the squared norm
 void fm_grad_post(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim, float clip,
@@ -175,6 +202,15 @@ void sort_by_score(const float* py, const float* label, int64_t n, float* py_sor
                    float* label_sorted, void* tmp, size_t tmp_bytes, hipStream_t s);
 void auc_from_sorted(const float* label_sorted, int64_t n, double* out, int64_t* tmp_i64,
                      hipStream_t s);
+// Sort-free exact AUC (bucketed rank-sum, see metrics.hip), accumulated into
+// *auc_sum on the device. persist: auc_ws_persistent_bytes(), zero except
+// the uint64 at auc_ws_lohi_offset() = ~0 (every call restores that state;
+// one per device, used in stream order). scratch: auc_ws_bytes(n).
+int64_t auc_ws_bytes(int64_t n);
+int64_t auc_ws_persistent_bytes();
+int64_t auc_ws_lohi_offset();
+void auc_accumulate(const float* py, const float* label, int64_t n, void* persist, void* scratch,
+                    double* auc_sum, hipStream_t s);
 
 // ------------------------------------------------------------ synth.hip
 // Criteo-1TB-shaped synthetic minibatch: 13 integer + 26 categorical fields,

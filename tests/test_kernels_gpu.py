@@ -172,6 +172,82 @@ def test_auc(hip):
     assert float(one) == 1.0
 
 
+def test_auc_ties_and_accumulate(hip):
+    """Sort-free bucketed AUC vs the stable-sort reference and the rocPRIM
+    sort path: heavy ties (quantised scores), all-equal scores (a zero
+    model), +-0, and on-device accumulation over repeated calls."""
+    g = torch.Generator().manual_seed(6)
+    cases = []
+    for n in [1, 2, 777, 65536, 300001]:
+        py = torch.randn(n, generator=g)
+        cases.append((py, (torch.rand(n, generator=g) < torch.sigmoid(2 * py)).float()))
+        q = torch.round(py * 4) / 4  # few distinct values: long tie runs
+        cases.append((q, (torch.rand(n, generator=g) < 0.3).float()))
+    z = torch.zeros(4096)
+    z[::3] = -0.0
+    cases.append((z, (torch.rand(4096, generator=g) < 0.5).float()))
+    acc = torch.zeros(1, dtype=torch.float64, device=DEV)
+    tot = 0.0
+    for py, lab in cases:
+        r = float(ref.auc(py, lab))
+        a = float(hip.auc(py.to(DEV), lab.to(DEV)))
+        b = float(hip.auc_sorted(py.to(DEV), lab.to(DEV)))
+        assert abs(a - r) < 1e-9, (py.numel(), a, r)
+        assert abs(b - r) < 1e-9
+        hip.auc_acc(py.to(DEV), lab.to(DEV), acc)
+        tot += r
+    assert abs(float(acc) - tot) < 1e-8
+
+
+def test_lookback_fused_paths_large(hip):
+    """Fused single-pass scans over many tiles (multi-window look-back):
+    pull, vidx renumbering and backward chunk planning at U ~ 200k."""
+    from wormhole_amd.kv.cpu_store import CpuKVStore
+    n = 200_003
+    gk = torch.Generator().manual_seed(11)
+    keys = torch.unique(torch.randint(1, 1 << 40, (2 * n,), generator=gk))[:n]
+    keys = keys[torch.randperm(n, generator=gk)] * 2 + 1
+    gs = hip.KVStore(1 << 19, 1 << 18, 16, 0)
+    cs = CpuKVStore(1 << 19, 1 << 18, 16)
+    hp = [0.1, 1.0, 0.0, 0.0, 0.1, 1.0, 0.0, 0.01]
+    cnt = (torch.rand(n) * 4).floor()
+    sg = gs.find(keys.to(DEV), True)
+    sc = cs.find(keys, True)
+    gs.difacto_push_cnt(sg, cnt.int().to(DEV), hp, 1, False, 3)
+    cs.difacto_push_cnt(sc, cnt, hp, 1, False, 3)
+    for _ in range(2):  # second call: a fresh epoch over stale granules
+        hg, vg, vpg = gs.difacto_pull(sg, False)
+    hc, vcc, vpc = cs.difacto_pull(sc, False)
+    assert torch.equal(ref.hdr_vidx(hg.cpu()), ref.hdr_vidx(hc))
+    assert torch.equal(vpg.cpu(), vpc)
+    m = int(vpc[-1])
+    assert torch.allclose(vg.cpu()[:m], vcc[:m])
+    # renumber a header whose vidx are scattered
+    h = hg.clone()
+    vi = ref.hdr_vidx(h.cpu()).long()
+    exp = torch.where(vi >= 0, torch.cumsum((vi >= 0).long(), 0) - 1, -1)
+    mm = hip.vidx_renumber(h)
+    assert int(mm) == int((vi >= 0).sum())
+    assert torch.equal(ref.hdr_vidx(h.cpu()).long(), exp)
+    # backward with ~200k unique ids
+    keys2, off, _, label = _rand_batch(40000, 12, 400000, 9, False, skew=False)
+    uniq, ucnt, oc, lid, csc_off, csc_row, csc_val = hip.localize(keys2.to(DEV), off.to(DEV),
+                                                                  None, 1)[:7]
+    U = uniq.numel()
+    assert U > 100000
+    hdr, vc = _pulled(U, 16, 16, 4)
+    dual = torch.randn(40000)
+    xv = torch.randn(40000, 16)
+    gw, gvc = hip.fm_backward(csc_off, csc_row, None, dual.to(DEV), xv.reshape(-1).to(DEV),
+                              hdr.to(DEV), vc.to(DEV), 16)
+    gw_r, gvc_r = ref.fm_backward(csc_off.cpu(), csc_row.cpu(), None, dual, xv.reshape(-1), hdr,
+                                  vc, 16)
+    assert torch.allclose(gw.cpu(), gw_r, atol=1e-4, rtol=1e-3)
+    live = ref.hdr_vidx(hdr).long()
+    live = live[live >= 0]
+    assert torch.allclose(gvc.cpu()[live], gvc_r[live], atol=1e-4, rtol=1e-3)
+
+
 @pytest.mark.parametrize("algo", [1, 2, 3])
 def test_linear_store_updates(hip, algo):
     from wormhole_amd.kv.cpu_store import CpuKVStore

@@ -141,7 +141,9 @@ class ShardedKV:
     def difacto_push_cnt(self, sess, hp, threshold, l1_shrk, seed):
         """Feature-count push (kPushFeaCnt); the counts travelled with the
         keys in :meth:`open`."""
-        c = sess.cnt.float() if sess.cnt.dtype != torch.float32 else sess.cnt
+        c = sess.cnt
+        if not (c.is_cuda and c.dtype == torch.int32) and c.dtype != torch.float32:
+            c = c.float()  # (the GPU kernel takes int32 counts directly)
         for a, b in sess.segments():
             if b > a:
                 self.store.difacto_push_cnt(sess.slots[a:b], c[a:b], hp, threshold, l1_shrk, seed)

@@ -71,7 +71,7 @@ class DifactoLearner:
             hdr, vc = hdr[:, 0].contiguous(), None
         py, dual, xv = ops.fm_forward(offset, lid, val, hdr, vc, self.vstride, label,
                                       ops.LOSS_LOGIT, self.met)
-        self.auc_sum += ops.auc(py, label)
+        ops.auc_acc(py, label, self.auc_sum)
         self.n_mb += 1
         if train:
             gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, hdr, vc, self.vstride)

@@ -41,7 +41,7 @@ class LinearLearner:
         sess = self.kv.open(uniq, owner_cnt, insert=train, recv=loc[7] if ex is not None else None)
         w = self.kv.linear_pull(sess)
         py, dual, _ = ops.fm_forward(offset, lid, val, w, None, 0, label, self.conf.loss, self.met)
-        self.auc_sum += ops.auc(py, label)
+        ops.auc_acc(py, label, self.auc_sum)
         self.n_mb += 1
         if train:
             grad, _ = ops.fm_backward(csc_off, csc_row, csc_val, dual, None, w, None, 0)

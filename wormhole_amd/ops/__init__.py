@@ -124,3 +124,12 @@ def auc(py, label):
     if _gpu(py):
         return _native.hip().auc(py, label)
     return ref.auc(py, label)
+
+
+def auc_acc(py, label, auc_sum):
+    """auc_sum (float64 [1]) += exact AUC of the minibatch, on the device."""
+    if _gpu(py):
+        _native.hip().auc_acc(py, label, auc_sum)
+        return auc_sum
+    auc_sum += ref.auc(py, label)
+    return auc_sum
