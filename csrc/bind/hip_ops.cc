@@ -179,10 +179,11 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
                  reinterpret_cast<uint64_t*>(uniq.data_ptr()), s);
   ws.loc_dirty = false;
   auto row_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
-  wh::row_of_nnz(ptr<int64_t>(offset), nrows, ptr<int32_t>(row_of), s);
   const int64_t n1 = std::max<int64_t>(nnz, 1);
   auto lid = torch::empty({nnz}, i32);
   auto work = torch::empty({3 * n1}, i32);  // pos | sorted lid | sorted pos
+  wh::loc_rows_lid(ptr<int64_t>(offset), nrows, ptr<int32_t>(slot_of), ptr<int32_t>(tlid),
+                   ptr<int32_t>(row_of), ptr<int32_t>(lid), vp ? ptr<int32_t>(work) : nullptr, s);
   const size_t sbytes = wh::loc_sort_tmp_bytes(nnz, U);
   auto stmp = torch::empty({(int64_t)sbytes + 16}, keys.options().dtype(torch::kUInt8));
   auto csc_off = torch::empty({U + 1}, i64);
@@ -191,7 +192,7 @@ std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
   auto csc_val = vp ? torch::empty({nnz}, keys.options().dtype(torch::kFloat32))
                     : torch::empty({0}, keys.options().dtype(torch::kFloat32));
   int32_t* wp = ptr<int32_t>(work);
-  wh::loc_csc(ptr<int32_t>(slot_of), ptr<int32_t>(tlid), ptr<int32_t>(row_of), vp, nnz, U,
+  wh::loc_csc(ptr<int32_t>(row_of), vp, nnz, U,
               ptr<int32_t>(lid), wp, wp + n1, wp + 2 * n1, stmp.data_ptr(), sbytes,
               ptr<int64_t>(csc_off), ptr<int32_t>(ucnt), ptr<int32_t>(csc_row),
               vp ? ptr<float>(csc_val) : nullptr, s);
@@ -340,6 +341,44 @@ class KVStore {
                             ptr<int64_t>(vpos), ptr<float>(hdr), ptr<float>(vc), s);
     }
     return {hdr, vc, vpos};
+  }
+
+  // Single-shard open + pull in one launch. Returns (slot i32 [n], hdr, vc,
+  // vpos) like find() followed by difacto_push_cnt() (when cnt is given) and
+  // difacto_pull(). Keys must be distinct.
+  std::vector<Tensor> difacto_open_pull(const Tensor& keys, bool insert,
+                                        const c10::optional<Tensor>& cnt,
+                                        const std::vector<double>& h, int64_t threshold,
+                                        bool l1_shrk, int64_t seed) {
+    CHECK_IN(keys, torch::kInt64);
+    const int32_t* cp = nullptr;
+    if (cnt.has_value() && cnt->defined()) {
+      CHECK_IN((*cnt), torch::kInt32);
+      TORCH_CHECK(cnt->numel() >= keys.numel(), "open_pull: count size mismatch");
+      cp = ptr<int32_t>(*cnt);
+    }
+    c10::DeviceGuard g(keys.device());
+    auto s = cur_stream(keys);
+    const int64_t n = keys.numel();
+    auto f32 = keys.options().dtype(torch::kFloat32);
+    auto slot = torch::empty({n}, keys.options().dtype(torch::kInt32));
+    auto hdr = torch::empty({n, 2}, f32);
+    auto vpos = torch::empty({n + 1}, keys.options());
+    auto vc = torch::empty({vstride_ > 0 ? n : 0, (int64_t)std::max(vstride_, 1)}, f32);
+    if (n == 0) {
+      vpos.zero_();
+      return {slot, hdr, vc, vpos};
+    }
+    if (!wh::difacto_open_pull(table(), reinterpret_cast<const uint64_t*>(keys.data_ptr()), n,
+                               cp, dhp(h, threshold, l1_shrk, seed), insert ? 1 : 0,
+                               lookback(keys.device()), ptr<int32_t>(slot), ptr<float>(hdr),
+                               ptr<int64_t>(vpos), ptr<float>(vc), s)) {
+      slot = find(keys, insert);
+      if (cp) difacto_push_cnt(slot, *cnt, h, threshold, l1_shrk, seed);
+      auto r = difacto_pull(slot, l1_shrk);
+      return {slot, r[0], r[1], r[2]};
+    }
+    return {slot, hdr, vc, vpos};
   }
 
   // hdr: this shard's pull header for the same keys (owner vidx numbering)
@@ -784,6 +823,7 @@ PYBIND11_MODULE(_hip, m) {
       .def("linear_push", &KVStore::linear_push)
       .def("difacto_push_cnt", &KVStore::difacto_push_cnt)
       .def("difacto_pull", &KVStore::difacto_pull)
+      .def("difacto_open_pull", &KVStore::difacto_open_pull)
       .def("difacto_push", &KVStore::difacto_push)
       .def_property_readonly("dim", &KVStore::dim)
       .def_property_readonly("vstride", &KVStore::vstride)

@@ -319,6 +319,147 @@ __global__ __launch_bounds__(kThreads) void k_difacto_pull(KVTable t, const int3
   }
 }
 
+// One-launch minibatch open on a single shard: find-or-insert every key,
+// (data pass 0) add its feature count and lazily allocate + initialise its
+// embedding row, then the variable-length pull (look-back scan of the V
+// flags, header, compact rows). Replaces kv_find -> difacto_push_cnt ->
+// difacto_pull: the three passes re-visited the same 32-byte slot of every
+// key. Keys must be distinct (one worker's minibatch).
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_difacto_open_pull(
+    KVTable t, const uint64_t* __restrict__ keys, int64_t n, const int32_t* __restrict__ cnt,
+    DifactoHP hp, int insert, Lookback lb, int ntiles, int32_t* __restrict__ slot_out,
+    float2* hdr, int64_t* vpos, float* vc) {
+  __shared__ uint32_t shs[16];
+  __shared__ int sht;
+  const int tile = lb_tile(lb, ntiles, &sht);
+  const int lane = threadIdx.x & 63;
+  const int64_t i0 = (int64_t)tile * kPullTile + threadIdx.x * kPullPer;
+  const uint64_t mask = (uint64_t)t.cap - 1;
+  uint64_t k[kPullPer];
+  int32_t sl[kPullPer];
+  uint64_t h[kPullPer], prev[kPullPer];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) k[r] = i0 + r < n ? keys[i0 + r] : kEmptyKey;
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {  // all home-slot probes in flight together
+    h[r] = mix64(k[r]) & mask;
+    prev[r] = k[r] != kEmptyKey ? ld_relaxed(&t.sl[h[r]].key) : 0;
+  }
+  int created = 0, failed = 0;
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    sl[r] = -1;
+    if (k[r] == kEmptyKey) continue;
+    uint64_t hh = h[r], pv = prev[r];
+    for (int64_t probe = 0; probe < t.cap; ++probe) {
+      if (pv == k[r]) { sl[r] = (int32_t)hh; break; }
+      if (pv == kEmptyKey) {
+        if (!insert) break;
+        const uint64_t old = atomicCAS((unsigned long long*)(&t.sl[hh].key),
+                                       (unsigned long long)kEmptyKey, (unsigned long long)k[r]);
+        if (old == kEmptyKey) { sl[r] = (int32_t)hh; ++created; break; }
+        if (old == k[r]) { sl[r] = (int32_t)hh; break; }
+      }
+      hh = (hh + 1) & mask;
+      pv = ld_relaxed(&t.sl[hh].key);
+    }
+    if (insert && sl[r] < 0) ++failed;
+    if (i0 + r < n) slot_out[i0 + r] = sl[r];
+  }
+  float w[kPullPer];
+  int32_t row[kPullPer];
+  bool fresh[kPullPer];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    w[r] = 0.f;
+    row[r] = -1;
+    fresh[r] = false;
+    if (sl[r] < 0) continue;
+    KVSlot& e = t.sl[sl[r]];
+    w[r] = e.w;
+    row[r] = t.vstride > 0 ? e.vrow : -1;
+    if (cnt) {
+      const uint32_t c = e.cnt + (uint32_t)cnt[i0 + r];
+      e.cnt = c;
+      fresh[r] = t.vstride > 0 && c > hp.threshold && row[r] < 0 &&
+                 (!hp.l1_shrk || w[r] != 0.f);
+    }
+  }
+  long long newv = 0;
+  if (cnt && t.vstride > 0) {
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r) {
+      const int32_t nr = wave_alloc_rows(t, fresh[r]);
+      fresh[r] = nr >= 0;
+      if (nr >= 0) {
+        t.sl[sl[r]].vrow = nr;
+        row[r] = nr;
+        newv += t.dim;
+      }
+    }
+  }
+  uint32_t f[1] = {0u}, ex[1], tot[1];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    if (hp.l1_shrk && w[r] == 0.f) row[r] = -1;  // (a fresh row has w != 0)
+    f[0] += row[r] >= 0 ? 1u : 0u;
+  }
+  lb_block_scan<1>(lb, tile, f, ex, tot, shs);
+  int32_t vp[kPullPer];
+  uint32_t run = ex[0];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    vp[r] = row[r] >= 0 ? (int32_t)run : -1;
+    if (i0 + r < n) {
+      hdr[i0 + r] = make_float2(w[r], __int_as_float(vp[r]));
+      vpos[i0 + r] = run;
+    }
+    run += row[r] >= 0 ? 1u : 0u;
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) vpos[n] = tot[0];
+  // event counters: inserts / failed inserts / new embedding weights
+  const long long ci = wave_sum_ll(created), cf = wave_sum_ll(failed), cv = wave_sum_ll(newv);
+  if (lane == 0) {
+    if (ci) atomicAdd(stat_ptr(t.stats, 4), (unsigned long long)ci);
+    if (cf) atomicAdd(stat_ptr(t.stats, 2), (unsigned long long)cf);
+    if (cv) atomicAdd(stat_ptr(t.stats, 1), (unsigned long long)cv);
+  }
+  if (t.vstride == 0) return;
+  // row jobs: a fresh row is initialised into the table AND written to its
+  // pull position from the same registers; an existing row is copied
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    for_each_row_job<G>(row[r] >= 0, [&](int src, int gl) {
+      const int s2 = src >= 0 ? src : lane;
+      const int32_t jr = __shfl(row[r], s2, 64), jp = __shfl(vp[r], s2, 64);
+      const int jf = __shfl((int)fresh[r], s2, 64);
+      const uint64_t jk = __shfl(k[r], s2, 64);
+      if (src < 0) return;
+      float* V = t.V + (int64_t)jr * t.vstride;
+      float* o = vc + (int64_t)jp * t.vstride;
+      if (jf) {
+        float* VG = t.VG + (int64_t)jr * t.vstride;
+        for (int c = gl * 4; c < t.vstride; c += 4 * G) {
+          float4 v;
+          float* pv = &v.x;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int d = c + e;
+            pv[e] = d < t.dim ? (uhash01(hp.seed, jk, (uint64_t)d) * 2.f - 1.f) * hp.v_init : 0.f;
+          }
+          *reinterpret_cast<float4*>(V + c) = v;
+          *reinterpret_cast<float4*>(VG + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(o + c) = v;
+        }
+      } else {
+        for (int c = gl * 4; c < t.vstride; c += 4 * G)
+          *reinterpret_cast<float4*>(o + c) = *reinterpret_cast<const float4*>(V + c);
+      }
+    });
+  }
+}
+
 // worker side of a multi-shard pull, fused: flag -> scan -> renumber
 __global__ __launch_bounds__(kThreads) void k_vidx_renumber(float2* hdr, int64_t n, Lookback lb,
                                                             int ntiles, int64_t* count) {
@@ -565,6 +706,22 @@ bool vidx_renumber_fused(float* hdr, int64_t n, const Lookback& lb, int64_t* cou
   if (n <= 0 || ntiles > kLbMaxTiles) return false;
   hipLaunchKernelGGL(k_vidx_renumber, dim3((unsigned)ntiles), dim3(kThreads), 0, s,
                      reinterpret_cast<float2*>(hdr), n, lb, (int)ntiles, count);
+  return true;
+}
+
+}  // namespace wh
+
+namespace wh {
+
+bool difacto_open_pull(const KVTable& t, const uint64_t* keys, int64_t n, const int32_t* cnt,
+                       DifactoHP hp, int insert, const Lookback& lb, int32_t* slot, float* hdr,
+                       int64_t* vpos, float* vc, hipStream_t s) {
+  const int64_t ntiles = (n + kPullTile - 1) / kPullTile;
+  if (n <= 0 || ntiles > kLbMaxTiles) return false;
+  const int G = lanes_per_key(t.vstride);
+  const dim3 grid((unsigned)ntiles), block(kThreads);
+  WH_DISPATCH_G(G, k_difacto_open_pull, grid, block, 0, s, t, keys, n, cnt, hp, insert, lb,
+                (int)ntiles, slot, reinterpret_cast<float2*>(hdr), vpos, vc);
   return true;
 }
 

@@ -14,8 +14,9 @@
 //                 ids, grouped by owning shard so the id order IS the send
 //                 order of the key exchange (no separate partition pass);
 //                 per-block owner counts + one scan, no global atomics.
-//   loc_csc     : lid[j] = tlid[slot_of[j]] (the nnz -> local id map), then
-//                 a radix sort of (lid, j) pairs on ceil(log2 U) bits
+//   loc_rows_lid: lid[j] = tlid[slot_of[j]] (the nnz -> local id map) and
+//                 the row of every non-zero, one wave per row;
+//   loc_csc     : a radix sort of (lid, j) pairs on ceil(log2 U) bits
 //                 (rocPRIM onesweep; stable, so every id's occurrence list
 //                 comes out in row order -> a deterministic CSC), then
 //                 csc_row/csc_val gathered through the sorted positions and
@@ -245,20 +246,20 @@ __global__ __launch_bounds__(kThreads) void k_assign(uint64_t* __restrict__ tkey
   }
 }
 
-__global__ void k_row_of(const int64_t* __restrict__ off, int64_t nrows, int32_t* row_of) {
-  // one wave per row: lanes stride over the row's non-zeros
-  const int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+// one wave per CSR row: the row id and the local id of each of its non-zeros
+// (lid[j] = tlid[slot_of[j]]), plus the position payload for valued data
+__global__ __launch_bounds__(kThreads) void k_rows_lid(const int64_t* __restrict__ off,
+                                                       int64_t nrows,
+                                                       const int32_t* __restrict__ slot_of,
+                                                       const int32_t* __restrict__ tlid,
+                                                       int32_t* __restrict__ row_of,
+                                                       int32_t* __restrict__ lid,
+                                                       int32_t* __restrict__ pos) {
+  const int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (row >= nrows) return;
-  for (int64_t j = off[row] + lane; j < off[row + 1]; j += 64) row_of[j] = (int32_t)row;
-}
-
-__global__ __launch_bounds__(kThreads) void k_loc_lid(const int32_t* __restrict__ slot_of,
-                                                      const int32_t* __restrict__ tlid,
-                                                      int64_t nnz, int32_t* __restrict__ lid,
-                                                      int32_t* __restrict__ pos) {
-  const int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (j < nnz) {
+  for (int64_t j = off[row] + lane; j < off[row + 1]; j += 64) {
+    row_of[j] = (int32_t)row;
     lid[j] = tlid[slot_of[j]];
     if (pos) pos[j] = (int32_t)j;
   }
@@ -325,11 +326,13 @@ void loc_assign(uint64_t* tkeys, int64_t tsize, int nshard, const int64_t* blkof
                      blkoff, tlid, uniq);
 }
 
-void row_of_nnz(const int64_t* offset, int64_t nrows, int32_t* row_of, hipStream_t s) {
+void loc_rows_lid(const int64_t* offset, int64_t nrows, const int32_t* slot_of,
+                  const int32_t* tlid, int32_t* row_of, int32_t* lid, int32_t* pos,
+                  hipStream_t s) {
   if (nrows <= 0) return;
   const int64_t threads = nrows * 64;
-  hipLaunchKernelGGL(k_row_of, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, offset,
-                     nrows, row_of);
+  hipLaunchKernelGGL(k_rows_lid, dim3((unsigned)((threads + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, s, offset, nrows, slot_of, tlid, row_of, lid, pos);
 }
 
 size_t loc_sort_tmp_bytes(int64_t nnz, int64_t nuniq) {
@@ -341,8 +344,8 @@ size_t loc_sort_tmp_bytes(int64_t nnz, int64_t nuniq) {
   return bytes;
 }
 
-void loc_csc(const int32_t* slot_of, const int32_t* tlid, const int32_t* row_of,
-             const float* val, int64_t nnz, int64_t nuniq, int32_t* lid, int32_t* pos,
+void loc_csc(const int32_t* row_of, const float* val, int64_t nnz, int64_t nuniq,
+             int32_t* lid, int32_t* pos,
              int32_t* slid, int32_t* spos, void* sort_tmp, size_t sort_tmp_bytes,
              int64_t* csc_off, int32_t* ucnt, int32_t* csc_row, float* csc_val, hipStream_t s) {
   if (nnz <= 0) {
@@ -354,8 +357,6 @@ void loc_csc(const int32_t* slot_of, const int32_t* tlid, const int32_t* row_of,
   // straight into csc_row; valued data: sort positions, then gather
   int32_t* vin = val ? pos : const_cast<int32_t*>(row_of);
   int32_t* vout = val ? spos : csc_row;
-  hipLaunchKernelGGL(k_loc_lid, dim3(grid_for(nnz, kThreads)), dim3(kThreads), 0, s, slot_of,
-                     tlid, nnz, lid, val ? pos : nullptr);
   size_t bytes = sort_tmp_bytes;
   WH_HIP_CHECK(rocprim::radix_sort_pairs(sort_tmp, bytes, lid, slid, vin, vout, (size_t)nnz, 0,
                                          bits_for(nuniq), s));

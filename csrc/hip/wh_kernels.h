@@ -52,13 +52,16 @@ void loc_owner_count(const uint64_t* tkeys, int64_t tsize, int nshard, int64_t* 
 // empties every slot it read, so a persistent table needs no clearing pass.
 void loc_assign(uint64_t* tkeys, int64_t tsize, int nshard, const int64_t* blkoff,
                 int32_t* tlid, uint64_t* uniq, hipStream_t s);
-// CSR row id of every non-zero
-void row_of_nnz(const int64_t* offset, int64_t nrows, int32_t* row_of, hipStream_t s);
-// nnz -> local id map and the CSC (per-id occurrence lists, in row order)
-// plus per-id counts. Scratch: pos/slid/spos [nnz] int32, sort_tmp.
+// CSR row id and local id (lid[j] = tlid[slot_of[j]]) of every non-zero;
+// pos[j] = j when non-null (the sort payload of valued data)
+void loc_rows_lid(const int64_t* offset, int64_t nrows, const int32_t* slot_of,
+                  const int32_t* tlid, int32_t* row_of, int32_t* lid, int32_t* pos,
+                  hipStream_t s);
+// the CSC (per-id occurrence lists, in row order) plus per-id counts from
+// lid / row_of. Scratch: pos/slid/spos [nnz] int32, sort_tmp.
 size_t loc_sort_tmp_bytes(int64_t nnz, int64_t nuniq);
-void loc_csc(const int32_t* slot_of, const int32_t* tlid, const int32_t* row_of,
-             const float* val, int64_t nnz, int64_t nuniq, int32_t* lid, int32_t* pos,
+void loc_csc(const int32_t* row_of, const float* val, int64_t nnz, int64_t nuniq,
+             int32_t* lid, int32_t* pos,
              int32_t* slid, int32_t* spos, void* sort_tmp, size_t sort_tmp_bytes,
              int64_t* csc_off, int32_t* ucnt, int32_t* csc_row, float* csc_val, hipStream_t s);
 
@@ -149,6 +152,11 @@ void vidx_renumber(float* hdr, int64_t n, int32_t* flag_tmp, int64_t* pos_tmp, i
 // = m) and the V rows.
 bool difacto_pull_fused(const KVTable& t, const int32_t* slot, int64_t n, int l1_shrk,
                         const Lookback& lb, float* hdr, int64_t* vpos, float* vc, hipStream_t s);
+// single-shard minibatch open: find-or-insert the (distinct) keys -> slot,
+// add cnt (int32, may be null) with lazy V allocation, then the fused pull
+bool difacto_open_pull(const KVTable& t, const uint64_t* keys, int64_t n, const int32_t* cnt,
+                       DifactoHP hp, int insert, const Lookback& lb, int32_t* slot, float* hdr,
+                       int64_t* vpos, float* vc, hipStream_t s);
 bool vidx_renumber_fused(float* hdr, int64_t n, const Lookback& lb, int64_t* count,
                          hipStream_t s);
 

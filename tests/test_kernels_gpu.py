@@ -386,3 +386,34 @@ def test_spmv_kernels(hip):
     yt = hip.spmv_t(csc_off, csc_row, csc_val, p.to(DEV)).cpu()
     ref_t = torch.zeros(uniq.numel()).index_add_(0, lid.cpu().long(), val * p[rows])
     assert torch.allclose(yt, ref_t, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("l1_shrk", [False, True])
+def test_difacto_open_pull_fused(hip, l1_shrk):
+    """The one-launch find + count push + pull against the host store doing
+    the three steps: slots resolve to the same keys, counts cross the
+    threshold at the same step, and the pulled headers / rows agree."""
+    from wormhole_amd.kv.cpu_store import CpuKVStore
+    gs = hip.KVStore(1 << 16, 1 << 14, 16, 0)
+    cs = CpuKVStore(1 << 16, 1 << 14, 16)
+    hp = [0.1, 1.0, 0.0, 0.0, 0.1, 1.0, 0.0, 0.01]
+    g = torch.Generator().manual_seed(12)
+    for step in range(4):
+        keys = torch.unique(torch.randint(1, 5000, (3000,), generator=g)) * 7 + 3
+        keys = keys[torch.randperm(keys.numel(), generator=g)]
+        cnt = torch.randint(0, 3, (keys.numel(),), generator=g)
+        sg, hg, vg, pg = gs.difacto_open_pull(keys.to(DEV), True, cnt.int().to(DEV), hp, 2,
+                                              l1_shrk, 5)
+        sc, hc, vcc, pc = cs.difacto_open_pull(keys, True, cnt.float(), hp, 2, l1_shrk, 5)
+        assert bool((sg >= 0).all())
+        assert torch.equal(gs.keys.cpu()[sg.long().cpu()], keys)
+        assert torch.equal(ref.hdr_vidx(hg.cpu()), ref.hdr_vidx(hc))
+        assert torch.equal(pg.cpu(), pc)
+        m = int(pc[-1])
+        assert torch.allclose(vg.cpu()[:m], vcc[:m])
+        assert torch.allclose(hg.cpu()[:, 0], hc[:, 0], atol=1e-6, rtol=1e-5)
+        # a push so that w moves (l1_shrk then filters on w != 0)
+        gw = torch.randn(keys.numel(), generator=g)
+        gv = torch.randn(max(m, 1), 16, generator=g) * 0.1
+        gs.difacto_push(sg, hg, gw.to(DEV), gv[:m].contiguous().to(DEV), hp, 2, l1_shrk, 5)
+        cs.difacto_push(sc, hc, gw, gv[:m].contiguous(), hp, 2, l1_shrk, 5)

@@ -148,6 +148,30 @@ class ShardedKV:
             if b > a:
                 self.store.difacto_push_cnt(sess.slots[a:b], c[a:b], hp, threshold, l1_shrk, seed)
 
+    def difacto_open_pull(self, uniq, owner_cnt, insert, cnt, hp, threshold, l1_shrk, seed,
+                          recv=None):
+        """open() + (pass 0) difacto_push_cnt() + difacto_pull() as one call.
+        On one shard this is ONE fused device pass over the keys (find,
+        count, lazy V allocation, variable-length pull); with peers it is the
+        exchange sequence of the three calls. Returns (sess, hdr, vc)."""
+        if self.comm.size > 1:
+            sess = self.open(uniq, owner_cnt, insert, cnt=cnt, recv=recv)
+            if cnt is not None:
+                self.difacto_push_cnt(sess, hp, threshold, l1_shrk, seed)
+            hdr, vc = self.difacto_pull(sess, l1_shrk)
+            return sess, hdr, vc
+        send = [int(x) for x in (owner_cnt.tolist() if hasattr(owner_cnt, "tolist") else owner_cnt)]
+        sess = Session(send, send, uniq)
+        self.flush()
+        if cnt is not None and not (cnt.is_cuda and cnt.dtype == torch.int32):
+            cnt = cnt.int() if cnt.is_cuda else cnt.float()
+        slots, hdr, vc, vpos = self.store.difacto_open_pull(uniq, insert, cnt, hp, threshold,
+                                                            l1_shrk, seed)
+        sess.slots = slots
+        sess.hdr_own = hdr
+        sess.m = vpos[-1:]
+        return sess, hdr, vc
+
     def difacto_pull(self, sess, l1_shrk):
         """Returns (hdr [U, 2], vc [mcap, vstride]) in the worker's key order;
         sess.m holds the live embedding-row count on the device."""

@@ -247,6 +247,14 @@ class CpuKVStore:
                     and (not l1_shrk or self._w[s] != 0)):
                 self._alloc_v(s, seed, h[7])
 
+    def difacto_open_pull(self, keys, insert, cnt, h, threshold, l1_shrk, seed):
+        """find + (optional) count push + pull, like the HIP store's fused op."""
+        slot = self.find(keys, insert)
+        if cnt is not None:
+            self.difacto_push_cnt(slot, cnt, h, threshold, l1_shrk, seed)
+        hdr, vc, vpos = self.difacto_pull(slot, l1_shrk)
+        return slot, hdr, vc, vpos
+
     def difacto_pull(self, slot, l1_shrk):
         """Variable-length pull: (hdr [n, 2] {w, vidx bits}, vc [m, vstride],
         vpos int64 [n+1]) -- the layout of the HIP store (vc is exact here)."""

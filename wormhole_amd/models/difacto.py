@@ -61,11 +61,9 @@ class DifactoLearner:
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
         self.uhint = uniq.numel()
         push_cnt = train and data_pass == 0 and self.dim > 0
-        sess = self.kv.open(uniq, owner_cnt, insert=train, cnt=ucnt if push_cnt else None,
-                            recv=loc[7] if ex is not None else None)
-        if push_cnt:
-            self.kv.difacto_push_cnt(sess, self.hp, self.threshold, self.l1_shrk, self.seed)
-        hdr, vc = self.kv.difacto_pull(sess, self.l1_shrk)
+        sess, hdr, vc = self.kv.difacto_open_pull(
+            uniq, owner_cnt, train, ucnt if push_cnt else None, self.hp, self.threshold,
+            self.l1_shrk, self.seed, recv=loc[7] if ex is not None else None)
         self.last_sizes = (uniq.numel(), sess.m)  # (unique keys, embedding rows; device)
         if self.vstride == 0:  # no embedding: a plain linear model over w
             hdr, vc = hdr[:, 0].contiguous(), None
