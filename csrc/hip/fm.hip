@@ -113,7 +113,14 @@ template <int G>
 struct Shape {
   static constexpr int SUB = 64 / G;             // rows per wave-instruction
   static constexpr int NI = G;                   // instructions per 64 items
-  static constexpr int TI = G < 16 ? G : 16;     // instructions in flight
+#ifndef WH_FM_TI
+#define WH_FM_TI 4
+#endif
+  // instructions per gather batch: a batch only runs while it covers live
+  // slots, so short rows / chunks issue ceil(n / (SUB * TI)) batches instead
+  // of all NI instructions (rocprof: the forward was issue-bound at 43 %
+  // instruction share with 64 slots per row for 39 non-zeros)
+  static constexpr int TI = G < WH_FM_TI ? G : WH_FM_TI;
   static constexpr int VS = 4 * G;               // row stride in floats (= vstride)
 };
 
@@ -133,6 +140,24 @@ __device__ __forceinline__ void stage_pairs(int2* st, int lane, int idx_val, flo
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Forward staging: only the ids that HAVE an embedding row are staged,
+// compacted to the front (the others contribute nothing to the
+// second-order term). Slots past the returned count hold stale pairs: the
+// reader masks them by position.
+template <int G>
+__device__ __forceinline__ int stage_pairs_compact(int2* st, int lane, int vid, float f) {
+  using S = Shape<G>;
+  const bool has = vid >= 0;
+  const uint64_t m = __ballot(has);
+  const int nv = __popcll(m);
+  const int pos = __popcll(m & ((1ull << lane) - 1ull));
+  if (has) st[(pos % S::SUB) * S::NI + pos / S::SUB] = make_int2(vid, __float_as_int(f));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return nv;
 }
 
 template <int G>
@@ -181,7 +206,8 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
   // gather the embedding rows of one 64-id pass and accumulate them
   auto gather = [&](int n, int vid, float x, float4& s, float4& q2, bool prefetch_first,
                     auto&& prefetch) {
-    stage_pairs<G>(st, lane, vid, x);
+    (void)n;
+    n = stage_pairs_compact<G>(st, lane, vid, x);
 #pragma unroll
     for (int t0 = 0; t0 < S::NI; t0 += S::TI) {
       if (t0 * S::SUB >= n) break;
@@ -190,8 +216,9 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
 #pragma unroll
       for (int t = 0; t < S::TI; ++t) {
         const int2 e = st[sub * S::NI + t0 + t];
-        xs[t] = __int_as_float(e.y);
-        const float* src = e.x >= 0 ? vc + (uint32_t)e.x * (uint32_t)S::VS : kZeroRow;
+        const bool live = (t0 + t) * S::SUB + sub < n;  // compacted slots only
+        xs[t] = live ? __int_as_float(e.y) : 0.f;
+        const float* src = live ? vc + (uint32_t)e.x * (uint32_t)S::VS : kZeroRow;
         v[t] = reinterpret_cast<const float4*>(src)[gl];
       }
       if (t0 == 0 && prefetch_first) prefetch();
