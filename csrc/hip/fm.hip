@@ -26,6 +26,7 @@
 #include "wh_lookback.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace wh {
 namespace {
@@ -663,13 +664,13 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     stage_pairs<G>(st, lane, rc, dc);
+    // one gather batch of TB instructions starting at instruction t0
+    auto batch = [&](auto tb, int t0) {
+      constexpr int TB = decltype(tb)::value;
+      float4 a[TB];
+      float du[TB];
 #pragma unroll
-    for (int t0 = 0; t0 < S::NI; t0 += S::TI) {
-      if (t0 * S::SUB >= n) break;
-      float4 a[S::TI];
-      float du[S::TI];
-#pragma unroll
-      for (int t = 0; t < S::TI; ++t) {
+      for (int t = 0; t < TB; ++t) {
         const int2 e = st[sub * S::NI + t0 + t];
         du[t] = __int_as_float(e.y);
         const float* src = e.x >= 0 ? xv + (uint32_t)e.x * (uint32_t)S::VS : kZeroRow;
@@ -683,9 +684,20 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
         m3 = get_meta(c + 3 * nw);
       }
 #pragma unroll
-      for (int t = 0; t < S::TI; ++t) {
+      for (int t = 0; t < TB; ++t) {
         acc.x += du[t] * a[t].x; acc.y += du[t] * a[t].y;
         acc.z += du[t] * a[t].z; acc.w += du[t] * a[t].w;
+      }
+    };
+    // full chunks (hot keys) issue every instruction in one batch for the
+    // most loads in flight; short chunks issue only the live instructions
+    if (n > S::NI * S::SUB / 2) {
+      batch(std::integral_constant<int, S::NI>(), 0);
+    } else {
+#pragma unroll
+      for (int t0 = 0; t0 < S::NI; t0 += S::TI) {
+        if (t0 * S::SUB >= n) break;
+        batch(std::integral_constant<int, S::TI>(), t0);
       }
     }
     if (n == 0) {  // (chunks are never empty; keep the pipeline consistent anyway)

@@ -8,44 +8,80 @@
 // (learn/base/criteo_parser.h:69-70,81-82): (hash64(token) >> 10) | (field << 54).
 // Labels come from a hidden logistic model over (field, rank) so the
 // learners see real signal (logloss falls, AUC rises).
+#include <cstdio>
+#include <cstdlib>
+
 #include "wh_common.h"
 #include "wh_kernels.h"
 
 namespace wh {
 namespace {
 
-__global__ __launch_bounds__(256) void k_synth_criteo(int64_t nrows, uint64_t seed, uint64_t step,
-                                                      const int64_t* card, int nfield,
-                                                      uint64_t* keys, float* label,
-                                                      int64_t* offset) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r > nrows) return;
-  offset[r] = r * nfield;
-  if (r == nrows) return;
-  const uint64_t gid = step * (uint64_t)nrows + (uint64_t)r;
-  float logit = -1.2f;
-  for (int f = 0; f < nfield; ++f) {
+// One thread per (row, field): a block owns kRowsPerBlock whole rows, so the
+// key stores are contiguous across the block and each row's label is summed
+// from LDS (was: one thread per row, 39 serial fields, 312-byte-strided
+// stores).
+constexpr int kSynthThreads = 256;
+constexpr int kMaxField = 64;
+
+__global__ __launch_bounds__(kSynthThreads) void k_synth_criteo(int64_t nrows, uint64_t seed,
+                                                                uint64_t step,
+                                                                const int64_t* card, int nfield,
+                                                                int rows_per_block,
+                                                                uint64_t* keys, float* label,
+                                                                int64_t* offset) {
+  __shared__ float th[kSynthThreads];
+  __shared__ double lc[kMaxField];
+  __shared__ int64_t cd[kMaxField];
+  for (int f = threadIdx.x; f < nfield; f += kSynthThreads) {
+    cd[f] = card[f];
+    lc[f] = log((double)cd[f]);
+  }
+  __syncthreads();
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int lr = threadIdx.x / nfield, f = threadIdx.x % nfield;
+  const int64_t r = r0 + lr;
+  float t = 0.f;
+  if (lr < rows_per_block && r < nrows) {
+    const uint64_t gid = step * (uint64_t)nrows + (uint64_t)r;
     const float u = uhash01(seed, gid, (uint64_t)f);
-    const double c = (double)card[f];
-    int64_t rank = (int64_t)exp(log(c) * (double)u) - 1;
+    int64_t rank = (int64_t)exp(lc[f] * (double)u) - 1;
     if (rank < 0) rank = 0;
-    if (rank >= card[f]) rank = card[f] - 1;
+    if (rank >= cd[f]) rank = cd[f] - 1;
     const uint64_t tok = mix64(((uint64_t)f << 40) ^ (uint64_t)rank ^ 0x5bd1e995ull);
     keys[r * nfield + f] = (tok >> 10) | ((uint64_t)f << 54);
     // hidden weight of this (field, value); head values carry most signal
-    const float th = uhash01(0x7e57ull, (uint64_t)f, (uint64_t)rank) - 0.5f;
-    logit += th * 0.9f;
+    t = (uhash01(0x7e57ull, (uint64_t)f, (uint64_t)rank) - 0.5f) * 0.9f;
   }
-  const float p = 1.f / (1.f + __expf(-logit));
-  label[r] = uhash01(seed ^ 0xabcdefull, gid, 977) < p ? 1.f : 0.f;
+  th[threadIdx.x] = t;
+  __syncthreads();
+  if (threadIdx.x < rows_per_block) {
+    const int64_t rr = r0 + threadIdx.x;
+    if (rr < nrows) {
+      float logit = -1.2f;
+      for (int q = 0; q < nfield; ++q) logit += th[threadIdx.x * nfield + q];
+      const float p = 1.f / (1.f + __expf(-logit));
+      const uint64_t gid = step * (uint64_t)nrows + (uint64_t)rr;
+      label[rr] = uhash01(seed ^ 0xabcdefull, gid, 977) < p ? 1.f : 0.f;
+      offset[rr] = rr * nfield;
+    }
+    if (rr == nrows) offset[rr] = rr * nfield;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) offset[nrows] = nrows * (int64_t)nfield;
 }
 
 }  // namespace
 
 void synth_criteo(int64_t nrows, uint64_t seed, uint64_t step, const int64_t* card, int nfield,
                   uint64_t* keys, float* label, int64_t* offset, hipStream_t s) {
-  hipLaunchKernelGGL(k_synth_criteo, dim3(grid_for(nrows + 1, 256)), dim3(256), 0, s, nrows, seed,
-                     step, card, nfield, keys, label, offset);
+  if (nfield < 1 || nfield > kMaxField) {
+    fprintf(stderr, "synth_criteo: nfield must be in [1, %d]\n", kMaxField);
+    abort();
+  }
+  const int rpb = kSynthThreads / nfield;
+  const int64_t nb = (nrows + rpb - 1) / rpb;
+  hipLaunchKernelGGL(k_synth_criteo, dim3((unsigned)(nb > 0 ? nb : 1)), dim3(kSynthThreads), 0, s,
+                     nrows, seed, step, card, nfield, rpb, keys, label, offset);
 }
 
 }  // namespace wh
