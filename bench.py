@@ -38,7 +38,8 @@ def build(args, comm, device):
         from wormhole_amd.models.difacto import DifactoLearner
         emb = Embedding(dim=args.dim, threshold=100, lambda_l2=1.0, lr_eta=0.01)
         emb._set = {"dim", "threshold", "lambda_l2", "lr_eta"}
-        conf = DifactoConfig(minibatch=args.batch, lr_eta=0.01, embedding=[emb])
+        conf = DifactoConfig(minibatch=args.batch, lr_eta=0.01, embedding=[emb],
+                             fixed_bytes=args.fixed_bytes)
         return DifactoLearner(conf, comm, device, cap=args.cap, vcap=args.vcap, seed=1)
     from wormhole_amd.models.linear import LinearLearner
     conf = LinearConfig(minibatch=args.batch, lambda_l1=4.0, lr_eta=0.1)
@@ -55,6 +56,9 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--cap", type=int, default=1 << 27, help="KV slots per GPU shard")
     ap.add_argument("--vcap", type=int, default=1 << 24, help="embedding rows per shard")
+    ap.add_argument("--fixed-bytes", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="ps-lite FIXING_FLOAT filter on the exchanged embedding rows "
+                         "(lossy; the reference default 0 is used for the headline)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo rehearsal of the distributed path (tiny batches only)")
     args = ap.parse_args()

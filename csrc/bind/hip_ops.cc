@@ -577,6 +577,40 @@ Tensor auc_sorted(const Tensor& py, const Tensor& label) {
   return out.narrow(0, 0, 1);
 }
 
+// ------------------------------------------------------- payload filter
+// x [rows, w] f32 -> uint8 [rows, record_bytes]
+Tensor quant_rows(const Tensor& x, int64_t nb, int64_t seed) {
+  CHECK_IN(x, torch::kFloat32);
+  TORCH_CHECK(nb >= 1 && nb <= 3, "fixed_bytes must be 1, 2 or 3");
+  TORCH_CHECK(x.dim() == 2, "quant_rows: x must be [rows, w]");
+  c10::DeviceGuard g(x.device());
+  const int w = (int)x.size(1);
+  auto out = torch::empty({x.size(0), wh::quant_record_bytes(w, (int)nb)},
+                          x.options().dtype(torch::kUInt8));
+  wh::quant_rows(ptr<float>(x), x.size(0), w, (int)nb, (uint64_t)seed, ptr<uint8_t>(out),
+                 cur_stream(x));
+  return out;
+}
+
+Tensor dequant_rows(const Tensor& q, int64_t w, int64_t nb) {
+  CHECK_IN(q, torch::kUInt8);
+  TORCH_CHECK(nb >= 1 && nb <= 3, "fixed_bytes must be 1, 2 or 3");
+  TORCH_CHECK(q.dim() == 2 && q.size(1) == wh::quant_record_bytes((int)w, (int)nb),
+              "dequant_rows: bad record size");
+  c10::DeviceGuard g(q.device());
+  auto x = torch::empty({q.size(0), w}, q.options().dtype(torch::kFloat32));
+  wh::dequant_rows(ptr<uint8_t>(q), q.size(0), (int)w, (int)nb, ptr<float>(x), cur_stream(q));
+  return x;
+}
+
+Tensor trunc_u8(const Tensor& c) {
+  CHECK_IN(c, torch::kInt32);
+  c10::DeviceGuard g(c.device());
+  auto out = torch::empty({c.numel()}, c.options().dtype(torch::kUInt8));
+  wh::trunc_u8(ptr<int32_t>(c), c.numel(), ptr<uint8_t>(out), cur_stream(c));
+  return out;
+}
+
 // ---------------------------------------------------------------- synth
 std::vector<Tensor> synth_criteo(int64_t nrows, int64_t seed, int64_t step, const Tensor& card) {
   CHECK_IN(card, torch::kInt64);
@@ -796,6 +830,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fm_grad_post", &fm_grad_post);
   m.def("vidx_renumber", &vidx_renumber);
   m.def("auc", &auc);
+  m.def("quant_rows", &quant_rows);
+  m.def("dequant_rows", &dequant_rows);
+  m.def("trunc_u8", &trunc_u8);
   m.def("auc_acc", &auc_acc);
   m.def("auc_sorted", &auc_sorted);
   m.def("synth_criteo", &synth_criteo);

@@ -262,6 +262,16 @@ void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const f
                   const int32_t* left, const int32_t* right, const uint8_t* defl,
                   const float* leaf, float* margin, hipStream_t s);
 
+// -------------------------------------------------------------- quant.hip
+// fixed_bytes payload filter: rows of w floats <-> packed records of
+// quant_record_bytes(w, nb) bytes {float scale, w signed nb-byte ints},
+// unbiased stochastic rounding (nb = 1, 2 or 3)
+int64_t quant_record_bytes(int w, int nb);
+void quant_rows(const float* x, int64_t rows, int w, int nb, uint64_t seed, uint8_t* out,
+                hipStream_t s);
+void dequant_rows(const uint8_t* in, int64_t rows, int w, int nb, float* x, hipStream_t s);
+void trunc_u8(const int32_t* c, int64_t n, uint8_t* out, hipStream_t s);
+
 // -------------------------------------------------------------- exchange
 // gather rows: out[i, :] = in[idx[i], :]   (row width in floats)
 void gather_rows(const float* in, const int32_t* idx, int64_t n, int width, float* out,

@@ -54,13 +54,38 @@ class Session:
 
 
 class ShardedKV:
-    def __init__(self, store, comm, nshard=None):
+    def __init__(self, store, comm, nshard=None, fixed_bytes=0, seed=0):
         self.store = store
         self.comm = comm
+        # ps-lite FIXING_FLOAT / TRUNCATE_FLOAT filters (conf fixed_bytes,
+        # learn/difacto/async_sgd.h:429-446): embedding rows cross the wire as
+        # n-byte fixed point with random rounding, feature counts as uint8.
+        # Scalars (w, gw, the header) travel exact. Only applied to data that
+        # actually moves between ranks.
+        self.fixed_bytes = int(fixed_bytes or 0)
+        if self.fixed_bytes not in (0, 1, 2, 3):
+            raise ValueError("fixed_bytes must be 0, 1, 2 or 3")
+        self.qseed = (int(seed) * 0x9E3779B1 + 17 * comm.rank + 1) & 0x7FFFFFFFFFFF
+        self.qcalls = 0
         # keys are owned by the first `nshard` ranks (the conf's -s S servers)
         self.nshard = comm.size if nshard is None else max(1, min(int(nshard), comm.size))
         self.push_count = 0  # number of push requests applied (SGD's t)
         self.pending = None  # a deferred push: (handle, apply)
+
+    # ------------------------------------------------------ payload filter
+    def _rows_out(self, x):
+        """rows about to be sent: quantised records when fixed_bytes > 0"""
+        if not self.fixed_bytes or x.numel() == 0:
+            return x
+        self.qcalls += 1
+        return ops.quant_rows(x, self.fixed_bytes, self.qseed + (self.qcalls << 20))
+
+    def _rows_in(self, q, width):
+        if not self.fixed_bytes:
+            return q
+        if q.numel() == 0:
+            return torch.zeros((q.shape[0], width), dtype=torch.float32, device=q.device)
+        return ops.dequant_rows(q, width, self.fixed_bytes)
 
     def flush(self):
         """Complete a deferred push (wait for its transfers, apply it)."""
@@ -101,9 +126,10 @@ class ShardedKV:
                 keys = self.comm.all_to_all_v(uniq, send, recv)
                 sess = Session(send, recv, keys)
             else:
-                keys, c = self.comm.all_to_all_v_multi([(uniq, send, recv), (cnt, send, recv)])
+                cw = ops.trunc_u8(cnt) if self.fixed_bytes else cnt
+                keys, c = self.comm.all_to_all_v_multi([(uniq, send, recv), (cw, send, recv)])
                 sess = Session(send, recv, keys)
-                sess.cnt = c
+                sess.cnt = c.int() if self.fixed_bytes else c
         self.flush()  # a deferred push lands before this minibatch's lookups
         sess.slots = self.store.find(sess.keys, insert)
         return sess
@@ -193,7 +219,8 @@ class ShardedKV:
         sess.vrecv, sess.vsend = both[:P], both[P:]
         hdr_w, vc_w = self.comm.all_to_all_v_multi([
             (hdr, sess.recv, sess.send),
-            (vc[:sum(sess.vrecv)], sess.vrecv, sess.vsend)])
+            (self._rows_out(vc[:sum(sess.vrecv)]), sess.vrecv, sess.vsend)])
+        vc_w = self._rows_in(vc_w, vc.shape[1])
         sess.m = ops.vidx_renumber(hdr_w)
         return hdr_w, vc_w
 
@@ -213,9 +240,10 @@ class ShardedKV:
         if self.comm.size == 1:
             apply(gw, gvc)
             return
+        width = gvc.shape[1] if gvc.dim() == 2 else 0
         (g, gv), handle = self.comm.all_to_all_v_multi([
             (gw, sess.send, sess.recv),
-            (gvc[:sum(sess.vsend)], sess.vsend, sess.vrecv)], async_op=True)
-        self.pending = (handle, lambda: apply(g, gv))
+            (self._rows_out(gvc[:sum(sess.vsend)]), sess.vsend, sess.vrecv)], async_op=True)
+        self.pending = (handle, lambda: apply(g, self._rows_in(gv, width).contiguous()))
         if not defer:
             self.flush()

@@ -29,7 +29,8 @@ class DifactoLearner:
         self.emb = emb
         self.vstride = ops.vstride_for(self.dim)
         self.store = make_store(cap, vcap, self.dim, self.device)
-        self.kv = ShardedKV(self.store, comm, nshard)
+        self.kv = ShardedKV(self.store, comm, nshard, fixed_bytes=getattr(conf, "fixed_bytes", 0),
+                            seed=seed)
         self.seed = seed
         self.l1_shrk = bool(conf.l1_shrk)
         if emb is not None:

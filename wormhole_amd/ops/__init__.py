@@ -133,3 +133,23 @@ def auc_acc(py, label, auc_sum):
         return auc_sum
     auc_sum += ref.auc(py, label)
     return auc_sum
+
+
+def quant_rows(x, nb, seed):
+    """fixed_bytes payload filter: [rows, w] float32 -> uint8 records."""
+    if _gpu(x):
+        return _native.hip().quant_rows(x.contiguous(), int(nb), int(seed))
+    return ref.quant_rows(x, nb, seed)
+
+
+def dequant_rows(q, w, nb):
+    if _gpu(q):
+        return _native.hip().dequant_rows(q.contiguous(), int(w), int(nb))
+    return ref.dequant_rows(q, w, nb)
+
+
+def trunc_u8(c):
+    """feature counts -> uint8, saturating (the count push's TRUNCATE filter)."""
+    if _gpu(c) and c.dtype == torch.int32:
+        return _native.hip().trunc_u8(c.contiguous())
+    return ref.trunc_u8(c)

@@ -186,3 +186,53 @@ def vstride_for(dim):
 
 def sigmoid(x):
     return 1.0 / (1.0 + math.exp(-x))
+
+
+# ----------------------------------------------------------- payload filter
+def quant_record_bytes(w, nb):
+    return (4 + w * nb + 3) // 4 * 4
+
+
+def _qmax(nb):
+    return float((1 << (8 * nb - 1)) - 1)
+
+
+def quant_rows(x, nb, seed):
+    """fixed_bytes filter (csrc/hip/quant.hip): rows of w floats -> uint8
+    records {float scale, w signed nb-byte ints}, unbiased random rounding."""
+    import numpy as np
+    from ..kv.cpu_store import uhash01
+    xn = x.detach().cpu().numpy().astype(np.float32)
+    rows, w = xn.shape
+    lim = _qmax(nb)
+    m = np.abs(xn).max(axis=1) if w else np.zeros(rows, np.float32)
+    scale = np.where(m > 0, m / np.float32(lim), np.float32(1.0)).astype(np.float32)
+    inv = (np.float32(1.0) / scale).astype(np.float32)
+    r = np.arange(rows, dtype=np.uint64)[:, None]
+    c = np.arange(w, dtype=np.uint64)[None, :]
+    u = uhash01(seed, r, c)
+    q = np.clip(np.floor(xn * inv[:, None] + u), -lim, lim).astype(np.int64)
+    rec = quant_record_bytes(w, nb)
+    out = np.zeros((rows, rec), dtype=np.uint8)
+    out[:, :4] = scale.view(np.uint8).reshape(rows, 4)
+    uq = (q & ((1 << (8 * nb)) - 1)).astype(np.uint64)
+    for b in range(nb):
+        out[:, 4 + b:4 + w * nb:nb] = ((uq >> np.uint64(8 * b)) & np.uint64(0xff)).astype(np.uint8)
+    return torch.from_numpy(out)
+
+
+def dequant_rows(q, w, nb):
+    import numpy as np
+    qn = q.cpu().numpy()
+    rows = qn.shape[0]
+    scale = qn[:, :4].copy().view(np.float32).reshape(rows)
+    u = np.zeros((rows, w), dtype=np.int64)
+    for b in range(nb):
+        u |= qn[:, 4 + b:4 + w * nb:nb].astype(np.int64) << (8 * b)
+    sign = 1 << (8 * nb - 1)
+    v = (u ^ sign) - sign
+    return torch.from_numpy((v.astype(np.float32) * scale[:, None]).astype(np.float32))
+
+
+def trunc_u8(c):
+    return c.clamp(0, 255).to(torch.uint8)
