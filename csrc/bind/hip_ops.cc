@@ -577,6 +577,17 @@ Tensor auc_sorted(const Tensor& py, const Tensor& label) {
   return out.narrow(0, 0, 1);
 }
 
+// keys % m (uint64 semantics), returned as a new tensor
+Tensor key_mod(const Tensor& keys, int64_t m) {
+  CHECK_IN(keys, torch::kInt64);
+  TORCH_CHECK(m > 0, "max_key must be positive");
+  c10::DeviceGuard g(keys.device());
+  auto out = keys.clone();
+  wh::key_mod(reinterpret_cast<uint64_t*>(out.data_ptr()), out.numel(), (uint64_t)m,
+              cur_stream(keys));
+  return out;
+}
+
 // ------------------------------------------------------- payload filter
 // x [rows, w] f32 -> uint8 [rows, record_bytes]
 Tensor quant_rows(const Tensor& x, int64_t nb, int64_t seed) {
@@ -831,6 +842,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("vidx_renumber", &vidx_renumber);
   m.def("auc", &auc);
   m.def("quant_rows", &quant_rows);
+  m.def("key_mod", &key_mod);
   m.def("dequant_rows", &dequant_rows);
   m.def("trunc_u8", &trunc_u8);
   m.def("auc_acc", &auc_acc);

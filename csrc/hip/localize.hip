@@ -292,6 +292,11 @@ __global__ __launch_bounds__(kThreads) void k_ucnt(const int64_t* __restrict__ c
   if (k < nuniq) ucnt[k] = (int32_t)(csc_off[k + 1] - csc_off[k]);
 }
 
+__global__ __launch_bounds__(kThreads) void k_key_mod(uint64_t* keys, int64_t n, uint64_t m) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < n) keys[i] %= m;
+}
+
 inline int bits_for(int64_t n) {
   int b = 1;
   while (b < 31 && ((int64_t)1 << b) < n) ++b;
@@ -364,6 +369,15 @@ void loc_csc(const int32_t* row_of, const float* val, int64_t nnz, int64_t nuniq
                      val ? spos : nullptr, row_of, val, nnz, nuniq, csc_row, csc_val, csc_off);
   hipLaunchKernelGGL(k_ucnt, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s, csc_off,
                      nuniq, ucnt);
+}
+
+}  // namespace wh
+
+namespace wh {
+
+void key_mod(uint64_t* keys, int64_t n, uint64_t m, hipStream_t s) {
+  if (n <= 0 || m == 0) return;
+  hipLaunchKernelGGL(k_key_mod, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, keys, n, m);
 }
 
 }  // namespace wh

@@ -41,6 +41,9 @@ Lookback lookback_bind(void* ws);
 // tsize >= 2*nnz (which cannot overflow). tkeys[tsize] (init ~0) is scratch.
 void loc_insert(const uint64_t* keys, int64_t nnz, uint64_t* tkeys, int64_t tsize,
                 int32_t* slot_of, int64_t* overflow, hipStream_t s);
+// keys[i] %= m (uint64): the ps-lite max_key key-space folding applied by
+// the reference Localizer (learn/base/localizer.h:108-115)
+void key_mod(uint64_t* keys, int64_t n, uint64_t m, hipStream_t s);
 // per-owner counts of the occupied slots (owner = mix64b(key) % nshard):
 // blkcnt [nshard * loc_owner_blocks(tsize)] becomes the owner-major exclusive
 // scan of the per-block counts (= blkoff for loc_assign); owner_cnt[0..nshard)

@@ -48,14 +48,44 @@ def _make(kind, conf):
     return schema.DifactoConfig, DifactoProgress, stop_fn
 
 
-def _learner(kind, conf, comm, device, nshard):
+def _learner(kind, conf, comm, device, nshard, max_key=0):
     cap = int(os.environ.get("WH_KV_CAP", 1 << (24 if device.type == "cuda" else 16)))
     vcap = int(os.environ.get("WH_KV_VCAP", 1 << (20 if device.type == "cuda" else 14)))
     if kind == "linear":
         from ..models.linear import LinearLearner
-        return LinearLearner(conf, comm, device, cap=cap, nshard=nshard)
-    from ..models.difacto import DifactoLearner
-    return DifactoLearner(conf, comm, device, cap=cap, vcap=vcap, nshard=nshard)
+        lr = LinearLearner(conf, comm, device, cap=cap, nshard=nshard)
+    else:
+        from ..models.difacto import DifactoLearner
+        lr = DifactoLearner(conf, comm, device, cap=cap, vcap=vcap, nshard=nshard)
+    lr.max_key = int(max_key)
+    return lr
+
+
+def split_system_flags(argv):
+    """Separate ps-lite system flags (gflags style ``-name=value`` /
+    ``--name=value`` / ``-name value``) from the conf file and its
+    ``key=value`` overrides. Known: ``max_key`` (fold feature ids into
+    [0, max_key), reference learn/base/localizer.h:108-115)."""
+    flags, rest = {}, []
+    i = 0
+    while i < len(argv):
+        a = argv[i]
+        if a.startswith("-") and len(a) > 1 and not a[1:2].isdigit():
+            name = a.lstrip("-")
+            if "=" in name:
+                name, val = name.split("=", 1)
+            elif i + 1 < len(argv):
+                i += 1
+                val = argv[i]
+            else:
+                raise SystemExit("flag %s needs a value" % a)
+            if name != "max_key":
+                raise SystemExit("unknown system flag -%s" % name)
+            flags[name] = int(val)
+        else:
+            rest.append(a)
+        i += 1
+    return flags, rest
 
 
 def main(kind, argv):
@@ -63,6 +93,7 @@ def main(kind, argv):
     from ..parallel.comm import Comm
     from ..solver.ps import Scheduler, Worker
 
+    sysflags, argv = split_system_flags(list(argv))
     if len(argv) < 1:
         print("usage: %s.dmlc <conf|none> [key=value ...]" % kind, file=sys.stderr)
         return 1
@@ -96,7 +127,8 @@ def main(kind, argv):
         comm = Comm(dev)
         van = host.Van()
         van.connect("127.0.0.1", port, "worker-0")
-        Worker(conf, kind, _learner(kind, conf, comm, dev, 1), comm, van, 1, kind).serve()
+        Worker(conf, kind, _learner(kind, conf, comm, dev, 1, sysflags.get("max_key", 0)), comm,
+               van, 1, kind).serve()
         th.join()
         van.close()
         van_s.close()
@@ -119,7 +151,8 @@ def main(kind, argv):
     van = host.Van()
     van.connect(uri, port, "worker-%d" % comm.rank)
     try:
-        Worker(conf, kind, _learner(kind, conf, comm, dev, nshard), comm, van, nshard, kind).serve()
+        Worker(conf, kind, _learner(kind, conf, comm, dev, nshard, sysflags.get("max_key", 0)),
+               comm, van, nshard, kind).serve()
     finally:
         van.close()
         comm.finalize()

@@ -27,6 +27,7 @@ class LinearLearner:
         self.met = torch.zeros(4, dtype=torch.float64, device=self.device)
         self.auc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.n_mb = 0
+        self.max_key = 0  # set from the -max_key system flag (apps/ps_app.py)
         self.uhint = 0  # unique ids of the previous minibatch (localize table size)
         # overlap each push's all-to-all with the next minibatch's localize
         # (same semantics: the push is applied before the next lookup)
@@ -34,6 +35,8 @@ class LinearLearner:
 
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0):
         train = wtype == TRAIN
+        if self.max_key:  # ps-lite -max_key: fold the key space (reference Localizer)
+            keys = ops.key_mod(keys, self.max_key)
         ex = self.kv.count_exchange()
         loc = ops.localize(keys, offset, val, self.kv.nshard, self.uhint, exchange=ex)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]

@@ -153,3 +153,14 @@ def trunc_u8(c):
     if _gpu(c) and c.dtype == torch.int32:
         return _native.hip().trunc_u8(c.contiguous())
     return ref.trunc_u8(c)
+
+
+def key_mod(keys, max_key):
+    """Fold 64-bit feature ids into [0, max_key) (uint64 modulo): the ps-lite
+    ``max_key`` flag as applied by the reference Localizer
+    (learn/base/localizer.h:108-115)."""
+    if _gpu(keys):
+        return _native.hip().key_mod(keys.contiguous(), int(max_key))
+    import numpy as np
+    k = keys.contiguous().numpy().view(np.uint64) % np.uint64(max_key)
+    return torch.from_numpy(k.view(np.int64).copy())
