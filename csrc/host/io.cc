@@ -13,16 +13,40 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <cctype>
+#include <cstdlib>
 #include <cstring>
 
 namespace wh {
 namespace host {
 
-namespace {
-std::string strip_scheme(const std::string& p) {
-  if (p.rfind("file://", 0) == 0) return p.substr(7);
-  return p;
+// Local paths / file:// directly; any other scheme through the local mount
+// named by WH_FS_MOUNT_<SCHEME> (hdfs/viewfs drop the name-node authority,
+// object stores keep their bucket). Mirrors wormhole_amd/utils/fs.py.
+std::string ResolvePath(const std::string& p) {
+  const size_t sep = p.find("://");
+  if (sep == std::string::npos) return p;
+  std::string scheme = p.substr(0, sep);
+  std::string rest = p.substr(sep + 3);
+  for (auto& c : scheme) c = (char)std::tolower((unsigned char)c);
+  if (scheme == "file") return rest;
+  std::string var = "WH_FS_MOUNT_";
+  for (char c : scheme) var += (char)std::toupper((unsigned char)c);
+  const char* root = std::getenv(var.c_str());
+  if (!root || !*root)
+    throw std::runtime_error("no filesystem for '" + scheme + "://' (" + p + "): set " + var +
+                             " to a local mount of it");
+  if (scheme == "hdfs" || scheme == "viewfs") {
+    const size_t slash = rest.find('/');
+    rest = slash == std::string::npos ? "" : rest.substr(slash + 1);
+  }
+  std::string out = root;
+  if (!out.empty() && out.back() != '/') out += "/";
+  return out + rest;
 }
+
+namespace {
+std::string strip_scheme(const std::string& p) { return ResolvePath(p); }
 }  // namespace
 
 std::vector<std::string> ListDirectory(const std::string& dir_in) {
@@ -201,7 +225,8 @@ bool InputSplit::NextRecord(std::string* out) {
 }
 
 // --------------------------------------------------------------- recordio
-RecordIOWriter::RecordIOWriter(const std::string& path) {
+RecordIOWriter::RecordIOWriter(const std::string& path_in) {
+  const std::string path = ResolvePath(path_in);
   fp_ = std::fopen(path.c_str(), "wb");
   if (!fp_) throw std::runtime_error("cannot open " + path + " for writing");
 }

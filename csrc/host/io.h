@@ -10,6 +10,9 @@ namespace host {
 
 constexpr uint32_t kRecordIOMagic = 0xced7230a;
 
+// URI -> local path (file://, plain paths; other schemes through the mount
+// named by WH_FS_MOUNT_<SCHEME>; throws when none is configured)
+std::string ResolvePath(const std::string& uri);
 std::vector<std::string> ListDirectory(const std::string& dir);
 std::vector<std::string> MatchFile(const std::string& pattern);
 int64_t FileSize(const std::string& path);

@@ -172,6 +172,7 @@ void register_all(py::module& m) {
     return py::bytes(out);
   });
   m.def("match_file", &MatchFile);
+  m.def("resolve_path", &ResolvePath);
   m.def("list_directory", &ListDirectory);
   m.def("file_size", &FileSize);
   m.def("load_split", &load_split, py::arg("path"), py::arg("part") = 0, py::arg("nparts") = 1,

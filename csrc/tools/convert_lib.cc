@@ -112,7 +112,7 @@ ConvertStats Convert(const std::string& in, const std::string& out, const std::s
       if (fmt_out == "crb") {
         crb.reset(new RecordIOWriter(name));
       } else {
-        fp = std::fopen(name.c_str(), "wb");
+        fp = std::fopen(ResolvePath(name).c_str(), "wb");
         WH_CHECK(fp != nullptr, "cannot open " + name);
       }
       nwrite = 0;

@@ -12,6 +12,7 @@ import sys
 import torch
 
 from .ps_app import _device
+from ..utils.fs import open_uri  # noqa: E402
 
 
 def main(kind, argv):
@@ -56,7 +57,7 @@ def main(kind, argv):
         pred = obj.predict(w).float().cpu()
         parts = bsp.comm.allgather_object(pred.tolist())
         if bsp.rank == 0:
-            with open(name_pred, "w") as f:
+            with open_uri(name_pred, "w") as f:
                 for part in parts:
                     f.write("".join("%g\n" % p for p in part))
             print("Finishing writing to %s" % name_pred, flush=True)

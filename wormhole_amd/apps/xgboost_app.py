@@ -15,6 +15,7 @@ import sys
 import torch
 
 from .ps_app import _device
+from ..utils.fs import open_uri  # noqa: E402
 
 
 def _strip(v):
@@ -28,7 +29,7 @@ def parse_args(argv):
     from .. import _native
     items = []
     if argv and argv[0] != "none" and "=" not in argv[0]:
-        for key, kind, val in _native.host().parse_conf(open(argv[0]).read()):
+        for key, kind, val in _native.host().parse_conf(open_uri(argv[0]).read()):
             if kind == "m":
                 raise ValueError("nested messages are not valid in an xgboost conf")
             items.append((key, val))
@@ -112,7 +113,7 @@ def main(argv):
         if bsp.rank == 0:
             b = G.Booster.load(model_in, param)
             fm = G.load_fmap(fmap) if fmap else None
-            with open(name_dump, "w") as f:
+            with open_uri(name_dump, "w") as f:
                 f.write(b.dump(fm, bool(dump_stats)))
         bsp.finalize()
         return 0
@@ -131,7 +132,7 @@ def main(argv):
         else:
             parts = bsp.comm.allgather_object(pred.float().cpu().tolist())
             if bsp.rank == 0:
-                with open(name_pred, "w") as f:
+                with open_uri(name_pred, "w") as f:
                     for part in parts:
                         f.write("".join("%g\n" % p for p in part))
         bsp.finalize()

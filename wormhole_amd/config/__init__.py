@@ -9,6 +9,7 @@ import dataclasses
 
 from .. import _native
 from .schema import DifactoConfig, Embedding, LinearConfig  # noqa: F401
+from ..utils.fs import open_uri  # noqa: E402
 
 _BOOL = {"true": True, "false": False, "1": True, "0": False, "True": True, "False": False}
 
@@ -73,7 +74,7 @@ def arg2proto(text):
 def load_dmlc(cls, conf_path):
     """Load a dmlc::Config-style conf (``key = value`` lines, repeated keys
     allowed) into a schema object through :func:`arg2proto`."""
-    with open(conf_path) as f:
+    with open_uri(conf_path) as f:
         return parse_text(cls, arg2proto(f.read()))
 
 
@@ -81,7 +82,7 @@ def load(cls, conf_path, argv=()):
     """Reference ArgParser: ReadFile(conf) then ReadArgs(argv) (later wins)."""
     obj = cls()
     if conf_path and conf_path != "none":
-        with open(conf_path) as f:
+        with open_uri(conf_path) as f:
             parse_text(cls, f.read(), obj)
     if argv:
         parse_text(cls, "\n".join(argv), obj)

@@ -16,6 +16,7 @@ import struct
 
 import numpy as np
 import torch
+from ..utils.fs import open_uri  # noqa: E402
 
 
 def model_name(base, it, shard):
@@ -42,7 +43,7 @@ def save_linear(store, path):
     rec = np.empty(int(m.sum()), dtype=[("k", "<u8"), ("w", "<f4")])
     rec["k"] = keys[m]
     rec["w"] = w[m]
-    with open(path, "wb") as f:
+    with open_uri(path, "wb") as f:
         f.write(rec.tobytes())
     return len(rec)
 
@@ -89,7 +90,7 @@ def save_difacto(store, path):
         rv["sq"], rv["z"] = sq[has_v], z[has_v]
         rv["V"] = store.V[rows.to(store.V.device)].cpu().numpy()[:, :dim]
         rv["VG"] = store.VG[rows.to(store.VG.device)].cpu().numpy()[:, :dim]
-    with open(path, "wb") as f:
+    with open_uri(path, "wb") as f:
         f.write(r1.tobytes())
         f.write(rv.tobytes())
     return len(r1) + len(rv)
@@ -146,7 +147,7 @@ def _parse_difacto(data, dim):
 
 
 def load_difacto(store, path):
-    data = open(path, "rb").read()
+    data = open_uri(path, "rb").read()
     dim = int(store.dim)
     keys, w, z, sq, vk, V, VG = _parse_difacto(data, dim)
     if len(vk) and V.shape[1] != dim:

@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from .. import _native
+from ..utils.fs import open_uri  # noqa: E402
 
 RT_EPS = 1e-6
 MISSING_BIN = 255
@@ -372,7 +373,7 @@ def _fmt(x):
 
 def load_fmap(path):
     names = []
-    for line in open(path):
+    for line in open_uri(path):
         parts = line.rstrip("\n").split("\t")
         if len(parts) < 3:
             continue
@@ -754,7 +755,7 @@ class Booster:
 
     def save(self, path):
         p = self.param
-        with open(path, "wb") as f:
+        with open_uri(path, "wb") as f:
             f.write(self.MAGIC)
             hdr = ("%s|%g|%d|%d" % (p.objective, p.base_score, self.num_feature,
                                      len(self.trees))).encode()
@@ -771,7 +772,7 @@ class Booster:
 
     @staticmethod
     def load(path, param):
-        with open(path, "rb") as f:
+        with open_uri(path, "rb") as f:
             if f.read(4) != Booster.MAGIC:
                 raise ValueError("invalid model file " + path)
             (ln,) = struct.unpack("<I", f.read(4))

@@ -13,6 +13,7 @@ exit(-1).
 import torch
 
 from .. import _native
+from ..utils.fs import open_uri  # noqa: E402
 
 
 def densify(keys, offset, val, nrows, ncol, device):
@@ -99,6 +100,6 @@ class KMeans:
         return float(tot[0] / tot[1])
 
     def save_text(self, path):
-        with open(path, "w") as f:
+        with open_uri(path, "w") as f:
             for row in self.C.cpu().tolist():
                 f.write(" ".join("%g" % v for v in row) + "\n")

@@ -22,6 +22,7 @@ import struct
 import torch
 
 from .. import ops
+from ..utils.fs import open_uri  # noqa: E402
 
 _PARAM_FMT = "<f4xQi16i4x"  # 88 bytes, matches the padded C++ struct
 
@@ -175,13 +176,13 @@ class LinearObjective:
 
     # ------------------------------------------------------------- I/O
     def save_model(self, path, w):
-        with open(path, "wb") as f:
+        with open_uri(path, "wb") as f:
             f.write(b"binf")
             f.write(self.param.pack())
             f.write(w.detach().float().cpu().numpy().tobytes())
 
     def load_model(self, path):
-        with open(path, "rb") as f:
+        with open_uri(path, "rb") as f:
             if f.read(4) != b"binf":
                 raise ValueError("invalid model file")
             self.param.unpack(f.read(struct.calcsize(_PARAM_FMT)))

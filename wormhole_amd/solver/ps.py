@@ -30,6 +30,7 @@ import torch
 from .. import _native
 from ..kv import checkpoint
 from ..models.progress import merge
+from ..utils.fs import open_uri  # noqa: E402
 
 TRAIN, VAL, PRED = 0, 1, 2
 _TYPE_NAME = {TRAIN: "training", VAL: "validation", PRED: "prediction"}
@@ -396,7 +397,7 @@ class Worker:
                     if name != pred_name:
                         if pred_f:
                             pred_f.close()
-                        pred_f = open(name, "w")
+                        pred_f = open_uri(name, "w")
                         pred_name = name
             if it is not None:
                 batch = it.next()
