@@ -117,3 +117,17 @@ def test_split_search_matches_brute_force():
                     best = (float(gain), (j, b))
     assert tree.feat[0] == best[1][0]
     assert abs(tree.gain[0] - best[0]) < 1e-6 * max(1.0, abs(best[0]))
+
+
+def test_external_memory_cache_suffix(work):
+    """xgboost's "data#name.cache" syntax: the first run writes a binary CRB
+    page per rank, the second run loads it and trains the same model."""
+    args = ["-n", "2", XGB, "learn/xgboost/mushroom.conf",
+            "data=learn/data/agaricus.txt.train#dtrain.cache"]
+    r = run(args + ["model_out=a.model"], work)
+    assert r.returncode == 0, r.stderr[-2000:]
+    pages = sorted(p.name for p in work.iterdir() if p.name.startswith("dtrain.cache"))
+    assert pages == ["dtrain.cache.r0of2.crb", "dtrain.cache.r1of2.crb"]
+    r2 = run(args + ["model_out=b.model"], work)
+    assert r2.returncode == 0, r2.stderr[-2000:]
+    assert open(work / "a.model", "rb").read() == open(work / "b.model", "rb").read()

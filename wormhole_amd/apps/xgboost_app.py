@@ -106,8 +106,33 @@ def main(argv):
     host = _native.host()
 
     def load(path):
-        keys, off, val, lab, wt = host.load_split(path, bsp.rank, bsp.world, "libsvm")
-        return keys, off, val, lab, wt
+        # xgboost external-memory syntax "data#name.cache": the first run parses
+        # the text split and writes this rank's rows as a binary CRB page
+        # (RecordIO + LZ4, the reference's compressed row block) next to the
+        # cache name; later runs load the page instead of re-parsing. The
+        # matrix itself is then binned into HBM (288 GB per GPU holds any
+        # split this tool is pointed at).
+        cache = None
+        if "#" in path:
+            path, cache = path.split("#", 1)
+        if cache:
+            cpath = "%s.r%dof%d.crb" % (cache, bsp.rank, bsp.world)
+            if host.file_size(cpath) > 0:
+                return host.load_split(cpath, 0, 1, "crb")
+        blk = host.load_split(path, bsp.rank, bsp.world, "libsvm")
+        if cache:
+            keys, off, val, lab, wt = blk
+            w = host.RecordIOWriter(cpath)
+            n = lab.numel()
+            for r0 in range(0, max(n, 1), 1 << 18):  # records stay far below 2^29 bytes
+                r1 = min(n, r0 + (1 << 18))
+                a, b = int(off[r0]), int(off[r1])
+                w.write(host.crb_encode(keys[a:b].contiguous(), (off[r0:r1 + 1] - a).contiguous(),
+                                        val[a:b].contiguous() if val is not None and val.numel() else None,
+                                        lab[r0:r1].contiguous(),
+                                        wt[r0:r1].contiguous() if wt is not None and wt.numel() else None))
+            w.close()
+        return blk
 
     if task == "dump":
         if bsp.rank == 0:
