@@ -29,6 +29,13 @@ inline hipStream_t cur_stream(const Tensor& t) {
 template <typename T>
 T* ptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
 
+#define WH_HIP_CHECK_HOST(expr)                                                   \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    TORCH_CHECK(_e == hipSuccess, "HIP error ", hipGetErrorString(_e), " at ",  \
+                __FILE__, ":", __LINE__);                                       \
+  } while (0)
+
 template <typename T>
 const T* optptr(const c10::optional<Tensor>& t) {
   return (t.has_value() && t->defined() && t->numel() > 0) ? reinterpret_cast<const T*>(t->data_ptr())
@@ -48,9 +55,14 @@ struct DevWs {
   Tensor lb;          // look-back scan granules + ticket (wh_lookback.h)
   Tensor auc;         // AUC bucket counters / min-max / area / ticket
   Tensor fwd_ticket;  // arrival counter of the forward's last-block reduction
-  Tensor loc_tab;     // localize hash table (all ~0 between minibatches)
-  Tensor loc_ovf;     // localize overflow counter (0 between minibatches)
-  bool loc_dirty = false;
+  // localize hash tables (all ~0 between minibatches) and overflow counters
+  // (0 between minibatches), double-buffered so that minibatch i+1's insert
+  // can be enqueued before minibatch i's assign has emptied its table
+  Tensor loc_tab[2];
+  Tensor loc_ovf[2];
+  bool loc_dirty[2] = {false, false};
+  bool loc_busy[2] = {false, false};
+  int loc_next = 0;
 };
 
 DevWs& dev_ws(const torch::Device& d) {
@@ -64,8 +76,10 @@ DevWs& dev_ws(const torch::Device& d) {
     w->auc = torch::zeros({wh::auc_ws_persistent_bytes() / 8}, o.dtype(torch::kInt64));
     w->auc.select(0, wh::auc_ws_lohi_offset() / 8).fill_(-1);
     w->fwd_ticket = torch::zeros({4}, o.dtype(torch::kInt32));
-    w->loc_tab = torch::full({1024}, -1, o.dtype(torch::kInt64));
-    w->loc_ovf = torch::zeros({1}, o.dtype(torch::kInt64));
+    for (int b = 0; b < 2; ++b) {
+      w->loc_tab[b] = torch::full({1024}, -1, o.dtype(torch::kInt64));
+      w->loc_ovf[b] = torch::zeros({1}, o.dtype(torch::kInt64));
+    }
     ws[i] = w;
   }
   return *ws[i];
@@ -101,103 +115,176 @@ Tensor scan_excl(const Tensor& in) {
 // It runs before the one host read, so the read returns both this rank's
 // counts and its peers' (one synchronisation per minibatch instead of two).
 // Every rank sees every rank's overflow flag, so all ranks retry together.
+//
+// Two phases, so that a caller can hide the host read: begin() enqueues the
+// hash insert, the owner counts, the count exchange and an ASYNC copy of the
+// counts into pinned host memory (+ an event); finish() waits for that event
+// only, sizes the outputs and enqueues the rest. A learner begins minibatch
+// i+1 right after finishing minibatch i, so the wait overlaps i's training.
+class LocalizeJob {
+ public:
+  LocalizeJob(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+              int64_t nshard, int64_t hint, py::object exchange)
+      : keys_(keys), offset_(offset), nshard_(nshard), exchange_(exchange) {
+    CHECK_IN(keys, torch::kInt64);
+    CHECK_IN(offset, torch::kInt64);
+    TORCH_CHECK(nshard >= 1 && nshard <= 1024, "nshard out of range");
+    nnz_ = keys.numel();
+    TORCH_CHECK(nnz_ < (int64_t)INT32_MAX, "minibatch too large for int32 local ids");
+    if (val.has_value() && val->defined() && val->numel() > 0) {
+      CHECK_IN((*val), torch::kFloat32);
+      TORCH_CHECK(val->numel() == nnz_);
+      val_ = *val;
+    }
+    // Table size: >= 2*nnz can never overflow; with a hint (the previous
+    // minibatch's unique count) use ~2.5x the hint instead, which keeps the
+    // scratch table small enough to stay cache resident, and fall back to the
+    // safe size if this minibatch overflowed it.
+    safe_ = next_pow2(std::max<int64_t>(2 * nnz_, 1024));
+    tsize_ = hint > 0 ? std::min(safe_, next_pow2(std::max<int64_t>(hint * 5 / 2, 1024))) : safe_;
+    c10::DeviceGuard g(keys.device());
+    DevWs& ws = dev_ws(keys.device());
+    tab_ = ws.loc_next;
+    if (ws.loc_busy[tab_]) tab_ ^= 1;
+    TORCH_CHECK(!ws.loc_busy[tab_], "localize: at most two minibatches in flight per device");
+    ws.loc_busy[tab_] = true;
+    ws.loc_next = tab_ ^ 1;
+    enqueue();
+  }
+
+  ~LocalizeJob() {
+    if (event_) (void)hipEventDestroy(event_);
+    if (tab_ >= 0 && !done_) {
+      DevWs& ws = dev_ws(keys_.device());
+      ws.loc_busy[tab_] = false;  // abandoned: the table may hold keys
+      ws.loc_dirty[tab_] = true;
+    }
+  }
+
+  std::vector<Tensor> finish() {
+    TORCH_CHECK(!done_, "localize job already finished");
+    c10::DeviceGuard g(keys_.device());
+    auto s = cur_stream(keys_);
+    DevWs& ws = dev_ws(keys_.device());
+    auto i32 = keys_.options().dtype(torch::kInt32);
+    auto i64 = keys_.options().dtype(torch::kInt64);
+    while (true) {
+      WH_HIP_CHECK_HOST(hipEventSynchronize(event_));
+      const int64_t* h = host_.data_ptr<int64_t>();
+      const bool own = h[nshard_] != 0;
+      bool over = own;
+      for (int64_t q = 1; q < nrecv_; q += 2) over |= h[nshard_ + 1 + q] != 0;
+      if (!over) break;
+      TORCH_CHECK(!(own && tsize_ >= safe_), "localize: table overflow");
+      // every rank saw the same flags: all retry at the safe size together
+      ws.loc_dirty[tab_] = true;
+      tsize_ = safe_;
+      enqueue();
+    }
+    const int64_t* h = host_.data_ptr<int64_t>();
+    auto owner_cnt_h = torch::empty({nshard_}, torch::kInt64);
+    int64_t U = 0;
+    for (int64_t p = 0; p < nshard_; ++p) {
+      owner_cnt_h.data_ptr<int64_t>()[p] = h[p];
+      U += h[p];
+    }
+    Tensor recv_h = torch::empty({nrecv_}, torch::kInt64);
+    for (int64_t q = 0; q < nrecv_; ++q) recv_h.data_ptr<int64_t>()[q] = h[nshard_ + 1 + q];
+    const int64_t nnz = nnz_, nrows = offset_.numel() - 1;
+    const float* vp = val_.defined() ? ptr<float>(val_) : nullptr;
+    auto tlid = torch::empty({tsize_}, i32);
+    auto uniq = torch::empty({U}, i64);
+    wh::loc_assign(reinterpret_cast<uint64_t*>(tkeys_.data_ptr()), tsize_, (int)nshard_,
+                   ptr<int64_t>(blkoff_), ptr<int32_t>(tlid),
+                   reinterpret_cast<uint64_t*>(uniq.data_ptr()), s);
+    ws.loc_dirty[tab_] = false;  // loc_assign empties the table again
+    ws.loc_busy[tab_] = false;
+    done_ = true;
+    auto row_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
+    const int64_t n1 = std::max<int64_t>(nnz, 1);
+    auto lid = torch::empty({nnz}, i32);
+    auto work = torch::empty({3 * n1}, i32);  // pos | sorted lid | sorted pos
+    wh::loc_rows_lid(ptr<int64_t>(offset_), nrows, ptr<int32_t>(slot_of_), ptr<int32_t>(tlid),
+                     ptr<int32_t>(row_of), ptr<int32_t>(lid), vp ? ptr<int32_t>(work) : nullptr,
+                     s);
+    const size_t sbytes = wh::loc_sort_tmp_bytes(nnz, U);
+    auto stmp = torch::empty({(int64_t)sbytes + 16}, keys_.options().dtype(torch::kUInt8));
+    auto csc_off = torch::empty({U + 1}, i64);
+    auto ucnt = torch::empty({U}, i32);
+    auto csc_row = torch::empty({nnz}, i32);
+    auto csc_val = vp ? torch::empty({nnz}, keys_.options().dtype(torch::kFloat32))
+                      : torch::empty({0}, keys_.options().dtype(torch::kFloat32));
+    int32_t* wp = ptr<int32_t>(work);
+    wh::loc_csc(ptr<int32_t>(row_of), vp, nnz, U, ptr<int32_t>(lid), wp, wp + n1, wp + 2 * n1,
+                stmp.data_ptr(), sbytes, ptr<int64_t>(csc_off), ptr<int32_t>(ucnt),
+                ptr<int32_t>(csc_row), vp ? ptr<float>(csc_val) : nullptr, s);
+    return {uniq, ucnt, owner_cnt_h, lid, csc_off, csc_row, csc_val, recv_h};
+  }
+
+ private:
+  void enqueue() {
+    auto s = cur_stream(keys_);
+    DevWs& ws = dev_ws(keys_.device());
+    auto i32 = keys_.options().dtype(torch::kInt32);
+    auto i64 = keys_.options().dtype(torch::kInt64);
+    // The table is a persistent per-device slab that loc_assign leaves
+    // empty, so a minibatch costs no clearing pass; it is re-filled only
+    // after an overflow retry or an abandoned job (loc_dirty).
+    if (ws.loc_tab[tab_].numel() < tsize_) {
+      ws.loc_tab[tab_] = torch::full({safe_}, -1, i64);
+      ws.loc_ovf[tab_].zero_();
+      ws.loc_dirty[tab_] = false;
+    } else if (ws.loc_dirty[tab_]) {
+      ws.loc_tab[tab_].fill_(-1);
+      ws.loc_ovf[tab_].zero_();
+      ws.loc_dirty[tab_] = false;
+    }
+    tkeys_ = ws.loc_tab[tab_].narrow(0, 0, tsize_);
+    ws.loc_dirty[tab_] = true;  // until loc_assign has run
+    slot_of_ = torch::empty({std::max<int64_t>(nnz_, 1)}, i32);
+    auto owner_cnt = torch::empty({nshard_ + 1}, i64);  // [nshard] = overflow count
+    wh::loc_insert(reinterpret_cast<const uint64_t*>(keys_.data_ptr()), nnz_,
+                   reinterpret_cast<uint64_t*>(tkeys_.data_ptr()), tsize_,
+                   ptr<int32_t>(slot_of_), ptr<int64_t>(ws.loc_ovf[tab_]), s);
+    blkoff_ = torch::empty({nshard_ * wh::loc_owner_blocks(tsize_)}, i64);
+    wh::loc_owner_count(reinterpret_cast<const uint64_t*>(tkeys_.data_ptr()), tsize_,
+                        (int)nshard_, ptr<int64_t>(blkoff_), ptr<int64_t>(owner_cnt),
+                        ptr<int64_t>(ws.loc_ovf[tab_]), s);
+    Tensor both = owner_cnt;
+    nrecv_ = 0;
+    if (!exchange_.is_none()) {
+      Tensor recv = exchange_(owner_cnt).cast<Tensor>();
+      TORCH_CHECK(recv.scalar_type() == torch::kInt64 && recv.numel() % 2 == 0,
+                  "localize: exchange must return int64 [2 * world]");
+      nrecv_ = recv.numel();
+      both = torch::cat({owner_cnt, recv.reshape({-1}).to(owner_cnt.device())});
+    }
+    dev_counts_ = both.contiguous();
+    if (!host_.defined() || host_.numel() < dev_counts_.numel())
+      host_ = torch::empty({dev_counts_.numel()},
+                           torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
+    // an async copy into pinned memory + an event: nothing blocks here
+    WH_HIP_CHECK_HOST(hipMemcpyAsync(host_.data_ptr(), dev_counts_.data_ptr(),
+                                     dev_counts_.numel() * sizeof(int64_t),
+                                     hipMemcpyDeviceToHost, s));
+    if (!event_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&event_, hipEventDisableTiming));
+    WH_HIP_CHECK_HOST(hipEventRecord(event_, s));
+  }
+
+  Tensor keys_, offset_, val_;
+  int64_t nshard_, nnz_ = 0, safe_ = 0, tsize_ = 0, nrecv_ = 0;
+  py::object exchange_;
+  int tab_ = -1;
+  bool done_ = false;
+  Tensor tkeys_, slot_of_, blkoff_, dev_counts_, host_;
+  hipEvent_t event_ = nullptr;
+};
+
 std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
                              const c10::optional<Tensor>& val, int64_t nshard, int64_t hint,
                              py::object exchange) {
-  CHECK_IN(keys, torch::kInt64);
-  CHECK_IN(offset, torch::kInt64);
-  TORCH_CHECK(nshard >= 1 && nshard <= 1024, "nshard out of range");
-  c10::DeviceGuard g(keys.device());
-  auto s = cur_stream(keys);
-  const int64_t nnz = keys.numel();
-  const int64_t nrows = offset.numel() - 1;
-  TORCH_CHECK(nnz < (int64_t)INT32_MAX, "minibatch too large for int32 local ids");
-  const float* vp = optptr<float>(val);
-  if (vp) { CHECK_IN((*val), torch::kFloat32); TORCH_CHECK(val->numel() == nnz); }
-  auto i32 = keys.options().dtype(torch::kInt32);
-  auto i64 = keys.options().dtype(torch::kInt64);
-  // Table size: >= 2*nnz can never overflow; with a hint (the previous
-  // minibatch's unique count) use ~2.5x the hint instead, which keeps the
-  // scratch table small enough to stay cache resident, and fall back to the
-  // safe size if this minibatch overflowed it.
-  const int64_t safe = next_pow2(std::max<int64_t>(2 * nnz, 1024));
-  int64_t tsize = hint > 0 ? std::min(safe, next_pow2(std::max<int64_t>(hint * 5 / 2, 1024)))
-                           : safe;
-  Tensor tkeys, slot_of, owner_cnt, owner_cnt_h, recv_h, blkoff;
-  const bool ex = !exchange.is_none();
-  // The table is a persistent per-device slab that loc_assign leaves empty,
-  // so a minibatch costs no clearing pass; it is re-filled only after an
-  // overflow retry or an aborted call (loc_dirty).
-  DevWs& ws = dev_ws(keys.device());
-  while (true) {
-    if (ws.loc_tab.numel() < tsize) {
-      ws.loc_tab = torch::full({safe}, -1, i64);
-      ws.loc_dirty = false;
-    } else if (ws.loc_dirty) {
-      ws.loc_tab.fill_(-1);
-      ws.loc_ovf.zero_();
-      ws.loc_dirty = false;
-    }
-    tkeys = ws.loc_tab.narrow(0, 0, tsize);
-    ws.loc_dirty = true;
-    slot_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
-    owner_cnt = torch::empty({nshard + 1}, i64);  // [nshard] = overflow count
-    wh::loc_insert(reinterpret_cast<const uint64_t*>(keys.data_ptr()), nnz,
-                   reinterpret_cast<uint64_t*>(tkeys.data_ptr()), tsize, ptr<int32_t>(slot_of),
-                   ptr<int64_t>(ws.loc_ovf), s);
-    blkoff = torch::empty({nshard * wh::loc_owner_blocks(tsize)}, i64);
-    wh::loc_owner_count(reinterpret_cast<const uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
-                        ptr<int64_t>(blkoff), ptr<int64_t>(owner_cnt), ptr<int64_t>(ws.loc_ovf),
-                        s);
-    // the number of unique keys sizes everything downstream: one host sync
-    if (ex) {
-      Tensor recv = exchange(owner_cnt).cast<Tensor>();
-      TORCH_CHECK(recv.scalar_type() == torch::kInt64 && recv.numel() % 2 == 0,
-                  "localize: exchange must return int64 [2 * world]");
-      auto both = torch::cat({owner_cnt, recv.reshape({-1})}).to(torch::kCPU);
-      owner_cnt_h = both.narrow(0, 0, nshard + 1);
-      recv_h = both.narrow(0, nshard + 1, recv.numel()).contiguous();
-      const bool own = owner_cnt_h.data_ptr<int64_t>()[nshard] != 0;
-      bool over = own;
-      for (int64_t q = 1; q < recv_h.numel(); q += 2) over |= recv_h.data_ptr<int64_t>()[q] != 0;
-      if (!over) break;
-      TORCH_CHECK(!(own && tsize >= safe), "localize: table overflow");
-    } else {
-      owner_cnt_h = owner_cnt.to(torch::kCPU);
-      if (owner_cnt_h.data_ptr<int64_t>()[nshard] == 0 || tsize >= safe) break;
-    }
-    tsize = safe;
-  }
-  TORCH_CHECK(owner_cnt_h.data_ptr<int64_t>()[nshard] == 0, "localize: table overflow");
-  owner_cnt_h = owner_cnt_h.narrow(0, 0, nshard).contiguous();
-  int64_t U = 0;
-  for (int64_t p = 0; p < nshard; ++p) U += owner_cnt_h.data_ptr<int64_t>()[p];
-  auto tlid = torch::empty({tsize}, i32);
-  auto uniq = torch::empty({U}, i64);
-  wh::loc_assign(reinterpret_cast<uint64_t*>(tkeys.data_ptr()), tsize, (int)nshard,
-                 ptr<int64_t>(blkoff), ptr<int32_t>(tlid),
-                 reinterpret_cast<uint64_t*>(uniq.data_ptr()), s);
-  ws.loc_dirty = false;
-  auto row_of = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
-  const int64_t n1 = std::max<int64_t>(nnz, 1);
-  auto lid = torch::empty({nnz}, i32);
-  auto work = torch::empty({3 * n1}, i32);  // pos | sorted lid | sorted pos
-  wh::loc_rows_lid(ptr<int64_t>(offset), nrows, ptr<int32_t>(slot_of), ptr<int32_t>(tlid),
-                   ptr<int32_t>(row_of), ptr<int32_t>(lid), vp ? ptr<int32_t>(work) : nullptr, s);
-  const size_t sbytes = wh::loc_sort_tmp_bytes(nnz, U);
-  auto stmp = torch::empty({(int64_t)sbytes + 16}, keys.options().dtype(torch::kUInt8));
-  auto csc_off = torch::empty({U + 1}, i64);
-  auto ucnt = torch::empty({U}, i32);
-  auto csc_row = torch::empty({nnz}, i32);
-  auto csc_val = vp ? torch::empty({nnz}, keys.options().dtype(torch::kFloat32))
-                    : torch::empty({0}, keys.options().dtype(torch::kFloat32));
-  int32_t* wp = ptr<int32_t>(work);
-  wh::loc_csc(ptr<int32_t>(row_of), vp, nnz, U,
-              ptr<int32_t>(lid), wp, wp + n1, wp + 2 * n1, stmp.data_ptr(), sbytes,
-              ptr<int64_t>(csc_off), ptr<int32_t>(ucnt), ptr<int32_t>(csc_row),
-              vp ? ptr<float>(csc_val) : nullptr, s);
-  if (!recv_h.defined()) recv_h = torch::empty({0}, torch::kInt64);
-  return {uniq, ucnt, owner_cnt_h, lid, csc_off, csc_row, csc_val, recv_h};
+  LocalizeJob job(keys, offset, val, nshard, hint, exchange);
+  return job.finish();
 }
 
 // --------------------------------------------------------------- KVStore
@@ -834,6 +921,12 @@ Tensor spmv_t(const Tensor& csc_off, const Tensor& csc_row, const c10::optional<
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "wormhole_amd gfx950 HIP kernels";
   m.def("scan_excl", &scan_excl);
+  py::class_<LocalizeJob>(m, "LocalizeJob")
+      .def(py::init<const Tensor&, const Tensor&, const c10::optional<Tensor>&, int64_t, int64_t,
+                    py::object>(),
+           py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(), py::arg("nshard") = 1,
+           py::arg("hint") = 0, py::arg("exchange") = py::none())
+      .def("finish", &LocalizeJob::finish);
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
         py::arg("nshard") = 1, py::arg("hint") = 0, py::arg("exchange") = py::none());
   m.def("fm_forward", &fm_forward);

@@ -417,3 +417,51 @@ def test_difacto_open_pull_fused(hip, l1_shrk):
         gv = torch.randn(max(m, 1), 16, generator=g) * 0.1
         gs.difacto_push(sg, hg, gw.to(DEV), gv[:m].contiguous().to(DEV), hp, 2, l1_shrk, 5)
         cs.difacto_push(sc, hc, gw, gv[:m].contiguous(), hp, 2, l1_shrk, 5)
+
+
+def test_localize_job_pipelined(hip):
+    """Two-phase localize (begin: insert + counts + async read; finish): two
+    jobs in flight on the double-buffered tables, an under-sized table that
+    retries inside finish(), and the same results as the one-shot call."""
+    from wormhole_amd import ops
+    batches = [_rand_batch(2000, 20, 8000, s, s % 2 == 1) for s in range(4)]
+    dev = [(k.to(DEV), o.to(DEV), v.to(DEV) if v is not None else None) for k, o, v, _ in batches]
+    ref_out = [ops.localize(k, o, v, 3, 0) for k, o, v in dev]
+    j0 = ops.localize_begin(*dev[0], 3, 1)       # hint 1: overflows, retries at the safe size
+    j1 = ops.localize_begin(*dev[1], 3, 5000)    # second job in flight (other table)
+    outs = [ops.localize_finish(j0), ops.localize_finish(j1)]
+    j2 = ops.localize_begin(*dev[2], 3, 0)
+    outs.append(ops.localize_finish(j2))
+    j3 = ops.localize_begin(*dev[3], 3, 0)
+    del j3  # abandoned: its table must be cleaned before reuse
+    outs.append(ops.localize(*dev[3], 3, 0))
+    for (k, o, v), a, b in zip(dev, outs, ref_out):
+        assert torch.equal(torch.sort(a[0]).values, torch.sort(b[0]).values)
+        assert torch.equal(a[0][a[3].long()], k)
+        assert torch.equal(a[2], b[2])
+        cnt_a = torch.zeros(a[0].numel(), dtype=torch.int64, device=DEV)
+        assert torch.equal(a[1].long().sum(), torch.tensor(k.numel(), device=DEV))
+        assert torch.equal(a[4][1:] - a[4][:-1], a[1].long())
+
+
+def test_learner_pipelined_matches_plain(hip):
+    from wormhole_amd.config.schema import DifactoConfig, Embedding
+    from wormhole_amd.data.synthetic import CRITEO_TB_CARD
+    from wormhole_amd.models.difacto import DifactoLearner
+    from wormhole_amd.parallel.comm import Comm
+    card = torch.tensor(CRITEO_TB_CARD, dtype=torch.int64, device=DEV)
+    res = []
+    for pipelined in (False, True):
+        emb = Embedding(dim=16, threshold=2)
+        lr = DifactoLearner(DifactoConfig(minibatch=5000, embedding=[emb]),
+                            Comm(DEV, init=False), DEV, cap=1 << 20, vcap=1 << 16, seed=3)
+        data = [hip.synth_criteo(5000, 9, s, card) for s in range(6)]
+        for s, (k, l, o) in enumerate(data):
+            nb = None
+            if pipelined and s + 1 < len(data):
+                nb = (data[s + 1][0], data[s + 1][2], None)
+            lr.process(k, o, None, l, 0, 0, next_batch=nb)
+        res.append(lr.take_progress())
+    a, b = res
+    assert a[4] == b[4] and a[5] == b[5] and a[7] == b[7]
+    assert abs(a[0] - b[0]) < 1e-4 * abs(b[0]) and abs(a[1] - b[1]) < 1e-6

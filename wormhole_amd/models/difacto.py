@@ -48,6 +48,7 @@ class DifactoLearner:
         self.auc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.n_mb = 0
         self.max_key = 0  # set from the -max_key system flag (apps/ps_app.py)
+        self._job = None  # (keys, localize job) begun for the next minibatch
         self.uhint = 0  # unique ids of the previous minibatch (localize table size)
         # overlap each push's all-to-all with the next minibatch's localize
         # (same semantics: the push is applied before the next lookup)
@@ -55,19 +56,36 @@ class DifactoLearner:
         self.step = 0
 
     # ------------------------------------------------------------------ step
-    def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0):
+    def _localize(self, keys, offset, val, next_batch):
+        """Localize this minibatch (finishing the job begun by the previous
+        call when it was told about this one), then begin the next one, so
+        the host read of the unique-id counts overlaps this minibatch's
+        kernels. next_batch = (keys, offset, val) of the NEXT call; every rank
+        must pass it in lockstep (the count exchange is a collective)."""
+        job, self._job = self._job, None
+        if job is not None and job[0] is keys:
+            loc = ops.localize_finish(job[1])
+        else:
+            k = ops.key_mod(keys, self.max_key) if self.max_key else keys
+            loc = ops.localize(k, offset, val, self.kv.nshard, self.uhint,
+                               exchange=self.kv.count_exchange())
+        if next_batch is not None:
+            nk, no, nv = next_batch
+            k = ops.key_mod(nk, self.max_key) if self.max_key else nk
+            self._job = (nk, ops.localize_begin(k, no, nv, self.kv.nshard, loc[0].numel(),
+                                                exchange=self.kv.count_exchange()))
+        return loc
+
+    def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):
         """One minibatch. Returns predictions (py) for PRED, else None."""
         train = wtype == TRAIN
-        if self.max_key:  # ps-lite -max_key: fold the key space (reference Localizer)
-            keys = ops.key_mod(keys, self.max_key)
-        ex = self.kv.count_exchange()
-        loc = ops.localize(keys, offset, val, self.kv.nshard, self.uhint, exchange=ex)
+        loc = self._localize(keys, offset, val, next_batch)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
         self.uhint = uniq.numel()
         push_cnt = train and data_pass == 0 and self.dim > 0
         sess, hdr, vc = self.kv.difacto_open_pull(
             uniq, owner_cnt, train, ucnt if push_cnt else None, self.hp, self.threshold,
-            self.l1_shrk, self.seed, recv=loc[7] if ex is not None else None)
+            self.l1_shrk, self.seed, recv=loc[7] if len(loc) > 7 else None)
         self.last_sizes = (uniq.numel(), sess.m)  # (unique keys, embedding rows; device)
         if self.vstride == 0:  # no embedding: a plain linear model over w
             hdr, vc = hdr[:, 0].contiguous(), None

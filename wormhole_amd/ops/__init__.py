@@ -46,6 +46,33 @@ def localize(keys, offset, val=None, nshard=1, hint=0, exchange=None):
     return out + (exchange(dev)[0::2].tolist(),)
 
 
+class _CpuJob:
+    def __init__(self, args):
+        self.args = args
+
+    def finish(self):
+        return localize(*self.args)
+
+
+def localize_begin(keys, offset, val=None, nshard=1, hint=0, exchange=None):
+    """Start localizing a minibatch (hash insert, owner counts, count exchange,
+    async read of the counts); :func:`localize_finish` completes it with the
+    same results as :func:`localize`. Beginning minibatch i+1 before training
+    minibatch i hides the one host read of the counts behind i's kernels."""
+    if _gpu(keys):
+        return _native.hip().LocalizeJob(keys, offset, val, nshard, int(hint), exchange)
+    return _CpuJob((keys, offset, val, nshard, hint, exchange))
+
+
+def localize_finish(job):
+    out = job.finish()
+    if isinstance(job, _CpuJob) or len(out) == 7:
+        return tuple(out)
+    if out[7].numel() == 0:
+        return tuple(out[:7])
+    return tuple(out[:7]) + (out[7][0::2].tolist(),)
+
+
 def fm_forward(offset, lid, val, w_or_hdr, vc, vstride, label, loss, met):
     """difacto: w_or_hdr = pull header [U, 2] {w, vidx}, vc = [m, vstride]
     embedding rows; linear (vstride == 0): w_or_hdr = w [U], vc = None."""
