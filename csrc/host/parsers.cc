@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 
@@ -68,6 +69,11 @@ void ParseLibSVM(const char* p, const char* end, RowBlock* blk) {
 // criteo TSV: [label] 13 integer fields, 26 categorical (8-char hex) fields
 void ParseCriteo(const char* p, const char* end, bool is_train, RowBlock* blk) {
   blk->clear();
+  // a Criteo line is ~200-250 bytes with up to 39 ids: reserve once
+  const size_t rows_est = (size_t)(end - p) / 180 + 16;
+  blk->label.reserve(rows_est);
+  blk->offset.reserve(rows_est + 1);
+  blk->index.reserve(rows_est * 39);
   auto find = [&](const char* s, char c) {
     while (s != end && *s != c && !is_eol(*s)) ++s;
     return s;
@@ -79,7 +85,7 @@ void ParseCriteo(const char* p, const char* end, bool is_train, RowBlock* blk) {
     if (is_train) {
       pp = find(p, '\t');
       if (pp == p) throw std::runtime_error("criteo: no label, try criteo_test");
-      blk->label.push_back((float)std::atof(std::string(p, pp).c_str()));
+      blk->label.push_back(std::strtof(p, nullptr));  // stops at the tab
       p = pp < end ? pp + 1 : pp;
     } else {
       blk->label.push_back(0.f);
@@ -223,30 +229,49 @@ BlockReader::BlockReader(const std::string& path, int part, int nparts, const st
   split_.reset(new InputSplit(path, part, nparts, fmt == "crb"));
 }
 
+bool BlockReader::NextRaw(std::string* buf) {
+  if (fmt_ == "crb") return split_->NextRecord(buf);
+  return split_->NextChunk(buf);
+}
+
+void BlockReader::ParseRaw(const std::string& fmt, const std::string& buf, RowBlock* blk) {
+  if (fmt == "crb") {
+    CRBDecode(buf.data(), buf.size(), blk);
+    return;
+  }
+  const char* p = buf.data();
+  const char* e = p + buf.size();
+  if (fmt == "libsvm") ParseLibSVM(p, e, blk);
+  else if (fmt == "criteo") ParseCriteo(p, e, true, blk);
+  else if (fmt == "criteo_test") ParseCriteo(p, e, false, blk);
+  else ParseAdfea(p, e, blk);
+}
+
 bool BlockReader::Next(RowBlock* blk) {
   std::string buf;
-  if (fmt_ == "crb") {
-    if (!split_->NextRecord(&buf)) return false;
-    CRBDecode(buf.data(), buf.size(), blk);
-    return true;
-  }
   while (true) {
-    if (!split_->NextChunk(&buf)) return false;
-    const char* p = buf.data();
-    const char* e = p + buf.size();
-    if (fmt_ == "libsvm") ParseLibSVM(p, e, blk);
-    else if (fmt_ == "criteo") ParseCriteo(p, e, true, blk);
-    else if (fmt_ == "criteo_test") ParseCriteo(p, e, false, blk);
-    else ParseAdfea(p, e, blk);
-    if (blk->size() > 0) return true;
+    if (!NextRaw(&buf)) return false;
+    ParseRaw(fmt_, buf, blk);
+    if (fmt_ == "crb" || blk->size() > 0) return true;
   }
 }
 
 // ------------------------------------------------------ threaded parser
+int ThreadedReader::DefaultThreads() {
+  if (const char* e = std::getenv("WH_PARSE_THREADS")) {
+    const int n = std::atoi(e);
+    if (n > 0) return n;
+  }
+  const int hw = (int)std::thread::hardware_concurrency();
+  return std::max(1, std::min(16, hw));
+}
+
 ThreadedReader::ThreadedReader(const std::string& path, int part, int nparts,
-                               const std::string& fmt, size_t depth)
-    : reader_(path, part, nparts, fmt), depth_(depth) {
-  th_ = std::thread([this] { Run(); });
+                               const std::string& fmt, int nthreads, size_t depth)
+    : reader_(path, part, nparts, fmt) {
+  const int n = nthreads > 0 ? nthreads : DefaultThreads();
+  window_ = depth * (size_t)n;
+  for (int t = 0; t < n; ++t) th_.emplace_back([this] { Work(); });
 }
 
 ThreadedReader::~ThreadedReader() {
@@ -255,55 +280,83 @@ ThreadedReader::~ThreadedReader() {
     stop_ = true;
   }
   cv_.notify_all();
-  if (th_.joinable()) th_.join();
+  for (auto& t : th_)
+    if (t.joinable()) t.join();
 }
 
-void ThreadedReader::Run() {
+void ThreadedReader::Work() {
   try {
     while (true) {
-      RowBlock b;
-      const bool ok = reader_.Next(&b);
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || q_.size() < depth_; });
-      if (stop_) return;
+      {  // bounded look-ahead: at most window_ chunks parsed ahead of the consumer
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] {
+          return stop_ || total_ >= 0 || next_read_ - next_out_ < (int64_t)window_;
+        });
+        if (stop_ || total_ >= 0) return;
+      }
+      std::string buf;
+      int64_t seq;
+      bool ok;
+      {
+        std::lock_guard<std::mutex> io(io_mu_);
+        ok = reader_.NextRaw(&buf);
+        std::lock_guard<std::mutex> lk(mu_);
+        seq = next_read_;
+        if (ok) {
+          ++next_read_;
+        } else if (total_ < 0) {
+          total_ = next_read_;
+        }
+      }
       if (!ok) {
-        done_ = true;
         cv_.notify_all();
         return;
       }
-      q_.push_back(std::move(b));
+      RowBlock b;
+      BlockReader::ParseRaw(reader_.fmt(), buf, &b);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        ready_.emplace(seq, std::move(b));
+      }
       cv_.notify_all();
     }
   } catch (const std::exception& e) {
     std::lock_guard<std::mutex> lk(mu_);
-    err_ = e.what();
-    done_ = true;
+    if (err_.empty()) err_ = e.what();
+    if (total_ < 0) total_ = next_read_;
     cv_.notify_all();
   }
 }
 
 bool ThreadedReader::Next(RowBlock* out) {
   std::unique_lock<std::mutex> lk(mu_);
-  cv_.wait(lk, [&] { return !q_.empty() || done_; });
-  if (!err_.empty()) throw std::runtime_error(err_);
-  if (q_.empty()) return false;
-  *out = std::move(q_.front());
-  q_.pop_front();
-  cv_.notify_all();
-  return true;
+  while (true) {
+    cv_.wait(lk, [&] {
+      return !err_.empty() || ready_.count(next_out_) ||
+             (total_ >= 0 && next_out_ >= total_);
+    });
+    if (!err_.empty()) throw std::runtime_error(err_);
+    auto it = ready_.find(next_out_);
+    if (it == ready_.end()) return false;  // all chunks consumed
+    *out = std::move(it->second);
+    ready_.erase(it);
+    ++next_out_;
+    cv_.notify_all();
+    if (out->size() > 0 || reader_.fmt() == "crb") return true;
+  }
 }
 
 // ------------------------------------------------------- minibatch iter
 MinibatchIter::MinibatchIter(const std::string& path, int part, int nparts,
                              const std::string& fmt, size_t mb_size, size_t shuf_buf,
-                             float neg_sampling, uint64_t seed)
+                             float neg_sampling, uint64_t seed, int nthreads)
     : mb_size_(mb_size), shuf_buf_(shuf_buf), neg_(neg_sampling), rng_(seed) {
   WH_CHECK(mb_size > 0, "minibatch size must be positive");
   if (shuf_buf) {
     WH_CHECK(shuf_buf > mb_size, "shuffle buffer must exceed the minibatch size");
-    inner_.reset(new MinibatchIter(path, part, nparts, fmt, shuf_buf, 0, 1.f, seed + 1));
+    inner_.reset(new MinibatchIter(path, part, nparts, fmt, shuf_buf, 0, 1.f, seed + 1, nthreads));
   } else {
-    reader_.reset(new ThreadedReader(path, part, nparts, fmt));
+    reader_.reset(new ThreadedReader(path, part, nparts, fmt, nthreads));
   }
 }
 

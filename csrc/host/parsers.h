@@ -1,6 +1,7 @@
 #pragma once
 #include <condition_variable>
 #include <deque>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <random>
@@ -24,37 +25,48 @@ class BlockReader {
  public:
   BlockReader(const std::string& path, int part, int nparts, const std::string& fmt);
   bool Next(RowBlock* blk);
+  // I/O only: the next raw chunk (text: whole lines; crb: one record)
+  bool NextRaw(std::string* buf);
+  // CPU only: parse a raw chunk of format fmt
+  static void ParseRaw(const std::string& fmt, const std::string& buf, RowBlock* blk);
+  const std::string& fmt() const { return fmt_; }
 
  private:
   std::string fmt_;
   std::unique_ptr<InputSplit> split_;
 };
 
-// BlockReader on a background thread with a bounded queue (dmlc ThreadedParser)
+// Parser threads over one split (dmlc ThreadedParser + the reference's
+// OpenMP LibSVMParser): chunks are read in order under a lock, parsed by
+// nthreads workers in parallel, and handed out IN READ ORDER (results do not
+// depend on the thread count). nthreads = 0 picks WH_PARSE_THREADS or
+// min(16, hardware threads).
 class ThreadedReader {
  public:
   ThreadedReader(const std::string& path, int part, int nparts, const std::string& fmt,
-                 size_t depth = 4);
+                 int nthreads = 0, size_t depth = 4);
   ~ThreadedReader();
   bool Next(RowBlock* out);
+  static int DefaultThreads();
 
  private:
-  void Run();
+  void Work();
   BlockReader reader_;
-  size_t depth_;
-  std::deque<RowBlock> q_;
-  std::mutex mu_;
+  size_t window_;
+  std::mutex io_mu_, mu_;
   std::condition_variable cv_;
-  bool done_ = false, stop_ = false;
+  int64_t next_read_ = 0, next_out_ = 0, total_ = -1;  // total_: chunks once EOF is seen
+  std::map<int64_t, RowBlock> ready_;
+  bool stop_ = false;
   std::string err_;
-  std::thread th_;
+  std::vector<std::thread> th_;
 };
 
 class MinibatchIter {
  public:
   MinibatchIter(const std::string& path, int part, int nparts, const std::string& fmt,
                 size_t mb_size, size_t shuf_buf = 0, float neg_sampling = 1.f,
-                uint64_t seed = 0);
+                uint64_t seed = 0, int nthreads = 0);
   bool Next();
   const RowBlock& Value() const { return mb_; }
 

@@ -68,7 +68,7 @@ RowBlock py_to_block(const Tensor& keys, const Tensor& offset, const c10::option
 // whole split of a file as one block (for the BSP apps that keep their split resident)
 py::tuple load_split(const std::string& path, int part, int nparts, const std::string& fmt) {
   py::gil_scoped_release nogil;
-  BlockReader r(path, part, nparts, fmt);
+  ThreadedReader r(path, part, nparts, fmt);
   RowBlock all, b;
   bool any_val = false;
   while (r.Next(&b)) {

@@ -289,3 +289,40 @@ def test_van_messaging_and_failure_notice(host):
     for c in clients[:2]:
         c.close()
     srv.close()
+
+
+def test_parallel_parser_is_ordered(tmp_path, monkeypatch):
+    """Chunks parsed by many threads come out in file order: the minibatches
+    do not depend on the parser thread count."""
+    import random
+    from wormhole_amd import _native
+    host = _native.host()
+    rnd = random.Random(3)
+    path = tmp_path / "c.txt"
+    with open(path, "w") as f:
+        for i in range(40000):
+            ints = [str(rnd.randint(0, 99)) if rnd.random() > 0.2 else "" for _ in range(13)]
+            cats = ["%08x" % rnd.getrandbits(32) if rnd.random() > 0.1 else "" for _ in range(26)]
+            f.write("\t".join([str(i % 2)] + ints + cats) + "\n")
+    outs = []
+    for nt in ("1", "7"):
+        monkeypatch.setenv("WH_PARSE_THREADS", nt)
+        it = host.MinibatchIter(str(path), 0, 1, "criteo", 1000, 0, 1.0, 0)
+        got = []
+        while True:
+            r = it.next()
+            if r is None:
+                break
+            got.append([t.clone() if t is not None else None for t in r[:4]])
+        outs.append(got)
+        full = host.load_split(str(path), 0, 1, "criteo")
+        outs.append([[full[0], full[1], full[2], full[3]]])
+    a, b = outs[0], outs[2]
+    assert len(a) == len(b) == 40
+    def same(u, v):
+        return (u is None and v is None) or (u is not None and v is not None and torch.equal(u, v))
+    for x, y in zip(a, b):
+        for u, v in zip(x, y):
+            assert same(u, v)
+    for u, v in zip(outs[1][0], outs[3][0]):
+        assert same(u, v)
