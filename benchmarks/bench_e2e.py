@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""End-to-end throughput from FILES through the whole PS stack -- the path a
+user of the reference's Criteo tutorial runs (doc/tutorial/criteo_kaggle.rst:
+`dmlc_local.py -n W -s S bin/linear.dmlc ...`, published 1.85 M examples/s):
+tracker -> scheduler (workload pool over virtual file parts) -> worker
+(parallel text parser -> minibatches -> H2D -> localize -> pull -> loss ->
+push -> FTRL) -> progress table.
+
+The Criteo-format text (label, 13 integer, 26 categorical fields) is
+synthesised with fixed-width fields by vectorised numpy (no dataset is
+reachable here), optionally converted to CRB with bin/convert.dmlc, and
+trained for one data pass. Throughput = examples / wall time of the job's
+training pass, read from the scheduler's progress table.
+
+    python benchmarks/bench_e2e.py [--rows 2000000] [--files 4] [--model linear|difacto]
+                                   [--format criteo|crb] [-n 1]
+"""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+HEX = np.frombuffer(b"0123456789abcdef", dtype=np.uint8)
+DIG = np.frombuffer(b"0123456789", dtype=np.uint8)
+
+
+def criteo_text(nrows, seed):
+    """nrows lines of fixed-width Criteo TSV: 1-char label, 13 4-digit ints,
+    26 8-hex categoricals (power-law values so ids repeat like real data)."""
+    rng = np.random.default_rng(seed)
+    width = 1 + 13 * 5 + 26 * 9 + 1
+    buf = np.empty((nrows, width), dtype=np.uint8)
+    lab = (rng.random(nrows) < 0.25).astype(np.uint8)
+    buf[:, 0] = DIG[lab]
+    col = 1
+    for _ in range(13):
+        v = np.minimum((rng.pareto(1.2, nrows) * 3).astype(np.int64), 9999)
+        buf[:, col] = 9  # tab
+        for d in range(4):
+            buf[:, col + 4 - d] = DIG[(v // 10 ** d) % 10]
+        col += 5
+    for f in range(26):
+        card = int(10 ** rng.uniform(1, 6.5))
+        v = (np.minimum(rng.pareto(1.1, nrows) * 2, card - 1).astype(np.int64) * 2654435761
+             + f * 97) & 0xFFFFFFFF
+        buf[:, col] = 9
+        for d in range(8):
+            buf[:, col + 8 - d] = HEX[(v >> (4 * d)) & 15]
+        col += 9
+    buf[:, col] = 10  # newline
+    return buf.tobytes()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=2_000_000)
+    ap.add_argument("--files", type=int, default=4)
+    ap.add_argument("--model", default="linear", choices=["linear", "difacto"])
+    ap.add_argument("--format", default="criteo", choices=["criteo", "crb"])
+    ap.add_argument("-n", type=int, default=1, help="workers (one GPU each)")
+    ap.add_argument("--minibatch", type=int, default=100000)
+    ap.add_argument("--dir", default=None)
+    args = ap.parse_args()
+    work = args.dir or tempfile.mkdtemp(prefix="wh_e2e_")
+    os.makedirs(work, exist_ok=True)
+    t0 = time.time()
+    per = args.rows // args.files
+    for i in range(args.files):
+        p = os.path.join(work, "train-part_%d.txt" % i)
+        with open(p, "wb") as f:
+            f.write(criteo_text(per, 100 + i))
+        if args.format == "crb":
+            subprocess.run([os.path.join(ROOT, "bin", "convert.dmlc"),
+                            "-data_in", p, "-data_out", p[:-4] + ".crb", "-format_in", "criteo",
+                            "-format_out", "crb"], check=True)
+            os.remove(p)
+    gen_s = time.time() - t0
+    pattern = os.path.join(work, "train-part_.*\\.%s" % ("crb" if args.format == "crb" else "txt"))
+    conf = os.path.join(work, "job.conf")
+    with open(conf, "w") as f:
+        f.write('train_data = "%s"\ndata_format = "%s"\nminibatch = %d\nmax_data_pass = 1\n'
+                "print_sec = 1\n" % (pattern, args.format, args.minibatch))
+        if args.model == "linear":
+            f.write("lambda_l1 = 4\nlr_eta = 0.1\n")
+        else:
+            f.write("lr_eta = 0.01\nembedding {\n  dim = 64\n  threshold = 100\n"
+                    "  lambda_l2 = 1\n  lr_eta = 0.01\n}\n")
+    binp = os.path.join(ROOT, "bin", "%s.dmlc" % args.model)
+    cmd = [sys.executable, os.path.join(ROOT, "tracker", "dmlc_local.py"), "-n", str(args.n),
+           "-s", str(args.n), binp, conf]
+    # the scheduler's stdout is timestamped as it streams: the training pass
+    # runs from "Training: iter = 0" to the next "Validating"/"Hit max" line
+    t1 = time.time()
+    proc = subprocess.Popen(cmd, cwd=work, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                            text=True, bufsize=1)
+    lines, t_start, t_end = [], None, None
+    for line in proc.stdout:
+        now = time.time()
+        lines.append(line)
+        if t_start is None and line.startswith("Training: iter = 0"):
+            t_start = now
+        elif t_start is not None and t_end is None and (
+                line.startswith("Validating") or line.startswith("Hit max")):
+            t_end = now
+    err = proc.stderr.read()
+    rc = proc.wait()
+    wall = time.time() - t1
+    out = "".join(lines)
+    if rc != 0:
+        sys.stderr.write(out[-3000:] + err[-3000:])
+        raise SystemExit(rc)
+    rows = [l for l in lines if re.match(r"^\s*[\d.]+\s+[\d.e+]+\s+[\d.e+]+", l)]
+    ttl = float(rows[-1].split()[1])
+    sec = (t_end or time.time()) - t_start
+    print(out[-1500:], file=sys.stderr)
+    print(json.dumps({
+        "metric": "end-to-end examples/sec from %s files, %s.dmlc, %d worker(s)" % (
+            args.format, args.model, args.n),
+        "value": ttl / sec if sec > 0 else None, "unit": "examples/s",
+        "examples": ttl, "train_sec": sec, "job_wall_sec": wall, "datagen_sec": gen_s,
+        "reference_linear_published": 1.85e6,
+        "config": {"rows": args.rows, "files": args.files, "minibatch": args.minibatch},
+    }))
+
+
+if __name__ == "__main__":
+    main()

@@ -143,18 +143,24 @@ int64_t InputSplit::Align(int64_t pos, int64_t size) {
     }
     return size;
   }
-  // recordio: first 4-aligned magic whose cflag is 0 (full) or 1 (start)
+  // recordio: first 4-aligned magic whose cflag is 0 (full) or 1 (start),
+  // scanned in 1 MB blocks (a record can be megabytes long; one fseek+fread
+  // per 4-byte step made every part boundary cost ~0.3 s)
   int64_t p = (pos + 3) & ~int64_t(3);
-  std::fseek(fp_, p, SEEK_SET);
-  uint32_t w[2];
+  constexpr int64_t kBlock = 1 << 20;
+  std::vector<uint32_t> w(kBlock / 4 + 2);
   while (p + 8 <= size) {
     std::fseek(fp_, p, SEEK_SET);
-    if (std::fread(w, 4, 2, fp_) != 2) break;
-    if (w[0] == kRecordIOMagic) {
-      const uint32_t cflag = w[1] >> 29;
-      if (cflag == 0 || cflag == 1) return p;
+    const int64_t want = std::min<int64_t>(kBlock + 8, size - p) / 4;
+    const size_t got = std::fread(w.data(), 4, (size_t)want, fp_);
+    if (got < 2) break;
+    for (size_t i = 0; i + 1 < got; ++i) {
+      if (w[i] == kRecordIOMagic) {
+        const uint32_t cflag = w[i + 1] >> 29;
+        if (cflag == 0 || cflag == 1) return p + 4 * (int64_t)i;
+      }
     }
-    p += 4;
+    p += 4 * (int64_t)(got - 1);  // the last word may start a header
   }
   return size;
 }

@@ -246,6 +246,7 @@ void register_all(py::module& m) {
         return py::make_tuple(a.filename, a.k, a.n);
       })
       .def("finish", &WorkloadPool::Finish)
+      .def("finish_one", &WorkloadPool::FinishOne)
       .def("reset", &WorkloadPool::Reset)
       .def("remove_straggler", &WorkloadPool::RemoveStraggler)
       .def("is_finished", &WorkloadPool::IsFinished)

@@ -123,6 +123,18 @@ void WorkloadPool::Set(const std::string& node, bool done) {
   }
 }
 
+void WorkloadPool::FinishOne(const std::string& node, const std::string& file, int k) {
+  std::lock_guard<std::mutex> lk(mu_);
+  for (auto it = assigned_.begin(); it != assigned_.end(); ++it) {
+    if (it->node == node && it->filename == file && it->k == k) {
+      time_.push_back(now_sec() - it->start);
+      Mark(it->filename, it->k, 2);
+      assigned_.erase(it);
+      return;
+    }
+  }
+}
+
 void WorkloadPool::Mark(const std::string& f, int k, int mark) {
   auto it = task_.find(f);
   if (it == task_.end()) return;

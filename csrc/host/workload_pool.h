@@ -27,6 +27,9 @@ class WorkloadPool {
   void Clear();
   bool Get(const std::string& node, Assignment* out);
   void Finish(const std::string& node) { Set(node, true); }
+  // finish ONE workload of node (a worker that prefetches its next workload
+  // has two assigned; Finish(node) would mark both)
+  void FinishOne(const std::string& node, const std::string& file, int k);
   void Reset(const std::string& node) { Set(node, false); }
   void RemoveStraggler();
   bool IsFinished();

@@ -21,6 +21,7 @@ bounds the minibatches in flight per worker exactly as before (the device
 queue depth), with zero staleness inside a step.
 """
 import json
+import collections
 import os
 import sys
 import time
@@ -222,8 +223,14 @@ class Scheduler:
                 m = d["msg"]
                 if m == "__closed__":
                     self._on_dead(who)
+                elif m == "finished":
+                    fin = d["finished"]
+                    self.pool.finish_one(who, fin["file"], int(fin["k"]))
                 elif m == "request":
-                    if d.get("finished"):
+                    fin = d.get("finished")
+                    if isinstance(fin, dict):  # one specific workload (prefetching worker)
+                        self.pool.finish_one(who, fin["file"], int(fin["k"]))
+                    elif fin:
                         self.pool.finish(who)
                     if stop:
                         self.van.send(who, _msg(cmd="workload", file=None))
@@ -371,26 +378,41 @@ class Worker:
         mb = c.minibatch if train else 10_000_000 if wtype == PRED else 100_000
         shuf = c.minibatch * c.rand_shuffle if (train and c.rand_shuffle > 0) else 0
         neg = c.neg_sampling if train else 1.0
-        it = None
-        cur = None
-        finished_one = False
-        exhausted = False
         pred_f = None
         pred_name = None
         last = time.time()
         seed = 1000003 * (data_pass + 1) + self.comm.rank
+        # Workloads are prefetched one ahead: as soon as one starts, the next
+        # is requested and its MinibatchIter built, so its parser threads run
+        # while this one trains (the reference's worker keeps max_concurrency
+        # minibatches in flight for the same reason). A finished workload is
+        # reported by name, so the prefetched one stays assigned.
+        queue = collections.deque()
+        exhausted = False
+        done_prev = None
+
+        def fetch():
+            nonlocal exhausted, done_prev
+            if exhausted:
+                if done_prev is not None:  # nothing left to request: report it alone
+                    self.send(msg="finished", finished=done_prev)
+                    done_prev = None
+                return
+            self.send(msg="request", finished=done_prev)
+            done_prev = None
+            d = self.recv()
+            if d.get("file") is None:
+                exhausted = True
+                return
+            it = self.host.MinibatchIter(d["file"], d["k"], d["n"], fmt, int(mb), int(shuf),
+                                         float(neg), seed + d["k"])
+            queue.append((d, it))
+
+        fetch()
         while True:
             batch = None
-            while it is None and not exhausted:
-                self.send(msg="request", finished=finished_one)
-                finished_one = False
-                d = self.recv()
-                if d.get("file") is None:
-                    exhausted = True
-                    break
-                cur = d
-                it = self.host.MinibatchIter(d["file"], d["k"], d["n"], fmt, int(mb), int(shuf),
-                                             float(neg), seed + d["k"])
+            while queue and batch is None:
+                d, it = queue[0]
                 if wtype == PRED:
                     base = os.path.basename(d["file"])
                     name = "%s%s_part-%d" % (c.predict_out, base, d["k"])
@@ -399,12 +421,14 @@ class Worker:
                             pred_f.close()
                         pred_f = open_uri(name, "w")
                         pred_name = name
-            if it is not None:
+                if len(queue) == 1:
+                    fetch()  # the next workload starts parsing now
                 batch = it.next()
                 if batch is None:
-                    it = None
-                    finished_one = True
-                    continue
+                    queue.popleft()
+                    done_prev = {"file": d["file"], "k": d["k"]}
+                    if not queue:
+                        fetch()
             have = 1 if batch is not None else 0
             if self.comm.size > 1:
                 flag = torch.tensor([have], dtype=torch.int32, device=self.comm.device)
@@ -428,7 +452,6 @@ class Worker:
                 self.send(msg="progress", data=self.learner.take_progress())
         if pred_f:
             pred_f.close()
-        if finished_one:
-            self.send(msg="request", finished=True)
-            self.recv()  # the (empty) answer
+        if done_prev is not None:
+            self.send(msg="finished", finished=done_prev)
         self.send(msg="pass_done", progress=self.learner.take_progress())
