@@ -6,6 +6,7 @@
 #include <stdexcept>
 #include <sstream>
 #include <string>
+#include <cstring>
 #include <vector>
 
 namespace wh {
@@ -48,6 +49,49 @@ struct RowBlock {
       else if (!value.empty()) value.push_back(1.f);
     }
     offset.push_back((int64_t)index.size());
+  }
+  // rows [r0, r1) of b appended in bulk (memcpy of the id / value ranges)
+  void append_rows(const RowBlock& b, size_t r0, size_t r1) {
+    if (r1 <= r0) return;
+    const int64_t s = b.offset[r0], e = b.offset[r1];
+    const int64_t base = (int64_t)index.size();
+    const bool bval = !b.value.empty();
+    if (bval && value.size() < index.size()) value.resize(index.size(), 1.f);
+    label.insert(label.end(), b.label.begin() + r0, b.label.begin() + r1);
+    if (!b.weight.empty()) weight.insert(weight.end(), b.weight.begin() + r0, b.weight.begin() + r1);
+    index.insert(index.end(), b.index.begin() + s, b.index.begin() + e);
+    if (bval) value.insert(value.end(), b.value.begin() + s, b.value.begin() + e);
+    else if (!value.empty()) value.resize(index.size(), 1.f);
+    const size_t o0 = offset.size();
+    offset.resize(o0 + (r1 - r0));
+    for (size_t r = r0; r < r1; ++r) offset[o0 + (r - r0)] = base + (b.offset[r + 1] - s);
+  }
+  // rows[0..n) of b appended in that order (the shuffle buffer's gather):
+  // one resize per array, then a memcpy per row
+  void append_gather(const RowBlock& b, const size_t* rows, size_t n) {
+    if (n == 0) return;
+    const bool bval = !b.value.empty(), bw = !b.weight.empty();
+    if (bval && value.size() < index.size()) value.resize(index.size(), 1.f);
+    size_t add = 0;
+    for (size_t i = 0; i < n; ++i) add += (size_t)(b.offset[rows[i] + 1] - b.offset[rows[i]]);
+    size_t pos = index.size();
+    const size_t l0 = label.size(), o0 = offset.size(), w0 = weight.size();
+    index.resize(pos + add);
+    if (bval || !value.empty()) value.resize(pos + add, 1.f);
+    label.resize(l0 + n);
+    offset.resize(o0 + n);
+    if (bw) weight.resize(w0 + n);
+    for (size_t i = 0; i < n; ++i) {
+      const size_t r = rows[i];
+      const int64_t s = b.offset[r], e = b.offset[r + 1];
+      const size_t len = (size_t)(e - s);
+      std::memcpy(&index[pos], &b.index[s], len * sizeof(uint64_t));
+      if (bval) std::memcpy(&value[pos], &b.value[s], len * sizeof(float));
+      pos += len;
+      label[l0 + i] = b.label[r];
+      if (bw) weight[w0 + i] = b.weight[r];
+      offset[o0 + i] = (int64_t)pos;
+    }
   }
   // drop the value array when every value is 1 (reference minibatch_iter.h:114-116)
   void compact_binary() {

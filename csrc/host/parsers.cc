@@ -363,6 +363,11 @@ MinibatchIter::MinibatchIter(const std::string& path, int part, int nparts,
 
 bool MinibatchIter::Next() {
   mb_.clear();
+  if (mb_.index.capacity() == 0) {  // first minibatch: reserve for ~40 ids per row
+    mb_.label.reserve(mb_size_);
+    mb_.offset.reserve(mb_size_ + 1);
+    mb_.index.reserve(mb_size_ * 40);
+  }
   while (mb_.size() < mb_size_) {
     if (start_ == end_) {
       if (!inner_) {
@@ -378,14 +383,20 @@ bool MinibatchIter::Next() {
       end_ = in_.size();
     }
     const size_t len = std::min(end_ - start_, mb_size_ - mb_.size());
-    std::uniform_real_distribution<float> U(0.f, 1.f);
-    for (size_t i = start_; i < start_ + len; ++i) {
-      const size_t r = inner_ ? perm_[i] : i;
-      // negative down-sampling keeps a negative with probability neg_sampling
-      // (the reference drops with that probability, §2.9 item 7: fixed here
-      // to the documented "down sampling ratio" meaning)
-      if (inner_ && neg_ < 1.f && in_.label[r] <= 0.f && U(rng_) > neg_) continue;
-      mb_.push_row(in_, r);
+    if (!inner_) {  // in order: one bulk copy
+      mb_.append_rows(in_, start_, start_ + len);
+    } else {
+      std::uniform_real_distribution<float> U(0.f, 1.f);
+      sel_.clear();
+      for (size_t i = start_; i < start_ + len; ++i) {
+        const size_t r = perm_[i];
+        // negative down-sampling keeps a negative with probability neg_sampling
+        // (the reference drops with that probability, §2.9 item 7: fixed here
+        // to the documented "down sampling ratio" meaning)
+        if (neg_ < 1.f && in_.label[r] <= 0.f && U(rng_) > neg_) continue;
+        sel_.push_back(r);
+      }
+      mb_.append_gather(in_, sel_.data(), sel_.size());
     }
     start_ += len;
   }

@@ -78,7 +78,7 @@ class MinibatchIter {
   std::unique_ptr<MinibatchIter> inner_;
   RowBlock in_, mb_;
   size_t start_ = 0, end_ = 0;
-  std::vector<size_t> perm_;
+  std::vector<size_t> perm_, sel_;
 };
 
 }  // namespace host

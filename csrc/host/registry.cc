@@ -30,19 +30,22 @@ py::list conf_to_py(const std::vector<ConfItem>& items) {
   return out;
 }
 
+// pinned = page-locked host memory (torch's caching host allocator), so the
+// learner's .to(device, non_blocking=True) is a real asynchronous DMA
 template <typename T>
-Tensor vec_to_tensor(const std::vector<T>& v, torch::ScalarType dt) {
-  auto t = torch::empty({(int64_t)v.size()}, torch::TensorOptions().dtype(dt));
+Tensor vec_to_tensor(const std::vector<T>& v, torch::ScalarType dt, bool pinned = false) {
+  auto t = torch::empty({(int64_t)v.size()}, torch::TensorOptions().dtype(dt).pinned_memory(pinned));
   if (!v.empty()) std::memcpy(t.data_ptr(), v.data(), v.size() * sizeof(T));
   return t;
 }
 
-py::tuple block_to_py(const RowBlock& b) {
+py::tuple block_to_py(const RowBlock& b, bool pinned = false) {
   py::object val = py::none(), wt = py::none();
-  if (!b.value.empty()) val = py::cast(vec_to_tensor(b.value, torch::kFloat32));
-  if (!b.weight.empty()) wt = py::cast(vec_to_tensor(b.weight, torch::kFloat32));
-  return py::make_tuple(vec_to_tensor(b.index, torch::kInt64), vec_to_tensor(b.offset, torch::kInt64),
-                        val, vec_to_tensor(b.label, torch::kFloat32), wt);
+  if (!b.value.empty()) val = py::cast(vec_to_tensor(b.value, torch::kFloat32, pinned));
+  if (!b.weight.empty()) wt = py::cast(vec_to_tensor(b.weight, torch::kFloat32, pinned));
+  return py::make_tuple(vec_to_tensor(b.index, torch::kInt64, pinned),
+                        vec_to_tensor(b.offset, torch::kInt64, pinned), val,
+                        vec_to_tensor(b.label, torch::kFloat32, pinned), wt);
 }
 
 RowBlock py_to_block(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
@@ -93,8 +96,9 @@ py::tuple load_split(const std::string& path, int part, int nparts, const std::s
 class PyMinibatchIter {
  public:
   PyMinibatchIter(const std::string& path, int part, int nparts, const std::string& fmt,
-                  int64_t mb, int64_t shuf, double neg, int64_t seed)
-      : it_(path, part, nparts, fmt, (size_t)mb, (size_t)shuf, (float)neg, (uint64_t)seed) {}
+                  int64_t mb, int64_t shuf, double neg, int64_t seed, bool pinned)
+      : it_(path, part, nparts, fmt, (size_t)mb, (size_t)shuf, (float)neg, (uint64_t)seed),
+        pinned_(pinned) {}
   py::object next() {
     bool ok;
     {
@@ -102,11 +106,12 @@ class PyMinibatchIter {
       ok = it_.Next();
     }
     if (!ok) return py::none();
-    return block_to_py(it_.Value());
+    return block_to_py(it_.Value(), pinned_);
   }
 
  private:
   MinibatchIter it_;
+  bool pinned_;
 };
 
 py::tuple localize_cpu(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
@@ -227,10 +232,10 @@ void register_all(py::module& m) {
 
   py::class_<PyMinibatchIter>(m, "MinibatchIter")
       .def(py::init<const std::string&, int, int, const std::string&, int64_t, int64_t, double,
-                    int64_t>(),
+                    int64_t, bool>(),
            py::arg("path"), py::arg("part"), py::arg("nparts"), py::arg("fmt"),
            py::arg("minibatch"), py::arg("shuffle_buf") = 0, py::arg("neg_sampling") = 1.0,
-           py::arg("seed") = 0)
+           py::arg("seed") = 0, py::arg("pinned") = false)
       .def("next", &PyMinibatchIter::next);
 
   py::class_<WorkloadPool>(m, "WorkloadPool")

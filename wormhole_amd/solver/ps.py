@@ -405,7 +405,8 @@ class Worker:
                 exhausted = True
                 return
             it = self.host.MinibatchIter(d["file"], d["k"], d["n"], fmt, int(mb), int(shuf),
-                                         float(neg), seed + d["k"])
+                                         float(neg), seed + d["k"],
+                                         self.device.type == "cuda")  # pinned: async H2D
             queue.append((d, it))
 
         fetch()
