@@ -120,11 +120,44 @@ def gen_ninja():
         lines.append("build %s: tool %s" % (obj, os.path.join(ROOT, "csrc/tools/%s.cc" % tool)))
         lines.append("build %s: link_tool %s %s" % (os.path.join(ROOT, "bin", "native", tool), obj,
                                                     " ".join(core)))
+    # host runtime self-test (no torch): bin/native/host_selftest
+    st = []
+    for name in ("workload_pool", "conf_parser", "van"):
+        obj = os.path.join(BUILD, "tool", name + ".o")
+        lines.append("build %s: tool %s" % (obj, os.path.join(ROOT, "csrc/host/%s.cc" % name)))
+        st.append(obj)
+    obj = os.path.join(BUILD, "tool", "host_selftest.o")
+    lines.append("build %s: tool %s" % (obj, os.path.join(ROOT, "csrc/tests/host_selftest.cc")))
+    lines.append("build %s: link_tool %s %s %s" % (
+        os.path.join(ROOT, "bin", "native", "host_selftest"), obj, " ".join(st),
+        " ".join(o for o in core if not o.endswith("convert_lib.o"))))
     lines.append("build %s: link_hip %s" % (os.path.join(PKG, "_hip.so"), " ".join(hip_objs)))
     lines.append("build %s: link_host %s" % (os.path.join(PKG, "_host.so"), " ".join(host_objs)))
     os.makedirs(BUILD, exist_ok=True)
     with open(os.path.join(BUILD, "build.ninja"), "w") as f:
         f.write("\n".join(lines) + "\n")
+
+
+SELFTEST_SRCS = ("csrc/tests/host_selftest.cc", "csrc/host/parsers.cc", "csrc/host/io.cc",
+                 "csrc/host/lz4.cc", "csrc/host/cityhash.cc", "csrc/host/workload_pool.cc",
+                 "csrc/host/conf_parser.cc", "csrc/host/van.cc")
+
+
+def build_sanitized(kind, jobs=None):
+    """The host self-test under -fsanitize=<kind> (address | thread |
+    undefined), host code only: build/san-<kind>/host_selftest."""
+    out_dir = os.path.join(BUILD, "san-" + kind)
+    os.makedirs(out_dir, exist_ok=True)
+    flags = ["-O1", "-g", "-std=c++17", "-pthread", "-fno-omit-frame-pointer",
+             "-fsanitize=" + kind, "-I" + os.path.join(ROOT, "csrc")]
+    objs = []
+    for src in SELFTEST_SRCS:
+        obj = os.path.join(out_dir, os.path.basename(src) + ".o")
+        subprocess.run(["g++"] + flags + ["-c", os.path.join(ROOT, src), "-o", obj], check=True)
+        objs.append(obj)
+    exe = os.path.join(out_dir, "host_selftest")
+    subprocess.run(["g++"] + flags + objs + ["-o", exe], check=True)
+    return exe
 
 
 def build(jobs=None, clean=False, verbose=False):
@@ -145,6 +178,11 @@ if __name__ == "__main__":
     ap.add_argument("-j", type=int, default=None)
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-v", action="store_true")
+    ap.add_argument("--sanitize", choices=["address", "thread", "undefined"], default=None,
+                    help="build the host self-test under a sanitizer instead")
     a = ap.parse_args()
+    if a.sanitize:
+        print(build_sanitized(a.sanitize, a.j))
+        sys.exit(0)
     build(a.j, a.clean, a.v)
     sys.exit(0)

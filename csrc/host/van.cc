@@ -80,15 +80,19 @@ int Van::Listen(int port) {
   socklen_t len = sizeof(a);
   getsockname(lfd_, (sockaddr*)&a, &len);
   port_ = ntohs(a.sin_port);
-  accept_th_ = std::thread([this] { AcceptLoop(); });
+  const int lfd = lfd_;
+  accept_th_ = std::thread([this, lfd] { AcceptLoop(lfd); });
   return port_;
 }
 
-void Van::AcceptLoop() {
+// lfd is the accept thread's own copy: Close() shuts the socket down (which
+// wakes accept), joins this thread, and only then closes the descriptor, so
+// accept() can never run on a closed or reused fd number.
+void Van::AcceptLoop(int lfd) {
   while (!closing_) {
     sockaddr_in a{};
     socklen_t len = sizeof(a);
-    int fd = ::accept(lfd_, (sockaddr*)&a, &len);
+    int fd = ::accept(lfd, (sockaddr*)&a, &len);
     if (fd < 0) {
       if (closing_) return;
       continue;
@@ -99,10 +103,8 @@ void Van::AcceptLoop() {
       ::close(fd);
       continue;
     }
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      peers_[hello] = fd;
-    }
+    std::lock_guard<std::mutex> lk(mu_);
+    peers_[hello] = fd;
     readers_.emplace_back([this, fd, hello] { ReadLoop(fd, hello); });
   }
 }
@@ -141,10 +143,8 @@ void Van::Connect(const std::string& host, int port, const std::string& my_id, d
   WH_CHECK(fd >= 0, "cannot connect to " + host + ":" + std::to_string(port));
   tune(fd);
   WH_CHECK(send_frame(fd, my_id), "hello failed");
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    peers_["scheduler"] = fd;
-  }
+  std::lock_guard<std::mutex> lk(mu_);
+  peers_["scheduler"] = fd;
   readers_.emplace_back([this, fd] { ReadLoop(fd, "scheduler"); });
 }
 
@@ -162,8 +162,12 @@ bool Van::Send(const std::string& to, const std::string& msg) {
 
 bool Van::Recv(double timeout_s, std::string* from, std::string* msg) {
   std::unique_lock<std::mutex> lk(mu_);
-  if (!cv_.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return !q_.empty(); }))
-    return false;
+  // system_clock deadline (see WorkloadPool::Loop: steady-clock waits use
+  // pthread_cond_clockwait, invisible to ThreadSanitizer)
+  const auto until = std::chrono::system_clock::now() +
+                     std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                         std::chrono::duration<double>(timeout_s));
+  if (!cv_.wait_until(lk, until, [&] { return !q_.empty(); })) return false;
   *from = q_.front().first;
   *msg = q_.front().second;
   q_.pop_front();
@@ -178,19 +182,20 @@ std::vector<std::string> Van::Peers() {
 }
 
 void Van::Close() {
-  if (closing_) return;
-  closing_ = true;
+  if (closing_.exchange(true)) return;
+  if (lfd_ >= 0) ::shutdown(lfd_, SHUT_RDWR);  // wakes accept()
+  if (accept_th_.joinable()) accept_th_.join();
   if (lfd_ >= 0) {
-    ::shutdown(lfd_, SHUT_RDWR);
     ::close(lfd_);
     lfd_ = -1;
   }
+  std::vector<std::thread> readers;
   {
     std::lock_guard<std::mutex> lk(mu_);
     for (auto& p : peers_) ::shutdown(p.second, SHUT_RDWR);
+    readers.swap(readers_);
   }
-  if (accept_th_.joinable()) accept_th_.join();
-  for (auto& t : readers_)
+  for (auto& t : readers)
     if (t.joinable()) t.join();
   std::lock_guard<std::mutex> lk(mu_);
   for (auto& p : peers_) ::close(p.second);

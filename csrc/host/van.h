@@ -26,7 +26,7 @@ class Van {
   int port() const { return port_; }
 
  private:
-  void AcceptLoop();
+  void AcceptLoop(int lfd);
   void ReadLoop(int fd, std::string id);
   void Push(const std::string& from, const std::string& msg);
 

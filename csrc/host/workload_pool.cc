@@ -36,7 +36,11 @@ WorkloadPool::~WorkloadPool() {
 void WorkloadPool::Loop() {
   std::unique_lock<std::mutex> lk(mu_);
   while (!done_) {
-    cv_.wait_for(lk, std::chrono::duration<double>(period_));
+    // (system_clock deadline: libstdc++ implements steady-clock waits with
+    // pthread_cond_clockwait, which ThreadSanitizer does not intercept)
+    cv_.wait_until(lk, std::chrono::system_clock::now() +
+                           std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                               std::chrono::duration<double>(period_)));
     if (done_) break;
     RemoveStragglerLocked();
   }
