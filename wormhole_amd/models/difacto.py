@@ -15,6 +15,7 @@ import torch
 
 from .. import ops
 from ..kv import ShardedKV, make_store
+from ..utils import trace
 
 TRAIN, VAL, PRED = 0, 1, 2
 
@@ -79,28 +80,34 @@ class DifactoLearner:
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):
         """One minibatch. Returns predictions (py) for PRED, else None."""
         train = wtype == TRAIN
-        loc = self._localize(keys, offset, val, next_batch)
+        with trace.span("localize"):
+            loc = self._localize(keys, offset, val, next_batch)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
         self.uhint = uniq.numel()
         push_cnt = train and data_pass == 0 and self.dim > 0
-        sess, hdr, vc = self.kv.difacto_open_pull(
-            uniq, owner_cnt, train, ucnt if push_cnt else None, self.hp, self.threshold,
-            self.l1_shrk, self.seed, recv=loc[7] if len(loc) > 7 else None)
+        with trace.span("pull"):
+            sess, hdr, vc = self.kv.difacto_open_pull(
+                uniq, owner_cnt, train, ucnt if push_cnt else None, self.hp, self.threshold,
+                self.l1_shrk, self.seed, recv=loc[7] if len(loc) > 7 else None)
         self.last_sizes = (uniq.numel(), sess.m)  # (unique keys, embedding rows; device)
         if self.vstride == 0:  # no embedding: a plain linear model over w
             hdr, vc = hdr[:, 0].contiguous(), None
-        py, dual, xv = ops.fm_forward(offset, lid, val, hdr, vc, self.vstride, label,
-                                      ops.LOSS_LOGIT, self.met)
-        ops.auc_acc(py, label, self.auc_sum)
+        with trace.span("forward"):
+            py, dual, xv = ops.fm_forward(offset, lid, val, hdr, vc, self.vstride, label,
+                                          ops.LOSS_LOGIT, self.met)
+            ops.auc_acc(py, label, self.auc_sum)
         self.n_mb += 1
         if train:
-            gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, hdr, vc, self.vstride)
-            if self.emb is not None and self.vstride > 0:
-                ops.fm_grad_post(gvc, sess.m, self.dim, self.emb.grad_clipping,
-                                 self.emb.dropout, self.seed + 7919 * self.step + 1,
-                                 bool(self.emb.grad_normalization))
-            self.kv.difacto_push(sess, gw, gvc, self.hp, self.threshold, self.l1_shrk,
-                                 self.seed, defer=self.defer_push)
+            with trace.span("backward"):
+                gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, hdr, vc,
+                                          self.vstride)
+                if self.emb is not None and self.vstride > 0:
+                    ops.fm_grad_post(gvc, sess.m, self.dim, self.emb.grad_clipping,
+                                     self.emb.dropout, self.seed + 7919 * self.step + 1,
+                                     bool(self.emb.grad_normalization))
+            with trace.span("push"):
+                self.kv.difacto_push(sess, gw, gvc, self.hp, self.threshold, self.l1_shrk,
+                                     self.seed, defer=self.defer_push)
         self.step += 1
         return py if wtype == PRED else None
 

@@ -10,6 +10,7 @@ import torch
 
 from .. import ops
 from ..kv import ShardedKV, make_store
+from ..utils import trace
 
 TRAIN, VAL, PRED = 0, 1, 2
 
@@ -56,18 +57,26 @@ class LinearLearner:
 
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):
         train = wtype == TRAIN
-        loc = self._localize(keys, offset, val, next_batch)
+        with trace.span("localize"):
+            loc = self._localize(keys, offset, val, next_batch)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
         self.uhint = uniq.numel()
-        sess = self.kv.open(uniq, owner_cnt, insert=train, recv=loc[7] if len(loc) > 7 else None)
-        w = self.kv.linear_pull(sess)
-        py, dual, _ = ops.fm_forward(offset, lid, val, w, None, 0, label, self.conf.loss, self.met)
-        ops.auc_acc(py, label, self.auc_sum)
+        with trace.span("pull"):
+            sess = self.kv.open(uniq, owner_cnt, insert=train,
+                                recv=loc[7] if len(loc) > 7 else None)
+            w = self.kv.linear_pull(sess)
+        with trace.span("forward"):
+            py, dual, _ = ops.fm_forward(offset, lid, val, w, None, 0, label, self.conf.loss,
+                                         self.met)
+            ops.auc_acc(py, label, self.auc_sum)
         self.n_mb += 1
         if train:
-            grad, _ = ops.fm_backward(csc_off, csc_row, csc_val, dual, None, w, None, 0)
-            self.kv.linear_push(sess, grad, self.conf.algo, self.alpha, self.beta,
-                                self.conf.lambda_l1, self.conf.lambda_l2, defer=self.defer_push)
+            with trace.span("backward"):
+                grad, _ = ops.fm_backward(csc_off, csc_row, csc_val, dual, None, w, None, 0)
+            with trace.span("push"):
+                self.kv.linear_push(sess, grad, self.conf.algo, self.alpha, self.beta,
+                                    self.conf.lambda_l1, self.conf.lambda_l2,
+                                    defer=self.defer_push)
         return py if wtype == PRED else None
 
     def flush(self):

@@ -32,6 +32,7 @@ from .. import _native
 from ..kv import checkpoint
 from ..models.progress import merge
 from ..utils.fs import open_uri  # noqa: E402
+from ..utils import trace  # noqa: E402
 
 TRAIN, VAL, PRED = 0, 1, 2
 _TYPE_NAME = {TRAIN: "training", VAL: "validation", PRED: "prediction"}
@@ -302,6 +303,7 @@ class Worker:
         self.host = _native.host()
         self.report_sec = max(0.1, float(conf.print_sec) / 2)
         self.n_done = 0
+        self.metrics = trace.MetricsStream(comm.rank)
         self.fault = _parse_fault(os.environ.get("WH_FAULT", ""), comm.rank)
 
     def send(self, **kw):
@@ -390,6 +392,10 @@ class Worker:
         queue = collections.deque()
         exhausted = False
         done_prev = None
+        n_pass = n_ex = ex_last = 0
+        pass_stages = {}
+        trace.take()  # stage times of this pass only
+        t_pass = time.time()
 
         def fetch():
             nonlocal exhausted, done_prev
@@ -424,7 +430,8 @@ class Worker:
                         pred_name = name
                 if len(queue) == 1:
                     fetch()  # the next workload starts parsing now
-                batch = it.next()
+                with trace.stage("parse"):
+                    batch = it.next()
                 if batch is None:
                     queue.popleft()
                     done_prev = {"file": d["file"], "k": d["k"]}
@@ -438,21 +445,50 @@ class Worker:
                     break
             elif not have:
                 break
-            args = self._to_dev(batch) if batch is not None else self._empty_batch()
+            with trace.stage("h2d"):
+                args = self._to_dev(batch) if batch is not None else self._empty_batch()
             if self.fault and batch is not None:
                 self._inject_fault()
-            py = self.learner.process(*args, wtype=wtype, data_pass=data_pass)
+            with trace.stage("process"):
+                py = self.learner.process(*args, wtype=wtype, data_pass=data_pass)
             self.n_done += 1
+            n_pass += 1
+            n_ex += int(args[3].numel())
             if wtype == PRED and batch is not None:
                 p = py.float().cpu()
                 if c.prob_predict:
                     p = torch.sigmoid(p)
                 pred_f.write("".join("%g\n" % v for v in p.tolist()))
             if time.time() - last > self.report_sec:
-                last = time.time()
+                now = time.time()
+                if self.metrics.f is not None:
+                    st = trace.take()
+                    for k, v in st.items():
+                        a = pass_stages.setdefault(k, [0.0, 0])
+                        a[0] += v[0]
+                        a[1] += v[1]
+                    self.metrics.write(event="progress", wtype=int(wtype), data_pass=data_pass,
+                                       examples=n_ex - ex_last,
+                                       examples_per_sec=(n_ex - ex_last) / max(now - last, 1e-9),
+                                       stages_sec={k: v[0] for k, v in st.items()})
+                    ex_last = n_ex
+                last = now
                 self.send(msg="progress", data=self.learner.take_progress())
         if pred_f:
             pred_f.close()
+        # the reference worker's summary line (minibatch_solver.h:244-248)
+        for k, v in trace.take().items():
+            a = pass_stages.setdefault(k, [0.0, 0])
+            a[0] += v[0]
+            a[1] += v[1]
+        wall = time.time() - t_pass
+        if n_pass:
+            _log("[worker %d] %s" % (self.comm.rank, trace.overhead_line(
+                {k: tuple(v) for k, v in pass_stages.items()}, wall, n_pass)))
+        self.metrics.write(event="pass_done", wtype=int(wtype), data_pass=data_pass,
+                           minibatches=n_pass, examples=n_ex, wall_sec=wall,
+                           examples_per_sec=n_ex / max(wall, 1e-9),
+                           stages_sec={k: v[0] for k, v in pass_stages.items()})
         if done_prev is not None:
             self.send(msg="finished", finished=done_prev)
         self.send(msg="pass_done", progress=self.learner.take_progress())
