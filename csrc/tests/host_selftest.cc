@@ -230,6 +230,7 @@ static void test_van() {
   int n = 0;
   std::string from, msg;
   while (n < 800 && server.Recv(10.0, &from, &msg)) {
+    if (msg == "__closed__") continue;  // a client that already got all its acks
     ++n;
     EXPECT(msg.rfind(from + ":", 0) == 0);
     EXPECT(server.Send(from, "ack"));
