@@ -122,7 +122,7 @@ def gen_ninja():
                                                     " ".join(core)))
     # host runtime self-test (no torch): bin/native/host_selftest
     st = []
-    for name in ("workload_pool", "conf_parser", "van"):
+    for name in ("workload_pool", "conf_parser", "van", "json"):
         obj = os.path.join(BUILD, "tool", name + ".o")
         lines.append("build %s: tool %s" % (obj, os.path.join(ROOT, "csrc/host/%s.cc" % name)))
         st.append(obj)
@@ -140,7 +140,7 @@ def gen_ninja():
 
 SELFTEST_SRCS = ("csrc/tests/host_selftest.cc", "csrc/host/parsers.cc", "csrc/host/io.cc",
                  "csrc/host/lz4.cc", "csrc/host/cityhash.cc", "csrc/host/workload_pool.cc",
-                 "csrc/host/conf_parser.cc", "csrc/host/van.cc")
+                 "csrc/host/conf_parser.cc", "csrc/host/van.cc", "csrc/host/json.cc")
 
 
 def build_sanitized(kind, jobs=None):

@@ -8,6 +8,7 @@
 #include "io.h"
 #include "localizer.h"
 #include "parsers.h"
+#include "scheduler.h"
 #include "van.h"
 #include "workload_pool.h"
 
@@ -260,6 +261,36 @@ void register_all(py::module& m) {
       .def_property_readonly("num_assigned", &WorkloadPool::num_assigned)
       .def_property_readonly("num_requeued", &WorkloadPool::num_requeued);
 
+  m.def("run_scheduler", [](py::dict conf, int num_workers, int num_servers, Van& van) {
+    SchedulerConf c;
+    auto str = [&](const char* k, std::string* v) {
+      if (conf.contains(k) && !conf[k].is_none()) *v = py::cast<std::string>(conf[k]);
+    };
+    auto i32 = [&](const char* k, int* v) {
+      if (conf.contains(k) && !conf[k].is_none()) *v = py::cast<int>(conf[k]);
+    };
+    auto f64 = [&](const char* k, double* v) {
+      if (conf.contains(k) && !conf[k].is_none()) *v = py::cast<double>(conf[k]);
+    };
+    auto bol = [&](const char* k, bool* v) {
+      if (conf.contains(k) && !conf[k].is_none()) *v = py::cast<bool>(conf[k]);
+    };
+    str("app", &c.app); str("train_data", &c.train_data); str("val_data", &c.val_data);
+    str("data_format", &c.data_format); str("model_in", &c.model_in);
+    str("model_out", &c.model_out); str("predict_out", &c.predict_out);
+    i32("max_data_pass", &c.max_data_pass); i32("save_iter", &c.save_iter);
+    i32("load_iter", &c.load_iter); i32("num_parts_per_file", &c.num_parts_per_file);
+    f64("print_sec", &c.print_sec); bol("local_data", &c.local_data);
+    bol("early_stop", &c.early_stop); f64("min_objv_decr", &c.min_objv_decr);
+    if (conf.contains("max_objv") && !conf["max_objv"].is_none()) {
+      c.has_max_objv = true;
+      c.max_objv = py::cast<double>(conf["max_objv"]);
+    }
+    py::gil_scoped_release nogil;
+    Scheduler(c, num_workers, num_servers, &van).Run();
+  }, py::arg("conf"), py::arg("num_workers"), py::arg("num_servers"), py::arg("van"),
+     "Run the native parameter-server scheduler (epoch loop, workload dispatch, progress "
+     "table, load/save fan-out) until the job ends");
   py::class_<Van>(m, "Van")
       .def(py::init<>())
       .def("listen", &Van::Listen)

@@ -17,6 +17,7 @@
 
 #include "host/common.h"
 #include "host/io.h"
+#include "host/json.h"
 #include "host/parsers.h"
 #include "host/van.h"
 #include "host/workload_pool.h"
@@ -206,6 +207,32 @@ static void test_pool_concurrent() {
   EXPECT(pool.num_finished() == 200);
 }
 
+static void test_json() {
+  // the control-plane messages: Python json.dumps output in, ours out
+  Json d = Json::Parse(
+      "{\"msg\": \"request\", \"finished\": {\"file\": \"a\\\"b\\u00e9\", \"k\": 3},"
+      " \"data\": [1.5, -2e-3, 0, NaN], \"files\": [], \"x\": null, \"ok\": true}");
+  EXPECT(d["msg"].str() == "request");
+  EXPECT(d["finished"]["k"].num() == 3);
+  EXPECT(d["finished"]["file"].str() == "a\"b\xc3\xa9");
+  const auto v = d["data"].nums();
+  EXPECT(v.size() == 4 && v[0] == 1.5 && v[1] == -2e-3 && v[3] != v[3]);
+  EXPECT(d["files"].strs().empty() && d["x"].is_null() && d["ok"].truthy());
+  EXPECT(!d["missing"].truthy());
+  Json o = Json::Obj().set("cmd", Json::Str("workload")).set("file", Json::Null())
+               .set("k", Json::Num(7)).set("w", Json::Num(0.25));
+  Json back = Json::Parse(o.Dump());
+  EXPECT(back["cmd"].str() == "workload" && back["file"].is_null());
+  EXPECT(back["k"].num() == 7 && back["w"].num() == 0.25);
+  bool threw = false;
+  try {
+    Json::Parse("{\"a\": }");
+  } catch (const std::exception&) {
+    threw = true;
+  }
+  EXPECT(threw);
+}
+
 static void test_van() {
   // control-plane transport: 4 clients x 200 frames into one listener, and
   // replies back, with every connection's reader thread live
@@ -248,6 +275,7 @@ int main() {
   test_splits_and_reader();
   test_conf();
   test_pool_concurrent();
+  test_json();
   test_van();
   if (g_fail) {
     std::fprintf(stderr, "host_selftest: %d failure(s)\n", g_fail);

@@ -91,12 +91,11 @@ def test_standalone_single_process(work):
 
 def test_scheduler_dispatches_every_part_once(work):
     """Port of learn/test/data_parallel_test.cc with assertions: fake workers
-    request workloads from a real Scheduler; every (file, part) is handed out
+    request workloads from the native scheduler; every (file, part) is handed out
     exactly once and the pass ends when all report done."""
     from wormhole_amd import _native
+    from wormhole_amd.apps.ps_app import scheduler_conf
     from wormhole_amd.config.schema import LinearConfig
-    from wormhole_amd.models.progress import LinearProgress
-    from wormhole_amd.solver.ps import Scheduler
     host = _native.host()
     data = work / "data"
     data.mkdir()
@@ -106,7 +105,6 @@ def test_scheduler_dispatches_every_part_once(work):
                         max_data_pass=1, print_sec=0.1)
     van = host.Van()
     port = van.listen(0)
-    sched = Scheduler(conf, "linear", 4, 2, van=van, progress_cls=LinearProgress)
     got = []
     lock = threading.Lock()
 
@@ -136,7 +134,7 @@ def test_scheduler_dispatches_every_part_once(work):
     ths = [threading.Thread(target=fake_worker, args=(i,)) for i in range(4)]
     for t in ths:
         t.start()
-    sched.run()
+    host.run_scheduler(scheduler_conf("linear", conf), 4, 2, van)
     for t in ths:
         t.join(timeout=30)
     van.close()

@@ -10,6 +10,7 @@ worker owns one parameter shard).  Without a launcher the binary runs a
 import os
 import sys
 import threading
+import time
 
 import torch
 
@@ -27,25 +28,33 @@ def _device():
     return torch.device("cuda", idx)
 
 
-def _make(kind, conf):
+def _conf_cls(kind):
     from ..config import schema
-    if kind == "linear":
-        from ..models.progress import LinearProgress
-        return schema.LinearConfig, LinearProgress, None
-    from ..models.progress import DifactoProgress
+    return schema.LinearConfig if kind == "linear" else schema.DifactoConfig
 
-    def stop_fn(agg, train, state={"pre": 100.0}):
-        cur = agg[0] / agg[5] if agg[5] else 0.0
-        if train:
-            return conf.has("max_objv") and cur > conf.max_objv
-        diff = state["pre"] - cur
-        state["pre"] = cur
-        if conf.early_stop and diff < conf.min_objv_decr:
-            print("The decrease of validation objective is smaller than the minimal "
-                  "requirement: %g vs %g" % (diff, conf.min_objv_decr), flush=True)
-            return True
-        return False
-    return schema.DifactoConfig, DifactoProgress, stop_fn
+
+def scheduler_conf(kind, conf):
+    """The fields the native scheduler (csrc/host/scheduler.cc) reads."""
+    d = {"app": kind}
+    for k in ("train_data", "val_data", "data_format", "model_in", "model_out", "predict_out",
+              "max_data_pass", "save_iter", "load_iter", "num_parts_per_file", "print_sec",
+              "local_data"):
+        v = getattr(conf, k, None)
+        if v is not None:
+            d[k] = v
+    if kind == "difacto":
+        d["early_stop"] = bool(conf.early_stop)
+        d["min_objv_decr"] = float(conf.min_objv_decr)
+        if conf.has("max_objv"):
+            d["max_objv"] = float(conf.max_objv)
+    return d
+
+
+def run_scheduler(host, kind, conf, nw, ns, van):
+    """The native scheduler (GIL released while it runs); a short grace period
+    lets the workers read the final exit command before the van closes."""
+    host.run_scheduler(scheduler_conf(kind, conf), nw, ns, van)
+    time.sleep(0.2)
 
 
 def _learner(kind, conf, comm, device, nshard, max_key=0):
@@ -91,15 +100,13 @@ def split_system_flags(argv):
 def main(kind, argv):
     from .. import _native, config
     from ..parallel.comm import Comm
-    from ..solver.ps import Scheduler, Worker
+    from ..solver.ps import Worker
 
     sysflags, argv = split_system_flags(list(argv))
     if len(argv) < 1:
         print("usage: %s.dmlc <conf|none> [key=value ...]" % kind, file=sys.stderr)
         return 1
-    cls, prog_cls, _ = _make(kind, None)
-    conf = config.load(cls, argv[0], argv[1:])
-    _, prog_cls, stop_fn = _make(kind, conf)
+    conf = config.load(_conf_cls(kind), argv[0], argv[1:])
     if kind == "difacto" and conf.early_stop and not conf.val_data:
         raise SystemExit("early stop needs validation dataset")
     role = os.environ.get("DMLC_ROLE")
@@ -111,12 +118,11 @@ def main(kind, argv):
         # standalone: scheduler in a thread, one worker here
         van_s = host.Van()
         port = van_s.listen(0)
-        sched = Scheduler(conf, kind, 1, 1, van=van_s, progress_cls=prog_cls, stop_fn=stop_fn)
         err = []
 
         def run_sched():
             try:
-                sched.run()
+                run_scheduler(host, kind, conf, 1, 1, van_s)
             except Exception as e:  # pragma: no cover - surfaced below
                 err.append(e)
         th = threading.Thread(target=run_sched, daemon=True)
@@ -140,7 +146,7 @@ def main(kind, argv):
     if role == "scheduler":
         van = host.Van()
         van.listen(port)
-        Scheduler(conf, kind, nw, nshard, van=van, progress_cls=prog_cls, stop_fn=stop_fn).run()
+        run_scheduler(host, kind, conf, nw, nshard, van)
         van.close()
         return 0
     if role == "server":

@@ -1,4 +1,5 @@
-"""Parameter-server solver runtime: scheduler + workers.
+"""Parameter-server solver runtime, worker side; the
+scheduler is native (csrc/host/scheduler.cc, ``_host.run_scheduler``).
 
 Reference layering (learn/solver/): DataParScheduler/Worker (dynamic
 workload dispatch, data_parallel.h) < IterScheduler/Server/Worker (model
@@ -30,7 +31,6 @@ import torch
 
 from .. import _native
 from ..kv import checkpoint
-from ..models.progress import merge
 from ..utils.fs import open_uri  # noqa: E402
 from ..utils import trace  # noqa: E402
 
@@ -55,233 +55,6 @@ def _parse_fault(spec, rank):
     if int(r) != rank:
         return None
     return kind, float(arg)
-
-
-# --------------------------------------------------------------------------
-# scheduler
-# --------------------------------------------------------------------------
-class Scheduler:
-    """MinibatchScheduler (learn/solver/minibatch_solver.h:10-195)."""
-
-    def __init__(self, conf, app, num_workers, num_servers, van=None, port=0,
-                 progress_cls=None, stop_fn=None):
-        self.conf = conf
-        self.app = app
-        self.nw = num_workers
-        self.ns = num_servers
-        self.host = _native.host()
-        self.van = van or self.host.Van()
-        self.port = self.van.port if van else self.van.listen(port)
-        self.progress_cls = progress_cls
-        self.stop_fn = stop_fn
-        self.workers = []
-        self.pool = None
-        self.dead = set()
-        self.start = time.time()
-
-    # ---------------------------------------------------------- plumbing
-    def wait_workers(self, timeout=600):
-        t0 = time.time()
-        while len(self.workers) < self.nw:
-            m = self.van.recv(1.0)
-            if m is None:
-                if time.time() - t0 > timeout:
-                    raise RuntimeError("only %d of %d workers connected" % (len(self.workers), self.nw))
-                continue
-            who, raw = m
-            d = json.loads(raw)
-            if d.get("msg") == "ready":
-                self.workers.append(who)
-        self.workers.sort(key=lambda w: int(w.split("-")[1]))
-
-    def broadcast(self, **kw):
-        for w in self.workers:
-            self.van.send(w, _msg(**kw))
-
-    def _recv(self, timeout=1.0):
-        m = self.van.recv(timeout)
-        if m is None:
-            return None, None
-        who, raw = m
-        if raw == b"__closed__":
-            return who, {"msg": "__closed__"}
-        return who, json.loads(raw)
-
-    def _on_dead(self, who):
-        if who in self.dead:
-            return
-        self.dead.add(who)
-        _log("[scheduler] node %s died" % who)
-        if self.pool is not None:
-            self.pool.reset(who)  # re-queue its workload (data_parallel.h:131-135)
-        raise RuntimeError("worker %s failed; its workload was re-queued, restart from the "
-                           "last saved model (model_in / load_iter)" % who)
-
-    def command(self, cmd, **kw):
-        """Send a command to all workers and wait for every ack."""
-        self.broadcast(cmd=cmd, **kw)
-        acks = 0
-        prog = None
-        while acks < len(self.workers):
-            who, d = self._recv()
-            if d is None:
-                continue
-            if d["msg"] == "__closed__":
-                self._on_dead(who)
-            elif d["msg"] == "ack":
-                acks += 1
-                if d.get("progress"):
-                    prog = merge(prog, d["progress"])
-        return prog
-
-    # ------------------------------------------------------------ epochs
-    def run(self):
-        c = self.conf
-        self.wait_workers()
-        print("Connected %d servers and %d workers" % (self.ns, self.nw), flush=True)
-        self.start = time.time()
-        is_pred = bool(c.predict_out)
-        if is_pred and not c.model_in:
-            raise RuntimeError("should provide model_in for predicting")
-        cur = 0
-        if c.model_in:
-            if c.load_iter > 0:
-                print("Loading model from iter = %d" % c.load_iter, flush=True)
-                cur = c.load_iter
-            else:
-                print("Loading the last model", flush=True)
-                cur = -1
-            self.command("load", file=c.model_in, iter=cur)
-            self.iterate(cur, PRED)
-            cur += 1
-        if is_pred:
-            print("Prediction is finished!", flush=True)
-            self.shutdown()
-            return True
-        while cur < c.max_data_pass:
-            if self.iterate(cur, TRAIN) or self.iterate(cur, VAL):
-                print("Hit stop critera", flush=True)
-                break
-            if cur == c.max_data_pass - 1:
-                print("Hit max number of data passes %d" % c.max_data_pass, flush=True)
-                break
-            if c.model_out and c.save_iter > 0 and (cur + 1) % c.save_iter == 0:
-                print("Saving model for iter = %d" % cur, flush=True)
-                self.command("save", file=c.model_out, iter=cur)
-            cur += 1
-        if c.model_out:
-            print("Saving the final model", flush=True)
-            self.command("save", file=c.model_out, iter=-1)
-        print("Training is finished!", flush=True)
-        self.shutdown()
-        return True
-
-    def shutdown(self):
-        self.broadcast(cmd="exit")
-        time.sleep(0.2)
-
-    def iterate(self, it, wtype):
-        """One data pass; returns True when the stop criterion fires."""
-        c = self.conf
-        train = wtype == TRAIN
-        if train:
-            data = c.train_data
-            print("Training: iter = %d" % it, flush=True)
-        else:
-            data = c.val_data
-            if wtype == PRED:
-                print("Predicting", flush=True)
-            else:
-                print("Validating: iter = %d" % it, flush=True)
-                if not data:
-                    return False
-        self.pool = self.host.WorkloadPool(shuffle=train, seed=it + 1)
-        if c.local_data:
-            # every worker matches the pattern on its own file system and its
-            # parts are preferably handed to it (reference StartDispatch with
-            # use_worker_local_data_, data_parallel.h:96-101 + node affinity)
-            nfiles = self.match_on_workers(data)
-            if nfiles == 0:
-                raise RuntimeError("no worker has a file matching '%s'" % data)
-        else:
-            files = self.host.match_file(data)
-            if not files:
-                raise RuntimeError("no file matches '%s'" % data)
-            if c.num_parts_per_file * len(files) < self.nw:
-                _log("[scheduler] #parts (%d) < #workers (%d): some workers idle; increase "
-                     "num_parts_per_file" % (c.num_parts_per_file * len(files), self.nw))
-            self.pool.add(files, int(c.num_parts_per_file))
-        prog_printer = self.progress_cls()
-        print("  sec %s" % prog_printer.head(), flush=True)
-        self.broadcast(cmd="iterate", type=wtype, data_pass=it, fmt=c.data_format)
-        done = 0
-        agg = None
-        stop = False
-        last = time.time()
-        while done < len(self.workers):
-            who, d = self._recv(0.05)
-            if d is not None:
-                m = d["msg"]
-                if m == "__closed__":
-                    self._on_dead(who)
-                elif m == "finished":
-                    fin = d["finished"]
-                    self.pool.finish_one(who, fin["file"], int(fin["k"]))
-                elif m == "request":
-                    fin = d.get("finished")
-                    if isinstance(fin, dict):  # one specific workload (prefetching worker)
-                        self.pool.finish_one(who, fin["file"], int(fin["k"]))
-                    elif fin:
-                        self.pool.finish(who)
-                    if stop:
-                        self.van.send(who, _msg(cmd="workload", file=None))
-                        continue
-                    a = self.pool.get(who)
-                    if a is None:
-                        self.van.send(who, _msg(cmd="workload", file=None))
-                    else:
-                        self.van.send(who, _msg(cmd="workload", file=a[0], k=a[1], n=a[2]))
-                elif m == "progress":
-                    agg = merge(agg, d["data"])
-                elif m == "pass_done":
-                    done += 1
-                    if d.get("progress"):
-                        agg = merge(agg, d["progress"])
-            if train and time.time() - last >= c.print_sec:
-                last = time.time()
-                if agg is not None:
-                    s = self.show(prog_printer, agg, True)
-                    agg = None
-                    if s and not stop:
-                        stop = True
-                        self.pool.clear()  # reference StopDispatch
-        if agg is not None:
-            s = self.show(prog_printer, agg, train)
-            stop = stop or s
-        return stop
-
-    def match_on_workers(self, pattern):
-        self.broadcast(cmd="match", data=pattern)
-        got, nfiles = 0, 0
-        while got < len(self.workers):
-            who, d = self._recv()
-            if d is None:
-                continue
-            if d["msg"] == "__closed__":
-                self._on_dead(who)
-            elif d["msg"] == "matched":
-                got += 1
-                if d["files"]:
-                    nfiles += len(d["files"])
-                    self.pool.add(d["files"], int(self.conf.num_parts_per_file), who)
-        return nfiles
-
-    def show(self, printer, agg, train):
-        line = printer.line(agg)
-        if not line:
-            return False
-        print("%5.0f  %s" % (time.time() - self.start, line), flush=True)
-        return bool(self.stop_fn and self.stop_fn(agg, train))
 
 
 # --------------------------------------------------------------------------
