@@ -26,14 +26,15 @@ def _val_lines(out):
 
 @pytest.mark.parametrize("app,conf", [("linear", "learn/linear/guide/demo.conf"),
                                       ("difacto", "learn/difacto/guide/demo.conf")])
-def test_ps_demo_gpu_matches_cpu(work, capsys, monkeypatch, app, conf):
+def test_ps_demo_gpu_matches_cpu(work, capfd, monkeypatch, app, conf):
+    # (capfd: the native scheduler prints the table on the process's fd 1)
     from wormhole_amd.apps.ps_app import main
     monkeypatch.setenv("WH_DEVICE", "auto")
     assert main(app, [conf, "rand_shuffle=0"]) == 0
-    gpu = capsys.readouterr().out
+    gpu = capfd.readouterr().out
     monkeypatch.setenv("WH_DEVICE", "cpu")
     assert main(app, [conf, "rand_shuffle=0"]) == 0
-    cpu = capsys.readouterr().out
+    cpu = capfd.readouterr().out
     g, c = _val_lines(gpu), _val_lines(cpu)
     assert len(g) == len(c) == 3
     for lg, lc in zip(g, c):
