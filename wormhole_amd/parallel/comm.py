@@ -175,13 +175,13 @@ class Comm:
         return out
 
     def all_to_all_v_multi(self, items, async_op=False):
-        """Several row-wise all-to-all-v exchanges fused into ONE group of
-        point-to-point transfers (one RCCL group launch; on xGMI every peer
-        pair has its own link, so the transfers of all tensors to all peers
-        run concurrently).  items: [(x, send_rows, recv_rows), ...].
-        async_op: return (outputs, handle) and leave the wait to the caller
-        (handle.wait() orders the current stream after the transfers); the
-        inputs must stay alive until then."""
+        """Several row-wise all-to-all-v exchanges issued back to back, one
+        RCCL all-to-all-v per tensor (RCCL runs each as one grouped
+        send/recv over every xGMI peer link at once; the collectives queue on
+        the same stream, so the tensors' transfers pipeline). items:
+        [(x, send_rows, recv_rows), ...]. async_op: return (outputs, handle)
+        and leave the wait to the caller (handle.wait() orders the current
+        stream after the transfers); the inputs must stay alive until then."""
         if self.size == 1:
             outs = [x for x, _, _ in items]
             return (outs, _Done()) if async_op else outs
@@ -190,29 +190,24 @@ class Comm:
             outs = self.all_to_all_v_multi([(x.cpu(), s, r) for x, s, r in items])
             outs = [o.to(d) for o, d in zip(outs, dev)]
             return (outs, _Done()) if async_op else outs
-        outs, ops = [], []
+        outs, reqs, keep = [], [], []
         for x, send, recv in items:
             x = x.contiguous()
+            keep.append(x)
             out = torch.empty((sum(recv),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-            so = ro = 0
-            for p in range(self.size):
-                sn, rn = send[p], recv[p]
-                if p == self.rank:
-                    if sn:
-                        out[ro:ro + rn].copy_(x[so:so + sn])
-                else:
-                    if sn:
-                        ops.append(dist.P2POp(dist.isend, x[so:so + sn], p))
-                    if rn:
-                        ops.append(dist.P2POp(dist.irecv, out[ro:ro + rn], p))
-                so += sn
-                ro += rn
             outs.append(out)
-        reqs = dist.batch_isend_irecv(ops) if ops else []
+            width = 1
+            for d in x.shape[1:]:
+                width *= int(d)
+            if x.numel() == 0 and out.numel() == 0 and width == 0:
+                continue
+            req = dist.all_to_all_single(out.view(-1), x.view(-1),
+                                         [r * width for r in recv], [s_ * width for s_ in send],
+                                         async_op=async_op)
+            if async_op:
+                reqs.append(req)
         if async_op:
-            return outs, _Reqs(reqs, [x for x, _, _ in items])
-        for req in reqs:
-            req.wait()
+            return outs, _Reqs(reqs, keep)
         return outs
 
     def exchange_counts_dev(self, send_dev):
