@@ -28,8 +28,8 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--dim", type=int, default=128)
     ap.add_argument("--k", type=int, default=1000)
-    ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
     torch.cuda.set_device(env_local_rank())
     dev = torch.device("cuda", env_local_rank())

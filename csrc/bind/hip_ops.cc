@@ -6,6 +6,8 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "hip/wh_kernels.h"
@@ -886,6 +888,18 @@ Tensor kmeans_accum(const Tensor& X, const Tensor& assign, int64_t k) {
   const int f = (int)X.size(1);
   TORCH_CHECK(assign.numel() == n);
   auto sums = torch::zeros({k, f + 1}, X.options());
+  // counting-sort path unless WH_KMEANS_ACCUM=atomic (A/B) or k / f too large
+  static const bool atomic_only = [] {
+    const char* e = std::getenv("WH_KMEANS_ACCUM");
+    return e && std::string(e) == "atomic";
+  }();
+  if (!atomic_only && n > 0) {
+    auto scratch = torch::empty({wh::kmeans_accum_scratch(n, (int)k)},
+                                X.options().dtype(torch::kUInt8));
+    if (wh::kmeans_accum_sorted(ptr<float>(X), n, f, (int)k, ptr<int32_t>(assign),
+                                ptr<float>(sums), scratch.data_ptr(), cur_stream(X)))
+      return sums;
+  }
   wh::kmeans_accum(ptr<float>(X), n, f, ptr<int32_t>(assign), ptr<float>(sums), cur_stream(X));
   return sums;
 }

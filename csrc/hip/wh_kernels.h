@@ -240,6 +240,11 @@ void kmeans_assign(const float* Xp, int64_t n, int f, const float* Cp, int k, in
                    float* score, hipStream_t s);
 void kmeans_accum(const float* X, int64_t n, int f, const int32_t* assign, float* sums,
                   hipStream_t s);
+// the same sums through a counting sort by cluster + register segment sums
+// (returns false when k / f exceed its LDS / register limits: use the above)
+int64_t kmeans_accum_scratch(int64_t n, int k);
+bool kmeans_accum_sorted(const float* X, int64_t n, int f, int k, const int32_t* assign,
+                         float* sums, void* scratch, hipStream_t s);
 
 // -------------------------------------------------------------- gbdt.hip
 void gbdt_bin(const float* X, int64_t n, int f, const float* cuts, const int32_t* cut_off,

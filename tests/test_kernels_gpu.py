@@ -373,6 +373,25 @@ def test_kmeans_assign_accum(hip, n, f, k):
     assert torch.allclose(sums, ref_s, atol=1e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("n,f,k,skew", [(200_003, 128, 1000, False), (100_000, 64, 5, True),
+                                        (50_000, 600, 10, False), (70_000, 33, 20000, False)])
+def test_kmeans_accum_sorted(hip, n, f, k, skew):
+    """Counting-sort accumulation (multi-block histograms, segments crossing
+    waves, a dominant cluster) and its atomic fallback (f > 512, k > 16384)
+    against index_add."""
+    g = torch.Generator().manual_seed(n + k)
+    X = torch.randn(n, f, generator=g)
+    a = torch.randint(0, k, (n,), generator=g)
+    if skew:
+        a[torch.rand(n, generator=g) < 0.9] = 3
+    sums = hip.kmeans_accum(X.to(DEV), a.to(torch.int32).to(DEV), k).cpu()
+    ref_s = torch.zeros(k, f + 1, dtype=torch.float64)
+    ref_s[:, :f].index_add_(0, a, X.double())
+    ref_s[:, f].index_add_(0, a, torch.ones(n, dtype=torch.float64))
+    assert torch.equal(sums[:, f], ref_s[:, f].float())
+    assert torch.allclose(sums.double(), ref_s, atol=5e-3 * (n / k) ** 0.5, rtol=1e-4)
+
+
 def test_spmv_kernels(hip):
     keys, off, val, label = _rand_batch(3000, 20, 5000, 9, True)
     uniq, ucnt, oc, lid, csc_off, csc_row, csc_val = hip.localize(
