@@ -121,6 +121,7 @@ class DifactoLearner:
         """Progress vector in the reference layout (learn/difacto/progress.h):
         [objv, auc, objv_w, copc, count, new_ex, new_w, new_V]; resets."""
         self.flush()
+        ops.auc_join(self.auc_sum)
         m = self.met.tolist()
         a = float(self.auc_sum.item())
         st = self.store.stats

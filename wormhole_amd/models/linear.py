@@ -88,6 +88,7 @@ class LinearLearner:
         """Reference layout (learn/linear/progress.h): [objv, acc, auc, count,
         new_ex, new_w]; accuracy is the per-minibatch-mean convention."""
         self.flush()
+        ops.auc_join(self.auc_sum)
         m = self.met.tolist()
         a = float(self.auc_sum.item())
         st = self.store.stats
