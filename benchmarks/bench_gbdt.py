@@ -38,9 +38,18 @@ def main():
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--max-bin", type=int, default=256)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: the framework's PyTorch CPU path (anchor numbers)")
     a = ap.parse_args()
-    torch.cuda.set_device(env_local_rank())
-    dev = torch.device("cuda", env_local_rank())
+    if a.device == "cuda":
+        torch.cuda.set_device(env_local_rank())
+        dev = torch.device("cuda", env_local_rank())
+    else:
+        dev = torch.device("cpu")
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
     bsp = BSP(dev)
     n = a.rows // bsp.world
     X, y = higgs_like(n, a.features, 7 + bsp.rank, dev)
@@ -50,23 +59,23 @@ def main():
     p.max_depth = a.depth
     p.eta = 0.1
     p.max_bin = a.max_bin
-    torch.cuda.synchronize()
+    sync()
     t_prep = time.perf_counter()
     cuts = G.Cuts.build(dm, p.max_bin, bsp)
     B = cuts.bin(dm)
-    torch.cuda.synchronize()
+    sync()
     t_prep = time.perf_counter() - t_prep
     obj = G.Objective(p.objective)
     tb = G.TreeBuilder(p, bsp, dm, cuts, B)
     margin = torch.zeros(n, device=dev)
     for _ in range(a.warmup):
         tb.build(obj.gpair(margin, dm.label, None), margin)
-    torch.cuda.synchronize()
+    sync()
     bsp.barrier()
     t0 = time.perf_counter()
     for _ in range(a.trees):
         tb.build(obj.gpair(margin, dm.label, None), margin)
-    torch.cuda.synchronize()
+    sync()
     bsp.barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -75,7 +84,7 @@ def main():
     err = G.eval_metric("error", torch.sigmoid(margin), dm.label, None, bsp)
     if bsp.rank == 0:
         print(json.dumps({"metric": "GBDT trees/s (hist, depth %d, %dx%d)" % (a.depth, a.rows, a.features),
-                          "value": a.trees / dt, "unit": "trees/s", "n_gpus": bsp.world,
+                          "value": a.trees / dt, "unit": "trees/s", "n_gpus": bsp.world if dev.type == "cuda" else 0, "device": dev.type,
                           "ms_per_tree": 1000 * dt / a.trees,
                           "projected_500_trees_s": 500 * dt / a.trees, "sketch_bin_s": t_prep,
                           "train_error": err, "scaling": "strong", "data": "synthetic Higgs-shaped"}),

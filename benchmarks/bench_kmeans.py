@@ -30,9 +30,18 @@ def main():
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: the framework's PyTorch CPU path (anchor numbers)")
     a = ap.parse_args()
-    torch.cuda.set_device(env_local_rank())
-    dev = torch.device("cuda", env_local_rank())
+    if a.device == "cuda":
+        torch.cuda.set_device(env_local_rank())
+        dev = torch.device("cuda", env_local_rank())
+    else:
+        dev = torch.device("cpu")
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
     bsp = BSP(dev)
     n = a.rows // bsp.world
     g = torch.Generator(device=dev).manual_seed(1234 + bsp.rank)
@@ -44,12 +53,12 @@ def main():
     km.init_centroids(0)
     for _ in range(a.warmup):
         km.step()
-    torch.cuda.synchronize()
+    sync()
     bsp.barrier()
     t0 = time.perf_counter()
     for _ in range(a.iters):
         km.step()
-    torch.cuda.synchronize()
+    sync()
     bsp.barrier()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -58,10 +67,10 @@ def main():
     flops = 2.0 * a.rows * a.k * a.dim * a.iters
     if bsp.rank == 0:
         print(json.dumps({"metric": "k-means iterations/s (k=%d, dense %dx%d)" % (a.k, a.rows, a.dim),
-                          "value": a.iters / dt, "unit": "iter/s", "n_gpus": bsp.world,
+                          "value": a.iters / dt, "unit": "iter/s", "n_gpus": bsp.world if dev.type == "cuda" else 0, "device": dev.type,
                           "ms_per_iter": 1000 * dt / a.iters, "rows_per_s": a.rows * a.iters / dt,
                           "assign_tflops": flops / dt / 1e12, "scaling": "strong",
-                          "dtype": "fp32 (exact fp32 MFMA)", "data": "synthetic gaussian mixture"}),
+                          "dtype": "fp32 (exact fp32 MFMA)" if dev.type == "cuda" else "fp64 (CPU reference path)", "data": "synthetic gaussian mixture"}),
               flush=True)
     bsp.finalize()
 
