@@ -93,13 +93,29 @@ def main():
     # i trains (learner.process(next_batch=...)): the one host read of the
     # unique-id counts then overlaps i's kernels. The pipeline does not cross
     # the warm-up / timed boundary, so every timed step's work is timed.
+    # On the GPU the next minibatch is generated on its own stream (as the
+    # file path's H2D copies run on theirs), concurrently with this
+    # minibatch's localize; the learner waits on its event just before the
+    # next localize begins.
+    gen = torch.cuda.Stream(device) if device.type == "cuda" else None
+
+    def batch_async(step):
+        if gen is None:
+            return batch(step), None
+        with torch.cuda.stream(gen):
+            out = batch(step)
+            ev = torch.cuda.Event()
+            ev.record(gen)
+        out[1].record_stream(torch.cuda.current_stream(device))  # the label
+        return out, ev
+
     def run(first, n):
-        nxt = batch(first)
+        nxt, ev = batch(first), None
         for s in range(first, first + n):
             keys, label, offset = nxt
-            nxt = batch(s + 1) if s + 1 < first + n else None
+            nxt, ev = batch_async(s + 1) if s + 1 < first + n else (None, None)
             learner.process(keys, offset, None, label, 0, 0,
-                            next_batch=(nxt[0], nxt[2], None) if nxt is not None else None)
+                            next_batch=(nxt[0], nxt[2], None, ev) if nxt is not None else None)
 
     def sync():
         if device.type == "cuda":

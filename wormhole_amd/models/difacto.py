@@ -14,6 +14,7 @@ learn/difacto/async_sgd.h:363-425), re-expressed on the GPU:
 import torch
 
 from .. import ops
+from ._pipeline import localize_pipelined
 from ..kv import ShardedKV, make_store
 from ..utils import trace
 
@@ -58,24 +59,7 @@ class DifactoLearner:
 
     # ------------------------------------------------------------------ step
     def _localize(self, keys, offset, val, next_batch):
-        """Localize this minibatch (finishing the job begun by the previous
-        call when it was told about this one), then begin the next one, so
-        the host read of the unique-id counts overlaps this minibatch's
-        kernels. next_batch = (keys, offset, val) of the NEXT call; every rank
-        must pass it in lockstep (the count exchange is a collective)."""
-        job, self._job = self._job, None
-        if job is not None and job[0] is keys:
-            loc = ops.localize_finish(job[1])
-        else:
-            k = ops.key_mod(keys, self.max_key) if self.max_key else keys
-            loc = ops.localize(k, offset, val, self.kv.nshard, self.uhint,
-                               exchange=self.kv.count_exchange())
-        if next_batch is not None:
-            nk, no, nv = next_batch
-            k = ops.key_mod(nk, self.max_key) if self.max_key else nk
-            self._job = (nk, ops.localize_begin(k, no, nv, self.kv.nshard, loc[0].numel(),
-                                                exchange=self.kv.count_exchange()))
-        return loc
+        return localize_pipelined(self, keys, offset, val, next_batch)
 
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):
         """One minibatch. Returns predictions (py) for PRED, else None."""
