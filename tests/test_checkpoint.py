@@ -66,3 +66,17 @@ def test_linear_roundtrip(tmp_path):
     st2 = CpuKVStore(1 << 10, 0, 0)
     checkpoint.load_linear(st2, str(tmp_path / "l"))
     assert torch.equal(st.linear_pull(st.find(keys, False)), st2.linear_pull(st2.find(keys, False)))
+
+
+def test_async_saver_host_store(tmp_path):
+    st, _ = _trained_store()
+    checkpoint.save_difacto(st, str(tmp_path / "a"))
+    sv = checkpoint.AsyncSaver()
+    sv.save("difacto", st, str(tmp_path / "b"))
+    sv.join()
+    assert (tmp_path / "a").read_bytes() == (tmp_path / "b").read_bytes()
+    lin = CpuKVStore(1 << 10, 0, 0)
+    lin.find(torch.arange(5), True)
+    checkpoint.save_linear(lin, str(tmp_path / "l1"))
+    sv.save("linear", lin, str(tmp_path / "l2"))
+    assert (tmp_path / "l1").read_bytes() == (tmp_path / "l2").read_bytes()

@@ -484,3 +484,33 @@ def test_learner_pipelined_matches_plain(hip):
     a, b = res
     assert a[4] == b[4] and a[5] == b[5] and a[7] == b[7]
     assert abs(a[0] - b[0]) < 1e-4 * abs(b[0]) and abs(a[1] - b[1]) < 1e-6
+
+
+def test_async_saver_snapshot(hip, tmp_path):
+    """The background save writes the state at the save call: updates
+    issued right after it (before the file is written) must not leak in, and
+    the file equals the synchronous dump byte for byte."""
+    from wormhole_amd.kv import checkpoint
+    gs = hip.KVStore(1 << 14, 1 << 12, 16, 0)
+    hp = [0.05, 1.0, 0.01, 0.1, 0.02, 1.0, 0.5, 0.01]
+    g = torch.Generator().manual_seed(5)
+    keys = torch.unique(torch.randint(0, 1 << 40, (3000,), generator=g)).to(DEV)
+
+    def step():
+        s = gs.find(keys, True)
+        gs.difacto_push_cnt(s, torch.randint(1, 4, (keys.numel(),), generator=g).float().to(DEV),
+                            hp, 3, False, 7)
+        hd, vc, _ = gs.difacto_pull(s, False)
+        gs.difacto_push(s, hd, torch.randn(keys.numel(), generator=g).to(DEV),
+                        torch.randn(vc.shape[0], vc.shape[1], generator=g).to(DEV), hp, 3, False, 7)
+
+    for _ in range(3):
+        step()
+    checkpoint.save_difacto(gs, str(tmp_path / "sync"))
+    saver = checkpoint.AsyncSaver()
+    saver.save("difacto", gs, str(tmp_path / "async"))
+    for _ in range(3):
+        step()  # mutates the live table while the snapshot is written
+    saver.join()
+    a = (tmp_path / "sync").read_bytes()
+    assert len(a) > 0 and a == (tmp_path / "async").read_bytes()

@@ -27,25 +27,13 @@ def model_name(base, it, shard):
 
 
 def _occupied(store):
-    slots = store.occupied().long()
-    return slots
-
-
-def _arr(t, slots):
-    return t[slots.to(t.device)].cpu().numpy() if t.numel() else np.zeros(0)
+    # table order (the device compaction is unordered): identical model
+    # files for identical tables
+    return store.occupied().long().sort().values
 
 
 def save_linear(store, path):
-    slots = _occupied(store)
-    keys = _arr(store.keys, slots).astype(np.uint64)
-    w = _arr(store.w, slots).astype(np.float32)
-    m = w != 0
-    rec = np.empty(int(m.sum()), dtype=[("k", "<u8"), ("w", "<f4")])
-    rec["k"] = keys[m]
-    rec["w"] = w[m]
-    with open_uri(path, "wb") as f:
-        f.write(rec.tobytes())
-    return len(rec)
+    return _write("linear", _numpy(_gather(store, "linear")), 0, path)
 
 
 def load_linear(store, path):
@@ -71,29 +59,126 @@ def _recv(dim):
 def save_difacto(store, path):
     """Vectorised dump: all scalar (size 1) records, then all embedding
     records -- a valid record stream in the reference layout."""
+    return _write("difacto", _numpy(_gather(store, "difacto")), int(store.dim), path)
+
+
+def _gather(store, kind):
+    """Snapshot of the occupied entries as tensors on the store's device
+    (gathers only: the live table can be updated as soon as they ran)."""
     slots = _occupied(store)
-    keys = _arr(store.keys, slots).astype(np.uint64)
-    w = _arr(store.w, slots).astype(np.float32)
-    z = _arr(store.z, slots).astype(np.float32)
-    sq = _arr(store.sq, slots).astype(np.float32)
-    dim = int(store.dim)
-    has_v = np.zeros(len(keys), dtype=bool)
-    if dim > 0 and len(keys):
-        has_v = _arr(store.vrow, slots).astype(np.int64) >= 0
+
+    def g(t):
+        return t[slots.to(t.device)] if t.numel() else t.new_zeros(0)
+
+    snap = {"keys": g(store.keys), "w": g(store.w)}
+    if kind == "difacto":
+        snap["z"], snap["sq"] = g(store.z), g(store.sq)
+        dim = int(store.dim)
+        if dim > 0 and slots.numel():
+            vrow = g(store.vrow).long()
+            has_v = vrow >= 0
+            rows = vrow[has_v]
+            snap["has_v"] = has_v
+            snap["V"] = store.V[rows.to(store.V.device)][:, :dim]
+            snap["VG"] = store.VG[rows.to(store.VG.device)][:, :dim]
+    return snap
+
+
+def _numpy(snap):
+    return {k: v.cpu().numpy() for k, v in snap.items()}
+
+
+def _write(kind, snap, dim, path):
+    keys = snap["keys"].astype(np.uint64)
+    w = snap["w"].astype(np.float32)
+    if kind == "linear":
+        m = w != 0
+        rec = np.empty(int(m.sum()), dtype=[("k", "<u8"), ("w", "<f4")])
+        rec["k"] = keys[m]
+        rec["w"] = w[m]
+        with open_uri(path, "wb") as f:
+            f.write(rec.tobytes())
+        return len(rec)
+    z = snap["z"].astype(np.float32)
+    sq = snap["sq"].astype(np.float32)
+    has_v = snap.get("has_v")
+    if has_v is None:
+        has_v = np.zeros(len(keys), dtype=bool)
     one = ~has_v & (w != 0)  # Empty(): w0 == 0 && size == 1
     r1 = np.zeros(int(one.sum()), dtype=_rec1())
     r1["k"], r1["size"], r1["w"], r1["sq"], r1["z"] = keys[one], 1, w[one], sq[one], z[one]
     rv = np.zeros(int(has_v.sum()), dtype=_recv(max(dim, 1)))
     if len(rv):
-        rows = torch.from_numpy(_arr(store.vrow, slots).astype(np.int64)[has_v])
         rv["k"], rv["size"], rv["w"] = keys[has_v], dim + 1, w[has_v]
         rv["sq"], rv["z"] = sq[has_v], z[has_v]
-        rv["V"] = store.V[rows.to(store.V.device)].cpu().numpy()[:, :dim]
-        rv["VG"] = store.VG[rows.to(store.VG.device)].cpu().numpy()[:, :dim]
+        rv["V"], rv["VG"] = snap["V"], snap["VG"]
     with open_uri(path, "wb") as f:
         f.write(r1.tobytes())
         f.write(rv.tobytes())
     return len(r1) + len(rv)
+
+
+class AsyncSaver:
+    """Model-shard saves that do not stall training.
+
+    The occupied entries are gathered on a side stream (the compute stream
+    waits only for these gathers, so later updates cannot leak into the
+    snapshot), copied device -> pinned host memory asynchronously, and a
+    background thread writes the shard file once the copy's event fired.
+    ``join()`` waits for every pending write and re-raises its error; the
+    worker joins before acknowledging a final save, a load, or exit.
+    Host (CPU) stores save synchronously."""
+
+    def __init__(self):
+        self._pending = []
+        self._stream = None
+
+    def save(self, kind, store, path):
+        dev = store.keys.device
+        if dev.type != "cuda":
+            return _write(kind, _numpy(_gather(store, kind)), int(getattr(store, "dim", 0)), path)
+        import threading
+        main = torch.cuda.current_stream(dev)
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=dev)
+        side = self._stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            snap = _gather(store, kind)
+            gathered = torch.cuda.Event()
+            gathered.record(side)
+            host = {}
+            for k, v in snap.items():
+                h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+                h.copy_(v, non_blocking=True)
+                host[k] = h
+            copied = torch.cuda.Event()
+            copied.record(side)
+        main.wait_event(gathered)
+        dim = int(getattr(store, "dim", 0))
+        box = {}
+
+        def finish():
+            try:
+                copied.synchronize()
+                box["n"] = _write(kind, {k: v.numpy() for k, v in host.items()}, dim, path)
+            except BaseException as e:  # surfaced by join()
+                box["err"] = e
+
+        t = threading.Thread(target=finish, name="wh-save", daemon=True)
+        t.start()
+        self._pending.append((t, box, snap))
+        return None
+
+    def join(self):
+        pending, self._pending = self._pending, []
+        n = 0
+        for t, box, _ in pending:
+            t.join()
+            if "err" in box:
+                raise box["err"]
+            n += box.get("n", 0)
+        return n
 
 
 def _parse_difacto(data, dim):

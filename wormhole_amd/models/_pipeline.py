@@ -1,0 +1,79 @@
+"""Minibatch localize pipeline shared by the PS learners (difacto, linear).
+
+Localize minibatch i (finishing the job begun during minibatch i-1 when it
+was told about i), then begin i+1, so the one host read of the unique-id
+counts overlaps i's kernels (the reference overlaps the same stages with
+threads: learn/solver/minibatch_solver.h:284-315 keeps max_concurrency
+minibatches in flight).
+
+``next_batch`` is ``(keys, offset, val)`` of the NEXT call, optionally with a
+fourth item: a ``torch.cuda.Event`` recorded on the stream that produced the
+tensors (a data generator or H2D copy stream). The compute stream waits on it
+only right before the next minibatch's localize begins, so the producer runs
+concurrently with minibatch i's localize finish. Every rank must pass
+``next_batch`` in lockstep (the count exchange is a collective).
+"""
+import os
+
+import torch
+
+from .. import ops
+
+
+def localize_pipelined(lrn, keys, offset, val, next_batch):
+    job, lrn._job = lrn._job, None
+    if job is not None and job[0] is keys:
+        loc = ops.localize_finish(job[1])
+    else:
+        k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
+        loc = ops.localize(k, offset, val, lrn.kv.nshard, lrn.uhint,
+                           exchange=lrn.kv.count_exchange())
+    if next_batch is not None:
+        nk, no, nv = next_batch[:3]
+        ready = next_batch[3] if len(next_batch) > 3 else None
+        if nk.is_cuda and _OVERLAP:
+            # The next minibatch's hash insert + owner grouping run on their
+            # own stream, concurrently with this minibatch's pull / forward /
+            # backward on the compute stream. The side stream first waits for
+            # everything queued on the compute stream so far (this
+            # minibatch's localize finish, which empties the table slot the
+            # job reuses); the job's finish host-syncs its event before any
+            # compute-stream kernel reads its buffers.
+            cur = torch.cuda.current_stream(nk.device)
+            side = _loc_stream(nk.device)
+            side.wait_stream(cur)
+            if ready is not None:
+                side.wait_event(ready)
+            for t in (nk, no, nv):
+                if t is not None:
+                    t.record_stream(side)
+                    t.record_stream(cur)
+            with torch.cuda.stream(side):
+                k = ops.key_mod(nk, lrn.max_key) if lrn.max_key else nk
+                job = ops.localize_begin(k, no, nv, lrn.kv.nshard, loc[0].numel(),
+                                         exchange=lrn.kv.count_exchange())
+            lrn._job = (nk, job)
+            return loc
+        if ready is not None and nk.is_cuda:
+            cur = torch.cuda.current_stream(nk.device)
+            cur.wait_event(ready)
+            for t in (nk, no, nv):  # produced on another stream, consumed here
+                if t is not None:
+                    t.record_stream(cur)
+        k = ops.key_mod(nk, lrn.max_key) if lrn.max_key else nk
+        lrn._job = (nk, ops.localize_begin(k, no, nv, lrn.kv.nshard, loc[0].numel(),
+                                           exchange=lrn.kv.count_exchange()))
+    return loc
+
+
+# measured slower on one MI355X (106 vs 112 M ex/s: the concurrent hash
+# insert costs the gather-bound FM kernels more than it hides): opt-in only
+_OVERLAP = os.environ.get("WH_LOCALIZE_STREAM", "0") != "0"
+_streams = {}
+
+
+def _loc_stream(dev):
+    s = _streams.get(dev)
+    if s is None:
+        s = _streams[dev] = torch.cuda.Stream(device=dev)
+    return s

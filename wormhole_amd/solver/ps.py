@@ -78,6 +78,7 @@ class Worker:
         self.n_done = 0
         self.metrics = trace.MetricsStream(comm.rank)
         self.fault = _parse_fault(os.environ.get("WH_FAULT", ""), comm.rank)
+        self.saver = checkpoint.AsyncSaver()
 
     def send(self, **kw):
         self.van.send("scheduler", _msg(**kw))
@@ -98,17 +99,23 @@ class Worker:
             d = self.recv()
             cmd = d.get("cmd")
             if cmd == "exit":
+                self.saver.join()
                 return
             if cmd in ("save", "load"):
                 self.learner.flush()
             if cmd == "save":
                 if self.comm.rank < self.nshard:
                     name = checkpoint.model_name(d["file"], d["iter"], self.comm.rank)
-                    fn = checkpoint.save_linear if self.kind == "linear" else checkpoint.save_difacto
-                    fn(self.learner.store, name)
+                    # periodic saves (save_iter) write in the background while
+                    # the next pass trains; the final save completes before
+                    # its ack
+                    self.saver.save(self.kind, self.learner.store, name)
+                    if d["iter"] < 0:
+                        self.saver.join()
                 self.comm.barrier()
                 self.send(msg="ack")
             elif cmd == "load":
+                self.saver.join()
                 if self.comm.rank < self.nshard:
                     name = checkpoint.model_name(d["file"], d["iter"], self.comm.rank)
                     fn = checkpoint.load_linear if self.kind == "linear" else checkpoint.load_difacto
