@@ -40,24 +40,36 @@ def main():
             acc[label] += time.perf_counter() - t
             return r
         setattr(mod, name, g)
-    for n in ["localize", "fm_forward", "fm_backward", "fm_grad_post", "auc_acc"]:
+    for n in ["localize", "localize_begin", "localize_finish", "fm_forward", "fm_backward",
+              "fm_grad_post", "auc_acc"]:
         wrap(ops, n, "ops." + n)
     emb = Embedding(dim=64, threshold=100, lambda_l2=1.0, lr_eta=0.01)
     emb._set = {"dim", "threshold", "lambda_l2", "lr_eta"}
     conf = DifactoConfig(minibatch=args.batch, lr_eta=0.01, embedding=[emb])
     lr = DifactoLearner(conf, Comm(dev, init=False), dev, cap=1 << 27, vcap=1 << 24, seed=1)
-    for n in ["open", "difacto_push_cnt", "difacto_pull", "difacto_push"]:
+    for n in ["open", "difacto_open_pull", "difacto_push_cnt", "difacto_pull", "difacto_push"]:
         wrap(lr.kv, n, "kv." + n)
     card = torch.tensor(CRITEO_TB_CARD, dtype=torch.int64, device=dev)
-    for s in range(10):
-        k, l, o = hip.synth_criteo(args.batch, 1, s, card)
-        lr.process(k, o, None, l, 0, 0)
+
+    def synth(s):
+        t = time.perf_counter()
+        r = hip.synth_criteo(args.batch, 1, s, card)
+        acc["synth"] += time.perf_counter() - t
+        return r
+
+    def run(first, n):  # pipelined like bench.py (next minibatch's localize begun early)
+        nxt = synth(first)
+        for s in range(first, first + n):
+            k, l, o = nxt
+            nxt = synth(s + 1) if s + 1 < first + n else None
+            lr.process(k, o, None, l, 0, 0,
+                       next_batch=(nxt[0], nxt[2], None) if nxt is not None else None)
+    run(0, 10)
+    lr.flush()
     torch.cuda.synchronize()
     acc.clear()
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        k, l, o = hip.synth_criteo(args.batch, 1, 10 + s, card)
-        lr.process(k, o, None, l, 0, 0)
+    run(10, args.steps)
     t_host = time.perf_counter() - t0
     torch.cuda.synchronize()
     t_all = time.perf_counter() - t0
