@@ -539,31 +539,48 @@ __global__ __launch_bounds__(kThreads) void k_vchunk_hist(const int64_t* __restr
   for (int i = threadIdx.x; i < kBuckets; i += kThreads) hist[blockIdx.x * kBuckets + i] = h[i];
 }
 
-// one block, thread per bucket: hist[block][bucket] -> bucket-major exclusive
-// offsets in place (reads coalesced across the bucket threads)
-__global__ __launch_bounds__(kBuckets) void k_vchunk_scan(int32_t* hist, int nblk) {
-  __shared__ int32_t tot[kBuckets];
-  const int b = threadIdx.x;
+// one block of 1024: hist[block][bucket] -> bucket-major exclusive offsets in
+// place. Four threads per bucket each own a quarter of the blocks, so every
+// load is independent (the serial per-bucket walk took ~15-20 us of load
+// latency); the 256 bucket totals are scanned by the first four waves.
+constexpr int kScanParts = 4;
+constexpr int kScanPer = kBucketBlocks / kScanParts;
+
+__global__ __launch_bounds__(kBuckets * kScanParts) void k_vchunk_scan(int32_t* hist) {
+  __shared__ int32_t part[kScanParts][kBuckets];
+  __shared__ int32_t excl[kBuckets];
+  __shared__ int32_t wtot[kBuckets / 64];
+  const int b = threadIdx.x & (kBuckets - 1), q = threadIdx.x / kBuckets;
+  int32_t v[kScanPer];
+#pragma unroll
+  for (int i = 0; i < kScanPer; ++i) v[i] = hist[(q * kScanPer + i) * kBuckets + b];
   int32_t sum = 0;
-#pragma unroll 8
-  for (int i = 0; i < nblk; ++i) sum += hist[i * kBuckets + b];
-  tot[b] = sum;
+#pragma unroll
+  for (int i = 0; i < kScanPer; ++i) sum += v[i];
+  part[q][b] = sum;
   __syncthreads();
-  if (b == 0) {
-    int32_t run = 0;
-    for (int i = 0; i < kBuckets; ++i) {
-      const int32_t t = tot[i];
-      tot[i] = run;
-      run += t;
+  if (q == 0) {  // bucket totals -> wave-local inclusive scans
+    int32_t t = 0;
+#pragma unroll
+    for (int r = 0; r < kScanParts; ++r) t += part[r][b];
+    const int lane = b & 63;
+    int32_t x = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
     }
+    if (lane == 63) wtot[b >> 6] = x;
+    excl[b] = x - t;
   }
   __syncthreads();
-  int32_t run = tot[b];
-#pragma unroll 8
-  for (int i = 0; i < nblk; ++i) {
-    const int32_t t = hist[i * kBuckets + b];
-    hist[i * kBuckets + b] = run;
-    run += t;
+  int32_t base = excl[b];
+  for (int w = 0; w < (b >> 6); ++w) base += wtot[w];
+  for (int r = 0; r < q; ++r) base += part[r][b];
+#pragma unroll
+  for (int i = 0; i < kScanPer; ++i) {
+    hist[(q * kScanPer + i) * kBuckets + b] = base;
+    base += v[i];
   }
 }
 
@@ -886,7 +903,7 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
   const int shift = bucket_shift(std::max<int64_t>(nrows, 1));
   hipLaunchKernelGGL(k_vchunk_hist, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
                      meta_v, csc_row, shift, bucket_hist);
-  hipLaunchKernelGGL(k_vchunk_scan, dim3(1), dim3(kBuckets), 0, s, bucket_hist, kBucketBlocks);
+  hipLaunchKernelGGL(k_vchunk_scan, dim3(1), dim3(kBuckets * kScanParts), 0, s, bucket_hist);
   hipLaunchKernelGGL(k_vchunk_scatter, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
                      meta_v, csc_row, shift, bucket_hist, meta_sorted);
   const int G = vstride / 4;
