@@ -248,6 +248,12 @@ __global__ __launch_bounds__(kThreads) void k_assign(uint64_t* __restrict__ tkey
 
 // one wave per CSR row: the row id and the local id of each of its non-zeros
 // (lid[j] = tlid[slot_of[j]]), plus the position payload for valued data
+// A block owns kRowsPerBlk consecutive rows, i.e. one contiguous nnz range:
+// every lane works (a wave per row left 25 of 64 lanes idle on 39-field rows)
+// and each nnz finds its row by a binary search over the block's offsets in
+// LDS; four slot -> local-id gathers per thread are in flight at once.
+constexpr int kRowsPerBlk = 64;
+
 __global__ __launch_bounds__(kThreads) void k_rows_lid(const int64_t* __restrict__ off,
                                                        int64_t nrows,
                                                        const int32_t* __restrict__ slot_of,
@@ -255,13 +261,40 @@ __global__ __launch_bounds__(kThreads) void k_rows_lid(const int64_t* __restrict
                                                        int32_t* __restrict__ row_of,
                                                        int32_t* __restrict__ lid,
                                                        int32_t* __restrict__ pos) {
-  const int64_t row = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (row >= nrows) return;
-  for (int64_t j = off[row] + lane; j < off[row + 1]; j += 64) {
-    row_of[j] = (int32_t)row;
-    lid[j] = tlid[slot_of[j]];
-    if (pos) pos[j] = (int32_t)j;
+  __shared__ int64_t so[kRowsPerBlk + 1];
+  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlk;
+  const int nr = (int)(nrows - r0 < kRowsPerBlk ? nrows - r0 : kRowsPerBlk);
+  if (threadIdx.x <= nr) so[threadIdx.x] = off[r0 + threadIdx.x];
+  __syncthreads();
+  const int64_t j0 = so[0], j1 = so[nr];
+  auto row_at = [&](int64_t j) {  // largest k < nr with so[k] <= j
+    int lo = 0, hi = nr - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (so[mid] <= j) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
+  for (int64_t b = j0; b < j1; b += 4 * kThreads) {
+    int sl[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = b + u * kThreads + threadIdx.x;
+      sl[u] = j < j1 ? slot_of[j] : 0;
+    }
+    int li[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) li[u] = tlid[sl[u]];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t j = b + u * kThreads + threadIdx.x;
+      if (j < j1) {
+        row_of[j] = (int32_t)(r0 + row_at(j));
+        lid[j] = li[u];
+        if (pos) pos[j] = (int32_t)j;
+      }
+    }
   }
 }
 
@@ -335,8 +368,8 @@ void loc_rows_lid(const int64_t* offset, int64_t nrows, const int32_t* slot_of,
                   const int32_t* tlid, int32_t* row_of, int32_t* lid, int32_t* pos,
                   hipStream_t s) {
   if (nrows <= 0) return;
-  const int64_t threads = nrows * 64;
-  hipLaunchKernelGGL(k_rows_lid, dim3((unsigned)((threads + kThreads - 1) / kThreads)),
+  static_assert(kRowsPerBlk < kThreads, "offset staging needs a thread per row");
+  hipLaunchKernelGGL(k_rows_lid, dim3((unsigned)((nrows + kRowsPerBlk - 1) / kRowsPerBlk)),
                      dim3(kThreads), 0, s, offset, nrows, slot_of, tlid, row_of, lid, pos);
 }
 
