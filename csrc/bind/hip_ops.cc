@@ -783,6 +783,26 @@ void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& 
                 cur_stream(B));
 }
 
+Tensor gbdt_split(const Tensor& hist, const Tensor& totals, const Tensor& valid, double alpha,
+                  double lambda, double min_child_weight) {
+  CHECK_IN(hist, torch::kFloat64);
+  CHECK_IN(totals, torch::kFloat64);
+  CHECK_IN(valid, torch::kBool);
+  c10::DeviceGuard g(hist.device());
+  TORCH_CHECK(hist.dim() == 4 && hist.size(3) == 2, "hist must be [S, F, nbin, 2]");
+  const int S = (int)hist.size(0), F = (int)hist.size(1), nbin = (int)hist.size(2);
+  TORCH_CHECK(totals.numel() == 2 * (int64_t)S, "totals must be [S, 2]");
+  TORCH_CHECK(valid.numel() == (int64_t)F * nbin, "valid must be [F, nbin]");
+  auto out = torch::empty({S, 6}, hist.options());
+  auto cand = torch::empty({std::max<int64_t>((int64_t)S * F * 4, 1)}, hist.options());
+  TORCH_CHECK(wh::gbdt_split(ptr<double>(hist), ptr<double>(totals),
+                             reinterpret_cast<const uint8_t*>(valid.data_ptr()), S, F, nbin,
+                             alpha, lambda, min_child_weight, ptr<double>(cand), ptr<double>(out),
+                             cur_stream(hist)),
+              "gbdt_split: nbin > 1024 or empty input");
+  return out;
+}
+
 Tensor gbdt_seg_fill(const Tensor& beg, const Tensor& node, int64_t n) {
   CHECK_IN(beg, torch::kInt32);
   CHECK_IN(node, torch::kInt32);
@@ -962,6 +982,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gbdt_hist", &gbdt_hist);
   m.def("gbdt_partition", &gbdt_partition);
   m.def("gbdt_seg_fill", &gbdt_seg_fill);
+  m.def("gbdt_split", &gbdt_split);
   m.def("gbdt_leaf_add", &gbdt_leaf_add);
   m.def("gbdt_predict", &gbdt_predict);
   m.def("kmeans_pack_x", &kmeans_pack_x);

@@ -332,3 +332,196 @@ void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const f
 }
 
 }  // namespace wh
+
+// ---- split search -----------------------------------------------------
+// One block per (node, feature): inclusive scan of the feature's (g, h) bins
+// in double, both default directions for the rows missing the feature, the
+// regularised gain of every threshold, and the block's best candidate; then
+// one wave per node picks the best feature. Ties resolve to the smallest
+// flat index ((f * nbin + b) * 2 + dir), like a row-major argmax.
+namespace {
+
+constexpr int kSplitThreads = 256;
+constexpr int kSplitMaxPer = 4;  // bins per thread (nbin <= 1024)
+
+struct SplitParam {
+  double alpha, lambda, mcw;
+};
+
+__device__ __forceinline__ double split_gain(double G, double H, const SplitParam& p) {
+  if (H < p.mcw) return 0.0;
+  double g = G;
+  if (p.alpha != 0.0) g = G > p.alpha ? G - p.alpha : (G < -p.alpha ? G + p.alpha : 0.0);
+  return g * g / (H + p.lambda);
+}
+
+__device__ __forceinline__ double shfl_up_d(double v, int o) {
+  return __shfl_up(v, o, 64);
+}
+
+__device__ __forceinline__ bool better(double g, long long i, double bg, long long bi) {
+  return g > bg || (g == bg && i < bi);
+}
+
+__global__ __launch_bounds__(kSplitThreads) void k_split_feat(
+    const double* __restrict__ hist, const double* __restrict__ totals,
+    const uint8_t* __restrict__ valid, int F, int nbin, SplitParam p, double* __restrict__ cand) {
+  const int s = blockIdx.x / F, f = blockIdx.x % F;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const double* hb = hist + ((int64_t)s * F + f) * nbin * 2;
+  const int per = (nbin + kSplitThreads - 1) / kSplitThreads;
+  double lg[kSplitMaxPer], lh[kSplitMaxPer];
+  double sg = 0.0, sh = 0.0;
+#pragma unroll
+  for (int u = 0; u < kSplitMaxPer; ++u) {
+    const int b = t * per + u;
+    const bool ok = u < per && b < nbin;
+    sg += ok ? hb[2 * b] : 0.0;
+    sh += ok ? hb[2 * b + 1] : 0.0;
+    lg[u] = sg;
+    lh[u] = sh;
+  }
+  // exclusive prefix of the thread totals: wave scans + wave totals in LDS
+  __shared__ double wg[kSplitThreads / 64], wh[kSplitThreads / 64];
+  double xg = sg, xh = sh;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double yg = shfl_up_d(xg, o), yh = shfl_up_d(xh, o);
+    if (lane >= o) {
+      xg += yg;
+      xh += yh;
+    }
+  }
+  if (lane == 63) {
+    wg[w] = xg;
+    wh[w] = xh;
+  }
+  __syncthreads();
+  double og = xg - sg, oh = xh - sh, pg = 0.0, ph = 0.0;
+  for (int i = 0; i < kSplitThreads / 64; ++i) {
+    if (i < w) {
+      og += wg[i];
+      oh += wh[i];
+    }
+    pg += wg[i];
+    ph += wh[i];
+  }
+  const double TG = totals[2 * s], TH = totals[2 * s + 1];
+  const double mg = TG - pg, mh = TH - ph;  // rows missing this feature
+  const double parent = split_gain(TG, TH, p);
+  double best = -INFINITY;
+  long long bidx = 0x7fffffffffffffffll;
+  double bgl = 0.0, bhl = 0.0;
+#pragma unroll
+  for (int u = 0; u < kSplitMaxPer; ++u) {
+    const int b = t * per + u;
+    if (u >= per || b >= nbin) break;
+    if (!valid[(int64_t)f * nbin + b]) continue;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const double GL = og + lg[u] + (d ? mg : 0.0), HL = oh + lh[u] + (d ? mh : 0.0);
+      const double GR = TG - GL, HR = TH - HL;
+      if (!(HL >= p.mcw && HR >= p.mcw)) continue;
+      const double g = split_gain(GL, HL, p) + split_gain(GR, HR, p) - parent;
+      const long long idx = ((long long)f * nbin + b) * 2 + d;
+      if (better(g, idx, best, bidx)) {
+        best = g;
+        bidx = idx;
+        bgl = GL;
+        bhl = HL;
+      }
+    }
+  }
+  // block argmax (gain desc, index asc)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double g2 = __shfl_xor(best, o, 64);
+    const long long i2 = __shfl_xor(bidx, o, 64);
+    const double l2 = __shfl_xor(bgl, o, 64), h2 = __shfl_xor(bhl, o, 64);
+    if (better(g2, i2, best, bidx)) {
+      best = g2;
+      bidx = i2;
+      bgl = l2;
+      bhl = h2;
+    }
+  }
+  __shared__ double rg[kSplitThreads / 64], rl[kSplitThreads / 64], rh[kSplitThreads / 64];
+  __shared__ long long ri[kSplitThreads / 64];
+  if (lane == 0) {
+    rg[w] = best;
+    ri[w] = bidx;
+    rl[w] = bgl;
+    rh[w] = bhl;
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int i = 1; i < kSplitThreads / 64; ++i)
+      if (better(rg[i], ri[i], best, bidx)) {
+        best = rg[i];
+        bidx = ri[i];
+        bgl = rl[i];
+        bhl = rh[i];
+      }
+    double* c = cand + ((int64_t)s * F + f) * 4;
+    c[0] = best;
+    c[1] = (double)bidx;
+    c[2] = bgl;
+    c[3] = bhl;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_split_node(const double* __restrict__ cand, int F,
+                                                   int nbin, double* __restrict__ out) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  double best = -INFINITY, bgl = 0.0, bhl = 0.0;
+  long long bidx = 0x7fffffffffffffffll;
+  for (int f = lane; f < F; f += 64) {
+    const double* c = cand + ((int64_t)s * F + f) * 4;
+    const long long i = c[0] == -INFINITY ? (long long)f * nbin * 2 : (long long)c[1];
+    if (better(c[0], i, best, bidx)) {
+      best = c[0];
+      bidx = i;
+      bgl = c[2];
+      bhl = c[3];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double g2 = __shfl_xor(best, o, 64);
+    const long long i2 = __shfl_xor(bidx, o, 64);
+    const double l2 = __shfl_xor(bgl, o, 64), h2 = __shfl_xor(bhl, o, 64);
+    if (better(g2, i2, best, bidx)) {
+      best = g2;
+      bidx = i2;
+      bgl = l2;
+      bhl = h2;
+    }
+  }
+  if (lane == 0) {
+    if (best == -INFINITY) bidx = 0;  // all candidates invalid: argmax of -inf is index 0
+    double* o = out + (int64_t)s * 6;
+    o[0] = best;
+    o[1] = (double)(bidx / 2 / nbin);
+    o[2] = (double)((bidx / 2) % nbin);
+    o[3] = (double)(bidx % 2);
+    o[4] = bgl;
+    o[5] = bhl;
+  }
+}
+
+}  // namespace
+
+namespace wh {
+
+bool gbdt_split(const double* hist, const double* totals, const uint8_t* valid, int S, int F,
+                int nbin, double alpha, double lambda, double mcw, double* cand, double* out,
+                hipStream_t s) {
+  if (nbin > kSplitThreads * kSplitMaxPer || S <= 0 || F <= 0) return false;
+  const SplitParam p{alpha, lambda, mcw};
+  hipLaunchKernelGGL(k_split_feat, dim3((unsigned)(S * F)), dim3(kSplitThreads), 0, s, hist,
+                     totals, valid, F, nbin, p, cand);
+  hipLaunchKernelGGL(k_split_node, dim3((unsigned)S), dim3(64), 0, s, cand, F, nbin, out);
+  return true;
+}
+
+}  // namespace wh

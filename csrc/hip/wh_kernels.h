@@ -266,6 +266,12 @@ void gbdt_scatter(const int32_t* ridx, int64_t n, const int32_t* pos_node, const
                   const int64_t* lscan, int32_t* out, hipStream_t s);
 void gbdt_leaf_add(const int32_t* ridx, int64_t n, const int32_t* pos_node, const float* leaf,
                    float* margin, hipStream_t s);
+// best split per node over hist [S, F, nbin, 2] (double) and totals [S, 2]:
+// out [S, 6] = (gain, feature, bin, default_left, G_left, H_left); cand is
+// [S * F * 4] double scratch. false when nbin > 1024.
+bool gbdt_split(const double* hist, const double* totals, const uint8_t* valid, int S, int F,
+                int nbin, double alpha, double lambda, double mcw, double* cand, double* out,
+                hipStream_t s);
 void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const float* thr,
                   const int32_t* left, const int32_t* right, const uint8_t* defl,
                   const float* leaf, float* margin, hipStream_t s);

@@ -514,3 +514,37 @@ def test_async_saver_snapshot(hip, tmp_path):
     saver.join()
     a = (tmp_path / "sync").read_bytes()
     assert len(a) > 0 and a == (tmp_path / "async").read_bytes()
+
+
+@pytest.mark.parametrize("S,F,nbin,alpha,mcw", [(5, 7, 33, 0.0, 1.0), (3, 28, 256, 0.5, 0.1),
+                                                (2, 4, 1000, 0.0, 5.0)])
+def test_gbdt_split_kernel(hip, S, F, nbin, alpha, mcw):
+    """Fused split search vs the torch reference (_find_splits_ref): same
+    feature / bin / direction, gains and left sums to fp64 rounding; a node
+    with no valid candidate reports -inf."""
+    from wormhole_amd.models import gbdt as G
+    g = torch.Generator().manual_seed(S * F + nbin)
+    hist = torch.zeros(S, F, nbin, 2, dtype=torch.float64)
+    hist[..., 0] = torch.randn(S, F, nbin, generator=g, dtype=torch.float64)
+    hist[..., 1] = torch.rand(S, F, nbin, generator=g, dtype=torch.float64) * 2
+    present = hist.sum(2)  # [S, F, 2]
+    totals = present.max(1).values + torch.rand(S, 2, generator=g, dtype=torch.float64)
+    totals[:, 0] = present[:, :, 0].mean(1)  # rows missing a feature move the totals
+    valid = torch.rand(F, nbin, generator=g) < 0.8
+    valid[0] = False
+    tb = G.TreeBuilder.__new__(G.TreeBuilder)
+    tb.p = G.GBDTParam()
+    tb.p.alpha, tb.p.min_child_weight = alpha, mcw
+    tb.nbin, tb.valid_mask, tb._valid_dev = nbin, valid, None
+    ref = tb._find_splits_ref(hist, totals)
+    if S > 2:
+        hist[2].zero_()  # no candidate passes min_child_weight on either side
+        totals[2] = 0.0
+        ref = tb._find_splits_ref(hist, totals)
+    got = tb._find_splits(hist.to(DEV), totals.to(DEV))
+    ok = torch.isfinite(ref[0])
+    assert torch.equal(torch.isfinite(got[0]), ok)
+    assert torch.allclose(got[0][ok], ref[0][ok], rtol=1e-9, atol=1e-9)
+    for k in (1, 2, 3):
+        assert torch.equal(got[k][ok], ref[k][ok])
+    assert torch.allclose(got[4][ok], ref[4][ok], rtol=1e-9, atol=1e-9)
