@@ -85,6 +85,16 @@ class GBDTParam:
         return -g / (H + self.reg_lambda)
 
 
+def _h2d(t, dev):
+    """Host -> device without a synchronous pageable copy: the per-level
+    tables (segments, split descriptions, hist tasks) go through pinned
+    memory, asynchronously on the current stream."""
+    dev = torch.device(dev)
+    if dev.type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def _threshold_l1(G, alpha):
     if alpha == 0:
         return G
@@ -458,7 +468,7 @@ class TreeBuilder:
             if tasks:
                 both = torch.tensor(tasks, dtype=torch.int32).reshape(-1)
                 both = torch.cat([both, torch.tensor(red, dtype=torch.int32).reshape(-1)])
-                both = both.to(self.device)
+                both = _h2d(both, self.device)
                 t = both[:5 * len(tasks)].view(-1, 5)
                 rd = both[5 * len(tasks):].view(-1, 6)
                 _native.hip().gbdt_hist(self.B, self.nbin, ridx, gpair, self._qscale, t, rd,
@@ -567,7 +577,7 @@ class TreeBuilder:
                 break
             S = len(frontier)
             H_all = H_front
-            T_all = torch.stack([totals[nd] for nd in frontier]).to(H_all.device)
+            T_all = _h2d(torch.stack([totals[nd] for nd in frontier]), H_all.device)
             bg, bf, bb, bd, bL = self._find_splits(H_all, T_all)
             split_nodes = []
             for k, nd in enumerate(frontier):
@@ -624,12 +634,12 @@ class TreeBuilder:
             # sibling subtraction for every split node at once; the new
             # frontier is [l, r] per split node, in split order
             fpos = {nd: i for i, nd in enumerate(frontier)}
-            par = torch.tensor([fpos[nd] for nd in split_nodes], dtype=torch.int64,
-                               device=H_front.device)
+            par = _h2d(torch.tensor([fpos[nd] for nd in split_nodes], dtype=torch.int64),
+                       H_front.device)
             hbig = H_front.index_select(0, par) - hsmall
-            small_is_left = torch.tensor([small[k] == tree.left[nd]
-                                          for k, nd in enumerate(split_nodes)],
-                                         device=H_front.device)
+            small_is_left = _h2d(torch.tensor([small[k] == tree.left[nd]
+                                               for k, nd in enumerate(split_nodes)]),
+                                 H_front.device)
             hl = torch.where(small_is_left[:, None, None, None], hsmall, hbig)
             hr = torch.where(small_is_left[:, None, None, None], hbig, hsmall)
             H_front = torch.stack([hl, hr], 1).reshape(-1, *H_front.shape[1:])
@@ -658,7 +668,7 @@ class TreeBuilder:
             for ln in lens:
                 begs.append(acc)
                 acc += ln
-            seg = torch.tensor([begs, ids], dtype=torch.int32).to(dev)
+            seg = _h2d(torch.tensor([begs, ids], dtype=torch.int32), dev)
             return _native.hip().gbdt_seg_fill(seg[0].contiguous(), seg[1].contiguous(), n)
         return torch.repeat_interleave(torch.tensor(ids, dtype=torch.int32, device=dev),
                                        torch.tensor(lens, dtype=torch.int64, device=dev),
@@ -668,8 +678,8 @@ class TreeBuilder:
         dev = self.device
         if self.gpu:
             nleft = torch.zeros(node_feat.numel(), dtype=torch.int32, device=dev)
-            pk = torch.stack([node_feat, node_bin, node_defl.to(torch.int32), seg_beg,
-                              seg_end]).to(dev)  # one host->device copy
+            pk = _h2d(torch.stack([node_feat, node_bin, node_defl.to(torch.int32), seg_beg,
+                                   seg_end]), dev)  # one host->device copy
             out = _native.hip().gbdt_partition(self.B, ridx, pos_node, pk[0], pk[1],
                                                pk[2].to(torch.uint8), pk[3], pk[4], nleft)
             return out, nleft.cpu()
