@@ -817,17 +817,25 @@ Tensor gbdt_seg_fill(const Tensor& beg, const Tensor& node, int64_t n) {
 // partition the positions of the split nodes; returns the new ridx
 Tensor gbdt_partition(const Tensor& B, const Tensor& ridx, const Tensor& pos_node,
                       const Tensor& node_feat, const Tensor& node_bin, const Tensor& node_defl,
-                      const Tensor& seg_beg, const Tensor& seg_end, Tensor nleft_out) {
+                      const Tensor& seg_beg, const Tensor& seg_end, Tensor nleft_out,
+                      const c10::optional<Tensor>& Bc) {
   CHECK_IN(B, torch::kUInt8);
+  const uint8_t* bc = nullptr;
+  if (Bc.has_value() && Bc->defined()) {
+    CHECK_IN((*Bc), torch::kUInt8);
+    TORCH_CHECK(Bc->dim() == 2 && Bc->size(0) == B.size(1) && Bc->size(1) == B.size(0),
+                "Bc must be B transposed ([f, nrows])");
+    bc = ptr<uint8_t>(*Bc);
+  }
   CHECK_IN(ridx, torch::kInt32);
   CHECK_IN(pos_node, torch::kInt32);
   c10::DeviceGuard g(B.device());
   auto s = cur_stream(B);
   const int64_t n = ridx.numel();
   auto left = torch::empty({n}, ridx.options());
-  wh::gbdt_goleft(ptr<uint8_t>(B), (int)B.size(1), ptr<int32_t>(ridx), n, ptr<int32_t>(pos_node),
-                  ptr<int32_t>(node_feat), ptr<int32_t>(node_bin), ptr<uint8_t>(node_defl),
-                  ptr<int32_t>(left), s);
+  wh::gbdt_goleft(ptr<uint8_t>(B), bc, B.size(0), (int)B.size(1), ptr<int32_t>(ridx), n,
+                  ptr<int32_t>(pos_node), ptr<int32_t>(node_feat), ptr<int32_t>(node_bin),
+                  ptr<uint8_t>(node_defl), ptr<int32_t>(left), s);
   auto lscan = torch::empty({n + 1}, ridx.options().dtype(torch::kInt64));
   auto tmp = torch::empty({wh::scan_tmp_elems(n)}, lscan.options());
   wh::scan_i32(ptr<int32_t>(left), ptr<int64_t>(lscan), n, ptr<int64_t>(tmp), s);
@@ -980,7 +988,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("spmv", &spmv, py::arg("offset"), py::arg("col"), py::arg("val"), py::arg("x"));
   m.def("gbdt_bin", &gbdt_bin);
   m.def("gbdt_hist", &gbdt_hist);
-  m.def("gbdt_partition", &gbdt_partition);
+  m.def("gbdt_partition", &gbdt_partition, py::arg("B"), py::arg("ridx"), py::arg("pos_node"),
+        py::arg("node_feat"), py::arg("node_bin"), py::arg("node_defl"), py::arg("seg_beg"),
+        py::arg("seg_end"), py::arg("nleft"), py::arg("Bc") = py::none());
   m.def("gbdt_seg_fill", &gbdt_seg_fill);
   m.def("gbdt_split", &gbdt_split);
   m.def("gbdt_leaf_add", &gbdt_leaf_add);

@@ -194,7 +194,11 @@ __global__ __launch_bounds__(256) void k_seg_fill(const int32_t* __restrict__ be
   out[i] = node[lo];
 }
 
-__global__ void k_goleft(const uint8_t* __restrict__ B, int f, const int32_t* __restrict__ ridx,
+// Bc (optional): the bin matrix feature-major [f][nrows]. Rows of a segment
+// are ascending, so one feature's bytes of consecutive rows share cache lines
+// (row-major, each row's byte costs a line of its own on deep levels).
+__global__ void k_goleft(const uint8_t* __restrict__ B, const uint8_t* __restrict__ Bc,
+                         int64_t nrows, int f, const int32_t* __restrict__ ridx,
                          int64_t nrows_seg, const int32_t* __restrict__ pos_node,
                          const int32_t* __restrict__ node_feat, const int32_t* __restrict__ node_bin,
                          const uint8_t* __restrict__ node_defl, int32_t* __restrict__ left) {
@@ -204,7 +208,7 @@ __global__ void k_goleft(const uint8_t* __restrict__ B, int f, const int32_t* __
   int l = 0;
   const int feat = nd >= 0 ? node_feat[nd] : -1;
   if (feat >= 0) {
-    const int b = B[(int64_t)ridx[i] * f + feat];
+    const int b = Bc ? Bc[(int64_t)feat * nrows + ridx[i]] : B[(int64_t)ridx[i] * f + feat];
     l = (b == kMissing) ? (int)node_defl[nd] : (b <= node_bin[nd] ? 1 : 0);
   }
   left[i] = l;
@@ -300,12 +304,12 @@ void gbdt_seg_fill(const int32_t* beg, const int32_t* node, int nseg, int64_t n,
   hipLaunchKernelGGL(k_seg_fill, dim3(grid_for(n, 256)), dim3(256), 0, s, beg, node, nseg, n, out);
 }
 
-void gbdt_goleft(const uint8_t* B, int f, const int32_t* ridx, int64_t n, const int32_t* pos_node,
-                 const int32_t* node_feat, const int32_t* node_bin, const uint8_t* node_defl,
-                 int32_t* left, hipStream_t s) {
+void gbdt_goleft(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f, const int32_t* ridx,
+                 int64_t n, const int32_t* pos_node, const int32_t* node_feat,
+                 const int32_t* node_bin, const uint8_t* node_defl, int32_t* left, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_goleft, dim3(grid_for(n, 256)), dim3(256), 0, s, B, f, ridx, n, pos_node,
-                     node_feat, node_bin, node_defl, left);
+  hipLaunchKernelGGL(k_goleft, dim3(grid_for(n, 256)), dim3(256), 0, s, B, Bc, nrows, f, ridx, n,
+                     pos_node, node_feat, node_bin, node_defl, left);
 }
 
 void gbdt_scatter(const int32_t* ridx, int64_t n, const int32_t* pos_node, const int32_t* node_feat,

@@ -258,9 +258,10 @@ void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const flo
 // position -> node id over sorted segments tiling [0, n)
 void gbdt_seg_fill(const int32_t* beg, const int32_t* node, int nseg, int64_t n, int32_t* out,
                    hipStream_t s);
-void gbdt_goleft(const uint8_t* B, int f, const int32_t* ridx, int64_t n, const int32_t* pos_node,
-                 const int32_t* node_feat, const int32_t* node_bin, const uint8_t* node_defl,
-                 int32_t* left, hipStream_t s);
+// Bc: optional feature-major copy of B ([f][nrows]) for the per-row gather
+void gbdt_goleft(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f, const int32_t* ridx,
+                 int64_t n, const int32_t* pos_node, const int32_t* node_feat,
+                 const int32_t* node_bin, const uint8_t* node_defl, int32_t* left, hipStream_t s);
 void gbdt_scatter(const int32_t* ridx, int64_t n, const int32_t* pos_node, const int32_t* node_feat,
                   const int32_t* seg_beg, const int32_t* nleft, const int32_t* left,
                   const int64_t* lscan, int32_t* out, hipStream_t s);

@@ -421,6 +421,7 @@ class TreeBuilder:
         self.valid_mask = self.bin_mask.clone()
         self._nglobal = None
         self._valid_dev = None
+        self._Bc = None
 
     def _hist_scale(self, gpair):
         """Fixed-point scales {2^eg, 2^eh} of the GPU histograms: the largest
@@ -680,8 +681,11 @@ class TreeBuilder:
             nleft = torch.zeros(node_feat.numel(), dtype=torch.int32, device=dev)
             pk = _h2d(torch.stack([node_feat, node_bin, node_defl.to(torch.int32), seg_beg,
                                    seg_end]), dev)  # one host->device copy
+            if self._Bc is None:  # feature-major copy for the partition gathers
+                self._Bc = self.B.t().contiguous()
             out = _native.hip().gbdt_partition(self.B, ridx, pos_node, pk[0], pk[1],
-                                               pk[2].to(torch.uint8), pk[3], pk[4], nleft)
+                                               pk[2].to(torch.uint8), pk[3], pk[4], nleft,
+                                               self._Bc)
             return out, nleft.cpu()
         out = ridx.clone()
         nleft = torch.zeros(node_feat.numel(), dtype=torch.int32)
