@@ -265,6 +265,16 @@ void gbdt_goleft(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f, cons
 void gbdt_scatter(const int32_t* ridx, int64_t n, const int32_t* pos_node, const int32_t* node_feat,
                   const int32_t* seg_beg, const int32_t* nleft, const int32_t* left,
                   const int64_t* lscan, int32_t* out, hipStream_t s);
+// partition flags + exclusive scan in one look-back pass: lscan int32 [n + 1]
+// (false when n needs more than kLbMaxTiles tiles: use goleft + scan_i32)
+bool gbdt_partition_fused(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f,
+                          const int32_t* ridx, int64_t n, const int32_t* pos_node,
+                          const int32_t* node_feat, const int32_t* node_bin,
+                          const uint8_t* node_defl, const Lookback& lb, int32_t* lscan,
+                          hipStream_t s);
+void gbdt_scatter32(const int32_t* ridx, int64_t n, const int32_t* pos_node,
+                    const int32_t* node_feat, const int32_t* seg_beg, const int32_t* nleft,
+                    const int32_t* lscan, int32_t* out, hipStream_t s);
 void gbdt_leaf_add(const int32_t* ridx, int64_t n, const int32_t* pos_node, const float* leaf,
                    float* margin, hipStream_t s);
 // best split per node over hist [S, F, nbin, 2] (double) and totals [S, 2]:
