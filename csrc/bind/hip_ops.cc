@@ -783,6 +783,54 @@ void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& 
                 cur_stream(B));
 }
 
+// ------------------------------------------------------------------ lbfgs
+Tensor owlqn_dir(const Tensor& g, const Tensor& w, double l1) {
+  CHECK_IN(g, torch::kFloat32);
+  CHECK_IN(w, torch::kFloat32);
+  TORCH_CHECK(g.numel() == w.numel());
+  c10::DeviceGuard dg(g.device());
+  auto d = torch::empty_like(g);
+  wh::owlqn_dir(ptr<float>(g), ptr<float>(w), g.numel(), (float)l1, ptr<float>(d), cur_stream(g));
+  return d;
+}
+
+Tensor owlqn_fix_dot(const Tensor& d, const Tensor& steep, bool fix) {
+  CHECK_IN(d, torch::kFloat32);
+  CHECK_IN(steep, torch::kFloat32);
+  TORCH_CHECK(d.numel() == steep.numel());
+  c10::DeviceGuard dg(d.device());
+  auto v = torch::zeros({1}, d.options().dtype(torch::kFloat64));
+  wh::owlqn_fix_dot(ptr<float>(d), ptr<float>(steep), d.numel(), fix ? 1 : 0, ptr<double>(v),
+                    cur_stream(d));
+  return v;
+}
+
+std::vector<Tensor> owlqn_step(const Tensor& w, const Tensor& d, double alpha, bool fix) {
+  CHECK_IN(w, torch::kFloat32);
+  CHECK_IN(d, torch::kFloat32);
+  TORCH_CHECK(w.numel() == d.numel());
+  c10::DeviceGuard dg(w.device());
+  auto nw = torch::empty_like(w);
+  auto l1 = torch::zeros({1}, w.options().dtype(torch::kFloat64));
+  wh::owlqn_step(ptr<float>(w), ptr<float>(d), w.numel(), (float)alpha, fix ? 1 : 0,
+                 ptr<float>(nw), ptr<double>(l1), cur_stream(w));
+  return {nw, l1};
+}
+
+Tensor multi_dot(const Tensor& H, const Tensor& ia, const Tensor& ib) {
+  CHECK_IN(H, torch::kFloat32);
+  CHECK_IN(ia, torch::kInt32);
+  CHECK_IN(ib, torch::kInt32);
+  TORCH_CHECK(H.dim() == 2 && ia.numel() == ib.numel());
+  c10::DeviceGuard dg(H.device());
+  const int R = (int)H.size(0), np = (int)ia.numel();
+  auto out = torch::zeros({np}, H.options().dtype(torch::kFloat64));
+  TORCH_CHECK(wh::multi_dot(ptr<float>(H), R, H.size(1), ptr<int32_t>(ia), ptr<int32_t>(ib), np,
+                            ptr<double>(out), cur_stream(H)),
+              "multi_dot: at most 64 rows and 64 pairs");
+  return out;
+}
+
 Tensor gbdt_split(const Tensor& hist, const Tensor& totals, const Tensor& valid, double alpha,
                   double lambda, double min_child_weight) {
   CHECK_IN(hist, torch::kFloat64);
@@ -1017,6 +1065,10 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("seg_end"), py::arg("nleft"), py::arg("Bc") = py::none());
   m.def("gbdt_seg_fill", &gbdt_seg_fill);
   m.def("gbdt_split", &gbdt_split);
+  m.def("owlqn_dir", &owlqn_dir);
+  m.def("owlqn_fix_dot", &owlqn_fix_dot);
+  m.def("owlqn_step", &owlqn_step);
+  m.def("multi_dot", &multi_dot);
   m.def("gbdt_leaf_add", &gbdt_leaf_add);
   m.def("gbdt_predict", &gbdt_predict);
   m.def("kmeans_pack_x", &kmeans_pack_x);

@@ -246,6 +246,17 @@ int64_t kmeans_accum_scratch(int64_t n, int k);
 bool kmeans_accum_sorted(const float* X, int64_t n, int f, int k, const int32_t* assign,
                          float* sums, void* scratch, hipStream_t s);
 
+// -------------------------------------------------------------- lbfgs.hip
+void owlqn_dir(const float* g, const float* w, int64_t n, float l1, float* d, hipStream_t s);
+// vdot (fp64, accumulated) += sum d * steep after the optional sign fix
+void owlqn_fix_dot(float* d, const float* steep, int64_t n, int fix, double* vdot, hipStream_t s);
+// nw = fix(w + alpha d); l1sum (fp64, accumulated) += |nw|_1
+void owlqn_step(const float* w, const float* d, int64_t n, float alpha, int fix, float* nw,
+                double* l1sum, hipStream_t s);
+// out[p] (fp64, accumulated) += <H[ia[p]], H[ib[p]]>; false if R > 64 or np > 64
+bool multi_dot(const float* H, int R, int64_t n, const int32_t* ia, const int32_t* ib, int np,
+               double* out, hipStream_t s);
+
 // -------------------------------------------------------------- gbdt.hip
 void gbdt_bin(const float* X, int64_t n, int f, const float* cuts, const int32_t* cut_off,
               uint8_t* B, hipStream_t s);

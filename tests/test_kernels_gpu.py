@@ -548,3 +548,36 @@ def test_gbdt_split_kernel(hip, S, F, nbin, alpha, mcw):
     for k in (1, 2, 3):
         assert torch.equal(got[k][ok], ref[k][ok])
     assert torch.allclose(got[4][ok], ref[4][ok], rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("l1", [0.0, 0.3])
+def test_owlqn_kernels(hip, l1):
+    """OWL-QN direction / sign fix + dot / fused step + |w|_1 and the batched
+    history dots against the solver's torch forms (fp32 data, fp64 sums)."""
+    from wormhole_amd.solver.lbfgs import LBFGSSolver
+    g = torch.Generator().manual_seed(11)
+    n = 100_003
+    grad = torch.randn(n, generator=g)
+    w = torch.randn(n, generator=g)
+    w[torch.rand(n, generator=g) < 0.3] = 0.0
+    sv = LBFGSSolver.__new__(LBFGSSolver)
+    sv.reg_L1 = l1
+    ref_d = sv.set_l1_dir(grad, w)
+    d = hip.owlqn_dir(grad.to(DEV), w.to(DEV), l1)
+    assert torch.equal(d.cpu(), ref_d)
+    steep = torch.randn(n, generator=g)
+    ref_fixed = sv.fix_dir_l1_sign(ref_d.clone(), steep)
+    ref_v = float((ref_fixed.double() * steep.double()).sum())
+    v = hip.owlqn_fix_dot(d, steep.to(DEV), l1 != 0.0)
+    assert torch.equal(d.cpu(), ref_fixed)
+    assert abs(float(v) - ref_v) <= 1e-9 * max(1.0, abs(ref_v))
+    nw, s1 = hip.owlqn_step(w.to(DEV), d, 0.37, l1 != 0.0)
+    ref_nw = sv.fix_weight_l1_sign(w + ref_fixed * 0.37, w)
+    assert torch.allclose(nw.cpu(), ref_nw, rtol=1e-6, atol=1e-6)
+    assert abs(float(s1) - float(nw.cpu().double().abs().sum())) <= 1e-6 * float(s1)
+    H = torch.randn(21, 5000, generator=g)
+    ia = torch.tensor([0, 3, 20, 5, 7], dtype=torch.int32)
+    ib = torch.tensor([20, 3, 20, 9, 1], dtype=torch.int32)
+    dots = hip.multi_dot(H.to(DEV), ia.to(DEV), ib.to(DEV)).cpu()
+    ref = (H[ia.long()].double() * H[ib.long()].double()).sum(1)
+    assert torch.allclose(dots, ref, rtol=1e-10, atol=1e-9)

@@ -16,6 +16,8 @@ import math
 
 import torch
 
+from .. import _native
+
 
 class LBFGSSolver:
     def __init__(self, bsp, obj):
@@ -126,10 +128,13 @@ class LBFGSSolver:
         return g, loc
 
     # ---------------------------------------------------------- iteration
-    def eval(self, w):
+    def eval(self, w, l1norm=None):
+        """l1norm: |w|_1 when the caller already has it (the fused step)."""
         val = self.bsp.allreduce_scalar(float(self.obj.eval(w)))
         if self.reg_L1 != 0.0:
-            val += float(w.abs().sum(dtype=torch.float64)) * self.reg_L1
+            if l1norm is None:
+                l1norm = float(w.abs().sum(dtype=torch.float64))
+            val += l1norm * self.reg_L1
         return val
 
     def update_one_iter(self):
@@ -168,6 +173,8 @@ class LBFGSSolver:
     # ------------------------------------------------------------ OWL-QN
     def set_l1_dir(self, grad, weight):
         l1 = self.reg_L1
+        if grad.is_cuda:  # csrc/hip/lbfgs.hip k_owlqn_dir
+            return _native.hip().owlqn_dir(grad.contiguous(), weight.contiguous(), float(l1))
         if l1 == 0.0:
             return -grad
         d = torch.where(weight > 0, -grad - l1, torch.where(weight < 0, -grad + l1, torch.zeros_like(grad)))
@@ -203,7 +210,10 @@ class LBFGSSolver:
             ia = torch.tensor([self._map(a) for a, _ in idx], device=self.device)
             ib = torch.tensor([self._map(b) for _, b in idx], device=self.device)
             # all new partial dots in ONE batched reduction, then one allreduce
-            tmp = (self.hist[ia] * self.hist[ib]).sum(1, dtype=torch.float64)
+            if self.hist.is_cuda:  # one pass over the history (k_multi_dot)
+                tmp = _native.hip().multi_dot(self.hist, ia.int(), ib.int())
+            else:
+                tmp = (self.hist[ia] * self.hist[ib]).sum(1, dtype=torch.float64)
             self.bsp.allreduce(tmp)
             tmp = tmp.cpu()
             for k, (a, b) in enumerate(idx):
@@ -228,8 +238,13 @@ class LBFGSSolver:
                 coef[self._map(k)] = delta[k]
             dirsub = coef.to(self.device) @ self.hist  # skinny GEMV over the shard
             steep = self.H(2 * m)
-            dirsub = self.fix_dir_l1_sign(dirsub, steep)
-            vdot = -float((dirsub * steep).sum(dtype=torch.float64))
+            if dirsub.is_cuda:  # sign fix + dot in one pass (k_owlqn_fix_dot)
+                dirsub = dirsub.contiguous()
+                vdot = -float(_native.hip().owlqn_fix_dot(dirsub, steep.contiguous(),
+                                                          self.reg_L1 != 0.0))
+            else:
+                dirsub = self.fix_dir_l1_sign(dirsub, steep)
+                vdot = -float((dirsub * steep).sum(dtype=torch.float64))
             d = self._allgather_dir(dirsub)
             vdot = self.bsp.allreduce_scalar(vdot)
         else:
@@ -267,8 +282,13 @@ class LBFGSSolver:
             it += 1
             if it >= self.max_linesearch_iter:
                 return new_w, it
-            new_w = self.fix_weight_l1_sign(w + d * alpha, w)
-            new_val = self.eval(new_w)
+            if w.is_cuda:  # step + sign fix + |w|_1 in one pass (k_owlqn_step)
+                new_w, l1 = _native.hip().owlqn_step(w.contiguous(), d.contiguous(), alpha,
+                                                     self.reg_L1 != 0.0)
+                new_val = self.eval(new_w, float(l1) if self.reg_L1 != 0.0 else None)
+            else:
+                new_w = self.fix_weight_l1_sign(w + d * alpha, w)
+                new_val = self.eval(new_w)
             if new_val - old_val <= c1 * vdot * alpha:
                 self.new_objval = new_val
                 break
