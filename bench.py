@@ -39,7 +39,7 @@ def build(args, comm, device):
         emb = Embedding(dim=args.dim, threshold=100, lambda_l2=1.0, lr_eta=0.01)
         emb._set = {"dim", "threshold", "lambda_l2", "lr_eta"}
         conf = DifactoConfig(minibatch=args.batch, lr_eta=0.01, embedding=[emb],
-                             fixed_bytes=args.fixed_bytes)
+                             fixed_bytes=args.fixed_bytes, max_concurrency=args.max_concurrency)
         return DifactoLearner(conf, comm, device, cap=args.cap, vcap=args.vcap, seed=1)
     from wormhole_amd.models.linear import LinearLearner
     conf = LinearConfig(minibatch=args.batch, lambda_l1=4.0, lr_eta=0.1)
@@ -61,7 +61,20 @@ def main():
                          "(lossy; the reference default 0 is used for the headline)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: gloo rehearsal of the distributed path (tiny batches only)")
+    ap.add_argument("--prewarm", type=int, default=None,
+                    help="untimed training steps run before --warmup to bring the model "
+                         "to a fixed warm state (embedding rows allocated by the count "
+                         "threshold grow with the steps seen; default 1000 for difacto)")
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="P > 1: run the multi-shard exchange path with P virtual shards "
+                         "in this one process (identity transport; measures that path's "
+                         "device + host overhead on one GPU)")
+    ap.add_argument("--max-concurrency", type=int, default=2,
+                    help="minibatches in flight per worker (reference default 2): with >= 2 "
+                         "the multi-shard step is pipelined one minibatch deep")
     args = ap.parse_args()
+    if args.prewarm is None:
+        args.prewarm = 1000 if args.model == "difacto" else 0
 
     local = env_local_rank()
     if os.environ.get("WH_BENCH_SAME_GPU") == "1":
@@ -72,8 +85,12 @@ def main():
     else:
         device = torch.device("cpu")
         args.cap, args.vcap = min(args.cap, 1 << 16), min(args.vcap, 1 << 14)
-    comm = Comm(device)
-    n = comm.size
+    if args.loopback > 1:
+        from wormhole_amd.parallel.comm import LoopbackComm
+        comm = LoopbackComm(args.loopback, device)
+    else:
+        comm = Comm(device)
+    n = 1 if args.loopback > 1 else comm.size  # GPUs doing work
     learner = build(args, comm, device)
     seed = 1000 + comm.rank
     if device.type == "cuda":
@@ -121,6 +138,13 @@ def main():
         if device.type == "cuda":
             torch.cuda.synchronize()
 
+    # fixed warm state: the same number of untimed steps whatever --warmup is
+    # (seeded apart from the timed steps' data)
+    if args.prewarm > 0:
+        seed0 = seed
+        seed = 7000000 + comm.rank
+        run(0, args.prewarm)
+        seed = seed0
     run(0, args.warmup)
     learner.flush()
     sync()
@@ -137,6 +161,9 @@ def main():
     comm.allreduce(t, "max")
     dt = float(t.item())
     prog = learner.take_progress()
+    guard = learner.kv.guard
+    guard.after_open()
+    guard.read()  # raises on any dropped key or embedding row
     sizes = getattr(learner, "last_sizes", None)
     if sizes is not None:  # last minibatch: unique keys and embedding rows per GPU
         sizes = [int(sizes[0]), int(sizes[1].reshape(-1)[0].item()) if torch.is_tensor(sizes[1]) else int(sizes[1])]
@@ -161,11 +188,17 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": vs, "dtype": "fp32",
             "data": "synthetic (Criteo-1TB-shaped: 13 int + 26 cat fields, power-law, device-generated each step); random-init model",
             "config": {"model": model, "global_batch": args.batch * n, "seq_len": 39,
-                       "parallelism": "dp%d+kvshard%d" % (n, n),
+                       "parallelism": ("loopback%d(1 GPU)" % args.loopback if args.loopback > 1
+                                       else "dp%d+kvshard%d" % (n, n)),
                        "minibatch_per_gpu": args.batch, "threshold": 100, "nnz_per_example": 39},
             "train_logloss": logloss, "train_auc": auc,
             "uniq_keys_per_gpu_step": sizes[0] if sizes else None,
             "emb_rows_per_gpu_step": sizes[1] if sizes else None,
+            "prewarm_steps": args.prewarm,
+            "table_keys_per_gpu": guard.keys, "table_load": guard.keys / learner.store.cap,
+            "table_grows": guard.grows, "vslab_rows_per_gpu": guard.vused,
+            "dropped_keys": 0, "max_concurrency": args.max_concurrency,
+            "loopback_shards": args.loopback if args.loopback > 1 else None,
         }), flush=True)
     comm.finalize()
 

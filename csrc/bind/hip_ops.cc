@@ -175,7 +175,7 @@ class LocalizeJob {
       const int64_t* h = host_.data_ptr<int64_t>();
       const bool own = h[nshard_] != 0;
       bool over = own;
-      for (int64_t q = 1; q < nrecv_; q += 2) over |= h[nshard_ + 1 + q] != 0;
+      for (int64_t q = 1; q < nrecv_; q += stride_) over |= h[nshard_ + 1 + q] != 0;
       if (!over) break;
       TORCH_CHECK(!(own && tsize_ >= safe_), "localize: table overflow");
       // every rank saw the same flags: all retry at the safe size together
@@ -190,8 +190,10 @@ class LocalizeJob {
       owner_cnt_h.data_ptr<int64_t>()[p] = h[p];
       U += h[p];
     }
-    Tensor recv_h = torch::empty({nrecv_}, torch::kInt64);
-    for (int64_t q = 0; q < nrecv_; ++q) recv_h.data_ptr<int64_t>()[q] = h[nshard_ + 1 + q];
+    // everything after the owner counts (the peers' values and any extra)
+    const int64_t ntail = dev_counts_.numel() - nshard_ - 1;
+    Tensor recv_h = torch::empty({nrecv_ ? ntail : 0}, torch::kInt64);
+    for (int64_t q = 0; q < recv_h.numel(); ++q) recv_h.data_ptr<int64_t>()[q] = h[nshard_ + 1 + q];
     const int64_t nnz = nnz_, nrows = offset_.numel() - 1;
     const float* vp = val_.defined() ? ptr<float>(val_) : nullptr;
     auto tlid = torch::empty({tsize_}, i32);
@@ -254,12 +256,33 @@ class LocalizeJob {
                         ptr<int64_t>(ws.loc_ovf[tab_]), s);
     Tensor both = owner_cnt;
     nrecv_ = 0;
+    hipStream_t cs = s;  // stream of the count read
     if (!exchange_.is_none()) {
-      Tensor recv = exchange_(owner_cnt).cast<Tensor>();
-      TORCH_CHECK(recv.scalar_type() == torch::kInt64 && recv.numel() % 2 == 0,
-                  "localize: exchange must return int64 [2 * world]");
-      nrecv_ = recv.numel();
-      both = torch::cat({owner_cnt, recv.reshape({-1}).to(owner_cnt.device())});
+      py::object r = exchange_(owner_cnt);
+      if (py::isinstance<py::tuple>(r)) {
+        // extended protocol (kv/psx.py): (payload, stream handle, stride,
+        // world). payload = [owner_cnt (nshard+1) | stride values per peer,
+        // {count, overflow flag, ...} | extra], already on that stream;
+        // the read goes on that stream so the compute stream never waits
+        // for the exchange.
+        auto t = r.cast<py::tuple>();
+        TORCH_CHECK(t.size() == 4, "localize: extended exchange returns 4 items");
+        both = t[0].cast<Tensor>();
+        cs = reinterpret_cast<hipStream_t>(t[1].cast<intptr_t>());
+        stride_ = t[2].cast<int64_t>();
+        const int64_t world = t[3].cast<int64_t>();
+        TORCH_CHECK(both.scalar_type() == torch::kInt64 && stride_ >= 2 &&
+                        both.numel() >= nshard_ + 1 + stride_ * world,
+                    "localize: bad extended exchange payload");
+        nrecv_ = stride_ * world;
+      } else {
+        Tensor recv = r.cast<Tensor>();
+        TORCH_CHECK(recv.scalar_type() == torch::kInt64 && recv.numel() % 2 == 0,
+                    "localize: exchange must return int64 [2 * world]");
+        stride_ = 2;
+        nrecv_ = recv.numel();
+        both = torch::cat({owner_cnt, recv.reshape({-1}).to(owner_cnt.device())});
+      }
     }
     dev_counts_ = both.contiguous();
     if (!host_.defined() || host_.numel() < dev_counts_.numel())
@@ -268,13 +291,13 @@ class LocalizeJob {
     // an async copy into pinned memory + an event: nothing blocks here
     WH_HIP_CHECK_HOST(hipMemcpyAsync(host_.data_ptr(), dev_counts_.data_ptr(),
                                      dev_counts_.numel() * sizeof(int64_t),
-                                     hipMemcpyDeviceToHost, s));
+                                     hipMemcpyDeviceToHost, cs));
     if (!event_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&event_, hipEventDisableTiming));
-    WH_HIP_CHECK_HOST(hipEventRecord(event_, s));
+    WH_HIP_CHECK_HOST(hipEventRecord(event_, cs));
   }
 
   Tensor keys_, offset_, val_;
-  int64_t nshard_, nnz_ = 0, safe_ = 0, tsize_ = 0, nrecv_ = 0;
+  int64_t nshard_, nnz_ = 0, safe_ = 0, tsize_ = 0, nrecv_ = 0, stride_ = 2;
   py::object exchange_;
   int tab_ = -1;
   bool done_ = false;
@@ -302,17 +325,10 @@ class KVStore {
     auto f32 = torch::TensorOptions().dtype(torch::kFloat32).device(dev);
     // AoS slot table [cap, 8] x 4 bytes = wh::KVSlot; the per-field tensors
     // below are strided views into it (shared storage, writable)
-    slots_ = torch::zeros({cap, 8}, f32.dtype(torch::kInt32));
-    auto as_i64 = slots_.view(torch::kInt64);   // [cap, 4]
-    auto as_f32 = slots_.view(torch::kFloat32); // [cap, 8]
-    keys_ = as_i64.select(1, 0);
-    keys_.fill_(-1);
-    w_ = as_f32.select(1, 2);
-    z_ = as_f32.select(1, 3);
-    sq_ = as_f32.select(1, 4);
-    cnt_ = slots_.select(1, 5);
-    vrow_ = slots_.select(1, 6);
-    vrow_.fill_(-1);
+    auto sl = torch::zeros({cap, 8}, f32.dtype(torch::kInt32));
+    sl.view(torch::kInt64).select(1, 0).fill_(-1);  // key: empty
+    sl.select(1, 6).fill_(-1);                      // vrow: none
+    set_slots(sl);
     if (dim > 0) {
       V_ = torch::zeros({std::max<int64_t>(vcap, 1), vstride_}, f32);
       VG_ = torch::zeros({std::max<int64_t>(vcap, 1), vstride_}, f32);
@@ -488,6 +504,122 @@ class KVStore {
                      cur_stream(slot));
   }
 
+  // ---------------------------------------------------- multi-shard (psx.hip)
+  // Owner side of a P-shard minibatch. keys: int64 [n] or int32 records
+  // [n, 3] {key lo, key hi, count}; segS / segHS: device int64 [P+1]; rows_cap:
+  // rows of the reply buffer to allocate (>= segHS[P] + n). Returns (slot,
+  // vpos [n+1], chain [n] (int32 view of the chain words), rbuf
+  // [rows_cap, vstride], vcnt [P]).
+  std::vector<Tensor> ps_open(const Tensor& keys, bool use_cnt, const Tensor& segS,
+                              const Tensor& segHS, int64_t rows_cap, bool insert, bool chains,
+                              int64_t epoch, const std::vector<double>& h, int64_t threshold,
+                              bool l1_shrk, int64_t seed) {
+    CHECK_DEV(keys); CHECK_CONT(keys);
+    CHECK_IN(segS, torch::kInt64);
+    CHECK_IN(segHS, torch::kInt64);
+    TORCH_CHECK(vstride_ > 0, "ps_open needs an embedding store");
+    const bool rec = keys.scalar_type() == torch::kInt32;
+    TORCH_CHECK(rec ? (keys.dim() == 2 && keys.size(1) == 3) : keys.scalar_type() == torch::kInt64,
+                "ps_open: keys must be int64 [n] or int32 records [n, 3]");
+    TORCH_CHECK(!use_cnt || rec, "ps_open: counts travel in the records");
+    const int64_t n = keys.size(0);
+    const int P = (int)segS.numel() - 1;
+    TORCH_CHECK(P >= 1 && segHS.numel() == P + 1, "ps_open: bad segment tables");
+    TORCH_CHECK(n < (1 << 24), "ps_open: at most 2^24 - 1 keys per minibatch and shard");
+    TORCH_CHECK(epoch >= 1 && epoch <= 255, "ps_open: epoch must be in 1..255");
+    TORCH_CHECK(rows_cap >= n, "ps_open: reply buffer too small");
+    c10::DeviceGuard g(keys.device());
+    auto s = cur_stream(keys);
+    auto i32 = keys.options().dtype(torch::kInt32);
+    auto f32 = keys.options().dtype(torch::kFloat32);
+    auto slot = torch::empty({std::max<int64_t>(n, 1)}, i32);
+    auto wout = torch::empty({std::max<int64_t>(n, 1)}, f32);
+    auto vpos = torch::empty({n + 1}, keys.options().dtype(torch::kInt64));
+    auto chain = torch::empty({std::max<int64_t>(n, 1)}, i32);
+    auto rbuf = torch::empty({rows_cap, (int64_t)vstride_}, f32);
+    auto vcnt = torch::empty({P}, keys.options().dtype(torch::kInt64));
+    auto vbase = vnext_.clone();
+    const bool ok = wh::ps_open(
+        table(), rec ? nullptr : reinterpret_cast<const uint64_t*>(keys.data_ptr()),
+        rec ? ptr<int32_t>(keys) : nullptr, n, use_cnt ? 1 : 0, dhp(h, threshold, l1_shrk, seed),
+        insert ? 1 : 0, chains ? 1 : 0, (uint32_t)epoch, ptr<int32_t>(vbase), ptr<int64_t>(segS),
+        ptr<int64_t>(segHS), P, lookback(keys.device()), ptr<int32_t>(slot), ptr<float>(wout),
+        ptr<int64_t>(vpos), reinterpret_cast<uint32_t*>(chain.data_ptr()), ptr<float>(rbuf),
+        ptr<int64_t>(vcnt), s);
+    TORCH_CHECK(ok, "ps_open: limits exceeded (P <= 1024, n < 2^24)");
+    return {slot.narrow(0, 0, n), vpos, chain.narrow(0, 0, n), rbuf, vcnt};
+  }
+
+  // Owner side push of a P-shard minibatch: gbuf = the received push buffer
+  // (rows in the reply layout of the matching ps_open).
+  void ps_push(const Tensor& slot, const Tensor& vpos, const c10::optional<Tensor>& chain,
+               const Tensor& segS, const Tensor& segHS, const Tensor& gbuf,
+               const std::vector<double>& h, int64_t threshold, bool l1_shrk, int64_t seed) {
+    CHECK_IN(slot, torch::kInt32);
+    CHECK_IN(vpos, torch::kInt64);
+    CHECK_IN(segS, torch::kInt64);
+    CHECK_IN(segHS, torch::kInt64);
+    CHECK_IN(gbuf, torch::kFloat32);
+    const int64_t n = slot.numel();
+    TORCH_CHECK(vpos.numel() == n + 1, "ps_push: vpos size mismatch");
+    const uint32_t* cp = nullptr;
+    if (chain.has_value() && chain->defined()) {
+      CHECK_IN((*chain), torch::kInt32);
+      TORCH_CHECK(chain->numel() == n, "ps_push: chain size mismatch");
+      cp = reinterpret_cast<const uint32_t*>(chain->data_ptr());
+    }
+    const int P = (int)segS.numel() - 1;
+    c10::DeviceGuard g(slot.device());
+    TORCH_CHECK(wh::ps_push(table(), ptr<int32_t>(slot), ptr<int64_t>(vpos), cp, n,
+                            ptr<int64_t>(segS), ptr<int64_t>(segHS), P, ptr<float>(gbuf),
+                            dhp(h, threshold, l1_shrk, seed), cur_stream(slot)),
+                "ps_push: limits exceeded");
+  }
+
+  // ------------------------------------------------------- growth / health
+  // Re-hash into a table of newcap (power of two) slots; returns the old ->
+  // new slot map (int32 [old cap]) for the slot ids of in-flight sessions.
+  Tensor grow(int64_t newcap) {
+    TORCH_CHECK(newcap > cap_ && (newcap & (newcap - 1)) == 0,
+                "grow: new capacity must be a larger power of two");
+    c10::DeviceGuard g(slots_.device());
+    auto s = cur_stream(slots_);
+    auto ns = torch::zeros({newcap, 8}, slots_.options());
+    ns.view(torch::kInt64).select(1, 0).fill_(-1);
+    ns.select(1, 6).fill_(-1);
+    auto remap = torch::empty({cap_}, slots_.options());
+    wh::kv_rehash(reinterpret_cast<const wh::KVSlot*>(slots_.data_ptr()), cap_,
+                  reinterpret_cast<wh::KVSlot*>(ns.data_ptr()), newcap, ptr<int32_t>(remap),
+                  ptr<int64_t>(stats_), s);
+    set_slots(ns);
+    cap_ = newcap;
+    return remap;
+  }
+
+  // enlarge the V slab to newvcap rows (rows keep their ids)
+  void grow_v(int64_t newvcap) {
+    TORCH_CHECK(dim_ > 0 && newvcap > vcap_, "grow_v: new capacity must be larger");
+    c10::DeviceGuard g(slots_.device());
+    auto f32 = V_.options();
+    auto nv = torch::empty({newvcap, vstride_}, f32);
+    auto ng = torch::empty({newvcap, vstride_}, f32);
+    nv.narrow(0, 0, V_.size(0)).copy_(V_);
+    ng.narrow(0, 0, VG_.size(0)).copy_(VG_);
+    nv.narrow(0, V_.size(0), newvcap - V_.size(0)).zero_();
+    ng.narrow(0, VG_.size(0), newvcap - VG_.size(0)).zero_();
+    V_ = nv;
+    VG_ = ng;
+    vcap_ = newvcap;
+  }
+
+  // device int64 [4] {keys, failed inserts, V-slab overflows, V rows used}
+  Tensor summary() {
+    c10::DeviceGuard g(slots_.device());
+    auto out = torch::empty({4}, stats_.options());
+    wh::kv_summary(table(), ptr<int64_t>(out), cur_stream(slots_));
+    return out;
+  }
+
   int64_t dim() const { return dim_; }
   int64_t vstride() const { return vstride_; }
   int64_t cap() const { return cap_; }
@@ -496,6 +628,18 @@ class KVStore {
   Tensor slots_, keys_, w_, z_, sq_, cnt_, vrow_, V_, VG_, vnext_, stats_;
 
  private:
+  void set_slots(const Tensor& sl) {
+    slots_ = sl;
+    auto as_i64 = slots_.view(torch::kInt64);   // [cap, 4]
+    auto as_f32 = slots_.view(torch::kFloat32); // [cap, 8]
+    keys_ = as_i64.select(1, 0);
+    w_ = as_f32.select(1, 2);
+    z_ = as_f32.select(1, 3);
+    sq_ = as_f32.select(1, 4);
+    cnt_ = slots_.select(1, 5);
+    vrow_ = slots_.select(1, 6);
+  }
+
   int64_t cap_ = 0, vcap_ = 0, dim_ = 0;
   int vstride_ = 0;
 };
@@ -604,6 +748,46 @@ void fm_grad_post(const Tensor& gvc, const Tensor& m, int64_t dim, double clip, 
   if (normalize)
     wh::fm_grad_scale(ptr<int64_t>(m), gvc.size(0), ptr<float>(gvc), (int)vstride, (int)dim,
                       ptr<double>(sumsq), s);
+}
+
+// worker side of the multi-shard exchange (psx.hip). rbuf: the received pull
+// reply [R, vstride]; segS/segHS: int64 [P+1] over the keys sent per owner;
+// vrecv: int64 [P] V rows received per owner. Returns (hdr [U, 2], rows
+// int64 [1] = R actually used).
+std::vector<Tensor> ps_unpack(const Tensor& rbuf, int64_t U, const Tensor& segS,
+                              const Tensor& segHS, const Tensor& vrecv) {
+  CHECK_IN(rbuf, torch::kFloat32);
+  CHECK_IN(segS, torch::kInt64);
+  CHECK_IN(segHS, torch::kInt64);
+  CHECK_IN(vrecv, torch::kInt64);
+  TORCH_CHECK(rbuf.dim() == 2, "ps_unpack: rbuf must be [R, vstride]");
+  const int P = (int)segS.numel() - 1;
+  TORCH_CHECK(segHS.numel() == P + 1 && vrecv.numel() == P, "ps_unpack: bad segment tables");
+  c10::DeviceGuard g(rbuf.device());
+  auto hdr = torch::empty({U, 2}, rbuf.options());
+  auto rows = torch::empty({1}, segS.options());
+  TORCH_CHECK(wh::ps_unpack(ptr<float>(rbuf), U, (int)rbuf.size(1), ptr<int64_t>(segS),
+                            ptr<int64_t>(segHS), ptr<int64_t>(vrecv), P, ptr<float>(hdr),
+                            ptr<int64_t>(rows), cur_stream(rbuf)),
+              "ps_unpack: limits exceeded");
+  return {hdr, rows};
+}
+
+// gw [U] into the header rows of the push buffer gbuf [R, vstride] (in place)
+void ps_pack_gw(const Tensor& gw, const Tensor& gbuf, const Tensor& segS, const Tensor& segHS,
+                const Tensor& vrecv) {
+  CHECK_IN(gw, torch::kFloat32);
+  CHECK_IN(gbuf, torch::kFloat32);
+  CHECK_IN(segS, torch::kInt64);
+  CHECK_IN(segHS, torch::kInt64);
+  CHECK_IN(vrecv, torch::kInt64);
+  TORCH_CHECK(gbuf.dim() == 2, "ps_pack_gw: gbuf must be [R, vstride]");
+  const int P = (int)segS.numel() - 1;
+  c10::DeviceGuard g(gw.device());
+  TORCH_CHECK(wh::ps_pack_gw(ptr<float>(gw), gw.numel(), (int)gbuf.size(1), ptr<int64_t>(segS),
+                             ptr<int64_t>(segHS), ptr<int64_t>(vrecv), P, ptr<float>(gbuf),
+                             cur_stream(gw)),
+              "ps_pack_gw: limits exceeded");
 }
 
 // worker side of a multi-shard pull: renumber hdr vidx into local compact
@@ -1047,6 +1231,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("fm_backward", &fm_backward);
   m.def("fm_grad_post", &fm_grad_post);
   m.def("vidx_renumber", &vidx_renumber);
+  m.def("ps_unpack", &ps_unpack);
+  m.def("ps_pack_gw", &ps_pack_gw);
   m.def("auc", &auc);
   m.def("quant_rows", &quant_rows);
   m.def("key_mod", &key_mod);
@@ -1088,6 +1274,11 @@ PYBIND11_MODULE(_hip, m) {
       .def("difacto_pull", &KVStore::difacto_pull)
       .def("difacto_open_pull", &KVStore::difacto_open_pull)
       .def("difacto_push", &KVStore::difacto_push)
+      .def("ps_open", &KVStore::ps_open)
+      .def("ps_push", &KVStore::ps_push)
+      .def("grow", &KVStore::grow)
+      .def("grow_v", &KVStore::grow_v)
+      .def("summary", &KVStore::summary)
       .def_property_readonly("dim", &KVStore::dim)
       .def_property_readonly("vstride", &KVStore::vstride)
       .def_property_readonly("cap", &KVStore::cap)

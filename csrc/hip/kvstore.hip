@@ -13,22 +13,12 @@
 #include "wh_common.h"
 #include "wh_kernels.h"
 #include "wh_lookback.h"
+#include "kv_device.h"
 
 namespace wh {
 namespace {
 
-constexpr int kThreads = 256;
-
-__device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// counter `idx` of this wave's shard (see kStatShards)
-__device__ __forceinline__ unsigned long long* stat_ptr(int64_t* stats, int idx) {
-  const int shard =
-      (int)((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (kStatShards - 1));
-  return reinterpret_cast<unsigned long long*>(stats + shard * kStatStride + idx);
-}
+using namespace kvd;
 
 __global__ __launch_bounds__(kThreads) void k_kv_find(const uint64_t* keys_in, int64_t n,
                                                       KVSlot* tsl, int64_t cap, int insert,
@@ -38,20 +28,8 @@ __global__ __launch_bounds__(kThreads) void k_kv_find(const uint64_t* keys_in, i
   if (i < n) {
     const uint64_t k = keys_in[i];
     const uint64_t mask = (uint64_t)cap - 1;
-    uint64_t h = mix64(k) & mask;
-    int64_t res = -1;
-    for (int64_t probe = 0; probe < cap; ++probe) {
-      uint64_t prev = ld_relaxed(&tsl[h].key);
-      if (prev == k) { res = (int64_t)h; break; }
-      if (prev == kEmptyKey) {
-        if (!insert) break;
-        uint64_t old = atomicCAS((unsigned long long*)(&tsl[h].key),
-                                 (unsigned long long)kEmptyKey, (unsigned long long)k);
-        if (old == kEmptyKey) { res = (int64_t)h; created = true; break; }
-        if (old == k) { res = (int64_t)h; break; }
-      }
-      h = (h + 1) & mask;
-    }
+    const uint64_t h = mix64(k) & mask;
+    const int32_t res = probe_slot(tsl, mask, k, h, ld_relaxed(&tsl[h].key), insert, &created);
     if (insert && res < 0) failed = true;
     slot[i] = (int32_t)res;
   }
@@ -82,12 +60,6 @@ __device__ __forceinline__ float l1l2_solve(float z, float eta, float l1, float 
   // argmin_x 0.5*eta*(x - z/eta)^2 + l1|x| + l2 x^2 (soft threshold)
   if (z <= l1 && z >= -l1) return 0.f;
   return (z > 0 ? z - l1 : z + l1) / (eta + l2);
-}
-
-__device__ __forceinline__ void count_nnz_delta(float oldw, float neww, int64_t* stats) {
-  const int d = (oldw == 0.f && neww != 0.f) ? 1 : ((oldw != 0.f && neww == 0.f) ? -1 : 0);
-  long long s = wave_sum_ll(d);
-  if ((threadIdx.x & 63) == 0 && s) atomicAdd(stat_ptr(stats, 0), (unsigned long long)s);
 }
 
 __global__ __launch_bounds__(kThreads) void k_linear_pull(const KVSlot* tsl, const int32_t* slot,
@@ -140,42 +112,6 @@ __global__ __launch_bounds__(kThreads) void k_linear_push(KVTable t, const int32
 // Most keys of a power-law minibatch have no V, so lane-per-key keeps all 64
 // lanes busy on the scalar part instead of 1 of every G.
 
-// wave-aggregated bump allocation of V rows; returns the row or -1
-__device__ __forceinline__ int32_t wave_alloc_rows(const KVTable& t, bool want) {
-  const uint64_t m = __ballot(want);
-  if (!m) return -1;
-  const int lane = threadIdx.x & 63;
-  int32_t base = 0;
-  const int leader = __ffsll((unsigned long long)m) - 1;
-  if (lane == leader) base = atomicAdd(t.vnext, (int)__popcll(m));
-  base = __shfl(base, leader, 64);
-  if (!want) return -1;
-  const int32_t row = base + (int32_t)__popcll(m & ((1ull << lane) - 1));
-  if (row >= t.vcap) {
-    atomicAdd(stat_ptr(t.stats, 3), 1ull);
-    return -1;
-  }
-  return row;
-}
-
-__device__ __forceinline__ void init_v_row(const KVTable& t, int32_t s, int32_t row, int gl, int G,
-                                           const DifactoHP& hp) {
-  const uint64_t key = t.sl[s].key;
-  float* V = t.V + (int64_t)row * t.vstride;
-  float* VG = t.VG + (int64_t)row * t.vstride;
-  for (int c = gl * 4; c < t.vstride; c += 4 * G) {
-    float4 v;
-    float* pv = &v.x;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int d = c + e;
-      pv[e] = d < t.dim ? (uhash01(hp.seed, key, (uint64_t)d) * 2.f - 1.f) * hp.v_init : 0.f;
-    }
-    *reinterpret_cast<float4*>(V + c) = v;
-    *reinterpret_cast<float4*>(VG + c) = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const int32_t* slot,
                                                                const float* cnt,
@@ -201,7 +137,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push_cnt(KVTable t, const 
   for_each_row_job<G>(row >= 0, [&](int src, int gl) {
     const int sl = src >= 0 ? src : lane;
     const int32_t js = __shfl(s, sl, 64), jr = __shfl(row, sl, 64);
-    if (src >= 0) init_v_row(t, js, jr, gl, G, hp);
+    if (src >= 0) init_v_row(t, t.sl[js].key, jr, gl, G, hp);
   });
   newv = wave_sum_ll(newv);
   if (lane == 0 && newv) atomicAdd(stat_ptr(t.stats, 1), (unsigned long long)newv);
@@ -256,8 +192,6 @@ __global__ __launch_bounds__(kThreads) void k_difacto_pull_rows(KVTable t, const
 // A tile is 1024 consecutive keys, 4 per thread (vector loads of the slot
 // ids, 32-byte header stores), so a 515k-key minibatch is ~500 tiles and the
 // look-back finishes in ~2 windows.
-constexpr int kPullPer = 4;
-constexpr int kPullTile = kThreads * kPullPer;
 
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_difacto_pull(KVTable t, const int32_t* slot,
@@ -351,19 +285,9 @@ __global__ __launch_bounds__(kThreads) void k_difacto_open_pull(
   for (int r = 0; r < kPullPer; ++r) {
     sl[r] = -1;
     if (k[r] == kEmptyKey) continue;
-    uint64_t hh = h[r], pv = prev[r];
-    for (int64_t probe = 0; probe < t.cap; ++probe) {
-      if (pv == k[r]) { sl[r] = (int32_t)hh; break; }
-      if (pv == kEmptyKey) {
-        if (!insert) break;
-        const uint64_t old = atomicCAS((unsigned long long*)(&t.sl[hh].key),
-                                       (unsigned long long)kEmptyKey, (unsigned long long)k[r]);
-        if (old == kEmptyKey) { sl[r] = (int32_t)hh; ++created; break; }
-        if (old == k[r]) { sl[r] = (int32_t)hh; break; }
-      }
-      hh = (hh + 1) & mask;
-      pv = ld_relaxed(&t.sl[hh].key);
-    }
+    bool cr = false;
+    sl[r] = probe_slot(t.sl, mask, k[r], h[r], prev[r], insert, &cr);
+    created += cr ? 1 : 0;
     if (insert && sl[r] < 0) ++failed;
     if (i0 + r < n) slot_out[i0 + r] = sl[r];
   }
@@ -544,7 +468,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int3
     const int jk = __shfl(kind, sl, 64), jv = __shfl(gvid, sl, 64);
     if (src < 0) return;
     if (jk == 1) {
-      init_v_row(t, js, jr, gl, G, hp);
+      init_v_row(t, t.sl[js].key, jr, gl, G, hp);
       return;
     }
     // AdaGrad on V (reference UpdateV, learn/difacto/async_sgd.h:289-296)
@@ -589,12 +513,6 @@ __global__ __launch_bounds__(kThreads) void k_gather_rows(const float* in, const
   }
 }
 
-inline int lanes_per_key(int vstride) {
-  if (vstride <= 0) return 1;
-  int q = vstride / 4;
-  return q >= 64 ? 64 : q;
-}
-
 }  // namespace
 
 void kv_find(const KVTable& t, const uint64_t* keys, int64_t n, int insert, int32_t* slot,
@@ -621,17 +539,6 @@ void linear_push(const KVTable& t, const int32_t* slot, const float* grad, int64
   hipLaunchKernelGGL(k_linear_push, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t, slot,
                      grad, n, hp);
 }
-
-#define WH_DISPATCH_G(G, KERNEL, ...)                                            \
-  switch (G) {                                                                   \
-    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                   \
-    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                   \
-    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                   \
-    case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                   \
-    case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                 \
-    case 32: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                 \
-    default: hipLaunchKernelGGL(KERNEL<64>, __VA_ARGS__); break;                 \
-  }
 
 void difacto_push_cnt(const KVTable& t, const int32_t* slot, const float* cnt,
                       const int32_t* cnti, int64_t n, DifactoHP hp, hipStream_t s) {
@@ -723,6 +630,84 @@ bool difacto_open_pull(const KVTable& t, const uint64_t* keys, int64_t n, const 
   WH_DISPATCH_G(G, k_difacto_open_pull, grid, block, 0, s, t, keys, n, cnt, hp, insert, lb,
                 (int)ntiles, slot, reinterpret_cast<float2*>(hdr), vpos, vc);
   return true;
+}
+
+}  // namespace wh
+
+// ------------------------------------------------------------ growth / health
+namespace wh {
+namespace {
+
+using namespace kvd;
+
+// Re-insert every occupied slot of `old` into the (larger, empty) table
+// `nt`; remap[old slot] = new slot (or -1 for an empty old slot), so the
+// slot ids held by in-flight minibatch sessions can be translated. Slots are
+// copied whole (w, FTRL/AdaGrad state, count, V row, chain tag); the V slab
+// is untouched.
+__global__ __launch_bounds__(kThreads) void k_kv_rehash(const KVSlot* __restrict__ old,
+                                                        int64_t oldcap, KVSlot* nt, int64_t newcap,
+                                                        int32_t* remap, int64_t* stats) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  bool failed = false;
+  if (i < oldcap) {
+    const KVSlot e = old[i];
+    int32_t ns = -1;
+    if (e.key != kEmptyKey) {
+      const uint64_t mask = (uint64_t)newcap - 1;
+      const uint64_t h = mix64(e.key) & mask;
+      bool created = false;
+      ns = probe_slot(nt, mask, e.key, h, ld_relaxed(&nt[h].key), 1, &created);
+      if (ns >= 0) {
+        // the key word is already published by the CAS; copy the rest
+        nt[ns].w = e.w;
+        nt[ns].z = e.z;
+        nt[ns].sq = e.sq;
+        nt[ns].cnt = e.cnt;
+        nt[ns].vrow = e.vrow;
+        nt[ns].tag = e.tag;
+      } else {
+        failed = true;
+      }
+    }
+    remap[i] = ns;
+  }
+  const uint64_t bf = __ballot(failed);
+  if ((threadIdx.x & 63) == 0 && bf) atomicAdd(stat_ptr(stats, 2), (unsigned long long)__popcll(bf));
+}
+
+// out[0..3] = {keys in the table, failed inserts, V-slab overflows, V rows used}
+__global__ __launch_bounds__(64) void k_kv_summary(const int64_t* stats, const int32_t* vnext,
+                                                   int64_t* out) {
+  const int lane = threadIdx.x;
+  long long a = 0, b = 0, c = 0;
+  for (int s = lane; s < kStatShards; s += 64) {
+    a += stats[s * kStatStride + 4];
+    b += stats[s * kStatStride + 2];
+    c += stats[s * kStatStride + 3];
+  }
+  a = wave_sum_ll(a);
+  b = wave_sum_ll(b);
+  c = wave_sum_ll(c);
+  if (lane == 0) {
+    out[0] = a;
+    out[1] = b;
+    out[2] = c;
+    out[3] = vnext ? (int64_t)*vnext : 0;
+  }
+}
+
+}  // namespace
+
+void kv_rehash(const KVSlot* old, int64_t oldcap, KVSlot* nt, int64_t newcap, int32_t* remap,
+               int64_t* stats, hipStream_t s) {
+  if (oldcap <= 0) return;
+  hipLaunchKernelGGL(k_kv_rehash, dim3(grid_for(oldcap, kThreads)), dim3(kThreads), 0, s, old,
+                     oldcap, nt, newcap, remap, stats);
+}
+
+void kv_summary(const KVTable& t, int64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_kv_summary, dim3(1), dim3(64), 0, s, t.stats, t.vnext, out);
 }
 
 }  // namespace wh

@@ -1,0 +1,469 @@
+// Multi-shard parameter-server exchange: owner- and worker-side kernels of
+// the lean DiFacto step over P > 1 shards (P ranks over RCCL, or P virtual
+// shards on one GPU for the loopback rehearsal).
+//
+// Reference flow (learn/difacto/async_sgd.h:372-424): ZPush(feature counts)
+// -> ZVPull(w, V) -> ZVPush(gw, gV), each a ps-lite request per server.
+// Here a minibatch is FOUR collectives on the wire, none of which the host
+// has to wait for inside the step:
+//   C0  tiny all-to-all: {key count, table overflow, V rows of the previous
+//       step's pull} per peer (rides on localize's count exchange)
+//   C1  keys (+ counts in data pass 0) as 12-byte records
+//   C2  pull reply: per peer ONE contiguous region of vstride-float rows
+//       [H_p header rows | v_p embedding rows]
+//   C3  push: the same regions in reverse, [gw | gV rows]
+//
+// Row-aligned regions. With S_p / HS_p the prefix sums of the per-peer key
+// counts n_p and header rows H_p = ceil(2 n_p / vstride), and VS_p the prefix
+// of the per-peer embedding-row counts, region p starts at row HS_p + VS_p.
+// The owner's open kernel writes the embedding row of key i (segment p) at
+// row HS_{p+1} + vpos(i) -- VS_p cancels out -- so rows go straight from the
+// table into the wire buffer in the same launch that decides them; only the
+// 8-byte headers need VS_p and are packed by a second small kernel. The
+// worker consumes the received buffer IN PLACE: its header unpack rewrites
+// each key's row id to the row inside that buffer, the FM kernels gather
+// from it, and the backward writes gV rows at the same positions, so the
+// gradient buffer already has the push layout (pack_gw only adds gw).
+//
+// Duplicates. Unlike one worker's minibatch, the keys an owner receives from
+// different peers overlap (hot features). The open kernel therefore counts
+// with atomics and allocates an embedding row with a CAS on the slot's vrow
+// (exactly one winner initialises it; any other lane that sees a row created
+// in this launch computes the identical initial values from the key hash
+// instead of reading half-written memory). It also threads each key's
+// duplicates into a chain (atomicExch on the slot's tag word); the header
+// pack marks the chain heads and clears the tags before the next minibatch's
+// open can run. The push kernel lets only a head lane update its key, over
+// its chain in ascending index = peer-rank order, so each worker's push is
+// applied as one sequential update, deterministically (like the ps-lite
+// server handling requests one at a time), in ONE launch.
+#include "wh_common.h"
+#include "wh_kernels.h"
+#include "wh_lookback.h"
+#include "kv_device.h"
+
+namespace wh {
+namespace {
+
+using namespace kvd;
+
+constexpr int kMaxSeg = 1024;  // peers (LDS copies of the segment tables)
+
+// chain word: bits 0-29 = next index + 1 (0 = end), bit 30 = chain head
+constexpr uint32_t kHeadBit = 1u << 30;
+constexpr uint32_t kNextMask = kHeadBit - 1;
+
+// segment of item i: largest p with S[p] <= i (S in LDS, P+1 entries)
+__device__ __forceinline__ int seg_of(const int64_t* S, int P, int64_t i) {
+  int lo = 0, hi = P - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (S[mid] <= i) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void load_seg(const int64_t* g, int64_t* sh, int P) {
+  for (int p = threadIdx.x; p <= P; p += blockDim.x) sh[p] = g[p];
+}
+
+// ---------------------------------------------------------------- owner open
+// keys: u64 [n] (rec == null) or 12-byte records rec [n x 3] int32 {key lo,
+// key hi, count}. Writes slot[n], w_out[n], vpos[n+1], chain[n] (train) and
+// the embedding rows into rbuf.
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_ps_open(
+    KVTable t, const uint64_t* __restrict__ keys, const int32_t* __restrict__ rec, int64_t n,
+    DifactoHP hp, int insert, int use_cnt, int chains, uint32_t epoch,
+    const int32_t* __restrict__ vbase_p, const int64_t* __restrict__ segS,
+    const int64_t* __restrict__ segHS, int P, Lookback lb, int ntiles, int32_t* __restrict__ slot_out,
+    float* __restrict__ w_out, int64_t* __restrict__ vpos, uint32_t* __restrict__ chain,
+    float* __restrict__ rbuf) {
+  __shared__ uint32_t shs[16];
+  __shared__ int sht;
+  __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1];
+  load_seg(segS, sS, P);
+  load_seg(segHS, sHS, P);
+  const int tile = lb_tile(lb, ntiles, &sht);  // (syncs the block)
+  const int lane = threadIdx.x & 63;
+  const int64_t i0 = (int64_t)tile * kPullTile + threadIdx.x * kPullPer;
+  const uint64_t mask = (uint64_t)t.cap - 1;
+  const int32_t vbase = *vbase_p;
+  uint64_t k[kPullPer], h[kPullPer], prev[kPullPer];
+  int32_t c[kPullPer], sl[kPullPer];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    const int64_t i = i0 + r;
+    k[r] = kEmptyKey;
+    c[r] = 0;
+    if (i < n) {
+      if (rec) {
+        const uint32_t lo = (uint32_t)rec[3 * i], hi = (uint32_t)rec[3 * i + 1];
+        k[r] = ((uint64_t)hi << 32) | lo;
+        c[r] = use_cnt ? rec[3 * i + 2] : 0;
+      } else {
+        k[r] = keys[i];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {  // all home-slot probes in flight together
+    h[r] = mix64(k[r]) & mask;
+    prev[r] = k[r] != kEmptyKey ? ld_relaxed(&t.sl[h[r]].key) : 0;
+  }
+  int created = 0, failed = 0;
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    sl[r] = -1;
+    if (k[r] == kEmptyKey) continue;
+    bool cr = false;
+    sl[r] = probe_slot(t.sl, mask, k[r], h[r], prev[r], insert, &cr);
+    created += cr ? 1 : 0;
+    if (insert && sl[r] < 0) ++failed;
+    if (i0 + r < n) slot_out[i0 + r] = sl[r];
+  }
+  float w[kPullPer];
+  int32_t row[kPullPer];
+  bool want[kPullPer];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    w[r] = 0.f;
+    row[r] = -1;
+    want[r] = false;
+    if (sl[r] < 0) continue;
+    KVSlot& e = t.sl[sl[r]];
+    w[r] = e.w;
+    row[r] = t.vstride > 0 ? ld_relaxed_i32(&e.vrow) : -1;
+    if (use_cnt) {
+      // only the lane whose add crosses the threshold may allocate: with a
+      // key's duplicates adding concurrently, exactly one lane crosses (a key
+      // that crossed while l1_shrk held w at 0 is allocated by the push that
+      // makes w non-zero)
+      const uint32_t old = atomicAdd(&e.cnt, (uint32_t)c[r]);
+      want[r] = t.vstride > 0 && old <= hp.threshold && old + (uint32_t)c[r] > hp.threshold &&
+                row[r] < 0 && (!hp.l1_shrk || w[r] != 0.f);
+    }
+    if (chains) {
+      const uint32_t mine = (epoch << 24) | (uint32_t)(i0 + r + 1);
+      const uint32_t pv = atomicExch(&e.tag, mine);
+      uint32_t nx = 0;
+      if ((pv >> 24) == epoch) {
+        const uint32_t j = (pv & 0xffffffu) - 1;
+        if ((int64_t)j < n && (int64_t)j != i0 + r) nx = j + 1;
+      }
+      chain[i0 + r] = nx;
+    }
+  }
+  // allocation: exactly one CAS winner per key initialises the row
+  bool mine_fresh[kPullPer];
+  long long newv = 0;
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    mine_fresh[r] = false;
+    if (!use_cnt || t.vstride == 0) continue;
+    const int32_t nr = wave_alloc_rows(t, want[r]);
+    if (nr >= 0) {
+      const int32_t o = atomicCAS(&t.sl[sl[r]].vrow, -1, nr);
+      if (o == -1) {
+        row[r] = nr;
+        mine_fresh[r] = true;
+        newv += t.dim;
+      } else {
+        row[r] = o;  // another peer's duplicate won (nr stays unused)
+      }
+    }
+  }
+  uint32_t f[1] = {0u}, ex[1], tot[1];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    if (hp.l1_shrk && w[r] == 0.f) row[r] = -1;
+    f[0] += row[r] >= 0 ? 1u : 0u;
+  }
+  lb_block_scan<1>(lb, tile, f, ex, tot, shs);
+  int32_t orow[kPullPer];  // output row in rbuf
+  uint32_t run = ex[0];
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    orow[r] = -1;
+    if (i0 + r < n) {
+      w_out[i0 + r] = w[r];
+      vpos[i0 + r] = run;
+      if (row[r] >= 0) {
+        const int p = seg_of(sS, P, i0 + r);
+        orow[r] = (int32_t)(sHS[p + 1] + run);
+      }
+    }
+    run += row[r] >= 0 ? 1u : 0u;
+  }
+  if (tile == ntiles - 1 && threadIdx.x == 0) vpos[n] = tot[0];
+  const long long ci = wave_sum_ll(created), cf = wave_sum_ll(failed), cv = wave_sum_ll(newv);
+  if (lane == 0) {
+    if (ci) atomicAdd(stat_ptr(t.stats, 4), (unsigned long long)ci);
+    if (cf) atomicAdd(stat_ptr(t.stats, 2), (unsigned long long)cf);
+    if (cv) atomicAdd(stat_ptr(t.stats, 1), (unsigned long long)cv);
+  }
+  if (t.vstride == 0) return;
+  // row jobs: 0 copy from the slab, 1 initialise (CAS winner: table + wire),
+  // 2 recompute the initial values (a row another lane created in this launch)
+#pragma unroll
+  for (int r = 0; r < kPullPer; ++r) {
+    const int kind = mine_fresh[r] ? 1 : (row[r] >= vbase ? 2 : 0);
+    for_each_row_job<G>(orow[r] >= 0, [&](int src, int gl) {
+      const int s2 = src >= 0 ? src : lane;
+      const int32_t jr = __shfl(row[r], s2, 64), jo = __shfl(orow[r], s2, 64);
+      const int jk = __shfl(kind, s2, 64);
+      const uint64_t jkey = __shfl(k[r], s2, 64);
+      if (src < 0) return;
+      float* V = t.V + (int64_t)jr * t.vstride;
+      float* o = rbuf + (int64_t)jo * t.vstride;
+      for (int cc = gl * 4; cc < t.vstride; cc += 4 * G) {
+        float4 v;
+        if (jk == 0) {
+          v = *reinterpret_cast<const float4*>(V + cc);
+        } else {
+          v = v_init4(hp, jkey, cc, t.dim);
+          if (jk == 1) {
+            *reinterpret_cast<float4*>(V + cc) = v;
+            *reinterpret_cast<float4*>(t.VG + (int64_t)jr * t.vstride + cc) =
+                make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+        *reinterpret_cast<float4*>(o + cc) = v;
+      }
+    });
+  }
+}
+
+// header pack (owner, after the open): {w, row index inside the peer's V
+// block or -1} at float (HS_p + VS_p) * vstride + 2 (i - S_p); the per-peer V
+// row counts; chain heads marked and the slot tags cleared
+__global__ __launch_bounds__(kThreads) void k_ps_pack_hdr(
+    KVSlot* sl, const int32_t* __restrict__ slot, const float* __restrict__ w_out,
+    const int64_t* __restrict__ vpos, int64_t n, int vstride, int chains, uint32_t epoch,
+    const int64_t* __restrict__ segS, const int64_t* __restrict__ segHS, int P,
+    uint32_t* __restrict__ chain, float* __restrict__ rbuf, int64_t* __restrict__ vcnt) {
+  __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1];
+  load_seg(segS, sS, P);
+  load_seg(segHS, sHS, P);
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int p = threadIdx.x; p < P; p += blockDim.x) vcnt[p] = vpos[sS[p + 1]] - vpos[sS[p]];
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const int p = seg_of(sS, P, i);
+  const int64_t vs0 = vpos[sS[p]];
+  const int64_t v = vpos[i];
+  const bool has = vpos[i + 1] > v;
+  const int32_t j = has ? (int32_t)(v - vs0) : -1;
+  *reinterpret_cast<float2*>(rbuf + (sHS[p] + vs0) * vstride + 2 * (i - sS[p])) =
+      make_float2(w_out[i], __int_as_float(j));
+  if (chains) {
+    const int32_t s = slot[i];
+    if (s >= 0) {
+      const uint32_t mine = (epoch << 24) | (uint32_t)(i + 1);
+      if (sl[s].tag == mine) {  // the last exchanger heads the chain
+        chain[i] |= kHeadBit;
+        sl[s].tag = 0u;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- worker side
+// hdr[k] = {w, row of key k's embedding inside the received buffer or -1};
+// rows_total[0] = rows of the received buffer
+__global__ __launch_bounds__(kThreads) void k_ps_unpack(
+    const float* __restrict__ rbuf, int64_t U, int vstride, const int64_t* __restrict__ segS,
+    const int64_t* __restrict__ segHS, const int64_t* __restrict__ vrecv, int P,
+    float2* __restrict__ hdr, int64_t* __restrict__ rows_total) {
+  __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1], sVS[kMaxSeg + 1];
+  load_seg(segS, sS, P);
+  load_seg(segHS, sHS, P);
+  if (threadIdx.x == 0) {  // P is small (peers): a serial prefix is fine
+    int64_t a = 0;
+    for (int p = 0; p < P; ++p) { sVS[p] = a; a += vrecv[p]; }
+    sVS[P] = a;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) rows_total[0] = sHS[P] + sVS[P];
+  const int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (k >= U) return;
+  const int q = seg_of(sS, P, k);
+  const float2 e =
+      *reinterpret_cast<const float2*>(rbuf + (sHS[q] + sVS[q]) * vstride + 2 * (k - sS[q]));
+  const int32_t j = __float_as_int(e.y);
+  const int32_t vid = j >= 0 ? (int32_t)(sHS[q + 1] + sVS[q] + j) : -1;
+  hdr[k] = make_float2(e.x, __int_as_float(vid));
+}
+
+// gw[k] into the header rows of its owner's region of the push buffer
+__global__ __launch_bounds__(kThreads) void k_ps_pack_gw(
+    const float* __restrict__ gw, int64_t U, int vstride, const int64_t* __restrict__ segS,
+    const int64_t* __restrict__ segHS, const int64_t* __restrict__ vrecv, int P,
+    float* __restrict__ gbuf) {
+  __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1], sVS[kMaxSeg + 1];
+  load_seg(segS, sS, P);
+  load_seg(segHS, sHS, P);
+  if (threadIdx.x == 0) {
+    int64_t a = 0;
+    for (int p = 0; p < P; ++p) { sVS[p] = a; a += vrecv[p]; }
+    sVS[P] = a;
+  }
+  __syncthreads();
+  const int64_t k = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (k >= U) return;
+  const int q = seg_of(sS, P, k);
+  gbuf[(sHS[q] + sVS[q]) * vstride + (k - sS[q])] = gw[k];
+}
+
+// ---------------------------------------------------------------- owner push
+// next element of a chain in ascending index order after `last` (the chains
+// hold at most one entry per peer, so a selection walk is cheap)
+__device__ __forceinline__ int64_t chain_next_after(const uint32_t* chain, int64_t head,
+                                                    int64_t last) {
+  int64_t best = -1;
+  for (int64_t e = head; e >= 0;) {
+    if (e > last && (best < 0 || e < best)) best = e;
+    const uint32_t nx = chain[e] & kNextMask;
+    e = nx ? (int64_t)nx - 1 : -1;
+  }
+  return best;
+}
+
+template <int G>
+__global__ __launch_bounds__(kThreads) void k_ps_push(
+    KVTable t, const int32_t* __restrict__ slot, const int64_t* __restrict__ vpos,
+    const uint32_t* __restrict__ chain, int64_t n, const int64_t* __restrict__ segS,
+    const int64_t* __restrict__ segHS, int P, const float* __restrict__ gbuf, DifactoHP hp) {
+  __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1];
+  load_seg(segS, sS, P);
+  load_seg(segHS, sHS, P);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  float w0 = 0.f, w = 0.f;
+  int32_t s = -1, row = -1;
+  bool head = false, any_v = false, alloc = false;
+  if (i < n) {
+    s = slot[i];
+    head = s >= 0 && (!chain || (chain[i] & kHeadBit));
+  }
+  if (head) {
+    KVSlot& e = t.sl[s];
+    w0 = w = e.w;
+    float z = e.z, sq = e.sq;
+    bool up = false;  // w went 0 -> non-zero at some push of the chain
+    for (int64_t el = chain ? chain_next_after(chain, i, -1) : i; el >= 0;
+         el = chain ? chain_next_after(chain, i, el) : -1) {
+      const int p = seg_of(sS, P, el);
+      const int64_t vs0 = vpos[sS[p]];
+      const float g = gbuf[(sHS[p] + vs0) * t.vstride + (el - sS[p])];
+      const float nw = difacto_ftrl(w, g, sq, z, hp);
+      up |= (w == 0.f && nw != 0.f);
+      w = nw;
+      any_v |= vpos[el + 1] > vpos[el];
+    }
+    e.w = w;
+    e.z = z;
+    e.sq = sq;
+    if (t.vstride > 0) {
+      row = e.vrow;
+      alloc = up && row < 0 && e.cnt > hp.threshold;
+    }
+  }
+  count_nnz_delta(w0, w, t.stats);
+  if (t.vstride == 0) return;
+  const int32_t nrow = wave_alloc_rows(t, alloc);
+  int kind = 0;  // 1 initialise a new row, 2 AdaGrad over the chain's gradients
+  if (nrow >= 0) {
+    t.sl[s].vrow = nrow;
+    row = nrow;
+    kind = 1;
+  } else if (head && row >= 0 && any_v) {
+    kind = 2;
+  }
+  long long newv = kind == 1 ? t.dim : 0;
+  for_each_row_job<G>(kind != 0, [&](int src, int gl) {
+    const int s2 = src >= 0 ? src : lane;
+    const int32_t jr = __shfl(row, s2, 64), jk = __shfl(kind, s2, 64);
+    const int32_t js = __shfl(s, s2, 64);
+    const int64_t ji = __shfl(i, s2, 64);
+    if (src < 0) return;
+    if (jk == 1) {
+      init_v_row(t, t.sl[js].key, jr, gl, G, hp);
+      return;
+    }
+    float* V = t.V + (int64_t)jr * t.vstride;
+    float* VG = t.VG + (int64_t)jr * t.vstride;
+    for (int cc = gl * 4; cc < t.vstride; cc += 4 * G) {
+      float4 v = *reinterpret_cast<float4*>(V + cc);
+      float4 cg = *reinterpret_cast<float4*>(VG + cc);
+      for (int64_t el = chain ? chain_next_after(chain, ji, -1) : ji; el >= 0;
+           el = chain ? chain_next_after(chain, ji, el) : -1) {
+        if (vpos[el + 1] <= vpos[el]) continue;  // that peer pulled no V row
+        const int p = seg_of(sS, P, el);
+        const float4 g = *reinterpret_cast<const float4*>(
+            gbuf + (sHS[p + 1] + vpos[el]) * t.vstride + cc);
+        adagrad4(v, cg, g, hp);
+      }
+      *reinterpret_cast<float4*>(V + cc) = v;
+      *reinterpret_cast<float4*>(VG + cc) = cg;
+    }
+  });
+  newv = wave_sum_ll(newv);
+  if (lane == 0 && newv) atomicAdd(stat_ptr(t.stats, 1), (unsigned long long)newv);
+}
+
+}  // namespace
+
+bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t n, int use_cnt,
+             DifactoHP hp, int insert, int chains, uint32_t epoch, const int32_t* vbase,
+             const int64_t* segS, const int64_t* segHS, int P, const Lookback& lb, int32_t* slot,
+             float* w_out, int64_t* vpos, uint32_t* chain, float* rbuf, int64_t* vcnt,
+             hipStream_t s) {
+  const int64_t ntiles = (n + kPullTile - 1) / kPullTile;
+  if (P < 1 || P > kMaxSeg || ntiles > kLbMaxTiles || n >= (1 << 24) || t.vstride == 0)
+    return false;
+  if (n > 0) {
+    const int G = lanes_per_key(t.vstride);
+    WH_DISPATCH_G(G, k_ps_open, dim3((unsigned)ntiles), dim3(kThreads), 0, s, t, keys, rec, n, hp,
+                  insert, use_cnt, chains, epoch, vbase, segS, segHS, P, lb, (int)ntiles, slot,
+                  w_out, vpos, chain, rbuf);
+  } else {
+    WH_HIP_CHECK(hipMemsetAsync(vpos, 0, sizeof(int64_t), s));
+  }
+  hipLaunchKernelGGL(k_ps_pack_hdr, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t.sl, slot,
+                     w_out, vpos, n, t.vstride, chains, epoch, segS, segHS, P, chain, rbuf, vcnt);
+  return true;
+}
+
+bool ps_push(const KVTable& t, const int32_t* slot, const int64_t* vpos, const uint32_t* chain,
+             int64_t n, const int64_t* segS, const int64_t* segHS, int P, const float* gbuf,
+             DifactoHP hp, hipStream_t s) {
+  if (P < 1 || P > kMaxSeg || t.vstride == 0) return false;
+  if (n <= 0) return true;
+  const int G = lanes_per_key(t.vstride);
+  WH_DISPATCH_G(G, k_ps_push, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t, slot, vpos,
+                chain, n, segS, segHS, P, gbuf, hp);
+  return true;
+}
+
+bool ps_unpack(const float* rbuf, int64_t U, int vstride, const int64_t* segS,
+               const int64_t* segHS, const int64_t* vrecv, int P, float* hdr, int64_t* rows_total,
+               hipStream_t s) {
+  if (P < 1 || P > kMaxSeg) return false;
+  hipLaunchKernelGGL(k_ps_unpack, dim3(grid_for(U, kThreads)), dim3(kThreads), 0, s, rbuf, U,
+                     vstride, segS, segHS, vrecv, P, reinterpret_cast<float2*>(hdr), rows_total);
+  return true;
+}
+
+bool ps_pack_gw(const float* gw, int64_t U, int vstride, const int64_t* segS,
+                const int64_t* segHS, const int64_t* vrecv, int P, float* gbuf, hipStream_t s) {
+  if (P < 1 || P > kMaxSeg) return false;
+  if (U <= 0) return true;
+  hipLaunchKernelGGL(k_ps_pack_gw, dim3(grid_for(U, kThreads)), dim3(kThreads), 0, s, gw, U,
+                     vstride, segS, segHS, vrecv, P, gbuf);
+  return true;
+}
+
+}  // namespace wh

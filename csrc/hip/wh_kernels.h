@@ -81,7 +81,8 @@ struct alignas(32) KVSlot {
   float sq;        // sqrt of cumulative squared gradient
   uint32_t cnt;    // feature count (difacto)
   int32_t vrow;    // row into the V slab, -1 = no embedding
-  float pad;
+  uint32_t tag;    // multi-shard push: duplicate-chain head of the open
+                   // minibatch session (psx.hip), 0 = none
 };
 static_assert(sizeof(KVSlot) == 32, "KVSlot must be one 32-byte sector");
 // Event counters are sharded over 64 cache lines: one counter word takes
@@ -105,6 +106,12 @@ void kv_find(const KVTable& t, const uint64_t* keys, int64_t n, int insert, int3
              hipStream_t s);
 // dump: indices of occupied slots (compaction); out_n[0] receives the count
 void kv_occupied(const KVTable& t, int32_t* out_slots, int64_t* out_n, hipStream_t s);
+// growth: re-insert the occupied slots of `old` into the empty table `nt`
+// (power-of-two newcap > oldcap); remap[oldcap] receives old -> new slot ids
+void kv_rehash(const KVSlot* old, int64_t oldcap, KVSlot* nt, int64_t newcap, int32_t* remap,
+               int64_t* stats, hipStream_t s);
+// health read: out[4] = {keys, failed inserts, V-slab overflows, V rows used}
+void kv_summary(const KVTable& t, int64_t* out, hipStream_t s);
 
 // ------------------------------------------------------------ linear optim
 // algo: 1 SGD, 2 AdaGrad, 3 FTRL (reference learn/linear/async_sgd.h:71-180)
@@ -162,6 +169,34 @@ bool difacto_open_pull(const KVTable& t, const uint64_t* keys, int64_t n, const 
                        int64_t* vpos, float* vc, hipStream_t s);
 bool vidx_renumber_fused(float* hdr, int64_t n, const Lookback& lb, int64_t* count,
                          hipStream_t s);
+
+// ------------------------------------------------------------- psx.hip
+// Multi-shard DiFacto exchange (see psx.hip for the row-aligned region
+// layout). seg tables are device int64 [P+1] prefix sums: segS = key
+// segment starts, segHS = header-row starts (H_p = ceil(2 n_p / vstride)).
+// ps_open: owner find/insert + (use_cnt) atomic count push with lazy V
+//   allocation + variable-length pull of n received keys (u64 keys, or
+//   12-byte {lo, hi, count} records), writing slot/w_out/vpos[n+1], the
+//   duplicate chains (chains != 0; epoch 1..255) and the reply buffer rbuf
+//   (embedding rows and packed headers); vcnt[P] = V rows per peer.
+//   vbase: device int32 copy of vnext taken before the launch.
+// ps_push: owner applies the received push buffer (same layout as rbuf).
+// ps_unpack / ps_pack_gw: worker side (segments = keys sent per owner,
+//   vrecv[P] = V rows received per owner).
+// Each returns false when its limits are exceeded (P > 1024, n >= 2^24).
+bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t n, int use_cnt,
+             DifactoHP hp, int insert, int chains, uint32_t epoch, const int32_t* vbase,
+             const int64_t* segS, const int64_t* segHS, int P, const Lookback& lb, int32_t* slot,
+             float* w_out, int64_t* vpos, uint32_t* chain, float* rbuf, int64_t* vcnt,
+             hipStream_t s);
+bool ps_push(const KVTable& t, const int32_t* slot, const int64_t* vpos, const uint32_t* chain,
+             int64_t n, const int64_t* segS, const int64_t* segHS, int P, const float* gbuf,
+             DifactoHP hp, hipStream_t s);
+bool ps_unpack(const float* rbuf, int64_t U, int vstride, const int64_t* segS,
+               const int64_t* segHS, const int64_t* vrecv, int P, float* hdr, int64_t* rows_total,
+               hipStream_t s);
+bool ps_pack_gw(const float* gw, int64_t U, int vstride, const int64_t* segS,
+                const int64_t* segHS, const int64_t* vrecv, int P, float* gbuf, hipStream_t s);
 
 // ---------------------------------------------------------------- fm.hip
 // Forward of FM / linear model on a localized minibatch.

@@ -1,0 +1,210 @@
+"""The lean multi-shard DiFacto step (kv/psx.py, csrc/hip/psx.hip).
+
+* loopback P shards in one process with max_concurrency=1 (staleness 0)
+  computes the same model as the single-shard fused path;
+* the default pipelined step (staleness 1) trains and drains cleanly;
+* 2 ranks over gloo: the owners' feature counts are exactly the total
+  occurrences over both workers, every embedding row exists where the count
+  crossed the threshold, and every worker pulls exactly the owner's values;
+* the HIP kernels of the same path match the host oracle (GPU).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+CARD = [50, 400, 3000, 20, 7, 900]
+
+
+def _conf(max_conc=2, l1_shrk=False, dim=8, thr=3):
+    from wormhole_amd.config.schema import DifactoConfig, Embedding
+    emb = Embedding(dim=dim, threshold=thr)
+    return DifactoConfig(embedding=[emb], lambda_l1=0.01, l1_shrk=l1_shrk,
+                         max_concurrency=max_conc)
+
+
+def _run(comm, conf, device, steps=6, rows=300, seed=17, nxt=True):
+    from wormhole_amd.data.synthetic import criteo_batch_cpu
+    from wormhole_amd.models.difacto import DifactoLearner
+    lr = DifactoLearner(conf, comm, device, cap=1 << 14, vcap=1 << 12, seed=5)
+    batches = [[t.to(device) for t in criteo_batch_cpu(rows, seed, s, CARD)] for s in range(steps)]
+    for s, (keys, label, off) in enumerate(batches):
+        nb = None
+        if nxt and s + 1 < steps:
+            nb = (batches[s + 1][0], batches[s + 1][2], None)
+        lr.process(keys, off, None, label, 0, 0, next_batch=nb)
+    prog = lr.take_progress()
+    return lr, prog, batches
+
+
+def _model(lr):
+    st = lr.store
+    occ = st.occupied().long()
+    keys = st.keys[occ.to(st.keys.device)].cpu().tolist()
+    w = st.w[occ.to(st.w.device)].cpu().tolist()
+    cnt = st.cnt[occ.to(st.cnt.device)].cpu().tolist()
+    vrow = st.vrow[occ.to(st.vrow.device)].cpu().tolist()
+    V = st.V.cpu()
+    out = {}
+    for k, ww, c, r in zip(keys, w, cnt, vrow):
+        out[int(np.int64(k))] = (float(ww), int(c), None if r < 0 else V[r][:lr.dim].clone())
+    return out
+
+
+def test_loopback_strict_matches_single_shard():
+    from wormhole_amd.parallel.comm import Comm, LoopbackComm
+    one, p1, _ = _run(Comm("cpu", init=False), _conf(max_conc=1), "cpu")
+    lb, p4, _ = _run(LoopbackComm(4, "cpu"), _conf(max_conc=1), "cpu")
+    assert lb.psx is not None and one.psx is None
+    m1, m4 = _model(one), _model(lb)
+    assert m1.keys() == m4.keys()
+    for k, (w, c, v) in m1.items():
+        w4, c4, v4 = m4[k]
+        assert c == c4, k
+        assert abs(w - w4) < 1e-5, (k, w, w4)
+        assert (v is None) == (v4 is None), k
+        if v is not None:
+            assert torch.allclose(v, v4, atol=1e-5), k
+    for a, b in zip(p1, p4):
+        assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (p1, p4)
+
+
+def test_loopback_pipelined_trains_and_drains():
+    from wormhole_amd.parallel.comm import Comm, LoopbackComm
+    lb, prog, batches = _run(LoopbackComm(3, "cpu"), _conf(), "cpu", steps=8)
+    assert lb.psx.tau == 1
+    assert lb.psx.pull is None and lb.psx.push is None and lb.psx.job is None
+    assert prog[4] == 8 and prog[5] == 8 * 300  # every minibatch forwarded once
+    one, prog1, _ = _run(Comm("cpu", init=False), _conf(), "cpu", steps=8)
+    # staleness 1 perturbs the trajectory only slightly on this problem
+    assert abs(prog[0] / prog[5] - prog1[0] / prog1[5]) < 0.02
+    m, m1 = _model(lb), _model(one)
+    assert m.keys() == m1.keys()
+    # counts are exact regardless of the pipelining
+    assert all(m[k][1] == m1[k][1] for k in m1)
+    assert all((m[k][2] is None) == (m1[k][2] is None) for k in m1)
+
+
+def test_loopback_without_lookahead():
+    """next_batch omitted: every call begins its own localize; same model
+    as with the lookahead."""
+    from wormhole_amd.parallel.comm import LoopbackComm
+    a, pa, _ = _run(LoopbackComm(2, "cpu"), _conf(), "cpu", nxt=True)
+    b, pb, _ = _run(LoopbackComm(2, "cpu"), _conf(), "cpu", nxt=False)
+    ma, mb = _model(a), _model(b)
+    assert ma.keys() == mb.keys()
+    for k in ma:
+        assert ma[k][0] == mb[k][0] and ma[k][1] == mb[k][1]
+    assert pa == pb
+
+
+def test_loopback_validation_pass():
+    from wormhole_amd.data.synthetic import criteo_batch_cpu
+    from wormhole_amd.parallel.comm import LoopbackComm
+    lb, _, _ = _run(LoopbackComm(3, "cpu"), _conf(), "cpu", steps=4)
+    nkeys = len(_model(lb))
+    keys, label, off = criteo_batch_cpu(200, 99, 0, CARD)
+    py = lb.process(keys, off, None, label, 2, 0)  # PRED: no insert, no push
+    assert py.shape == (200,) and bool(torch.isfinite(py).all())
+    assert len(_model(lb)) == nkeys
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _two_rank_main(rank, world, port, out_dir, device, max_conc):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    from wormhole_amd import ops
+    from wormhole_amd.parallel.comm import Comm
+    dev = torch.device(device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(0)
+        comm = Comm(dev, backend="gloo")
+    else:
+        comm = Comm(dev)
+    lr, prog, batches = _run(comm, _conf(max_conc=max_conc), dev, steps=6, seed=17 + rank)
+    assert lr.psx is not None
+    # every key's count on its owner = its occurrences over all workers
+    occ = {}
+    for keys, _, _ in batches:
+        u, c = torch.unique(keys.cpu(), return_counts=True)
+        for k, n in zip(u.tolist(), c.tolist()):
+            occ[k] = occ.get(k, 0) + n
+    allocc = comm.allgather_object(occ)
+    mine = _model(lr)
+    allm = comm.allgather_object({k: (w, c, None if v is None else v.tolist())
+                                  for k, (w, c, v) in mine.items()})
+    tot, owner = {}, {}
+    for o in allocc:
+        for k, n in o.items():
+            tot[k] = tot.get(k, 0) + n
+    for m in allm:
+        assert not (owner.keys() & m.keys())  # each key lives on one shard
+        owner.update(m)
+    assert owner.keys() == tot.keys()
+    for k, n in tot.items():
+        w, c, v = owner[k]
+        assert c == n, (k, c, n)
+        assert (v is not None) == (n > 3), (k, n)
+    # a fresh pull through the old exchange sees the owners' values
+    keys, label, off = [t.to(dev) for t in batches[-1]]
+    uniq, ucnt, owner_cnt, lid, *_ = ops.localize(keys, off, None, comm.size)
+    sess = lr.kv.open(uniq, owner_cnt, insert=False)
+    hdr, vc = lr.kv.difacto_pull(sess, False)
+    vid = ops.hdr_vidx(hdr.cpu()).tolist()
+    for i, k in enumerate(uniq.cpu().tolist()):
+        w, c, v = owner[k]
+        assert abs(float(hdr[i, 0]) - w) < 1e-7
+        assert (vid[i] >= 0) == (v is not None)
+    comm.barrier()
+    with open(os.path.join(out_dir, "r%d" % rank), "w") as f:
+        f.write("%r\n" % (prog[0] / prog[5]))
+    comm.finalize()
+
+
+@pytest.mark.parametrize("max_conc", [1, 2])
+def test_psx_two_ranks_gloo(tmp_path, max_conc):
+    mp.spawn(_two_rank_main, args=(2, _free_port(), str(tmp_path), "cpu", max_conc), nprocs=2,
+             join=True)
+    for r in range(2):
+        assert 0 < float(open(tmp_path / ("r%d" % r)).read()) < 1.0
+
+
+@pytest.mark.gpu
+def test_psx_two_ranks_gpu_staged(tmp_path):
+    """The same multi-rank invariants with the HIP kernels (2 ranks sharing
+    the GPU, transfers staged through gloo)."""
+    mp.spawn(_two_rank_main, args=(2, _free_port(), str(tmp_path), "cuda", 2), nprocs=2,
+             join=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_conc", [1, 2])
+def test_loopback_gpu_matches_cpu(max_conc):
+    """Loopback P=4 through the HIP kernels vs the host oracle: no duplicates
+    across segments, so the model must agree to float tolerance."""
+    from wormhole_amd.parallel.comm import LoopbackComm
+    dev = torch.device("cuda", 0)
+    g, pg, _ = _run(LoopbackComm(4, dev), _conf(max_conc=max_conc), dev, steps=6, rows=2000)
+    c, pc, _ = _run(LoopbackComm(4, "cpu"), _conf(max_conc=max_conc), "cpu", steps=6, rows=2000)
+    mg, mc = _model(g), _model(c)
+    assert mg.keys() == mc.keys()
+    bad = 0
+    for k, (w, cn, v) in mc.items():
+        wg, cg, vg = mg[k]
+        assert cn == cg, k
+        assert (v is None) == (vg is None), k
+        if abs(w - wg) > 1e-4 or (v is not None and not torch.allclose(v, vg, atol=1e-4)):
+            bad += 1
+    assert bad == 0, bad
+    assert abs(pg[0] / pg[5] - pc[0] / pc[5]) < 1e-4

@@ -23,6 +23,89 @@ from .. import _native, ops
 from .cpu_store import CpuKVStore
 
 
+class StoreError(RuntimeError):
+    """The parameter store lost data (a failed insert or a full V slab)."""
+
+
+class StoreGuard:
+    """Load-factor control and loud failure for one parameter store shard.
+
+    The reference server allocates an entry per key without bound and grows
+    V per key on demand (learn/difacto/async_sgd.h:139-160, 247-259). The
+    HBM store is an open-addressing table plus a V-row slab, so this guard
+    keeps it there: after every open it enqueues a 32-byte summary read
+    (keys, failed inserts, V-slab overflows, V rows used), and before the
+    next open it checks that read -- raising :class:`StoreError` on any lost
+    key or row -- and grows the table (device rehash, at most ``max_load``
+    occupancy) or the V slab so that the coming minibatch cannot overflow
+    either, whatever it inserts. The read is one minibatch behind, so it
+    never stalls the stream."""
+
+    def __init__(self, store, max_load=0.7):
+        self.store = store
+        self.max_load = float(max_load)
+        self.pend = None      # (pinned host tensor, event) of the last summary
+        self.keys = 0
+        self.vused = 0
+        self.since = 0        # keys opened since the last completed summary
+        self.grows = 0
+        self.vgrows = 0
+        self.cuda = not isinstance(store, CpuKVStore)
+
+    def after_open(self):
+        s = self.store.summary()
+        if self.cuda:
+            h = torch.empty(4, dtype=torch.int64, pin_memory=True)
+            h.copy_(s, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self.pend = (h, ev)
+        else:
+            self.pend = (s, None)
+        self.since = 0
+
+    def read(self):
+        """Apply the last summary; raises StoreError on lost data."""
+        if self.pend is None:
+            return
+        h, ev = self.pend
+        self.pend = None
+        if ev is not None:
+            ev.synchronize()
+        keys, fail, vover, vused = [int(x) for x in h.tolist()]
+        self.keys, self.vused = keys, vused
+        if fail or vover:
+            raise StoreError(
+                "parameter store shard lost data: %d failed inserts, %d embedding rows "
+                "dropped (table %d/%d keys, V slab %d/%d rows)" % (
+                    fail, vover, keys, self.store.cap, vused, self.store.vcap))
+
+    def before_open(self, n, remap_cb=None):
+        """Make room for a minibatch of n incoming keys (before its open)."""
+        self.read()
+        st = self.store
+        need = self.keys + self.since + n
+        if need > self.max_load * st.cap:
+            cap = st.cap
+            while need > 0.5 * cap:  # leave room to grow into
+                cap *= 2
+            remap = st.grow(cap)
+            self.grows += 1
+            if remap_cb is not None:
+                remap_cb(remap)
+        if getattr(st, "vstride", 0) > 0:
+            # V rows: this open and the in-flight push may each allocate one
+            # row per key at most
+            vneed = self.vused + 2 * (self.since + n)
+            if vneed > st.vcap:
+                vcap = max(st.vcap, 1)
+                while vneed > vcap:
+                    vcap *= 2
+                st.grow_v(vcap)
+                self.vgrows += 1
+        self.since += n
+
+
 def make_store(cap, vcap, dim, device):
     device = torch.device(device)
     if device.type == "cuda":
@@ -71,6 +154,7 @@ class ShardedKV:
         self.nshard = comm.size if nshard is None else max(1, min(int(nshard), comm.size))
         self.push_count = 0  # number of push requests applied (SGD's t)
         self.pending = None  # a deferred push: (handle, apply)
+        self.guard = StoreGuard(store)
 
     # ------------------------------------------------------ payload filter
     def _rows_out(self, x):
@@ -131,7 +215,11 @@ class ShardedKV:
                 sess = Session(send, recv, keys)
                 sess.cnt = c.int() if self.fixed_bytes else c
         self.flush()  # a deferred push lands before this minibatch's lookups
+        if insert:
+            self.guard.before_open(sess.keys.shape[0])
         sess.slots = self.store.find(sess.keys, insert)
+        if insert:
+            self.guard.after_open()
         return sess
 
     def _to_owner(self, sess, x):
@@ -191,8 +279,12 @@ class ShardedKV:
         self.flush()
         if cnt is not None and not (cnt.is_cuda and cnt.dtype == torch.int32):
             cnt = cnt.int() if cnt.is_cuda else cnt.float()
+        if insert:
+            self.guard.before_open(uniq.shape[0])
         slots, hdr, vc, vpos = self.store.difacto_open_pull(uniq, insert, cnt, hp, threshold,
                                                             l1_shrk, seed)
+        if insert:
+            self.guard.after_open()
         sess.slots = slots
         sess.hdr_own = hdr
         sess.m = vpos[-1:]

@@ -322,3 +322,101 @@ class CpuKVStore:
                     gv = gv_all[vid_all[i]].astype(np.float32) + v_l2 * v
                     cgv[:] = np.sqrt(cgv * cgv + gv * gv)
                     v -= v_alpha / (cgv + v_beta) * gv
+
+    # ----------------------------------------------- multi-shard (psx) ops
+    def ps_open(self, keys, use_cnt, segS, segHS, rows_cap, insert, chains, epoch, h, threshold,
+                l1_shrk, seed):
+        """Owner side of a P-shard minibatch (host oracle of psx.hip ps_open):
+        segments in peer order, each one find/insert + count push (the lane
+        whose add crosses the threshold allocates) + variable-length pull
+        into the row-aligned reply buffer. Returns (slot, vpos, chain, rbuf,
+        vcnt); chain is unused on the host (duplicates are applied in peer
+        order by ps_push)."""
+        if keys.dtype == torch.int32:
+            rec = keys.reshape(-1, 3).numpy()
+            ks = (rec[:, 0].astype(np.int64) & 0xFFFFFFFF) | (rec[:, 1].astype(np.int64) << 32)
+            cnt = rec[:, 2].astype(np.int64) if use_cnt else None
+        else:
+            ks = keys.numpy().astype(np.int64)
+            cnt = None
+        n = ks.shape[0]
+        S = [int(x) for x in segS.tolist()]
+        HS = [int(x) for x in segHS.tolist()]
+        P = len(S) - 1
+        vs = self.vstride
+        slot = self.find(torch.from_numpy(ks), insert).numpy()
+        w = np.zeros(n, dtype=np.float32)
+        rows = np.full(n, -1, dtype=np.int64)
+        for i in range(n):
+            s = int(slot[i])
+            if s < 0:
+                continue
+            if cnt is not None:
+                old = int(self._cnt[s])
+                new = old + int(cnt[i])
+                self._cnt[s] = np.uint32(new)
+                if (vs > 0 and old <= threshold < new and self._vrow[s] < 0
+                        and (not l1_shrk or self._w[s] != 0)):
+                    self._alloc_v(s, seed, h[7])
+            w[i] = self._w[s]
+            r = int(self._vrow[s]) if vs > 0 else -1
+            if l1_shrk and w[i] == 0:
+                r = -1
+            rows[i] = r
+        flag = (rows >= 0).astype(np.int64)
+        vpos = np.zeros(n + 1, dtype=np.int64)
+        vpos[1:] = np.cumsum(flag)
+        rbuf = np.zeros((rows_cap, max(vs, 1)), dtype=np.float32)
+        vcnt = np.zeros(P, dtype=np.int64)
+        for p in range(P):
+            a, b = S[p], S[p + 1]
+            vs0 = int(vpos[a])
+            vcnt[p] = int(vpos[b]) - vs0
+            flat = rbuf.reshape(-1)
+            base = (HS[p] + vs0) * vs
+            for i in range(a, b):
+                j = int(vpos[i] - vs0) if rows[i] >= 0 else -1
+                flat[base + 2 * (i - a)] = w[i]
+                flat[base + 2 * (i - a) + 1:base + 2 * (i - a) + 2].view(np.int32)[0] = j
+                if rows[i] >= 0:
+                    rbuf[HS[p + 1] + int(vpos[i])] = self._V[rows[i]]
+        return (torch.from_numpy(slot.astype(np.int32)), torch.from_numpy(vpos),
+                torch.zeros(n, dtype=torch.int32), torch.from_numpy(rbuf), torch.from_numpy(vcnt))
+
+    def ps_push(self, slot, vpos, chain, segS, segHS, gbuf, h, threshold, l1_shrk, seed):
+        """Owner side push of a P-shard minibatch: every peer's segment in
+        peer order (ps-lite server: one request at a time)."""
+        S = [int(x) for x in segS.tolist()]
+        HS = [int(x) for x in segHS.tolist()]
+        vs = self.vstride
+        vp = vpos.numpy()
+        flat = gbuf.reshape(-1).numpy()
+        for p in range(len(S) - 1):
+            a, b = S[p], S[p + 1]
+            if b <= a:
+                continue
+            vs0 = int(vp[a])
+            gw = flat[(HS[p] + vs0) * vs + np.arange(b - a)]
+            vid = np.where(vp[a + 1:b + 1] > vp[a:b], vp[a:b] - vs0, -1).astype(np.int32)
+            hdr = np.zeros((b - a, 2), dtype=np.float32)
+            hdr.view(np.int32)[:, 1] = vid
+            nv = int(vp[b] - vs0)
+            gv = gbuf.reshape(-1, max(vs, 1))[HS[p + 1] + vs0:HS[p + 1] + vs0 + nv]
+            self.difacto_push(slot[a:b], torch.from_numpy(hdr), torch.from_numpy(gw.copy()),
+                              gv.contiguous(), h, threshold, l1_shrk, seed)
+
+    def grow(self, newcap):
+        """Host table: capacity bookkeeping only (slots never move)."""
+        if newcap <= self.cap:
+            raise ValueError("grow: new capacity must be larger")
+        self.cap = int(newcap)
+        return torch.arange(self._keys.shape[0], dtype=torch.int32)
+
+    def grow_v(self, newvcap):
+        if newvcap <= self.vcap:
+            raise ValueError("grow_v: new capacity must be larger")
+        self.vcap = int(newvcap)
+
+    def summary(self):
+        return torch.tensor([self._n, self._stats[2], self._stats[3], self._vnext],
+                            dtype=torch.int64)

@@ -1,0 +1,391 @@
+"""Lean multi-shard DiFacto step: P > 1 ranks over RCCL/xGMI, or P virtual
+shards on one GPU (:class:`wormhole_amd.parallel.comm.LoopbackComm`).
+
+Reference per-minibatch flow (learn/difacto/async_sgd.h:372-424): push the
+feature counts (kPushFeaCnt) -> ZVPull(w, V) -> compute -> ZVPush(gw, gV),
+with ``max_concurrency`` (default 2, learn/difacto/config.proto:154)
+minibatches in flight per worker, so minibatch i+1 may pull before
+minibatch i's push has landed.
+
+Here a minibatch costs four collectives and no extra host synchronisation
+(see csrc/hip/psx.hip for the row-aligned wire layout):
+
+  C0  {key count, overflow flag, V rows of the previous pull} per peer: the
+      localize count exchange, read by the host together with the counts
+      (the ONE host read of the step)
+  C1  keys (+ counts in data pass 0), 12-byte records
+  C2  pull reply: per peer one region [header rows | V rows]
+  C3  push: the same regions back, [gw | gV rows]
+
+The owner's open (find/insert, count, lazy V, variable-length pull) and its
+push are one kernel each over all P segments. With ``max_concurrency >= 2``
+the step is software-pipelined one minibatch deep (staleness 1, as the
+reference allows by default); a call of :meth:`PsxDifacto.train` enqueues,
+on the compute stream S,
+
+    localize finish(i) | unpack(i-1) fwd(i-1) | owner push(i-2) |
+    owner open(i) pack(i) | localize begin(i+1) | bwd(i-1) pack_gw(i-1)
+
+and on the comm stream C: C2(i-1), C1(i), C0(i+1) + the count read, C3(i-1).
+The host's wait for the read of C0(i+1) happens in the NEXT call while S
+still holds bwd(i-1), so S never drains. ``max_concurrency = 1`` gives the
+strict (staleness 0) order at the cost of one pipeline drain per step.
+"""
+import contextlib
+
+import numpy as np
+import torch
+
+from .. import _native, ops
+
+TRAIN, VAL, PRED = 0, 1, 2
+
+
+def _cdiv(a, b):
+    return -(-a // b)
+
+
+class _Step:
+    """One minibatch in flight through the exchange."""
+
+    __slots__ = ("train", "use_cnt", "U", "uniq", "ucnt", "lid", "offset", "val", "csc",
+                 "label", "send", "recv", "Hw", "Ho", "tabs", "segS_w", "segHS_w", "segS_o",
+                 "segHS_o", "keys_o", "slot", "vpos", "chain", "rbuf", "vcnt", "ev_open",
+                 "vown", "vrecv", "vrecv_d", "rrecv", "hdr", "rows", "py", "dual", "xv",
+                 "gpush", "ev_push", "seed_step")
+
+    def __init__(self):
+        for s in self.__slots__:
+            setattr(self, s, None)
+
+
+class PsxDifacto:
+    def __init__(self, lrn):
+        self.lrn = lrn
+        self.comm = lrn.comm
+        self.store = lrn.store
+        self.P = self.comm.size
+        self.vs = self.store.vstride
+        self.dev = lrn.device
+        self.cuda = self.dev.type == "cuda"
+        self.cs = torch.cuda.Stream(device=self.dev) if self.cuda else None
+        self.tau = 1 if int(getattr(lrn.conf, "max_concurrency", 2) or 2) >= 2 else 0
+        self.epoch = 0
+        self.job = None     # (keys, LocalizeJob | finished tuple, carried step)
+        self.pull = None    # opened, reply not yet exchanged
+        self.push = None    # push in flight to the owners
+        self.uhint = 0
+
+    # ------------------------------------------------------------ streams
+    def _S(self):
+        return torch.cuda.current_stream(self.dev) if self.cuda else None
+
+    @contextlib.contextmanager
+    def _on_cs(self, *inputs):
+        """Run a collective on the comm stream after the compute stream's
+        queued work; its outputs are consumed on S after :meth:`_join`."""
+        if not self.cuda:
+            yield
+            return
+        S = self._S()
+        self.cs.wait_stream(S)
+        for t in inputs:
+            if t is not None and t.is_cuda:
+                t.record_stream(self.cs)
+        with torch.cuda.stream(self.cs):
+            yield
+
+    def _mark(self):
+        if not self.cuda:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(self.cs)
+        return ev
+
+    def _join(self, ev, *outputs):
+        if ev is None:
+            return
+        S = self._S()
+        S.wait_event(ev)
+        for t in outputs:
+            if t is not None and t.is_cuda:
+                t.record_stream(S)
+
+    # ------------------------------------------------------------ localize
+    def _exchange(self, carried):
+        """The C0 closure handed to localize: owner counts + overflow flag +
+        the carried step's per-peer V row counts, all-to-all on the comm
+        stream, then (payload, stream, 3, P) for the native job's read."""
+        P = self.P
+
+        def ex(owner_cnt):
+            with self._on_cs(owner_cnt, carried.vcnt if carried is not None else None):
+                send = torch.zeros(P, 3, dtype=torch.int64, device=owner_cnt.device)
+                send[:, 0] = owner_cnt[:P]
+                send[:, 1] = owner_cnt[P]
+                vc = carried.vcnt if carried is not None else torch.zeros(
+                    P, dtype=torch.int64, device=owner_cnt.device)
+                send[:, 2] = vc
+                recv = self.comm.exchange_counts_dev(send.reshape(-1))
+                payload = torch.cat([owner_cnt, recv.reshape(-1), vc])
+            if self.cuda:
+                return payload, self.cs.cuda_stream, 3, P
+            return payload
+        return ex
+
+    def _begin(self, keys, offset, val, carried, ready=None):
+        lrn = self.lrn
+        if ready is not None and self.cuda:
+            S = self._S()
+            S.wait_event(ready)
+            for t in (keys, offset, val):
+                if t is not None:
+                    t.record_stream(S)
+        k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
+        ex = self._exchange(carried)
+        if self.cuda:
+            job = _native.hip().LocalizeJob(k, offset, val, self.P, int(self.uhint), ex)
+        else:
+            out = list(_native.host().localize_cpu(k, offset, val, self.P))
+            oc = torch.cat([out[2].to(torch.int64), torch.zeros(1, dtype=torch.int64)])
+            payload = ex(oc)
+            out[2] = oc[:self.P].clone()
+            out.append(payload[self.P + 1:].clone())
+            job = tuple(out)
+        self.job = (keys, job, carried)
+
+    def _finish(self):
+        keys, job, carried = self.job
+        self.job = None
+        out = tuple(job) if isinstance(job, tuple) else tuple(job.finish())
+        P = self.P
+        tail = out[7].tolist()
+        recv = tail[0:3 * P:3]
+        if carried is not None:
+            carried.vrecv = tail[2:3 * P:3]
+            carried.vown = tail[3 * P:4 * P]
+        send = [int(x) for x in out[2].tolist()]
+        return out, send, [int(x) for x in recv], carried
+
+    def _localized(self, keys, offset, val):
+        """Finish this minibatch's localize (begun by the previous call or
+        now); returns (loc, send, recv)."""
+        if self.job is None or self.job[0] is not keys:
+            if self.job is not None:
+                self._finish()  # a stale job (never expected): discard in order
+            self._begin(keys, offset, val, self.pull if (self.pull is not None and
+                                                         self.pull.vown is None) else None)
+        return self._finish()
+
+    def _vcount_exchange(self, st):
+        """Standalone C0 for a step whose V row counts rode on no localize
+        (pipeline drain, validation): one extra host read."""
+        P = self.P
+        send = torch.zeros(P, 3, dtype=torch.int64, device=self.dev)
+        with self._on_cs(st.vcnt):
+            send[:, 2] = st.vcnt
+            recv = self.comm.exchange_counts_dev(send.reshape(-1))
+            both = torch.cat([recv.reshape(-1), st.vcnt]).cpu()
+        v = both.tolist()
+        st.vrecv = v[2:3 * P:3]
+        st.vown = v[3 * P:4 * P]
+
+    # ---------------------------------------------------------------- tables
+    def _upload(self, st, prev):
+        """Device copies of the host-known segment tables of `st` (and the V
+        row counts of `prev`): one pinned host -> device copy."""
+        P = self.P
+        st.Hw = [_cdiv(2 * n, self.vs) for n in st.send]
+        st.Ho = [_cdiv(2 * n, self.vs) for n in st.recv]
+        a = np.zeros(4 * (P + 1) + P, dtype=np.int64)
+        a[1:P + 1] = np.cumsum(st.send)
+        a[P + 2:2 * P + 2] = np.cumsum(st.Hw)
+        a[2 * P + 3:3 * P + 3] = np.cumsum(st.recv)
+        a[3 * P + 4:4 * P + 4] = np.cumsum(st.Ho)
+        if prev is not None:
+            a[4 * P + 4:] = prev.vrecv
+        t = torch.from_numpy(a)
+        if self.cuda:
+            t = t.pin_memory().to(self.dev, non_blocking=True)
+        st.tabs = t
+        st.segS_w, st.segHS_w = t[0:P + 1], t[P + 1:2 * P + 2]
+        st.segS_o, st.segHS_o = t[2 * P + 2:3 * P + 3], t[3 * P + 3:4 * P + 4]
+        if prev is not None:
+            prev.vrecv_d = t[4 * P + 4:]
+
+    # -------------------------------------------------------------- phases
+    def _open(self, st, insert):
+        lrn = self.lrn
+        U = st.U
+        if st.use_cnt:
+            rec = torch.empty(U, 3, dtype=torch.int32, device=self.dev)
+            rec[:, 0:2] = st.uniq.view(torch.int32).view(U, 2)
+            rec[:, 2] = st.ucnt
+        else:
+            rec = st.uniq
+        with self._on_cs(rec):
+            keys_o = self.comm.all_to_all_v(rec, st.send, st.recv)
+        self._join(self._mark(), keys_o)
+        n = sum(st.recv)
+        lrn.kv.guard.before_open(n, self._remap)
+        self.epoch = self.epoch % 255 + 1
+        st.keys_o = keys_o
+        st.slot, st.vpos, st.chain, st.rbuf, st.vcnt = self.store.ps_open(
+            keys_o, st.use_cnt, st.segS_o, st.segHS_o, sum(st.Ho) + n, insert, st.train,
+            self.epoch, lrn.hp,
+            lrn.threshold, lrn.l1_shrk, lrn.seed)
+        lrn.kv.guard.after_open()
+
+    def _reply(self, st):
+        """C2 + worker unpack + forward (+ AUC) of an opened step."""
+        lrn = self.lrn
+        P = self.P
+        send_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
+        recv_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
+        with self._on_cs(st.rbuf):
+            rrecv = self.comm.all_to_all_v(st.rbuf[:sum(send_rows)], send_rows, recv_rows)
+        self._join(self._mark(), rrecv)
+        st.rrecv = rrecv
+        st.rbuf = None
+        st.hdr, st.rows = ops.ps_unpack(rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d)
+        st.py, st.dual, st.xv = ops.fm_forward(st.offset, st.lid, st.val, st.hdr, rrecv, self.vs,
+                                               st.label, ops.LOSS_LOGIT, lrn.met)
+        ops.auc_acc(st.py, st.label, lrn.auc_sum)
+        lrn.n_mb += 1
+        lrn.last_sizes = (st.U, sum(st.vrecv))
+
+    def _grad(self, st):
+        """Backward + gradient post-processing + C3 of a forwarded step."""
+        lrn = self.lrn
+        emb = lrn.emb
+        P = self.P
+        csc_off, csc_row, csc_val = st.csc
+        gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, st.dual, st.xv, st.hdr, st.rrecv,
+                                  self.vs)
+        if emb is not None and (emb.grad_clipping > 0 or emb.dropout > 0 or
+                                emb.grad_normalization):
+            if emb.grad_normalization:  # header rows must not enter the norm
+                self._zero_header_rows(st, gvc)
+            ops.fm_grad_post(gvc, st.rows, lrn.dim, emb.grad_clipping, emb.dropout,
+                             lrn.seed + 7919 * st.seed_step + 1, bool(emb.grad_normalization))
+        ops.ps_pack_gw(gw, gvc, st.segS_w, st.segHS_w, st.vrecv_d)
+        send_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
+        recv_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
+        with self._on_cs(gvc):
+            gpush = self.comm.all_to_all_v(gvc, send_rows, recv_rows)
+        st.ev_push = self._mark()
+        st.gpush = gpush
+        # the worker-side tensors of this step are done
+        st.rrecv = st.hdr = st.dual = st.xv = st.lid = st.csc = None
+
+    def _zero_header_rows(self, st, gvc):
+        idx, base = [], 0
+        for q in range(self.P):
+            idx.extend(range(base, base + st.Hw[q]))
+            base += st.Hw[q] + st.vrecv[q]
+        if idx:
+            gvc[torch.tensor(idx, dtype=torch.int64, device=gvc.device)] = 0
+
+    def _owner_push(self, st):
+        lrn = self.lrn
+        self._join(st.ev_push, st.gpush)
+        self.store.ps_push(st.slot, st.vpos, st.chain, st.segS_o, st.segHS_o, st.gpush, lrn.hp,
+                           lrn.threshold, lrn.l1_shrk, lrn.seed)
+        st.gpush = st.slot = st.vpos = st.chain = st.keys_o = None
+
+    def _remap(self, remap):
+        """The table grew: translate the slot ids of in-flight steps."""
+        for st in (self.pull, self.push):
+            if st is not None and st.slot is not None and st.slot.numel():
+                st.slot = remap[st.slot.long()]
+
+    # ----------------------------------------------------------------- API
+    def _new_step(self, loc, send, recv, label, train, data_pass, prev):
+        lrn = self.lrn
+        st = _Step()
+        st.uniq, st.ucnt, _, st.lid, csc_off, csc_row, csc_val = loc[:7]
+        st.csc = (csc_off, csc_row, csc_val)
+        st.U = st.uniq.numel()
+        st.send, st.recv = send, recv
+        st.label = label
+        st.train = train
+        st.use_cnt = train and data_pass == 0
+        st.seed_step = lrn.step
+        self.uhint = st.U
+        self._upload(st, prev)
+        return st
+
+    def train(self, keys, offset, val, label, data_pass, next_batch):
+        loc, send, recv, carried = self._localized(keys, offset, val)
+        prev = self.pull
+        if prev is not None and prev.vown is None:
+            self._vcount_exchange(prev)
+        st = self._new_step(loc, send, recv, label, True, data_pass, prev)
+        st.offset, st.val = offset, val
+        if self.tau == 0:
+            if prev is not None:
+                self._reply(prev)
+                if prev.train:
+                    self._grad(prev)
+                    self._owner_push(prev)
+            self._open(st, True)
+            self.pull = st
+        else:
+            if prev is not None:
+                self._reply(prev)
+            if self.push is not None:
+                self._owner_push(self.push)
+                self.push = None
+            self._open(st, True)
+            self.pull = st
+        if next_batch is not None:
+            nk, no, nv = next_batch[:3]
+            self._begin(nk, no, nv, st, next_batch[3] if len(next_batch) > 3 else None)
+        if self.tau == 1 and prev is not None and prev.train:
+            self._grad(prev)
+            self.push = prev
+        self.lrn.step += 1
+
+    def evaluate(self, keys, offset, val, label):
+        """A validation / prediction minibatch: drain the training pipeline,
+        then open (no insert), reply and forward synchronously."""
+        self.flush()
+        loc, send, recv, _ = self._localized(keys, offset, val)
+        st = self._new_step(loc, send, recv, label, False, 1, None)
+        st.offset, st.val = offset, val
+        self._open(st, False)
+        self._vcount_exchange(st)
+        self._upload_vrecv(st)
+        self._reply(st)
+        self.lrn.step += 1
+        return st.py
+
+    def _upload_vrecv(self, st):
+        t = torch.tensor(st.vrecv, dtype=torch.int64)
+        st.vrecv_d = t.pin_memory().to(self.dev, non_blocking=True) if self.cuda else t
+
+    def flush(self):
+        """Complete every minibatch in flight (end of a pass, before reading
+        or saving the model, end of a timed run)."""
+        if self.job is not None and self.job[2] is not None:
+            # the next minibatch's localize already carries the last pull's
+            # V counts: finish it now (keeping its result for the next call)
+            keys = self.job[0]
+            out, send, recv, _ = self._finish()
+            self.job = (keys, tuple(out[:7]) + (torch.tensor(
+                [x for q in range(self.P) for x in (recv[q], 0, 0)] + [0] * self.P,
+                dtype=torch.int64),), None)
+        st = self.pull
+        if st is not None:
+            if st.vown is None:
+                self._vcount_exchange(st)
+            self._upload_vrecv(st)
+            self._reply(st)
+            if st.train:
+                self._grad(st)
+        if self.push is not None:
+            self._owner_push(self.push)
+            self.push = None
+        if st is not None and st.train:
+            self._owner_push(st)
+        self.pull = None

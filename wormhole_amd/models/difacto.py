@@ -56,6 +56,12 @@ class DifactoLearner:
         # (same semantics: the push is applied before the next lookup)
         self.defer_push = True
         self.step = 0
+        self.last_sizes = None
+        # P > 1 shards: the lean pipelined exchange (kv/psx.py)
+        self.psx = None
+        if comm.size > 1 and self.vstride > 0 and self.kv.nshard == comm.size:
+            from ..kv.psx import PsxDifacto
+            self.psx = PsxDifacto(self)
 
     # ------------------------------------------------------------------ step
     def _localize(self, keys, offset, val, next_batch):
@@ -64,6 +70,12 @@ class DifactoLearner:
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):
         """One minibatch. Returns predictions (py) for PRED, else None."""
         train = wtype == TRAIN
+        if self.psx is not None:
+            if train:
+                self.psx.train(keys, offset, val, label, data_pass, next_batch)
+                return None
+            py = self.psx.evaluate(keys, offset, val, label)
+            return py if wtype == PRED else None
         with trace.span("localize"):
             loc = self._localize(keys, offset, val, next_batch)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
@@ -99,6 +111,8 @@ class DifactoLearner:
     def flush(self):
         """Complete the last minibatch's deferred push (before reading the
         model: progress counters, save, end of pass, end of a timed run)."""
+        if self.psx is not None:
+            self.psx.flush()
         self.kv.flush()
 
     def take_progress(self):

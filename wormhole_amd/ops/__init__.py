@@ -219,3 +219,17 @@ def key_mod(keys, max_key):
     import numpy as np
     k = keys.contiguous().numpy().view(np.uint64) % np.uint64(max_key)
     return torch.from_numpy(k.view(np.int64).copy())
+
+
+def ps_unpack(rbuf, U, segS, segHS, vrecv):
+    """Worker side of the multi-shard pull (kv/psx.py): (hdr [U, 2], rows [1])."""
+    if _gpu(rbuf):
+        return tuple(_native.hip().ps_unpack(rbuf, int(U), segS, segHS, vrecv))
+    return ref.ps_unpack(rbuf, U, segS, segHS, vrecv)
+
+
+def ps_pack_gw(gw, gbuf, segS, segHS, vrecv):
+    """gw [U] into the header rows of the multi-shard push buffer (in place)."""
+    if _gpu(gw):
+        return _native.hip().ps_pack_gw(gw, gbuf, segS, segHS, vrecv)
+    return ref.ps_pack_gw(gw, gbuf, segS, segHS, vrecv)

@@ -236,3 +236,41 @@ def dequant_rows(q, w, nb):
 
 def trunc_u8(c):
     return c.clamp(0, 255).to(torch.uint8)
+
+
+# ------------------------------------------------- multi-shard exchange (psx)
+def ps_unpack(rbuf, U, segS, segHS, vrecv):
+    """Worker side of the P-shard pull (oracle of psx.hip k_ps_unpack):
+    hdr [U, 2] {w, row of the key's embedding inside rbuf or -1}, rows [1]."""
+    vs = rbuf.shape[1]
+    S = [int(x) for x in segS.tolist()]
+    HS = [int(x) for x in segHS.tolist()]
+    vr = [int(x) for x in vrecv.tolist()]
+    flat = rbuf.reshape(-1)
+    hdr = torch.zeros(U, 2, dtype=torch.float32)
+    hv = hdr.view(torch.int32)
+    VS = 0
+    for q in range(len(S) - 1):
+        a, b = S[q], S[q + 1]
+        base = (HS[q] + VS) * vs
+        pairs = flat[base:base + 2 * (b - a)].reshape(-1, 2)
+        j = pairs.contiguous().view(torch.int32)[:, 1]
+        hdr[a:b, 0] = pairs[:, 0]
+        hv[a:b, 1] = torch.where(j >= 0, HS[q + 1] + VS + j, torch.full_like(j, -1))
+        VS += vr[q]
+    return hdr, torch.tensor([HS[-1] + VS], dtype=torch.int64)
+
+
+def ps_pack_gw(gw, gbuf, segS, segHS, vrecv):
+    """gw [U] into the header rows of the push buffer (in place)."""
+    vs = gbuf.shape[1]
+    S = [int(x) for x in segS.tolist()]
+    HS = [int(x) for x in segHS.tolist()]
+    vr = [int(x) for x in vrecv.tolist()]
+    flat = gbuf.view(-1)
+    VS = 0
+    for q in range(len(S) - 1):
+        a, b = S[q], S[q + 1]
+        base = (HS[q] + VS) * vs
+        flat[base:base + (b - a)] = gw[a:b]
+        VS += vr[q]

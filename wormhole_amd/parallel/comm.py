@@ -224,3 +224,54 @@ class Comm:
     def finalize(self):
         if self.size > 1 and dist.is_initialized():
             dist.destroy_process_group()
+
+
+class LoopbackComm(Comm):
+    """``nshard`` virtual ranks in ONE process: every exchange is the
+    identity (peer q sends this rank exactly what this rank sends q), so the
+    multi-shard parameter-server code path -- owner grouping, packed records,
+    row-aligned regions, multi-segment owner kernels, the pipelined step --
+    runs end to end on a single GPU with no transport underneath. Used to
+    measure that path's device and host overhead on one GPU (``bench.py
+    --loopback P``); it owns every shard itself, so its table holds the whole
+    key space like a 1-rank run."""
+
+    def __init__(self, nshard, device=None):
+        self.rank = 0
+        self.size = int(nshard)
+        self.device = torch.device(device if device is not None else "cpu")
+        self.backend = "loopback"
+        self.stage = False
+        self.pg = None
+
+    def barrier(self):
+        pass
+
+    def allreduce(self, t, op="sum"):
+        return t
+
+    def broadcast(self, t, root=0):
+        return t
+
+    def allgather_object(self, obj):
+        return [obj] * self.size
+
+    def allgather(self, t):
+        return [t] * self.size
+
+    def exchange_counts(self, send_counts):
+        return list(send_counts)
+
+    def all_to_all_v(self, x, send_rows, recv_rows):
+        assert list(send_rows) == list(recv_rows), "loopback exchange must be symmetric"
+        return x
+
+    def all_to_all_v_multi(self, items, async_op=False):
+        outs = [self.all_to_all_v(x, s, r) for x, s, r in items]
+        return (outs, _Done()) if async_op else outs
+
+    def exchange_counts_dev(self, send_dev):
+        return send_dev.clone()
+
+    def finalize(self):
+        pass
