@@ -282,6 +282,7 @@ void register_all(py::module& m) {
     i32("load_iter", &c.load_iter); i32("num_parts_per_file", &c.num_parts_per_file);
     f64("print_sec", &c.print_sec); bol("local_data", &c.local_data);
     bol("early_stop", &c.early_stop); f64("min_objv_decr", &c.min_objv_decr);
+    bol("resume", &c.resume);
     if (conf.contains("max_objv") && !conf["max_objv"].is_none()) {
       c.has_max_objv = true;
       c.max_objv = py::cast<double>(conf["max_objv"]);

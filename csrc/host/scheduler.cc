@@ -9,8 +9,12 @@
 //     worker's response marks its part done (data_parallel.h:93-158);
 //   * progress vectors from the workers are sum-merged and printed every
 //     print_sec in the reference table layout (linear/difacto progress.h);
-//   * a dead worker's connection re-queues its parts and fails the job
-//     (checkpoint-restart recovery);
+//   * a dead worker's connection re-queues its parts and fails the job; the
+//     launcher restarts it (--max-restart) and the restarted scheduler
+//     resumes from the newest checkpoint whose save completed (every
+//     periodic save is sealed by a `<model_out>_iter-<k>.done` marker once
+//     all workers acknowledged it; SURVEY §5.3, reference
+//     data_parallel.h:131-135 + minibatch_solver.h:96-109);
 //   * DiFacto stop rules: training objective above max_objv, or a validation
 //     decrease below min_objv_decr with early_stop (difacto/async_sgd.h:14-55).
 // Messages are JSON objects over the Van (csrc/host/van.cc).
@@ -20,6 +24,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <fstream>
 #include <memory>
 #include <stdexcept>
 
@@ -309,7 +314,11 @@ void Scheduler::Run() {
   if (is_pred && c_.model_in.empty())
     throw std::runtime_error("should provide model_in for predicting");
   int cur = 0;
-  if (!c_.model_in.empty()) {
+  if (c_.resume && !c_.model_in.empty()) {
+    out(fmt("Resuming from the model saved at iter = %d", c_.load_iter));
+    Command("load", c_.model_in, c_.load_iter);
+    cur = c_.load_iter + 1;
+  } else if (!c_.model_in.empty()) {
     if (c_.load_iter > 0) {
       out(fmt("Loading model from iter = %d", c_.load_iter));
       cur = c_.load_iter;
@@ -339,6 +348,9 @@ void Scheduler::Run() {
     if (!c_.model_out.empty() && c_.save_iter > 0 && (cur + 1) % c_.save_iter == 0) {
       out(fmt("Saving model for iter = %d", cur));
       Command("save", c_.model_out, cur);
+      // seal the checkpoint: every worker acknowledged its shard
+      std::ofstream mark(ResolvePath(c_.model_out) + fmt("_iter-%d.done", cur));
+      mark << workers_.size() << "\n";
     }
     ++cur;
   }

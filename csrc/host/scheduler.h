@@ -20,6 +20,9 @@ struct SchedulerConf {
   int max_data_pass = 10, save_iter = -1, load_iter = -1, num_parts_per_file = 10;
   double print_sec = 1;
   bool local_data = false;
+  // restart of a failed job (launcher --max-restart): model_in / load_iter
+  // name the newest complete checkpoint and training resumes right after it
+  bool resume = false;
   // difacto stop rules (learn/difacto/async_sgd.h:14-55)
   bool early_stop = false;
   double min_objv_decr = 1e-5;

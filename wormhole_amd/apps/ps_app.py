@@ -33,14 +33,39 @@ def _conf_cls(kind):
     return schema.LinearConfig if kind == "linear" else schema.DifactoConfig
 
 
+def latest_checkpoint(model_out):
+    """Newest iteration k whose periodic save completed (the scheduler seals
+    it with ``<model_out>_iter-<k>.done``), or -1."""
+    import glob
+    import re
+    from ..utils.fs import resolve
+    base = resolve(model_out)
+    best = -1
+    for f in glob.glob(glob.escape(base) + "_iter-*.done"):
+        m = re.match(r".*_iter-(\d+)\.done$", f)
+        if m:
+            best = max(best, int(m.group(1)))
+    return best
+
+
 def scheduler_conf(kind, conf):
-    """The fields the native scheduler (csrc/host/scheduler.cc) reads."""
+    """The fields the native scheduler (csrc/host/scheduler.cc) reads.
+
+    On a restarted job (launcher ``--max-restart``: WH_RESTART_ATTEMPT > 0)
+    with periodic saves, training resumes after the newest sealed
+    checkpoint instead of starting over (reference: reload with model_in /
+    load_iter, learn/solver/minibatch_solver.h:96-109)."""
     d = {"app": kind}
+    attempt = int(os.environ.get("WH_RESTART_ATTEMPT", "0") or 0)
+    if attempt > 0 and conf.model_out and int(conf.save_iter or 0) > 0:
+        k = latest_checkpoint(conf.model_out)
+        if k >= 0:
+            d.update(model_in=conf.model_out, load_iter=k, resume=True)
     for k in ("train_data", "val_data", "data_format", "model_in", "model_out", "predict_out",
               "max_data_pass", "save_iter", "load_iter", "num_parts_per_file", "print_sec",
               "local_data"):
         v = getattr(conf, k, None)
-        if v is not None:
+        if v is not None and k not in d:
             d[k] = v
     if kind == "difacto":
         d["early_stop"] = bool(conf.early_stop)

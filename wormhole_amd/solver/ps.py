@@ -54,6 +54,8 @@ def _parse_fault(spec, rank):
     kind, r, arg = spec.split(":")
     if int(r) != rank:
         return None
+    if kind == "kill" and int(os.environ.get("WH_RESTART_ATTEMPT", "0") or 0) > 0:
+        return None  # the injected failure happens once; the restarted job runs clean
     return kind, float(arg)
 
 
