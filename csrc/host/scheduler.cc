@@ -11,9 +11,9 @@
 //     print_sec in the reference table layout (linear/difacto progress.h);
 //   * a dead worker's connection re-queues its parts and fails the job; the
 //     launcher restarts it (--max-restart) and the restarted scheduler
-//     resumes from the newest checkpoint whose save completed (every
-//     periodic save is sealed by a `<model_out>_iter-<k>.done` marker once
-//     all workers acknowledged it; SURVEY §5.3, reference
+//     resumes from the newest checkpoint whose save completed on every
+//     shard (each worker seals its shard file with a `.ok` marker once it
+//     and its optimizer-state side file are written; SURVEY §5.3, reference
 //     data_parallel.h:131-135 + minibatch_solver.h:96-109);
 //   * DiFacto stop rules: training objective above max_objv, or a validation
 //     decrease below min_objv_decr with early_stop (difacto/async_sgd.h:14-55).
@@ -24,7 +24,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
-#include <fstream>
+#include <cstdlib>
 #include <memory>
 #include <stdexcept>
 
@@ -151,11 +151,13 @@ void Scheduler::OnDead(const std::string& who) {
                            "model (model_in / load_iter)");
 }
 
-void Scheduler::Command(const std::string& cmd, const std::string& file, int iter) {
+void Scheduler::Command(const std::string& cmd, const std::string& file, int iter,
+                        bool resume) {
   Broadcast(Json::Obj()
                 .set("cmd", Json::Str(cmd))
                 .set("file", Json::Str(file))
                 .set("iter", Json::Num(iter))
+                .set("resume", Json::Bool(resume))
                 .Dump());
   int acks = 0;
   while (acks < (int)workers_.size()) {
@@ -225,7 +227,16 @@ bool Scheduler::Iterate(int it, int wtype) {
       if (data.empty()) return false;
     }
   }
-  std::unique_ptr<WorkloadPool> pool(new WorkloadPool(train, (uint64_t)it + 1));
+  // straggler knobs (defaults = the reference's: 2x the mean part time, at
+  // least 5 s, after 10 finished parts) can be tuned per job from the env
+  auto envd = [](const char* k, double d) {
+    const char* v = std::getenv(k);
+    return v && *v ? std::atof(v) : d;
+  };
+  std::unique_ptr<WorkloadPool> pool(new WorkloadPool(
+      train, (uint64_t)it + 1, envd("WH_STRAGGLER_FACTOR", 2.0), envd("WH_STRAGGLER_MIN_SEC", 5.0),
+      (int)envd("WH_STRAGGLER_MIN_DONE", 10)));
+  pool->set_verbose(envd("WH_POOL_VERBOSE", 0) != 0);
   pool_ = pool.get();
   if (c_.local_data) {
     // every worker matches the pattern on its own file system and its parts
@@ -316,7 +327,7 @@ void Scheduler::Run() {
   int cur = 0;
   if (c_.resume && !c_.model_in.empty()) {
     out(fmt("Resuming from the model saved at iter = %d", c_.load_iter));
-    Command("load", c_.model_in, c_.load_iter);
+    Command("load", c_.model_in, c_.load_iter, true);
     cur = c_.load_iter + 1;
   } else if (!c_.model_in.empty()) {
     if (c_.load_iter > 0) {
@@ -348,9 +359,6 @@ void Scheduler::Run() {
     if (!c_.model_out.empty() && c_.save_iter > 0 && (cur + 1) % c_.save_iter == 0) {
       out(fmt("Saving model for iter = %d", cur));
       Command("save", c_.model_out, cur);
-      // seal the checkpoint: every worker acknowledged its shard
-      std::ofstream mark(ResolvePath(c_.model_out) + fmt("_iter-%d.done", cur));
-      mark << workers_.size() << "\n";
     }
     ++cur;
   }

@@ -42,7 +42,7 @@ class Scheduler {
   void Broadcast(const std::string& msg);
   bool Recv(double timeout_s, std::string* who, Json* d);
   void OnDead(const std::string& who);
-  void Command(const std::string& cmd, const std::string& file, int iter);
+  void Command(const std::string& cmd, const std::string& file, int iter, bool resume = false);
   bool Iterate(int it, int wtype);
   int MatchOnWorkers(const std::string& pattern);
   bool Show(Printer* p, const std::vector<double>& agg, bool train);

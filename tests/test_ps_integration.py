@@ -142,11 +142,67 @@ def test_scheduler_dispatches_every_part_once(work):
 
 
 def test_killed_worker_fails_the_job(work):
+    """Without --max-restart a dead worker ends the job (its parameter shard
+    is gone)."""
     r = run(["-n", "2", "-s", "1", os.path.join(ROOT, "bin", "linear.dmlc"),
              "learn/linear/guide/demo.conf", "minibatch=100"], work,
             env_extra={"WH_FAULT": "kill:1:3"}, timeout=120)
     assert r.returncode != 0
     assert "WH_FAULT" in r.stderr
+
+
+def _final_val_logloss(out):
+    vals = [float(l.split()[4]) for l in out.splitlines() if re.match(r"^\s+\d+\s+1\.61e\+03", l)]
+    return vals
+
+
+@pytest.mark.parametrize("app,conf", [("linear", "learn/linear/guide/demo.conf"),
+                                      ("difacto", "learn/difacto/guide/demo.conf")])
+def test_killed_worker_job_resumes(work, app, conf):
+    """--max-restart: the launcher restarts the whole PS job; the scheduler
+    finds the newest checkpoint sealed on every shard and resumes training
+    right after it (reference: dead node's parts re-queued,
+    data_parallel.h:131-135; restart from model_in/load_iter,
+    minibatch_solver.h:96-109). The job completes its passes and ends where
+    a no-fault run ends."""
+    args = ["-n", "2", "-s", "2", os.path.join(ROOT, "bin", app + ".dmlc"), conf,
+            "minibatch=100", "save_iter=1", "max_data_pass=3", "model_out=./m"]
+    r = run(["--max-restart", "1"] + args, work, env_extra={"WH_FAULT": "kill:1:45"},
+            timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "WH_FAULT: killing" in r.stderr and "restarting the job" in r.stderr
+    assert "Resuming from the model saved at iter = 0" in r.stdout, r.stdout
+    assert "Hit max number of data passes 3" in r.stdout
+    for p in range(2):
+        assert os.path.exists(work / ("m_part-%d" % p))
+        assert os.path.exists(work / ("m_iter-0_part-%d.ok" % p))
+    ref_dir = work / "nofault"
+    ref_dir.mkdir()
+    os.symlink(os.path.join(ROOT, "learn"), ref_dir / "learn")
+    r0 = run(args, ref_dir, timeout=300)
+    assert r0.returncode == 0, r0.stderr[-3000:]
+    # the resumed run reaches (within dispatch-order noise) the same model
+    if app == "linear":
+        a, b = _final_val_logloss(r.stdout), _final_val_logloss(r0.stdout)
+        assert a and b and abs(a[-1] - b[-1]) < 0.02, (a, b)
+
+
+def test_straggler_part_requeued_end_to_end(work):
+    """A worker that stalls on its part: the scheduler's pool re-queues the
+    part after the straggler bound and another worker takes it; the job
+    still covers the data and completes (reference
+    learn/base/workload_pool.h:197-228)."""
+    r = run(["-n", "2", "-s", "1", os.path.join(ROOT, "bin", "linear.dmlc"),
+             "learn/linear/guide/demo.conf", "minibatch=100", "max_data_pass=1",
+             "num_parts_per_file=20", 'val_data=""'], work,
+            env_extra={"WH_FAULT": "stall:1:4:12", "WH_STRAGGLER_MIN_SEC": "1",
+                       "WH_STRAGGLER_MIN_DONE": "1", "WH_POOL_VERBOSE": "1"}, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "WH_FAULT: stalling" in r.stderr
+    assert "reassign" in r.stderr, r.stderr[-3000:]
+    ttl = [float(l.split()[1]) for l in r.stdout.splitlines()
+           if re.match(r"^\s+\d+\s+[\d.e+]+\s+[\d.e+]+\s", l)]
+    assert ttl and ttl[-1] >= 6513  # every example trained at least once
 
 
 def test_linear_local_data(work):

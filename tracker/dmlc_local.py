@@ -15,8 +15,11 @@ Every worker gets the torch.distributed rendezvous (RANK, WORLD_SIZE,
 LOCAL_RANK, MASTER_ADDR=127.0.0.1, MASTER_PORT) and the DMLC_* role
 variables; worker i is pinned to GPU i mod #GPUs via LOCAL_RANK.  The
 launcher monitors the children: the first failure terminates the job
-(process groups), and ``--max-restart K`` relaunches a failed BSP job up to K
-times (ranks resume from their last checkpoint).
+(process groups), and ``--max-restart K`` relaunches a failed job up to K
+times with WH_RESTART_ATTEMPT set: BSP ranks resume from their
+last versioned checkpoint; a parameter-server job resumes after the newest
+``save_iter`` checkpoint sealed on every shard (its scheduler loads it as
+model_in / load_iter and continues with the next pass).
 """
 import argparse
 import os
@@ -93,7 +96,8 @@ def main(argv=None):
     ap.add_argument("-n", "--num-workers", type=int, required=True)
     ap.add_argument("-s", "--num-servers", type=int, default=0)
     ap.add_argument("--max-restart", type=int, default=0,
-                    help="relaunch a failed BSP job up to this many times")
+                    help="relaunch a failed job up to this many times (BSP: from the last "
+                         "checkpoint; PS: after the last sealed save_iter checkpoint)")
     ap.add_argument("command", nargs=argparse.REMAINDER)
     args = ap.parse_args(argv)
     if not args.command:

@@ -33,22 +33,24 @@ def _conf_cls(kind):
     return schema.LinearConfig if kind == "linear" else schema.DifactoConfig
 
 
-def latest_checkpoint(model_out):
-    """Newest iteration k whose periodic save completed (the scheduler seals
-    it with ``<model_out>_iter-<k>.done``), or -1."""
+def latest_checkpoint(model_out, nshard):
+    """Newest iteration k whose periodic save completed on every shard (each
+    worker seals its shard with ``<model_out>_iter-<k>_part-<r>.ok`` once
+    the shard and its resume state are written), or -1."""
     import glob
     import re
     from ..utils.fs import resolve
     base = resolve(model_out)
-    best = -1
-    for f in glob.glob(glob.escape(base) + "_iter-*.done"):
-        m = re.match(r".*_iter-(\d+)\.done$", f)
+    seen = {}
+    for f in glob.glob(glob.escape(base) + "_iter-*_part-*.ok"):
+        m = re.match(r".*_iter-(\d+)_part-(\d+)\.ok$", f)
         if m:
-            best = max(best, int(m.group(1)))
-    return best
+            seen.setdefault(int(m.group(1)), set()).add(int(m.group(2)))
+    done = [k for k, parts in seen.items() if parts >= set(range(nshard))]
+    return max(done) if done else -1
 
 
-def scheduler_conf(kind, conf):
+def scheduler_conf(kind, conf, nshard=1):
     """The fields the native scheduler (csrc/host/scheduler.cc) reads.
 
     On a restarted job (launcher ``--max-restart``: WH_RESTART_ATTEMPT > 0)
@@ -58,7 +60,7 @@ def scheduler_conf(kind, conf):
     d = {"app": kind}
     attempt = int(os.environ.get("WH_RESTART_ATTEMPT", "0") or 0)
     if attempt > 0 and conf.model_out and int(conf.save_iter or 0) > 0:
-        k = latest_checkpoint(conf.model_out)
+        k = latest_checkpoint(conf.model_out, nshard)
         if k >= 0:
             d.update(model_in=conf.model_out, load_iter=k, resume=True)
     for k in ("train_data", "val_data", "data_format", "model_in", "model_out", "predict_out",
@@ -78,7 +80,7 @@ def scheduler_conf(kind, conf):
 def run_scheduler(host, kind, conf, nw, ns, van):
     """The native scheduler (GIL released while it runs); a short grace period
     lets the workers read the final exit command before the van closes."""
-    host.run_scheduler(scheduler_conf(kind, conf), nw, ns, van)
+    host.run_scheduler(scheduler_conf(kind, conf, ns), nw, ns, van)
     time.sleep(0.2)
 
 

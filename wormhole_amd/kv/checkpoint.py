@@ -64,15 +64,16 @@ def save_difacto(store, path):
 
 def _gather(store, kind):
     """Snapshot of the occupied entries as tensors on the store's device
-    (gathers only: the live table can be updated as soon as they ran)."""
+    (gathers only: the live table can be updated as soon as they ran).
+    z / sq / cnt also feed the resume side file (:func:`write_state`)."""
     slots = _occupied(store)
 
     def g(t):
         return t[slots.to(t.device)] if t.numel() else t.new_zeros(0)
 
-    snap = {"keys": g(store.keys), "w": g(store.w)}
+    snap = {"keys": g(store.keys), "w": g(store.w), "z": g(store.z), "sq": g(store.sq),
+            "cnt": g(store.cnt)}
     if kind == "difacto":
-        snap["z"], snap["sq"] = g(store.z), g(store.sq)
         dim = int(store.dim)
         if dim > 0 and slots.numel():
             vrow = g(store.vrow).long()
@@ -118,6 +119,48 @@ def _write(kind, snap, dim, path):
     return len(r1) + len(rv)
 
 
+# ------------------------------------------------------------ resume state
+# The reference shard formats omit optimizer state (linear keeps only w != 0,
+# DiFacto keeps no feature counts), so a job restarted from them would not
+# continue where it stopped. Next to every shard the worker writes
+# ``<shard>.state`` (every occupied entry: key, w, z, sq, count) and, once
+# both files are complete, ``<shard>.ok``; a restarted job resumes from the
+# newest iteration whose every shard is sealed (apps/ps_app.py).
+_STATE = np.dtype([("k", "<u8"), ("w", "<f4"), ("z", "<f4"), ("sq", "<f4"), ("cnt", "<u4")])
+
+
+def write_state(snap, path):
+    rec = np.zeros(len(snap["keys"]), dtype=_STATE)
+    rec["k"] = snap["keys"].astype(np.uint64)
+    rec["w"], rec["z"], rec["sq"] = snap["w"], snap["z"], snap["sq"]
+    rec["cnt"] = snap["cnt"].astype(np.uint32)
+    with open_uri(path + ".state", "wb") as f:
+        f.write(rec.tobytes())
+    with open_uri(path + ".ok", "w") as f:
+        f.write("%d\n" % len(rec))
+
+
+def load_state(store, path):
+    """Restore the full optimizer state saved next to a shard (if any)."""
+    import os
+    from ..utils.fs import resolve
+    if not os.path.exists(resolve(path + ".state")):
+        return 0
+    rec = np.frombuffer(open_uri(path + ".state", "rb").read(), dtype=_STATE)
+    kt = torch.from_numpy(rec["k"].view(np.int64).copy())
+    _put(store, kt, {"w": torch.from_numpy(rec["w"].copy()),
+                     "z": torch.from_numpy(rec["z"].copy()),
+                     "sq": torch.from_numpy(rec["sq"].copy()),
+                     "cnt": torch.from_numpy(rec["cnt"].view(np.int32).copy())})
+    return len(rec)
+
+
+def _write_all(kind, snap, dim, path):
+    n = _write(kind, snap, dim, path)
+    write_state(snap, path)
+    return n
+
+
 class AsyncSaver:
     """Model-shard saves that do not stall training.
 
@@ -136,7 +179,8 @@ class AsyncSaver:
     def save(self, kind, store, path):
         dev = store.keys.device
         if dev.type != "cuda":
-            return _write(kind, _numpy(_gather(store, kind)), int(getattr(store, "dim", 0)), path)
+            return _write_all(kind, _numpy(_gather(store, kind)), int(getattr(store, "dim", 0)),
+                              path)
         import threading
         main = torch.cuda.current_stream(dev)
         if self._stream is None:
@@ -161,7 +205,7 @@ class AsyncSaver:
         def finish():
             try:
                 copied.synchronize()
-                box["n"] = _write(kind, {k: v.numpy() for k, v in host.items()}, dim, path)
+                box["n"] = _write_all(kind, {k: v.numpy() for k, v in host.items()}, dim, path)
             except BaseException as e:  # surfaced by join()
                 box["err"] = e
 

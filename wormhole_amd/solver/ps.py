@@ -48,12 +48,16 @@ def _log(*a):
 
 def _parse_fault(spec, rank):
     """WH_FAULT=kill:<rank>:<after_n_minibatches> | sleep:<rank>:<sec_per_minibatch>
-    (fault injection for the failure / straggler tests)."""
+    | stall:<rank>:<sec>[:<after_n_minibatches>] (once) -- fault injection for
+    the failure / straggler tests. A kill fires only in the
+    first attempt of a job (the launcher's restart runs clean)."""
     if not spec:
         return None
-    kind, r, arg = spec.split(":")
+    kind, r, arg, *after = spec.split(":")
     if int(r) != rank:
         return None
+    if kind == "stall":
+        return kind, float(arg), int(after[0]) if after else 0
     if kind == "kill" and int(os.environ.get("WH_RESTART_ATTEMPT", "0") or 0) > 0:
         return None  # the injected failure happens once; the restarted job runs clean
     return kind, float(arg)
@@ -122,6 +126,8 @@ class Worker:
                     name = checkpoint.model_name(d["file"], d["iter"], self.comm.rank)
                     fn = checkpoint.load_linear if self.kind == "linear" else checkpoint.load_difacto
                     fn(self.learner.store, name)
+                    if d.get("resume"):
+                        checkpoint.load_state(self.learner.store, name)
                 self.comm.barrier()
                 self.send(msg="ack")
             elif cmd == "match":
@@ -130,12 +136,16 @@ class Worker:
                 self.run_pass(d["type"], d["data_pass"], d.get("fmt", self.conf.data_format))
 
     def _inject_fault(self):
-        kind, arg = self.fault
+        kind, arg = self.fault[:2]
         if kind == "kill" and self.n_done >= arg:
             _log("[worker %d] WH_FAULT: killing myself after %d minibatches" % (
                 self.comm.rank, self.n_done))
             os._exit(17)
         if kind == "sleep":
+            time.sleep(arg)
+        if kind == "stall" and self.n_done >= self.fault[2]:
+            self.fault = None
+            _log("[worker %d] WH_FAULT: stalling %.1f s" % (self.comm.rank, arg))
             time.sleep(arg)
 
     # -------------------------------------------------------- one pass
