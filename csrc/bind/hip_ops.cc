@@ -508,12 +508,12 @@ class KVStore {
   // Owner side of a P-shard minibatch. keys: int64 [n] or int32 records
   // [n, 3] {key lo, key hi, count}; segS / segHS: device int64 [P+1]; rows_cap:
   // rows of the reply buffer to allocate (>= segHS[P] + n). Returns (slot,
-  // vpos [n+1], chain [n] (int32 view of the chain words), rbuf
-  // [rows_cap, vstride], vcnt [P]).
+  // vpos [n+1], chain [n] (int32 view of the chain links), head uint8 [n],
+  // rbuf [rows_cap, vstride], vcnt [P]).
   std::vector<Tensor> ps_open(const Tensor& keys, bool use_cnt, const Tensor& segS,
                               const Tensor& segHS, int64_t rows_cap, bool insert, bool chains,
-                              int64_t epoch, const std::vector<double>& h, int64_t threshold,
-                              bool l1_shrk, int64_t seed) {
+                              const std::vector<double>& h, int64_t threshold, bool l1_shrk,
+                              int64_t seed) {
     CHECK_DEV(keys); CHECK_CONT(keys);
     CHECK_IN(segS, torch::kInt64);
     CHECK_IN(segHS, torch::kInt64);
@@ -526,7 +526,7 @@ class KVStore {
     const int P = (int)segS.numel() - 1;
     TORCH_CHECK(P >= 1 && segHS.numel() == P + 1, "ps_open: bad segment tables");
     TORCH_CHECK(n < (1 << 24), "ps_open: at most 2^24 - 1 keys per minibatch and shard");
-    TORCH_CHECK(epoch >= 1 && epoch <= 255, "ps_open: epoch must be in 1..255");
+    epoch_ = epoch_ % 255 + 1;  // 1..255; a wrap to 1 sweeps the table's tags
     TORCH_CHECK(rows_cap >= n, "ps_open: reply buffer too small");
     c10::DeviceGuard g(keys.device());
     auto s = cur_stream(keys);
@@ -536,25 +536,27 @@ class KVStore {
     auto wout = torch::empty({std::max<int64_t>(n, 1)}, f32);
     auto vpos = torch::empty({n + 1}, keys.options().dtype(torch::kInt64));
     auto chain = torch::empty({std::max<int64_t>(n, 1)}, i32);
+    auto head = torch::empty({std::max<int64_t>(n, 1)}, keys.options().dtype(torch::kUInt8));
     auto rbuf = torch::empty({rows_cap, (int64_t)vstride_}, f32);
     auto vcnt = torch::empty({P}, keys.options().dtype(torch::kInt64));
-    auto vbase = vnext_.clone();
+    if (!vbase_.defined()) vbase_ = torch::empty({1}, vnext_.options());
     const bool ok = wh::ps_open(
         table(), rec ? nullptr : reinterpret_cast<const uint64_t*>(keys.data_ptr()),
         rec ? ptr<int32_t>(keys) : nullptr, n, use_cnt ? 1 : 0, dhp(h, threshold, l1_shrk, seed),
-        insert ? 1 : 0, chains ? 1 : 0, (uint32_t)epoch, ptr<int32_t>(vbase), ptr<int64_t>(segS),
-        ptr<int64_t>(segHS), P, lookback(keys.device()), ptr<int32_t>(slot), ptr<float>(wout),
-        ptr<int64_t>(vpos), reinterpret_cast<uint32_t*>(chain.data_ptr()), ptr<float>(rbuf),
-        ptr<int64_t>(vcnt), s);
-    TORCH_CHECK(ok, "ps_open: limits exceeded (P <= 1024, n < 2^24)");
-    return {slot.narrow(0, 0, n), vpos, chain.narrow(0, 0, n), rbuf, vcnt};
+        insert ? 1 : 0, chains ? 1 : 0, (uint32_t)epoch_, ptr<int32_t>(vbase_),
+        ptr<int64_t>(segS), ptr<int64_t>(segHS), P, lookback(keys.device()), ptr<int32_t>(slot),
+        ptr<float>(wout), ptr<int64_t>(vpos), reinterpret_cast<uint32_t*>(chain.data_ptr()),
+        reinterpret_cast<uint8_t*>(head.data_ptr()), ptr<float>(rbuf), ptr<int64_t>(vcnt), s);
+    TORCH_CHECK(ok, "ps_open: limits exceeded (P <= 256, n < 2^24)");
+    return {slot.narrow(0, 0, n), vpos, chain.narrow(0, 0, n), head.narrow(0, 0, n), rbuf, vcnt};
   }
 
   // Owner side push of a P-shard minibatch: gbuf = the received push buffer
   // (rows in the reply layout of the matching ps_open).
   void ps_push(const Tensor& slot, const Tensor& vpos, const c10::optional<Tensor>& chain,
-               const Tensor& segS, const Tensor& segHS, const Tensor& gbuf,
-               const std::vector<double>& h, int64_t threshold, bool l1_shrk, int64_t seed) {
+               const c10::optional<Tensor>& head, const Tensor& segS, const Tensor& segHS,
+               const Tensor& gbuf, const std::vector<double>& h, int64_t threshold, bool l1_shrk,
+               int64_t seed) {
     CHECK_IN(slot, torch::kInt32);
     CHECK_IN(vpos, torch::kInt64);
     CHECK_IN(segS, torch::kInt64);
@@ -563,14 +565,18 @@ class KVStore {
     const int64_t n = slot.numel();
     TORCH_CHECK(vpos.numel() == n + 1, "ps_push: vpos size mismatch");
     const uint32_t* cp = nullptr;
+    const uint8_t* hp = nullptr;
     if (chain.has_value() && chain->defined()) {
       CHECK_IN((*chain), torch::kInt32);
-      TORCH_CHECK(chain->numel() == n, "ps_push: chain size mismatch");
+      TORCH_CHECK(head.has_value() && head->defined(), "ps_push: chain without head flags");
+      CHECK_IN((*head), torch::kUInt8);
+      TORCH_CHECK(chain->numel() == n && head->numel() == n, "ps_push: chain size mismatch");
       cp = reinterpret_cast<const uint32_t*>(chain->data_ptr());
+      hp = reinterpret_cast<const uint8_t*>(head->data_ptr());
     }
     const int P = (int)segS.numel() - 1;
     c10::DeviceGuard g(slot.device());
-    TORCH_CHECK(wh::ps_push(table(), ptr<int32_t>(slot), ptr<int64_t>(vpos), cp, n,
+    TORCH_CHECK(wh::ps_push(table(), ptr<int32_t>(slot), ptr<int64_t>(vpos), cp, hp, n,
                             ptr<int64_t>(segS), ptr<int64_t>(segHS), P, ptr<float>(gbuf),
                             dhp(h, threshold, l1_shrk, seed), cur_stream(slot)),
                 "ps_push: limits exceeded");
@@ -625,7 +631,8 @@ class KVStore {
   int64_t cap() const { return cap_; }
   int64_t vcap() const { return vcap_; }
 
-  Tensor slots_, keys_, w_, z_, sq_, cnt_, vrow_, V_, VG_, vnext_, stats_;
+  Tensor slots_, keys_, w_, z_, sq_, cnt_, vrow_, V_, VG_, vnext_, stats_, vbase_;
+  int64_t epoch_ = 0;  // ps_open chain-tag epoch (1..255)
 
  private:
   void set_slots(const Tensor& sl) {
@@ -771,6 +778,43 @@ std::vector<Tensor> ps_unpack(const Tensor& rbuf, int64_t U, const Tensor& segS,
                             ptr<int64_t>(rows), cur_stream(rbuf)),
               "ps_unpack: limits exceeded");
   return {hdr, rows};
+}
+
+// 12-byte key records {lo, hi, count} int32 [U, 3] (ucnt optional)
+Tensor ps_records(const Tensor& uniq, const c10::optional<Tensor>& ucnt) {
+  CHECK_IN(uniq, torch::kInt64);
+  const int32_t* cp = nullptr;
+  if (ucnt.has_value() && ucnt->defined()) {
+    CHECK_IN((*ucnt), torch::kInt32);
+    TORCH_CHECK(ucnt->numel() == uniq.numel(), "ps_records: count size mismatch");
+    cp = ptr<int32_t>(*ucnt);
+  }
+  c10::DeviceGuard g(uniq.device());
+  auto rec = torch::empty({uniq.numel(), 3}, uniq.options().dtype(torch::kInt32));
+  wh::ps_records(reinterpret_cast<const uint64_t*>(uniq.data_ptr()), cp, uniq.numel(),
+                 ptr<int32_t>(rec), cur_stream(uniq));
+  return rec;
+}
+
+// C0 buffers from the owner counts [P+1] and the V row counts [P] (optional):
+// (send int64 [3P], payload int64 [5P+1]; payload[P+1 : 4P+1] is the
+// exchange's receive slot)
+std::vector<Tensor> ps_c0(const Tensor& owner_cnt, const c10::optional<Tensor>& vcnt) {
+  CHECK_IN(owner_cnt, torch::kInt64);
+  const int P = (int)owner_cnt.numel() - 1;
+  const int64_t* vp = nullptr;
+  if (vcnt.has_value() && vcnt->defined()) {
+    CHECK_IN((*vcnt), torch::kInt64);
+    TORCH_CHECK(vcnt->numel() == P, "ps_c0: vcnt size mismatch");
+    vp = ptr<int64_t>(*vcnt);
+  }
+  c10::DeviceGuard g(owner_cnt.device());
+  auto send = torch::empty({3 * P}, owner_cnt.options());
+  auto payload = torch::empty({5 * P + 1}, owner_cnt.options());
+  TORCH_CHECK(wh::ps_c0(ptr<int64_t>(owner_cnt), vp, P, ptr<int64_t>(send), ptr<int64_t>(payload),
+                        cur_stream(owner_cnt)),
+              "ps_c0: too many peers");
+  return {send, payload};
 }
 
 // gw [U] into the header rows of the push buffer gbuf [R, vstride] (in place)
@@ -1233,6 +1277,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("vidx_renumber", &vidx_renumber);
   m.def("ps_unpack", &ps_unpack);
   m.def("ps_pack_gw", &ps_pack_gw);
+  m.def("ps_records", &ps_records);
+  m.def("ps_c0", &ps_c0);
   m.def("auc", &auc);
   m.def("quant_rows", &quant_rows);
   m.def("key_mod", &key_mod);

@@ -31,12 +31,15 @@
 // (exactly one winner initialises it; any other lane that sees a row created
 // in this launch computes the identical initial values from the key hash
 // instead of reading half-written memory). It also threads each key's
-// duplicates into a chain (atomicExch on the slot's tag word); the header
-// pack marks the chain heads and clears the tags before the next minibatch's
-// open can run. The push kernel lets only a head lane update its key, over
-// its chain in ascending index = peer-rank order, so each worker's push is
-// applied as one sequential update, deterministically (like the ps-lite
-// server handling requests one at a time), in ONE launch.
+// duplicates into a forward chain: every lane swaps its (epoch, index) tag
+// into the slot's tag word; the lane that finds no tag of this launch is the
+// key's head, every other lane links itself behind the lane it displaced.
+// The tags are never cleared per minibatch (a stale tag carries an older
+// epoch); the host sweeps the table's tags once per 255 minibatches, before
+// the 8-bit epoch wraps. The push kernel lets only a head lane update its
+// key, over its chain in ascending index = peer-rank order, so each worker's
+// push is applied as one sequential update, deterministically (like the
+// ps-lite server handling requests one at a time), in ONE launch.
 #include "wh_common.h"
 #include "wh_kernels.h"
 #include "wh_lookback.h"
@@ -47,11 +50,11 @@ namespace {
 
 using namespace kvd;
 
-constexpr int kMaxSeg = 1024;  // peers (LDS copies of the segment tables)
+constexpr int kMaxSeg = 256;  // peers (LDS copies of the segment tables)
 
-// chain word: bits 0-29 = next index + 1 (0 = end), bit 30 = chain head
-constexpr uint32_t kHeadBit = 1u << 30;
-constexpr uint32_t kNextMask = kHeadBit - 1;
+// chain[i] = index + 1 of the next duplicate of key i (0 = end; zeroed
+// before the open, written only by that successor); head[i] = 1 when lane i
+// heads its key's chain (written only by lane i)
 
 // segment of item i: largest p with S[p] <= i (S in LDS, P+1 entries)
 __device__ __forceinline__ int seg_of(const int64_t* S, int P, int64_t i) {
@@ -78,7 +81,7 @@ __global__ __launch_bounds__(kThreads) void k_ps_open(
     const int32_t* __restrict__ vbase_p, const int64_t* __restrict__ segS,
     const int64_t* __restrict__ segHS, int P, Lookback lb, int ntiles, int32_t* __restrict__ slot_out,
     float* __restrict__ w_out, int64_t* __restrict__ vpos, uint32_t* __restrict__ chain,
-    float* __restrict__ rbuf) {
+    uint8_t* __restrict__ head, float* __restrict__ rbuf) {
   __shared__ uint32_t shs[16];
   __shared__ int sht;
   __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1];
@@ -146,12 +149,10 @@ __global__ __launch_bounds__(kThreads) void k_ps_open(
     if (chains) {
       const uint32_t mine = (epoch << 24) | (uint32_t)(i0 + r + 1);
       const uint32_t pv = atomicExch(&e.tag, mine);
-      uint32_t nx = 0;
-      if ((pv >> 24) == epoch) {
-        const uint32_t j = (pv & 0xffffffu) - 1;
-        if ((int64_t)j < n && (int64_t)j != i0 + r) nx = j + 1;
-      }
-      chain[i0 + r] = nx;
+      const uint32_t j = (pv & 0xffffffu) - 1;
+      const bool linked = (pv >> 24) == epoch && (int64_t)j < n && (int64_t)j != i0 + r;
+      if (linked) chain[j] = (uint32_t)(i0 + r + 1);  // behind the lane we displaced
+      head[i0 + r] = linked ? 0 : 1;
     }
   }
   // allocation: exactly one CAS winner per key initialises the row
@@ -235,13 +236,12 @@ __global__ __launch_bounds__(kThreads) void k_ps_open(
 }
 
 // header pack (owner, after the open): {w, row index inside the peer's V
-// block or -1} at float (HS_p + VS_p) * vstride + 2 (i - S_p); the per-peer V
-// row counts; chain heads marked and the slot tags cleared
+// block or -1} at float (HS_p + VS_p) * vstride + 2 (i - S_p), and the
+// per-peer V row counts
 __global__ __launch_bounds__(kThreads) void k_ps_pack_hdr(
-    KVSlot* sl, const int32_t* __restrict__ slot, const float* __restrict__ w_out,
-    const int64_t* __restrict__ vpos, int64_t n, int vstride, int chains, uint32_t epoch,
+    const float* __restrict__ w_out, const int64_t* __restrict__ vpos, int64_t n, int vstride,
     const int64_t* __restrict__ segS, const int64_t* __restrict__ segHS, int P,
-    uint32_t* __restrict__ chain, float* __restrict__ rbuf, int64_t* __restrict__ vcnt) {
+    float* __restrict__ rbuf, int64_t* __restrict__ vcnt) {
   __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1];
   load_seg(segS, sS, P);
   load_seg(segHS, sHS, P);
@@ -257,14 +257,50 @@ __global__ __launch_bounds__(kThreads) void k_ps_pack_hdr(
   const int32_t j = has ? (int32_t)(v - vs0) : -1;
   *reinterpret_cast<float2*>(rbuf + (sHS[p] + vs0) * vstride + 2 * (i - sS[p])) =
       make_float2(w_out[i], __int_as_float(j));
-  if (chains) {
-    const int32_t s = slot[i];
-    if (s >= 0) {
-      const uint32_t mine = (epoch << 24) | (uint32_t)(i + 1);
-      if (sl[s].tag == mine) {  // the last exchanger heads the chain
-        chain[i] |= kHeadBit;
-        sl[s].tag = 0u;
-      }
+}
+
+// before an open: zero the chain links and snapshot the V-row bump pointer
+// (rows at or above it are created by the coming launch)
+__global__ __launch_bounds__(kThreads) void k_ps_prep(uint32_t* __restrict__ chain, int64_t n,
+                                                      const int32_t* __restrict__ vnext,
+                                                      int32_t* __restrict__ vbase) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < n) chain[i] = 0u;
+  if (i == 0) *vbase = *vnext;
+}
+
+// clear every slot's chain tag (once per 255 opens, before the epoch wraps)
+__global__ __launch_bounds__(kThreads) void k_ps_sweep_tags(KVSlot* sl, int64_t cap) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < cap) sl[i].tag = 0u;
+}
+
+// worker: 12-byte key records {lo, hi, count} of the C1 exchange
+__global__ __launch_bounds__(kThreads) void k_ps_records(const uint64_t* __restrict__ uniq,
+                                                         const int32_t* __restrict__ ucnt,
+                                                         int64_t U, int32_t* __restrict__ rec) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= U) return;
+  const uint64_t k = uniq[i];
+  rec[3 * i] = (int32_t)(uint32_t)k;
+  rec[3 * i + 1] = (int32_t)(uint32_t)(k >> 32);
+  rec[3 * i + 2] = ucnt ? ucnt[i] : 0;
+}
+
+// C0: send[3p..] = {keys for p, own table-overflow flag, V rows for p};
+// payload = [owner_cnt (P+1) | received 3P (filled by the exchange) | vcnt P]
+__global__ __launch_bounds__(256) void k_ps_c0(const int64_t* __restrict__ owner_cnt,
+                                               const int64_t* __restrict__ vcnt, int P,
+                                               int64_t* __restrict__ send,
+                                               int64_t* __restrict__ payload) {
+  for (int p = threadIdx.x; p <= P; p += blockDim.x) {
+    payload[p] = owner_cnt[p];
+    if (p < P) {
+      const int64_t v = vcnt ? vcnt[p] : 0;
+      send[3 * p] = owner_cnt[p];
+      send[3 * p + 1] = owner_cnt[P];
+      send[3 * p + 2] = v;
+      payload[4 * P + 1 + p] = v;
     }
   }
 }
@@ -324,7 +360,7 @@ __device__ __forceinline__ int64_t chain_next_after(const uint32_t* chain, int64
   int64_t best = -1;
   for (int64_t e = head; e >= 0;) {
     if (e > last && (best < 0 || e < best)) best = e;
-    const uint32_t nx = chain[e] & kNextMask;
+    const uint32_t nx = chain[e];
     e = nx ? (int64_t)nx - 1 : -1;
   }
   return best;
@@ -333,11 +369,14 @@ __device__ __forceinline__ int64_t chain_next_after(const uint32_t* chain, int64
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_ps_push(
     KVTable t, const int32_t* __restrict__ slot, const int64_t* __restrict__ vpos,
-    const uint32_t* __restrict__ chain, int64_t n, const int64_t* __restrict__ segS,
-    const int64_t* __restrict__ segHS, int P, const float* __restrict__ gbuf, DifactoHP hp) {
-  __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1];
+    const uint32_t* __restrict__ chain, const uint8_t* __restrict__ headf, int64_t n,
+    const int64_t* __restrict__ segS, const int64_t* __restrict__ segHS, int P,
+    const float* __restrict__ gbuf, DifactoHP hp) {
+  __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1], sVS[kMaxSeg + 1];
   load_seg(segS, sS, P);
   load_seg(segHS, sHS, P);
+  __syncthreads();
+  for (int p = threadIdx.x; p <= P; p += blockDim.x) sVS[p] = vpos[sS[p]];
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -346,7 +385,7 @@ __global__ __launch_bounds__(kThreads) void k_ps_push(
   bool head = false, any_v = false, alloc = false;
   if (i < n) {
     s = slot[i];
-    head = s >= 0 && (!chain || (chain[i] & kHeadBit));
+    head = s >= 0 && (!chain || headf[i]);
   }
   if (head) {
     KVSlot& e = t.sl[s];
@@ -356,8 +395,7 @@ __global__ __launch_bounds__(kThreads) void k_ps_push(
     for (int64_t el = chain ? chain_next_after(chain, i, -1) : i; el >= 0;
          el = chain ? chain_next_after(chain, i, el) : -1) {
       const int p = seg_of(sS, P, el);
-      const int64_t vs0 = vpos[sS[p]];
-      const float g = gbuf[(sHS[p] + vs0) * t.vstride + (el - sS[p])];
+      const float g = gbuf[(sHS[p] + sVS[p]) * t.vstride + (el - sS[p])];
       const float nw = difacto_ftrl(w, g, sq, z, hp);
       up |= (w == 0.f && nw != 0.f);
       w = nw;
@@ -417,34 +455,55 @@ __global__ __launch_bounds__(kThreads) void k_ps_push(
 }  // namespace
 
 bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t n, int use_cnt,
-             DifactoHP hp, int insert, int chains, uint32_t epoch, const int32_t* vbase,
+             DifactoHP hp, int insert, int chains, uint32_t epoch, int32_t* vbase,
              const int64_t* segS, const int64_t* segHS, int P, const Lookback& lb, int32_t* slot,
-             float* w_out, int64_t* vpos, uint32_t* chain, float* rbuf, int64_t* vcnt,
-             hipStream_t s) {
+             float* w_out, int64_t* vpos, uint32_t* chain, uint8_t* head, float* rbuf,
+             int64_t* vcnt, hipStream_t s) {
   const int64_t ntiles = (n + kPullTile - 1) / kPullTile;
-  if (P < 1 || P > kMaxSeg || ntiles > kLbMaxTiles || n >= (1 << 24) || t.vstride == 0)
+  if (P < 1 || P > kMaxSeg || ntiles > kLbMaxTiles || n >= (1 << 24) || t.vstride == 0 ||
+      epoch < 1 || epoch > 255)
     return false;
+  hipLaunchKernelGGL(k_ps_prep, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, chain,
+                     chains ? n : 0, t.vnext, vbase);
+  if (epoch == 1) {  // a new epoch cycle: no tag of the previous cycle may survive
+    hipLaunchKernelGGL(k_ps_sweep_tags, dim3(grid_for(t.cap, kThreads)), dim3(kThreads), 0, s,
+                       t.sl, t.cap);
+  }
   if (n > 0) {
     const int G = lanes_per_key(t.vstride);
     WH_DISPATCH_G(G, k_ps_open, dim3((unsigned)ntiles), dim3(kThreads), 0, s, t, keys, rec, n, hp,
                   insert, use_cnt, chains, epoch, vbase, segS, segHS, P, lb, (int)ntiles, slot,
-                  w_out, vpos, chain, rbuf);
+                  w_out, vpos, chain, head, rbuf);
   } else {
     WH_HIP_CHECK(hipMemsetAsync(vpos, 0, sizeof(int64_t), s));
   }
-  hipLaunchKernelGGL(k_ps_pack_hdr, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t.sl, slot,
-                     w_out, vpos, n, t.vstride, chains, epoch, segS, segHS, P, chain, rbuf, vcnt);
+  hipLaunchKernelGGL(k_ps_pack_hdr, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, w_out,
+                     vpos, n, t.vstride, segS, segHS, P, rbuf, vcnt);
   return true;
 }
 
 bool ps_push(const KVTable& t, const int32_t* slot, const int64_t* vpos, const uint32_t* chain,
-             int64_t n, const int64_t* segS, const int64_t* segHS, int P, const float* gbuf,
-             DifactoHP hp, hipStream_t s) {
+             const uint8_t* head, int64_t n, const int64_t* segS, const int64_t* segHS, int P,
+             const float* gbuf, DifactoHP hp, hipStream_t s) {
   if (P < 1 || P > kMaxSeg || t.vstride == 0) return false;
   if (n <= 0) return true;
   const int G = lanes_per_key(t.vstride);
   WH_DISPATCH_G(G, k_ps_push, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t, slot, vpos,
-                chain, n, segS, segHS, P, gbuf, hp);
+                chain, head, n, segS, segHS, P, gbuf, hp);
+  return true;
+}
+
+void ps_records(const uint64_t* uniq, const int32_t* ucnt, int64_t U, int32_t* rec,
+                hipStream_t s) {
+  if (U <= 0) return;
+  hipLaunchKernelGGL(k_ps_records, dim3(grid_for(U, kThreads)), dim3(kThreads), 0, s, uniq, ucnt,
+                     U, rec);
+}
+
+bool ps_c0(const int64_t* owner_cnt, const int64_t* vcnt, int P, int64_t* send, int64_t* payload,
+           hipStream_t s) {
+  if (P < 1 || P > 4096) return false;
+  hipLaunchKernelGGL(k_ps_c0, dim3(1), dim3(256), 0, s, owner_cnt, vcnt, P, send, payload);
   return true;
 }
 

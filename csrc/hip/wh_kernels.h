@@ -183,15 +183,21 @@ bool vidx_renumber_fused(float* hdr, int64_t n, const Lookback& lb, int64_t* cou
 // ps_push: owner applies the received push buffer (same layout as rbuf).
 // ps_unpack / ps_pack_gw: worker side (segments = keys sent per owner,
 //   vrecv[P] = V rows received per owner).
-// Each returns false when its limits are exceeded (P > 1024, n >= 2^24).
+// Each returns false when its limits are exceeded (P > 256, n >= 2^24).
 bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t n, int use_cnt,
-             DifactoHP hp, int insert, int chains, uint32_t epoch, const int32_t* vbase,
+             DifactoHP hp, int insert, int chains, uint32_t epoch, int32_t* vbase,
              const int64_t* segS, const int64_t* segHS, int P, const Lookback& lb, int32_t* slot,
-             float* w_out, int64_t* vpos, uint32_t* chain, float* rbuf, int64_t* vcnt,
-             hipStream_t s);
+             float* w_out, int64_t* vpos, uint32_t* chain, uint8_t* head, float* rbuf,
+             int64_t* vcnt, hipStream_t s);
 bool ps_push(const KVTable& t, const int32_t* slot, const int64_t* vpos, const uint32_t* chain,
-             int64_t n, const int64_t* segS, const int64_t* segHS, int P, const float* gbuf,
-             DifactoHP hp, hipStream_t s);
+             const uint8_t* head, int64_t n, const int64_t* segS, const int64_t* segHS, int P,
+             const float* gbuf, DifactoHP hp, hipStream_t s);
+// worker: 12-byte {lo, hi, count} records of the key exchange (ucnt may be null)
+void ps_records(const uint64_t* uniq, const int32_t* ucnt, int64_t U, int32_t* rec,
+                hipStream_t s);
+// C0 count exchange buffers: send[3P] and payload[5P+1] (see psx.hip)
+bool ps_c0(const int64_t* owner_cnt, const int64_t* vcnt, int P, int64_t* send, int64_t* payload,
+           hipStream_t s);
 bool ps_unpack(const float* rbuf, int64_t U, int vstride, const int64_t* segS,
                const int64_t* segHS, const int64_t* vrecv, int P, float* hdr, int64_t* rows_total,
                hipStream_t s);

@@ -324,14 +324,14 @@ class CpuKVStore:
                     v -= v_alpha / (cgv + v_beta) * gv
 
     # ----------------------------------------------- multi-shard (psx) ops
-    def ps_open(self, keys, use_cnt, segS, segHS, rows_cap, insert, chains, epoch, h, threshold,
+    def ps_open(self, keys, use_cnt, segS, segHS, rows_cap, insert, chains, h, threshold,
                 l1_shrk, seed):
         """Owner side of a P-shard minibatch (host oracle of psx.hip ps_open):
         segments in peer order, each one find/insert + count push (the lane
         whose add crosses the threshold allocates) + variable-length pull
-        into the row-aligned reply buffer. Returns (slot, vpos, chain, rbuf,
-        vcnt); chain is unused on the host (duplicates are applied in peer
-        order by ps_push)."""
+        into the row-aligned reply buffer. Returns (slot, vpos, chain, head,
+        rbuf, vcnt); chain / head are unused on the host (duplicates are
+        applied in peer order by ps_push)."""
         if keys.dtype == torch.int32:
             rec = keys.reshape(-1, 3).numpy()
             ks = (rec[:, 0].astype(np.int64) & 0xFFFFFFFF) | (rec[:, 1].astype(np.int64) << 32)
@@ -381,9 +381,10 @@ class CpuKVStore:
                 if rows[i] >= 0:
                     rbuf[HS[p + 1] + int(vpos[i])] = self._V[rows[i]]
         return (torch.from_numpy(slot.astype(np.int32)), torch.from_numpy(vpos),
-                torch.zeros(n, dtype=torch.int32), torch.from_numpy(rbuf), torch.from_numpy(vcnt))
+                torch.zeros(n, dtype=torch.int32), torch.ones(n, dtype=torch.uint8),
+                torch.from_numpy(rbuf), torch.from_numpy(vcnt))
 
-    def ps_push(self, slot, vpos, chain, segS, segHS, gbuf, h, threshold, l1_shrk, seed):
+    def ps_push(self, slot, vpos, chain, head, segS, segHS, gbuf, h, threshold, l1_shrk, seed):
         """Owner side push of a P-shard minibatch: every peer's segment in
         peer order (ps-lite server: one request at a time)."""
         S = [int(x) for x in segS.tolist()]

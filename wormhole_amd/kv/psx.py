@@ -50,7 +50,8 @@ class _Step:
 
     __slots__ = ("train", "use_cnt", "U", "uniq", "ucnt", "lid", "offset", "val", "csc",
                  "label", "send", "recv", "Hw", "Ho", "tabs", "segS_w", "segHS_w", "segS_o",
-                 "segHS_o", "keys_o", "slot", "vpos", "chain", "rbuf", "vcnt", "ev_open",
+                 "segHS_o", "keys_o", "slot", "vpos", "chain", "head", "rbuf", "vcnt",
+                 "ev_open",
                  "vown", "vrecv", "vrecv_d", "rrecv", "hdr", "rows", "py", "dual", "xv",
                  "gpush", "ev_push", "seed_step")
 
@@ -70,7 +71,6 @@ class PsxDifacto:
         self.cuda = self.dev.type == "cuda"
         self.cs = torch.cuda.Stream(device=self.dev) if self.cuda else None
         self.tau = 1 if int(getattr(lrn.conf, "max_concurrency", 2) or 2) >= 2 else 0
-        self.epoch = 0
         self.job = None     # (keys, LocalizeJob | finished tuple, carried step)
         self.pull = None    # opened, reply not yet exchanged
         self.push = None    # push in flight to the owners
@@ -119,15 +119,10 @@ class PsxDifacto:
         P = self.P
 
         def ex(owner_cnt):
-            with self._on_cs(owner_cnt, carried.vcnt if carried is not None else None):
-                send = torch.zeros(P, 3, dtype=torch.int64, device=owner_cnt.device)
-                send[:, 0] = owner_cnt[:P]
-                send[:, 1] = owner_cnt[P]
-                vc = carried.vcnt if carried is not None else torch.zeros(
-                    P, dtype=torch.int64, device=owner_cnt.device)
-                send[:, 2] = vc
-                recv = self.comm.exchange_counts_dev(send.reshape(-1))
-                payload = torch.cat([owner_cnt, recv.reshape(-1), vc])
+            vc = carried.vcnt if carried is not None else None
+            with self._on_cs(owner_cnt, vc):
+                send, payload = ops.ps_c0(owner_cnt, vc)
+                payload[P + 1:4 * P + 1] = self.comm.exchange_counts_dev(send)
             if self.cuda:
                 return payload, self.cs.cuda_stream, 3, P
             return payload
@@ -181,14 +176,13 @@ class PsxDifacto:
         """Standalone C0 for a step whose V row counts rode on no localize
         (pipeline drain, validation): one extra host read."""
         P = self.P
-        send = torch.zeros(P, 3, dtype=torch.int64, device=self.dev)
-        with self._on_cs(st.vcnt):
-            send[:, 2] = st.vcnt
-            recv = self.comm.exchange_counts_dev(send.reshape(-1))
-            both = torch.cat([recv.reshape(-1), st.vcnt]).cpu()
-        v = both.tolist()
-        st.vrecv = v[2:3 * P:3]
-        st.vown = v[3 * P:4 * P]
+        zero = torch.zeros(P + 1, dtype=torch.int64, device=self.dev)
+        with self._on_cs(st.vcnt, zero):
+            send, payload = ops.ps_c0(zero, st.vcnt)
+            payload[P + 1:4 * P + 1] = self.comm.exchange_counts_dev(send)
+            v = payload.cpu().tolist()
+        st.vrecv = v[P + 3:4 * P + 1:3]
+        st.vown = v[4 * P + 1:5 * P + 1]
 
     # ---------------------------------------------------------------- tables
     def _upload(self, st, prev):
@@ -216,23 +210,15 @@ class PsxDifacto:
     # -------------------------------------------------------------- phases
     def _open(self, st, insert):
         lrn = self.lrn
-        U = st.U
-        if st.use_cnt:
-            rec = torch.empty(U, 3, dtype=torch.int32, device=self.dev)
-            rec[:, 0:2] = st.uniq.view(torch.int32).view(U, 2)
-            rec[:, 2] = st.ucnt
-        else:
-            rec = st.uniq
+        rec = ops.ps_records(st.uniq, st.ucnt if st.use_cnt else None)
         with self._on_cs(rec):
             keys_o = self.comm.all_to_all_v(rec, st.send, st.recv)
         self._join(self._mark(), keys_o)
         n = sum(st.recv)
         lrn.kv.guard.before_open(n, self._remap)
-        self.epoch = self.epoch % 255 + 1
         st.keys_o = keys_o
-        st.slot, st.vpos, st.chain, st.rbuf, st.vcnt = self.store.ps_open(
-            keys_o, st.use_cnt, st.segS_o, st.segHS_o, sum(st.Ho) + n, insert, st.train,
-            self.epoch, lrn.hp,
+        st.slot, st.vpos, st.chain, st.head, st.rbuf, st.vcnt = self.store.ps_open(
+            keys_o, st.use_cnt, st.segS_o, st.segHS_o, sum(st.Ho) + n, insert, st.train, lrn.hp,
             lrn.threshold, lrn.l1_shrk, lrn.seed)
         lrn.kv.guard.after_open()
 
@@ -289,9 +275,9 @@ class PsxDifacto:
     def _owner_push(self, st):
         lrn = self.lrn
         self._join(st.ev_push, st.gpush)
-        self.store.ps_push(st.slot, st.vpos, st.chain, st.segS_o, st.segHS_o, st.gpush, lrn.hp,
-                           lrn.threshold, lrn.l1_shrk, lrn.seed)
-        st.gpush = st.slot = st.vpos = st.chain = st.keys_o = None
+        self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o, st.gpush,
+                           lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
+        st.gpush = st.slot = st.vpos = st.chain = st.head = st.keys_o = None
 
     def _remap(self, remap):
         """The table grew: translate the slot ids of in-flight steps."""

@@ -233,3 +233,17 @@ def ps_pack_gw(gw, gbuf, segS, segHS, vrecv):
     if _gpu(gw):
         return _native.hip().ps_pack_gw(gw, gbuf, segS, segHS, vrecv)
     return ref.ps_pack_gw(gw, gbuf, segS, segHS, vrecv)
+
+
+def ps_records(uniq, ucnt=None):
+    """12-byte key records {lo, hi, count} int32 [U, 3] of the key exchange."""
+    if _gpu(uniq):
+        return _native.hip().ps_records(uniq, ucnt)
+    return ref.ps_records(uniq, ucnt)
+
+
+def ps_c0(owner_cnt, vcnt=None):
+    """C0 count-exchange buffers (send [3P], payload [5P+1]); see kv/psx.py."""
+    if _gpu(owner_cnt):
+        return tuple(_native.hip().ps_c0(owner_cnt, vcnt))
+    return ref.ps_c0(owner_cnt, vcnt)

@@ -274,3 +274,24 @@ def ps_pack_gw(gw, gbuf, segS, segHS, vrecv):
         base = (HS[q] + VS) * vs
         flat[base:base + (b - a)] = gw[a:b]
         VS += vr[q]
+
+
+def ps_records(uniq, ucnt=None):
+    U = uniq.numel()
+    rec = torch.empty(U, 3, dtype=torch.int32)
+    rec[:, 0:2] = uniq.contiguous().view(torch.int32).view(U, 2)
+    rec[:, 2] = ucnt if ucnt is not None else 0
+    return rec
+
+
+def ps_c0(owner_cnt, vcnt=None):
+    P = owner_cnt.numel() - 1
+    send = torch.zeros(P, 3, dtype=torch.int64)
+    send[:, 0] = owner_cnt[:P]
+    send[:, 1] = owner_cnt[P]
+    v = vcnt if vcnt is not None else torch.zeros(P, dtype=torch.int64)
+    send[:, 2] = v
+    payload = torch.zeros(5 * P + 1, dtype=torch.int64)
+    payload[:P + 1] = owner_cnt
+    payload[4 * P + 1:] = v
+    return send.reshape(-1), payload
