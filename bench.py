@@ -150,6 +150,11 @@ def main():
     sync()
     comm.barrier()
     sync()
+    prof = None
+    if os.environ.get("WH_HOST_PROFILE"):  # host-side (Python) profile of the timed steps
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     run(args.warmup, args.steps)
     learner.flush()  # the last step's (deferred) push is part of the timed work
@@ -157,6 +162,11 @@ def main():
     comm.barrier()
     sync()
     dt = time.perf_counter() - t0
+    if prof is not None:
+        import pstats
+        prof.disable()
+        with open(os.environ["WH_HOST_PROFILE"] + ".%d" % comm.rank, "w") as f:
+            pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     comm.allreduce(t, "max")
     dt = float(t.item())

@@ -163,13 +163,15 @@ class LocalizeJob {
     }
   }
 
-  std::vector<Tensor> finish() {
+  // The one host read: waits for the count exchange (retrying the whole
+  // begin at the safe table size if any rank overflowed) and returns the
+  // host (owner counts [nshard], everything the exchange appended). A
+  // caller may enqueue unrelated work between counts() and finish().
+  std::vector<Tensor> counts() {
     TORCH_CHECK(!done_, "localize job already finished");
+    if (owner_cnt_h_.defined()) return {owner_cnt_h_, recv_h_};
     c10::DeviceGuard g(keys_.device());
-    auto s = cur_stream(keys_);
     DevWs& ws = dev_ws(keys_.device());
-    auto i32 = keys_.options().dtype(torch::kInt32);
-    auto i64 = keys_.options().dtype(torch::kInt64);
     while (true) {
       WH_HIP_CHECK_HOST(hipEventSynchronize(event_));
       const int64_t* h = host_.data_ptr<int64_t>();
@@ -184,16 +186,26 @@ class LocalizeJob {
       enqueue();
     }
     const int64_t* h = host_.data_ptr<int64_t>();
-    auto owner_cnt_h = torch::empty({nshard_}, torch::kInt64);
-    int64_t U = 0;
-    for (int64_t p = 0; p < nshard_; ++p) {
-      owner_cnt_h.data_ptr<int64_t>()[p] = h[p];
-      U += h[p];
-    }
+    owner_cnt_h_ = torch::empty({nshard_}, torch::kInt64);
+    for (int64_t p = 0; p < nshard_; ++p) owner_cnt_h_.data_ptr<int64_t>()[p] = h[p];
     // everything after the owner counts (the peers' values and any extra)
     const int64_t ntail = dev_counts_.numel() - nshard_ - 1;
-    Tensor recv_h = torch::empty({nrecv_ ? ntail : 0}, torch::kInt64);
-    for (int64_t q = 0; q < recv_h.numel(); ++q) recv_h.data_ptr<int64_t>()[q] = h[nshard_ + 1 + q];
+    recv_h_ = torch::empty({nrecv_ ? ntail : 0}, torch::kInt64);
+    for (int64_t q = 0; q < recv_h_.numel(); ++q)
+      recv_h_.data_ptr<int64_t>()[q] = h[nshard_ + 1 + q];
+    return {owner_cnt_h_, recv_h_};
+  }
+
+  std::vector<Tensor> finish() {
+    counts();
+    c10::DeviceGuard g(keys_.device());
+    auto s = cur_stream(keys_);
+    DevWs& ws = dev_ws(keys_.device());
+    auto i32 = keys_.options().dtype(torch::kInt32);
+    auto i64 = keys_.options().dtype(torch::kInt64);
+    Tensor owner_cnt_h = owner_cnt_h_, recv_h = recv_h_;
+    int64_t U = 0;
+    for (int64_t p = 0; p < nshard_; ++p) U += owner_cnt_h.data_ptr<int64_t>()[p];
     const int64_t nnz = nnz_, nrows = offset_.numel() - 1;
     const float* vp = val_.defined() ? ptr<float>(val_) : nullptr;
     auto tlid = torch::empty({tsize_}, i32);
@@ -301,7 +313,7 @@ class LocalizeJob {
   py::object exchange_;
   int tab_ = -1;
   bool done_ = false;
-  Tensor tkeys_, slot_of_, blkoff_, dev_counts_, host_;
+  Tensor tkeys_, slot_of_, blkoff_, dev_counts_, host_, owner_cnt_h_, recv_h_;
   hipEvent_t event_ = nullptr;
 };
 
@@ -1268,6 +1280,7 @@ PYBIND11_MODULE(_hip, m) {
                     py::object>(),
            py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(), py::arg("nshard") = 1,
            py::arg("hint") = 0, py::arg("exchange") = py::none())
+      .def("counts", &LocalizeJob::counts)
       .def("finish", &LocalizeJob::finish);
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
         py::arg("nshard") = 1, py::arg("hint") = 0, py::arg("exchange") = py::none());

@@ -149,28 +149,35 @@ class PsxDifacto:
             job = tuple(out)
         self.job = (keys, job, carried)
 
-    def _finish(self):
+    def _counts(self):
+        """The one host read of the step (count exchange C0 of the begun
+        localize): returns (send, recv); fills the carried step's V counts."""
         keys, job, carried = self.job
-        self.job = None
-        out = tuple(job) if isinstance(job, tuple) else tuple(job.finish())
+        if isinstance(job, tuple):
+            oc, tail = job[2], job[7]
+        else:
+            oc, tail = job.counts()
         P = self.P
-        tail = out[7].tolist()
-        recv = tail[0:3 * P:3]
-        if carried is not None:
+        tail = tail.tolist()
+        if carried is not None and carried.vown is None:
             carried.vrecv = tail[2:3 * P:3]
             carried.vown = tail[3 * P:4 * P]
-        send = [int(x) for x in out[2].tolist()]
-        return out, send, [int(x) for x in recv], carried
+        return [int(x) for x in oc.tolist()], [int(x) for x in tail[0:3 * P:3]]
 
-    def _localized(self, keys, offset, val):
-        """Finish this minibatch's localize (begun by the previous call or
-        now); returns (loc, send, recv)."""
+    def _finish(self):
+        """Enqueue the rest of the begun localize (after :meth:`_counts`)."""
+        keys, job, carried = self.job
+        self.job = None
+        return tuple(job) if isinstance(job, tuple) else tuple(job.finish())
+
+    def _ensure_job(self, keys, offset, val):
+        """This minibatch's localize: begun by the previous call, or now."""
         if self.job is None or self.job[0] is not keys:
-            if self.job is not None:
-                self._finish()  # a stale job (never expected): discard in order
+            if self.job is not None:  # a stale job (never expected): finish it in order
+                self._counts()
+                self._finish()
             self._begin(keys, offset, val, self.pull if (self.pull is not None and
                                                          self.pull.vown is None) else None)
-        return self._finish()
 
     def _vcount_exchange(self, st):
         """Standalone C0 for a step whose V row counts rode on no localize
@@ -286,44 +293,46 @@ class PsxDifacto:
                 st.slot = remap[st.slot.long()]
 
     # ----------------------------------------------------------------- API
-    def _new_step(self, loc, send, recv, label, train, data_pass, prev):
-        lrn = self.lrn
+    def _new_step(self, send, recv, label, train, data_pass, prev):
         st = _Step()
-        st.uniq, st.ucnt, _, st.lid, csc_off, csc_row, csc_val = loc[:7]
-        st.csc = (csc_off, csc_row, csc_val)
-        st.U = st.uniq.numel()
         st.send, st.recv = send, recv
         st.label = label
         st.train = train
         st.use_cnt = train and data_pass == 0
-        st.seed_step = lrn.step
-        self.uhint = st.U
+        st.seed_step = self.lrn.step
         self._upload(st, prev)
         return st
 
+    def _set_loc(self, st, loc, offset, val):
+        st.uniq, st.ucnt, _, st.lid, csc_off, csc_row, csc_val = loc[:7]
+        st.csc = (csc_off, csc_row, csc_val)
+        st.U = st.uniq.numel()
+        st.offset, st.val = offset, val
+        self.uhint = st.U
+
     def train(self, keys, offset, val, label, data_pass, next_batch):
-        loc, send, recv, carried = self._localized(keys, offset, val)
+        self._ensure_job(keys, offset, val)
+        send, recv = self._counts()  # the step's one host read
         prev = self.pull
         if prev is not None and prev.vown is None:
             self._vcount_exchange(prev)
-        st = self._new_step(loc, send, recv, label, True, data_pass, prev)
-        st.offset, st.val = offset, val
+        st = self._new_step(send, recv, label, True, data_pass, prev)
+        if self.tau == 1 and prev is not None:
+            # the previous minibatch's reply + forward go first: the device
+            # gets work the moment the host read returns
+            self._reply(prev)
+        self._set_loc(st, self._finish(), offset, val)
         if self.tau == 0:
             if prev is not None:
                 self._reply(prev)
                 if prev.train:
                     self._grad(prev)
                     self._owner_push(prev)
-            self._open(st, True)
-            self.pull = st
-        else:
-            if prev is not None:
-                self._reply(prev)
-            if self.push is not None:
-                self._owner_push(self.push)
-                self.push = None
-            self._open(st, True)
-            self.pull = st
+        elif self.push is not None:
+            self._owner_push(self.push)
+            self.push = None
+        self._open(st, True)
+        self.pull = st
         if next_batch is not None:
             nk, no, nv = next_batch[:3]
             self._begin(nk, no, nv, st, next_batch[3] if len(next_batch) > 3 else None)
@@ -336,9 +345,10 @@ class PsxDifacto:
         """A validation / prediction minibatch: drain the training pipeline,
         then open (no insert), reply and forward synchronously."""
         self.flush()
-        loc, send, recv, _ = self._localized(keys, offset, val)
-        st = self._new_step(loc, send, recv, label, False, 1, None)
-        st.offset, st.val = offset, val
+        self._ensure_job(keys, offset, val)
+        send, recv = self._counts()
+        st = self._new_step(send, recv, label, False, 1, None)
+        self._set_loc(st, self._finish(), offset, val)
         self._open(st, False)
         self._vcount_exchange(st)
         self._upload_vrecv(st)
@@ -355,12 +365,8 @@ class PsxDifacto:
         or saving the model, end of a timed run)."""
         if self.job is not None and self.job[2] is not None:
             # the next minibatch's localize already carries the last pull's
-            # V counts: finish it now (keeping its result for the next call)
-            keys = self.job[0]
-            out, send, recv, _ = self._finish()
-            self.job = (keys, tuple(out[:7]) + (torch.tensor(
-                [x for q in range(self.P) for x in (recv[q], 0, 0)] + [0] * self.P,
-                dtype=torch.int64),), None)
+            # V counts: read them now (the job itself stays begun)
+            self._counts()
         st = self.pull
         if st is not None:
             if st.vown is None:
