@@ -167,6 +167,7 @@ def main():
         prof.disable()
         with open(os.environ["WH_HOST_PROFILE"] + ".%d" % comm.rank, "w") as f:
             pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
+            pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     comm.allreduce(t, "max")
     dt = float(t.item())

@@ -339,7 +339,7 @@ class KVStore {
     // below are strided views into it (shared storage, writable)
     auto sl = torch::zeros({cap, 8}, f32.dtype(torch::kInt32));
     sl.view(torch::kInt64).select(1, 0).fill_(-1);  // key: empty
-    sl.select(1, 6).fill_(-1);                      // vrow: none
+    sl.select(1, 5).fill_(-1);                      // vrow: none
     set_slots(sl);
     if (dim > 0) {
       V_ = torch::zeros({std::max<int64_t>(vcap, 1), vstride_}, f32);
@@ -604,7 +604,7 @@ class KVStore {
     auto s = cur_stream(slots_);
     auto ns = torch::zeros({newcap, 8}, slots_.options());
     ns.view(torch::kInt64).select(1, 0).fill_(-1);
-    ns.select(1, 6).fill_(-1);
+    ns.select(1, 5).fill_(-1);
     auto remap = torch::empty({cap_}, slots_.options());
     wh::kv_rehash(reinterpret_cast<const wh::KVSlot*>(slots_.data_ptr()), cap_,
                   reinterpret_cast<wh::KVSlot*>(ns.data_ptr()), newcap, ptr<int32_t>(remap),
@@ -655,8 +655,8 @@ class KVStore {
     w_ = as_f32.select(1, 2);
     z_ = as_f32.select(1, 3);
     sq_ = as_f32.select(1, 4);
-    cnt_ = slots_.select(1, 5);
-    vrow_ = slots_.select(1, 6);
+    vrow_ = slots_.select(1, 5);
+    cnt_ = slots_.select(1, 6);
   }
 
   int64_t cap_ = 0, vcap_ = 0, dim_ = 0;

@@ -137,22 +137,32 @@ __global__ __launch_bounds__(kThreads) void k_ps_open(
     KVSlot& e = t.sl[sl[r]];
     w[r] = e.w;
     row[r] = t.vstride > 0 ? ld_relaxed_i32(&e.vrow) : -1;
-    if (use_cnt) {
-      // only the lane whose add crosses the threshold may allocate: with a
-      // key's duplicates adding concurrently, exactly one lane crosses (a key
-      // that crossed while l1_shrk held w at 0 is allocated by the push that
-      // makes w non-zero)
-      const uint32_t old = atomicAdd(&e.cnt, (uint32_t)c[r]);
-      want[r] = t.vstride > 0 && old <= hp.threshold && old + (uint32_t)c[r] > hp.threshold &&
-                row[r] < 0 && (!hp.l1_shrk || w[r] != 0.f);
-    }
-    if (chains) {
+    if (use_cnt || chains) {
+      // {cnt, tag} in one 64-bit CAS: add the count and swap in this lane's
+      // chain tag. Only the lane whose add crosses the threshold may
+      // allocate: with a key's duplicates adding concurrently, exactly one
+      // lane crosses (a key that crossed while l1_shrk held w at 0 is
+      // allocated by the push that makes w non-zero).
+      unsigned long long* ct = reinterpret_cast<unsigned long long*>(&e.cnt);
       const uint32_t mine = (epoch << 24) | (uint32_t)(i0 + r + 1);
-      const uint32_t pv = atomicExch(&e.tag, mine);
-      const uint32_t j = (pv & 0xffffffu) - 1;
-      const bool linked = (pv >> 24) == epoch && (int64_t)j < n && (int64_t)j != i0 + r;
-      if (linked) chain[j] = (uint32_t)(i0 + r + 1);  // behind the lane we displaced
-      head[i0 + r] = linked ? 0 : 1;
+      const uint32_t add = use_cnt ? (uint32_t)c[r] : 0u;
+      unsigned long long cur = __hip_atomic_load(ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (true) {
+        const uint32_t nt = chains ? mine : (uint32_t)(cur >> 32);
+        const unsigned long long nv = ((unsigned long long)nt << 32) | (uint32_t)((uint32_t)cur + add);
+        const unsigned long long seen = atomicCAS(ct, cur, nv);
+        if (seen == cur) break;
+        cur = seen;
+      }
+      const uint32_t old = (uint32_t)cur, pv = (uint32_t)(cur >> 32);
+      want[r] = use_cnt && t.vstride > 0 && old <= hp.threshold && old + add > hp.threshold &&
+                row[r] < 0 && (!hp.l1_shrk || w[r] != 0.f);
+      if (chains) {
+        const uint32_t j = (pv & 0xffffffu) - 1;
+        const bool linked = (pv >> 24) == epoch && (int64_t)j < n && (int64_t)j != i0 + r;
+        if (linked) chain[j] = (uint32_t)(i0 + r + 1);  // behind the lane we displaced
+        head[i0 + r] = linked ? 0 : 1;
+      }
     }
   }
   // allocation: exactly one CAS winner per key initialises the row
@@ -382,24 +392,36 @@ __global__ __launch_bounds__(kThreads) void k_ps_push(
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   float w0 = 0.f, w = 0.f;
   int32_t s = -1, row = -1;
-  bool head = false, any_v = false, alloc = false;
+  bool head = false, any_v = false, alloc = false, single = true;
+  int64_t gvrow = -1;  // singleton: the gradient row of this key
   if (i < n) {
     s = slot[i];
     head = s >= 0 && (!chain || headf[i]);
+    single = !chain || chain[i] == 0u;
   }
   if (head) {
     KVSlot& e = t.sl[s];
     w0 = w = e.w;
     float z = e.z, sq = e.sq;
     bool up = false;  // w went 0 -> non-zero at some push of the chain
-    for (int64_t el = chain ? chain_next_after(chain, i, -1) : i; el >= 0;
-         el = chain ? chain_next_after(chain, i, el) : -1) {
-      const int p = seg_of(sS, P, el);
-      const float g = gbuf[(sHS[p] + sVS[p]) * t.vstride + (el - sS[p])];
-      const float nw = difacto_ftrl(w, g, sq, z, hp);
-      up |= (w == 0.f && nw != 0.f);
-      w = nw;
-      any_v |= vpos[el + 1] > vpos[el];
+    if (single) {  // the common case: one peer pushed this key
+      const int p = seg_of(sS, P, i);
+      const float g = gbuf[(sHS[p] + sVS[p]) * t.vstride + (i - sS[p])];
+      w = difacto_ftrl(w, g, sq, z, hp);
+      up = w0 == 0.f && w != 0.f;
+      const int64_t v0 = vpos[i];
+      any_v = vpos[i + 1] > v0;
+      gvrow = sHS[p + 1] + v0;
+    } else {
+      for (int64_t el = chain_next_after(chain, i, -1); el >= 0;
+           el = chain_next_after(chain, i, el)) {
+        const int p = seg_of(sS, P, el);
+        const float g = gbuf[(sHS[p] + sVS[p]) * t.vstride + (el - sS[p])];
+        const float nw = difacto_ftrl(w, g, sq, z, hp);
+        up |= (w == 0.f && nw != 0.f);
+        w = nw;
+        any_v |= vpos[el + 1] > vpos[el];
+      }
     }
     e.w = w;
     e.z = z;
@@ -426,6 +448,7 @@ __global__ __launch_bounds__(kThreads) void k_ps_push(
     const int32_t jr = __shfl(row, s2, 64), jk = __shfl(kind, s2, 64);
     const int32_t js = __shfl(s, s2, 64);
     const int64_t ji = __shfl(i, s2, 64);
+    const int64_t jg = __shfl(single ? gvrow : -1, s2, 64);
     if (src < 0) return;
     if (jk == 1) {
       init_v_row(t, t.sl[js].key, jr, gl, G, hp);
@@ -433,6 +456,17 @@ __global__ __launch_bounds__(kThreads) void k_ps_push(
     }
     float* V = t.V + (int64_t)jr * t.vstride;
     float* VG = t.VG + (int64_t)jr * t.vstride;
+    if (jg >= 0) {  // singleton: one gradient row, known to the key's lane
+      const float* gv = gbuf + jg * t.vstride;
+      for (int cc = gl * 4; cc < t.vstride; cc += 4 * G) {
+        float4 v = *reinterpret_cast<float4*>(V + cc);
+        float4 cg = *reinterpret_cast<float4*>(VG + cc);
+        adagrad4(v, cg, *reinterpret_cast<const float4*>(gv + cc), hp);
+        *reinterpret_cast<float4*>(V + cc) = v;
+        *reinterpret_cast<float4*>(VG + cc) = cg;
+      }
+      return;
+    }
     for (int cc = gl * 4; cc < t.vstride; cc += 4 * G) {
       float4 v = *reinterpret_cast<float4*>(V + cc);
       float4 cg = *reinterpret_cast<float4*>(VG + cc);

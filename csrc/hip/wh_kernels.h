@@ -79,10 +79,11 @@ struct alignas(32) KVSlot {
   float w;
   float z;         // FTRL z (linear sign convention per app)
   float sq;        // sqrt of cumulative squared gradient
-  uint32_t cnt;    // feature count (difacto)
   int32_t vrow;    // row into the V slab, -1 = no embedding
-  uint32_t tag;    // multi-shard push: duplicate-chain head of the open
-                   // minibatch session (psx.hip), 0 = none
+  uint32_t cnt;    // feature count (difacto)
+  uint32_t tag;    // multi-shard open: duplicate-chain tag {epoch, index}
+                   // (psx.hip); cnt and tag share one 8-byte word so the
+                   // open updates both with one 64-bit atomic
 };
 static_assert(sizeof(KVSlot) == 32, "KVSlot must be one 32-byte sector");
 // Event counters are sharded over 64 cache lines: one counter word takes

@@ -55,9 +55,13 @@ class StoreGuard:
     def after_open(self):
         s = self.store.summary()
         if self.cuda:
-            h = torch.empty(4, dtype=torch.int64, pin_memory=True)
+            if getattr(self, "_pin", None) is None:  # two alternating pinned slots
+                self._pin = [torch.empty(4, dtype=torch.int64, pin_memory=True) for _ in range(2)]
+                self._ev = [torch.cuda.Event() for _ in range(2)]
+                self._k = 0
+            k = self._k = self._k ^ 1
+            h, ev = self._pin[k], self._ev[k]
             h.copy_(s, non_blocking=True)
-            ev = torch.cuda.Event()
             ev.record()
             self.pend = (h, ev)
         else:

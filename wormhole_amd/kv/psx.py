@@ -26,7 +26,11 @@ on the compute stream S,
     localize finish(i) | unpack(i-1) fwd(i-1) | owner push(i-2) |
     owner open(i) pack(i) | localize begin(i+1) | bwd(i-1) pack_gw(i-1)
 
-and on the comm stream C: C2(i-1), C1(i), C0(i+1) + the count read, C3(i-1).
+and the collectives C2(i-1), C1(i), C0(i+1), C3(i-1) in that order. C1-C3
+are issued asynchronously on the process group's stream and waited on (a
+stream dependency, not a host wait) right before the kernel that consumes
+them, so each overlaps the compute-stream work queued in between; C0 and its
+pinned host read run from a side stream the compute stream never waits on.
 The host's wait for the read of C0(i+1) happens in the NEXT call while S
 still holds bwd(i-1), so S never drains. ``max_concurrency = 1`` gives the
 strict (staleness 0) order at the cost of one pipeline drain per step.
@@ -53,11 +57,53 @@ class _Step:
                  "segHS_o", "keys_o", "slot", "vpos", "chain", "head", "rbuf", "vcnt",
                  "ev_open",
                  "vown", "vrecv", "vrecv_d", "rrecv", "hdr", "rows", "py", "dual", "xv",
-                 "gpush", "ev_push", "seed_step")
+                 "gpush", "seed_step", "w_c1", "w_c2", "w_c3")
 
     def __init__(self):
         for s in self.__slots__:
             setattr(self, s, None)
+
+
+class _PinRing:
+    """Host -> device uploads of small int64 tables through a ring of
+    pre-pinned buffers (no pinned allocation per step); a slot is reused only
+    after its previous copy's event completed (long before, in practice)."""
+
+    def __init__(self, dev, n=8, width=4096):
+        self.dev = dev
+        self.buf = [torch.empty(width, dtype=torch.int64, pin_memory=True) for _ in range(n)]
+        self.ev = [None] * n
+        self.i = 0
+
+    def put(self, arr):
+        k = self.i
+        self.i = (k + 1) % len(self.buf)
+        if arr.shape[0] > self.buf[k].numel():
+            self.buf[k] = torch.empty(2 * arr.shape[0], dtype=torch.int64, pin_memory=True)
+        if self.ev[k] is not None:
+            self.ev[k].synchronize()
+        h = self.buf[k][:arr.shape[0]]
+        h.numpy()[:] = arr
+        d = h.to(self.dev, non_blocking=True)
+        if self.ev[k] is None:
+            self.ev[k] = torch.cuda.Event()
+        self.ev[k].record()
+        return d
+
+
+class _EventRing:
+    """Reusable events: a stream wait captures the record it sees when it is
+    enqueued, so an event may be re-recorded once its waits are queued."""
+
+    def __init__(self, n=64):
+        self.ev = [torch.cuda.Event() for _ in range(n)]
+        self.i = 0
+
+    def record(self, stream):
+        ev = self.ev[self.i]
+        self.i = (self.i + 1) % len(self.ev)
+        ev.record(stream)
+        return ev
 
 
 class PsxDifacto:
@@ -70,6 +116,9 @@ class PsxDifacto:
         self.dev = lrn.device
         self.cuda = self.dev.type == "cuda"
         self.cs = torch.cuda.Stream(device=self.dev) if self.cuda else None
+        self.S = torch.cuda.current_stream(self.dev) if self.cuda else None
+        self.pins = _PinRing(self.dev) if self.cuda else None
+        self.events = _EventRing() if self.cuda else None
         self.tau = 1 if int(getattr(lrn.conf, "max_concurrency", 2) or 2) >= 2 else 0
         self.job = None     # (keys, LocalizeJob | finished tuple, carried step)
         self.pull = None    # opened, reply not yet exchanged
@@ -78,12 +127,13 @@ class PsxDifacto:
 
     # ------------------------------------------------------------ streams
     def _S(self):
-        return torch.cuda.current_stream(self.dev) if self.cuda else None
+        return self.S
 
     @contextlib.contextmanager
     def _on_cs(self, *inputs):
-        """Run a collective on the comm stream after the compute stream's
-        queued work; its outputs are consumed on S after :meth:`_join`."""
+        """Run work on the side stream (the C0 count exchange and its host
+        read) after the compute stream's queued work, without making the
+        compute stream wait for it."""
         if not self.cuda:
             yield
             return
@@ -94,22 +144,6 @@ class PsxDifacto:
                 t.record_stream(self.cs)
         with torch.cuda.stream(self.cs):
             yield
-
-    def _mark(self):
-        if not self.cuda:
-            return None
-        ev = torch.cuda.Event()
-        ev.record(self.cs)
-        return ev
-
-    def _join(self, ev, *outputs):
-        if ev is None:
-            return
-        S = self._S()
-        S.wait_event(ev)
-        for t in outputs:
-            if t is not None and t.is_cuda:
-                t.record_stream(S)
 
     # ------------------------------------------------------------ localize
     def _exchange(self, carried):
@@ -205,9 +239,7 @@ class PsxDifacto:
         a[3 * P + 4:4 * P + 4] = np.cumsum(st.Ho)
         if prev is not None:
             a[4 * P + 4:] = prev.vrecv
-        t = torch.from_numpy(a)
-        if self.cuda:
-            t = t.pin_memory().to(self.dev, non_blocking=True)
+        t = self.pins.put(a) if self.cuda else torch.from_numpy(a)
         st.tabs = t
         st.segS_w, st.segHS_w = t[0:P + 1], t[P + 1:2 * P + 2]
         st.segS_o, st.segHS_o = t[2 * P + 2:3 * P + 3], t[3 * P + 3:4 * P + 4]
@@ -215,40 +247,46 @@ class PsxDifacto:
             prev.vrecv_d = t[4 * P + 4:]
 
     # -------------------------------------------------------------- phases
-    def _open(self, st, insert):
-        lrn = self.lrn
+    def _c1(self, st):
+        """Issue C1: this minibatch's keys (+ counts) to their owners."""
         rec = ops.ps_records(st.uniq, st.ucnt if st.use_cnt else None)
-        with self._on_cs(rec):
-            keys_o = self.comm.all_to_all_v(rec, st.send, st.recv)
-        self._join(self._mark(), keys_o)
+        st.keys_o, st.w_c1 = self.comm.all_to_all_v_async(rec, st.send, st.recv)
+
+    def _open(self, st, insert):
+        """Owner side: wait for C1, then one fused open + header pack."""
+        lrn = self.lrn
+        st.w_c1.wait()
         n = sum(st.recv)
         lrn.kv.guard.before_open(n, self._remap)
-        st.keys_o = keys_o
         st.slot, st.vpos, st.chain, st.head, st.rbuf, st.vcnt = self.store.ps_open(
-            keys_o, st.use_cnt, st.segS_o, st.segHS_o, sum(st.Ho) + n, insert, st.train, lrn.hp,
-            lrn.threshold, lrn.l1_shrk, lrn.seed)
+            st.keys_o, st.use_cnt, st.segS_o, st.segHS_o, sum(st.Ho) + n, insert, st.train,
+            lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
+        st.keys_o = st.w_c1 = None
         lrn.kv.guard.after_open()
 
-    def _reply(self, st):
-        """C2 + worker unpack + forward (+ AUC) of an opened step."""
-        lrn = self.lrn
+    def _c2(self, st):
+        """Issue C2: the owner's pull reply regions back to the workers."""
         P = self.P
         send_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
         recv_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
-        with self._on_cs(st.rbuf):
-            rrecv = self.comm.all_to_all_v(st.rbuf[:sum(send_rows)], send_rows, recv_rows)
-        self._join(self._mark(), rrecv)
-        st.rrecv = rrecv
+        st.rrecv, st.w_c2 = self.comm.all_to_all_v_async(st.rbuf[:sum(send_rows)], send_rows,
+                                                         recv_rows)
         st.rbuf = None
-        st.hdr, st.rows = ops.ps_unpack(rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d)
-        st.py, st.dual, st.xv = ops.fm_forward(st.offset, st.lid, st.val, st.hdr, rrecv, self.vs,
-                                               st.label, ops.LOSS_LOGIT, lrn.met)
+
+    def _reply(self, st):
+        """Worker side: wait for C2, unpack, forward (+ AUC)."""
+        lrn = self.lrn
+        st.w_c2.wait()
+        st.w_c2 = None
+        st.hdr, st.rows = ops.ps_unpack(st.rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d)
+        st.py, st.dual, st.xv = ops.fm_forward(st.offset, st.lid, st.val, st.hdr, st.rrecv,
+                                               self.vs, st.label, ops.LOSS_LOGIT, lrn.met)
         ops.auc_acc(st.py, st.label, lrn.auc_sum)
         lrn.n_mb += 1
         lrn.last_sizes = (st.U, sum(st.vrecv))
 
     def _grad(self, st):
-        """Backward + gradient post-processing + C3 of a forwarded step."""
+        """Backward + gradient post-processing, then issue C3 (the push)."""
         lrn = self.lrn
         emb = lrn.emb
         P = self.P
@@ -264,10 +302,7 @@ class PsxDifacto:
         ops.ps_pack_gw(gw, gvc, st.segS_w, st.segHS_w, st.vrecv_d)
         send_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
         recv_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
-        with self._on_cs(gvc):
-            gpush = self.comm.all_to_all_v(gvc, send_rows, recv_rows)
-        st.ev_push = self._mark()
-        st.gpush = gpush
+        st.gpush, st.w_c3 = self.comm.all_to_all_v_async(gvc, send_rows, recv_rows)
         # the worker-side tensors of this step are done
         st.rrecv = st.hdr = st.dual = st.xv = st.lid = st.csc = None
 
@@ -281,7 +316,8 @@ class PsxDifacto:
 
     def _owner_push(self, st):
         lrn = self.lrn
-        self._join(st.ev_push, st.gpush)
+        st.w_c3.wait()
+        st.w_c3 = None
         self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o, st.gpush,
                            lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
         st.gpush = st.slot = st.vpos = st.chain = st.head = st.keys_o = None
@@ -311,24 +347,24 @@ class PsxDifacto:
         self.uhint = st.U
 
     def train(self, keys, offset, val, label, data_pass, next_batch):
+        if self.cuda:
+            self.S = torch.cuda.current_stream(self.dev)
         self._ensure_job(keys, offset, val)
         send, recv = self._counts()  # the step's one host read
         prev = self.pull
         if prev is not None and prev.vown is None:
             self._vcount_exchange(prev)
         st = self._new_step(send, recv, label, True, data_pass, prev)
-        if self.tau == 1 and prev is not None:
-            # the previous minibatch's reply + forward go first: the device
-            # gets work the moment the host read returns
-            self._reply(prev)
+        if prev is not None:
+            self._c2(prev)  # transfers while this minibatch's localize finishes
         self._set_loc(st, self._finish(), offset, val)
-        if self.tau == 0:
-            if prev is not None:
-                self._reply(prev)
-                if prev.train:
-                    self._grad(prev)
-                    self._owner_push(prev)
-        elif self.push is not None:
+        self._c1(st)        # transfers while the previous minibatch computes
+        if prev is not None:
+            self._reply(prev)
+            if self.tau == 0 and prev.train:
+                self._grad(prev)
+                self._owner_push(prev)
+        if self.push is not None:
             self._owner_push(self.push)
             self.push = None
         self._open(st, True)
@@ -337,7 +373,7 @@ class PsxDifacto:
             nk, no, nv = next_batch[:3]
             self._begin(nk, no, nv, st, next_batch[3] if len(next_batch) > 3 else None)
         if self.tau == 1 and prev is not None and prev.train:
-            self._grad(prev)
+            self._grad(prev)  # its push (C3) lands before the next call's open
             self.push = prev
         self.lrn.step += 1
 
@@ -349,16 +385,18 @@ class PsxDifacto:
         send, recv = self._counts()
         st = self._new_step(send, recv, label, False, 1, None)
         self._set_loc(st, self._finish(), offset, val)
+        self._c1(st)
         self._open(st, False)
         self._vcount_exchange(st)
         self._upload_vrecv(st)
+        self._c2(st)
         self._reply(st)
         self.lrn.step += 1
         return st.py
 
     def _upload_vrecv(self, st):
-        t = torch.tensor(st.vrecv, dtype=torch.int64)
-        st.vrecv_d = t.pin_memory().to(self.dev, non_blocking=True) if self.cuda else t
+        a = np.array(st.vrecv, dtype=np.int64)
+        st.vrecv_d = self.pins.put(a) if self.cuda else torch.from_numpy(a)
 
     def flush(self):
         """Complete every minibatch in flight (end of a pass, before reading
@@ -372,6 +410,7 @@ class PsxDifacto:
             if st.vown is None:
                 self._vcount_exchange(st)
             self._upload_vrecv(st)
+            self._c2(st)
             self._reply(st)
             if st.train:
                 self._grad(st)

@@ -50,6 +50,19 @@ class _Done:
         pass
 
 
+class _Keep:
+    """A pending collective plus the input it reads."""
+
+    def __init__(self, work, keep):
+        self.work = work
+        self.keep = keep
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+        self.work, self.keep = None, None
+
+
 class _Reqs:
     """Pending point-to-point group; keeps the send buffers alive."""
 
@@ -174,6 +187,28 @@ class Comm:
                                    [s * width for s in send_rows])
         return out
 
+    def all_to_all_v_async(self, x, send_rows, recv_rows):
+        """:meth:`all_to_all_v` without blocking the current stream: returns
+        (out, work); ``work.wait()`` orders the CURRENT stream (at the time
+        of the wait) after the transfer, so independent kernels queued in
+        between overlap it. RCCL runs it on the process group's own stream,
+        which waits for the current stream's queued work at issue time."""
+        if self.size == 1:
+            return x, _Done()
+        if self.stage and x.is_cuda:
+            return self.all_to_all_v(x, send_rows, recv_rows), _Done()
+        x = x.contiguous()
+        width = 1
+        for d in x.shape[1:]:
+            width *= int(d)
+        out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        if x.numel() == 0 and out.numel() == 0:
+            return out, _Done()
+        work = dist.all_to_all_single(out.view(-1), x.view(-1),
+                                      [r * width for r in recv_rows],
+                                      [s_ * width for s_ in send_rows], async_op=True)
+        return out, _Keep(work, x)
+
     def all_to_all_v_multi(self, items, async_op=False):
         """Several row-wise all-to-all-v exchanges issued back to back, one
         RCCL all-to-all-v per tensor (RCCL runs each as one grouped
@@ -265,6 +300,31 @@ class LoopbackComm(Comm):
     def all_to_all_v(self, x, send_rows, recv_rows):
         assert list(send_rows) == list(recv_rows), "loopback exchange must be symmetric"
         return x
+
+    def all_to_all_v_async(self, x, send_rows, recv_rows):
+        """:meth:`all_to_all_v` without blocking the current stream: returns
+        (out, work); ``work.wait()`` orders the CURRENT stream (at the time
+        of the wait) after the transfer, so independent kernels queued in
+        between overlap it. RCCL runs it on the process group's own stream,
+        which waits for the current stream's queued work at issue time."""
+        if self.size == 1:
+            return x, _Done()
+        if self.stage and x.is_cuda:
+            return self.all_to_all_v(x, send_rows, recv_rows), _Done()
+        x = x.contiguous()
+        width = 1
+        for d in x.shape[1:]:
+            width *= int(d)
+        out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        if x.numel() == 0 and out.numel() == 0:
+            return out, _Done()
+        work = dist.all_to_all_single(out.view(-1), x.view(-1),
+                                      [r * width for r in recv_rows],
+                                      [s_ * width for s_ in send_rows], async_op=True)
+        return out, _Keep(work, x)
+
+    def all_to_all_v_async(self, x, send_rows, recv_rows):
+        return self.all_to_all_v(x, send_rows, recv_rows), _Done()
 
     def all_to_all_v_multi(self, items, async_op=False):
         outs = [self.all_to_all_v(x, s, r) for x, s, r in items]
