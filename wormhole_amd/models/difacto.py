@@ -117,8 +117,13 @@ class DifactoLearner:
 
     def take_progress(self):
         """Progress vector in the reference layout (learn/difacto/progress.h):
-        [objv, auc, objv_w, copc, count, new_ex, new_w, new_V]; resets."""
-        self.flush()
+        [objv, auc, objv_w, copc, count, new_ex, new_w, new_V]; resets.
+
+        Local only: it may run at different minibatches on different ranks
+        (the worker reports on its own clock), so it must not issue
+        collectives -- minibatches still in the multi-shard pipeline are
+        counted by the next report; the end of a pass flushes first."""
+        self.kv.flush()
         ops.auc_join(self.auc_sum)
         m = self.met.tolist()
         a = float(self.auc_sum.item())

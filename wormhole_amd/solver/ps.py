@@ -283,4 +283,5 @@ class Worker:
                            stages_sec={k: v[0] for k, v in pass_stages.items()})
         if done_prev is not None:
             self.send(msg="finished", finished=done_prev)
+        self.learner.flush()  # collective: every rank leaves the loop together
         self.send(msg="pass_done", progress=self.learner.take_progress())
