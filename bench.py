@@ -73,8 +73,8 @@ def main():
                     help="minibatches in flight per worker (reference default 2): with >= 2 "
                          "the multi-shard step is pipelined one minibatch deep")
     args = ap.parse_args()
-    if args.prewarm is None:
-        args.prewarm = 1000 if args.model == "difacto" else 0
+    if args.prewarm is None:  # (the CPU rehearsal of the distributed path skips it)
+        args.prewarm = 1000 if (args.model == "difacto" and args.device == "cuda") else 0
 
     local = env_local_rank()
     if os.environ.get("WH_BENCH_SAME_GPU") == "1":

@@ -62,6 +62,16 @@ struct DevWs {
   // can be enqueued before minibatch i's assign has emptied its table
   Tensor loc_tab[2];
   Tensor loc_ovf[2];
+  // partitioned localize: its own look-back workspace (a localize may be
+  // begun on a side stream, concurrently with other look-back users) and
+  // {per-partition publish words, arrival counter}
+  Tensor lb_loc, part_ws;
+  // heavy-id hints, double-buffered by job parity: keys [2][kPartMaxHeavy]
+  // u64, then counts [2][kPartMaxOwners] u32
+  Tensor heavy_ws;
+  int heavy_parity = 0;
+  int64_t heavy_layout = -1;  // nshard * 65536 + nho of the set the last job elected
+  int part_inflight = 0;
   bool loc_dirty[2] = {false, false};
   bool loc_busy[2] = {false, false};
   int loc_next = 0;
@@ -78,6 +88,9 @@ DevWs& dev_ws(const torch::Device& d) {
     w->auc = torch::zeros({wh::auc_ws_persistent_bytes() / 8}, o.dtype(torch::kInt64));
     w->auc.select(0, wh::auc_ws_lohi_offset() / 8).fill_(-1);
     w->fwd_ticket = torch::zeros({4}, o.dtype(torch::kInt32));
+    w->lb_loc = torch::zeros({wh::lookback_ws_words()}, o.dtype(torch::kInt64));
+    w->part_ws = torch::zeros({wh::kPartMaxDigits + 2}, o.dtype(torch::kInt64));
+    w->heavy_ws = torch::zeros({2 * wh::kPartMaxHeavy + wh::kPartMaxOwners}, o.dtype(torch::kInt64));
     for (int b = 0; b < 2; ++b) {
       w->loc_tab[b] = torch::full({1024}, -1, o.dtype(torch::kInt64));
       w->loc_ovf[b] = torch::zeros({1}, o.dtype(torch::kInt64));
@@ -123,6 +136,32 @@ Tensor scan_excl(const Tensor& in) {
 // counts into pinned host memory (+ an event); finish() waits for that event
 // only, sizes the outputs and enqueues the rest. A learner begins minibatch
 // i+1 right after finishing minibatch i, so the wait overlaps i's training.
+// WH_DETERMINISTIC=1: bitwise-repeatable training steps: the
+// hash + stable-sort localize and ordered (atomic-free) gradient reductions
+bool deterministic() {
+  static int on = -1;
+  if (on < 0) {
+    const char* d = std::getenv("WH_DETERMINISTIC");
+    on = d && std::string(d) == "1";
+  }
+  return on == 1;
+}
+
+// WH_LOC_TIMING=1: the partitioned dedup stores per-partition phase
+// timestamps (100 MHz) into a device buffer (loc_timing_read) -- a profiling aid
+bool loc_timing() {
+  static int on = -1;
+  if (on < 0) on = std::getenv("WH_LOC_TIMING") != nullptr;
+  return on == 1;
+}
+Tensor& loc_timing_buf() {
+  static Tensor t;
+  if (!t.defined())
+    t = torch::zeros({4 * wh::kPartMaxDigits},
+                     torch::TensorOptions().dtype(torch::kInt64).device(torch::kCUDA));
+  return t;
+}
+
 class LocalizeJob {
  public:
   LocalizeJob(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
@@ -145,17 +184,27 @@ class LocalizeJob {
     safe_ = next_pow2(std::max<int64_t>(2 * nnz_, 1024));
     tsize_ = hint > 0 ? std::min(safe_, next_pow2(std::max<int64_t>(hint * 5 / 2, 1024))) : safe_;
     c10::DeviceGuard g(keys.device());
-    DevWs& ws = dev_ws(keys.device());
-    tab_ = ws.loc_next;
-    if (ws.loc_busy[tab_]) tab_ ^= 1;
-    TORCH_CHECK(!ws.loc_busy[tab_], "localize: at most two minibatches in flight per device");
-    ws.loc_busy[tab_] = true;
-    ws.loc_next = tab_ ^ 1;
+    // the partitioned path unless a deterministic localize is asked for (or
+    // the minibatch does not fit its plan); the hash path is the fallback
+    const int64_t uest = hint > 0 ? std::min<int64_t>(nnz_, hint * 5 / 4 + 1024) : nnz_;
+    plan_ = wh::loc_part_plan(nnz_, offset.numel() - 1, (int)nshard, uest, true);
+    part_ = plan_.ok && part_enabled();
+    if (!part_) acquire_table();
     enqueue();
+  }
+
+  static bool part_enabled() {
+    static int on = -1;
+    if (on < 0) {
+      const char* m = std::getenv("WH_LOCALIZE");
+      on = !(m && std::string(m) == "hash") && !deterministic();
+    }
+    return on == 1;
   }
 
   ~LocalizeJob() {
     if (event_) (void)hipEventDestroy(event_);
+    if (counted_) dev_ws(keys_.device()).part_inflight--;
     if (tab_ >= 0 && !done_) {
       DevWs& ws = dev_ws(keys_.device());
       ws.loc_busy[tab_] = false;  // abandoned: the table may hold keys
@@ -179,6 +228,17 @@ class LocalizeJob {
       bool over = own;
       for (int64_t q = 1; q < nrecv_; q += stride_) over |= h[nshard_ + 1 + q] != 0;
       if (!over) break;
+      if (part_) {  // a partition overflowed its LDS table (here or on a peer)
+        part_ = false;
+        if (counted_) {
+          ws.part_inflight--;
+          counted_ = false;
+        }
+        acquire_table();
+        tsize_ = safe_;
+        enqueue();
+        continue;
+      }
       TORCH_CHECK(!(own && tsize_ >= safe_), "localize: table overflow");
       // every rank saw the same flags: all retry at the safe size together
       ws.loc_dirty[tab_] = true;
@@ -206,6 +266,15 @@ class LocalizeJob {
     Tensor owner_cnt_h = owner_cnt_h_, recv_h = recv_h_;
     int64_t U = 0;
     for (int64_t p = 0; p < nshard_; ++p) U += owner_cnt_h.data_ptr<int64_t>()[p];
+    if (part_) {  // everything was computed before the host read
+      done_ = true;
+      if (counted_) {
+        ws.part_inflight--;
+        counted_ = false;
+      }
+      return {uniq_.narrow(0, 0, U), ucnt_.narrow(0, 0, U), owner_cnt_h, lid_,
+              csc_off_.narrow(0, 0, U + 1), csc_row_, csc_val_, recv_h};
+    }
     const int64_t nnz = nnz_, nrows = offset_.numel() - 1;
     const float* vp = val_.defined() ? ptr<float>(val_) : nullptr;
     auto tlid = torch::empty({tsize_}, i32);
@@ -238,11 +307,98 @@ class LocalizeJob {
   }
 
  private:
+  void acquire_table() {
+    DevWs& ws = dev_ws(keys_.device());
+    tab_ = ws.loc_next;
+    if (ws.loc_busy[tab_]) tab_ ^= 1;
+    TORCH_CHECK(!ws.loc_busy[tab_], "localize: at most two minibatches in flight per device");
+    ws.loc_busy[tab_] = true;
+    ws.loc_next = tab_ ^ 1;
+  }
+
+  // partitioned path: every output is produced before the count read
+  Tensor enqueue_part() {
+    auto s = cur_stream(keys_);
+    DevWs& ws = dev_ws(keys_.device());
+    auto i32 = keys_.options().dtype(torch::kInt32);
+    auto i64 = keys_.options().dtype(torch::kInt64);
+    const int64_t nnz = nnz_, nrows = offset_.numel() - 1;
+    const int nsh = (int)nshard_;
+    const float* vp = val_.defined() ? ptr<float>(val_) : nullptr;
+    auto owner_cnt = torch::empty({nshard_ + 1}, i64);
+    uniq_ = torch::empty({nnz}, i64);
+    ucnt_ = torch::empty({nnz}, i32);
+    csc_off_ = torch::empty({nnz + 1}, i64);
+    csc_row_ = torch::empty({nnz}, i32);
+    csc_val_ = torch::empty({vp ? nnz : 0}, keys_.options().dtype(torch::kFloat32));
+    lid_ = torch::empty({nnz}, i32);
+    // heavy-id hints: read the set the previous job elected, elect into the
+    // other buffer; a job begun while another is in flight uses none
+    wh::PartHeavy hv{};
+    if (plan_.nho > 0) {
+      auto* hk = reinterpret_cast<uint64_t*>(ws.heavy_ws.data_ptr());
+      auto* hc = reinterpret_cast<uint32_t*>(hk + 2 * wh::kPartMaxHeavy);
+      const int cur = ws.heavy_parity, nxt = cur ^ 1;
+      if (ws.part_inflight == 0) {
+        const int64_t layout = nshard_ * 65536 + plan_.nho;
+        hv.keys = hk + cur * wh::kPartMaxHeavy;
+        hv.cnt = hc + cur * wh::kPartMaxOwners;
+        hv.nho = ws.heavy_layout == layout ? plan_.nho : 0;  // else: elected for another layout
+        ws.heavy_layout = layout;
+        hv.next_keys = hk + nxt * wh::kPartMaxHeavy;
+        hv.next_cnt = hc + nxt * wh::kPartMaxOwners;
+        hv.nho_next = plan_.nho;
+        hv.thr = (uint32_t)std::max<int64_t>(1024, nnz / 1024);
+        ws.heavy_parity = nxt;
+      }
+    }
+    ws.part_inflight++;
+    counted_ = true;
+    const int64_t nh = (int64_t)plan_.ndig * plan_.ntiles;
+    auto hist = torch::empty({nh}, i32);
+    const auto* kp = reinterpret_cast<const uint64_t*>(keys_.data_ptr());
+    wh::loc_part_hist(kp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv,
+                      reinterpret_cast<uint32_t*>(hist.data_ptr()), s);
+    auto blkoff = torch::empty({nh + 1}, i64);
+    auto tmp = torch::empty({wh::scan_tmp_elems(nh)}, i64);
+    wh::scan_i32(ptr<int32_t>(hist), ptr<int64_t>(blkoff), nh, ptr<int64_t>(tmp), s);
+    auto pk = torch::empty({nnz}, i64);
+    auto pr = torch::empty({nnz}, i32);
+    auto pv = torch::empty({vp ? nnz : 0}, keys_.options().dtype(torch::kFloat32));
+    auto pos_of = torch::empty({nnz}, i32);
+    wh::loc_part_scatter(kp, vp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv, ptr<int64_t>(blkoff),
+                         reinterpret_cast<uint64_t*>(pk.data_ptr()), ptr<int32_t>(pr),
+                         vp ? ptr<float>(pv) : nullptr, ptr<int32_t>(pos_of), s);
+    auto plid = torch::empty({nnz}, i32);
+    auto* pw = reinterpret_cast<unsigned long long*>(ws.part_ws.data_ptr());
+    wh::loc_part_dedup(reinterpret_cast<const uint64_t*>(pk.data_ptr()), ptr<int32_t>(pr),
+                       vp ? ptr<float>(pv) : nullptr, nnz, nsh, plan_, hv, ptr<int64_t>(blkoff),
+                       wh::lookback_bind(ws.lb_loc.data_ptr()),
+                       reinterpret_cast<uint64_t*>(uniq_.data_ptr()), ptr<int32_t>(ucnt_),
+                       ptr<int64_t>(csc_off_), ptr<int32_t>(csc_row_),
+                       vp ? ptr<float>(csc_val_) : nullptr, ptr<int32_t>(plid), pw,
+                       reinterpret_cast<unsigned int*>(pw + wh::kPartMaxDigits),
+                       ptr<int64_t>(owner_cnt), s, loc_timing() ? ptr<int64_t>(loc_timing_buf()) : nullptr);
+    wh::loc_part_lid(ptr<int32_t>(pos_of), ptr<int32_t>(plid), nnz, ptr<int32_t>(lid_), s);
+    return owner_cnt;
+  }
+
   void enqueue() {
     auto s = cur_stream(keys_);
     DevWs& ws = dev_ws(keys_.device());
     auto i32 = keys_.options().dtype(torch::kInt32);
     auto i64 = keys_.options().dtype(torch::kInt64);
+    Tensor owner_cnt;
+    if (part_) {
+      owner_cnt = enqueue_part();
+    } else {
+      owner_cnt = enqueue_hash(ws, s, i32, i64);
+    }
+    exchange_and_read(owner_cnt, s);
+  }
+
+  Tensor enqueue_hash(DevWs& ws, hipStream_t s, const torch::TensorOptions& i32,
+                      const torch::TensorOptions& i64) {
     // The table is a persistent per-device slab that loc_assign leaves
     // empty, so a minibatch costs no clearing pass; it is re-filled only
     // after an overflow retry or an abandoned job (loc_dirty).
@@ -266,6 +422,10 @@ class LocalizeJob {
     wh::loc_owner_count(reinterpret_cast<const uint64_t*>(tkeys_.data_ptr()), tsize_,
                         (int)nshard_, ptr<int64_t>(blkoff_), ptr<int64_t>(owner_cnt),
                         ptr<int64_t>(ws.loc_ovf[tab_]), s);
+    return owner_cnt;
+  }
+
+  void exchange_and_read(const Tensor& owner_cnt, hipStream_t s) {
     Tensor both = owner_cnt;
     nrecv_ = 0;
     hipStream_t cs = s;  // stream of the count read
@@ -314,6 +474,10 @@ class LocalizeJob {
   int tab_ = -1;
   bool done_ = false;
   Tensor tkeys_, slot_of_, blkoff_, dev_counts_, host_, owner_cnt_h_, recv_h_;
+  Tensor uniq_, ucnt_, csc_off_, csc_row_, csc_val_, lid_;  // partitioned path outputs
+  wh::PartPlan plan_{};
+  bool part_ = false;
+  bool counted_ = false;  // in DevWs::part_inflight
   hipEvent_t event_ = nullptr;
 };
 
@@ -739,13 +903,16 @@ std::vector<Tensor> fm_backward(const Tensor& csc_off, const Tensor& csc_row,
   auto chunk_off = torch::empty({2 * (U + 1)}, i64);
   auto stmp = torch::empty({wh::scan_tmp_elems(U)}, i64);
   const wh::Lookback lb = lookback(csc_off.device());
+  Tensor det;
+  if (deterministic())
+    det = torch::empty({wh::fm_bwd_det_floats(U, nnz, (int)vstride)}, f32);
   wh::fm_backward(U, nnz, nrows, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row),
                   optptr<float>(csc_val), ptr<float>(dual),
                   vstride > 0 ? optptr<float>(xv) : nullptr, ptr<float>(w_or_hdr), vcp,
                   (int)vstride, ptr<float>(gw), gvc.numel() ? ptr<float>(gvc) : nullptr,
                   ptr<int32_t>(chunk_key), ptr<int32_t>(chunk_beg), ptr<int32_t>(meta_v),
                   ptr<int32_t>(bucket_hist), ptr<int64_t>(chunk_cnt), ptr<int64_t>(chunk_off),
-                  ptr<int64_t>(stmp), &lb, s);
+                  ptr<int64_t>(stmp), &lb, s, det.defined() ? ptr<float>(det) : nullptr);
   return {gw, gvc};
 }
 
@@ -1282,6 +1449,7 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("hint") = 0, py::arg("exchange") = py::none())
       .def("counts", &LocalizeJob::counts)
       .def("finish", &LocalizeJob::finish);
+  m.def("loc_timing_read", []() { return loc_timing_buf().clone(); });
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
         py::arg("nshard") = 1, py::arg("hint") = 0, py::arg("exchange") = py::none());
   m.def("fm_forward", &fm_forward);

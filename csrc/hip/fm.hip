@@ -611,7 +611,8 @@ __global__ __launch_bounds__(kThreads) void k_bwd_scalar(const int64_t* __restri
                                                          const int32_t* __restrict__ csc_row,
                                                          const float* __restrict__ csc_val,
                                                          const float* __restrict__ dual,
-                                                         float* __restrict__ gw_out) {
+                                                         float* __restrict__ gw_out,
+                                                         float* __restrict__ part_gw) {
   const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (c >= *nchunk_p) return;
   const int k = chunk_key[c];
@@ -632,8 +633,9 @@ __global__ __launch_bounds__(kThreads) void k_bwd_scalar(const int64_t* __restri
     for (int u = 0; u < 4; ++u) gw += dual[i[u]] * x[u];
   }
   for (; p < e; ++p) gw += dual[csc_row[p]] * (csc_val ? csc_val[p] : 1.f);
-  if (ke - kb > kChunk) atomicAdd(gw_out + k, gw);
-  else gw_out[k] = gw;
+  if (ke - kb <= kChunk) gw_out[k] = gw;
+  else if (part_gw) part_gw[c] = gw;  // deterministic: summed in chunk order later
+  else atomicAdd(gw_out + k, gw);
 }
 
 // V chunks: one wave per chunk, persistent over the (device-counted) list,
@@ -649,7 +651,9 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
                                                     const float* __restrict__ xv,
                                                     const float* __restrict__ vc, int vstride,
                                                     float* __restrict__ gw_out,
-                                                    float* __restrict__ gvc) {
+                                                    float* __restrict__ gvc,
+                                                    float* __restrict__ part_gw,
+                                                    float* __restrict__ part_gv) {
   using S = Shape<G>;
   __shared__ int2 stage[kThreads / 64][64];
   int2* st = stage[threadIdx.x >> 6];
@@ -730,17 +734,31 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
       acc.z += __shfl_xor(acc.z, o, 64); acc.w += __shfl_xor(acc.w, o, 64);
     }
     if (lane == 0) {
-      if (multi) atomicAdd(gw_out + mc.x, gw);
-      else gw_out[mc.x] = gw;
+      if (!multi) gw_out[mc.x] = gw;
+      else if (part_gw) part_gw[c] = gw;
+      else atomicAdd(gw_out + mc.x, gw);
     }
-    if (sub == 0) {
-      acc.x -= xxp * v.x; acc.y -= xxp * v.y; acc.z -= xxp * v.z; acc.w -= xxp * v.w;
-      float* gv = gvc + (int64_t)mc.w * vstride + gl * 4;
-      if (!multi) {
-        *reinterpret_cast<float4*>(gv) = acc;
-      } else {
-        atomicAdd(gv + 0, acc.x); atomicAdd(gv + 1, acc.y);
-        atomicAdd(gv + 2, acc.z); atomicAdd(gv + 3, acc.w);
+    acc.x -= xxp * v.x; acc.y -= xxp * v.y; acc.z -= xxp * v.z; acc.w -= xxp * v.w;
+    if (!multi || part_gv) {
+      // single chunk: the row itself; deterministic mode: this chunk's
+      // partial row (the list is key-major, unbucketed), summed in order later
+      float* dst = multi ? part_gv + c * (int64_t)vstride : gvc + (int64_t)mc.w * vstride;
+      if (sub == 0) *reinterpret_cast<float4*>(dst + gl * 4) = acc;
+    } else {
+      // every sub-group holds the whole row after the butterfly: lane l adds
+      // dim l (+ 64 c), so each atomic wave-instruction covers 256
+      // contiguous bytes (4 memory-side requests) instead of 16 lanes at a
+      // 16-byte stride (16 requests per row)
+      float* gv = gvc + (int64_t)mc.w * vstride;
+#pragma unroll
+      for (int c = 0; c < (S::VS + 63) / 64; ++c) {
+        const int d = c * 64 + lane;
+        const int src = (d >> 2) & (G - 1);
+        const float ax = __shfl(acc.x, src, 64), ay = __shfl(acc.y, src, 64);
+        const float az = __shfl(acc.z, src, 64), aw = __shfl(acc.w, src, 64);
+        const int comp = d & 3;
+        const float a = comp == 0 ? ax : comp == 1 ? ay : comp == 2 ? az : aw;
+        if (d < S::VS) atomicAdd(gv + d, a);
       }
     }
     // rotate the pipeline
@@ -748,6 +766,49 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
     mn = m2; rn = r2; xn = x2;
     m2 = m3;
   }
+}
+
+// Deterministic mode: the partials of every multi-chunk key, summed in chunk
+// order (= occurrence order) by one wave per key, found at its first chunk.
+__global__ __launch_bounds__(kThreads) void k_bwd_reduce_s(const int64_t* __restrict__ nchunk_p,
+                                                           const int32_t* __restrict__ chunk_key,
+                                                           const int32_t* __restrict__ chunk_beg,
+                                                           const int64_t* __restrict__ csc_off,
+                                                           const float* __restrict__ part_gw,
+                                                           float* __restrict__ gw_out) {
+  const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (c >= *nchunk_p) return;
+  const int k = chunk_key[c];
+  const int64_t kb = csc_off[k], cnt = csc_off[k + 1] - kb;
+  if (cnt <= kChunk || chunk_beg[c] != kb) return;
+  const int64_t n = (cnt + kChunk - 1) / kChunk;
+  float s = 0.f;
+  for (int64_t q = 0; q < n; ++q) s += part_gw[c + q];
+  gw_out[k] = s;
+}
+
+__global__ __launch_bounds__(kThreads) void k_bwd_reduce_v(const int64_t* __restrict__ nchunk_p,
+                                                           const int4* __restrict__ meta,
+                                                           const int64_t* __restrict__ csc_off,
+                                                           const float* __restrict__ part_gw,
+                                                           const float* __restrict__ part_gv,
+                                                           int vstride, float* __restrict__ gw_out,
+                                                           float* __restrict__ gvc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t c = ((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  if (c >= *nchunk_p) return;
+  const int4 m = meta[c];
+  if ((m.z >> 8) == 0 || (int64_t)m.y != csc_off[m.x]) return;  // not a hot key's first chunk
+  const int64_t cnt = csc_off[m.x + 1] - m.y;
+  const int64_t n = (cnt + kChunkV - 1) / kChunkV;
+  float g = 0.f;
+  for (int64_t q = 0; q < n; ++q) g += part_gw[c + q];
+  for (int d = lane; d < vstride; d += 64) {
+    float a = 0.f;
+    for (int64_t q = 0; q < n; ++q) a += part_gv[(c + q) * vstride + d];
+    gvc[(int64_t)m.w * vstride + d] = a;
+  }
+  if (lane == 0) gw_out[m.x] = g;
 }
 
 // gradient clipping / dropout / normalisation on the m embedding-gradient
@@ -867,7 +928,7 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
                  const float* hdr_f, const float* vc, int vstride, float* gw, float* gvc,
                  int32_t* chunk_key, int32_t* chunk_beg, int32_t* meta_v_i32, int32_t* bucket_hist,
                  int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, const Lookback* lb,
-                 hipStream_t s) {
+                 hipStream_t s, float* det_part) {
   int4* meta_v = reinterpret_cast<int4*>(meta_v_i32);
   if (nuniq <= 0) return;
   const float2* hdr = vstride > 0 ? reinterpret_cast<const float2*>(hdr_f) : nullptr;
@@ -894,24 +955,43 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
   // chunk counts are device values (off[nuniq]); the scalar kernel launches
   // over the host-side bound and surplus lanes exit; the V kernel is
   // persistent. No host synchronisation in the step.
-  hipLaunchKernelGGL(k_bwd_scalar, dim3(grid_for(cap_s, kThreads)), dim3(kThreads), 0, s,
-                     off_s + nuniq, key_s, beg_s, csc_off, csc_row, csc_val, dual, gw);
-  if (!hdr) return;
-  // order the V chunks by first-row bucket (meta_v[cap..2cap) receives the list)
+  // deterministic scratch: [cap_s] scalar partials | [vcap] V-chunk gw | [vcap, vstride] rows
   const int64_t vcap = v_cap(nuniq, nnz);
+  float* pgs = det_part;
+  float* pgv_w = det_part ? det_part + cap_s : nullptr;
+  float* pgv = det_part ? pgv_w + vcap : nullptr;
+  hipLaunchKernelGGL(k_bwd_scalar, dim3(grid_for(cap_s, kThreads)), dim3(kThreads), 0, s,
+                     off_s + nuniq, key_s, beg_s, csc_off, csc_row, csc_val, dual, gw, pgs);
+  if (det_part)
+    hipLaunchKernelGGL(k_bwd_reduce_s, dim3(grid_for(cap_s, kThreads)), dim3(kThreads), 0, s,
+                       off_s + nuniq, key_s, beg_s, csc_off, pgs, gw);
+  if (!hdr) return;
+  // order the V chunks by first-row bucket (meta_v[cap..2cap) receives the
+  // list); deterministic mode keeps the key-major list (partials by index)
   int4* meta_sorted = meta_v + vcap;
-  const int shift = bucket_shift(std::max<int64_t>(nrows, 1));
-  hipLaunchKernelGGL(k_vchunk_hist, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
-                     meta_v, csc_row, shift, bucket_hist);
-  hipLaunchKernelGGL(k_vchunk_scan, dim3(1), dim3(kBuckets * kScanParts), 0, s, bucket_hist);
-  hipLaunchKernelGGL(k_vchunk_scatter, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
-                     meta_v, csc_row, shift, bucket_hist, meta_sorted);
+  if (det_part) {
+    meta_sorted = meta_v;
+  } else {
+    const int shift = bucket_shift(std::max<int64_t>(nrows, 1));
+    hipLaunchKernelGGL(k_vchunk_hist, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
+                       meta_v, csc_row, shift, bucket_hist);
+    hipLaunchKernelGGL(k_vchunk_scan, dim3(1), dim3(kBuckets * kScanParts), 0, s, bucket_hist);
+    hipLaunchKernelGGL(k_vchunk_scatter, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
+                       meta_v, csc_row, shift, bucket_hist, meta_sorted);
+  }
   const int G = vstride / 4;
   const int64_t vblk = std::min<int64_t>((v_cap(nuniq, nnz) + 3) / 4,
                                          WH_RESIDENT(G, k_bwd_v, 2048));
   const dim3 grid((unsigned)vblk), block(kThreads);
   WH_DISPATCH_G(G, k_bwd_v, grid, block, 0, s, off_v + nuniq, meta_sorted, csc_row, csc_val,
-                dual, xv, vc, vstride, gw, gvc);
+                dual, xv, vc, vstride, gw, gvc, pgv_w, pgv);
+  if (det_part)
+    hipLaunchKernelGGL(k_bwd_reduce_v, dim3(grid_for(vcap * 64, kThreads)), dim3(kThreads), 0, s,
+                       off_v + nuniq, meta_v, csc_off, pgv_w, pgv, vstride, gw, gvc);
+}
+
+int64_t fm_bwd_det_floats(int64_t nuniq, int64_t nnz, int vstride) {
+  return scalar_cap(nuniq, nnz) + v_cap(nuniq, nnz) * (1 + (int64_t)vstride);
 }
 
 void fm_grad_post(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim, float clip,

@@ -68,6 +68,61 @@ void loc_csc(const int32_t* row_of, const float* val, int64_t nnz, int64_t nuniq
              int32_t* slid, int32_t* spos, void* sort_tmp, size_t sort_tmp_bytes,
              int64_t* csc_off, int32_t* ucnt, int32_t* csc_row, float* csc_val, hipStream_t s);
 
+// ------------------------------------------------------ localize_part.hip
+// Partitioned localize (the default path; no global atomics, no sort): a
+// radix-partition pass on an owner-major digit, then one workgroup per
+// partition de-duplicates, counts and places its non-zeros in LDS. Same
+// outputs as the path above (uniq/ucnt/csc_off sized by an upper bound; U =
+// sum of owner_cnt[0..nshard)); owner_cnt[nshard] != 0 flags a partition
+// whose distinct ids overflowed its LDS table (retry on the hash path).
+constexpr int kPartMaxDigits = 1024;
+constexpr int kPartMaxRows = 1024;
+constexpr int kPartMaxOwners = 1024;
+constexpr int kPartMaxHeavy = 512;  // heavy-id partitions over all owners
+struct PartPlan {
+  bool ok;
+  int npo_bits, nho, stride, ndig, R;  // owner o: digits [o*stride, o*stride + 2^npo_bits)
+  int64_t ntiles;                      // hashed, then nho heavy-id digits
+};
+// Heavy-id hint: the previous minibatch's ids with >= thr occurrences, per
+// owner (keys [nshard * nho], cnt [nshard]); the dedup elects this
+// minibatch's into next_* (next_cnt zeroed by loc_part_hist). Any content is
+// correct -- it only decides which ids get single-id partitions.
+struct PartHeavy {
+  const uint64_t* keys;
+  const uint32_t* cnt;
+  uint64_t* next_keys;
+  uint32_t* next_cnt;
+  int nho;       // heavy slots per owner read (0: none)
+  int nho_next;  // heavy slots per owner written (0: none)
+  uint32_t thr;
+};
+// uest: an upper estimate of the unique ids (nnz when nothing is known)
+PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, bool heavy);
+// hist [ndig * ntiles] uint32 (digit-major)
+void loc_part_hist(const uint64_t* keys, const int64_t* offset, int64_t nrows, int nshard,
+                   const PartPlan& pl, const PartHeavy& hv, uint32_t* hist, hipStream_t s);
+// blkoff = exclusive scan of hist (ndig * ntiles + 1 entries); pk/pr [nnz]
+// (+ pv [nnz] when val) in partition order; pos_of [nnz] in CSR order
+void loc_part_scatter(const uint64_t* keys, const float* val, const int64_t* offset,
+                      int64_t nrows, int nshard, const PartPlan& pl, const PartHeavy& hv,
+                      const int64_t* blkoff, uint64_t* pk, int32_t* pr, float* pv,
+                      int32_t* pos_of, hipStream_t s);
+// up [kPartMaxDigits] u64 and *arrive (0 between calls): a workspace of its
+// own; lb: a look-back workspace no concurrent kernel uses. plid [nnz]:
+// local ids in partition order.
+void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const float* pv, int64_t nnz,
+                    int nshard, const PartPlan& pl, const PartHeavy& hv, const int64_t* blkoff,
+                    const Lookback& lb,
+                    uint64_t* uniq, int32_t* ucnt, int64_t* csc_off, int32_t* csc_row,
+                    float* csc_val, int32_t* plid, unsigned long long* up, unsigned int* arrive,
+                    int64_t* owner_cnt, hipStream_t s, int64_t* tim = nullptr);
+// lid[j] = plid[pos_of[j]]
+void loc_part_lid(const int32_t* pos_of, const int32_t* plid, int64_t nnz, int32_t* lid,
+                  hipStream_t s);
+// nnz == 0: zero owner counts and csc_off[0]
+void loc_part_empty(int nshard, int64_t* owner_cnt, int64_t* csc_off, hipStream_t s);
+
 // ---------------------------------------------------------- kvstore.hip
 // Sharded parameter store (replaces the ps-lite server KVStore). Open
 // addressing, linear probing, 64-bit CAS insert.
@@ -231,7 +286,11 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
                  const float* hdr, const float* vc, int vstride, float* gw, float* gvc,
                  int32_t* chunk_key, int32_t* chunk_beg, int32_t* meta_v, int32_t* bucket_hist,
                  int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, const Lookback* lb,
-                 hipStream_t s);
+                 hipStream_t s, float* det_part = nullptr);
+// det_part (deterministic mode, WH_DETERMINISTIC=1): scratch of
+// fm_bwd_det_floats floats; hot keys' chunk partials are then summed in
+// occurrence order by a second pass instead of float atomics
+int64_t fm_bwd_det_floats(int64_t nuniq, int64_t nnz, int vstride);
 // post-process the m (device count) V-gradient rows: clip to [-c, c] (c>0),
 // dropout with prob p (p>0); sumsq (optional) receives the squared norm
 void fm_grad_post(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int dim, float clip,

@@ -302,28 +302,6 @@ class LoopbackComm(Comm):
         return x
 
     def all_to_all_v_async(self, x, send_rows, recv_rows):
-        """:meth:`all_to_all_v` without blocking the current stream: returns
-        (out, work); ``work.wait()`` orders the CURRENT stream (at the time
-        of the wait) after the transfer, so independent kernels queued in
-        between overlap it. RCCL runs it on the process group's own stream,
-        which waits for the current stream's queued work at issue time."""
-        if self.size == 1:
-            return x, _Done()
-        if self.stage and x.is_cuda:
-            return self.all_to_all_v(x, send_rows, recv_rows), _Done()
-        x = x.contiguous()
-        width = 1
-        for d in x.shape[1:]:
-            width *= int(d)
-        out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-        if x.numel() == 0 and out.numel() == 0:
-            return out, _Done()
-        work = dist.all_to_all_single(out.view(-1), x.view(-1),
-                                      [r * width for r in recv_rows],
-                                      [s_ * width for s_ in send_rows], async_op=True)
-        return out, _Keep(work, x)
-
-    def all_to_all_v_async(self, x, send_rows, recv_rows):
         return self.all_to_all_v(x, send_rows, recv_rows), _Done()
 
     def all_to_all_v_multi(self, items, async_op=False):

@@ -207,8 +207,10 @@ class Worker:
                                          self.device.type == "cuda")  # pinned: async H2D
             queue.append((d, it))
 
-        fetch()
-        while True:
+        def next_parsed():
+            """The next minibatch of this worker (None once its parts are
+            exhausted); prediction output files follow the workload."""
+            nonlocal pred_f, pred_name, done_prev
             batch = None
             while queue and batch is None:
                 d, it = queue[0]
@@ -229,20 +231,43 @@ class Worker:
                     done_prev = {"file": d["file"], "k": d["k"]}
                     if not queue:
                         fetch()
+            return batch
+
+        # Training parses one minibatch ahead and hands it to the learner
+        # (next_batch), which begins its localization -- and, on several
+        # ranks, the count exchange -- before training the current one, as
+        # bench.py does. The "have data" allreduce carries both flags so that
+        # every rank decides in lockstep whether a next minibatch is begun.
+        ahead = train
+        fetch()
+        batch = next_parsed()
+        nxt = next_parsed() if (ahead and batch is not None) else None
+        while True:
             have = 1 if batch is not None else 0
+            have_next = 1 if nxt is not None else 0
             if self.comm.size > 1:
-                flag = torch.tensor([have], dtype=torch.int32, device=self.comm.device)
+                flag = torch.tensor([have, have_next], dtype=torch.int32, device=self.comm.device)
                 self.comm.allreduce(flag)
-                if int(flag.item()) == 0:
+                have_all, next_all = (int(x) for x in flag.tolist())
+                if have_all == 0:
                     break
             elif not have:
                 break
+            else:
+                next_all = have_next
             with trace.stage("h2d"):
                 args = self._to_dev(batch) if batch is not None else self._empty_batch()
+                nargs = None
+                if ahead and next_all:
+                    nargs = self._to_dev(nxt) if nxt is not None else self._empty_batch()
             if self.fault and batch is not None:
                 self._inject_fault()
             with trace.stage("process"):
-                py = self.learner.process(*args, wtype=wtype, data_pass=data_pass)
+                if nargs is not None:
+                    py = self.learner.process(*args, wtype=wtype, data_pass=data_pass,
+                                              next_batch=(nargs[0], nargs[1], nargs[2]))
+                else:
+                    py = self.learner.process(*args, wtype=wtype, data_pass=data_pass)
             self.n_done += 1
             n_pass += 1
             n_ex += int(args[3].numel())
@@ -266,6 +291,10 @@ class Worker:
                     ex_last = n_ex
                 last = now
                 self.send(msg="progress", data=self.learner.take_progress())
+            if ahead:
+                batch, nxt = nxt, (next_parsed() if nxt is not None else None)
+            else:
+                batch = next_parsed()
         if pred_f:
             pred_f.close()
         # the reference worker's summary line (minibatch_solver.h:244-248)
