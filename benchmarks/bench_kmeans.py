@@ -70,7 +70,8 @@ def main():
                           "value": a.iters / dt, "unit": "iter/s", "n_gpus": bsp.world if dev.type == "cuda" else 0, "device": dev.type,
                           "ms_per_iter": 1000 * dt / a.iters, "rows_per_s": a.rows * a.iters / dt,
                           "assign_tflops": flops / dt / 1e12, "scaling": "strong",
-                          "dtype": "fp32 (exact fp32 MFMA)" if dev.type == "cuda" else "fp64 (CPU reference path)", "data": "synthetic gaussian mixture"}),
+                          "dtype": ("exact fp32 argmax (bf16x3 split MFMA + fp32 re-score of near-ties)" if km.split else "fp32 (exact fp32 MFMA)") if dev.type == "cuda" else "fp64 (CPU reference path)",
+                          "rescored_rows_last_iter": int(km.rescored.item()) if km.rescored is not None else None, "data": "synthetic gaussian mixture"}),
               flush=True)
     bsp.finalize()
 

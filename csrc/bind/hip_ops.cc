@@ -1387,6 +1387,54 @@ std::vector<Tensor> kmeans_assign(const Tensor& Xp, int64_t n, int64_t f, const 
   return {assign, score};
 }
 
+// split precision: X [n, f] -> (packed bf16 hi/lo fragments (uint8), row norms)
+std::vector<Tensor> kmeans_pack_x3(const Tensor& X) {
+  CHECK_IN(X, torch::kFloat32);
+  TORCH_CHECK(X.dim() == 2, "X must be [n, f]");
+  c10::DeviceGuard g(X.device());
+  const int64_t n = X.size(0);
+  const int f = (int)X.size(1);
+  TORCH_CHECK(wh::kmeans_x3_supported(f), "split-precision assign needs 1 <= f <= 128");
+  auto Xp = torch::empty({wh::kmeans_x3_xp_bytes(n, f)}, X.options().dtype(torch::kUInt8));
+  wh::kmeans_pack_x3(ptr<float>(X), n, f, Xp.data_ptr(), cur_stream(X));
+  auto xn = X.norm(2, {1}).contiguous();
+  return {Xp, xn};
+}
+
+Tensor kmeans_pack_c3(const Tensor& C) {
+  CHECK_IN(C, torch::kFloat32);
+  c10::DeviceGuard g(C.device());
+  const int k = (int)C.size(0), f = (int)C.size(1);
+  TORCH_CHECK(wh::kmeans_x3_supported(f), "split-precision assign needs 1 <= f <= 128");
+  auto Cp = torch::empty({wh::kmeans_x3_cp_bytes(k, f)}, C.options().dtype(torch::kUInt8));
+  wh::kmeans_pack_c3(ptr<float>(C), k, f, Cp.data_ptr(), cur_stream(C));
+  return Cp;
+}
+
+// returns (assign i32 [n], score f32 [n], near-tie count (device i32 [1]))
+std::vector<Tensor> kmeans_assign_x3(const Tensor& Xp, const Tensor& xnorm, const Tensor& X,
+                                     const Tensor& Cp, const Tensor& C) {
+  CHECK_IN(X, torch::kFloat32);
+  CHECK_IN(C, torch::kFloat32);
+  CHECK_IN(xnorm, torch::kFloat32);
+  CHECK_DEV(Xp);
+  CHECK_DEV(Cp);
+  c10::DeviceGuard g(X.device());
+  const int64_t n = X.size(0);
+  const int f = (int)X.size(1), k = (int)C.size(0);
+  TORCH_CHECK(C.size(1) == f && xnorm.numel() == n, "shape mismatch");
+  TORCH_CHECK(Xp.numel() == wh::kmeans_x3_xp_bytes(n, f), "packed X size mismatch");
+  TORCH_CHECK(Cp.numel() == wh::kmeans_x3_cp_bytes(k, f), "packed C size mismatch");
+  auto assign = torch::empty({n}, X.options().dtype(torch::kInt32));
+  auto score = torch::empty({n}, X.options());
+  auto amb = torch::empty({n + 1}, X.options().dtype(torch::kInt32));
+  auto ct = torch::empty({(int64_t)k * f}, X.options());
+  wh::kmeans_assign_x3(Xp.data_ptr(), ptr<float>(xnorm), ptr<float>(X), n, f, Cp.data_ptr(),
+                       ptr<float>(C), k, ptr<int32_t>(assign), ptr<float>(score),
+                       ptr<int32_t>(amb), ptr<float>(ct), cur_stream(X));
+  return {assign, score, amb.narrow(0, 0, 1)};
+}
+
 Tensor kmeans_accum(const Tensor& X, const Tensor& assign, int64_t k) {
   CHECK_IN(X, torch::kFloat32);
   CHECK_IN(assign, torch::kInt32);
@@ -1488,6 +1536,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_pack_c", &kmeans_pack_c);
   m.def("kmeans_assign", &kmeans_assign);
   m.def("kmeans_accum", &kmeans_accum);
+  m.def("kmeans_pack_x3", &kmeans_pack_x3);
+  m.def("kmeans_pack_c3", &kmeans_pack_c3);
+  m.def("kmeans_assign_x3", &kmeans_assign_x3);
   m.def("spmv_t", &spmv_t, py::arg("csc_off"), py::arg("csc_row"), py::arg("csc_val"),
         py::arg("p"));
   py::class_<KVStore>(m, "KVStore")

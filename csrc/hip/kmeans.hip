@@ -509,3 +509,404 @@ bool kmeans_accum_sorted(const float* X, int64_t n, int f, int k, const int32_t*
 }
 
 }  // namespace wh
+
+// ---- split-precision assignment (bf16 x 3 on the bf16 MFMA) ---------------
+// x.c = (xh + xl).(ch + cl) ~ xh.ch + xh.cl + xl.ch with hi = bf16(v), lo =
+// bf16(v - hi): three v_mfma_f32_32x32x16_bf16 per k-step of 16 features, at
+// 16x the fp32 MFMA rate (5.3x the arithmetic for 3 products). The dropped /
+// rounded terms are bounded by 3 * 2^-18 * |x| |c| plus the fp32 accumulation
+// (eps * |x|, |c| <= 1 for the normalised centroids), so a row whose best
+// and second-best approximate scores differ by at least 2 eps |x| has the
+// exact argmax; every other row (a near-tie) is re-scored in fp32 by
+// k_refine_rows. The result is the exact fp32 argmax, as the fp32 kernel's.
+namespace wh {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t bf16_rne(float v) {
+  const uint32_t u = __float_as_uint(v);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+// hi/lo bf16 pair of v packed as {hi, lo} 16-bit halves
+__device__ __forceinline__ void split_bf16(float v, uint32_t& hi, uint32_t& lo) {
+  hi = bf16_rne(v);
+  lo = bf16_rne(v - __uint_as_float(hi << 16));
+}
+
+// Xp3[((tile * ks + s) * 2 + hl) * 64 + lane] = 8 bf16 (uint4): lane l holds
+// X[row = tile*32 + (l&31)][16 s + 8 (l>>5) + j], j = 0..7 (the A-operand map
+// of mfma_f32_32x32x16_bf16)
+__global__ void k_pack_x3(const float* __restrict__ X, int64_t n, int f, int ks,
+                          uint4* __restrict__ Xp) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t ntiles = (n + 31) / 32;
+  if (t >= ntiles * ks * 64) return;
+  const int lane = (int)(t & 63);
+  const int64_t ts = t >> 6;
+  const int s = (int)(ts % ks);
+  const int64_t tile = ts / ks;
+  const int64_t row = tile * 32 + (lane & 31);
+  uint32_t h[8], l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = 16 * s + 8 * (lane >> 5) + j;
+    const float v = (row < n && col < f) ? X[row * f + col] : 0.f;
+    split_bf16(v, h[j], l[j]);
+  }
+  const int64_t base = (tile * ks + s) * 2 * 64 + lane;
+  Xp[base] = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16);
+  Xp[base + 64] =
+      make_uint4(l[0] | l[1] << 16, l[2] | l[3] << 16, l[4] | l[5] << 16, l[6] | l[7] << 16);
+}
+
+// Cp3[(((chunk * ks + s) * nsub + j) * 2 + hl) * 64 + lane]: the B-operand map,
+// centroid chunk * 32 nsub + 32 j + (lane & 31)
+__global__ void k_pack_c3(const float* __restrict__ C, int k, int f, int ks, int nchunk, int nsub,
+                          uint4* __restrict__ Cp) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)nchunk * ks * nsub * 64) return;
+  const int lane = (int)(t & 63);
+  int64_t q = t >> 6;
+  const int j = (int)(q % nsub);
+  q /= nsub;
+  const int s = (int)(q % ks);
+  const int chunk = (int)(q / ks);
+  const int cl = chunk * 32 * nsub + 32 * j + (lane & 31);
+  uint32_t h[8], l[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int col = 16 * s + 8 * (lane >> 5) + e;
+    const float v = (cl < k && col < f) ? C[(int64_t)cl * f + col] : 0.f;
+    split_bf16(v, h[e], l[e]);
+  }
+  const int64_t base = ((((int64_t)chunk * ks + s) * nsub + j) * 2) * 64 + lane;
+  Cp[base] = make_uint4(h[0] | h[1] << 16, h[2] | h[3] << 16, h[4] | h[5] << 16, h[6] | h[7] << 16);
+  Cp[base + 64] =
+      make_uint4(l[0] | l[1] << 16, l[2] | l[3] << 16, l[4] | l[5] << 16, l[6] | l[7] << 16);
+}
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// 8 waves (256 rows) share each centroid chunk, streamed through a 3-slot
+// LDS ring by LDS-DMA two chunks ahead: a chunk is only 48 MFMAs per wave
+// (~0.6 us), less than an L2 round trip, so a double buffer drained by a
+// full __syncthreads left the matrix pipe idle most of the time (21 ms/iter).
+constexpr int kX3Waves = 8;
+constexpr int kX3Threads = 64 * kX3Waves;
+
+template <int KS, int NSUB, int SLOTS>
+__global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __restrict__ Xp,
+                                                             const float* __restrict__ xnorm,
+                                                             int64_t n,
+                                                             const uint4* __restrict__ Cp,
+                                                             int nchunk, int k, float eps,
+                                                             int32_t* __restrict__ assign,
+                                                             float* __restrict__ score,
+                                                             int32_t* __restrict__ amb) {
+  constexpr int CH = 32 * NSUB;
+  constexpr int CF = KS * NSUB * 2 * 64;  // uint4 per chunk
+  constexpr int PER = CF / kX3Threads;    // 16-byte DMA pieces per thread per chunk
+  static_assert(PER * kX3Threads == CF, "chunk must split evenly");
+  __shared__ uint4 lds[SLOTS * CF];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t tile = (int64_t)blockIdx.x * kX3Waves + wid;
+  const bool live = tile < ntiles;
+  auto stage = [&](int slot, int c) {
+    const uint4* src = Cp + (int64_t)c * CF;
+    uint4* dst = lds + slot * CF;
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+      __builtin_amdgcn_global_load_lds(
+          src + i * kX3Threads + threadIdx.x,
+          (__attribute__((address_space(3))) void*)(dst + i * kX3Threads + wid * 64), 16, 0, 0);
+  };
+  bf16x8 ah[KS], al[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int64_t b = (tile * KS + s) * 2 * 64 + lane;
+    ah[s] = as_bf16x8(live ? Xp[b] : make_uint4(0, 0, 0, 0));
+    al[s] = as_bf16x8(live ? Xp[b + 64] : make_uint4(0, 0, 0, 0));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A fragments before the DMA count
+  stage(0, 0);
+  if (SLOTS == 3 && nchunk > 1) stage(1, 1);
+  float b1[16], b2[16];
+  int i1[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    b1[r] = -INFINITY;
+    b2[r] = -INFINITY;
+    i1[r] = 0x7fffffff;
+  }
+  // (padded centroid columns >= k start their accumulators at -1e30, so no
+  // per-score bounds test is needed; 5 VALU per score)
+  auto top2 = [&](const f32x16 (&sc)[NSUB], int cbase) {
+    const int col0 = cbase + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j) {
+        const float v = sc[j][r];
+        const bool nb = v > b1[r];
+        b2[r] = fmaxf(b2[r], fminf(b1[r], v));
+        i1[r] = nb ? col0 + 32 * j : i1[r];
+        b1[r] = fmaxf(b1[r], v);
+      }
+    }
+  };
+  for (int c = 0; c < nchunk; ++c) {
+    // this wave's pieces of chunk c have landed once at most the next
+    // chunk's PER pieces are outstanding; the barrier makes every wave's
+    // pieces visible and marks the slot of chunk c-1 free for chunk c+2
+    if (SLOTS == 3 && c + 1 < nchunk) {
+      static_assert(PER == 1 || PER == 2 || PER == 4 || PER == 8, "vmcnt immediates below");
+      if (PER == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (PER == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (PER == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+#if !defined(WH_X3_VARIANT) || WH_X3_VARIANT != 2
+    if (c + SLOTS - 1 < nchunk) stage((c + SLOTS - 1) % SLOTS, c + SLOTS - 1);
+#endif
+#if defined(WH_X3_VARIANT) && WH_X3_VARIANT == 2
+    const uint4* cur = lds;  // (microbench: chunk 0 only, no DMA in the loop)
+#else
+    const uint4* cur = lds + (c % SLOTS) * CF;
+#endif
+    f32x16 acc[NSUB];
+#pragma unroll
+    for (int j = 0; j < NSUB; ++j) {
+      const float init = c * CH + 32 * j + (lane & 31) < k ? 0.f : -1e30f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = init;
+    }
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 ch[NSUB], cl[NSUB];
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j) {
+        ch[j] = as_bf16x8(cur[((s * NSUB + j) * 2) * 64 + lane]);
+        cl[j] = as_bf16x8(cur[((s * NSUB + j) * 2 + 1) * 64 + lane]);
+      }
+      // independent accumulators interleaved between dependent MFMAs
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], ch[j], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], cl[j], acc[j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < NSUB; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], ch[j], acc[j], 0, 0, 0);
+    }
+#if !defined(WH_X3_VARIANT) || WH_X3_VARIANT != 1
+    top2(acc, c * CH);
+#else
+    if (acc[0][0] == 12345.f) b1[0] = 1.f;  // (microbench: no epilogue)
+#endif
+  }
+  if (!live) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v1 = b1[r], v2 = b2[r];
+    int kk = i1[r];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+      const float o1 = __shfl_xor(v1, o, 64), o2 = __shfl_xor(v2, o, 64);
+      const int ok = __shfl_xor(kk, o, 64);
+      if (o1 > v1 || (o1 == v1 && ok < kk)) {
+        v2 = fmaxf(v1, o2);
+        v1 = o1;
+        kk = ok;
+      } else {
+        v2 = fmaxf(v2, o1);
+      }
+    }
+    if ((lane & 31) == 0) {
+      const int64_t row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (row < n) {
+        assign[row] = kk == 0x7fffffff ? 0 : kk;
+        if (score) score[row] = v1;
+        if (!(v1 - v2 >= 2.f * eps * xnorm[row])) {  // a near-tie: exact re-score
+          const int q = atomicAdd(amb, 1);
+          amb[1 + q] = (int32_t)row;
+        }
+      }
+    }
+  }
+}
+
+// exact fp32 argmax over all k centroids for the near-tie rows: a wave takes
+// 4 listed rows (their features in LDS, broadcast) and lane l the centroids
+// l, l + 64, ... of the transposed C (coalesced 256-byte loads, each shared by
+// the 4 rows); persistent over the device-counted list; ties -> lowest index.
+constexpr int kRefRows = 4;
+constexpr int kRefMaxF = 128;
+
+__global__ void k_transpose_c(const float* __restrict__ C, int k, int f, float* __restrict__ CT) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)k * f) return;
+  const int c = (int)(t / f), e = (int)(t % f);
+  CT[(int64_t)e * k + c] = C[t];
+}
+
+__global__ __launch_bounds__(256) void k_refine_rows(const float* __restrict__ X, int f,
+                                                     const float* __restrict__ CT, int k,
+                                                     const int32_t* __restrict__ amb,
+                                                     int32_t* __restrict__ assign,
+                                                     float* __restrict__ score) {
+  __shared__ float sx[4][kRefRows][kRefMaxF];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int cnt = amb[0];
+  const int ngroups = (cnt + kRefRows - 1) / kRefRows;
+  for (int g = blockIdx.x * 4 + wid; g < ngroups; g += gridDim.x * 4) {
+    int64_t rows[kRefRows];
+#pragma unroll
+    for (int q = 0; q < kRefRows; ++q) {
+      const int i = g * kRefRows + q;
+      rows[q] = i < cnt ? amb[1 + i] : -1;
+      for (int e = lane; e < kRefMaxF; e += 64)
+        sx[wid][q][e] = (rows[q] >= 0 && e < f) ? X[rows[q] * f + e] : 0.f;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float bv[kRefRows];
+    int bi[kRefRows];
+#pragma unroll
+    for (int q = 0; q < kRefRows; ++q) {
+      bv[q] = -INFINITY;
+      bi[q] = 0x7fffffff;
+    }
+    for (int c0 = 0; c0 < k; c0 += 64 * 4) {
+      float d[kRefRows][4];
+#pragma unroll
+      for (int q = 0; q < kRefRows; ++q)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) d[q][u] = 0.f;
+      for (int e = 0; e < f; ++e) {
+        float cv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int c = c0 + u * 64 + lane;
+          cv[u] = c < k ? CT[(int64_t)e * k + c] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < kRefRows; ++q) {
+          const float xe = sx[wid][q][e];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) d[q][u] = fmaf(xe, cv[u], d[q][u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // centroid index increases with u: '>' keeps the lowest
+        const int c = c0 + u * 64 + lane;
+        if (c < k) {
+#pragma unroll
+          for (int q = 0; q < kRefRows; ++q)
+            if (d[q][u] > bv[q]) {
+              bv[q] = d[q][u];
+              bi[q] = c;
+            }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kRefRows; ++q) {
+      float v = bv[q];
+      int kk = bi[q];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(v, o, 64);
+        const int ok = __shfl_xor(kk, o, 64);
+        if (ov > v || (ov == v && ok < kk)) {
+          v = ov;
+          kk = ok;
+        }
+      }
+      if (lane == 0 && rows[q] >= 0) {
+        assign[rows[q]] = kk == 0x7fffffff ? 0 : kk;
+        if (score) score[rows[q]] = v;
+      }
+    }
+  }
+}
+
+#ifndef WH_X3_NSUB
+#define WH_X3_NSUB 4
+#endif
+constexpr int kX3Nsub = WH_X3_NSUB;
+constexpr int kX3Slots = kX3Nsub == 4 ? 2 : 3;  // LDS ring: SLOTS x (KS * NSUB * 2 KiB)
+
+int x3_ks(int f) {  // k-steps of 16 features, padded to the template widths
+  const int ks = (f + 15) / 16;
+  return ks <= 2 ? 2 : ks <= 4 ? 4 : 8;
+}
+
+}  // namespace
+
+bool kmeans_x3_supported(int f) { return f >= 1 && f <= 128; }
+
+int64_t kmeans_x3_xp_bytes(int64_t n, int f) {
+  return (n + 31) / 32 * x3_ks(f) * 2 * 64 * 16;
+}
+
+int64_t kmeans_x3_cp_bytes(int k, int f) {
+  const int nchunk = (k + 32 * kX3Nsub - 1) / (32 * kX3Nsub);
+  return (int64_t)nchunk * x3_ks(f) * kX3Nsub * 2 * 64 * 16;
+}
+
+void kmeans_pack_x3(const float* X, int64_t n, int f, void* Xp, hipStream_t s) {
+  const int ks = x3_ks(f);
+  const int64_t total = (n + 31) / 32 * ks * 64;
+  if (total <= 0) return;
+  hipLaunchKernelGGL(k_pack_x3, dim3(grid_for(total, 256)), dim3(256), 0, s, X, n, f, ks,
+                     static_cast<uint4*>(Xp));
+}
+
+void kmeans_pack_c3(const float* C, int k, int f, void* Cp, hipStream_t s) {
+  const int ks = x3_ks(f);
+  const int nchunk = (k + 32 * kX3Nsub - 1) / (32 * kX3Nsub);
+  const int64_t total = (int64_t)nchunk * ks * kX3Nsub * 64;
+  hipLaunchKernelGGL(k_pack_c3, dim3(grid_for(total, 256)), dim3(256), 0, s, C, k, f, ks, nchunk,
+                     kX3Nsub, static_cast<uint4*>(Cp));
+}
+
+void kmeans_assign_x3(const void* Xp, const float* xnorm, const float* X, int64_t n, int f,
+                      const void* Cp, const float* C, int k, int32_t* assign, float* score,
+                      int32_t* amb, float* ct, hipStream_t s) {
+  if (n <= 0) return;
+  const int ks = x3_ks(f);
+  const int nchunk = (k + 32 * kX3Nsub - 1) / (32 * kX3Nsub);
+  const dim3 grid((unsigned)(((n + 31) / 32 + kX3Waves - 1) / kX3Waves)), block(kX3Threads);
+  // eps: 3 * 2^-18 for the split + 2^-24 * (3 * 16 * ks) for the fp32 sums, x2 margin
+  const float eps = 2.f * (3.f / 262144.f + (48.f * ks) / 16777216.f);
+  WH_HIP_CHECK(hipMemsetAsync(amb, 0, sizeof(int32_t), s));
+  const uint4* xp = static_cast<const uint4*>(Xp);
+  const uint4* cp = static_cast<const uint4*>(Cp);
+  switch (ks) {
+    case 2:
+      hipLaunchKernelGGL((k_assign_x3<2, kX3Nsub, kX3Slots>), grid, block, 0, s, xp, xnorm, n, cp, nchunk, k,
+                         eps, assign, score, amb);
+      break;
+    case 4:
+      hipLaunchKernelGGL((k_assign_x3<4, kX3Nsub, kX3Slots>), grid, block, 0, s, xp, xnorm, n, cp, nchunk, k,
+                         eps, assign, score, amb);
+      break;
+    default:
+      hipLaunchKernelGGL((k_assign_x3<8, kX3Nsub, kX3Slots>), grid, block, 0, s, xp, xnorm, n, cp, nchunk, k,
+                         eps, assign, score, amb);
+      break;
+  }
+  hipLaunchKernelGGL(k_transpose_c, dim3(grid_for((int64_t)k * f, 256)), dim3(256), 0, s, C, k, f,
+                     ct);
+  hipLaunchKernelGGL(k_refine_rows, dim3(1024), dim3(256), 0, s, X, f, ct, k, amb, assign, score);
+}
+
+}  // namespace wh

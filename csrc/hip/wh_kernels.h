@@ -334,6 +334,18 @@ void synth_criteo(int64_t nrows, uint64_t seed, uint64_t step, const int64_t* ca
 
 // ------------------------------------------------------------ kmeans.hip
 int kmeans_ks(int f);  // padded MFMA k-steps (2 features each)
+// split-precision assignment (bf16 x 3 MFMA + exact fp32 re-score of the
+// near-tie rows): the exact fp32 argmax for f <= 128. Xp3 / Cp3 are opaque
+// packed buffers of the given byte sizes; xnorm [n] = row L2 norms; amb
+// [1 + n] int32 scratch (count, then the re-scored rows).
+bool kmeans_x3_supported(int f);
+int64_t kmeans_x3_xp_bytes(int64_t n, int f);
+int64_t kmeans_x3_cp_bytes(int k, int f);
+void kmeans_pack_x3(const float* X, int64_t n, int f, void* Xp3, hipStream_t s);
+void kmeans_pack_c3(const float* C, int k, int f, void* Cp3, hipStream_t s);
+void kmeans_assign_x3(const void* Xp3, const float* xnorm, const float* X, int64_t n, int f,
+                      const void* Cp3, const float* C, int k, int32_t* assign, float* score,
+                      int32_t* amb, float* ct, hipStream_t s);  // ct: [f * k] scratch
 void kmeans_pack_x(const float* X, int64_t n, int f, float* Xp, hipStream_t s);
 int64_t kmeans_cp_elems(int k, int f);  // packed centroid floats
 void kmeans_pack_c(const float* C, int k, int f, float* Cp, hipStream_t s);

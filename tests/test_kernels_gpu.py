@@ -581,3 +581,33 @@ def test_owlqn_kernels(hip, l1):
     dots = hip.multi_dot(H.to(DEV), ia.to(DEV), ib.to(DEV)).cpu()
     ref = (H[ia.long()].double() * H[ib.long()].double()).sum(1)
     assert torch.allclose(dots, ref, rtol=1e-10, atol=1e-9)
+
+
+@pytest.mark.parametrize("n,f,k", [(1000, 5, 7), (4096, 64, 33), (5000, 127, 100),
+                                   (3000, 128, 1000), (2000, 17, 300)])
+def test_kmeans_split_precision_matches_fp32(hip, n, f, k):
+    """bf16 x 3 MFMA scores + exact fp32 re-score of near-ties: the argmax is
+    the fp32 kernel's on random data, and planted near-ties (duplicated
+    centroids perturbed below the split's error bound) are re-scored."""
+    g = torch.Generator().manual_seed(7 * n + f + k)
+    X = torch.randn(n, f, generator=g)
+    C = torch.nn.functional.normalize(torch.randn(k, f, generator=g), dim=1)
+    if k >= 7:  # near-duplicate centroids: rows near them tie within the bound
+        C[1] = torch.nn.functional.normalize(C[0] + 1e-6 * torch.randn(f, generator=g), dim=0)
+        X[: n // 10] = C[0] * 3 + 1e-3 * torch.randn(n // 10, f, generator=g)
+    Xd, Cd = X.to(DEV), C.to(DEV)
+    a32, _ = hip.kmeans_assign(hip.kmeans_pack_x(Xd), n, f, hip.kmeans_pack_c(Cd), k)
+    Xp3, xn = hip.kmeans_pack_x3(Xd)
+    a3, s3, namb = hip.kmeans_assign_x3(Xp3, xn, Xd, hip.kmeans_pack_c3(Cd), Cd)
+    S = X.double() @ C.double().t()
+    best = S.max(1).values
+    got = S.gather(1, a3.cpu().long()[:, None])[:, 0]
+    assert bool(((best - got) <= 1e-5 * best.abs().clamp_min(1)).all())
+    differ = (a3 != a32).cpu()
+    if k >= 7:
+        assert int(namb.item()) >= n // 10  # the planted ties took the exact path
+        # any disagreement with the fp32 kernel is a planted (fp32-level) tie
+        assert bool((differ.nonzero()[:, 0] < n // 10).all())
+    else:
+        assert not bool(differ.any())
+    assert torch.allclose(s3.cpu().double(), got, atol=1e-4, rtol=1e-4)

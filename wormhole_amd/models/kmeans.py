@@ -5,11 +5,19 @@ fragment-packed copy), so one iteration is: pack C -> fused MFMA X.C^T +
 row argmax -> per-cluster sum/count with row-contiguous atomics -> one
 allreduce of K x (F+1) floats (RCCL) -> mean + L2 normalise -> checkpoint.
 
+Assignment precision (MI355X): for F <= 128 the scores come from the bf16
+MFMA as a three-product hi/lo split (bf16 x 3, 16x the fp32 MFMA rate) with
+a proven error bound; every row whose best two scores are closer than twice
+the bound is re-scored in exact fp32, so the argmax is the exact fp32 one.
+WH_KMEANS_PREC=fp32 selects the plain fp32 MFMA kernel.
+
 Deviations from the reference (fixed): a zero-norm
 centroid row is skipped instead of aborting the normalisation of the rest,
 and an empty cluster keeps its previous centroid (with a warning) instead of
 exit(-1).
 """
+import os
+
 import torch
 
 from .. import _native
@@ -40,8 +48,15 @@ class KMeans:
         self.k = int(k)
         self.device = X.device
         self.gpu = X.is_cuda
-        self.Xp = _native.hip().kmeans_pack_x(self.X) if self.gpu else None
+        self.split = (self.gpu and 1 <= self.f <= 128 and
+                      os.environ.get("WH_KMEANS_PREC", "split") != "fp32")
+        self.Xp = self.xnorm = None
+        if self.split:
+            self.Xp, self.xnorm = _native.hip().kmeans_pack_x3(self.X)
+        elif self.gpu:
+            self.Xp = _native.hip().kmeans_pack_x(self.X)
         self.C = None
+        self.rescored = None  # device count of near-tie rows re-scored in fp32 (last assign)
 
     def init_centroids(self, seed=0):
         """Reference InitCentroids: every rank draws num_cluster random rows of
@@ -57,6 +72,12 @@ class KMeans:
         self.C = normalize_rows(C)
 
     def assign(self):
+        if self.split:
+            hip = _native.hip()
+            C = self.C.contiguous()
+            a, _, self.rescored = hip.kmeans_assign_x3(self.Xp, self.xnorm, self.X,
+                                                       hip.kmeans_pack_c3(C), C)
+            return a
         if self.gpu:
             hip = _native.hip()
             Cp = hip.kmeans_pack_c(self.C.contiguous())
