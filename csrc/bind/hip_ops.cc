@@ -2,11 +2,16 @@
 // wormhole_amd._hip). Host-only translation unit: validates tensors, sizes
 // outputs and launches on the current PyTorch HIP stream.
 #include <torch/extension.h>
+#include <pybind11/stl.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <array>
 #include <cstdlib>
+#include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -1485,6 +1490,308 @@ Tensor spmv_t(const Tensor& csc_off, const Tensor& csc_row, const c10::optional<
   return y;
 }
 
+
+// ------------------------------------------------------------ gbdt grower
+// Depth-wise histogram tree growth with the level loop in C++ (reference:
+// xgboost hist updater driven by bin/xgboost.dmlc). Per level
+// ONE host synchronisation: the split results of this level and the
+// partition counts of the previous one come back in a single pinned copy;
+// the child row segments the histograms need are derived on the device
+// (k_child_segs), histogram tasks address them by chunk index, and the
+// sibling histograms are parent - built child in one kernel. Host tables go
+// down as one pinned upload per level. (The Python level loop it replaces
+// left the GPU idle ~60% of each tree on per-node Python work and two syncs
+// per level.)
+struct GrowParams {
+  double eta, alpha, lambda, mcw, rt_eps;
+  int max_depth;
+};
+
+class PinnedBuf {
+ public:
+  template <typename T>
+  T* get(int64_t n) {
+    const int64_t bytes = std::max<int64_t>(n * (int64_t)sizeof(T), 8);
+    if (!t_.defined() || t_.numel() < bytes)
+      t_ = torch::empty({bytes * 2}, torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(true));
+    return reinterpret_cast<T*>(t_.data_ptr());
+  }
+  Tensor tensor() const { return t_; }
+
+ private:
+  Tensor t_;
+};
+
+static double l1_threshold(double g, double alpha) {
+  if (alpha <= 0) return g;
+  return g > alpha ? g - alpha : (g < -alpha ? g + alpha : 0.0);
+}
+
+py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, const Tensor& gpair,
+                    const Tensor& qscale, const Tensor& valid, int64_t nbin,
+                    std::vector<std::pair<int64_t, int64_t>> fgroups, int64_t max_fcnt,
+                    std::vector<double> root_tot, std::vector<float> cut_vals,
+                    std::vector<int64_t> cut_off, double eta, double alpha, double lambda,
+                    double mcw, int64_t max_depth, double rt_eps, py::object allreduce) {
+  CHECK_IN(B, torch::kUInt8);
+  CHECK_IN(Bc, torch::kUInt8);
+  CHECK_IN(ridx0, torch::kInt32);
+  CHECK_IN(gpair, torch::kFloat32);
+  CHECK_IN(qscale, torch::kFloat32);
+  CHECK_DEV(valid);
+  c10::DeviceGuard g(B.device());
+  auto s = cur_stream(B);
+  const int64_t n = ridx0.numel();
+  const int F = (int)B.size(1);
+  TORCH_CHECK(n < (int64_t)INT32_MAX, "rows must fit int32");
+  const int G = (int)fgroups.size();
+  const bool dw = F % 4 == 0 && max_fcnt % 4 == 0;
+  const int64_t per = (int64_t)F * nbin * 2;
+  auto f64 = B.options().dtype(torch::kFloat64);
+  auto i32 = B.options().dtype(torch::kInt32);
+  const int chunk = (int)std::max<int64_t>(8192, (n + 1023) / 1024);
+  const bool reduce = !allreduce.is_none();
+  // host tree
+  std::vector<int> feat, bin, defl, left, right, parent;
+  std::vector<double> gain, cover, bw, leaf;
+  std::vector<std::array<double, 2>> tot;
+  auto add = [&](int par) {
+    feat.push_back(-1), bin.push_back(0), defl.push_back(0), left.push_back(-1),
+        right.push_back(-1), parent.push_back(par), gain.push_back(0), cover.push_back(0),
+        bw.push_back(0), leaf.push_back(0), tot.push_back({0, 0});
+    return (int)feat.size() - 1;
+  };
+  auto weight = [&](double G_, double H_) {
+    if (H_ < mcw) return 0.0;
+    return -l1_threshold(G_, alpha) / (H_ + lambda);
+  };
+  const int root = add(-1);
+  tot[root] = {root_tot[0], root_tot[1]};
+  std::map<int, std::pair<int, int>> seg;  // live frontier segments (node -> [b, e))
+  seg[root] = {0, (int)n};
+  std::vector<std::array<int, 3>> done;    // finished leaves: node, b, e
+  PinnedBuf up, up_tasks, down;  // separate staging: an upload may still be in flight
+  Tensor ridx = ridx0;
+  // histogram of the given (slot -> [b, e) device segments); tasks by chunk
+  auto build_hist = [&](const Tensor& dseg, const std::vector<int64_t>& seglen) -> Tensor {
+    const int S = (int)seglen.size();
+    std::vector<int32_t> tasks, red;
+    for (int k = 0; k < S; ++k) {
+      const int64_t nch = std::max<int64_t>(1, (seglen[k] + chunk - 1) / chunk);
+      const int t0 = (int)(tasks.size() / 5);
+      for (int64_t c = 0; c < nch; ++c)
+        for (auto& fg : fgroups) {
+          tasks.insert(tasks.end(), {k, (int)fg.first, (int)fg.second, (int)c, chunk});
+        }
+      for (int gi = 0; gi < G; ++gi)
+        red.insert(red.end(), {k, (int)fgroups[gi].first, (int)fgroups[gi].second, t0 + gi,
+                               (int)nch, G});
+    }
+    const int64_t nt = (int64_t)tasks.size() / 5, nr = (int64_t)red.size() / 6;
+    int32_t* h = up_tasks.get<int32_t>(tasks.size() + red.size());
+    std::memcpy(h, tasks.data(), tasks.size() * 4);
+    std::memcpy(h + tasks.size(), red.data(), red.size() * 4);
+    auto d = up_tasks.tensor().narrow(0, 0, (int64_t)(tasks.size() + red.size()) * 4)
+                 .to(B.device(), /*non_blocking=*/true).view(torch::kInt32);
+    auto hist = torch::empty({S, F, nbin, 2}, f64);
+    auto part = torch::empty({nt * wh::gbdt_hist_pstride((int)max_fcnt, (int)nbin)},
+                             gpair.options().dtype(torch::kInt64));
+    wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
+                  ptr<float>(qscale), ptr<int32_t>(d), (int)nt, ptr<int32_t>(d) + nt * 5,
+                  (int)nr, (int)max_fcnt, dw, ptr<int64_t>(part), ptr<double>(hist), s,
+                  ptr<int32_t>(dseg), chunk);
+    // the pinned staging buffer is reused by the next upload: wait for this one
+    WH_HIP_CHECK_HOST(hipStreamSynchronize(s));
+    if (reduce) allreduce(hist);
+    return hist;
+  };
+  Tensor dseg_root = torch::tensor({0, (int)n}, torch::TensorOptions().dtype(torch::kInt32))
+                         .to(B.device());
+  Tensor H_front = build_hist(dseg_root, {n});
+  std::vector<int> frontier{root};
+  // splits whose children's segments wait for the partition counts
+  std::vector<std::array<int, 5>> pending;  // nd, l, r, b, e
+  Tensor nleft_dev;
+  for (int depth = 0; depth <= max_depth && !frontier.empty(); ++depth) {
+    const int S = (int)frontier.size();
+    const bool last = depth == max_depth;
+    Tensor split_out;
+    if (!last) {
+      double* th = up.get<double>(2 * S);
+      for (int k = 0; k < S; ++k) th[2 * k] = tot[frontier[k]][0], th[2 * k + 1] = tot[frontier[k]][1];
+      auto T = up.tensor().narrow(0, 0, 16 * S).to(B.device(), true).view(torch::kFloat64);
+      split_out = torch::empty({S, 6}, f64);
+      auto cand = torch::empty({std::max<int64_t>((int64_t)S * F * 4, 1)}, f64);
+      TORCH_CHECK(wh::gbdt_split(ptr<double>(H_front), ptr<double>(T),
+                                 reinterpret_cast<const uint8_t*>(valid.data_ptr()), S, F,
+                                 (int)nbin, alpha, lambda, mcw, ptr<double>(cand),
+                                 ptr<double>(split_out), s),
+                  "gbdt_split failed");
+    }
+    // the level's one synchronisation: split results + previous partition counts
+    const int64_t nl_n = nleft_dev.defined() ? nleft_dev.numel() : 0;
+    double* hdown = down.get<double>(6 * (last ? 0 : S) + nl_n / 2 + 2);
+    if (!last)
+      WH_HIP_CHECK_HOST(hipMemcpyAsync(hdown, split_out.data_ptr(), 48 * S, hipMemcpyDeviceToHost, s));
+    int32_t* nl_h = reinterpret_cast<int32_t*>(hdown + 6 * (last ? 0 : S));
+    if (nl_n)
+      WH_HIP_CHECK_HOST(hipMemcpyAsync(nl_h, nleft_dev.data_ptr(), 4 * nl_n, hipMemcpyDeviceToHost, s));
+    WH_HIP_CHECK_HOST(hipStreamSynchronize(s));
+    for (auto& pd : pending) {
+      const int m = pd[3] + nl_h[pd[0]];
+      seg[pd[1]] = {pd[3], m};
+      seg[pd[2]] = {m, pd[4]};
+    }
+    pending.clear();
+    for (int nd : frontier) {
+      cover[nd] = tot[nd][1];
+      bw[nd] = weight(tot[nd][0], tot[nd][1]);
+      leaf[nd] = eta * bw[nd];
+    }
+    if (last) break;
+    std::vector<int> split_k;
+    for (int k = 0; k < S; ++k) {
+      const double* o = hdown + 6 * k;
+      if (!(o[0] > rt_eps)) continue;
+      const int nd = frontier[k];
+      const int f = (int)o[1], b = (int)o[2];
+      feat[nd] = f, bin[nd] = b, defl[nd] = (int)o[3], gain[nd] = o[0];
+      const int l = add(nd), r = add(nd);
+      left[nd] = l, right[nd] = r;
+      tot[l] = {o[4], o[5]};
+      tot[r] = {tot[nd][0] - o[4], tot[nd][1] - o[5]};
+      split_k.push_back(k);
+    }
+    if (split_k.empty()) break;
+    const int nnode = (int)feat.size();
+    const int nsplit = (int)split_k.size();
+    // segment tiling of [0, n) for the position -> node map (gaps: -1)
+    std::vector<std::pair<int, int>> tiles;  // (begin, node)
+    {
+      std::vector<std::array<int, 3>> all;
+      for (auto& kv : seg) all.push_back({kv.second.first, kv.second.second, kv.first});
+      std::sort(all.begin(), all.end());
+      int cur = 0;
+      for (auto& a : all) {
+        if (a[0] > cur) tiles.push_back({cur, -1});
+        tiles.push_back({a[0], a[2]});
+        cur = a[1];
+      }
+      if (cur < n) tiles.push_back({cur, -1});
+    }
+    const int nt = (int)tiles.size();
+    // one pinned upload: node feat / bin / seg_beg / seg_end [nnode], defl
+    // (bytes) [nnode], tiles beg / node [nt], split table [nsplit x 4], parent slots
+    const int64_t nwords = 6LL * nnode + (nnode + 3) / 4 + 2LL * nt + 5LL * nsplit;
+    int32_t* hw = up.get<int32_t>(nwords);
+    std::memset(hw, 0, nwords * 4);
+    int32_t *h_feat = hw, *h_bin = hw + nnode, *h_sb = hw + 2 * nnode, *h_se = hw + 3 * nnode;
+    uint8_t* h_defl = reinterpret_cast<uint8_t*>(hw + 4 * nnode);
+    int32_t* h_tb = hw + 4 * nnode + (nnode + 3) / 4;
+    int32_t* h_tn = h_tb + nt;
+    int32_t* h_sp = h_tn + nt;
+    int32_t* h_par = h_sp + 4 * nsplit;
+    int32_t* h_lc = h_par + nsplit;      // partition cursors (device-updated)
+    int32_t* h_rc = h_lc + nnode;
+    for (int i = 0; i < nnode; ++i) h_feat[i] = -1;
+    std::vector<int64_t> small_len(nsplit);
+    for (int q = 0; q < nsplit; ++q) {
+      const int k = split_k[q], nd = frontier[k];
+      h_feat[nd] = feat[nd], h_bin[nd] = bin[nd], h_defl[nd] = (uint8_t)defl[nd];
+      const auto sg = seg[nd];
+      h_sb[nd] = sg.first, h_se[nd] = sg.second;
+      h_lc[nd] = sg.first, h_rc[nd] = sg.second;
+      // build the child with the smaller GLOBAL hessian, derive the other
+      const int l = left[nd], r = right[nd];
+      const int build_left = tot[l][1] <= tot[r][1] ? 1 : 0;
+      h_sp[4 * q] = nd, h_sp[4 * q + 1] = sg.first, h_sp[4 * q + 2] = sg.second,
+      h_sp[4 * q + 3] = build_left;
+      h_par[q] = k;
+      small_len[q] = sg.second - sg.first;  // upper bound of the built child's rows
+    }
+    for (int i = 0; i < nt; ++i) h_tb[i] = tiles[i].first, h_tn[i] = tiles[i].second;
+    auto dw32 = up.tensor().narrow(0, 0, nwords * 4).to(B.device(), true).view(torch::kInt32);
+    const int32_t* d = ptr<int32_t>(dw32);
+    const int32_t *d_feat = d, *d_bin = d + nnode, *d_sb = d + 2 * nnode;
+    const uint8_t* d_defl = reinterpret_cast<const uint8_t*>(d + 4 * nnode);
+    const int32_t* d_tb = d + 4 * nnode + (nnode + 3) / 4;
+    const int32_t* d_tn = d_tb + nt;
+    const int32_t* d_sp = d_tn + nt;
+    const int32_t* d_par = d_sp + 4 * nsplit;
+    int32_t* d_lc = const_cast<int32_t*>(d_par + nsplit);
+    int32_t* d_rc = d_lc + nnode;
+    auto ridx_new = torch::empty_like(ridx);
+    nleft_dev = torch::empty({nnode}, i32);
+    if (!wh::gbdt_partition_cursor(ptr<uint8_t>(B), ptr<uint8_t>(Bc), B.size(0), F,
+                                   ptr<int32_t>(ridx), n, d_tb, d_tn, nt, d_feat, d_bin, d_defl,
+                                   d_lc, d_rc, d_sb, nnode, ptr<int32_t>(nleft_dev),
+                                   ptr<int32_t>(ridx_new), s)) {
+      // position -> node map, flags, scan, per-node left counts, stable scatter
+      auto pos_node = torch::empty({n}, i32);
+      wh::gbdt_seg_fill(d_tb, d_tn, nt, n, ptr<int32_t>(pos_node), s);
+      auto sb64 = dw32.narrow(0, 2 * nnode, nnode).to(torch::kInt64);
+      auto se64 = dw32.narrow(0, 3 * nnode, nnode).to(torch::kInt64);
+      auto leftf = torch::empty({n}, i32);
+      wh::gbdt_goleft(ptr<uint8_t>(B), ptr<uint8_t>(Bc), B.size(0), F, ptr<int32_t>(ridx), n,
+                      ptr<int32_t>(pos_node), d_feat, d_bin, d_defl, ptr<int32_t>(leftf), s);
+      auto lscan = torch::empty({n + 1}, B.options().dtype(torch::kInt64));
+      auto stmp = torch::empty({wh::scan_tmp_elems(n)}, lscan.options());
+      wh::scan_i32(ptr<int32_t>(leftf), ptr<int64_t>(lscan), n, ptr<int64_t>(stmp), s);
+      nleft_dev = (lscan.index_select(0, se64) - lscan.index_select(0, sb64)).to(torch::kInt32);
+      wh::gbdt_scatter(ptr<int32_t>(ridx), n, ptr<int32_t>(pos_node), d_feat, d_sb,
+                       ptr<int32_t>(nleft_dev), ptr<int32_t>(leftf), ptr<int64_t>(lscan),
+                       ptr<int32_t>(ridx_new), s);
+    }
+    ridx = ridx_new;
+    // built children's rows, from the device counts
+    auto dseg = torch::empty({2 * nsplit}, i32);
+    wh::gbdt_child_segs(d_sp, nsplit, ptr<int32_t>(nleft_dev), ptr<int32_t>(dseg), s);
+    Tensor hs = build_hist(dseg, small_len);  // (synchronises the upload buffer)
+    auto H_next = torch::empty({2 * nsplit, F, nbin, 2}, f64);
+    wh::gbdt_sibling(ptr<double>(H_front), ptr<double>(hs), d_sp, d_par, nsplit, per,
+                     ptr<double>(H_next), s);
+    // next frontier [l, r] per split; unsplit frontier nodes are final leaves
+    std::vector<int> nf;
+    std::vector<bool> was_split(S, false);
+    for (int q = 0; q < nsplit; ++q) {
+      const int k = split_k[q], nd = frontier[k];
+      was_split[k] = true;
+      const auto sg = seg[nd];
+      pending.push_back({nd, left[nd], right[nd], sg.first, sg.second});
+      seg.erase(nd);
+      nf.push_back(left[nd]), nf.push_back(right[nd]);
+    }
+    for (int k = 0; k < S; ++k)
+      if (!was_split[k]) {
+        const int nd = frontier[k];
+        auto it = seg.find(nd);
+        if (it != seg.end()) {
+          done.push_back({nd, it->second.first, it->second.second});
+          seg.erase(it);
+        }
+      }
+    frontier = nf;
+    H_front = H_next;
+  }
+  if (!pending.empty()) {  // (a loop that ended right after a partition)
+    std::vector<int32_t> nl(nleft_dev.numel());
+    auto hn = nleft_dev.cpu();
+    for (auto& pd : pending) {
+      const int m = pd[3] + hn.data_ptr<int32_t>()[pd[0]];
+      seg[pd[1]] = {pd[3], m};
+      seg[pd[2]] = {m, pd[4]};
+    }
+  }
+  for (auto& kv : seg) done.push_back({kv.first, kv.second.first, kv.second.second});
+  std::vector<float> cond(feat.size(), 0.f);
+  for (size_t i = 0; i < feat.size(); ++i)
+    if (feat[i] >= 0) cond[i] = cut_vals[cut_off[feat[i]] + bin[i]];
+  py::list segs;
+  for (auto& dn : done) segs.append(py::make_tuple(dn[0], dn[1], dn[2]));
+  return py::make_tuple(feat, bin, cond, defl, left, right, parent, gain, cover, bw, leaf, segs,
+                        ridx);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_hip, m) {
@@ -1537,6 +1844,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_assign", &kmeans_assign);
   m.def("kmeans_accum", &kmeans_accum);
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
+  m.def("gbdt_grow", &gbdt_grow);
   m.def("kmeans_pack_c3", &kmeans_pack_c3);
   m.def("kmeans_assign_x3", &kmeans_assign_x3);
   m.def("spmv_t", &spmv_t, py::arg("csc_off"), py::arg("csc_row"), py::arg("csc_val"),

@@ -97,9 +97,17 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(const uint8_t* __restrict
                                                        const float* __restrict__ qscale,
                                                        const HistTask* __restrict__ tasks,
                                                        long long* __restrict__ part,
-                                                       int64_t pstride) {
+                                                       int64_t pstride,
+                                                       const int32_t* __restrict__ dseg) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
-  const HistTask tk = tasks[blockIdx.x];
+  HistTask tk = tasks[blockIdx.x];
+  if (dseg) {  // dynamic rows: {chunk index, chunk rows} of the slot's device segment
+    const int32_t sb = dseg[2 * tk.node], se = dseg[2 * tk.node + 1];
+    const int32_t rb = sb + tk.rbeg * tk.rend;
+    if (rb >= se) return;  // past the segment: the reduce skips this task
+    tk.rend = rb + tk.rend < se ? rb + tk.rend : se;
+    tk.rbeg = rb;
+  }
   const float sg = qscale[0], sh = qscale[1];
   const int nl2 = 2 * tk.fcnt * nbin;
   for (int i = threadIdx.x; i < nl2; i += blockDim.x) lds64[i] = 0ull;
@@ -158,9 +166,15 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(const uint8_t* __restrict
 constexpr int kRedE = 64, kRedK = 16;
 __global__ __launch_bounds__(kRedE * kRedK) void k_hist_reduce(
     const long long* __restrict__ part, int64_t pstride, const HistReduce* __restrict__ red, int f,
-    int nbin, const float* __restrict__ qscale, double* __restrict__ hist) {
+    int nbin, const float* __restrict__ qscale, double* __restrict__ hist,
+    const int32_t* __restrict__ dseg, int chunk) {
   __shared__ unsigned long long acc_s[kRedK][kRedE];
-  const HistReduce rd = red[blockIdx.y];
+  HistReduce rd = red[blockIdx.y];
+  if (dseg) {  // only the chunks that cover the slot's device segment wrote
+    const int64_t len = (int64_t)dseg[2 * rd.node + 1] - dseg[2 * rd.node];
+    const int64_t live = len > 0 ? (len + chunk - 1) / chunk : 0;
+    rd.nt = live < rd.nt ? (int32_t)live : rd.nt;
+  }
   const int ei = threadIdx.x % kRedE, kj = threadIdx.x / kRedE;
   const int e = blockIdx.x * kRedE + ei;
   const int nl2 = 2 * rd.fcnt * nbin;
@@ -336,7 +350,8 @@ int64_t gbdt_hist_pstride(int max_fcnt, int nbin) { return ((int64_t)2 * max_fcn
 
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
                const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
-               int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s) {
+               int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s,
+               const int32_t* dseg, int chunk) {
   if (ntask <= 0) return;
   static bool attr = false;
   if (!attr) {  // dynamic LDS above 64 KB must be opted into per kernel
@@ -353,14 +368,165 @@ void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const flo
   auto* pt = reinterpret_cast<long long*>(part);
   if (dword_rows)
     hipLaunchKernelGGL(k_hist<true>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx, gp,
-                       qscale, tk, pt, ps);
+                       qscale, tk, pt, ps, dseg);
   else
     hipLaunchKernelGGL(k_hist<false>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx,
-                       gp, qscale, tk, pt, ps);
+                       gp, qscale, tk, pt, ps, dseg);
   if (nred > 0)
     hipLaunchKernelGGL(k_hist_reduce, dim3((unsigned)((2 * max_fcnt * nbin + kRedE - 1) / kRedE), nred),
                        dim3(kRedE * kRedK), 0, s, pt, ps, reinterpret_cast<const HistReduce*>(red), f, nbin,
-                       qscale, hist);
+                       qscale, hist, dseg, chunk);
+}
+
+// Level bookkeeping on the device (the host tree grower, csrc/bind/gbdt_grow.cc):
+// sp[k] = {parent node, parent begin, parent end, build_left} of split k ->
+// dseg[k] = rows of the child whose histogram is built (nleft from the
+// partition, never read by the host before the next level).
+__global__ void k_child_segs(const int32_t* __restrict__ sp, int nsplit,
+                             const int32_t* __restrict__ nleft, int32_t* __restrict__ dseg) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nsplit) return;
+  const int nd = sp[4 * k], b = sp[4 * k + 1], e = sp[4 * k + 2], bl = sp[4 * k + 3];
+  const int m = b + nleft[nd];
+  dseg[2 * k] = bl ? b : m;
+  dseg[2 * k + 1] = bl ? m : e;
+}
+
+// next frontier histograms: for split k (parent slot par[k]) with built child
+// histogram hs[k], out[2k] = left child, out[2k+1] = right child, the other
+// one being parent - built
+__global__ void k_sibling(const double* __restrict__ hf, const double* __restrict__ hs,
+                          const int32_t* __restrict__ sp, const int32_t* __restrict__ par,
+                          int nsplit, int64_t per, double* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)nsplit * per) return;
+  const int k = (int)(t / per);
+  const int64_t e = t - (int64_t)k * per;
+  const double built = hs[t];
+  const double other = hf[(int64_t)par[k] * per + e] - built;
+  const bool bl = sp[4 * k + 3] != 0;
+  out[(int64_t)(2 * k) * per + e] = bl ? built : other;
+  out[(int64_t)(2 * k + 1) * per + e] = bl ? other : built;
+}
+
+// One-pass partition of the split nodes' rows (the grower's default): a block
+// takes 4096 positions, finds each one's segment by a binary search over the
+// segment table in LDS, counts its left / right rows per segment in LDS, then
+// reserves room with ONE global atomic per (block, segment, side) on the
+// node's cursors (left rows fill the segment from its start, right rows from
+// its end down) and scatters. Replaces position->node fill + flags + a
+// 3-kernel scan + scatter (5 passes over n per level). Row order inside a
+// child is not preserved -- the histograms are exact fixed-point sums, so
+// every tree is unchanged.
+constexpr int kPcThreads = 256, kPcPer = 16, kPcTile = kPcThreads * kPcPer;
+constexpr int kPcMaxTiles = 2048, kPcMaxLocal = 512;
+
+__global__ __launch_bounds__(kPcThreads) void k_part_cursor(
+    const uint8_t* __restrict__ B, const uint8_t* __restrict__ Bc, int64_t nrows, int f,
+    const int32_t* __restrict__ ridx, int64_t n, const int32_t* __restrict__ tb,
+    const int32_t* __restrict__ tn, int nt, const int32_t* __restrict__ node_feat,
+    const int32_t* __restrict__ node_bin, const uint8_t* __restrict__ node_defl,
+    int32_t* __restrict__ lcur, int32_t* __restrict__ rcur, int32_t* __restrict__ out) {
+  __shared__ int32_t s_tb[kPcMaxTiles];
+  __shared__ uint32_t cnt[2][kPcMaxLocal];
+  __shared__ int32_t base[2][kPcMaxLocal];
+  for (int i = threadIdx.x; i < nt; i += kPcThreads) s_tb[i] = tb[i];
+  for (int i = threadIdx.x; i < kPcMaxLocal; i += kPcThreads) cnt[0][i] = cnt[1][i] = 0;
+  __syncthreads();
+  const int64_t p0 = (int64_t)blockIdx.x * kPcTile;
+  auto seg_of = [&](int64_t i) {  // last segment with begin <= i
+    int lo = 0, hi = nt - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_tb[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
+  const int sg0 = seg_of(p0);
+  int ls[kPcPer], side[kPcPer];
+  uint32_t rk[kPcPer];
+  int32_t rw[kPcPer];
+#pragma unroll
+  for (int u = 0; u < kPcPer; ++u) {
+    const int64_t i = p0 + u * kPcThreads + threadIdx.x;
+    ls[u] = -1;
+    side[u] = 0;
+    rk[u] = 0;
+    rw[u] = i < n ? ridx[i] : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < kPcPer; ++u) {
+    const int64_t i = p0 + u * kPcThreads + threadIdx.x;
+    if (i >= n) continue;
+    const int sg = seg_of(i);
+    const int nd = tn[sg];
+    const int feat = nd >= 0 ? node_feat[nd] : -1;
+    if (feat < 0) {
+      out[i] = rw[u];  // finished leaf / unsplit node: the row stays put
+      continue;
+    }
+    const int b = Bc ? Bc[(int64_t)feat * nrows + rw[u]] : B[(int64_t)rw[u] * f + feat];
+    const int l = (b == kMissing) ? (int)node_defl[nd] : (b <= node_bin[nd] ? 1 : 0);
+    side[u] = l ? 0 : 1;
+    ls[u] = sg - sg0;
+    if (ls[u] < kPcMaxLocal) {
+      rk[u] = atomicAdd(&cnt[side[u]][ls[u]], 1u);
+    } else {  // (a tile crossing > kPcMaxLocal segments: a global cursor each)
+      rk[u] = 0;
+      out[l ? atomicAdd(&lcur[nd], 1) : atomicSub(&rcur[nd], 1) - 1] = rw[u];
+      ls[u] = -1;
+    }
+  }
+  __syncthreads();
+  const int nloc = min(seg_of(min(p0 + kPcTile, n) - 1) - sg0 + 1, kPcMaxLocal);
+  for (int q = threadIdx.x; q < 2 * nloc; q += kPcThreads) {
+    const int sd = q / nloc, l = q - sd * nloc;
+    const uint32_t c = cnt[sd][l];
+    if (c == 0) continue;
+    const int nd = tn[sg0 + l];
+    base[sd][l] = sd == 0 ? atomicAdd(&lcur[nd], (int)c) : atomicSub(&rcur[nd], (int)c) - (int)c;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kPcPer; ++u)
+    if (ls[u] >= 0) out[base[side[u]][ls[u]] + (int)rk[u]] = rw[u];
+}
+
+__global__ void k_nleft(const int32_t* __restrict__ lcur, const int32_t* __restrict__ sb, int nnode,
+                        int32_t* __restrict__ nleft) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nnode) nleft[i] = lcur[i] - sb[i];
+}
+
+bool gbdt_partition_cursor(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f,
+                           const int32_t* ridx, int64_t n, const int32_t* tb, const int32_t* tn,
+                           int nt, const int32_t* node_feat, const int32_t* node_bin,
+                           const uint8_t* node_defl, int32_t* lcur, int32_t* rcur,
+                           const int32_t* seg_beg, int nnode, int32_t* nleft, int32_t* out,
+                           hipStream_t s) {
+  if (nt > kPcMaxTiles || n <= 0) return false;
+  hipLaunchKernelGGL(k_part_cursor, dim3((unsigned)((n + kPcTile - 1) / kPcTile)),
+                     dim3(kPcThreads), 0, s, B, Bc, nrows, f, ridx, n, tb, tn, nt, node_feat,
+                     node_bin, node_defl, lcur, rcur, out);
+  hipLaunchKernelGGL(k_nleft, dim3((nnode + 255) / 256), dim3(256), 0, s, lcur, seg_beg, nnode,
+                     nleft);
+  return true;
+}
+
+void gbdt_child_segs(const int32_t* sp, int nsplit, const int32_t* nleft, int32_t* dseg,
+                     hipStream_t s) {
+  if (nsplit <= 0) return;
+  hipLaunchKernelGGL(k_child_segs, dim3((nsplit + 255) / 256), dim3(256), 0, s, sp, nsplit, nleft,
+                     dseg);
+}
+
+void gbdt_sibling(const double* hf, const double* hs, const int32_t* sp, const int32_t* par,
+                  int nsplit, int64_t per, double* out, hipStream_t s) {
+  const int64_t n = (int64_t)nsplit * per;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_sibling, dim3(grid_for(n, 256)), dim3(256), 0, s, hf, hs, sp, par, nsplit,
+                     per, out);
 }
 
 void gbdt_seg_fill(const int32_t* beg, const int32_t* node, int nseg, int64_t n, int32_t* out,

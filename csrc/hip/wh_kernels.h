@@ -378,7 +378,24 @@ size_t gbdt_hist_lds(int fcnt, int nbin);
 int64_t gbdt_hist_pstride(int max_fcnt, int nbin);
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
                const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
-               int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s);
+               int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s,
+               const int32_t* dseg = nullptr, int chunk = 0);
+// dseg (optional) [slots x 2] device row segments: a task's {rbeg, rend} is
+// then {chunk index, chunk rows} inside its slot's segment (empty past it)
+// level bookkeeping of the device-resident tree grower (see gbdt.hip)
+void gbdt_child_segs(const int32_t* sp, int nsplit, const int32_t* nleft, int32_t* dseg,
+                     hipStream_t s);
+// one-pass (order-free) partition by per-node cursors: lcur = seg_beg, rcur =
+// seg_end of the split nodes on entry; nleft [nnode] out. false: too many
+// segments for the LDS table (use goleft + scan + scatter)
+bool gbdt_partition_cursor(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f,
+                           const int32_t* ridx, int64_t n, const int32_t* tb, const int32_t* tn,
+                           int nt, const int32_t* node_feat, const int32_t* node_bin,
+                           const uint8_t* node_defl, int32_t* lcur, int32_t* rcur,
+                           const int32_t* seg_beg, int nnode, int32_t* nleft, int32_t* out,
+                           hipStream_t s);
+void gbdt_sibling(const double* hf, const double* hs, const int32_t* sp, const int32_t* par,
+                  int nsplit, int64_t per, double* out, hipStream_t s);
 // position -> node id over sorted segments tiling [0, n)
 void gbdt_seg_fill(const int32_t* beg, const int32_t* node, int nseg, int64_t n, int32_t* out,
                    hipStream_t s);

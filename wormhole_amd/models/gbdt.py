@@ -547,6 +547,43 @@ class TreeBuilder:
 
     # ----------------------------------------------------------------- build
     def build(self, gpair, margin):
+        if self.gpu and self.dm.n > 0:
+            return self._build_native(gpair, margin)
+        return self._build_py(gpair, margin)
+
+    def _build_native(self, gpair, margin):
+        """The level loop in C++ (``_hip.gbdt_grow``): one host sync per
+        level, device-derived child segments, fused sibling subtraction.
+        Same tree as :meth:`_build_py` (which stays the CPU path and the
+        reference)."""
+        p = self.p
+        n = self.dm.n
+        tot = gpair.double().sum(0)
+        self.bsp.allreduce(tot)
+        self._qscale = self._hist_scale(gpair)
+        if self._Bc is None:
+            self._Bc = self.B.t().contiguous()
+        if self._valid_dev is None or self._valid_dev[0] is not self.valid_mask:
+            self._valid_dev = (self.valid_mask, self.valid_mask.to(self.device).contiguous())
+        if not hasattr(self, "_cut_lists"):
+            self._cut_lists = (self.cuts.values.tolist(), self.cuts.offsets.tolist())
+        ar = (lambda t: self.bsp.allreduce(t)) if self.bsp.world > 1 else None
+        out = _native.hip().gbdt_grow(
+            self.B, self._Bc, torch.arange(n, dtype=torch.int32, device=self.device), gpair,
+            self._qscale, self._valid_dev[1], self.nbin, self.fgroups, self.max_fcnt,
+            tot.cpu().tolist(), self._cut_lists[0], self._cut_lists[1], float(p.eta),
+            float(p.alpha), float(p.reg_lambda), float(p.min_child_weight), int(p.max_depth),
+            RT_EPS, ar)
+        (feat, bin_, cond, defl, left, right, parent, gain, cover, bw, leaf, segs, ridx) = out
+        tree = RegTree()
+        tree.feat, tree.bin, tree.cond, tree.defl = list(feat), list(bin_), list(cond), list(defl)
+        tree.left, tree.right, tree.parent = list(left), list(right), list(parent)
+        tree.gain, tree.cover, tree.base_weight = list(gain), list(cover), list(bw)
+        tree.leaf = list(leaf)
+        self._finish(tree, ridx, margin, n, {nd: (b, e) for nd, b, e in segs})
+        return tree
+
+    def _build_py(self, gpair, margin):
         p = self.p
         n = self.dm.n
         dev = self.device
@@ -645,10 +682,9 @@ class TreeBuilder:
             hr = torch.where(small_is_left[:, None, None, None], hbig, hsmall)
             H_front = torch.stack([hl, hr], 1).reshape(-1, *H_front.shape[1:])
             frontier = new_frontier
-        self._prune(tree)
         # margins of the training rows from the final leaf segments
         done.update(seg)
-        self._apply_leaves(tree, ridx, margin, n, done)
+        self._finish(tree, ridx, margin, n, done)
         return tree
 
     def _pos_node(self, seg, n):
@@ -706,6 +742,11 @@ class TreeBuilder:
 
     def _prune(self, tree):
         """xgboost prune updater: collapse splits whose loss_chg < gamma."""
+        self._prune_mark(tree)
+        self._compact(tree)
+
+    def _prune_mark(self, tree):
+        """The collapse itself, node ids unchanged (see :meth:`_compact`)."""
         changed = True
         while changed:
             changed = False
@@ -717,7 +758,27 @@ class TreeBuilder:
                     tree.feat[i] = -1
                     tree.leaf[i] = self.p.eta * tree.base_weight[i]
                     changed = True
+
+    def _finish(self, tree, ridx, margin, n, leaf_segs):
+        """Prune, then add the leaf values to the training margins from the
+        final (pre-prune) leaf segments, then renumber: a pruned-away
+        subtree's rows take the value of its nearest ancestor that is a leaf
+        after pruning, looked up BEFORE the BFS renumbering changes ids."""
+        self._prune_mark(tree)
+        if n and self.gpu:
+            val = torch.zeros(len(tree.feat), dtype=torch.float32)
+            for nd in leaf_segs:
+                a, top = nd, nd
+                while tree.parent[a] >= 0:
+                    a = tree.parent[a]
+                    if tree.is_leaf(a):
+                        top = a
+                val[nd] = tree.leaf[top]
+            pos = self._pos_node(leaf_segs, n)
+            _native.hip().gbdt_leaf_add(ridx, pos, val.to(self.device), margin)
         self._compact(tree)
+        if n and not self.gpu:
+            tree.predict_margin(self.dm.X, margin)
 
     @staticmethod
     def _compact(tree):
@@ -743,29 +804,6 @@ class TreeBuilder:
                 t.left[i], t.right[i] = remap[tree.left[old]], remap[tree.right[old]]
         tree.__dict__.update(t.__dict__)
         tree._remap = remap
-
-    def _apply_leaves(self, tree, ridx, margin, n, leaf_segs):
-        """margin[row] += leaf value, for the rows of every leaf segment.
-
-        Rows sit in the ridx segments of the (pre-prune) leaves; a pruned-away
-        subtree's rows take the value of its nearest ancestor that is a leaf
-        after pruning.  Same result as walking the tree on the raw values
-        (bin <= b <=> value < cut[b]; missing follows the default direction)."""
-        if n == 0:
-            return
-        if not self.gpu:
-            tree.predict_margin(self.dm.X, margin)
-            return
-        val = torch.zeros(len(tree.feat), dtype=torch.float32)
-        for nd in leaf_segs:
-            a, top = nd, nd
-            while tree.parent[a] >= 0:
-                a = tree.parent[a]
-                if tree.is_leaf(a):
-                    top = a
-            val[nd] = tree.leaf[top]
-        pos = self._pos_node(leaf_segs, n)
-        _native.hip().gbdt_leaf_add(ridx, pos, val.to(self.device), margin)
 
 
 # ---------------------------------------------------------------- booster
