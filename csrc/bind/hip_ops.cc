@@ -1491,6 +1491,100 @@ Tensor spmv_t(const Tensor& csc_off, const Tensor& csc_row, const c10::optional<
 }
 
 
+// ------------------------------------------------------------- gbdt (CSR)
+Tensor gbdt_bin_csr(const Tensor& fid, const c10::optional<Tensor>& val, int64_t ncol,
+                    const Tensor& cuts, const Tensor& cut_off) {
+  CHECK_IN(fid, torch::kInt32);
+  CHECK_IN(cuts, torch::kFloat32);
+  CHECK_IN(cut_off, torch::kInt32);
+  TORCH_CHECK(cut_off.numel() == ncol + 1, "cut_off must be [ncol + 1]");
+  c10::DeviceGuard g(fid.device());
+  auto gbin = torch::empty_like(fid);
+  wh::gbdt_bin_csr(ptr<int32_t>(fid), optptr<float>(val), fid.numel(), (int)ncol, ptr<float>(cuts),
+                   ptr<int32_t>(cut_off), ptr<int32_t>(gbin), cur_stream(fid));
+  return gbin;
+}
+
+// tasks [T, 3] {slot, rbeg, rend} (device int32) -> hist double [nslot, tb, 2]
+Tensor gbdt_hist_csr(const Tensor& row_off, const Tensor& gbin, const Tensor& ridx,
+                     const Tensor& gpair, const Tensor& qscale, const Tensor& tasks,
+                     int64_t max_rows, int64_t tb, int64_t nslot) {
+  CHECK_IN(row_off, torch::kInt64);
+  CHECK_IN(gbin, torch::kInt32);
+  CHECK_IN(ridx, torch::kInt32);
+  CHECK_IN(gpair, torch::kFloat32);
+  CHECK_IN(qscale, torch::kFloat32);
+  CHECK_IN(tasks, torch::kInt32);
+  c10::DeviceGuard g(gbin.device());
+  auto hist = torch::empty({nslot, tb, 2}, gpair.options().dtype(torch::kFloat64));
+  auto hq = torch::empty({std::max<int64_t>(nslot * tb * 2, 1)}, gpair.options().dtype(torch::kInt64));
+  wh::gbdt_hist_csr(ptr<int64_t>(row_off), ptr<int32_t>(gbin), ptr<int32_t>(ridx),
+                    ptr<float>(gpair), ptr<float>(qscale), ptr<int32_t>(tasks),
+                    (int)(tasks.numel() / 3), (int)max_rows, tb, (int)nslot, ptr<int64_t>(hq),
+                    ptr<double>(hist), cur_stream(gbin));
+  return hist;
+}
+
+Tensor gbdt_split_csr(const Tensor& hist, const Tensor& totals, const Tensor& cut_off,
+                      const c10::optional<Tensor>& fvalid, double alpha, double lambda, double mcw) {
+  CHECK_IN(hist, torch::kFloat64);
+  CHECK_IN(totals, torch::kFloat64);
+  CHECK_IN(cut_off, torch::kInt32);
+  c10::DeviceGuard g(hist.device());
+  const int S = (int)hist.size(0);
+  const int F = (int)cut_off.numel() - 1;
+  auto out = torch::empty({S, 6}, hist.options());
+  auto cand = torch::empty({std::max<int64_t>((int64_t)S * F * 5, 1)}, hist.options());
+  wh::gbdt_split_csr(ptr<double>(hist), hist.size(1), ptr<double>(totals), ptr<int32_t>(cut_off),
+                     optptr<uint8_t>(fvalid), S, F, alpha, lambda, mcw, ptr<double>(cand),
+                     ptr<double>(out), cur_stream(hist));
+  return out;
+}
+
+Tensor gbdt_partition_csr(const Tensor& row_off, const Tensor& fid, const Tensor& gbin,
+                          const Tensor& cut_off, const Tensor& ridx, const Tensor& pos_node,
+                          const Tensor& node_feat, const Tensor& node_bin, const Tensor& node_defl,
+                          const Tensor& seg_beg, const Tensor& seg_end, Tensor nleft_out) {
+  CHECK_IN(row_off, torch::kInt64);
+  CHECK_IN(fid, torch::kInt32);
+  CHECK_IN(gbin, torch::kInt32);
+  CHECK_IN(ridx, torch::kInt32);
+  CHECK_IN(pos_node, torch::kInt32);
+  c10::DeviceGuard g(ridx.device());
+  auto s = cur_stream(ridx);
+  const int64_t n = ridx.numel();
+  auto left = torch::empty({n}, ridx.options());
+  wh::gbdt_goleft_csr(ptr<int64_t>(row_off), ptr<int32_t>(fid), ptr<int32_t>(gbin),
+                      ptr<int32_t>(cut_off), ptr<int32_t>(ridx), n, ptr<int32_t>(pos_node),
+                      ptr<int32_t>(node_feat), ptr<int32_t>(node_bin), ptr<uint8_t>(node_defl),
+                      ptr<int32_t>(left), s);
+  auto lscan = torch::empty({n + 1}, ridx.options().dtype(torch::kInt64));
+  auto tmp = torch::empty({wh::scan_tmp_elems(n)}, lscan.options());
+  wh::scan_i32(ptr<int32_t>(left), ptr<int64_t>(lscan), n, ptr<int64_t>(tmp), s);
+  auto nl = (lscan.index_select(0, seg_end.to(torch::kInt64)) -
+             lscan.index_select(0, seg_beg.to(torch::kInt64))).to(torch::kInt32);
+  nleft_out.copy_(nl);
+  auto out = torch::empty_like(ridx);
+  wh::gbdt_scatter(ptr<int32_t>(ridx), n, ptr<int32_t>(pos_node), ptr<int32_t>(node_feat),
+                   ptr<int32_t>(seg_beg), ptr<int32_t>(nleft_out), ptr<int32_t>(left),
+                   ptr<int64_t>(lscan), ptr<int32_t>(out), s);
+  return out;
+}
+
+void gbdt_predict_csr(const Tensor& row_off, const Tensor& fid, const c10::optional<Tensor>& val,
+                      const Tensor& feat, const Tensor& thr, const Tensor& left,
+                      const Tensor& right, const Tensor& defl, const Tensor& leaf,
+                      const Tensor& margin) {
+  CHECK_IN(row_off, torch::kInt64);
+  CHECK_IN(fid, torch::kInt32);
+  CHECK_IN(margin, torch::kFloat32);
+  c10::DeviceGuard g(fid.device());
+  wh::gbdt_predict_csr(ptr<int64_t>(row_off), ptr<int32_t>(fid), optptr<float>(val),
+                       row_off.numel() - 1, ptr<int32_t>(feat), ptr<float>(thr),
+                       ptr<int32_t>(left), ptr<int32_t>(right), ptr<uint8_t>(defl),
+                       ptr<float>(leaf), ptr<float>(margin), cur_stream(fid));
+}
+
 // ------------------------------------------------------------ gbdt grower
 // Depth-wise histogram tree growth with the level loop in C++ (reference:
 // xgboost hist updater driven by bin/xgboost.dmlc). Per level
@@ -1845,6 +1939,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_accum", &kmeans_accum);
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
   m.def("gbdt_grow", &gbdt_grow);
+  m.def("gbdt_bin_csr", &gbdt_bin_csr);
+  m.def("gbdt_hist_csr", &gbdt_hist_csr);
+  m.def("gbdt_split_csr", &gbdt_split_csr);
+  m.def("gbdt_partition_csr", &gbdt_partition_csr);
+  m.def("gbdt_predict_csr", &gbdt_predict_csr);
   m.def("kmeans_pack_c3", &kmeans_pack_c3);
   m.def("kmeans_assign_x3", &kmeans_assign_x3);
   m.def("spmv_t", &spmv_t, py::arg("csc_off"), py::arg("csc_row"), py::arg("csc_val"),

@@ -36,7 +36,7 @@ __global__ void k_bin(const float* __restrict__ X, int64_t n, int f, const float
     int bin = lo - base;
     const int nb = cut_off[j + 1] - base;
     if (bin >= nb) bin = nb - 1;
-    b = (uint8_t)bin;
+    b = nb > 0 ? (uint8_t)bin : (uint8_t)kMissing;  // (a feature without cuts)
   }
   B[t] = b;
 }
@@ -777,6 +777,261 @@ bool gbdt_split(const double* hist, const double* totals, const uint8_t* valid, 
                      totals, valid, F, nbin, p, cand);
   hipLaunchKernelGGL(k_split_node, dim3((unsigned)S), dim3(64), 0, s, cand, F, nbin, out);
   return true;
+}
+
+}  // namespace wh
+
+// ---- sparse (CSR) input -------------------------------------------------
+// A libsvm-style matrix stays CSR: each stored value gets a GLOBAL bin id
+// cut_off[feature] + bin (features own cut_off[f+1] - cut_off[f] bins, 0 for
+// a feature that never occurs), histograms are [slots][total bins][2] in that
+// compact layout (no F x max_bin padding, no dense n x F matrix), and a row
+// missing a feature takes the split's default direction (the split search
+// derives the missing mass as node total - the feature's stored mass, as in
+// the dense path). Row feature ids are ascending within a row.
+namespace wh {
+namespace {
+
+__global__ void k_bin_csr(const int32_t* __restrict__ fid, const float* __restrict__ val,
+                          int64_t nnz, int ncol, const float* __restrict__ cuts,
+                          const int32_t* __restrict__ cut_off, int32_t* __restrict__ gbin) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nnz) return;
+  const int f = fid[i];
+  if (f < 0 || f >= ncol) {
+    gbin[i] = -1;
+    return;
+  }
+  const int lo0 = cut_off[f], hi0 = cut_off[f + 1];
+  if (hi0 <= lo0) {
+    gbin[i] = -1;
+    return;
+  }
+  const float v = val ? val[i] : 1.f;
+  int lo = lo0, hi = hi0 - 1;  // first cut > v (upper_bound), capped at the last bin
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cuts[mid] > v) hi = mid;
+    else lo = mid + 1;
+  }
+  gbin[i] = lo;
+}
+
+// one thread per row of the task: adds its stored values' (g, h) into the
+// slot's compact histogram (fixed-point int64 global atomics: exact and
+// order-free; total bins can be far beyond an LDS tile)
+__global__ void k_hist_csr(const int64_t* __restrict__ row_off, const int32_t* __restrict__ gbin,
+                           const int32_t* __restrict__ ridx, const float2* __restrict__ gpair,
+                           const float* __restrict__ qscale, const int32_t* __restrict__ tasks,
+                           int64_t tb, unsigned long long* __restrict__ hist) {
+  const int32_t* tk = tasks + 3 * blockIdx.y;  // {slot, rbeg, rend}
+  const int r = tk[1] + blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= tk[2]) return;
+  const int row = ridx[r];
+  const float2 gh = gpair[row];
+  const long long qg = __float2ll_rn(gh.x * qscale[0]), qh = __float2ll_rn(gh.y * qscale[1]);
+  unsigned long long* h = hist + (int64_t)tk[0] * tb * 2;
+  for (int64_t j = row_off[row]; j < row_off[row + 1]; ++j) {
+    const int b = gbin[j];
+    if (b < 0) continue;
+    atomicAdd(h + 2 * (int64_t)b, (unsigned long long)qg);
+    atomicAdd(h + 2 * (int64_t)b + 1, (unsigned long long)qh);
+  }
+}
+
+__global__ void k_hist_csr_fin(const unsigned long long* __restrict__ q, int64_t n,
+                               const float* __restrict__ qscale, double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (double)(long long)q[i] / (double)qscale[i & 1];
+}
+
+// best split per (node, feature): one thread walks the feature's bins; then
+// per node the best feature (ties: smallest (feature, bin, dir) as dense).
+// cand [S][F] = {gain, bin, dir, GL, HL}
+__global__ void k_split_csr_feat(const double* __restrict__ hist, int64_t tb,
+                                 const double* __restrict__ totals,
+                                 const int32_t* __restrict__ cut_off,
+                                 const uint8_t* __restrict__ fvalid, int F, SplitParam p,
+                                 double* __restrict__ cand) {
+  const int s = blockIdx.y;
+  const int f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  double* c = cand + ((int64_t)s * F + f) * 5;
+  c[0] = -INFINITY;
+  const int b0 = cut_off[f], b1 = cut_off[f + 1];
+  if (b1 <= b0 || (fvalid && !fvalid[f])) return;
+  const double* hb = hist + (int64_t)s * tb * 2;
+  const double TG = totals[2 * s], TH = totals[2 * s + 1];
+  double pg = 0.0, ph = 0.0;
+  for (int b = b0; b < b1; ++b) pg += hb[2 * b], ph += hb[2 * b + 1];
+  const double mg = TG - pg, mh = TH - ph, parent = split_gain(TG, TH, p);
+  double best = -INFINITY, gl = 0.0, hl = 0.0, sg = 0.0, sh = 0.0;
+  int bb = 0, bd = 0;
+  for (int b = b0; b < b1; ++b) {
+    sg += hb[2 * b];
+    sh += hb[2 * b + 1];
+    for (int d = 0; d < 2; ++d) {
+      const double GL = sg + (d ? mg : 0.0), HL = sh + (d ? mh : 0.0);
+      const double GR = TG - GL, HR = TH - HL;
+      if (!(HL >= p.mcw && HR >= p.mcw)) continue;
+      const double g = split_gain(GL, HL, p) + split_gain(GR, HR, p) - parent;
+      if (g > best) {
+        best = g, bb = b - b0, bd = d, gl = GL, hl = HL;
+      }
+    }
+  }
+  c[0] = best, c[1] = bb, c[2] = bd, c[3] = gl, c[4] = hl;
+}
+
+__global__ __launch_bounds__(256) void k_split_csr_node(const double* __restrict__ cand, int F,
+                                                        double* __restrict__ out) {
+  const int s = blockIdx.x;
+  double best = -INFINITY;
+  long long bi = 0x7fffffffffffffffll;
+  for (int f = threadIdx.x; f < F; f += 256) {
+    const double* c = cand + ((int64_t)s * F + f) * 5;
+    const long long idx = (long long)f * 2048 + (long long)c[1] * 2 + (long long)c[2];
+    if (better(c[0], idx, best, bi)) best = c[0], bi = idx;
+  }
+  __shared__ double sb[256];
+  __shared__ long long si[256];
+  sb[threadIdx.x] = best;
+  si[threadIdx.x] = bi;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o && better(sb[threadIdx.x + o], si[threadIdx.x + o], sb[threadIdx.x],
+                                  si[threadIdx.x])) {
+      sb[threadIdx.x] = sb[threadIdx.x + o];
+      si[threadIdx.x] = si[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double* o = out + 6 * s;
+    if (!(sb[0] > -INFINITY)) {
+      o[0] = -INFINITY, o[1] = o[2] = o[3] = o[4] = o[5] = 0.0;
+      return;
+    }
+    const int f = (int)(si[0] / 2048);
+    const double* c = cand + ((int64_t)s * F + f) * 5;
+    o[0] = c[0], o[1] = f, o[2] = c[1], o[3] = c[2], o[4] = c[3], o[5] = c[4];
+  }
+}
+
+// go-left flag of every position: the row's stored value of the node's
+// feature (binary search in the row's ascending ids), else the default
+__global__ void k_goleft_csr(const int64_t* __restrict__ row_off, const int32_t* __restrict__ fid,
+                             const int32_t* __restrict__ gbin, const int32_t* __restrict__ cut_off,
+                             const int32_t* __restrict__ ridx, int64_t n,
+                             const int32_t* __restrict__ pos_node,
+                             const int32_t* __restrict__ node_feat,
+                             const int32_t* __restrict__ node_bin,
+                             const uint8_t* __restrict__ node_defl, int32_t* __restrict__ left) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int nd = pos_node[i];
+  const int f = nd >= 0 ? node_feat[nd] : -1;
+  int l = 0;
+  if (f >= 0) {
+    const int row = ridx[i];
+    int64_t lo = row_off[row], hi = row_off[row + 1];
+    int b = -1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      const int v = fid[mid];
+      if (v == f) {
+        b = gbin[mid];
+        break;
+      }
+      if (v < f) lo = mid + 1;
+      else hi = mid;
+    }
+    l = b < 0 ? (int)node_defl[nd] : (b - cut_off[f] <= node_bin[nd] ? 1 : 0);
+  }
+  left[i] = l;
+}
+
+// tree walk on CSR rows (raw values; missing -> default direction)
+__global__ void k_predict_csr(const int64_t* __restrict__ row_off, const int32_t* __restrict__ fid,
+                              const float* __restrict__ val, int64_t n,
+                              const int32_t* __restrict__ feat, const float* __restrict__ thr,
+                              const int32_t* __restrict__ left, const int32_t* __restrict__ right,
+                              const uint8_t* __restrict__ defl, const float* __restrict__ leaf,
+                              float* __restrict__ margin) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  int nd = 0;
+  for (int depth = 0; depth < 64 && feat[nd] >= 0; ++depth) {
+    const int f = feat[nd];
+    int64_t lo = row_off[r], hi = row_off[r + 1];
+    bool found = false;
+    float v = 0.f;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      const int x = fid[mid];
+      if (x == f) {
+        found = true;
+        v = val ? val[mid] : 1.f;
+        break;
+      }
+      if (x < f) lo = mid + 1;
+      else hi = mid;
+    }
+    const bool goleft = found ? (v < thr[nd]) : (defl[nd] != 0);
+    nd = goleft ? left[nd] : right[nd];
+  }
+  margin[r] += leaf[nd];
+}
+
+}  // namespace
+
+void gbdt_bin_csr(const int32_t* fid, const float* val, int64_t nnz, int ncol, const float* cuts,
+                  const int32_t* cut_off, int32_t* gbin, hipStream_t s) {
+  if (nnz <= 0) return;
+  hipLaunchKernelGGL(k_bin_csr, dim3(grid_for(nnz, 256)), dim3(256), 0, s, fid, val, nnz, ncol,
+                     cuts, cut_off, gbin);
+}
+
+void gbdt_hist_csr(const int64_t* row_off, const int32_t* gbin, const int32_t* ridx,
+                   const float* gpair, const float* qscale, const int32_t* tasks, int ntask,
+                   int max_rows, int64_t tb, int nslot, int64_t* hq, double* hist, hipStream_t s) {
+  const int64_t ne = (int64_t)nslot * tb * 2;
+  if (ne <= 0) return;
+  WH_HIP_CHECK(hipMemsetAsync(hq, 0, ne * 8, s));
+  if (ntask > 0 && max_rows > 0)
+    hipLaunchKernelGGL(k_hist_csr, dim3((unsigned)((max_rows + 255) / 256), ntask), dim3(256), 0,
+                       s, row_off, gbin, ridx, reinterpret_cast<const float2*>(gpair), qscale,
+                       tasks, tb, reinterpret_cast<unsigned long long*>(hq));
+  hipLaunchKernelGGL(k_hist_csr_fin, dim3(grid_for(ne, 256)), dim3(256), 0, s,
+                     reinterpret_cast<const unsigned long long*>(hq), ne, qscale, hist);
+}
+
+void gbdt_split_csr(const double* hist, int64_t tb, const double* totals,
+                    const int32_t* cut_off, const uint8_t* fvalid, int S, int F, double alpha,
+                    double lambda, double mcw, double* cand, double* out, hipStream_t s) {
+  if (S <= 0 || F <= 0) return;
+  const SplitParam p{alpha, lambda, mcw};
+  hipLaunchKernelGGL(k_split_csr_feat, dim3((unsigned)((F + 255) / 256), S), dim3(256), 0, s,
+                     hist, tb, totals, cut_off, fvalid, F, p, cand);
+  hipLaunchKernelGGL(k_split_csr_node, dim3((unsigned)S), dim3(256), 0, s, cand, F, out);
+}
+
+void gbdt_goleft_csr(const int64_t* row_off, const int32_t* fid, const int32_t* gbin,
+                     const int32_t* cut_off, const int32_t* ridx, int64_t n,
+                     const int32_t* pos_node, const int32_t* node_feat, const int32_t* node_bin,
+                     const uint8_t* node_defl, int32_t* left, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_goleft_csr, dim3(grid_for(n, 256)), dim3(256), 0, s, row_off, fid, gbin,
+                     cut_off, ridx, n, pos_node, node_feat, node_bin, node_defl, left);
+}
+
+void gbdt_predict_csr(const int64_t* row_off, const int32_t* fid, const float* val, int64_t n,
+                      const int32_t* feat, const float* thr, const int32_t* left,
+                      const int32_t* right, const uint8_t* defl, const float* leaf, float* margin,
+                      hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_predict_csr, dim3(grid_for(n, 256)), dim3(256), 0, s, row_off, fid, val, n,
+                     feat, thr, left, right, defl, leaf, margin);
 }
 
 }  // namespace wh

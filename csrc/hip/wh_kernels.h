@@ -424,6 +424,27 @@ void gbdt_leaf_add(const int32_t* ridx, int64_t n, const int32_t* pos_node, cons
 bool gbdt_split(const double* hist, const double* totals, const uint8_t* valid, int S, int F,
                 int nbin, double alpha, double lambda, double mcw, double* cand, double* out,
                 hipStream_t s);
+// sparse (CSR) input: global bin ids (cut_off[f] + bin, -1 = unbinned),
+// compact [slots][total bins][2] histograms (tasks [ntask x 3] = {slot,
+// rbeg, rend}, hq: int64 scratch of the histogram's size), split search over
+// the compact layout (cand: [S x F x 5] scratch; out [S x 6] as gbdt_split,
+// bin local to the feature), partition flags and tree walk on CSR rows
+void gbdt_bin_csr(const int32_t* fid, const float* val, int64_t nnz, int ncol, const float* cuts,
+                  const int32_t* cut_off, int32_t* gbin, hipStream_t s);
+void gbdt_hist_csr(const int64_t* row_off, const int32_t* gbin, const int32_t* ridx,
+                   const float* gpair, const float* qscale, const int32_t* tasks, int ntask,
+                   int max_rows, int64_t tb, int nslot, int64_t* hq, double* hist, hipStream_t s);
+void gbdt_split_csr(const double* hist, int64_t tb, const double* totals,
+                    const int32_t* cut_off, const uint8_t* fvalid, int S, int F, double alpha,
+                    double lambda, double mcw, double* cand, double* out, hipStream_t s);
+void gbdt_goleft_csr(const int64_t* row_off, const int32_t* fid, const int32_t* gbin,
+                     const int32_t* cut_off, const int32_t* ridx, int64_t n,
+                     const int32_t* pos_node, const int32_t* node_feat, const int32_t* node_bin,
+                     const uint8_t* node_defl, int32_t* left, hipStream_t s);
+void gbdt_predict_csr(const int64_t* row_off, const int32_t* fid, const float* val, int64_t n,
+                      const int32_t* feat, const float* thr, const int32_t* left,
+                      const int32_t* right, const uint8_t* defl, const float* leaf, float* margin,
+                      hipStream_t s);
 void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const float* thr,
                   const int32_t* left, const int32_t* right, const uint8_t* defl,
                   const float* leaf, float* margin, hipStream_t s);

@@ -209,3 +209,51 @@ def test_gbdt_native_grower_matches_python_loop(gamma, colsample):
         assert a.left == b.left and a.right == b.right
         assert all(abs(x - z) < 1e-6 for x, z in zip(a.leaf, b.leaf))
     assert torch.allclose(res[0][1], res[1][1], atol=1e-6)
+
+
+def test_gbdt_csr_gpu_matches_dense_and_trains_wide_data():
+    """CSR kernels (global-bin histograms, compact split search, CSR
+    partition and tree walk) grow the dense path's trees on agaricus, and a
+    libsvm-shaped matrix with a 1M-feature space trains without densifying
+    (a dense float matrix of it would be 80 GB)."""
+    from wormhole_amd import _native
+    from wormhole_amd.models import gbdt as G
+    from wormhole_amd.parallel.bsp import BSP
+    dev = torch.device("cuda", 0)
+    host = _native.host()
+    keys, off, val, lab, _ = host.load_split(os.path.join(ROOT, "learn", "data",
+                                                          "agaricus.txt.train"), 0, 1, "libsvm")
+    bsp = BSP(torch.device("cpu"))
+    p = G.GBDTParam()
+    p.objective, p.max_depth, p.eta = "binary:logistic", 4, 0.5
+    ncol = int(keys.max()) + 1
+    obj = G.Objective(p.objective)
+    res = []
+    for sparse in (False, True):
+        dm = G.make_dmatrix(keys, off, val, lab, None, ncol, dev, sparse=sparse)
+        margin = torch.zeros(dm.n, device=dev)
+        cuts = G.Cuts.build(dm, 64, bsp, hess=obj.gpair(margin, dm.label, None)[:, 1])
+        tb = G.make_builder(p, bsp, dm, cuts, cuts.bin(dm))
+        res.append(([tb.build(obj.gpair(margin, dm.label, None), margin) for _ in range(3)],
+                    margin.cpu()))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert a.feat == b.feat and a.cond == b.cond and a.defl == b.defl
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-6)
+    # wide: 20k rows x 1M-feature space, ~40 stored values per row
+    g = torch.Generator().manual_seed(3)
+    n, F, per = 20000, 1_000_000, 40
+    k = torch.randint(0, F, (n, per), generator=g)
+    k[:, 0] = torch.randint(0, 50, (n,), generator=g)  # a few dense-ish informative ids
+    k = torch.sort(k, 1).values
+    y = ((k[:, 0] % 2) == 0).float()
+    offs = torch.arange(n + 1, dtype=torch.int64) * per
+    dm = G.make_dmatrix(k.reshape(-1), offs, None, y, None, F, dev)
+    assert getattr(dm, "sparse", False)
+    margin = torch.zeros(n, device=dev)
+    cuts = G.Cuts.build(dm, 64, bsp)
+    tb = G.make_builder(p, bsp, dm, cuts, cuts.bin(dm))
+    err0 = G.eval_metric("error", torch.sigmoid(margin), dm.label, None, bsp)
+    for _ in range(3):
+        tb.build(obj.gpair(margin, dm.label, None), margin)
+    err = G.eval_metric("error", torch.sigmoid(margin), dm.label, None, bsp)
+    assert err < 0.5 * err0, (err0, err)

@@ -131,3 +131,60 @@ def test_external_memory_cache_suffix(work):
     r2 = run(args + ["model_out=b.model"], work)
     assert r2.returncode == 0, r2.stderr[-2000:]
     assert open(work / "a.model", "rb").read() == open(work / "b.model", "rb").read()
+
+
+def _agaricus():
+    from wormhole_amd import _native
+    host = _native.host()
+    keys, off, val, lab, wt = host.load_split(os.path.join(ROOT, "learn", "data",
+                                                           "agaricus.txt.train"), 0, 1, "libsvm")
+    return keys, off, val, lab
+
+
+def _train(G, bsp, dm, p, rounds, hess_sketch=True):
+    obj = G.Objective(p.objective)
+    margin = torch.zeros(dm.n, device=dm.device)
+    hess = obj.gpair(margin, dm.label, None)[:, 1] if hess_sketch else None
+    cuts = G.Cuts.build(dm, p.max_bin, bsp, hess=hess)
+    tb = G.make_builder(p, bsp, dm, cuts, cuts.bin(dm))
+    trees = [tb.build(obj.gpair(margin, dm.label, None), margin) for _ in range(rounds)]
+    return trees, margin
+
+
+def test_csr_matrix_grows_the_dense_trees():
+    """Agaricus kept CSR (dsparse) grows the trees of the dense matrix: absent
+    features are missing in both, the sketch and split search agree."""
+    from wormhole_amd.models import gbdt as G
+    from wormhole_amd.parallel.bsp import BSP
+    keys, off, val, lab = _agaricus()
+    bsp = BSP(torch.device("cpu"))
+    p = G.GBDTParam()
+    p.objective, p.max_depth, p.eta = "binary:logistic", 3, 0.5
+    ncol = int(keys.max()) + 1
+    res = []
+    for sparse in (False, True):
+        dm = G.make_dmatrix(keys, off, val, lab, None, ncol, torch.device("cpu"), sparse=sparse)
+        assert getattr(dm, "sparse", False) == sparse
+        res.append(_train(G, bsp, dm, p, 2))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert a.feat == b.feat and a.cond == b.cond and a.defl == b.defl
+        assert all(abs(x - z) < 1e-9 for x, z in zip(a.leaf, b.leaf))
+    assert torch.allclose(res[0][1], res[1][1])
+
+
+def test_weighted_sketch_follows_hessian_mass():
+    """Cuts split each feature's HESSIAN weight evenly: rows with 9x the
+    weight pull the cuts into their value range."""
+    from wormhole_amd.models import gbdt as G
+    from wormhole_amd.parallel.bsp import BSP
+    n = 20000
+    x = torch.rand(n, 1)
+    dm = G.DMatrix.from_dense(x, torch.zeros(n), torch.device("cpu"))
+    bsp = BSP(torch.device("cpu"))
+    w = torch.where(x[:, 0] < 0.5, torch.full((n,), 9.0), torch.ones(n))
+    cuts = G.Cuts.build(dm, 16, bsp, hess=w)
+    c = cuts.values[:-1]
+    below = float((c < 0.5).float().mean())
+    assert 0.85 < below < 0.95, c  # 90 % of the weight sits below 0.5
+    cu = G.Cuts.build(dm, 16, bsp).values[:-1]  # unweighted: even in value
+    assert 0.4 < float((cu < 0.5).float().mean()) < 0.6

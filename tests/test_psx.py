@@ -36,6 +36,7 @@ def _run(comm, conf, device, steps=6, rows=300, seed=17, nxt=True):
         if nxt and s + 1 < steps:
             nb = (batches[s + 1][0], batches[s + 1][2], None)
         lr.process(keys, off, None, label, 0, 0, next_batch=nb)
+    lr.flush()  # (collective on several ranks; take_progress itself stays local)
     prog = lr.take_progress()
     return lr, prog, batches
 

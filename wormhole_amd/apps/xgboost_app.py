@@ -6,7 +6,8 @@ tasks ``train | pred | dump | eval``; parameters booster, objective, eta,
 gamma, min_child_weight, max_depth, lambda, alpha, base_score, max_bin,
 subsample, colsample_bytree, seed, eval_metric, num_round, save_period,
 eval_train, eval[name]=path, data, test:data, model_in, model_out, model_dir,
-fmap, name_dump, name_pred, dump_stats, dsplit=row, nthread (ignored),
+fmap, name_dump, name_pred, dump_stats, dsplit=row, dsparse (keep the rows CSR:
+wide libsvm data; default when num_feature > 4096), nthread (ignored),
 num_feature.  Output: ``[r]\\t<set>-<metric>:<value>`` lines per round.
 """
 import os
@@ -58,6 +59,7 @@ def main(argv):
     num_round, save_period, eval_train = 10, 0, 0
     fmap, name_dump, name_pred, dump_stats = None, "dump.txt", "pred.txt", 0
     num_feature = 0
+    dsparse = None  # dsparse=1|0: keep the data CSR / dense (default: by width)
     evals = []
     for k, v in parse_args(argv):
         if param.set(k, v):
@@ -94,6 +96,8 @@ def main(argv):
             dump_stats = int(v)
         elif k == "num_feature":
             num_feature = int(v)
+        elif k == "dsparse":
+            dsparse = bool(int(v))
         elif k in ("dsplit",):
             if v not in ("row", "auto"):
                 raise SystemExit("only dsplit=row is supported")
@@ -147,7 +151,7 @@ def main(argv):
         b = G.Booster.load(model_in, param)
         path = test_data or data
         raw = load(path)
-        dm = G.DMatrix(*raw, ncol=b.num_feature, device=dev)
+        dm = G.make_dmatrix(*raw, ncol=b.num_feature, device=dev, sparse=dsparse)
         pred = b.obj.pred(b.predict_margin(dm))
         if task == "eval":
             metrics = param.eval_metric or [b.obj.default_metric()]
@@ -172,8 +176,9 @@ def main(argv):
     ncol = max([int(r[0].max().item()) + 1 if r[0].numel() else 0
                 for r in [train_raw] + [e[1] for e in eval_raw]] + [num_feature])
     ncol = int(bsp.allreduce_scalar(ncol, "max", torch.int64))
-    dtrain = G.DMatrix(*train_raw, ncol=ncol, device=dev)
-    deval = [(name, G.DMatrix(*r, ncol=ncol, device=dev)) for name, r in eval_raw]
+    dtrain = G.make_dmatrix(*train_raw, ncol=ncol, device=dev, sparse=dsparse)
+    deval = [(name, G.make_dmatrix(*r, ncol=ncol, device=dev, sparse=dsparse))
+             for name, r in eval_raw]
     booster = G.Booster.load(model_in, param) if model_in else G.Booster(param, ncol)
     start = len(booster.trees)
     version, gstate, _ = bsp.load_checkpoint()
@@ -181,10 +186,12 @@ def main(argv):
         booster = _booster_from_state(G, gstate, param)
         start = len(booster.trees)
         print("restart from version=%d (round %d)" % (version, start), flush=True)
-    cuts = G.Cuts.build(dtrain, param.max_bin, bsp)
-    B = cuts.bin(dtrain)
-    builder = G.TreeBuilder(param, bsp, dtrain, cuts, B)
     margin = booster.predict_margin(dtrain)
+    # hessian-weighted sketch: weights at the starting margin
+    hess = booster.obj.gpair(margin, dtrain.label, None)[:, 1] if dtrain.n else None
+    cuts = G.Cuts.build(dtrain, param.max_bin, bsp, hess=hess)
+    B = cuts.bin(dtrain)
+    builder = G.make_builder(param, bsp, dtrain, cuts, B)
     emargins = [booster.predict_margin(d) for _, d in deval]
     metrics = param.eval_metric or [booster.obj.default_metric()]
     gen = torch.Generator().manual_seed(param.seed + 17 * bsp.rank)
@@ -199,7 +206,7 @@ def main(argv):
         booster.trees.append(tree)
         msg = "[%d]" % r
         for (name, d), em in zip(deval, emargins):
-            tree.predict_margin(d.X, em)
+            d.predict_tree(tree, em)
             p = booster.obj.pred(em)
             for m in metrics:
                 msg += "\t%s-%s:%f" % (name, m, G.eval_metric(m, p, d.label, d.weight, bsp))

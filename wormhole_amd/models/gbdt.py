@@ -199,6 +199,70 @@ class DMatrix:
         d.B = None
         return d
 
+    def predict_tree(self, tree, margin):
+        return tree.predict_margin(self.X, margin)
+
+
+class CSRMatrix:
+    """A rank's rows kept sparse (libsvm data with a wide feature space:
+    a dense n x ncol matrix would not fit). Row feature ids are sorted
+    ascending within each row; a feature a row does not store is missing
+    (default direction), exactly as NaN in the dense matrix."""
+
+    sparse = True
+
+    def __init__(self, keys, offset, val, label, weight, ncol, device):
+        n = offset.numel() - 1
+        self.n, self.ncol, self.device = n, int(ncol), device
+        off = offset.to(torch.int64)
+        k = keys.to(torch.int64)
+        v = val.float() if val is not None and val.numel() else None
+        if k.numel():
+            rows = torch.repeat_interleave(torch.arange(n, dtype=torch.int64), off[1:] - off[:-1])
+            order = torch.argsort(rows * (self.ncol + 1) + k.clamp(0, self.ncol), stable=True)
+            k = k[order]
+            v = v[order] if v is not None else None
+        self.row_off = off.to(device).contiguous()
+        self.fid = k.to(torch.int32).to(device).contiguous()
+        self.val = v.to(device).contiguous() if v is not None else None
+        self.label = label.to(device).float()
+        self.weight = weight.to(device).float() if weight is not None else None
+        self.gbin = None
+
+    def entry_rows(self):
+        return torch.repeat_interleave(torch.arange(self.n, device=self.device),
+                                       self.row_off[1:] - self.row_off[:-1])
+
+    def predict_tree(self, tree, margin):
+        if self.n == 0:
+            return margin
+        if self.device.type == "cuda":
+            _native.hip().gbdt_predict_csr(self.row_off, self.fid, self.val,
+                                           *tree.device_arrays(self.device), margin)
+            return margin
+        return tree.predict_margin(self.dense_cpu(), margin)
+
+    def dense_cpu(self):
+        """(CPU reference path only: small matrices)"""
+        X = torch.full((self.n, self.ncol), float("nan"))
+        rows = self.entry_rows().cpu()
+        ok = self.fid.cpu().long() < self.ncol
+        X[rows[ok], self.fid.cpu().long()[ok]] = (self.val.cpu()[ok] if self.val is not None
+                                                  else torch.ones(int(ok.sum())))
+        return X
+
+
+def make_dmatrix(keys, offset, val, label, weight, ncol, device, sparse=None):
+    """Dense device matrix, or CSR when asked (sparse=True) or when the dense
+    form would be large and mostly missing (auto: sparse=None)."""
+    n = offset.numel() - 1
+    if sparse is None:
+        cells = n * max(int(ncol), 1)
+        sparse = int(ncol) > 4096 or (cells > (1 << 28) and keys.numel() < cells // 8)
+    if sparse:
+        return CSRMatrix(keys, offset, val, label, weight, ncol, device)
+    return DMatrix(keys, offset, val, label, weight, ncol, device)
+
 
 class Cuts:
     def __init__(self, values, offsets):
@@ -211,44 +275,103 @@ class Cuts:
         return max(b - a for a, b in zip(o, o[1:])) if len(o) > 1 else 1
 
     @staticmethod
-    def build(dm, max_bin, bsp, nsample=2048):
-        """Merge rank-local order statistics into <= max_bin cuts per feature."""
+    def build(dm, max_bin, bsp, hess=None, nsummary=None):
+        """Hessian-weighted quantile sketch (xgboost's WQSketch semantics):
+        every stored value weighs its row's hessian (x instance weight; the
+        hessian at the base margin when not given), cuts split each
+        feature's weight evenly. Each rank summarises its values into <= 4 x
+        max_bin weighted points per feature; the summaries are all-gathered
+        and merged by the same weighted quantile rule."""
         max_bin = min(int(max_bin), 255)
-        F = dm.ncol
-        samples = []
-        counts = []
-        X = dm.X
-        for j in range(F):
-            col = X[:, j]
-            col = col[~torch.isnan(col)]
-            c = col.numel()
-            if c == 0:
-                s = torch.zeros(0)
-            else:
-                col, _ = torch.sort(col)
-                if c > nsample:
-                    idx = torch.linspace(0, c - 1, nsample, device=col.device).round().long()
-                    col = col[idx]
-                s = col.float().cpu()
-            samples.append(s)
-            counts.append(c)
-        gathered = bsp.comm.allgather_object((samples, counts)) if bsp.world > 1 else [
-            (samples, counts)]
+        nsummary = nsummary or 4 * max_bin
+        w_row = hess if hess is not None else torch.ones(dm.n, device=dm.device)
+        if dm.weight is not None:
+            w_row = w_row * dm.weight
+        w_row = w_row.float()
+        if getattr(dm, "sparse", False):
+            fid, v, w = dm.fid.long(), (dm.val if dm.val is not None else
+                                        torch.ones(dm.fid.numel(), device=dm.device)), None
+            w = w_row[dm.entry_rows()] if dm.n else torch.zeros(0, device=dm.device)
+            ok = (fid >= 0) & (fid < dm.ncol)
+            sf, sv, sw = Cuts._summary(fid[ok], v[ok].float(), w[ok], dm.ncol, nsummary)
+        else:
+            F = dm.ncol
+            parts = []
+            for j in range(F):
+                col = dm.X[:, j]
+                ok = ~torch.isnan(col)
+                parts.append((torch.full((int(ok.sum()),), j, dtype=torch.int64,
+                                         device=dm.device), col[ok], w_row[ok]))
+            sf, sv, sw = Cuts._summary(torch.cat([p[0] for p in parts]),
+                                       torch.cat([p[1] for p in parts]),
+                                       torch.cat([p[2] for p in parts]), F, nsummary)
+        local = (sf.cpu(), sv.double().cpu(), sw.double().cpu())
+        gathered = bsp.comm.allgather_object(local) if bsp.world > 1 else [local]
+        f_all = torch.cat([g[0] for g in gathered])
+        v_all = torch.cat([g[1] for g in gathered])
+        w_all = torch.cat([g[2] for g in gathered])
+        order = torch.argsort(f_all * 0 + v_all, stable=True)
+        order = order[torch.argsort(f_all[order], stable=True)]
+        f_all, v_all, w_all = f_all[order], v_all[order], w_all[order]
+        return Cuts._cuts_from_sorted(f_all, v_all, w_all, dm.ncol, max_bin)
+
+    @staticmethod
+    def _summary(fid, v, w, ncol, m):
+        """Per feature: the distinct values when there are <= m, else m
+        weighted quantile points each carrying its bucket's weight."""
+        if fid.numel() == 0:
+            z = torch.zeros(0)
+            return z.long(), z, z
+        order = torch.argsort(v, stable=True)
+        order = order[torch.argsort(fid[order], stable=True)]
+        fid, v, w = fid[order], v[order].double(), w[order].double()
+        # merge equal (feature, value) runs
+        new = torch.ones(fid.numel(), dtype=torch.bool, device=fid.device)
+        new[1:] = (fid[1:] != fid[:-1]) | (v[1:] != v[:-1])
+        grp = torch.cumsum(new.long(), 0) - 1
+        ng = int(grp[-1]) + 1
+        fid, v = fid[new], v[new]
+        w = torch.zeros(ng, dtype=torch.float64, device=w.device).index_add_(0, grp, w)
+        cnt = torch.bincount(fid, minlength=ncol)
+        start = torch.cumsum(cnt, 0) - cnt
+        big = cnt[fid] > m
+        if bool(big.any()):
+            cw = torch.cumsum(w, 0)
+            fw = torch.zeros(ncol, dtype=torch.float64, device=w.device).index_add_(0, fid, w)
+            base = cw[start[fid]] - w[start[fid]]
+            q = ((cw - base) / fw[fid].clamp_min(1e-300) * m).floor().clamp(max=m - 1)
+            key = fid * (m + 1) + q.long()
+            keep_bkt = torch.ones_like(new[: fid.numel()])
+            keep_bkt[1:] = key[1:] != key[:-1]
+            # a big feature keeps the last value of each weight bucket with
+            # the bucket's weight; small features keep every value
+            last = torch.ones_like(keep_bkt)
+            last[:-1] = key[1:] != key[:-1]
+            bid = torch.cumsum(keep_bkt.long(), 0) - 1
+            bw = torch.zeros(int(bid[-1]) + 1, dtype=torch.float64, device=w.device).index_add_(0, bid, w)
+            keep = ~big | last
+            wout = torch.where(big, bw[bid], w)
+            return fid[keep], v[keep], wout[keep]
+        return fid, v, w
+
+    @staticmethod
+    def _cuts_from_sorted(fid, v, w, ncol, max_bin):
         vals, offs = [], [0]
-        for j in range(F):
-            parts = [(g[0][j], g[1][j]) for g in gathered]
-            v = torch.cat([p for p, _ in parts]) if parts else torch.zeros(0)
-            w = torch.cat([torch.full((p.numel(),), c / max(p.numel(), 1), dtype=torch.float64)
-                           for p, c in parts]) if parts else torch.zeros(0, dtype=torch.float64)
-            cuts = Cuts._feature_cuts(v, w, max_bin)
-            vals.extend(cuts)
+        fid, v, w = fid.long(), v.double(), w.double()
+        cnt = torch.bincount(fid, minlength=ncol).tolist() if fid.numel() else [0] * ncol
+        pos = 0
+        for j in range(ncol):
+            c = cnt[j]
+            if c:
+                vals.extend(Cuts._feature_cuts(v[pos:pos + c], w[pos:pos + c], max_bin))
+            pos += c
             offs.append(len(vals))
         return Cuts(torch.tensor(vals, dtype=torch.float32), torch.tensor(offs, dtype=torch.int32))
 
     @staticmethod
     def _feature_cuts(v, w, max_bin):
         if v.numel() == 0:
-            return [float("inf")]
+            return []
         order = torch.argsort(v)
         v, w = v[order].double(), w[order]
         uniq, inv = torch.unique_consecutive(v, return_inverse=True)
@@ -272,6 +395,22 @@ class Cuts:
         return [float(np.float32(c)) for c in cuts]
 
     def bin(self, dm):
+        if getattr(dm, "sparse", False):
+            if dm.device.type == "cuda":
+                return _native.hip().gbdt_bin_csr(dm.fid, dm.val, dm.ncol,
+                                                  self.values.to(dm.device),
+                                                  self.offsets.to(dm.device))
+            fid = dm.fid.long()
+            v = dm.val if dm.val is not None else torch.ones(fid.numel())
+            o = self.offsets.tolist()
+            g = torch.full((fid.numel(),), -1, dtype=torch.int32)
+            for j in range(dm.ncol):
+                m = fid == j
+                if o[j + 1] > o[j] and bool(m.any()):
+                    c = self.values[o[j]:o[j + 1]]
+                    b = torch.searchsorted(c, v[m], right=True).clamp(max=c.numel() - 1)
+                    g[m] = (b + o[j]).to(torch.int32)
+            return g
         if dm.X.is_cuda:
             return _native.hip().gbdt_bin(dm.X, self.values.to(dm.device),
                                           self.offsets.to(dm.device))
@@ -547,7 +686,7 @@ class TreeBuilder:
 
     # ----------------------------------------------------------------- build
     def build(self, gpair, margin):
-        if self.gpu and self.dm.n > 0:
+        if self.gpu and self.dm.n > 0 and not getattr(self.dm, "sparse", False):
             return self._build_native(gpair, margin)
         return self._build_py(gpair, margin)
 
@@ -678,8 +817,9 @@ class TreeBuilder:
             small_is_left = _h2d(torch.tensor([small[k] == tree.left[nd]
                                                for k, nd in enumerate(split_nodes)]),
                                  H_front.device)
-            hl = torch.where(small_is_left[:, None, None, None], hsmall, hbig)
-            hr = torch.where(small_is_left[:, None, None, None], hbig, hsmall)
+            sil = small_is_left.view(-1, *([1] * (hsmall.dim() - 1)))
+            hl = torch.where(sil, hsmall, hbig)
+            hr = torch.where(sil, hbig, hsmall)
             H_front = torch.stack([hl, hr], 1).reshape(-1, *H_front.shape[1:])
             frontier = new_frontier
         # margins of the training rows from the final leaf segments
@@ -778,7 +918,7 @@ class TreeBuilder:
             _native.hip().gbdt_leaf_add(ridx, pos, val.to(self.device), margin)
         self._compact(tree)
         if n and not self.gpu:
-            tree.predict_margin(self.dm.X, margin)
+            self.dm.predict_tree(tree, margin)
 
     @staticmethod
     def _compact(tree):
@@ -806,6 +946,134 @@ class TreeBuilder:
         tree._remap = remap
 
 
+class CSRTreeBuilder(TreeBuilder):
+    """Tree growth on a :class:`CSRMatrix`: the same depth-wise level loop
+    (smaller-child histograms, sibling subtraction, both default directions)
+    over compact [slots][total bins][2] histograms -- no F x max_bin padding
+    and no dense n x F bin matrix."""
+
+    def __init__(self, param, bsp, dm, cuts, gbin):
+        self.p, self.bsp, self.dm, self.cuts = param, bsp, dm, cuts
+        self.gbin = gbin
+        self.F = dm.ncol
+        self.device = dm.device
+        self.gpu = dm.device.type == "cuda"
+        self.tb = int(cuts.offsets[-1]) if cuts.offsets.numel() else 0
+        self.cut_off = cuts.offsets.to(self.device).contiguous()
+        self.fvalid = None
+        self._nglobal = None
+        self._rows = None
+
+    def sample_features(self, gen):
+        self.fvalid = None
+        if self.p.colsample_bytree < 1.0 and self.F > 0:
+            k = max(1, int(round(self.p.colsample_bytree * self.F)))
+            keep = torch.randperm(self.F, generator=gen)[:k]
+            m = torch.zeros(self.F, dtype=torch.uint8)
+            m[keep] = 1
+            self.fvalid = m.to(self.device)
+
+    def _build_hist(self, ridx, gpair, segs, slots, nslot):
+        if self.gpu:
+            chunk, tasks = 16384, []
+            for (b, e), sl in zip(segs, slots):
+                for r in range(b, e, chunk):
+                    tasks += [sl, r, min(e, r + chunk)]
+            t = _h2d(torch.tensor(tasks or [0, 0, 0], dtype=torch.int32), self.device)
+            return _native.hip().gbdt_hist_csr(self.dm.row_off, self.gbin, ridx, gpair,
+                                               self._qscale, t, chunk if tasks else 0, self.tb,
+                                               nslot)
+        hist = torch.zeros(nslot, self.tb, 2, dtype=torch.float64)
+        if self._rows is None:
+            self._rows = self.dm.entry_rows()
+        for (b, e), sl in zip(segs, slots):
+            if e <= b:
+                continue
+            inseg = torch.zeros(self.dm.n, dtype=torch.bool)
+            inseg[ridx[b:e].long()] = True
+            m = inseg[self._rows] & (self.gbin >= 0)
+            gb = self.gbin[m].long()
+            gh = gpair[self._rows[m]].double()
+            for c in range(2):
+                hist[sl, :, c].index_add_(0, gb, gh[:, c])
+        return hist
+
+    def _find_splits(self, hist, totals):
+        p = self.p
+        if self.gpu:
+            out = _native.hip().gbdt_split_csr(hist.contiguous(), totals.double().contiguous(),
+                                               self.cut_off, self.fvalid, float(p.alpha),
+                                               float(p.reg_lambda),
+                                               float(p.min_child_weight)).cpu()
+            return (out[:, 0], out[:, 1].long(), out[:, 2].long(), out[:, 3].long(),
+                    out[:, 4:6])
+        # reference: per feature scans over its compact bins
+        o = self.cuts.offsets.tolist()
+        S = hist.shape[0]
+        res = torch.zeros(S, 6, dtype=torch.float64)
+        for s_ in range(S):
+            TG, TH = float(totals[s_, 0]), float(totals[s_, 1])
+            parent = float(p.calc_gain(torch.tensor(TG), torch.tensor(TH)))
+            best = (-float("inf"), 0, 0, 0, 0.0, 0.0)
+            for f in range(self.F):
+                if o[f + 1] <= o[f] or (self.fvalid is not None and not int(self.fvalid[f])):
+                    continue
+                hb = hist[s_, o[f]:o[f + 1]]
+                cum = hb.cumsum(0)
+                mg, mh = TG - float(cum[-1, 0]), TH - float(cum[-1, 1])
+                for b in range(hb.shape[0]):
+                    for d in (0, 1):
+                        GL = float(cum[b, 0]) + (mg if d else 0.0)
+                        HL = float(cum[b, 1]) + (mh if d else 0.0)
+                        GR, HR = TG - GL, TH - HL
+                        if not (HL >= p.min_child_weight and HR >= p.min_child_weight):
+                            continue
+                        g = (float(p.calc_gain(torch.tensor(GL), torch.tensor(HL))) +
+                             float(p.calc_gain(torch.tensor(GR), torch.tensor(HR))) - parent)
+                        if g > best[0]:
+                            best = (g, f, b, d, GL, HL)
+            res[s_] = torch.tensor(best, dtype=torch.float64)
+        return res[:, 0], res[:, 1].long(), res[:, 2].long(), res[:, 3].long(), res[:, 4:6]
+
+    def _partition(self, ridx, pos_node, node_feat, node_bin, node_defl, seg_beg, seg_end):
+        if self.gpu:
+            nleft = torch.zeros(node_feat.numel(), dtype=torch.int32, device=self.device)
+            pk = _h2d(torch.stack([node_feat, node_bin, node_defl.to(torch.int32), seg_beg,
+                                   seg_end]), self.device)
+            out = _native.hip().gbdt_partition_csr(self.dm.row_off, self.dm.fid, self.gbin,
+                                                   self.cut_off, ridx, pos_node, pk[0], pk[1],
+                                                   pk[2].to(torch.uint8), pk[3], pk[4], nleft)
+            return out, nleft.cpu()
+        if self._rows is None:
+            self._rows = self.dm.entry_rows()
+        out = ridx.clone()
+        nleft = torch.zeros(node_feat.numel(), dtype=torch.int32)
+        o = self.cuts.offsets
+        for nd in range(node_feat.numel()):
+            f = int(node_feat[nd])
+            if f < 0:
+                continue
+            b, e = int(seg_beg[nd]), int(seg_end[nd])
+            rows = ridx[b:e].long()
+            lb = torch.full((self.dm.n,), -1, dtype=torch.long)
+            m = self.dm.fid.long() == f
+            lb[self._rows[m]] = self.gbin[m].long() - int(o[f])
+            v = lb[rows]
+            left = torch.where(v < 0, torch.full_like(v, int(node_defl[nd])),
+                               (v <= int(node_bin[nd])).long()).bool()
+            nl = int(left.sum())
+            out[b:b + nl] = ridx[b:e][left]
+            out[b + nl:e] = ridx[b:e][~left]
+            nleft[nd] = nl
+        return out, nleft
+
+
+def make_builder(param, bsp, dm, cuts, B):
+    if getattr(dm, "sparse", False):
+        return CSRTreeBuilder(param, bsp, dm, cuts, B)
+    return TreeBuilder(param, bsp, dm, cuts, B)
+
+
 # ---------------------------------------------------------------- booster
 class Booster:
     MAGIC = b"WHGB"
@@ -821,7 +1089,7 @@ class Booster:
         margin = torch.full((dm.n,), self.base_margin, dtype=torch.float32, device=dm.device)
         trees = self.trees[:ntree_limit] if ntree_limit else self.trees
         for t in trees:
-            t.predict_margin(dm.X, margin)
+            dm.predict_tree(t, margin)
         return margin
 
     def save(self, path):
