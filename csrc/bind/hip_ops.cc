@@ -1585,6 +1585,40 @@ void gbdt_predict_csr(const Tensor& row_off, const Tensor& fid, const c10::optio
                        ptr<float>(leaf), ptr<float>(margin), cur_stream(fid));
 }
 
+// ------------------------------------------------------------ text ingest
+// text: uint8 [nbytes] of nlines whole lines (device) -> (keys i64 [nnz],
+// label f32 [nlines], offset i64 [nlines + 1]); one host read (the key
+// count) sizes the compacted keys
+std::vector<Tensor> parse_criteo(const Tensor& text, int64_t nlines, bool train) {
+  CHECK_IN(text, torch::kUInt8);
+  c10::DeviceGuard g(text.device());
+  auto s = cur_stream(text);
+  auto o = text.options();
+  const int64_t nb = text.numel();
+  const int64_t nt = wh::criteo_tiles(nb);
+  auto tile_cnt = torch::empty({std::max<int64_t>(nt, 1)}, o.dtype(torch::kInt32));
+  auto tile_off = torch::empty({nt + 1}, o.dtype(torch::kInt64));
+  auto stmp = torch::empty({wh::scan_tmp_elems(std::max<int64_t>(nt, 1))}, o.dtype(torch::kInt64));
+  auto start = torch::empty({nlines + 1}, o.dtype(torch::kInt64));
+  wh::criteo_lines(ptr<uint8_t>(text), nb, ptr<int32_t>(tile_cnt), ptr<int64_t>(tile_off),
+                   ptr<int64_t>(stmp), ptr<int64_t>(start), s);
+  auto padded = torch::empty({std::max<int64_t>(nlines * 39, 1)}, o.dtype(torch::kInt64));
+  auto cnt = torch::empty({std::max<int64_t>(nlines, 1)}, o.dtype(torch::kInt32));
+  auto label = torch::empty({nlines}, o.dtype(torch::kFloat32));
+  wh::criteo_fields(ptr<uint8_t>(text), nb, ptr<int64_t>(start), nlines, train,
+                    reinterpret_cast<uint64_t*>(padded.data_ptr()), ptr<int32_t>(cnt),
+                    ptr<float>(label), s);
+  auto off = torch::empty({nlines + 1}, o.dtype(torch::kInt64));
+  auto stmp2 = torch::empty({wh::scan_tmp_elems(std::max<int64_t>(nlines, 1))}, o.dtype(torch::kInt64));
+  if (nlines > 0) wh::scan_i32(ptr<int32_t>(cnt), ptr<int64_t>(off), nlines, ptr<int64_t>(stmp2), s);
+  else off.zero_();
+  const int64_t nnz = off[nlines].item<int64_t>();
+  auto keys = torch::empty({nnz}, o.dtype(torch::kInt64));
+  wh::criteo_compact(reinterpret_cast<const uint64_t*>(padded.data_ptr()), ptr<int64_t>(off),
+                     nlines, reinterpret_cast<uint64_t*>(keys.data_ptr()), s);
+  return {keys, label, off};
+}
+
 // ------------------------------------------------------------ gbdt grower
 // Depth-wise histogram tree growth with the level loop in C++ (reference:
 // xgboost hist updater driven by bin/xgboost.dmlc). Per level
@@ -1939,6 +1973,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_accum", &kmeans_accum);
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
   m.def("gbdt_grow", &gbdt_grow);
+  m.def("parse_criteo", &parse_criteo);
   m.def("gbdt_bin_csr", &gbdt_bin_csr);
   m.def("gbdt_hist_csr", &gbdt_hist_csr);
   m.def("gbdt_split_csr", &gbdt_split_csr);

@@ -449,6 +449,21 @@ void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const f
                   const int32_t* left, const int32_t* right, const uint8_t* defl,
                   const float* leaf, float* margin, hipStream_t s);
 
+// ------------------------------------------------------------- ingest.hip
+// Criteo text -> CSR minibatch on the device (keys bit-identical to the host
+// parser's CityHash64 keys). criteo_lines: start [nlines + 1] of the lines of
+// `text` (tile_cnt [criteo_tiles], tile_off [criteo_tiles + 1], scan_tmp
+// [scan_tmp_elems(criteo_tiles)]); criteo_fields: padded [nlines x 39] keys +
+// per-line counts + labels; criteo_compact: keys [sum counts] from the
+// scanned counts.
+int64_t criteo_tiles(int64_t nbytes);
+int64_t criteo_lines(const uint8_t* text, int64_t nbytes, int32_t* tile_cnt, int64_t* tile_off,
+                     int64_t* scan_tmp, int64_t* start, hipStream_t s);
+void criteo_fields(const uint8_t* text, int64_t nbytes, const int64_t* start, int64_t nlines,
+                   bool train, uint64_t* padded, int32_t* cnt, float* label, hipStream_t s);
+void criteo_compact(const uint64_t* padded, const int64_t* off, int64_t nlines, uint64_t* keys,
+                    hipStream_t s);
+
 // -------------------------------------------------------------- quant.hip
 // fixed_bytes payload filter: rows of w floats <-> packed records of
 // quant_record_bytes(w, nb) bytes {float scale, w signed nb-byte ints},

@@ -86,7 +86,7 @@ void ParseCriteo(const char* p, const char* end, bool is_train, RowBlock* blk) {
       pp = find(p, '\t');
       if (pp == p) throw std::runtime_error("criteo: no label, try criteo_test");
       blk->label.push_back(std::strtof(p, nullptr));  // stops at the tab
-      p = pp < end ? pp + 1 : pp;
+      p = (pp < end && *pp == '\t') ? pp + 1 : pp;  // a label-only line stays one row
     } else {
       blk->label.push_back(0.f);
     }

@@ -1,8 +1,12 @@
 // pybind11 registration of the native host runtime (wormhole_amd._host).
 #include <torch/extension.h>
 
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <memory>
+#include <mutex>
+#include <thread>
 
 #include "common.h"
 #include "io.h"
@@ -93,6 +97,152 @@ py::tuple load_split(const std::string& path, int part, int nparts, const std::s
   py::gil_scoped_acquire g;
   return block_to_py(all);
 }
+
+// Whole-line text batches for device-side parsing (csrc/hip/ingest.hip):
+// the part's byte range [begin, end) (line-aligned by InputSplit) is read in
+// large blocks by a background thread, cut after every mb-th newline with
+// memchr (empty lines do not count), each batch a (pinned) tensor (a final
+// line without a newline gets one). next() -> (uint8 tensor, lines) or None.
+class PyTextBatches {
+ public:
+  PyTextBatches(const std::string& path, int part, int nparts, int64_t mb, bool pinned,
+                int64_t depth)
+      : mb_(std::max<int64_t>(mb, 1)), pinned_(pinned), depth_(std::max<int64_t>(depth, 1)) {
+    InputSplit split(path, part, nparts, false);
+    begin_ = split.begin();
+    end_ = split.end();
+    path_ = ResolvePath(path);
+    th_ = std::thread([this] { Run(); });
+  }
+  ~PyTextBatches() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  py::object next() {
+    std::pair<Tensor, int64_t> item;
+    bool got = false;
+    std::string err;
+    {
+      py::gil_scoped_release nogil;
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait(lk, [&] { return !q_.empty() || done_ || !err_.empty(); });
+      if (!err_.empty()) {
+        err = err_;
+      } else if (!q_.empty()) {
+        item = std::move(q_.front());
+        q_.pop_front();
+        got = true;
+      }
+    }
+    cv_.notify_all();
+    if (!err.empty()) throw std::runtime_error(err);
+    if (!got) return py::none();
+    return py::make_tuple(item.first, item.second);
+  }
+
+ private:
+  Tensor Alloc(int64_t n) {
+    return torch::empty({n}, torch::TensorOptions().dtype(torch::kUInt8).pinned_memory(pinned_));
+  }
+  void Push(Tensor t, int64_t lines) {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return (int64_t)q_.size() < depth_ || stop_; });
+    q_.emplace_back(std::move(t), lines);
+    cv_.notify_all();
+  }
+  // file bytes are read straight into the (pinned) batch buffer; only the
+  // partial line after a cut is copied into the next buffer
+  void Run() {
+    try {
+      std::FILE* fp = std::fopen(path_.c_str(), "rb");
+      if (!fp) throw std::runtime_error("cannot open " + path_);
+      std::fseek(fp, begin_, SEEK_SET);
+      int64_t left = end_ - begin_;
+      int64_t cap = 4 << 20;
+      Tensor cur = Alloc(cap);
+      int64_t have = 0, scan = 0, lines = 0;
+      bool eof = left <= 0;
+      while (true) {
+        {
+          std::lock_guard<std::mutex> lk(mu_);
+          if (stop_) break;
+        }
+        char* b = static_cast<char*>(cur.data_ptr());
+        int64_t cut = 0;
+        while (scan < have) {
+          const char* q = static_cast<const char*>(std::memchr(b + scan, '\n', have - scan));
+          if (!q) {
+            scan = have;
+            break;
+          }
+          scan = (int64_t)(q - b) + 1;
+          // empty lines are not lines (parsers skip them; ingest.hip is_end)
+          if (q == b || q[-1] == '\n') continue;
+          if (++lines == mb_) {
+            cut = scan;
+            break;
+          }
+        }
+        if (cut) {
+          // the next buffer is sized from this batch (+1/8 headroom)
+          cap = std::max<int64_t>(cap, cut + cut / 8 + (have - cut) + 1);
+          Tensor nxt = Alloc(cap);
+          std::memcpy(nxt.data_ptr(), b + cut, have - cut);
+          Push(cur.narrow(0, 0, cut), mb_);
+          cur = nxt;
+          have -= cut;
+          scan = lines = 0;
+          continue;
+        }
+        if (eof) {
+          if (have) {
+            const bool add = b[have - 1] != '\n';
+            if (add) b[have++] = '\n';  // room: have < cap always holds here
+            Push(cur.narrow(0, 0, have), lines + (add ? 1 : 0));
+          }
+          break;
+        }
+        if (have + 1 >= cap) {  // a batch longer than the buffer: grow
+          cap *= 2;
+          Tensor g = Alloc(cap);
+          std::memcpy(g.data_ptr(), b, have);
+          cur = g;
+          b = static_cast<char*>(cur.data_ptr());
+        }
+        const int64_t want = std::min<int64_t>(left, cap - 1 - have);
+        const int64_t got = (int64_t)std::fread(b + have, 1, (size_t)want, fp);
+        have += got;
+        left -= got;
+        if (got == 0 || left <= 0) eof = true;
+      }
+      std::fclose(fp);
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> lk(mu_);
+      err_ = e.what();
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      done_ = true;
+    }
+    cv_.notify_all();
+  }
+
+  int64_t mb_;
+  bool pinned_;
+  int64_t depth_;
+  int64_t begin_ = 0, end_ = 0;
+  std::string path_;
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::pair<Tensor, int64_t>> q_;
+  bool stop_ = false, done_ = false;
+  std::string err_;
+};
 
 class PyMinibatchIter {
  public:
@@ -231,6 +381,11 @@ void register_all(py::module& m) {
       .def("close", &RecordIOWriter::Close)
       .def_property_readonly("bytes_written", &RecordIOWriter::bytes_written);
 
+  py::class_<PyTextBatches>(m, "TextBatches")
+      .def(py::init<const std::string&, int, int, int64_t, bool, int64_t>(), py::arg("path"),
+           py::arg("part"), py::arg("nparts"), py::arg("minibatch"), py::arg("pinned") = true,
+           py::arg("depth") = 3)
+      .def("next", &PyTextBatches::next);
   py::class_<PyMinibatchIter>(m, "MinibatchIter")
       .def(py::init<const std::string&, int, int, const std::string&, int64_t, int64_t, double,
                     int64_t, bool>(),

@@ -63,6 +63,48 @@ def _parse_fault(spec, rank):
     return kind, float(arg)
 
 
+class _TextBatch:
+    """Whole lines of Criteo text (pinned host bytes) parsed on the device."""
+
+    __slots__ = ("text", "lines", "train")
+
+    def __init__(self, text, lines, train):
+        self.text, self.lines, self.train = text, lines, train
+
+    def parse(self, dev):
+        """H2D + tokenize + hash on a side stream (its one host read, the key
+        count, then waits for this batch only, not for the training step in
+        flight); the main stream waits for the result."""
+        main = torch.cuda.current_stream(dev)
+        side = _parse_stream(dev)
+        with torch.cuda.stream(side):
+            t = self.text.to(dev, non_blocking=True)
+            keys, label, off = _native.hip().parse_criteo(t, int(self.lines), self.train)
+        main.wait_stream(side)
+        for x in (keys, label, off):
+            x.record_stream(main)
+        return keys, off, None, label
+
+
+_PARSE_STREAMS = {}
+
+
+def _parse_stream(dev):
+    s = _PARSE_STREAMS.get(dev)
+    if s is None:
+        s = _PARSE_STREAMS[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+class _TextIter:
+    def __init__(self, tb, train):
+        self.tb, self.train = tb, train
+
+    def next(self):
+        b = self.tb.next()
+        return None if b is None else _TextBatch(b[0], b[1], self.train)
+
+
 # --------------------------------------------------------------------------
 # worker
 # --------------------------------------------------------------------------
@@ -155,7 +197,19 @@ class Worker:
                 torch.zeros(1, dtype=torch.int64, device=dev), None,
                 torch.zeros(0, dtype=torch.float32, device=dev))
 
+    def _device_text(self, fmt, path, shuf, neg):
+        """Criteo text is split into whole-line batches on the host and
+        tokenized + hashed on the GPU (csrc/hip/ingest.hip) when nothing
+        needs the rows on the host: plain files, no shuffle, no negative
+        sampling. WH_DEVICE_PARSE=0 keeps the host parser."""
+        return (fmt in ("criteo", "criteo_test") and self.device.type == "cuda" and shuf == 0
+                and neg >= 1.0 and os.environ.get("WH_DEVICE_PARSE", "1") != "0"
+                and not path.endswith((".gz", ".crb", ".rec")) and "://" not in path.replace(
+                    "file://", ""))
+
     def _to_dev(self, b):
+        if isinstance(b, _TextBatch):
+            return b.parse(self.device)
         keys, off, val, label, _w = b
         dev = self.device
         nb = dev.type == "cuda"
@@ -202,9 +256,13 @@ class Worker:
             if d.get("file") is None:
                 exhausted = True
                 return
-            it = self.host.MinibatchIter(d["file"], d["k"], d["n"], fmt, int(mb), int(shuf),
-                                         float(neg), seed + d["k"],
-                                         self.device.type == "cuda")  # pinned: async H2D
+            if self._device_text(fmt, d["file"], shuf, neg):
+                it = _TextIter(self.host.TextBatches(d["file"], d["k"], d["n"], int(mb), True),
+                               fmt == "criteo")
+            else:
+                it = self.host.MinibatchIter(d["file"], d["k"], d["n"], fmt, int(mb), int(shuf),
+                                             float(neg), seed + d["k"],
+                                             self.device.type == "cuda")  # pinned: async H2D
             queue.append((d, it))
 
         def next_parsed():
@@ -240,6 +298,7 @@ class Worker:
         # every rank decides in lockstep whether a next minibatch is begun.
         ahead = train
         fetch()
+        dev_next = None
         batch = next_parsed()
         nxt = next_parsed() if (ahead and batch is not None) else None
         while True:
@@ -256,10 +315,15 @@ class Worker:
             else:
                 next_all = have_next
             with trace.stage("h2d"):
-                args = self._to_dev(batch) if batch is not None else self._empty_batch()
+                # the look-ahead batch went to the device last step
+                if dev_next is not None:
+                    args = dev_next
+                else:
+                    args = self._to_dev(batch) if batch is not None else self._empty_batch()
                 nargs = None
                 if ahead and next_all:
                     nargs = self._to_dev(nxt) if nxt is not None else self._empty_batch()
+                dev_next = nargs if nxt is not None else None
             if self.fault and batch is not None:
                 self._inject_fault()
             with trace.stage("process"):
