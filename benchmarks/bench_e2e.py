@@ -67,6 +67,8 @@ def main():
     ap.add_argument("--format", default="criteo", choices=["criteo", "crb"])
     ap.add_argument("-n", type=int, default=1, help="workers (one GPU each)")
     ap.add_argument("--minibatch", type=int, default=100000)
+    ap.add_argument("--rand-shuffle", type=int, default=10,
+                    help="shuffle buffer in minibatches (the reference default is 10)")
     ap.add_argument("--dir", default=None)
     args = ap.parse_args()
     work = args.dir or tempfile.mkdtemp(prefix="wh_e2e_")
@@ -87,7 +89,8 @@ def main():
     conf = os.path.join(work, "job.conf")
     with open(conf, "w") as f:
         f.write('train_data = "%s"\ndata_format = "%s"\nminibatch = %d\nmax_data_pass = 1\n'
-                "print_sec = 1\n" % (pattern, args.format, args.minibatch))
+                "print_sec = 1\nrand_shuffle = %d\n" % (pattern, args.format, args.minibatch,
+                                                   args.rand_shuffle))
         if args.model == "linear":
             f.write("lambda_l1 = 4\nlr_eta = 0.1\n")
         else:
@@ -127,7 +130,9 @@ def main():
         "value": ttl / sec if sec > 0 else None, "unit": "examples/s",
         "examples": ttl, "train_sec": sec, "job_wall_sec": wall, "datagen_sec": gen_s,
         "reference_linear_published": 1.85e6,
-        "config": {"rows": args.rows, "files": args.files, "minibatch": args.minibatch},
+        "config": {"rows": args.rows, "files": args.files, "minibatch": args.minibatch,
+                   "rand_shuffle": args.rand_shuffle,
+                   "device_parse": os.environ.get("WH_DEVICE_PARSE", "1") != "0"},
     }))
 
 

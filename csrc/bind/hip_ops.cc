@@ -1595,12 +1595,12 @@ std::vector<Tensor> parse_criteo(const Tensor& text, int64_t nlines, bool train)
   auto s = cur_stream(text);
   auto o = text.options();
   const int64_t nb = text.numel();
-  const int64_t nt = wh::criteo_tiles(nb);
+  const int64_t nt = wh::text_tiles(nb);
   auto tile_cnt = torch::empty({std::max<int64_t>(nt, 1)}, o.dtype(torch::kInt32));
   auto tile_off = torch::empty({nt + 1}, o.dtype(torch::kInt64));
   auto stmp = torch::empty({wh::scan_tmp_elems(std::max<int64_t>(nt, 1))}, o.dtype(torch::kInt64));
   auto start = torch::empty({nlines + 1}, o.dtype(torch::kInt64));
-  wh::criteo_lines(ptr<uint8_t>(text), nb, ptr<int32_t>(tile_cnt), ptr<int64_t>(tile_off),
+  wh::text_lines(ptr<uint8_t>(text), nb, ptr<int32_t>(tile_cnt), ptr<int64_t>(tile_off),
                    ptr<int64_t>(stmp), ptr<int64_t>(start), s);
   auto padded = torch::empty({std::max<int64_t>(nlines * 39, 1)}, o.dtype(torch::kInt64));
   auto cnt = torch::empty({std::max<int64_t>(nlines, 1)}, o.dtype(torch::kInt32));
@@ -1617,6 +1617,69 @@ std::vector<Tensor> parse_criteo(const Tensor& text, int64_t nlines, bool train)
   wh::criteo_compact(reinterpret_cast<const uint64_t*>(padded.data_ptr()), ptr<int64_t>(off),
                      nlines, reinterpret_cast<uint64_t*>(keys.data_ptr()), s);
   return {keys, label, off};
+}
+
+// text: uint8 [nbytes] of nlines whole libsvm lines (device) -> (keys i64,
+// label f32, offset i64, value f32 or None when every value is 1, weight f32
+// or None when no line has one), as the host parser returns them
+py::tuple parse_libsvm(const Tensor& text, int64_t nlines) {
+  CHECK_IN(text, torch::kUInt8);
+  c10::DeviceGuard g(text.device());
+  auto s = cur_stream(text);
+  auto o = text.options();
+  const int64_t nb = text.numel();
+  const int64_t nt = wh::text_tiles(nb);
+  auto tile_cnt = torch::empty({std::max<int64_t>(nt, 1)}, o.dtype(torch::kInt32));
+  auto tile_off = torch::empty({nt + 1}, o.dtype(torch::kInt64));
+  auto stmp = torch::empty({wh::scan_tmp_elems(std::max<int64_t>(std::max(nt, nlines), 1))},
+                           o.dtype(torch::kInt64));
+  auto start = torch::empty({nlines + 1}, o.dtype(torch::kInt64));
+  wh::text_lines(ptr<uint8_t>(text), nb, ptr<int32_t>(tile_cnt), ptr<int64_t>(tile_off),
+                 ptr<int64_t>(stmp), ptr<int64_t>(start), s);
+  auto cnt = torch::empty({std::max<int64_t>(nlines, 1)}, o.dtype(torch::kInt32));
+  auto off = torch::zeros({nlines + 1}, o.dtype(torch::kInt64));
+  wh::libsvm_count(ptr<uint8_t>(text), nb, ptr<int64_t>(start), nlines, ptr<int32_t>(cnt), s);
+  if (nlines > 0) wh::scan_i32(ptr<int32_t>(cnt), ptr<int64_t>(off), nlines, ptr<int64_t>(stmp), s);
+  const int64_t nnz = off[nlines].item<int64_t>();
+  auto keys = torch::empty({nnz}, o.dtype(torch::kInt64));
+  auto val = torch::empty({nnz}, o.dtype(torch::kFloat32));
+  auto label = torch::empty({nlines}, o.dtype(torch::kFloat32));
+  auto weight = torch::empty({nlines}, o.dtype(torch::kFloat32));
+  auto flags = torch::zeros({2}, o.dtype(torch::kInt32));
+  wh::libsvm_fill(ptr<uint8_t>(text), nb, ptr<int64_t>(start), nlines, ptr<int64_t>(off),
+                  reinterpret_cast<uint64_t*>(keys.data_ptr()), ptr<float>(val), ptr<float>(label),
+                  ptr<float>(weight), ptr<int32_t>(flags), s);
+  auto f = flags.cpu();
+  const int32_t* fp = f.data_ptr<int32_t>();
+  return py::make_tuple(keys, label, off, fp[0] ? py::cast(val) : py::none(),
+                        fp[1] ? py::cast(weight) : py::none());
+}
+
+// rows `sel` of a CSR block (keys, off, val?, label) -> (keys, val?, label)
+// of the gathered block whose offsets `noff` [nsel + 1] hold nnz at the end
+py::tuple csr_gather(const Tensor& keys, const Tensor& off, const c10::optional<Tensor>& val,
+                     const Tensor& label, const Tensor& sel, const Tensor& noff, int64_t nnz) {
+  CHECK_IN(keys, torch::kInt64);
+  CHECK_IN(off, torch::kInt64);
+  CHECK_IN(label, torch::kFloat32);
+  CHECK_IN(sel, torch::kInt64);
+  CHECK_IN(noff, torch::kInt64);
+  TORCH_CHECK(noff.numel() == sel.numel() + 1 && label.numel() + 1 == off.numel());
+  if (val) {
+    CHECK_IN((*val), torch::kFloat32);
+    TORCH_CHECK(val->numel() == keys.numel());
+  }
+  c10::DeviceGuard g(keys.device());
+  auto s = cur_stream(keys);
+  auto okeys = torch::empty({nnz}, keys.options());
+  auto olabel = torch::empty({sel.numel()}, label.options());
+  Tensor oval;
+  if (val) oval = torch::empty({nnz}, val->options());
+  wh::csr_gather(ptr<int64_t>(off), reinterpret_cast<const uint64_t*>(keys.data_ptr()),
+                 val ? ptr<float>(*val) : nullptr, ptr<float>(label), ptr<int64_t>(sel),
+                 sel.numel(), ptr<int64_t>(noff), reinterpret_cast<uint64_t*>(okeys.data_ptr()),
+                 val ? ptr<float>(oval) : nullptr, ptr<float>(olabel), s);
+  return py::make_tuple(okeys, val ? py::cast(oval) : py::none(), olabel);
 }
 
 // ------------------------------------------------------------ gbdt grower
@@ -1974,6 +2037,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
   m.def("gbdt_grow", &gbdt_grow);
   m.def("parse_criteo", &parse_criteo);
+  m.def("parse_libsvm", &parse_libsvm);
+  m.def("csr_gather", &csr_gather);
   m.def("gbdt_bin_csr", &gbdt_bin_csr);
   m.def("gbdt_hist_csr", &gbdt_hist_csr);
   m.def("gbdt_split_csr", &gbdt_split_csr);

@@ -1,4 +1,4 @@
-// Device-side Criteo text ingest (K1 in SURVEY §2.5): raw bytes of whole
+// Device-side text ingest (Criteo, libsvm) (K1 in SURVEY §2.5): raw bytes of whole
 // lines are copied to the GPU and tokenized there, every field hashed with
 // CityHash64 exactly as the host parser does (csrc/host/parsers.cc
 // ParseCriteo, reference learn/base/criteo_parser.h:64-86):
@@ -13,6 +13,9 @@
 //                            ballot; lane f then hashes field f
 //   k_criteo_compact       : the per-line keys packed into the CSR minibatch
 //                            (row offsets = scan of the per-line counts)
+//   k_libsvm_count / _fill : libsvm lines, one wave per line: token starts by
+//                            ballot, the lane at a token start parses it
+//                            (index exactly, value strtof-compatible)
 // The host only splits the file into whole-line batches (memchr) and copies
 // them into pinned memory.
 #include "wh_common.h"
@@ -316,9 +319,205 @@ __global__ __launch_bounds__(256) void k_criteo_compact(const uint64_t* __restri
   if (lane < c) keys[o + lane] = padded[line * kCriteoFields + lane];
 }
 
+
+// ---- libsvm ----------------------------------------------------------------
+// label[:weight] idx[:value] ... separated by blanks; the host parser is
+// csrc/host/parsers.cc ParseLibSVM (dmlc LibSVMParser semantics). Numbers are
+// converted as strtoull / strtof do: integers exactly; decimals correctly
+// rounded when the significand has <= 7 digits and |exponent| <= 10 (one
+// exact float operation, Clinger's fast path) -- every value the usual
+// libsvm writers print -- and via one correctly rounded double otherwise
+// (which can differ from strtof in the last bit only at a double-rounding
+// tie, probability ~2^-29 per value).
+__device__ __forceinline__ bool is_blank(uint8_t c) { return c == ' ' || c == '\t'; }
+__device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
+
+__device__ const uint8_t* parse_u64(const uint8_t* s, const uint8_t* e, uint64_t* v) {
+  uint64_t m = 0;
+  while (s < e && is_digit(*s)) m = m * 10 + (*s++ - '0');
+  *v = m;
+  return s;
+}
+
+__device__ const uint8_t* parse_f32(const uint8_t* s, const uint8_t* e, float* out) {
+  const uint8_t* s0 = s;
+  bool neg = false;
+  if (s < e && (*s == '-' || *s == '+')) neg = *s++ == '-';
+  uint64_t m = 0;
+  int nd = 0, e10 = 0;
+  bool any = false, trunc = false;
+  for (; s < e && is_digit(*s); ++s) {
+    const int d = *s - '0';
+    any = true;
+    if (m == 0 && d == 0) continue;
+    if (nd < 19) m = m * 10 + d, ++nd;
+    else ++e10, trunc |= d != 0;
+  }
+  if (s < e && *s == '.') {
+    for (++s; s < e && is_digit(*s); ++s) {
+      const int d = *s - '0';
+      any = true;
+      if (m == 0 && d == 0) {
+        --e10;
+        continue;
+      }
+      if (nd < 19) m = m * 10 + d, ++nd, --e10;
+      else trunc |= d != 0;
+    }
+  }
+  if (!any) {
+    *out = 0.f;
+    return s0;
+  }
+  if (s < e && (*s == 'e' || *s == 'E')) {
+    const uint8_t* q = s + 1;
+    bool eneg = false;
+    if (q < e && (*q == '-' || *q == '+')) eneg = *q++ == '-';
+    if (q < e && is_digit(*q)) {
+      int x = 0;
+      for (; q < e && is_digit(*q); ++q) x = x < 100000 ? x * 10 + (*q - '0') : x;
+      e10 += eneg ? -x : x;
+      s = q;
+    }
+  }
+  float f;
+  if (m == 0) {
+    f = 0.f;
+  } else if (!trunc && m < (1ull << 24) && e10 >= -10 && e10 <= 10) {
+    const float p10[11] = {1e0f, 1e1f, 1e2f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+    f = e10 >= 0 ? (float)m * p10[e10] : (float)m / p10[-e10];
+  } else {
+    double d = (double)m;
+    int x = e10;
+    if (x > 400) x = 400;
+    if (x < -400) x = -400;
+    while (x > 22) d *= 1e22, x -= 22;
+    while (x < -22) d /= 1e22, x += 22;
+    const double p22[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                            1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    d = x >= 0 ? d * p22[x] : d / p22[-x];
+    f = (float)d;
+  }
+  *out = neg ? -f : f;
+  return s;
+}
+
+// the content of line `line`: [b, e) without leading newlines and trailing
+// carriage returns
+__device__ __forceinline__ void line_span(const uint8_t* t, int64_t n, const int64_t* start,
+                                          int64_t line, int64_t& b, int64_t& e) {
+  b = start[line];
+  e = start[line + 1] - 1;
+  if (e > n) e = n;
+  while (b < e && (t[b] == '\n' || t[b] == '\r')) ++b;
+  while (e > b && t[e - 1] == '\r') --e;
+}
+
+// token starts of a 64-byte window: a non-blank byte after a blank (the byte
+// before the line counts as blank); `prev` carries the last byte's blankness
+__device__ __forceinline__ uint64_t token_starts(const uint8_t* t, int64_t b, int64_t len,
+                                                 int64_t w0, int lane, uint64_t& prev) {
+  const int64_t i = w0 + lane;
+  const bool blank = i >= len || is_blank(t[b + i]);
+  const uint64_t bm = __ballot(blank);
+  const uint64_t st = ~bm & ((bm << 1) | prev);
+  prev = bm >> 63;
+  return st;
+}
+
+__global__ __launch_bounds__(256) void k_libsvm_count(const uint8_t* __restrict__ t, int64_t n,
+                                                      const int64_t* __restrict__ start,
+                                                      int64_t nlines, int32_t* __restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t line = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (line >= nlines) return;
+  int64_t b, e;
+  line_span(t, n, start, line, b, e);
+  const int64_t len = e - b;
+  uint64_t prev = 1;
+  int ntok = 0;
+  for (int64_t w0 = 0; w0 < len; w0 += 64) ntok += __popcll(token_starts(t, b, len, w0, lane, prev));
+  if (lane == 0) cnt[line] = ntok > 0 ? ntok - 1 : 0;
+}
+
+// flags[0] = 1 if any value != 1, flags[1] = 1 if any line has a weight
+__global__ __launch_bounds__(256) void k_libsvm_fill(
+    const uint8_t* __restrict__ t, int64_t n, const int64_t* __restrict__ start, int64_t nlines,
+    const int64_t* __restrict__ off, uint64_t* __restrict__ keys, float* __restrict__ val,
+    float* __restrict__ label, float* __restrict__ weight, int32_t* __restrict__ flags) {
+  const int lane = threadIdx.x & 63;
+  const int64_t line = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (line >= nlines) return;
+  int64_t b, e;
+  line_span(t, n, start, line, b, e);
+  const int64_t len = e - b;
+  const uint8_t* le = t + e;
+  const int64_t o = off[line];
+  uint64_t prev = 1;
+  int tok = 0;
+  bool anyv = false, anyw = false;
+  for (int64_t w0 = 0; w0 < len; w0 += 64) {
+    const uint64_t st = token_starts(t, b, len, w0, lane, prev);
+    if ((st >> lane) & 1) {
+      const int k = tok + __popcll(st & ((1ull << lane) - 1ull));
+      const uint8_t* p = t + b + w0 + lane;
+      if (k == 0) {  // the label lane
+        float lab = 0.f, w = 1.f;
+        p = parse_f32(p, le, &lab);
+        if (p < le && *p == ':') {
+          parse_f32(p + 1, le, &w);
+          anyw = true;
+        }
+        label[line] = lab;
+        weight[line] = w;
+      } else {
+        uint64_t idx;
+        p = parse_u64(p, le, &idx);
+        float v = 1.f;
+        if (p < le && *p == ':') parse_f32(p + 1, le, &v);
+        keys[o + k - 1] = idx;
+        val[o + k - 1] = v;
+        anyv |= v != 1.f;
+      }
+    }
+    tok += __popcll(st);
+  }
+  const uint64_t vm = __ballot(anyv), wm = __ballot(anyw);
+  if (vm && lane == 0) flags[0] = 1;
+  if (wm && lane == 0) flags[1] = 1;
+  if (tok == 0 && lane == 0) label[line] = 0.f, weight[line] = 1.f;  // a blank line
+}
+
+// rows sel[i] of a CSR block -> row i of a new CSR block (noff: its offsets);
+// one wave per row, the device half of the shuffle buffer
+__global__ __launch_bounds__(256) void k_csr_gather(
+    const int64_t* __restrict__ off, const uint64_t* __restrict__ keys,
+    const float* __restrict__ val, const float* __restrict__ label,
+    const int64_t* __restrict__ sel, int64_t nsel, const int64_t* __restrict__ noff,
+    uint64_t* __restrict__ okeys, float* __restrict__ oval, float* __restrict__ olabel) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (i >= nsel) return;
+  const int64_t r = sel[i];
+  const int64_t a = off[r], c = off[r + 1] - a, o = noff[i];
+  for (int64_t j = lane; j < c; j += 64) {
+    okeys[o + j] = keys[a + j];
+    if (val) oval[o + j] = val[a + j];
+  }
+  if (lane == 0) olabel[i] = label[r];
+}
+
 }  // namespace
 
-int64_t criteo_lines(const uint8_t* text, int64_t nbytes, int32_t* tile_cnt, int64_t* tile_off,
+void csr_gather(const int64_t* off, const uint64_t* keys, const float* val, const float* label,
+                const int64_t* sel, int64_t nsel, const int64_t* noff, uint64_t* okeys,
+                float* oval, float* olabel, hipStream_t s) {
+  if (nsel <= 0) return;
+  hipLaunchKernelGGL(k_csr_gather, dim3((unsigned)((nsel + 3) / 4)), dim3(256), 0, s, off, keys,
+                     val, label, sel, nsel, noff, okeys, oval, olabel);
+}
+
+int64_t text_lines(const uint8_t* text, int64_t nbytes, int32_t* tile_cnt, int64_t* tile_off,
                      int64_t* scan_tmp, int64_t* start, hipStream_t s) {
   const int64_t ntile = (nbytes + kNlTile - 1) / kNlTile;
   if (ntile <= 0) return 0;
@@ -329,13 +528,29 @@ int64_t criteo_lines(const uint8_t* text, int64_t nbytes, int32_t* tile_cnt, int
   return ntile;
 }
 
-int64_t criteo_tiles(int64_t nbytes) { return (nbytes + kNlTile - 1) / kNlTile; }
+int64_t text_tiles(int64_t nbytes) { return (nbytes + kNlTile - 1) / kNlTile; }
 
 void criteo_fields(const uint8_t* text, int64_t nbytes, const int64_t* start, int64_t nlines,
                    bool train, uint64_t* padded, int32_t* cnt, float* label, hipStream_t s) {
   if (nlines <= 0) return;
   hipLaunchKernelGGL(k_criteo_fields, dim3((unsigned)((nlines + 3) / 4)), dim3(256), 0, s, text,
                      nbytes, start, nlines, train ? 1 : 0, padded, cnt, label);
+}
+
+int64_t libsvm_count(const uint8_t* text, int64_t nbytes, const int64_t* start, int64_t nlines,
+                     int32_t* cnt, hipStream_t s) {
+  if (nlines <= 0) return 0;
+  hipLaunchKernelGGL(k_libsvm_count, dim3((unsigned)((nlines + 3) / 4)), dim3(256), 0, s, text,
+                     nbytes, start, nlines, cnt);
+  return nlines;
+}
+
+void libsvm_fill(const uint8_t* text, int64_t nbytes, const int64_t* start, int64_t nlines,
+                 const int64_t* off, uint64_t* keys, float* val, float* label, float* weight,
+                 int32_t* flags, hipStream_t s) {
+  if (nlines <= 0) return;
+  hipLaunchKernelGGL(k_libsvm_fill, dim3((unsigned)((nlines + 3) / 4)), dim3(256), 0, s, text,
+                     nbytes, start, nlines, off, keys, val, label, weight, flags);
 }
 
 void criteo_compact(const uint64_t* padded, const int64_t* off, int64_t nlines, uint64_t* keys,

@@ -450,19 +450,31 @@ void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const f
                   const float* leaf, float* margin, hipStream_t s);
 
 // ------------------------------------------------------------- ingest.hip
-// Criteo text -> CSR minibatch on the device (keys bit-identical to the host
-// parser's CityHash64 keys). criteo_lines: start [nlines + 1] of the lines of
+// Criteo / libsvm text -> CSR minibatch on the device (keys bit-identical to
+// the host parsers'). text_lines: start [nlines + 1] of the lines of
 // `text` (tile_cnt [criteo_tiles], tile_off [criteo_tiles + 1], scan_tmp
-// [scan_tmp_elems(criteo_tiles)]); criteo_fields: padded [nlines x 39] keys +
+// [scan_tmp_elems(text_tiles)]); criteo_fields: padded [nlines x 39] keys +
 // per-line counts + labels; criteo_compact: keys [sum counts] from the
 // scanned counts.
-int64_t criteo_tiles(int64_t nbytes);
-int64_t criteo_lines(const uint8_t* text, int64_t nbytes, int32_t* tile_cnt, int64_t* tile_off,
+int64_t text_tiles(int64_t nbytes);
+int64_t text_lines(const uint8_t* text, int64_t nbytes, int32_t* tile_cnt, int64_t* tile_off,
                      int64_t* scan_tmp, int64_t* start, hipStream_t s);
 void criteo_fields(const uint8_t* text, int64_t nbytes, const int64_t* start, int64_t nlines,
                    bool train, uint64_t* padded, int32_t* cnt, float* label, hipStream_t s);
 void criteo_compact(const uint64_t* padded, const int64_t* off, int64_t nlines, uint64_t* keys,
                     hipStream_t s);
+// rows sel [nsel] of a CSR block gathered into a new block with offsets noff
+// [nsel + 1] (val may be null)
+void csr_gather(const int64_t* off, const uint64_t* keys, const float* val, const float* label,
+                const int64_t* sel, int64_t nsel, const int64_t* noff, uint64_t* okeys,
+                float* oval, float* olabel, hipStream_t s);
+// libsvm: cnt [nlines] features per line; then keys/val [sum cnt], label,
+// weight [nlines], flags [2] (zeroed by the caller: any value != 1, any weight)
+int64_t libsvm_count(const uint8_t* text, int64_t nbytes, const int64_t* start, int64_t nlines,
+                     int32_t* cnt, hipStream_t s);
+void libsvm_fill(const uint8_t* text, int64_t nbytes, const int64_t* start, int64_t nlines,
+                 const int64_t* off, uint64_t* keys, float* val, float* label, float* weight,
+                 int32_t* flags, hipStream_t s);
 
 // -------------------------------------------------------------- quant.hip
 // fixed_bytes payload filter: rows of w floats <-> packed records of

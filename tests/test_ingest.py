@@ -101,7 +101,8 @@ def test_ps_worker_device_parse_trains_like_host_parse(tmp_path):
     for dp in ("1", "0"):
         conf = tmp_path / ("c%s.conf" % dp)
         conf.write_text('train_data = "%s"\ndata_format = "criteo"\nmax_data_pass = 1\n'
-                        'minibatch = 1000\nmodel_out = "%s/m%s"\n' % (p, tmp_path, dp))
+                        'minibatch = 1000\nrand_shuffle = 0\nmodel_out = "%s/m%s"\n'
+                        % (p, tmp_path, dp))
         env = dict(os.environ, WH_DEVICE_PARSE=dp)
         r = subprocess.run([sys.executable, os.path.join(root, "tracker", "dmlc_local.py"), "-n",
                             "1", "-s", "1", os.path.join(root, "bin", "linear.dmlc"), str(conf)],
@@ -113,3 +114,85 @@ def test_ps_worker_device_parse_trains_like_host_parse(tmp_path):
     a, b = models
     assert len(a) > 1000 and np.array_equal(a["k"], b["k"])
     np.testing.assert_allclose(a["w"], b["w"], rtol=1e-4, atol=1e-6)
+
+
+def _libsvm_text(nlines, seed, values=True, weights=True):
+    rng = random.Random(seed)
+    fmts = [lambda: "%d" % rng.randrange(0, 100), lambda: "%.6g" % rng.uniform(-1e3, 1e3),
+            lambda: "%.3e" % rng.uniform(-1, 1), lambda: "%.9f" % rng.random(),
+            lambda: "%.17g" % rng.lognormvariate(0, 20), lambda: "0.%s" % ("0" * rng.randrange(12)
+                                                                         + "37")]
+    out = []
+    for i in range(nlines):
+        lab = rng.choice(["1", "-1", "+1", "0", "0.5"])
+        if weights and i % 5 == 2:
+            lab += ":%g" % rng.uniform(0.1, 3)
+        toks = [lab]
+        for _ in range(rng.randrange(0, 150 if i % 9 == 0 else 12)):
+            idx = str(rng.randrange(0, 1 << rng.choice([8, 20, 40])))
+            if values and rng.random() < 0.7:
+                idx += ":" + rng.choice(fmts)()
+            toks.append(idx)
+        sep = "\t" if i % 4 == 1 else " "
+        out.append(sep.join(toks) + (" \r\n" if i % 6 == 3 else "\n"))
+    return "".join(out).encode()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("values,weights", [(True, True), (False, False)])
+def test_device_libsvm_parse_matches_host_parser(tmp_path, values, weights):
+    host = _native.host()
+    hip = _native.hip()
+    data = _libsvm_text(3000, 4, values, weights)
+    keys_h, off_h, val_h, lab_h, w_h = host.parse_text(data, "libsvm")
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    keys, lab, off, val, w = hip.parse_libsvm(t.cuda(), 3000)
+    assert torch.equal(off.cpu(), off_h)
+    assert torch.equal(keys.cpu(), keys_h)
+    assert torch.equal(lab.cpu(), lab_h)
+    assert (val is None) == (val_h is None) and (w is None) == (w_h is None)
+    if val is not None:
+        bad = (val.cpu() != val_h).nonzero()
+        assert bad.numel() == 0, (bad[:5], val.cpu()[bad[:5]], val_h[bad[:5]])
+    if w is not None:
+        assert torch.equal(w.cpu(), w_h)
+
+
+@pytest.mark.gpu
+def test_device_shuffle_buffer_is_a_permutation_and_neg_sampling_drops_negatives(tmp_path):
+    """rand_shuffle on the device: every row of the part exactly once,
+    minibatches of exactly `mb` rows (spanning shuffle blocks), a different
+    order than the file; neg_sampling keeps ~that share of the negatives."""
+    from wormhole_amd.data.device_text import DeviceTextIter
+    host = _native.host()
+    dev = torch.device("cuda")
+    data = _criteo_text(5000, 5)
+    p = tmp_path / "d.txt"
+    p.write_bytes(data)
+    keys_h, off_h, _, lab_h, _ = host.parse_text(data, "criteo")
+    rows_h = [tuple(keys_h[off_h[i]:off_h[i + 1]].tolist()) + (float(lab_h[i]),)
+              for i in range(5000)]
+    it = DeviceTextIter(host, str(p), 0, 1, "criteo", 300, 300 * 4, 1.0, 7, dev)
+    rows, sizes = [], []
+    while True:
+        b = it.next()
+        if b is None:
+            break
+        keys, off, val, lab = [x.cpu() if x is not None else None for x in b.to_main(dev)]
+        assert val is None
+        sizes.append(lab.numel())
+        rows += [tuple(keys[off[i]:off[i + 1]].tolist()) + (float(lab[i]),)
+                 for i in range(lab.numel())]
+    assert sorted(rows) == sorted(rows_h) and rows != rows_h
+    assert sizes[:-1] == [300] * (len(sizes) - 1)
+    it = DeviceTextIter(host, str(p), 0, 1, "criteo", 300, 0, 0.25, 7, dev)
+    labs = []
+    while True:
+        b = it.next()
+        if b is None:
+            break
+        labs.append(b.to_main(dev)[3].cpu())
+    labs = torch.cat(labs)
+    npos, nneg = int((lab_h > 0).sum()), int((lab_h <= 0).sum())
+    assert int((labs > 0).sum()) == npos
+    assert abs(int((labs <= 0).sum()) - 0.25 * nneg) < 0.05 * nneg

@@ -33,6 +33,7 @@ from .. import _native
 from ..kv import checkpoint
 from ..utils.fs import open_uri  # noqa: E402
 from ..utils import trace  # noqa: E402
+from ..data import device_text
 
 TRAIN, VAL, PRED = 0, 1, 2
 _TYPE_NAME = {TRAIN: "training", VAL: "validation", PRED: "prediction"}
@@ -61,48 +62,6 @@ def _parse_fault(spec, rank):
     if kind == "kill" and int(os.environ.get("WH_RESTART_ATTEMPT", "0") or 0) > 0:
         return None  # the injected failure happens once; the restarted job runs clean
     return kind, float(arg)
-
-
-class _TextBatch:
-    """Whole lines of Criteo text (pinned host bytes) parsed on the device."""
-
-    __slots__ = ("text", "lines", "train")
-
-    def __init__(self, text, lines, train):
-        self.text, self.lines, self.train = text, lines, train
-
-    def parse(self, dev):
-        """H2D + tokenize + hash on a side stream (its one host read, the key
-        count, then waits for this batch only, not for the training step in
-        flight); the main stream waits for the result."""
-        main = torch.cuda.current_stream(dev)
-        side = _parse_stream(dev)
-        with torch.cuda.stream(side):
-            t = self.text.to(dev, non_blocking=True)
-            keys, label, off = _native.hip().parse_criteo(t, int(self.lines), self.train)
-        main.wait_stream(side)
-        for x in (keys, label, off):
-            x.record_stream(main)
-        return keys, off, None, label
-
-
-_PARSE_STREAMS = {}
-
-
-def _parse_stream(dev):
-    s = _PARSE_STREAMS.get(dev)
-    if s is None:
-        s = _PARSE_STREAMS[dev] = torch.cuda.Stream(dev)
-    return s
-
-
-class _TextIter:
-    def __init__(self, tb, train):
-        self.tb, self.train = tb, train
-
-    def next(self):
-        b = self.tb.next()
-        return None if b is None else _TextBatch(b[0], b[1], self.train)
 
 
 # --------------------------------------------------------------------------
@@ -197,19 +156,9 @@ class Worker:
                 torch.zeros(1, dtype=torch.int64, device=dev), None,
                 torch.zeros(0, dtype=torch.float32, device=dev))
 
-    def _device_text(self, fmt, path, shuf, neg):
-        """Criteo text is split into whole-line batches on the host and
-        tokenized + hashed on the GPU (csrc/hip/ingest.hip) when nothing
-        needs the rows on the host: plain files, no shuffle, no negative
-        sampling. WH_DEVICE_PARSE=0 keeps the host parser."""
-        return (fmt in ("criteo", "criteo_test") and self.device.type == "cuda" and shuf == 0
-                and neg >= 1.0 and os.environ.get("WH_DEVICE_PARSE", "1") != "0"
-                and not path.endswith((".gz", ".crb", ".rec")) and "://" not in path.replace(
-                    "file://", ""))
-
     def _to_dev(self, b):
-        if isinstance(b, _TextBatch):
-            return b.parse(self.device)
+        if isinstance(b, device_text.DeviceBatch):
+            return b.to_main(self.device)
         keys, off, val, label, _w = b
         dev = self.device
         nb = dev.type == "cuda"
@@ -236,6 +185,11 @@ class Worker:
         # minibatches in flight for the same reason). A finished workload is
         # reported by name, so the prefetched one stays assigned.
         queue = collections.deque()
+        # workloads in flight: the threaded host parser keeps 16 threads busy
+        # on one; device-parsed text only reads on the host (one thread per
+        # workload), so more workloads read ahead in parallel
+        dev_text = device_text.applies(fmt, "", self.device)
+        prefetch = int(os.environ.get("WH_PREFETCH_PARTS", "4" if dev_text else "2"))
         exhausted = False
         done_prev = None
         n_pass = n_ex = ex_last = 0
@@ -256,9 +210,9 @@ class Worker:
             if d.get("file") is None:
                 exhausted = True
                 return
-            if self._device_text(fmt, d["file"], shuf, neg):
-                it = _TextIter(self.host.TextBatches(d["file"], d["k"], d["n"], int(mb), True),
-                               fmt == "criteo")
+            if device_text.applies(fmt, d["file"], self.device):
+                it = device_text.DeviceTextIter(self.host, d["file"], d["k"], d["n"], fmt, int(mb),
+                                                int(shuf), float(neg), seed + d["k"], self.device)
             else:
                 it = self.host.MinibatchIter(d["file"], d["k"], d["n"], fmt, int(mb), int(shuf),
                                              float(neg), seed + d["k"],
@@ -280,8 +234,8 @@ class Worker:
                             pred_f.close()
                         pred_f = open_uri(name, "w")
                         pred_name = name
-                if len(queue) == 1:
-                    fetch()  # the next workload starts parsing now
+                if len(queue) < prefetch:
+                    fetch()  # the next workload starts reading / parsing now
                 with trace.stage("parse"):
                     batch = it.next()
                 if batch is None:
