@@ -17,20 +17,21 @@
 namespace wh {
 namespace {
 
-// One thread per (row, field): a block owns kRowsPerBlock whole rows, so the
-// key stores are contiguous across the block and each row's label is summed
-// from LDS (was: one thread per row, 39 serial fields, 312-byte-strided
-// stores).
+// A block owns kSynthRows whole rows; its threads stride over the rows'
+// (row, field) elements, so key stores are contiguous and each row's label is
+// summed from LDS. Rows per block are many enough that a thread has ~10
+// independent elements in flight (one element per thread and 6 rows per block
+// made the kernel a latency chain of 16k tiny blocks: 108 us per 100k rows).
 constexpr int kSynthThreads = 256;
+constexpr int kSynthRows = 64;
 constexpr int kMaxField = 64;
 
 __global__ __launch_bounds__(kSynthThreads) void k_synth_criteo(int64_t nrows, uint64_t seed,
                                                                 uint64_t step,
                                                                 const int64_t* card, int nfield,
-                                                                int rows_per_block,
                                                                 uint64_t* keys, float* label,
                                                                 int64_t* offset) {
-  __shared__ float th[kSynthThreads];
+  __shared__ float th[kSynthRows * kMaxField];
   __shared__ double lc[kMaxField];
   __shared__ int64_t cd[kMaxField];
   for (int f = threadIdx.x; f < nfield; f += kSynthThreads) {
@@ -38,34 +39,31 @@ __global__ __launch_bounds__(kSynthThreads) void k_synth_criteo(int64_t nrows, u
     lc[f] = log((double)cd[f]);
   }
   __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  const int lr = threadIdx.x / nfield, f = threadIdx.x % nfield;
-  const int64_t r = r0 + lr;
-  float t = 0.f;
-  if (lr < rows_per_block && r < nrows) {
+  const int64_t r0 = (int64_t)blockIdx.x * kSynthRows;
+  const int64_t nr = nrows - r0 < kSynthRows ? nrows - r0 : kSynthRows;
+  const int ne = (int)nr * nfield;
+  for (int e = threadIdx.x; e < ne; e += kSynthThreads) {
+    const int lr = e / nfield, f = e - lr * nfield;
+    const int64_t r = r0 + lr;
     const uint64_t gid = step * (uint64_t)nrows + (uint64_t)r;
     const float u = uhash01(seed, gid, (uint64_t)f);
     int64_t rank = (int64_t)exp(lc[f] * (double)u) - 1;
     if (rank < 0) rank = 0;
     if (rank >= cd[f]) rank = cd[f] - 1;
     const uint64_t tok = mix64(((uint64_t)f << 40) ^ (uint64_t)rank ^ 0x5bd1e995ull);
-    keys[r * nfield + f] = (tok >> 10) | ((uint64_t)f << 54);
+    keys[r0 * nfield + e] = (tok >> 10) | ((uint64_t)f << 54);
     // hidden weight of this (field, value); head values carry most signal
-    t = (uhash01(0x7e57ull, (uint64_t)f, (uint64_t)rank) - 0.5f) * 0.9f;
+    th[e] = (uhash01(0x7e57ull, (uint64_t)f, (uint64_t)rank) - 0.5f) * 0.9f;
   }
-  th[threadIdx.x] = t;
   __syncthreads();
-  if (threadIdx.x < rows_per_block) {
+  if (threadIdx.x < nr) {
     const int64_t rr = r0 + threadIdx.x;
-    if (rr < nrows) {
-      float logit = -1.2f;
-      for (int q = 0; q < nfield; ++q) logit += th[threadIdx.x * nfield + q];
-      const float p = 1.f / (1.f + __expf(-logit));
-      const uint64_t gid = step * (uint64_t)nrows + (uint64_t)rr;
-      label[rr] = uhash01(seed ^ 0xabcdefull, gid, 977) < p ? 1.f : 0.f;
-      offset[rr] = rr * nfield;
-    }
-    if (rr == nrows) offset[rr] = rr * nfield;
+    float logit = -1.2f;
+    for (int q = 0; q < nfield; ++q) logit += th[threadIdx.x * nfield + q];
+    const float p = 1.f / (1.f + __expf(-logit));
+    const uint64_t gid = step * (uint64_t)nrows + (uint64_t)rr;
+    label[rr] = uhash01(seed ^ 0xabcdefull, gid, 977) < p ? 1.f : 0.f;
+    offset[rr] = rr * nfield;
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) offset[nrows] = nrows * (int64_t)nfield;
 }
@@ -78,10 +76,9 @@ void synth_criteo(int64_t nrows, uint64_t seed, uint64_t step, const int64_t* ca
     fprintf(stderr, "synth_criteo: nfield must be in [1, %d]\n", kMaxField);
     abort();
   }
-  const int rpb = kSynthThreads / nfield;
-  const int64_t nb = (nrows + rpb - 1) / rpb;
+  const int64_t nb = (nrows + kSynthRows - 1) / kSynthRows;
   hipLaunchKernelGGL(k_synth_criteo, dim3((unsigned)(nb > 0 ? nb : 1)), dim3(kSynthThreads), 0, s,
-                     nrows, seed, step, card, nfield, rpb, keys, label, offset);
+                     nrows, seed, step, card, nfield, keys, label, offset);
 }
 
 }  // namespace wh
