@@ -16,6 +16,9 @@
 //     the reference's strict '>' scan order).
 // Accumulation: one wave per row adds the row into its cluster's sum with
 // 256-byte-contiguous float atomics (the chip-wide atomic rate shape).
+#include <algorithm>
+#include <cstdlib>
+
 #include "wh_common.h"
 #include "wh_kernels.h"
 
@@ -610,10 +613,21 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __rest
   constexpr int PER = CF / kX3Threads;    // 16-byte DMA pieces per thread per chunk
   static_assert(PER * kX3Threads == CF, "chunk must split evenly");
   __shared__ uint4 lds[SLOTS * CF];
+  __shared__ uint4 pf_sink[kX3Threads];  // L2-prefetch DMA target, never read
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t ntiles = (n + 31) / 32;
-  const int64_t tile = (int64_t)blockIdx.x * kX3Waves + wid;
-  const bool live = tile < ntiles;
+  const int64_t ngroups = (ntiles + kX3Waves - 1) / kX3Waves;
+  // persistent: the workgroup walks row groups blockIdx.x, + gridDim.x, ...;
+  // the C ring runs over the global chunk sequence q (chunk q % nchunk), so it
+  // never drains between groups. The next group's A fragments are pulled into
+  // L2 during the current group's last chunk (LDS-DMA into a scratch slot: no
+  // registers held; VGPRs are at 222 of 256) and loaded into the A registers
+  // right after the last chunk's MFMAs, under the top-2 epilogue (a fresh
+  // workgroup per group left the matrix pipe idle for an HBM round trip and
+  // the DMA prologue of every group)
+  const int64_t mygroups =
+      blockIdx.x < ngroups ? (ngroups - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int64_t total = mygroups * nchunk;
   auto stage = [&](int slot, int c) {
     const uint4* src = Cp + (int64_t)c * CF;
     uint4* dst = lds + slot * CF;
@@ -623,24 +637,33 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __rest
           src + i * kX3Threads + threadIdx.x,
           (__attribute__((address_space(3))) void*)(dst + i * kX3Threads + wid * 64), 16, 0, 0);
   };
-  bf16x8 ah[KS], al[KS];
+  auto load_a = [&](int64_t g, bf16x8 (&h)[KS], bf16x8 (&l)[KS]) {
+    const int64_t t = g * kX3Waves + wid;
+    const bool lv = g < ngroups && t < ntiles;
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int64_t b = (tile * KS + s) * 2 * 64 + lane;
-    ah[s] = as_bf16x8(live ? Xp[b] : make_uint4(0, 0, 0, 0));
-    al[s] = as_bf16x8(live ? Xp[b + 64] : make_uint4(0, 0, 0, 0));
-  }
+    for (int s = 0; s < KS; ++s) {
+      const int64_t b = (t * KS + s) * 2 * 64 + lane;
+      h[s] = as_bf16x8(lv ? Xp[b] : make_uint4(0, 0, 0, 0));
+      l[s] = as_bf16x8(lv ? Xp[b + 64] : make_uint4(0, 0, 0, 0));
+    }
+  };
+  auto prefetch_a = [&](int64_t g) {
+    const int64_t t = g * kX3Waves + wid;
+    if (g >= ngroups || t >= ntiles) return;
+#pragma unroll
+    for (int i = 0; i < 2 * KS; ++i)
+      __builtin_amdgcn_global_load_lds(
+          Xp + t * KS * 2 * 64 + i * 64 + lane,
+          (__attribute__((address_space(3))) void*)(pf_sink + wid * 64), 16, 0, 0);
+  };
+  bf16x8 ah[KS], al[KS];
+  int64_t grp = blockIdx.x;
+  load_a(grp, ah, al);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A fragments before the DMA count
-  stage(0, 0);
-  if (SLOTS == 3 && nchunk > 1) stage(1, 1);
+  if (total > 0) stage(0, 0);
+  if (SLOTS == 3 && total > 1) stage(1, 1 % nchunk);
   float b1[16], b2[16];
   int i1[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    b1[r] = -INFINITY;
-    b2[r] = -INFINITY;
-    i1[r] = 0x7fffffff;
-  }
   // (padded centroid columns >= k start their accumulators at -1e30, so no
   // per-score bounds test is needed; 5 VALU per score)
   auto top2 = [&](const f32x16 (&sc)[NSUB], int cbase) {
@@ -657,85 +680,103 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __rest
       }
     }
   };
-  for (int c = 0; c < nchunk; ++c) {
-    // this wave's pieces of chunk c have landed once at most the next
-    // chunk's PER pieces are outstanding; the barrier makes every wave's
-    // pieces visible and marks the slot of chunk c-1 free for chunk c+2
-    if (SLOTS == 3 && c + 1 < nchunk) {
-      static_assert(PER == 1 || PER == 2 || PER == 4 || PER == 8, "vmcnt immediates below");
-      if (PER == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else if (PER == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (PER == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int64_t q = 0;
+  for (; grp < ngroups; grp += gridDim.x) {
+    const int64_t tile = grp * kX3Waves + wid;
+    const bool live = tile < ntiles;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      b1[r] = -INFINITY;
+      b2[r] = -INFINITY;
+      i1[r] = 0x7fffffff;
     }
-    __builtin_amdgcn_s_barrier();
+    for (int c = 0; c < nchunk; ++c, ++q) {
+      // this wave's pieces of chunk q have landed once at most the next
+      // chunk's PER pieces are outstanding; the barrier makes every wave's
+      // pieces visible and marks the slot of chunk q-1 free for chunk q+2
+      if (SLOTS == 3 && q + 1 < total) {
+        static_assert(PER == 1 || PER == 2 || PER == 4 || PER == 8, "vmcnt immediates below");
+        if (PER == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (PER == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (PER == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      // the next group's A fragments into L2, ahead of the C DMA (the wait
+      // above -- all but the newest C pieces -- covers them a chunk later)
+      if (c == nchunk - 1 && grp + gridDim.x < ngroups) prefetch_a(grp + gridDim.x);
 #if !defined(WH_X3_VARIANT) || WH_X3_VARIANT != 2
-    if (c + SLOTS - 1 < nchunk) stage((c + SLOTS - 1) % SLOTS, c + SLOTS - 1);
+      if (q + SLOTS - 1 < total) stage((int)((q + SLOTS - 1) % SLOTS), (int)((q + SLOTS - 1) % nchunk));
 #endif
 #if defined(WH_X3_VARIANT) && WH_X3_VARIANT == 2
-    const uint4* cur = lds;  // (microbench: chunk 0 only, no DMA in the loop)
+      const uint4* cur = lds;  // (microbench: chunk 0 only, no DMA in the loop)
 #else
-    const uint4* cur = lds + (c % SLOTS) * CF;
+      const uint4* cur = lds + (q % SLOTS) * CF;
 #endif
-    f32x16 acc[NSUB];
-#pragma unroll
-    for (int j = 0; j < NSUB; ++j) {
-      const float init = c * CH + 32 * j + (lane & 31) < k ? 0.f : -1e30f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = init;
-    }
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      bf16x8 ch[NSUB], cl[NSUB];
+      f32x16 acc[NSUB];
 #pragma unroll
       for (int j = 0; j < NSUB; ++j) {
-        ch[j] = as_bf16x8(cur[((s * NSUB + j) * 2) * 64 + lane]);
-        cl[j] = as_bf16x8(cur[((s * NSUB + j) * 2 + 1) * 64 + lane]);
+        const float init = c * CH + 32 * j + (lane & 31) < k ? 0.f : -1e30f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = init;
       }
-      // independent accumulators interleaved between dependent MFMAs
 #pragma unroll
-      for (int j = 0; j < NSUB; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], ch[j], acc[j], 0, 0, 0);
+      for (int s = 0; s < KS; ++s) {
+        bf16x8 ch[NSUB], cl[NSUB];
 #pragma unroll
-      for (int j = 0; j < NSUB; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], cl[j], acc[j], 0, 0, 0);
+        for (int j = 0; j < NSUB; ++j) {
+          ch[j] = as_bf16x8(cur[((s * NSUB + j) * 2) * 64 + lane]);
+          cl[j] = as_bf16x8(cur[((s * NSUB + j) * 2 + 1) * 64 + lane]);
+        }
+        // independent accumulators interleaved between dependent MFMAs
 #pragma unroll
-      for (int j = 0; j < NSUB; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], ch[j], acc[j], 0, 0, 0);
-    }
+        for (int j = 0; j < NSUB; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], ch[j], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < NSUB; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[s], cl[j], acc[j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < NSUB; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[s], ch[j], acc[j], 0, 0, 0);
+      }
+      // after the group's last MFMAs the A registers are free: the next
+      // group's fragments (L2 hits) load under the epilogue
+      if (c == nchunk - 1 && grp + gridDim.x < ngroups) load_a(grp + gridDim.x, ah, al);
 #if !defined(WH_X3_VARIANT) || WH_X3_VARIANT != 1
-    top2(acc, c * CH);
+      top2(acc, c * CH);
 #else
-    if (acc[0][0] == 12345.f) b1[0] = 1.f;  // (microbench: no epilogue)
+      if (acc[0][0] == 12345.f) b1[0] = 1.f;  // (microbench: no epilogue)
 #endif
-  }
-  if (!live) return;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    float v1 = b1[r], v2 = b2[r];
-    int kk = i1[r];
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-      const float o1 = __shfl_xor(v1, o, 64), o2 = __shfl_xor(v2, o, 64);
-      const int ok = __shfl_xor(kk, o, 64);
-      if (o1 > v1 || (o1 == v1 && ok < kk)) {
-        v2 = fmaxf(v1, o2);
-        v1 = o1;
-        kk = ok;
-      } else {
-        v2 = fmaxf(v2, o1);
-      }
     }
-    if ((lane & 31) == 0) {
-      const int64_t row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      if (row < n) {
-        assign[row] = kk == 0x7fffffff ? 0 : kk;
-        if (score) score[row] = v1;
-        if (!(v1 - v2 >= 2.f * eps * xnorm[row])) {  // a near-tie: exact re-score
-          const int q = atomicAdd(amb, 1);
-          amb[1 + q] = (int32_t)row;
+    if (live) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v1 = b1[r], v2 = b2[r];
+        int kk = i1[r];
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) {
+          const float o1 = __shfl_xor(v1, o, 64), o2 = __shfl_xor(v2, o, 64);
+          const int ok = __shfl_xor(kk, o, 64);
+          if (o1 > v1 || (o1 == v1 && ok < kk)) {
+            v2 = fmaxf(v1, o2);
+            v1 = o1;
+            kk = ok;
+          } else {
+            v2 = fmaxf(v2, o1);
+          }
+        }
+        if ((lane & 31) == 0) {
+          const int64_t row = tile * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          if (row < n) {
+            assign[row] = kk == 0x7fffffff ? 0 : kk;
+            if (score) score[row] = v1;
+            if (!(v1 - v2 >= 2.f * eps * xnorm[row])) {  // a near-tie: exact re-score
+              const int qq = atomicAdd(amb, 1);
+              amb[1 + qq] = (int32_t)row;
+            }
+          }
         }
       }
     }
@@ -884,7 +925,22 @@ void kmeans_assign_x3(const void* Xp, const float* xnorm, const float* X, int64_
   if (n <= 0) return;
   const int ks = x3_ks(f);
   const int nchunk = (k + 32 * kX3Nsub - 1) / (32 * kX3Nsub);
-  const dim3 grid((unsigned)(((n + 31) / 32 + kX3Waves - 1) / kX3Waves)), block(kX3Threads);
+  // persistent grid: one workgroup per CU (128 KiB of LDS each), or one per
+  // row group with WH_X3_PERSIST=0
+  const int64_t ngroups = ((n + 31) / 32 + kX3Waves - 1) / kX3Waves;
+  static int ncu = [] {
+    int dev = 0, v = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      v = 256;
+    return v;
+  }();
+  static const bool persist = [] {
+    const char* e = std::getenv("WH_X3_PERSIST");
+    return !(e && e[0] == '0');
+  }();
+  const int64_t g = persist ? std::min<int64_t>(ngroups, ncu) : ngroups;
+  const dim3 grid((unsigned)g), block(kX3Threads);
   // eps: 3 * 2^-18 for the split + 2^-24 * (3 * 16 * ks) for the fp32 sums, x2 margin
   const float eps = 2.f * (3.f / 262144.f + (48.f * ks) / 16777216.f);
   WH_HIP_CHECK(hipMemsetAsync(amb, 0, sizeof(int32_t), s));

@@ -33,6 +33,7 @@ def main(argv):
         km.C = g["centroids"].to(dev)
     for r in range(version, max_iter):
         km.step()
+        km.flush_warnings()  # this iteration's empty-cluster warning, in order
         v = bsp.lazy_checkpoint({"centroids": km.C.cpu()})
         fault_point(bsp.rank, v)
         bsp.tracker_print("Finish %d-th iteration" % r)

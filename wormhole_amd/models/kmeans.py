@@ -57,6 +57,8 @@ class KMeans:
             self.Xp = _native.hip().kmeans_pack_x(self.X)
         self.C = None
         self.rescored = None  # device count of near-tie rows re-scored in fp32 (last assign)
+        self._empty_host = None  # pinned count of empty clusters of the last step
+        self._empty_ev = None
 
     def init_centroids(self, seed=0):
         """Reference InitCentroids: every rank draws num_cluster random rows of
@@ -100,14 +102,36 @@ class KMeans:
         self.bsp.allreduce(sums)  # rabit::Allreduce<Sum>(temp, K*(F+1), lazy_fn)
         cnt = sums[:, self.f]
         empty = cnt == 0
-        if bool(empty.any()):
-            self.bsp.tracker_print("Warning: found %d zero size cluster(s), maybe too less number "
-                                   "of datapoints? keeping their previous centroids"
-                                   % int(empty.sum()))
+        self._warn_empty(empty.sum())
         newC = sums[:, : self.f] / torch.where(empty, torch.ones_like(cnt), cnt)[:, None]
         newC = torch.where(empty[:, None], self.C, newC)
         self.C = normalize_rows(newC)
         return a
+
+    def _warn_empty(self, n_empty):
+        """The reference's zero-size-cluster warning without a host sync per
+        iteration: the count goes to pinned memory asynchronously and is
+        reported one iteration later (and by :meth:`flush_warnings`)."""
+        self.flush_warnings()
+        if self.gpu:
+            if self._empty_host is None:
+                self._empty_host = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self._empty_host.copy_(n_empty.reshape(1), non_blocking=True)
+            self._empty_ev = torch.cuda.Event()
+            self._empty_ev.record()
+        elif int(n_empty):
+            self._print_empty(int(n_empty))
+
+    def _print_empty(self, n):
+        self.bsp.tracker_print("Warning: found %d zero size cluster(s), maybe too less number "
+                               "of datapoints? keeping their previous centroids" % n)
+
+    def flush_warnings(self):
+        if self._empty_ev is not None:
+            self._empty_ev.synchronize()
+            self._empty_ev = None
+            if int(self._empty_host[0]):
+                self._print_empty(int(self._empty_host[0]))
 
     def objective(self, a=None):
         """Mean cosine similarity of rows to their centroid (diagnostic)."""
