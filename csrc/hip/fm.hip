@@ -517,6 +517,7 @@ __global__ __launch_bounds__(kThreads) void k_chunk_plan(int64_t nuniq,
 // radix_sort_pairs picks a 10-pass merge sort at this size (124 us).
 constexpr int kBuckets = 256;
 constexpr int kBucketBlocks = 128;
+constexpr int kBucketU = 8;  // chunks per thread with loads in flight together
 
 __device__ __forceinline__ int row_bucket(int row, int shift) {
   const int b = row >> shift;
@@ -533,8 +534,21 @@ __global__ __launch_bounds__(kThreads) void k_vchunk_hist(const int64_t* __restr
   const int64_t n = *nchunk_p;
   const int64_t per = (n + gridDim.x - 1) / gridDim.x;
   const int64_t c0 = per * blockIdx.x, c1 = c0 + per < n ? c0 + per : n;
-  for (int64_t c = c0 + threadIdx.x; c < c1; c += kThreads)
-    atomicAdd(&h[row_bucket(csc_row[meta[c].y], shift)], 1);
+  // kBucketU independent meta -> row load chains in flight per thread (one
+  // chain at a time left this kernel waiting on ~17 round trips)
+  for (int64_t cb = c0 + threadIdx.x; cb < c1; cb += kThreads * kBucketU) {
+    int idx[kBucketU], row[kBucketU];
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int64_t c = cb + (int64_t)u * kThreads;
+      idx[u] = c < c1 ? meta[c].y : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) row[u] = idx[u] >= 0 ? csc_row[idx[u]] : -1;
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u)
+      if (row[u] >= 0) atomicAdd(&h[row_bucket(row[u], shift)], 1);
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < kBuckets; i += kThreads) hist[blockIdx.x * kBuckets + i] = h[i];
 }
@@ -596,10 +610,19 @@ __global__ __launch_bounds__(kThreads) void k_vchunk_scatter(const int64_t* __re
   const int64_t n = *nchunk_p;
   const int64_t per = (n + gridDim.x - 1) / gridDim.x;
   const int64_t c0 = per * blockIdx.x, c1 = c0 + per < n ? c0 + per : n;
-  for (int64_t c = c0 + threadIdx.x; c < c1; c += kThreads) {
-    const int4 m = meta[c];
-    const int pos = atomicAdd(&base[row_bucket(csc_row[m.y], shift)], 1);
-    out[pos] = m;
+  for (int64_t cb = c0 + threadIdx.x; cb < c1; cb += kThreads * kBucketU) {
+    int4 m[kBucketU];
+    int row[kBucketU];
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int64_t c = cb + (int64_t)u * kThreads;
+      m[u] = c < c1 ? meta[c] : make_int4(0, -1, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) row[u] = m[u].y >= 0 ? csc_row[m[u].y] : -1;
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u)
+      if (row[u] >= 0) out[atomicAdd(&base[row_bucket(row[u], shift)], 1)] = m[u];
   }
 }
 
@@ -879,7 +902,22 @@ static int resident_blocks(K kernel, int cap) {
   return n < cap ? n : cap;
 }
 
+// WH_FM_BLOCKS_PER_CU overrides the occupancy query (experiments)
+static int blocks_override(int cap) {
+  static int per_cu = [] {
+    const char* e = std::getenv("WH_FM_BLOCKS_PER_CU");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (per_cu <= 0) return 0;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return std::min(per_cu * cus, cap);
+}
+
 #define WH_RESIDENT(G, KERNEL, CAP)                                              \
+  (blocks_override(CAP) > 0 ? blocks_override(CAP) : WH_RESIDENT_Q(G, KERNEL, CAP))
+#define WH_RESIDENT_Q(G, KERNEL, CAP)                                            \
   ((G) == 1 ? resident_blocks(KERNEL<1>, CAP) : (G) == 2 ? resident_blocks(KERNEL<2>, CAP) \
    : (G) == 4 ? resident_blocks(KERNEL<4>, CAP) : (G) == 8 ? resident_blocks(KERNEL<8>, CAP) \
    : (G) == 16 ? resident_blocks(KERNEL<16>, CAP) : (G) == 32 ? resident_blocks(KERNEL<32>, CAP) \

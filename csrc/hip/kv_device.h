@@ -16,6 +16,8 @@ constexpr int kMaxProbe = 256;
 // pull / open tiles: 4 keys per thread
 constexpr int kPullPer = 4;
 constexpr int kPullTile = kThreads * kPullPer;
+constexpr int kRowBatch = 8;   // row loads a G-lane group issues before its stores
+constexpr int kPushBatch = 4;  // (V, VG, gV) row triples per G-lane group in the push
 
 __device__ __forceinline__ uint64_t ld_relaxed(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

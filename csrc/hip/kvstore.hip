@@ -351,7 +351,59 @@ __global__ __launch_bounds__(kThreads) void k_difacto_open_pull(
   }
   if (t.vstride == 0) return;
   // row jobs: a fresh row is initialised into the table AND written to its
-  // pull position from the same registers; an existing row is copied
+  // pull position from the same registers; an existing row is copied.
+  if (t.vstride == 4 * G) {
+    // Batched: the wave's jobs (up to kPullPer x 64) are listed in LDS and
+    // every G-lane group issues kRowBatch row loads before its stores, so the
+    // wave waits ~jobs / (64/G * kRowBatch) memory round trips instead of one
+    // per 64/G jobs (the load -> store chain of each job serialised them).
+    constexpr int NG = 64 / G;
+    __shared__ int4 jobs[kThreads / 64][kPullPer * 64];
+    int4* jl = jobs[threadIdx.x >> 6];
+    int nj = 0;
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r) {
+      const bool has = row[r] >= 0;
+      const uint64_t m = __ballot(has);
+      if (has)
+        jl[nj + __popcll(m & ((1ull << lane) - 1ull))] =
+            make_int4(row[r], vp[r] | (fresh[r] ? (int)0x80000000 : 0), (int)(uint32_t)k[r],
+                      (int)(uint32_t)(k[r] >> 32));
+      nj += __popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int grp = lane / G, gl = lane & (G - 1), c = gl * 4;
+    for (int j0 = 0; j0 < nj; j0 += NG * kRowBatch) {
+      float4 v[kRowBatch];
+#pragma unroll
+      for (int b = 0; b < kRowBatch; ++b) {
+        const int jj = j0 + b * NG + grp;
+        v[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (jj < nj) {
+          const int4 d = jl[jj];
+          if (d.y >= 0) v[b] = *reinterpret_cast<const float4*>(t.V + (int64_t)d.x * t.vstride + c);
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < kRowBatch; ++b) {
+        const int jj = j0 + b * NG + grp;
+        if (jj >= nj) continue;
+        const int4 d = jl[jj];
+        const int jp = d.y & 0x7fffffff;
+        if (d.y < 0) {  // fresh
+          const uint64_t jk = (uint64_t)(uint32_t)d.z | ((uint64_t)(uint32_t)d.w << 32);
+          v[b] = v_init4(hp, jk, c, t.dim);
+          *reinterpret_cast<float4*>(t.V + (int64_t)d.x * t.vstride + c) = v[b];
+          *reinterpret_cast<float4*>(t.VG + (int64_t)d.x * t.vstride + c) =
+              make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        *reinterpret_cast<float4*>(vc + (int64_t)jp * t.vstride + c) = v[b];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < kPullPer; ++r) {
     for_each_row_job<G>(row[r] >= 0, [&](int src, int gl) {
@@ -365,13 +417,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_open_pull(
       if (jf) {
         float* VG = t.VG + (int64_t)jr * t.vstride;
         for (int c = gl * 4; c < t.vstride; c += 4 * G) {
-          float4 v;
-          float* pv = &v.x;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int d = c + e;
-            pv[e] = d < t.dim ? (uhash01(hp.seed, jk, (uint64_t)d) * 2.f - 1.f) * hp.v_init : 0.f;
-          }
+          const float4 v = v_init4(hp, jk, c, t.dim);
           *reinterpret_cast<float4*>(V + c) = v;
           *reinterpret_cast<float4*>(VG + c) = make_float4(0.f, 0.f, 0.f, 0.f);
           *reinterpret_cast<float4*>(o + c) = v;
@@ -462,6 +508,66 @@ __global__ __launch_bounds__(kThreads) void k_difacto_push(KVTable t, const int3
     kind = 2;
   }
   long long newv = kind == 1 ? t.dim : 0;
+  if (t.vstride == 4 * G) {
+    // Batched as in k_difacto_open_pull: jobs listed in LDS, kPushBatch jobs'
+    // loads (V, VG, gV rows) in flight per G-lane group before the updates
+    constexpr int NG = 64 / G;
+    __shared__ int4 jobs[kThreads / 64][64];
+    int4* jl = jobs[threadIdx.x >> 6];
+    const uint64_t m = __ballot(kind != 0);
+    if (kind != 0) jl[__popcll(m & ((1ull << lane) - 1ull))] = make_int4(row, gvid, kind, s);
+    const int nj = __popcll(m);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int grp = lane / G, gl = lane & (G - 1), c = gl * 4;
+    for (int j0 = 0; j0 < nj; j0 += NG * kPushBatch) {
+      float4 v[kPushBatch], cg[kPushBatch], g[kPushBatch];
+      uint64_t kk[kPushBatch];
+#pragma unroll
+      for (int b = 0; b < kPushBatch; ++b) {
+        const int jj = j0 + b * NG + grp;
+        kk[b] = 0;
+        if (jj >= nj) continue;
+        const int4 d = jl[jj];
+        if (d.z == 2) {
+          v[b] = *reinterpret_cast<const float4*>(t.V + (int64_t)d.x * t.vstride + c);
+          cg[b] = *reinterpret_cast<const float4*>(t.VG + (int64_t)d.x * t.vstride + c);
+          g[b] = *reinterpret_cast<const float4*>(gvc + (int64_t)d.y * t.vstride + c);
+        } else {
+          kk[b] = t.sl[d.w].key;
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < kPushBatch; ++b) {
+        const int jj = j0 + b * NG + grp;
+        if (jj >= nj) continue;
+        const int4 d = jl[jj];
+        float* V = t.V + (int64_t)d.x * t.vstride + c;
+        float* VG = t.VG + (int64_t)d.x * t.vstride + c;
+        if (d.z == 1) {
+          *reinterpret_cast<float4*>(V) = v_init4(hp, kk[b], c, t.dim);
+          *reinterpret_cast<float4*>(VG) = make_float4(0.f, 0.f, 0.f, 0.f);
+          continue;
+        }
+        // AdaGrad on V (reference UpdateV, learn/difacto/async_sgd.h:289-296)
+        float* pv = &v[b].x;
+        float* pc = &cg[b].x;
+        const float* pg = &g[b].x;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gg = pg[e] + hp.v_l2 * pv[e];
+          pc[e] = sqrtf(pc[e] * pc[e] + gg * gg);
+          pv[e] -= hp.v_alpha / (pc[e] + hp.v_beta) * gg;
+        }
+        *reinterpret_cast<float4*>(V) = v[b];
+        *reinterpret_cast<float4*>(VG) = cg[b];
+      }
+    }
+    newv = wave_sum_ll(newv);
+    if (lane == 0 && newv) atomicAdd(stat_ptr(t.stats, 1), (unsigned long long)newv);
+    return;
+  }
   for_each_row_job<G>(kind != 0, [&](int src, int gl) {
     const int sl = src >= 0 ? src : lane;
     const int32_t js = __shfl(s, sl, 64), jr = __shfl(row, sl, 64);
