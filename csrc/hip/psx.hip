@@ -216,6 +216,60 @@ __global__ __launch_bounds__(kThreads) void k_ps_open(
   if (t.vstride == 0) return;
   // row jobs: 0 copy from the slab, 1 initialise (CAS winner: table + wire),
   // 2 recompute the initial values (a row another lane created in this launch)
+  if (t.vstride == 4 * G) {
+    // batched through a per-wave LDS job list, as k_difacto_open_pull
+    // (kvstore.hip): kRowBatch slab loads in flight per G-lane group
+    constexpr int NG = 64 / G;
+    __shared__ int4 jobs[kThreads / 64][kPullPer * 64];
+    int4* jl = jobs[threadIdx.x >> 6];
+    int nj = 0;
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r) {
+      const int kind = mine_fresh[r] ? 1 : (row[r] >= vbase ? 2 : 0);
+      const bool has = orow[r] >= 0;
+      const uint64_t m = __ballot(has);
+      if (has)
+        jl[nj + __popcll(m & ((1ull << lane) - 1ull))] =
+            make_int4(row[r] | (kind << 30), orow[r], (int)(uint32_t)k[r],
+                      (int)(uint32_t)(k[r] >> 32));
+      nj += __popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int grp = lane / G, c = (lane & (G - 1)) * 4;
+    for (int j0 = 0; j0 < nj; j0 += NG * kRowBatch) {
+      float4 v[kRowBatch];
+#pragma unroll
+      for (int b = 0; b < kRowBatch; ++b) {
+        const int jj = j0 + b * NG + grp;
+        v[b] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (jj < nj) {
+          const int4 d = jl[jj];
+          if ((d.x >> 30) == 0)
+            v[b] = *reinterpret_cast<const float4*>(t.V + (int64_t)d.x * t.vstride + c);
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < kRowBatch; ++b) {
+        const int jj = j0 + b * NG + grp;
+        if (jj >= nj) continue;
+        const int4 d = jl[jj];
+        const int kind = (d.x >> 30) & 3, jr = d.x & 0x3fffffff;
+        if (kind != 0) {
+          const uint64_t jk = (uint64_t)(uint32_t)d.z | ((uint64_t)(uint32_t)d.w << 32);
+          v[b] = v_init4(hp, jk, c, t.dim);
+          if (kind == 1) {
+            *reinterpret_cast<float4*>(t.V + (int64_t)jr * t.vstride + c) = v[b];
+            *reinterpret_cast<float4*>(t.VG + (int64_t)jr * t.vstride + c) =
+                make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+        *reinterpret_cast<float4*>(rbuf + (int64_t)d.y * t.vstride + c) = v[b];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int r = 0; r < kPullPer; ++r) {
     const int kind = mine_fresh[r] ? 1 : (row[r] >= vbase ? 2 : 0);
@@ -443,7 +497,59 @@ __global__ __launch_bounds__(kThreads) void k_ps_push(
     kind = 2;
   }
   long long newv = kind == 1 ? t.dim : 0;
-  for_each_row_job<G>(kind != 0, [&](int src, int gl) {
+  bool rest = kind != 0;
+  if (t.vstride == 4 * G) {
+    // initialisations and single-peer AdaGrad steps batched through an LDS
+    // job list (as k_difacto_push); keys pushed by several peers (chains)
+    // take the general loop below
+    constexpr int NG = 64 / G;
+    __shared__ int4 jobs[kThreads / 64][64];
+    int4* jl = jobs[threadIdx.x >> 6];
+    const bool bat = kind == 1 || (kind == 2 && single);
+    rest = kind != 0 && !bat;
+    const uint64_t m = __ballot(bat);
+    if (bat) jl[__popcll(m & ((1ull << lane) - 1ull))] = make_int4(row, (int)gvrow, kind, s);
+    const int nj = __popcll(m);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int grp = lane / G, c = (lane & (G - 1)) * 4;
+    for (int j0 = 0; j0 < nj; j0 += NG * kPushBatch) {
+      float4 v[kPushBatch], cg[kPushBatch], g[kPushBatch];
+      uint64_t kk[kPushBatch];
+#pragma unroll
+      for (int b = 0; b < kPushBatch; ++b) {
+        const int jj = j0 + b * NG + grp;
+        kk[b] = 0;
+        if (jj >= nj) continue;
+        const int4 d = jl[jj];
+        if (d.z == 2) {
+          v[b] = *reinterpret_cast<const float4*>(t.V + (int64_t)d.x * t.vstride + c);
+          cg[b] = *reinterpret_cast<const float4*>(t.VG + (int64_t)d.x * t.vstride + c);
+          g[b] = *reinterpret_cast<const float4*>(gbuf + (int64_t)d.y * t.vstride + c);
+        } else {
+          kk[b] = t.sl[d.w].key;
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < kPushBatch; ++b) {
+        const int jj = j0 + b * NG + grp;
+        if (jj >= nj) continue;
+        const int4 d = jl[jj];
+        float* V = t.V + (int64_t)d.x * t.vstride + c;
+        float* VG = t.VG + (int64_t)d.x * t.vstride + c;
+        if (d.z == 1) {
+          *reinterpret_cast<float4*>(V) = v_init4(hp, kk[b], c, t.dim);
+          *reinterpret_cast<float4*>(VG) = make_float4(0.f, 0.f, 0.f, 0.f);
+          continue;
+        }
+        adagrad4(v[b], cg[b], g[b], hp);
+        *reinterpret_cast<float4*>(V) = v[b];
+        *reinterpret_cast<float4*>(VG) = cg[b];
+      }
+    }
+  }
+  for_each_row_job<G>(rest, [&](int src, int gl) {
     const int s2 = src >= 0 ? src : lane;
     const int32_t jr = __shfl(row, s2, 64), jk = __shfl(kind, s2, 64);
     const int32_t js = __shfl(s, s2, 64);
