@@ -13,6 +13,7 @@ no GPU).  They follow the reference formulas literally:
 """
 import math
 
+import numpy as np
 import torch
 
 LOSS_SQUARE, LOSS_LOGIT, LOSS_SQUARE_HINGE = 1, 2, 4
@@ -37,9 +38,16 @@ def owner_of(keys, nshard):
     """Shard owner of each int64-encoded uint64 key (matches wh::owner_of)."""
     if nshard <= 1:
         return torch.zeros(keys.numel(), dtype=torch.int64, device=keys.device)
-    lst = keys.cpu().tolist()
-    own = [mix64b_int(k) % nshard for k in lst]
-    return torch.tensor(own, dtype=torch.int64, device=keys.device)
+    # vectorised uint64 arithmetic (numpy wraps modulo 2^64 like the device)
+    x = keys.detach().cpu().numpy().astype(np.int64).view(np.uint64).copy()
+    s33 = np.uint64(33)
+    x ^= x >> s33
+    x *= np.uint64(0xff51afd7ed558ccd)
+    x ^= x >> s33
+    x *= np.uint64(0xc4ceb9fe1a85ec53)
+    x ^= x >> s33
+    own = (x % np.uint64(nshard)).astype(np.int64)
+    return torch.from_numpy(own).to(keys.device)
 
 
 def localize(keys, offset, val=None, nshard=1):
