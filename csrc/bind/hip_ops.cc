@@ -364,20 +364,23 @@ class LocalizeJob {
     const auto* kp = reinterpret_cast<const uint64_t*>(keys_.data_ptr());
     wh::loc_part_hist(kp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv,
                       reinterpret_cast<uint32_t*>(hist.data_ptr()), s);
-    auto blkoff = torch::empty({nh + 1}, i64);
-    auto tmp = torch::empty({wh::scan_tmp_elems(nh)}, i64);
-    wh::scan_i32(ptr<int32_t>(hist), ptr<int64_t>(blkoff), nh, ptr<int64_t>(tmp), s);
+    auto gsum = torch::empty({wh::loc_part_groups(plan_) * plan_.ndig}, i32);
+    auto base = torch::empty({plan_.ndig + 1}, i64);
+    wh::loc_part_offsets(plan_, reinterpret_cast<uint32_t*>(hist.data_ptr()),
+                         reinterpret_cast<uint32_t*>(gsum.data_ptr()), ptr<int64_t>(base), s);
     auto pk = torch::empty({nnz}, i64);
     auto pr = torch::empty({nnz}, i32);
     auto pv = torch::empty({vp ? nnz : 0}, keys_.options().dtype(torch::kFloat32));
     auto pos_of = torch::empty({nnz}, i32);
-    wh::loc_part_scatter(kp, vp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv, ptr<int64_t>(blkoff),
+    wh::loc_part_scatter(kp, vp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv, ptr<int64_t>(base),
+                         reinterpret_cast<const uint32_t*>(gsum.data_ptr()),
+                         reinterpret_cast<const uint32_t*>(hist.data_ptr()),
                          reinterpret_cast<uint64_t*>(pk.data_ptr()), ptr<int32_t>(pr),
                          vp ? ptr<float>(pv) : nullptr, ptr<int32_t>(pos_of), s);
     auto plid = torch::empty({nnz}, i32);
     auto* pw = reinterpret_cast<unsigned long long*>(ws.part_ws.data_ptr());
     wh::loc_part_dedup(reinterpret_cast<const uint64_t*>(pk.data_ptr()), ptr<int32_t>(pr),
-                       vp ? ptr<float>(pv) : nullptr, nnz, nsh, plan_, hv, ptr<int64_t>(blkoff),
+                       vp ? ptr<float>(pv) : nullptr, nnz, nsh, plan_, hv, ptr<int64_t>(base),
                        wh::lookback_bind(ws.lb_loc.data_ptr()),
                        reinterpret_cast<uint64_t*>(uniq_.data_ptr()), ptr<int32_t>(ucnt_),
                        ptr<int64_t>(csc_off_), ptr<int32_t>(csc_row_),

@@ -152,11 +152,71 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(const uint64_t* __re
     }
   }
   __syncthreads();
+  // tile-major: one coalesced row per tile (a digit-major layout made every
+  // block store its ndig counters to ndig different cache lines)
   for (int i = threadIdx.x; i < ndig; i += kPartThreads)
-    hist[(int64_t)i * gridDim.x + blockIdx.x] = h[i];
+    hist[(int64_t)blockIdx.x * ndig + i] = h[i];
 }
 
-// Each tile's non-zeros go to [blkoff[d][tile] ...) of their digit. A tile is
+// Partition offsets from the tile-major histogram without a transposing
+// scan: off(t, d) = base[d] + gpre[t / kColTB][d] + hist'[t][d], where hist'
+// is the exclusive prefix of digit d over the tiles of t's group (in place),
+// gpre the exclusive prefix over groups and base the exclusive prefix of the
+// digit totals (base[ndig] = nnz). Every access is a coalesced row.
+constexpr int kColTB = 16;  // tiles per group
+
+__global__ __launch_bounds__(256) void k_part_colpre(uint32_t* __restrict__ hist, int ntiles,
+                                                     int ndig, uint32_t* __restrict__ gsum) {
+  const int t0 = blockIdx.x * kColTB;
+  const int t1 = t0 + kColTB < ntiles ? t0 + kColTB : ntiles;
+  for (int d = threadIdx.x; d < ndig; d += 256) {
+    uint32_t v[kColTB];
+#pragma unroll
+    for (int u = 0; u < kColTB; ++u) v[u] = t0 + u < t1 ? hist[(int64_t)(t0 + u) * ndig + d] : 0u;
+    uint32_t run = 0;
+#pragma unroll
+    for (int u = 0; u < kColTB; ++u) {
+      if (t0 + u < t1) hist[(int64_t)(t0 + u) * ndig + d] = run;
+      run += v[u];
+    }
+    gsum[(int64_t)blockIdx.x * ndig + d] = run;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_part_base(uint32_t* __restrict__ gsum, int ngroups,
+                                                    int ndig, int64_t* __restrict__ base) {
+  __shared__ uint32_t wt[16];
+  const int d = threadIdx.x, lane = d & 63, w = d >> 6;
+  uint32_t run = 0;
+  if (d < ndig) {
+    for (int g0 = 0; g0 < ngroups; g0 += 8) {  // 8 independent loads in flight
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = g0 + u < ngroups ? gsum[(int64_t)(g0 + u) * ndig + d] : 0u;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (g0 + u < ngroups) gsum[(int64_t)(g0 + u) * ndig + d] = run;
+        run += v[u];
+      }
+    }
+  }
+  // exclusive scan of the digit totals (ndig <= 1024 = blockDim)
+  uint32_t x = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wt[w] = x;
+  __syncthreads();
+  uint32_t pre = 0;
+  for (int q = 0; q < w; ++q) pre += wt[q];
+  if (d < ndig) base[d] = (int64_t)(pre + x - run);
+  if (d == ndig - 1) base[ndig] = (int64_t)(pre + x);
+}
+
+// Each tile's non-zeros go to [off(tile, d) ...) of their digit (off: see
+// k_part_colpre). A tile is
 // processed in chunks of kChunk non-zeros that are counting-sorted by digit
 // in LDS first, so that consecutive lanes store consecutive addresses of a
 // digit's run (scattered 4/8-byte stores cost one memory request each:
@@ -176,7 +236,8 @@ size_t scatter_lds_bytes(int ndig, bool has_val) {
 __global__ __launch_bounds__(kScatThreads, 4) void k_part_scatter(
     const uint64_t* __restrict__ keys, const float* __restrict__ val,
     const int64_t* __restrict__ off, int64_t nrows, int R, int nshard, int npo_bits, int stride,
-    int nho, int ndig, PartHeavy hv, const int64_t* __restrict__ blkoff, uint64_t* __restrict__ pk,
+    int nho, int ndig, PartHeavy hv, const int64_t* __restrict__ base,
+    const uint32_t* __restrict__ gpre, const uint32_t* __restrict__ tpre, uint64_t* __restrict__ pk,
     int32_t* __restrict__ pr, float* __restrict__ pv, int32_t* __restrict__ pos_of) {
   extern __shared__ __align__(16) unsigned char lds[];
   uint32_t* gbase = reinterpret_cast<uint32_t*>(lds);   // next free position per digit
@@ -197,7 +258,8 @@ __global__ __launch_bounds__(kScatThreads, 4) void k_part_scatter(
   const int nr = (int)(r1 - r0);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < ndig; i += kScatThreads)
-    gbase[i] = (uint32_t)blkoff[(int64_t)i * gridDim.x + blockIdx.x];
+    gbase[i] = (uint32_t)base[i] + gpre[(int64_t)(blockIdx.x / kColTB) * ndig + i] +
+               tpre[(int64_t)blockIdx.x * ndig + i];
   for (int i = threadIdx.x; i <= nr; i += kScatThreads) so[i] = off[r0 + i];
   __syncthreads();
   const int64_t j0 = so[0], j1 = so[nr];
@@ -363,7 +425,7 @@ __device__ __forceinline__ void heavy_elect(const PartHeavy& hv, int own, uint64
 template <bool kVal>
 __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
     const uint64_t* __restrict__ pk, const int32_t* __restrict__ pr,
-    const float* __restrict__ pv, const int64_t* __restrict__ blkoff, int ntiles, int ndig,
+    const float* __restrict__ pv, const int64_t* __restrict__ base, int ntiles, int ndig,
     int nshard, int npo_bits, int stride, int nho, PartHeavy hv, Lookback lb, int64_t nnz,
     uint64_t* __restrict__ uniq, int32_t* __restrict__ ucnt, int64_t* __restrict__ csc_off,
     int32_t* __restrict__ csc_row, float* __restrict__ csc_val, int32_t* __restrict__ plid,
@@ -382,7 +444,7 @@ __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
   const int own = p / stride;
   const int gsz = (1 << (npo_bits - log2_nho(nho))) + 1;
   const bool heavy = nho > 0 && (p - own * stride) % gsz == gsz - 1;  // a single-id partition
-  const int64_t ps = blkoff[(int64_t)p * ntiles], pe = blkoff[(int64_t)(p + 1) * ntiles];
+  const int64_t ps = base[p], pe = base[p + 1];
   uint32_t occ[kDedupPer], cnt[kDedupPer], so = 0, sn = 0, io = 0, in = 0;
   if (!heavy) {
     for (int i = threadIdx.x; i < kDedupSlots; i += kDedupThreads) {
@@ -624,24 +686,34 @@ void loc_part_hist(const uint64_t* keys, const int64_t* offset, int64_t nrows, i
                      offset, nrows, pl.R, nshard, pl.npo_bits, pl.stride, pl.nho, pl.ndig, hv, hist);
 }
 
+int64_t loc_part_groups(const PartPlan& pl) { return (pl.ntiles + kColTB - 1) / kColTB; }
+
+void loc_part_offsets(const PartPlan& pl, uint32_t* hist, uint32_t* gsum, int64_t* base,
+                      hipStream_t s) {
+  const int64_t ng = loc_part_groups(pl);
+  hipLaunchKernelGGL(k_part_colpre, dim3((unsigned)ng), dim3(256), 0, s, hist, (int)pl.ntiles,
+                     pl.ndig, gsum);
+  hipLaunchKernelGGL(k_part_base, dim3(1), dim3(1024), 0, s, gsum, (int)ng, pl.ndig, base);
+}
+
 void loc_part_scatter(const uint64_t* keys, const float* val, const int64_t* offset,
                       int64_t nrows, int nshard, const PartPlan& pl, const PartHeavy& hv,
-                      const int64_t* blkoff, uint64_t* pk, int32_t* pr, float* pv,
-                      int32_t* pos_of, hipStream_t s) {
+                      const int64_t* base, const uint32_t* gpre, const uint32_t* tpre,
+                      uint64_t* pk, int32_t* pr, float* pv, int32_t* pos_of, hipStream_t s) {
   const size_t lds = scatter_lds_bytes(pl.ndig, val != nullptr) + 16;
   hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)pl.ntiles), dim3(kScatThreads), lds, s, keys,
-                     val, offset, nrows, pl.R, nshard, pl.npo_bits, pl.stride, pl.nho, pl.ndig, hv, blkoff,
-                     pk, pr, pv, pos_of);
+                     val, offset, nrows, pl.R, nshard, pl.npo_bits, pl.stride, pl.nho, pl.ndig, hv,
+                     base, gpre, tpre, pk, pr, pv, pos_of);
 }
 
 void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const float* pv, int64_t nnz,
-                    int nshard, const PartPlan& pl, const PartHeavy& hv, const int64_t* blkoff,
+                    int nshard, const PartPlan& pl, const PartHeavy& hv, const int64_t* base,
                     const Lookback& lb,
                     uint64_t* uniq, int32_t* ucnt, int64_t* csc_off, int32_t* csc_row,
                     float* csc_val, int32_t* plid, unsigned long long* up, unsigned int* arrive,
                     int64_t* owner_cnt, hipStream_t s, int64_t* tim) {
   auto kern = pv ? k_part_dedup<true> : k_part_dedup<false>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)pl.ndig), dim3(kDedupThreads), 0, s, pk, pr, pv, blkoff,
+  hipLaunchKernelGGL(kern, dim3((unsigned)pl.ndig), dim3(kDedupThreads), 0, s, pk, pr, pv, base,
                      (int)pl.ntiles, pl.ndig, nshard, pl.npo_bits, pl.stride, pl.nho, hv, lb, nnz, uniq,
                      ucnt, csc_off,
                      csc_row, csc_val, plid, up, arrive, owner_cnt, tim);

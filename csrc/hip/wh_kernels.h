@@ -99,20 +99,26 @@ struct PartHeavy {
 };
 // uest: an upper estimate of the unique ids (nnz when nothing is known)
 PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, bool heavy);
-// hist [ndig * ntiles] uint32 (digit-major)
+// hist [ntiles * ndig] uint32 (tile-major)
 void loc_part_hist(const uint64_t* keys, const int64_t* offset, int64_t nrows, int nshard,
                    const PartPlan& pl, const PartHeavy& hv, uint32_t* hist, hipStream_t s);
-// blkoff = exclusive scan of hist (ndig * ntiles + 1 entries); pk/pr [nnz]
-// (+ pv [nnz] when val) in partition order; pos_of [nnz] in CSR order
+// partition offsets: hist becomes the in-group tile prefix, gsum
+// [loc_part_groups * ndig] the group prefix, base [ndig + 1] the digit starts
+// (base[ndig] = nnz)
+int64_t loc_part_groups(const PartPlan& pl);
+void loc_part_offsets(const PartPlan& pl, uint32_t* hist, uint32_t* gsum, int64_t* base,
+                      hipStream_t s);
+// pk/pr [nnz] (+ pv [nnz] when val) in partition order; pos_of [nnz] in CSR
+// order (gpre / tpre: gsum / hist after loc_part_offsets)
 void loc_part_scatter(const uint64_t* keys, const float* val, const int64_t* offset,
                       int64_t nrows, int nshard, const PartPlan& pl, const PartHeavy& hv,
-                      const int64_t* blkoff, uint64_t* pk, int32_t* pr, float* pv,
-                      int32_t* pos_of, hipStream_t s);
+                      const int64_t* base, const uint32_t* gpre, const uint32_t* tpre,
+                      uint64_t* pk, int32_t* pr, float* pv, int32_t* pos_of, hipStream_t s);
 // up [kPartMaxDigits] u64 and *arrive (0 between calls): a workspace of its
 // own; lb: a look-back workspace no concurrent kernel uses. plid [nnz]:
 // local ids in partition order.
 void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const float* pv, int64_t nnz,
-                    int nshard, const PartPlan& pl, const PartHeavy& hv, const int64_t* blkoff,
+                    int nshard, const PartPlan& pl, const PartHeavy& hv, const int64_t* base,
                     const Lookback& lb,
                     uint64_t* uniq, int32_t* ucnt, int64_t* csc_off, int32_t* csc_row,
                     float* csc_val, int32_t* plid, unsigned long long* up, unsigned int* arrive,
