@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--format", default="criteo", choices=["criteo", "crb"])
     ap.add_argument("-n", type=int, default=1, help="workers (one GPU each)")
     ap.add_argument("--minibatch", type=int, default=100000)
+    ap.add_argument("--val-rows", type=int, default=0,
+                    help="also write this many validation rows (val_data) and time the "
+                         "validation pass (the reference log's 0.93 M ex/s)")
     ap.add_argument("--rand-shuffle", type=int, default=10,
                     help="shuffle buffer in minibatches (the reference default is 10)")
     ap.add_argument("--dir", default=None)
@@ -84,6 +87,10 @@ def main():
                             "-data_in", p, "-data_out", p[:-4] + ".crb", "-format_in", "criteo",
                             "-format_out", "crb"], check=True)
             os.remove(p)
+    vper = args.val_rows // args.files if args.val_rows else 0
+    for i in range(args.files if vper else 0):
+        with open(os.path.join(work, "val-part_%d.txt" % i), "wb") as f:
+            f.write(criteo_text(vper, 900 + i))
     gen_s = time.time() - t0
     pattern = os.path.join(work, "train-part_.*\\.%s" % ("crb" if args.format == "crb" else "txt"))
     conf = os.path.join(work, "job.conf")
@@ -91,6 +98,8 @@ def main():
         f.write('train_data = "%s"\ndata_format = "%s"\nminibatch = %d\nmax_data_pass = 1\n'
                 "print_sec = 1\nrand_shuffle = %d\n" % (pattern, args.format, args.minibatch,
                                                    args.rand_shuffle))
+        if vper:
+            f.write('val_data = "%s"\n' % os.path.join(work, "val-part_.*\\.txt"))
         if args.model == "linear":
             f.write("lambda_l1 = 4\nlr_eta = 0.1\n")
         else:
@@ -104,7 +113,7 @@ def main():
     t1 = time.time()
     proc = subprocess.Popen(cmd, cwd=work, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                             text=True, bufsize=1)
-    lines, t_start, t_end = [], None, None
+    lines, t_start, t_end, v_start, v_end = [], None, None, None, None
     for line in proc.stdout:
         now = time.time()
         lines.append(line)
@@ -113,6 +122,10 @@ def main():
         elif t_start is not None and t_end is None and (
                 line.startswith("Validating") or line.startswith("Hit max")):
             t_end = now
+        if v_start is None and line.startswith("Validating"):
+            v_start = now
+        elif v_start is not None and v_end is None and line.startswith("Hit max"):
+            v_end = now
     err = proc.stderr.read()
     rc = proc.wait()
     wall = time.time() - t1
@@ -121,7 +134,15 @@ def main():
         sys.stderr.write(out[-3000:] + err[-3000:])
         raise SystemExit(rc)
     rows = [l for l in lines if re.match(r"^\s*[\d.]+\s+[\d.e+]+\s+[\d.e+]+", l)]
-    ttl = float(rows[-1].split()[1])
+    if vper:  # the last table row is the validation pass's; the training rows precede it
+        vi = [i for i, l in enumerate(lines) if l.startswith("Validating")][0]
+        trows = [l for l in rows if lines.index(l) < vi]
+        vrows = [l for l in rows if lines.index(l) > vi]
+        ttl = float(trows[-1].split()[1])
+        vttl = float(vrows[-1].split()[1]) if vrows else 0.0
+    else:
+        ttl = float(rows[-1].split()[1])
+        vttl = 0.0
     sec = (t_end or time.time()) - t_start
     print(out[-1500:], file=sys.stderr)
     print(json.dumps({
@@ -130,7 +151,11 @@ def main():
         "value": ttl / sec if sec > 0 else None, "unit": "examples/s",
         "examples": ttl, "train_sec": sec, "job_wall_sec": wall, "datagen_sec": gen_s,
         "reference_linear_published": 1.85e6,
+        "val_examples_per_s": (vttl / (v_end - v_start)) if (vper and v_start and v_end) else None,
+        "val_examples": vttl if vper else None,
+        "reference_linear_val_published": 0.93e6,
         "config": {"rows": args.rows, "files": args.files, "minibatch": args.minibatch,
+                   "val_rows": args.val_rows,
                    "rand_shuffle": args.rand_shuffle,
                    "device_parse": os.environ.get("WH_DEVICE_PARSE", "1") != "0"},
     }))
