@@ -145,6 +145,9 @@ def main():
         vttl = 0.0
     sec = (t_end or time.time()) - t_start
     print(out[-1500:], file=sys.stderr)
+    for l in err.splitlines():  # the workers' per-pass stage summaries
+        if "minibatches" in l:
+            print(l, file=sys.stderr)
     print(json.dumps({
         "metric": "end-to-end examples/sec from %s files, %s.dmlc, %d worker(s)" % (
             args.format, args.model, args.n),

@@ -1625,7 +1625,7 @@ std::vector<Tensor> parse_criteo(const Tensor& text, int64_t nlines, bool train)
 // text: uint8 [nbytes] of nlines whole libsvm lines (device) -> (keys i64,
 // label f32, offset i64, value f32 or None when every value is 1, weight f32
 // or None when no line has one), as the host parser returns them
-py::tuple parse_libsvm(const Tensor& text, int64_t nlines) {
+std::vector<Tensor> parse_libsvm(const Tensor& text, int64_t nlines) {
   CHECK_IN(text, torch::kUInt8);
   c10::DeviceGuard g(text.device());
   auto s = cur_stream(text);
@@ -1654,13 +1654,13 @@ py::tuple parse_libsvm(const Tensor& text, int64_t nlines) {
                   ptr<float>(weight), ptr<int32_t>(flags), s);
   auto f = flags.cpu();
   const int32_t* fp = f.data_ptr<int32_t>();
-  return py::make_tuple(keys, label, off, fp[0] ? py::cast(val) : py::none(),
-                        fp[1] ? py::cast(weight) : py::none());
+  // (an undefined tensor reaches Python as None)
+  return {keys, label, off, fp[0] ? val : Tensor(), fp[1] ? weight : Tensor()};
 }
 
 // rows `sel` of a CSR block (keys, off, val?, label) -> (keys, val?, label)
 // of the gathered block whose offsets `noff` [nsel + 1] hold nnz at the end
-py::tuple csr_gather(const Tensor& keys, const Tensor& off, const c10::optional<Tensor>& val,
+std::vector<Tensor> csr_gather(const Tensor& keys, const Tensor& off, const c10::optional<Tensor>& val,
                      const Tensor& label, const Tensor& sel, const Tensor& noff, int64_t nnz) {
   CHECK_IN(keys, torch::kInt64);
   CHECK_IN(off, torch::kInt64);
@@ -1682,7 +1682,7 @@ py::tuple csr_gather(const Tensor& keys, const Tensor& off, const c10::optional<
                  val ? ptr<float>(*val) : nullptr, ptr<float>(label), ptr<int64_t>(sel),
                  sel.numel(), ptr<int64_t>(noff), reinterpret_cast<uint64_t*>(okeys.data_ptr()),
                  val ? ptr<float>(oval) : nullptr, ptr<float>(olabel), s);
-  return py::make_tuple(okeys, val ? py::cast(oval) : py::none(), olabel);
+  return {okeys, val ? oval : Tensor(), olabel};
 }
 
 // ------------------------------------------------------------ gbdt grower
@@ -2039,9 +2039,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_accum", &kmeans_accum);
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
   m.def("gbdt_grow", &gbdt_grow);
-  m.def("parse_criteo", &parse_criteo);
-  m.def("parse_libsvm", &parse_libsvm);
-  m.def("csr_gather", &csr_gather);
+  // the ingest ops block on one small device read each: the GIL is released
+  // so a producer thread's parsing overlaps the training loop
+  m.def("parse_criteo", &parse_criteo, py::call_guard<py::gil_scoped_release>());
+  m.def("parse_libsvm", &parse_libsvm, py::call_guard<py::gil_scoped_release>());
+  m.def("csr_gather", &csr_gather, py::call_guard<py::gil_scoped_release>());
   m.def("gbdt_bin_csr", &gbdt_bin_csr);
   m.def("gbdt_hist_csr", &gbdt_hist_csr);
   m.def("gbdt_split_csr", &gbdt_split_csr);

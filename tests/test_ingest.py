@@ -185,6 +185,11 @@ def test_device_shuffle_buffer_is_a_permutation_and_neg_sampling_drops_negatives
                  for i in range(lab.numel())]
     assert sorted(rows) == sorted(rows_h) and rows != rows_h
     assert sizes[:-1] == [300] * (len(sizes) - 1)
+    # a part shorter than a minibatch: one partial batch, then None, repeatedly
+    it = DeviceTextIter(host, str(p), 3, 20, "criteo", 1000, 4000, 1.0, 7, dev)
+    b = it.next()
+    assert b is not None and 0 < b.to_main(dev)[3].numel() < 1000
+    assert it.next() is None and it.next() is None
     it = DeviceTextIter(host, str(p), 0, 1, "criteo", 300, 0, 0.25, 7, dev)
     labs = []
     while True:

@@ -18,26 +18,17 @@ are gathered into one CSR block (``k_csr_gather``) whose consecutive slices
 are the minibatches -- spanning buffer boundaries like the host iterator's.
 Without a shuffle buffer, text batches are minibatches.
 
-All device work runs on a per-device side stream: its host reads (the key
-count of a block, the size of a gather) wait for that stream only, not for
-the training step in flight on the main stream, which waits for the batch
-when it is handed over (``DeviceBatch.to_main``).
+A producer thread per file part does the reading, copying and parsing on
+its own stream, a block or two ahead: the ingest ops release the GIL during
+their single device read each, so the training loop keeps enqueueing work
+meanwhile, and the main stream waits for a batch (event) only when it is
+handed over (``DeviceBatch.to_main``).
 """
 import os
 
 import torch
 
 from .. import _native
-
-_STREAMS = {}
-
-
-def _side(dev):
-    s = _STREAMS.get(dev)
-    if s is None:
-        s = _STREAMS[dev] = torch.cuda.Stream(dev)
-    return s
-
 
 def applies(fmt, path, device):
     """Device parsing is used for plain Criteo / libsvm files on a GPU worker
@@ -59,22 +50,18 @@ def parse_block(text, lines, fmt):
 
 
 class DeviceBatch:
-    """A minibatch produced on the side stream; ``to_main`` hands it to the
-    current stream."""
+    """A minibatch produced on a producer stream; ``to_main`` makes the
+    current stream wait for it (event) and hands the tensors over."""
 
-    __slots__ = ("args", "text", "lines", "fmt")
+    __slots__ = ("args", "event")
 
-    def __init__(self, args=None, text=None, lines=0, fmt=None):
-        self.args, self.text, self.lines, self.fmt = args, text, lines, fmt
+    def __init__(self, args, event=None):
+        self.args, self.event = args, event
 
     def to_main(self, dev):
-        side = _side(dev)
-        if self.args is None:  # an unshuffled block: parsed when handed over
-            with torch.cuda.stream(side):
-                self.args = parse_block(self.text.to(dev, non_blocking=True), self.lines,
-                                        self.fmt)
         main = torch.cuda.current_stream(dev)
-        main.wait_stream(side)
+        if self.event is not None:
+            main.wait_event(self.event)
         for x in self.args:
             if x is not None:
                 x.record_stream(main)
@@ -97,28 +84,93 @@ def concat_blocks(parts):
     return keys, torch.cat(offs), vals, torch.cat([p[3] for p in parts])
 
 
+_STREAM_POOL = {}
+
+
+def _producer_stream(dev):
+    """Producer streams, a small pool per device (one per live iterator in
+    the usual prefetch depth)."""
+    pool = _STREAM_POOL.setdefault(dev, [[], 0])
+    if len(pool[0]) < 4:
+        pool[0].append(torch.cuda.Stream(dev))
+    pool[1] = (pool[1] + 1) % len(pool[0])
+    return pool[0][pool[1]]
+
+
 class DeviceTextIter:
     """Minibatches of one file part, parsed on the device (the
-    ``_host.MinibatchIter`` contract: ``next()`` -> batch or None)."""
+    ``_host.MinibatchIter`` contract: ``next()`` -> batch or None).
 
-    def __init__(self, host, path, part, nparts, fmt, mb, shuf, neg, seed, device):
+    A producer thread reads the part's text batches, copies them to the
+    device and parses (and, with a shuffle buffer, permutes and gathers)
+    them on its own stream, ``depth`` blocks ahead of the consumer; the
+    parse ops release the GIL while they wait for their one device read, so
+    ingest overlaps the training loop instead of running between its steps.
+    """
+
+    def __init__(self, host, path, part, nparts, fmt, mb, shuf, neg, seed, device, depth=2):
+        import queue
+        import threading
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
         self.fmt, self.mb, self.neg, self.dev = fmt, mb, neg, device
         # a shuffle buffer is needed for negative sampling too (as on the host)
         self.shuffled = shuf > 0 or neg < 1.0
         # host reads stay minibatch-sized (pinned buffers are reused); a
-        # shuffle buffer is assembled from several parsed blocks on the device
+        # shuffle buffer is assembled from several text batches on the device
         self.per_block = max(1, -(-max(shuf, mb + 1) // mb)) if self.shuffled else 1
         self.tb = host.TextBatches(path, part, nparts, mb, True)
         self.gen = None
         if self.shuffled:
             self.gen = torch.Generator(device=device)
             self.gen.manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
-        self.cur = None  # (block, sel, pos)
+        self.stream = _producer_stream(device)
+        self.q = queue.Queue(maxsize=max(1, depth))
+        self.stop = False
+        self.done = False
+        self.cur = None  # shuffled: [keys, noff, val, label, cuts->offset, pos, n]
+        self.th = threading.Thread(target=self._produce, daemon=True)
+        self.th.start()
 
-    def _next_block(self, first):
-        """Read, parse and permute the next shuffle buffer; ``first`` rows
-        complete the minibatch begun in the previous buffer. Three host
-        reads per buffer (key count, rows kept, minibatch boundaries)."""
+    # ---------------------------------------------------------- producer
+    def _put(self, item):
+        import queue
+        while not self.stop:
+            try:
+                self.q.put(item, timeout=0.5)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def _produce(self):
+        try:
+            torch.cuda.set_device(self.dev)
+            with torch.cuda.stream(self.stream):
+                while not self.stop:
+                    item = self._block() if self.shuffled else self._minibatch()
+                    if item is None:
+                        break
+                    if not self._put(item):
+                        return
+        except BaseException as e:  # surfaced by the consumer
+            self._put(e)
+            return
+        self._put(None)
+
+    def _minibatch(self):
+        b = self.tb.next()
+        if b is None:
+            return None
+        args = parse_block(b[0].to(self.dev, non_blocking=True), b[1], self.fmt)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return DeviceBatch(args, ev)
+
+    def _block(self):
+        """The next shuffle buffer: parsed, permuted and gathered into one CSR
+        block whose consecutive slices are minibatches; host reads: the key
+        count, the rows kept (negative sampling), the slice boundaries."""
         texts, lines = [], 0
         for _ in range(self.per_block):
             b = self.tb.next()
@@ -127,7 +179,7 @@ class DeviceTextIter:
             texts.append(b[0])
             lines += int(b[1])
         if not texts:
-            return False
+            return None
         # the text batches go into one device buffer: one parse per buffer
         text = torch.empty(sum(t.numel() for t in texts), dtype=torch.uint8, device=self.dev)
         o = 0
@@ -142,37 +194,66 @@ class DeviceTextIter:
             keep = (label.index_select(0, sel) > 0) | (r <= self.neg)
             sel = sel[keep]
         n = sel.numel()
-        # the permuted buffer as one CSR block: minibatches are slices of it
         noff = torch.zeros(n + 1, dtype=torch.int64, device=self.dev)
         torch.cumsum((off[1:] - off[:-1]).index_select(0, sel), 0, out=noff[1:])
-        cuts = [0] + list(range(min(first, n), n, self.mb)) + [n]
-        cuts = sorted(set(cuts))
-        at = noff.index_select(0, torch.tensor(cuts, device=self.dev)).cpu().tolist()
-        pk, pv, pl = _native.hip().csr_gather(keys, off, val, label, sel, noff, int(at[-1]))
-        self.cur = [pk, noff, pv, pl, dict(zip(cuts, at)), 0, n]
-        return True
+        # the row offsets come to the host once (8 bytes per row): they size
+        # the gather, and slices of any length are then views plus one
+        # subtraction (the event wait releases the GIL)
+        hoff = torch.empty(n + 1, dtype=torch.int64, pin_memory=True)
+        hoff.copy_(noff, non_blocking=True)
+        e0 = torch.cuda.Event()
+        e0.record(self.stream)
+        e0.synchronize()
+        pk, pv, pl = _native.hip().csr_gather(keys, off, val, label, sel, noff, int(hoff[n]))
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return [pk, noff, pv, pl, hoff, n, ev]
+
+    # ---------------------------------------------------------- consumer
+    def _get(self):
+        if self.done:  # the producer's end marker was taken already
+            return None
+        item = self.q.get()
+        if isinstance(item, BaseException):
+            raise item
+        if item is None:
+            self.done = True
+        return item
 
     def _slice(self, take):
-        pk, noff, pv, pl, at, pos, n = self.cur
-        a, b = at[pos], at[pos + take]
+        pk, noff, pv, pl, hoff, pos, n = self.cur
+        a, b = int(hoff[pos]), int(hoff[pos + take])
         self.cur[5] = pos + take
         return (pk[a:b], noff[pos:pos + take + 1] - a, pv[a:b] if pv is not None else None,
                 pl[pos:pos + take])
 
     def next(self):
         if not self.shuffled:
-            b = self.tb.next()
-            return None if b is None else DeviceBatch(text=b[0], lines=b[1], fmt=self.fmt)
-        with torch.cuda.stream(_side(self.dev)):
-            parts, need = [], self.mb
-            while need > 0:
-                if self.cur is None or self.cur[5] == self.cur[6]:
-                    if not self._next_block(need):
-                        break
-                    continue
-                take = min(need, self.cur[6] - self.cur[5])
-                parts.append(self._slice(take))
-                need -= take
-            if not parts:
-                return None
-            return DeviceBatch(args=concat_blocks(parts))
+            return self._get()
+        dev = self.dev
+        main = torch.cuda.current_stream(dev)
+        parts, need = [], self.mb
+        while need > 0:
+            if self.cur is None or self.cur[5] == self.cur[6]:
+                blk = self._get()
+                if blk is None:
+                    self.cur = None
+                    break
+                main.wait_event(blk[6])
+                for x in blk[:4]:
+                    if x is not None:
+                        x.record_stream(main)
+                self.cur = [blk[0], blk[1], blk[2], blk[3], blk[4], 0, blk[5]]
+                continue
+            take = min(need, self.cur[6] - self.cur[5])
+            parts.append(self._slice(take))
+            need -= take
+        if not parts:
+            return None
+        return DeviceBatch(concat_blocks(parts))
+
+    def close(self):
+        self.stop = True
+
+    def __del__(self):
+        self.stop = True

@@ -85,6 +85,9 @@ class Worker:
         self.n_done = 0
         self.metrics = trace.MetricsStream(comm.rank)
         self.fault = _parse_fault(os.environ.get("WH_FAULT", ""), comm.rank)
+        if os.environ.get("WH_HANG_DUMP"):  # debug aid: all threads' stacks every N s
+            import faulthandler
+            faulthandler.dump_traceback_later(float(os.environ["WH_HANG_DUMP"]), repeat=True)
         self.saver = checkpoint.AsyncSaver()
 
     def send(self, **kw):
