@@ -66,6 +66,7 @@ __device__ __forceinline__ int heavy_digit(int own, int q, int stride, int gbits
 // of the rows) lands in one hashed partition whose workgroup serialises the
 // whole step (dedup timing: 50 us of 115 us in that one partition).
 constexpr int kHeavySlots = 1024;  // LDS hash of <= kPartMaxHeavy ids
+constexpr int kPartHeavyTotal = 128;  // heavy-id partitions over all owners (target)
 
 __host__ __device__ __forceinline__ int log2_nho(int nho) {
   int b = 0;
@@ -657,7 +658,12 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
   // heavy-id partitions per owner (a power of two, <= kPartMaxHeavy in all)
   int nho = 0;
   if (heavy) {
+    // ~128 heavy ids over all owners: the power-law head is spread over the
+    // owners by the hash, so 128 / nshard per owner covers the same ids as
+    // 128 on one shard, and the digit count (hence the scatter's run length)
+    // stays that of one shard
     nho = 128;
+    while (nho > 1 && (int64_t)nho * nshard > kPartHeavyTotal) nho >>= 1;
     while (nho > 1 && (int64_t)nho * nshard > kPartMaxHeavy) nho >>= 1;
     if ((int64_t)nho * nshard > kPartMaxHeavy) nho = 0;
   }
