@@ -5,6 +5,8 @@
 #include <pybind11/stl.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -865,8 +867,10 @@ std::vector<Tensor> fm_forward(const Tensor& offset, const Tensor& lid,
   auto dual = torch::empty({nrows}, f32);
   auto xv = torch::empty({vstride > 0 ? nrows * vstride : 0}, f32);
   auto part = torch::empty({wh::fm_fwd_partials()}, met.options());
+  // a 5th metric slot asks for the per-minibatch flipped accuracy (linear)
+  const int lossf = (int)loss | (met.numel() >= 5 ? 256 : 0);
   wh::fm_forward(nrows, ptr<int64_t>(offset), ptr<int32_t>(lid), vp, ptr<float>(w_or_hdr), vcp,
-                 (int)vstride, ptr<float>(label), (int)loss, ptr<float>(py), ptr<float>(dual),
+                 (int)vstride, ptr<float>(label), lossf, ptr<float>(py), ptr<float>(dual),
                  vstride > 0 ? ptr<float>(xv) : nullptr, ptr<double>(met), ptr<double>(part),
                  ptr<unsigned int>(dev_ws(offset.device()).fwd_ticket), cur_stream(offset));
   return {py, dual, xv};
@@ -1054,6 +1058,55 @@ void auc_acc(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
   auto scratch = torch::empty({wh::auc_ws_bytes(n)}, py.options().dtype(torch::kUInt8));
   wh::auc_accumulate(ptr<float>(py), ptr<float>(label), n, dev_ws(py.device()).auc.data_ptr(),
                      scratch.data_ptr(), ptr<double>(auc_sum), cur_stream(py));
+}
+
+// The same on a per-device side stream owned here (it waits for the current
+// stream first; auc_join makes the current stream wait for it): the Python
+// form of this (stream objects, wait_stream, a stream context) cost ~30 us
+// of host time per minibatch, which bounds small-minibatch training.
+struct AucSide {
+  c10::hip::HIPStream s;
+  hipEvent_t in, out;
+};
+
+AucSide* auc_side(c10::DeviceIndex d, bool create) {
+  static std::map<int, AucSide*> m;
+  auto it = m.find(d);
+  if (it != m.end()) return it->second;
+  if (!create) return nullptr;
+  auto* a = new AucSide{c10::hip::getStreamFromPool(false, d), nullptr, nullptr};
+  WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->in, hipEventDisableTiming));
+  WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->out, hipEventDisableTiming));
+  m[d] = a;
+  return a;
+}
+
+void auc_acc_side(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
+  CHECK_IN(py, torch::kFloat32);
+  CHECK_IN(label, torch::kFloat32);
+  CHECK_IN(auc_sum, torch::kFloat64);
+  TORCH_CHECK(py.numel() == label.numel(), "auc: py/label size mismatch");
+  TORCH_CHECK(py.numel() < (int64_t)1 << 30, "auc: at most 2^30 examples per call");
+  c10::DeviceGuard g(py.device());
+  AucSide* a = auc_side(py.device().index(), true);
+  WH_HIP_CHECK_HOST(hipEventRecord(a->in, cur_stream(py)));
+  WH_HIP_CHECK_HOST(hipStreamWaitEvent(a->s.stream(), a->in, 0));
+  c10::hip::HIPCachingAllocator::recordStream(py.storage().data_ptr(), a->s);
+  c10::hip::HIPCachingAllocator::recordStream(label.storage().data_ptr(), a->s);
+  c10::hip::HIPStreamGuard sg(a->s);  // the scratch is the side stream's
+  const int64_t n = py.numel();
+  auto scratch = torch::empty({wh::auc_ws_bytes(n)}, py.options().dtype(torch::kUInt8));
+  wh::auc_accumulate(ptr<float>(py), ptr<float>(label), n, dev_ws(py.device()).auc.data_ptr(),
+                     scratch.data_ptr(), ptr<double>(auc_sum), a->s.stream());
+}
+
+void auc_join(const Tensor& auc_sum) {
+  if (!auc_sum.is_cuda()) return;
+  AucSide* a = auc_side(auc_sum.device().index(), false);
+  if (!a) return;
+  c10::DeviceGuard g(auc_sum.device());
+  WH_HIP_CHECK_HOST(hipEventRecord(a->out, a->s.stream()));
+  WH_HIP_CHECK_HOST(hipStreamWaitEvent(cur_stream(auc_sum), a->out, 0));
 }
 
 Tensor auc(const Tensor& py, const Tensor& label) {
@@ -2015,6 +2068,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("dequant_rows", &dequant_rows);
   m.def("trunc_u8", &trunc_u8);
   m.def("auc_acc", &auc_acc);
+  m.def("auc_acc_side", &auc_acc_side);
+  m.def("auc_join", &auc_join);
   m.def("auc_sorted", &auc_sorted);
   m.def("synth_criteo", &synth_criteo);
   m.def("gather_rows", &gather_rows);

@@ -42,9 +42,12 @@ constexpr int kFwdBlocks = 2048;  // persistent forward grid: 8192 waves = 32 pe
 // the forward is one launch: partials are stored write-through (agent-scope
 // atomic stores) and drained before the ticket add, and read back with
 // agent-scope loads (wh_lookback.h: no fences needed in this form).
+// acc5: met[4] += this launch's accuracy, flipped below 0.5 (the reference
+// sums per-minibatch accuracies: learn/base/binary_class_evaluation.h:40-51,
+// learn/linear/loss.h:85)
 __device__ __forceinline__ void block_partials(double* part, double* sh, double a, double b,
                                                double c, double d, double* met,
-                                               unsigned int* ticket) {
+                                               unsigned int* ticket, int acc5 = 0) {
   __shared__ int last;
   double v[4] = {a, b, c, d};
 #pragma unroll
@@ -64,13 +67,18 @@ __device__ __forceinline__ void block_partials(double* part, double* sh, double 
   __syncthreads();
   if (!last) return;
   const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(part);
+  double tot[4];
   for (int i = 0; i < 4; ++i) {
     double s = 0;
     for (int bidx = threadIdx.x; bidx < (int)gridDim.x; bidx += blockDim.x)
       s += __longlong_as_double((long long)lb_load(pp + bidx * 4 + i));
-    const double r = block_sum_d(s, sh);
-    if (threadIdx.x == 0) met[i] += r;
+    tot[i] = block_sum_d(s, sh);
+    if (threadIdx.x == 0) met[i] += tot[i];
     __syncthreads();
+  }
+  if (acc5 && threadIdx.x == 0 && tot[3] > 0) {
+    const double acc = tot[2] / tot[3];
+    met[4] += acc > 0.5 ? acc : 1.0 - acc;
   }
 }
 
@@ -171,7 +179,7 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
                                                      float* __restrict__ py_out,
                                                      float* __restrict__ dual_out,
                                                      float* __restrict__ xv, double* part,
-                                                     double* met, unsigned int* ticket) {
+                                                     double* met, unsigned int* ticket, int acc5) {
   // Persistent waves, one example (row) at a time, software-pipelined over
   // the wave's rows so each row exposes ~one memory round trip instead of
   // four: while row i's embedding rows are gathered, the headers of row i+1,
@@ -293,7 +301,7 @@ __global__ __launch_bounds__(kThreads) void k_fm_fwd(int64_t nrows, const int64_
     bn = b2; en = e2; ln = l2; xn = x2;
     b2 = b3; e2 = e3;
   }
-  block_partials(part, sh, m_objv, m_objw, m_corr, m_n, met, ticket);
+  block_partials(part, sh, m_objv, m_objw, m_corr, m_n, met, ticket, acc5);
 }
 
 // linear model: G lanes stride over one row's non-zeros; persistent over rows
@@ -305,7 +313,7 @@ __global__ __launch_bounds__(kThreads) void k_lin_fwd(int64_t nrows, const int64
                                                       const float* __restrict__ label, int loss,
                                                       float* __restrict__ py_out,
                                                       float* __restrict__ dual_out, double* part,
-                                                      double* met, unsigned int* ticket) {
+                                                      double* met, unsigned int* ticket, int acc5) {
   __shared__ double sh[kThreads / 64];
   const int lane = threadIdx.x & 63, gl = lane & (G - 1);
   const int64_t ngroups = (int64_t)gridDim.x * (kThreads / G);
@@ -327,7 +335,7 @@ __global__ __launch_bounds__(kThreads) void k_lin_fwd(int64_t nrows, const int64
     }
   }
   (void)lane;
-  block_partials(part, sh, m_objv, m_objv, m_corr, m_n, met, ticket);
+  block_partials(part, sh, m_objv, m_objv, m_corr, m_n, met, ticket, acc5);
 }
 
 // ---------------------------------------------------------------- backward
@@ -928,19 +936,21 @@ void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const 
                 float* py, float* dual, float* xv, double* met, double* part,
                 unsigned int* ticket, hipStream_t s) {
   if (nrows <= 0) return;
+  const int acc5 = (loss >> 8) & 1;  // kLossAcc5: met[4] += flipped accuracy
+  loss &= 0xff;
   int nblk;
   if (vstride == 0) {
     constexpr int G = 8;
     nblk = grid_for(nrows * G, kThreads, kFwdBlocks);
     hipLaunchKernelGGL(k_lin_fwd<G>, dim3(nblk), dim3(kThreads), 0, s, nrows, offset, lid, val,
-                       w_or_hdr, label, loss, py, dual, part, met, ticket);
+                       w_or_hdr, label, loss, py, dual, part, met, ticket, acc5);
   } else {
     const int G = vstride / 4;  // vstride <= 256 enforced by the binding
     const float2* hdr = reinterpret_cast<const float2*>(w_or_hdr);
     nblk = grid_for(nrows * 64, kThreads, WH_RESIDENT(G, k_fm_fwd, kFwdBlocks));
     const dim3 grid(nblk), block(kThreads);
     WH_DISPATCH_G(G, k_fm_fwd, grid, block, 0, s, nrows, offset, lid, val, hdr, vc, vstride,
-                  label, loss, py, dual, xv, part, met, ticket);
+                  label, loss, py, dual, xv, part, met, ticket, acc5);
   }
 }
 

@@ -271,7 +271,8 @@ bool ps_pack_gw(const float* gw, int64_t U, int vstride, const int64_t* segS,
 //   difacto: w_or_hdr = hdr[U] float2 {w, vidx}, vc = [m, vstride]
 //   linear (vstride == 0): w_or_hdr = w[U], vc unused
 //   loss: 1 square, 2 logit, 4 squared hinge
-//   met[0..3] += {objv, objv_w, correct(threshold 0), n}  (double)
+//   met[0..3] += {objv, objv_w, correct(threshold 0), n}  (double); with
+//   loss | 256, met[4] += this minibatch's accuracy flipped below 0.5
 //   part: scratch of fm_fwd_partials() doubles (per-block metric partials)
 int64_t fm_fwd_partials();
 void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,

@@ -39,7 +39,7 @@ def localize_pipelined(lrn, keys, offset, val, next_batch):
             # minibatch's localize finish, which empties the table slot the
             # job reuses); the job's finish host-syncs its event before any
             # compute-stream kernel reads its buffers.
-            cur = torch.cuda.current_stream(nk.device)
+            cur = torch.cuda.current_stream(nk.device.index)  # (an int: the fast path)
             side = _loc_stream(nk.device)
             side.wait_stream(cur)
             if ready is not None:
@@ -55,7 +55,7 @@ def localize_pipelined(lrn, keys, offset, val, next_batch):
             lrn._job = (nk, job)
             return loc
         if ready is not None and nk.is_cuda:
-            cur = torch.cuda.current_stream(nk.device)
+            cur = torch.cuda.current_stream(nk.device.index)  # (an int: the fast path)
             cur.wait_event(ready)
             for t in (nk, no, nv):  # produced on another stream, consumed here
                 if t is not None:

@@ -26,12 +26,10 @@ class LinearLearner:
         self.seed = seed
         self.alpha = conf.lr_eta
         self.beta = conf.lr_beta
-        self.met = torch.zeros(4, dtype=torch.float64, device=self.device)
-        # this minibatch's [objv, -, correct, count] and the sum of the
-        # per-minibatch accuracies (flipped below 0.5 per minibatch, as
-        # learn/base/binary_class_evaluation.h:40-51 + linear/loss.h:85 do)
-        self.mb_met = torch.zeros(4, dtype=torch.float64, device=self.device)
-        self.acc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
+        # [objv, -, correct, count, sum of per-minibatch accuracies flipped
+        # below 0.5] (learn/base/binary_class_evaluation.h:40-51 +
+        # learn/linear/loss.h:85), all summed by the forward kernel
+        self.met = torch.zeros(5, dtype=torch.float64, device=self.device)
         self.auc_sum = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.n_mb = 0
         self.max_key = 0  # set from the -max_key system flag (apps/ps_app.py)
@@ -56,14 +54,10 @@ class LinearLearner:
             w = self.kv.linear_pull(sess)
         with trace.span("forward"):
             py, dual, _ = ops.fm_forward(offset, lid, val, w, None, 0, label, self.conf.loss,
-                                         self.mb_met)
+                                         self.met)
             ops.auc_acc(py, label, self.auc_sum)
-            if label.numel():
-                a = self.mb_met[2:3] / self.mb_met[3:4]
-                self.acc_sum += torch.where(a > 0.5, a, 1 - a)
-                self.n_mb += 1
-            self.met += self.mb_met
-            self.mb_met.zero_()
+        if label.numel():
+            self.n_mb += 1
         if train:
             with trace.span("backward"):
                 grad, _ = ops.fm_backward(csc_off, csc_row, csc_val, dual, None, w, None, 0)
@@ -88,9 +82,8 @@ class LinearLearner:
         st = self.store.stats
         new_w = float(st.tolist()[0])
         self.store.reset_stats(0, 1)
-        prog = [m[0], float(self.acc_sum.item()), a, float(self.n_mb), m[3], new_w]
+        prog = [m[0], m[4], a, float(self.n_mb), m[3], new_w]
         self.met.zero_()
-        self.acc_sum.zero_()
         self.auc_sum.zero_()
         self.n_mb = 0
         return prog

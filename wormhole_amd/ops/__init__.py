@@ -154,31 +154,19 @@ def auc(py, label):
     return ref.auc(py, label)
 
 
-_side = {}
 
-
-def _side_stream(dev):
-    s = _side.get(dev)
-    if s is None:
-        s = _side[dev] = torch.cuda.Stream(device=dev)
-    return s
 
 
 def auc_acc(py, label, auc_sum):
     """auc_sum (float64 [1]) += exact AUC of the minibatch, on the device.
 
     The AUC chain (min/max, bucket, one-block scan, place, count: ~60 us of
-    small, latency-bound launches) runs on a side stream, overlapped with the
+    small, latency-bound launches) runs on a side stream owned by the native
+    layer (it waits for the current stream first), overlapped with the
     backward pass that follows on the compute stream; :func:`auc_join` makes
     the current stream wait for it before ``auc_sum`` is read or reset."""
     if _gpu(py):
-        main = torch.cuda.current_stream(py.device)
-        side = _side_stream(py.device)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            _native.hip().auc_acc(py, label, auc_sum)
-        py.record_stream(side)
-        label.record_stream(side)
+        _native.hip().auc_acc_side(py, label, auc_sum)
         return auc_sum
     auc_sum += ref.auc(py, label)
     return auc_sum
@@ -186,8 +174,8 @@ def auc_acc(py, label, auc_sum):
 
 def auc_join(auc_sum):
     """Order the current stream after every queued :func:`auc_acc`."""
-    if auc_sum.is_cuda and auc_sum.device in _side:
-        torch.cuda.current_stream(auc_sum.device).wait_stream(_side[auc_sum.device])
+    if auc_sum.is_cuda:
+        _native.hip().auc_join(auc_sum)
 
 
 def quant_rows(x, nb, seed):

@@ -136,6 +136,9 @@ def fm_forward(offset, lid, val, w_or_hdr, vc, vstride, label, loss, met):
     met[1] += objw.double().sum().to(met.device)
     met[2] += correct.double().sum().to(met.device)
     met[3] += float(nrows)
+    if met.numel() >= 5 and nrows > 0:  # per-minibatch accuracy, flipped below 0.5
+        acc = float(correct.double().sum()) / nrows
+        met[4] += acc if acc > 0.5 else 1.0 - acc
     return py, dual, xv.reshape(-1)
 
 
