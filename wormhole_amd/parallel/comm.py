@@ -202,8 +202,8 @@ class Comm:
         for d in x.shape[1:]:
             width *= int(d)
         out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-        if x.numel() == 0 and out.numel() == 0:
-            return out, _Done()
+        # (issued even when this rank moves nothing: a collective every rank
+        # must join; skipping it here would hang the peers)
         work = dist.all_to_all_single(out.view(-1), x.view(-1),
                                       [r * width for r in recv_rows],
                                       [s_ * width for s_ in send_rows], async_op=True)
