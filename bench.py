@@ -69,6 +69,9 @@ def main():
                     help="P > 1: run the multi-shard exchange path with P virtual shards "
                          "in this one process (identity transport; measures that path's "
                          "device + host overhead on one GPU)")
+    ap.add_argument("--loopback-rccl", action="store_true",
+                    help="with --loopback: issue every exchange as a real RCCL all-to-all on a "
+                         "1-rank group (the RCCL stream/async semantics of the multi-GPU step)")
     ap.add_argument("--max-concurrency", type=int, default=2,
                     help="minibatches in flight per worker (reference default 2): with >= 2 "
                          "the multi-shard step is pipelined one minibatch deep")
@@ -87,7 +90,7 @@ def main():
         args.cap, args.vcap = min(args.cap, 1 << 16), min(args.vcap, 1 << 14)
     if args.loopback > 1:
         from wormhole_amd.parallel.comm import LoopbackComm
-        comm = LoopbackComm(args.loopback, device)
+        comm = LoopbackComm(args.loopback, device, rccl=args.loopback_rccl)
     else:
         comm = Comm(device)
     n = 1 if args.loopback > 1 else comm.size  # GPUs doing work
@@ -199,7 +202,8 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": vs, "dtype": "fp32",
             "data": "synthetic (Criteo-1TB-shaped: 13 int + 26 cat fields, power-law, device-generated each step); random-init model",
             "config": {"model": model, "global_batch": args.batch * n, "seq_len": 39,
-                       "parallelism": ("loopback%d(1 GPU)" % args.loopback if args.loopback > 1
+                       "parallelism": ("loopback%d%s(1 GPU)" % (args.loopback, "-rccl" if args.loopback_rccl else "")
+                                       if args.loopback > 1
                                        else "dp%d+kvshard%d" % (n, n)),
                        "minibatch_per_gpu": args.batch, "threshold": 100, "nnz_per_example": 39},
             "train_logloss": logloss, "train_auc": auc,

@@ -271,13 +271,38 @@ class LoopbackComm(Comm):
     --loopback P``); it owns every shard itself, so its table holds the whole
     key space like a 1-rank run."""
 
-    def __init__(self, nshard, device=None):
+    def __init__(self, nshard, device=None, rccl=False):
         self.rank = 0
         self.size = int(nshard)
         self.device = torch.device(device if device is not None else "cpu")
         self.backend = "loopback"
         self.stage = False
         self.pg = None
+        # rccl=True: every exchange still moves this process's own bytes, but
+        # through a real RCCL all-to-all on a 1-rank process group (async work
+        # handles, the process group's stream, input lifetimes: exactly the
+        # calls Comm makes over xGMI), so the RCCL stream semantics of the
+        # multi-shard step are exercised on a one-GPU box, where RCCL refuses
+        # two ranks on one device.
+        self.rccl = bool(rccl) and self.device.type == "cuda"
+        if self.rccl:
+            if not dist.is_initialized():
+                os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+                os.environ.setdefault("MASTER_PORT", "29531")
+                dist.init_process_group(backend="nccl", rank=0, world_size=1,
+                                        device_id=self.device)
+            assert dist.get_world_size() == 1, "rccl loopback needs a 1-rank group"
+            self.pg = dist.group.WORLD
+            self.backend = "loopback-rccl"
+
+    def _a2a(self, x, async_op):
+        """Identity exchange through RCCL (1-rank all-to-all = self copy)."""
+        x = x.contiguous()
+        out = torch.empty_like(x)
+        if x.numel() == 0:
+            return out, _Done()
+        work = dist.all_to_all_single(out.view(-1), x.view(-1), async_op=async_op)
+        return out, (_Keep(work, x) if async_op else _Done())
 
     def barrier(self):
         pass
@@ -299,17 +324,33 @@ class LoopbackComm(Comm):
 
     def all_to_all_v(self, x, send_rows, recv_rows):
         assert list(send_rows) == list(recv_rows), "loopback exchange must be symmetric"
+        if self.rccl and x.is_cuda:
+            return self._a2a(x, False)[0]
         return x
 
     def all_to_all_v_async(self, x, send_rows, recv_rows):
-        return self.all_to_all_v(x, send_rows, recv_rows), _Done()
+        assert list(send_rows) == list(recv_rows), "loopback exchange must be symmetric"
+        if self.rccl and x.is_cuda:
+            return self._a2a(x, True)
+        return x, _Done()
 
     def all_to_all_v_multi(self, items, async_op=False):
+        if self.rccl:
+            outs, hs = [], []
+            for x, s, r in items:
+                assert list(s) == list(r), "loopback exchange must be symmetric"
+                o, h = self._a2a(x, async_op)
+                outs.append(o)
+                hs.append(h)
+            return (outs, _Reqs(hs, None)) if async_op else outs
         outs = [self.all_to_all_v(x, s, r) for x, s, r in items]
         return (outs, _Done()) if async_op else outs
 
     def exchange_counts_dev(self, send_dev):
+        if self.rccl and send_dev.is_cuda:
+            return self._a2a(send_dev, False)[0]
         return send_dev.clone()
 
     def finalize(self):
-        pass
+        if self.rccl and dist.is_initialized():
+            dist.destroy_process_group()
