@@ -66,9 +66,16 @@ def localize_pipelined(lrn, keys, offset, val, next_batch):
     return loc
 
 
-# measured slower on one MI355X (106 vs 112 M ex/s: the concurrent hash
-# insert costs the gather-bound FM kernels more than it hides): opt-in only
-_OVERLAP = os.environ.get("WH_LOCALIZE_STREAM", "0") != "0"
+# On by default since the partitioned localize (LDS dedup, no global
+# atomics): DiFacto 117.5 -> 127 M ex/s on one MI355X (tools/gpu/env_ab.sh).
+# With the round-1 hash localize it was slower (106 vs 112: its concurrent
+# atomic inserts cost the gather-bound FM kernels more than they hid).
+# Memory safety of the side-stream outputs: they are allocated on the side
+# stream and read on the compute stream; the side stream's next job first
+# waits for the compute stream (side.wait_stream(cur) below), so a block the
+# allocator hands back to the side stream is never rewritten before the
+# compute-stream kernels that read it have run.
+_OVERLAP = os.environ.get("WH_LOCALIZE_STREAM", "1") != "0"
 _streams = {}
 
 
