@@ -36,6 +36,7 @@ still holds bwd(i-1), so S never drains. ``max_concurrency = 1`` gives the
 strict (staleness 0) order at the cost of one pipeline drain per step.
 """
 import contextlib
+import os
 
 import numpy as np
 import torch
@@ -43,6 +44,11 @@ import torch
 from .. import _native, ops
 
 TRAIN, VAL, PRED = 0, 1, 2
+# opt-in: measured slower here than on one shard (loopback P=8: 106 with vs
+# 108 M ex/s without, tools/gpu/r2_psxls.sh): in this step the localize
+# already sits between the owner open and the backward on S, and running it
+# concurrently only stretches the backward it would overlap
+_LOC_STREAM = os.environ.get("WH_PSX_LOCALIZE_STREAM", "0") != "0"
 
 
 def _cdiv(a, b):
@@ -116,6 +122,11 @@ class PsxDifacto:
         self.dev = lrn.device
         self.cuda = self.dev.type == "cuda"
         self.cs = torch.cuda.Stream(device=self.dev) if self.cuda else None
+        # the next minibatch's localize runs on its own stream, concurrently
+        # with the previous minibatch's backward on S (as on one shard,
+        # models/_pipeline.py), when WH_PSX_LOCALIZE_STREAM=1
+        self.ls = (torch.cuda.Stream(device=self.dev)
+                   if self.cuda and _LOC_STREAM else None)
         self.S = torch.cuda.current_stream(self.dev) if self.cuda else None
         self.pins = _PinRing(self.dev) if self.cuda else None
         self.events = _EventRing() if self.cuda else None
@@ -139,6 +150,9 @@ class PsxDifacto:
             return
         S = self._S()
         self.cs.wait_stream(S)
+        cur = torch.cuda.current_stream(self.dev)
+        if cur != S:  # called from a localize job on its own stream
+            self.cs.wait_stream(cur)
         for t in inputs:
             if t is not None and t.is_cuda:
                 t.record_stream(self.cs)
@@ -164,6 +178,26 @@ class PsxDifacto:
 
     def _begin(self, keys, offset, val, carried, ready=None):
         lrn = self.lrn
+        if self.cuda and self.ls is not None:
+            # Outputs are allocated on ls and read on S; ls first waits for
+            # everything queued on S, so a block the allocator hands back to
+            # ls is rewritten only after the S kernels that read it have run.
+            # S itself reads the job's outputs only after the host has waited
+            # for the job's count read (which follows `ready` on ls).
+            S, ls = self._S(), self.ls
+            ls.wait_stream(S)
+            if ready is not None:
+                ls.wait_event(ready)
+            for t in (keys, offset, val):
+                if t is not None:
+                    t.record_stream(ls)
+                    t.record_stream(S)
+            with torch.cuda.stream(ls):
+                k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
+                job = _native.hip().LocalizeJob(k, offset, val, self.P, int(self.uhint),
+                                                self._exchange(carried))
+            self.job = (keys, job, carried)
+            return
         if ready is not None and self.cuda:
             S = self._S()
             S.wait_event(ready)
