@@ -21,49 +21,68 @@ from .. import ops
 
 
 def localize_pipelined(lrn, keys, offset, val, next_batch):
+    loc = localize_current(lrn, keys, offset, val)
+    if next_batch is not None:
+        begin_next(lrn, next_batch, loc[0].numel())
+    return loc
+
+
+def localize_current(lrn, keys, offset, val):
+    """This minibatch's localize: finish the job begun for it, or run it."""
     job, lrn._job = lrn._job, None
     if job is not None and job[0] is keys:
-        loc = ops.localize_finish(job[1])
-    else:
-        k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
-        loc = ops.localize(k, offset, val, lrn.kv.nshard, lrn.uhint,
-                           exchange=lrn.kv.count_exchange())
-    if next_batch is not None:
-        nk, no, nv = next_batch[:3]
-        ready = next_batch[3] if len(next_batch) > 3 else None
-        if nk.is_cuda and _OVERLAP:
-            # The next minibatch's hash insert + owner grouping run on their
-            # own stream, concurrently with this minibatch's pull / forward /
-            # backward on the compute stream. The side stream first waits for
-            # everything queued on the compute stream so far (this
-            # minibatch's localize finish, which empties the table slot the
-            # job reuses); the job's finish host-syncs its event before any
-            # compute-stream kernel reads its buffers.
-            cur = torch.cuda.current_stream(nk.device.index)  # (an int: the fast path)
-            side = _loc_stream(nk.device)
-            side.wait_stream(cur)
-            if ready is not None:
-                side.wait_event(ready)
-            for t in (nk, no, nv):
-                if t is not None:
-                    t.record_stream(side)
-                    t.record_stream(cur)
-            with torch.cuda.stream(side):
-                k = ops.key_mod(nk, lrn.max_key) if lrn.max_key else nk
-                job = ops.localize_begin(k, no, nv, lrn.kv.nshard, loc[0].numel(),
-                                         exchange=lrn.kv.count_exchange())
-            lrn._job = (nk, job)
-            return loc
-        if ready is not None and nk.is_cuda:
-            cur = torch.cuda.current_stream(nk.device.index)  # (an int: the fast path)
-            cur.wait_event(ready)
-            for t in (nk, no, nv):  # produced on another stream, consumed here
-                if t is not None:
-                    t.record_stream(cur)
-        k = ops.key_mod(nk, lrn.max_key) if lrn.max_key else nk
-        lrn._job = (nk, ops.localize_begin(k, no, nv, lrn.kv.nshard, loc[0].numel(),
-                                           exchange=lrn.kv.count_exchange()))
-    return loc
+        return ops.localize_finish(job[1])
+    k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
+    return ops.localize(k, offset, val, lrn.kv.nshard, lrn.uhint,
+                        exchange=lrn.kv.count_exchange())
+
+
+# DiFacto begins the next minibatch's localize right AFTER enqueueing this
+# minibatch's pull (not before it): the host reaches the pull launch sooner
+# after its count read, and the side-stream job then starts behind the pull
+# on the compute stream, still well ahead of the next count read. Measured
+# (tools/gpu/r2_late.sh): DiFacto 127.0 -> 131.7 M ex/s; the linear model,
+# whose step is short enough that the job's count read comes late, is 5 %
+# slower this way and keeps the early begin (localize_pipelined).
+BEGIN_LATE = os.environ.get("WH_BEGIN_LATE", "1") != "0"
+
+
+def begin_next(lrn, next_batch, uhint):
+    """Begin the localize of ``next_batch`` (see the module docstring);
+    ``uhint``: this minibatch's unique-id count (sizes the job's table)."""
+    nk, no, nv = next_batch[:3]
+    ready = next_batch[3] if len(next_batch) > 3 else None
+    if nk.is_cuda and _OVERLAP:
+        # The next minibatch's partitioned localize runs on its own stream,
+        # concurrently with this minibatch's forward / backward / push on the
+        # compute stream. The side stream first waits for everything queued
+        # on the compute stream so far (memory safety, below); the job's
+        # finish host-syncs its event before any compute-stream kernel reads
+        # its buffers.
+        cur = torch.cuda.current_stream(nk.device.index)  # (an int: the fast path)
+        side = _loc_stream(nk.device)
+        side.wait_stream(cur)
+        if ready is not None:
+            side.wait_event(ready)
+        for t in (nk, no, nv):
+            if t is not None:
+                t.record_stream(side)
+                t.record_stream(cur)
+        with torch.cuda.stream(side):
+            k = ops.key_mod(nk, lrn.max_key) if lrn.max_key else nk
+            job = ops.localize_begin(k, no, nv, lrn.kv.nshard, uhint,
+                                     exchange=lrn.kv.count_exchange())
+        lrn._job = (nk, job)
+        return
+    if ready is not None and nk.is_cuda:
+        cur = torch.cuda.current_stream(nk.device.index)  # (an int: the fast path)
+        cur.wait_event(ready)
+        for t in (nk, no, nv):  # produced on another stream, consumed here
+            if t is not None:
+                t.record_stream(cur)
+    k = ops.key_mod(nk, lrn.max_key) if lrn.max_key else nk
+    lrn._job = (nk, ops.localize_begin(k, no, nv, lrn.kv.nshard, uhint,
+                                       exchange=lrn.kv.count_exchange()))
 
 
 # On by default since the partitioned localize (LDS dedup, no global

@@ -14,7 +14,7 @@ learn/difacto/async_sgd.h:363-425), re-expressed on the GPU:
 import torch
 
 from .. import ops
-from ._pipeline import localize_pipelined
+from ._pipeline import BEGIN_LATE, begin_next, localize_current, localize_pipelined
 from ..kv import ShardedKV, make_store
 from ..utils import trace
 
@@ -77,7 +77,10 @@ class DifactoLearner:
             py = self.psx.evaluate(keys, offset, val, label)
             return py if wtype == PRED else None
         with trace.span("localize"):
-            loc = self._localize(keys, offset, val, next_batch)
+            if BEGIN_LATE:
+                loc = localize_current(self, keys, offset, val)
+            else:
+                loc = self._localize(keys, offset, val, next_batch)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
         self.uhint = uniq.numel()
         push_cnt = train and data_pass == 0 and self.dim > 0
@@ -86,6 +89,8 @@ class DifactoLearner:
                 uniq, owner_cnt, train, ucnt if push_cnt else None, self.hp, self.threshold,
                 self.l1_shrk, self.seed, recv=loc[7] if len(loc) > 7 else None)
         self.last_sizes = (uniq.numel(), sess.m)  # (unique keys, embedding rows; device)
+        if BEGIN_LATE and next_batch is not None:  # after the pull launch
+            begin_next(self, next_batch, uniq.numel())
         if self.vstride == 0:  # no embedding: a plain linear model over w
             hdr, vc = hdr[:, 0].contiguous(), None
         with trace.span("forward"):
