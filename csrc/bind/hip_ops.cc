@@ -171,9 +171,15 @@ Tensor& loc_timing_buf() {
 
 class LocalizeJob {
  public:
+  // defer_exchange: enqueue the localize kernels now, but call the count
+  // exchange (and its async host read) only at exchange(): the multi-shard
+  // step begins the next minibatch's localize early on its own stream and
+  // issues its count collective later, once the payload it carries (the V
+  // row counts of this minibatch's open) exists.
   LocalizeJob(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
-              int64_t nshard, int64_t hint, py::object exchange)
-      : keys_(keys), offset_(offset), nshard_(nshard), exchange_(exchange) {
+              int64_t nshard, int64_t hint, py::object exchange, bool defer_exchange = false)
+      : keys_(keys), offset_(offset), nshard_(nshard), exchange_(exchange),
+        defer_(defer_exchange) {
     CHECK_IN(keys, torch::kInt64);
     CHECK_IN(offset, torch::kInt64);
     TORCH_CHECK(nshard >= 1 && nshard <= 1024, "nshard out of range");
@@ -223,9 +229,19 @@ class LocalizeJob {
   // begin at the safe table size if any rank overflowed) and returns the
   // host (owner counts [nshard], everything the exchange appended). A
   // caller may enqueue unrelated work between counts() and finish().
+  // the deferred count exchange (a no-op unless defer_exchange was given)
+  void exchange() {
+    TORCH_CHECK(!done_, "localize job already finished");
+    if (!defer_ || exchanged_) return;
+    c10::DeviceGuard g(keys_.device());
+    exchanged_ = true;
+    exchange_and_read(owner_cnt_, cur_stream(keys_));
+  }
+
   std::vector<Tensor> counts() {
     TORCH_CHECK(!done_, "localize job already finished");
     if (owner_cnt_h_.defined()) return {owner_cnt_h_, recv_h_};
+    TORCH_CHECK(!defer_ || exchanged_, "localize: counts() before the deferred exchange()");
     c10::DeviceGuard g(keys_.device());
     DevWs& ws = dev_ws(keys_.device());
     while (true) {
@@ -404,7 +420,10 @@ class LocalizeJob {
     } else {
       owner_cnt = enqueue_hash(ws, s, i32, i64);
     }
-    exchange_and_read(owner_cnt, s);
+    owner_cnt_ = owner_cnt;
+    // (an overflow retry from counts() exchanges at once: every rank retries
+    // there together)
+    if (!defer_ || exchanged_) exchange_and_read(owner_cnt, s);
   }
 
   Tensor enqueue_hash(DevWs& ws, hipStream_t s, const torch::TensorOptions& i32,
@@ -481,6 +500,8 @@ class LocalizeJob {
   Tensor keys_, offset_, val_;
   int64_t nshard_, nnz_ = 0, safe_ = 0, tsize_ = 0, nrecv_ = 0, stride_ = 2;
   py::object exchange_;
+  bool defer_ = false, exchanged_ = false;
+  Tensor owner_cnt_;
   int tab_ = -1;
   bool done_ = false;
   Tensor tkeys_, slot_of_, blkoff_, dev_counts_, host_, owner_cnt_h_, recv_h_;
@@ -2046,9 +2067,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("scan_excl", &scan_excl);
   py::class_<LocalizeJob>(m, "LocalizeJob")
       .def(py::init<const Tensor&, const Tensor&, const c10::optional<Tensor>&, int64_t, int64_t,
-                    py::object>(),
+                    py::object, bool>(),
            py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(), py::arg("nshard") = 1,
-           py::arg("hint") = 0, py::arg("exchange") = py::none())
+           py::arg("hint") = 0, py::arg("exchange") = py::none(),
+           py::arg("defer_exchange") = false)
+      .def("exchange", &LocalizeJob::exchange)
       .def("counts", &LocalizeJob::counts)
       .def("finish", &LocalizeJob::finish);
   m.def("loc_timing_read", []() { return loc_timing_buf().clone(); });

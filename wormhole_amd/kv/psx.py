@@ -44,11 +44,20 @@ import torch
 from .. import _native, ops
 
 TRAIN, VAL, PRED = 0, 1, 2
-# opt-in: measured slower here than on one shard (loopback P=8: 106 with vs
-# 108 M ex/s without, tools/gpu/r2_psxls.sh): in this step the localize
-# already sits between the owner open and the backward on S, and running it
-# concurrently only stretches the backward it would overlap
-_LOC_STREAM = os.environ.get("WH_PSX_LOCALIZE_STREAM", "0") != "0"
+# Where the next minibatch's localize runs (WH_PSX_LOCALIZE):
+#   "s"     on the compute stream S, between the owner open and the backward;
+#   "ls"    on its own stream at the same point (measured slower: loopback
+#           P=8 106 vs 108 M ex/s -- it only stretches the backward it
+#           overlaps, and S drains while the host waits for its count read);
+#   "early" on its own stream, begun as soon as this minibatch's localize is
+#           finished (overlapping the forward, the owner push and the open),
+#           with its count collective C0 issued after the open (deferred
+#           exchange: C0 carries the open's V row counts). The default on
+#           GPUs: loopback P=8 108.2 -> 116.4 M ex/s, RCCL loopback 88.1 ->
+#           92.5 (tools/gpu/r2_early.sh).
+_LOC_MODE = os.environ.get("WH_PSX_LOCALIZE", "early")
+_LOC_STREAM = _LOC_MODE in ("ls", "early")
+_LOC_EARLY = _LOC_MODE == "early"
 
 
 def _cdiv(a, b):
@@ -176,7 +185,7 @@ class PsxDifacto:
             return payload
         return ex
 
-    def _begin(self, keys, offset, val, carried, ready=None):
+    def _begin(self, keys, offset, val, carried, ready=None, defer=False):
         lrn = self.lrn
         if self.cuda and self.ls is not None:
             # Outputs are allocated on ls and read on S; ls first waits for
@@ -195,7 +204,7 @@ class PsxDifacto:
             with torch.cuda.stream(ls):
                 k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
                 job = _native.hip().LocalizeJob(k, offset, val, self.P, int(self.uhint),
-                                                self._exchange(carried))
+                                                self._exchange(carried), defer)
             self.job = (keys, job, carried)
             return
         if ready is not None and self.cuda:
@@ -217,9 +226,16 @@ class PsxDifacto:
             job = tuple(out)
         self.job = (keys, job, carried)
 
+    def _exchange_deferred(self):
+        """Issue C0 of an early-begun localize (after the open it carries)."""
+        if self.job is not None and self.ls is not None and not isinstance(self.job[1], tuple):
+            with torch.cuda.stream(self.ls):
+                self.job[1].exchange()  # (no-op unless the job deferred it)
+
     def _counts(self):
         """The one host read of the step (count exchange C0 of the begun
         localize): returns (send, recv); fills the carried step's V counts."""
+        self._exchange_deferred()
         keys, job, carried = self.job
         if isinstance(job, tuple):
             oc, tail = job[2], job[7]
@@ -392,6 +408,11 @@ class PsxDifacto:
         if prev is not None:
             self._c2(prev)  # transfers while this minibatch's localize finishes
         self._set_loc(st, self._finish(), offset, val)
+        early = _LOC_EARLY and self.cuda and next_batch is not None
+        if early:  # next minibatch's localize kernels now; its C0 after the open
+            nk, no, nv = next_batch[:3]
+            self._begin(nk, no, nv, st, next_batch[3] if len(next_batch) > 3 else None,
+                        defer=True)
         self._c1(st)        # transfers while the previous minibatch computes
         if prev is not None:
             self._reply(prev)
@@ -403,7 +424,9 @@ class PsxDifacto:
             self.push = None
         self._open(st, True)
         self.pull = st
-        if next_batch is not None:
+        if early:
+            self._exchange_deferred()
+        elif next_batch is not None:
             nk, no, nv = next_batch[:3]
             self._begin(nk, no, nv, st, next_batch[3] if len(next_batch) > 3 else None)
         if self.tau == 1 and prev is not None and prev.train:
