@@ -327,6 +327,70 @@ void register_all(py::module& m) {
     if (n != size) throw std::runtime_error("lz4: corrupt input");
     return py::bytes(out);
   });
+  // ps-lite COMPRESSING filter for host (gloo) transfers: each peer's chunk
+  // of an all-to-all-v LZ4-compressed on its own; a chunk LZ4 cannot shrink
+  // travels raw (its size negated). Returns (packed bytes, signed sizes).
+  m.def("lz4_pack", [](const Tensor& src, const std::vector<int64_t>& nbytes) {
+    TORCH_CHECK(src.device().is_cpu() && src.is_contiguous() && src.scalar_type() == torch::kUInt8,
+                "lz4_pack: contiguous uint8 CPU tensor");
+    int64_t bound = 0, total = 0;
+    for (int64_t n : nbytes) {
+      TORCH_CHECK(n >= 0 && n < (int64_t)INT32_MAX / 2, "lz4_pack: chunk size out of range");
+      bound += LZ4CompressBound((int)n);
+      total += n;
+    }
+    TORCH_CHECK(total == src.numel(), "lz4_pack: chunk sizes do not cover the input");
+    Tensor out = torch::empty({std::max<int64_t>(bound, 1)}, torch::kUInt8);
+    std::vector<int64_t> csz(nbytes.size());
+    int64_t used = 0;
+    {
+      py::gil_scoped_release nogil;
+      const char* in = reinterpret_cast<const char*>(src.data_ptr());
+      char* o = reinterpret_cast<char*>(out.data_ptr());
+      for (size_t i = 0; i < nbytes.size(); ++i) {
+        const int n = (int)nbytes[i];
+        int c = n > 0 ? LZ4Compress(in, o + used, n, LZ4CompressBound(n)) : 0;
+        if (n > 0 && (c <= 0 || c >= n)) {  // incompressible: stored
+          std::memcpy(o + used, in, n);
+          csz[i] = -(int64_t)n;
+          c = n;
+        } else {
+          csz[i] = c;
+        }
+        in += n;
+        used += c;
+      }
+    }
+    return py::make_tuple(out.narrow(0, 0, used), csz);
+  });
+  m.def("lz4_unpack", [](const Tensor& packed, const std::vector<int64_t>& csz,
+                         const std::vector<int64_t>& nbytes, Tensor dst) {
+    TORCH_CHECK(packed.device().is_cpu() && packed.is_contiguous() &&
+                    dst.device().is_cpu() && dst.is_contiguous() &&
+                    packed.scalar_type() == torch::kUInt8 && dst.scalar_type() == torch::kUInt8,
+                "lz4_unpack: contiguous uint8 CPU tensors");
+    TORCH_CHECK(csz.size() == nbytes.size(), "lz4_unpack: size lists differ");
+    int64_t need = 0, have = 0;
+    for (size_t i = 0; i < csz.size(); ++i) {
+      need += std::llabs(csz[i]);
+      have += nbytes[i];
+    }
+    TORCH_CHECK(need == packed.numel() && have == dst.numel(), "lz4_unpack: sizes do not match");
+    py::gil_scoped_release nogil;
+    const char* in = reinterpret_cast<const char*>(packed.data_ptr());
+    char* o = reinterpret_cast<char*>(dst.data_ptr());
+    for (size_t i = 0; i < csz.size(); ++i) {
+      const int64_t n = nbytes[i], c = csz[i];
+      if (c < 0) {
+        if (-c != n) throw std::runtime_error("lz4_unpack: stored chunk size mismatch");
+        std::memcpy(o, in, n);
+      } else if (n > 0) {
+        if (LZ4Decompress(in, o, (int)c, (int)n) != n) throw std::runtime_error("lz4: corrupt chunk");
+      }
+      in += std::llabs(c);
+      o += n;
+    }
+  });
   m.def("match_file", &MatchFile);
   m.def("resolve_path", &ResolvePath);
   m.def("list_directory", &ListDirectory);

@@ -33,6 +33,9 @@ class DifactoLearner:
         self.store = make_store(cap, vcap, self.dim, self.device)
         self.kv = ShardedKV(self.store, comm, nshard, fixed_bytes=getattr(conf, "fixed_bytes", 0),
                             seed=seed)
+        # ps-lite COMPRESSING filter on the pushes / pulls (host transfers)
+        if hasattr(comm, "set_compression"):
+            comm.set_compression(getattr(conf, "msg_compression", False))
         self.seed = seed
         self.l1_shrk = bool(conf.l1_shrk)
         if emb is not None:

@@ -23,6 +23,9 @@ class LinearLearner:
         self.device = torch.device(device)
         self.store = make_store(cap, 0, 0, self.device)
         self.kv = ShardedKV(self.store, comm, nshard)
+        # ps-lite COMPRESSING filter on the pushes / pulls (host transfers)
+        if hasattr(comm, "set_compression"):
+            comm.set_compression(getattr(conf, "msg_compression", False))
         self.seed = seed
         self.alpha = conf.lr_eta
         self.beta = conf.lr_beta

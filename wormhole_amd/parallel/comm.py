@@ -94,6 +94,10 @@ class Comm:
         # staged through host memory around every transfer
         self.stage = backend == "gloo" and self.device.type == "cuda"
         self.pg = None
+        # ps-lite COMPRESSING filter (msg_compression): LZ4 per peer chunk on
+        # HOST transfers (gloo; also the staged GPU rehearsal). Device
+        # transfers over RCCL/xGMI stay raw (docs/linear.md msg_compression).
+        self.compress = False
         if self.size > 1 and init:
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -168,6 +172,35 @@ class Comm:
         dist.all_to_all_single(r, s)
         return r.tolist()
 
+    def set_compression(self, on):
+        """Enable the LZ4 filter (applies to host transfers only)."""
+        self.compress = bool(on) and self.backend == "gloo"
+
+    def _a2a_lz4(self, x, send_rows, recv_rows):
+        """all_to_all_v of a CPU tensor with every peer chunk LZ4-compressed
+        (ps-lite COMPRESSING, learn/linear/async_sgd.h:290-301): the signed
+        compressed sizes are exchanged first, then the packed bytes."""
+        from .. import _native
+        host = _native.host()
+        x = x.contiguous()
+        row = x.element_size()
+        for d in x.shape[1:]:
+            row *= int(d)
+        sb = [int(r) * row for r in send_rows]
+        rb = [int(r) * row for r in recv_rows]
+        packed, csz = host.lz4_pack(x.view(-1).view(torch.uint8) if x.numel() else
+                                    torch.empty(0, dtype=torch.uint8), sb)
+        rcsz = torch.empty(self.size, dtype=torch.int64)
+        dist.all_to_all_single(rcsz, torch.tensor(csz, dtype=torch.int64))
+        rc = rcsz.tolist()
+        got = torch.empty(sum(abs(c) for c in rc), dtype=torch.uint8)
+        dist.all_to_all_single(got, packed.contiguous(), [abs(c) for c in rc],
+                               [abs(c) for c in csz])
+        out = torch.empty((sum(recv_rows),) + tuple(x.shape[1:]), dtype=x.dtype)
+        host.lz4_unpack(got, rc, rb, out.view(-1).view(torch.uint8) if out.numel() else
+                        torch.empty(0, dtype=torch.uint8))
+        return out
+
     def all_to_all_v(self, x, send_rows, recv_rows):
         """Row-wise all-to-all-v: rank p receives send_rows[p] rows of x from
         this rank.  x may be 1-D or 2-D [rows, width]."""
@@ -175,6 +208,8 @@ class Comm:
             return x
         if self.stage and x.is_cuda:
             return self.all_to_all_v(x.cpu(), send_rows, recv_rows).to(x.device)
+        if self.compress and not x.is_cuda:
+            return self._a2a_lz4(x, send_rows, recv_rows)
         width = x[0].numel() if x.dim() > 1 and x.shape[0] > 0 else (
             x.shape[1] if x.dim() > 1 else 1)
         shape = (sum(recv_rows),) + tuple(x.shape[1:])
@@ -195,7 +230,7 @@ class Comm:
         which waits for the current stream's queued work at issue time."""
         if self.size == 1:
             return x, _Done()
-        if self.stage and x.is_cuda:
+        if (self.stage and x.is_cuda) or (self.compress and not x.is_cuda):
             return self.all_to_all_v(x, send_rows, recv_rows), _Done()
         x = x.contiguous()
         width = 1
@@ -224,6 +259,9 @@ class Comm:
             dev = [x.device for x, _, _ in items]
             outs = self.all_to_all_v_multi([(x.cpu(), s, r) for x, s, r in items])
             outs = [o.to(d) for o, d in zip(outs, dev)]
+            return (outs, _Done()) if async_op else outs
+        if self.compress and not any(x.is_cuda for x, _, _ in items):
+            outs = [self.all_to_all_v(x, s_, r) for x, s_, r in items]
             return (outs, _Done()) if async_op else outs
         outs, reqs, keep = [], [], []
         for x, send, recv in items:
@@ -278,6 +316,7 @@ class LoopbackComm(Comm):
         self.backend = "loopback"
         self.stage = False
         self.pg = None
+        self.compress = False
         # rccl=True: every exchange still moves this process's own bytes, but
         # through a real RCCL all-to-all on a 1-rank process group (async work
         # handles, the process group's stream, input lifetimes: exactly the
