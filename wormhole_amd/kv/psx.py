@@ -58,6 +58,10 @@ TRAIN, VAL, PRED = 0, 1, 2
 _LOC_MODE = os.environ.get("WH_PSX_LOCALIZE", "early")
 _LOC_STREAM = _LOC_MODE in ("ls", "early")
 _LOC_EARLY = _LOC_MODE == "early"
+# opt-in: measured 9 % slower at loopback P=8 (106.4 vs 117.2 M ex/s,
+# tools/gpu/r2_push.sh) -- the push's table atomics and the forward's row
+# gathers contend for the same memory pipeline and both stretch
+_PUSH_STREAM = os.environ.get("WH_PSX_PUSH_STREAM", "0") != "0"
 
 
 def _cdiv(a, b):
@@ -136,6 +140,11 @@ class PsxDifacto:
         # models/_pipeline.py), when WH_PSX_LOCALIZE_STREAM=1
         self.ls = (torch.cuda.Stream(device=self.dev)
                    if self.cuda and _LOC_STREAM else None)
+        # the owner applies the previous push on its own stream, concurrently
+        # with the forward, when WH_PSX_PUSH_STREAM=1
+        self.os = (torch.cuda.Stream(device=self.dev)
+                   if self.cuda and _PUSH_STREAM else None)
+        self.push_side = False
         self.S = torch.cuda.current_stream(self.dev) if self.cuda else None
         self.pins = _PinRing(self.dev) if self.cuda else None
         self.events = _EventRing() if self.cuda else None
@@ -364,13 +373,36 @@ class PsxDifacto:
         if idx:
             gvc[torch.tensor(idx, dtype=torch.int64, device=gvc.device)] = 0
 
-    def _owner_push(self, st):
+    def _owner_push(self, st, side=False):
+        """Apply a landed push on the owner. side=True: on the owner stream,
+        concurrently with the worker-side forward queued next on S (the two
+        touch disjoint memory: the table vs the pulled copy); S joins it
+        before the next open (:meth:`_join_push`)."""
         lrn = self.lrn
-        st.w_c3.wait()
+        if side and self.os is not None:
+            os_ = self.os
+            os_.wait_stream(self._S())  # the previous open / push are ordered first
+            with torch.cuda.stream(os_):
+                st.w_c3.wait()
+                self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o,
+                                   st.gpush, lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
+            # inputs allocated on S, read on os: not reused before os is done
+            for t in (st.gpush, st.slot, st.vpos, st.chain, st.head, st.tabs):
+                if t is not None and t.is_cuda:
+                    t.record_stream(os_)
+            self.push_side = True
+        else:
+            st.w_c3.wait()
+            self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o,
+                               st.gpush, lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
         st.w_c3 = None
-        self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o, st.gpush,
-                           lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
         st.gpush = st.slot = st.vpos = st.chain = st.head = st.keys_o = None
+
+    def _join_push(self):
+        """S waits for an owner push running on the owner stream."""
+        if self.push_side:
+            self._S().wait_stream(self.os)
+            self.push_side = False
 
     def _remap(self, remap):
         """The table grew: translate the slot ids of in-flight steps."""
@@ -414,6 +446,9 @@ class PsxDifacto:
             self._begin(nk, no, nv, st, next_batch[3] if len(next_batch) > 3 else None,
                         defer=True)
         self._c1(st)        # transfers while the previous minibatch computes
+        if self.push is not None and self.os is not None:
+            self._owner_push(self.push, side=True)  # overlaps the forward below
+            self.push = None
         if prev is not None:
             self._reply(prev)
             if self.tau == 0 and prev.train:
@@ -422,6 +457,7 @@ class PsxDifacto:
         if self.push is not None:
             self._owner_push(self.push)
             self.push = None
+        self._join_push()
         self._open(st, True)
         self.pull = st
         if early:
@@ -476,4 +512,5 @@ class PsxDifacto:
             self.push = None
         if st is not None and st.train:
             self._owner_push(st)
+        self._join_push()
         self.pull = None
