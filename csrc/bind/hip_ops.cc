@@ -897,56 +897,111 @@ std::vector<Tensor> fm_forward(const Tensor& offset, const Tensor& lid,
   return {py, dual, xv};
 }
 
+// Backward scratch + outputs, allocated by phase 1 (the plan):
+// {gw, gvc, chunk_key, chunk_beg, meta_v, bucket_hist, chunk_cnt, chunk_off,
+//  scan_tmp, det (empty unless deterministic)}
+static std::vector<Tensor> fm_bwd_alloc(const Tensor& csc_off, int64_t nnz, int64_t U,
+                                        int64_t vc_rows, int64_t vstride) {
+  auto f32 = csc_off.options().dtype(torch::kFloat32);
+  auto i32 = csc_off.options().dtype(torch::kInt32);
+  auto i64 = csc_off.options().dtype(torch::kInt64);
+  auto gw = torch::empty({U}, f32);
+  Tensor gvc = vstride > 0 ? torch::empty({vc_rows, vstride}, f32) : torch::empty({0}, f32);
+  const int64_t cap = wh::fm_bwd_chunks_bound(U, nnz);
+  const int64_t mb = vstride > 0 ? wh::fm_bwd_meta_bound(U, nnz) : 1;
+  Tensor det = deterministic() ? torch::empty({wh::fm_bwd_det_floats(U, nnz, (int)vstride)}, f32)
+                               : torch::empty({0}, f32);
+  return {gw, gvc, torch::empty({cap}, i32), torch::empty({cap}, i32),
+          torch::empty({2 * 4 * mb}, i32), torch::empty({wh::fm_bwd_bucket_scratch()}, i32),
+          torch::empty({std::max<int64_t>(2 * U, 1)}, i64), torch::empty({2 * (U + 1)}, i64),
+          torch::empty({wh::scan_tmp_elems(U)}, i64), det};
+}
+
+static void fm_bwd_launch(const std::vector<Tensor>& pl, const Tensor& csc_off,
+                          const Tensor& csc_row, const float* csc_val, const float* dual,
+                          const float* xv, const Tensor& w_or_hdr, const float* vcp,
+                          int64_t vstride, int64_t nrows, int phase) {
+  const int64_t U = csc_off.numel() - 1;
+  const wh::Lookback lb = lookback(csc_off.device());
+  const Tensor& gvc = pl[1];
+  wh::fm_backward(U, csc_row.numel(), nrows, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row),
+                  csc_val, dual, xv, ptr<float>(w_or_hdr), vcp, (int)vstride, ptr<float>(pl[0]),
+                  gvc.numel() ? ptr<float>(gvc) : nullptr, ptr<int32_t>(pl[2]),
+                  ptr<int32_t>(pl[3]), ptr<int32_t>(pl[4]), ptr<int32_t>(pl[5]),
+                  ptr<int64_t>(pl[6]), ptr<int64_t>(pl[7]), ptr<int64_t>(pl[8]), &lb,
+                  cur_stream(csc_off), pl[9].numel() ? ptr<float>(pl[9]) : nullptr, phase);
+}
+
+static void fm_bwd_check(const Tensor& csc_off, const Tensor& csc_row, const Tensor& w_or_hdr,
+                         int64_t vstride) {
+  CHECK_IN(csc_off, torch::kInt64);
+  CHECK_IN(csc_row, torch::kInt32);
+  CHECK_IN(w_or_hdr, torch::kFloat32);
+  TORCH_CHECK(vstride >= 0 && vstride <= 256 && vstride % 4 == 0, "bad vstride");
+  TORCH_CHECK(w_or_hdr.numel() == (csc_off.numel() - 1) * (vstride > 0 ? 2 : 1),
+              "w/hdr must have U rows");
+}
+
 // returns (gw [U], gvc [like vc]) (linear: gvc is empty)
 std::vector<Tensor> fm_backward(const Tensor& csc_off, const Tensor& csc_row,
                                 const c10::optional<Tensor>& csc_val, const Tensor& dual,
                                 const c10::optional<Tensor>& xv, const Tensor& w_or_hdr,
                                 const c10::optional<Tensor>& vc, int64_t vstride) {
-  CHECK_IN(csc_off, torch::kInt64);
-  CHECK_IN(csc_row, torch::kInt32);
+  fm_bwd_check(csc_off, csc_row, w_or_hdr, vstride);
   CHECK_IN(dual, torch::kFloat32);
-  CHECK_IN(w_or_hdr, torch::kFloat32);
-  TORCH_CHECK(vstride >= 0 && vstride <= 256 && vstride % 4 == 0, "bad vstride");
   c10::DeviceGuard g(csc_off.device());
-  auto s = cur_stream(csc_off);
-  const int64_t U = csc_off.numel() - 1;
-  const int64_t nnz = csc_row.numel();
-  TORCH_CHECK(w_or_hdr.numel() == U * (vstride > 0 ? 2 : 1), "w/hdr must have U rows");
-  auto f32 = csc_off.options().dtype(torch::kFloat32);
-  auto i32 = csc_off.options().dtype(torch::kInt32);
-  auto i64 = csc_off.options().dtype(torch::kInt64);
-  auto gw = torch::empty({U}, f32);
-  Tensor gvc = torch::empty({0}, f32);
+  const float* vcp = nullptr;
+  int64_t vrows = 0;
+  if (vstride > 0) {
+    TORCH_CHECK(vc.has_value() && vc->defined() && xv.has_value() && xv->defined(), "vc/xv required");
+    CHECK_IN((*vc), torch::kFloat32);
+    CHECK_IN((*xv), torch::kFloat32);
+    vrows = vc->numel() ? vc->size(0) : 0;
+    vcp = vc->numel() ? ptr<float>(*vc) : nullptr;
+  }
+  auto pl = fm_bwd_alloc(csc_off, csc_row.numel(), csc_off.numel() - 1, vrows, vstride);
+  fm_bwd_launch(pl, csc_off, csc_row, optptr<float>(csc_val), ptr<float>(dual),
+                vstride > 0 ? optptr<float>(xv) : nullptr, w_or_hdr, vcp, vstride, dual.numel(), 0);
+  return {pl[0], pl[1]};
+}
+
+// Phase 1 of the backward on the CURRENT stream (the planning that needs no
+// dual: chunk lists, zeroed multi-chunk gradients, V-chunk bucketing); the
+// returned plan is finished by fm_backward_run (same CSC / header / vc).
+std::vector<Tensor> fm_backward_plan(const Tensor& csc_off, const Tensor& csc_row,
+                                     const Tensor& w_or_hdr, int64_t vc_rows, int64_t nrows,
+                                     int64_t vstride) {
+  fm_bwd_check(csc_off, csc_row, w_or_hdr, vstride);
+  TORCH_CHECK(vc_rows >= 0 && nrows >= 0, "bad sizes");
+  c10::DeviceGuard g(csc_off.device());
+  auto pl = fm_bwd_alloc(csc_off, csc_row.numel(), csc_off.numel() - 1, vc_rows, vstride);
+  fm_bwd_launch(pl, csc_off, csc_row, nullptr, nullptr, nullptr, w_or_hdr, nullptr, vstride,
+                nrows, 1);
+  return pl;
+}
+
+std::vector<Tensor> fm_backward_run(const std::vector<Tensor>& plan, const Tensor& csc_off,
+                                    const Tensor& csc_row, const c10::optional<Tensor>& csc_val,
+                                    const Tensor& dual, const c10::optional<Tensor>& xv,
+                                    const Tensor& w_or_hdr, const c10::optional<Tensor>& vc,
+                                    int64_t vstride) {
+  fm_bwd_check(csc_off, csc_row, w_or_hdr, vstride);
+  CHECK_IN(dual, torch::kFloat32);
+  TORCH_CHECK(plan.size() == 10, "fm_backward_run: not a backward plan");
+  c10::DeviceGuard g(csc_off.device());
   const float* vcp = nullptr;
   if (vstride > 0) {
     TORCH_CHECK(vc.has_value() && vc->defined() && xv.has_value() && xv->defined(), "vc/xv required");
     CHECK_IN((*vc), torch::kFloat32);
     CHECK_IN((*xv), torch::kFloat32);
-    gvc = torch::empty({vc->numel() ? vc->size(0) : 0, vstride}, f32);
+    TORCH_CHECK(plan[1].dim() == 2 && plan[1].size(0) == (vc->numel() ? vc->size(0) : 0),
+                "fm_backward_run: vc rows differ from the plan's");
     vcp = vc->numel() ? ptr<float>(*vc) : nullptr;
   }
-  const int64_t cap = wh::fm_bwd_chunks_bound(U, nnz);
-  auto chunk_key = torch::empty({cap}, i32);
-  auto chunk_beg = torch::empty({cap}, i32);
-  const int64_t nrows = dual.numel();
-  const int64_t mb = vstride > 0 ? wh::fm_bwd_meta_bound(U, nnz) : 1;
-  auto meta_v = torch::empty({2 * 4 * mb}, i32);
-  auto bucket_hist = torch::empty({wh::fm_bwd_bucket_scratch()}, i32);
-  auto chunk_cnt = torch::empty({std::max<int64_t>(2 * U, 1)}, i64);
-  auto chunk_off = torch::empty({2 * (U + 1)}, i64);
-  auto stmp = torch::empty({wh::scan_tmp_elems(U)}, i64);
-  const wh::Lookback lb = lookback(csc_off.device());
-  Tensor det;
-  if (deterministic())
-    det = torch::empty({wh::fm_bwd_det_floats(U, nnz, (int)vstride)}, f32);
-  wh::fm_backward(U, nnz, nrows, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row),
-                  optptr<float>(csc_val), ptr<float>(dual),
-                  vstride > 0 ? optptr<float>(xv) : nullptr, ptr<float>(w_or_hdr), vcp,
-                  (int)vstride, ptr<float>(gw), gvc.numel() ? ptr<float>(gvc) : nullptr,
-                  ptr<int32_t>(chunk_key), ptr<int32_t>(chunk_beg), ptr<int32_t>(meta_v),
-                  ptr<int32_t>(bucket_hist), ptr<int64_t>(chunk_cnt), ptr<int64_t>(chunk_off),
-                  ptr<int64_t>(stmp), &lb, s, det.defined() ? ptr<float>(det) : nullptr);
-  return {gw, gvc};
+  TORCH_CHECK(plan[0].numel() == csc_off.numel() - 1, "fm_backward_run: U differs from the plan's");
+  fm_bwd_launch(plan, csc_off, csc_row, optptr<float>(csc_val), ptr<float>(dual),
+                vstride > 0 ? optptr<float>(xv) : nullptr, w_or_hdr, vcp, vstride, dual.numel(), 2);
+  return {plan[0], plan[1]};
 }
 
 // gvc [mcap, vstride]; m: device int64 tensor holding the live row count
@@ -2079,6 +2134,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("nshard") = 1, py::arg("hint") = 0, py::arg("exchange") = py::none());
   m.def("fm_forward", &fm_forward);
   m.def("fm_backward", &fm_backward);
+  m.def("fm_backward_plan", &fm_backward_plan);
+  m.def("fm_backward_run", &fm_backward_run);
   m.def("fm_grad_post", &fm_grad_post);
   m.def("vidx_renumber", &vidx_renumber);
   m.def("ps_unpack", &ps_unpack);

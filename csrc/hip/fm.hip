@@ -976,7 +976,7 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
                  const float* hdr_f, const float* vc, int vstride, float* gw, float* gvc,
                  int32_t* chunk_key, int32_t* chunk_beg, int32_t* meta_v_i32, int32_t* bucket_hist,
                  int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, const Lookback* lb,
-                 hipStream_t s, float* det_part) {
+                 hipStream_t s, float* det_part, int phase) {
   int4* meta_v = reinterpret_cast<int4*>(meta_v_i32);
   if (nuniq <= 0) return;
   const float2* hdr = vstride > 0 ? reinterpret_cast<const float2*>(hdr_f) : nullptr;
@@ -988,6 +988,11 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
   int32_t* key_s = chunk_key;
   int32_t* beg_s = chunk_beg;
   const int64_t ntiles = (nuniq + kPlanTile - 1) / kPlanTile;
+  const int64_t vcap = v_cap(nuniq, nnz);
+  // V chunks ordered by first-row bucket (meta_v[cap..2cap) receives the
+  // list); deterministic mode keeps the key-major list (partials by index)
+  int4* meta_sorted = (det_part || !hdr) ? meta_v : meta_v + vcap;
+  if (phase != 2) {
   if (lb && ntiles <= kLbMaxTiles) {  // one launch
     hipLaunchKernelGGL(k_chunk_plan, dim3((unsigned)ntiles), dim3(kThreads), 0, s, nuniq, csc_off,
                        hdr, vstride, *lb, (int)ntiles, off_s + nuniq, off_v + nuniq, key_s, beg_s,
@@ -1000,11 +1005,20 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
     hipLaunchKernelGGL(k_chunk_fill, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s,
                        nuniq, csc_off, off_s, off_v, hdr, vstride, key_s, beg_s, meta_v, gw, gvc);
   }
+  if (hdr && !det_part) {
+    const int shift = bucket_shift(std::max<int64_t>(nrows, 1));
+    hipLaunchKernelGGL(k_vchunk_hist, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
+                       meta_v, csc_row, shift, bucket_hist);
+    hipLaunchKernelGGL(k_vchunk_scan, dim3(1), dim3(kBuckets * kScanParts), 0, s, bucket_hist);
+    hipLaunchKernelGGL(k_vchunk_scatter, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
+                       meta_v, csc_row, shift, bucket_hist, meta_sorted);
+  }
+  }
+  if (phase == 1) return;
   // chunk counts are device values (off[nuniq]); the scalar kernel launches
   // over the host-side bound and surplus lanes exit; the V kernel is
   // persistent. No host synchronisation in the step.
   // deterministic scratch: [cap_s] scalar partials | [vcap] V-chunk gw | [vcap, vstride] rows
-  const int64_t vcap = v_cap(nuniq, nnz);
   float* pgs = det_part;
   float* pgv_w = det_part ? det_part + cap_s : nullptr;
   float* pgv = det_part ? pgv_w + vcap : nullptr;
@@ -1014,19 +1028,6 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
     hipLaunchKernelGGL(k_bwd_reduce_s, dim3(grid_for(cap_s, kThreads)), dim3(kThreads), 0, s,
                        off_s + nuniq, key_s, beg_s, csc_off, pgs, gw);
   if (!hdr) return;
-  // order the V chunks by first-row bucket (meta_v[cap..2cap) receives the
-  // list); deterministic mode keeps the key-major list (partials by index)
-  int4* meta_sorted = meta_v + vcap;
-  if (det_part) {
-    meta_sorted = meta_v;
-  } else {
-    const int shift = bucket_shift(std::max<int64_t>(nrows, 1));
-    hipLaunchKernelGGL(k_vchunk_hist, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
-                       meta_v, csc_row, shift, bucket_hist);
-    hipLaunchKernelGGL(k_vchunk_scan, dim3(1), dim3(kBuckets * kScanParts), 0, s, bucket_hist);
-    hipLaunchKernelGGL(k_vchunk_scatter, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
-                       meta_v, csc_row, shift, bucket_hist, meta_sorted);
-  }
   const int G = vstride / 4;
   const int64_t vblk = std::min<int64_t>((v_cap(nuniq, nnz) + 3) / 4,
                                          WH_RESIDENT(G, k_bwd_v, 2048));

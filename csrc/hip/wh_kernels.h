@@ -293,7 +293,11 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
                  const float* hdr, const float* vc, int vstride, float* gw, float* gvc,
                  int32_t* chunk_key, int32_t* chunk_beg, int32_t* meta_v, int32_t* bucket_hist,
                  int64_t* chunk_cnt, int64_t* chunk_off, int64_t* scan_tmp, const Lookback* lb,
-                 hipStream_t s, float* det_part = nullptr);
+                 hipStream_t s, float* det_part = nullptr, int phase = 0);
+// phase: 0 = the whole backward; 1 = only the planning that needs no dual
+// (chunk lists + V-chunk bucketing: CSC offsets and the pull header), so it
+// can run on a side stream concurrently with the forward; 2 = the rest
+// (dual / xv dependent), after phase 1 with the same scratch.
 // det_part (deterministic mode, WH_DETERMINISTIC=1): scratch of
 // fm_bwd_det_floats floats; hot keys' chunk partials are then summed in
 // occurrence order by a second pass instead of float atomics

@@ -118,6 +118,17 @@ def test_fm_forward_backward(hip, dim, with_val):
     live = ref.hdr_vidx(hdr).long()
     live = live[live >= 0]
     assert torch.allclose(gvc.cpu()[live], gvc_r[live], atol=1e-4, rtol=1e-3)
+    # the two-phase backward (plan on a side stream, run after the forward)
+    side = torch.cuda.Stream(device=DEV)
+    side.wait_stream(torch.cuda.current_stream(DEV))
+    with torch.cuda.stream(side):
+        plan = hip.fm_backward_plan(csc_off, csc_row, hdr.to(DEV), vc.shape[0],
+                                    off.numel() - 1, vs)
+    torch.cuda.current_stream(DEV).wait_stream(side)
+    gw2, gvc2 = hip.fm_backward_run(plan, csc_off, csc_row, csc_val if with_val else None, dual,
+                                    xv, hdr.to(DEV), vc.to(DEV), vs)
+    assert torch.allclose(gw2.cpu(), gw_r, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(gvc2.cpu()[live], gvc_r[live], atol=1e-4, rtol=1e-3)
 
 
 def test_grad_post_and_renumber(hip):

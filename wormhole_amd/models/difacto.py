@@ -11,6 +11,8 @@ learn/difacto/async_sgd.h:363-425), re-expressed on the GPU:
   ->  gradient clip / dropout / normalisation  ->  push  ->  owner applies
   FTRL on w and AdaGrad on V in one fused kernel.
 """
+import os
+
 import torch
 
 from .. import ops
@@ -19,6 +21,11 @@ from ..kv import ShardedKV, make_store
 from ..utils import trace
 
 TRAIN, VAL, PRED = 0, 1, 2
+# WH_BWD_PLAN_STREAM=1: plan the backward on its own stream, overlapping the
+# forward. Opt-in: measured 15 % slower on one MI355X (110 vs 130 M ex/s,
+# tools/gpu/r2_plan.sh) -- the plan's look-back tiles and the one-block
+# bucket scan wait behind the persistent forward's workgroups for CU slots.
+_PLAN_STREAM = os.environ.get("WH_BWD_PLAN_STREAM", "0") != "0"
 
 
 class DifactoLearner:
@@ -61,6 +68,7 @@ class DifactoLearner:
         self.step = 0
         self.last_sizes = None
         # P > 1 shards: the lean pipelined exchange (kv/psx.py)
+        self._plan_stream = None
         self.psx = None
         if comm.size > 1 and self.vstride > 0 and self.kv.nshard == comm.size:
             from ..kv.psx import PsxDifacto
@@ -96,6 +104,11 @@ class DifactoLearner:
             begin_next(self, next_batch, uniq.numel())
         if self.vstride == 0:  # no embedding: a plain linear model over w
             hdr, vc = hdr[:, 0].contiguous(), None
+        plan = None
+        if train and _PLAN_STREAM and self.vstride > 0 and hdr.is_cuda:
+            # the backward's planning (chunk lists + bucketing: CSC offsets and
+            # the pull header only) on its own stream, overlapping the forward
+            plan = self._bwd_plan(csc_off, csc_row, hdr, vc, offset.numel() - 1)
         with trace.span("forward"):
             py, dual, xv = ops.fm_forward(offset, lid, val, hdr, vc, self.vstride, label,
                                           ops.LOSS_LOGIT, self.met)
@@ -103,8 +116,17 @@ class DifactoLearner:
         self.n_mb += 1
         if train:
             with trace.span("backward"):
-                gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, hdr, vc,
-                                          self.vstride)
+                if plan is not None:
+                    pl, ev = plan
+                    cur = torch.cuda.current_stream(hdr.device.index)
+                    cur.wait_event(ev)
+                    for t in pl:  # allocated on the plan stream, used here
+                        t.record_stream(cur)
+                    gw, gvc = ops.fm_backward_run(pl, csc_off, csc_row, csc_val, dual, xv, hdr,
+                                                  vc, self.vstride)
+                else:
+                    gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, hdr, vc,
+                                              self.vstride)
                 if self.emb is not None and self.vstride > 0:
                     ops.fm_grad_post(gvc, sess.m, self.dim, self.emb.grad_clipping,
                                      self.emb.dropout, self.seed + 7919 * self.step + 1,
@@ -114,6 +136,26 @@ class DifactoLearner:
                                      self.seed, defer=self.defer_push)
         self.step += 1
         return py if wtype == PRED else None
+
+    def _bwd_plan(self, csc_off, csc_row, hdr, vc, nrows):
+        """Enqueue the backward's phase 1 on the plan stream after everything
+        queued on the compute stream so far (this minibatch's pull, which
+        also last used the shared look-back workspace); returns (plan, event).
+        Inputs are read there (record_stream keeps their blocks from reuse)."""
+        dev = hdr.device
+        cur = torch.cuda.current_stream(dev.index)
+        if self._plan_stream is None:
+            self._plan_stream = torch.cuda.Stream(device=dev)
+        ps = self._plan_stream
+        ps.wait_stream(cur)
+        for t in (csc_off, csc_row, hdr):
+            t.record_stream(ps)
+        with torch.cuda.stream(ps):
+            pl = ops.fm_backward_plan(csc_off, csc_row, hdr, vc.shape[0] if vc is not None else 0,
+                                      nrows, self.vstride)
+            ev = torch.cuda.Event()
+            ev.record(ps)
+        return pl, ev
 
     # -------------------------------------------------------------- progress
     def flush(self):

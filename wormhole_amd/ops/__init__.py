@@ -89,6 +89,20 @@ def fm_backward(csc_off, csc_row, csc_val, dual, xv, w_or_hdr, vc, vstride):
     return ref.fm_backward(csc_off, csc_row, csc_val, dual, xv, w_or_hdr, vc, vstride)
 
 
+def fm_backward_plan(csc_off, csc_row, hdr, vc_rows, nrows, vstride):
+    """GPU: phase 1 of :func:`fm_backward` on the current stream -- the
+    planning that needs no dual (chunk lists, V-chunk bucketing), so it can
+    overlap the forward; :func:`fm_backward_run` finishes it."""
+    return _native.hip().fm_backward_plan(csc_off, csc_row, hdr, int(vc_rows), int(nrows),
+                                          int(vstride))
+
+
+def fm_backward_run(plan, csc_off, csc_row, csc_val, dual, xv, hdr, vc, vstride):
+    """Phase 2 of :func:`fm_backward` (dual / xv dependent); (gw, gvc)."""
+    return _native.hip().fm_backward_run(plan, csc_off, csc_row, csc_val, dual, xv, hdr, vc,
+                                         vstride)
+
+
 def fm_grad_post(gvc, m, dim, clip, dropout, seed, normalize):
     """Clip / dropout / normalise the first m (device int64 [1]) rows of the
     embedding gradient gvc [mcap, vstride] (learn/difacto/loss.h:131-155)."""
