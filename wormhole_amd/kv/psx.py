@@ -62,6 +62,8 @@ _LOC_EARLY = _LOC_MODE == "early"
 # tools/gpu/r2_push.sh) -- the push's table atomics and the forward's row
 # gathers contend for the same memory pipeline and both stretch
 _PUSH_STREAM = os.environ.get("WH_PSX_PUSH_STREAM", "0") != "0"
+# a training step's AUC enqueued after its backward (models/difacto.py)
+_AUC_LATE = os.environ.get("WH_AUC_LATE", "1") != "0"
 
 
 def _cdiv(a, b):
@@ -340,7 +342,8 @@ class PsxDifacto:
         st.hdr, st.rows = ops.ps_unpack(st.rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d)
         st.py, st.dual, st.xv = ops.fm_forward(st.offset, st.lid, st.val, st.hdr, st.rrecv,
                                                self.vs, st.label, ops.LOSS_LOGIT, lrn.met)
-        ops.auc_acc(st.py, st.label, lrn.auc_sum)
+        if not (_AUC_LATE and st.train):  # (a training step's AUC follows its backward)
+            ops.auc_acc(st.py, st.label, lrn.auc_sum)
         lrn.n_mb += 1
         lrn.last_sizes = (st.U, sum(st.vrecv))
 
@@ -362,6 +365,8 @@ class PsxDifacto:
         send_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
         recv_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
         st.gpush, st.w_c3 = self.comm.all_to_all_v_async(gvc, send_rows, recv_rows)
+        if _AUC_LATE:
+            ops.auc_acc(st.py, st.label, lrn.auc_sum)
         # the worker-side tensors of this step are done
         st.rrecv = st.hdr = st.dual = st.xv = st.lid = st.csc = None
 

@@ -26,6 +26,12 @@ TRAIN, VAL, PRED = 0, 1, 2
 # tools/gpu/r2_plan.sh) -- the plan's look-back tiles and the one-block
 # bucket scan wait behind the persistent forward's workgroups for CU slots.
 _PLAN_STREAM = os.environ.get("WH_BWD_PLAN_STREAM", "0") != "0"
+# A training minibatch's AUC (side stream) is enqueued after its backward
+# instead of right after its forward, so its kernels overlap the push / open
+# rather than the small backward-planning kernels on the critical path:
+# 130.0 -> 134.3 M ex/s on one MI355X (tools/gpu/r2_auc.sh). WH_AUC_LATE=0
+# restores the early placement.
+_AUC_LATE = os.environ.get("WH_AUC_LATE", "1") != "0"
 
 
 class DifactoLearner:
@@ -112,7 +118,8 @@ class DifactoLearner:
         with trace.span("forward"):
             py, dual, xv = ops.fm_forward(offset, lid, val, hdr, vc, self.vstride, label,
                                           ops.LOSS_LOGIT, self.met)
-            ops.auc_acc(py, label, self.auc_sum)
+            if not (_AUC_LATE and train):
+                ops.auc_acc(py, label, self.auc_sum)
         self.n_mb += 1
         if train:
             with trace.span("backward"):
@@ -131,6 +138,8 @@ class DifactoLearner:
                     ops.fm_grad_post(gvc, sess.m, self.dim, self.emb.grad_clipping,
                                      self.emb.dropout, self.seed + 7919 * self.step + 1,
                                      bool(self.emb.grad_normalization))
+            if _AUC_LATE:  # the AUC side stream starts behind the backward
+                ops.auc_acc(py, label, self.auc_sum)
             with trace.span("push"):
                 self.kv.difacto_push(sess, gw, gvc, self.hp, self.threshold, self.l1_shrk,
                                      self.seed, defer=self.defer_push)
