@@ -53,19 +53,26 @@ class StoreGuard:
         self.cuda = not isinstance(store, CpuKVStore)
 
     def after_open(self):
-        s = self.store.summary()
         if self.cuda:
             if getattr(self, "_pin", None) is None:  # two alternating pinned slots
                 self._pin = [torch.empty(4, dtype=torch.int64, pin_memory=True) for _ in range(2)]
                 self._ev = [torch.cuda.Event() for _ in range(2)]
                 self._k = 0
+                self._side = torch.cuda.Stream()
             k = self._k = self._k ^ 1
             h, ev = self._pin[k], self._ev[k]
-            h.copy_(s, non_blocking=True)
-            ev.record()
+            # the summary (a one-wave read of the table's counters) and its
+            # copy run on a side stream behind the open, off the compute
+            # stream's critical path; read() waits for them one open later
+            side = self._side
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                s = self.store.summary()
+                h.copy_(s, non_blocking=True)
+                ev.record(side)
             self.pend = (h, ev)
         else:
-            self.pend = (s, None)
+            self.pend = (self.store.summary(), None)
         self.since = 0
 
     def read(self):
