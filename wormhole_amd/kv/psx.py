@@ -64,6 +64,9 @@ _LOC_EARLY = _LOC_MODE == "early"
 _PUSH_STREAM = os.environ.get("WH_PSX_PUSH_STREAM", "0") != "0"
 # a training step's AUC enqueued after its backward (models/difacto.py)
 _AUC_LATE = os.environ.get("WH_AUC_LATE", "1") != "0"
+# C3 (the push) of a pipelined step is issued at the start of the next call,
+# right after that call's C2 (WH_PSX_C3_LATE=0: at the end of the backward)
+_C3_LATE = os.environ.get("WH_PSX_C3_LATE", "1") != "0"
 
 
 def _cdiv(a, b):
@@ -78,7 +81,7 @@ class _Step:
                  "segHS_o", "keys_o", "slot", "vpos", "chain", "head", "rbuf", "vcnt",
                  "ev_open",
                  "vown", "vrecv", "vrecv_d", "rrecv", "hdr", "rows", "py", "dual", "xv",
-                 "gpush", "seed_step", "w_c1", "w_c2", "w_c3")
+                 "gpush", "gvc", "seed_step", "w_c1", "w_c2", "w_c3")
 
     def __init__(self):
         for s in self.__slots__:
@@ -347,8 +350,17 @@ class PsxDifacto:
         lrn.n_mb += 1
         lrn.last_sizes = (st.U, sum(st.vrecv))
 
-    def _grad(self, st):
-        """Backward + gradient post-processing, then issue C3 (the push)."""
+    def _c3(self, st):
+        """Issue C3: the packed push regions back to their owners."""
+        P = self.P
+        send_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
+        recv_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
+        st.gpush, st.w_c3 = self.comm.all_to_all_v_async(st.gvc, send_rows, recv_rows)
+        st.gvc = None
+
+    def _grad(self, st, issue=True):
+        """Backward + gradient post-processing, then issue C3 (the push), or
+        leave it for :meth:`_c3` (issue=False)."""
         lrn = self.lrn
         emb = lrn.emb
         P = self.P
@@ -362,9 +374,9 @@ class PsxDifacto:
             ops.fm_grad_post(gvc, st.rows, lrn.dim, emb.grad_clipping, emb.dropout,
                              lrn.seed + 7919 * st.seed_step + 1, bool(emb.grad_normalization))
         ops.ps_pack_gw(gw, gvc, st.segS_w, st.segHS_w, st.vrecv_d)
-        send_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
-        recv_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
-        st.gpush, st.w_c3 = self.comm.all_to_all_v_async(gvc, send_rows, recv_rows)
+        st.gvc = gvc
+        if issue:
+            self._c3(st)
         if _AUC_LATE:
             ops.auc_acc(st.py, st.label, lrn.auc_sum)
         # the worker-side tensors of this step are done
@@ -444,6 +456,13 @@ class PsxDifacto:
         st = self._new_step(send, recv, label, True, data_pass, prev)
         if prev is not None:
             self._c2(prev)  # transfers while this minibatch's localize finishes
+        if self.push is not None and self.push.gvc is not None:
+            # the previous backward's push, issued only now: behind this
+            # step's pull reply on the (in-order) RCCL stream, so the reply
+            # overlaps the end of that backward and the push overlaps the
+            # forward below, instead of both transfers running back to back
+            # between the backward and the forward
+            self._c3(self.push)
         self._set_loc(st, self._finish(), offset, val)
         early = _LOC_EARLY and self.cuda and next_batch is not None
         if early:  # next minibatch's localize kernels now; its C0 after the open
@@ -471,7 +490,7 @@ class PsxDifacto:
             nk, no, nv = next_batch[:3]
             self._begin(nk, no, nv, st, next_batch[3] if len(next_batch) > 3 else None)
         if self.tau == 1 and prev is not None and prev.train:
-            self._grad(prev)  # its push (C3) lands before the next call's open
+            self._grad(prev, issue=not _C3_LATE)  # pushed before the next call's open
             self.push = prev
         self.lrn.step += 1
 
@@ -499,6 +518,8 @@ class PsxDifacto:
     def flush(self):
         """Complete every minibatch in flight (end of a pass, before reading
         or saving the model, end of a timed run)."""
+        if self.push is not None and self.push.gvc is not None:
+            self._c3(self.push)
         if self.job is not None and self.job[2] is not None:
             # the next minibatch's localize already carries the last pull's
             # V counts: read them now (the job itself stays begun)
