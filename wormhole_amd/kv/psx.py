@@ -23,17 +23,23 @@ the step is software-pipelined one minibatch deep (staleness 1, as the
 reference allows by default); a call of :meth:`PsxDifacto.train` enqueues,
 on the compute stream S,
 
-    localize finish(i) | unpack(i-1) fwd(i-1) | owner push(i-2) |
-    owner open(i) pack(i) | localize begin(i+1) | bwd(i-1) pack_gw(i-1)
+    unpack(i-1) fwd(i-1) | owner push(i-2) | owner open(i) pack(i) |
+    bwd(i-1) pack_gw(i-1) [+ AUC(i-1) on its side stream]
 
-and the collectives C2(i-1), C1(i), C0(i+1), C3(i-1) in that order. C1-C3
-are issued asynchronously on the process group's stream and waited on (a
-stream dependency, not a host wait) right before the kernel that consumes
-them, so each overlaps the compute-stream work queued in between; C0 and its
-pinned host read run from a side stream the compute stream never waits on.
-The host's wait for the read of C0(i+1) happens in the NEXT call while S
-still holds bwd(i-1), so S never drains. ``max_concurrency = 1`` gives the
-strict (staleness 0) order at the cost of one pipeline drain per step.
+while the localize of minibatch i+1 runs on its own stream, begun as soon as
+minibatch i's localize is finished (its count collective deferred until
+after open(i), whose V row counts it carries). The collectives go out in the
+order C2(i-1), C3(i-2), C1(i), C0(i+1): RCCL runs them in issue order on the
+process group's stream, so the push of the previous backward (C3(i-2)) is
+issued behind this call's pull reply rather than at the end of that
+backward -- C2 then overlaps the backward's tail and C3 the forward, instead
+of the two big transfers running back to back between them. C1-C3 are
+waited on (a stream dependency, not a host wait) right before the kernel
+that consumes them; C0 and its pinned host read run from a side stream the
+compute stream never waits on. The host's wait for the read of C0(i+1)
+happens in the NEXT call while S still holds bwd(i-1), so S never drains.
+``max_concurrency = 1`` gives the strict (staleness 0) order at the cost of
+one pipeline drain per step.
 """
 import contextlib
 import os
