@@ -296,6 +296,10 @@ class Comm:
 
     def finalize(self):
         if self.size > 1 and dist.is_initialized():
+            # every rank is past its last collective before any tears the
+            # group down (a gloo rank whose peer closed its sockets early
+            # could abort in a transport thread: seen under CPU overload)
+            self.barrier()
             dist.destroy_process_group()
 
 
