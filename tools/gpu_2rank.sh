@@ -13,7 +13,7 @@ tail -2 $OUT/test.log
 for NP in $NPS; do
   for M in difacto linear; do
     WH_BENCH_SAME_GPU=1 WH_COMM_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $NP \
-      --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus $NP --steps 5 --warmup 2 --model $M --batch 20000 $BENCH_EXTRA > $OUT/bench$NP.$M.log 2>&1 || { tail -40 $OUT/bench$NP.$M.log; exit 1; }
+      --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus $NP --steps 5 --warmup 2 --prewarm 0 --model $M --batch 20000 $BENCH_EXTRA > $OUT/bench$NP.$M.log 2>&1 || { tail -40 $OUT/bench$NP.$M.log; exit 1; }
     echo "np=$NP $M: $(tail -1 $OUT/bench$NP.$M.log | cut -c1-200)"
   done
 done

@@ -95,7 +95,8 @@ class Comm:
         self.stage = backend == "gloo" and self.device.type == "cuda"
         self.pg = None
         # ps-lite COMPRESSING filter (msg_compression): LZ4 per peer chunk on
-        # HOST transfers (gloo; also the staged GPU rehearsal). Device
+        # HOST transfers (gloo between CPU ranks; not the staged multi-rank GPU
+        # rehearsal, whose payloads are device rows staged per step). Device
         # transfers over RCCL/xGMI stay raw (docs/linear.md msg_compression).
         self.compress = False
         if self.size > 1 and init:
@@ -174,7 +175,7 @@ class Comm:
 
     def set_compression(self, on):
         """Enable the LZ4 filter (applies to host transfers only)."""
-        self.compress = bool(on) and self.backend == "gloo"
+        self.compress = bool(on) and self.backend == "gloo" and self.device.type == "cpu"
 
     def _a2a_lz4(self, x, send_rows, recv_rows):
         """all_to_all_v of a CPU tensor with every peer chunk LZ4-compressed
