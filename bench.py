@@ -15,6 +15,12 @@ Weak scaling: each GPU processes its own minibatch of --batch rows per step;
 the keys are sharded over all GPUs (ps-lite server group -> xGMI all-to-all).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model difacto|linear]
+
+``--gpus N`` with N > 1 and no launcher around it starts the N ranks itself
+(``torch.distributed.run`` on 127.0.0.1, one process per GPU, the launch the
+driver uses); every rank checks that the group has N members on N distinct
+GPUs. The JSON line also reports the RCCL rank count, the per-rank step time
+spread and the bytes each GPU sends to its peers per step in each collective.
 """
 import argparse
 import json
@@ -29,6 +35,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from wormhole_amd.config.schema import DifactoConfig, Embedding, LinearConfig  # noqa: E402
 from wormhole_amd.data.synthetic import CRITEO_TB_CARD  # noqa: E402
 from wormhole_amd.parallel.comm import Comm, env_local_rank  # noqa: E402
+from wormhole_amd.parallel import launch  # noqa: E402
 
 LINEAR_REF_EX_PER_S = 1.85e6  # linear.dmlc FTRL, Criteo, CPU host
 
@@ -52,7 +59,9 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--model", default="difacto", choices=["difacto", "linear"])
-    ap.add_argument("--batch", type=int, default=100000, help="rows per GPU per step")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="rows per GPU per step (default: difacto 100000 as the reference's "
+                         "criteo.conf; linear 10000 as the published criteo_kaggle.rst run)")
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--cap", type=int, default=1 << 27, help="KV slots per GPU shard")
     ap.add_argument("--vcap", type=int, default=1 << 24, help="embedding rows per shard")
@@ -75,7 +84,16 @@ def main():
     ap.add_argument("--max-concurrency", type=int, default=2,
                     help="minibatches in flight per worker (reference default 2): with >= 2 "
                          "the multi-shard step is pipelined one minibatch deep")
+    ap.add_argument("--launch-timeout", type=int, default=3600,
+                    help="self-launched multi-rank runs are killed after this many seconds")
     args = ap.parse_args()
+    if args.gpus > 1 and args.loopback <= 1 and not launch.launched():
+        # no launcher around us: start the N ranks ourselves (before any GPU
+        # call in this process) and pass their exit code through
+        return launch.self_launch(os.path.abspath(__file__), sys.argv[1:], args.gpus,
+                                  args.device, args.launch_timeout)
+    if args.batch is None:
+        args.batch = 100000 if args.model == "difacto" else 10000
     if args.prewarm is None:  # (the CPU rehearsal of the distributed path skips it)
         args.prewarm = 1000 if (args.model == "difacto" and args.device == "cuda") else 0
 
@@ -93,6 +111,9 @@ def main():
         comm = LoopbackComm(args.loopback, device, rccl=args.loopback_rccl)
     else:
         comm = Comm(device)
+        # the group is what --gpus says, on distinct devices
+        launch.verify_world(comm, args.gpus if launch.launched() else 1,
+                            same_gpu_ok=os.environ.get("WH_BENCH_SAME_GPU") == "1")
     n = 1 if args.loopback > 1 else comm.size  # GPUs doing work
     learner = build(args, comm, device)
     seed = 1000 + comm.rank
@@ -158,6 +179,9 @@ def main():
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
+    psx = getattr(learner, "psx", None)
+    if psx is not None:
+        psx.wire_reset()  # count the timed steps' exchange bytes only
     t0 = time.perf_counter()
     run(args.warmup, args.steps)
     learner.flush()  # the last step's (deferred) push is part of the timed work
@@ -171,9 +195,12 @@ def main():
         with open(os.environ["WH_HOST_PROFILE"] + ".%d" % comm.rank, "w") as f:
             pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
             pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
+    per_rank = [float(x) for x in comm.allgather_object(dt)] if comm.size > 1 and \
+        args.loopback <= 1 else [dt]
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     comm.allreduce(t, "max")
     dt = float(t.item())
+    wire = psx.wire_report(args.steps) if psx is not None else None
     prog = learner.take_progress()
     guard = learner.kv.guard
     guard.after_open()
@@ -214,9 +241,15 @@ def main():
             "table_grows": guard.grows, "vslab_rows_per_gpu": guard.vused,
             "dropped_keys": 0, "max_concurrency": args.max_concurrency,
             "loopback_shards": args.loopback if args.loopback > 1 else None,
+            "rccl_ranks": comm.size if (comm.backend == "nccl" and args.loopback <= 1) else 0,
+            "comm_backend": comm.backend,
+            "rank_ms_per_step_min": 1000.0 * min(per_rank) / args.steps,
+            "rank_ms_per_step_max": 1000.0 * max(per_rank) / args.steps,
+            "wire_bytes_per_gpu_step": wire,
         }), flush=True)
     comm.finalize()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from wormhole_amd.models import gbdt as G  # noqa: E402
 from wormhole_amd.parallel.bsp import BSP  # noqa: E402
 from wormhole_amd.parallel.comm import env_local_rank  # noqa: E402
+from wormhole_amd.parallel import launch  # noqa: E402
 
 
 def higgs_like(n, f, seed, dev):
@@ -40,7 +41,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the framework's PyTorch CPU path (anchor numbers)")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); > 1 without a launcher: started here")
     a = ap.parse_args()
+    if a.gpus > 1 and not launch.launched():  # before any GPU call in this process
+        return launch.self_launch(os.path.abspath(__file__), sys.argv[1:], a.gpus, a.device)
     if a.device == "cuda":
         torch.cuda.set_device(env_local_rank())
         dev = torch.device("cuda", env_local_rank())
@@ -51,6 +56,7 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize()
     bsp = BSP(dev)
+    launch.verify_world(bsp.comm, a.gpus if launch.launched() else 1)
     n = a.rows // bsp.world
     X, y = higgs_like(n, a.features, 7 + bsp.rank, dev)
     dm = G.DMatrix.from_dense(X, y, dev)
@@ -84,13 +90,14 @@ def main():
     err = G.eval_metric("error", torch.sigmoid(margin), dm.label, None, bsp)
     if bsp.rank == 0:
         print(json.dumps({"metric": "GBDT trees/s (hist, depth %d, %dx%d)" % (a.depth, a.rows, a.features),
-                          "value": a.trees / dt, "unit": "trees/s", "n_gpus": bsp.world if dev.type == "cuda" else 0, "device": dev.type,
+                          "value": a.trees / dt, "unit": "trees/s", "n_gpus": bsp.world if dev.type == "cuda" else 0, "ranks": bsp.world, "device": dev.type,
                           "ms_per_tree": 1000 * dt / a.trees,
                           "projected_500_trees_s": 500 * dt / a.trees, "sketch_bin_s": t_prep,
                           "train_error": err, "scaling": "strong", "data": "synthetic Higgs-shaped"}),
               flush=True)
     bsp.finalize()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

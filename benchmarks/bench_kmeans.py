@@ -21,6 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from wormhole_amd.models.kmeans import KMeans  # noqa: E402
 from wormhole_amd.parallel.bsp import BSP  # noqa: E402
 from wormhole_amd.parallel.comm import env_local_rank  # noqa: E402
+from wormhole_amd.parallel import launch  # noqa: E402
 
 
 def main():
@@ -32,7 +33,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: the framework's PyTorch CPU path (anchor numbers)")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); > 1 without a launcher: started here")
     a = ap.parse_args()
+    if a.gpus > 1 and not launch.launched():  # before any GPU call in this process
+        return launch.self_launch(os.path.abspath(__file__), sys.argv[1:], a.gpus, a.device)
     if a.device == "cuda":
         torch.cuda.set_device(env_local_rank())
         dev = torch.device("cuda", env_local_rank())
@@ -43,6 +48,7 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize()
     bsp = BSP(dev)
+    launch.verify_world(bsp.comm, a.gpus if launch.launched() else 1)
     n = a.rows // bsp.world
     g = torch.Generator(device=dev).manual_seed(1234 + bsp.rank)
     centers = torch.randn(a.k, a.dim, device=dev, generator=g)
@@ -67,14 +73,15 @@ def main():
     flops = 2.0 * a.rows * a.k * a.dim * a.iters
     if bsp.rank == 0:
         print(json.dumps({"metric": "k-means iterations/s (k=%d, dense %dx%d)" % (a.k, a.rows, a.dim),
-                          "value": a.iters / dt, "unit": "iter/s", "n_gpus": bsp.world if dev.type == "cuda" else 0, "device": dev.type,
+                          "value": a.iters / dt, "unit": "iter/s", "n_gpus": bsp.world if dev.type == "cuda" else 0, "ranks": bsp.world, "device": dev.type,
                           "ms_per_iter": 1000 * dt / a.iters, "rows_per_s": a.rows * a.iters / dt,
                           "assign_tflops": flops / dt / 1e12, "scaling": "strong",
                           "dtype": ("exact fp32 argmax (bf16x3 split MFMA + fp32 re-score of near-ties)" if km.split else "fp32 (exact fp32 MFMA)") if dev.type == "cuda" else "fp64 (CPU reference path)",
                           "rescored_rows_last_iter": int(km.rescored.item()) if km.rescored is not None else None, "data": "synthetic gaussian mixture"}),
               flush=True)
     bsp.finalize()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

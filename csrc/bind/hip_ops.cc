@@ -734,6 +734,7 @@ class KVStore {
     TORCH_CHECK(P >= 1 && segHS.numel() == P + 1, "ps_open: bad segment tables");
     TORCH_CHECK(n < (1 << 24), "ps_open: at most 2^24 - 1 keys per minibatch and shard");
     epoch_ = epoch_ % 255 + 1;  // 1..255; a wrap to 1 sweeps the table's tags
+    ++opens_;
     TORCH_CHECK(rows_cap >= n, "ps_open: reply buffer too small");
     c10::DeviceGuard g(keys.device());
     auto s = cur_stream(keys);
@@ -840,6 +841,7 @@ class KVStore {
 
   Tensor slots_, keys_, w_, z_, sq_, cnt_, vrow_, V_, VG_, vnext_, stats_, vbase_;
   int64_t epoch_ = 0;  // ps_open chain-tag epoch (1..255)
+  int64_t opens_ = 0;  // ps_open calls so far (tests: the epoch wrapped)
 
  private:
   void set_slots(const Tensor& sl) {
@@ -2133,6 +2135,9 @@ PYBIND11_MODULE(_hip, m) {
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
         py::arg("nshard") = 1, py::arg("hint") = 0, py::arg("exchange") = py::none());
   m.def("fm_forward", &fm_forward);
+  m.def("set_cu_reserve", [](int64_t n) { wh::fm_set_cu_reserve((int)n); },
+        "CUs the persistent FM kernels leave free for concurrent collectives");
+  m.def("cu_reserve", []() { return (int64_t)wh::fm_cu_reserve(); });
   m.def("fm_backward", &fm_backward);
   m.def("fm_backward_plan", &fm_backward_plan);
   m.def("fm_backward_run", &fm_backward_run);
@@ -2208,6 +2213,7 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("vstride", &KVStore::vstride)
       .def_property_readonly("cap", &KVStore::cap)
       .def_property_readonly("vcap", &KVStore::vcap)
+      .def_readonly("ps_opens", &KVStore::opens_)
       .def_readonly("slots", &KVStore::slots_)
       .def_readonly("keys", &KVStore::keys_)
       .def_readonly("w", &KVStore::w_)

@@ -893,17 +893,33 @@ __global__ __launch_bounds__(kThreads) void k_grad_scale(const int64_t* __restri
 
 int64_t fm_fwd_partials() { return 4 * kFwdBlocks; }
 
-// Persistent grids are sized to what is actually resident: blocks per CU from
-// the occupancy API (register-limited kernels fit fewer than 8) x CU count,
-// so no block waits for a second round behind a full machine.
-template <typename K>
-static int resident_blocks(K kernel, int cap) {
+// CUs the persistent FM kernels leave free for concurrent collectives. A
+// persistent grid that fills every CU's wave slots keeps RCCL's channel
+// workgroups (all-to-all over xGMI, issued beside the compute) from being
+// dispatched until the whole kernel drains, which serialises the transfer
+// behind the compute instead of overlapping it. Set by the multi-rank step
+// (kv/psx.py: WH_RCCL_CU_RESERVE); 0 on one GPU.
+static int g_cu_reserve = 0;
+
+void fm_set_cu_reserve(int cus) { g_cu_reserve = cus < 0 ? 0 : cus; }
+int fm_cu_reserve() { return g_cu_reserve; }
+
+static int device_cus() {
   static int cus = 0;
   if (cus == 0) {
     int dev = 0;
     WH_HIP_CHECK(hipGetDevice(&dev));
     WH_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
+  return std::max(1, cus - std::min(g_cu_reserve, cus / 2));
+}
+
+// Persistent grids are sized to what is actually resident: blocks per CU from
+// the occupancy API (register-limited kernels fit fewer than 8) x CU count,
+// so no block waits for a second round behind a full machine.
+template <typename K>
+static int resident_blocks(K kernel, int cap) {
+  const int cus = device_cus();
   int per_cu = 0;
   WH_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0));
   const int n = std::max(1, per_cu) * cus;
@@ -917,10 +933,7 @@ static int blocks_override(int cap) {
     return e ? std::atoi(e) : 0;
   }();
   if (per_cu <= 0) return 0;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  return std::min(per_cu * cus, cap);
+  return std::min(per_cu * device_cus(), cap);
 }
 
 #define WH_RESIDENT(G, KERNEL, CAP)                                              \

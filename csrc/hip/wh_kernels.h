@@ -275,6 +275,9 @@ bool ps_pack_gw(const float* gw, int64_t U, int vstride, const int64_t* segS,
 //   loss | 256, met[4] += this minibatch's accuracy flipped below 0.5
 //   part: scratch of fm_fwd_partials() doubles (per-block metric partials)
 int64_t fm_fwd_partials();
+// CUs the persistent FM grids leave free for concurrent RCCL kernels
+void fm_set_cu_reserve(int cus);
+int fm_cu_reserve();
 void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const float* val,
                 const float* w_or_hdr, const float* vc, int vstride, const float* label, int loss,
                 float* py, float* dual, float* xv, double* met, double* part,

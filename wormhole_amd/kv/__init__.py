@@ -17,7 +17,6 @@ DiFacto values are variable length (ps-lite ZVPull/ZVPush with sizes 1 or
 a second all-to-all whose per-peer row counts come from the owner's pull.
 The gradient push mirrors it (4-byte gw per key + the embedding rows).
 """
-import os
 
 import torch
 
@@ -66,7 +65,7 @@ class StoreGuard:
             # the summary (a one-wave read of the table's counters) and its
             # copy run on a side stream behind the open, off the compute
             # stream's critical path; read() waits for them one open later
-            side = self._side if _GUARD_SIDE else torch.cuda.current_stream()
+            side = self._side
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
                 s = self.store.summary()
@@ -117,10 +116,6 @@ class StoreGuard:
                 st.grow_v(vcap)
                 self.vgrows += 1
         self.since += n
-
-
-# WH_GUARD_SIDE=0: the per-open summary on the compute stream
-_GUARD_SIDE = os.environ.get("WH_GUARD_SIDE", "1") != "0"
 
 
 def make_store(cap, vcap, dim, device):

@@ -50,29 +50,17 @@ import torch
 from .. import _native, ops
 
 TRAIN, VAL, PRED = 0, 1, 2
-# Where the next minibatch's localize runs (WH_PSX_LOCALIZE):
-#   "s"     on the compute stream S, between the owner open and the backward;
-#   "ls"    on its own stream at the same point (measured slower: loopback
-#           P=8 106 vs 108 M ex/s -- it only stretches the backward it
-#           overlaps, and S drains while the host waits for its count read);
-#   "early" on its own stream, begun as soon as this minibatch's localize is
-#           finished (overlapping the forward, the owner push and the open),
-#           with its count collective C0 issued after the open (deferred
-#           exchange: C0 carries the open's V row counts). The default on
-#           GPUs: loopback P=8 108.2 -> 116.4 M ex/s, RCCL loopback 88.1 ->
-#           92.5 (tools/gpu/r2_early.sh).
-_LOC_MODE = os.environ.get("WH_PSX_LOCALIZE", "early")
-_LOC_STREAM = _LOC_MODE in ("ls", "early")
-_LOC_EARLY = _LOC_MODE == "early"
-# opt-in: measured 9 % slower at loopback P=8 (106.4 vs 117.2 M ex/s,
-# tools/gpu/r2_push.sh) -- the push's table atomics and the forward's row
-# gathers contend for the same memory pipeline and both stretch
-_PUSH_STREAM = os.environ.get("WH_PSX_PUSH_STREAM", "0") != "0"
-# a training step's AUC enqueued after its backward (models/difacto.py)
-_AUC_LATE = os.environ.get("WH_AUC_LATE", "1") != "0"
-# C3 (the push) of a pipelined step is issued at the start of the next call,
-# right after that call's C2 (WH_PSX_C3_LATE=0: at the end of the backward)
-_C3_LATE = os.environ.get("WH_PSX_C3_LATE", "1") != "0"
+# (Stream placements measured and dropped -- docs/performance.md "Measured
+# dead ends": the owner push on its own stream beside the forward, the next
+# localize on a side stream at the open instead of right after this one's
+# localize, C3 issued at the end of the backward instead of behind the next
+# call's C2, a training step's AUC right after its forward.)
+_COMM_TIMING = os.environ.get("WH_COMM_TIMING", "0") not in ("", "0")
+# CUs the persistent FM kernels leave free for RCCL's channel workgroups when
+# the exchange runs over RCCL (csrc/hip/fm.hip fm_set_cu_reserve): C2 / C3
+# are issued while a forward / backward holds the machine, and must start
+# then rather than after it drains.
+_CU_RESERVE = int(os.environ.get("WH_RCCL_CU_RESERVE", "32"))
 
 
 def _cdiv(a, b):
@@ -136,6 +124,44 @@ class _EventRing:
         return ev
 
 
+class _CollTimer:
+    """GPU time of each collective from the moment its inputs are ready on
+    the issuing stream to the moment it has landed (a timing stream waits
+    on the work, then records): RCCL's own queueing behind earlier
+    collectives is included, which is what the step waits for."""
+
+    def __init__(self, dev):
+        self.ts = torch.cuda.Stream(device=dev)
+        self.pairs = []
+        self.pend = {}
+
+    def ready(self, c):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.pend[c] = ev
+
+    def done(self, c, work):
+        w = getattr(work, "work", None)
+        end = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(self.ts):
+            if w is not None:
+                w.wait()
+            else:
+                self.ts.wait_stream(torch.cuda.current_stream())
+            end.record(self.ts)
+        self.pairs.append((c, self.pend.pop(c), end))
+
+    def reset(self):
+        self.pairs = []
+
+    def report(self):
+        out = {}
+        for c, a, b in self.pairs:
+            b.synchronize()
+            out[c] = out.get(c, 0.0) + a.elapsed_time(b)
+        return out
+
+
 class PsxDifacto:
     def __init__(self, lrn):
         self.lrn = lrn
@@ -146,17 +172,13 @@ class PsxDifacto:
         self.dev = lrn.device
         self.cuda = self.dev.type == "cuda"
         self.cs = torch.cuda.Stream(device=self.dev) if self.cuda else None
-        # the next minibatch's localize runs on its own stream, concurrently
-        # with the previous minibatch's backward on S (as on one shard,
-        # models/_pipeline.py), when WH_PSX_LOCALIZE_STREAM=1
-        self.ls = (torch.cuda.Stream(device=self.dev)
-                   if self.cuda and _LOC_STREAM else None)
-        # the owner applies the previous push on its own stream, concurrently
-        # with the forward, when WH_PSX_PUSH_STREAM=1
-        self.os = (torch.cuda.Stream(device=self.dev)
-                   if self.cuda and _PUSH_STREAM else None)
-        self.push_side = False
+        # the next minibatch's localize runs on its own stream, begun as soon
+        # as this minibatch's localize is finished (as on one shard,
+        # models/_pipeline.py), concurrently with the forward / push / open
+        self.ls = torch.cuda.Stream(device=self.dev) if self.cuda else None
         self.S = torch.cuda.current_stream(self.dev) if self.cuda else None
+        if self.cuda and getattr(self.comm, "backend", "") in ("nccl", "loopback-rccl"):
+            _native.hip().set_cu_reserve(_CU_RESERVE)
         self.pins = _PinRing(self.dev) if self.cuda else None
         self.events = _EventRing() if self.cuda else None
         self.tau = 1 if int(getattr(lrn.conf, "max_concurrency", 2) or 2) >= 2 else 0
@@ -164,6 +186,47 @@ class PsxDifacto:
         self.pull = None    # opened, reply not yet exchanged
         self.push = None    # push in flight to the owners
         self.uhint = 0
+        # bytes this rank sends to OTHER ranks per collective (C0..C3): what
+        # crosses xGMI; (own-segment rows stay in HBM)
+        self.wire = [0, 0, 0, 0]
+        self.wire_steps = 0
+        # WH_COMM_TIMING=1: per-collective (issue-ready -> landed) GPU times
+        self.timer = _CollTimer(self.dev) if (self.cuda and _COMM_TIMING) else None
+
+    # ------------------------------------------------------------ wire stats
+    def _tally(self, c, x, send_rows):
+        row = x.element_size()
+        for d in x.shape[1:]:
+            row *= int(d)
+        r = getattr(self.comm, "rank", 0)
+        self.wire[c] += row * (sum(int(v) for v in send_rows) - int(send_rows[r]))
+
+    def _a2a(self, c, x, send_rows, recv_rows):
+        """Issue collective Cc (async) and account for its bytes."""
+        self._tally(c, x, send_rows)
+        if self.timer is not None:
+            self.timer.ready(c)
+        out, work = self.comm.all_to_all_v_async(x, send_rows, recv_rows)
+        if self.timer is not None:
+            self.timer.done(c, work)
+        return out, work
+
+    def wire_reset(self):
+        self.wire = [0, 0, 0, 0]
+        self.wire_steps = 0
+        if self.timer is not None:
+            self.timer.reset()
+
+    def wire_report(self, steps):
+        """Per-step averages since :meth:`wire_reset`: bytes each collective
+        sent to peers (and, with WH_COMM_TIMING=1, its GPU time in ms)."""
+        steps = max(int(steps), 1)
+        out = {"c%d" % c: self.wire[c] / steps for c in range(4)}
+        out["c0"] = 24 * (self.P - 1)  # {keys, overflow, V rows} per peer
+        if self.timer is not None:
+            for c, ms in self.timer.report().items():
+                out["c%d_ms" % c] = ms / steps
+        return out
 
     # ------------------------------------------------------------ streams
     def _S(self):
@@ -320,7 +383,7 @@ class PsxDifacto:
     def _c1(self, st):
         """Issue C1: this minibatch's keys (+ counts) to their owners."""
         rec = ops.ps_records(st.uniq, st.ucnt if st.use_cnt else None)
-        st.keys_o, st.w_c1 = self.comm.all_to_all_v_async(rec, st.send, st.recv)
+        st.keys_o, st.w_c1 = self._a2a(1, rec, st.send, st.recv)
 
     def _open(self, st, insert):
         """Owner side: wait for C1, then one fused open + header pack."""
@@ -339,8 +402,7 @@ class PsxDifacto:
         P = self.P
         send_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
         recv_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
-        st.rrecv, st.w_c2 = self.comm.all_to_all_v_async(st.rbuf[:sum(send_rows)], send_rows,
-                                                         recv_rows)
+        st.rrecv, st.w_c2 = self._a2a(2, st.rbuf[:sum(send_rows)], send_rows, recv_rows)
         st.rbuf = None
 
     def _reply(self, st):
@@ -351,7 +413,7 @@ class PsxDifacto:
         st.hdr, st.rows = ops.ps_unpack(st.rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d)
         st.py, st.dual, st.xv = ops.fm_forward(st.offset, st.lid, st.val, st.hdr, st.rrecv,
                                                self.vs, st.label, ops.LOSS_LOGIT, lrn.met)
-        if not (_AUC_LATE and st.train):  # (a training step's AUC follows its backward)
+        if not st.train:  # (a training step's AUC follows its backward)
             ops.auc_acc(st.py, st.label, lrn.auc_sum)
         lrn.n_mb += 1
         lrn.last_sizes = (st.U, sum(st.vrecv))
@@ -361,7 +423,8 @@ class PsxDifacto:
         P = self.P
         send_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
         recv_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
-        st.gpush, st.w_c3 = self.comm.all_to_all_v_async(st.gvc, send_rows, recv_rows)
+        st.gpush, st.w_c3 = self._a2a(3, st.gvc, send_rows, recv_rows)
+        self.wire_steps += 1
         st.gvc = None
 
     def _grad(self, st, issue=True):
@@ -383,8 +446,7 @@ class PsxDifacto:
         st.gvc = gvc
         if issue:
             self._c3(st)
-        if _AUC_LATE:
-            ops.auc_acc(st.py, st.label, lrn.auc_sum)
+        ops.auc_acc(st.py, st.label, lrn.auc_sum)
         # the worker-side tensors of this step are done
         st.rrecv = st.hdr = st.dual = st.xv = st.lid = st.csc = None
 
@@ -396,42 +458,22 @@ class PsxDifacto:
         if idx:
             gvc[torch.tensor(idx, dtype=torch.int64, device=gvc.device)] = 0
 
-    def _owner_push(self, st, side=False):
-        """Apply a landed push on the owner. side=True: on the owner stream,
-        concurrently with the worker-side forward queued next on S (the two
-        touch disjoint memory: the table vs the pulled copy); S joins it
-        before the next open (:meth:`_join_push`)."""
+    def _owner_push(self, st):
+        """Apply a landed push on the owner (one launch over all segments)."""
         lrn = self.lrn
-        if side and self.os is not None:
-            os_ = self.os
-            os_.wait_stream(self._S())  # the previous open / push are ordered first
-            with torch.cuda.stream(os_):
-                st.w_c3.wait()
-                self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o,
-                                   st.gpush, lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
-            # inputs allocated on S, read on os: not reused before os is done
-            for t in (st.gpush, st.slot, st.vpos, st.chain, st.head, st.tabs):
-                if t is not None and t.is_cuda:
-                    t.record_stream(os_)
-            self.push_side = True
-        else:
-            st.w_c3.wait()
-            self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o,
-                               st.gpush, lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
+        st.w_c3.wait()
+        self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o,
+                           st.gpush, lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
         st.w_c3 = None
         st.gpush = st.slot = st.vpos = st.chain = st.head = st.keys_o = None
-
-    def _join_push(self):
-        """S waits for an owner push running on the owner stream."""
-        if self.push_side:
-            self._S().wait_stream(self.os)
-            self.push_side = False
 
     def _remap(self, remap):
         """The table grew: translate the slot ids of in-flight steps."""
         for st in (self.pull, self.push):
             if st is not None and st.slot is not None and st.slot.numel():
-                st.slot = remap[st.slot.long()]
+                # (a -1 slot -- a failed insert or a miss -- stays -1)
+                s_ = st.slot.long()
+                st.slot = torch.where(s_ >= 0, remap[s_.clamp_min(0)], st.slot)
 
     # ----------------------------------------------------------------- API
     def _new_step(self, send, recv, label, train, data_pass, prev):
@@ -470,15 +512,12 @@ class PsxDifacto:
             # between the backward and the forward
             self._c3(self.push)
         self._set_loc(st, self._finish(), offset, val)
-        early = _LOC_EARLY and self.cuda and next_batch is not None
+        early = self.cuda and next_batch is not None
         if early:  # next minibatch's localize kernels now; its C0 after the open
             nk, no, nv = next_batch[:3]
             self._begin(nk, no, nv, st, next_batch[3] if len(next_batch) > 3 else None,
                         defer=True)
         self._c1(st)        # transfers while the previous minibatch computes
-        if self.push is not None and self.os is not None:
-            self._owner_push(self.push, side=True)  # overlaps the forward below
-            self.push = None
         if prev is not None:
             self._reply(prev)
             if self.tau == 0 and prev.train:
@@ -487,7 +526,6 @@ class PsxDifacto:
         if self.push is not None:
             self._owner_push(self.push)
             self.push = None
-        self._join_push()
         self._open(st, True)
         self.pull = st
         if early:
@@ -496,7 +534,7 @@ class PsxDifacto:
             nk, no, nv = next_batch[:3]
             self._begin(nk, no, nv, st, next_batch[3] if len(next_batch) > 3 else None)
         if self.tau == 1 and prev is not None and prev.train:
-            self._grad(prev, issue=not _C3_LATE)  # pushed before the next call's open
+            self._grad(prev, issue=False)  # C3 goes out behind the next call's C2
             self.push = prev
         self.lrn.step += 1
 
@@ -544,5 +582,4 @@ class PsxDifacto:
             self.push = None
         if st is not None and st.train:
             self._owner_push(st)
-        self._join_push()
         self.pull = None

@@ -13,8 +13,6 @@ only right before the next minibatch's localize begins, so the producer runs
 concurrently with minibatch i's localize finish. Every rank must pass
 ``next_batch`` in lockstep (the count exchange is a collective).
 """
-import os
-
 import torch
 
 from .. import ops
@@ -38,13 +36,10 @@ def localize_current(lrn, keys, offset, val):
 
 
 # DiFacto begins the next minibatch's localize right AFTER enqueueing this
-# minibatch's pull (not before it): the host reaches the pull launch sooner
-# after its count read, and the side-stream job then starts behind the pull
-# on the compute stream, still well ahead of the next count read. Measured
-# (tools/gpu/r2_late.sh): DiFacto 127.0 -> 131.7 M ex/s; the linear model,
-# whose step is short enough that the job's count read comes late, is 5 %
-# slower this way and keeps the early begin (localize_pipelined).
-BEGIN_LATE = os.environ.get("WH_BEGIN_LATE", "1") != "0"
+# minibatch's pull (localize_current + begin_next): the host reaches the pull
+# launch sooner after its count read (127.0 -> 131.7 M ex/s). The linear
+# model, whose step is short enough that the job's count read comes late, is
+# 5 % slower that way and begins it before (localize_pipelined).
 
 
 def begin_next(lrn, next_batch, uhint):
@@ -52,7 +47,7 @@ def begin_next(lrn, next_batch, uhint):
     ``uhint``: this minibatch's unique-id count (sizes the job's table)."""
     nk, no, nv = next_batch[:3]
     ready = next_batch[3] if len(next_batch) > 3 else None
-    if nk.is_cuda and _OVERLAP:
+    if nk.is_cuda:
         # The next minibatch's partitioned localize runs on its own stream,
         # concurrently with this minibatch's forward / backward / push on the
         # compute stream. The side stream first waits for everything queued
@@ -85,16 +80,14 @@ def begin_next(lrn, next_batch, uhint):
                                        exchange=lrn.kv.count_exchange()))
 
 
-# On by default since the partitioned localize (LDS dedup, no global
-# atomics): DiFacto 117.5 -> 127 M ex/s on one MI355X (tools/gpu/env_ab.sh).
-# With the round-1 hash localize it was slower (106 vs 112: its concurrent
-# atomic inserts cost the gather-bound FM kernels more than they hid).
-# Memory safety of the side-stream outputs: they are allocated on the side
+# Since the partitioned localize (LDS dedup, no global atomics) the side
+# stream pays: DiFacto 117.5 -> 127 M ex/s on one MI355X. (With the round-1
+# hash localize it was slower: its concurrent atomic inserts cost the
+# gather-bound FM kernels more than they hid.) Memory safety of the side-stream outputs: they are allocated on the side
 # stream and read on the compute stream; the side stream's next job first
 # waits for the compute stream (side.wait_stream(cur) below), so a block the
 # allocator hands back to the side stream is never rewritten before the
 # compute-stream kernels that read it have run.
-_OVERLAP = os.environ.get("WH_LOCALIZE_STREAM", "1") != "0"
 _streams = {}
 
 

@@ -11,27 +11,14 @@ learn/difacto/async_sgd.h:363-425), re-expressed on the GPU:
   ->  gradient clip / dropout / normalisation  ->  push  ->  owner applies
   FTRL on w and AdaGrad on V in one fused kernel.
 """
-import os
-
 import torch
 
 from .. import ops
-from ._pipeline import BEGIN_LATE, begin_next, localize_current, localize_pipelined
+from ._pipeline import begin_next, localize_current
 from ..kv import ShardedKV, make_store
 from ..utils import trace
 
 TRAIN, VAL, PRED = 0, 1, 2
-# WH_BWD_PLAN_STREAM=1: plan the backward on its own stream, overlapping the
-# forward. Opt-in: measured 15 % slower on one MI355X (110 vs 130 M ex/s,
-# tools/gpu/r2_plan.sh) -- the plan's look-back tiles and the one-block
-# bucket scan wait behind the persistent forward's workgroups for CU slots.
-_PLAN_STREAM = os.environ.get("WH_BWD_PLAN_STREAM", "0") != "0"
-# A training minibatch's AUC (side stream) is enqueued after its backward
-# instead of right after its forward, so its kernels overlap the push / open
-# rather than the small backward-planning kernels on the critical path:
-# 130.0 -> 134.3 M ex/s on one MI355X (tools/gpu/r2_auc.sh). WH_AUC_LATE=0
-# restores the early placement.
-_AUC_LATE = os.environ.get("WH_AUC_LATE", "1") != "0"
 
 
 class DifactoLearner:
@@ -81,9 +68,6 @@ class DifactoLearner:
             self.psx = PsxDifacto(self)
 
     # ------------------------------------------------------------------ step
-    def _localize(self, keys, offset, val, next_batch):
-        return localize_pipelined(self, keys, offset, val, next_batch)
-
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):
         """One minibatch. Returns predictions (py) for PRED, else None."""
         train = wtype == TRAIN
@@ -94,10 +78,7 @@ class DifactoLearner:
             py = self.psx.evaluate(keys, offset, val, label)
             return py if wtype == PRED else None
         with trace.span("localize"):
-            if BEGIN_LATE:
-                loc = localize_current(self, keys, offset, val)
-            else:
-                loc = self._localize(keys, offset, val, next_batch)
+            loc = localize_current(self, keys, offset, val)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
         self.uhint = uniq.numel()
         push_cnt = train and data_pass == 0 and self.dim > 0
@@ -106,65 +87,35 @@ class DifactoLearner:
                 uniq, owner_cnt, train, ucnt if push_cnt else None, self.hp, self.threshold,
                 self.l1_shrk, self.seed, recv=loc[7] if len(loc) > 7 else None)
         self.last_sizes = (uniq.numel(), sess.m)  # (unique keys, embedding rows; device)
-        if BEGIN_LATE and next_batch is not None:  # after the pull launch
+        # The next minibatch's localize begins right AFTER this pull's launch
+        # (the host reaches the pull sooner after its count read; the job's
+        # count read still comes well before the next call needs it)
+        if next_batch is not None:
             begin_next(self, next_batch, uniq.numel())
         if self.vstride == 0:  # no embedding: a plain linear model over w
             hdr, vc = hdr[:, 0].contiguous(), None
-        plan = None
-        if train and _PLAN_STREAM and self.vstride > 0 and hdr.is_cuda:
-            # the backward's planning (chunk lists + bucketing: CSC offsets and
-            # the pull header only) on its own stream, overlapping the forward
-            plan = self._bwd_plan(csc_off, csc_row, hdr, vc, offset.numel() - 1)
         with trace.span("forward"):
             py, dual, xv = ops.fm_forward(offset, lid, val, hdr, vc, self.vstride, label,
                                           ops.LOSS_LOGIT, self.met)
-            if not (_AUC_LATE and train):
+            if not train:  # (a training step's AUC follows its backward)
                 ops.auc_acc(py, label, self.auc_sum)
         self.n_mb += 1
         if train:
             with trace.span("backward"):
-                if plan is not None:
-                    pl, ev = plan
-                    cur = torch.cuda.current_stream(hdr.device.index)
-                    cur.wait_event(ev)
-                    for t in pl:  # allocated on the plan stream, used here
-                        t.record_stream(cur)
-                    gw, gvc = ops.fm_backward_run(pl, csc_off, csc_row, csc_val, dual, xv, hdr,
-                                                  vc, self.vstride)
-                else:
-                    gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, hdr, vc,
-                                              self.vstride)
+                gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, hdr, vc,
+                                          self.vstride)
                 if self.emb is not None and self.vstride > 0:
                     ops.fm_grad_post(gvc, sess.m, self.dim, self.emb.grad_clipping,
                                      self.emb.dropout, self.seed + 7919 * self.step + 1,
                                      bool(self.emb.grad_normalization))
-            if _AUC_LATE:  # the AUC side stream starts behind the backward
-                ops.auc_acc(py, label, self.auc_sum)
+            # the AUC side stream starts behind the backward, so its kernels
+            # overlap the push / next open rather than the backward planning
+            ops.auc_acc(py, label, self.auc_sum)
             with trace.span("push"):
                 self.kv.difacto_push(sess, gw, gvc, self.hp, self.threshold, self.l1_shrk,
                                      self.seed, defer=self.defer_push)
         self.step += 1
         return py if wtype == PRED else None
-
-    def _bwd_plan(self, csc_off, csc_row, hdr, vc, nrows):
-        """Enqueue the backward's phase 1 on the plan stream after everything
-        queued on the compute stream so far (this minibatch's pull, which
-        also last used the shared look-back workspace); returns (plan, event).
-        Inputs are read there (record_stream keeps their blocks from reuse)."""
-        dev = hdr.device
-        cur = torch.cuda.current_stream(dev.index)
-        if self._plan_stream is None:
-            self._plan_stream = torch.cuda.Stream(device=dev)
-        ps = self._plan_stream
-        ps.wait_stream(cur)
-        for t in (csc_off, csc_row, hdr):
-            t.record_stream(ps)
-        with torch.cuda.stream(ps):
-            pl = ops.fm_backward_plan(csc_off, csc_row, hdr, vc.shape[0] if vc is not None else 0,
-                                      nrows, self.vstride)
-            ev = torch.cuda.Event()
-            ev.record(ps)
-        return pl, ev
 
     # -------------------------------------------------------------- progress
     def flush(self):
