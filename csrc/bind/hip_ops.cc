@@ -724,7 +724,6 @@ class KVStore {
     CHECK_DEV(keys); CHECK_CONT(keys);
     CHECK_IN(segS, torch::kInt64);
     CHECK_IN(segHS, torch::kInt64);
-    TORCH_CHECK(vstride_ > 0, "ps_open needs an embedding store");
     const bool rec = keys.scalar_type() == torch::kInt32;
     TORCH_CHECK(rec ? (keys.dim() == 2 && keys.size(1) == 3) : keys.scalar_type() == torch::kInt64,
                 "ps_open: keys must be int64 [n] or int32 records [n, 3]");
@@ -745,8 +744,10 @@ class KVStore {
     auto vpos = torch::empty({n + 1}, keys.options().dtype(torch::kInt64));
     auto chain = torch::empty({std::max<int64_t>(n, 1)}, i32);
     auto head = torch::empty({std::max<int64_t>(n, 1)}, keys.options().dtype(torch::kUInt8));
-    auto rbuf = torch::empty({rows_cap, (int64_t)vstride_}, f32);
+    // linear (vstride 0): the reply is w_out itself (returned in rbuf's place)
+    auto rbuf = torch::empty({vstride_ > 0 ? rows_cap : 0, (int64_t)std::max(vstride_, 1)}, f32);
     auto vcnt = torch::empty({P}, keys.options().dtype(torch::kInt64));
+    if (vstride_ == 0) vcnt.zero_();
     if (!vbase_.defined()) vbase_ = torch::empty({1}, vnext_.options());
     const bool ok = wh::ps_open(
         table(), rec ? nullptr : reinterpret_cast<const uint64_t*>(keys.data_ptr()),
@@ -756,7 +757,35 @@ class KVStore {
         ptr<float>(wout), ptr<int64_t>(vpos), reinterpret_cast<uint32_t*>(chain.data_ptr()),
         reinterpret_cast<uint8_t*>(head.data_ptr()), ptr<float>(rbuf), ptr<int64_t>(vcnt), s);
     TORCH_CHECK(ok, "ps_open: limits exceeded (P <= 256, n < 2^24)");
-    return {slot.narrow(0, 0, n), vpos, chain.narrow(0, 0, n), head.narrow(0, 0, n), rbuf, vcnt};
+    return {slot.narrow(0, 0, n), vpos, chain.narrow(0, 0, n), head.narrow(0, 0, n),
+            vstride_ > 0 ? rbuf : wout.narrow(0, 0, n), vcnt};
+  }
+
+  // Linear owner push of a P-shard minibatch: g [n] = the gradients pushed
+  // for this owner's received keys (segment order); t0 = SGD requests so far.
+  void ps_push_linear(const Tensor& slot, const c10::optional<Tensor>& chain,
+                      const c10::optional<Tensor>& head, const Tensor& segS, const Tensor& g,
+                      int64_t algo, double alpha, double beta, double l1, double l2, double t0) {
+    CHECK_IN(slot, torch::kInt32);
+    CHECK_IN(segS, torch::kInt64);
+    CHECK_IN(g, torch::kFloat32);
+    const int64_t n = slot.numel();
+    TORCH_CHECK(g.numel() == n, "ps_push_linear: gradient size mismatch");
+    TORCH_CHECK(vstride_ == 0, "ps_push_linear needs a linear store");
+    const uint32_t* cp = nullptr;
+    const uint8_t* hp = nullptr;
+    if (chain.has_value() && chain->defined()) {
+      CHECK_IN((*chain), torch::kInt32);
+      TORCH_CHECK(head.has_value() && head->defined() && chain->numel() == n &&
+                      head->numel() == n, "ps_push_linear: chain / head size mismatch");
+      cp = reinterpret_cast<const uint32_t*>(chain->data_ptr());
+      hp = reinterpret_cast<const uint8_t*>(head->data_ptr());
+    }
+    c10::DeviceGuard dg(slot.device());
+    wh::LinearHP h{(int)algo, (float)alpha, (float)beta, (float)l1, (float)l2, 0.f};
+    TORCH_CHECK(wh::ps_push_linear(table(), ptr<int32_t>(slot), cp, hp, n, ptr<int64_t>(segS),
+                                   (int)segS.numel() - 1, ptr<float>(g), h, t0, cur_stream(slot)),
+                "ps_push_linear: limits exceeded (P <= 256)");
   }
 
   // Owner side push of a P-shard minibatch: gbuf = the received push buffer
@@ -1065,12 +1094,15 @@ Tensor ps_records(const Tensor& uniq, const c10::optional<Tensor>& ucnt) {
   return rec;
 }
 
-// C0 buffers from the owner counts [P+1] and the V row counts [P] (optional):
-// (send int64 [3P], payload int64 [5P+1]; payload[P+1 : 4P+1] is the
-// exchange's receive slot)
-std::vector<Tensor> ps_c0(const Tensor& owner_cnt, const c10::optional<Tensor>& vcnt) {
+// C0 buffers from the owner counts [S+1] (S shards + the overflow flag), the
+// V row counts [P] (optional) and this rank's has-data flag: (send int64
+// [4P], payload int64 [S+1+5P]; payload[S+1 : S+1+4P] is the exchange's
+// receive slot)
+std::vector<Tensor> ps_c0(const Tensor& owner_cnt, const c10::optional<Tensor>& vcnt, int64_t P,
+                          int64_t flag) {
   CHECK_IN(owner_cnt, torch::kInt64);
-  const int P = (int)owner_cnt.numel() - 1;
+  const int S = (int)owner_cnt.numel() - 1;
+  TORCH_CHECK(S >= 1 && S <= P, "ps_c0: owner counts must cover 1..P shards");
   const int64_t* vp = nullptr;
   if (vcnt.has_value() && vcnt->defined()) {
     CHECK_IN((*vcnt), torch::kInt64);
@@ -1078,10 +1110,10 @@ std::vector<Tensor> ps_c0(const Tensor& owner_cnt, const c10::optional<Tensor>& 
     vp = ptr<int64_t>(*vcnt);
   }
   c10::DeviceGuard g(owner_cnt.device());
-  auto send = torch::empty({3 * P}, owner_cnt.options());
-  auto payload = torch::empty({5 * P + 1}, owner_cnt.options());
-  TORCH_CHECK(wh::ps_c0(ptr<int64_t>(owner_cnt), vp, P, ptr<int64_t>(send), ptr<int64_t>(payload),
-                        cur_stream(owner_cnt)),
+  auto send = torch::empty({4 * P}, owner_cnt.options());
+  auto payload = torch::empty({S + 1 + 5 * P}, owner_cnt.options());
+  TORCH_CHECK(wh::ps_c0(ptr<int64_t>(owner_cnt), vp, S, (int)P, flag, ptr<int64_t>(send),
+                        ptr<int64_t>(payload), cur_stream(owner_cnt)),
               "ps_c0: too many peers");
   return {send, payload};
 }
@@ -2206,6 +2238,7 @@ PYBIND11_MODULE(_hip, m) {
       .def("difacto_push", &KVStore::difacto_push)
       .def("ps_open", &KVStore::ps_open)
       .def("ps_push", &KVStore::ps_push)
+      .def("ps_push_linear", &KVStore::ps_push_linear)
       .def("grow", &KVStore::grow)
       .def("grow_v", &KVStore::grow_v)
       .def("summary", &KVStore::summary)

@@ -120,6 +120,40 @@ __device__ __forceinline__ void adagrad4(float4& v, float4& cg, const float4& g,
   }
 }
 
+__device__ __forceinline__ float l1l2_solve(float z, float eta, float l1, float l2) {
+  // argmin_x 0.5*eta*(x - z/eta)^2 + l1|x| + l2 x^2 (soft threshold)
+  // (reference L1L2::Solve, learn/linear/penalty.h:36-41)
+  if (z <= l1 && z >= -l1) return 0.f;
+  return (z > 0 ? z - l1 : z + l1) / (eta + l2);
+}
+
+// one linear-model push of gradient g into slot e (reference SGD / AdaGrad /
+// FTRL handles, learn/linear/async_sgd.h:85-99, 123-135, 160-175); returns
+// the new w. sgd_eta: SGD only, (beta + sqrt(t)) / alpha for this push.
+__device__ __forceinline__ float linear_update(KVSlot& e, float g, const LinearHP& hp,
+                                               float sgd_eta) {
+  const float oldw = e.w;
+  float neww;
+  if (hp.algo == 1) {  // SGD
+    neww = l1l2_solve(sgd_eta * oldw - g, sgd_eta, hp.l1, hp.l2);
+  } else if (hp.algo == 2) {  // AdaGrad
+    const float sq = sqrtf(e.sq * e.sq + g * g);
+    e.sq = sq;
+    const float eta = (sq + hp.beta) / hp.alpha;
+    neww = l1l2_solve(eta * oldw - g, eta, hp.l1, hp.l2);
+  } else {  // FTRL
+    const float sq0 = e.sq;
+    const float sq = sqrtf(sq0 * sq0 + g * g);
+    e.sq = sq;
+    const float sigma = (sq - sq0) / hp.alpha;
+    const float z = e.z + g - sigma * oldw;
+    e.z = z;
+    neww = l1l2_solve(-z, (hp.beta + sq) / hp.alpha, hp.l1, hp.l2);
+  }
+  e.w = neww;
+  return neww;
+}
+
 __device__ __forceinline__ void count_nnz_delta(float oldw, float neww, int64_t* stats) {
   const int d = (oldw == 0.f && neww != 0.f) ? 1 : ((oldw != 0.f && neww == 0.f) ? -1 : 0);
   long long s = wave_sum_ll(d);

@@ -56,12 +56,6 @@ __global__ __launch_bounds__(kThreads) void k_kv_occupied(const KVSlot* tsl, int
   }
 }
 
-__device__ __forceinline__ float l1l2_solve(float z, float eta, float l1, float l2) {
-  // argmin_x 0.5*eta*(x - z/eta)^2 + l1|x| + l2 x^2 (soft threshold)
-  if (z <= l1 && z >= -l1) return 0.f;
-  return (z > 0 ? z - l1 : z + l1) / (eta + l2);
-}
-
 __global__ __launch_bounds__(kThreads) void k_linear_pull(const KVSlot* tsl, const int32_t* slot,
                                                           int64_t n, float* out) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -79,25 +73,8 @@ __global__ __launch_bounds__(kThreads) void k_linear_push(KVTable t, const int32
   if (i < n) {
     const int32_t s = slot[i];
     if (s >= 0) {
-      const float g = grad[i];
       oldw = t.sl[s].w;
-      if (hp.algo == 1) {  // SGD, eta = (beta + sqrt(t)) / alpha
-        neww = l1l2_solve(hp.sgd_eta * oldw - g, hp.sgd_eta, hp.l1, hp.l2);
-      } else if (hp.algo == 2) {  // AdaGrad
-        const float sq = sqrtf(t.sl[s].sq * t.sl[s].sq + g * g);
-        t.sl[s].sq = sq;
-        const float eta = (sq + hp.beta) / hp.alpha;
-        neww = l1l2_solve(eta * oldw - g, eta, hp.l1, hp.l2);
-      } else {  // FTRL
-        const float sq0 = t.sl[s].sq;
-        const float sq = sqrtf(sq0 * sq0 + g * g);
-        t.sl[s].sq = sq;
-        const float sigma = (sq - sq0) / hp.alpha;
-        const float z = t.sl[s].z + g - sigma * oldw;
-        t.sl[s].z = z;
-        neww = l1l2_solve(-z, (hp.beta + sq) / hp.alpha, hp.l1, hp.l2);
-      }
-      t.sl[s].w = neww;
+      neww = linear_update(t.sl[s], grad[i], hp, hp.sgd_eta);
     }
   }
   count_nnz_delta(oldw, neww, t.stats);

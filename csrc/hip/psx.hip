@@ -351,21 +351,21 @@ __global__ __launch_bounds__(kThreads) void k_ps_records(const uint64_t* __restr
   rec[3 * i + 2] = ucnt ? ucnt[i] : 0;
 }
 
-// C0: send[3p..] = {keys for p, own table-overflow flag, V rows for p};
-// payload = [owner_cnt (P+1) | received 3P (filled by the exchange) | vcnt P]
+// C0: send[4p..] = {keys for p (0 for a peer that owns no shard: p >= S),
+// own table-overflow flag, V rows for p, this rank's has-data flag};
+// payload = [owner_cnt (S+1) | received 4P (filled by the exchange) | vcnt P]
 __global__ __launch_bounds__(256) void k_ps_c0(const int64_t* __restrict__ owner_cnt,
-                                               const int64_t* __restrict__ vcnt, int P,
-                                               int64_t* __restrict__ send,
+                                               const int64_t* __restrict__ vcnt, int S, int P,
+                                               int64_t flag, int64_t* __restrict__ send,
                                                int64_t* __restrict__ payload) {
-  for (int p = threadIdx.x; p <= P; p += blockDim.x) {
-    payload[p] = owner_cnt[p];
-    if (p < P) {
-      const int64_t v = vcnt ? vcnt[p] : 0;
-      send[3 * p] = owner_cnt[p];
-      send[3 * p + 1] = owner_cnt[P];
-      send[3 * p + 2] = v;
-      payload[4 * P + 1 + p] = v;
-    }
+  for (int p = threadIdx.x; p <= S; p += blockDim.x) payload[p] = owner_cnt[p];
+  for (int p = threadIdx.x; p < P; p += blockDim.x) {
+    const int64_t v = vcnt ? vcnt[p] : 0;
+    send[4 * p] = p < S ? owner_cnt[p] : 0;
+    send[4 * p + 1] = owner_cnt[S];
+    send[4 * p + 2] = v;
+    send[4 * p + 3] = flag;
+    payload[S + 1 + 4 * P + p] = v;
   }
 }
 
@@ -592,7 +592,50 @@ __global__ __launch_bounds__(kThreads) void k_ps_push(
   if (lane == 0 && newv) atomicAdd(stat_ptr(t.stats, 1), (unsigned long long)newv);
 }
 
+// Linear model (vstride 0): the owner's push. g[i] is the gradient a peer
+// pushed for key i of this owner's received list (segments in peer order).
+// Only a key's chain head updates it, over the chain in ascending index =
+// peer order, so each worker's push lands as one sequential request (the
+// ps-lite server handles requests one at a time). SGD's t counts requests:
+// segment p of this batch is request t0 + p + 1.
+__global__ __launch_bounds__(kThreads) void k_psl_push(
+    KVTable t, const int32_t* __restrict__ slot, const uint32_t* __restrict__ chain,
+    const uint8_t* __restrict__ headf, int64_t n, const int64_t* __restrict__ segS, int P,
+    const float* __restrict__ g, LinearHP hp, double t0) {
+  __shared__ int64_t sS[kMaxSeg + 1];
+  load_seg(segS, sS, P);
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  float w0 = 0.f, w = 0.f;
+  if (i < n) {
+    const int32_t s = slot[i];
+    const bool head = s >= 0 && (!chain || headf[i]);
+    if (head) {
+      KVSlot& e = t.sl[s];
+      w0 = w = e.w;
+      const bool single = !chain || chain[i] == 0u;
+      for (int64_t el = single ? i : chain_next_after(chain, i, -1); el >= 0;
+           el = single ? -1 : chain_next_after(chain, i, el)) {
+        float eta = 0.f;
+        if (hp.algo == 1) eta = (float)((hp.beta + sqrt(t0 + seg_of(sS, P, el) + 1.0)) / hp.alpha);
+        w = linear_update(e, g[el], hp, eta);
+      }
+    }
+  }
+  count_nnz_delta(w0, w, t.stats);
+}
+
 }  // namespace
+
+bool ps_push_linear(const KVTable& t, const int32_t* slot, const uint32_t* chain,
+                    const uint8_t* head, int64_t n, const int64_t* segS, int P, const float* g,
+                    LinearHP hp, double t0, hipStream_t s) {
+  if (P < 1 || P > kMaxSeg || t.vstride != 0) return false;
+  if (n <= 0) return true;
+  hipLaunchKernelGGL(k_psl_push, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t, slot,
+                     chain, head, n, segS, P, g, hp, t0);
+  return true;
+}
 
 bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t n, int use_cnt,
              DifactoHP hp, int insert, int chains, uint32_t epoch, int32_t* vbase,
@@ -600,8 +643,8 @@ bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t
              float* w_out, int64_t* vpos, uint32_t* chain, uint8_t* head, float* rbuf,
              int64_t* vcnt, hipStream_t s) {
   const int64_t ntiles = (n + kPullTile - 1) / kPullTile;
-  if (P < 1 || P > kMaxSeg || ntiles > kLbMaxTiles || n >= (1 << 24) || t.vstride == 0 ||
-      epoch < 1 || epoch > 255)
+  if (P < 1 || P > kMaxSeg || ntiles > kLbMaxTiles || n >= (1 << 24) || epoch < 1 ||
+      epoch > 255)
     return false;
   hipLaunchKernelGGL(k_ps_prep, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, chain,
                      chains ? n : 0, t.vnext, vbase);
@@ -617,8 +660,10 @@ bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t
   } else {
     WH_HIP_CHECK(hipMemsetAsync(vpos, 0, sizeof(int64_t), s));
   }
-  hipLaunchKernelGGL(k_ps_pack_hdr, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, w_out,
-                     vpos, n, t.vstride, segS, segHS, P, rbuf, vcnt);
+  // linear (vstride 0): the reply is w_out itself, one float per key
+  if (t.vstride > 0)
+    hipLaunchKernelGGL(k_ps_pack_hdr, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, w_out,
+                       vpos, n, t.vstride, segS, segHS, P, rbuf, vcnt);
   return true;
 }
 
@@ -640,10 +685,11 @@ void ps_records(const uint64_t* uniq, const int32_t* ucnt, int64_t U, int32_t* r
                      U, rec);
 }
 
-bool ps_c0(const int64_t* owner_cnt, const int64_t* vcnt, int P, int64_t* send, int64_t* payload,
-           hipStream_t s) {
-  if (P < 1 || P > 4096) return false;
-  hipLaunchKernelGGL(k_ps_c0, dim3(1), dim3(256), 0, s, owner_cnt, vcnt, P, send, payload);
+bool ps_c0(const int64_t* owner_cnt, const int64_t* vcnt, int S, int P, int64_t flag,
+           int64_t* send, int64_t* payload, hipStream_t s) {
+  if (P < 1 || P > 4096 || S < 1 || S > P) return false;
+  hipLaunchKernelGGL(k_ps_c0, dim3(1), dim3(256), 0, s, owner_cnt, vcnt, S, P, flag, send,
+                     payload);
   return true;
 }
 

@@ -257,9 +257,14 @@ bool ps_push(const KVTable& t, const int32_t* slot, const int64_t* vpos, const u
 // worker: 12-byte {lo, hi, count} records of the key exchange (ucnt may be null)
 void ps_records(const uint64_t* uniq, const int32_t* ucnt, int64_t U, int32_t* rec,
                 hipStream_t s);
-// C0 count exchange buffers: send[3P] and payload[5P+1] (see psx.hip)
-bool ps_c0(const int64_t* owner_cnt, const int64_t* vcnt, int P, int64_t* send, int64_t* payload,
-           hipStream_t s);
+// C0 count exchange buffers: send[4P] and payload[S+1+5P] (see psx.hip)
+bool ps_c0(const int64_t* owner_cnt, const int64_t* vcnt, int S, int P, int64_t flag,
+           int64_t* send, int64_t* payload, hipStream_t s);
+// linear model (vstride 0) owner push over all P segments: chain heads apply
+// their key's gradients in peer order; SGD request counter starts at t0
+bool ps_push_linear(const KVTable& t, const int32_t* slot, const uint32_t* chain,
+                    const uint8_t* head, int64_t n, const int64_t* segS, int P, const float* g,
+                    LinearHP hp, double t0, hipStream_t s);
 bool ps_unpack(const float* rbuf, int64_t U, int vstride, const int64_t* segS,
                const int64_t* segHS, const int64_t* vrecv, int P, float* hdr, int64_t* rows_total,
                hipStream_t s);

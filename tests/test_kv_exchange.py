@@ -35,13 +35,15 @@ def _rank_main(rank, world, port, out_dir, defer=True, device="cpu", fixed_bytes
     else:
         comm = Comm(dev)
     emb = Embedding(dim=8, threshold=3)
-    conf = DifactoConfig(embedding=[emb], lambda_l1=0.01, l1_shrk=False, fixed_bytes=fixed_bytes)
+    conf = DifactoConfig(embedding=[emb], lambda_l1=0.01, l1_shrk=False, fixed_bytes=fixed_bytes,
+                         max_concurrency=1)  # (staleness 0 on both exchange paths)
     card = [50, 400, 3000, 20, 7]
     lr = DifactoLearner(conf, comm, device, cap=1 << 14, vcap=1 << 12, seed=5)
     lr.defer_push = defer
     for step in range(4):
         keys, label, off = [t.to(dev) for t in criteo_batch_cpu(300, 17 + rank, step, card)]
         lr.process(keys, off, None, label, 0, 0)
+    lr.flush()  # (the multi-shard step keeps its last minibatch in flight)
     # pull check: every worker sees exactly the owner's stored values
     keys, label, off = [t.to(dev) for t in criteo_batch_cpu(300, 99 + rank, 0, card)]
     uniq, ucnt, owner_cnt, lid, *_ = ops.localize(keys, off, None, comm.size)

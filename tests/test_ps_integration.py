@@ -213,3 +213,21 @@ def test_linear_local_data(work):
     assert r.returncode == 0, r.stderr[-3000:]
     rows = [l for l in r.stdout.splitlines() if re.match(r"^\s+\d+\s+\S+\s+\S+\s+", l)]
     assert any("6.51e+03" in l for l in rows), r.stdout
+
+
+@pytest.mark.parametrize("app,conf", [("linear", "learn/linear/guide/demo.conf"),
+                                      ("difacto", "learn/difacto/guide/demo.conf")])
+def test_uneven_parts_end_in_lockstep(work, app, conf):
+    """3 parts over 2 workers: one worker trains twice as many minibatches
+    and the other keeps joining the exchange with empty ones until the
+    has-data flags of the count exchange say no rank has data (no
+    per-minibatch allreduce). Every example is trained exactly once and the
+    job ends cleanly (the look-ahead batch must stay the same
+    object, or a rank issues an extra count collective and the ranks hang)."""
+    r = run(["-n", "2", "-s", "2", os.path.join(ROOT, "bin", app + ".dmlc"), conf,
+             "minibatch=100", "max_data_pass=1", "num_parts_per_file=3", 'val_data=""',
+             'model_out=""'], work, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ttl = [float(l.split()[1]) for l in r.stdout.splitlines()
+           if re.match(r"^\s+\d+\s+[\d.e+]+\s+[\d.e+]+\s", l)]
+    assert ttl and abs(ttl[-1] - 6513) < 10, r.stdout  # (printed with 3 digits)

@@ -26,10 +26,10 @@ def _conf(max_conc=2, l1_shrk=False, dim=8, thr=3):
                          max_concurrency=max_conc)
 
 
-def _run(comm, conf, device, steps=6, rows=300, seed=17, nxt=True):
+def _run(comm, conf, device, steps=6, rows=300, seed=17, nxt=True, nshard=None):
     from wormhole_amd.data.synthetic import criteo_batch_cpu
     from wormhole_amd.models.difacto import DifactoLearner
-    lr = DifactoLearner(conf, comm, device, cap=1 << 14, vcap=1 << 12, seed=5)
+    lr = DifactoLearner(conf, comm, device, cap=1 << 14, vcap=1 << 12, seed=5, nshard=nshard)
     batches = [[t.to(device) for t in criteo_batch_cpu(rows, seed, s, CARD)] for s in range(steps)]
     for s, (keys, label, off) in enumerate(batches):
         nb = None
@@ -121,7 +121,7 @@ def _free_port():
     return p
 
 
-def _two_rank_main(rank, world, port, out_dir, device, max_conc):
+def _two_rank_main(rank, world, port, out_dir, device, max_conc, nshard=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     torch.set_num_threads(1)
@@ -133,8 +133,11 @@ def _two_rank_main(rank, world, port, out_dir, device, max_conc):
         comm = Comm(dev, backend="gloo")
     else:
         comm = Comm(dev)
-    lr, prog, batches = _run(comm, _conf(max_conc=max_conc), dev, steps=6, seed=17 + rank)
+    lr, prog, batches = _run(comm, _conf(max_conc=max_conc), dev, steps=6, seed=17 + rank,
+                             nshard=nshard)
     assert lr.psx is not None
+    if nshard is not None and rank >= nshard:
+        assert not _model(lr)  # a worker that owns no shard stores nothing
     # every key's count on its owner = its occurrences over all workers
     occ = {}
     for keys, _, _ in batches:
@@ -159,7 +162,7 @@ def _two_rank_main(rank, world, port, out_dir, device, max_conc):
         assert (v is not None) == (n > 3), (k, n)
     # a fresh pull through the old exchange sees the owners' values
     keys, label, off = [t.to(dev) for t in batches[-1]]
-    uniq, ucnt, owner_cnt, lid, *_ = ops.localize(keys, off, None, comm.size)
+    uniq, ucnt, owner_cnt, lid, *_ = ops.localize(keys, off, None, lr.kv.nshard)
     sess = lr.kv.open(uniq, owner_cnt, insert=False)
     hdr, vc = lr.kv.difacto_pull(sess, False)
     vid = ops.hdr_vidx(hdr.cpu()).tolist()
@@ -173,10 +176,11 @@ def _two_rank_main(rank, world, port, out_dir, device, max_conc):
     comm.finalize()
 
 
-@pytest.mark.parametrize("max_conc", [1, 2])
-def test_psx_two_ranks_gloo(tmp_path, max_conc):
-    mp.spawn(_two_rank_main, args=(2, _free_port(), str(tmp_path), "cpu", max_conc), nprocs=2,
-             join=True)
+@pytest.mark.parametrize("max_conc,nshard", [(1, None), (2, None), (2, 1)])
+def test_psx_two_ranks_gloo(tmp_path, max_conc, nshard):
+    """(nshard = 1: the demo's `-n 2 -s 1`, one server shard, two workers)"""
+    mp.spawn(_two_rank_main, args=(2, _free_port(), str(tmp_path), "cpu", max_conc, nshard),
+             nprocs=2, join=True)
     for r in range(2):
         assert 0 < float(open(tmp_path / ("r%d" % r)).read()) < 1.0
 
@@ -270,3 +274,124 @@ def test_loopback_gpu_long_run_crosses_tag_wrap(max_conc):
     assert bad <= len(m1) // 1000, bad
     assert plb[4] == steps and plb[5] == steps * 1000
     assert abs(plb[0] / plb[5] - p1[0] / p1[5]) < (1e-3 if max_conc == 1 else 0.02)
+
+
+# ---------------------------------------------------------------- linear
+def _lin_run(comm, device, algo=3, steps=6, rows=300, seed=17, max_conc=1, nshard=None,
+             batches=None):
+    from wormhole_amd.config.schema import LinearConfig
+    from wormhole_amd.data.synthetic import criteo_batch_cpu
+    from wormhole_amd.models.linear import LinearLearner
+    conf = LinearConfig(algo=algo, lambda_l1=0.1, lr_eta=0.1, max_concurrency=max_conc)
+    lr = LinearLearner(conf, comm, device, cap=1 << 14, seed=5, nshard=nshard)
+    if batches is None:
+        batches = [[t.to(device) for t in criteo_batch_cpu(rows, seed, s, CARD)]
+                   for s in range(steps)]
+    for s, (keys, label, off) in enumerate(batches):
+        nb = (batches[s + 1][0], batches[s + 1][2], None) if s + 1 < len(batches) else None
+        lr.process(keys, off, None, label, 0, 0, next_batch=nb)
+    lr.flush()
+    return lr, lr.take_progress(), batches
+
+
+def _lin_model(lr):
+    st = lr.store
+    occ = st.occupied().long()
+    keys = st.keys[occ.to(st.keys.device)].cpu().tolist()
+    w = st.w[occ.to(st.w.device)].cpu().tolist()
+    return {int(np.int64(k)): float(x) for k, x in zip(keys, w)}
+
+
+@pytest.mark.parametrize("algo", [1, 2, 3])
+def test_linear_loopback_strict_matches_single_shard(algo):
+    """The linear model through the multi-shard step (P = 4 virtual shards,
+    staleness 0) trains the same model as the single-shard path, for SGD,
+    AdaGrad and FTRL (learn/linear/async_sgd.h:71-180)."""
+    from wormhole_amd.parallel.comm import Comm, LoopbackComm
+    one, p1, b = _lin_run(Comm("cpu", init=False), "cpu", algo)
+    lb, p4, _ = _lin_run(LoopbackComm(4, "cpu"), "cpu", algo, batches=b)
+    assert lb.psx is not None and lb.psx.linear and one.psx is None
+    m1, m4 = _lin_model(one), _lin_model(lb)
+    assert m1.keys() == m4.keys()
+    if algo == 1:  # SGD's eta follows ps-lite's request count t: 4 per step here vs 1
+        return
+    for k, w in m1.items():
+        assert abs(w - m4[k]) < 1e-5, (k, w, m4[k])
+    for a, c in zip(p1, p4):
+        assert abs(a - c) <= 1e-4 * max(1.0, abs(a)), (p1, p4)
+
+
+def test_linear_loopback_pipelined():
+    from wormhole_amd.parallel.comm import LoopbackComm
+    lb, prog, _ = _lin_run(LoopbackComm(3, "cpu"), "cpu", max_conc=2, steps=8)
+    assert lb.psx.tau == 1 and lb.psx.pull is None and lb.psx.push is None
+    assert prog[3] == 8 and prog[4] == 8 * 300
+    assert 0 < prog[0] / prog[4] < 1.0
+
+
+def _lin_oracle(all_batches, algo, l1, alpha, beta):
+    """Two workers in lockstep against one server, strict order: every step
+    both pull the same model, then the owner applies worker 0's push, then
+    worker 1's (ps-lite: one request at a time)."""
+    from wormhole_amd import _native
+    from wormhole_amd.kv.cpu_store import CpuKVStore
+    from wormhole_amd.ops import ref
+    st = CpuKVStore(1 << 16, 0, 0)
+    host = _native.host()
+    t = 0
+    for step in range(len(all_batches[0])):
+        pend = []
+        for r in range(len(all_batches)):
+            keys, label, off = all_batches[r][step]
+            uniq, ucnt, oc, lid, co, cr, cv = host.localize_cpu(keys, off, None, 1)
+            slot = st.find(uniq, True)
+            w = st.linear_pull(slot)
+            met = torch.zeros(5, dtype=torch.float64)
+            py, dual, _ = ref.fm_forward(off, lid, None, w, None, 0, label, 2, met)
+            g, _ = ref.fm_backward(co, cr, cv, dual, None, w, None, 0)
+            pend.append((slot, g))
+        for slot, g in pend:
+            t += 1
+            st.linear_push(slot, g, algo, alpha, beta, l1, 0.0, (beta + t ** 0.5) / alpha)
+    return {int(k): float(x) for k, x in zip(st.keys.tolist(), st.w.tolist())}
+
+
+def _lin_two_rank_main(rank, world, port, out_dir, nshard, algo):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    from wormhole_amd.data.synthetic import criteo_batch_cpu
+    from wormhole_amd.parallel.comm import Comm
+    comm = Comm("cpu")
+    mine = [[t for t in criteo_batch_cpu(300, 17 + rank, s, CARD)] for s in range(5)]
+    lr, prog, _ = _lin_run(comm, "cpu", algo=algo, max_conc=1, nshard=nshard, batches=mine)
+    assert lr.psx is not None and lr.psx.nshard == nshard
+    model = _lin_model(lr)
+    if rank >= nshard:
+        assert not model  # a worker that owns no shard stores nothing
+    allm = comm.allgather_object(model)
+    allb = comm.allgather_object(mine)
+    owner = {}
+    for m in allm:
+        assert not (owner.keys() & m.keys())
+        owner.update(m)
+    ref_m = _lin_oracle(allb, algo, 0.1, 0.1, 1.0)
+    assert owner.keys() == ref_m.keys()
+    for k, w in ref_m.items():
+        assert abs(owner[k] - w) < 1e-5, (k, owner[k], w)
+    comm.barrier()
+    with open(os.path.join(out_dir, "r%d" % rank), "w") as f:
+        f.write("ok\n")
+    comm.finalize()
+
+
+@pytest.mark.parametrize("nshard,algo", [(2, 3), (1, 3), (2, 1), (1, 2)])
+def test_linear_two_ranks_gloo_matches_oracle(tmp_path, nshard, algo):
+    """2 workers over gloo, S = 2 or 1 server shards (`-n 2 -s 1`): the
+    owners' weights equal a host oracle of two lockstep workers pushing to
+    one server in worker order, for FTRL, SGD (ps-lite's request count t)
+    and AdaGrad."""
+    mp.spawn(_lin_two_rank_main, args=(2, _free_port(), str(tmp_path), nshard, algo), nprocs=2,
+             join=True)
+    for r in range(2):
+        assert (tmp_path / ("r%d" % r)).read_text() == "ok\n"

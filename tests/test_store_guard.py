@@ -76,3 +76,35 @@ def test_device_store_grows_and_remaps():
     assert torch.equal(st.keys[held[1].long()], held[0])
     s = st.summary().tolist()
     assert s[0] == k.unique().numel() and s[1] == 0
+
+
+@pytest.mark.parametrize("nshard", [1, 2])
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_shrinking_minibatch_keeps_room_for_the_inflight_push(device, nshard):
+    """with l1_shrk a key's embedding row is allocated by the PUSH
+    that first makes w non-zero. A large minibatch followed by a small one:
+    the guard must reserve V rows for the large minibatch's push still in
+    flight, not only for the small coming open."""
+    from wormhole_amd.config.schema import DifactoConfig, Embedding
+    from wormhole_amd.models.difacto import DifactoLearner
+    from wormhole_amd.parallel.comm import Comm, LoopbackComm
+    dev = torch.device(device)
+    emb = Embedding(dim=4, threshold=0)
+    conf = DifactoConfig(embedding=[emb], lambda_l1=1e-6, l1_shrk=True, lr_eta=0.5)
+    comm = Comm(dev, init=False) if nshard == 1 else LoopbackComm(nshard, dev)
+    lr = DifactoLearner(conf, comm, dev, cap=1 << 12, vcap=64, seed=1)
+    g = torch.Generator().manual_seed(0)
+
+    def batch(rows, nkeys, base):
+        keys = torch.randint(0, nkeys, (rows * 4,), generator=g) + base
+        off = torch.arange(0, rows * 4 + 1, 4)
+        label = (torch.rand(rows, generator=g) > 0.5).float()
+        return keys.to(dev), off.to(dev), label.to(dev)
+    for k, (rows, nkeys) in enumerate([(20, 60), (30, 90), (600, 2000), (5, 10), (5, 10),
+                                       (5, 10)]):
+        keys, off, label = batch(rows, nkeys, 100000 * k)
+        lr.process(keys, off, None, label, 0, 0)
+    lr.flush()
+    lr.kv.guard.after_open()
+    lr.kv.guard.read()  # raises StoreError on any dropped embedding row
+    assert lr.kv.guard.vgrows >= 1 and lr.store.vcap > 64

@@ -51,6 +51,10 @@ class StoreGuard:
         self.since = 0        # keys opened since the last completed summary
         self.grows = 0
         self.vgrows = 0
+        # key counts of the last two opens: their pushes may still be in
+        # flight (the deferred push; push(i-2) under the pipelined multi-shard
+        # step) and each may allocate one V row per key after the summary
+        self.recent = [0, 0]
         self.cuda = not isinstance(store, CpuKVStore)
 
     def after_open(self):
@@ -106,9 +110,9 @@ class StoreGuard:
             if remap_cb is not None:
                 remap_cb(remap)
         if getattr(st, "vstride", 0) > 0:
-            # V rows: this open and the in-flight push may each allocate one
-            # row per key at most
-            vneed = self.vused + 2 * (self.since + n)
+            # V rows: this open, and the pushes of the previous opens not yet
+            # in the summary, may each allocate one row per key at most
+            vneed = self.vused + self.since + n + sum(self.recent)
             if vneed > st.vcap:
                 vcap = max(st.vcap, 1)
                 while vneed > vcap:
@@ -116,6 +120,7 @@ class StoreGuard:
                 st.grow_v(vcap)
                 self.vgrows += 1
         self.since += n
+        self.recent = [self.recent[1], n]
 
 
 def make_store(cap, vcap, dim, device):

@@ -345,6 +345,11 @@ class CpuKVStore:
         P = len(S) - 1
         vs = self.vstride
         slot = self.find(torch.from_numpy(ks), insert).numpy()
+        if vs == 0:  # linear: the reply is w, one float per key
+            w = np.where(slot >= 0, self._w[np.maximum(slot, 0)], 0).astype(np.float32)
+            return (torch.from_numpy(slot.astype(np.int32)), torch.zeros(n + 1, dtype=torch.int64),
+                    torch.zeros(n, dtype=torch.int32), torch.ones(n, dtype=torch.uint8),
+                    torch.from_numpy(w), torch.zeros(P, dtype=torch.int64))
         w = np.zeros(n, dtype=np.float32)
         rows = np.full(n, -1, dtype=np.int64)
         for i in range(n):
@@ -405,6 +410,16 @@ class CpuKVStore:
             gv = gbuf.reshape(-1, max(vs, 1))[HS[p + 1] + vs0:HS[p + 1] + vs0 + nv]
             self.difacto_push(slot[a:b], torch.from_numpy(hdr), torch.from_numpy(gw.copy()),
                               gv.contiguous(), h, threshold, l1_shrk, seed)
+
+    def ps_push_linear(self, slot, chain, head, segS, g, algo, alpha, beta, l1, l2, t0):
+        """Linear owner push of a P-shard minibatch: segment p (peer p's
+        request) in peer order; SGD's request counter t = t0 + p + 1."""
+        S = [int(x) for x in segS.tolist()]
+        for p in range(len(S) - 1):
+            a, b = S[p], S[p + 1]
+            if b > a:
+                eta = (beta + (t0 + p + 1) ** 0.5) / alpha
+                self.linear_push(slot[a:b], g[a:b], algo, alpha, beta, l1, l2, eta)
 
     def grow(self, newcap):
         """Host table: capacity bookkeeping only (slots never move)."""

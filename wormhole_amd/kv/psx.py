@@ -1,5 +1,7 @@
-"""Lean multi-shard DiFacto step: P > 1 ranks over RCCL/xGMI, or P virtual
-shards on one GPU (:class:`wormhole_amd.parallel.comm.LoopbackComm`).
+"""Lean multi-shard parameter-server step of DiFacto and the linear model:
+P > 1 ranks over RCCL/xGMI, or P virtual shards on one GPU
+(:class:`wormhole_amd.parallel.comm.LoopbackComm`); keys owned by the first
+S <= P ranks (``-s S``).
 
 Reference per-minibatch flow (learn/difacto/async_sgd.h:372-424): push the
 feature counts (kPushFeaCnt) -> ZVPull(w, V) -> compute -> ZVPush(gw, gV),
@@ -10,9 +12,12 @@ minibatch i's push has landed.
 Here a minibatch costs four collectives and no extra host synchronisation
 (see csrc/hip/psx.hip for the row-aligned wire layout):
 
-  C0  {key count, overflow flag, V rows of the previous pull} per peer: the
-      localize count exchange, read by the host together with the counts
-      (the ONE host read of the step)
+  C0  {key count, overflow flag, V rows of the previous pull, has data} per
+      peer: the localize count exchange, read by the host together with the
+      counts (the ONE host read of the step). The has-data flags end a pass
+      without any other collective: once no rank has a minibatch left, every
+      rank sees it in the same read (learn/solver/minibatch_solver.h:284-322
+      streams minibatches without a per-minibatch barrier either).
   C1  keys (+ counts in data pass 0), 12-byte records
   C2  pull reply: per peer one region [header rows | V rows]
   C3  push: the same regions back, [gw | gV rows]
@@ -20,7 +25,7 @@ Here a minibatch costs four collectives and no extra host synchronisation
 The owner's open (find/insert, count, lazy V, variable-length pull) and its
 push are one kernel each over all P segments. With ``max_concurrency >= 2``
 the step is software-pipelined one minibatch deep (staleness 1, as the
-reference allows by default); a call of :meth:`PsxDifacto.train` enqueues,
+reference allows by default); a call of :meth:`Psx.train` enqueues,
 on the compute stream S,
 
     unpack(i-1) fwd(i-1) | owner push(i-2) | owner open(i) pack(i) |
@@ -40,6 +45,11 @@ compute stream never waits on. The host's wait for the read of C0(i+1)
 happens in the NEXT call while S still holds bwd(i-1), so S never drains.
 ``max_concurrency = 1`` gives the strict (staleness 0) order at the cost of
 one pipeline drain per step.
+
+The linear model (learn/linear/async_sgd.h:240-301: ZPull w -> gradient ->
+ZPush) runs the same pipeline with C1 = 8-byte keys, C2 = one w per key, C3 =
+one gradient per key; its owner push applies SGD / AdaGrad / FTRL over all
+segments in one launch, each worker's gradients as one request in peer order.
 """
 import contextlib
 import os
@@ -59,8 +69,11 @@ _COMM_TIMING = os.environ.get("WH_COMM_TIMING", "0") not in ("", "0")
 # CUs the persistent FM kernels leave free for RCCL's channel workgroups when
 # the exchange runs over RCCL (csrc/hip/fm.hip fm_set_cu_reserve): C2 / C3
 # are issued while a forward / backward holds the machine, and must start
-# then rather than after it drains.
-_CU_RESERVE = int(os.environ.get("WH_RCCL_CU_RESERVE", "32"))
+# then rather than after it drains. (The forward's persistent grid fills all
+# 32 wave slots of every CU.) 16 CUs leave ~500 wave slots for RCCL's channel
+# workgroups; on one GPU (RCCL loopback, one channel) the reserve costs 1 %
+# at 16 CUs, 3 % at 32, 7 % at 64 (99.4 / 98.5 / 96.3 / 92.9 M ex/s).
+_CU_RESERVE = int(os.environ.get("WH_RCCL_CU_RESERVE", "16"))
 
 
 def _cdiv(a, b):
@@ -109,21 +122,6 @@ class _PinRing:
         return d
 
 
-class _EventRing:
-    """Reusable events: a stream wait captures the record it sees when it is
-    enqueued, so an event may be re-recorded once its waits are queued."""
-
-    def __init__(self, n=64):
-        self.ev = [torch.cuda.Event() for _ in range(n)]
-        self.i = 0
-
-    def record(self, stream):
-        ev = self.ev[self.i]
-        self.i = (self.i + 1) % len(self.ev)
-        ev.record(stream)
-        return ev
-
-
 class _CollTimer:
     """GPU time of each collective from the moment its inputs are ready on
     the issuing stream to the moment it has landed (a timing stream waits
@@ -162,13 +160,21 @@ class _CollTimer:
         return out
 
 
-class PsxDifacto:
+class Psx:
+    """The pipelined multi-shard step of both PS learners (DiFacto:
+    vstride > 0; linear: vstride == 0, where C1 moves 8-byte keys, C2 one
+    float w per key and C3 one float gradient per key). Keys are owned by
+    the first S = ``lrn.kv.nshard`` ranks (the conf's ``-s S`` servers);
+    every rank is a worker."""
+
     def __init__(self, lrn):
         self.lrn = lrn
         self.comm = lrn.comm
         self.store = lrn.store
         self.P = self.comm.size
+        self.nshard = max(1, min(int(lrn.kv.nshard), self.P))
         self.vs = self.store.vstride
+        self.linear = self.vs == 0
         self.dev = lrn.device
         self.cuda = self.dev.type == "cuda"
         self.cs = torch.cuda.Stream(device=self.dev) if self.cuda else None
@@ -180,16 +186,20 @@ class PsxDifacto:
         if self.cuda and getattr(self.comm, "backend", "") in ("nccl", "loopback-rccl"):
             _native.hip().set_cu_reserve(_CU_RESERVE)
         self.pins = _PinRing(self.dev) if self.cuda else None
-        self.events = _EventRing() if self.cuda else None
         self.tau = 1 if int(getattr(lrn.conf, "max_concurrency", 2) or 2) >= 2 else 0
         self.job = None     # (keys, LocalizeJob | finished tuple, carried step)
         self.pull = None    # opened, reply not yet exchanged
         self.push = None    # push in flight to the owners
         self.uhint = 0
+        # set by train / evaluate: no rank had data for that call's minibatch
+        # (read from the has-data flags every C0 carries), so the call did
+        # nothing but its count exchange and the pass is over
+        self.last_empty = False
+        # linear SGD: push requests this owner has applied (ps-lite's t)
+        self.requests = 0
         # bytes this rank sends to OTHER ranks per collective (C0..C3): what
-        # crosses xGMI; (own-segment rows stay in HBM)
+        # crosses xGMI (own-segment rows stay in HBM)
         self.wire = [0, 0, 0, 0]
-        self.wire_steps = 0
         # WH_COMM_TIMING=1: per-collective (issue-ready -> landed) GPU times
         self.timer = _CollTimer(self.dev) if (self.cuda and _COMM_TIMING) else None
 
@@ -213,7 +223,6 @@ class PsxDifacto:
 
     def wire_reset(self):
         self.wire = [0, 0, 0, 0]
-        self.wire_steps = 0
         if self.timer is not None:
             self.timer.reset()
 
@@ -222,16 +231,13 @@ class PsxDifacto:
         sent to peers (and, with WH_COMM_TIMING=1, its GPU time in ms)."""
         steps = max(int(steps), 1)
         out = {"c%d" % c: self.wire[c] / steps for c in range(4)}
-        out["c0"] = 24 * (self.P - 1)  # {keys, overflow, V rows} per peer
+        out["c0"] = 32 * (self.P - 1)  # {keys, overflow, V rows, has data} per peer
         if self.timer is not None:
             for c, ms in self.timer.report().items():
                 out["c%d_ms" % c] = ms / steps
         return out
 
     # ------------------------------------------------------------ streams
-    def _S(self):
-        return self.S
-
     @contextlib.contextmanager
     def _on_cs(self, *inputs):
         """Run work on the side stream (the C0 count exchange and its host
@@ -240,7 +246,7 @@ class PsxDifacto:
         if not self.cuda:
             yield
             return
-        S = self._S()
+        S = self.S
         self.cs.wait_stream(S)
         cur = torch.cuda.current_stream(self.dev)
         if cur != S:  # called from a localize job on its own stream
@@ -252,72 +258,65 @@ class PsxDifacto:
             yield
 
     # ------------------------------------------------------------ localize
-    def _exchange(self, carried):
+    def _exchange(self, carried, flag):
         """The C0 closure handed to localize: owner counts + overflow flag +
-        the carried step's per-peer V row counts, all-to-all on the comm
-        stream, then (payload, stream, 3, P) for the native job's read."""
-        P = self.P
+        the carried step's per-peer V row counts + this rank's has-data flag,
+        all-to-all on the comm stream, then (payload, stream, 4, P) for the
+        native job's read."""
+        P, S = self.P, self.nshard
 
         def ex(owner_cnt):
             vc = carried.vcnt if carried is not None else None
             with self._on_cs(owner_cnt, vc):
-                send, payload = ops.ps_c0(owner_cnt, vc)
-                payload[P + 1:4 * P + 1] = self.comm.exchange_counts_dev(send)
+                send, payload = ops.ps_c0(owner_cnt, vc, P, flag)
+                payload[S + 1:S + 1 + 4 * P] = self.comm.exchange_counts_dev(send)
             if self.cuda:
-                return payload, self.cs.cuda_stream, 3, P
+                return payload, self.cs.cuda_stream, 4, P
             return payload
         return ex
 
     def _begin(self, keys, offset, val, carried, ready=None, defer=False):
         lrn = self.lrn
-        if self.cuda and self.ls is not None:
+        flag = 1 if offset.numel() > 1 else 0  # (a host-side shape: no sync)
+        S = self.nshard
+        if self.cuda:
             # Outputs are allocated on ls and read on S; ls first waits for
             # everything queued on S, so a block the allocator hands back to
             # ls is rewritten only after the S kernels that read it have run.
             # S itself reads the job's outputs only after the host has waited
             # for the job's count read (which follows `ready` on ls).
-            S, ls = self._S(), self.ls
-            ls.wait_stream(S)
+            cs, ls = self.S, self.ls
+            ls.wait_stream(cs)
             if ready is not None:
                 ls.wait_event(ready)
             for t in (keys, offset, val):
                 if t is not None:
                     t.record_stream(ls)
-                    t.record_stream(S)
+                    t.record_stream(cs)
             with torch.cuda.stream(ls):
                 k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
-                job = _native.hip().LocalizeJob(k, offset, val, self.P, int(self.uhint),
-                                                self._exchange(carried), defer)
+                job = _native.hip().LocalizeJob(k, offset, val, S, int(self.uhint),
+                                                self._exchange(carried, flag), defer)
             self.job = (keys, job, carried)
             return
-        if ready is not None and self.cuda:
-            S = self._S()
-            S.wait_event(ready)
-            for t in (keys, offset, val):
-                if t is not None:
-                    t.record_stream(S)
         k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
-        ex = self._exchange(carried)
-        if self.cuda:
-            job = _native.hip().LocalizeJob(k, offset, val, self.P, int(self.uhint), ex)
-        else:
-            out = list(_native.host().localize_cpu(k, offset, val, self.P))
-            oc = torch.cat([out[2].to(torch.int64), torch.zeros(1, dtype=torch.int64)])
-            payload = ex(oc)
-            out[2] = oc[:self.P].clone()
-            out.append(payload[self.P + 1:].clone())
-            job = tuple(out)
-        self.job = (keys, job, carried)
+        out = list(_native.host().localize_cpu(k, offset, val, S))
+        oc = torch.cat([out[2].to(torch.int64), torch.zeros(1, dtype=torch.int64)])
+        payload = self._exchange(carried, flag)(oc)
+        out[2] = oc[:S].clone()
+        out.append(payload[S + 1:].clone())
+        self.job = (keys, tuple(out), carried)
 
     def _exchange_deferred(self):
         """Issue C0 of an early-begun localize (after the open it carries)."""
-        if self.job is not None and self.ls is not None and not isinstance(self.job[1], tuple):
+        if self.job is not None and self.cuda and not isinstance(self.job[1], tuple):
             with torch.cuda.stream(self.ls):
                 self.job[1].exchange()  # (no-op unless the job deferred it)
 
     def _counts(self):
         """The one host read of the step (count exchange C0 of the begun
-        localize): returns (send, recv); fills the carried step's V counts."""
+        localize): returns (send, recv, all_empty); fills the carried step's
+        V counts. Idempotent (the job keeps its read)."""
         self._exchange_deferred()
         keys, job, carried = self.job
         if isinstance(job, tuple):
@@ -327,9 +326,11 @@ class PsxDifacto:
         P = self.P
         tail = tail.tolist()
         if carried is not None and carried.vown is None:
-            carried.vrecv = tail[2:3 * P:3]
-            carried.vown = tail[3 * P:4 * P]
-        return [int(x) for x in oc.tolist()], [int(x) for x in tail[0:3 * P:3]]
+            carried.vrecv = tail[2:4 * P:4]
+            carried.vown = tail[4 * P:5 * P]
+        send = [int(x) for x in oc.tolist()] + [0] * (P - self.nshard)
+        empty = not any(tail[3:4 * P:4])
+        return send, [int(x) for x in tail[0:4 * P:4]], empty
 
     def _finish(self):
         """Enqueue the rest of the begun localize (after :meth:`_counts`)."""
@@ -348,23 +349,28 @@ class PsxDifacto:
 
     def _vcount_exchange(self, st):
         """Standalone C0 for a step whose V row counts rode on no localize
-        (pipeline drain, validation): one extra host read."""
-        P = self.P
-        zero = torch.zeros(P + 1, dtype=torch.int64, device=self.dev)
+        (pipeline drain, validation): one extra host read. (Linear models
+        move no V rows: nothing to exchange.)"""
+        P, S = self.P, self.nshard
+        if self.linear:
+            st.vrecv, st.vown = [0] * P, [0] * P
+            return
+        zero = torch.zeros(S + 1, dtype=torch.int64, device=self.dev)
         with self._on_cs(st.vcnt, zero):
-            send, payload = ops.ps_c0(zero, st.vcnt)
-            payload[P + 1:4 * P + 1] = self.comm.exchange_counts_dev(send)
+            send, payload = ops.ps_c0(zero, st.vcnt, P, 1)
+            payload[S + 1:S + 1 + 4 * P] = self.comm.exchange_counts_dev(send)
             v = payload.cpu().tolist()
-        st.vrecv = v[P + 3:4 * P + 1:3]
-        st.vown = v[4 * P + 1:5 * P + 1]
+        st.vrecv = v[S + 3:S + 1 + 4 * P:4]
+        st.vown = v[S + 1 + 4 * P:S + 1 + 5 * P]
 
     # ---------------------------------------------------------------- tables
     def _upload(self, st, prev):
         """Device copies of the host-known segment tables of `st` (and the V
         row counts of `prev`): one pinned host -> device copy."""
         P = self.P
-        st.Hw = [_cdiv(2 * n, self.vs) for n in st.send]
-        st.Ho = [_cdiv(2 * n, self.vs) for n in st.recv]
+        vs = max(self.vs, 1)
+        st.Hw = [_cdiv(2 * n, vs) for n in st.send] if not self.linear else [0] * P
+        st.Ho = [_cdiv(2 * n, vs) for n in st.recv] if not self.linear else [0] * P
         a = np.zeros(4 * (P + 1) + P, dtype=np.int64)
         a[1:P + 1] = np.cumsum(st.send)
         a[P + 2:2 * P + 2] = np.cumsum(st.Hw)
@@ -382,26 +388,34 @@ class PsxDifacto:
     # -------------------------------------------------------------- phases
     def _c1(self, st):
         """Issue C1: this minibatch's keys (+ counts) to their owners."""
-        rec = ops.ps_records(st.uniq, st.ucnt if st.use_cnt else None)
+        if self.linear:
+            rec = st.uniq  # 8-byte keys
+        else:
+            rec = ops.ps_records(st.uniq, st.ucnt if st.use_cnt else None)
         st.keys_o, st.w_c1 = self._a2a(1, rec, st.send, st.recv)
 
     def _open(self, st, insert):
-        """Owner side: wait for C1, then one fused open + header pack."""
+        """Owner side: wait for C1, then one fused open (+ header pack)."""
         lrn = self.lrn
         st.w_c1.wait()
         n = sum(st.recv)
-        lrn.kv.guard.before_open(n, self._remap)
+        if insert:
+            lrn.kv.guard.before_open(n, self._remap)
+        rows = sum(st.Ho) + n if not self.linear else 0
         st.slot, st.vpos, st.chain, st.head, st.rbuf, st.vcnt = self.store.ps_open(
-            st.keys_o, st.use_cnt, st.segS_o, st.segHS_o, sum(st.Ho) + n, insert, st.train,
+            st.keys_o, st.use_cnt, st.segS_o, st.segHS_o, rows, insert, st.train,
             lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
         st.keys_o = st.w_c1 = None
-        lrn.kv.guard.after_open()
+        if insert:
+            lrn.kv.guard.after_open()
 
     def _c2(self, st):
         """Issue C2: the owner's pull reply regions back to the workers."""
         P = self.P
         send_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
         recv_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
+        if self.linear:  # one w per key
+            send_rows, recv_rows = st.recv, st.send
         st.rrecv, st.w_c2 = self._a2a(2, st.rbuf[:sum(send_rows)], send_rows, recv_rows)
         st.rbuf = None
 
@@ -410,12 +424,18 @@ class PsxDifacto:
         lrn = self.lrn
         st.w_c2.wait()
         st.w_c2 = None
-        st.hdr, st.rows = ops.ps_unpack(st.rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d)
-        st.py, st.dual, st.xv = ops.fm_forward(st.offset, st.lid, st.val, st.hdr, st.rrecv,
-                                               self.vs, st.label, ops.LOSS_LOGIT, lrn.met)
+        if self.linear:
+            st.hdr = st.rrecv
+            st.py, st.dual, st.xv = ops.fm_forward(st.offset, st.lid, st.val, st.rrecv, None, 0,
+                                                   st.label, lrn.loss, lrn.met)
+        else:
+            st.hdr, st.rows = ops.ps_unpack(st.rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d)
+            st.py, st.dual, st.xv = ops.fm_forward(st.offset, st.lid, st.val, st.hdr, st.rrecv,
+                                                   self.vs, st.label, lrn.loss, lrn.met)
         if not st.train:  # (a training step's AUC follows its backward)
             ops.auc_acc(st.py, st.label, lrn.auc_sum)
-        lrn.n_mb += 1
+        if st.label.numel():
+            lrn.n_mb += 1
         lrn.last_sizes = (st.U, sum(st.vrecv))
 
     def _c3(self, st):
@@ -423,8 +443,9 @@ class PsxDifacto:
         P = self.P
         send_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
         recv_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
+        if self.linear:  # one gradient per key
+            send_rows, recv_rows = st.send, st.recv
         st.gpush, st.w_c3 = self._a2a(3, st.gvc, send_rows, recv_rows)
-        self.wire_steps += 1
         st.gvc = None
 
     def _grad(self, st, issue=True):
@@ -432,18 +453,21 @@ class PsxDifacto:
         leave it for :meth:`_c3` (issue=False)."""
         lrn = self.lrn
         emb = lrn.emb
-        P = self.P
         csc_off, csc_row, csc_val = st.csc
-        gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, st.dual, st.xv, st.hdr, st.rrecv,
-                                  self.vs)
-        if emb is not None and (emb.grad_clipping > 0 or emb.dropout > 0 or
-                                emb.grad_normalization):
-            if emb.grad_normalization:  # header rows must not enter the norm
-                self._zero_header_rows(st, gvc)
-            ops.fm_grad_post(gvc, st.rows, lrn.dim, emb.grad_clipping, emb.dropout,
-                             lrn.seed + 7919 * st.seed_step + 1, bool(emb.grad_normalization))
-        ops.ps_pack_gw(gw, gvc, st.segS_w, st.segHS_w, st.vrecv_d)
-        st.gvc = gvc
+        if self.linear:
+            gw, _ = ops.fm_backward(csc_off, csc_row, csc_val, st.dual, None, st.hdr, None, 0)
+            st.gvc = gw.reshape(-1)
+        else:
+            gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, st.dual, st.xv, st.hdr,
+                                      st.rrecv, self.vs)
+            if emb is not None and (emb.grad_clipping > 0 or emb.dropout > 0 or
+                                    emb.grad_normalization):
+                if emb.grad_normalization:  # header rows must not enter the norm
+                    self._zero_header_rows(st, gvc)
+                ops.fm_grad_post(gvc, st.rows, lrn.dim, emb.grad_clipping, emb.dropout,
+                                 lrn.seed + 7919 * st.seed_step + 1, bool(emb.grad_normalization))
+            ops.ps_pack_gw(gw, gvc, st.segS_w, st.segHS_w, st.vrecv_d)
+            st.gvc = gvc
         if issue:
             self._c3(st)
         ops.auc_acc(st.py, st.label, lrn.auc_sum)
@@ -462,8 +486,14 @@ class PsxDifacto:
         """Apply a landed push on the owner (one launch over all segments)."""
         lrn = self.lrn
         st.w_c3.wait()
-        self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o,
-                           st.gpush, lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
+        if self.linear:
+            self.store.ps_push_linear(st.slot, st.chain, st.head, st.segS_o, st.gpush,
+                                      lrn.conf.algo, lrn.alpha, lrn.beta, lrn.conf.lambda_l1,
+                                      lrn.conf.lambda_l2, float(self.requests))
+            self.requests += self.P  # one request per worker (ps-lite SGD's t)
+        else:
+            self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o,
+                               st.gpush, lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
         st.w_c3 = None
         st.gpush = st.slot = st.vpos = st.chain = st.head = st.keys_o = None
 
@@ -481,7 +511,7 @@ class PsxDifacto:
         st.send, st.recv = send, recv
         st.label = label
         st.train = train
-        st.use_cnt = train and data_pass == 0
+        st.use_cnt = train and data_pass == 0 and not self.linear
         st.seed_step = self.lrn.step
         self._upload(st, prev)
         return st
@@ -493,11 +523,22 @@ class PsxDifacto:
         st.offset, st.val = offset, val
         self.uhint = st.U
 
+    def _drop_empty(self):
+        """Every rank's minibatch of this call is empty (C0's flags): the
+        pass is over. Drop the job; the pipeline keeps what is in flight for
+        :meth:`flush`."""
+        self._finish()
+        self.last_empty = True
+
     def train(self, keys, offset, val, label, data_pass, next_batch):
         if self.cuda:
             self.S = torch.cuda.current_stream(self.dev)
+        self.last_empty = False
         self._ensure_job(keys, offset, val)
-        send, recv = self._counts()  # the step's one host read
+        send, recv, empty = self._counts()  # the step's one host read
+        if empty:
+            self._drop_empty()
+            return
         prev = self.pull
         if prev is not None and prev.vown is None:
             self._vcount_exchange(prev)
@@ -540,10 +581,15 @@ class PsxDifacto:
 
     def evaluate(self, keys, offset, val, label):
         """A validation / prediction minibatch: drain the training pipeline,
-        then open (no insert), reply and forward synchronously."""
+        then open (no insert), reply and forward synchronously. Returns the
+        predictions, or None when no rank had data (``last_empty``)."""
         self.flush()
+        self.last_empty = False
         self._ensure_job(keys, offset, val)
-        send, recv = self._counts()
+        send, recv, empty = self._counts()
+        if empty:
+            self._drop_empty()
+            return None
         st = self._new_step(send, recv, label, False, 1, None)
         self._set_loc(st, self._finish(), offset, val)
         self._c1(st)
@@ -583,3 +629,6 @@ class PsxDifacto:
         if st is not None and st.train:
             self._owner_push(st)
         self.pull = None
+
+
+PsxDifacto = Psx  # (round-2 name)

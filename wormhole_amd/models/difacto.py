@@ -60,12 +60,17 @@ class DifactoLearner:
         self.defer_push = True
         self.step = 0
         self.last_sizes = None
-        # P > 1 shards: the lean pipelined exchange (kv/psx.py)
-        self._plan_stream = None
+        self.loss = ops.LOSS_LOGIT
+        # True after a process() call in which no rank had data (the pass is
+        # over; kv/psx.py reads it from the count exchange's flags)
+        self.last_empty = False
+        # P > 1 ranks: the lean pipelined exchange (kv/psx.py), whatever the
+        # number of server shards S <= P. (The ShardedKV exchange remains for
+        # the lossy fixed_bytes payload filter and embedding-free models.)
         self.psx = None
-        if comm.size > 1 and self.vstride > 0 and self.kv.nshard == comm.size:
-            from ..kv.psx import PsxDifacto
-            self.psx = PsxDifacto(self)
+        if comm.size > 1 and self.vstride > 0 and not self.kv.fixed_bytes:
+            from ..kv.psx import Psx
+            self.psx = Psx(self)
 
     # ------------------------------------------------------------------ step
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):
@@ -74,9 +79,12 @@ class DifactoLearner:
         if self.psx is not None:
             if train:
                 self.psx.train(keys, offset, val, label, data_pass, next_batch)
+                self.last_empty = self.psx.last_empty
                 return None
             py = self.psx.evaluate(keys, offset, val, label)
+            self.last_empty = self.psx.last_empty
             return py if wtype == PRED else None
+        self.last_empty = offset.numel() <= 1 and self.comm.size == 1
         with trace.span("localize"):
             loc = localize_current(self, keys, offset, val)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
@@ -99,7 +107,8 @@ class DifactoLearner:
                                           ops.LOSS_LOGIT, self.met)
             if not train:  # (a training step's AUC follows its backward)
                 ops.auc_acc(py, label, self.auc_sum)
-        self.n_mb += 1
+        if label.numel():
+            self.n_mb += 1
         if train:
             with trace.span("backward"):
                 gw, gvc = ops.fm_backward(csc_off, csc_row, csc_val, dual, xv, hdr, vc,

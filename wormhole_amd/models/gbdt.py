@@ -546,6 +546,7 @@ class TreeBuilder:
         self.F = dm.ncol
         self.nbin = max(1, cuts.nbin_max)
         self.gpu = B.is_cuda
+        self._native = None  # grower choice, made collectively at the first build()
         self.device = B.device
         # features per LDS histogram block: int64 (g, h) per bin in <= 160 KB
         fg = max(1, (160 * 1024) // (self.nbin * 16))
@@ -686,7 +687,12 @@ class TreeBuilder:
 
     # ----------------------------------------------------------------- build
     def build(self, gpair, margin):
-        if self.gpu and self.dm.n > 0 and not getattr(self.dm, "sparse", False):
+        if getattr(self, "_native", None) is None:
+            # every rank must take the same grower (their allreduce sequences
+            # differ): native only if every rank can, decided once, together
+            ok = self.gpu and self.dm.n > 0 and not getattr(self.dm, "sparse", False)
+            self._native = bool(self.bsp.allreduce_scalar(1.0 if ok else 0.0, "min") > 0)
+        if self._native:
             return self._build_native(gpair, margin)
         return self._build_py(gpair, margin)
 

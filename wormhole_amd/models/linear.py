@@ -41,12 +41,37 @@ class LinearLearner:
         # overlap each push's all-to-all with the next minibatch's localize
         # (same semantics: the push is applied before the next lookup)
         self.defer_push = True
+        # the attributes the multi-shard step reads (kv/psx.py)
+        self.loss = conf.loss
+        self.hp = [0.0] * 8   # (no embedding: DiFacto's hyper-parameters unused)
+        self.threshold = 0
+        self.l1_shrk = False
+        self.emb = None
+        self.dim = 0
+        self.step = 0
+        self.last_sizes = None
+        self.last_empty = False
+        # P > 1 ranks: the lean pipelined exchange (kv/psx.py) over S <= P
+        # server shards: keys out, w back, gradients out, one owner launch
+        self.psx = None
+        if comm.size > 1:
+            from ..kv.psx import Psx
+            self.psx = Psx(self)
 
     def _localize(self, keys, offset, val, next_batch):
         return localize_pipelined(self, keys, offset, val, next_batch)
 
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):
         train = wtype == TRAIN
+        if self.psx is not None:
+            if train:
+                self.psx.train(keys, offset, val, label, data_pass, next_batch)
+                self.last_empty = self.psx.last_empty
+                return None
+            py = self.psx.evaluate(keys, offset, val, label)
+            self.last_empty = self.psx.last_empty
+            return py if wtype == PRED else None
+        self.last_empty = offset.numel() <= 1 and self.comm.size == 1
         with trace.span("localize"):
             loc = self._localize(keys, offset, val, next_batch)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
@@ -73,12 +98,18 @@ class LinearLearner:
     def flush(self):
         """Complete the last minibatch's deferred push (before reading the
         model: progress counters, save, end of pass, end of a timed run)."""
+        if self.psx is not None:
+            self.psx.flush()
         self.kv.flush()
 
     def take_progress(self):
         """Reference layout (learn/linear/progress.h): [objv, acc, auc, count,
-        new_ex, new_w]; accuracy is the per-minibatch-mean convention."""
-        self.flush()
+        new_ex, new_w]; accuracy is the per-minibatch-mean convention.
+
+        Local only (no collectives: a worker reports on its own clock);
+        minibatches still in the multi-shard pipeline count in the next
+        report, and the end of a pass flushes first."""
+        self.kv.flush()
         ops.auc_join(self.auc_sum)
         m = self.met.tolist()
         a = float(self.auc_sum.item())

@@ -244,8 +244,9 @@ def ps_records(uniq, ucnt=None):
     return ref.ps_records(uniq, ucnt)
 
 
-def ps_c0(owner_cnt, vcnt=None):
-    """C0 count-exchange buffers (send [3P], payload [5P+1]); see kv/psx.py."""
+def ps_c0(owner_cnt, vcnt, P, flag):
+    """C0 count-exchange buffers (send [4P], payload [S+1+5P]) from the owner
+    counts [S+1] over S <= P shards; see kv/psx.py."""
     if _gpu(owner_cnt):
-        return tuple(_native.hip().ps_c0(owner_cnt, vcnt))
-    return ref.ps_c0(owner_cnt, vcnt)
+        return tuple(_native.hip().ps_c0(owner_cnt, vcnt, int(P), int(flag)))
+    return ref.ps_c0(owner_cnt, vcnt, P, flag)

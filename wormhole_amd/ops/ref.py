@@ -295,14 +295,18 @@ def ps_records(uniq, ucnt=None):
     return rec
 
 
-def ps_c0(owner_cnt, vcnt=None):
-    P = owner_cnt.numel() - 1
-    send = torch.zeros(P, 3, dtype=torch.int64)
-    send[:, 0] = owner_cnt[:P]
-    send[:, 1] = owner_cnt[P]
+def ps_c0(owner_cnt, vcnt, P, flag):
+    """Oracle of psx.hip k_ps_c0: send[4p..] = {keys for p (0 when p >= S),
+    overflow flag, V rows for p, has-data flag}; payload = [owner_cnt (S+1) |
+    4P receive slot | vcnt P]."""
+    S = owner_cnt.numel() - 1
+    send = torch.zeros(P, 4, dtype=torch.int64)
+    send[:S, 0] = owner_cnt[:S]
+    send[:, 1] = owner_cnt[S]
     v = vcnt if vcnt is not None else torch.zeros(P, dtype=torch.int64)
     send[:, 2] = v
-    payload = torch.zeros(5 * P + 1, dtype=torch.int64)
-    payload[:P + 1] = owner_cnt
-    payload[4 * P + 1:] = v
+    send[:, 3] = int(flag)
+    payload = torch.zeros(S + 1 + 5 * P, dtype=torch.int64)
+    payload[:S + 1] = owner_cnt
+    payload[S + 1 + 4 * P:] = v
     return send.reshape(-1), payload

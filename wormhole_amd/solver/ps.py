@@ -16,10 +16,11 @@ reference progress table every ``print_sec``, and fans out load/save.
 
 Because collectives are group-synchronous, workers step in lockstep: a worker
 whose current part is exhausted asks for another; once the pool is empty it
-keeps joining the collectives with empty minibatches until an allreduce of
-"have data" flags is zero (SURVEY §7.5 hard part 1).  ``max_concurrency``
-bounds the minibatches in flight per worker exactly as before (the device
-queue depth), with zero staleness inside a step.
+keeps joining the collectives with empty minibatches until no rank has data,
+which every rank learns from the has-data flags the per-step count exchange
+already carries (SURVEY §7.5 hard part 1; no extra collective per
+minibatch).  ``max_concurrency`` bounds the minibatches in flight per worker
+(the multi-shard step pipelines one minibatch deep by default).
 """
 import json
 import collections
@@ -251,44 +252,51 @@ class Worker:
         # Training parses one minibatch ahead and hands it to the learner
         # (next_batch), which begins its localization -- and, on several
         # ranks, the count exchange -- before training the current one, as
-        # bench.py does. The "have data" allreduce carries both flags so that
-        # every rank decides in lockstep whether a next minibatch is begun.
-        ahead = train
+        # bench.py does.
+        #
+        # Several ranks (the multi-shard step, kv/psx.py): every rank calls
+        # process() once per step, with an empty minibatch once its parts are
+        # exhausted, and always hands a look-ahead (empty if it has none), so
+        # the count collectives stay in lockstep. Each count exchange carries
+        # a has-data flag per rank: the first call in which NO rank had data
+        # reports learner.last_empty on every rank at once, and the pass ends
+        # there -- no per-minibatch collective or host read of its own
+        # (learn/solver/minibatch_solver.h:284-322). The embedding-free /
+        # quantised-payload learners without that step fall back to one
+        # "have data" allreduce per minibatch.
+        multi = self.comm.size > 1
+        flags = multi and getattr(self.learner, "psx", None) is not None
+        # (the allreduce fallback gives no lockstep look-ahead decision, so it
+        # runs without one)
+        ahead = train and (flags or not multi)
+
+        def dev_or_empty(b):
+            return self._to_dev(b) if b is not None else self._empty_batch()
+
         fetch()
-        dev_next = None
         batch = next_parsed()
+        args = dev_or_empty(batch) if (batch is not None or multi) else None
         nxt = next_parsed() if (ahead and batch is not None) else None
+        nargs = None
+        if ahead and (nxt is not None or flags):
+            nargs = dev_or_empty(nxt)
         while True:
-            have = 1 if batch is not None else 0
-            have_next = 1 if nxt is not None else 0
-            if self.comm.size > 1:
-                flag = torch.tensor([have, have_next], dtype=torch.int32, device=self.comm.device)
-                self.comm.allreduce(flag)
-                have_all, next_all = (int(x) for x in flag.tolist())
-                if have_all == 0:
-                    break
-            elif not have:
+            if not multi and batch is None:
                 break
-            else:
-                next_all = have_next
-            with trace.stage("h2d"):
-                # the look-ahead batch went to the device last step
-                if dev_next is not None:
-                    args = dev_next
-                else:
-                    args = self._to_dev(batch) if batch is not None else self._empty_batch()
-                nargs = None
-                if ahead and next_all:
-                    nargs = self._to_dev(nxt) if nxt is not None else self._empty_batch()
-                dev_next = nargs if nxt is not None else None
+            if multi and not flags:
+                flag = torch.tensor([1 if batch is not None else 0], dtype=torch.int32,
+                                    device=self.comm.device)
+                self.comm.allreduce(flag)
+                if int(flag.item()) == 0:
+                    break
             if self.fault and batch is not None:
                 self._inject_fault()
             with trace.stage("process"):
-                if nargs is not None:
-                    py = self.learner.process(*args, wtype=wtype, data_pass=data_pass,
-                                              next_batch=(nargs[0], nargs[1], nargs[2]))
-                else:
-                    py = self.learner.process(*args, wtype=wtype, data_pass=data_pass)
+                nb = (nargs[0], nargs[1], nargs[2]) if nargs is not None else None
+                py = self.learner.process(*args, wtype=wtype, data_pass=data_pass,
+                                          next_batch=nb)
+            if flags and self.learner.last_empty:
+                break  # no rank had data in this step: every rank stops here
             self.n_done += 1
             n_pass += 1
             n_ex += int(args[3].numel())
@@ -312,10 +320,18 @@ class Worker:
                     ex_last = n_ex
                 last = now
                 self.send(msg="progress", data=self.learner.take_progress())
-            if ahead:
-                batch, nxt = nxt, (next_parsed() if nxt is not None else None)
-            else:
-                batch = next_parsed()
+            with trace.stage("h2d"):
+                if ahead:
+                    # the look-ahead batch (already on the device, its
+                    # localize begun) is the next step's: the SAME objects
+                    batch, args = nxt, nargs
+                    nxt = next_parsed() if batch is not None else None
+                    nargs = dev_or_empty(nxt) if (nxt is not None or flags) else None
+                    if args is None and multi:
+                        args = self._empty_batch()
+                else:
+                    batch = next_parsed()
+                    args = dev_or_empty(batch) if (batch is not None or multi) else None
         if pred_f:
             pred_f.close()
         # the reference worker's summary line (minibatch_solver.h:244-248)
