@@ -13,7 +13,9 @@
 #include <array>
 #include <cstdlib>
 #include <cstring>
+#include <cmath>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -734,7 +736,7 @@ class KVStore {
     TORCH_CHECK(n < (1 << 24), "ps_open: at most 2^24 - 1 keys per minibatch and shard");
     epoch_ = epoch_ % 255 + 1;  // 1..255; a wrap to 1 sweeps the table's tags
     ++opens_;
-    TORCH_CHECK(rows_cap >= n, "ps_open: reply buffer too small");
+    TORCH_CHECK(vstride_ == 0 || rows_cap >= n, "ps_open: reply buffer too small");
     c10::DeviceGuard g(keys.device());
     auto s = cur_stream(keys);
     auto i32 = keys.options().dtype(torch::kInt32);
@@ -1510,6 +1512,29 @@ void gbdt_leaf_add(const Tensor& ridx, const Tensor& pos_node, const Tensor& lea
                     ptr<float>(margin), cur_stream(ridx));
 }
 
+// tree arrays: int32 feat / bin / left / right, uint8 defl, float val [nodes]
+void gbdt_leaf_walk(const Tensor& B, const Tensor& feat, const Tensor& bin, const Tensor& defl,
+                    const Tensor& left, const Tensor& right, const Tensor& val,
+                    const Tensor& margin) {
+  CHECK_IN(B, torch::kUInt8);
+  CHECK_IN(feat, torch::kInt32);
+  CHECK_IN(bin, torch::kInt32);
+  CHECK_IN(defl, torch::kUInt8);
+  CHECK_IN(left, torch::kInt32);
+  CHECK_IN(right, torch::kInt32);
+  CHECK_IN(val, torch::kFloat32);
+  CHECK_IN(margin, torch::kFloat32);
+  TORCH_CHECK(B.dim() == 2 && margin.numel() == B.size(0), "leaf_walk: B must be [n, f]");
+  const int64_t nn = feat.numel();
+  TORCH_CHECK(bin.numel() == nn && defl.numel() == nn && left.numel() == nn &&
+                  right.numel() == nn && val.numel() == nn && nn > 0,
+              "leaf_walk: tree array sizes differ");
+  c10::DeviceGuard g(B.device());
+  wh::gbdt_leaf_walk(ptr<uint8_t>(B), B.size(0), (int)B.size(1), ptr<int32_t>(feat),
+                     ptr<int32_t>(bin), ptr<uint8_t>(defl), ptr<int32_t>(left),
+                     ptr<int32_t>(right), ptr<float>(val), ptr<float>(margin), cur_stream(B));
+}
+
 void gbdt_predict(const Tensor& X, const Tensor& feat, const Tensor& thr, const Tensor& left,
                   const Tensor& right, const Tensor& defl, const Tensor& leaf, const Tensor& margin) {
   CHECK_IN(X, torch::kFloat32);
@@ -2151,6 +2176,171 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
 
 }  // namespace
 
+// ------------------------------------------------------ native P=1 step
+// The single-shard linear training step in ONE native call (reference
+// AsgdWorker::ProcessMinibatch, learn/linear/async_sgd.h:240-288, on one
+// server shard): finish this minibatch's localize (begun by the previous
+// call) -> begin the next one on the localize stream -> store guard (summary
+// of the previous open; device rehash past the load bound) -> find/insert ->
+// pull -> forward + loss + metrics -> AUC on its side stream -> backward ->
+// push (SGD / AdaGrad / FTRL). At the reference's minibatch of 10000 rows
+// the GPU work is ~80 us of kernels per step while the same sequence driven
+// from Python cost ~250 us of host time per step; here the host only pays
+// the launches.
+class LinearStep {
+ public:
+  LinearStep(KVStore* store, int64_t algo, double alpha, double beta, double l1, double l2,
+             int64_t loss, double max_load)
+      : store_(store), algo_(algo), alpha_(alpha), beta_(beta), l1_(l1), l2_(l2), loss_(loss),
+        max_load_(max_load) {
+    TORCH_CHECK(store->vstride() == 0, "LinearStep needs a linear store");
+    dev_ = store->slots_.device().index();
+    c10::DeviceGuard g(store->slots_.device());
+    ls_ = c10::hip::getStreamFromPool(false, dev_);
+    WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_s_, hipEventDisableTiming));
+    WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_sum_, hipEventDisableTiming));
+    WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_ls_, hipEventDisableTiming));
+    sum_h_ = torch::zeros({4}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
+  }
+  ~LinearStep() {
+    job_.reset();
+    (void)hipEventDestroy(ev_s_);
+    (void)hipEventDestroy(ev_sum_);
+    (void)hipEventDestroy(ev_ls_);
+  }
+
+  // WH_LS_WAIT=1: the localize stream waits for S before every job (the
+  // conservative order of the Python path; A/B of the record-stream handoff)
+  static bool ls_waits_s() {
+    static int on = -1;
+    if (on < 0) on = std::getenv("WH_LS_WAIT") && std::string(std::getenv("WH_LS_WAIT")) == "1";
+    return on == 1;
+  }
+
+  // one minibatch; returns the predictions py [rows]. next_*: the next
+  // call's minibatch, whose localize begins now (on the localize stream,
+  // after `ready` -- a hipEvent_t handle of its producer, or 0).
+  Tensor step(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+              const Tensor& label, bool train, const Tensor& met, const Tensor& auc_sum,
+              const c10::optional<Tensor>& nkeys, const c10::optional<Tensor>& noffset,
+              const c10::optional<Tensor>& nval, int64_t ready) {
+    c10::DeviceGuard g(keys.device());
+    const hipStream_t S = cur_stream(keys);
+    // this minibatch's localize
+    std::vector<Tensor> loc;
+    if (job_ && job_keys_.is_same(keys)) {
+      loc = job_->finish();
+      // the job's outputs were allocated on the localize stream and are read
+      // on S from here on: their blocks go back to the localize stream's
+      // pool only once S's queued work is done (so the localize stream
+      // never has to wait for S before the next job)
+      for (const Tensor& t : loc)
+        if (t.defined() && t.is_cuda() && t.numel())
+          c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(),
+                                                      c10::hip::getCurrentHIPStream(dev_));
+    } else {
+      // (no job begun for this minibatch) localize on S, after any job still
+      // running on the localize stream: both use the device's localize
+      // workspace
+      if (job_) {
+        WH_HIP_CHECK_HOST(hipEventRecord(ev_ls_, ls_.stream()));
+        WH_HIP_CHECK_HOST(hipStreamWaitEvent(S, ev_ls_, 0));
+      }
+      job_.reset();
+      LocalizeJob j(keys, offset, val, 1, hint_, py::none());
+      loc = j.finish();
+      s_job_ = true;
+    }
+    job_.reset();
+    const Tensor &uniq = loc[0], &lid = loc[3], &csc_off = loc[4], &csc_row = loc[5],
+                 &csc_val = loc[6];
+    const int64_t U = uniq.numel();
+    hint_ = U;
+    // the next minibatch's localize, on its own stream behind everything
+    // queued on S so far (its outputs may reuse blocks S still reads)
+    if (nkeys.has_value() && nkeys->defined()) {
+      if (s_job_ || ls_waits_s()) {  // a localize ran on S: the workspace is S's until then
+        WH_HIP_CHECK_HOST(hipEventRecord(ev_s_, S));
+        WH_HIP_CHECK_HOST(hipStreamWaitEvent(ls_.stream(), ev_s_, 0));
+        s_job_ = false;
+      }
+      if (ready) WH_HIP_CHECK_HOST(hipStreamWaitEvent(ls_.stream(), reinterpret_cast<hipEvent_t>(ready), 0));
+      for (const Tensor* t : {&*nkeys, &*noffset}) {
+        c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), ls_);
+        c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(),
+                                                    c10::hip::getCurrentHIPStream(dev_));
+      }
+      c10::optional<Tensor> nv;
+      if (nval.has_value() && nval->defined() && nval->numel()) {
+        nv = *nval;
+        c10::hip::HIPCachingAllocator::recordStream(nval->storage().data_ptr(), ls_);
+      }
+      c10::hip::HIPStreamGuard sg(ls_);
+      job_ = std::make_unique<LocalizeJob>(*nkeys, *noffset, nv, 1, hint_, py::none());
+      job_keys_ = *nkeys;
+    }
+    // store guard: the previous open's summary (long complete), then room
+    // for this open's inserts
+    if (sum_pending_) {
+      WH_HIP_CHECK_HOST(hipEventSynchronize(ev_sum_));
+      sum_pending_ = false;
+      const int64_t* h = sum_h_.data_ptr<int64_t>();
+      keys_ = h[0];
+      TORCH_CHECK(h[1] == 0, "parameter store shard lost data: ", h[1], " failed inserts (table ",
+                  h[0], "/", store_->cap(), " keys)");
+    }
+    if (train && keys_ + U > max_load_ * store_->cap()) {
+      int64_t cap = store_->cap();
+      while (keys_ + U > 0.5 * cap) cap *= 2;
+      store_->grow(cap);  // (nothing in flight references the old slots)
+      ++grows_;
+    }
+    Tensor slot = store_->find(uniq, train);
+    if (train) {
+      Tensor sm = store_->summary();
+      WH_HIP_CHECK_HOST(hipMemcpyAsync(sum_h_.data_ptr(), sm.data_ptr(), 32, hipMemcpyDeviceToHost, S));
+      WH_HIP_CHECK_HOST(hipEventRecord(ev_sum_, S));
+      sum_pending_ = true;
+      keys_ += U;  // an upper bound until the summary is read
+    }
+    Tensor w = store_->linear_pull(slot);
+    auto fw = fm_forward(offset, lid, val, w, c10::nullopt, 0, label, loss_, met);
+    auc_acc_side(fw[0], label, auc_sum);
+    if (train && U > 0) {
+      auto bw = fm_backward(csc_off, csc_row,
+                            csc_val.numel() ? c10::optional<Tensor>(csc_val) : c10::nullopt,
+                            fw[1], c10::nullopt, w, c10::nullopt, 0);
+      ++pushes_;
+      const double eta = (beta_ + std::sqrt((double)pushes_)) / alpha_;
+      store_->linear_push(slot, bw[0], algo_, alpha_, beta_, l1_, l2_, eta);
+    }
+    return fw[0];
+  }
+
+  // drop a begun localize (end of a pass)
+  void reset() { job_.reset(); job_keys_ = Tensor(); }
+
+  int64_t grows() const { return grows_; }
+  int64_t pushes() const { return pushes_; }
+  void set_pushes(int64_t p) { pushes_ = p; }
+
+ private:
+  KVStore* store_;
+  int64_t algo_;
+  double alpha_, beta_, l1_, l2_;
+  int64_t loss_;
+  double max_load_;
+  int dev_ = 0;
+  c10::hip::HIPStream ls_ = c10::hip::getDefaultHIPStream();
+  hipEvent_t ev_s_ = nullptr, ev_sum_ = nullptr, ev_ls_ = nullptr;
+  bool s_job_ = false;
+  std::unique_ptr<LocalizeJob> job_;
+  Tensor job_keys_;
+  Tensor sum_h_;
+  bool sum_pending_ = false;
+  int64_t keys_ = 0, hint_ = 0, grows_ = 0, pushes_ = 0;
+};
+
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "wormhole_amd gfx950 HIP kernels";
   m.def("scan_excl", &scan_excl);
@@ -2164,6 +2354,17 @@ PYBIND11_MODULE(_hip, m) {
       .def("counts", &LocalizeJob::counts)
       .def("finish", &LocalizeJob::finish);
   m.def("loc_timing_read", []() { return loc_timing_buf().clone(); });
+  py::class_<LinearStep>(m, "LinearStep")
+      .def(py::init<KVStore*, int64_t, double, double, double, double, int64_t, double>(),
+           py::arg("store"), py::arg("algo"), py::arg("alpha"), py::arg("beta"), py::arg("l1"),
+           py::arg("l2"), py::arg("loss"), py::arg("max_load") = 0.7, py::keep_alive<1, 2>())
+      .def("step", &LinearStep::step, py::arg("keys"), py::arg("offset"), py::arg("val"),
+           py::arg("label"), py::arg("train"), py::arg("met"), py::arg("auc_sum"),
+           py::arg("next_keys") = py::none(), py::arg("next_offset") = py::none(),
+           py::arg("next_val") = py::none(), py::arg("ready") = 0)
+      .def("reset", &LinearStep::reset)
+      .def_property_readonly("grows", &LinearStep::grows)
+      .def_property("pushes", &LinearStep::pushes, &LinearStep::set_pushes);
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
         py::arg("nshard") = 1, py::arg("hint") = 0, py::arg("exchange") = py::none());
   m.def("fm_forward", &fm_forward);
@@ -2204,6 +2405,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("owlqn_step", &owlqn_step);
   m.def("multi_dot", &multi_dot);
   m.def("gbdt_leaf_add", &gbdt_leaf_add);
+  m.def("gbdt_leaf_walk", &gbdt_leaf_walk);
   m.def("gbdt_predict", &gbdt_predict);
   m.def("kmeans_pack_x", &kmeans_pack_x);
   m.def("kmeans_pack_c", &kmeans_pack_c);

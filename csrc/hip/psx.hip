@@ -70,6 +70,14 @@ __device__ __forceinline__ void load_seg(const int64_t* g, int64_t* sh, int P) {
   for (int p = threadIdx.x; p <= P; p += blockDim.x) sh[p] = g[p];
 }
 
+// the new {cnt, tag} word of lane `idx` (index idx + 1 in the chain tag)
+__device__ __forceinline__ unsigned long long next_ct(unsigned long long cur, uint32_t epoch,
+                                                      int64_t idx, uint32_t add, int chains) {
+  const uint32_t mine = (epoch << 24) | (uint32_t)(idx + 1);
+  const uint32_t nt = chains ? mine : (uint32_t)(cur >> 32);
+  return ((unsigned long long)nt << 32) | (uint32_t)((uint32_t)cur + add);
+}
+
 // ---------------------------------------------------------------- owner open
 // keys: u64 [n] (rec == null) or 12-byte records rec [n x 3] int32 {key lo,
 // key hi, count}. Writes slot[n], w_out[n], vpos[n+1], chain[n] (train) and
@@ -128,33 +136,47 @@ __global__ __launch_bounds__(kThreads) void k_ps_open(
   float w[kPullPer];
   int32_t row[kPullPer];
   bool want[kPullPer];
+  // {cnt, tag} in one 64-bit CAS: add the count and swap in this lane's
+  // chain tag. The kPullPer keys' slot reads, first CAS attempts and (rare)
+  // retries are issued phase by phase, so their memory round trips overlap
+  // instead of running key after key.
+  const bool ctag = use_cnt || chains;
+  unsigned long long cur[kPullPer], seen[kPullPer];
 #pragma unroll
   for (int r = 0; r < kPullPer; ++r) {
     w[r] = 0.f;
     row[r] = -1;
     want[r] = false;
+    cur[r] = seen[r] = 0ull;
     if (sl[r] < 0) continue;
     KVSlot& e = t.sl[sl[r]];
     w[r] = e.w;
     row[r] = t.vstride > 0 ? ld_relaxed_i32(&e.vrow) : -1;
-    if (use_cnt || chains) {
-      // {cnt, tag} in one 64-bit CAS: add the count and swap in this lane's
-      // chain tag. Only the lane whose add crosses the threshold may
-      // allocate: with a key's duplicates adding concurrently, exactly one
-      // lane crosses (a key that crossed while l1_shrk held w at 0 is
-      // allocated by the push that makes w non-zero).
-      unsigned long long* ct = reinterpret_cast<unsigned long long*>(&e.cnt);
-      const uint32_t mine = (epoch << 24) | (uint32_t)(i0 + r + 1);
-      const uint32_t add = use_cnt ? (uint32_t)c[r] : 0u;
-      unsigned long long cur = __hip_atomic_load(ct, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while (true) {
-        const uint32_t nt = chains ? mine : (uint32_t)(cur >> 32);
-        const unsigned long long nv = ((unsigned long long)nt << 32) | (uint32_t)((uint32_t)cur + add);
-        const unsigned long long seen = atomicCAS(ct, cur, nv);
-        if (seen == cur) break;
-        cur = seen;
+    if (ctag)
+      cur[r] = __hip_atomic_load(reinterpret_cast<unsigned long long*>(&e.cnt), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (ctag) {
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r)
+      if (sl[r] >= 0)
+        seen[r] = atomicCAS(reinterpret_cast<unsigned long long*>(&t.sl[sl[r]].cnt), cur[r],
+                            next_ct(cur[r], epoch, i0 + r, use_cnt ? (uint32_t)c[r] : 0u, chains));
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r) {
+      if (sl[r] < 0) continue;
+      unsigned long long* ct = reinterpret_cast<unsigned long long*>(&t.sl[sl[r]].cnt);
+      while (seen[r] != cur[r]) {  // another lane of this launch updated the word
+        cur[r] = seen[r];
+        seen[r] = atomicCAS(ct, cur[r],
+                            next_ct(cur[r], epoch, i0 + r, use_cnt ? (uint32_t)c[r] : 0u, chains));
       }
-      const uint32_t old = (uint32_t)cur, pv = (uint32_t)(cur >> 32);
+      const uint32_t add = use_cnt ? (uint32_t)c[r] : 0u;
+      const uint32_t old = (uint32_t)cur[r], pv = (uint32_t)(cur[r] >> 32);
+      // Only the lane whose add crosses the threshold may allocate: with a
+      // key's duplicates adding concurrently, exactly one lane crosses (a
+      // key that crossed while l1_shrk held w at 0 is allocated by the push
+      // that makes w non-zero).
       want[r] = use_cnt && t.vstride > 0 && old <= hp.threshold && old + add > hp.threshold &&
                 row[r] < 0 && (!hp.l1_shrk || w[r] != 0.f);
       if (chains) {

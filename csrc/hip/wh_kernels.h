@@ -464,6 +464,11 @@ void gbdt_predict_csr(const int64_t* row_off, const int32_t* fid, const float* v
                       const int32_t* feat, const float* thr, const int32_t* left,
                       const int32_t* right, const uint8_t* defl, const float* leaf, float* margin,
                       hipStream_t s);
+// training margins after a tree: margin[i] += val[leaf of row i], walking the
+// pruned tree on the row's bins (B row-major [n, f])
+void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, const int32_t* feat, const int32_t* bin,
+                    const uint8_t* defl, const int32_t* left, const int32_t* right,
+                    const float* val, float* margin, hipStream_t s);
 void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const float* thr,
                   const int32_t* left, const int32_t* right, const uint8_t* defl,
                   const float* leaf, float* margin, hipStream_t s);

@@ -252,12 +252,26 @@ class PyMinibatchIter {
         pinned_(pinned) {}
   py::object next() {
     bool ok;
+    Tensor k, o, l, v, w;
     {
+      // the assembly AND the copies into (pinned) tensors run without the
+      // GIL: a shuffle-buffer block is hundreds of MB of keys, and the
+      // training loop keeps running meanwhile
       py::gil_scoped_release nogil;
       ok = it_.Next();
+      if (ok) {
+        const RowBlock& b = it_.Value();
+        k = vec_to_tensor(b.index, torch::kInt64, pinned_);
+        o = vec_to_tensor(b.offset, torch::kInt64, pinned_);
+        l = vec_to_tensor(b.label, torch::kFloat32, pinned_);
+        if (!b.value.empty()) v = vec_to_tensor(b.value, torch::kFloat32, pinned_);
+        if (!b.weight.empty()) w = vec_to_tensor(b.weight, torch::kFloat32, pinned_);
+      }
     }
     if (!ok) return py::none();
-    return block_to_py(it_.Value(), pinned_);
+    py::object val = v.defined() ? py::cast(v) : py::none();
+    py::object wt = w.defined() ? py::cast(w) : py::none();
+    return py::make_tuple(k, o, val, l, wt);
   }
 
  private:

@@ -257,3 +257,71 @@ def test_gbdt_csr_gpu_matches_dense_and_trains_wide_data():
         tb.build(obj.gpair(margin, dm.label, None), margin)
     err = G.eval_metric("error", torch.sigmoid(margin), dm.label, None, bsp)
     assert err < 0.5 * err0, (err0, err)
+
+
+@pytest.mark.parametrize("algo", [1, 2, 3])
+def test_native_linear_step_matches_python_step(algo):
+    """The single-shard linear step as ONE native call (LinearStep) trains
+    the same model as the Python-driven sequence of the same kernels, with
+    the next minibatch's localize begun early, a table that has to grow, and
+    SGD's request-count step size."""
+    import torch
+    from wormhole_amd.config.schema import LinearConfig
+    from wormhole_amd.data.synthetic import criteo_batch
+    from wormhole_amd.models.linear import LinearLearner
+    from wormhole_amd.parallel.comm import Comm
+    dev = torch.device("cuda", 0)
+    card = [50, 400, 3000, 20, 7, 900, 100000]
+    batches = [criteo_batch(3000, 5, s, dev, card) for s in range(8)]
+
+    def run(native):
+        conf = LinearConfig(algo=algo, lambda_l1=0.1, lr_eta=0.1)
+        lr = LinearLearner(conf, Comm(dev, init=False), dev, cap=1 << 12, seed=1)
+        assert lr._native is not None
+        if not native:
+            lr._native = None
+        for s, (keys, label, off) in enumerate(batches):
+            nb = (batches[s + 1][0], batches[s + 1][2], None) if s + 1 < len(batches) else None
+            lr.process(keys, off, None, label, 0, 0, next_batch=nb)
+        lr.flush()
+        prog = lr.take_progress()
+        st = lr.store
+        occ = st.occupied().long()
+        m = dict(zip(st.keys[occ].cpu().tolist(), st.w[occ].cpu().tolist()))
+        return m, prog, lr
+    a, pa, la = run(True)
+    b, pb, lb = run(False)
+    assert la.kv.guard.grows >= 1  # the 4096-slot table had to grow on both paths
+    assert a.keys() == b.keys()
+    bad = sum(1 for k, w in b.items() if abs(w - a[k]) > 1e-5 * max(1.0, abs(w)))
+    assert bad <= len(b) // 1000, bad
+    for x, y in zip(pa, pb):
+        assert abs(x - y) <= 1e-4 * max(1.0, abs(y)), (pa, pb)
+
+
+def test_gbdt_leaf_walk_matches_raw_value_predict():
+    """The training margins after each tree come from a per-row walk of the
+    pruned tree on the bins (k_leaf_walk); predicting the same (compacted)
+    trees on the raw values must give the same margins (missing values,
+    gamma pruning included)."""
+    from wormhole_amd.models import gbdt as G
+    from wormhole_amd.parallel.bsp import BSP
+    g = torch.Generator().manual_seed(4)
+    n, f = 50000, 16
+    X = torch.randn(n, f, generator=g)
+    X[torch.rand(n, f, generator=g) < 0.08] = float("nan")
+    y = (torch.nan_to_num(X[:, 0]) + torch.nan_to_num(X[:, 3]) * X[:, 5].abs() > 0.2).float()
+    bsp = BSP(torch.device("cpu"))
+    p = G.GBDTParam()
+    p.max_depth, p.objective, p.gamma = 6, "binary:logistic", 1.0
+    dev = torch.device("cuda", 0)
+    dm = G.DMatrix.from_dense(X, y, dev)
+    cuts = G.Cuts.build(dm, 64, bsp)
+    tb = G.TreeBuilder(p, bsp, dm, cuts, cuts.bin(dm))
+    obj = G.Objective(p.objective)
+    margin = torch.zeros(n, device=dev)
+    ref = torch.zeros(n, device=dev)
+    for _ in range(4):
+        tree = tb.build(obj.gpair(margin, dm.label, None), margin)
+        dm.predict_tree(tree, ref)
+        assert torch.allclose(margin, ref, atol=1e-5), (margin - ref).abs().max()

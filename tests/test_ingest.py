@@ -201,3 +201,42 @@ def test_device_shuffle_buffer_is_a_permutation_and_neg_sampling_drops_negatives
     npos, nneg = int((lab_h > 0).sum()), int((lab_h <= 0).sum())
     assert int((labs > 0).sum()) == npos
     assert abs(int((labs <= 0).sum()) - 0.25 * nneg) < 0.05 * nneg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shuf", [0, 1200])
+def test_device_crb_blocks_match_host_records(tmp_path, shuf):
+    """CRB input on a GPU worker: records decoded by the host reader threads,
+    minibatches (and, with a shuffle buffer, the permutation) on the device.
+    Unshuffled: the same minibatches as the host iterator; shuffled: every
+    row of the part exactly once, in another order."""
+    from wormhole_amd.data.device_text import DeviceTextIter, applies
+    host = _native.host()
+    dev = torch.device("cuda")
+    data = _criteo_text(3000, 9)
+    keys_h, off_h, _, lab_h, _ = host.parse_text(data, "criteo")
+    p = tmp_path / "d.crb"
+    w = host.RecordIOWriter(str(p))
+    for a in range(0, 3000, 700):  # several records, not aligned to the minibatch
+        b = min(a + 700, 3000)
+        o = off_h[a:b + 1] - off_h[a]
+        w.write(host.crb_encode(keys_h[off_h[a]:off_h[b]], o, None, lab_h[a:b], None))
+    w.close()
+    assert applies("crb", str(p), dev)
+    rows_h = [tuple(keys_h[off_h[i]:off_h[i + 1]].tolist()) + (float(lab_h[i]),)
+              for i in range(3000)]
+    it = DeviceTextIter(host, str(p), 0, 1, "crb", 500, shuf, 1.0, 3, dev)
+    rows, sizes = [], []
+    while True:
+        bt = it.next()
+        if bt is None:
+            break
+        keys, off, val, lab = [x.cpu() if x is not None else None for x in bt.to_main(dev)]
+        sizes.append(lab.numel())
+        rows += [tuple(keys[off[i]:off[i + 1]].tolist()) + (float(lab[i]),)
+                 for i in range(lab.numel())]
+    assert sizes[:-1] == [500] * (len(sizes) - 1)
+    if shuf:
+        assert sorted(rows) == sorted(rows_h) and rows != rows_h
+    else:
+        assert rows == rows_h

@@ -395,3 +395,23 @@ def test_linear_two_ranks_gloo_matches_oracle(tmp_path, nshard, algo):
              join=True)
     for r in range(2):
         assert (tmp_path / ("r%d" % r)).read_text() == "ok\n"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("algo,max_conc", [(3, 1), (2, 2), (1, 1)])
+def test_linear_loopback_gpu_matches_cpu(algo, max_conc):
+    """The linear multi-shard step through the HIP kernels (ps_open on a
+    linear store, the chain-ordered ps_push_linear) vs the host oracle."""
+    from wormhole_amd.parallel.comm import LoopbackComm
+    dev = torch.device("cuda", 0)
+    g, pg, b = _lin_run(LoopbackComm(4, dev), dev, algo, steps=6, rows=2000, max_conc=max_conc)
+    c, pc, _ = _lin_run(LoopbackComm(4, "cpu"), "cpu", algo, max_conc=max_conc,
+                        batches=[[t.cpu() for t in x] for x in b])
+    mg, mc = _lin_model(g), _lin_model(c)
+    assert mg.keys() == mc.keys()
+    # (float contraction and gradient summation order differ between the
+    # device and the host: a weight near the L1 threshold may land on the
+    # other side of it)
+    bad = sum(1 for k, w in mc.items() if abs(w - mg[k]) > 1e-4 * max(1.0, abs(w)))
+    assert bad <= len(mc) // 1000, bad
+    assert abs(pg[0] / pg[4] - pc[0] / pc[4]) < 1e-4

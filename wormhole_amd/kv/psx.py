@@ -86,7 +86,7 @@ class _Step:
     __slots__ = ("train", "use_cnt", "U", "uniq", "ucnt", "lid", "offset", "val", "csc",
                  "label", "send", "recv", "Hw", "Ho", "tabs", "segS_w", "segHS_w", "segS_o",
                  "segHS_o", "keys_o", "slot", "vpos", "chain", "head", "rbuf", "vcnt",
-                 "ev_open",
+                 "ev_open", "ev_grad",
                  "vown", "vrecv", "vrecv_d", "rrecv", "hdr", "rows", "py", "dual", "xv",
                  "gpush", "gvc", "seed_step", "w_c1", "w_c2", "w_c3")
 
@@ -182,6 +182,11 @@ class Psx:
         # as this minibatch's localize is finished (as on one shard,
         # models/_pipeline.py), concurrently with the forward / push / open
         self.ls = torch.cuda.Stream(device=self.dev) if self.cuda else None
+        # C2 / C3 are issued from xs, each behind its producer's event only
+        # (see _a2a)
+        self.xs = torch.cuda.Stream(device=self.dev) if self.cuda else None
+        self._evring = [torch.cuda.Event() for _ in range(16)] if self.cuda else None
+        self._evi = 0
         self.S = torch.cuda.current_stream(self.dev) if self.cuda else None
         if self.cuda and getattr(self.comm, "backend", "") in ("nccl", "loopback-rccl"):
             _native.hip().set_cu_reserve(_CU_RESERVE)
@@ -211,15 +216,43 @@ class Psx:
         r = getattr(self.comm, "rank", 0)
         self.wire[c] += row * (sum(int(v) for v in send_rows) - int(send_rows[r]))
 
-    def _a2a(self, c, x, send_rows, recv_rows):
-        """Issue collective Cc (async) and account for its bytes."""
+    def _a2a(self, c, x, send_rows, recv_rows, ready=None):
+        """Issue collective Cc (async) and account for its bytes.
+
+        ready: an event recorded on the compute stream right after the
+        kernel that produced ``x``. The collective is then issued from the
+        exchange stream xs, which waits for that event only: RCCL's stream
+        waits for the ISSUING stream's queued work, so issued from S it
+        would also wait for every kernel enqueued on S after x's producer
+        (C2 of minibatch i-1 behind the backward of i-2) and the transfer
+        could not overlap that compute. The consumer still orders itself
+        after the transfer with ``work.wait()`` on S."""
         self._tally(c, x, send_rows)
         if self.timer is not None:
             self.timer.ready(c)
-        out, work = self.comm.all_to_all_v_async(x, send_rows, recv_rows)
+        if ready is not None and self.cuda:
+            xs = self.xs
+            xs.wait_event(ready)
+            x.record_stream(xs)
+            with torch.cuda.stream(xs):
+                out, work = self.comm.all_to_all_v_async(x, send_rows, recv_rows)
+            if out.is_cuda:
+                out.record_stream(self.S)  # allocated on xs, read on S
+        else:
+            out, work = self.comm.all_to_all_v_async(x, send_rows, recv_rows)
         if self.timer is not None:
             self.timer.done(c, work)
         return out, work
+
+    def _event(self):
+        """An event recorded on S now (a ring: an event is re-recorded only
+        long after the stream wait that consumed it was enqueued)."""
+        if not self.cuda:
+            return None
+        ev = self._evring[self._evi]
+        self._evi = (self._evi + 1) % len(self._evring)
+        ev.record(self.S)
+        return ev
 
     def wire_reset(self):
         self.wire = [0, 0, 0, 0]
@@ -406,6 +439,7 @@ class Psx:
             st.keys_o, st.use_cnt, st.segS_o, st.segHS_o, rows, insert, st.train,
             lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
         st.keys_o = st.w_c1 = None
+        st.ev_open = self._event()  # C2 of this step waits for this only
         if insert:
             lrn.kv.guard.after_open()
 
@@ -416,7 +450,9 @@ class Psx:
         recv_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
         if self.linear:  # one w per key
             send_rows, recv_rows = st.recv, st.send
-        st.rrecv, st.w_c2 = self._a2a(2, st.rbuf[:sum(send_rows)], send_rows, recv_rows)
+        st.rrecv, st.w_c2 = self._a2a(2, st.rbuf[:sum(send_rows)], send_rows, recv_rows,
+                                      st.ev_open)
+        st.ev_open = None
         st.rbuf = None
 
     def _reply(self, st):
@@ -445,7 +481,8 @@ class Psx:
         recv_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
         if self.linear:  # one gradient per key
             send_rows, recv_rows = st.send, st.recv
-        st.gpush, st.w_c3 = self._a2a(3, st.gvc, send_rows, recv_rows)
+        st.gpush, st.w_c3 = self._a2a(3, st.gvc, send_rows, recv_rows, st.ev_grad)
+        st.ev_grad = None
         st.gvc = None
 
     def _grad(self, st, issue=True):
@@ -468,6 +505,7 @@ class Psx:
                                  lrn.seed + 7919 * st.seed_step + 1, bool(emb.grad_normalization))
             ops.ps_pack_gw(gw, gvc, st.segS_w, st.segHS_w, st.vrecv_d)
             st.gvc = gvc
+        st.ev_grad = self._event()  # C3 of this step waits for this only
         if issue:
             self._c3(st)
         ops.auc_acc(st.py, st.label, lrn.auc_sum)

@@ -911,7 +911,20 @@ class TreeBuilder:
         subtree's rows take the value of its nearest ancestor that is a leaf
         after pruning, looked up BEFORE the BFS renumbering changes ids."""
         self._prune_mark(tree)
-        if n and self.gpu:
+        B = getattr(self, "B", None)
+        if (n and self.gpu and B is not None and B.dim() == 2 and B.shape[0] == n
+                and B.dtype == torch.uint8 and not getattr(self.dm, "sparse", False)):
+            # walk the pruned tree per row on its bins (a pruned-away
+            # subtree's rows stop at its collapsed root, whose leaf value
+            # _prune_mark set): coalesced, instead of a scatter by ridx
+            dev = self.device
+            t32 = lambda v: torch.tensor(v, dtype=torch.int32).to(dev, non_blocking=True)  # noqa: E731
+            _native.hip().gbdt_leaf_walk(
+                B, t32(tree.feat), t32(tree.bin),
+                torch.tensor(tree.defl, dtype=torch.uint8).to(dev, non_blocking=True),
+                t32(tree.left), t32(tree.right),
+                torch.tensor(tree.leaf, dtype=torch.float32).to(dev, non_blocking=True), margin)
+        elif n and self.gpu:
             val = torch.zeros(len(tree.feat), dtype=torch.float32)
             for nd in leaf_segs:
                 a, top = nd, nd

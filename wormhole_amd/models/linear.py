@@ -11,6 +11,7 @@ import torch
 from .. import ops
 from ._pipeline import localize_pipelined
 from ..kv import ShardedKV, make_store
+from ..parallel.comm import LoopbackComm
 from ..utils import trace
 
 TRAIN, VAL, PRED = 0, 1, 2
@@ -57,6 +58,18 @@ class LinearLearner:
         if comm.size > 1:
             from ..kv.psx import Psx
             self.psx = Psx(self)
+        # one GPU, one shard: the whole step is one native call
+        # (csrc/bind/hip_ops.cc LinearStep) -- at the reference's minibatch
+        # of 10000 rows the Python glue of the step cost more host time than
+        # the GPU work it launches
+        self._native = None
+        if (self.device.type == "cuda" and comm.size == 1 and self.kv.nshard == 1
+                and not isinstance(comm, LoopbackComm)):
+            from .. import _native
+            self._native = _native.hip().LinearStep(self.store, int(conf.algo), conf.lr_eta,
+                                                    conf.lr_beta, conf.lambda_l1,
+                                                    conf.lambda_l2, int(conf.loss),
+                                                    self.kv.guard.max_load)
 
     def _localize(self, keys, offset, val, next_batch):
         return localize_pipelined(self, keys, offset, val, next_batch)
@@ -72,6 +85,18 @@ class LinearLearner:
             self.last_empty = self.psx.last_empty
             return py if wtype == PRED else None
         self.last_empty = offset.numel() <= 1 and self.comm.size == 1
+        if self._native is not None and not self.max_key:
+            nk = no = nv = None
+            ready = 0
+            if next_batch is not None:
+                nk, no, nv = next_batch[:3]
+                if len(next_batch) > 3 and next_batch[3] is not None:
+                    ready = next_batch[3].cuda_event
+            py = self._native.step(keys, offset, val, label, train, self.met, self.auc_sum,
+                                   nk, no, nv, ready)
+            if label.numel():
+                self.n_mb += 1
+            return py if wtype == PRED else None
         with trace.span("localize"):
             loc = self._localize(keys, offset, val, next_batch)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
@@ -100,6 +125,9 @@ class LinearLearner:
         model: progress counters, save, end of pass, end of a timed run)."""
         if self.psx is not None:
             self.psx.flush()
+        if self._native is not None:
+            self._native.reset()  # (a localize begun for a minibatch never trained)
+            self.kv.guard.grows = self._native.grows
         self.kv.flush()
 
     def take_progress(self):
