@@ -2194,6 +2194,10 @@ class LinearStep {
       : store_(store), algo_(algo), alpha_(alpha), beta_(beta), l1_(l1), l2_(l2), loss_(loss),
         max_load_(max_load) {
     TORCH_CHECK(store->vstride() == 0, "LinearStep needs a linear store");
+    // the localize-free step unless a bitwise-repeatable one is asked for
+    // (its per-slot gradient sums are float atomics)
+    direct_ = !deterministic() && !(std::getenv("WH_LINEAR_STEP") &&
+                                    std::string(std::getenv("WH_LINEAR_STEP")) == "localize");
     dev_ = store->slots_.device().index();
     c10::DeviceGuard g(store->slots_.device());
     ls_ = c10::hip::getStreamFromPool(false, dev_);
@@ -2224,6 +2228,107 @@ class LinearStep {
               const Tensor& label, bool train, const Tensor& met, const Tensor& auc_sum,
               const c10::optional<Tensor>& nkeys, const c10::optional<Tensor>& noffset,
               const c10::optional<Tensor>& nval, int64_t ready) {
+    if (direct_) return step_direct(keys, offset, val, label, train, met, auc_sum, ready);
+    return step_localize(keys, offset, val, label, train, met, auc_sum, nkeys, noffset, nval,
+                         ready);
+  }
+
+  // The localize-free step (csrc/hip/linear_direct.hip): touch (dedup per
+  // row tile in LDS, find-or-insert, slot list) -> forward on the slots ->
+  // AUC -> per-slot gradient sums -> push over the slot list. No host read;
+  // the next minibatch's producer event is waited for at the END of this
+  // step's work on S.
+  Tensor step_direct(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+                     const Tensor& label, bool train, const Tensor& met, const Tensor& auc_sum,
+                     int64_t ready) {
+    CHECK_IN(keys, torch::kInt64);
+    CHECK_IN(offset, torch::kInt64);
+    CHECK_IN(label, torch::kFloat32);
+    CHECK_IN(met, torch::kFloat64);
+    const int64_t nrows = offset.numel() - 1, nnz = keys.numel();
+    TORCH_CHECK(label.numel() == nrows, "label size mismatch");
+    const float* vp = nullptr;
+    if (val.has_value() && val->defined() && val->numel()) {
+      CHECK_IN((*val), torch::kFloat32);
+      TORCH_CHECK(val->numel() == nnz, "val size mismatch");
+      vp = ptr<float>(*val);
+    }
+    c10::DeviceGuard g(keys.device());
+    const hipStream_t S = cur_stream(keys);
+    auto i32 = keys.options().dtype(torch::kInt32);
+    // inputs produced on another stream (a data generator / copy stream)
+    // are read on S: their blocks are not reused before S is done with them
+    {
+      auto cs = c10::hip::getCurrentHIPStream(dev_);
+      for (const Tensor* x : {&keys, &offset, &label})
+        c10::hip::HIPCachingAllocator::recordStream(x->storage().data_ptr(), cs);
+      if (vp) c10::hip::HIPCachingAllocator::recordStream(val->storage().data_ptr(), cs);
+    }
+    // store guard: the previous step's summary (long complete), then room
+    // for every id of this minibatch to be new
+    if (sum_pending_) {
+      WH_HIP_CHECK_HOST(hipEventSynchronize(ev_sum_));
+      sum_pending_ = false;
+      const int64_t* h = sum_h_.data_ptr<int64_t>();
+      keys_ = h[0];
+      TORCH_CHECK(h[1] == 0, "parameter store shard lost data: ", h[1], " failed inserts (table ",
+                  h[0], "/", store_->cap(), " keys)");
+    }
+    if (train && keys_ + nnz > max_load_ * store_->cap()) {
+      int64_t cap = store_->cap();
+      while (keys_ + nnz > 0.5 * cap) cap *= 2;
+      store_->grow(cap);
+      ++grows_;
+    }
+    if (!grad_.defined() || grad_.numel() < store_->cap())
+      grad_ = torch::zeros({store_->cap()}, keys.options().dtype(torch::kFloat32));
+    if (!ucount_.defined()) ucount_ = torch::empty({1}, i32);
+    WH_HIP_CHECK_HOST(hipMemsetAsync(ucount_.data_ptr(), 0, 4, S));
+    auto lid = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
+    auto ulist = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
+    const int R = wh::ld_rows_per_tile(nnz, nrows);
+    ++stamp_;
+    if (stamp_ == 0) stamp_ = 1;
+    wh::KVTable t = store_->table();
+    wh::ld_touch(t, reinterpret_cast<const uint64_t*>(keys.data_ptr()), ptr<int64_t>(offset),
+                 nrows, R, stamp_, train ? 1 : 0, ptr<int32_t>(lid), ptr<int32_t>(ulist),
+                 reinterpret_cast<unsigned int*>(ucount_.data_ptr()), S);
+    if (train) {
+      Tensor sm = store_->summary();
+      WH_HIP_CHECK_HOST(hipMemcpyAsync(sum_h_.data_ptr(), sm.data_ptr(), 32, hipMemcpyDeviceToHost, S));
+      WH_HIP_CHECK_HOST(hipEventRecord(ev_sum_, S));
+      sum_pending_ = true;
+      keys_ += nnz;  // an upper bound until the summary is read
+    }
+    auto f32 = keys.options().dtype(torch::kFloat32);
+    auto py = torch::empty({nrows}, f32);
+    auto dual = torch::empty({nrows}, f32);
+    auto part = torch::empty({wh::fm_fwd_partials()}, met.options());
+    const int lossf = (int)loss_ | (met.numel() >= 5 ? 256 : 0);
+    wh::lin_forward_strided(nrows, ptr<int64_t>(offset), ptr<int32_t>(lid), vp,
+                            reinterpret_cast<const float*>(t.sl) + 2, 8, ptr<float>(label), lossf,
+                            ptr<float>(py), ptr<float>(dual), ptr<double>(met), ptr<double>(part),
+                            ptr<unsigned int>(dev_ws(keys.device()).fwd_ticket), S);
+    auc_acc_side(py, label, auc_sum);
+    if (train && nnz > 0) {
+      wh::ld_backward(ptr<int32_t>(lid), vp, ptr<int64_t>(offset), nrows, R, ptr<float>(dual),
+                      ptr<float>(grad_), S);
+      ++pushes_;
+      wh::LinearHP hp{(int)algo_, (float)alpha_, (float)beta_, (float)l1_, (float)l2_,
+                      (float)((beta_ + std::sqrt((double)pushes_)) / alpha_)};
+      wh::ld_push(t, ptr<int32_t>(ulist), reinterpret_cast<unsigned int*>(ucount_.data_ptr()),
+                  std::min<int64_t>(nnz, store_->cap()), ptr<float>(grad_), hp, S);
+    }
+    // the next minibatch (produced on another stream) is read by S after
+    // this step's work: order S after its producer now
+    if (ready) WH_HIP_CHECK_HOST(hipStreamWaitEvent(S, reinterpret_cast<hipEvent_t>(ready), 0));
+    return py;
+  }
+
+  Tensor step_localize(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+                       const Tensor& label, bool train, const Tensor& met, const Tensor& auc_sum,
+                       const c10::optional<Tensor>& nkeys, const c10::optional<Tensor>& noffset,
+                       const c10::optional<Tensor>& nval, int64_t ready) {
     c10::DeviceGuard g(keys.device());
     const hipStream_t S = cur_stream(keys);
     // this minibatch's localize
@@ -2321,6 +2426,7 @@ class LinearStep {
   void reset() { job_.reset(); job_keys_ = Tensor(); }
 
   int64_t grows() const { return grows_; }
+  bool direct() const { return direct_; }
   int64_t pushes() const { return pushes_; }
   void set_pushes(int64_t p) { pushes_ = p; }
 
@@ -2334,6 +2440,9 @@ class LinearStep {
   c10::hip::HIPStream ls_ = c10::hip::getDefaultHIPStream();
   hipEvent_t ev_s_ = nullptr, ev_sum_ = nullptr, ev_ls_ = nullptr;
   bool s_job_ = false;
+  bool direct_ = true;
+  Tensor grad_, ucount_;  // direct step: per-slot gradient sums (all zero between steps)
+  uint32_t stamp_ = 0;
   std::unique_ptr<LocalizeJob> job_;
   Tensor job_keys_;
   Tensor sum_h_;
@@ -2364,6 +2473,7 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("next_val") = py::none(), py::arg("ready") = 0)
       .def("reset", &LinearStep::reset)
       .def_property_readonly("grows", &LinearStep::grows)
+      .def_property_readonly("direct", [](const LinearStep& l) { return l.direct(); })
       .def_property("pushes", &LinearStep::pushes, &LinearStep::set_pushes);
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
         py::arg("nshard") = 1, py::arg("hint") = 0, py::arg("exchange") = py::none());

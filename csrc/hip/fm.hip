@@ -309,7 +309,7 @@ template <int G>
 __global__ __launch_bounds__(kThreads) void k_lin_fwd(int64_t nrows, const int64_t* __restrict__ off,
                                                       const int32_t* __restrict__ lid,
                                                       const float* __restrict__ val,
-                                                      const float* __restrict__ w,
+                                                      const float* __restrict__ w, int wstride,
                                                       const float* __restrict__ label, int loss,
                                                       float* __restrict__ py_out,
                                                       float* __restrict__ dual_out, double* part,
@@ -322,7 +322,11 @@ __global__ __launch_bounds__(kThreads) void k_lin_fwd(int64_t nrows, const int64
        row += ngroups) {
     float acc = 0.f;
     const int64_t b = off[row], e = off[row + 1];
-    for (int64_t j = b + gl; j < e; j += G) acc += (val ? val[j] : 1.f) * w[lid[j]];
+    for (int64_t j = b + gl; j < e; j += G) {
+      const int32_t l = lid[j];
+      if (wstride == 1) acc += (val ? val[j] : 1.f) * w[l];
+      else if (l >= 0) acc += (val ? val[j] : 1.f) * w[(int64_t)l * wstride];  // (table slots)
+    }
     acc = group_sum<G>(acc);
     if (gl == 0) {
       const float y = label[row];
@@ -956,7 +960,7 @@ void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const 
     constexpr int G = 8;
     nblk = grid_for(nrows * G, kThreads, kFwdBlocks);
     hipLaunchKernelGGL(k_lin_fwd<G>, dim3(nblk), dim3(kThreads), 0, s, nrows, offset, lid, val,
-                       w_or_hdr, label, loss, py, dual, part, met, ticket, acc5);
+                       w_or_hdr, 1, label, loss, py, dual, part, met, ticket, acc5);
   } else {
     const int G = vstride / 4;  // vstride <= 256 enforced by the binding
     const float2* hdr = reinterpret_cast<const float2*>(w_or_hdr);
@@ -965,6 +969,19 @@ void fm_forward(int64_t nrows, const int64_t* offset, const int32_t* lid, const 
     WH_DISPATCH_G(G, k_fm_fwd, grid, block, 0, s, nrows, offset, lid, val, hdr, vc, vstride,
                   label, loss, py, dual, xv, part, met, ticket, acc5);
   }
+}
+
+void lin_forward_strided(int64_t nrows, const int64_t* offset, const int32_t* lid,
+                         const float* val, const float* w, int wstride, const float* label,
+                         int loss, float* py, float* dual, double* met, double* part,
+                         unsigned int* ticket, hipStream_t s) {
+  if (nrows <= 0) return;
+  const int acc5 = (loss >> 8) & 1;
+  loss &= 0xff;
+  constexpr int G = 8;
+  const int nblk = grid_for(nrows * G, kThreads, kFwdBlocks);
+  hipLaunchKernelGGL(k_lin_fwd<G>, dim3(nblk), dim3(kThreads), 0, s, nrows, offset, lid, val, w,
+                     wstride, label, loss, py, dual, part, met, ticket, acc5);
 }
 
 static int64_t scalar_cap(int64_t nuniq, int64_t nnz) { return nuniq + nnz / kChunk + 1; }

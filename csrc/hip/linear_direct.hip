@@ -1,0 +1,253 @@
+// Single-shard linear step WITHOUT a localize: the minibatch's feature ids
+// go straight to the parameter table, and gradients are summed per table
+// slot. For one GPU (P = 1) the localize (unique ids + per-id occurrence
+// lists) exists only to dedup the lookups and to order the transposed
+// product; both jobs are done here per row tile in LDS:
+//
+//   k_ld_touch  per tile of rows: dedup the tile's ids in an LDS hash table,
+//               find-or-insert each distinct id in the HBM table once, stamp
+//               the slot with the step number (the first tile to stamp a
+//               slot appends it to the minibatch's slot list: wave-aggregated
+//               appends), and write the slot of every non-zero (lid = slot).
+//   (forward)   fm.hip k_lin_fwd reads w straight from the slots (stride 8).
+//   k_ld_bwd    per tile: g = x * dual[row] accumulated per distinct slot in
+//               LDS, then one float atomic per (tile, slot) into a dense
+//               per-slot gradient array -- hot ids cost one atomic per tile,
+//               not one per occurrence.
+//   k_ld_push   per listed slot: take (and clear) its summed gradient, apply
+//               SGD / AdaGrad / FTRL (reference learn/linear/async_sgd.h:
+//               71-180, penalty.h:36-41).
+//
+// No host synchronisation: the list length stays on the device (the push
+// launches over the non-zero count, surplus lanes exit), so a 10000-row
+// minibatch (the reference's published configuration) costs a handful of
+// launches. The gradient sums use float atomics (order-free up to rounding);
+// WH_DETERMINISTIC=1 keeps the localize path.
+#include "wh_common.h"
+#include "wh_kernels.h"
+#include "kv_device.h"
+
+namespace wh {
+namespace {
+
+using namespace kvd;
+
+constexpr int kLdThreads = 256;
+constexpr int kLdTable = 4096;          // LDS hash entries per tile (>= 2x the tile's ids)
+constexpr int kLdProbe = 64;            // LDS probe bound (a full table falls back to global)
+
+// the tile's row range [r0, r1) and its non-zero range [j0, j1); row offsets
+// of the tile staged in LDS (R + 1 entries) for the row of a non-zero
+__device__ __forceinline__ int row_in_tile(const int64_t* so, int nr, int64_t j) {
+  int lo = 0, hi = nr - 1;  // largest r with so[r] <= j
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (so[mid] <= j) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint32_t lhash(uint64_t k) { return (uint32_t)(mix64(k) & (kLdTable - 1)); }
+
+__global__ __launch_bounds__(kLdThreads) void k_ld_touch(
+    KVTable t, const uint64_t* __restrict__ keys, const int64_t* __restrict__ off, int64_t nrows,
+    int R, uint32_t stamp, int insert, int32_t* __restrict__ lid, int32_t* __restrict__ ulist,
+    unsigned int* __restrict__ ucount) {
+  __shared__ unsigned long long lk[kLdTable];
+  __shared__ int32_t lslot[kLdTable];
+  __shared__ int32_t lst[kLdTable];  // occupied entries, in insertion order
+  __shared__ unsigned int nlist;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  if (r0 >= nrows) return;
+  const int64_t r1 = r0 + R < nrows ? r0 + R : nrows;
+  const int64_t j0 = off[r0], j1 = off[r1];
+  for (int e = threadIdx.x; e < kLdTable; e += kLdThreads) lk[e] = kEmptyKey;
+  if (threadIdx.x == 0) nlist = 0;
+  __syncthreads();
+  // phase A: distinct ids of the tile (LDS CAS); ids that do not fit are
+  // resolved per occurrence in phase C
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += kLdThreads) {
+    const uint64_t k = keys[j];
+    if (k == kEmptyKey) continue;
+    uint32_t h = lhash(k);
+    for (int p = 0; p < kLdProbe; ++p, h = (h + 1) & (kLdTable - 1)) {
+      const unsigned long long o = atomicCAS(&lk[h], (unsigned long long)kEmptyKey,
+                                             (unsigned long long)k);
+      if (o == kEmptyKey) {
+        lst[atomicAdd(&nlist, 1u)] = (int32_t)h;
+        break;
+      }
+      if (o == k) break;
+    }
+  }
+  __syncthreads();
+  // phase B: one table probe per distinct id, kPullPer in flight per lane
+  const int nl = (int)nlist;
+  const uint64_t mask = (uint64_t)t.cap - 1;
+  int created = 0, failed = 0;
+  for (int b = threadIdx.x * kPullPer; b < nl; b += kLdThreads * kPullPer) {
+    uint64_t k[kPullPer], h[kPullPer], pv[kPullPer];
+    int32_t sl[kPullPer];
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r) {
+      k[r] = b + r < nl ? lk[lst[b + r]] : kEmptyKey;
+      h[r] = mix64(k[r]) & mask;
+      pv[r] = k[r] != kEmptyKey ? ld_relaxed(&t.sl[h[r]].key) : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r) {
+      sl[r] = -1;
+      if (k[r] == kEmptyKey) continue;
+      bool cr = false;
+      sl[r] = probe_slot(t.sl, mask, k[r], h[r], pv[r], insert, &cr);
+      created += cr ? 1 : 0;
+      if (insert && sl[r] < 0) ++failed;
+      lslot[lst[b + r]] = sl[r];
+    }
+    // stamp: the first tile of this step to reach a slot lists it
+    uint32_t old[kPullPer];
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r)
+      old[r] = sl[r] >= 0 ? atomicExch(&t.sl[sl[r]].cnt, stamp) : stamp;
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r) {
+      const bool first = old[r] != stamp;
+      const uint64_t m = __ballot(first);
+      unsigned int base = 0;
+      const int lane = threadIdx.x & 63;
+      const int leader = m ? __ffsll((unsigned long long)m) - 1 : 0;
+      if (m && lane == leader) base = atomicAdd(ucount, (unsigned int)__popcll(m));
+      base = __shfl(base, leader, 64);
+      if (first) ulist[base + __popcll(m & ((1ull << lane) - 1ull))] = sl[r];
+    }
+  }
+  const long long ci = wave_sum_ll(created), cf = wave_sum_ll(failed);
+  if ((threadIdx.x & 63) == 0) {
+    if (ci) atomicAdd(stat_ptr(t.stats, 4), (unsigned long long)ci);
+    if (cf) atomicAdd(stat_ptr(t.stats, 2), (unsigned long long)cf);
+  }
+  __syncthreads();
+  // phase C: the slot of every non-zero
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += kLdThreads) {
+    const uint64_t k = keys[j];
+    int32_t s = -1;
+    if (k != kEmptyKey) {
+      uint32_t h = lhash(k);
+      int p = 0;
+      for (; p < kLdProbe; ++p, h = (h + 1) & (kLdTable - 1))
+        if (lk[h] == k) break;
+      if (p < kLdProbe) {
+        s = lslot[h];
+      } else {  // the tile overflowed its LDS table: resolve this one directly
+        bool cr = false;
+        const uint64_t hh = mix64(k) & mask;
+        s = probe_slot(t.sl, mask, k, hh, ld_relaxed(&t.sl[hh].key), insert, &cr);
+        if (cr) atomicAdd(stat_ptr(t.stats, 4), 1ull);
+        if (s >= 0 && atomicExch(&t.sl[s].cnt, stamp) != stamp)
+          ulist[atomicAdd(ucount, 1u)] = s;
+      }
+    }
+    lid[j] = s;
+  }
+}
+
+__global__ __launch_bounds__(kLdThreads) void k_ld_bwd(
+    const int32_t* __restrict__ lid, const float* __restrict__ val,
+    const int64_t* __restrict__ off, int64_t nrows, int R, const float* __restrict__ dual,
+    float* __restrict__ grad) {
+  __shared__ int32_t ls[kLdTable];
+  __shared__ float lg[kLdTable];
+  __shared__ int32_t lst[kLdTable];
+  __shared__ int64_t so[1025];
+  __shared__ float sd[1024];
+  __shared__ unsigned int nlist;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  if (r0 >= nrows) return;
+  const int64_t r1 = r0 + R < nrows ? r0 + R : nrows;
+  const int nr = (int)(r1 - r0);
+  for (int e = threadIdx.x; e < kLdTable; e += kLdThreads) {
+    ls[e] = -1;
+    lg[e] = 0.f;
+  }
+  for (int r = threadIdx.x; r <= nr; r += kLdThreads) so[r] = off[r0 + r];
+  for (int r = threadIdx.x; r < nr; r += kLdThreads) sd[r] = dual[r0 + r];
+  if (threadIdx.x == 0) nlist = 0;
+  __syncthreads();
+  const int64_t j0 = so[0], j1 = so[nr];
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += kLdThreads) {
+    const int32_t s = lid[j];
+    if (s < 0) continue;
+    const float g = (val ? val[j] : 1.f) * sd[row_in_tile(so, nr, j)];
+    uint32_t h = (uint32_t)(mix64((uint64_t)s) & (kLdTable - 1));
+    int p = 0;
+    for (; p < kLdProbe; ++p, h = (h + 1) & (kLdTable - 1)) {
+      const int32_t o = atomicCAS(&ls[h], -1, s);
+      if (o == -1) {
+        lst[atomicAdd(&nlist, 1u)] = (int32_t)h;
+        break;
+      }
+      if (o == s) break;
+    }
+    if (p < kLdProbe) atomicAdd(&lg[h], g);
+    else atomicAdd(&grad[s], g);  // (table full: straight to the slot)
+  }
+  __syncthreads();
+  const int nl = (int)nlist;
+  for (int i = threadIdx.x; i < nl; i += kLdThreads) {
+    const int e = lst[i];
+    atomicAdd(&grad[ls[e]], lg[e]);
+  }
+}
+
+__global__ __launch_bounds__(kLdThreads) void k_ld_push(KVTable t, const int32_t* __restrict__ ulist,
+                                                        const unsigned int* __restrict__ ucount,
+                                                        int64_t cap_list, float* __restrict__ grad,
+                                                        LinearHP hp) {
+  const int64_t i = (int64_t)blockIdx.x * kLdThreads + threadIdx.x;
+  const int64_t n = *ucount;
+  float oldw = 0.f, neww = 0.f;
+  if (i < n && i < cap_list) {
+    const int32_t s = ulist[i];
+    const float g = grad[s];
+    grad[s] = 0.f;  // the array is all-zero again after the push
+    oldw = t.sl[s].w;
+    neww = linear_update(t.sl[s], g, hp, hp.sgd_eta);
+  }
+  count_nnz_delta(oldw, neww, t.stats);
+}
+
+}  // namespace
+
+int ld_rows_per_tile(int64_t nnz, int64_t nrows) {
+  // ~2048 non-zeros per tile (the LDS table holds 4096 distinct ids), at
+  // most 1024 rows (the tile's LDS row offsets)
+  const int64_t avg = nrows > 0 ? (nnz + nrows - 1) / nrows : 1;
+  int64_t R = 2048 / (avg > 0 ? avg : 1);
+  return (int)(R < 1 ? 1 : (R > 1024 ? 1024 : R));
+}
+
+void ld_touch(const KVTable& t, const uint64_t* keys, const int64_t* off, int64_t nrows, int R,
+              uint32_t stamp, int insert, int32_t* lid, int32_t* ulist, unsigned int* ucount,
+              hipStream_t s) {
+  if (nrows <= 0) return;
+  const int64_t nb = (nrows + R - 1) / R;
+  hipLaunchKernelGGL(k_ld_touch, dim3((unsigned)nb), dim3(kLdThreads), 0, s, t, keys, off, nrows,
+                     R, stamp, insert, lid, ulist, ucount);
+}
+
+void ld_backward(const int32_t* lid, const float* val, const int64_t* off, int64_t nrows, int R,
+                 const float* dual, float* grad, hipStream_t s) {
+  if (nrows <= 0) return;
+  const int64_t nb = (nrows + R - 1) / R;
+  hipLaunchKernelGGL(k_ld_bwd, dim3((unsigned)nb), dim3(kLdThreads), 0, s, lid, val, off, nrows,
+                     R, dual, grad);
+}
+
+void ld_push(const KVTable& t, const int32_t* ulist, const unsigned int* ucount, int64_t cap_list,
+             float* grad, LinearHP hp, hipStream_t s) {
+  if (cap_list <= 0) return;
+  hipLaunchKernelGGL(k_ld_push, dim3(grid_for(cap_list, kLdThreads)), dim3(kLdThreads), 0, s, t,
+                     ulist, ucount, cap_list, grad, hp);
+}
+
+}  // namespace wh

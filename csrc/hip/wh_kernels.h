@@ -280,6 +280,22 @@ bool ps_pack_gw(const float* gw, int64_t U, int vstride, const int64_t* segS,
 //   loss | 256, met[4] += this minibatch's accuracy flipped below 0.5
 //   part: scratch of fm_fwd_partials() doubles (per-block metric partials)
 int64_t fm_fwd_partials();
+// linear forward with w read at w[lid * wstride] (lid < 0: no weight):
+// w = &table.sl[0].w, wstride = 8 reads the weights straight from the slots
+void lin_forward_strided(int64_t nrows, const int64_t* offset, const int32_t* lid,
+                         const float* val, const float* w, int wstride, const float* label,
+                         int loss, float* py, float* dual, double* met, double* part,
+                         unsigned int* ticket, hipStream_t s);
+// ------------------------------------------------------- linear_direct.hip
+// single-shard linear step without a localize (see the file header)
+int ld_rows_per_tile(int64_t nnz, int64_t nrows);
+void ld_touch(const KVTable& t, const uint64_t* keys, const int64_t* off, int64_t nrows, int R,
+              uint32_t stamp, int insert, int32_t* lid, int32_t* ulist, unsigned int* ucount,
+              hipStream_t s);
+void ld_backward(const int32_t* lid, const float* val, const int64_t* off, int64_t nrows, int R,
+                 const float* dual, float* grad, hipStream_t s);
+void ld_push(const KVTable& t, const int32_t* ulist, const unsigned int* ucount, int64_t cap_list,
+             float* grad, LinearHP hp, hipStream_t s);
 // CUs the persistent FM grids leave free for concurrent RCCL kernels
 void fm_set_cu_reserve(int cus);
 int fm_cu_reserve();

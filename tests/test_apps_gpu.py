@@ -288,9 +288,13 @@ def test_native_linear_step_matches_python_step(algo):
         st = lr.store
         occ = st.occupied().long()
         m = dict(zip(st.keys[occ].cpu().tolist(), st.w[occ].cpu().tolist()))
-        return m, prog, lr
-    a, pa, la = run(True)
-    b, pb, lb = run(False)
+        keys, label, off = criteo_batch(2000, 6, 0, dev, card)  # unseen ids too
+        py = lr.process(keys, off, None, label, 2, 0)  # PRED: no insert, no push
+        return m, prog, lr, py
+    a, pa, la, ya = run(True)
+    assert la._native.direct  # the localize-free step is the default
+    b, pb, lb, yb = run(False)
+    assert torch.allclose(ya, yb, atol=1e-4, rtol=1e-4)
     assert la.kv.guard.grows >= 1  # the 4096-slot table had to grow on both paths
     assert a.keys() == b.keys()
     bad = sum(1 for k, w in b.items() if abs(w - a[k]) > 1e-5 * max(1.0, abs(w)))
