@@ -246,6 +246,7 @@ def main():
             "rank_ms_per_step_min": 1000.0 * min(per_rank) / args.steps,
             "rank_ms_per_step_max": 1000.0 * max(per_rank) / args.steps,
             "wire_bytes_per_gpu_step": wire,
+            "localize_retries": (_native.hip().loc_retries() if device.type == "cuda" else 0),
         }), flush=True)
     comm.finalize()
     return 0

@@ -171,6 +171,12 @@ Tensor& loc_timing_buf() {
   return t;
 }
 
+// localize retries after a partition overflowed its LDS table (diagnostics)
+int64_t& loc_retries() {
+  static int64_t n = 0;
+  return n;
+}
+
 class LocalizeJob {
  public:
   // defer_exchange: enqueue the localize kernels now, but call the count
@@ -254,6 +260,7 @@ class LocalizeJob {
       for (int64_t q = 1; q < nrecv_; q += stride_) over |= h[nshard_ + 1 + q] != 0;
       if (!over) break;
       if (part_) {  // a partition overflowed its LDS table (here or on a peer)
+        ++loc_retries();
         part_ = false;
         if (counted_) {
           ws.part_inflight--;
@@ -280,6 +287,12 @@ class LocalizeJob {
       recv_h_.data_ptr<int64_t>()[q] = h[nshard_ + 1 + q];
     return {owner_cnt_h_, recv_h_};
   }
+
+  // the partitioned path: every output is produced on the job's stream
+  // before the count read. (The hash path finishes on the caller's stream
+  // and returns its scratch table to the device pool from there: a job
+  // begun later on another stream must be ordered after that finish.)
+  bool partitioned() const { return part_; }
 
   std::vector<Tensor> finish() {
     counts();
@@ -1904,6 +1917,35 @@ class PinnedBuf {
   Tensor t_;
 };
 
+// A ring of pinned staging buffers for stream-ordered uploads: a slot is
+// rewritten only after the copy that last read it has run (its event), so
+// the host never has to drain the stream to reuse staging memory.
+class PinnedRing {
+ public:
+  static constexpr int N = 4;
+  ~PinnedRing() {
+    for (auto& e : ev_)
+      if (e) (void)hipEventDestroy(e);
+  }
+  template <typename T>
+  T* get(int64_t n) {
+    cur_ = (cur_ + 1) % N;
+    if (ev_[cur_]) WH_HIP_CHECK_HOST(hipEventSynchronize(ev_[cur_]));
+    return buf_[cur_].get<T>(n);
+  }
+  Tensor tensor() const { return buf_[cur_].tensor(); }
+  // after enqueuing the copy that reads the current slot
+  void mark(hipStream_t s) {
+    if (!ev_[cur_]) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_[cur_], hipEventDisableTiming));
+    WH_HIP_CHECK_HOST(hipEventRecord(ev_[cur_], s));
+  }
+
+ private:
+  PinnedBuf buf_[N];
+  hipEvent_t ev_[N] = {nullptr, nullptr, nullptr, nullptr};
+  int cur_ = N - 1;
+};
+
 static double l1_threshold(double g, double alpha) {
   if (alpha <= 0) return g;
   return g > alpha ? g - alpha : (g < -alpha ? g + alpha : 0.0);
@@ -1952,7 +1994,10 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
   std::map<int, std::pair<int, int>> seg;  // live frontier segments (node -> [b, e))
   seg[root] = {0, (int)n};
   std::vector<std::array<int, 3>> done;    // finished leaves: node, b, e
-  PinnedBuf up, up_tasks, down;  // separate staging: an upload may still be in flight
+  // staging rings for the uploads (node tables, task lists), a plain buffer
+  // for the one download per level (read right after its synchronisation)
+  PinnedRing up, up_tasks;
+  PinnedBuf down;
   Tensor ridx = ridx0;
   // histogram of the given (slot -> [b, e) device segments); tasks by chunk
   auto build_hist = [&](const Tensor& dseg, const std::vector<int64_t>& seglen) -> Tensor {
@@ -1975,6 +2020,7 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
     std::memcpy(h + tasks.size(), red.data(), red.size() * 4);
     auto d = up_tasks.tensor().narrow(0, 0, (int64_t)(tasks.size() + red.size()) * 4)
                  .to(B.device(), /*non_blocking=*/true).view(torch::kInt32);
+    up_tasks.mark(s);
     auto hist = torch::empty({S, F, nbin, 2}, f64);
     auto part = torch::empty({nt * wh::gbdt_hist_pstride((int)max_fcnt, (int)nbin)},
                              gpair.options().dtype(torch::kInt64));
@@ -1982,8 +2028,8 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
                   ptr<float>(qscale), ptr<int32_t>(d), (int)nt, ptr<int32_t>(d) + nt * 5,
                   (int)nr, (int)max_fcnt, dw, ptr<int64_t>(part), ptr<double>(hist), s,
                   ptr<int32_t>(dseg), chunk);
-    // the pinned staging buffer is reused by the next upload: wait for this one
-    WH_HIP_CHECK_HOST(hipStreamSynchronize(s));
+    // (no drain here: the staging ring waits for this copy only when its slot
+    // comes round again; the histogram allreduce is stream-ordered)
     if (reduce) allreduce(hist);
     return hist;
   };
@@ -2002,6 +2048,7 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
       double* th = up.get<double>(2 * S);
       for (int k = 0; k < S; ++k) th[2 * k] = tot[frontier[k]][0], th[2 * k + 1] = tot[frontier[k]][1];
       auto T = up.tensor().narrow(0, 0, 16 * S).to(B.device(), true).view(torch::kFloat64);
+      up.mark(s);
       split_out = torch::empty({S, 6}, f64);
       auto cand = torch::empty({std::max<int64_t>((int64_t)S * F * 4, 1)}, f64);
       TORCH_CHECK(wh::gbdt_split(ptr<double>(H_front), ptr<double>(T),
@@ -2093,6 +2140,7 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
     }
     for (int i = 0; i < nt; ++i) h_tb[i] = tiles[i].first, h_tn[i] = tiles[i].second;
     auto dw32 = up.tensor().narrow(0, 0, nwords * 4).to(B.device(), true).view(torch::kInt32);
+    up.mark(s);
     const int32_t* d = ptr<int32_t>(dw32);
     const int32_t *d_feat = d, *d_bin = d + nnode, *d_sb = d + 2 * nnode;
     const uint8_t* d_defl = reinterpret_cast<const uint8_t*>(d + 4 * nnode);
@@ -2189,6 +2237,13 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
 // the launches.
 class LinearStep {
  public:
+  struct Summ {
+    Tensor h;
+    hipEvent_t ev = nullptr;
+    int64_t issued = 0;
+    bool pending = false;
+  };
+  static constexpr int kSumm = 4;
   LinearStep(KVStore* store, int64_t algo, double alpha, double beta, double l1, double l2,
              int64_t loss, double max_load)
       : store_(store), algo_(algo), alpha_(alpha), beta_(beta), l1_(l1), l2_(l2), loss_(loss),
@@ -2202,15 +2257,14 @@ class LinearStep {
     c10::DeviceGuard g(store->slots_.device());
     ls_ = c10::hip::getStreamFromPool(false, dev_);
     WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_s_, hipEventDisableTiming));
-    WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_sum_, hipEventDisableTiming));
     WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_ls_, hipEventDisableTiming));
-    sum_h_ = torch::zeros({4}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
   }
   ~LinearStep() {
     job_.reset();
     (void)hipEventDestroy(ev_s_);
-    (void)hipEventDestroy(ev_sum_);
     (void)hipEventDestroy(ev_ls_);
+    for (Summ& m : sum_)
+      if (m.ev) (void)hipEventDestroy(m.ev);
   }
 
   // WH_LS_WAIT=1: the localize stream waits for S before every job (the
@@ -2228,9 +2282,18 @@ class LinearStep {
               const Tensor& label, bool train, const Tensor& met, const Tensor& auc_sum,
               const c10::optional<Tensor>& nkeys, const c10::optional<Tensor>& noffset,
               const c10::optional<Tensor>& nval, int64_t ready) {
-    if (direct_) return step_direct(keys, offset, val, label, train, met, auc_sum, ready);
-    return step_localize(keys, offset, val, label, train, met, auc_sum, nkeys, noffset, nval,
-                         ready);
+    if (use_direct(keys.numel())) {
+      if (job_) reset();  // (a localize begun for this minibatch by a larger one before)
+      return step_direct(keys, offset, val, label, train, met, auc_sum, ready);
+    }
+    // begin the next minibatch's localize only if it will take this path
+    const bool nl = nkeys.has_value() && nkeys->defined() && !use_direct(nkeys->numel());
+    Tensor py = step_localize(keys, offset, val, label, train, met, auc_sum,
+                              nl ? nkeys : c10::nullopt, nl ? noffset : c10::nullopt,
+                              nl ? nval : c10::nullopt, nl ? ready : 0);
+    if (!nl && ready)  // the next (direct-path) minibatch is read on S after this step
+      WH_HIP_CHECK_HOST(hipStreamWaitEvent(cur_stream(keys), reinterpret_cast<hipEvent_t>(ready), 0));
+    return py;
   }
 
   // The localize-free step (csrc/hip/linear_direct.hip): touch (dedup per
@@ -2266,20 +2329,7 @@ class LinearStep {
     }
     // store guard: the previous step's summary (long complete), then room
     // for every id of this minibatch to be new
-    if (sum_pending_) {
-      WH_HIP_CHECK_HOST(hipEventSynchronize(ev_sum_));
-      sum_pending_ = false;
-      const int64_t* h = sum_h_.data_ptr<int64_t>();
-      keys_ = h[0];
-      TORCH_CHECK(h[1] == 0, "parameter store shard lost data: ", h[1], " failed inserts (table ",
-                  h[0], "/", store_->cap(), " keys)");
-    }
-    if (train && keys_ + nnz > max_load_ * store_->cap()) {
-      int64_t cap = store_->cap();
-      while (keys_ + nnz > 0.5 * cap) cap *= 2;
-      store_->grow(cap);
-      ++grows_;
-    }
+    if (train) guard_before(nnz);
     if (!grad_.defined() || grad_.numel() < store_->cap())
       grad_ = torch::zeros({store_->cap()}, keys.options().dtype(torch::kFloat32));
     if (!ucount_.defined()) ucount_ = torch::empty({1}, i32);
@@ -2293,13 +2343,7 @@ class LinearStep {
     wh::ld_touch(t, reinterpret_cast<const uint64_t*>(keys.data_ptr()), ptr<int64_t>(offset),
                  nrows, R, stamp_, train ? 1 : 0, ptr<int32_t>(lid), ptr<int32_t>(ulist),
                  reinterpret_cast<unsigned int*>(ucount_.data_ptr()), S);
-    if (train) {
-      Tensor sm = store_->summary();
-      WH_HIP_CHECK_HOST(hipMemcpyAsync(sum_h_.data_ptr(), sm.data_ptr(), 32, hipMemcpyDeviceToHost, S));
-      WH_HIP_CHECK_HOST(hipEventRecord(ev_sum_, S));
-      sum_pending_ = true;
-      keys_ += nnz;  // an upper bound until the summary is read
-    }
+    if (train) guard_after(S, nnz);
     auto f32 = keys.options().dtype(torch::kFloat32);
     auto py = torch::empty({nrows}, f32);
     auto dual = torch::empty({nrows}, f32);
@@ -2335,6 +2379,9 @@ class LinearStep {
     std::vector<Tensor> loc;
     if (job_ && job_keys_.is_same(keys)) {
       loc = job_->finish();
+      // a hash-path job emptied its scratch table on S: the next job on the
+      // localize stream (which may reuse that table) waits for S
+      if (!job_->partitioned()) s_job_ = true;
       // the job's outputs were allocated on the localize stream and are read
       // on S from here on: their blocks go back to the localize stream's
       // pool only once S's queued work is done (so the localize stream
@@ -2386,28 +2433,9 @@ class LinearStep {
     }
     // store guard: the previous open's summary (long complete), then room
     // for this open's inserts
-    if (sum_pending_) {
-      WH_HIP_CHECK_HOST(hipEventSynchronize(ev_sum_));
-      sum_pending_ = false;
-      const int64_t* h = sum_h_.data_ptr<int64_t>();
-      keys_ = h[0];
-      TORCH_CHECK(h[1] == 0, "parameter store shard lost data: ", h[1], " failed inserts (table ",
-                  h[0], "/", store_->cap(), " keys)");
-    }
-    if (train && keys_ + U > max_load_ * store_->cap()) {
-      int64_t cap = store_->cap();
-      while (keys_ + U > 0.5 * cap) cap *= 2;
-      store_->grow(cap);  // (nothing in flight references the old slots)
-      ++grows_;
-    }
+    if (train) guard_before(U);
     Tensor slot = store_->find(uniq, train);
-    if (train) {
-      Tensor sm = store_->summary();
-      WH_HIP_CHECK_HOST(hipMemcpyAsync(sum_h_.data_ptr(), sm.data_ptr(), 32, hipMemcpyDeviceToHost, S));
-      WH_HIP_CHECK_HOST(hipEventRecord(ev_sum_, S));
-      sum_pending_ = true;
-      keys_ += U;  // an upper bound until the summary is read
-    }
+    if (train) guard_after(S, U);
     Tensor w = store_->linear_pull(slot);
     auto fw = fm_forward(offset, lid, val, w, c10::nullopt, 0, label, loss_, met);
     auc_acc_side(fw[0], label, auc_sum);
@@ -2425,8 +2453,77 @@ class LinearStep {
   // drop a begun localize (end of a pass)
   void reset() { job_.reset(); job_keys_ = Tensor(); }
 
+  // ---- store guard without a per-step host wait: table summaries (keys,
+  // failed inserts) are read when their event has completed (polled), the
+  // key count in between is bounded by the inserts issued since; only a
+  // table close to its load bound waits for the newest summary before
+  // deciding to grow (nothing in flight references old slots: a grow is
+  // stream-ordered before this step's inserts)
+  void guard_read(Summ& m) {
+    const int64_t* h = m.h.data_ptr<int64_t>();
+    m.pending = false;
+    TORCH_CHECK(h[1] == 0, "parameter store shard lost data: ", h[1], " failed inserts (table ",
+                h[0], "/", store_->cap(), " keys)");
+    if (m.issued >= base_issued_) {
+      base_keys_ = h[0];
+      base_issued_ = m.issued;
+    }
+  }
+  void guard_poll(bool block) {
+    for (Summ& m : sum_) {
+      if (!m.pending) continue;
+      if (block) WH_HIP_CHECK_HOST(hipEventSynchronize(m.ev));
+      else if (hipEventQuery(m.ev) != hipSuccess) continue;
+      guard_read(m);
+    }
+  }
+  int64_t keys_bound() const { return base_keys_ + (issued_ - base_issued_); }
+  void guard_before(int64_t n_new) {
+    guard_poll(false);
+    const double lim = max_load_ * (double)store_->cap();
+    if (keys_bound() + n_new > lim) {
+      guard_poll(true);  // the exact count before growing
+      if (keys_bound() + n_new > lim) {
+        int64_t cap = store_->cap();
+        while (keys_bound() + n_new > 0.5 * cap) cap *= 2;
+        store_->grow(cap);
+        ++grows_;
+      }
+    }
+  }
+  void guard_after(hipStream_t S, int64_t n_new) {
+    issued_ += n_new;
+    Summ& m = sum_[sum_i_];
+    sum_i_ = (sum_i_ + 1) % kSumm;
+    if (m.pending) {  // (the GPU is kSumm steps behind: wait for the oldest)
+      WH_HIP_CHECK_HOST(hipEventSynchronize(m.ev));
+      guard_read(m);
+    }
+    if (!m.h.defined()) {
+      m.h = torch::zeros({4}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
+      WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&m.ev, hipEventDisableTiming));
+    }
+    Tensor sm = store_->summary();
+    WH_HIP_CHECK_HOST(hipMemcpyAsync(m.h.data_ptr(), sm.data_ptr(), 32, hipMemcpyDeviceToHost, S));
+    WH_HIP_CHECK_HOST(hipEventRecord(m.ev, S));
+    m.issued = issued_;
+    m.pending = true;
+  }
+
   int64_t grows() const { return grows_; }
   bool direct() const { return direct_; }
+  // the localize-free step pays off while a minibatch is small (launch- and
+  // latency-bound: the reference's 10000 rows); above WH_LINEAR_DIRECT_NNZ
+  // non-zeros (default 2^20, ~27k Criteo rows) the localize's global dedup
+  // does fewer table probes and atomics than per-tile dedup
+  bool use_direct(int64_t nnz) const {
+    static int64_t lim = -1;
+    if (lim < 0) {
+      const char* e = std::getenv("WH_LINEAR_DIRECT_NNZ");
+      lim = e ? std::atoll(e) : (1 << 20);
+    }
+    return direct_ && nnz <= lim;
+  }
   int64_t pushes() const { return pushes_; }
   void set_pushes(int64_t p) { pushes_ = p; }
 
@@ -2438,16 +2535,17 @@ class LinearStep {
   double max_load_;
   int dev_ = 0;
   c10::hip::HIPStream ls_ = c10::hip::getDefaultHIPStream();
-  hipEvent_t ev_s_ = nullptr, ev_sum_ = nullptr, ev_ls_ = nullptr;
+  hipEvent_t ev_s_ = nullptr, ev_ls_ = nullptr;
   bool s_job_ = false;
   bool direct_ = true;
   Tensor grad_, ucount_;  // direct step: per-slot gradient sums (all zero between steps)
   uint32_t stamp_ = 0;
   std::unique_ptr<LocalizeJob> job_;
   Tensor job_keys_;
-  Tensor sum_h_;
-  bool sum_pending_ = false;
-  int64_t keys_ = 0, hint_ = 0, grows_ = 0, pushes_ = 0;
+  Summ sum_[kSumm];
+  int sum_i_ = 0;
+  int64_t issued_ = 0, base_keys_ = 0, base_issued_ = 0;
+  int64_t hint_ = 0, grows_ = 0, pushes_ = 0;
 };
 
 PYBIND11_MODULE(_hip, m) {
@@ -2463,6 +2561,8 @@ PYBIND11_MODULE(_hip, m) {
       .def("counts", &LocalizeJob::counts)
       .def("finish", &LocalizeJob::finish);
   m.def("loc_timing_read", []() { return loc_timing_buf().clone(); });
+  m.def("loc_retries", []() { return loc_retries(); },
+        "localize jobs redone on the hash path after a partition overflow (count)");
   py::class_<LinearStep>(m, "LinearStep")
       .def(py::init<KVStore*, int64_t, double, double, double, double, int64_t, double>(),
            py::arg("store"), py::arg("algo"), py::arg("alpha"), py::arg("beta"), py::arg("l1"),

@@ -7,8 +7,9 @@
 //   k_ld_touch  per tile of rows: dedup the tile's ids in an LDS hash table,
 //               find-or-insert each distinct id in the HBM table once, stamp
 //               the slot with the step number (the first tile to stamp a
-//               slot appends it to the minibatch's slot list: wave-aggregated
-//               appends), and write the slot of every non-zero (lid = slot).
+//               slot appends it to the minibatch's slot list: one global
+//               atomic per tile), and write the slot of every non-zero
+//               (lid = slot).
 //   (forward)   fm.hip k_lin_fwd reads w straight from the slots (stride 8).
 //   k_ld_bwd    per tile: g = x * dual[row] accumulated per distinct slot in
 //               LDS, then one float atomic per (tile, slot) into a dense
@@ -56,13 +57,14 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
   __shared__ unsigned long long lk[kLdTable];
   __shared__ int32_t lslot[kLdTable];
   __shared__ int32_t lst[kLdTable];  // occupied entries, in insertion order
-  __shared__ unsigned int nlist;
+  __shared__ int32_t lfirst[kLdTable];  // slots this tile stamped first
+  __shared__ unsigned int nlist, nfirst, fbase;
   const int64_t r0 = (int64_t)blockIdx.x * R;
   if (r0 >= nrows) return;
   const int64_t r1 = r0 + R < nrows ? r0 + R : nrows;
   const int64_t j0 = off[r0], j1 = off[r1];
   for (int e = threadIdx.x; e < kLdTable; e += kLdThreads) lk[e] = kEmptyKey;
-  if (threadIdx.x == 0) nlist = 0;
+  if (threadIdx.x == 0) nlist = nfirst = 0;
   __syncthreads();
   // phase A: distinct ids of the tile (LDS CAS); ids that do not fit are
   // resolved per occurrence in phase C
@@ -110,17 +112,15 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
     for (int r = 0; r < kPullPer; ++r)
       old[r] = sl[r] >= 0 ? atomicExch(&t.sl[sl[r]].cnt, stamp) : stamp;
 #pragma unroll
-    for (int r = 0; r < kPullPer; ++r) {
-      const bool first = old[r] != stamp;
-      const uint64_t m = __ballot(first);
-      unsigned int base = 0;
-      const int lane = threadIdx.x & 63;
-      const int leader = m ? __ffsll((unsigned long long)m) - 1 : 0;
-      if (m && lane == leader) base = atomicAdd(ucount, (unsigned int)__popcll(m));
-      base = __shfl(base, leader, 64);
-      if (first) ulist[base + __popcll(m & ((1ull << lane) - 1ull))] = sl[r];
-    }
+    for (int r = 0; r < kPullPer; ++r)
+      if (old[r] != stamp) lfirst[atomicAdd(&nfirst, 1u)] = sl[r];
   }
+  __syncthreads();
+  // the tile's first-stamped slots join the minibatch's list with ONE global
+  // atomic per tile (a same-address atomic per wave serialised ~6k of them)
+  if (threadIdx.x == 0) fbase = nfirst ? atomicAdd(ucount, nfirst) : 0u;
+  __syncthreads();
+  for (unsigned int i = threadIdx.x; i < nfirst; i += kLdThreads) ulist[fbase + i] = lfirst[i];
   const long long ci = wave_sum_ll(created), cf = wave_sum_ll(failed);
   if ((threadIdx.x & 63) == 0) {
     if (ci) atomicAdd(stat_ptr(t.stats, 4), (unsigned long long)ci);

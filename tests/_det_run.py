@@ -38,4 +38,19 @@ vrow_rank = np.cumsum(snap["has_v"]) - 1  # V rows in slot order -> reorder by k
 vidx = vrow_rank[order][hv]
 h.update(np.ascontiguousarray(snap["V"][vidx]).tobytes())
 h.update(np.ascontiguousarray(snap["VG"][vidx]).tobytes())
+# the linear model's single-GPU native step with the look-ahead localize (in
+# deterministic mode: the hash localize, finished on the compute stream)
+from wormhole_amd.config.schema import LinearConfig  # noqa: E402
+from wormhole_amd.models.linear import LinearLearner  # noqa: E402
+lin = LinearLearner(LinearConfig(minibatch=20000), Comm(dev, init=False), dev, cap=1 << 22)
+for s, (k, l, o) in enumerate(data):
+    nb = (data[s + 1][0], data[s + 1][2], None) if s + 1 < len(data) else None
+    lin.process(k, o, None, l, 0, 0, next_batch=nb)
+lin.flush()
+lp = lin.take_progress()
+ls = _numpy(_gather(lin.store, "linear"))
+lo = np.argsort(ls["keys"].astype(np.uint64))
+h.update(np.array(lp, dtype=np.float64).tobytes())
+for name in ("keys", "w"):
+    h.update(np.ascontiguousarray(ls[name][lo]).tobytes())
 print("DIGEST", h.hexdigest(), "LOSS %.9g" % (prog[0] / prog[5]))
