@@ -2513,14 +2513,15 @@ class LinearStep {
   int64_t grows() const { return grows_; }
   bool direct() const { return direct_; }
   // the localize-free step pays off while a minibatch is small (launch- and
-  // latency-bound: the reference's 10000 rows); above WH_LINEAR_DIRECT_NNZ
-  // non-zeros (default 2^20, ~27k Criteo rows) the localize's global dedup
-  // does fewer table probes and atomics than per-tile dedup
+  // latency-bound: the reference's 10000 rows: 71.0 vs 55.1 M ex/s); above
+  // WH_LINEAR_DIRECT_NNZ non-zeros (default 600k, ~15k Criteo rows; at 25k
+  // rows the localize path is ahead, 129 vs 109 M ex/s) the localize's global
+  // dedup does fewer table probes and atomics than per-tile dedup
   bool use_direct(int64_t nnz) const {
     static int64_t lim = -1;
     if (lim < 0) {
       const char* e = std::getenv("WH_LINEAR_DIRECT_NNZ");
-      lim = e ? std::atoll(e) : (1 << 20);
+      lim = e ? std::atoll(e) : 600000;
     }
     return direct_ && nnz <= lim;
   }
