@@ -139,16 +139,18 @@ def main():
     # minibatch's localize; the learner waits on its event just before the
     # next localize begins.
     gen = torch.cuda.Stream(device) if device.type == "cuda" else None
+    main = torch.cuda.current_stream(device) if device.type == "cuda" else None
+    if gen is not None:
+        from wormhole_amd.utils import streams
+        evs = streams.EventRing(8)
 
     def batch_async(step):
         if gen is None:
             return batch(step), None
-        with torch.cuda.stream(gen):
+        with streams.on(gen):
             out = batch(step)
-            ev = torch.cuda.Event()
-            ev.record(gen)
-        out[1].record_stream(torch.cuda.current_stream(device))  # the label
-        return out, ev
+        out[1].record_stream(main)  # the label (keys / offsets: recorded by the learner)
+        return out, evs.record(gen)
 
     def run(first, n):
         nxt, ev = batch(first), None

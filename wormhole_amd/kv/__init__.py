@@ -21,6 +21,7 @@ The gradient push mirrors it (4-byte gw per key + the embedding rows).
 import torch
 
 from .. import _native, ops
+from ..utils import streams
 from .cpu_store import CpuKVStore
 
 
@@ -55,6 +56,8 @@ class StoreGuard:
         # flight (the deferred push; push(i-2) under the pipelined multi-shard
         # step) and each may allocate one V row per key after the summary
         self.recent = [0, 0]
+        self._ring = None
+        self._main = None  # the stream opens run on (cached)
         self.cuda = not isinstance(store, CpuKVStore)
 
     def after_open(self):
@@ -70,8 +73,14 @@ class StoreGuard:
             # copy run on a side stream behind the open, off the compute
             # stream's critical path; read() waits for them one open later
             side = self._side
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
+            if self._ring is None:
+                self._ring = streams.EventRing(4)
+            main = torch.cuda.current_stream() if self._main is None else self._main
+            if streams.current_id(main.device_index) != main.stream_id:
+                main = torch.cuda.current_stream()
+            self._main = main
+            self._ring.wait(side, main)
+            with streams.on(side):
                 s = self.store.summary()
                 h.copy_(s, non_blocking=True)
                 ev.record(side)

@@ -58,6 +58,7 @@ import numpy as np
 import torch
 
 from .. import _native, ops
+from ..utils import streams
 
 TRAIN, VAL, PRED = 0, 1, 2
 # (Stream placements measured and dropped -- docs/performance.md "Measured
@@ -185,8 +186,7 @@ class Psx:
         # C2 / C3 are issued from xs, each behind its producer's event only
         # (see _a2a)
         self.xs = torch.cuda.Stream(device=self.dev) if self.cuda else None
-        self._evring = [torch.cuda.Event() for _ in range(16)] if self.cuda else None
-        self._evi = 0
+        self._ring = streams.EventRing(32) if self.cuda else None
         self.S = torch.cuda.current_stream(self.dev) if self.cuda else None
         if self.cuda and getattr(self.comm, "backend", "") in ("nccl", "loopback-rccl"):
             _native.hip().set_cu_reserve(_CU_RESERVE)
@@ -235,7 +235,7 @@ class Psx:
             xs = self.xs
             xs.wait_event(ready)
             x.record_stream(xs)
-            with torch.cuda.stream(xs):
+            with streams.on(xs):
                 out, work = self.comm.all_to_all_v_async(x, send_rows, recv_rows)
             if out.is_cuda:
                 out.record_stream(self.S)  # allocated on xs, read on S
@@ -250,10 +250,7 @@ class Psx:
         long after the stream wait that consumed it was enqueued)."""
         if not self.cuda:
             return None
-        ev = self._evring[self._evi]
-        self._evi = (self._evi + 1) % len(self._evring)
-        ev.record(self.S)
-        return ev
+        return self._ring.record(self.S)
 
     def wire_reset(self):
         self.wire = [0, 0, 0, 0]
@@ -281,14 +278,15 @@ class Psx:
             yield
             return
         S = self.S
-        self.cs.wait_stream(S)
-        cur = torch.cuda.current_stream(self.dev)
-        if cur != S:  # called from a localize job on its own stream
-            self.cs.wait_stream(cur)
+        ring = self._ring
+        ring.wait(self.cs, S)
+        if streams.current_id(self.dev.index) != S.stream_id:
+            # called from a localize job on its own stream (ls)
+            ring.wait(self.cs, self.ls)
         for t in inputs:
             if t is not None and t.is_cuda:
                 t.record_stream(self.cs)
-        with torch.cuda.stream(self.cs):
+        with streams.on(self.cs):
             yield
 
     # ------------------------------------------------------------ localize
@@ -320,14 +318,14 @@ class Psx:
             # S itself reads the job's outputs only after the host has waited
             # for the job's count read (which follows `ready` on ls).
             cs, ls = self.S, self.ls
-            ls.wait_stream(cs)
+            self._ring.wait(ls, cs)
             if ready is not None:
                 ls.wait_event(ready)
             for t in (keys, offset, val):
                 if t is not None:
                     t.record_stream(ls)
                     t.record_stream(cs)
-            with torch.cuda.stream(ls):
+            with streams.on(ls):
                 k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
                 job = _native.hip().LocalizeJob(k, offset, val, S, int(self.uhint),
                                                 self._exchange(carried, flag), defer)
@@ -344,7 +342,7 @@ class Psx:
     def _exchange_deferred(self):
         """Issue C0 of an early-begun localize (after the open it carries)."""
         if self.job is not None and self.cuda and not isinstance(self.job[1], tuple):
-            with torch.cuda.stream(self.ls):
+            with streams.on(self.ls):
                 self.job[1].exchange()  # (no-op unless the job deferred it)
 
     def _counts(self):
@@ -570,7 +568,7 @@ class Psx:
         self.last_empty = True
 
     def train(self, keys, offset, val, label, data_pass, next_batch):
-        if self.cuda:
+        if self.cuda and streams.current_id(self.dev.index) != self.S.stream_id:
             self.S = torch.cuda.current_stream(self.dev)
         self.last_empty = False
         self._ensure_job(keys, offset, val)

@@ -16,6 +16,7 @@ concurrently with minibatch i's localize finish. Every rank must pass
 import torch
 
 from .. import ops
+from ..utils import streams
 
 
 def localize_pipelined(lrn, keys, offset, val, next_batch):
@@ -54,23 +55,23 @@ def begin_next(lrn, next_batch, uhint):
         # on the compute stream so far (memory safety, below); the job's
         # finish host-syncs its event before any compute-stream kernel reads
         # its buffers.
-        cur = torch.cuda.current_stream(nk.device.index)  # (an int: the fast path)
+        cur = _cur_stream(nk.device)
         side = _loc_stream(nk.device)
-        side.wait_stream(cur)
+        _ring(nk.device).wait(side, cur)
         if ready is not None:
             side.wait_event(ready)
         for t in (nk, no, nv):
             if t is not None:
                 t.record_stream(side)
                 t.record_stream(cur)
-        with torch.cuda.stream(side):
+        with streams.on(side):
             k = ops.key_mod(nk, lrn.max_key) if lrn.max_key else nk
             job = ops.localize_begin(k, no, nv, lrn.kv.nshard, uhint,
                                      exchange=lrn.kv.count_exchange())
         lrn._job = (nk, job)
         return
     if ready is not None and nk.is_cuda:
-        cur = torch.cuda.current_stream(nk.device.index)  # (an int: the fast path)
+        cur = _cur_stream(nk.device)
         cur.wait_event(ready)
         for t in (nk, no, nv):  # produced on another stream, consumed here
             if t is not None:
@@ -89,6 +90,23 @@ def begin_next(lrn, next_batch, uhint):
 # allocator hands back to the side stream is never rewritten before the
 # compute-stream kernels that read it have run.
 _streams = {}
+_rings = {}
+_cur = {}
+
+
+def _ring(dev):
+    r = _rings.get(dev)
+    if r is None:
+        r = _rings[dev] = streams.EventRing(8)
+    return r
+
+
+def _cur_stream(dev):
+    """The current stream of dev (a cached Stream while it stays current)."""
+    s = _cur.get(dev)
+    if s is None or streams.current_id(dev.index) != s.stream_id:
+        s = _cur[dev] = torch.cuda.current_stream(dev)
+    return s
 
 
 def _loc_stream(dev):
