@@ -2277,7 +2277,8 @@ class LinearStep {
 
   // one minibatch; returns the predictions py [rows]. next_*: the next
   // call's minibatch, whose localize begins now (on the localize stream,
-  // after `ready` -- a hipEvent_t handle of its producer, or 0).
+  // after `ready` -- a hipEvent_t handle of its producer -- or, with 0, after
+  // everything queued on the current stream).
   Tensor step(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
               const Tensor& label, bool train, const Tensor& met, const Tensor& auc_sum,
               const c10::optional<Tensor>& nkeys, const c10::optional<Tensor>& noffset,
@@ -2411,7 +2412,11 @@ class LinearStep {
     // the next minibatch's localize, on its own stream behind everything
     // queued on S so far (its outputs may reuse blocks S still reads)
     if (nkeys.has_value() && nkeys->defined()) {
-      if (s_job_ || ls_waits_s()) {  // a localize ran on S: the workspace is S's until then
+      // the localize stream waits for S when a localize ran on S (the
+      // workspace is S's until then) or when the next minibatch has no
+      // producer event: it was then made on S (slices, offset rebasing, the
+      // handover from a parse stream), possibly by work queued just now
+      if (s_job_ || ls_waits_s() || !ready) {
         WH_HIP_CHECK_HOST(hipEventRecord(ev_s_, S));
         WH_HIP_CHECK_HOST(hipStreamWaitEvent(ls_.stream(), ev_s_, 0));
         s_job_ = false;

@@ -303,6 +303,56 @@ def test_native_linear_step_matches_python_step(algo):
         assert abs(x - y) <= 1e-4 * max(1.0, abs(y)), (pa, pb)
 
 
+def test_native_linear_lookahead_made_on_the_compute_stream(monkeypatch):
+    """The file worker hands the look-ahead minibatch over without a producer
+    event (slices and offset rebasing queued on the compute stream just
+    before the step): the next localize must wait for the compute stream.
+    Each look-ahead here is produced behind a slow kernel chain, and the
+    model must equal the one trained on batches made long before."""
+    import torch
+    from wormhole_amd.config.schema import LinearConfig
+    from wormhole_amd.data.synthetic import criteo_batch
+    from wormhole_amd.models.linear import LinearLearner
+    from wormhole_amd.parallel.comm import Comm
+    monkeypatch.setenv("WH_LINEAR_STEP", "localize")
+    dev = torch.device("cuda", 0)
+    card = [50, 400, 3000, 20, 7, 900, 100000]
+    batches = [criteo_batch(3000, 5, s, dev, card) for s in range(8)]
+    torch.cuda.synchronize()
+    slow = torch.randn(2048, 2048, device=dev)
+
+    def late(b):  # a copy of b made on the current stream behind ~ms of work
+        x = slow
+        for _ in range(8):
+            x = x @ slow
+        keys, label, off = b
+        return keys + (x[0, 0] * 0).long(), label, off + (x[0, 1] * 0).long()
+
+    def run(fresh):
+        conf = LinearConfig(algo=3, lr_eta=0.1)
+        lr = LinearLearner(conf, Comm(dev, init=False), dev, cap=1 << 16, seed=1)
+        assert lr._native is not None and not lr._native.direct
+        cur = batches[0]
+        for s in range(len(batches)):
+            nb = None
+            if s + 1 < len(batches):
+                nxt = late(batches[s + 1]) if fresh else batches[s + 1]
+                nb = (nxt[0], nxt[2], None)
+            keys, label, off = cur
+            lr.process(keys, off, None, label, 0, 0, next_batch=nb)
+            if nb is not None:
+                cur = (nb[0], nxt[1], nb[1])
+        lr.flush()
+        st = lr.store
+        occ = st.occupied().long()
+        return dict(zip(st.keys[occ].cpu().tolist(), st.w[occ].cpu().tolist())), lr.take_progress()
+    a, pa = run(True)
+    b, pb = run(False)
+    assert a.keys() == b.keys()
+    assert max(abs(w - a[k]) for k, w in b.items()) <= 1e-6
+    assert pa == pytest.approx(pb, rel=1e-6)
+
+
 def test_gbdt_leaf_walk_matches_raw_value_predict():
     """The training margins after each tree come from a per-row walk of the
     pruned tree on the bins (k_leaf_walk); predicting the same (compacted)
