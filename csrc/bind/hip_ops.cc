@@ -1180,9 +1180,11 @@ void auc_acc(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
   TORCH_CHECK(py.numel() < (int64_t)1 << 30, "auc: at most 2^30 examples per call");
   c10::DeviceGuard g(py.device());
   const int64_t n = py.numel();
-  auto scratch = torch::empty({wh::auc_ws_bytes(n)}, py.options().dtype(torch::kUInt8));
+  const int64_t wsb = wh::auc_ws_bytes(n);
+  Tensor scratch;
+  if (wsb) scratch = torch::empty({wsb}, py.options().dtype(torch::kUInt8));
   wh::auc_accumulate(ptr<float>(py), ptr<float>(label), n, dev_ws(py.device()).auc.data_ptr(),
-                     scratch.data_ptr(), ptr<double>(auc_sum), cur_stream(py));
+                     wsb ? scratch.data_ptr() : nullptr, ptr<double>(auc_sum), cur_stream(py));
 }
 
 // The same on a per-device side stream owned here (it waits for the current
@@ -1220,9 +1222,11 @@ void auc_acc_side(const Tensor& py, const Tensor& label, const Tensor& auc_sum) 
   c10::hip::HIPCachingAllocator::recordStream(label.storage().data_ptr(), a->s);
   c10::hip::HIPStreamGuard sg(a->s);  // the scratch is the side stream's
   const int64_t n = py.numel();
-  auto scratch = torch::empty({wh::auc_ws_bytes(n)}, py.options().dtype(torch::kUInt8));
+  const int64_t wsb = wh::auc_ws_bytes(n);
+  Tensor scratch;
+  if (wsb) scratch = torch::empty({wsb}, py.options().dtype(torch::kUInt8));
   wh::auc_accumulate(ptr<float>(py), ptr<float>(label), n, dev_ws(py.device()).auc.data_ptr(),
-                     scratch.data_ptr(), ptr<double>(auc_sum), a->s.stream());
+                     wsb ? scratch.data_ptr() : nullptr, ptr<double>(auc_sum), a->s.stream());
 }
 
 void auc_join(const Tensor& auc_sum) {
@@ -2342,7 +2346,7 @@ class LinearStep {
     if (stamp_ == 0) stamp_ = 1;
     wh::KVTable t = store_->table();
     wh::ld_touch(t, reinterpret_cast<const uint64_t*>(keys.data_ptr()), ptr<int64_t>(offset),
-                 nrows, R, stamp_, train ? 1 : 0, ptr<int32_t>(lid), ptr<int32_t>(ulist),
+                 nrows, nnz, R, stamp_, train ? 1 : 0, ptr<int32_t>(lid), ptr<int32_t>(ulist),
                  reinterpret_cast<unsigned int*>(ucount_.data_ptr()), S);
     if (train) guard_after(S, nnz);
     auto f32 = keys.options().dtype(torch::kFloat32);
@@ -2356,7 +2360,7 @@ class LinearStep {
                             ptr<unsigned int>(dev_ws(keys.device()).fwd_ticket), S);
     auc_acc_side(py, label, auc_sum);
     if (train && nnz > 0) {
-      wh::ld_backward(ptr<int32_t>(lid), vp, ptr<int64_t>(offset), nrows, R, ptr<float>(dual),
+      wh::ld_backward(ptr<int32_t>(lid), vp, ptr<int64_t>(offset), nrows, nnz, R, ptr<float>(dual),
                       ptr<float>(grad_), S);
       ++pushes_;
       wh::LinearHP hp{(int)algo_, (float)alpha_, (float)beta_, (float)l1_, (float)l2_,

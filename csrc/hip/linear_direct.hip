@@ -28,14 +28,23 @@
 #include "wh_kernels.h"
 #include "kv_device.h"
 
+#include <stdexcept>
+
 namespace wh {
 namespace {
 
 using namespace kvd;
 
 constexpr int kLdThreads = 256;
-constexpr int kLdTable = 4096;          // LDS hash entries per tile (>= 2x the tile's ids)
 constexpr int kLdProbe = 64;            // LDS probe bound (a full table falls back to global)
+
+// LDS hash entries per tile (T >= 2x the tile's ids; a tile holds ~T/2
+// non-zeros). Small minibatches take small tiles: at the reference's 10000
+// rows (390k non-zeros) 4096-entry tiles gave 193 workgroups at ~80 KB of LDS
+// each -- fewer than the CUs, one resident per CU -- so each tile's chain of
+// dependent probes was exposed; 1024-entry tiles give ~760 workgroups at
+// ~20 KB, several resident per CU.
+__host__ __device__ constexpr int ld_rows_cap(int T) { return T / 2 < 1024 ? T / 2 : 1024; }
 
 // the tile's row range [r0, r1) and its non-zero range [j0, j1); row offsets
 // of the tile staged in LDS (R + 1 entries) for the row of a non-zero
@@ -48,22 +57,24 @@ __device__ __forceinline__ int row_in_tile(const int64_t* so, int nr, int64_t j)
   return lo;
 }
 
-__device__ __forceinline__ uint32_t lhash(uint64_t k) { return (uint32_t)(mix64(k) & (kLdTable - 1)); }
+template <int T>
+__device__ __forceinline__ uint32_t lhash(uint64_t k) { return (uint32_t)(mix64(k) & (T - 1)); }
 
+template <int T>
 __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
     KVTable t, const uint64_t* __restrict__ keys, const int64_t* __restrict__ off, int64_t nrows,
     int R, uint32_t stamp, int insert, int32_t* __restrict__ lid, int32_t* __restrict__ ulist,
     unsigned int* __restrict__ ucount) {
-  __shared__ unsigned long long lk[kLdTable];
-  __shared__ int32_t lslot[kLdTable];
-  __shared__ int32_t lst[kLdTable];  // occupied entries, in insertion order
-  __shared__ int32_t lfirst[kLdTable];  // slots this tile stamped first
+  __shared__ unsigned long long lk[T];
+  __shared__ int32_t lslot[T];
+  __shared__ int32_t lst[T];     // occupied entries, in insertion order
+  __shared__ int32_t lfirst[T];  // slots this tile stamped first
   __shared__ unsigned int nlist, nfirst, fbase;
   const int64_t r0 = (int64_t)blockIdx.x * R;
   if (r0 >= nrows) return;
   const int64_t r1 = r0 + R < nrows ? r0 + R : nrows;
   const int64_t j0 = off[r0], j1 = off[r1];
-  for (int e = threadIdx.x; e < kLdTable; e += kLdThreads) lk[e] = kEmptyKey;
+  for (int e = threadIdx.x; e < T; e += kLdThreads) lk[e] = kEmptyKey;
   if (threadIdx.x == 0) nlist = nfirst = 0;
   __syncthreads();
   // phase A: distinct ids of the tile (LDS CAS); ids that do not fit are
@@ -71,8 +82,8 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
   for (int64_t j = j0 + threadIdx.x; j < j1; j += kLdThreads) {
     const uint64_t k = keys[j];
     if (k == kEmptyKey) continue;
-    uint32_t h = lhash(k);
-    for (int p = 0; p < kLdProbe; ++p, h = (h + 1) & (kLdTable - 1)) {
+    uint32_t h = lhash<T>(k);
+    for (int p = 0; p < kLdProbe; ++p, h = (h + 1) & (T - 1)) {
       const unsigned long long o = atomicCAS(&lk[h], (unsigned long long)kEmptyKey,
                                              (unsigned long long)k);
       if (o == kEmptyKey) {
@@ -132,9 +143,9 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
     const uint64_t k = keys[j];
     int32_t s = -1;
     if (k != kEmptyKey) {
-      uint32_t h = lhash(k);
+      uint32_t h = lhash<T>(k);
       int p = 0;
-      for (; p < kLdProbe; ++p, h = (h + 1) & (kLdTable - 1))
+      for (; p < kLdProbe; ++p, h = (h + 1) & (T - 1))
         if (lk[h] == k) break;
       if (p < kLdProbe) {
         s = lslot[h];
@@ -151,21 +162,23 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
   }
 }
 
+template <int T>
 __global__ __launch_bounds__(kLdThreads) void k_ld_bwd(
     const int32_t* __restrict__ lid, const float* __restrict__ val,
     const int64_t* __restrict__ off, int64_t nrows, int R, const float* __restrict__ dual,
     float* __restrict__ grad) {
-  __shared__ int32_t ls[kLdTable];
-  __shared__ float lg[kLdTable];
-  __shared__ int32_t lst[kLdTable];
-  __shared__ int64_t so[1025];
-  __shared__ float sd[1024];
+  constexpr int RC = ld_rows_cap(T);
+  __shared__ int32_t ls[T];
+  __shared__ float lg[T];
+  __shared__ int32_t lst[T];
+  __shared__ int64_t so[RC + 1];
+  __shared__ float sd[RC];
   __shared__ unsigned int nlist;
   const int64_t r0 = (int64_t)blockIdx.x * R;
   if (r0 >= nrows) return;
   const int64_t r1 = r0 + R < nrows ? r0 + R : nrows;
   const int nr = (int)(r1 - r0);
-  for (int e = threadIdx.x; e < kLdTable; e += kLdThreads) {
+  for (int e = threadIdx.x; e < T; e += kLdThreads) {
     ls[e] = -1;
     lg[e] = 0.f;
   }
@@ -178,9 +191,9 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_bwd(
     const int32_t s = lid[j];
     if (s < 0) continue;
     const float g = (val ? val[j] : 1.f) * sd[row_in_tile(so, nr, j)];
-    uint32_t h = (uint32_t)(mix64((uint64_t)s) & (kLdTable - 1));
+    uint32_t h = (uint32_t)(mix64((uint64_t)s) & (T - 1));
     int p = 0;
-    for (; p < kLdProbe; ++p, h = (h + 1) & (kLdTable - 1)) {
+    for (; p < kLdProbe; ++p, h = (h + 1) & (T - 1)) {
       const int32_t o = atomicCAS(&ls[h], -1, s);
       if (o == -1) {
         lst[atomicAdd(&nlist, 1u)] = (int32_t)h;
@@ -218,29 +231,38 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_push(KVTable t, const int32_t
 
 }  // namespace
 
+// the tile table for a minibatch of nnz non-zeros (see ld_rows_cap)
+static int ld_table(int64_t nnz) { return nnz <= (int64_t)1 << 21 ? 1024 : 4096; }
+
 int ld_rows_per_tile(int64_t nnz, int64_t nrows) {
-  // ~2048 non-zeros per tile (the LDS table holds 4096 distinct ids), at
-  // most 1024 rows (the tile's LDS row offsets)
+  // ~T/2 non-zeros per tile, at most ld_rows_cap(T) rows (the tile's LDS
+  // row offsets)
+  const int T = ld_table(nnz);
   const int64_t avg = nrows > 0 ? (nnz + nrows - 1) / nrows : 1;
-  int64_t R = 2048 / (avg > 0 ? avg : 1);
-  return (int)(R < 1 ? 1 : (R > 1024 ? 1024 : R));
+  int64_t R = (T / 2) / (avg > 0 ? avg : 1);
+  const int64_t cap = ld_rows_cap(T);
+  return (int)(R < 1 ? 1 : (R > cap ? cap : R));
 }
 
-void ld_touch(const KVTable& t, const uint64_t* keys, const int64_t* off, int64_t nrows, int R,
-              uint32_t stamp, int insert, int32_t* lid, int32_t* ulist, unsigned int* ucount,
-              hipStream_t s) {
+void ld_touch(const KVTable& t, const uint64_t* keys, const int64_t* off, int64_t nrows,
+              int64_t nnz, int R, uint32_t stamp, int insert, int32_t* lid, int32_t* ulist,
+              unsigned int* ucount, hipStream_t s) {
   if (nrows <= 0) return;
   const int64_t nb = (nrows + R - 1) / R;
-  hipLaunchKernelGGL(k_ld_touch, dim3((unsigned)nb), dim3(kLdThreads), 0, s, t, keys, off, nrows,
-                     R, stamp, insert, lid, ulist, ucount);
+  auto kern = ld_table(nnz) == 1024 ? k_ld_touch<1024> : k_ld_touch<4096>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(kLdThreads), 0, s, t, keys, off, nrows, R,
+                     stamp, insert, lid, ulist, ucount);
 }
 
-void ld_backward(const int32_t* lid, const float* val, const int64_t* off, int64_t nrows, int R,
-                 const float* dual, float* grad, hipStream_t s) {
+void ld_backward(const int32_t* lid, const float* val, const int64_t* off, int64_t nrows,
+                 int64_t nnz, int R, const float* dual, float* grad, hipStream_t s) {
   if (nrows <= 0) return;
+  const int T = ld_table(nnz);
+  if (R > ld_rows_cap(T)) throw std::runtime_error("ld_backward: tile rows exceed the LDS bound");
   const int64_t nb = (nrows + R - 1) / R;
-  hipLaunchKernelGGL(k_ld_bwd, dim3((unsigned)nb), dim3(kLdThreads), 0, s, lid, val, off, nrows,
-                     R, dual, grad);
+  auto kern = T == 1024 ? k_ld_bwd<1024> : k_ld_bwd<4096>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(kLdThreads), 0, s, lid, val, off, nrows, R,
+                     dual, grad);
 }
 
 void ld_push(const KVTable& t, const int32_t* ulist, const unsigned int* ucount, int64_t cap_list,

@@ -262,6 +262,92 @@ __global__ __launch_bounds__(kThreads) void k_auc_count(const unsigned long long
   auc_sum[0] += auc;
 }
 
+// ---------------------------------------------------------------------------
+// Small minibatches (n <= kAucSmallMax, e.g. the reference's 10000 rows): the
+// same rank-sum by direct pair counting in ONE launch. Block (x, y) holds the
+// positives of row chunk y in LDS (compacted, as keys) and each thread counts,
+// for kAsJ negatives of tile x, the positives with a smaller key -- the
+// identical integer as the bucketed path. n^2 / 2 compares at n = 10000 are
+// a few microseconds spread over ~200 workgroups; the five bucketed launches
+// were ~40 us of mostly launch and single-workgroup scan latency.
+constexpr int64_t kAucSmallMax = 24576;
+constexpr int kAsThreads = 256;
+constexpr int kAsJ = 2;
+constexpr int kAsTileJ = kAsThreads * kAsJ;
+constexpr int kAsTileI = 1024;
+
+__global__ __launch_bounds__(kAsThreads) void k_auc_small(const float* __restrict__ py,
+                                                          const float* __restrict__ lab,
+                                                          int64_t n, unsigned long long* area,
+                                                          unsigned int* ticket,
+                                                          unsigned long long* ptot,
+                                                          double* auc_sum) {
+  __shared__ unsigned long long pk[kAsTileI];
+  __shared__ int wcnt[kAsThreads / 64];
+  __shared__ unsigned long long wsum[kAsThreads / 64];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t i0 = (int64_t)blockIdx.y * kAsTileI;
+  int np = 0;  // positives of the chunk staged so far (block-uniform)
+#pragma unroll
+  for (int r = 0; r < kAsTileI / kAsThreads; ++r) {
+    const int64_t i = i0 + r * kAsThreads + tid;
+    const bool pos = i < n && lab[i] > 0.f;
+    const uint64_t m = __ballot(pos);
+    if (lane == 0) wcnt[wid] = __popcll(m);
+    __syncthreads();
+    int off = np, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kAsThreads / 64; ++w) {
+      off += w < wid ? wcnt[w] : 0;
+      tot += wcnt[w];
+    }
+    if (pos) pk[off + __popcll(m & ((1ull << lane) - 1ull))] = auc_key(py[i], i, true);
+    np += tot;
+    __syncthreads();
+  }
+  unsigned long long kj[kAsJ];
+#pragma unroll
+  for (int u = 0; u < kAsJ; ++u) {
+    const int64_t j = (int64_t)blockIdx.x * kAsTileJ + u * kAsThreads + tid;
+    kj[u] = (j < n && !(lab[j] > 0.f)) ? auc_key(py[j], j, false) : 0ull;  // 0: counts nothing
+  }
+  uint32_t c[kAsJ] = {};
+  for (int p = 0; p < np; ++p) {
+    const unsigned long long k = pk[p];
+#pragma unroll
+    for (int u = 0; u < kAsJ; ++u) c[u] += k < kj[u] ? 1u : 0u;
+  }
+  unsigned long long a = 0;
+#pragma unroll
+  for (int u = 0; u < kAsJ; ++u) a += c[u];
+  a = (unsigned long long)wave_sum_ll((long long)a);
+  if (lane == 0) wsum[wid] = a;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+#pragma unroll
+    for (int w = 0; w < kAsThreads / 64; ++w) t += wsum[w];
+    if (t) atomicAdd(area, t);
+    if (blockIdx.x == 0 && np) atomicAdd(ptot, (unsigned long long)np);
+    // the adds must be performed before this block's ticket add
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned tk = atomicAdd(ticket, 1u);
+    last = tk == gridDim.x * gridDim.y - 1;
+  }
+  __syncthreads();
+  if (!last || tid != 0) return;
+  __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double tot = (double)atomicExch(area, 0ull);
+  const double tp = (double)atomicExch(ptot, 0ull);
+  double auc = 1.0;
+  if (tp != 0 && tp != (double)n) {
+    const double r = tot / (tp * ((double)n - tp));
+    auc = r < 0.5 ? 1 - r : r;
+  }
+  auc_sum[0] += auc;
+}
+
 }  // namespace
 
 size_t auc_sort_tmp_bytes(int64_t n) {
@@ -304,12 +390,14 @@ void auc_from_sorted(const float* label_sorted, int64_t n, double* out, int64_t*
 namespace wh {
 
 // persistent (zeroed once; lohi[0] = ~0): cnt, pcnt [NB] u32, lohi [2] u64,
-// area u64, ticket u32 (+pad).  scratch: off, poff [NB + 1] u32, {lo, width},
-// per-example (bucket, rank) and the bucket-ordered keys.
+// area u64, ticket u32 (+pad), positives u64 (pair path).  scratch: off,
+// poff [NB + 1] u32, {lo, width}, per-example (bucket, rank) and the
+// bucket-ordered keys (none for the pair path).
 int64_t auc_ws_bytes(int64_t n) {
+  if (n <= kAucSmallMax) return 0;
   return 2 * ((int64_t)kAucBuckets + 4) * 4 + 16 + 2 * 8 + 8 * n + 8 * n + 64;
 }
-int64_t auc_ws_persistent_bytes() { return 2 * (int64_t)kAucBuckets * 4 + 4 * 8; }
+int64_t auc_ws_persistent_bytes() { return 2 * (int64_t)kAucBuckets * 4 + 5 * 8; }
 int64_t auc_ws_lohi_offset() { return 2 * (int64_t)kAucBuckets * 4; }
 
 void auc_accumulate(const float* py, const float* label, int64_t n, void* persist, void* scratch,
@@ -321,6 +409,13 @@ void auc_accumulate(const float* py, const float* label, int64_t n, void* persis
   unsigned long long* lohi = reinterpret_cast<unsigned long long*>(pcnt + kAucBuckets);
   unsigned long long* area = lohi + 2;
   unsigned int* ticket = reinterpret_cast<unsigned int*>(lohi + 3);
+  if (n <= kAucSmallMax) {
+    const dim3 grid((unsigned)((n + kAsTileJ - 1) / kAsTileJ),
+                    (unsigned)((n + kAsTileI - 1) / kAsTileI));
+    hipLaunchKernelGGL(k_auc_small, grid, dim3(kAsThreads), 0, s, py, label, n, area, ticket,
+                       lohi + 4, auc_sum);
+    return;
+  }
   char* sc = static_cast<char*>(scratch);
   uint32_t* off = reinterpret_cast<uint32_t*>(sc);
   uint32_t* poff = off + kAucBuckets + 4;  // 16-byte aligned for the vector stores

@@ -184,12 +184,13 @@ def test_auc(hip):
 
 
 def test_auc_ties_and_accumulate(hip):
-    """Sort-free bucketed AUC vs the stable-sort reference and the rocPRIM
-    sort path: heavy ties (quantised scores), all-equal scores (a zero
-    model), +-0, and on-device accumulation over repeated calls."""
+    """Sort-free AUC (pair counting up to 24576 examples, bucketed above)
+    vs the stable-sort reference and the rocPRIM sort path: heavy ties
+    (quantised scores), all-equal scores (a zero model), +-0, and on-device
+    accumulation over repeated calls."""
     g = torch.Generator().manual_seed(6)
     cases = []
-    for n in [1, 2, 777, 65536, 300001]:
+    for n in [1, 2, 777, 10000, 24576, 24577, 65536, 300001]:
         py = torch.randn(n, generator=g)
         cases.append((py, (torch.rand(n, generator=g) < torch.sigmoid(2 * py)).float()))
         q = torch.round(py * 4) / 4  # few distinct values: long tie runs
