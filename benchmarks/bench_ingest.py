@@ -86,6 +86,44 @@ def main():
         torch.cuda.synchronize()
         return n / s / 1e6
 
+    # H2D copy rates: pinned (torch), pageable, and a host reader batch
+    def h2d_rate(x, reps=10):
+        x.to(dev, non_blocking=True)
+        torch.cuda.synchronize()
+        t = time.time()
+        for _ in range(reps):
+            x.to(dev, non_blocking=True)
+        torch.cuda.synchronize()
+        return round(reps * x.numel() / (time.time() - t) / 1e9, 2)
+    nbytes = 30 << 20
+    out["h2d_GBs_pinned"] = h2d_rate(torch.empty(nbytes, dtype=torch.uint8, pin_memory=True))
+    out["h2d_GBs_pageable"] = h2d_rate(torch.empty(nbytes, dtype=torch.uint8))
+    b0 = host.TextBatches(txt[0], 0, 1, mb, True).next()[0]
+    out["reader_batch_pinned"] = bool(b0.is_pinned())
+    out["h2d_GBs_reader_batch"] = h2d_rate(b0)
+    del b0
+    # synchronous stage split of one part: host batch wait, H2D copy, device parse
+    tb = host.TextBatches(txt[0], 0, 1, mb, True)
+    st = {"read": 0.0, "h2d": 0.0, "parse": 0.0}
+    nb = 0
+    while True:
+        t0 = time.time()
+        b = tb.next()
+        if b is None:
+            break
+        t1 = time.time()
+        text = b[0].to(dev, non_blocking=True)
+        torch.cuda.synchronize()
+        t2 = time.time()
+        device_text.parse_block(text, b[1], "criteo")
+        torch.cuda.synchronize()
+        t3 = time.time()
+        st["read"] += t1 - t0
+        st["h2d"] += t2 - t1
+        st["parse"] += t3 - t2
+        nb += 1
+    out["sync_stage_ms_per_batch"] = {k: round(1e3 * v / max(nb, 1), 3) for k, v in st.items()}
+    out["batch_bytes"] = int(os.path.getsize(txt[0]) // max(nb, 1))
     drain(lambda f: Count(host.TextBatches(f, 0, 1, mb, True), lambda b: int(b[1])), txt[:1])
     out["host_text_Mrows_s"] = sync_rate(
         lambda f: Count(host.TextBatches(f, 0, 1, mb, True), lambda b: int(b[1])), txt)

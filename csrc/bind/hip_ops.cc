@@ -11,8 +11,10 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <cmath>
 #include <map>
 #include <memory>
@@ -877,6 +879,31 @@ class KVStore {
     wh::kv_summary(table(), ptr<int64_t>(out), cur_stream(slots_));
     return out;
   }
+
+  // The summary written by its kernel straight into coherent host memory
+  // (slot 0..3; the store guard alternates two), on the current stream; read
+  // with summary_read once an event recorded after it has completed. A
+  // 32-byte copy into pinned memory instead cost ~40 us of host time.
+  void summary_async(int64_t slot) {
+    TORCH_CHECK(slot >= 0 && slot < 4, "summary slot out of range");
+    c10::DeviceGuard g(slots_.device());
+    if (!sum_host_) {
+      void* p = nullptr;
+      WH_HIP_CHECK_HOST(hipHostMalloc(&p, 4 * 64, hipHostMallocMapped | hipHostMallocCoherent));
+      std::memset(p, 0, 4 * 64);
+      sum_host_.reset(static_cast<int64_t*>(p));
+    }
+    wh::kv_summary(table(), sum_host_.get() + 8 * slot, cur_stream(slots_));
+  }
+  std::vector<int64_t> summary_read(int64_t slot) const {
+    TORCH_CHECK(sum_host_ && slot >= 0 && slot < 4, "no summary in that slot");
+    const volatile int64_t* h = sum_host_.get() + 8 * slot;
+    return {h[0], h[1], h[2], h[3]};
+  }
+  struct HostFree {
+    void operator()(int64_t* p) const { (void)hipHostFree(p); }
+  };
+  std::unique_ptr<int64_t, HostFree> sum_host_;
 
   int64_t dim() const { return dim_; }
   int64_t vstride() const { return vstride_; }
@@ -1924,6 +1951,44 @@ class PinnedBuf {
 // A ring of pinned staging buffers for stream-ordered uploads: a slot is
 // rewritten only after the copy that last read it has run (its event), so
 // the host never has to drain the stream to reuse staging memory.
+// WH_STEP_TIMING=1: host time per section of a native step, summed and
+// printed (mean us per call) at exit -- the launch-bound small-minibatch path
+struct HostSplit {
+  const char* name;
+  double us[10] = {};
+  int64_t calls = 0;
+  explicit HostSplit(const char* n) : name(n) {}
+  void print() const {
+    std::fprintf(stderr, "[%s host us/call over %lld]", name, (long long)calls);
+    for (int i = 0; i < 10; ++i)
+      if (us[i] > 0) std::fprintf(stderr, " s%d %.2f", i, us[i] / calls);
+    std::fprintf(stderr, "\n");
+  }
+};
+class HostTimer {
+ public:
+  explicit HostTimer(HostSplit* h) : h_(h) {
+    if (h_) t_ = std::chrono::steady_clock::now();
+  }
+  void mark(int i) {
+    if (!h_) return;
+    const auto n = std::chrono::steady_clock::now();
+    h_->us[i] += std::chrono::duration<double, std::micro>(n - t_).count();
+    t_ = n;
+  }
+  ~HostTimer() {
+    if (h_ && ++h_->calls % 1000 == 0) h_->print();
+  }
+
+ private:
+  HostSplit* h_;
+  std::chrono::steady_clock::time_point t_;
+};
+static HostSplit* host_split(const char* name) {
+  const char* e = std::getenv("WH_STEP_TIMING");
+  return e && e[0] == '1' ? new HostSplit(name) : nullptr;
+}
+
 class PinnedRing {
  public:
   static constexpr int N = 4;
@@ -2241,8 +2306,10 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
 // the launches.
 class LinearStep {
  public:
+  // h: 4 words of coherent host memory the summary kernel writes directly
+  // (a 32-byte hipMemcpyAsync to pinned memory cost ~40 us of host time)
   struct Summ {
-    Tensor h;
+    int64_t* h = nullptr;
     hipEvent_t ev = nullptr;
     int64_t issued = 0;
     bool pending = false;
@@ -2267,8 +2334,11 @@ class LinearStep {
     job_.reset();
     (void)hipEventDestroy(ev_s_);
     (void)hipEventDestroy(ev_ls_);
-    for (Summ& m : sum_)
+    for (Summ& m : sum_) {
+      if (m.ev) (void)hipEventSynchronize(m.ev);
       if (m.ev) (void)hipEventDestroy(m.ev);
+      if (m.h) (void)hipHostFree(m.h);
+    }
   }
 
   // WH_LS_WAIT=1: the localize stream waits for S before every job (the
@@ -2321,6 +2391,7 @@ class LinearStep {
       TORCH_CHECK(val->numel() == nnz, "val size mismatch");
       vp = ptr<float>(*val);
     }
+    HostTimer ht(timing_.get());
     c10::DeviceGuard g(keys.device());
     const hipStream_t S = cur_stream(keys);
     auto i32 = keys.options().dtype(torch::kInt32);
@@ -2332,45 +2403,61 @@ class LinearStep {
         c10::hip::HIPCachingAllocator::recordStream(x->storage().data_ptr(), cs);
       if (vp) c10::hip::HIPCachingAllocator::recordStream(val->storage().data_ptr(), cs);
     }
+    ht.mark(0);
     // store guard: the previous step's summary (long complete), then room
     // for every id of this minibatch to be new
     if (train) guard_before(nnz);
     if (!grad_.defined() || grad_.numel() < store_->cap())
       grad_ = torch::zeros({store_->cap()}, keys.options().dtype(torch::kFloat32));
-    if (!ucount_.defined()) ucount_ = torch::empty({1}, i32);
-    WH_HIP_CHECK_HOST(hipMemsetAsync(ucount_.data_ptr(), 0, 4, S));
-    auto lid = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
-    auto ulist = torch::empty({std::max<int64_t>(nnz, 1)}, i32);
+    // two list counters by step parity: this step's is zero (the previous
+    // direct step's touch cleared it), the other one is cleared by this touch
+    if (!ucount_.defined()) ucount_ = torch::zeros({2}, i32);
+    if (nrows > 0) par_ ^= 1;  // (an empty minibatch launches nothing)
+    unsigned int* ucnt = reinterpret_cast<unsigned int*>(ucount_.data_ptr()) + par_;
+    unsigned int* unext = reinterpret_cast<unsigned int*>(ucount_.data_ptr()) + (par_ ^ 1);
+    ht.mark(1);
+    // one int32 block (slot per non-zero | slot list) and one float block
+    // (py | dual): two allocations instead of four
+    const int64_t nz1 = std::max<int64_t>(nnz, 1);
+    auto iws = torch::empty({2 * nz1}, i32);
+    int32_t* lid = ptr<int32_t>(iws);
+    int32_t* ulist = lid + nz1;
+    auto fws = torch::empty({2 * std::max<int64_t>(nrows, 1)}, keys.options().dtype(torch::kFloat32));
+    auto py = fws.narrow(0, 0, nrows);
+    float* dual = ptr<float>(fws) + std::max<int64_t>(nrows, 1);
+    auto part = torch::empty({wh::fm_fwd_partials()}, met.options());
+    ht.mark(2);
     const int R = wh::ld_rows_per_tile(nnz, nrows);
     ++stamp_;
     if (stamp_ == 0) stamp_ = 1;
     wh::KVTable t = store_->table();
     wh::ld_touch(t, reinterpret_cast<const uint64_t*>(keys.data_ptr()), ptr<int64_t>(offset),
-                 nrows, nnz, R, stamp_, train ? 1 : 0, ptr<int32_t>(lid), ptr<int32_t>(ulist),
-                 reinterpret_cast<unsigned int*>(ucount_.data_ptr()), S);
+                 nrows, nnz, R, stamp_, train ? 1 : 0, lid, ulist, ucnt, unext, S);
+    ht.mark(3);
     if (train) guard_after(S, nnz);
-    auto f32 = keys.options().dtype(torch::kFloat32);
-    auto py = torch::empty({nrows}, f32);
-    auto dual = torch::empty({nrows}, f32);
-    auto part = torch::empty({wh::fm_fwd_partials()}, met.options());
+    ht.mark(4);
     const int lossf = (int)loss_ | (met.numel() >= 5 ? 256 : 0);
-    wh::lin_forward_strided(nrows, ptr<int64_t>(offset), ptr<int32_t>(lid), vp,
+    wh::lin_forward_strided(nrows, ptr<int64_t>(offset), lid, vp,
                             reinterpret_cast<const float*>(t.sl) + 2, 8, ptr<float>(label), lossf,
-                            ptr<float>(py), ptr<float>(dual), ptr<double>(met), ptr<double>(part),
+                            ptr<float>(fws), dual, ptr<double>(met), ptr<double>(part),
                             ptr<unsigned int>(dev_ws(keys.device()).fwd_ticket), S);
-    auc_acc_side(py, label, auc_sum);
+    ht.mark(5);
     if (train && nnz > 0) {
-      wh::ld_backward(ptr<int32_t>(lid), vp, ptr<int64_t>(offset), nrows, nnz, R, ptr<float>(dual),
-                      ptr<float>(grad_), S);
+      wh::ld_backward(lid, vp, ptr<int64_t>(offset), nrows, nnz, R, dual, ptr<float>(grad_), S);
       ++pushes_;
       wh::LinearHP hp{(int)algo_, (float)alpha_, (float)beta_, (float)l1_, (float)l2_,
                       (float)((beta_ + std::sqrt((double)pushes_)) / alpha_)};
-      wh::ld_push(t, ptr<int32_t>(ulist), reinterpret_cast<unsigned int*>(ucount_.data_ptr()),
-                  std::min<int64_t>(nnz, store_->cap()), ptr<float>(grad_), hp, S);
+      wh::ld_push(t, ulist, ucnt, std::min<int64_t>(nnz, store_->cap()), ptr<float>(grad_), hp, S);
     }
+    ht.mark(6);
+    // the AUC side stream is enqueued last: its host work (event, stream
+    // switch) no longer sits between the forward and backward launches
+    auc_acc_side(py, label, auc_sum);
+    ht.mark(7);
     // the next minibatch (produced on another stream) is read by S after
     // this step's work: order S after its producer now
     if (ready) WH_HIP_CHECK_HOST(hipStreamWaitEvent(S, reinterpret_cast<hipEvent_t>(ready), 0));
+    ht.mark(8);
     return py;
   }
 
@@ -2469,7 +2556,7 @@ class LinearStep {
   // deciding to grow (nothing in flight references old slots: a grow is
   // stream-ordered before this step's inserts)
   void guard_read(Summ& m) {
-    const int64_t* h = m.h.data_ptr<int64_t>();
+    const volatile int64_t* h = m.h;
     m.pending = false;
     TORCH_CHECK(h[1] == 0, "parameter store shard lost data: ", h[1], " failed inserts (table ",
                 h[0], "/", store_->cap(), " keys)");
@@ -2500,23 +2587,43 @@ class LinearStep {
       }
     }
   }
-  void guard_after(hipStream_t S, int64_t n_new) {
+  // A summary (a kernel and a 32-byte read-back on the compute stream) every
+  // kGuardEvery steps, or every step once the bound nears the load limit:
+  // between summaries the bound grows by the inserts issued, so a late
+  // summary only makes the grow decision more conservative, and a failed
+  // insert still stops training within kGuardEvery steps (and at the flush).
+  static constexpr int kGuardEvery = 8;
+  void guard_after(hipStream_t S, int64_t n_new, bool force = false) {
     issued_ += n_new;
+    const double lim = max_load_ * (double)store_->cap();
+    if (!force && ++guard_step_ % kGuardEvery != 0 &&
+        keys_bound() + (double)n_new * kGuardEvery < 0.9 * lim)
+      return;
     Summ& m = sum_[sum_i_];
     sum_i_ = (sum_i_ + 1) % kSumm;
     if (m.pending) {  // (the GPU is kSumm steps behind: wait for the oldest)
       WH_HIP_CHECK_HOST(hipEventSynchronize(m.ev));
       guard_read(m);
     }
-    if (!m.h.defined()) {
-      m.h = torch::zeros({4}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
+    if (!m.h) {
+      void* p = nullptr;
+      WH_HIP_CHECK_HOST(hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent));
+      m.h = static_cast<int64_t*>(p);
+      std::memset(p, 0, 64);
       WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&m.ev, hipEventDisableTiming));
     }
-    Tensor sm = store_->summary();
-    WH_HIP_CHECK_HOST(hipMemcpyAsync(m.h.data_ptr(), sm.data_ptr(), 32, hipMemcpyDeviceToHost, S));
+    wh::kv_summary(store_->table(), m.h, S);
     WH_HIP_CHECK_HOST(hipEventRecord(m.ev, S));
     m.issued = issued_;
     m.pending = true;
+  }
+
+  // a summary now, waited for: raises on a failed insert (end of a pass,
+  // before the model is read)
+  void guard_sync() {
+    c10::DeviceGuard g(store_->slots_.device());
+    guard_after(c10::hip::getCurrentHIPStream(dev_).stream(), 0, true);
+    guard_poll(true);
   }
 
   int64_t grows() const { return grows_; }
@@ -2550,6 +2657,9 @@ class LinearStep {
   bool direct_ = true;
   Tensor grad_, ucount_;  // direct step: per-slot gradient sums (all zero between steps)
   uint32_t stamp_ = 0;
+  int par_ = 0;  // direct step parity (selects the list counter)
+  std::unique_ptr<HostSplit> timing_{host_split("linear direct step")};
+  int64_t guard_step_ = 0;
   std::unique_ptr<LocalizeJob> job_;
   Tensor job_keys_;
   Summ sum_[kSumm];
@@ -2582,6 +2692,7 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("next_keys") = py::none(), py::arg("next_offset") = py::none(),
            py::arg("next_val") = py::none(), py::arg("ready") = 0)
       .def("reset", &LinearStep::reset)
+      .def("guard_sync", &LinearStep::guard_sync)
       .def_property_readonly("grows", &LinearStep::grows)
       .def_property_readonly("direct", [](const LinearStep& l) { return l.direct(); })
       .def_property("pushes", &LinearStep::pushes, &LinearStep::set_pushes);
@@ -2664,6 +2775,8 @@ PYBIND11_MODULE(_hip, m) {
       .def("grow", &KVStore::grow)
       .def("grow_v", &KVStore::grow_v)
       .def("summary", &KVStore::summary)
+      .def("summary_async", &KVStore::summary_async)
+      .def("summary_read", &KVStore::summary_read)
       .def_property_readonly("dim", &KVStore::dim)
       .def_property_readonly("vstride", &KVStore::vstride)
       .def_property_readonly("cap", &KVStore::cap)

@@ -64,13 +64,16 @@ template <int T>
 __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
     KVTable t, const uint64_t* __restrict__ keys, const int64_t* __restrict__ off, int64_t nrows,
     int R, uint32_t stamp, int insert, int32_t* __restrict__ lid, int32_t* __restrict__ ulist,
-    unsigned int* __restrict__ ucount) {
+    unsigned int* __restrict__ ucount, unsigned int* __restrict__ unext) {
   __shared__ unsigned long long lk[T];
   __shared__ int32_t lslot[T];
   __shared__ int32_t lst[T];     // occupied entries, in insertion order
   __shared__ int32_t lfirst[T];  // slots this tile stamped first
   __shared__ unsigned int nlist, nfirst, fbase;
   const int64_t r0 = (int64_t)blockIdx.x * R;
+  // the other step parity's list counter: its push has run (stream order),
+  // so it is zeroed here for the next step instead of by a memset launch
+  if (blockIdx.x == 0 && threadIdx.x == 0) *unext = 0u;
   if (r0 >= nrows) return;
   const int64_t r1 = r0 + R < nrows ? r0 + R : nrows;
   const int64_t j0 = off[r0], j1 = off[r1];
@@ -246,12 +249,12 @@ int ld_rows_per_tile(int64_t nnz, int64_t nrows) {
 
 void ld_touch(const KVTable& t, const uint64_t* keys, const int64_t* off, int64_t nrows,
               int64_t nnz, int R, uint32_t stamp, int insert, int32_t* lid, int32_t* ulist,
-              unsigned int* ucount, hipStream_t s) {
+              unsigned int* ucount, unsigned int* unext, hipStream_t s) {
   if (nrows <= 0) return;
   const int64_t nb = (nrows + R - 1) / R;
   auto kern = ld_table(nnz) == 1024 ? k_ld_touch<1024> : k_ld_touch<4096>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(kLdThreads), 0, s, t, keys, off, nrows, R,
-                     stamp, insert, lid, ulist, ucount);
+                     stamp, insert, lid, ulist, ucount, unext);
 }
 
 void ld_backward(const int32_t* lid, const float* val, const int64_t* off, int64_t nrows,

@@ -5,6 +5,7 @@
 
 #include "wh_common.h"
 #include "wh_kernels.h"
+#include "wh_lookback.h"
 
 #include <algorithm>
 
@@ -267,22 +268,26 @@ __global__ __launch_bounds__(kThreads) void k_auc_count(const unsigned long long
 // same rank-sum by direct pair counting in ONE launch. Block (x, y) holds the
 // positives of row chunk y in LDS (compacted, as keys) and each thread counts,
 // for kAsJ negatives of tile x, the positives with a smaller key -- the
-// identical integer as the bucketed path. n^2 / 2 compares at n = 10000 are
-// a few microseconds spread over ~200 workgroups; the five bucketed launches
-// were ~40 us of mostly launch and single-workgroup scan latency.
+// identical integer as the bucketed path. Each block stores its count to its
+// own word (no same-address atomics besides the arrival ticket) and the last
+// block to arrive sums them. n^2 / 2 compares at n = 10000 spread over ~400
+// workgroups; the five bucketed launches were ~40 us of mostly launch and
+// single-workgroup scan latency.
 constexpr int64_t kAucSmallMax = 24576;
 constexpr int kAsThreads = 256;
 constexpr int kAsJ = 2;
 constexpr int kAsTileJ = kAsThreads * kAsJ;
-constexpr int kAsTileI = 1024;
+constexpr int kAsTileI = 512;
+constexpr int kAsMaxX = (int)((kAucSmallMax + kAsTileJ - 1) / kAsTileJ);
+constexpr int kAsMaxY = (int)((kAucSmallMax + kAsTileI - 1) / kAsTileI);
+constexpr int kAsUnroll = 8;  // LDS keys per batch of loads in flight
 
 __global__ __launch_bounds__(kAsThreads) void k_auc_small(const float* __restrict__ py,
                                                           const float* __restrict__ lab,
-                                                          int64_t n, unsigned long long* area,
+                                                          int64_t n, unsigned long long* part,
                                                           unsigned int* ticket,
-                                                          unsigned long long* ptot,
                                                           double* auc_sum) {
-  __shared__ unsigned long long pk[kAsTileI];
+  __shared__ __attribute__((aligned(16))) unsigned long long pk[kAsTileI + kAsUnroll];
   __shared__ int wcnt[kAsThreads / 64];
   __shared__ unsigned long long wsum[kAsThreads / 64];
   __shared__ int last;
@@ -306,17 +311,25 @@ __global__ __launch_bounds__(kAsThreads) void k_auc_small(const float* __restric
     np += tot;
     __syncthreads();
   }
+  // pad to whole batches with keys no negative exceeds
+  if (tid < kAsUnroll) pk[np + tid] = ~0ull;
   unsigned long long kj[kAsJ];
 #pragma unroll
   for (int u = 0; u < kAsJ; ++u) {
     const int64_t j = (int64_t)blockIdx.x * kAsTileJ + u * kAsThreads + tid;
     kj[u] = (j < n && !(lab[j] > 0.f)) ? auc_key(py[j], j, false) : 0ull;  // 0: counts nothing
   }
+  __syncthreads();
   uint32_t c[kAsJ] = {};
-  for (int p = 0; p < np; ++p) {
-    const unsigned long long k = pk[p];
+  const ulonglong2* pk2 = reinterpret_cast<const ulonglong2*>(pk);
+  for (int p = 0; p < np; p += kAsUnroll) {
+    ulonglong2 k[kAsUnroll / 2];
 #pragma unroll
-    for (int u = 0; u < kAsJ; ++u) c[u] += k < kj[u] ? 1u : 0u;
+    for (int q = 0; q < kAsUnroll / 2; ++q) k[q] = pk2[p / 2 + q];
+#pragma unroll
+    for (int q = 0; q < kAsUnroll / 2; ++q)
+#pragma unroll
+      for (int u = 0; u < kAsJ; ++u) c[u] += (k[q].x < kj[u] ? 1u : 0u) + (k[q].y < kj[u] ? 1u : 0u);
   }
   unsigned long long a = 0;
 #pragma unroll
@@ -324,25 +337,45 @@ __global__ __launch_bounds__(kAsThreads) void k_auc_small(const float* __restric
   a = (unsigned long long)wave_sum_ll((long long)a);
   if (lane == 0) wsum[wid] = a;
   __syncthreads();
+  const int nblk = (int)(gridDim.x * gridDim.y);
   if (tid == 0) {
     unsigned long long t = 0;
 #pragma unroll
     for (int w = 0; w < kAsThreads / 64; ++w) t += wsum[w];
-    if (t) atomicAdd(area, t);
-    if (blockIdx.x == 0 && np) atomicAdd(ptot, (unsigned long long)np);
-    // the adds must be performed before this block's ticket add
+    // part[block] = this block's count; part[kAsMaxX * kAsMaxY + y] = the
+    // positives of chunk y (from the x = 0 blocks); stores drained before
+    // the ticket add, read back by the last block with agent-scope loads
+    lb_store(part + blockIdx.y * gridDim.x + blockIdx.x, t);
+    if (blockIdx.x == 0) lb_store(part + kAsMaxX * kAsMaxY + blockIdx.y, (unsigned long long)np);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned tk = atomicAdd(ticket, 1u);
-    last = tk == gridDim.x * gridDim.y - 1;
+    last = tk == (unsigned)nblk - 1;
   }
   __syncthreads();
-  if (!last || tid != 0) return;
+  if (!last) return;
+  unsigned long long tot = 0, tp = 0;
+  for (int b = tid; b < nblk; b += kAsThreads) tot += lb_load(part + b);
+  for (int y = tid; y < (int)gridDim.y; y += kAsThreads) tp += lb_load(part + kAsMaxX * kAsMaxY + y);
+  tot = (unsigned long long)wave_sum_ll((long long)tot);
+  tp = (unsigned long long)wave_sum_ll((long long)tp);
+  __syncthreads();
+  if (lane == 0) {
+    wsum[wid] = tot;
+    wcnt[wid] = (int)tp;
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  unsigned long long at = 0, pt = 0;
+#pragma unroll
+  for (int w = 0; w < kAsThreads / 64; ++w) {
+    at += wsum[w];
+    pt += (unsigned long long)wcnt[w];
+  }
   __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const double tot = (double)atomicExch(area, 0ull);
-  const double tp = (double)atomicExch(ptot, 0ull);
+  const double area = (double)at, npos = (double)pt;
   double auc = 1.0;
-  if (tp != 0 && tp != (double)n) {
-    const double r = tot / (tp * ((double)n - tp));
+  if (npos != 0 && npos != (double)n) {
+    const double r = area / (npos * ((double)n - npos));
     auc = r < 0.5 ? 1 - r : r;
   }
   auc_sum[0] += auc;
@@ -390,14 +423,17 @@ void auc_from_sorted(const float* label_sorted, int64_t n, double* out, int64_t*
 namespace wh {
 
 // persistent (zeroed once; lohi[0] = ~0): cnt, pcnt [NB] u32, lohi [2] u64,
-// area u64, ticket u32 (+pad), positives u64 (pair path).  scratch: off,
+// area u64, ticket u32 (+pad), pair-path partials u64 [kAsMaxX kAsMaxY +
+// kAsMaxY] (every word written before it is read).  scratch: off,
 // poff [NB + 1] u32, {lo, width}, per-example (bucket, rank) and the
 // bucket-ordered keys (none for the pair path).
 int64_t auc_ws_bytes(int64_t n) {
   if (n <= kAucSmallMax) return 0;
   return 2 * ((int64_t)kAucBuckets + 4) * 4 + 16 + 2 * 8 + 8 * n + 8 * n + 64;
 }
-int64_t auc_ws_persistent_bytes() { return 2 * (int64_t)kAucBuckets * 4 + 5 * 8; }
+int64_t auc_ws_persistent_bytes() {
+  return 2 * (int64_t)kAucBuckets * 4 + 4 * 8 + (int64_t)(kAsMaxX * kAsMaxY + kAsMaxY) * 8;
+}
 int64_t auc_ws_lohi_offset() { return 2 * (int64_t)kAucBuckets * 4; }
 
 void auc_accumulate(const float* py, const float* label, int64_t n, void* persist, void* scratch,
@@ -412,8 +448,8 @@ void auc_accumulate(const float* py, const float* label, int64_t n, void* persis
   if (n <= kAucSmallMax) {
     const dim3 grid((unsigned)((n + kAsTileJ - 1) / kAsTileJ),
                     (unsigned)((n + kAsTileI - 1) / kAsTileI));
-    hipLaunchKernelGGL(k_auc_small, grid, dim3(kAsThreads), 0, s, py, label, n, area, ticket,
-                       lohi + 4, auc_sum);
+    hipLaunchKernelGGL(k_auc_small, grid, dim3(kAsThreads), 0, s, py, label, n, lohi + 4, ticket,
+                       auc_sum);
     return;
   }
   char* sc = static_cast<char*>(scratch);

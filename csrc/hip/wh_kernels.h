@@ -290,10 +290,11 @@ void lin_forward_strided(int64_t nrows, const int64_t* offset, const int32_t* li
 // single-shard linear step without a localize (see the file header)
 int ld_rows_per_tile(int64_t nnz, int64_t nrows);
 // (nnz picks the tile table size: pass the same value to ld_rows_per_tile,
-// ld_touch and ld_backward)
+// ld_touch and ld_backward; ucount must be zero on entry and unext -- the
+// other step parity's counter, whose push has been enqueued -- is zeroed)
 void ld_touch(const KVTable& t, const uint64_t* keys, const int64_t* off, int64_t nrows,
               int64_t nnz, int R, uint32_t stamp, int insert, int32_t* lid, int32_t* ulist,
-              unsigned int* ucount, hipStream_t s);
+              unsigned int* ucount, unsigned int* unext, hipStream_t s);
 void ld_backward(const int32_t* lid, const float* val, const int64_t* off, int64_t nrows,
                  int64_t nnz, int R, const float* dual, float* grad, hipStream_t s);
 void ld_push(const KVTable& t, const int32_t* ulist, const unsigned int* ucount, int64_t cap_list,

@@ -62,16 +62,16 @@ class StoreGuard:
 
     def after_open(self):
         if self.cuda:
-            if getattr(self, "_pin", None) is None:  # two alternating pinned slots
-                self._pin = [torch.empty(4, dtype=torch.int64, pin_memory=True) for _ in range(2)]
+            if getattr(self, "_ev", None) is None:  # two alternating host slots
                 self._ev = [torch.cuda.Event() for _ in range(2)]
                 self._k = 0
                 self._side = torch.cuda.Stream()
             k = self._k = self._k ^ 1
-            h, ev = self._pin[k], self._ev[k]
-            # the summary (a one-wave read of the table's counters) and its
-            # copy run on a side stream behind the open, off the compute
-            # stream's critical path; read() waits for them one open later
+            ev = self._ev[k]
+            # the summary (a one-wave read of the table's counters, written
+            # straight into host memory) runs on a side stream behind the
+            # open, off the compute stream's critical path; read() waits for
+            # it one open later
             side = self._side
             if self._ring is None:
                 self._ring = streams.EventRing(4)
@@ -81,10 +81,9 @@ class StoreGuard:
             self._main = main
             self._ring.wait(side, main)
             with streams.on(side):
-                s = self.store.summary()
-                h.copy_(s, non_blocking=True)
+                self.store.summary_async(k)
                 ev.record(side)
-            self.pend = (h, ev)
+            self.pend = (k, ev)
         else:
             self.pend = (self.store.summary(), None)
         self.since = 0
@@ -97,7 +96,9 @@ class StoreGuard:
         self.pend = None
         if ev is not None:
             ev.synchronize()
-        keys, fail, vover, vused = [int(x) for x in h.tolist()]
+            keys, fail, vover, vused = self.store.summary_read(h)
+        else:
+            keys, fail, vover, vused = [int(x) for x in h.tolist()]
         self.keys, self.vused = keys, vused
         if fail or vover:
             raise StoreError(

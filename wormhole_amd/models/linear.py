@@ -127,6 +127,7 @@ class LinearLearner:
             self.psx.flush()
         if self._native is not None:
             self._native.reset()  # (a localize begun for a minibatch never trained)
+            self._native.guard_sync()  # a failed insert raises here at the latest
             self.kv.guard.grows = self._native.grows
         self.kv.flush()
 

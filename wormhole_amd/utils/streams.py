@@ -13,7 +13,10 @@ _set = torch._C._cuda_setStream
 
 
 def current_id(device_index):
-    """Id of the current stream of a device (compare with ``Stream.stream_id``)."""
+    """Id of the current stream of a device (compare with ``Stream.stream_id``);
+    ``None``: the current device."""
+    if device_index is None:
+        device_index = torch.cuda.current_device()
     return _get(device_index)[0]
 
 
