@@ -167,7 +167,7 @@ def test_killed_worker_job_resumes(work, app, conf):
     a no-fault run ends."""
     args = ["-n", "2", "-s", "2", os.path.join(ROOT, "bin", app + ".dmlc"), conf,
             "minibatch=100", "save_iter=1", "max_data_pass=3", "model_out=./m"]
-    r = run(["--max-restart", "1"] + args, work, env_extra={"WH_FAULT": "kill:1:45"},
+    r = run(["--max-restart", "1"] + args, work, env_extra={"WH_FAULT": "kill:1:60"},
             timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "WH_FAULT: killing" in r.stderr and "restarting the job" in r.stderr

@@ -179,6 +179,8 @@ def auc_acc(py, label, auc_sum):
     layer (it waits for the current stream first), overlapped with the
     backward pass that follows on the compute stream; :func:`auc_join` makes
     the current stream wait for it before ``auc_sum`` is read or reset."""
+    if py.numel() == 0:  # an empty step of a lockstep rank: no minibatch, no AUC term
+        return auc_sum
     if _gpu(py):
         _native.hip().auc_acc_side(py, label, auc_sum)
         return auc_sum
