@@ -90,7 +90,8 @@ def test_device_criteo_parse_matches_host_parser(tmp_path):
 @pytest.mark.gpu
 def test_ps_worker_device_parse_trains_like_host_parse(tmp_path):
     """The same linear job on Criteo text with the device parser and with the
-    host parser learns the same model (same keys, same row order)."""
+    host parser learns the same model (same keys, same row order: one device
+    reader per part, WH_TEXT_READERS=1, reads in the host parser's order)."""
     import subprocess
     import sys
     import numpy as np
@@ -103,7 +104,7 @@ def test_ps_worker_device_parse_trains_like_host_parse(tmp_path):
         conf.write_text('train_data = "%s"\ndata_format = "criteo"\nmax_data_pass = 1\n'
                         'minibatch = 1000\nrand_shuffle = 0\nmodel_out = "%s/m%s"\n'
                         % (p, tmp_path, dp))
-        env = dict(os.environ, WH_DEVICE_PARSE=dp)
+        env = dict(os.environ, WH_DEVICE_PARSE=dp, WH_TEXT_READERS="1")
         r = subprocess.run([sys.executable, os.path.join(root, "tracker", "dmlc_local.py"), "-n",
                             "1", "-s", "1", os.path.join(root, "bin", "linear.dmlc"), str(conf)],
                            capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
@@ -185,6 +186,19 @@ def test_device_shuffle_buffer_is_a_permutation_and_neg_sampling_drops_negatives
                  for i in range(lab.numel())]
     assert sorted(rows) == sorted(rows_h) and rows != rows_h
     assert sizes[:-1] == [300] * (len(sizes) - 1)
+    # no shuffle buffer: the part's sub-range readers, round-robin; every
+    # row once, each reader's rows in file order
+    it = DeviceTextIter(host, str(p), 0, 1, "criteo", 300, 0, 1.0, 7, dev)
+    rows = []
+    while True:
+        b = it.next()
+        if b is None:
+            break
+        keys, off, val, lab = [x.cpu() if x is not None else None for x in b.to_main(dev)]
+        rows += [tuple(keys[off[i]:off[i + 1]].tolist()) + (float(lab[i]),)
+                 for i in range(lab.numel())]
+    assert sorted(rows) == sorted(rows_h)
+    assert rows[:300] == rows_h[:300]  # the first batch: sub-range 0's first lines
     # a part shorter than a minibatch: one partial batch, then None, repeatedly
     it = DeviceTextIter(host, str(p), 3, 20, "criteo", 1000, 4000, 1.0, 7, dev)
     b = it.next()
