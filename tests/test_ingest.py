@@ -90,8 +90,9 @@ def test_device_criteo_parse_matches_host_parser(tmp_path):
 @pytest.mark.gpu
 def test_ps_worker_device_parse_trains_like_host_parse(tmp_path):
     """The same linear job on Criteo text with the device parser and with the
-    host parser learns the same model (same keys, same row order: one device
-    reader per part, WH_TEXT_READERS=1, reads in the host parser's order)."""
+    host parser learns the same model (same keys, same row order: without a
+    shuffle buffer the device path reads each part with ONE reader, in the
+    host parser's order, whatever WH_TEXT_READERS says)."""
     import subprocess
     import sys
     import numpy as np
@@ -104,7 +105,7 @@ def test_ps_worker_device_parse_trains_like_host_parse(tmp_path):
         conf.write_text('train_data = "%s"\ndata_format = "criteo"\nmax_data_pass = 1\n'
                         'minibatch = 1000\nrand_shuffle = 0\nmodel_out = "%s/m%s"\n'
                         % (p, tmp_path, dp))
-        env = dict(os.environ, WH_DEVICE_PARSE=dp, WH_TEXT_READERS="1")
+        env = dict(os.environ, WH_DEVICE_PARSE=dp, WH_TEXT_READERS="4")
         r = subprocess.run([sys.executable, os.path.join(root, "tracker", "dmlc_local.py"), "-n",
                             "1", "-s", "1", os.path.join(root, "bin", "linear.dmlc"), str(conf)],
                            capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))

@@ -137,8 +137,13 @@ class DeviceTextIter:
         else:
             # several readers over line-aligned sub-ranges of the part, taken
             # round-robin in a fixed order (one reader thread copies ~7 GB/s
-            # of page cache into pinned buffers: ~22 M Criteo rows/s)
-            nsub = max(1, int(os.environ.get("WH_TEXT_READERS", "4")))
+            # of page cache into pinned buffers: ~22 M Criteo rows/s). Only
+            # behind a shuffle buffer: without one, the reference trains on
+            # the part's rows in file order, mb rows per minibatch
+            # (learn/base/minibatch_iter.h:75-121), and interleaved
+            # sub-ranges would reorder them and cut a short minibatch at
+            # every sub-range end.
+            nsub = max(1, int(os.environ.get("WH_TEXT_READERS", "4"))) if self.shuffled else 1
             self.tbs = [host.TextBatches(path, part * nsub + j, nparts * nsub, mb, True)
                         for j in range(nsub)]
             self.tb_i = 0
