@@ -678,7 +678,7 @@ class KVStore {
   std::vector<Tensor> difacto_open_pull(const Tensor& keys, bool insert,
                                         const c10::optional<Tensor>& cnt,
                                         const std::vector<double>& h, int64_t threshold,
-                                        bool l1_shrk, int64_t seed) {
+                                        bool l1_shrk, int64_t seed, bool direct) {
     CHECK_IN(keys, torch::kInt64);
     const int32_t* cp = nullptr;
     if (cnt.has_value() && cnt->defined()) {
@@ -693,7 +693,11 @@ class KVStore {
     auto slot = torch::empty({n}, keys.options().dtype(torch::kInt32));
     auto hdr = torch::empty({n, 2}, f32);
     auto vpos = torch::empty({n + 1}, keys.options());
-    auto vc = torch::empty({vstride_ > 0 ? n : 0, (int64_t)std::max(vstride_, 1)}, f32);
+    // direct: no pulled copy -- hdr's vidx column holds the table's V row and
+    // the "pulled rows" are the V slab itself (one shard: the forward and
+    // backward read the rows in place; the push writes them after both)
+    direct = direct && vstride_ > 0;
+    auto vc = direct ? V_ : torch::empty({vstride_ > 0 ? n : 0, (int64_t)std::max(vstride_, 1)}, f32);
     if (n == 0) {
       vpos.zero_();
       return {slot, hdr, vc, vpos};
@@ -701,7 +705,8 @@ class KVStore {
     if (!wh::difacto_open_pull(table(), reinterpret_cast<const uint64_t*>(keys.data_ptr()), n,
                                cp, dhp(h, threshold, l1_shrk, seed), insert ? 1 : 0,
                                lookback(keys.device()), ptr<int32_t>(slot), ptr<float>(hdr),
-                               ptr<int64_t>(vpos), ptr<float>(vc), s)) {
+                               ptr<int64_t>(vpos), direct ? nullptr : ptr<float>(vc), s)) {
+      // (too many keys for the one-launch path: the compact pull below)
       slot = find(keys, insert);
       if (cp) difacto_push_cnt(slot, *cnt, h, threshold, l1_shrk, seed);
       auto r = difacto_pull(slot, l1_shrk);
@@ -2767,7 +2772,9 @@ PYBIND11_MODULE(_hip, m) {
       .def("linear_push", &KVStore::linear_push)
       .def("difacto_push_cnt", &KVStore::difacto_push_cnt)
       .def("difacto_pull", &KVStore::difacto_pull)
-      .def("difacto_open_pull", &KVStore::difacto_open_pull)
+      .def("difacto_open_pull", &KVStore::difacto_open_pull, py::arg("keys"), py::arg("insert"),
+           py::arg("cnt"), py::arg("h"), py::arg("threshold"), py::arg("l1_shrk"), py::arg("seed"),
+           py::arg("direct") = false)
       .def("difacto_push", &KVStore::difacto_push)
       .def("ps_open", &KVStore::ps_open)
       .def("ps_push", &KVStore::ps_push)

@@ -306,6 +306,9 @@ __global__ __launch_bounds__(kThreads) void k_difacto_open_pull(
     if (hp.l1_shrk && w[r] == 0.f) row[r] = -1;  // (a fresh row has w != 0)
     f[0] += row[r] >= 0 ? 1u : 0u;
   }
+  // direct (vc == null): the header points at the table's own V rows; only
+  // the count of pulled rows is scanned (vpos[n])
+  const bool direct = vc == nullptr;
   lb_block_scan<1>(lb, tile, f, ex, tot, shs);
   int32_t vp[kPullPer];
   uint32_t run = ex[0];
@@ -313,8 +316,8 @@ __global__ __launch_bounds__(kThreads) void k_difacto_open_pull(
   for (int r = 0; r < kPullPer; ++r) {
     vp[r] = row[r] >= 0 ? (int32_t)run : -1;
     if (i0 + r < n) {
-      hdr[i0 + r] = make_float2(w[r], __int_as_float(vp[r]));
-      vpos[i0 + r] = run;
+      hdr[i0 + r] = make_float2(w[r], __int_as_float(direct ? row[r] : vp[r]));
+      if (!direct) vpos[i0 + r] = run;
     }
     run += row[r] >= 0 ? 1u : 0u;
   }
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_open_pull(
     int nj = 0;
 #pragma unroll
     for (int r = 0; r < kPullPer; ++r) {
-      const bool has = row[r] >= 0;
+      const bool has = row[r] >= 0 && (!direct || fresh[r]);  // direct: initialise only
       const uint64_t m = __ballot(has);
       if (has)
         jl[nj + __popcll(m & ((1ull << lane) - 1ull))] =
@@ -376,14 +379,14 @@ __global__ __launch_bounds__(kThreads) void k_difacto_open_pull(
           *reinterpret_cast<float4*>(t.VG + (int64_t)d.x * t.vstride + c) =
               make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        *reinterpret_cast<float4*>(vc + (int64_t)jp * t.vstride + c) = v[b];
+        if (!direct) *reinterpret_cast<float4*>(vc + (int64_t)jp * t.vstride + c) = v[b];
       }
     }
     return;
   }
 #pragma unroll
   for (int r = 0; r < kPullPer; ++r) {
-    for_each_row_job<G>(row[r] >= 0, [&](int src, int gl) {
+    for_each_row_job<G>(row[r] >= 0 && (!direct || fresh[r]), [&](int src, int gl) {
       const int s2 = src >= 0 ? src : lane;
       const int32_t jr = __shfl(row[r], s2, 64), jp = __shfl(vp[r], s2, 64);
       const int jf = __shfl((int)fresh[r], s2, 64);
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(kThreads) void k_difacto_open_pull(
           const float4 v = v_init4(hp, jk, c, t.dim);
           *reinterpret_cast<float4*>(V + c) = v;
           *reinterpret_cast<float4*>(VG + c) = make_float4(0.f, 0.f, 0.f, 0.f);
-          *reinterpret_cast<float4*>(o + c) = v;
+          if (!direct) *reinterpret_cast<float4*>(o + c) = v;
         }
       } else {
         for (int c = gl * 4; c < t.vstride; c += 4 * G)

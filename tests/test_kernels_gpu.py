@@ -498,6 +498,46 @@ def test_learner_pipelined_matches_plain(hip):
     assert abs(a[0] - b[0]) < 1e-4 * abs(b[0]) and abs(a[1] - b[1]) < 1e-6
 
 
+@pytest.mark.parametrize("l1_shrk", [False, True])
+def test_difacto_direct_pull_matches_copy(hip, l1_shrk):
+    """One shard: the FM kernels reading V in place in the slab (direct pull,
+    the default) train the same model as the pulled compact copy, through a
+    V-slab growth, with the next localize begun early; prediction agrees."""
+    from wormhole_amd.config.schema import DifactoConfig, Embedding
+    from wormhole_amd.data.synthetic import CRITEO_TB_CARD
+    from wormhole_amd.models.difacto import DifactoLearner
+    from wormhole_amd.parallel.comm import Comm
+    card = torch.tensor(CRITEO_TB_CARD, dtype=torch.int64, device=DEV)
+    data = [hip.synth_criteo(4000, 21, s, card) for s in range(8)]
+    out = []
+    for direct in (True, False):
+        emb = Embedding(dim=16, threshold=2)
+        conf = DifactoConfig(minibatch=4000, embedding=[emb], l1_shrk=l1_shrk, lambda_l1=0.01)
+        lr = DifactoLearner(conf, Comm(DEV, init=False), DEV, cap=1 << 20, vcap=1 << 10, seed=3)
+        assert lr.direct_pull
+        lr.direct_pull = direct
+        for s, (k, l, o) in enumerate(data):
+            nb = (data[s + 1][0], data[s + 1][2], None) if s + 1 < len(data) else None
+            lr.process(k, o, None, l, 0, 0, next_batch=nb)
+        lr.flush()
+        k, l, o = hip.synth_criteo(3000, 22, 0, card)
+        py = lr.process(k, o, None, l, 2, 0)
+        st = lr.store
+        occ = st.occupied().long()
+        rows = st.vrow[occ].long()
+        V = torch.where((rows >= 0)[:, None], st.V[rows.clamp_min(0)], torch.zeros_like(st.V[:1]))
+        keys = st.keys[occ]
+        order = torch.argsort(keys)  # (slot order depends on insert timing)
+        out.append((lr.take_progress(), keys[order].cpu(), st.w[occ][order].cpu(),
+                    V[order].cpu(), py.cpu(), lr.kv.guard.vgrows))
+    (pa, ka, wa, va, ya, ga), (pb, kb, wb, vb, yb, gb) = out
+    assert ga >= 1  # the 1024-row V slab had to grow
+    assert torch.equal(ka, kb)
+    assert torch.allclose(wa, wb, atol=1e-6) and torch.allclose(va, vb, atol=1e-6)
+    assert torch.allclose(ya, yb, atol=1e-5)
+    assert pa[4:] == pb[4:] and abs(pa[0] - pb[0]) < 1e-5 * abs(pb[0])
+
+
 def test_async_saver_snapshot(hip, tmp_path):
     """The background save writes the state at the save call: updates
     issued right after it (before the file is written) must not leak in, and

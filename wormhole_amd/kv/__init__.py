@@ -290,11 +290,16 @@ class ShardedKV:
                 self.store.difacto_push_cnt(sess.slots[a:b], c[a:b], hp, threshold, l1_shrk, seed)
 
     def difacto_open_pull(self, uniq, owner_cnt, insert, cnt, hp, threshold, l1_shrk, seed,
-                          recv=None):
+                          recv=None, direct=False):
         """open() + (pass 0) difacto_push_cnt() + difacto_pull() as one call.
         On one shard this is ONE fused device pass over the keys (find,
         count, lazy V allocation, variable-length pull); with peers it is the
-        exchange sequence of the three calls. Returns (sess, hdr, vc)."""
+        exchange sequence of the three calls. Returns (sess, hdr, vc).
+
+        direct (one shard, device store): no pulled copy of the V rows --
+        hdr's vidx column holds table rows and vc IS the store's V slab, so
+        the FM kernels read the rows in place (the gradient rows then follow
+        the slab numbering too; the push takes them that way)."""
         if self.comm.size > 1:
             sess = self.open(uniq, owner_cnt, insert, cnt=cnt, recv=recv)
             if cnt is not None:
@@ -309,7 +314,7 @@ class ShardedKV:
         if insert:
             self.guard.before_open(uniq.shape[0])
         slots, hdr, vc, vpos = self.store.difacto_open_pull(uniq, insert, cnt, hp, threshold,
-                                                            l1_shrk, seed)
+                                                            l1_shrk, seed, direct)
         if insert:
             self.guard.after_open()
         sess.slots = slots

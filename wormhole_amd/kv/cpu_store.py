@@ -247,8 +247,9 @@ class CpuKVStore:
                     and (not l1_shrk or self._w[s] != 0)):
                 self._alloc_v(s, seed, h[7])
 
-    def difacto_open_pull(self, keys, insert, cnt, h, threshold, l1_shrk, seed):
-        """find + (optional) count push + pull, like the HIP store's fused op."""
+    def difacto_open_pull(self, keys, insert, cnt, h, threshold, l1_shrk, seed, direct=False):
+        """find + (optional) count push + pull, like the HIP store's fused op
+        (always the compact pull: ``direct`` is a device-path layout)."""
         slot = self.find(keys, insert)
         if cnt is not None:
             self.difacto_push_cnt(slot, cnt, h, threshold, l1_shrk, seed)

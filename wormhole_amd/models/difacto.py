@@ -11,6 +11,8 @@ learn/difacto/async_sgd.h:363-425), re-expressed on the GPU:
   ->  gradient clip / dropout / normalisation  ->  push  ->  owner applies
   FTRL on w and AdaGrad on V in one fused kernel.
 """
+import os
+
 import torch
 
 from .. import ops
@@ -67,6 +69,14 @@ class DifactoLearner:
         # P > 1 ranks: the lean pipelined exchange (kv/psx.py), whatever the
         # number of server shards S <= P. (The ShardedKV exchange remains for
         # the lossy fixed_bytes payload filter and embedding-free models.)
+        # One shard on the GPU: the FM kernels read the V rows in place in the
+        # table's slab instead of a pulled copy (kv.difacto_open_pull direct)
+        # -- unless the embedding gradients are post-processed (clipping /
+        # dropout / normalisation walk the compact gradient rows).
+        post = emb is not None and (emb.grad_clipping > 0 or emb.dropout > 0
+                                    or bool(emb.grad_normalization))
+        self.direct_pull = (self.device.type == "cuda" and comm.size == 1 and self.vstride > 0
+                            and not post and os.environ.get("WH_DIFACTO_PULL", "") != "copy")
         self.psx = None
         if comm.size > 1 and self.vstride > 0 and not self.kv.fixed_bytes:
             from ..kv.psx import Psx
@@ -93,7 +103,8 @@ class DifactoLearner:
         with trace.span("pull"):
             sess, hdr, vc = self.kv.difacto_open_pull(
                 uniq, owner_cnt, train, ucnt if push_cnt else None, self.hp, self.threshold,
-                self.l1_shrk, self.seed, recv=loc[7] if len(loc) > 7 else None)
+                self.l1_shrk, self.seed, recv=loc[7] if len(loc) > 7 else None,
+                direct=self.direct_pull)
         self.last_sizes = (uniq.numel(), sess.m)  # (unique keys, embedding rows; device)
         # The next minibatch's localize begins right AFTER this pull's launch
         # (the host reaches the pull sooner after its count read; the job's
