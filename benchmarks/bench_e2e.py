@@ -146,7 +146,7 @@ def main():
     sec = (t_end or time.time()) - t_start
     print(out[-1500:], file=sys.stderr)
     for l in err.splitlines():  # the workers' per-pass stage summaries
-        if "minibatches" in l:
+        if "minibatches" in l or "[ingest]" in l:
             print(l, file=sys.stderr)
     print(json.dumps({
         "metric": "end-to-end examples/sec from %s files, %s.dmlc, %d worker(s)" % (

@@ -152,6 +152,7 @@ class DeviceTextIter:
             self.gen = torch.Generator(device=device)
             self.gen.manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
         self.stream = _producer_stream(device)
+        depth = int(os.environ.get("WH_TEXT_DEPTH", depth))
         self.q = queue.Queue(maxsize=max(1, depth))
         self.stop = False
         self.done = False
@@ -171,18 +172,33 @@ class DeviceTextIter:
         return False
 
     def _produce(self):
+        # WH_INGEST_TIMING=1: the producer's seconds waiting for the readers,
+        # working (copy / parse / shuffle), and blocked on a full queue
+        timing = os.environ.get("WH_INGEST_TIMING") == "1"
+        self.t_read = self.t_work = self.t_put = 0.0
         try:
+            import time
             torch.cuda.set_device(self.dev)
             with torch.cuda.stream(self.stream):
                 while not self.stop:
+                    t0 = time.perf_counter()
+                    self.t_read_blk = 0.0
                     item = self._block() if self.shuffled else self._minibatch()
+                    t1 = time.perf_counter()
                     if item is None:
                         break
                     if not self._put(item):
                         return
+                    self.t_read += self.t_read_blk
+                    self.t_work += t1 - t0 - self.t_read_blk
+                    self.t_put += time.perf_counter() - t1
         except BaseException as e:  # surfaced by the consumer
             self._put(e)
             return
+        if timing:
+            import sys
+            print("[ingest] part producer: read wait %.3f s, work %.3f s, queue full %.3f s"
+                  % (self.t_read, self.t_work, self.t_put), file=sys.stderr)
         self._put(None)
 
     def _csr_block(self, b):
@@ -196,6 +212,14 @@ class DeviceTextIter:
     def _text_next(self):
         """The next text batch from the sub-range readers, round-robin;
         None once all are exhausted."""
+        import time
+        t0 = time.perf_counter()
+        try:
+            return self._text_next_()
+        finally:
+            self.t_read_blk += time.perf_counter() - t0
+
+    def _text_next_(self):
         while self.tbs:
             i = self.tb_i % len(self.tbs)
             b = self.tbs[i].next()
