@@ -98,7 +98,7 @@ DevWs& dev_ws(const torch::Device& d) {
     w->lb = torch::zeros({wh::lookback_ws_words()}, o.dtype(torch::kInt64));
     w->auc = torch::zeros({wh::auc_ws_persistent_bytes() / 8}, o.dtype(torch::kInt64));
     w->auc.select(0, wh::auc_ws_lohi_offset() / 8).fill_(-1);
-    w->fwd_ticket = torch::zeros({4}, o.dtype(torch::kInt32));
+    w->fwd_ticket = torch::zeros({wh::fwd_ticket_words()}, o.dtype(torch::kInt32));
     w->lb_loc = torch::zeros({wh::lookback_ws_words()}, o.dtype(torch::kInt64));
     w->part_ws = torch::zeros({wh::kPartMaxDigits + 2}, o.dtype(torch::kInt64));
     w->heavy_ws = torch::zeros({2 * wh::kPartMaxHeavy + wh::kPartMaxOwners}, o.dtype(torch::kInt64));
@@ -2414,30 +2414,31 @@ class LinearStep {
     if (train) guard_before(nnz);
     if (!grad_.defined() || grad_.numel() < store_->cap())
       grad_ = torch::zeros({store_->cap()}, keys.options().dtype(torch::kFloat32));
-    // two list counters by step parity: this step's is zero (the previous
-    // direct step's touch cleared it), the other one is cleared by this touch
-    if (!ucount_.defined()) ucount_ = torch::zeros({2}, i32);
-    if (nrows > 0) par_ ^= 1;  // (an empty minibatch launches nothing)
-    unsigned int* ucnt = reinterpret_cast<unsigned int*>(ucount_.data_ptr()) + par_;
-    unsigned int* unext = reinterpret_cast<unsigned int*>(ucount_.data_ptr()) + (par_ ^ 1);
+    // the overflow list's counter: zero between steps (the push re-zeroes it)
+    if (!ovf_cnt_.defined()) ovf_cnt_ = torch::zeros({1}, i32);
     ht.mark(1);
-    // one int32 block (slot per non-zero | slot list) and one float block
-    // (py | dual): two allocations instead of four
+    // one int32 block (slot per non-zero | per-tile slot lists | overflow
+    // list | per-tile counts) and one float block (py | dual)
+    const int R = wh::ld_rows_per_tile(nnz, nrows);
+    const int T = wh::ld_tile_table(nnz);
     const int64_t nz1 = std::max<int64_t>(nnz, 1);
-    auto iws = torch::empty({2 * nz1}, i32);
+    const int64_t ntiles = nrows > 0 ? (nrows + R - 1) / R : 0;
+    auto iws = torch::empty({2 * nz1 + ntiles * (T + 1)}, i32);
     int32_t* lid = ptr<int32_t>(iws);
-    int32_t* ulist = lid + nz1;
+    int32_t* ovf = lid + nz1;
+    int32_t* tlist = ovf + nz1;
+    unsigned int* tcnt = reinterpret_cast<unsigned int*>(tlist + ntiles * T);
+    unsigned int* ovf_cnt = reinterpret_cast<unsigned int*>(ovf_cnt_.data_ptr());
     auto fws = torch::empty({2 * std::max<int64_t>(nrows, 1)}, keys.options().dtype(torch::kFloat32));
     auto py = fws.narrow(0, 0, nrows);
     float* dual = ptr<float>(fws) + std::max<int64_t>(nrows, 1);
     auto part = torch::empty({wh::fm_fwd_partials()}, met.options());
     ht.mark(2);
-    const int R = wh::ld_rows_per_tile(nnz, nrows);
     ++stamp_;
     if (stamp_ == 0) stamp_ = 1;
     wh::KVTable t = store_->table();
     wh::ld_touch(t, reinterpret_cast<const uint64_t*>(keys.data_ptr()), ptr<int64_t>(offset),
-                 nrows, nnz, R, stamp_, train ? 1 : 0, lid, ulist, ucnt, unext, S);
+                 nrows, nnz, R, stamp_, train ? 1 : 0, lid, tlist, tcnt, ovf, ovf_cnt, S);
     ht.mark(3);
     if (train) guard_after(S, nnz);
     ht.mark(4);
@@ -2452,7 +2453,7 @@ class LinearStep {
       ++pushes_;
       wh::LinearHP hp{(int)algo_, (float)alpha_, (float)beta_, (float)l1_, (float)l2_,
                       (float)((beta_ + std::sqrt((double)pushes_)) / alpha_)};
-      wh::ld_push(t, ulist, ucnt, std::min<int64_t>(nnz, store_->cap()), ptr<float>(grad_), hp, S);
+      wh::ld_push(t, ntiles, T, tlist, tcnt, ovf, ovf_cnt, ptr<float>(grad_), hp, S);
     }
     ht.mark(6);
     // the AUC side stream is enqueued last: its host work (event, stream
@@ -2660,9 +2661,10 @@ class LinearStep {
   hipEvent_t ev_s_ = nullptr, ev_ls_ = nullptr;
   bool s_job_ = false;
   bool direct_ = true;
-  Tensor grad_, ucount_;  // direct step: per-slot gradient sums (all zero between steps)
+  // direct step: per-slot gradient sums (all zero between steps), the
+  // overflow slot list's counter (zero between steps)
+  Tensor grad_, ovf_cnt_;
   uint32_t stamp_ = 0;
-  int par_ = 0;  // direct step parity (selects the list counter)
   std::unique_ptr<HostSplit> timing_{host_split("linear direct step")};
   int64_t guard_step_ = 0;
   std::unique_ptr<LocalizeJob> job_;

@@ -7,15 +7,15 @@
 //   k_ld_touch  per tile of rows: dedup the tile's ids in an LDS hash table,
 //               find-or-insert each distinct id in the HBM table once, stamp
 //               the slot with the step number (the first tile to stamp a
-//               slot appends it to the minibatch's slot list: one global
-//               atomic per tile), and write the slot of every non-zero
-//               (lid = slot).
+//               slot lists it in the tile's own part of the minibatch's slot
+//               list), and write the slot of every non-zero (lid = slot).
 //   (forward)   fm.hip k_lin_fwd reads w straight from the slots (stride 8).
 //   k_ld_bwd    per tile: g = x * dual[row] accumulated per distinct slot in
 //               LDS, then one float atomic per (tile, slot) into a dense
 //               per-slot gradient array -- hot ids cost one atomic per tile,
 //               not one per occurrence.
-//   k_ld_push   per listed slot: take (and clear) its summed gradient, apply
+//   k_ld_push   per listed slot (a block per tile's list): take (and clear)
+//               its summed gradient, apply
 //               SGD / AdaGrad / FTRL (reference learn/linear/async_sgd.h:
 //               71-180, penalty.h:36-41).
 //
@@ -28,6 +28,7 @@
 #include "wh_kernels.h"
 #include "kv_device.h"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace wh {
@@ -63,17 +64,14 @@ __device__ __forceinline__ uint32_t lhash(uint64_t k) { return (uint32_t)(mix64(
 template <int T>
 __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
     KVTable t, const uint64_t* __restrict__ keys, const int64_t* __restrict__ off, int64_t nrows,
-    int R, uint32_t stamp, int insert, int32_t* __restrict__ lid, int32_t* __restrict__ ulist,
-    unsigned int* __restrict__ ucount, unsigned int* __restrict__ unext) {
+    int R, uint32_t stamp, int insert, int32_t* __restrict__ lid, int32_t* __restrict__ tlist,
+    unsigned int* __restrict__ tcnt, int32_t* __restrict__ ovf, unsigned int* __restrict__ ovf_cnt) {
   __shared__ unsigned long long lk[T];
   __shared__ int32_t lslot[T];
   __shared__ int32_t lst[T];     // occupied entries, in insertion order
   __shared__ int32_t lfirst[T];  // slots this tile stamped first
-  __shared__ unsigned int nlist, nfirst, fbase;
+  __shared__ unsigned int nlist, nfirst;
   const int64_t r0 = (int64_t)blockIdx.x * R;
-  // the other step parity's list counter: its push has run (stream order),
-  // so it is zeroed here for the next step instead of by a memset launch
-  if (blockIdx.x == 0 && threadIdx.x == 0) *unext = 0u;
   if (r0 >= nrows) return;
   const int64_t r1 = r0 + R < nrows ? r0 + R : nrows;
   const int64_t j0 = off[r0], j1 = off[r1];
@@ -130,11 +128,12 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
       if (old[r] != stamp) lfirst[atomicAdd(&nfirst, 1u)] = sl[r];
   }
   __syncthreads();
-  // the tile's first-stamped slots join the minibatch's list with ONE global
-  // atomic per tile (a same-address atomic per wave serialised ~6k of them)
-  if (threadIdx.x == 0) fbase = nfirst ? atomicAdd(ucount, nfirst) : 0u;
-  __syncthreads();
-  for (unsigned int i = threadIdx.x; i < nfirst; i += kLdThreads) ulist[fbase + i] = lfirst[i];
+  // the tile's first-stamped slots are its part of the minibatch's slot list:
+  // stored in the tile's own range with its count (no shared counter: one
+  // same-address atomic per tile serialised ~770 of them, ~9 us at 10k rows)
+  for (unsigned int i = threadIdx.x; i < nfirst; i += kLdThreads)
+    tlist[(int64_t)blockIdx.x * T + i] = lfirst[i];
+  if (threadIdx.x == 0) tcnt[blockIdx.x] = nfirst;
   const long long ci = wave_sum_ll(created), cf = wave_sum_ll(failed);
   if ((threadIdx.x & 63) == 0) {
     if (ci) atomicAdd(stat_ptr(t.stats, 4), (unsigned long long)ci);
@@ -157,8 +156,8 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_touch(
         const uint64_t hh = mix64(k) & mask;
         s = probe_slot(t.sl, mask, k, hh, ld_relaxed(&t.sl[hh].key), insert, &cr);
         if (cr) atomicAdd(stat_ptr(t.stats, 4), 1ull);
-        if (s >= 0 && atomicExch(&t.sl[s].cnt, stamp) != stamp)
-          ulist[atomicAdd(ucount, 1u)] = s;
+        if (insert && s >= 0 && atomicExch(&t.sl[s].cnt, stamp) != stamp)
+          ovf[atomicAdd(ovf_cnt, 1u)] = s;  // (rare: a tile whose ids overflowed LDS)
       }
     }
     lid[j] = s;
@@ -215,27 +214,46 @@ __global__ __launch_bounds__(kLdThreads) void k_ld_bwd(
   }
 }
 
-__global__ __launch_bounds__(kLdThreads) void k_ld_push(KVTable t, const int32_t* __restrict__ ulist,
-                                                        const unsigned int* __restrict__ ucount,
-                                                        int64_t cap_list, float* __restrict__ grad,
-                                                        LinearHP hp) {
-  const int64_t i = (int64_t)blockIdx.x * kLdThreads + threadIdx.x;
-  const int64_t n = *ucount;
-  float oldw = 0.f, neww = 0.f;
-  if (i < n && i < cap_list) {
-    const int32_t s = ulist[i];
-    const float g = grad[s];
-    grad[s] = 0.f;  // the array is all-zero again after the push
-    oldw = t.sl[s].w;
-    neww = linear_update(t.sl[s], g, hp, hp.sgd_eta);
+// block b < ntiles: tile b's listed slots; block ntiles: the overflow list
+// (whose counter it re-zeroes for the next step, after reading it)
+__global__ __launch_bounds__(kLdThreads) void k_ld_push(KVTable t, const int32_t* __restrict__ tlist,
+                                                        const unsigned int* __restrict__ tcnt,
+                                                        int T, const int32_t* __restrict__ ovf,
+                                                        unsigned int* __restrict__ ovf_cnt,
+                                                        float* __restrict__ grad, LinearHP hp) {
+  const bool last = blockIdx.x == gridDim.x - 1;
+  const unsigned int n = last ? *ovf_cnt : tcnt[blockIdx.x];
+  const int32_t* list = last ? ovf : tlist + (int64_t)blockIdx.x * T;
+  for (unsigned int i0 = 0; i0 < n; i0 += kLdThreads) {  // (block-uniform trips)
+    const unsigned int i = i0 + threadIdx.x;
+    float oldw = 0.f, neww = 0.f;
+    if (i < n) {
+      const int32_t s = list[i];
+      const float g = grad[s];
+      grad[s] = 0.f;  // the array is all-zero again after the push
+      oldw = t.sl[s].w;
+      neww = linear_update(t.sl[s], g, hp, hp.sgd_eta);
+    }
+    count_nnz_delta(oldw, neww, t.stats);
   }
-  count_nnz_delta(oldw, neww, t.stats);
+  if (last) {
+    __syncthreads();
+    if (threadIdx.x == 0 && n) *ovf_cnt = 0u;
+  }
 }
 
 }  // namespace
 
 // the tile table for a minibatch of nnz non-zeros (see ld_rows_cap)
-static int ld_table(int64_t nnz) { return nnz <= (int64_t)1 << 21 ? 1024 : 4096; }
+static int ld_table(int64_t nnz) {
+  static int small = -1;  // WH_LD_TABLE: the small-minibatch tile table (512 / 1024)
+  if (small < 0) {
+    const char* e = std::getenv("WH_LD_TABLE");
+    const int v = e ? std::atoi(e) : 1024;
+    small = (v == 512 || v == 2048) ? v : 1024;
+  }
+  return nnz <= (int64_t)1 << 21 ? small : 4096;
+}
 
 int ld_rows_per_tile(int64_t nnz, int64_t nrows) {
   // ~T/2 non-zeros per tile, at most ld_rows_cap(T) rows (the tile's LDS
@@ -247,14 +265,18 @@ int ld_rows_per_tile(int64_t nnz, int64_t nrows) {
   return (int)(R < 1 ? 1 : (R > cap ? cap : R));
 }
 
+int ld_tile_table(int64_t nnz) { return ld_table(nnz); }
+
 void ld_touch(const KVTable& t, const uint64_t* keys, const int64_t* off, int64_t nrows,
-              int64_t nnz, int R, uint32_t stamp, int insert, int32_t* lid, int32_t* ulist,
-              unsigned int* ucount, unsigned int* unext, hipStream_t s) {
+              int64_t nnz, int R, uint32_t stamp, int insert, int32_t* lid, int32_t* tlist,
+              unsigned int* tcnt, int32_t* ovf, unsigned int* ovf_cnt, hipStream_t s) {
   if (nrows <= 0) return;
   const int64_t nb = (nrows + R - 1) / R;
-  auto kern = ld_table(nnz) == 1024 ? k_ld_touch<1024> : k_ld_touch<4096>;
+  const int T = ld_table(nnz);
+  auto kern = T == 512 ? k_ld_touch<512> : T == 1024 ? k_ld_touch<1024>
+             : T == 2048 ? k_ld_touch<2048> : k_ld_touch<4096>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(kLdThreads), 0, s, t, keys, off, nrows, R,
-                     stamp, insert, lid, ulist, ucount, unext);
+                     stamp, insert, lid, tlist, tcnt, ovf, ovf_cnt);
 }
 
 void ld_backward(const int32_t* lid, const float* val, const int64_t* off, int64_t nrows,
@@ -263,16 +285,18 @@ void ld_backward(const int32_t* lid, const float* val, const int64_t* off, int64
   const int T = ld_table(nnz);
   if (R > ld_rows_cap(T)) throw std::runtime_error("ld_backward: tile rows exceed the LDS bound");
   const int64_t nb = (nrows + R - 1) / R;
-  auto kern = T == 1024 ? k_ld_bwd<1024> : k_ld_bwd<4096>;
+  auto kern = T == 512 ? k_ld_bwd<512> : T == 1024 ? k_ld_bwd<1024>
+             : T == 2048 ? k_ld_bwd<2048> : k_ld_bwd<4096>;
   hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(kLdThreads), 0, s, lid, val, off, nrows, R,
                      dual, grad);
 }
 
-void ld_push(const KVTable& t, const int32_t* ulist, const unsigned int* ucount, int64_t cap_list,
-             float* grad, LinearHP hp, hipStream_t s) {
-  if (cap_list <= 0) return;
-  hipLaunchKernelGGL(k_ld_push, dim3(grid_for(cap_list, kLdThreads)), dim3(kLdThreads), 0, s, t,
-                     ulist, ucount, cap_list, grad, hp);
+void ld_push(const KVTable& t, int64_t ntiles, int T, const int32_t* tlist,
+             const unsigned int* tcnt, const int32_t* ovf, unsigned int* ovf_cnt, float* grad,
+             LinearHP hp, hipStream_t s) {
+  if (ntiles <= 0) return;
+  hipLaunchKernelGGL(k_ld_push, dim3((unsigned)(ntiles + 1)), dim3(kLdThreads), 0, s, t, tlist,
+                     tcnt, T, ovf, ovf_cnt, grad, hp);
 }
 
 }  // namespace wh

@@ -241,19 +241,33 @@ __global__ __launch_bounds__(kThreads) void k_auc_count(const unsigned long long
       }
     }
   }
+  // the block's count to its own word (a same-address atomic per wave
+  // serialised ~1.5k of them at 100k rows), drained before the arrival
+  __shared__ unsigned long long ws[kThreads / 64];
   a = wave_sum_ll((long long)a);
-  if ((threadIdx.x & 63) == 0 && a) atomicAdd(area, a);
-  // the area adds must be performed before this block's ticket add
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = a;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned t = atomicAdd(ticket, 1u);
-    last = t == gridDim.x - 1;
+    unsigned long long b = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) b += ws[w];
+    lb_store(area + blockIdx.x, b);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = arrive_last(ticket, blockIdx.x, gridDim.x);
   }
   __syncthreads();
-  if (!last || threadIdx.x != 0) return;
-  __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const double tot = (double)atomicExch(area, 0ull);
+  if (!last) return;
+  unsigned long long t = 0;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += kThreads) t += lb_load(area + b);
+  t = (unsigned long long)wave_sum_ll((long long)t);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  unsigned long long at = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) at += ws[w];
+  const double tot = (double)at;
   const double tp = (double)poff[kAucBuckets];
   double auc = 1.0;
   if (tp != 0 && tp != (double)n) {
@@ -348,8 +362,7 @@ __global__ __launch_bounds__(kAsThreads) void k_auc_small(const float* __restric
     lb_store(part + blockIdx.y * gridDim.x + blockIdx.x, t);
     if (blockIdx.x == 0) lb_store(part + kAsMaxX * kAsMaxY + blockIdx.y, (unsigned long long)np);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned tk = atomicAdd(ticket, 1u);
-    last = tk == (unsigned)nblk - 1;
+    last = arrive_last(ticket, blockIdx.y * gridDim.x + blockIdx.x, (unsigned)nblk);
   }
   __syncthreads();
   if (!last) return;
@@ -371,7 +384,6 @@ __global__ __launch_bounds__(kAsThreads) void k_auc_small(const float* __restric
     at += wsum[w];
     pt += (unsigned long long)wcnt[w];
   }
-  __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const double area = (double)at, npos = (double)pt;
   double auc = 1.0;
   if (npos != 0 && npos != (double)n) {
@@ -423,17 +435,21 @@ void auc_from_sorted(const float* label_sorted, int64_t n, double* out, int64_t*
 namespace wh {
 
 // persistent (zeroed once; lohi[0] = ~0): cnt, pcnt [NB] u32, lohi [2] u64,
-// area u64, ticket u32 (+pad), pair-path partials u64 [kAsMaxX kAsMaxY +
+// (unused) u64 [2], pair-path partials u64 [kAsMaxX kAsMaxY +
 // kAsMaxY] (every word written before it is read).  scratch: off,
 // poff [NB + 1] u32, {lo, width}, per-example (bucket, rank) and the
 // bucket-ordered keys (none for the pair path).
 int64_t auc_ws_bytes(int64_t n) {
   if (n <= kAucSmallMax) return 0;
-  return 2 * ((int64_t)kAucBuckets + 4) * 4 + 16 + 2 * 8 + 8 * n + 8 * n + 64;
+  // ... + the count kernel's per-block partials
+  return 2 * ((int64_t)kAucBuckets + 4) * 4 + 16 + 2 * 8 + 8 * n + 8 * n + 64 +
+         8 * (int64_t)grid_for(n, kThreads);
 }
-int64_t auc_ws_persistent_bytes() {
+// (+ the arrival ticket: kArriveWords u32 at the end)
+static int64_t auc_ticket_offset() {
   return 2 * (int64_t)kAucBuckets * 4 + 4 * 8 + (int64_t)(kAsMaxX * kAsMaxY + kAsMaxY) * 8;
 }
+int64_t auc_ws_persistent_bytes() { return auc_ticket_offset() + (int64_t)kArriveWords * 4; }
 int64_t auc_ws_lohi_offset() { return 2 * (int64_t)kAucBuckets * 4; }
 
 void auc_accumulate(const float* py, const float* label, int64_t n, void* persist, void* scratch,
@@ -443,8 +459,7 @@ void auc_accumulate(const float* py, const float* label, int64_t n, void* persis
   uint32_t* cnt = reinterpret_cast<uint32_t*>(base);
   uint32_t* pcnt = cnt + kAucBuckets;
   unsigned long long* lohi = reinterpret_cast<unsigned long long*>(pcnt + kAucBuckets);
-  unsigned long long* area = lohi + 2;
-  unsigned int* ticket = reinterpret_cast<unsigned int*>(lohi + 3);
+  unsigned int* ticket = reinterpret_cast<unsigned int*>(base + auc_ticket_offset());
   if (n <= kAucSmallMax) {
     const dim3 grid((unsigned)((n + kAsTileJ - 1) / kAsTileJ),
                     (unsigned)((n + kAsTileI - 1) / kAsTileI));
@@ -459,6 +474,7 @@ void auc_accumulate(const float* py, const float* label, int64_t n, void* persis
       (reinterpret_cast<uintptr_t>(poff + kAucBuckets + 4) + 15) & ~(uintptr_t)15);
   int2* br = reinterpret_cast<int2*>(lw + 2);
   unsigned long long* sorted = reinterpret_cast<unsigned long long*>(br + n);
+  unsigned long long* area = sorted + n;  // per-block counts of k_auc_count
   const int g = grid_for(n, kThreads);
   hipLaunchKernelGGL(k_auc_minmax, dim3(grid_for(n, 1024, 64)), dim3(1024), 0, s, py, label, n,
                      lohi);

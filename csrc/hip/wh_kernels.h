@@ -280,6 +280,8 @@ bool ps_pack_gw(const float* gw, int64_t U, int vstride, const int64_t* segS,
 //   loss | 256, met[4] += this minibatch's accuracy flipped below 0.5
 //   part: scratch of fm_fwd_partials() doubles (per-block metric partials)
 int64_t fm_fwd_partials();
+// words of the forward's arrival ticket (zeroed once; left zeroed)
+int64_t fwd_ticket_words();
 // linear forward with w read at w[lid * wstride] (lid < 0: no weight):
 // w = &table.sl[0].w, wstride = 8 reads the weights straight from the slots
 void lin_forward_strided(int64_t nrows, const int64_t* offset, const int32_t* lid,
@@ -289,16 +291,20 @@ void lin_forward_strided(int64_t nrows, const int64_t* offset, const int32_t* li
 // ------------------------------------------------------- linear_direct.hip
 // single-shard linear step without a localize (see the file header)
 int ld_rows_per_tile(int64_t nnz, int64_t nrows);
-// (nnz picks the tile table size: pass the same value to ld_rows_per_tile,
-// ld_touch and ld_backward; ucount must be zero on entry and unext -- the
-// other step parity's counter, whose push has been enqueued -- is zeroed)
+// (nnz picks the tile table size T = ld_tile_table(nnz): pass the same value
+// to ld_rows_per_tile, ld_touch and ld_backward). Slot lists: tile b writes
+// its first-stamped slots to tlist[b * T ..] and their count to tcnt[b];
+// ovf / *ovf_cnt hold the rare slots resolved outside a tile's LDS table
+// (*ovf_cnt zero on entry; ld_push reads and re-zeroes it)
+int ld_tile_table(int64_t nnz);
 void ld_touch(const KVTable& t, const uint64_t* keys, const int64_t* off, int64_t nrows,
-              int64_t nnz, int R, uint32_t stamp, int insert, int32_t* lid, int32_t* ulist,
-              unsigned int* ucount, unsigned int* unext, hipStream_t s);
+              int64_t nnz, int R, uint32_t stamp, int insert, int32_t* lid, int32_t* tlist,
+              unsigned int* tcnt, int32_t* ovf, unsigned int* ovf_cnt, hipStream_t s);
 void ld_backward(const int32_t* lid, const float* val, const int64_t* off, int64_t nrows,
                  int64_t nnz, int R, const float* dual, float* grad, hipStream_t s);
-void ld_push(const KVTable& t, const int32_t* ulist, const unsigned int* ucount, int64_t cap_list,
-             float* grad, LinearHP hp, hipStream_t s);
+void ld_push(const KVTable& t, int64_t ntiles, int T, const int32_t* tlist,
+             const unsigned int* tcnt, const int32_t* ovf, unsigned int* ovf_cnt, float* grad,
+             LinearHP hp, hipStream_t s);
 // CUs the persistent FM grids leave free for concurrent RCCL kernels
 void fm_set_cu_reserve(int cus);
 int fm_cu_reserve();

@@ -31,6 +31,29 @@ __device__ __forceinline__ void lb_store(unsigned long long* p, unsigned long lo
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Arrival ticket in two levels: blocks count in at kArriveGroups counters
+// (bid % groups, one 64-byte line each), the last of each group at the final
+// counter; true in the one block (of nb) that arrives last, which may then
+// read every block's drained partials. Same-address atomics serialise at
+// ~11 ns each, so ONE counter cost ~3.5 us at 313 blocks and ~14 us at 1250
+// once every block finishes at about the same time (a short kernel).
+// ticket: kArriveWords zeroed words, left zeroed. Called by one thread per
+// block, after its partials were stored and drained (s_waitcnt vmcnt(0)).
+constexpr int kArriveGroups = 16;
+constexpr int kArriveStride = 16;  // words: one cache line per group counter
+constexpr int kArriveWords = (kArriveGroups + 1) * kArriveStride;
+__device__ __forceinline__ bool arrive_last(unsigned int* ticket, unsigned bid, unsigned nb) {
+  const unsigned ng = nb < (unsigned)kArriveGroups ? nb : (unsigned)kArriveGroups;
+  const unsigned g = bid % ng, gsize = (nb - g + ng - 1) / ng;
+  unsigned int* gc = ticket + g * kArriveStride;
+  if (atomicAdd(gc, 1u) != gsize - 1) return false;
+  __hip_atomic_store(gc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned int* fc = ticket + kArriveGroups * kArriveStride;
+  if (atomicAdd(fc, 1u) != ng - 1) return false;
+  __hip_atomic_store(fc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 // Block-wide: the tile index of this block (ticket order). `sh` is one
 // shared int. Must be called by every thread of the block.
 __device__ __forceinline__ int lb_tile(const Lookback& lb, int ntiles, int* sh) {

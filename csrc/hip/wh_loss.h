@@ -33,9 +33,7 @@ __device__ __forceinline__ void block_partials(double* part, double* sh, double 
   }
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = atomicAdd(ticket, 1u);
-    last = t == gridDim.x - 1;
-    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = arrive_last(ticket, blockIdx.x, gridDim.x);
   }
   __syncthreads();
   if (!last) return;
