@@ -663,3 +663,23 @@ def test_kmeans_split_precision_matches_fp32(hip, n, f, k):
     else:
         assert not bool(differ.any())
     assert torch.allclose(s3.cpu().double(), got, atol=1e-4, rtol=1e-4)
+
+
+def test_ps_open_rejects_more_than_2_24_keys(hip):
+    """The owner open numbers a minibatch's keys in 24 bits (the duplicate
+    chain links, kv/psx.py): a shard receiving 2^24 keys in one minibatch
+    is refused loudly, before anything is launched, and the store stays
+    usable."""
+    from wormhole_amd.kv import make_store
+    st = make_store(1 << 10, 1 << 8, 16, DEV)
+    seg = torch.tensor([0, 1 << 24], dtype=torch.int64, device=DEV)
+    hseg = torch.zeros(2, dtype=torch.int64, device=DEV)  # (no header rows)
+    big = torch.arange(1 << 24, dtype=torch.int64, device=DEV)
+    hp = [0.1, 1.0, 0.0, 0.0, 0.1, 1.0, 0.0, 0.01]
+    with pytest.raises(RuntimeError, match="2\\^24"):
+        st.ps_open(big, False, seg, hseg, 1 << 24, True, False, hp, 0, False, 0)
+    del big
+    small = torch.arange(100, dtype=torch.int64, device=DEV) * 7 + 1
+    seg = torch.tensor([0, 100], dtype=torch.int64, device=DEV)
+    out = st.ps_open(small, False, seg, hseg, 100, True, False, hp, 0, False, 0)
+    assert int((out[0] >= 0).sum()) == 100  # every key got a slot
