@@ -73,6 +73,8 @@ def main():
     ap.add_argument("--rand-shuffle", type=int, default=10,
                     help="shuffle buffer in minibatches (the reference default is 10)")
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--reuse", action="store_true",
+                    help="keep the data files already in --dir (A/B runs over the same files)")
     args = ap.parse_args()
     work = args.dir or tempfile.mkdtemp(prefix="wh_e2e_")
     os.makedirs(work, exist_ok=True)
@@ -80,6 +82,8 @@ def main():
     per = args.rows // args.files
     for i in range(args.files):
         p = os.path.join(work, "train-part_%d.txt" % i)
+        if args.reuse and os.path.exists(p[:-4] + (".crb" if args.format == "crb" else ".txt")):
+            continue
         with open(p, "wb") as f:
             f.write(criteo_text(per, 100 + i))
         if args.format == "crb":
@@ -89,6 +93,8 @@ def main():
             os.remove(p)
     vper = args.val_rows // args.files if args.val_rows else 0
     for i in range(args.files if vper else 0):
+        if args.reuse and os.path.exists(os.path.join(work, "val-part_%d.txt" % i)):
+            continue
         with open(os.path.join(work, "val-part_%d.txt" % i), "wb") as f:
             f.write(criteo_text(vper, 900 + i))
     gen_s = time.time() - t0

@@ -83,6 +83,12 @@ struct DevWs {
   int heavy_parity = 0;
   int64_t heavy_layout = -1;  // nshard * 65536 + nho of the set the last job elected
   int part_inflight = 0;
+  // (non-zeros, unique ids) of the last finished localize: a caller's hint
+  // is the previous minibatch's unique count, scaled here by the non-zero
+  // ratio when this minibatch is larger (uneven minibatches: CRB records cut
+  // parts into short and long blocks; an unscaled hint under-sized the plan,
+  // every partition overflowed LDS and the job fell back to the hash path)
+  int64_t last_nnz = 0, last_u = -1;
   bool loc_dirty[2] = {false, false};
   bool loc_busy[2] = {false, false};
   int loc_next = 0;
@@ -200,6 +206,11 @@ class LocalizeJob {
       TORCH_CHECK(val->numel() == nnz_);
       val_ = *val;
     }
+    {
+      DevWs& ws = dev_ws(keys.device());
+      if (hint > 0 && hint == ws.last_u && ws.last_nnz > 0 && nnz_ > ws.last_nnz)
+        hint = std::min<int64_t>(nnz_, hint * nnz_ / ws.last_nnz + 1);
+    }
     // Table size: >= 2*nnz can never overflow; with a hint (the previous
     // minibatch's unique count) use ~2.5x the hint instead, which keeps the
     // scratch table small enough to stay cache resident, and fall back to the
@@ -306,6 +317,8 @@ class LocalizeJob {
     Tensor owner_cnt_h = owner_cnt_h_, recv_h = recv_h_;
     int64_t U = 0;
     for (int64_t p = 0; p < nshard_; ++p) U += owner_cnt_h.data_ptr<int64_t>()[p];
+    ws.last_nnz = nnz_;
+    ws.last_u = U;
     if (part_) {  // everything was computed before the host read
       done_ = true;
       if (counted_) {

@@ -1,6 +1,7 @@
 // pybind11 registration of the native host runtime (wormhole_amd._host).
 #include <torch/extension.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -279,6 +280,117 @@ class PyMinibatchIter {
   bool pinned_;
 };
 
+// CSR blocks of `rows` rows straight from a ThreadedReader's decoded chunks
+// (CRB records or parsed text chunks, in file order) into (pinned) tensors,
+// for the device shuffle buffer (wormhole_amd/data/device_text.py). Each
+// chunk's row range is copied into its final slice by a pool of threads: ONE
+// copy per byte, in parallel. MinibatchIter assembled a RowBlock first and
+// then copied it into tensors, both on one thread -- the bound of CRB input
+// (two copies of ~330 MB per million Criteo rows).
+class PyBlockIter {
+ public:
+  PyBlockIter(const std::string& path, int part, int nparts, const std::string& fmt,
+              int64_t rows, bool pinned, int nthreads)
+      : reader_(path, part, nparts, fmt, nthreads), rows_(std::max<int64_t>(rows, 1)),
+        pinned_(pinned), ncopy_(std::max(1, std::min(8, (int)std::thread::hardware_concurrency()))) {}
+
+  py::object next() {
+    struct Piece {
+      std::shared_ptr<RowBlock> b;
+      int64_t r0, r1, row_base, nnz_base;
+    };
+    std::vector<Piece> pieces;
+    Tensor k, o, l, v, w;
+    {
+      py::gil_scoped_release nogil;
+      int64_t have = 0, nnz = 0;
+      bool any_v = false, any_w = false;
+      while (have < rows_) {
+        if (!cur_ || cur_pos_ == (int64_t)cur_->size()) {
+          auto b = std::make_shared<RowBlock>();
+          if (!reader_.Next(b.get())) {
+            cur_.reset();
+            break;
+          }
+          cur_ = std::move(b);
+          cur_pos_ = 0;
+          continue;
+        }
+        const int64_t take = std::min(rows_ - have, (int64_t)cur_->size() - cur_pos_);
+        const int64_t pn = cur_->offset[cur_pos_ + take] - cur_->offset[cur_pos_];
+        pieces.push_back({cur_, cur_pos_, cur_pos_ + take, have, nnz});
+        any_v = any_v || !cur_->value.empty();
+        any_w = any_w || !cur_->weight.empty();
+        cur_pos_ += take;
+        have += take;
+        nnz += pn;
+      }
+      if (pieces.empty()) {
+        py::gil_scoped_acquire g;
+        return py::none();
+      }
+      auto opt = [&](torch::ScalarType dt) {
+        return torch::TensorOptions().dtype(dt).pinned_memory(pinned_);
+      };
+      k = torch::empty({nnz}, opt(torch::kInt64));
+      o = torch::empty({have + 1}, opt(torch::kInt64));
+      l = torch::empty({have}, opt(torch::kFloat32));
+      if (any_v) v = torch::empty({nnz}, opt(torch::kFloat32));
+      if (any_w) w = torch::empty({have}, opt(torch::kFloat32));
+      uint64_t* kp = reinterpret_cast<uint64_t*>(k.data_ptr());
+      int64_t* op = o.data_ptr<int64_t>();
+      float* lp = l.data_ptr<float>();
+      float* vp = any_v ? v.data_ptr<float>() : nullptr;
+      float* wp = any_w ? w.data_ptr<float>() : nullptr;
+      op[0] = 0;
+      std::atomic<size_t> next{0};
+      std::atomic<bool> non_one{false};
+      auto work = [&] {
+        for (size_t i = next++; i < pieces.size(); i = next++) {
+          const Piece& pc = pieces[i];
+          const RowBlock& b = *pc.b;
+          const int64_t s = b.offset[pc.r0], e = b.offset[pc.r1], n = pc.r1 - pc.r0;
+          std::memcpy(kp + pc.nnz_base, b.index.data() + s, (e - s) * sizeof(uint64_t));
+          std::memcpy(lp + pc.row_base, b.label.data() + pc.r0, n * sizeof(float));
+          for (int64_t r = 0; r < n; ++r)
+            op[pc.row_base + r + 1] = pc.nnz_base + (b.offset[pc.r0 + r + 1] - s);
+          if (vp) {
+            if (b.value.empty()) {
+              std::fill(vp + pc.nnz_base, vp + pc.nnz_base + (e - s), 1.f);
+            } else {
+              std::memcpy(vp + pc.nnz_base, b.value.data() + s, (e - s) * sizeof(float));
+              for (int64_t j = s; j < e && !non_one.load(std::memory_order_relaxed); ++j)
+                if (b.value[j] != 1.f) non_one = true;
+            }
+          }
+          if (wp) {
+            if (b.weight.empty()) std::fill(wp + pc.row_base, wp + pc.row_base + n, 1.f);
+            else std::memcpy(wp + pc.row_base, b.weight.data() + pc.r0, n * sizeof(float));
+          }
+        }
+      };
+      const int nt = (int)std::min<size_t>((size_t)ncopy_, pieces.size());
+      std::vector<std::thread> th;
+      for (int t = 1; t < nt; ++t) th.emplace_back(work);
+      work();
+      for (auto& t : th) t.join();
+      // every value 1: binary data (reference minibatch_iter.h:114-116)
+      if (vp && !non_one) v = Tensor();
+    }
+    py::object val = v.defined() ? py::cast(v) : py::none();
+    py::object wt = w.defined() ? py::cast(w) : py::none();
+    return py::make_tuple(k, o, val, l, wt);
+  }
+
+ private:
+  ThreadedReader reader_;
+  int64_t rows_;
+  bool pinned_;
+  int ncopy_;
+  std::shared_ptr<RowBlock> cur_;
+  int64_t cur_pos_ = 0;
+};
+
 py::tuple localize_cpu(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
                        int64_t nshard, int64_t nthreads) {
   auto k = keys.contiguous();
@@ -471,6 +583,11 @@ void register_all(py::module& m) {
            py::arg("minibatch"), py::arg("shuffle_buf") = 0, py::arg("neg_sampling") = 1.0,
            py::arg("seed") = 0, py::arg("pinned") = false)
       .def("next", &PyMinibatchIter::next);
+  py::class_<PyBlockIter>(m, "BlockIter")
+      .def(py::init<const std::string&, int, int, const std::string&, int64_t, bool, int>(),
+           py::arg("path"), py::arg("part"), py::arg("nparts"), py::arg("fmt"), py::arg("rows"),
+           py::arg("pinned") = true, py::arg("nthreads") = 0)
+      .def("next", &PyBlockIter::next);
 
   py::class_<WorkloadPool>(m, "WorkloadPool")
       .def(py::init<bool, uint64_t, double, double, int, double>(), py::arg("shuffle") = false,

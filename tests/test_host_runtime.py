@@ -205,6 +205,48 @@ def test_crb_file_split_via_minibatch_iter(host, tmp_path):
     assert rows == 6513
 
 
+@pytest.mark.parametrize("with_val", [False, True])
+@pytest.mark.parametrize("rows", [777, 2000, 100000])
+def test_block_iter_matches_minibatch_iter(host, tmp_path, with_val, rows):
+    """BlockIter (decoded chunks copied in parallel straight into the block
+    tensors) yields the same blocks as MinibatchIter without a shuffle buffer:
+    same rows in file order, same CSR, values dropped when all are 1."""
+    path = os.path.join(DATA, "agaricus.txt.train")
+    keys, off, val, lab, _ = host.load_split(path, 0, 1, "libsvm")
+    g = torch.Generator().manual_seed(3)
+    v = (torch.rand(keys.numel(), generator=g) + 0.5) if with_val else None
+    p = str(tmp_path / "a.crb")
+    w = host.RecordIOWriter(p)
+    for r0 in range(0, 6513, 1000):
+        r1 = min(r0 + 1000, 6513)
+        o = off[r0:r1 + 1] - off[r0]
+        w.write(host.crb_encode(keys[off[r0]:off[r1]], o,
+                                v[off[r0]:off[r1]] if with_val else None, lab[r0:r1]))
+    w.close()
+    for k in range(2):
+        a = host.MinibatchIter(p, k, 2, "crb", rows)
+        b = host.BlockIter(p, k, 2, "crb", rows, pinned=False)
+        n = 0
+        while True:
+            x, y = a.next(), b.next()
+            assert (x is None) == (y is None)
+            if x is None:
+                break
+            n += 1
+            for i in range(5):
+                assert (x[i] is None) == (y[i] is None), i
+                if x[i] is not None:
+                    assert torch.equal(x[i], y[i]), i
+        assert n >= 1
+    # text chunks too (the host parser's blocks)
+    a = host.MinibatchIter(path, 0, 1, "libsvm", rows)
+    b = host.BlockIter(path, 0, 1, "libsvm", rows, pinned=False)
+    while (x := a.next()) is not None:
+        y = b.next()
+        assert torch.equal(x[0], y[0]) and torch.equal(x[1], y[1]) and torch.equal(x[3], y[3])
+    assert b.next() is None
+
+
 # -------------------------------------------------------------- localize
 @pytest.mark.parametrize("nshard", [1, 4])
 def test_localize_cpu_matches_reference(host, nshard):

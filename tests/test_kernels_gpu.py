@@ -683,3 +683,21 @@ def test_ps_open_rejects_more_than_2_24_keys(hip):
     seg = torch.tensor([0, 100], dtype=torch.int64, device=DEV)
     out = st.ps_open(small, False, seg, hseg, 100, True, False, hp, 0, False, 0)
     assert int((out[0] >= 0).sum()) == 100  # every key got a slot
+
+
+def test_localize_hint_scales_with_minibatch_size(hip):
+    """Uneven minibatches (CRB records cut parts into short and long blocks):
+    a job begun with the previous, much smaller minibatch's unique count as
+    its hint is sized by the non-zero ratio, so its partition plan fits and
+    nothing falls back to the hash path; results stay exact."""
+    card = torch.tensor([50, 400, 3000, 20, 7, 900, 100000, 2000000], dtype=torch.int64,
+                        device=DEV)
+    before = hip.loc_retries()
+    hint = 0
+    for s, n in enumerate([200000, 2000, 200000, 500, 150000, 3000, 200000]):
+        keys, label, off = hip.synth_criteo(n, 11, s, card)
+        job = hip.LocalizeJob(keys, off, None, 1, hint)
+        uniq, ucnt, oc, lid = job.finish()[:4]
+        assert torch.equal(uniq[lid.long()], keys)
+        hint = uniq.numel()
+    assert hip.loc_retries() == before

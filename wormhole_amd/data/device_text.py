@@ -125,15 +125,21 @@ class DeviceTextIter:
         # shuffle buffer is assembled from several text batches on the device
         self.per_block = max(1, -(-max(shuf, mb + 1) // mb)) if self.shuffled else 1
         # CRB (binary records, LZ4 sections): the host's reader threads decode
-        # the records in parallel (csrc/host/parsers.cc ThreadedReader) into
-        # pinned CSR blocks of per_block minibatches, in file order; the
+        # the records in parallel (csrc/host/parsers.cc ThreadedReader) and a
+        # copy pool assembles pinned CSR blocks of per_block minibatches, in
+        # file order (csrc/host/registry.cc BlockIter); the
         # shuffle buffer, negative sampling and minibatch slicing then run on
         # the device exactly as for parsed text (the host shuffle was the
         # single-threaded bottleneck of CRB input: 4.9 M rows/s)
+        # blocks go straight from the decoded records into pinned tensors,
+        # copied by a thread pool (host.BlockIter; one copy per byte)
         self.blocks = fmt == "crb"
         if self.blocks:
-            self.tb = host.MinibatchIter(path, part, nparts, fmt, int(mb * self.per_block), 0,
-                                         1.0, int(seed), True)
+            if os.environ.get("WH_CRB_BLOCKITER", "1") == "0":  # (A/B: the assembling iterator)
+                self.tb = host.MinibatchIter(path, part, nparts, fmt, int(mb * self.per_block), 0,
+                                             1.0, int(seed), True)
+            else:
+                self.tb = host.BlockIter(path, part, nparts, fmt, int(mb * self.per_block), True)
         else:
             # several readers over line-aligned sub-ranges of the part, taken
             # round-robin in a fixed order (one reader thread copies ~7 GB/s
