@@ -1717,6 +1717,22 @@ Tensor kmeans_accum(const Tensor& X, const Tensor& assign, int64_t k) {
   return sums;
 }
 
+// (new C [k, f], empty-cluster count int64 [1]) from sums [k, f + 1] and C
+std::vector<Tensor> kmeans_update(const Tensor& sums, const Tensor& C) {
+  CHECK_IN(sums, torch::kFloat32);
+  CHECK_IN(C, torch::kFloat32);
+  TORCH_CHECK(C.dim() == 2 && sums.dim() == 2 && sums.size(0) == C.size(0) &&
+                  sums.size(1) == C.size(1) + 1,
+              "kmeans_update: sums must be [k, f + 1] for C [k, f]");
+  c10::DeviceGuard g(C.device());
+  auto out = torch::empty_like(C);
+  auto nempty = torch::zeros({1}, C.options().dtype(torch::kInt64));
+  wh::kmeans_update(ptr<float>(sums), ptr<float>(C), (int)C.size(0), (int)C.size(1),
+                    ptr<float>(out), reinterpret_cast<unsigned long long*>(nempty.data_ptr()),
+                    cur_stream(C));
+  return {out, nempty};
+}
+
 Tensor spmv(const Tensor& offset, const Tensor& col, const c10::optional<Tensor>& val,
             const Tensor& x) {
   CHECK_IN(offset, torch::kInt64);
@@ -2762,6 +2778,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_pack_c", &kmeans_pack_c);
   m.def("kmeans_assign", &kmeans_assign);
   m.def("kmeans_accum", &kmeans_accum);
+  m.def("kmeans_update", &kmeans_update);
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
   m.def("gbdt_grow", &gbdt_grow);
   // the ingest ops block on one small device read each: the GIL is released

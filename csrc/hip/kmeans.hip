@@ -475,6 +475,46 @@ void kmeans_accum(const float* X, int64_t n, int f, const int32_t* assign, float
   hipLaunchKernelGGL(k_accum, dim3(grid_for(n * 64, 256)), dim3(256), 0, s, X, n, f, assign, sums);
 }
 
+namespace {
+// Centroid update in one launch, one block per centroid (reference
+// learn/kmeans/kmeans.cc: divide the summed rows by the count, then L2
+// normalise): c = sums[r, f]; v = sums[r, :f] / c, or the previous centroid
+// when the cluster is empty; out[r] = v * (float)(1 / ||v||) with the norm in
+// double and rows of norm < 1e-6 left unscaled (models/kmeans.py
+// normalize_rows); *nempty += the empty clusters. Replaces ~10 small torch
+// launches per iteration.
+__global__ __launch_bounds__(128) void k_km_update(const float* __restrict__ sums,
+                                                   const float* __restrict__ C, int f,
+                                                   float* __restrict__ out,
+                                                   unsigned long long* nempty) {
+  __shared__ double sh[2];
+  const int r = blockIdx.x;
+  const float c = sums[(int64_t)r * (f + 1) + f];
+  const bool empty = c == 0.f;
+  double ss = 0;
+  for (int j = threadIdx.x; j < f; j += 128) {
+    const float v = empty ? C[(int64_t)r * f + j] : sums[(int64_t)r * (f + 1) + j] / c;
+    ss += (double)v * v;
+  }
+  ss = wave_sum_d(ss);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const double nrm = sqrt(sh[0] + sh[1]);
+  const float scale = nrm < 1e-6 ? 1.f : (float)(1.0 / nrm);
+  for (int j = threadIdx.x; j < f; j += 128) {
+    const float v = empty ? C[(int64_t)r * f + j] : sums[(int64_t)r * (f + 1) + j] / c;
+    out[(int64_t)r * f + j] = v * scale;
+  }
+  if (threadIdx.x == 0 && empty) atomicAdd(nempty, 1ull);
+}
+}  // namespace
+
+void kmeans_update(const float* sums, const float* C, int k, int f, float* out,
+                   unsigned long long* nempty, hipStream_t s) {
+  if (k <= 0) return;
+  hipLaunchKernelGGL(k_km_update, dim3((unsigned)k), dim3(128), 0, s, sums, C, f, out, nempty);
+}
+
 }  // namespace wh
 
 namespace wh {

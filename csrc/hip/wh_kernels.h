@@ -400,6 +400,10 @@ void kmeans_accum(const float* X, int64_t n, int f, const int32_t* assign, float
 // the same sums through a counting sort by cluster + register segment sums
 // (returns false when k / f exceed its LDS / register limits: use the above)
 int64_t kmeans_accum_scratch(int64_t n, int k);
+// new centroids from sums [k, f + 1] (count last) and the previous C [k, f]:
+// mean (previous row if empty), L2-normalised; *nempty += empty clusters
+void kmeans_update(const float* sums, const float* C, int k, int f, float* out,
+                   unsigned long long* nempty, hipStream_t s);
 bool kmeans_accum_sorted(const float* X, int64_t n, int f, int k, const int32_t* assign,
                          float* sums, void* scratch, hipStream_t s);
 

@@ -701,3 +701,24 @@ def test_localize_hint_scales_with_minibatch_size(hip):
         assert torch.equal(uniq[lid.long()], keys)
         hint = uniq.numel()
     assert hip.loc_retries() == before
+
+
+def test_kmeans_update_matches_torch(hip):
+    """One-launch centroid update = mean of the summed rows (the previous
+    centroid for an empty cluster), L2-normalised as models/kmeans.py does."""
+    from wormhole_amd.models.kmeans import normalize_rows
+    g = torch.Generator().manual_seed(4)
+    k, f = 37, 100
+    sums = torch.randn(k, f + 1, generator=g)
+    sums[:, f] = torch.randint(0, 50, (k,), generator=g).float()
+    sums[3, f] = 0
+    sums[11, f] = 0
+    sums[20, :f] = 0  # a zero-norm mean stays unscaled
+    C = normalize_rows(torch.randn(k, f, generator=g))
+    cnt = sums[:, f]
+    empty = cnt == 0
+    exp = torch.where(empty[:, None], C, sums[:, :f] / torch.where(empty, 1.0, cnt)[:, None])
+    exp = normalize_rows(exp)
+    got, ne = hip.kmeans_update(sums.to(DEV), C.to(DEV))
+    assert int(ne) == int(empty.sum())
+    assert torch.allclose(got.cpu(), exp, atol=1e-6, rtol=1e-6)

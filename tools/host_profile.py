@@ -49,6 +49,9 @@ def main():
     lr = DifactoLearner(conf, Comm(dev, init=False), dev, cap=1 << 27, vcap=1 << 24, seed=1)
     for n in ["open", "difacto_open_pull", "difacto_push_cnt", "difacto_pull", "difacto_push"]:
         wrap(lr.kv, n, "kv." + n)
+    from wormhole_amd.models import difacto as dmod
+    wrap(dmod, "begin_next", "begin_next")
+    wrap(dmod, "localize_current", "localize_current")
     card = torch.tensor(CRITEO_TB_CARD, dtype=torch.int64, device=dev)
 
     def synth(s):

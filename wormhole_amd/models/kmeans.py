@@ -100,6 +100,10 @@ class KMeans:
         a = self.assign()
         sums = self.accumulate(a)
         self.bsp.allreduce(sums)  # rabit::Allreduce<Sum>(temp, K*(F+1), lazy_fn)
+        if self.gpu:  # mean + normalise + empty count in one launch
+            self.C, n_empty = _native.hip().kmeans_update(sums, self.C.contiguous())
+            self._warn_empty(n_empty)
+            return a
         cnt = sums[:, self.f]
         empty = cnt == 0
         self._warn_empty(empty.sum())
