@@ -893,6 +893,8 @@ class TreeBuilder:
 
     def _prune_mark(self, tree):
         """The collapse itself, node ids unchanged (see :meth:`_compact`)."""
+        if self.p.gamma <= 0:  # accepted splits have gain > RT_EPS > 0: nothing to prune
+            return
         changed = True
         while changed:
             changed = False
@@ -917,13 +919,18 @@ class TreeBuilder:
             # walk the pruned tree per row on its bins (a pruned-away
             # subtree's rows stop at its collapsed root, whose leaf value
             # _prune_mark set): coalesced, instead of a scatter by ridx
-            dev = self.device
-            t32 = lambda v: torch.tensor(v, dtype=torch.int32).to(dev, non_blocking=True)  # noqa: E731
+            # the six node arrays in ONE upload (six small copies cost ~20 us
+            # of queue time each between the level loop and the walk)
+            import numpy as np
+            nn = len(tree.feat)
+            h = np.empty(6 * nn, dtype=np.int32)
+            for q, v in enumerate((tree.feat, tree.bin, tree.left, tree.right, tree.defl)):
+                h[q * nn:(q + 1) * nn] = v
+            h[5 * nn:].view(np.float32)[:] = tree.leaf
+            d = torch.from_numpy(h).to(self.device, non_blocking=True)
             _native.hip().gbdt_leaf_walk(
-                B, t32(tree.feat), t32(tree.bin),
-                torch.tensor(tree.defl, dtype=torch.uint8).to(dev, non_blocking=True),
-                t32(tree.left), t32(tree.right),
-                torch.tensor(tree.leaf, dtype=torch.float32).to(dev, non_blocking=True), margin)
+                B, d[:nn], d[nn:2 * nn], d[4 * nn:5 * nn].to(torch.uint8), d[2 * nn:3 * nn],
+                d[3 * nn:4 * nn], d[5 * nn:].view(torch.float32), margin)
         elif n and self.gpu:
             val = torch.zeros(len(tree.feat), dtype=torch.float32)
             for nd in leaf_segs:
