@@ -1575,6 +1575,32 @@ void gbdt_leaf_add(const Tensor& ridx, const Tensor& pos_node, const Tensor& lea
 }
 
 // tree arrays: int32 feat / bin / left / right, uint8 defl, float val [nodes]
+// (gpair f32 [n, 2], stats f64 [4] = {sum g, sum h, max|g|, max|h|})
+std::vector<Tensor> gbdt_gpair(const Tensor& margin, const Tensor& label,
+                               const c10::optional<Tensor>& weight, bool logistic) {
+  CHECK_IN(margin, torch::kFloat32);
+  CHECK_IN(label, torch::kFloat32);
+  const int64_t n = margin.numel();
+  TORCH_CHECK(label.numel() == n, "gbdt_gpair: label size mismatch");
+  const float* wp = nullptr;
+  if (weight.has_value() && weight->defined()) {
+    CHECK_IN((*weight), torch::kFloat32);
+    TORCH_CHECK(weight->numel() == n, "gbdt_gpair: weight size mismatch");
+    wp = ptr<float>(*weight);
+  }
+  c10::DeviceGuard g(margin.device());
+  static std::vector<Tensor> scratch(64);  // per device, the ticket tail stays zeroed
+  const int dev = margin.device().index();
+  if (!scratch[dev].defined())
+    scratch[dev] = torch::zeros({wh::gbdt_gpair_scratch()}, margin.options().dtype(torch::kFloat64));
+  auto gp = torch::empty({n, 2}, margin.options());
+  auto st = torch::zeros({4}, margin.options().dtype(torch::kFloat64));
+  if (n > 0)
+    wh::gbdt_gpair(n, ptr<float>(margin), ptr<float>(label), wp, logistic, ptr<float>(gp),
+                   ptr<double>(scratch[dev]), ptr<double>(st), cur_stream(margin));
+  return {gp, st};
+}
+
 void gbdt_leaf_walk(const Tensor& B, const Tensor& feat, const Tensor& bin, const Tensor& defl,
                     const Tensor& left, const Tensor& right, const Tensor& val,
                     const Tensor& margin) {
@@ -2781,6 +2807,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_update", &kmeans_update);
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
   m.def("gbdt_grow", &gbdt_grow);
+  m.def("gbdt_gpair", &gbdt_gpair);
   // the ingest ops block on one small device read each: the GIL is released
   // so a producer thread's parsing overlaps the training loop
   m.def("parse_criteo", &parse_criteo, py::call_guard<py::gil_scoped_release>());

@@ -8,6 +8,8 @@
 //   gbdt_goleft / gbdt_scatter   stable per-node row partition after a split
 //   gbdt_leaf_add  margin += leaf value for the rows of every leaf segment
 //   gbdt_predict   one lane per row walks a tree on raw values (NaN = missing)
+#include <algorithm>
+
 #include "wh_common.h"
 #include "wh_kernels.h"
 #include "wh_lookback.h"
@@ -601,6 +603,96 @@ void gbdt_leaf_add(const int32_t* ridx, int64_t n, const int32_t* pos_node, cons
   if (n <= 0) return;
   hipLaunchKernelGGL(k_leaf_add, dim3(grid_for(n, 256)), dim3(256), 0, s, ridx, n, pos_node, leaf,
                      margin);
+}
+
+namespace {
+// Gradient pairs of one boosting round in one launch, with the tree's root
+// statistics (reference: xgboost's ObjFunction::GetGradient, then the
+// GPU hist updater's root sum): gpair[i] = {g, h} for binary:logistic
+// (p = sigmoid(margin), g = p - y, h = max(p (1 - p), 1e-16)) or squared
+// error (g = margin - y, h = 1), times the row weight; stats = {sum g,
+// sum h (fp64), max |g|, max |h|} by per-block partials + arrival ticket.
+// Replaced ~12 torch launches (~0.45 ms per tree at 11M rows).
+constexpr int kGpThreads = 256, kGpBlocks = 1024;
+__global__ __launch_bounds__(kGpThreads) void k_gpair(int64_t n, const float* __restrict__ margin,
+                                                      const float* __restrict__ label,
+                                                      const float* __restrict__ weight,
+                                                      int logistic, float2* __restrict__ out,
+                                                      double* __restrict__ part,
+                                                      unsigned int* ticket, double* stats) {
+  __shared__ double sh[4][kGpThreads / 64];
+  __shared__ int last;
+  double sg = 0, shh = 0, mg = 0, mh = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kGpThreads + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kGpThreads) {
+    const float m = margin[i], y = label[i];
+    float g, h;
+    if (logistic) {
+      const float p = 1.f / (1.f + expf(-m));
+      g = p - y;
+      h = fmaxf(p * (1.f - p), 1e-16f);
+    } else {
+      g = m - y;
+      h = 1.f;
+    }
+    if (weight) {
+      const float w = weight[i];
+      g *= w;
+      h *= w;
+    }
+    out[i] = make_float2(g, h);
+    sg += g;
+    shh += h;
+    mg = fmax(mg, (double)fabsf(g));
+    mh = fmax(mh, (double)fabsf(h));
+  }
+  sg = wave_sum_d(sg);
+  shh = wave_sum_d(shh);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mg = fmax(mg, __shfl_xor(mg, o, 64));
+    mh = fmax(mh, __shfl_xor(mh, o, 64));
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    sh[0][wid] = sg; sh[1][wid] = shh; sh[2][wid] = mg; sh[3][wid] = mh;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double v[4] = {0, 0, 0, 0};
+    for (int w = 0; w < kGpThreads / 64; ++w) {
+      v[0] += sh[0][w]; v[1] += sh[1][w];
+      v[2] = fmax(v[2], sh[2][w]); v[3] = fmax(v[3], sh[3][w]);
+    }
+    for (int q = 0; q < 4; ++q)
+      lb_store(reinterpret_cast<unsigned long long*>(part) + blockIdx.x * 4 + q,
+               (unsigned long long)__double_as_longlong(v[q]));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = arrive_last(ticket, blockIdx.x, gridDim.x);
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  double v[4] = {0, 0, 0, 0};
+  const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(part);
+  for (unsigned b = 0; b < gridDim.x; ++b) {  // (block order: the same sum every run)
+    v[0] += __longlong_as_double((long long)lb_load(pp + b * 4));
+    v[1] += __longlong_as_double((long long)lb_load(pp + b * 4 + 1));
+    v[2] = fmax(v[2], __longlong_as_double((long long)lb_load(pp + b * 4 + 2)));
+    v[3] = fmax(v[3], __longlong_as_double((long long)lb_load(pp + b * 4 + 3)));
+  }
+  for (int q = 0; q < 4; ++q) stats[q] = v[q];
+}
+}  // namespace
+
+int64_t gbdt_gpair_scratch() { return 4 * (int64_t)kGpBlocks + kArriveWords / 2 + 1; }
+
+void gbdt_gpair(int64_t n, const float* margin, const float* label, const float* weight,
+                bool logistic, float* gpair, double* scratch, double* stats, hipStream_t s) {
+  // scratch: per-block partials, then the (zeroed) arrival ticket words
+  unsigned int* ticket = reinterpret_cast<unsigned int*>(scratch + 4 * kGpBlocks);
+  const int nb = std::max(1, std::min<int>(kGpBlocks, grid_for(n, kGpThreads)));
+  hipLaunchKernelGGL(k_gpair, dim3(nb), dim3(kGpThreads), 0, s, n, margin, label, weight,
+                     logistic ? 1 : 0, reinterpret_cast<float2*>(gpair), scratch, ticket, stats);
 }
 
 void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, const int32_t* feat, const int32_t* bin,

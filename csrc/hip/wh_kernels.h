@@ -495,6 +495,11 @@ void gbdt_predict_csr(const int64_t* row_off, const int32_t* fid, const float* v
                       hipStream_t s);
 // training margins after a tree: margin[i] += val[leaf of row i], walking the
 // pruned tree on the row's bins (B row-major [n, f])
+// gradient pairs of a boosting round + {sum g, sum h, max|g|, max|h|} (fp64)
+// in one launch; scratch: gbdt_gpair_scratch() doubles, the tail zeroed once
+int64_t gbdt_gpair_scratch();
+void gbdt_gpair(int64_t n, const float* margin, const float* label, const float* weight,
+                bool logistic, float* gpair, double* scratch, double* stats, hipStream_t s);
 void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, const int32_t* feat, const int32_t* bin,
                     const uint8_t* defl, const int32_t* left, const int32_t* right,
                     const float* val, float* margin, hipStream_t s);

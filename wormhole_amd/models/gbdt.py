@@ -118,6 +118,13 @@ class Objective:
         return base
 
     def gpair(self, margin, label, weight):
+        if margin.is_cuda and margin.dtype == torch.float32 and label.dtype == torch.float32:
+            # one launch; the root statistics ride along (gpair_stats)
+            gp, st = _native.hip().gbdt_gpair(margin.contiguous(), label.contiguous(),
+                                              weight.contiguous() if weight is not None else None,
+                                              bool(self.logistic))
+            gp._wh_stats = st
+            return gp
         if self.logistic:
             p = torch.sigmoid(margin)
             g = p - label
@@ -136,6 +143,19 @@ class Objective:
 
     def default_metric(self):
         return "error" if self.name == "binary:logistic" else "rmse"
+
+
+def gpair_stats(gpair):
+    """(sum g, sum h) in fp64 and (max |g|, max |h|) of a gradient-pair
+    tensor: the ones the fused GPU gradient kernel computed alongside it,
+    else reduced here."""
+    st = getattr(gpair, "_wh_stats", None)
+    if st is not None:
+        return st[:2].clone(), st[2:4].float()
+    if gpair.shape[0] == 0:
+        z = torch.zeros(2, dtype=torch.float64, device=gpair.device)
+        return z, z.float()
+    return gpair.double().sum(0), gpair.abs().amax(0).float()
 
 
 def eval_metric(name, pred, label, weight, bsp):
@@ -569,7 +589,7 @@ class TreeBuilder:
         int64 sum can overflow on any rank (see csrc/hip/gbdt.hip)."""
         if self._nglobal is None:
             self._nglobal = max(1, int(self.bsp.allreduce_scalar(self.dm.n)))
-        m = gpair.abs().amax(0) if self.dm.n else torch.zeros(2, device=self.device)
+        m = gpair_stats(gpair)[1] if self.dm.n else torch.zeros(2, device=self.device)
         m = m.float().contiguous()
         self.bsp.allreduce(m, op="max")
         e = torch.floor(torch.log2(2.0 ** 61 / (self._nglobal * m.double().clamp_min(1e-30))))
@@ -703,7 +723,7 @@ class TreeBuilder:
         reference)."""
         p = self.p
         n = self.dm.n
-        tot = gpair.double().sum(0)
+        tot = gpair_stats(gpair)[0]
         self.bsp.allreduce(tot)
         self._qscale = self._hist_scale(gpair)
         if self._Bc is None:
@@ -714,7 +734,7 @@ class TreeBuilder:
             self._cut_lists = (self.cuts.values.tolist(), self.cuts.offsets.tolist())
         ar = (lambda t: self.bsp.allreduce(t)) if self.bsp.world > 1 else None
         out = _native.hip().gbdt_grow(
-            self.B, self._Bc, torch.arange(n, dtype=torch.int32, device=self.device), gpair,
+            self.B, self._Bc, self._iota(n), gpair,
             self._qscale, self._valid_dev[1], self.nbin, self.fgroups, self.max_fcnt,
             tot.cpu().tolist(), self._cut_lists[0], self._cut_lists[1], float(p.eta),
             float(p.alpha), float(p.reg_lambda), float(p.min_child_weight), int(p.max_depth),
@@ -728,6 +748,13 @@ class TreeBuilder:
         self._finish(tree, ridx, margin, n, {nd: (b, e) for nd, b, e in segs})
         return tree
 
+    def _iota(self, n):
+        """0..n-1 as int32 on the device (the grower only reads it)."""
+        t = getattr(self, "_iota_t", None)
+        if t is None or t.numel() != n:
+            t = self._iota_t = torch.arange(n, dtype=torch.int32, device=self.device)
+        return t
+
     def _build_py(self, gpair, margin):
         p = self.p
         n = self.dm.n
@@ -735,7 +762,7 @@ class TreeBuilder:
         tree = RegTree()
         root = tree.add(-1)
         ridx = torch.arange(n, dtype=torch.int32, device=dev)
-        tot = gpair.double().sum(0) if n else torch.zeros(2, dtype=torch.float64, device=dev)
+        tot = gpair_stats(gpair)[0] if n else torch.zeros(2, dtype=torch.float64, device=dev)
         self.bsp.allreduce(tot)
         totals = {root: tot.cpu()}
         seg = {root: (0, n)}
