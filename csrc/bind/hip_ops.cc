@@ -2129,7 +2129,15 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
   PinnedBuf down;
   Tensor ridx = ridx0;
   // histogram of the given (slot -> [b, e) device segments); tasks by chunk
-  auto build_hist = [&](const Tensor& dseg, const std::vector<int64_t>& seglen) -> Tensor {
+  // histogram of the given (slot -> [b, e) device segments); tasks by chunk.
+  // Prepared (task lists built and uploaded, outputs allocated) before the
+  // level's partition is enqueued, so the histogram launch follows the
+  // child segments without host work in between.
+  struct HistPlan {
+    Tensor d, hist, part;
+    int64_t nt = 0, nr = 0;
+  };
+  auto plan_hist = [&](const std::vector<int64_t>& seglen) -> HistPlan {
     const int S = (int)seglen.size();
     std::vector<int32_t> tasks, red;
     for (int k = 0; k < S; ++k) {
@@ -2143,28 +2151,33 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
         red.insert(red.end(), {k, (int)fgroups[gi].first, (int)fgroups[gi].second, t0 + gi,
                                (int)nch, G});
     }
-    const int64_t nt = (int64_t)tasks.size() / 5, nr = (int64_t)red.size() / 6;
+    HistPlan hp;
+    hp.nt = (int64_t)tasks.size() / 5;
+    hp.nr = (int64_t)red.size() / 6;
     int32_t* h = up_tasks.get<int32_t>(tasks.size() + red.size());
     std::memcpy(h, tasks.data(), tasks.size() * 4);
     std::memcpy(h + tasks.size(), red.data(), red.size() * 4);
-    auto d = up_tasks.tensor().narrow(0, 0, (int64_t)(tasks.size() + red.size()) * 4)
-                 .to(B.device(), /*non_blocking=*/true).view(torch::kInt32);
+    hp.d = up_tasks.tensor().narrow(0, 0, (int64_t)(tasks.size() + red.size()) * 4)
+               .to(B.device(), /*non_blocking=*/true).view(torch::kInt32);
     up_tasks.mark(s);
-    auto hist = torch::empty({S, F, nbin, 2}, f64);
-    auto part = torch::empty({nt * wh::gbdt_hist_pstride((int)max_fcnt, (int)nbin)},
-                             gpair.options().dtype(torch::kInt64));
+    hp.hist = torch::empty({S, F, nbin, 2}, f64);
+    hp.part = torch::empty({hp.nt * wh::gbdt_hist_pstride((int)max_fcnt, (int)nbin)},
+                           gpair.options().dtype(torch::kInt64));
+    return hp;
+  };
+  auto run_hist = [&](const HistPlan& hp, const Tensor& dseg) -> Tensor {
     wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
-                  ptr<float>(qscale), ptr<int32_t>(d), (int)nt, ptr<int32_t>(d) + nt * 5,
-                  (int)nr, (int)max_fcnt, dw, ptr<int64_t>(part), ptr<double>(hist), s,
-                  ptr<int32_t>(dseg), chunk);
+                  ptr<float>(qscale), ptr<int32_t>(hp.d), (int)hp.nt,
+                  ptr<int32_t>(hp.d) + hp.nt * 5, (int)hp.nr, (int)max_fcnt, dw,
+                  ptr<int64_t>(hp.part), ptr<double>(hp.hist), s, ptr<int32_t>(dseg), chunk);
     // (no drain here: the staging ring waits for this copy only when its slot
     // comes round again; the histogram allreduce is stream-ordered)
-    if (reduce) allreduce(hist);
-    return hist;
+    if (reduce) allreduce(hp.hist);
+    return hp.hist;
   };
   Tensor dseg_root = torch::tensor({0, (int)n}, torch::TensorOptions().dtype(torch::kInt32))
                          .to(B.device());
-  Tensor H_front = build_hist(dseg_root, {n});
+  Tensor H_front = run_hist(plan_hist({n}), dseg_root);
   std::vector<int> frontier{root};
   // splits whose children's segments wait for the partition counts
   std::vector<std::array<int, 5>> pending;  // nd, l, r, b, e
@@ -2279,6 +2292,8 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
     const int32_t* d_par = d_sp + 4 * nsplit;
     int32_t* d_lc = const_cast<int32_t*>(d_par + nsplit);
     int32_t* d_rc = d_lc + nnode;
+    // the built children's histogram tasks, sized by the host-side bounds
+    const HistPlan hplan = plan_hist(small_len);
     auto ridx_new = torch::empty_like(ridx);
     nleft_dev = torch::empty({nnode}, i32);
     if (!wh::gbdt_partition_cursor(ptr<uint8_t>(B), ptr<uint8_t>(Bc), B.size(0), F,
@@ -2305,7 +2320,7 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
     // built children's rows, from the device counts
     auto dseg = torch::empty({2 * nsplit}, i32);
     wh::gbdt_child_segs(d_sp, nsplit, ptr<int32_t>(nleft_dev), ptr<int32_t>(dseg), s);
-    Tensor hs = build_hist(dseg, small_len);  // (synchronises the upload buffer)
+    Tensor hs = run_hist(hplan, dseg);
     auto H_next = torch::empty({2 * nsplit, F, nbin, 2}, f64);
     wh::gbdt_sibling(ptr<double>(H_front), ptr<double>(hs), d_sp, d_par, nsplit, per,
                      ptr<double>(H_next), s);
