@@ -2366,6 +2366,174 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
                         ridx);
 }
 
+// The same tree as gbdt_grow with the level loop on the device: heap-numbered
+// nodes, the split decisions, partition set-up, child segments and the
+// histogram task lists are written by kernels (gbdt.hip k_gd_apply /
+// k_gd_children), so the host enqueues every level without waiting and reads
+// the finished tree ONCE (gbdt_grow syncs once per level: ~1.5 ms of idle
+// GPU per depth-8 tree of 11M rows). Every max_depth level is enqueued; the
+// levels below a tree's last split find no live node and do no row work but
+// the partition's pass.
+py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, const Tensor& gpair,
+                        const Tensor& qscale, const Tensor& valid, int64_t nbin,
+                        std::vector<std::pair<int64_t, int64_t>> fgroups, int64_t max_fcnt,
+                        std::vector<double> root_tot, std::vector<float> cut_vals,
+                        std::vector<int64_t> cut_off, double eta, double alpha, double lambda,
+                        double mcw, int64_t max_depth, double rt_eps, py::object allreduce) {
+  CHECK_IN(B, torch::kUInt8);
+  CHECK_IN(Bc, torch::kUInt8);
+  CHECK_IN(ridx0, torch::kInt32);
+  CHECK_IN(gpair, torch::kFloat32);
+  CHECK_IN(qscale, torch::kFloat32);
+  CHECK_DEV(valid);
+  TORCH_CHECK(max_depth >= 0 && max_depth <= 10, "gbdt_grow_dev: max_depth in [0, 10]");
+  c10::DeviceGuard g(B.device());
+  auto s = cur_stream(B);
+  const int64_t n = ridx0.numel();
+  const int F = (int)B.size(1);
+  TORCH_CHECK(n < (int64_t)INT32_MAX, "rows must fit int32");
+  const int G = (int)fgroups.size();
+  const bool dw = F % 4 == 0 && max_fcnt % 4 == 0;
+  const int64_t per = (int64_t)F * nbin * 2;
+  auto f64 = B.options().dtype(torch::kFloat64);
+  auto i32 = B.options().dtype(torch::kInt32);
+  auto u8 = B.options().dtype(torch::kUInt8);
+  const int chunk = (int)std::max<int64_t>(8192, (n + 1023) / 1024);
+  const bool reduce = !allreduce.is_none();
+  const int D = (int)max_depth, NN = (2 << D) - 1, Smax = 1 << D, REC = wh::gbdt_node_rec();
+  const int64_t pstride = wh::gbdt_hist_pstride((int)max_fcnt, (int)nbin);
+  // one small upload: root totals, root segment, feature groups, slot iota
+  std::vector<int32_t> hw;
+  hw.reserve(3 + 2 * G + Smax);
+  hw.push_back(0), hw.push_back((int32_t)n), hw.push_back(1);
+  for (auto& fg : fgroups) hw.push_back((int32_t)fg.first), hw.push_back((int32_t)fg.second);
+  for (int i = 0; i < Smax; ++i) hw.push_back(i);
+  auto hdev = torch::from_blob(hw.data(), {(int64_t)hw.size()}, torch::kInt32).to(B.device());
+  const int32_t* d_root_seg = ptr<int32_t>(hdev);
+  const int32_t* d_fg = d_root_seg + 3;
+  const int32_t* d_iota = d_fg + 2 * G;
+  Tensor tot_cur = torch::tensor(root_tot, torch::TensorOptions().dtype(torch::kFloat64)).to(B.device());
+  Tensor seg_cur = hdev.narrow(0, 0, 2);
+  Tensor alive_cur = torch::ones({1}, u8);
+  auto nodes = torch::zeros({NN, REC}, f64);
+  const uint8_t* vp = reinterpret_cast<const uint8_t*>(valid.data_ptr());
+  Tensor ridx = ridx0;
+  // root histogram: the host's task list over [0, n)
+  Tensor H_front;
+  {
+    const int64_t nch = std::max<int64_t>(1, (n + chunk - 1) / chunk);
+    std::vector<int32_t> tasks, red;
+    for (int64_t c = 0; c < nch; ++c)
+      for (auto& fg : fgroups) tasks.insert(tasks.end(), {0, (int)fg.first, (int)fg.second, (int)c, chunk});
+    for (int gi = 0; gi < G; ++gi)
+      red.insert(red.end(), {0, (int)fgroups[gi].first, (int)fgroups[gi].second, gi, (int)nch, G});
+    tasks.insert(tasks.end(), red.begin(), red.end());
+    auto d = torch::from_blob(tasks.data(), {(int64_t)tasks.size()}, torch::kInt32).to(B.device());
+    const int64_t nt = nch * G;
+    H_front = torch::empty({1, F, nbin, 2}, f64);
+    auto part = torch::empty({nt * pstride}, gpair.options().dtype(torch::kInt64));
+    wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
+                  ptr<float>(qscale), ptr<int32_t>(d), (int)nt, ptr<int32_t>(d) + nt * 5, G,
+                  (int)max_fcnt, dw, ptr<int64_t>(part), ptr<double>(H_front), s,
+                  ptr<int32_t>(seg_cur), chunk);
+    if (reduce) allreduce(H_front);
+  }
+  for (int d = 0; d <= D; ++d) {
+    const int S = 1 << d;
+    const bool last = d == D;
+    Tensor so;
+    if (!last) {
+      so = torch::empty({S, 6}, f64);
+      auto cand = torch::empty({(int64_t)S * F * 4}, f64);
+      TORCH_CHECK(wh::gbdt_split(ptr<double>(H_front), ptr<double>(tot_cur), vp, S, F, (int)nbin,
+                                 alpha, lambda, mcw, ptr<double>(cand), ptr<double>(so), s),
+                  "gbdt_split failed");
+    }
+    auto pi = torch::empty({4 * S}, i32);  // pfeat | pbin | lcur | rcur
+    auto pb = torch::empty({3 * S}, u8);   // pdefl | split | build_left
+    Tensor tot_next = last ? Tensor() : torch::empty({2 * S, 2}, f64);
+    int32_t* pfeat = ptr<int32_t>(pi);
+    uint8_t* pdefl = ptr<uint8_t>(pb);
+    wh::gbdt_dev_apply(S, S - 1, last, last ? nullptr : ptr<double>(so), ptr<double>(tot_cur),
+                       ptr<int32_t>(seg_cur), ptr<uint8_t>(alive_cur), eta, alpha, lambda, mcw,
+                       rt_eps, ptr<double>(nodes), pfeat, pfeat + S, pdefl, pfeat + 2 * S,
+                       pfeat + 3 * S, pdefl + S, pdefl + 2 * S,
+                       last ? nullptr : ptr<double>(tot_next), s);
+    if (last) break;
+    // partition of the split slots' rows on the device segment table
+    auto sbeg = seg_cur.view({S, 2}).select(1, 0).contiguous();
+    auto nleft = torch::zeros({S}, i32);
+    auto ridx_new = torch::empty_like(ridx);
+    if (n > 0)
+      TORCH_CHECK(wh::gbdt_partition_cursor(ptr<uint8_t>(B), ptr<uint8_t>(Bc), B.size(0), F,
+                                            ptr<int32_t>(ridx), n, ptr<int32_t>(sbeg), d_iota, S,
+                                            pfeat, pfeat + S, pdefl, pfeat + 2 * S, pfeat + 3 * S,
+                                            ptr<int32_t>(sbeg), S, ptr<int32_t>(nleft),
+                                            ptr<int32_t>(ridx_new), s),
+                  "gbdt_grow_dev: partition refused the segment table");
+    ridx = ridx_new;
+    // next level's segments, the built children, their histogram tasks
+    const int64_t ub = ((n + chunk - 1) / chunk + S) * G;  // >= the tasks of the built children
+    auto seg_next = torch::empty({4 * S}, i32);
+    auto alive_next = torch::empty({2 * S}, u8);
+    auto dseg = torch::empty({2 * S}, i32);
+    auto sp = torch::empty({5 * S + 1}, i32);  // sp [S x 4] | par [S] | ntask
+    auto tasks = torch::empty({std::max<int64_t>(ub, 1) * 5}, i32);
+    auto red = torch::empty({(int64_t)S * G * 6}, i32);
+    TORCH_CHECK(wh::gbdt_dev_children(S, ptr<int32_t>(seg_cur), pdefl + S, pdefl + 2 * S,
+                                      ptr<int32_t>(nleft), d_fg, G, chunk, ptr<int32_t>(seg_next),
+                                      ptr<uint8_t>(alive_next), ptr<int32_t>(dseg),
+                                      ptr<int32_t>(sp), ptr<int32_t>(sp) + 4 * S, ptr<int32_t>(tasks),
+                                      ptr<int32_t>(sp) + 5 * S, ptr<int32_t>(red), s),
+                "gbdt_grow_dev: too many slots");
+    auto hs = torch::empty({S, F, nbin, 2}, f64);
+    auto part = torch::empty({std::max<int64_t>(ub, 1) * pstride}, gpair.options().dtype(torch::kInt64));
+    wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
+                  ptr<float>(qscale), ptr<int32_t>(tasks), (int)std::max<int64_t>(ub, 1),
+                  ptr<int32_t>(red), S * G, (int)max_fcnt, dw, ptr<int64_t>(part),
+                  ptr<double>(hs), s, ptr<int32_t>(dseg), chunk, ptr<int32_t>(sp) + 5 * S);
+    if (reduce) allreduce(hs);
+    auto H_next = torch::empty({2 * S, F, nbin, 2}, f64);
+    wh::gbdt_sibling(ptr<double>(H_front), ptr<double>(hs), ptr<int32_t>(sp),
+                     ptr<int32_t>(sp) + 4 * S, S, per, ptr<double>(H_next), s);
+    H_front = H_next;
+    tot_cur = tot_next;
+    seg_cur = seg_next;
+    alive_cur = alive_next;
+  }
+  // the finished tree: ONE host read, renumbered breadth-first (the host
+  // grower's creation order)
+  auto hn = nodes.cpu();
+  const double* r = hn.data_ptr<double>();
+  std::vector<int> id_of(NN, -1), order;
+  for (int h = 0; h < NN; ++h)
+    if (r[(int64_t)h * REC] != 0.0) {
+      id_of[h] = (int)order.size();
+      order.push_back(h);
+    }
+  const size_t M = order.size();
+  std::vector<int> feat(M), bin(M), defl(M), left(M, -1), right(M, -1), parent(M, -1);
+  std::vector<double> gain(M), cover(M), bw(M), leaf(M);
+  std::vector<float> cond(M, 0.f);
+  py::list segs;
+  for (size_t i = 0; i < M; ++i) {
+    const int h = order[i];
+    const double* q = r + (int64_t)h * REC;
+    feat[i] = (int)q[1], bin[i] = (int)q[2], defl[i] = (int)q[3];
+    gain[i] = q[4], cover[i] = q[5], bw[i] = q[6], leaf[i] = q[7];
+    if (feat[i] >= 0) {
+      left[i] = id_of[2 * h + 1], right[i] = id_of[2 * h + 2];
+      TORCH_CHECK(left[i] >= 0 && right[i] >= 0, "gbdt_grow_dev: a split node lost a child");
+      parent[left[i]] = (int)i, parent[right[i]] = (int)i;
+      cond[i] = cut_vals[cut_off[feat[i]] + bin[i]];
+    } else {
+      segs.append(py::make_tuple((int)i, (int)q[8], (int)q[9]));
+    }
+  }
+  return py::make_tuple(feat, bin, cond, defl, left, right, parent, gain, cover, bw, leaf, segs,
+                        ridx);
+}
+
 }  // namespace
 
 // ------------------------------------------------------ native P=1 step
@@ -2822,6 +2990,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_update", &kmeans_update);
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
   m.def("gbdt_grow", &gbdt_grow);
+  m.def("gbdt_grow_dev", &gbdt_grow_dev);
   m.def("gbdt_gpair", &gbdt_gpair);
   // the ingest ops block on one small device read each: the GIL is released
   // so a producer thread's parsing overlaps the training loop

@@ -100,8 +100,11 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(const uint8_t* __restrict
                                                        const HistTask* __restrict__ tasks,
                                                        long long* __restrict__ part,
                                                        int64_t pstride,
-                                                       const int32_t* __restrict__ dseg) {
+                                                       const int32_t* __restrict__ dseg,
+                                                       const int32_t* __restrict__ ntask_dev) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds64[];
+  // (a device-built task list: the grid is its upper bound)
+  if (ntask_dev && (int)blockIdx.x >= *ntask_dev) return;
   HistTask tk = tasks[blockIdx.x];
   if (dseg) {  // dynamic rows: {chunk index, chunk rows} of the slot's device segment
     const int32_t sb = dseg[2 * tk.node], se = dseg[2 * tk.node + 1];
@@ -378,7 +381,7 @@ int64_t gbdt_hist_pstride(int max_fcnt, int nbin) { return ((int64_t)2 * max_fcn
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
                const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
                int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s,
-               const int32_t* dseg, int chunk) {
+               const int32_t* dseg, int chunk, const int32_t* ntask_dev) {
   if (ntask <= 0) return;
   static bool attr = false;
   if (!attr) {  // dynamic LDS above 64 KB must be opted into per kernel
@@ -395,14 +398,14 @@ void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const flo
   auto* pt = reinterpret_cast<long long*>(part);
   if (dword_rows)
     hipLaunchKernelGGL(k_hist<true>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx, gp,
-                       qscale, tk, pt, ps, dseg);
+                       qscale, tk, pt, ps, dseg, ntask_dev);
   else
     hipLaunchKernelGGL(k_hist<false>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx,
-                       gp, qscale, tk, pt, ps, dseg);
+                       gp, qscale, tk, pt, ps, dseg, ntask_dev);
   if (nred > 0)
     hipLaunchKernelGGL(k_hist_reduce, dim3((unsigned)((2 * max_fcnt * nbin + kRedE - 1) / kRedE), nred),
                        dim3(kRedE * kRedK), 0, s, pt, ps, reinterpret_cast<const HistReduce*>(red), f, nbin,
-                       qscale, hist, dseg, chunk);
+                       qscale, hist, ntask_dev ? nullptr : dseg, chunk);
 }
 
 // Level bookkeeping on the device (the host tree grower, csrc/bind/gbdt_grow.cc):
@@ -709,6 +712,172 @@ void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const f
   if (n <= 0) return;
   hipLaunchKernelGGL(k_predict, dim3(grid_for(n, 256)), dim3(256), 0, s, X, n, f, feat, thr, left,
                      right, defl, leaf, margin);
+}
+
+}  // namespace wh
+
+namespace wh {
+namespace {
+
+// ---- the level loop on the device (gbdt_grow_dev) --------------------------
+// Heap-numbered nodes: depth d holds slots s = 0..2^d - 1, node id 2^d - 1 + s,
+// children 2s / 2s + 1 at depth d + 1. Every slot owns a segment of ridx;
+// the segments of a depth tile [0, n) in slot order (a dead slot -- the
+// child of a leaf -- is empty, or carries its leaf parent's rows as one
+// "stay put" segment), so the one-pass cursor partition (k_part_cursor) runs
+// on the device's segment table. Node record (doubles): {alive, feat, bin,
+// defl, gain, cover, base weight, leaf, begin, end}.
+constexpr int kNodeRec = 10;
+
+// One block: for slot s of depth d (S slots), decide its split from the
+// split search's result, record the node, and set up the partition and the
+// next level's totals (the host grower's level bookkeeping).
+__global__ __launch_bounds__(256) void k_gd_apply(
+    int S, int node0, int last, const double* __restrict__ so, const double* __restrict__ tot,
+    const int32_t* __restrict__ seg, const uint8_t* __restrict__ alive, double eta, double alpha,
+    double lambda, double mcw, double rt_eps, double* __restrict__ nodes,
+    int32_t* __restrict__ pfeat, int32_t* __restrict__ pbin, uint8_t* __restrict__ pdefl,
+    int32_t* __restrict__ lcur, int32_t* __restrict__ rcur, uint8_t* __restrict__ split,
+    uint8_t* __restrict__ build_left, double* __restrict__ tot_next) {
+  for (int sl = threadIdx.x; sl < S; sl += blockDim.x) {
+    const double G = tot[2 * sl], H = tot[2 * sl + 1];
+    const int b = seg[2 * sl], e = seg[2 * sl + 1];
+    double* nd = nodes + (int64_t)(node0 + sl) * kNodeRec;
+    const bool al = alive[sl] != 0;
+    const double* o = so + (int64_t)sl * 6;
+    const bool sp = al && !last && o[0] > rt_eps;
+    double bw = 0.0;
+    if (H >= mcw) {
+      const double g = alpha <= 0 ? G : (G > alpha ? G - alpha : (G < -alpha ? G + alpha : 0.0));
+      bw = -g / (H + lambda);
+    }
+    nd[0] = al ? 1.0 : 0.0;
+    nd[1] = sp ? o[1] : -1.0;
+    nd[2] = sp ? o[2] : 0.0;
+    nd[3] = sp ? o[3] : 0.0;
+    nd[4] = sp ? o[0] : 0.0;
+    nd[5] = H;
+    nd[6] = bw;
+    nd[7] = eta * bw;
+    nd[8] = b;
+    nd[9] = e;
+    pfeat[sl] = sp ? (int32_t)o[1] : -1;
+    pbin[sl] = sp ? (int32_t)o[2] : 0;
+    pdefl[sl] = sp ? (uint8_t)o[3] : 0;
+    lcur[sl] = b;
+    rcur[sl] = e;
+    split[sl] = sp ? 1 : 0;
+    const double GL = sp ? o[4] : 0.0, HL = sp ? o[5] : 0.0;
+    const double GR = sp ? G - GL : 0.0, HR = sp ? H - HL : 0.0;
+    build_left[sl] = HL <= HR ? 1 : 0;  // build the child with the smaller global hessian
+    if (tot_next) {
+      tot_next[4 * sl] = GL;
+      tot_next[4 * sl + 1] = HL;
+      tot_next[4 * sl + 2] = GR;
+      tot_next[4 * sl + 3] = HR;
+    }
+  }
+}
+
+// One block (S <= 1024 slots): the next level's segments / alive flags, the
+// built children's rows (dseg), the sibling table, and the histogram task
+// list of the built children: per slot ceil(rows / chunk) chunks x G feature
+// groups (offsets by a block scan), its count, and the reduce entries.
+__global__ __launch_bounds__(1024) void k_gd_children(
+    int S, const int32_t* __restrict__ seg, const uint8_t* __restrict__ split,
+    const uint8_t* __restrict__ build_left, const int32_t* __restrict__ nleft,
+    const int32_t* __restrict__ fg, int G, int chunk, int32_t* __restrict__ seg_next,
+    uint8_t* __restrict__ alive_next, int32_t* __restrict__ dseg, int32_t* __restrict__ sp,
+    int32_t* __restrict__ par, HistTask* __restrict__ tasks, int32_t* __restrict__ ntask,
+    HistReduce* __restrict__ red) {
+  __shared__ int32_t ws[16];
+  const int sl = threadIdx.x, lane = sl & 63, w = sl >> 6;
+  int32_t nch = 0, b = 0, e = 0, m = 0;
+  bool s_ = false;
+  if (sl < S) {
+    b = seg[2 * sl];
+    e = seg[2 * sl + 1];
+    s_ = split[sl] != 0;
+    m = s_ ? b + nleft[sl] : e;
+    seg_next[4 * sl] = b;
+    seg_next[4 * sl + 1] = m;
+    seg_next[4 * sl + 2] = m;
+    seg_next[4 * sl + 3] = e;
+    alive_next[2 * sl] = alive_next[2 * sl + 1] = s_ ? 1 : 0;
+    const bool bl = build_left[sl] != 0;
+    const int32_t db = s_ ? (bl ? b : m) : 0, de = s_ ? (bl ? m : e) : 0;
+    dseg[2 * sl] = db;
+    dseg[2 * sl + 1] = de;
+    sp[4 * sl] = sl;
+    sp[4 * sl + 1] = b;
+    sp[4 * sl + 2] = e;
+    sp[4 * sl + 3] = bl ? 1 : 0;
+    par[sl] = sl;
+    nch = s_ ? (de - db + chunk - 1) / chunk : 0;
+  }
+  // exclusive scan of the chunk counts
+  int32_t x = nch;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) ws[w] = x;
+  __syncthreads();
+  int32_t base = x - nch, tot = 0;
+  for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
+    if (q < w) base += ws[q];
+    tot += ws[q];
+  }
+  if (sl < S) {
+    for (int c = 0; c < nch; ++c)
+      for (int gi = 0; gi < G; ++gi) {
+        HistTask t;
+        t.node = sl;
+        t.fbeg = fg[2 * gi];
+        t.fcnt = fg[2 * gi + 1];
+        t.rbeg = c;
+        t.rend = chunk;
+        tasks[(int64_t)(base + c) * G + gi] = t;
+      }
+    for (int gi = 0; gi < G; ++gi) {
+      HistReduce r;
+      r.node = sl;
+      r.fbeg = fg[2 * gi];
+      r.fcnt = fg[2 * gi + 1];
+      r.t0 = base * G + gi;
+      r.nt = nch;
+      r.tstride = G;
+      red[(int64_t)sl * G + gi] = r;
+    }
+  }
+  if (sl == 0) *ntask = tot * G;
+}
+
+}  // namespace
+
+int gbdt_node_rec() { return kNodeRec; }
+
+void gbdt_dev_apply(int S, int node0, bool last, const double* so, const double* tot,
+                    const int32_t* seg, const uint8_t* alive, double eta, double alpha,
+                    double lambda, double mcw, double rt_eps, double* nodes, int32_t* pfeat,
+                    int32_t* pbin, uint8_t* pdefl, int32_t* lcur, int32_t* rcur, uint8_t* split,
+                    uint8_t* build_left, double* tot_next, hipStream_t s) {
+  hipLaunchKernelGGL(k_gd_apply, dim3(1), dim3(256), 0, s, S, node0, last ? 1 : 0, so, tot, seg,
+                     alive, eta, alpha, lambda, mcw, rt_eps, nodes, pfeat, pbin, pdefl, lcur, rcur,
+                     split, build_left, tot_next);
+}
+
+bool gbdt_dev_children(int S, const int32_t* seg, const uint8_t* split, const uint8_t* build_left,
+                       const int32_t* nleft, const int32_t* fg, int G, int chunk,
+                       int32_t* seg_next, uint8_t* alive_next, int32_t* dseg, int32_t* sp,
+                       int32_t* par, int32_t* tasks, int32_t* ntask, int32_t* red,
+                       hipStream_t s) {
+  if (S > 1024) return false;
+  hipLaunchKernelGGL(k_gd_children, dim3(1), dim3(1024), 0, s, S, seg, split, build_left, nleft,
+                     fg, G, chunk, seg_next, alive_next, dseg, sp, par,
+                     reinterpret_cast<HistTask*>(tasks), ntask, reinterpret_cast<HistReduce*>(red));
+  return true;
 }
 
 }  // namespace wh

@@ -427,7 +427,22 @@ int64_t gbdt_hist_pstride(int max_fcnt, int nbin);
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
                const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
                int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s,
-               const int32_t* dseg = nullptr, int chunk = 0);
+               const int32_t* dseg = nullptr, int chunk = 0,
+               const int32_t* ntask_dev = nullptr);
+// ntask_dev (optional): the task count of a device-built list (ntask is then
+// its upper bound; the reduce entries carry exact task counts)
+// ---- the level loop on the device (gbdt_grow_dev in csrc/bind/hip_ops.cc)
+int gbdt_node_rec();
+void gbdt_dev_apply(int S, int node0, bool last, const double* so, const double* tot,
+                    const int32_t* seg, const uint8_t* alive, double eta, double alpha,
+                    double lambda, double mcw, double rt_eps, double* nodes, int32_t* pfeat,
+                    int32_t* pbin, uint8_t* pdefl, int32_t* lcur, int32_t* rcur, uint8_t* split,
+                    uint8_t* build_left, double* tot_next, hipStream_t s);
+bool gbdt_dev_children(int S, const int32_t* seg, const uint8_t* split, const uint8_t* build_left,
+                       const int32_t* nleft, const int32_t* fg, int G, int chunk,
+                       int32_t* seg_next, uint8_t* alive_next, int32_t* dseg, int32_t* sp,
+                       int32_t* par, int32_t* tasks, int32_t* ntask, int32_t* red,
+                       hipStream_t s);
 // dseg (optional) [slots x 2] device row segments: a task's {rbeg, rend} is
 // then {chunk index, chunk rows} inside its slot's segment (empty past it)
 // level bookkeeping of the device-resident tree grower (see gbdt.hip)

@@ -20,6 +20,7 @@ Algorithm (xgboost "hist" semantics, row split ``dsplit=row``):
   leaf segments, other sets by a device tree walk.
 """
 import math
+import os
 import struct
 
 import numpy as np
@@ -733,7 +734,12 @@ class TreeBuilder:
         if not hasattr(self, "_cut_lists"):
             self._cut_lists = (self.cuts.values.tolist(), self.cuts.offsets.tolist())
         ar = (lambda t: self.bsp.allreduce(t)) if self.bsp.world > 1 else None
-        out = _native.hip().gbdt_grow(
+        # the level loop on the device (one host read per tree) unless the
+        # per-level host grower is asked for; every rank takes the same one
+        # (WH_GBDT_GROWER is process-wide, set alike on every rank)
+        grow = (_native.hip().gbdt_grow if os.environ.get("WH_GBDT_GROWER", "") == "host"
+                or p.max_depth > 10 else _native.hip().gbdt_grow_dev)
+        out = grow(
             self.B, self._Bc, self._iota(n), gpair,
             self._qscale, self._valid_dev[1], self.nbin, self.fgroups, self.max_fcnt,
             tot.cpu().tolist(), self._cut_lists[0], self._cut_lists[1], float(p.eta),
