@@ -674,16 +674,37 @@ __global__ __launch_bounds__(kGpThreads) void k_gpair(int64_t n, const float* __
     last = arrive_last(ticket, blockIdx.x, gridDim.x);
   }
   __syncthreads();
-  if (!last || threadIdx.x != 0) return;
+  if (!last) return;
+  // the last block sums the partials: thread t takes blocks t, t + 256, ...
+  // (all loads in flight; one serial walk cost ~200 us of load latency), then
+  // a fixed-order tree -- the same sums every run
   double v[4] = {0, 0, 0, 0};
   const unsigned long long* pp = reinterpret_cast<const unsigned long long*>(part);
-  for (unsigned b = 0; b < gridDim.x; ++b) {  // (block order: the same sum every run)
+  for (unsigned b = threadIdx.x; b < gridDim.x; b += kGpThreads) {
     v[0] += __longlong_as_double((long long)lb_load(pp + b * 4));
     v[1] += __longlong_as_double((long long)lb_load(pp + b * 4 + 1));
     v[2] = fmax(v[2], __longlong_as_double((long long)lb_load(pp + b * 4 + 2)));
     v[3] = fmax(v[3], __longlong_as_double((long long)lb_load(pp + b * 4 + 3)));
   }
-  for (int q = 0; q < 4; ++q) stats[q] = v[q];
+  v[0] = wave_sum_d(v[0]);
+  v[1] = wave_sum_d(v[1]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v[2] = fmax(v[2], __shfl_xor(v[2], o, 64));
+    v[3] = fmax(v[3], __shfl_xor(v[3], o, 64));
+  }
+  __syncthreads();
+  if (lane == 0) {
+    sh[0][wid] = v[0]; sh[1][wid] = v[1]; sh[2][wid] = v[2]; sh[3][wid] = v[3];
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  double r[4] = {0, 0, 0, 0};
+  for (int w = 0; w < kGpThreads / 64; ++w) {
+    r[0] += sh[0][w]; r[1] += sh[1][w];
+    r[2] = fmax(r[2], sh[2][w]); r[3] = fmax(r[3], sh[3][w]);
+  }
+  for (int q = 0; q < 4; ++q) stats[q] = r[q];
 }
 }  // namespace
 
@@ -829,17 +850,31 @@ __global__ __launch_bounds__(1024) void k_gd_children(
     if (q < w) base += ws[q];
     tot += ws[q];
   }
+  __shared__ int32_t soff[1025];
+  if (sl < S) soff[sl] = base;
+  if (sl == 0) soff[S] = tot;
+  __syncthreads();
+  // the tasks, spread over the block: chunk q of the level belongs to the
+  // last slot whose offset is <= q (one slot's thread writing all its chunks
+  // serialised ~500 task stores at the root's children)
+  for (int q = sl; q < tot; q += blockDim.x) {
+    int lo = 0, hi = S - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (soff[mid] <= q) lo = mid;
+      else hi = mid - 1;
+    }
+    for (int gi = 0; gi < G; ++gi) {
+      HistTask t;
+      t.node = lo;
+      t.fbeg = fg[2 * gi];
+      t.fcnt = fg[2 * gi + 1];
+      t.rbeg = q - soff[lo];
+      t.rend = chunk;
+      tasks[(int64_t)q * G + gi] = t;
+    }
+  }
   if (sl < S) {
-    for (int c = 0; c < nch; ++c)
-      for (int gi = 0; gi < G; ++gi) {
-        HistTask t;
-        t.node = sl;
-        t.fbeg = fg[2 * gi];
-        t.fcnt = fg[2 * gi + 1];
-        t.rbeg = c;
-        t.rend = chunk;
-        tasks[(int64_t)(base + c) * G + gi] = t;
-      }
     for (int gi = 0; gi < G; ++gi) {
       HistReduce r;
       r.node = sl;
