@@ -1395,7 +1395,8 @@ Tensor gbdt_bin(const Tensor& X, const Tensor& cuts, const Tensor& cut_off) {
 
 // tasks [T, 5] (slot, fbeg, fcnt, rbeg, rend); red [R, 6] (slot, fbeg, fcnt,
 // t0, nt, tstride) sums the fp32 partials of tasks t0 + k * tstride into hist
-// qscale [2] float32 = {2^eg, 2^eh}: fixed-point scales of g and h (see gbdt.hip)
+// qscale [2] float32 = {2^eg, 2^eh}: fixed-point scales of g and h (see gbdt.hip);
+// [3] = {2^eg, 2^eh, R}: int32 LDS sums over <= R rows (k_hist W32)
 void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& gpair,
                const Tensor& qscale, const Tensor& tasks, const Tensor& red, int64_t max_fcnt,
                const Tensor& hist) {
@@ -1407,7 +1408,8 @@ void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& 
   CHECK_IN(hist, torch::kFloat64);
   TORCH_CHECK(nbin >= 1 && nbin <= 255, "nbin must be in [1, 255]");
   CHECK_IN(qscale, torch::kFloat32);
-  TORCH_CHECK(qscale.numel() == 2, "qscale must hold {scale_g, scale_h}");
+  TORCH_CHECK(qscale.numel() == 2 || qscale.numel() == 3,
+              "qscale must hold {scale_g, scale_h} or {scale_g, scale_h, int32 rows}");
   TORCH_CHECK(wh::gbdt_hist_lds((int)max_fcnt, (int)nbin) <= 160 * 1024, "feature group too wide");
   TORCH_CHECK(tasks.dim() == 2 && tasks.size(1) == 5);
   TORCH_CHECK(red.dim() == 2 && red.size(1) == 6);
@@ -1422,7 +1424,7 @@ void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& 
   wh::gbdt_hist(ptr<uint8_t>(B), f, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
                 ptr<float>(qscale), ptr<int32_t>(tasks), (int)tasks.size(0), ptr<int32_t>(red),
                 (int)red.size(0), (int)max_fcnt, dw, ptr<int64_t>(part), ptr<double>(hist),
-                cur_stream(B));
+                cur_stream(B), nullptr, 0, nullptr, qscale.numel() == 3);
 }
 
 // ------------------------------------------------------------------ lbfgs
@@ -2169,7 +2171,8 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
     wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
                   ptr<float>(qscale), ptr<int32_t>(hp.d), (int)hp.nt,
                   ptr<int32_t>(hp.d) + hp.nt * 5, (int)hp.nr, (int)max_fcnt, dw,
-                  ptr<int64_t>(hp.part), ptr<double>(hp.hist), s, ptr<int32_t>(dseg), chunk);
+                  ptr<int64_t>(hp.part), ptr<double>(hp.hist), s, ptr<int32_t>(dseg), chunk,
+                  nullptr, qscale.numel() == 3);
     // (no drain here: the staging ring waits for this copy only when its slot
     // comes round again; the histogram allreduce is stream-ordered)
     if (reduce) allreduce(hp.hist);
@@ -2435,7 +2438,7 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
     wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
                   ptr<float>(qscale), ptr<int32_t>(d), (int)nt, ptr<int32_t>(d) + nt * 5, G,
                   (int)max_fcnt, dw, ptr<int64_t>(part), ptr<double>(H_front), s,
-                  ptr<int32_t>(seg_cur), chunk);
+                  ptr<int32_t>(seg_cur), chunk, nullptr, qscale.numel() == 3);
     if (reduce) allreduce(H_front);
   }
   for (int d = 0; d <= D; ++d) {
@@ -2491,7 +2494,8 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
     wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
                   ptr<float>(qscale), ptr<int32_t>(tasks), (int)std::max<int64_t>(ub, 1),
                   ptr<int32_t>(red), S * G, (int)max_fcnt, dw, ptr<int64_t>(part),
-                  ptr<double>(hs), s, ptr<int32_t>(dseg), chunk, ptr<int32_t>(sp) + 5 * S);
+                  ptr<double>(hs), s, ptr<int32_t>(dseg), chunk, ptr<int32_t>(sp) + 5 * S,
+                  qscale.numel() == 3);
     if (reduce) allreduce(hs);
     auto H_next = torch::empty({2 * S, F, nbin, 2}, f64);
     wh::gbdt_sibling(ptr<double>(H_front), ptr<double>(hs), ptr<int32_t>(sp),

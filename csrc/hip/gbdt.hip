@@ -81,6 +81,20 @@ __device__ __forceinline__ void hist_add(unsigned long long* lds, int nbin, int 
   }
 }
 
+// 32-bit variant (W32): the caller picks the scale so that |q| <= 2^31 / R
+// for every row (R = qscale[2] rows); a block sums at most R rows in int32
+// LDS, adds them into its int64 partial and starts again.  ds_add_u32 issues
+// ~2x the rate of ds_add_u64 and the histogram takes half the LDS.  Rows are
+// rounded with the same scale in every block, so the sums stay exact integers:
+// any chunking, grower or the CSR kernel gives bit-identical histograms.
+__device__ __forceinline__ void hist_add32(unsigned* lds, int nbin, int fj, int b, int qg,
+                                           int qh) {
+  if (b != kMissing) {
+    atomicAdd(&lds[2 * (fj * nbin + b)], (unsigned)qg);
+    atomicAdd(&lds[2 * (fj * nbin + b) + 1], (unsigned)qh);
+  }
+}
+
 // LDS-privatised histogram of one task, written (not atomically added) to the
 // task's int64 partial slice; k_hist_reduce sums the slices per (node, group).
 // Plain coalesced stores instead of a per-block atomic flush make small row
@@ -92,7 +106,9 @@ __device__ __forceinline__ void hist_add(unsigned long long* lds, int nbin, int 
 // instead of one byte per lane per feature.  Four row batches are loaded
 // before any LDS atomic is issued, keeping 4 dependent gathers in flight per
 // wave.  Otherwise one thread per row walks the group's bytes.
-template <bool DW>
+//
+// W32: qscale = {2^eg, 2^eh, R}: int32 LDS sums over sub-batches of <= R rows.
+template <bool DW, bool W32>
 __global__ __launch_bounds__(kHistThreads) void k_hist(const uint8_t* __restrict__ B, int f,
                                                        int nbin, const int32_t* __restrict__ ridx,
                                                        const float2* __restrict__ gpair,
@@ -115,54 +131,84 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(const uint8_t* __restrict
   }
   const float sg = qscale[0], sh = qscale[1];
   const int nl2 = 2 * tk.fcnt * nbin;
-  for (int i = threadIdx.x; i < nl2; i += blockDim.x) lds64[i] = 0ull;
-  __syncthreads();
-  const int nrow = tk.rend - tk.rbeg;
-  const int32_t* rid = ridx + tk.rbeg;
-  if (DW) {
-    constexpr int U = 4;
-    const int D = tk.fcnt >> 2;
-    const int R = 64 / D;  // rows per wave batch
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int ri = lane / D, dj = lane - ri * D;
-    const bool act = ri < R;
-    const uint8_t* Bg = B + tk.fbeg + 4 * dj;
-    for (int base = wave * R; base < nrow; base += nw * R * U) {
-      uint32_t word[U];
-      float2 g[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int r = base + u * nw * R + ri;
-        const bool ok = act && r < nrow;
-        const int row = ok ? rid[r] : 0;
-        word[u] = ok ? *reinterpret_cast<const uint32_t*>(Bg + (int64_t)row * f) : 0xffffffffu;
-        g[u] = ok ? gpair[row] : make_float2(0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const long long qg = __float2ll_rn(g[u].x * sg), qh = __float2ll_rn(g[u].y * sh);
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          hist_add(lds64, nbin, 4 * dj + c, (word[u] >> (8 * c)) & 255, qg, qh);
-      }
-    }
-  } else {
-    const int lane = threadIdx.x & 63;
-    for (int r = threadIdx.x; r < nrow; r += blockDim.x) {
-      const int row = rid[r];
-      const float2 gh = gpair[row];
-      const long long qg = __float2ll_rn(gh.x * sg), qh = __float2ll_rn(gh.y * sh);
-      const uint8_t* brow = B + (int64_t)row * f + tk.fbeg;
-      int fj = lane % tk.fcnt;  // lane-rotated feature order spreads the atomics
-      for (int q = 0; q < tk.fcnt; ++q) {
-        hist_add(lds64, nbin, fj, brow[fj], qg, qh);
-        fj = fj + 1 == tk.fcnt ? 0 : fj + 1;
-      }
-    }
-  }
-  __syncthreads();
+  const int nall = tk.rend - tk.rbeg;
+  unsigned* lds32 = reinterpret_cast<unsigned*>(lds64);
+  const int R = W32 ? max(1, (int)qscale[2]) : max(1, nall);
   long long* out = part + (int64_t)blockIdx.x * pstride;
-  for (int i = threadIdx.x; i < nl2; i += blockDim.x) out[i] = (long long)lds64[i];
+  int r0 = 0;
+  do {  // (one pass unless W32 and the task holds more than R rows)
+    if (W32)
+      for (int i = threadIdx.x; i < nl2; i += blockDim.x) lds32[i] = 0u;
+    else
+      for (int i = threadIdx.x; i < nl2; i += blockDim.x) lds64[i] = 0ull;
+    __syncthreads();
+    const int nrow = min(R, nall - r0);
+    const int32_t* rid = ridx + tk.rbeg + r0;
+    if (DW) {
+      constexpr int U = 4;
+      const int D = tk.fcnt >> 2;
+      const int RW = 64 / D;  // rows per wave batch
+      const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+      const int ri = lane / D, dj = lane - ri * D;
+      const bool act = ri < RW;
+      const uint8_t* Bg = B + tk.fbeg + 4 * dj;
+      for (int base = wave * RW; base < nrow; base += nw * RW * U) {
+        uint32_t word[U];
+        float2 g[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int r = base + u * nw * RW + ri;
+          const bool ok = act && r < nrow;
+          const int row = ok ? rid[r] : 0;
+          word[u] = ok ? *reinterpret_cast<const uint32_t*>(Bg + (int64_t)row * f) : 0xffffffffu;
+          g[u] = ok ? gpair[row] : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (W32) {
+            const int qg = __float2int_rn(g[u].x * sg), qh = __float2int_rn(g[u].y * sh);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              hist_add32(lds32, nbin, 4 * dj + c, (word[u] >> (8 * c)) & 255, qg, qh);
+          } else {
+            const long long qg = __float2ll_rn(g[u].x * sg), qh = __float2ll_rn(g[u].y * sh);
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              hist_add(lds64, nbin, 4 * dj + c, (word[u] >> (8 * c)) & 255, qg, qh);
+          }
+        }
+      }
+    } else {
+      const int lane = threadIdx.x & 63;
+      for (int r = threadIdx.x; r < nrow; r += blockDim.x) {
+        const int row = rid[r];
+        const float2 gh = gpair[row];
+        const uint8_t* brow = B + (int64_t)row * f + tk.fbeg;
+        int fj = lane % tk.fcnt;  // lane-rotated feature order spreads the atomics
+        if (W32) {
+          const int qg = __float2int_rn(gh.x * sg), qh = __float2int_rn(gh.y * sh);
+          for (int q = 0; q < tk.fcnt; ++q) {
+            hist_add32(lds32, nbin, fj, brow[fj], qg, qh);
+            fj = fj + 1 == tk.fcnt ? 0 : fj + 1;
+          }
+        } else {
+          const long long qg = __float2ll_rn(gh.x * sg), qh = __float2ll_rn(gh.y * sh);
+          for (int q = 0; q < tk.fcnt; ++q) {
+            hist_add(lds64, nbin, fj, brow[fj], qg, qh);
+            fj = fj + 1 == tk.fcnt ? 0 : fj + 1;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // each thread owns the same elements in every pass: no race on out
+    for (int i = threadIdx.x; i < nl2; i += blockDim.x) {
+      const long long v = W32 ? (long long)(int)lds32[i] : (long long)lds64[i];
+      out[i] = r0 == 0 ? v : out[i] + v;
+    }
+    __syncthreads();  // before the next pass clears the LDS
+    r0 += R;
+  } while (r0 < nall);
 }
 
 // One block = 64 consecutive elements x 16 task slices: thread (e, k) sums
@@ -381,27 +427,25 @@ int64_t gbdt_hist_pstride(int max_fcnt, int nbin) { return ((int64_t)2 * max_fcn
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
                const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
                int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s,
-               const int32_t* dseg, int chunk, const int32_t* ntask_dev) {
+               const int32_t* dseg, int chunk, const int32_t* ntask_dev, bool w32) {
   if (ntask <= 0) return;
   static bool attr = false;
   if (!attr) {  // dynamic LDS above 64 KB must be opted into per kernel
-    WH_HIP_CHECK(hipFuncSetAttribute((const void*)k_hist<true>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, kHistLdsMax));
-    WH_HIP_CHECK(hipFuncSetAttribute((const void*)k_hist<false>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, kHistLdsMax));
+    const void* ks[4] = {(const void*)k_hist<true, false>, (const void*)k_hist<false, false>,
+                         (const void*)k_hist<true, true>, (const void*)k_hist<false, true>};
+    for (const void* k : ks)
+      WH_HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kHistLdsMax));
     attr = true;
   }
   const int64_t ps = gbdt_hist_pstride(max_fcnt, nbin);
-  const size_t lds = gbdt_hist_lds(max_fcnt, nbin);
+  const size_t lds = gbdt_hist_lds(max_fcnt, nbin) / (w32 ? 2 : 1);
   const auto* tk = reinterpret_cast<const HistTask*>(tasks);
   const auto* gp = reinterpret_cast<const float2*>(gpair);
   auto* pt = reinterpret_cast<long long*>(part);
-  if (dword_rows)
-    hipLaunchKernelGGL(k_hist<true>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx, gp,
-                       qscale, tk, pt, ps, dseg, ntask_dev);
-  else
-    hipLaunchKernelGGL(k_hist<false>, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx,
-                       gp, qscale, tk, pt, ps, dseg, ntask_dev);
+  auto kern = dword_rows ? (w32 ? k_hist<true, true> : k_hist<true, false>)
+                         : (w32 ? k_hist<false, true> : k_hist<false, false>);
+  hipLaunchKernelGGL(kern, dim3(ntask), dim3(kHistThreads), lds, s, B, f, nbin, ridx, gp, qscale, tk,
+                     pt, ps, dseg, ntask_dev);
   if (nred > 0)
     hipLaunchKernelGGL(k_hist_reduce, dim3((unsigned)((2 * max_fcnt * nbin + kRedE - 1) / kRedE), nred),
                        dim3(kRedE * kRedK), 0, s, pt, ps, reinterpret_cast<const HistReduce*>(red), f, nbin,

@@ -428,7 +428,9 @@ void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const flo
                const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
                int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s,
                const int32_t* dseg = nullptr, int chunk = 0,
-               const int32_t* ntask_dev = nullptr);
+               const int32_t* ntask_dev = nullptr, bool w32 = false);
+// w32: qscale holds {2^eg, 2^eh, R} and the blocks sum <= R rows at a time in
+// int32 (see k_hist)
 // ntask_dev (optional): the task count of a device-built list (ntask is then
 // its upper bound; the reduce entries carry exact task counts)
 // ---- the level loop on the device (gbdt_grow_dev in csrc/bind/hip_ops.cc)

@@ -1,5 +1,6 @@
 """End-to-end apps on the GPU (single process, HIP kernels): the PS learners
 (demo confs), L-BFGS linear/FM, k-means; results must match the CPU path."""
+import math
 import os
 import re
 
@@ -102,10 +103,13 @@ def test_gbdt_kernels_match_cpu():
     assert abs(lc - lg) < 1e-3 * lc, (lc, lg)
 
 
+@pytest.mark.parametrize("w32", [False, True])
 @pytest.mark.parametrize("f,nbin", [(40, 255), (40, 16), (13, 200)])
-def test_gbdt_hist_kernel(f, nbin):
+def test_gbdt_hist_kernel(f, nbin, w32):
     """Per-segment histograms (dword-row and byte-row paths, one and several
-    feature groups, several row chunks per segment) vs an fp64 index_add."""
+    feature groups, several row chunks per segment) vs an fp64 index_add;
+    w32: int32 LDS passes of <= 4096 rows (three per chunk) over rows rounded
+    to the given scale: exact sums of the rounded values."""
     from wormhole_amd import _native
     g = torch.Generator().manual_seed(f + nbin)
     n = 300000
@@ -132,6 +136,12 @@ def test_gbdt_hist_kernel(f, nbin):
     dev = torch.device("cuda", 0)
     hist = torch.zeros(len(segs), f, nbin, 2, dtype=torch.float64, device=dev)
     qscale = torch.tensor([2.0 ** 30, 2.0 ** 31], device=dev)
+    if w32:
+        R = 4096
+        sc = [2.0 ** math.floor(math.log2(2 ** 30 / (R * float(gp[:, c].abs().max()))))
+              for c in range(2)]
+        qscale = torch.tensor(sc + [float(R)], device=dev)
+        gp = torch.stack([torch.round(gp[:, c] * sc[c]) / sc[c] for c in range(2)], 1)
     _native.hip().gbdt_hist(B.to(dev), nbin, ridx.to(dev), gp.to(dev), qscale,
                             torch.tensor(tasks, dtype=torch.int32, device=dev),
                             torch.tensor(red, dtype=torch.int32, device=dev),
@@ -145,6 +155,7 @@ def test_gbdt_hist_kernel(f, nbin):
         for c in range(2):
             ref[:, c].index_add_(0, flat, gp[rows, c].double()[:, None].expand(-1, f)[ok])
         # int64 fixed point: exact up to the 2^-30 rounding of each gradient
+        # (w32: gp is pre-rounded to the scale, so the sums are exact)
         torch.testing.assert_close(hist[s].cpu().view(-1, 2), ref, rtol=1e-9, atol=1e-6)
 
 
@@ -172,12 +183,16 @@ def test_kmeans_gpu_matches_cpu(work, monkeypatch):
         assert max(abs(x - y) for x, y in zip(a, b)) < 1e-3
 
 
-@pytest.mark.parametrize("gamma,colsample", [(0.0, 1.0), (2.0, 0.6)])
-def test_gbdt_native_grower_matches_python_loop(gamma, colsample):
+@pytest.mark.parametrize("gamma,colsample,hist", [(0.0, 1.0, "32"), (2.0, 0.6, "32"),
+                                                  (0.0, 1.0, "64")])
+def test_gbdt_native_grower_matches_python_loop(gamma, colsample, hist, monkeypatch):
     """The C++ level loop (one sync per level, device child segments, fused
     sibling subtraction) grows the same trees as the Python level loop on the
     same GPU kernels (fixed-point histograms: exact), including gamma pruning
-    (leaf values looked up before the BFS renumbering) and colsample."""
+    (leaf values looked up before the BFS renumbering) and colsample.  The
+    two loops cut rows into different chunks; both histogram precisions must
+    give bit-identical sums for any chunking."""
+    monkeypatch.setenv("WH_GBDT_HIST", hist)
     from wormhole_amd.models import gbdt as G
     from wormhole_amd.parallel.bsp import BSP
     g = torch.Generator().manual_seed(2)

@@ -31,6 +31,7 @@ from ..utils.fs import open_uri  # noqa: E402
 
 RT_EPS = 1e-6
 MISSING_BIN = 255
+_HIST32_ROWS = 8192  # rows per int32 LDS pass of the GPU histogram
 
 
 # ------------------------------------------------------------------ params
@@ -587,14 +588,26 @@ class TreeBuilder:
     def _hist_scale(self, gpair):
         """Fixed-point scales {2^eg, 2^eh} of the GPU histograms: the largest
         powers of two with (global rows) * max|g| * 2^eg <= 2^61, so no node's
-        int64 sum can overflow on any rank (see csrc/hip/gbdt.hip)."""
+        int64 sum can overflow on any rank (see csrc/hip/gbdt.hip).  Unless
+        WH_GBDT_HIST=64, a third entry R selects the int32 LDS histograms:
+        every row is rounded to 2^-17 of max|g| (|q| <= 2^30 / R) and blocks
+        sum <= R rows at a time with 32-bit LDS atomics, ~2x the rate of the
+        int64 ones.  The rounding is the same in every block, so histograms
+        stay exact sums of the rounded rows (identical for any chunking)."""
         if self._nglobal is None:
             self._nglobal = max(1, int(self.bsp.allreduce_scalar(self.dm.n)))
         m = gpair_stats(gpair)[1] if self.dm.n else torch.zeros(2, device=self.device)
         m = m.float().contiguous()
         self.bsp.allreduce(m, op="max")
         e = torch.floor(torch.log2(2.0 ** 61 / (self._nglobal * m.double().clamp_min(1e-30))))
-        return torch.pow(2.0, e.clamp(-60, 100)).float()
+        if os.environ.get("WH_GBDT_HIST", "32") != "64":
+            # int32 LDS sums of <= R rows: |q| <= 2^30 / R per row (k_hist W32)
+            e32 = torch.floor(torch.log2(2.0 ** 30 / (_HIST32_ROWS * m.double().clamp_min(1e-30))))
+            e = torch.minimum(e, e32)
+            rows = torch.full((1,), float(_HIST32_ROWS), dtype=torch.float64, device=e.device)
+            return torch.cat([torch.pow(2.0, e.clamp(-60, 100)), rows]).float()
+        scale = torch.pow(2.0, e.clamp(-60, 100))
+        return scale.float()
 
     def sample_features(self, gen):
         """colsample_bytree: restrict this tree's candidate features."""
