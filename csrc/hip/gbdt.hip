@@ -504,6 +504,7 @@ __global__ __launch_bounds__(kPcThreads) void k_part_cursor(
   __shared__ int32_t s_tb[kPcMaxTiles];
   __shared__ uint32_t cnt[2][kPcMaxLocal];
   __shared__ int32_t base[2][kPcMaxLocal];
+  __shared__ int32_t s_feat[kPcMaxLocal], s_bin[kPcMaxLocal], s_defl[kPcMaxLocal];
   for (int i = threadIdx.x; i < nt; i += kPcThreads) s_tb[i] = tb[i];
   for (int i = threadIdx.x; i < kPcMaxLocal; i += kPcThreads) cnt[0][i] = cnt[1][i] = 0;
   __syncthreads();
@@ -518,6 +519,25 @@ __global__ __launch_bounds__(kPcThreads) void k_part_cursor(
     return lo;
   };
   const int sg0 = seg_of(p0);
+  const int sgl = seg_of(min(p0 + kPcTile, n) - 1);
+  // the tile's segments' split rules, read once per block into LDS
+  for (int l = threadIdx.x; l < min(sgl - sg0 + 1, kPcMaxLocal); l += kPcThreads) {
+    const int nd = tn[sg0 + l];
+    const int feat = nd >= 0 ? node_feat[nd] : -1;
+    s_feat[l] = feat;
+    s_bin[l] = feat >= 0 ? node_bin[nd] : 0;
+    s_defl[l] = feat >= 0 ? (int)node_defl[nd] : 0;
+  }
+  __syncthreads();
+  auto seg_in = [&](int64_t i) {  // seg_of over [sg0, sgl] only
+    int lo = sg0, hi = sgl;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_tb[mid] <= i) lo = mid;
+      else hi = mid - 1;
+    }
+    return lo;
+  };
   int ls[kPcPer], side[kPcPer];
   uint32_t rk[kPcPer];
   int32_t rw[kPcPer];
@@ -529,31 +549,49 @@ __global__ __launch_bounds__(kPcThreads) void k_part_cursor(
     rk[u] = 0;
     rw[u] = i < n ? ridx[i] : 0;
   }
+  // every bin gather of the thread issued before the first is used
+  int bv[kPcPer];
+#pragma unroll
+  for (int u = 0; u < kPcPer; ++u) {
+    const int64_t i = p0 + u * kPcThreads + threadIdx.x;
+    bv[u] = -2;  // -2: no row / finished leaf
+    if (i >= n) continue;
+    const int l = seg_in(i) - sg0;
+    ls[u] = l;
+    int feat;
+    if (l < kPcMaxLocal) {
+      feat = s_feat[l];
+    } else {
+      const int nd = tn[sg0 + l];
+      feat = nd >= 0 ? node_feat[nd] : -1;
+    }
+    if (feat >= 0)
+      bv[u] = Bc ? Bc[(int64_t)feat * nrows + rw[u]] : B[(int64_t)rw[u] * f + feat];
+  }
 #pragma unroll
   for (int u = 0; u < kPcPer; ++u) {
     const int64_t i = p0 + u * kPcThreads + threadIdx.x;
     if (i >= n) continue;
-    const int sg = seg_of(i);
-    const int nd = tn[sg];
-    const int feat = nd >= 0 ? node_feat[nd] : -1;
-    if (feat < 0) {
+    if (bv[u] == -2) {
       out[i] = rw[u];  // finished leaf / unsplit node: the row stays put
+      ls[u] = -1;
       continue;
     }
-    const int b = Bc ? Bc[(int64_t)feat * nrows + rw[u]] : B[(int64_t)rw[u] * f + feat];
-    const int l = (b == kMissing) ? (int)node_defl[nd] : (b <= node_bin[nd] ? 1 : 0);
-    side[u] = l ? 0 : 1;
-    ls[u] = sg - sg0;
+    const int b = bv[u];
     if (ls[u] < kPcMaxLocal) {
+      const int l = (b == kMissing) ? s_defl[ls[u]] : (b <= s_bin[ls[u]] ? 1 : 0);
+      side[u] = l ? 0 : 1;
       rk[u] = atomicAdd(&cnt[side[u]][ls[u]], 1u);
     } else {  // (a tile crossing > kPcMaxLocal segments: a global cursor each)
+      const int nd = tn[sg0 + ls[u]];
+      const int l = (b == kMissing) ? (int)node_defl[nd] : (b <= node_bin[nd] ? 1 : 0);
       rk[u] = 0;
       out[l ? atomicAdd(&lcur[nd], 1) : atomicSub(&rcur[nd], 1) - 1] = rw[u];
       ls[u] = -1;
     }
   }
   __syncthreads();
-  const int nloc = min(seg_of(min(p0 + kPcTile, n) - 1) - sg0 + 1, kPcMaxLocal);
+  const int nloc = min(sgl - sg0 + 1, kPcMaxLocal);
   for (int q = threadIdx.x; q < 2 * nloc; q += kPcThreads) {
     const int sd = q / nloc, l = q - sd * nloc;
     const uint32_t c = cnt[sd][l];

@@ -338,6 +338,17 @@ class Cuts:
         return Cuts._cuts_from_sorted(f_all, v_all, w_all, dm.ncol, max_bin)
 
     @staticmethod
+    def _segsum(w, ids, nseg):
+        """Sums of w over runs of equal, nondecreasing ids in [0, nseg): by
+        prefix-sum differences -- a GPU index_add over sorted ids piles
+        every row of a run onto one fp64 atomic address (seconds at 11M x 28)."""
+        cnt = torch.bincount(ids, minlength=nseg)
+        cwp = torch.zeros(w.numel() + 1, dtype=torch.float64, device=w.device)
+        torch.cumsum(w.double(), 0, out=cwp[1:])
+        end = torch.cumsum(cnt, 0)
+        return cwp[end] - cwp[end - cnt]
+
+    @staticmethod
     def _summary(fid, v, w, ncol, m):
         """Per feature: the distinct values when there are <= m, else m
         weighted quantile points each carrying its bucket's weight."""
@@ -353,13 +364,13 @@ class Cuts:
         grp = torch.cumsum(new.long(), 0) - 1
         ng = int(grp[-1]) + 1
         fid, v = fid[new], v[new]
-        w = torch.zeros(ng, dtype=torch.float64, device=w.device).index_add_(0, grp, w)
+        w = Cuts._segsum(w, grp, ng)
         cnt = torch.bincount(fid, minlength=ncol)
         start = torch.cumsum(cnt, 0) - cnt
         big = cnt[fid] > m
         if bool(big.any()):
             cw = torch.cumsum(w, 0)
-            fw = torch.zeros(ncol, dtype=torch.float64, device=w.device).index_add_(0, fid, w)
+            fw = Cuts._segsum(w, fid, ncol)
             base = cw[start[fid]] - w[start[fid]]
             q = ((cw - base) / fw[fid].clamp_min(1e-300) * m).floor().clamp(max=m - 1)
             key = fid * (m + 1) + q.long()
@@ -370,7 +381,7 @@ class Cuts:
             last = torch.ones_like(keep_bkt)
             last[:-1] = key[1:] != key[:-1]
             bid = torch.cumsum(keep_bkt.long(), 0) - 1
-            bw = torch.zeros(int(bid[-1]) + 1, dtype=torch.float64, device=w.device).index_add_(0, bid, w)
+            bw = Cuts._segsum(w, bid, int(bid[-1]) + 1)
             keep = ~big | last
             wout = torch.where(big, bw[bid], w)
             return fid[keep], v[keep], wout[keep]
