@@ -1596,11 +1596,22 @@ std::vector<Tensor> gbdt_gpair(const Tensor& margin, const Tensor& label,
   if (!scratch[dev].defined())
     scratch[dev] = torch::zeros({wh::gbdt_gpair_scratch()}, margin.options().dtype(torch::kFloat64));
   auto gp = torch::empty({n, 2}, margin.options());
-  auto st = torch::zeros({4}, margin.options().dtype(torch::kFloat64));
+  auto st = n > 0 ? torch::empty({4}, margin.options().dtype(torch::kFloat64))  // k_gpair writes all 4
+                  : torch::zeros({4}, margin.options().dtype(torch::kFloat64));
   if (n > 0)
     wh::gbdt_gpair(n, ptr<float>(margin), ptr<float>(label), wp, logistic, ptr<float>(gp),
                    ptr<double>(scratch[dev]), ptr<double>(st), cur_stream(margin));
   return {gp, st};
+}
+
+// {2^eg, 2^eh[, R]} (f32) from m = {max|g|, max|h|} (f32 [2], on the device)
+Tensor gbdt_qscale(const Tensor& m, double nglobal, int64_t R) {
+  CHECK_IN(m, torch::kFloat32);
+  TORCH_CHECK(m.numel() == 2 && nglobal >= 1 && R >= 0, "gbdt_qscale: bad arguments");
+  c10::DeviceGuard g(m.device());
+  auto out = torch::empty({R > 0 ? 3 : 2}, m.options());
+  wh::gbdt_qscale(ptr<float>(m), nglobal, (int)R, ptr<float>(out), cur_stream(m));
+  return out;
 }
 
 void gbdt_leaf_walk(const Tensor& B, const Tensor& feat, const Tensor& bin, const Tensor& defl,
@@ -2418,7 +2429,7 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
   Tensor tot_cur = torch::tensor(root_tot, torch::TensorOptions().dtype(torch::kFloat64)).to(B.device());
   Tensor seg_cur = hdev.narrow(0, 0, 2);
   Tensor alive_cur = torch::ones({1}, u8);
-  auto nodes = torch::zeros({NN, REC}, f64);
+  auto nodes = torch::empty({NN, REC}, f64);  // every depth's apply writes all its slots' records
   const uint8_t* vp = reinterpret_cast<const uint8_t*>(valid.data_ptr());
   Tensor ridx = ridx0;
   // root histogram: the host's task list over [0, n)
@@ -2452,6 +2463,7 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                                  alpha, lambda, mcw, ptr<double>(cand), ptr<double>(so), s),
                   "gbdt_split failed");
     }
+    auto nleft = last ? Tensor() : torch::empty({S}, i32);  // zeroed by the apply kernel
     auto pi = torch::empty({4 * S}, i32);  // pfeat | pbin | lcur | rcur
     auto pb = torch::empty({3 * S}, u8);   // pdefl | split | build_left
     Tensor tot_next = last ? Tensor() : torch::empty({2 * S, 2}, f64);
@@ -2461,11 +2473,10 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                        ptr<int32_t>(seg_cur), ptr<uint8_t>(alive_cur), eta, alpha, lambda, mcw,
                        rt_eps, ptr<double>(nodes), pfeat, pfeat + S, pdefl, pfeat + 2 * S,
                        pfeat + 3 * S, pdefl + S, pdefl + 2 * S,
-                       last ? nullptr : ptr<double>(tot_next), s);
+                       last ? nullptr : ptr<double>(tot_next), last ? nullptr : ptr<int32_t>(nleft), s);
     if (last) break;
     // partition of the split slots' rows on the device segment table
     auto sbeg = seg_cur.view({S, 2}).select(1, 0).contiguous();
-    auto nleft = torch::zeros({S}, i32);
     auto ridx_new = torch::empty_like(ridx);
     if (n > 0)
       TORCH_CHECK(wh::gbdt_partition_cursor(ptr<uint8_t>(B), ptr<uint8_t>(Bc), B.size(0), F,
@@ -2996,6 +3007,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("gbdt_grow", &gbdt_grow);
   m.def("gbdt_grow_dev", &gbdt_grow_dev);
   m.def("gbdt_gpair", &gbdt_gpair);
+  m.def("gbdt_qscale", &gbdt_qscale);
   // the ingest ops block on one small device read each: the GIL is released
   // so a producer thread's parsing overlaps the training loop
   m.def("parse_criteo", &parse_criteo, py::call_guard<py::gil_scoped_release>());

@@ -790,6 +790,30 @@ __global__ __launch_bounds__(kGpThreads) void k_gpair(int64_t n, const float* __
 }
 }  // namespace
 
+namespace {
+// Histogram fixed-point scales from the (allreduced) max |g|, max |h| in one
+// launch instead of ~12 torch ops per tree (models/gbdt.py GBTree._qscale):
+// out = {2^eg, 2^eh[, R]}, e = floor(log2(2^61 / (N m))), with R > 0 also
+// <= floor(log2(2^30 / (R m))), clamped to [-60, 100].
+__global__ void k_qscale(const float* __restrict__ m, double nglobal, int R,
+                         float* __restrict__ out) {
+  const int t = threadIdx.x;
+  if (t < 2) {
+    const double mm = fmax((double)m[t], 1e-30);
+    double e = floor(log2(0x1p61 / (nglobal * mm)));
+    if (R > 0) e = fmin(e, floor(log2(0x1p30 / ((double)R * mm))));
+    e = fmin(fmax(e, -60.0), 100.0);
+    out[t] = (float)exp2(e);
+  } else if (t == 2 && R > 0) {
+    out[2] = (float)R;
+  }
+}
+}  // namespace
+
+void gbdt_qscale(const float* m, double nglobal, int R, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_qscale, dim3(1), dim3(64), 0, s, m, nglobal, R, out);
+}
+
 int64_t gbdt_gpair_scratch() { return 4 * (int64_t)kGpBlocks + kArriveWords / 2 + 1; }
 
 void gbdt_gpair(int64_t n, const float* margin, const float* label, const float* weight,
@@ -841,8 +865,9 @@ __global__ __launch_bounds__(256) void k_gd_apply(
     double lambda, double mcw, double rt_eps, double* __restrict__ nodes,
     int32_t* __restrict__ pfeat, int32_t* __restrict__ pbin, uint8_t* __restrict__ pdefl,
     int32_t* __restrict__ lcur, int32_t* __restrict__ rcur, uint8_t* __restrict__ split,
-    uint8_t* __restrict__ build_left, double* __restrict__ tot_next) {
+    uint8_t* __restrict__ build_left, double* __restrict__ tot_next, int32_t* __restrict__ nleft) {
   for (int sl = threadIdx.x; sl < S; sl += blockDim.x) {
+    if (nleft) nleft[sl] = 0;  // the partition's left counts (no memset launch)
     const double G = tot[2 * sl], H = tot[2 * sl + 1];
     const int b = seg[2 * sl], e = seg[2 * sl + 1];
     double* nd = nodes + (int64_t)(node0 + sl) * kNodeRec;
@@ -979,10 +1004,10 @@ void gbdt_dev_apply(int S, int node0, bool last, const double* so, const double*
                     const int32_t* seg, const uint8_t* alive, double eta, double alpha,
                     double lambda, double mcw, double rt_eps, double* nodes, int32_t* pfeat,
                     int32_t* pbin, uint8_t* pdefl, int32_t* lcur, int32_t* rcur, uint8_t* split,
-                    uint8_t* build_left, double* tot_next, hipStream_t s) {
+                    uint8_t* build_left, double* tot_next, int32_t* nleft, hipStream_t s) {
   hipLaunchKernelGGL(k_gd_apply, dim3(1), dim3(256), 0, s, S, node0, last ? 1 : 0, so, tot, seg,
                      alive, eta, alpha, lambda, mcw, rt_eps, nodes, pfeat, pbin, pdefl, lcur, rcur,
-                     split, build_left, tot_next);
+                     split, build_left, tot_next, nleft);
 }
 
 bool gbdt_dev_children(int S, const int32_t* seg, const uint8_t* split, const uint8_t* build_left,

@@ -439,7 +439,7 @@ void gbdt_dev_apply(int S, int node0, bool last, const double* so, const double*
                     const int32_t* seg, const uint8_t* alive, double eta, double alpha,
                     double lambda, double mcw, double rt_eps, double* nodes, int32_t* pfeat,
                     int32_t* pbin, uint8_t* pdefl, int32_t* lcur, int32_t* rcur, uint8_t* split,
-                    uint8_t* build_left, double* tot_next, hipStream_t s);
+                    uint8_t* build_left, double* tot_next, int32_t* nleft, hipStream_t s);
 bool gbdt_dev_children(int S, const int32_t* seg, const uint8_t* split, const uint8_t* build_left,
                        const int32_t* nleft, const int32_t* fg, int G, int chunk,
                        int32_t* seg_next, uint8_t* alive_next, int32_t* dseg, int32_t* sp,
@@ -514,6 +514,8 @@ void gbdt_predict_csr(const int64_t* row_off, const int32_t* fid, const float* v
 // pruned tree on the row's bins (B row-major [n, f])
 // gradient pairs of a boosting round + {sum g, sum h, max|g|, max|h|} (fp64)
 // in one launch; scratch: gbdt_gpair_scratch() doubles, the tail zeroed once
+// fixed-point histogram scales {2^eg, 2^eh[, R]} from max |g|, |h| (GBTree._qscale)
+void gbdt_qscale(const float* m, double nglobal, int R, float* out, hipStream_t s);
 int64_t gbdt_gpair_scratch();
 void gbdt_gpair(int64_t n, const float* margin, const float* label, const float* weight,
                 bool logistic, float* gpair, double* scratch, double* stats, hipStream_t s);

@@ -440,3 +440,20 @@ def test_gbdt_leaf_walk_matches_raw_value_predict():
         tree = tb.build(obj.gpair(margin, dm.label, None), margin)
         dm.predict_tree(tree, ref)
         assert torch.allclose(margin, ref, atol=1e-5), (margin - ref).abs().max()
+
+
+@pytest.mark.parametrize("r32", [0, 8192])
+def test_gbdt_qscale_kernel_matches_torch(r32):
+    """k_qscale (one launch) == the torch formula of GBTree._qscale."""
+    from wormhole_amd import _native
+    for mg, mh, n in [(0.5, 0.25, 11_000_000), (1e-7, 3.0, 1), (0.0, 0.0, 6513), (123.4, 1e-30, 10 ** 9)]:
+        m = torch.tensor([mg, mh], dtype=torch.float32, device="cuda")
+        got = _native.hip().gbdt_qscale(m, float(n), r32).cpu()
+        md = m.double().cpu().clamp_min(1e-30)
+        e = torch.floor(torch.log2(2.0 ** 61 / (n * md)))
+        if r32:
+            e = torch.minimum(e, torch.floor(torch.log2(2.0 ** 30 / (r32 * md))))
+        want = torch.pow(2.0, e.clamp(-60, 100)).float()
+        if r32:
+            want = torch.cat([want, torch.tensor([float(r32)])])
+        assert torch.equal(got, want), (mg, mh, n, got, want)

@@ -610,8 +610,11 @@ class TreeBuilder:
         m = gpair_stats(gpair)[1] if self.dm.n else torch.zeros(2, device=self.device)
         m = m.float().contiguous()
         self.bsp.allreduce(m, op="max")
+        r32 = _HIST32_ROWS if os.environ.get("WH_GBDT_HIST", "32") != "64" else 0
+        if m.is_cuda:  # one launch (csrc/hip/gbdt.hip k_qscale), same formula as below
+            return _native.hip().gbdt_qscale(m, float(self._nglobal), r32)
         e = torch.floor(torch.log2(2.0 ** 61 / (self._nglobal * m.double().clamp_min(1e-30))))
-        if os.environ.get("WH_GBDT_HIST", "32") != "64":
+        if r32:
             # int32 LDS sums of <= R rows: |q| <= 2^30 / R per row (k_hist W32)
             e32 = torch.floor(torch.log2(2.0 ** 30 / (_HIST32_ROWS * m.double().clamp_min(1e-30))))
             e = torch.minimum(e, e32)
