@@ -2391,9 +2391,11 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
 py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, const Tensor& gpair,
                         const Tensor& qscale, const Tensor& valid, int64_t nbin,
                         std::vector<std::pair<int64_t, int64_t>> fgroups, int64_t max_fcnt,
-                        std::vector<double> root_tot, std::vector<float> cut_vals,
+                        const Tensor& root_tot, std::vector<float> cut_vals,
                         std::vector<int64_t> cut_off, double eta, double alpha, double lambda,
                         double mcw, int64_t max_depth, double rt_eps, py::object allreduce) {
+  CHECK_IN(root_tot, torch::kFloat64);  // {sum g, sum h} stays on the device: no host wait
+  TORCH_CHECK(root_tot.numel() == 2, "gbdt_grow_dev: root totals are {sum g, sum h}");
   CHECK_IN(B, torch::kUInt8);
   CHECK_IN(Bc, torch::kUInt8);
   CHECK_IN(ridx0, torch::kInt32);
@@ -2426,7 +2428,7 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
   const int32_t* d_root_seg = ptr<int32_t>(hdev);
   const int32_t* d_fg = d_root_seg + 3;
   const int32_t* d_iota = d_fg + 2 * G;
-  Tensor tot_cur = torch::tensor(root_tot, torch::TensorOptions().dtype(torch::kFloat64)).to(B.device());
+  Tensor tot_cur = root_tot;
   Tensor seg_cur = hdev.narrow(0, 0, 2);
   Tensor alive_cur = torch::ones({1}, u8);
   auto nodes = torch::empty({NN, REC}, f64);  // every depth's apply writes all its slots' records

@@ -227,11 +227,10 @@ def test_gbdt_native_grower_matches_python_loop(gamma, colsample, hist, monkeypa
 
 
 @pytest.mark.parametrize("gamma,colsample,depth", [(0.0, 1.0, 6), (2.0, 0.6, 8)])
-def test_gbdt_device_level_loop_matches_host_grower(gamma, colsample, depth):
+def test_gbdt_device_level_loop_matches_host_grower(gamma, colsample, depth, monkeypatch):
     """The level loop on the device (heap-numbered nodes, device split
     bookkeeping, device-built histogram tasks, one host read per tree) grows
     the same trees and margins as the per-level host grower."""
-    from wormhole_amd import _native
     from wormhole_amd.models import gbdt as G
     from wormhole_amd.parallel.bsp import BSP
     g = torch.Generator().manual_seed(3)
@@ -247,21 +246,16 @@ def test_gbdt_device_level_loop_matches_host_grower(gamma, colsample, depth):
     cuts = G.Cuts.build(dm, 64, bsp)
     B = cuts.bin(dm)
     obj = G.Objective(p.objective)
-    hip = _native.hip()
     res = []
-    for grow in (hip.gbdt_grow_dev, hip.gbdt_grow):
+    for grower in ("dev", "host"):  # (the builder calls the device loop by default)
+        monkeypatch.setenv("WH_GBDT_GROWER", grower)
         margin = torch.zeros(n, device=dev)
         tb = G.TreeBuilder(p, bsp, dm, cuts, B)
         gen = torch.Generator().manual_seed(5)
         trees = []
-        real = hip.gbdt_grow_dev
-        hip.gbdt_grow_dev = grow  # (the builder calls the device loop by default)
-        try:
-            for _ in range(3):
-                tb.sample_features(gen)
-                trees.append(tb._build_native(obj.gpair(margin, dm.label, None), margin))
-        finally:
-            hip.gbdt_grow_dev = real
+        for _ in range(3):
+            tb.sample_features(gen)
+            trees.append(tb._build_native(obj.gpair(margin, dm.label, None), margin))
         res.append((trees, margin.cpu()))
     assert sum(len(t.feat) for t in res[0][0]) > 3 * 7  # real trees, not stumps
     for a, b in zip(res[0][0], res[1][0]):

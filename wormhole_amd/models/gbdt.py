@@ -764,12 +764,12 @@ class TreeBuilder:
         # the level loop on the device (one host read per tree) unless the
         # per-level host grower is asked for; every rank takes the same one
         # (WH_GBDT_GROWER is process-wide, set alike on every rank)
-        grow = (_native.hip().gbdt_grow if os.environ.get("WH_GBDT_GROWER", "") == "host"
-                or p.max_depth > 10 else _native.hip().gbdt_grow_dev)
+        host = os.environ.get("WH_GBDT_GROWER", "") == "host" or p.max_depth > 10
+        grow = _native.hip().gbdt_grow if host else _native.hip().gbdt_grow_dev
         out = grow(
             self.B, self._Bc, self._iota(n), gpair,
             self._qscale, self._valid_dev[1], self.nbin, self.fgroups, self.max_fcnt,
-            tot.cpu().tolist(), self._cut_lists[0], self._cut_lists[1], float(p.eta),
+            tot.cpu().tolist() if host else tot.contiguous(),  # device grower: no host wait self._cut_lists[0], self._cut_lists[1], float(p.eta),
             float(p.alpha), float(p.reg_lambda), float(p.min_child_weight), int(p.max_depth),
             RT_EPS, ar)
         (feat, bin_, cond, defl, left, right, parent, gain, cover, bw, leaf, segs, ridx) = out
