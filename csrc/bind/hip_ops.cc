@@ -1631,7 +1631,8 @@ void gbdt_leaf_walk(const Tensor& B, const Tensor& feat, const Tensor& bin, cons
                   right.numel() == nn && val.numel() == nn && nn > 0,
               "leaf_walk: tree array sizes differ");
   c10::DeviceGuard g(B.device());
-  wh::gbdt_leaf_walk(ptr<uint8_t>(B), B.size(0), (int)B.size(1), ptr<int32_t>(feat),
+  TORCH_CHECK(nn <= INT32_MAX, "leaf_walk: too many nodes");
+  wh::gbdt_leaf_walk(ptr<uint8_t>(B), B.size(0), (int)B.size(1), (int)nn, ptr<int32_t>(feat),
                      ptr<int32_t>(bin), ptr<uint8_t>(defl), ptr<int32_t>(left),
                      ptr<int32_t>(right), ptr<float>(val), ptr<float>(margin), cur_stream(B));
 }

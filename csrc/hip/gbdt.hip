@@ -9,6 +9,7 @@
 //   gbdt_leaf_add  margin += leaf value for the rows of every leaf segment
 //   gbdt_predict   one lane per row walks a tree on raw values (NaN = missing)
 #include <algorithm>
+#include <cstdlib>
 
 #include "wh_common.h"
 #include "wh_kernels.h"
@@ -394,6 +395,52 @@ __global__ __launch_bounds__(256) void k_leaf_walk(
     nd = l ? left[nd] : right[nd];
   }
   margin[i] += val[nd];
+}
+
+// LDS variant: the block's rows are read ONCE, coalesced, into LDS (the
+// per-level byte gathers of k_leaf_walk re-fetch a 28-row x 64 B footprint
+// per wave at every level, ~8x the bytes of B through L2), and the tree is
+// packed into LDS as {feat:16 | bin:8 | defl:8, left:16 | right:16}; the walk
+// then touches no global memory until the margin update. Host guarantees:
+// f <= kWalkMaxF, nn <= 65535, bins < 256 (see gbdt_leaf_walk below).
+constexpr int kWalkRows = 256, kWalkMaxF = 96;
+__global__ __launch_bounds__(kWalkRows) void k_leaf_walk_lds(
+    const uint8_t* __restrict__ B, int64_t n, int f, int nn, const int32_t* __restrict__ feat,
+    const int32_t* __restrict__ bin, const uint8_t* __restrict__ defl,
+    const int32_t* __restrict__ left, const int32_t* __restrict__ right,
+    const float* __restrict__ val, float* __restrict__ margin) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t walk_lds[];
+  uint2* tree = reinterpret_cast<uint2*>(walk_lds);
+  uint8_t* rows = reinterpret_cast<uint8_t*>(walk_lds + 2 * nn);
+  for (int j = threadIdx.x; j < nn; j += blockDim.x) {
+    const int ft = feat[j];
+    const uint32_t w0 = ft < 0 ? 0xffffu : ((uint32_t)ft | ((uint32_t)bin[j] & 255u) << 16 |
+                                           (uint32_t)(defl[j] != 0) << 24);
+    tree[j] = make_uint2(w0, ((uint32_t)left[j] & 0xffffu) | ((uint32_t)right[j] << 16));
+  }
+  const int64_t i0 = (int64_t)blockIdx.x * kWalkRows;
+  const int nr = (int)min<int64_t>(kWalkRows, n - i0);
+  const int nbytes = nr * f;
+  const uint8_t* src = B + i0 * f;  // 4-aligned: i0 * f is a multiple of 4 (kWalkRows % 4 == 0)
+  const int nw = nbytes >> 2;
+  for (int k = threadIdx.x; k < nw; k += blockDim.x)
+    reinterpret_cast<uint32_t*>(rows)[k] = reinterpret_cast<const uint32_t*>(src)[k];
+  for (int k = 4 * nw + threadIdx.x; k < nbytes; k += blockDim.x) rows[k] = src[k];
+  __syncthreads();
+  if ((int)threadIdx.x >= nr) return;
+  const uint8_t* row = rows + threadIdx.x * f;
+  int nd = 0;
+  for (int d = 0; d < 64; ++d) {
+    const uint2 t = tree[nd];
+    const uint32_t ft = t.x & 0xffffu;
+    if (ft == 0xffffu) break;
+    const int b = row[ft];
+    const bool l = b == kMissing ? (t.x >> 24) != 0 : b <= (int)((t.x >> 16) & 255u);
+    const int nx = (int)(l ? (t.y & 0xffffu) : (t.y >> 16));
+    if (nx >= nn) break;  // (a malformed child id cannot read past the tree)
+    nd = nx;
+  }
+  margin[i0 + threadIdx.x] += val[nd];
 }
 
 __global__ void k_predict(const float* __restrict__ X, int64_t n, int f,
@@ -825,10 +872,17 @@ void gbdt_gpair(int64_t n, const float* margin, const float* label, const float*
                      logistic ? 1 : 0, reinterpret_cast<float2*>(gpair), scratch, ticket, stats);
 }
 
-void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, const int32_t* feat, const int32_t* bin,
+void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, int nn, const int32_t* feat, const int32_t* bin,
                     const uint8_t* defl, const int32_t* left, const int32_t* right,
                     const float* val, float* margin, hipStream_t s) {
   if (n <= 0) return;
+  const size_t lds = (size_t)nn * 8 + (size_t)kWalkRows * f;
+  if (nn > 0 && nn <= 65535 && f <= kWalkMaxF && lds <= 48 * 1024 && getenv("WH_GBDT_WALK") == nullptr) {
+    hipLaunchKernelGGL(k_leaf_walk_lds, dim3((unsigned)((n + kWalkRows - 1) / kWalkRows)),
+                       dim3(kWalkRows), lds, s, B, n, f, nn, feat, bin, defl, left, right, val,
+                       margin);
+    return;
+  }
   hipLaunchKernelGGL(k_leaf_walk, dim3(grid_for(n, 256)), dim3(256), 0, s, B, n, f, feat, bin, defl,
                      left, right, val, margin);
 }

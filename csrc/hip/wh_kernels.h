@@ -519,7 +519,7 @@ void gbdt_qscale(const float* m, double nglobal, int R, float* out, hipStream_t 
 int64_t gbdt_gpair_scratch();
 void gbdt_gpair(int64_t n, const float* margin, const float* label, const float* weight,
                 bool logistic, float* gpair, double* scratch, double* stats, hipStream_t s);
-void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, const int32_t* feat, const int32_t* bin,
+void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, int nn, const int32_t* feat, const int32_t* bin,
                     const uint8_t* defl, const int32_t* left, const int32_t* right,
                     const float* val, float* margin, hipStream_t s);
 void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const float* thr,

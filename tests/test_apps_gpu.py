@@ -408,15 +408,19 @@ def test_native_linear_lookahead_made_on_the_compute_stream(monkeypatch):
     assert pa == pytest.approx(pb, rel=1e-6)
 
 
-def test_gbdt_leaf_walk_matches_raw_value_predict():
+@pytest.mark.parametrize("f,walk", [(16, None), (13, None), (16, "global")])
+def test_gbdt_leaf_walk_matches_raw_value_predict(f, walk, monkeypatch):
     """The training margins after each tree come from a per-row walk of the
     pruned tree on the bins (k_leaf_walk); predicting the same (compacted)
     trees on the raw values must give the same margins (missing values,
-    gamma pruning included)."""
+    gamma pruning included). f = 13: the LDS walk's byte tail (rows not a
+    multiple of 4 bytes); WH_GBDT_WALK: the per-level gather kernel."""
     from wormhole_amd.models import gbdt as G
     from wormhole_amd.parallel.bsp import BSP
+    if walk:
+        monkeypatch.setenv("WH_GBDT_WALK", walk)
     g = torch.Generator().manual_seed(4)
-    n, f = 50000, 16
+    n = 50000
     X = torch.randn(n, f, generator=g)
     X[torch.rand(n, f, generator=g) < 0.08] = float("nan")
     y = (torch.nan_to_num(X[:, 0]) + torch.nan_to_num(X[:, 3]) * X[:, 5].abs() > 0.2).float()
