@@ -877,7 +877,8 @@ void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, int nn, const int32_t* f
                     const float* val, float* margin, hipStream_t s) {
   if (n <= 0) return;
   const size_t lds = (size_t)nn * 8 + (size_t)kWalkRows * f;
-  if (nn > 0 && nn <= 65535 && f <= kWalkMaxF && lds <= 48 * 1024 && getenv("WH_GBDT_WALK") == nullptr) {
+  if (nn > 0 && nn <= 65535 && f <= kWalkMaxF && lds <= 48 * 1024 &&
+      (reinterpret_cast<uintptr_t>(B) & 3) == 0 && getenv("WH_GBDT_WALK") == nullptr) {
     hipLaunchKernelGGL(k_leaf_walk_lds, dim3((unsigned)((n + kWalkRows - 1) / kWalkRows)),
                        dim3(kWalkRows), lds, s, B, n, f, nn, feat, bin, defl, left, right, val,
                        margin);
