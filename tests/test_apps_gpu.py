@@ -447,11 +447,11 @@ def test_gbdt_qscale_kernel_matches_torch(r32):
     for mg, mh, n in [(0.5, 0.25, 11_000_000), (1e-7, 3.0, 1), (0.0, 0.0, 6513), (123.4, 1e-30, 10 ** 9)]:
         m = torch.tensor([mg, mh], dtype=torch.float32, device="cuda")
         got = _native.hip().gbdt_qscale(m, float(n), r32).cpu()
-        md = m.double().cpu().clamp_min(1e-30)
+        md = m.double().clamp_min(1e-30)  # (the torch path ran on the device too)
         e = torch.floor(torch.log2(2.0 ** 61 / (n * md)))
         if r32:
             e = torch.minimum(e, torch.floor(torch.log2(2.0 ** 30 / (r32 * md))))
-        want = torch.pow(2.0, e.clamp(-60, 100)).float()
+        want = torch.pow(2.0, e.clamp(-60, 100)).float().cpu()
         if r32:
             want = torch.cat([want, torch.tensor([float(r32)])])
         assert torch.equal(got, want), (mg, mh, n, got, want)
