@@ -2988,7 +2988,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("vstride_for", &vstride_for);
   m.def("spmv", &spmv, py::arg("offset"), py::arg("col"), py::arg("val"), py::arg("x"));
   m.def("gbdt_bin", &gbdt_bin);
-  m.def("gbdt_hist", &gbdt_hist);
+  m.def("gbdt_hist", &gbdt_hist, py::arg("B"), py::arg("nbin"), py::arg("ridx"), py::arg("gpair"),
+        py::arg("qscale"), py::arg("tasks"), py::arg("red"), py::arg("max_fcnt"), py::arg("hist"));
   m.def("gbdt_partition", &gbdt_partition, py::arg("B"), py::arg("ridx"), py::arg("pos_node"),
         py::arg("node_feat"), py::arg("node_bin"), py::arg("node_defl"), py::arg("seg_beg"),
         py::arg("seg_end"), py::arg("nleft"), py::arg("Bc") = py::none());
@@ -3007,8 +3008,18 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_accum", &kmeans_accum);
   m.def("kmeans_update", &kmeans_update);
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
-  m.def("gbdt_grow", &gbdt_grow);
-  m.def("gbdt_grow_dev", &gbdt_grow_dev);
+  // every argument named: the Python side calls these by keyword (a dropped
+  // argument fails on the CPU signature test, tests/test_native_signatures.py)
+  m.def("gbdt_grow", &gbdt_grow, py::arg("B"), py::arg("Bc"), py::arg("ridx0"), py::arg("gpair"),
+        py::arg("qscale"), py::arg("valid"), py::arg("nbin"), py::arg("fgroups"), py::arg("max_fcnt"),
+        py::arg("root_tot"), py::arg("cut_vals"), py::arg("cut_off"), py::arg("eta"), py::arg("alpha"),
+        py::arg("reg_lambda"), py::arg("min_child_weight"), py::arg("max_depth"), py::arg("rt_eps"),
+        py::arg("allreduce"));
+  m.def("gbdt_grow_dev", &gbdt_grow_dev, py::arg("B"), py::arg("Bc"), py::arg("ridx0"), py::arg("gpair"),
+        py::arg("qscale"), py::arg("valid"), py::arg("nbin"), py::arg("fgroups"), py::arg("max_fcnt"),
+        py::arg("root_tot"), py::arg("cut_vals"), py::arg("cut_off"), py::arg("eta"), py::arg("alpha"),
+        py::arg("reg_lambda"), py::arg("min_child_weight"), py::arg("max_depth"), py::arg("rt_eps"),
+        py::arg("allreduce"));
   m.def("gbdt_gpair", &gbdt_gpair);
   m.def("gbdt_qscale", &gbdt_qscale);
   // the ingest ops block on one small device read each: the GIL is released
@@ -3038,9 +3049,15 @@ PYBIND11_MODULE(_hip, m) {
            py::arg("cnt"), py::arg("h"), py::arg("threshold"), py::arg("l1_shrk"), py::arg("seed"),
            py::arg("direct") = false)
       .def("difacto_push", &KVStore::difacto_push)
-      .def("ps_open", &KVStore::ps_open)
-      .def("ps_push", &KVStore::ps_push)
-      .def("ps_push_linear", &KVStore::ps_push_linear)
+      .def("ps_open", &KVStore::ps_open, py::arg("keys"), py::arg("use_cnt"), py::arg("segS"),
+           py::arg("segHS"), py::arg("rows_cap"), py::arg("insert"), py::arg("chains"), py::arg("h"),
+           py::arg("threshold"), py::arg("l1_shrk"), py::arg("seed"))
+      .def("ps_push", &KVStore::ps_push, py::arg("slot"), py::arg("vpos"), py::arg("chain"),
+           py::arg("head"), py::arg("segS"), py::arg("segHS"), py::arg("gbuf"), py::arg("h"),
+           py::arg("threshold"), py::arg("l1_shrk"), py::arg("seed"))
+      .def("ps_push_linear", &KVStore::ps_push_linear, py::arg("slot"), py::arg("chain"),
+           py::arg("head"), py::arg("segS"), py::arg("g"), py::arg("algo"), py::arg("alpha"),
+           py::arg("beta"), py::arg("l1"), py::arg("l2"), py::arg("t0"))
       .def("grow", &KVStore::grow)
       .def("grow_v", &KVStore::grow_v)
       .def("summary", &KVStore::summary)

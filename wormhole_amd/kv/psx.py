@@ -435,8 +435,9 @@ class Psx:
             lrn.kv.guard.before_open(n, self._remap)
         rows = sum(st.Ho) + n if not self.linear else 0
         st.slot, st.vpos, st.chain, st.head, st.rbuf, st.vcnt = self.store.ps_open(
-            st.keys_o, st.use_cnt, st.segS_o, st.segHS_o, rows, insert, st.train,
-            lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
+            keys=st.keys_o, use_cnt=st.use_cnt, segS=st.segS_o, segHS=st.segHS_o, rows_cap=rows,
+            insert=insert, chains=st.train, h=lrn.hp, threshold=lrn.threshold,
+            l1_shrk=lrn.l1_shrk, seed=lrn.seed)
         st.keys_o = st.w_c1 = None
         st.ev_open = self._event()  # C2 of this step waits for this only
         if insert:
@@ -524,13 +525,15 @@ class Psx:
         lrn = self.lrn
         st.w_c3.wait()
         if self.linear:
-            self.store.ps_push_linear(st.slot, st.chain, st.head, st.segS_o, st.gpush,
-                                      lrn.conf.algo, lrn.alpha, lrn.beta, lrn.conf.lambda_l1,
-                                      lrn.conf.lambda_l2, float(self.requests))
+            self.store.ps_push_linear(
+                slot=st.slot, chain=st.chain, head=st.head, segS=st.segS_o, g=st.gpush,
+                algo=lrn.conf.algo, alpha=lrn.alpha, beta=lrn.beta, l1=lrn.conf.lambda_l1,
+                l2=lrn.conf.lambda_l2, t0=float(self.requests))
             self.requests += self.P  # one request per worker (ps-lite SGD's t)
         else:
-            self.store.ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o,
-                               st.gpush, lrn.hp, lrn.threshold, lrn.l1_shrk, lrn.seed)
+            self.store.ps_push(slot=st.slot, vpos=st.vpos, chain=st.chain, head=st.head,
+                               segS=st.segS_o, segHS=st.segHS_o, gbuf=st.gpush, h=lrn.hp,
+                               threshold=lrn.threshold, l1_shrk=lrn.l1_shrk, seed=lrn.seed)
         st.w_c3 = None
         st.gpush = st.slot = st.vpos = st.chain = st.head = st.keys_o = None
 

@@ -660,8 +660,9 @@ class TreeBuilder:
                 both = _h2d(both, self.device)
                 t = both[:5 * len(tasks)].view(-1, 5)
                 rd = both[5 * len(tasks):].view(-1, 6)
-                _native.hip().gbdt_hist(self.B, self.nbin, ridx, gpair, self._qscale, t, rd,
-                                        self.max_fcnt, hist)
+                _native.hip().gbdt_hist(B=self.B, nbin=self.nbin, ridx=ridx, gpair=gpair,
+                                        qscale=self._qscale, tasks=t, red=rd,
+                                        max_fcnt=self.max_fcnt, hist=hist)
         else:
             for (b, e), s in zip(segs, slots):
                 if e <= b:
@@ -766,12 +767,15 @@ class TreeBuilder:
         # (WH_GBDT_GROWER is process-wide, set alike on every rank)
         host = os.environ.get("WH_GBDT_GROWER", "") == "host" or p.max_depth > 10
         grow = _native.hip().gbdt_grow if host else _native.hip().gbdt_grow_dev
+        # the device grower takes the root totals as a device tensor (no host wait)
         out = grow(
-            self.B, self._Bc, self._iota(n), gpair,
-            self._qscale, self._valid_dev[1], self.nbin, self.fgroups, self.max_fcnt,
-            tot.cpu().tolist() if host else tot.contiguous(),  # device grower: no host wait self._cut_lists[0], self._cut_lists[1], float(p.eta),
-            float(p.alpha), float(p.reg_lambda), float(p.min_child_weight), int(p.max_depth),
-            RT_EPS, ar)
+            B=self.B, Bc=self._Bc, ridx0=self._iota(n), gpair=gpair, qscale=self._qscale,
+            valid=self._valid_dev[1], nbin=self.nbin, fgroups=self.fgroups,
+            max_fcnt=self.max_fcnt, root_tot=tot.cpu().tolist() if host else tot.contiguous(),
+            cut_vals=self._cut_lists[0], cut_off=self._cut_lists[1], eta=float(p.eta),
+            alpha=float(p.alpha), reg_lambda=float(p.reg_lambda),
+            min_child_weight=float(p.min_child_weight), max_depth=int(p.max_depth),
+            rt_eps=RT_EPS, allreduce=ar)
         (feat, bin_, cond, defl, left, right, parent, gain, cover, bw, leaf, segs, ridx) = out
         tree = RegTree()
         tree.feat, tree.bin, tree.cond, tree.defl = list(feat), list(bin_), list(cond), list(defl)

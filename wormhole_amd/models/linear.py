@@ -66,10 +66,10 @@ class LinearLearner:
         if (self.device.type == "cuda" and comm.size == 1 and self.kv.nshard == 1
                 and not isinstance(comm, LoopbackComm)):
             from .. import _native
-            self._native = _native.hip().LinearStep(self.store, int(conf.algo), conf.lr_eta,
-                                                    conf.lr_beta, conf.lambda_l1,
-                                                    conf.lambda_l2, int(conf.loss),
-                                                    self.kv.guard.max_load)
+            self._native = _native.hip().LinearStep(
+                store=self.store, algo=int(conf.algo), alpha=conf.lr_eta, beta=conf.lr_beta,
+                l1=conf.lambda_l1, l2=conf.lambda_l2, loss=int(conf.loss),
+                max_load=self.kv.guard.max_load)
 
     def _localize(self, keys, offset, val, next_batch):
         return localize_pipelined(self, keys, offset, val, next_batch)
