@@ -10,6 +10,7 @@ import torch
 
 _get = torch._C._cuda_getCurrentStream
 _set = torch._C._cuda_setStream
+_getdev = torch._C._cuda_getDevice
 
 
 def current_id(device_index):
@@ -22,16 +23,22 @@ def current_id(device_index):
 
 class on:
     """``with on(stream):`` -- make ``stream`` current, restore the previous
-    current stream of its device on exit."""
+    current stream of its device on exit. Setting a stream also makes its
+    device current; like ``torch.cuda.stream``, the caller's current device
+    is restored too when it was a different one (one device per process is
+    the usual case, where this costs one integer compare)."""
 
-    __slots__ = ("s", "prev")
+    __slots__ = ("s", "prev", "dev")
 
     def __init__(self, s):
         self.s = s
         self.prev = None
+        self.dev = None
 
     def __enter__(self):
         s = self.s
+        cur = _getdev()
+        self.dev = cur if cur != s.device_index else None
         self.prev = _get(s.device_index)
         _set(stream_id=s.stream_id, device_index=s.device_index, device_type=s.device_type)
         return s
@@ -39,6 +46,8 @@ class on:
     def __exit__(self, *exc):
         p = self.prev
         _set(stream_id=p[0], device_index=p[1], device_type=p[2])
+        if self.dev is not None:
+            torch.cuda.set_device(self.dev)
         return False
 
 
