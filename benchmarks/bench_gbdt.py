@@ -78,6 +78,7 @@ def main():
         tb.build(obj.gpair(margin, dm.label, None), margin)
     sync()
     bsp.barrier()
+    b0 = tb.hist_bytes()
     t0 = time.perf_counter()
     for _ in range(a.trees):
         tb.build(obj.gpair(margin, dm.label, None), margin)
@@ -87,12 +88,16 @@ def main():
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
     bsp.allreduce(t, "max")
     dt = float(t.item())
+    hb = bsp.allreduce_scalar((tb.hist_bytes() - b0) / max(a.trees, 1), "max")
     err = G.eval_metric("error", torch.sigmoid(margin), dm.label, None, bsp)
     if bsp.rank == 0:
         print(json.dumps({"metric": "GBDT trees/s (hist, depth %d, %dx%d)" % (a.depth, a.rows, a.features),
                           "value": a.trees / dt, "unit": "trees/s", "n_gpus": bsp.world if dev.type == "cuda" else 0, "ranks": bsp.world, "device": dev.type,
                           "ms_per_tree": 1000 * dt / a.trees,
                           "trees": a.trees, "sketch_bin_s": t_prep,
+                          "hist_exchange": ("feature-reduce-scatter" if tb.xchg is not None
+                                            else "allreduce") if bsp.world > 1 else None,
+                          "hist_bytes_per_rank_per_tree": hb,
                           "train_error": err, "scaling": "strong", "data": "synthetic Higgs-shaped"}),
               flush=True)
     bsp.finalize()

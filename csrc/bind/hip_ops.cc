@@ -2394,7 +2394,14 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                         std::vector<std::pair<int64_t, int64_t>> fgroups, int64_t max_fcnt,
                         const Tensor& root_tot, std::vector<float> cut_vals,
                         std::vector<int64_t> cut_off, double eta, double alpha, double lambda,
-                        double mcw, int64_t max_depth, double rt_eps, py::object allreduce) {
+                        double mcw, int64_t max_depth, double rt_eps, py::object allreduce,
+                        py::object reduce_scatter, py::object pick, int64_t f_lo) {
+  // Multi-rank: either every level's built histograms are allreduced (all
+  // features on every rank), or -- reduce_scatter / pick given
+  // (models/gbdt.py HistExchange) -- each rank receives the global sums of
+  // its feature slice [f_lo, f_lo + Fl) only, keeps the node histograms of
+  // that slice, searches its features, and the per-slot best candidates are
+  // reduced over the ranks by `pick`.
   CHECK_IN(root_tot, torch::kFloat64);  // {sum g, sum h} stays on the device: no host wait
   TORCH_CHECK(root_tot.numel() == 2, "gbdt_grow_dev: root totals are {sum g, sum h}");
   CHECK_IN(B, torch::kUInt8);
@@ -2411,12 +2418,27 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
   TORCH_CHECK(n < (int64_t)INT32_MAX, "rows must fit int32");
   const int G = (int)fgroups.size();
   const bool dw = F % 4 == 0 && max_fcnt % 4 == 0;
-  const int64_t per = (int64_t)F * nbin * 2;
   auto f64 = B.options().dtype(torch::kFloat64);
   auto i32 = B.options().dtype(torch::kInt32);
   auto u8 = B.options().dtype(torch::kUInt8);
   const int chunk = (int)std::max<int64_t>(8192, (n + 1023) / 1024);
-  const bool reduce = !allreduce.is_none();
+  const bool shard = !reduce_scatter.is_none();
+  TORCH_CHECK(!shard || !pick.is_none(), "gbdt_grow_dev: reduce_scatter needs pick");
+  const bool reduce = shard || !allreduce.is_none();
+  // rank partials -> global sums: all features, or this rank's slice
+  auto reduce_hist = [&](Tensor h) -> Tensor {
+    if (!reduce) return h;
+    if (!shard) {
+      allreduce(h);
+      return h;
+    }
+    Tensor r = reduce_scatter(h).cast<Tensor>();
+    TORCH_CHECK(r.scalar_type() == torch::kFloat64 && r.is_contiguous() &&
+                    r.device() == h.device() && r.dim() == 4 && r.size(0) == h.size(0) &&
+                    r.size(1) <= F && f_lo + r.size(1) <= F,
+                "gbdt_grow_dev: reduce_scatter returned a bad slice");
+    return r;
+  };
   const int D = (int)max_depth, NN = (2 << D) - 1, Smax = 1 << D, REC = wh::gbdt_node_rec();
   const int64_t pstride = wh::gbdt_hist_pstride((int)max_fcnt, (int)nbin);
   // one small upload: root totals, root segment, feature groups, slot iota
@@ -2453,18 +2475,32 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                   ptr<float>(qscale), ptr<int32_t>(d), (int)nt, ptr<int32_t>(d) + nt * 5, G,
                   (int)max_fcnt, dw, ptr<int64_t>(part), ptr<double>(H_front), s,
                   ptr<int32_t>(seg_cur), chunk, nullptr, qscale.numel() == 3);
-    if (reduce) allreduce(H_front);
+    H_front = reduce_hist(H_front);
   }
+  const int Fl = (int)H_front.size(1);  // features of the node histograms kept here
+  const int64_t per = (int64_t)Fl * nbin * 2;
   for (int d = 0; d <= D; ++d) {
     const int S = 1 << d;
     const bool last = d == D;
     Tensor so;
     if (!last) {
       so = torch::empty({S, 6}, f64);
-      auto cand = torch::empty({(int64_t)S * F * 4}, f64);
-      TORCH_CHECK(wh::gbdt_split(ptr<double>(H_front), ptr<double>(tot_cur), vp, S, F, (int)nbin,
-                                 alpha, lambda, mcw, ptr<double>(cand), ptr<double>(so), s),
-                  "gbdt_split failed");
+      if (Fl > 0) {
+        auto cand = torch::empty({(int64_t)S * Fl * 4}, f64);
+        TORCH_CHECK(wh::gbdt_split(ptr<double>(H_front), ptr<double>(tot_cur),
+                                   vp + (int64_t)f_lo * nbin, S, Fl, (int)nbin, alpha, lambda, mcw,
+                                   ptr<double>(cand), ptr<double>(so), s),
+                    "gbdt_split failed");
+      } else {  // (more ranks than features: this rank owns none)
+        so.zero_();
+        so.select(1, 0).fill_(-std::numeric_limits<double>::infinity());
+      }
+      if (shard) {
+        so.select(1, 1).add_((double)f_lo);  // global feature ids
+        so = pick(so).cast<Tensor>().contiguous();
+        TORCH_CHECK(so.scalar_type() == torch::kFloat64 && so.size(0) == S && so.size(1) == 6,
+                    "gbdt_grow_dev: pick returned a bad candidate table");
+      }
     }
     auto nleft = last ? Tensor() : torch::empty({S}, i32);  // zeroed by the apply kernel
     auto pi = torch::empty({4 * S}, i32);  // pfeat | pbin | lcur | rcur
@@ -2510,8 +2546,8 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                   ptr<int32_t>(red), S * G, (int)max_fcnt, dw, ptr<int64_t>(part),
                   ptr<double>(hs), s, ptr<int32_t>(dseg), chunk, ptr<int32_t>(sp) + 5 * S,
                   qscale.numel() == 3);
-    if (reduce) allreduce(hs);
-    auto H_next = torch::empty({2 * S, F, nbin, 2}, f64);
+    hs = reduce_hist(hs);
+    auto H_next = torch::empty({2 * S, Fl, nbin, 2}, f64);
     wh::gbdt_sibling(ptr<double>(H_front), ptr<double>(hs), ptr<int32_t>(sp),
                      ptr<int32_t>(sp) + 4 * S, S, per, ptr<double>(H_next), s);
     H_front = H_next;
@@ -3019,7 +3055,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("qscale"), py::arg("valid"), py::arg("nbin"), py::arg("fgroups"), py::arg("max_fcnt"),
         py::arg("root_tot"), py::arg("cut_vals"), py::arg("cut_off"), py::arg("eta"), py::arg("alpha"),
         py::arg("reg_lambda"), py::arg("min_child_weight"), py::arg("max_depth"), py::arg("rt_eps"),
-        py::arg("allreduce"));
+        py::arg("allreduce"), py::arg("reduce_scatter") = py::none(), py::arg("pick") = py::none(),
+        py::arg("f_lo") = 0);
   m.def("gbdt_gpair", &gbdt_gpair);
   m.def("gbdt_qscale", &gbdt_qscale);
   // the ingest ops block on one small device read each: the GIL is released

@@ -159,8 +159,15 @@ def _calls(table, pydefs):
         scopes = [n for n in ast.walk(tree)
                   if isinstance(n, (ast.FunctionDef, ast.AsyncFunctionDef, ast.Module))]
         for scope in scopes:
-            alias = {}
+            alias, kwdicts = {}, {}
             for node in ast.walk(scope):
+                # kw = dict(a=..., b=...): the keywords of a later f(**kw)
+                if isinstance(node, ast.Assign) and len(node.targets) == 1 and \
+                        isinstance(node.targets[0], ast.Name) and \
+                        isinstance(node.value, ast.Call) and \
+                        isinstance(node.value.func, ast.Name) and node.value.func.id == "dict" \
+                        and not node.value.args and all(k.arg for k in node.value.keywords):
+                    kwdicts[node.targets[0].id] = [k.arg for k in node.value.keywords]
                 # grow = a.gbdt_grow if host else a.gbdt_grow_dev  /  f = a.name
                 if isinstance(node, ast.Assign) and len(node.targets) == 1 and \
                         isinstance(node.targets[0], ast.Name):
@@ -172,9 +179,23 @@ def _calls(table, pydefs):
             for node in ast.walk(scope):
                 if not isinstance(node, ast.Call):
                     continue
-                if any(isinstance(a, ast.Starred) for a in node.args) or \
-                        any(k.arg is None for k in node.keywords):
+                if any(isinstance(a, ast.Starred) for a in node.args):
                     continue
+                if any(k.arg is None for k in node.keywords):
+                    # f(**kw) with kw a dict(...) of this scope: expand it
+                    extra = []
+                    for k in node.keywords:
+                        if k.arg is None:
+                            if not (isinstance(k.value, ast.Name) and k.value.id in kwdicts):
+                                extra = None
+                                break
+                            extra += [ast.keyword(arg=a_, value=k.value)
+                                      for a_ in kwdicts[k.value.id]]
+                    if extra is None:
+                        continue
+                    node = ast.Call(func=node.func, args=node.args,
+                                    keywords=[k for k in node.keywords if k.arg] + extra,
+                                    lineno=node.lineno, col_offset=node.col_offset)
                 f = node.func
                 if isinstance(f, ast.Attribute) and f.attr in table:
                     if f.attr in pydefs and not _is_handle(f.value):

@@ -566,6 +566,68 @@ def load_fmap(path):
     return names
 
 
+# ------------------------------------------------------ histogram exchange
+class HistExchange:
+    """Feature-sharded histogram exchange of the multi-rank dense grower
+    (xgboost's row split, ``dsplit=row``, allreduces every
+    level's histograms, learn/xgboost/mushroom.hadoop.conf:33).
+
+    Rank r owns the contiguous feature slice ``ranges[r]``. A level's built
+    histograms -- the rank-local partial sums [S, F, nbin, 2] -- go out as
+    ONE all-to-all-v of feature-major rows (each peer receives its slice
+    only) and are summed locally in rank order: a reduce-scatter by feature,
+    (P-1)/P of the histogram bytes per rank on the wire where a ring
+    allreduce moves 2(P-1)/P. Each rank keeps only its slice of the node
+    histograms (sibling subtraction included), searches splits over its
+    features, and the per-slot best candidates [S, 6] are all-gathered and
+    reduced by gain (ties: lowest rank = lowest feature index, the same
+    winner as a row-major argmax over all features on one rank). Trees are
+    identical to the allreduce grower's (``WH_GBDT_XCHG=allreduce`` keeps
+    that path): on the GPU the histograms are exact fixed-point sums, so the
+    reduction order cannot matter."""
+
+    def __init__(self, bsp, F):
+        self.comm = bsp.comm
+        self.P, self.rank = bsp.world, bsp.rank
+        per = -(-F // self.P) if F else 0
+        self.ranges = [(min(F, r * per), min(F, (r + 1) * per)) for r in range(self.P)]
+        self.lo, self.hi = self.ranges[self.rank]
+        self.sent = 0  # bytes this rank sent to its peers (histograms + candidates)
+
+    @staticmethod
+    def mode(bsp, dense):
+        if bsp.world <= 1 or not dense:
+            return None
+        return None if os.environ.get("WH_GBDT_XCHG", "rs") == "allreduce" else "rs"
+
+    def reduce_scatter(self, h):
+        """h [S, F, nbin, 2] local partials -> [S, Fr, nbin, 2] global sums
+        of this rank's features."""
+        S, F = int(h.shape[0]), int(h.shape[1])
+        rest = tuple(h.shape[2:])
+        width = S
+        for d in rest:
+            width *= int(d)
+        x = h.transpose(0, 1).reshape(F, width)  # feature-major rows
+        send = [hi - lo for lo, hi in self.ranges]
+        fr = self.hi - self.lo
+        out = self.comm.all_to_all_v(x, send, [fr] * self.P)
+        self.sent += (F - fr) * width * x.element_size()
+        acc = out[0:fr].clone()
+        for q in range(1, self.P):  # rank order: deterministic on the CPU path too
+            acc += out[q * fr:(q + 1) * fr]
+        return acc.view((fr, S) + rest).transpose(0, 1).contiguous()
+
+    def pick(self, cand):
+        """cand [S, 6] {gain, feature (global), bin, dir, GL, HL}: this
+        rank's best per slot -> the best over all ranks."""
+        cand = cand.contiguous()
+        allc = torch.stack(self.comm.allgather(cand))  # [P, S, 6]
+        self.sent += (self.P - 1) * cand.numel() * cand.element_size()
+        r = torch.argmax(allc[:, :, 0], 0)  # first maximum: lowest rank on ties
+        return allc.gather(0, r[None, :, None].expand(1, cand.shape[0], cand.shape[1]))[0]
+
+
 # ---------------------------------------------------------------- builder
 class TreeBuilder:
     """Depth-wise histogram tree growth on one DMatrix split per rank."""
@@ -595,6 +657,9 @@ class TreeBuilder:
         self._nglobal = None
         self._valid_dev = None
         self._Bc = None
+        mode = HistExchange.mode(bsp, True)
+        self.xchg = HistExchange(bsp, self.F) if mode else None
+        self.ar_sent = 0  # allreduced histogram bytes per rank (ring model: 2 (P-1) / P)
 
     def _hist_scale(self, gpair):
         """Fixed-point scales {2^eg, 2^eh} of the GPU histograms: the largest
@@ -683,21 +748,42 @@ class TreeBuilder:
         On the GPU: the fused split-search kernels (csrc/hip/gbdt.hip
         k_split_feat / k_split_node: scan + gain + argmax in two launches
         instead of ~40 elementwise ops per level); the torch form below is
-        their reference."""
+        their reference. With a feature-sharded exchange, hist holds this
+        rank's feature slice only: the local best goes through
+        :meth:`HistExchange.pick`."""
+        x = self.xchg
+        if x is None:
+            return self._find_splits_local(hist, totals, self.valid_mask, 0)
+        S = hist.shape[0]
+        if x.hi > x.lo:
+            bg, bf, bb, bd, bL = self._find_splits_local(hist, totals,
+                                                         self.valid_mask[x.lo:x.hi], x.lo)
+            cand = torch.cat([bg[:, None].double(), (bf + x.lo)[:, None].double(),
+                              bb[:, None].double(), bd[:, None].double(), bL.double()], 1)
+        else:  # (more ranks than features: this rank owns none)
+            cand = torch.zeros(S, 6, dtype=torch.float64)
+            cand[:, 0] = -float("inf")
+        out = x.pick(cand.to(self.device)).cpu()
+        return out[:, 0], out[:, 1].long(), out[:, 2].long(), out[:, 3].long(), out[:, 4:6]
+
+    def _find_splits_local(self, hist, totals, valid, lo):
         if hist.is_cuda and hist.shape[0] > 0 and hist.shape[2] <= 1024:
             p = self.p
             if self._valid_dev is None or self._valid_dev[0] is not self.valid_mask:
                 self._valid_dev = (self.valid_mask,
                                    self.valid_mask.to(hist.device).contiguous())
+            vd = self._valid_dev[1][lo:lo + hist.shape[1]].contiguous()
             out = _native.hip().gbdt_split(hist.double().contiguous(),
-                                           totals.double().contiguous(), self._valid_dev[1],
+                                           totals.double().contiguous(), vd,
                                            float(p.alpha), float(p.reg_lambda),
                                            float(p.min_child_weight)).cpu()
             return (out[:, 0], out[:, 1].long(), out[:, 2].long(), out[:, 3].long(),
                     out[:, 4:6])
-        return self._find_splits_ref(hist, totals)
+        return self._find_splits_ref(hist, totals, valid)
 
-    def _find_splits_ref(self, hist, totals):
+    def _find_splits_ref(self, hist, totals, valid=None):
+        if valid is None:
+            valid = self.valid_mask
         p = self.p
         cum = hist.cumsum(2)
         present = cum[:, :, -1, :]
@@ -717,7 +803,7 @@ class TreeBuilder:
         gain = torch.stack([c[0] for c in cands], -1)  # [S, F, nbin, 2dir]
         # thresholds past a feature's own bin count, and features dropped by
         # colsample_bytree, are not candidates
-        gain = torch.where(self.valid_mask.to(gain.device)[None, :, :, None], gain,
+        gain = torch.where(valid.to(gain.device)[None, :, :, None], gain,
                            torch.full_like(gain, -float("inf")))
         S = gain.shape[0]
         flat = gain.reshape(S, -1)
@@ -761,21 +847,25 @@ class TreeBuilder:
             self._valid_dev = (self.valid_mask, self.valid_mask.to(self.device).contiguous())
         if not hasattr(self, "_cut_lists"):
             self._cut_lists = (self.cuts.values.tolist(), self.cuts.offsets.tolist())
-        ar = (lambda t: self.bsp.allreduce(t)) if self.bsp.world > 1 else None
+        ar = self._allreduce_hist if self.bsp.world > 1 else None
         # the level loop on the device (one host read per tree) unless the
         # per-level host grower is asked for; every rank takes the same one
         # (WH_GBDT_GROWER is process-wide, set alike on every rank)
         host = os.environ.get("WH_GBDT_GROWER", "") == "host" or p.max_depth > 10
-        grow = _native.hip().gbdt_grow if host else _native.hip().gbdt_grow_dev
-        # the device grower takes the root totals as a device tensor (no host wait)
-        out = grow(
-            B=self.B, Bc=self._Bc, ridx0=self._iota(n), gpair=gpair, qscale=self._qscale,
-            valid=self._valid_dev[1], nbin=self.nbin, fgroups=self.fgroups,
-            max_fcnt=self.max_fcnt, root_tot=tot.cpu().tolist() if host else tot.contiguous(),
-            cut_vals=self._cut_lists[0], cut_off=self._cut_lists[1], eta=float(p.eta),
-            alpha=float(p.alpha), reg_lambda=float(p.reg_lambda),
-            min_child_weight=float(p.min_child_weight), max_depth=int(p.max_depth),
-            rt_eps=RT_EPS, allreduce=ar)
+        kw = dict(B=self.B, Bc=self._Bc, ridx0=self._iota(n), gpair=gpair, qscale=self._qscale,
+                  valid=self._valid_dev[1], nbin=self.nbin, fgroups=self.fgroups,
+                  max_fcnt=self.max_fcnt, cut_vals=self._cut_lists[0],
+                  cut_off=self._cut_lists[1], eta=float(p.eta), alpha=float(p.alpha),
+                  reg_lambda=float(p.reg_lambda), min_child_weight=float(p.min_child_weight),
+                  max_depth=int(p.max_depth), rt_eps=RT_EPS, allreduce=ar)
+        if host:  # (the per-level host grower allreduces whole histograms)
+            out = _native.hip().gbdt_grow(root_tot=tot.cpu().tolist(), **kw)
+        else:  # root totals as a device tensor: no host wait
+            x = self.xchg
+            out = _native.hip().gbdt_grow_dev(
+                root_tot=tot.contiguous(), **kw,
+                reduce_scatter=x.reduce_scatter if x is not None else None,
+                pick=x.pick if x is not None else None, f_lo=x.lo if x is not None else 0)
         (feat, bin_, cond, defl, left, right, parent, gain, cover, bw, leaf, segs, ridx) = out
         tree = RegTree()
         tree.feat, tree.bin, tree.cond, tree.defl = list(feat), list(bin_), list(cond), list(defl)
@@ -806,8 +896,7 @@ class TreeBuilder:
         done = {}  # finished leaves -> their final ridx segment
         if self.gpu:
             self._qscale = self._hist_scale(gpair)
-        hist_root = self._build_hist(ridx, gpair, [seg[root]], [0], 1)
-        self.bsp.allreduce(hist_root)
+        hist_root = self._reduce_hist(self._build_hist(ridx, gpair, [seg[root]], [0], 1))
         H_front = hist_root  # [len(frontier), F, nbin, 2], frontier order
         frontier = [root]
         cuts_v = self.cuts.values.tolist()
@@ -876,8 +965,8 @@ class TreeBuilder:
             for nd in frontier:
                 if nd not in split_nodes and nd in seg:
                     done[nd] = seg.pop(nd)  # finished leaf: its rows are final
-            hsmall = self._build_hist(ridx, gpair, build_segs, build_slots, len(build_slots))
-            self.bsp.allreduce(hsmall)
+            hsmall = self._reduce_hist(self._build_hist(ridx, gpair, build_segs, build_slots,
+                                                        len(build_slots)))
             # sibling subtraction for every split node at once; the new
             # frontier is [l, r] per split node, in split order
             fpos = {nd: i for i, nd in enumerate(frontier)}
@@ -896,6 +985,25 @@ class TreeBuilder:
         done.update(seg)
         self._finish(tree, ridx, margin, n, done)
         return tree
+
+    def _reduce_hist(self, h):
+        """Rank partials -> global histograms: allreduced (all features), or
+        this rank's feature slice (:class:`HistExchange`)."""
+        if self.xchg is not None:
+            return self.xchg.reduce_scatter(h)
+        self._allreduce_hist(h)
+        return h
+
+    def _allreduce_hist(self, h):
+        P = self.bsp.world
+        if P > 1:
+            self.ar_sent += 2 * (P - 1) * h.numel() * h.element_size() // P
+        self.bsp.allreduce(h)
+
+    def hist_bytes(self):
+        """Histogram-exchange bytes this rank has sent to its peers so far
+        (all-to-all bytes + candidates, or the ring model of the allreduce)."""
+        return self.ar_sent + (self.xchg.sent if self.xchg is not None else 0)
 
     def _pos_node(self, seg, n):
         """Node id of every ridx position (-1 for rows of finished leaves),
@@ -1053,6 +1161,8 @@ class CSRTreeBuilder(TreeBuilder):
         self.fvalid = None
         self._nglobal = None
         self._rows = None
+        self.xchg = None  # compact global-bin histograms: allreduced (HistExchange is dense-only)
+        self.ar_sent = 0
 
     def sample_features(self, gen):
         self.fvalid = None
