@@ -1345,6 +1345,36 @@ Tensor dequant_rows(const Tensor& q, int64_t w, int64_t nb) {
   return x;
 }
 
+// region filter of the multi-shard exchange (quant.hip qregion_*): x the
+// float layout (flat view), desc int64 [P, 6] on the device, built and
+// bounds-checked on the host (kv/psx.py _QFilter) against x / out sizes.
+Tensor ps_qpack(const Tensor& x, const Tensor& desc, int64_t rows, int64_t W, int64_t nb,
+                int64_t seed) {
+  CHECK_IN(x, torch::kFloat32);
+  CHECK_IN(desc, torch::kInt64);
+  TORCH_CHECK(nb >= 1 && nb <= 3 && W >= 1 && W <= 1024, "ps_qpack: bad record shape");
+  TORCH_CHECK(desc.dim() == 2 && desc.size(1) == 6 && desc.size(0) >= 1, "ps_qpack: desc [P, 6]");
+  c10::DeviceGuard g(x.device());
+  auto out = torch::empty({rows, wh::quant_record_bytes((int)W, (int)nb)},
+                          x.options().dtype(torch::kUInt8));
+  wh::qregion_pack(ptr<float>(x), ptr<int64_t>(desc), (int)desc.size(0), rows, (int)W, (int)nb,
+                   (uint64_t)seed, ptr<uint8_t>(out), cur_stream(x));
+  return out;
+}
+
+void ps_qunpack(const Tensor& q, const Tensor& desc, int64_t W, int64_t nb, const Tensor& out) {
+  CHECK_IN(q, torch::kUInt8);
+  CHECK_IN(desc, torch::kInt64);
+  CHECK_IN(out, torch::kFloat32);
+  TORCH_CHECK(nb >= 1 && nb <= 3 && q.dim() == 2 &&
+                  q.size(1) == wh::quant_record_bytes((int)W, (int)nb),
+              "ps_qunpack: bad record size");
+  TORCH_CHECK(desc.dim() == 2 && desc.size(1) == 6 && desc.size(0) >= 1, "ps_qunpack: desc [P, 6]");
+  c10::DeviceGuard g(q.device());
+  wh::qregion_unpack(ptr<uint8_t>(q), ptr<int64_t>(desc), (int)desc.size(0), q.size(0), (int)W,
+                     (int)nb, ptr<float>(out), cur_stream(q));
+}
+
 Tensor trunc_u8(const Tensor& c) {
   CHECK_IN(c, torch::kInt32);
   c10::DeviceGuard g(c.device());
@@ -3015,6 +3045,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("key_mod", &key_mod);
   m.def("dequant_rows", &dequant_rows);
   m.def("trunc_u8", &trunc_u8);
+  m.def("ps_qpack", &ps_qpack, py::arg("x"), py::arg("desc"), py::arg("rows"), py::arg("W"),
+        py::arg("nb"), py::arg("seed"));
+  m.def("ps_qunpack", &ps_qunpack, py::arg("q"), py::arg("desc"), py::arg("W"), py::arg("nb"),
+        py::arg("out"));
   m.def("auc_acc", &auc_acc);
   m.def("auc_acc_side", &auc_acc_side);
   m.def("auc_join", &auc_join);

@@ -141,6 +141,18 @@ __device__ __forceinline__ float linear_update(KVSlot& e, float g, const LinearH
     e.sq = sq;
     const float eta = (sq + hp.beta) / hp.alpha;
     neww = l1l2_solve(eta * oldw - g, eta, hp.l1, hp.l2);
+  } else if (hp.algo == 4) {  // DiFacto's FTRL on w (an embedding-free DiFacto
+    // model over the linear wire format; reference UpdateW,
+    // learn/difacto/async_sgd.h:262-286: l2 in the gradient, l1 threshold)
+    const float gg = g + hp.l2 * oldw;
+    const float cg = e.sq;
+    const float cg_new = sqrtf(cg * cg + gg * gg);
+    e.sq = cg_new;
+    const float z = e.z - (gg - (cg_new - cg) / hp.alpha * oldw);
+    e.z = z;
+    neww = (z <= hp.l1 && z >= -hp.l1)
+               ? 0.f
+               : (z > 0 ? z - hp.l1 : z + hp.l1) / ((hp.beta + cg_new) / hp.alpha);
   } else {  // FTRL
     const float sq0 = e.sq;
     const float sq = sqrtf(sq0 * sq0 + g * g);

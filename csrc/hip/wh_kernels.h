@@ -561,6 +561,12 @@ int64_t quant_record_bytes(int w, int nb);
 void quant_rows(const float* x, int64_t rows, int w, int nb, uint64_t seed, uint8_t* out,
                 hipStream_t s);
 void dequant_rows(const uint8_t* in, int64_t rows, int w, int nb, float* x, hipStream_t s);
+// region filter of the multi-shard exchange: desc int64 [P, 6] {sf, a, vf,
+// nf, sq, ha} per peer (quant.hip); rows = wire rows of R bytes in all
+void qregion_pack(const float* x, const int64_t* desc, int P, int64_t rows, int W, int nb,
+                  uint64_t seed, uint8_t* out, hipStream_t s);
+void qregion_unpack(const uint8_t* in, const int64_t* desc, int P, int64_t rows, int W, int nb,
+                    float* x, hipStream_t s);
 void trunc_u8(const int32_t* c, int64_t n, uint8_t* out, hipStream_t s);
 
 // -------------------------------------------------------------- exchange

@@ -73,6 +73,25 @@ def test_loopback_strict_matches_single_shard():
         assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (p1, p4)
 
 
+def test_embedding_free_difacto_loopback_matches_single_shard():
+    """A DiFacto model without an embedding takes the multi-shard step's
+    linear wire format; the owner push applies DiFacto's FTRL on w (algo 4,
+    learn/difacto/async_sgd.h:262-286): the same model as one shard."""
+    from wormhole_amd.config.schema import DifactoConfig
+    from wormhole_amd.parallel.comm import Comm, LoopbackComm
+    conf = lambda: DifactoConfig(lambda_l1=0.01, lambda_l2=0.1, max_concurrency=1)  # noqa
+    one, p1, _ = _run(Comm("cpu", init=False), conf(), "cpu")
+    lb, p4, _ = _run(LoopbackComm(4, "cpu"), conf(), "cpu")
+    assert lb.psx is not None and lb.psx.linear and lb.psx.lin_hp[0] == 4
+    m1, m4 = _model(one), _model(lb)
+    assert m1.keys() == m4.keys() and len(m1) > 100
+    assert sum(1 for w, _, _ in m1.values() if w != 0.0) > 10
+    for k, (w, c, v) in m1.items():
+        assert abs(w - m4[k][0]) < 1e-6, (k, w, m4[k][0])
+    for a, c in zip(p1, p4):
+        assert abs(a - c) <= 1e-4 * max(1.0, abs(a)), (p1, p4)
+
+
 def test_loopback_pipelined_trains_and_drains():
     from wormhole_amd.parallel.comm import Comm, LoopbackComm
     lb, prog, batches = _run(LoopbackComm(3, "cpu"), _conf(), "cpu", steps=8)
@@ -160,16 +179,16 @@ def _two_rank_main(rank, world, port, out_dir, device, max_conc, nshard=None):
         w, c, v = owner[k]
         assert c == n, (k, c, n)
         assert (v is not None) == (n > 3), (k, n)
-    # a fresh pull through the old exchange sees the owners' values
-    keys, label, off = [t.to(dev) for t in batches[-1]]
-    uniq, ucnt, owner_cnt, lid, *_ = ops.localize(keys, off, None, lr.kv.nshard)
-    sess = lr.kv.open(uniq, owner_cnt, insert=False)
-    hdr, vc = lr.kv.difacto_pull(sess, False)
-    vid = ops.hdr_vidx(hdr.cpu()).tolist()
+    # a fresh read-only pull through the exchange sees the owners' values
+    uniq, wp, rows = lr.psx.pull_values(batches[-1][0].to(dev))
+    rows = rows.cpu()
     for i, k in enumerate(uniq.cpu().tolist()):
         w, c, v = owner[k]
-        assert abs(float(hdr[i, 0]) - w) < 1e-7
-        assert (vid[i] >= 0) == (v is not None)
+        assert abs(float(wp[i]) - w) < 1e-7
+        if v is None:
+            assert float(rows[i].abs().sum()) == 0.0
+        else:
+            assert torch.equal(rows[i, :len(v)], torch.tensor(v, dtype=torch.float32))
     comm.barrier()
     with open(os.path.join(out_dir, "r%d" % rank), "w") as f:
         f.write("%r\n" % (prog[0] / prog[5]))
@@ -278,11 +297,12 @@ def test_loopback_gpu_long_run_crosses_tag_wrap(max_conc):
 
 # ---------------------------------------------------------------- linear
 def _lin_run(comm, device, algo=3, steps=6, rows=300, seed=17, max_conc=1, nshard=None,
-             batches=None):
+             batches=None, fixed_bytes=0):
     from wormhole_amd.config.schema import LinearConfig
     from wormhole_amd.data.synthetic import criteo_batch_cpu
     from wormhole_amd.models.linear import LinearLearner
-    conf = LinearConfig(algo=algo, lambda_l1=0.1, lr_eta=0.1, max_concurrency=max_conc)
+    conf = LinearConfig(algo=algo, lambda_l1=0.1, lr_eta=0.1, max_concurrency=max_conc,
+                        fixed_bytes=fixed_bytes)
     lr = LinearLearner(conf, comm, device, cap=1 << 14, seed=5, nshard=nshard)
     if batches is None:
         batches = [[t.to(device) for t in criteo_batch_cpu(rows, seed, s, CARD)]
@@ -329,26 +349,36 @@ def test_linear_loopback_pipelined():
     assert 0 < prog[0] / prog[4] < 1.0
 
 
-def _lin_oracle(all_batches, algo, l1, alpha, beta):
+def _lin_oracle(all_batches, algo, l1, alpha, beta, fixed_bytes=0, nshard=1):
     """Two workers in lockstep against one server, strict order: every step
     both pull the same model, then the owner applies worker 0's push, then
-    worker 1's (ps-lite: one request at a time)."""
+    worker 1's (ps-lite: one request at a time). fixed_bytes: each worker's
+    pushed gradients pass through the payload filter's quantisation (the
+    host reference of the wire format, same records, seeds and rounding)."""
     from wormhole_amd import _native
     from wormhole_amd.kv.cpu_store import CpuKVStore
+    from wormhole_amd.kv.psx import _QFilter
     from wormhole_amd.ops import ref
     st = CpuKVStore(1 << 16, 0, 0)
     host = _native.host()
+    qf = [_QFilter(fixed_bytes, 0, 5, r, True) for r in range(len(all_batches))] \
+        if fixed_bytes else None
     t = 0
     for step in range(len(all_batches[0])):
         pend = []
         for r in range(len(all_batches)):
             keys, label, off = all_batches[r][step]
-            uniq, ucnt, oc, lid, co, cr, cv = host.localize_cpu(keys, off, None, 1)
+            uniq, ucnt, oc, lid, co, cr, cv = host.localize_cpu(keys, off, None, nshard)
             slot = st.find(uniq, True)
             w = st.linear_pull(slot)
             met = torch.zeros(5, dtype=torch.float64)
             py, dual, _ = ref.fm_forward(off, lid, None, w, None, 0, label, 2, met)
             g, _ = ref.fm_backward(co, cr, cv, dual, None, w, None, 0)
+            if qf is not None:
+                n = [int(x) for x in oc[:nshard].tolist()] + [0] * (len(all_batches) - nshard)
+                d, rows, _ = qf[r].layout(n, None, None)
+                q = ref.ps_qpack(g, d, sum(rows), qf[r].W, fixed_bytes, qf[r].next_seed())
+                g = ref.ps_qunpack(q, d, qf[r].W, fixed_bytes, torch.zeros_like(g))
             pend.append((slot, g))
         for slot, g in pend:
             t += 1
@@ -356,7 +386,7 @@ def _lin_oracle(all_batches, algo, l1, alpha, beta):
     return {int(k): float(x) for k, x in zip(st.keys.tolist(), st.w.tolist())}
 
 
-def _lin_two_rank_main(rank, world, port, out_dir, nshard, algo):
+def _lin_two_rank_main(rank, world, port, out_dir, nshard, algo, fixed_bytes=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     torch.set_num_threads(1)
@@ -364,7 +394,9 @@ def _lin_two_rank_main(rank, world, port, out_dir, nshard, algo):
     from wormhole_amd.parallel.comm import Comm
     comm = Comm("cpu")
     mine = [[t for t in criteo_batch_cpu(300, 17 + rank, s, CARD)] for s in range(5)]
-    lr, prog, _ = _lin_run(comm, "cpu", algo=algo, max_conc=1, nshard=nshard, batches=mine)
+    lr, prog, _ = _lin_run(comm, "cpu", algo=algo, max_conc=1, nshard=nshard, batches=mine,
+                           fixed_bytes=fixed_bytes)
+    assert (lr.psx.qf is not None) == bool(fixed_bytes)
     assert lr.psx is not None and lr.psx.nshard == nshard
     model = _lin_model(lr)
     if rank >= nshard:
@@ -375,7 +407,7 @@ def _lin_two_rank_main(rank, world, port, out_dir, nshard, algo):
     for m in allm:
         assert not (owner.keys() & m.keys())
         owner.update(m)
-    ref_m = _lin_oracle(allb, algo, 0.1, 0.1, 1.0)
+    ref_m = _lin_oracle(allb, algo, 0.1, 0.1, 1.0, fixed_bytes, nshard)
     assert owner.keys() == ref_m.keys()
     for k, w in ref_m.items():
         assert abs(owner[k] - w) < 1e-5, (k, owner[k], w)
@@ -393,6 +425,17 @@ def test_linear_two_ranks_gloo_matches_oracle(tmp_path, nshard, algo):
     and AdaGrad."""
     mp.spawn(_lin_two_rank_main, args=(2, _free_port(), str(tmp_path), nshard, algo), nprocs=2,
              join=True)
+    for r in range(2):
+        assert (tmp_path / ("r%d" % r)).read_text() == "ok\n"
+
+
+@pytest.mark.parametrize("nshard,nb", [(2, 2), (1, 1)])
+def test_linear_fixed_bytes_two_ranks_matches_quantized_oracle(tmp_path, nshard, nb):
+    """FIXING_FLOAT on the linear push (learn/linear/async_sgd.h:290-301):
+    the owners' weights equal the lockstep oracle whose pushes pass through
+    the same n-byte records (quantise -> dequantise, same seeds)."""
+    mp.spawn(_lin_two_rank_main, args=(2, _free_port(), str(tmp_path), nshard, 3, nb),
+             nprocs=2, join=True)
     for r in range(2):
         assert (tmp_path / ("r%d" % r)).read_text() == "ok\n"
 

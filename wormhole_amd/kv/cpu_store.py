@@ -207,6 +207,16 @@ class CpuKVStore:
             self._sq[s] = sq
             eta = (sq + f32(beta)) / f32(alpha)
             new = self._solve(eta * old - g, eta, f32(l1), f32(l2))
+        elif algo == 4:  # DiFacto's FTRL on w (learn/difacto/async_sgd.h:262-286)
+            gg = (g + f32(l2) * old).astype(np.float32)
+            cg = self._sq[s]
+            cg_new = np.sqrt(cg * cg + gg * gg).astype(np.float32)
+            self._sq[s] = cg_new
+            z = (self._z[s] - (gg - (cg_new - cg) / f32(alpha) * old)).astype(np.float32)
+            self._z[s] = z
+            eta = (f32(beta) + cg_new) / f32(alpha)
+            new = np.where((z <= f32(l1)) & (z >= -f32(l1)), f32(0),
+                           np.where(z > 0, z - f32(l1), z + f32(l1)) / eta).astype(np.float32)
         else:
             sq0 = self._sq[s]
             sq = np.sqrt(sq0 * sq0 + g * g).astype(np.float32)

@@ -50,6 +50,17 @@ The linear model (learn/linear/async_sgd.h:240-301: ZPull w -> gradient ->
 ZPush) runs the same pipeline with C1 = 8-byte keys, C2 = one w per key, C3 =
 one gradient per key; its owner push applies SGD / AdaGrad / FTRL over all
 segments in one launch, each worker's gradients as one request in peer order.
+An embedding-free DiFacto model takes the same wire format, its owner push
+applying DiFacto's FTRL on w (push algo 4).
+
+Payload filter (``fixed_bytes`` 1-3: ps-lite FIXING_FLOAT,
+learn/difacto/async_sgd.h:428-445, learn/linear/async_sgd.h:290-301): the
+embedding rows of C2 / C3 (DiFacto) and the gradients of C3 (linear: the
+reference filters its pushes only) travel as n-byte fixed point with one
+scale per 64-float record and unbiased random rounding, the {w, vidx}
+headers exact (csrc/hip/quant.hip qregion kernels: packed on the producer's
+stream right before the collective, unpacked by its consumer); the feature
+counts of C1 saturate at 255 (TRUNCATE_FLOAT(1) of the count push).
 """
 import contextlib
 import os
@@ -89,7 +100,7 @@ class _Step:
                  "segHS_o", "keys_o", "slot", "vpos", "chain", "head", "rbuf", "vcnt",
                  "ev_open", "ev_grad",
                  "vown", "vrecv", "vrecv_d", "rrecv", "hdr", "rows", "py", "dual", "xv",
-                 "gpush", "gvc", "seed_step", "w_c1", "w_c2", "w_c3")
+                 "gpush", "gvc", "seed_step", "w_c1", "w_c2", "w_c3", "q2", "q3")
 
     def __init__(self):
         for s in self.__slots__:
@@ -161,6 +172,48 @@ class _CollTimer:
         return out
 
 
+class _QFilter:
+    """The fixed_bytes payload filter's region tables (see the module doc):
+    per peer {sf, a, vf, nf, sq, ha} -- float offset of the region, exact
+    floats, offset and count of the quantised floats, first wire row, raw
+    wire rows -- from the host-known key / row counts of a step."""
+
+    def __init__(self, nb, vs, seed, rank, linear):
+        from ..ops import ref
+        self.nb = int(nb)
+        self.vs = max(int(vs), 1)
+        self.linear = linear
+        self.W = 64 if linear else self.vs  # floats per record
+        self.R = ref.quant_record_bytes(self.W, self.nb)
+        self.seed = (int(seed) * 0x9E3779B1 + 17 * int(rank) + 1) & 0x7FFFFFFFFFFF
+        self.calls = 0
+
+    def layout(self, n, v, H):
+        """n keys, v embedding rows, H header rows per peer -> (desc [P, 6],
+        wire rows per peer, floats of the float layout)."""
+        P = len(n)
+        d = np.zeros((P, 6), dtype=np.int64)
+        rows = []
+        sf = sq = 0
+        for p in range(P):
+            if self.linear:
+                a, vf, nf, ha = 0, 0, int(n[p]), 0
+                nr, ext = _cdiv(int(n[p]), self.W), int(n[p])
+            else:
+                a, vf, nf = 2 * int(n[p]), int(H[p]) * self.vs, int(v[p]) * self.vs
+                ha, nr = _cdiv(4 * a, self.R), int(v[p])
+                ext = (int(H[p]) + int(v[p])) * self.vs
+            d[p] = (sf, a, vf, nf, sq, ha)
+            rows.append(ha + nr)
+            sf += ext
+            sq += ha + nr
+        return d, rows, sf
+
+    def next_seed(self):
+        self.calls += 1
+        return self.seed + (self.calls << 20)
+
+
 class Psx:
     """The pipelined multi-shard step of both PS learners (DiFacto:
     vstride > 0; linear: vstride == 0, where C1 moves 8-byte keys, C2 one
@@ -207,6 +260,14 @@ class Psx:
         self.wire = [0, 0, 0, 0]
         # WH_COMM_TIMING=1: per-collective (issue-ready -> landed) GPU times
         self.timer = _CollTimer(self.dev) if (self.cuda and _COMM_TIMING) else None
+        fb = int(getattr(lrn.conf, "fixed_bytes", 0) or 0)
+        if fb not in (0, 1, 2, 3):
+            raise ValueError("fixed_bytes must be 0, 1, 2 or 3")
+        self.qf = _QFilter(fb, self.vs, lrn.seed, getattr(self.comm, "rank", 0),
+                           self.linear) if fb else None
+        # the owner-side update of the linear wire format: (algo, alpha,
+        # beta, l1, l2) -- the linear model's, or DiFacto's FTRL on w (algo 4)
+        self.lin_hp = lrn.psx_linear_hp() if self.linear else None
 
     # ------------------------------------------------------------ wire stats
     def _tally(self, c, x, send_rows):
@@ -215,6 +276,32 @@ class Psx:
             row *= int(d)
         r = getattr(self.comm, "rank", 0)
         self.wire[c] += row * (sum(int(v) for v in send_rows) - int(send_rows[r]))
+
+    def _qpack(self, x, send, recv, vsend, vrecv, Hs, Hr):
+        """fixed_bytes: quantise the float regions x (this side: n = send,
+        v = vsend, H = Hs per peer) into wire rows, on S behind x's producer.
+        Returns (wire tensor, wire rows per peer out / in, the unpack plan of
+        the receiving side)."""
+        qf = self.qf
+        ds, srows, ext = qf.layout(send, vsend, Hs)
+        dr, rrows, rext = qf.layout(recv, vrecv, Hr)
+        if ext != x.numel():
+            raise RuntimeError("psx filter: region layout %d floats vs buffer %d" % (
+                ext, x.numel()))
+        P = len(send)
+        a = np.concatenate([ds.reshape(-1), dr.reshape(-1)])
+        t = self.pins.put(a) if self.cuda else torch.from_numpy(a)
+        q = ops.ps_qpack(x, ds, t[:6 * P].view(P, 6), sum(srows), qf.W, qf.nb, qf.next_seed())
+        return q, srows, rrows, (dr, t[6 * P:].view(P, 6), rext)
+
+    def _qunpack(self, q, plan):
+        """The receiving side: wire rows -> the float layout the consumer
+        kernel expects (after the collective has landed)."""
+        dr, dd, rext = plan
+        vs = 1 if self.linear else self.vs
+        out = torch.empty((rext // vs, vs) if not self.linear else (rext,),
+                          dtype=torch.float32, device=q.device)
+        return ops.ps_qunpack(q, dr, dd, self.qf.W, self.qf.nb, out)
 
     def _a2a(self, c, x, send_rows, recv_rows, ready=None):
         """Issue collective Cc (async) and account for its bytes.
@@ -423,7 +510,10 @@ class Psx:
         if self.linear:
             rec = st.uniq  # 8-byte keys
         else:
-            rec = ops.ps_records(st.uniq, st.ucnt if st.use_cnt else None)
+            cnt = st.ucnt if st.use_cnt else None
+            if cnt is not None and self.qf is not None:
+                cnt = cnt.clamp(max=255)  # TRUNCATE_FLOAT(1) of the count push
+            rec = ops.ps_records(st.uniq, cnt)
         st.keys_o, st.w_c1 = self._a2a(1, rec, st.send, st.recv)
 
     def _open(self, st, insert):
@@ -450,8 +540,14 @@ class Psx:
         recv_rows = [st.Hw[q] + st.vrecv[q] for q in range(P)]
         if self.linear:  # one w per key
             send_rows, recv_rows = st.recv, st.send
-        st.rrecv, st.w_c2 = self._a2a(2, st.rbuf[:sum(send_rows)], send_rows, recv_rows,
-                                      st.ev_open)
+        x, ready = st.rbuf[:sum(send_rows)], st.ev_open
+        st.q2 = None
+        if self.qf is not None and not self.linear:  # (linear pulls travel exact)
+            with streams.on(self.S) if self.cuda else contextlib.nullcontext():
+                x, send_rows, recv_rows, st.q2 = self._qpack(x, st.recv, st.send, st.vown,
+                                                             st.vrecv, st.Ho, st.Hw)
+                ready = self._event()
+        st.rrecv, st.w_c2 = self._a2a(2, x, send_rows, recv_rows, ready)
         st.ev_open = None
         st.rbuf = None
 
@@ -460,6 +556,8 @@ class Psx:
         lrn = self.lrn
         st.w_c2.wait()
         st.w_c2 = None
+        if st.q2 is not None:
+            st.rrecv, st.q2 = self._qunpack(st.rrecv, st.q2), None
         if self.linear:
             st.hdr = st.rrecv
             st.py, st.dual, st.xv = ops.fm_forward(st.offset, st.lid, st.val, st.rrecv, None, 0,
@@ -481,7 +579,14 @@ class Psx:
         recv_rows = [st.Ho[p] + st.vown[p] for p in range(P)]
         if self.linear:  # one gradient per key
             send_rows, recv_rows = st.send, st.recv
-        st.gpush, st.w_c3 = self._a2a(3, st.gvc, send_rows, recv_rows, st.ev_grad)
+        x, ready = st.gvc, st.ev_grad
+        st.q3 = None
+        if self.qf is not None:
+            with streams.on(self.S) if self.cuda else contextlib.nullcontext():
+                x, send_rows, recv_rows, st.q3 = self._qpack(x, st.send, st.recv, st.vrecv,
+                                                             st.vown, st.Hw, st.Ho)
+                ready = self._event()
+        st.gpush, st.w_c3 = self._a2a(3, x, send_rows, recv_rows, ready)
         st.ev_grad = None
         st.gvc = None
 
@@ -524,11 +629,13 @@ class Psx:
         """Apply a landed push on the owner (one launch over all segments)."""
         lrn = self.lrn
         st.w_c3.wait()
+        if st.q3 is not None:
+            st.gpush, st.q3 = self._qunpack(st.gpush, st.q3), None
         if self.linear:
+            algo, alpha, beta, l1, l2 = self.lin_hp
             self.store.ps_push_linear(
                 slot=st.slot, chain=st.chain, head=st.head, segS=st.segS_o, g=st.gpush,
-                algo=lrn.conf.algo, alpha=lrn.alpha, beta=lrn.beta, l1=lrn.conf.lambda_l1,
-                l2=lrn.conf.lambda_l2, t0=float(self.requests))
+                algo=algo, alpha=alpha, beta=beta, l1=l1, l2=l2, t0=float(self.requests))
             self.requests += self.P  # one request per worker (ps-lite SGD's t)
         else:
             self.store.ps_push(slot=st.slot, vpos=st.vpos, chain=st.chain, head=st.head,
@@ -640,6 +747,40 @@ class Psx:
         self._reply(st)
         self.lrn.step += 1
         return st.py
+
+    def pull_values(self, keys):
+        """Read-only pull of ``keys``' current values from their owners
+        through the same exchange (no insert, no metrics) -- a collective,
+        every rank calls it with its own keys. Returns (uniq, w [U], rows)
+        with rows [U, vstride] (zero for keys without an embedding) or None
+        for the linear wire format; None if no rank has keys."""
+        self.flush()
+        n = int(keys.numel())
+        dev = keys.device
+        offset = torch.arange(n + 1, dtype=torch.int64, device=dev)
+        self._ensure_job(keys, offset, None)
+        send, recv, empty = self._counts()
+        if empty:
+            self._drop_empty()
+            return None
+        st = self._new_step(send, recv, None, False, 1, None)
+        self._set_loc(st, self._finish(), offset, None)
+        self._c1(st)
+        self._open(st, False)
+        self._vcount_exchange(st)
+        self._upload_vrecv(st)
+        self._c2(st)
+        st.w_c2.wait()
+        if st.q2 is not None:
+            st.rrecv, st.q2 = self._qunpack(st.rrecv, st.q2), None
+        if self.linear:
+            return st.uniq, st.rrecv.reshape(-1), None
+        hdr, _ = ops.ps_unpack(st.rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d)
+        vid = ops.hdr_vidx(hdr).long()
+        rows = torch.zeros(st.U, self.vs, dtype=torch.float32, device=dev)
+        has = vid >= 0
+        rows[has] = st.rrecv[vid[has]]
+        return st.uniq, hdr[:, 0].contiguous(), rows
 
     def _upload_vrecv(self, st):
         a = np.array(st.vrecv, dtype=np.int64)

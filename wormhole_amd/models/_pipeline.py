@@ -32,8 +32,7 @@ def localize_current(lrn, keys, offset, val):
     if job is not None and job[0] is keys:
         return ops.localize_finish(job[1])
     k = ops.key_mod(keys, lrn.max_key) if lrn.max_key else keys
-    return ops.localize(k, offset, val, lrn.kv.nshard, lrn.uhint,
-                        exchange=lrn.kv.count_exchange())
+    return ops.localize(k, offset, val, lrn.kv.nshard, lrn.uhint)
 
 
 # DiFacto begins the next minibatch's localize right AFTER enqueueing this
@@ -66,8 +65,7 @@ def begin_next(lrn, next_batch, uhint):
                 t.record_stream(cur)
         with streams.on(side):
             k = ops.key_mod(nk, lrn.max_key) if lrn.max_key else nk
-            job = ops.localize_begin(k, no, nv, lrn.kv.nshard, uhint,
-                                     exchange=lrn.kv.count_exchange())
+            job = ops.localize_begin(k, no, nv, lrn.kv.nshard, uhint)
         lrn._job = (nk, job)
         return
     if ready is not None and nk.is_cuda:
@@ -77,8 +75,7 @@ def begin_next(lrn, next_batch, uhint):
             if t is not None:
                 t.record_stream(cur)
     k = ops.key_mod(nk, lrn.max_key) if lrn.max_key else nk
-    lrn._job = (nk, ops.localize_begin(k, no, nv, lrn.kv.nshard, uhint,
-                                       exchange=lrn.kv.count_exchange()))
+    lrn._job = (nk, ops.localize_begin(k, no, nv, lrn.kv.nshard, uhint))
 
 
 # Since the partitioned localize (LDS dedup, no global atomics) the side

@@ -67,8 +67,8 @@ class DifactoLearner:
         # over; kv/psx.py reads it from the count exchange's flags)
         self.last_empty = False
         # P > 1 ranks: the lean pipelined exchange (kv/psx.py), whatever the
-        # number of server shards S <= P. (The ShardedKV exchange remains for
-        # the lossy fixed_bytes payload filter and embedding-free models.)
+        # number of server shards S <= P, with or without the fixed_bytes
+        # payload filter and embedding.
         # One shard on the GPU: the FM kernels read the V rows in place in the
         # table's slab instead of a pulled copy (kv.difacto_open_pull direct)
         # -- unless the embedding gradients are post-processed (clipping /
@@ -78,9 +78,16 @@ class DifactoLearner:
         self.direct_pull = (self.device.type == "cuda" and comm.size == 1 and self.vstride > 0
                             and not post and os.environ.get("WH_DIFACTO_PULL", "") != "copy")
         self.psx = None
-        if comm.size > 1 and self.vstride > 0 and not self.kv.fixed_bytes:
+        if comm.size > 1:
             from ..kv.psx import Psx
             self.psx = Psx(self)
+
+    def psx_linear_hp(self):
+        """Embedding-free model on the multi-shard step's linear wire format:
+        the owner applies DiFacto's FTRL on w (push algo 4,
+        learn/difacto/async_sgd.h:262-286)."""
+        c = self.conf
+        return 4, float(c.lr_eta), float(c.lr_beta), float(c.lambda_l1), float(c.lambda_l2)
 
     # ------------------------------------------------------------------ step
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):

@@ -74,6 +74,13 @@ class LinearLearner:
     def _localize(self, keys, offset, val, next_batch):
         return localize_pipelined(self, keys, offset, val, next_batch)
 
+    def psx_linear_hp(self):
+        """Owner update of the multi-shard step (kv/psx.py): the conf's
+        SGD / AdaGrad / FTRL (learn/linear/async_sgd.h:71-180)."""
+        c = self.conf
+        return int(c.algo), float(self.alpha), float(self.beta), float(c.lambda_l1), float(
+            c.lambda_l2)
+
     def process(self, keys, offset, val, label, wtype=TRAIN, data_pass=0, next_batch=None):
         train = wtype == TRAIN
         if self.psx is not None:

@@ -207,6 +207,24 @@ def dequant_rows(q, w, nb):
     return ref.dequant_rows(q, w, nb)
 
 
+def ps_qpack(x, desc_h, desc_d, rows, W, nb, seed):
+    """Multi-shard exchange payload filter (fixed_bytes): float regions ->
+    uint8 wire rows (see csrc/hip/quant.hip qregion). desc_h: the host copy
+    of the per-peer table (bounds-checked by the caller), desc_d: the same
+    on x's device."""
+    if _gpu(x):
+        return _native.hip().ps_qpack(x=x.contiguous(), desc=desc_d, rows=int(rows), W=int(W),
+                                      nb=int(nb), seed=int(seed))
+    return ref.ps_qpack(x, desc_h, rows, W, nb, seed)
+
+
+def ps_qunpack(q, desc_h, desc_d, W, nb, out):
+    if _gpu(q):
+        _native.hip().ps_qunpack(q=q.contiguous(), desc=desc_d, W=int(W), nb=int(nb), out=out)
+        return out
+    return ref.ps_qunpack(q, desc_h, W, nb, out)
+
+
 def trunc_u8(c):
     """feature counts -> uint8, saturating (the count push's TRUNCATE filter)."""
     if _gpu(c) and c.dtype == torch.int32:

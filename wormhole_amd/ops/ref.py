@@ -249,6 +249,73 @@ def trunc_u8(c):
     return c.clamp(0, 255).to(torch.uint8)
 
 
+def ps_qpack(x, desc, rows, W, nb, seed):
+    """Region payload filter of the multi-shard exchange (oracle of
+    csrc/hip/quant.hip k_qregion_pack): desc int64 [P, 6] {sf, a, vf, nf, sq,
+    ha} per peer -> uint8 [rows, R] wire rows."""
+    import numpy as np
+    from ..kv.cpu_store import uhash01
+    xf = x.detach().reshape(-1).cpu().numpy().astype(np.float32)
+    d = np.asarray(desc, dtype=np.int64).reshape(-1, 6)
+    R = quant_record_bytes(W, nb)
+    out = np.zeros((rows, R), dtype=np.uint8)
+    lim = _qmax(nb)
+    for sf, a, vf, nf, sq, ha in d.tolist():
+        if ha:  # raw words: the exact part, zero-padded to whole rows
+            raw = np.zeros(ha * (R // 4), dtype=np.float32)
+            raw[:a] = xf[sf:sf + a]
+            out[sq:sq + ha] = raw.view(np.uint8).reshape(ha, R)
+        nr = -(-nf // W)
+        if not nr:
+            continue
+        blk = np.zeros(nr * W, dtype=np.float32)
+        blk[:nf] = xf[sf + vf:sf + vf + nf]
+        blk = blk.reshape(nr, W)
+        valid = (np.arange(nr * W).reshape(nr, W) < nf)
+        m = np.abs(blk).max(axis=1)
+        scale = np.where(m > 0, m / np.float32(lim), np.float32(1.0)).astype(np.float32)
+        inv = (np.float32(1.0) / scale).astype(np.float32)
+        r0 = sq + ha
+        rr = np.arange(r0, r0 + nr, dtype=np.uint64)[:, None]
+        cc = np.arange(W, dtype=np.uint64)[None, :]
+        u = uhash01(seed, rr, cc)
+        q = np.clip(np.floor(blk * inv[:, None] + u), -lim, lim).astype(np.int64)
+        q = np.where(valid, q, 0)
+        rec = out[r0:r0 + nr]
+        rec[:, :4] = scale.view(np.uint8).reshape(nr, 4)
+        uq = (q & ((1 << (8 * nb)) - 1)).astype(np.uint64)
+        for bb in range(nb):
+            rec[:, 4 + bb:4 + W * nb:nb] = ((uq >> np.uint64(8 * bb)) & np.uint64(0xff)).astype(
+                np.uint8)
+    return torch.from_numpy(out)
+
+
+def ps_qunpack(q, desc, W, nb, out):
+    """Inverse of :func:`ps_qpack` into the float layout ``out`` (in place)."""
+    import numpy as np
+    qn = q.cpu().numpy()
+    d = np.asarray(desc, dtype=np.int64).reshape(-1, 6)
+    R = quant_record_bytes(W, nb)
+    of = out.view(-1)
+    for sf, a, vf, nf, sq, ha in d.tolist():
+        if a:
+            raw = np.ascontiguousarray(qn[sq:sq + ha]).reshape(-1).view(np.float32)
+            of[sf:sf + a] = torch.from_numpy(raw[:a].copy())
+        nr = -(-nf // W)
+        if not nr:
+            continue
+        rec = qn[sq + ha:sq + ha + nr]
+        scale = np.ascontiguousarray(rec[:, :4]).view(np.float32).reshape(nr)
+        u = np.zeros((nr, W), dtype=np.int64)
+        for bb in range(nb):
+            u |= rec[:, 4 + bb:4 + W * nb:nb].astype(np.int64) << (8 * bb)
+        sh = 64 - 8 * nb
+        iv = (u << sh) >> sh
+        vals = (iv.astype(np.float32) * scale[:, None]).reshape(-1)[:nf]
+        of[sf + vf:sf + vf + nf] = torch.from_numpy(vals.astype(np.float32))
+    return out
+
+
 # ------------------------------------------------- multi-shard exchange (psx)
 def ps_unpack(rbuf, U, segS, segHS, vrecv):
     """Worker side of the P-shard pull (oracle of psx.hip k_ps_unpack):
