@@ -1787,6 +1787,49 @@ Tensor kmeans_accum(const Tensor& X, const Tensor& assign, int64_t k) {
   return sums;
 }
 
+// sparse k-means (CSR rows): offset int64 [n + 1] (offset[0] == 0), col int32
+// [nnz] (all < F = Ct.size(0), checked by the caller once per dataset), val
+// float [nnz] or None (all ones), Ct [F, Kp] float (transposed centroids)
+Tensor kmeans_assign_csr(const Tensor& offset, const Tensor& col, const c10::optional<Tensor>& val,
+                         const Tensor& Ct, int64_t K) {
+  CHECK_IN(offset, torch::kInt64);
+  CHECK_IN(col, torch::kInt32);
+  CHECK_IN(Ct, torch::kFloat32);
+  const int64_t n = offset.numel() - 1;
+  TORCH_CHECK(n >= 0 && Ct.dim() == 2 && K >= 1 && Ct.size(1) >= K && Ct.size(1) % 4 == 0,
+              "kmeans_assign_csr: Ct must be [F, Kp >= K], Kp % 4 == 0");
+  const float* vp = nullptr;
+  if (val.has_value() && val->defined()) {
+    CHECK_IN((*val), torch::kFloat32);
+    TORCH_CHECK(val->numel() == col.numel(), "kmeans_assign_csr: val / col size");
+    vp = ptr<float>(*val);
+  }
+  c10::DeviceGuard g(Ct.device());
+  auto assign = torch::empty({std::max<int64_t>(n, 0)}, Ct.options().dtype(torch::kInt32));
+  wh::kmeans_assign_csr(ptr<int64_t>(offset), ptr<int32_t>(col), vp, n, ptr<float>(Ct), (int)K,
+                        (int)Ct.size(1), ptr<int32_t>(assign), cur_stream(Ct));
+  return assign;
+}
+
+Tensor kmeans_accum_csr(const Tensor& offset, const Tensor& col, const c10::optional<Tensor>& val,
+                        const Tensor& assign, int64_t K, int64_t F) {
+  CHECK_IN(offset, torch::kInt64);
+  CHECK_IN(col, torch::kInt32);
+  CHECK_IN(assign, torch::kInt32);
+  const int64_t n = offset.numel() - 1;
+  TORCH_CHECK(assign.numel() == n && K >= 1 && F >= 1, "kmeans_accum_csr: sizes");
+  const float* vp = nullptr;
+  if (val.has_value() && val->defined()) {
+    CHECK_IN((*val), torch::kFloat32);
+    vp = ptr<float>(*val);
+  }
+  c10::DeviceGuard g(col.device());
+  auto sums = torch::zeros({K, F + 1}, col.options().dtype(torch::kFloat32));
+  wh::kmeans_accum_csr(ptr<int64_t>(offset), ptr<int32_t>(col), vp, n, ptr<int32_t>(assign),
+                       (int)F, ptr<float>(sums), cur_stream(col));
+  return sums;
+}
+
 // (new C [k, f], empty-cluster count int64 [1]) from sums [k, f + 1] and C
 std::vector<Tensor> kmeans_update(const Tensor& sums, const Tensor& C) {
   CHECK_IN(sums, torch::kFloat32);
@@ -3077,6 +3120,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("kmeans_assign", &kmeans_assign);
   m.def("kmeans_accum", &kmeans_accum);
   m.def("kmeans_update", &kmeans_update);
+  m.def("kmeans_assign_csr", &kmeans_assign_csr, py::arg("offset"), py::arg("col"),
+        py::arg("val"), py::arg("Ct"), py::arg("K"));
+  m.def("kmeans_accum_csr", &kmeans_accum_csr, py::arg("offset"), py::arg("col"), py::arg("val"),
+        py::arg("assign"), py::arg("K"), py::arg("F"));
   m.def("kmeans_pack_x3", &kmeans_pack_x3);
   // every argument named: the Python side calls these by keyword (a dropped
   // argument fails on the CPU signature test, tests/test_native_signatures.py)

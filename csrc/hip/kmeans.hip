@@ -515,6 +515,138 @@ void kmeans_update(const float* sums, const float* C, int k, int f, float* out,
   hipLaunchKernelGGL(k_km_update, dim3((unsigned)k), dim3(128), 0, s, sums, C, f, out, nempty);
 }
 
+// ---- sparse (CSR) input ---------------------------------------------------
+// The reference clusters libsvm rows directly (learn/kmeans/kmeans.cc:108-130:
+// Cos() walks a Row<unsigned>, only the K x F centroids are dense). Here the
+// rows stay CSR in HBM; the centroids are read through their transpose Ct
+// [F, Kp] (Kp = K rounded up to 4), so each non-zero (j, x) of a row gathers
+// ONE contiguous centroid column Ct[j, :] -- float4 per lane, 1 KB per wave
+// instruction -- and the wave accumulates x * Ct[j, k] for its row in double
+// (the reference's `double rdot`), 4 * PER clusters per lane per pass. The
+// argmax (ties: the smaller k, the reference's strict `>`) is a wave
+// reduction; K beyond one pass re-walks the row per pass of 256 * PER
+// clusters. ||x|| does not change a row's argmax and is not computed.
+namespace {
+constexpr int kCsrRows = 4;  // rows (waves) per 256-thread block
+
+__device__ __forceinline__ bool km_better(double v, int k, double bv, int bk) {
+  return v > bv || (v == bv && k < bk);
+}
+
+template <int PER>
+__global__ __launch_bounds__(256) void k_assign_csr(const int64_t* __restrict__ off,
+                                                    const int32_t* __restrict__ col,
+                                                    const float* __restrict__ val, int64_t n,
+                                                    const float* __restrict__ Ct, int K, int Kp,
+                                                    int32_t* __restrict__ assign) {
+  const int64_t row = (int64_t)blockIdx.x * kCsrRows + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const int64_t b = off[row], e = off[row + 1];
+  double best = -INFINITY;
+  int bk = 0x7fffffff;
+  for (int k0 = 0; k0 < K; k0 += 256 * PER) {
+    double acc[PER][4];
+#pragma unroll
+    for (int g = 0; g < PER; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[g][q] = 0.0;
+    for (int64_t j0 = b; j0 < e; j0 += 64) {
+      const int m = e - j0 < 64 ? (int)(e - j0) : 64;
+      const int c = lane < m ? col[j0 + lane] : 0;
+      const float x = lane < m ? (val ? val[j0 + lane] : 1.f) : 0.f;
+      // kCsrU non-zeros per step: their centroid-column loads are all issued
+      // before the first accumulation (one dependent round trip per step)
+      constexpr int kCsrU = 4;
+      for (int t0 = 0; t0 < m; t0 += kCsrU) {
+        float4 v[kCsrU][PER];
+        double xj[kCsrU];
+#pragma unroll
+        for (int u = 0; u < kCsrU; ++u) {
+          const int t = t0 + u < m ? t0 + u : m - 1;
+          const int cj = __shfl(c, t, 64);
+          xj[u] = t0 + u < m ? (double)__shfl(x, t, 64) : 0.0;
+          const float* cr = Ct + (int64_t)cj * Kp + k0;
+#pragma unroll
+          for (int g = 0; g < PER; ++g) {
+            const int kk = 4 * (lane + 64 * g);
+            v[u][g] = k0 + kk < Kp ? *reinterpret_cast<const float4*>(cr + kk)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < kCsrU; ++u)
+#pragma unroll
+          for (int g = 0; g < PER; ++g) {
+            acc[g][0] += (double)v[u][g].x * xj[u];
+            acc[g][1] += (double)v[u][g].y * xj[u];
+            acc[g][2] += (double)v[u][g].z * xj[u];
+            acc[g][3] += (double)v[u][g].w * xj[u];
+          }
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < PER; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = k0 + 4 * (lane + 64 * g) + q;
+        if (k < K && km_better(acc[g][q], k, best, bk)) {
+          best = acc[g][q];
+          bk = k;
+        }
+      }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double v2 = __shfl_xor(best, o, 64);
+    const int k2 = __shfl_xor(bk, o, 64);
+    if (km_better(v2, k2, best, bk)) {
+      best = v2;
+      bk = k2;
+    }
+  }
+  if (lane == 0) assign[row] = bk;
+}
+
+// sums[a, col] += x and sums[a, F] += 1 for each row (a = its cluster)
+__global__ __launch_bounds__(256) void k_accum_csr(const int64_t* __restrict__ off,
+                                                   const int32_t* __restrict__ col,
+                                                   const float* __restrict__ val, int64_t n,
+                                                   const int32_t* __restrict__ assign, int F,
+                                                   float* __restrict__ sums) {
+  const int64_t row = (int64_t)blockIdx.x * kCsrRows + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= n) return;
+  const int64_t b = off[row], e = off[row + 1];
+  float* sr = sums + (int64_t)assign[row] * (F + 1);
+  if (lane == 0) atomicAdd(sr + F, 1.f);
+  for (int64_t j = b + lane; j < e; j += 64) atomicAdd(sr + col[j], val ? val[j] : 1.f);
+}
+}  // namespace
+
+int kmeans_csr_per(int K) {
+  return K <= 256 ? 1 : K <= 512 ? 2 : K <= 1024 ? 4 : 8;
+}
+
+void kmeans_assign_csr(const int64_t* off, const int32_t* col, const float* val, int64_t n,
+                       const float* Ct, int K, int Kp, int32_t* assign, hipStream_t s) {
+  if (n <= 0) return;
+  const dim3 grid((unsigned)((n + kCsrRows - 1) / kCsrRows)), block(256);
+  switch (kmeans_csr_per(K)) {
+    case 1: hipLaunchKernelGGL(k_assign_csr<1>, grid, block, 0, s, off, col, val, n, Ct, K, Kp, assign); break;
+    case 2: hipLaunchKernelGGL(k_assign_csr<2>, grid, block, 0, s, off, col, val, n, Ct, K, Kp, assign); break;
+    case 4: hipLaunchKernelGGL(k_assign_csr<4>, grid, block, 0, s, off, col, val, n, Ct, K, Kp, assign); break;
+    default: hipLaunchKernelGGL(k_assign_csr<8>, grid, block, 0, s, off, col, val, n, Ct, K, Kp, assign); break;
+  }
+}
+
+void kmeans_accum_csr(const int64_t* off, const int32_t* col, const float* val, int64_t n,
+                      const int32_t* assign, int F, float* sums, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_accum_csr, dim3((unsigned)((n + kCsrRows - 1) / kCsrRows)), dim3(256), 0,
+                     s, off, col, val, n, assign, F, sums);
+}
+
 }  // namespace wh
 
 namespace wh {

@@ -402,6 +402,13 @@ void kmeans_accum(const float* X, int64_t n, int f, const int32_t* assign, float
 int64_t kmeans_accum_scratch(int64_t n, int k);
 // new centroids from sums [k, f + 1] (count last) and the previous C [k, f]:
 // mean (previous row if empty), L2-normalised; *nempty += empty clusters
+// sparse rows (CSR, int32 columns < F) against Ct [F, Kp] (the transposed
+// centroids, Kp = K rounded up to 4): argmax_k x . c_k in double
+void kmeans_assign_csr(const int64_t* off, const int32_t* col, const float* val, int64_t n,
+                       const float* Ct, int K, int Kp, int32_t* assign, hipStream_t s);
+// sums [K, F + 1] += the rows of each cluster (atomics), column F = counts
+void kmeans_accum_csr(const int64_t* off, const int32_t* col, const float* val, int64_t n,
+                      const int32_t* assign, int F, float* sums, hipStream_t s);
 void kmeans_update(const float* sums, const float* C, int k, int f, float* out,
                    unsigned long long* nempty, hipStream_t s);
 bool kmeans_accum_sorted(const float* X, int64_t n, int f, int k, const int32_t* assign,

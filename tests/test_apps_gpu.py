@@ -455,3 +455,37 @@ def test_gbdt_qscale_kernel_matches_torch(r32):
         if r32:
             want = torch.cat([want, torch.tensor([float(r32)])])
         assert torch.equal(got, want), (mg, mh, n, got, want)
+
+
+def test_kmeans_csr_gpu_matches_cpu():
+    """Sparse k-means on the HIP kernels (k_assign_csr over the transposed
+    centroids, k_accum_csr) vs the host path: same assignments, centroids."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_bsp_apps import _sparse_rows
+    from wormhole_amd.models.kmeans import KMeansCSR
+    from wormhole_amd.parallel.bsp import BSP
+    cols, off, val = _sparse_rows(5000, 3000, 300, 9, 4)  # K = 300: 2 float4 groups per lane
+    kc = KMeansCSR(BSP(torch.device("cpu")), cols, off, val, 3000, 300, "cpu")
+    kg = KMeansCSR(BSP(torch.device("cuda", 0)), cols, off, val, 3000, 300, torch.device("cuda", 0))
+    kc.init_centroids(5)
+    kg.init_centroids(5)
+    for _ in range(3):
+        a, b = kc.step(), kg.step()
+        assert (a != b.cpu()).sum() <= 2  # (double sums in another order: near-ties only)
+        kg.C = kc.C.to(kg.C.device)  # continue from the same centroids
+    assert abs(kc.objective() - kg.objective()) < 1e-4
+
+
+def test_kmeans_csr_app_gpu_matches_cpu(work, monkeypatch):
+    from wormhole_amd.apps.kmeans_app import main
+    monkeypatch.setenv("WH_KMEANS_INPUT", "sparse")
+    monkeypatch.setenv("WH_DEVICE", "auto")
+    assert main([TRAIN, "6", "5", "g.txt"]) == 0
+    monkeypatch.setenv("WH_DEVICE", "cpu")
+    assert main([TRAIN, "6", "5", "c.txt"]) == 0
+    g = [list(map(float, l.split())) for l in open("g.txt")]
+    c = [list(map(float, l.split())) for l in open("c.txt")]
+    assert len(g) == len(c) == 6
+    for a, b in zip(g, c):
+        assert max(abs(x - y) for x, y in zip(a, b)) < 1e-4

@@ -140,3 +140,56 @@ def test_kmeans_converges_on_separated_clusters():
     for _ in range(3):
         km.step()
     assert km.objective() > 0.99
+
+
+def _sparse_rows(n, F, k, nnz, seed):
+    g = torch.Generator().manual_seed(seed)
+    lab = torch.randint(0, k, (n, 1), generator=g)
+    pick = torch.rand(n, 40, generator=g).argsort(1)[:, :nnz]  # distinct columns per row
+    cols = (lab * (F // k) + pick) % F
+    cols = torch.sort(cols, 1).values.reshape(-1)
+    off = torch.arange(0, n * nnz + 1, nnz, dtype=torch.int64)
+    val = torch.rand(n * nnz, generator=g) + 0.5
+    return cols, off, val
+
+
+def test_kmeans_csr_matches_dense_path():
+    """Sparse rows (KMeansCSR: never densified) follow the dense path's
+    iterations exactly on the CPU: same assignments, same centroids."""
+    from wormhole_amd.models.kmeans import KMeans, KMeansCSR, densify
+    from wormhole_amd.parallel.bsp import BSP
+    bsp = BSP(torch.device("cpu"))
+    cols, off, val = _sparse_rows(600, 500, 6, 7, 1)
+    kd = KMeans(bsp, densify(cols, off, val, 600, 500, "cpu"), 6)
+    ks = KMeansCSR(bsp, cols, off, val, 500, 6, "cpu")
+    kd.init_centroids(2)
+    ks.init_centroids(2)
+    assert torch.equal(kd.C, ks.C)
+    for _ in range(4):
+        a, b = kd.step(), ks.step()
+        assert torch.equal(a, b)
+        assert torch.allclose(kd.C, ks.C, atol=1e-6)
+    assert abs(kd.objective() - ks.objective()) < 1e-6
+
+
+def test_kmeans_input_form_choice(monkeypatch):
+    from wormhole_amd.models.kmeans import use_sparse
+    assert not use_sparse(6513, 126, 6513 * 22)          # agaricus: dense
+    assert use_sparse(1_000_000, 1_000_000, 32_000_000)  # wide and sparse
+    assert use_sparse(10_000_000, 1000, 10_000_000_000 // 2)  # dense split > 4 GiB
+    monkeypatch.setenv("WH_KMEANS_INPUT", "sparse")
+    assert use_sparse(6513, 126, 6513 * 22)
+
+
+def test_kmeans_app_sparse_input_matches_dense(tmp_path):
+    """bin/kmeans.dmlc on 2 ranks with the CSR form forced gives the dense
+    form's centroids."""
+    base = [os.path.join(ROOT, "bin", "kmeans.dmlc"), TRAIN, "4", "4"]
+    r1 = run(["-n", "2"] + base + ["d.txt"], tmp_path, {"WH_KMEANS_INPUT": "dense"})
+    r2 = run(["-n", "2"] + base + ["s.txt"], tmp_path, {"WH_KMEANS_INPUT": "sparse"})
+    assert r1.returncode == 0 and r2.returncode == 0, r2.stderr[-2000:]
+    d = [list(map(float, l.split())) for l in open(tmp_path / "d.txt")]
+    s = [list(map(float, l.split())) for l in open(tmp_path / "s.txt")]
+    assert len(d) == len(s) == 4
+    for a, b in zip(d, s):
+        assert max(abs(x - y) for x, y in zip(a, b)) < 1e-5

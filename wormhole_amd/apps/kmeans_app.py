@@ -9,7 +9,7 @@ from .ps_app import _device
 
 def main(argv):
     from .. import _native
-    from ..models.kmeans import KMeans, densify
+    from ..models.kmeans import KMeans, KMeansCSR, densify, use_sparse
     from ..parallel.bsp import BSP, fault_point
 
     dev = _device()
@@ -25,8 +25,14 @@ def main(argv):
         fdim = int(bsp.allreduce_scalar(fdim, "max", torch.int64))
     else:
         fdim = int(g["centroids"].shape[1])
-    X = densify(keys, off, val, off.numel() - 1, fdim, dev)
-    km = KMeans(bsp, X, k)
+    nrows = off.numel() - 1
+    # sparse or dense, decided together (every rank must run the same path)
+    sparse = bsp.allreduce_scalar(1.0 if use_sparse(nrows, fdim, keys.numel()) else 0.0,
+                                  "max") > 0
+    if sparse:
+        km = KMeansCSR(bsp, keys, off, val, fdim, k, dev)
+    else:
+        km = KMeans(bsp, densify(keys, off, val, nrows, fdim, dev), k)
     if version == 0:
         km.init_centroids(0)
     else:
