@@ -139,6 +139,10 @@ def main():
     # minibatch's localize; the learner waits on its event just before the
     # next localize begins.
     gen = torch.cuda.Stream(device) if device.type == "cuda" else None
+    if device.type == "cuda" and os.environ.get("WH_COMPUTE_PRIO", "0") != "0":
+        # (experiment) the compute stream as a high-priority HIP stream: its
+        # kernels' workgroups dispatch ahead of the localize / AUC side streams
+        torch.cuda.set_stream(torch.cuda.Stream(device, priority=-1))
     main = torch.cuda.current_stream(device) if device.type == "cuda" else None
     if gen is not None:
         from wormhole_amd.utils import streams

@@ -20,4 +20,5 @@ tail -1 $OUT/km_dense.log
 $T 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kprof -o run -- python3 benchmarks/bench_kmeans.py --sparse 1000000 --rows 1000000 --k 1000 --nnz 32 --iters 3 > $OUT/kprof.log 2>&1 || exit $?
 for i in 1 2; do $T 300 python bench.py > $OUT/bench$i.log 2>&1 || exit $?; tail -1 $OUT/bench$i.log | cut -c1-200; done
 $T 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bprof -o run -- python3 bench.py --steps 100 > $OUT/bprof.log 2>&1 || exit $?
+bash tools/gpu/env_ab.sh r4c/prio "WH_COMPUTE_PRIO=1" || exit $?
 echo all done rc=$rc rc2=$rc2
