@@ -20,12 +20,37 @@ namespace host {
 
 // CSR minibatch / parse block (reference dmlc::RowBlockContainer<uint64_t>):
 // offsets are absolute into index/value, value empty == all ones.
+// std::vector storage that resize() leaves uninitialised: a decoded block
+// (CRB sections, parsed chunks) overwrites every element anyway, and
+// value-initialising first cost a whole extra pass over ~330 MB per million
+// Criteo rows
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = DefaultInitAlloc<U>;
+  };
+  DefaultInitAlloc() = default;
+  template <class U>
+  DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+template <class T>
+using hvec = std::vector<T, DefaultInitAlloc<T>>;
+
 struct RowBlock {
-  std::vector<float> label;
-  std::vector<int64_t> offset{0};
-  std::vector<uint64_t> index;
-  std::vector<float> value;
-  std::vector<float> weight;
+  hvec<float> label;
+  hvec<int64_t> offset{0};
+  hvec<uint64_t> index;
+  hvec<float> value;
+  hvec<float> weight;
 
   size_t size() const { return offset.size() - 1; }
   size_t nnz() const { return index.size(); }

@@ -108,7 +108,11 @@ int LZ4Decompress(const char* src, char* dst, int csize, int cap) {
       } while (s == 255);
     }
     if ((size_t)(iend - ip) < lit || (size_t)(oend - op) < lit) return -1;
-    std::memcpy(op, ip, lit);
+    if (lit <= 16 && iend - ip >= 16 && oend - op >= 16) {
+      std::memcpy(op, ip, 16);  // one fixed-size copy for short literal runs
+    } else {
+      std::memcpy(op, ip, lit);
+    }
     op += lit;
     ip += lit;
     if (ip >= iend) break;  // last sequence
@@ -128,8 +132,42 @@ int LZ4Decompress(const char* src, char* dst, int csize, int cap) {
     mlen += kMinMatch;
     if ((size_t)(oend - op) < mlen) return -1;
     const char* m = op - off;
-    for (size_t i = 0; i < mlen; ++i) op[i] = m[i];  // overlap-safe
-    op += mlen;
+    char* const mend = op + mlen;
+    if (off >= 16 && oend - mend >= 16) {
+      // wild 16-byte copies (a source chunk ends at or before its
+      // destination chunk starts, so every source byte is final; the copy
+      // may run up to 15 bytes past the match, inside the output, where
+      // the next sequence overwrites them)
+      do {
+        std::memcpy(op, m, 16);
+        op += 16;
+        m += 16;
+      } while (op < mend);
+    } else if (off >= 8 && oend - mend >= 8) {
+      do {
+        std::memcpy(op, m, 8);
+        op += 8;
+        m += 8;
+      } while (op < mend);
+    } else if (oend - mend >= 8) {
+      // short offset: replicate the period byte-wise once, then copy in
+      // 8-byte steps from a source at least 8 behind
+      for (size_t i = 0; i < 8; ++i) op[i] = m[i];
+      char* q = op + 8;
+      const char* r = m + 8;
+      while (q < mend) {
+        if (q - r >= 8) {
+          std::memcpy(q, r, 8);
+          q += 8;
+          r += 8;
+        } else {
+          *q++ = *r++;
+        }
+      }
+    } else {
+      for (size_t i = 0; i < mlen; ++i) op[i] = m[i];  // overlapping (short offset)
+    }
+    op = mend;
   }
   return (int)(op - dst);
 }

@@ -38,8 +38,8 @@ py::list conf_to_py(const std::vector<ConfItem>& items) {
 
 // pinned = page-locked host memory (torch's caching host allocator), so the
 // learner's .to(device, non_blocking=True) is a real asynchronous DMA
-template <typename T>
-Tensor vec_to_tensor(const std::vector<T>& v, torch::ScalarType dt, bool pinned = false) {
+template <class T, class A>
+Tensor vec_to_tensor(const std::vector<T, A>& v, torch::ScalarType dt, bool pinned = false) {
   auto t = torch::empty({(int64_t)v.size()}, torch::TensorOptions().dtype(dt).pinned_memory(pinned));
   if (!v.empty()) std::memcpy(t.data_ptr(), v.data(), v.size() * sizeof(T));
   return t;
