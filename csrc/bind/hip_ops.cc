@@ -8,6 +8,8 @@
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/distributed/c10d/Work.hpp>
 
 #include <algorithm>
 #include <array>
@@ -16,8 +18,11 @@
 #include <cstring>
 #include <chrono>
 #include <cmath>
+#include <functional>
 #include <map>
 #include <memory>
+#include <numeric>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -185,6 +190,12 @@ int64_t& loc_retries() {
   return n;
 }
 
+// The count exchange of a localize job issued from C++ (kv/psx.py's C0,
+// ported by PsxStep): returns (payload [owner_cnt (nshard+1) | stride values
+// per peer | extra], the stream the payload is ready on, stride, world).
+using NativeExchange =
+    std::function<std::tuple<Tensor, hipStream_t, int64_t, int64_t>(const Tensor&)>;
+
 class LocalizeJob {
  public:
   // defer_exchange: enqueue the localize kernels now, but call the count
@@ -196,6 +207,19 @@ class LocalizeJob {
               int64_t nshard, int64_t hint, py::object exchange, bool defer_exchange = false)
       : keys_(keys), offset_(offset), nshard_(nshard), exchange_(exchange),
         defer_(defer_exchange) {
+    init(val, hint);
+  }
+  LocalizeJob(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+              int64_t nshard, int64_t hint, NativeExchange nex, bool defer_exchange)
+      : keys_(keys), offset_(offset), nshard_(nshard), exchange_(py::none()), nex_(std::move(nex)),
+        defer_(defer_exchange) {
+    init(val, hint);
+  }
+
+  void init(const c10::optional<Tensor>& val, int64_t hint) {
+    const Tensor& keys = keys_;
+    const Tensor& offset = offset_;
+    const int64_t nshard = nshard_;
     CHECK_IN(keys, torch::kInt64);
     CHECK_IN(offset, torch::kInt64);
     TORCH_CHECK(nshard >= 1 && nshard <= 1024, "nshard out of range");
@@ -486,7 +510,17 @@ class LocalizeJob {
     Tensor both = owner_cnt;
     nrecv_ = 0;
     hipStream_t cs = s;  // stream of the count read
-    if (!exchange_.is_none()) {
+    if (nex_) {
+      auto r = nex_(owner_cnt);
+      both = std::get<0>(r);
+      cs = std::get<1>(r);
+      stride_ = std::get<2>(r);
+      const int64_t world = std::get<3>(r);
+      TORCH_CHECK(both.scalar_type() == torch::kInt64 && stride_ >= 2 &&
+                      both.numel() >= nshard_ + 1 + stride_ * world,
+                  "localize: bad native exchange payload");
+      nrecv_ = stride_ * world;
+    } else if (!exchange_.is_none()) {
       py::object r = exchange_(owner_cnt);
       if (py::isinstance<py::tuple>(r)) {
         // extended protocol (kv/psx.py): (payload, stream handle, stride,
@@ -528,6 +562,7 @@ class LocalizeJob {
   Tensor keys_, offset_, val_;
   int64_t nshard_, nnz_ = 0, safe_ = 0, tsize_ = 0, nrecv_ = 0, stride_ = 2;
   py::object exchange_;
+  NativeExchange nex_;
   bool defer_ = false, exchanged_ = false;
   Tensor owner_cnt_;
   int tab_ = -1;
@@ -3038,6 +3073,8 @@ class LinearStep {
   int64_t hint_ = 0, grows_ = 0, pushes_ = 0;
 };
 
+#include "psx_native.inl"
+
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "wormhole_amd gfx950 HIP kernels";
   m.def("scan_excl", &scan_excl);
@@ -3066,6 +3103,31 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("grows", &LinearStep::grows)
       .def_property_readonly("direct", [](const LinearStep& l) { return l.direct(); })
       .def_property("pushes", &LinearStep::pushes, &LinearStep::set_pushes);
+  py::class_<PsxStep>(m, "PsxStep")
+      .def(py::init<KVStore*, int64_t, int64_t, int64_t, py::object, bool, std::vector<double>,
+                    std::vector<double>, int64_t, bool, int64_t, int64_t, Tensor, Tensor, int64_t,
+                    double, int64_t>(),
+           py::arg("store"), py::arg("P"), py::arg("S"), py::arg("rank"), py::arg("pg"),
+           py::arg("linear"), py::arg("lin_hp"), py::arg("hp"), py::arg("threshold"),
+           py::arg("l1_shrk"), py::arg("seed"), py::arg("loss"), py::arg("met"),
+           py::arg("auc_sum"), py::arg("tau"), py::arg("max_load"), py::arg("cu_reserve"),
+           py::keep_alive<1, 2>())
+      .def("train", &PsxStep::train, py::arg("keys"), py::arg("offset"), py::arg("val"),
+           py::arg("label"), py::arg("data_pass"), py::arg("next_keys") = py::none(),
+           py::arg("next_offset") = py::none(), py::arg("next_val") = py::none(),
+           py::arg("ready") = 0)
+      .def("flush", &PsxStep::flush)
+      .def("drop_job", &PsxStep::drop_job)
+      .def("guard_sync", &PsxStep::guard_sync)
+      .def("wire", &PsxStep::wire)
+      .def("wire_reset", &PsxStep::wire_reset)
+      .def_property_readonly("busy", &PsxStep::busy)
+      .def_property_readonly("grows", &PsxStep::grows)
+      .def_property_readonly("vgrows", &PsxStep::vgrows)
+      .def_property("requests", &PsxStep::requests, &PsxStep::set_requests)
+      .def_property("step", &PsxStep::step, &PsxStep::set_step);
+  m.def("c10d_a2a_rows", &c10d_a2a_rows, py::arg("pg"), py::arg("x"), py::arg("send_rows"),
+        py::arg("recv_rows"));
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),
         py::arg("nshard") = 1, py::arg("hint") = 0, py::arg("exchange") = py::none());
   m.def("fm_forward", &fm_forward);

@@ -1,0 +1,670 @@
+// Native driver of the pipelined multi-shard parameter-server step
+// (included by hip_ops.cc after LinearStep; the Python twin and the
+// reference of every phase is wormhole_amd/kv/psx.py Psx.train).
+//
+// Reference per-minibatch flow: learn/difacto/async_sgd.h:372-424 (push the
+// feature counts -> ZVPull(w, V) -> compute -> ZVPush(gw, gV)) and
+// learn/linear/async_sgd.h:240-301 (ZPull w -> gradient -> ZPush), with
+// max_concurrency minibatches in flight. A call of PsxStep::train enqueues
+// exactly what Psx.train does -- the same four collectives C0..C3, the same
+// streams (compute S, localize ls, count side cs, exchange xs), the same
+// event edges -- but from C++: the Python step spent ~300 us of host time
+// per call at the reference's minibatch of 10000 rows (~40 Python-level
+// operations and stream switches), more than the GPU work it launched.
+//
+// Transport: the process group's all-to-all through c10d (RCCL over xGMI;
+// c10d::ProcessGroup::alltoall_base, its work's wait() orders the CURRENT
+// stream after the transfer, no host wait), a 1-rank RCCL group for the
+// loopback-rccl rehearsal, or the identity (P virtual shards in one
+// process, the --loopback bench).
+
+namespace {
+
+struct PsxWork {  // an issued collective and the tensors it reads
+  c10::intrusive_ptr<c10d::Work> w;
+  Tensor keep;
+  void wait() {
+    if (w) w->wait();  // the current stream waits for the transfer
+    w.reset();
+    keep = Tensor();
+  }
+};
+
+struct PsxSt {  // one minibatch in flight (kv/psx.py _Step)
+  bool train = false, use_cnt = false, have_v = false;
+  int64_t U = 0, seed_step = 0;
+  std::vector<int64_t> send, recv, Hw, Ho, vown, vrecv;
+  Tensor label, uniq, ucnt, lid, offset, val, csc_off, csc_row, csc_val;
+  Tensor tabs, segS_w, segHS_w, segS_o, segHS_o, vrecv_d;
+  Tensor keys_o, slot, vpos, chain, head, rbuf, vcnt;
+  Tensor rrecv, hdr, py, dual, xv, gpush, gvc;
+  hipEvent_t ev_open = nullptr, ev_grad = nullptr;
+  PsxWork w_c1, w_c2, w_c3;
+};
+using PsxStP = std::shared_ptr<PsxSt>;
+
+int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
+int64_t vsum(const std::vector<int64_t>& v) { return std::accumulate(v.begin(), v.end(), (int64_t)0); }
+
+}  // namespace
+
+class PsxStep {
+ public:
+  // pg: the process group (None: loopback identity over P virtual shards);
+  // lin_hp: (algo, alpha, beta, l1, l2) of the linear wire format's owner
+  // push; hp / threshold / l1_shrk / seed: DiFacto's (kv/psx.py reads the
+  // same from the learner); met / auc_sum: the learner's device progress
+  // accumulators.
+  PsxStep(KVStore* store, int64_t P, int64_t S, int64_t rank, py::object pg, bool linear,
+          std::vector<double> lin_hp, std::vector<double> hp, int64_t threshold, bool l1_shrk,
+          int64_t seed, int64_t loss, Tensor met, Tensor auc_sum, int64_t tau, double max_load,
+          int64_t cu_reserve)
+      : store_(store), P_(P), S_(S), rank_(rank), linear_(linear), lin_hp_(std::move(lin_hp)),
+        hp_(std::move(hp)), threshold_(threshold), l1_shrk_(l1_shrk), seed_(seed), loss_(loss),
+        met_(std::move(met)), auc_sum_(std::move(auc_sum)), tau_(tau), max_load_(max_load) {
+    TORCH_CHECK(P >= 2 && S >= 1 && S <= P && rank >= 0 && rank < P, "PsxStep: bad P / S / rank");
+    TORCH_CHECK(lin_hp_.size() == 5 && hp_.size() == 8, "PsxStep: hyper-parameter sizes");
+    vs_ = store->vstride();
+    TORCH_CHECK(linear_ == (vs_ == 0), "PsxStep: the linear wire format is the vstride-0 store");
+    if (!pg.is_none()) pg_ = pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
+    TORCH_CHECK(!pg_ || pg_->getSize() == P || pg_->getSize() == 1,
+                "PsxStep: the process group must have P ranks (or 1: loopback-rccl)");
+    dev_ = store->slots_.device().index();
+    c10::DeviceGuard g(store->slots_.device());
+    ls_ = c10::hip::getStreamFromPool(false, dev_);
+    cs_ = c10::hip::getStreamFromPool(false, dev_);
+    xs_ = c10::hip::getStreamFromPool(false, dev_);
+    for (auto& e : ring_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : gev_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (pg_) wh::fm_set_cu_reserve((int)cu_reserve);
+    const int64_t dflt = std::max<int64_t>(4 * (P + 1) + P, 64);
+    for (int i = 0; i < kPins; ++i) {
+      pins_[i] = torch::empty({dflt}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
+      WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&pin_ev_[i], hipEventDisableTiming));
+    }
+  }
+
+  ~PsxStep() {
+    job_.reset();
+    (void)hipDeviceSynchronize();
+    for (auto& e : ring_) (void)hipEventDestroy(e);
+    for (auto& e : gev_) (void)hipEventDestroy(e);
+    for (auto& e : pin_ev_) (void)hipEventDestroy(e);
+  }
+
+  // One training minibatch (Psx.train). Returns (has_data, minibatches
+  // forwarded, unique keys, embedding rows) of the step whose forward ran.
+  py::tuple train(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+                  const Tensor& label, int64_t data_pass, const c10::optional<Tensor>& nkeys,
+                  const c10::optional<Tensor>& noffset, const c10::optional<Tensor>& nval,
+                  int64_t ready) {
+    c10::DeviceGuard g(keys.device());
+    S_stream_ = c10::hip::getCurrentHIPStream(dev_);
+    fwd_mb_ = 0;
+    ensure_job(keys, offset, val);
+    std::vector<int64_t> send, recv;
+    const bool empty = counts(send, recv);
+    if (empty) {
+      finish_job();
+      return py::make_tuple(false, 0, 0, 0);
+    }
+    PsxStP prev = pull_;
+    if (prev && !prev->have_v) vcount_exchange(*prev);
+    PsxStP st = new_step(send, recv, label, true, data_pass, prev.get());
+    if (prev) c2(*prev);
+    if (push_ && push_->gvc.defined()) c3(*push_);
+    set_loc(*st, finish_job(), offset, val);
+    const bool early = nkeys.has_value() && nkeys->defined();
+    if (early) begin(*nkeys, *noffset, nval, st, ready, true);
+    c1(*st);
+    if (prev) {
+      reply(*prev);
+      if (tau_ == 0 && prev->train) {
+        grad(*prev, true);
+        owner_push(*prev);
+      }
+    }
+    if (push_) {
+      owner_push(*push_);
+      push_.reset();
+    }
+    open(*st, true);
+    pull_ = st;
+    if (early) exchange_deferred();
+    if (tau_ == 1 && prev && prev->train) {
+      grad(*prev, false);  // C3 goes out behind the next call's C2
+      push_ = prev;
+    }
+    ++step_;
+    return py::make_tuple(true, fwd_mb_, last_u_, last_v_);
+  }
+
+  // Complete every minibatch in flight (Psx.flush). Returns the minibatches
+  // forwarded here.
+  int64_t flush() {
+    c10::DeviceGuard g(store_->slots_.device());
+    S_stream_ = c10::hip::getCurrentHIPStream(dev_);
+    fwd_mb_ = 0;
+    if (push_ && push_->gvc.defined()) c3(*push_);
+    if (job_ && job_carried_) {  // the begun job carries the last pull's V counts
+      std::vector<int64_t> a, b;
+      counts(a, b);
+    }
+    PsxStP st = pull_;
+    if (st) {
+      if (!st->have_v) vcount_exchange(*st);
+      upload_vrecv(*st);
+      c2(*st);
+      reply(*st);
+      if (st->train) grad(*st, true);
+    }
+    if (push_) {
+      owner_push(*push_);
+      push_.reset();
+    }
+    if (st && st->train) owner_push(*st);
+    pull_.reset();
+    return fwd_mb_;
+  }
+
+  // drop a begun localize (before the Python step runs an evaluation /
+  // read-only pull of its own: every rank does it at the same point)
+  void drop_job() {
+    if (job_) {
+      if (job_deferred_) {
+        c10::hip::HIPStreamGuard sg(ls_);
+        job_->exchange();
+      }
+      std::vector<int64_t> a, b;
+      counts(a, b);
+      finish_job();
+    }
+  }
+
+  bool busy() const { return (bool)pull_ || (bool)push_ || (bool)job_; }
+  std::vector<int64_t> wire() const { return {wire_[0], wire_[1], wire_[2], wire_[3]}; }
+  void wire_reset() { wire_[0] = wire_[1] = wire_[2] = wire_[3] = 0; }
+  int64_t grows() const { return grows_; }
+  int64_t vgrows() const { return vgrows_; }
+  int64_t requests() const { return requests_; }
+  void set_requests(int64_t r) { requests_ = r; }
+  int64_t step() const { return step_; }
+  void set_step(int64_t s) { step_ = s; }
+  // the guard's last summary {keys, failed inserts, V overflows, V rows}
+  std::vector<int64_t> guard_sync() {
+    guard_after(true);
+    guard_read();
+    return {gkeys_, 0, 0, gvused_};
+  }
+
+ private:
+  // ------------------------------------------------------------ transport
+  Tensor a2a(int c, const Tensor& x, const std::vector<int64_t>& send_rows,
+             const std::vector<int64_t>& recv_rows, hipEvent_t ready, PsxWork* work) {
+    int64_t row = x.element_size();
+    for (int64_t d = 1; d < x.dim(); ++d) row *= x.size(d);
+    wire_[c] += row * (vsum(send_rows) - send_rows[rank_]);
+    work->w.reset();
+    if (!pg_) return x;  // loopback identity
+    Tensor xc = x.contiguous();
+    int64_t width = 1;
+    for (int64_t d = 1; d < xc.dim(); ++d) width *= xc.size(d);
+    std::vector<int64_t> shape(xc.sizes().begin(), xc.sizes().end());
+    shape[0] = vsum(recv_rows);
+    c10::hip::HIPStream xs = ready ? xs_ : S_stream_;
+    if (ready) {
+      WH_HIP_CHECK_HOST(hipStreamWaitEvent(xs_.stream(), ready, 0));
+      c10::hip::HIPCachingAllocator::recordStream(xc.storage().data_ptr(), xs_);
+    }
+    c10::hip::HIPStreamGuard sg(xs);
+    Tensor out = torch::empty(shape, xc.options());
+    if (ready)  // allocated on xs, read on S
+      c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), S_stream_);
+    Tensor of = out.view({-1}), xf = xc.view({-1});
+    std::vector<int64_t> rs, ss;
+    if (pg_->getSize() > 1) {
+      for (int64_t r : recv_rows) rs.push_back(r * width);
+      for (int64_t r : send_rows) ss.push_back(r * width);
+    } else if (xc.numel() == 0) {  // (1-rank loopback-rccl: nothing to copy)
+      return out;
+    }
+    work->w = pg_->alltoall_base(of, xf, rs, ss);
+    work->keep = xc;
+    return out;
+  }
+
+  // int64 [4P] per peer -> the peers' [4P], on the current stream
+  Tensor exchange_counts(const Tensor& send) {
+    if (!pg_) return send.clone();
+    Tensor r = torch::empty_like(send);
+    std::vector<int64_t> none;
+    Tensor s = send.contiguous();
+    auto w = pg_->alltoall_base(r, s, none, none);
+    w->wait();
+    return r;
+  }
+
+  hipEvent_t record(const c10::hip::HIPStream& s) {
+    hipEvent_t e = ring_[ring_i_];
+    ring_i_ = (ring_i_ + 1) % kRing;
+    WH_HIP_CHECK_HOST(hipEventRecord(e, s.stream()));
+    return e;
+  }
+  void wait_on(const c10::hip::HIPStream& waiter, const c10::hip::HIPStream& producer) {
+    WH_HIP_CHECK_HOST(hipStreamWaitEvent(waiter.stream(), record(producer), 0));
+  }
+
+  // small int64 tables host -> device through a ring of pinned buffers
+  Tensor put(const std::vector<int64_t>& a) {
+    const int k = pin_i_;
+    pin_i_ = (pin_i_ + 1) % kPins;
+    if (pin_used_[k]) WH_HIP_CHECK_HOST(hipEventSynchronize(pin_ev_[k]));
+    if ((int64_t)a.size() > pins_[k].numel())
+      pins_[k] = torch::empty({2 * (int64_t)a.size()},
+                              torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
+    std::memcpy(pins_[k].data_ptr(), a.data(), a.size() * sizeof(int64_t));
+    Tensor d = torch::empty({(int64_t)a.size()},
+                            torch::TensorOptions().dtype(torch::kInt64).device(torch::kCUDA, dev_));
+    if (!a.empty())
+      WH_HIP_CHECK_HOST(hipMemcpyAsync(d.data_ptr(), pins_[k].data_ptr(), a.size() * 8,
+                                       hipMemcpyHostToDevice, S_stream_.stream()));
+    WH_HIP_CHECK_HOST(hipEventRecord(pin_ev_[k], S_stream_.stream()));
+    pin_used_[k] = true;
+    return d;
+  }
+
+  // ------------------------------------------------------------ localize
+  NativeExchange exchange_fn(PsxStP carried, int64_t flag) {
+    return [this, carried, flag](const Tensor& owner_cnt) {
+      Tensor vc = carried ? carried->vcnt : Tensor();
+      const auto cur = c10::hip::getCurrentHIPStream(dev_);
+      wait_on(cs_, S_stream_);
+      if (cur.stream() != S_stream_.stream()) wait_on(cs_, cur);  // (called on ls)
+      c10::hip::HIPCachingAllocator::recordStream(owner_cnt.storage().data_ptr(), cs_);
+      if (vc.defined()) c10::hip::HIPCachingAllocator::recordStream(vc.storage().data_ptr(), cs_);
+      c10::hip::HIPStreamGuard sg(cs_);
+      auto c0 = ps_c0(owner_cnt, vc.defined() ? c10::optional<Tensor>(vc) : c10::nullopt, P_, flag);
+      Tensor recv = exchange_counts(c0[0]);
+      c0[1].narrow(0, S_ + 1, 4 * P_).copy_(recv);
+      return std::make_tuple(c0[1], cs_.stream(), (int64_t)4, P_);
+    };
+  }
+
+  void begin(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
+             PsxStP carried, int64_t ready, bool defer) {
+    const int64_t flag = offset.numel() > 1 ? 1 : 0;
+    wait_on(ls_, S_stream_);
+    if (ready) WH_HIP_CHECK_HOST(hipStreamWaitEvent(ls_.stream(), reinterpret_cast<hipEvent_t>(ready), 0));
+    for (const Tensor* t : {&keys, &offset}) {
+      c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), ls_);
+      c10::hip::HIPCachingAllocator::recordStream(t->storage().data_ptr(), S_stream_);
+    }
+    c10::optional<Tensor> v;
+    if (val.has_value() && val->defined() && val->numel()) {
+      v = *val;
+      c10::hip::HIPCachingAllocator::recordStream(val->storage().data_ptr(), ls_);
+      c10::hip::HIPCachingAllocator::recordStream(val->storage().data_ptr(), S_stream_);
+    }
+    c10::hip::HIPStreamGuard sg(ls_);
+    job_ = std::make_unique<LocalizeJob>(keys, offset, v, S_, uhint_, exchange_fn(carried, flag),
+                                         defer);
+    job_keys_ = keys;
+    job_carried_ = carried;
+    job_deferred_ = defer;
+  }
+
+  void exchange_deferred() {
+    if (job_ && job_deferred_) {
+      c10::hip::HIPStreamGuard sg(ls_);
+      job_->exchange();
+      job_deferred_ = false;
+    }
+  }
+
+  void ensure_job(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val) {
+    if (job_ && job_keys_.is_same(keys)) return;
+    if (job_) {  // a stale job (never expected): finish it in order
+      std::vector<int64_t> a, b;
+      counts(a, b);
+      finish_job();
+    }
+    begin(keys, offset, val, (pull_ && !pull_->have_v) ? pull_ : PsxStP(), 0, false);
+  }
+
+  // the one host read of the step (count exchange C0 of the begun job):
+  // send / recv per peer; fills the carried step's V counts; true when no
+  // rank has data
+  bool counts(std::vector<int64_t>& send, std::vector<int64_t>& recv) {
+    exchange_deferred();
+    auto c = job_->counts();
+    const int64_t* oc = c[0].data_ptr<int64_t>();
+    const Tensor& tail = c[1];
+    const int64_t* t = tail.data_ptr<int64_t>();
+    TORCH_CHECK(tail.numel() >= 5 * P_, "psx: short count payload");
+    if (job_carried_ && !job_carried_->have_v) {
+      auto& ca = *job_carried_;
+      ca.vrecv.assign(P_, 0);
+      ca.vown.assign(P_, 0);
+      for (int64_t q = 0; q < P_; ++q) {
+        ca.vrecv[q] = t[2 + 4 * q];
+        ca.vown[q] = t[4 * P_ + q];
+      }
+      ca.have_v = true;
+    }
+    send.assign(P_, 0);
+    recv.assign(P_, 0);
+    bool any = false;
+    for (int64_t p = 0; p < S_; ++p) send[p] = oc[p];
+    for (int64_t q = 0; q < P_; ++q) {
+      recv[q] = t[4 * q];
+      any = any || t[3 + 4 * q] != 0;
+    }
+    return !any;
+  }
+
+  std::vector<Tensor> finish_job() {
+    std::vector<Tensor> out = job_->finish();
+    job_.reset();
+    job_keys_ = Tensor();
+    job_carried_.reset();
+    job_deferred_ = false;
+    return out;
+  }
+
+  void vcount_exchange(PsxSt& st) {
+    if (linear_) {
+      st.vrecv.assign(P_, 0);
+      st.vown.assign(P_, 0);
+      st.have_v = true;
+      return;
+    }
+    auto zero = torch::zeros({S_ + 1}, st.vcnt.options());
+    wait_on(cs_, S_stream_);
+    c10::hip::HIPStreamGuard sg(cs_);
+    auto c0 = ps_c0(zero, st.vcnt, P_, 1);
+    c0[1].narrow(0, S_ + 1, 4 * P_).copy_(exchange_counts(c0[0]));
+    Tensor v = c0[1].cpu();
+    const int64_t* h = v.data_ptr<int64_t>();
+    st.vrecv.assign(P_, 0);
+    st.vown.assign(P_, 0);
+    for (int64_t q = 0; q < P_; ++q) {
+      st.vrecv[q] = h[S_ + 3 + 4 * q];
+      st.vown[q] = h[S_ + 1 + 4 * P_ + q];
+    }
+    st.have_v = true;
+  }
+
+  // ------------------------------------------------------------ tables
+  PsxStP new_step(const std::vector<int64_t>& send, const std::vector<int64_t>& recv,
+                  const Tensor& label, bool train, int64_t data_pass, PsxSt* prev) {
+    auto st = std::make_shared<PsxSt>();
+    st->send = send;
+    st->recv = recv;
+    st->label = label;
+    st->train = train;
+    st->use_cnt = train && data_pass == 0 && !linear_;
+    st->seed_step = step_;
+    const int64_t vs = std::max<int64_t>(vs_, 1);
+    st->Hw.assign(P_, 0);
+    st->Ho.assign(P_, 0);
+    if (!linear_)
+      for (int64_t p = 0; p < P_; ++p) {
+        st->Hw[p] = cdiv64(2 * send[p], vs);
+        st->Ho[p] = cdiv64(2 * recv[p], vs);
+      }
+    std::vector<int64_t> a(4 * (P_ + 1) + P_, 0);
+    for (int64_t p = 0; p < P_; ++p) {
+      a[p + 1] = a[p] + send[p];
+      a[P_ + 2 + p] = a[P_ + 1 + p] + st->Hw[p];
+      a[2 * P_ + 3 + p] = a[2 * P_ + 2 + p] + recv[p];
+      a[3 * P_ + 4 + p] = a[3 * P_ + 3 + p] + st->Ho[p];
+    }
+    if (prev)
+      for (int64_t q = 0; q < P_; ++q) a[4 * P_ + 4 + q] = prev->vrecv[q];
+    Tensor t = put(a);
+    st->tabs = t;
+    st->segS_w = t.narrow(0, 0, P_ + 1);
+    st->segHS_w = t.narrow(0, P_ + 1, P_ + 1);
+    st->segS_o = t.narrow(0, 2 * P_ + 2, P_ + 1);
+    st->segHS_o = t.narrow(0, 3 * P_ + 3, P_ + 1);
+    if (prev) prev->vrecv_d = t.narrow(0, 4 * P_ + 4, P_);
+    return st;
+  }
+
+  void upload_vrecv(PsxSt& st) { st.vrecv_d = put(st.vrecv); }
+
+  void set_loc(PsxSt& st, const std::vector<Tensor>& loc, const Tensor& offset,
+               const c10::optional<Tensor>& val) {
+    st.uniq = loc[0];
+    st.ucnt = loc[1];
+    st.lid = loc[3];
+    st.csc_off = loc[4];
+    st.csc_row = loc[5];
+    st.csc_val = loc[6];
+    st.U = st.uniq.numel();
+    st.offset = offset;
+    if (val.has_value() && val->defined() && val->numel()) st.val = *val;
+    uhint_ = st.U;
+    // the job's outputs (allocated on ls) are read on S from here on
+    for (const Tensor* x : {&st.uniq, &st.ucnt, &st.lid, &st.csc_off, &st.csc_row, &st.csc_val})
+      if (x->defined() && x->numel())
+        c10::hip::HIPCachingAllocator::recordStream(x->storage().data_ptr(), S_stream_);
+  }
+
+  // ------------------------------------------------------------ phases
+  void c1(PsxSt& st) {
+    Tensor rec = linear_ ? st.uniq
+                         : ps_records(st.uniq, st.use_cnt ? c10::optional<Tensor>(st.ucnt)
+                                                          : c10::nullopt);
+    st.keys_o = a2a(1, rec, st.send, st.recv, nullptr, &st.w_c1);
+  }
+
+  void open(PsxSt& st, bool insert) {
+    st.w_c1.wait();
+    const int64_t n = vsum(st.recv);
+    if (insert) guard_before(n);
+    const int64_t rows = linear_ ? 0 : vsum(st.Ho) + n;
+    auto o = store_->ps_open(st.keys_o, st.use_cnt, st.segS_o, st.segHS_o, rows, insert, st.train,
+                             hp_, threshold_, l1_shrk_, seed_);
+    st.slot = o[0];
+    st.vpos = o[1];
+    st.chain = o[2];
+    st.head = o[3];
+    st.rbuf = o[4];
+    st.vcnt = o[5];
+    st.keys_o = Tensor();
+    st.ev_open = record(S_stream_);
+    if (insert) guard_after(false);
+  }
+
+  void c2(PsxSt& st) {
+    std::vector<int64_t> send_rows(P_), recv_rows(P_);
+    for (int64_t p = 0; p < P_; ++p) {
+      send_rows[p] = linear_ ? st.recv[p] : st.Ho[p] + st.vown[p];
+      recv_rows[p] = linear_ ? st.send[p] : st.Hw[p] + st.vrecv[p];
+    }
+    Tensor x = st.rbuf.narrow(0, 0, vsum(send_rows));
+    st.rrecv = a2a(2, x, send_rows, recv_rows, st.ev_open, &st.w_c2);
+    st.ev_open = nullptr;
+    st.rbuf = Tensor();
+  }
+
+  void reply(PsxSt& st) {
+    st.w_c2.wait();
+    const c10::optional<Tensor> val =
+        st.val.defined() ? c10::optional<Tensor>(st.val) : c10::nullopt;
+    std::vector<Tensor> fw;
+    if (linear_) {
+      st.hdr = st.rrecv;
+      fw = fm_forward(st.offset, st.lid, val, st.rrecv, c10::nullopt, 0, st.label, loss_, met_);
+    } else {
+      auto u = ps_unpack(st.rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d);
+      st.hdr = u[0];
+      fw = fm_forward(st.offset, st.lid, val, st.hdr, st.rrecv, vs_, st.label, loss_, met_);
+    }
+    st.py = fw[0];
+    st.dual = fw[1];
+    st.xv = fw[2];
+    if (!st.train) auc_acc_side(st.py, st.label, auc_sum_);
+    if (st.label.numel()) ++fwd_mb_;
+    last_u_ = st.U;
+    last_v_ = vsum(st.vrecv);
+  }
+
+  void grad(PsxSt& st, bool issue) {
+    const c10::optional<Tensor> cv =
+        st.csc_val.defined() && st.csc_val.numel() ? c10::optional<Tensor>(st.csc_val)
+                                                   : c10::nullopt;
+    if (linear_) {
+      auto b = fm_backward(st.csc_off, st.csc_row, cv, st.dual, c10::nullopt, st.hdr,
+                           c10::nullopt, 0);
+      st.gvc = b[0].reshape({-1});
+    } else {
+      auto b = fm_backward(st.csc_off, st.csc_row, cv, st.dual, st.xv, st.hdr, st.rrecv, vs_);
+      ps_pack_gw(b[0], b[1], st.segS_w, st.segHS_w, st.vrecv_d);
+      st.gvc = b[1];
+    }
+    st.ev_grad = record(S_stream_);
+    if (issue) c3(st);
+    auc_acc_side(st.py, st.label, auc_sum_);
+    st.rrecv = st.hdr = st.dual = st.xv = st.lid = Tensor();
+    st.csc_off = st.csc_row = st.csc_val = Tensor();
+  }
+
+  void c3(PsxSt& st) {
+    std::vector<int64_t> send_rows(P_), recv_rows(P_);
+    for (int64_t p = 0; p < P_; ++p) {
+      send_rows[p] = linear_ ? st.send[p] : st.Hw[p] + st.vrecv[p];
+      recv_rows[p] = linear_ ? st.recv[p] : st.Ho[p] + st.vown[p];
+    }
+    st.gpush = a2a(3, st.gvc, send_rows, recv_rows, st.ev_grad, &st.w_c3);
+    st.ev_grad = nullptr;
+    st.gvc = Tensor();
+  }
+
+  void owner_push(PsxSt& st) {
+    st.w_c3.wait();
+    if (linear_) {
+      store_->ps_push_linear(st.slot, st.chain, st.head, st.segS_o, st.gpush, (int64_t)lin_hp_[0],
+                             lin_hp_[1], lin_hp_[2], lin_hp_[3], lin_hp_[4], (double)requests_);
+      requests_ += P_;  // one request per worker (ps-lite SGD's t)
+    } else {
+      store_->ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o, st.gpush, hp_,
+                      threshold_, l1_shrk_, seed_);
+    }
+    st.gpush = st.slot = st.vpos = st.chain = st.head = Tensor();
+  }
+
+  // ------------------------------------------------------------ store guard
+  // kv/__init__.py StoreGuard: before an open, the previous summary (one
+  // open behind: long complete) is checked -- a lost key or row raises --
+  // and the table / V slab grow so the coming open cannot overflow them;
+  // after it a summary is enqueued on a side stream.
+  // (summary slots 2 / 3 of the store: 0 / 1 belong to the Python guard)
+  void guard_read() {
+    if (!gpend_) return;
+    WH_HIP_CHECK_HOST(hipEventSynchronize(gev_[gk_]));
+    gpend_ = false;
+    auto h = store_->summary_read(2 + gk_);
+    gkeys_ = h[0];
+    gvused_ = h[3];
+    TORCH_CHECK(h[1] == 0 && h[2] == 0, "parameter store shard lost data: ", h[1],
+                " failed inserts, ", h[2], " embedding rows dropped (table ", h[0], "/",
+                store_->cap(), " keys, V slab ", h[3], "/", store_->vcap(), " rows)");
+  }
+  void guard_before(int64_t n) {
+    guard_read();
+    const int64_t need = gkeys_ + gsince_ + n;
+    if ((double)need > max_load_ * (double)store_->cap()) {
+      int64_t cap = store_->cap();
+      while ((double)need > 0.5 * (double)cap) cap *= 2;
+      Tensor remap = store_->grow(cap);
+      ++grows_;
+      for (PsxSt* st : {pull_.get(), push_.get()})
+        if (st && st->slot.defined() && st->slot.numel()) {
+          auto s64 = st->slot.to(torch::kInt64);
+          st->slot = torch::where(s64 >= 0, remap.index_select(0, s64.clamp_min(0)), st->slot);
+        }
+    }
+    if (vs_ > 0) {
+      const int64_t vneed = gvused_ + gsince_ + n + grecent_[0] + grecent_[1];
+      if (vneed > store_->vcap()) {
+        int64_t vcap = std::max<int64_t>(store_->vcap(), 1);
+        while (vneed > vcap) vcap *= 2;
+        store_->grow_v(vcap);
+        ++vgrows_;
+      }
+    }
+    gsince_ += n;
+    grecent_[0] = grecent_[1];
+    grecent_[1] = n;
+  }
+  void guard_after(bool sync) {
+    gk_ ^= 1;
+    wait_on(cs_, S_stream_);
+    {
+      c10::hip::HIPStreamGuard sg(cs_);
+      store_->summary_async(2 + gk_);
+      WH_HIP_CHECK_HOST(hipEventRecord(gev_[gk_], cs_.stream()));
+    }
+    gpend_ = true;
+    gsince_ = 0;
+    if (sync) guard_read();
+  }
+
+  static constexpr int kRing = 32, kPins = 8;
+  KVStore* store_;
+  int64_t P_, S_, rank_;
+  bool linear_;
+  std::vector<double> lin_hp_, hp_;
+  int64_t threshold_;
+  bool l1_shrk_;
+  int64_t seed_, loss_;
+  Tensor met_, auc_sum_;
+  int64_t tau_;
+  double max_load_;
+  int vs_ = 0;
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  c10::DeviceIndex dev_ = 0;
+  c10::hip::HIPStream S_stream_ = c10::hip::getDefaultHIPStream();
+  c10::hip::HIPStream ls_ = c10::hip::getDefaultHIPStream();
+  c10::hip::HIPStream cs_ = c10::hip::getDefaultHIPStream();
+  c10::hip::HIPStream xs_ = c10::hip::getDefaultHIPStream();
+  hipEvent_t ring_[kRing] = {};
+  int ring_i_ = 0;
+  Tensor pins_[kPins];
+  hipEvent_t pin_ev_[kPins] = {};
+  bool pin_used_[kPins] = {};
+  int pin_i_ = 0;
+  std::unique_ptr<LocalizeJob> job_;
+  Tensor job_keys_;
+  PsxStP job_carried_, pull_, push_;
+  bool job_deferred_ = false;
+  int64_t uhint_ = 0, step_ = 0, requests_ = 0, fwd_mb_ = 0, last_u_ = 0, last_v_ = 0;
+  int64_t wire_[4] = {0, 0, 0, 0};
+  // guard
+  hipEvent_t gev_[2] = {};
+  int gk_ = 0;
+  bool gpend_ = false;
+  int64_t gkeys_ = 0, gvused_ = 0, gsince_ = 0, grecent_[2] = {0, 0}, grows_ = 0, vgrows_ = 0;
+};
+
+// The c10d call path PsxStep uses (py::object -> ProcessGroup, row-wise
+// alltoall_base, work wait), exposed for a multi-rank CPU test over gloo.
+Tensor c10d_a2a_rows(py::object pg, const Tensor& x, const std::vector<int64_t>& send_rows,
+                     const std::vector<int64_t>& recv_rows) {
+  auto g = pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
+  Tensor xc = x.contiguous();
+  int64_t width = 1;
+  for (int64_t d = 1; d < xc.dim(); ++d) width *= xc.size(d);
+  std::vector<int64_t> shape(xc.sizes().begin(), xc.sizes().end());
+  shape[0] = vsum(recv_rows);
+  Tensor out = torch::empty(shape, xc.options());
+  Tensor of = out.view({-1}), xf = xc.view({-1});
+  std::vector<int64_t> rs, ss;
+  for (int64_t r : recv_rows) rs.push_back(r * width);
+  for (int64_t r : send_rows) ss.push_back(r * width);
+  auto w = g->alltoall_base(of, xf, rs, ss);
+  w->wait();
+  return out;
+}

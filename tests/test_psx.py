@@ -458,3 +458,61 @@ def test_linear_loopback_gpu_matches_cpu(algo, max_conc):
     bad = sum(1 for k, w in mc.items() if abs(w - mg[k]) > 1e-4 * max(1.0, abs(w)))
     assert bad <= len(mc) // 1000, bad
     assert abs(pg[0] / pg[4] - pc[0] / pc[4]) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,max_conc", [("difacto", 2), ("difacto", 1), ("linear", 2),
+                                            ("linear", 1)])
+def test_native_step_matches_python_step(model, max_conc, monkeypatch):
+    """The C++ driver of the multi-shard step (csrc/bind/psx_native.inl
+    PsxStep) trains the same model as the Python step it ports (kv/psx.py
+    Psx.train, WH_PSX_NATIVE=0), pipelined and strict, on 4 loopback shards."""
+    from wormhole_amd.parallel.comm import LoopbackComm
+    dev = torch.device("cuda", 0)
+    runs = {}
+    for native in ("1", "0"):
+        monkeypatch.setenv("WH_PSX_NATIVE", native)
+        if model == "difacto":
+            lr, prog, b = _run(LoopbackComm(4, dev), _conf(max_conc=max_conc), dev, steps=8,
+                               rows=3000)
+            runs[native] = (_model(lr), prog, bool(lr.psx._nat))
+        else:
+            lr, prog, b = _lin_run(LoopbackComm(4, dev), dev, 3, steps=8, rows=3000,
+                                   max_conc=max_conc)
+            runs[native] = (_lin_model(lr), prog, bool(lr.psx._nat))
+    (mn, pn, isn), (mp_, pp, isp) = runs["1"], runs["0"]
+    assert isn and not isp
+    assert mn.keys() == mp_.keys() and len(mn) > 1000
+    if model == "difacto":
+        bad = sum(1 for k, (w, c, v) in mp_.items()
+                  if c != mn[k][1] or abs(w - mn[k][0]) > 1e-4 * max(1.0, abs(w)) or
+                  (v is None) != (mn[k][2] is None) or
+                  (v is not None and not torch.allclose(v, mn[k][2], atol=1e-4)))
+    else:
+        bad = sum(1 for k, w in mp_.items() if abs(w - mn[k]) > 1e-4 * max(1.0, abs(w)))
+    assert bad <= len(mp_) // 1000, bad
+    for a, c in zip(pn, pp):
+        assert abs(a - c) <= 1e-3 * max(1.0, abs(a)), (pn, pp)
+
+
+def _c10d_main(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from wormhole_amd import _native
+    send = [rank + 1 + q for q in range(world)]
+    x = torch.cat([torch.full((send[q], 3), float(100 * rank + q)) for q in range(world)])
+    recv = [p + 1 + rank for p in range(world)]
+    out = _native.hip().c10d_a2a_rows(pg=dist.group.WORLD, x=x, send_rows=send, recv_rows=recv)
+    o = 0
+    for p in range(world):
+        assert bool((out[o:o + recv[p]] == 100 * p + rank).all()), (rank, p)
+        o += recv[p]
+    dist.destroy_process_group()
+
+
+def test_native_c10d_all_to_all_three_ranks():
+    """The transport of the native step from C++: the Python process group
+    object cast to c10d::ProcessGroup, a row-wise uneven alltoall_base and
+    its work's wait (here over gloo between 3 CPU ranks; RCCL on GPUs)."""
+    mp.spawn(_c10d_main, args=(3, _free_port()), nprocs=3, join=True)

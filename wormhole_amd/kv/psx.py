@@ -268,6 +268,10 @@ class Psx:
         # the owner-side update of the linear wire format: (algo, alpha,
         # beta, l1, l2) -- the linear model's, or DiFacto's FTRL on w (algo 4)
         self.lin_hp = lrn.psx_linear_hp() if self.linear else None
+        # the native driver of train() (csrc/bind/psx_native.inl PsxStep):
+        # decided at the first training call (apps set max_key after
+        # construction); False = this Python step
+        self._nat = None
 
     # ------------------------------------------------------------ wire stats
     def _tally(self, c, x, send_rows):
@@ -341,6 +345,8 @@ class Psx:
 
     def wire_reset(self):
         self.wire = [0, 0, 0, 0]
+        if self._nat:
+            self._nat.wire_reset()
         if self.timer is not None:
             self.timer.reset()
 
@@ -348,7 +354,10 @@ class Psx:
         """Per-step averages since :meth:`wire_reset`: bytes each collective
         sent to peers (and, with WH_COMM_TIMING=1, its GPU time in ms)."""
         steps = max(int(steps), 1)
-        out = {"c%d" % c: self.wire[c] / steps for c in range(4)}
+        wire = list(self.wire)
+        if self._nat:
+            wire = [a + b for a, b in zip(wire, self._nat.wire())]
+        out = {"c%d" % c: wire[c] / steps for c in range(4)}
         out["c0"] = 32 * (self.P - 1)  # {keys, overflow, V rows, has data} per peer
         if self.timer is not None:
             for c, ms in self.timer.report().items():
@@ -677,7 +686,67 @@ class Psx:
         self._finish()
         self.last_empty = True
 
+    # ------------------------------------------------------------ native
+    def _native(self):
+        """The C++ driver of :meth:`train` when this configuration has one:
+        a GPU rank over RCCL, the loopback identity or the 1-rank RCCL
+        loopback; no payload filter, collective timer, key modulo or
+        embedding-gradient post-processing (those stay on this Python
+        step). ``WH_PSX_NATIVE=0`` keeps the Python step."""
+        if self._nat is None:
+            lrn, emb = self.lrn, self.lrn.emb
+            post = emb is not None and (emb.grad_clipping > 0 or emb.dropout > 0 or
+                                        bool(emb.grad_normalization))
+            backend = getattr(self.comm, "backend", "")
+            ok = (self.cuda and os.environ.get("WH_PSX_NATIVE", "1") != "0" and
+                  backend in ("nccl", "loopback", "loopback-rccl") and
+                  not getattr(self.comm, "stage", False) and self.qf is None and
+                  self.timer is None and not lrn.max_key and not post)
+            self._nat = False
+            if ok:
+                pg = self.comm.pg if backend in ("nccl", "loopback-rccl") else None
+                self._nat = _native.hip().PsxStep(
+                    store=self.store, P=self.P, S=self.nshard,
+                    rank=int(getattr(self.comm, "rank", 0)), pg=pg, linear=self.linear,
+                    lin_hp=list(self.lin_hp) if self.linear else [0.0] * 5,
+                    hp=list(lrn.hp), threshold=int(lrn.threshold), l1_shrk=bool(lrn.l1_shrk),
+                    seed=int(lrn.seed), loss=int(lrn.loss), met=lrn.met, auc_sum=lrn.auc_sum,
+                    tau=int(self.tau), max_load=float(lrn.kv.guard.max_load),
+                    cu_reserve=_CU_RESERVE if backend in ("nccl", "loopback-rccl") else 0)
+                self._nat.requests = self.requests
+        return self._nat or None
+
+    def _native_drain(self):
+        """Hand the pipeline back to the Python step (an evaluation or a
+        read-only pull): every minibatch in flight completed, the begun
+        localize dropped (all ranks reach this at the same point)."""
+        nat = self._nat
+        if nat:
+            self.lrn.n_mb += nat.flush()
+            nat.drop_job()
+            self.requests = nat.requests
+            g = self.lrn.kv.guard
+            g.grows = max(g.grows, nat.grows)
+
     def train(self, keys, offset, val, label, data_pass, next_batch):
+        nat = self._native() if self.cuda else None
+        if nat is not None:
+            nk = no = nv = None
+            ready = 0
+            if next_batch is not None:
+                nk, no, nv = next_batch[:3]
+                if len(next_batch) > 3 and next_batch[3] is not None:
+                    ready = next_batch[3].cuda_event
+            has, nmb, u, v = nat.train(keys=keys, offset=offset, val=val, label=label,
+                                       data_pass=int(data_pass), next_keys=nk, next_offset=no,
+                                       next_val=nv, ready=ready)
+            self.lrn.n_mb += nmb
+            if nmb:
+                self.lrn.last_sizes = (u, v)
+            self.last_empty = not has
+            if has:
+                self.lrn.step += 1
+            return
         if self.cuda and streams.current_id(self.dev.index) != self.S.stream_id:
             self.S = torch.cuda.current_stream(self.dev)
         self.last_empty = False
@@ -731,6 +800,7 @@ class Psx:
         then open (no insert), reply and forward synchronously. Returns the
         predictions, or None when no rank had data (``last_empty``)."""
         self.flush()
+        self._native_drain()
         self.last_empty = False
         self._ensure_job(keys, offset, val)
         send, recv, empty = self._counts()
@@ -755,6 +825,7 @@ class Psx:
         with rows [U, vstride] (zero for keys without an embedding) or None
         for the linear wire format; None if no rank has keys."""
         self.flush()
+        self._native_drain()
         n = int(keys.numel())
         dev = keys.device
         offset = torch.arange(n + 1, dtype=torch.int64, device=dev)
@@ -789,6 +860,10 @@ class Psx:
     def flush(self):
         """Complete every minibatch in flight (end of a pass, before reading
         or saving the model, end of a timed run)."""
+        if self._nat:
+            self.lrn.n_mb += self._nat.flush()
+            g = self.lrn.kv.guard
+            g.grows = max(g.grows, self._nat.grows)
         if self.push is not None and self.push.gvc is not None:
             self._c3(self.push)
         if self.job is not None and self.job[2] is not None:
