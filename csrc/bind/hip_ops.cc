@@ -443,21 +443,23 @@ class LocalizeJob {
     auto pk = torch::empty({nnz}, i64);
     auto pr = torch::empty({nnz}, i32);
     auto pv = torch::empty({vp ? nnz : 0}, keys_.options().dtype(torch::kFloat32));
-    auto pj = torch::empty({nnz}, i32);
+    auto pos_of = torch::empty({nnz}, i32);
     wh::loc_part_scatter(kp, vp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv, ptr<int64_t>(base),
                          reinterpret_cast<const uint32_t*>(gsum.data_ptr()),
                          reinterpret_cast<const uint32_t*>(hist.data_ptr()),
                          reinterpret_cast<uint64_t*>(pk.data_ptr()), ptr<int32_t>(pr),
-                         vp ? ptr<float>(pv) : nullptr, ptr<int32_t>(pj), s);
+                         vp ? ptr<float>(pv) : nullptr, ptr<int32_t>(pos_of), s);
+    auto plid = torch::empty({nnz}, i32);
     auto* pw = reinterpret_cast<unsigned long long*>(ws.part_ws.data_ptr());
     wh::loc_part_dedup(reinterpret_cast<const uint64_t*>(pk.data_ptr()), ptr<int32_t>(pr),
-                       ptr<int32_t>(pj), vp ? ptr<float>(pv) : nullptr, nnz, nsh, plan_, hv,
-                       ptr<int64_t>(base), wh::lookback_bind(ws.lb_loc.data_ptr()),
+                       vp ? ptr<float>(pv) : nullptr, nnz, nsh, plan_, hv, ptr<int64_t>(base),
+                       wh::lookback_bind(ws.lb_loc.data_ptr()),
                        reinterpret_cast<uint64_t*>(uniq_.data_ptr()), ptr<int32_t>(ucnt_),
                        ptr<int64_t>(csc_off_), ptr<int32_t>(csc_row_),
-                       vp ? ptr<float>(csc_val_) : nullptr, ptr<int32_t>(lid_), pw,
+                       vp ? ptr<float>(csc_val_) : nullptr, ptr<int32_t>(plid), pw,
                        reinterpret_cast<unsigned int*>(pw + wh::kPartMaxDigits),
                        ptr<int64_t>(owner_cnt), s, loc_timing() ? ptr<int64_t>(loc_timing_buf()) : nullptr);
+    wh::loc_part_lid(ptr<int32_t>(pos_of), ptr<int32_t>(plid), nnz, ptr<int32_t>(lid_), s);
     return owner_cnt;
   }
 

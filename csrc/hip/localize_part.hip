@@ -15,8 +15,7 @@
 //                  counted there, get their local ids (partition order; the
 //                  partition base by decoupled look-back) and occurrence
 //                  offsets (partition range + LDS scan), and every non-zero
-//                  is placed into the CSC and its local id stored at its CSR
-//                  position (the scatter carried that position along).
+//                  is placed into the CSC and mapped back to its local id.
 //
 // The previous path paid ~3M random global operations per 100k-row
 // minibatch (hash find-or-insert after LDS tile de-duplication, then three
@@ -224,9 +223,8 @@ __global__ __launch_bounds__(1024) void k_part_base(uint32_t* __restrict__ gsum,
 // digit's run (scattered 4/8-byte stores cost one memory request each:
 // storing in arrival order made this pass 140 us per 100k rows). The row of
 // a non-zero comes from a binary search over the tile's row offsets in LDS
-// (a tile owns whole rows), done as the staged entry is written out: the
-// stage holds the non-zero's CSR position j, which also goes out (pj) so the
-// dedup can write the local id of non-zero j directly.
+// (a tile owns whole rows); pos_of[j] (the non-zero's partition position) is
+// stored in CSR order by the thread that loaded it.
 constexpr int kScatThreads = 512;
 constexpr int kScatPer = 8;
 constexpr int kChunk = kScatThreads * kScatPer;  // 4096
@@ -241,15 +239,15 @@ __global__ __launch_bounds__(kScatThreads, 4) void k_part_scatter(
     const int64_t* __restrict__ off, int64_t nrows, int R, int nshard, int npo_bits, int stride,
     int nho, int ndig, PartHeavy hv, const int64_t* __restrict__ base,
     const uint32_t* __restrict__ gpre, const uint32_t* __restrict__ tpre, uint64_t* __restrict__ pk,
-    int32_t* __restrict__ pr, float* __restrict__ pv, int32_t* __restrict__ pj) {
+    int32_t* __restrict__ pr, float* __restrict__ pv, int32_t* __restrict__ pos_of) {
   extern __shared__ __align__(16) unsigned char lds[];
   uint32_t* gbase = reinterpret_cast<uint32_t*>(lds);   // next free position per digit
   uint32_t* cnt = gbase + ndig;                          // chunk counts -> chunk starts
   uint32_t* lst = cnt + ndig;
   int64_t* so = reinterpret_cast<int64_t*>(lst + ndig + (ndig & 1));
   uint64_t* sk = reinterpret_cast<uint64_t*>(so + kPartMaxRows + 1);
-  int32_t* sj = reinterpret_cast<int32_t*>(sk + kChunk);  // CSR position of each staged id
-  uint16_t* sd = reinterpret_cast<uint16_t*>(sj + kChunk);  // digit of each staged id
+  int32_t* sr = reinterpret_cast<int32_t*>(sk + kChunk);
+  uint16_t* sd = reinterpret_cast<uint16_t*>(sr + kChunk);  // digit of each staged id
   float* sv = reinterpret_cast<float*>(sd + kChunk);
   __shared__ uint32_t wsum[kScatThreads / 64];
   __shared__ unsigned long long hk[kHeavySlots];
@@ -310,32 +308,31 @@ __global__ __launch_bounds__(kScatThreads, 4) void k_part_scatter(
       run += c[q];
     }
     __syncthreads();
-    // stage digit-sorted
+    // stage digit-sorted; every loading thread knows its partition position
 #pragma unroll
     for (int u = 0; u < kScatPer; ++u) {
       if (d[u] < 0) continue;
       const int64_t j = b + u * kScatThreads + threadIdx.x;
       const uint32_t lp = lst[d[u]] + rk[u];
+      int lo = 0, hi = nr - 1;  // largest row index with so[row] <= j
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (so[mid] <= j) lo = mid;
+        else hi = mid - 1;
+      }
       sk[lp] = k[u];
-      sj[lp] = (int32_t)j;
+      sr[lp] = (int32_t)(r0 + lo);
       sd[lp] = (uint16_t)d[u];
       if (val) sv[lp] = val[j];
+      pos_of[j] = (int32_t)(gbase[d[u]] + rk[u]);
     }
     __syncthreads();
     const int n = (int)(j1 - b < kChunk ? j1 - b : kChunk);
     for (int i = threadIdx.x; i < n; i += kScatThreads) {
       const int dd = sd[i];
       const uint32_t gp = gbase[dd] + (uint32_t)i - lst[dd];
-      const int32_t j = sj[i];
-      int lo = 0, hi = nr - 1;  // the row: largest index with so[row] <= j
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (so[mid] <= j) lo = mid;
-        else hi = mid - 1;
-      }
       pk[gp] = sk[i];
-      pr[gp] = (int32_t)(r0 + lo);
-      pj[gp] = j;
+      pr[gp] = sr[i];
       if (val) pv[gp] = sv[i];
     }
     __syncthreads();
@@ -428,11 +425,11 @@ __device__ __forceinline__ void heavy_elect(const PartHeavy& hv, int own, uint64
 
 template <bool kVal>
 __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
-    const uint64_t* __restrict__ pk, const int32_t* __restrict__ pr, const int32_t* __restrict__ pj,
+    const uint64_t* __restrict__ pk, const int32_t* __restrict__ pr,
     const float* __restrict__ pv, const int64_t* __restrict__ base, int ntiles, int ndig,
     int nshard, int npo_bits, int stride, int nho, PartHeavy hv, Lookback lb, int64_t nnz,
     uint64_t* __restrict__ uniq, int32_t* __restrict__ ucnt, int64_t* __restrict__ csc_off,
-    int32_t* __restrict__ csc_row, float* __restrict__ csc_val, int32_t* __restrict__ lid,
+    int32_t* __restrict__ csc_row, float* __restrict__ csc_val, int32_t* __restrict__ plid,
     unsigned long long* __restrict__ up, unsigned int* arrive, int64_t* __restrict__ owner_cnt,
     int64_t* __restrict__ tim) {
   __shared__ unsigned long long sk[kDedupSlots];
@@ -542,7 +539,7 @@ __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
       for (int64_t i = ps + threadIdx.x; i < pe; i += kDedupThreads) {
         csc_row[i] = pr[i];
         if (kVal) csc_val[i] = pv[i];
-        lid[pj[i]] = L;
+        plid[i] = L;
       }
     }
   } else {
@@ -564,11 +561,11 @@ __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
       en += cnt[q];
     }
     __syncthreads();
-    // 3. place every occurrence: CSC row (and value); its local id goes to
-    // its CSR position
+    // 3. place every occurrence: CSC row (and value); its local id is stored
+    // in partition order (plid), mapped back to CSR order by k_part_lid
     for (int64_t b = ps; b < pe; b += kDU * kDedupThreads) {
       uint64_t k[kDU];
-      int32_t r[kDU], jj[kDU];
+      int32_t r[kDU];
       float v[kDU];
 #pragma unroll
       for (int u = 0; u < kDU; ++u) {
@@ -576,7 +573,6 @@ __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
         const bool ok = i < pe;
         k[u] = ok ? pk[i] : 0;
         r[u] = ok ? pr[i] : 0;
-        jj[u] = ok ? pj[i] : 0;
         if (kVal) v[u] = ok ? pv[i] : 0.f;
       }
       unsigned long long h0[kDU];
@@ -591,7 +587,7 @@ __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
           const int64_t dst = ps + q;
           csc_row[dst] = r[u];
           if (kVal) csc_val[dst] = v[u];
-          lid[jj[u]] = (int32_t)(gbase + sl[s]);
+          plid[i] = (int32_t)(gbase + sl[s]);
         }
       }
     }
@@ -618,6 +614,20 @@ __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
     __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   for (int i = threadIdx.x; i <= nshard; i += kDedupThreads) owner_cnt[i] = ocnt[i];
+}
+
+// lid[j] = plid[pos_of[j]]: CSR-order local ids. The reads of a wave are
+// partly contiguous (a tile's non-zeros of one partition sit together).
+__global__ __launch_bounds__(256) void k_part_lid(const int32_t* __restrict__ pos_of,
+                                                  const int32_t* __restrict__ plid, int64_t nnz,
+                                                  int32_t* __restrict__ lid) {
+  const int64_t j0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (j0 + 3 < nnz) {
+    const int4 p = *reinterpret_cast<const int4*>(pos_of + j0);
+    *reinterpret_cast<int4*>(lid + j0) = make_int4(plid[p.x], plid[p.y], plid[p.z], plid[p.w]);
+  } else {
+    for (int64_t j = j0; j < nnz; ++j) lid[j] = plid[pos_of[j]];
+  }
 }
 
 __global__ void k_part_empty(int nshard, int64_t* owner_cnt, int64_t* csc_off) {
@@ -695,25 +705,30 @@ void loc_part_offsets(const PartPlan& pl, uint32_t* hist, uint32_t* gsum, int64_
 void loc_part_scatter(const uint64_t* keys, const float* val, const int64_t* offset,
                       int64_t nrows, int nshard, const PartPlan& pl, const PartHeavy& hv,
                       const int64_t* base, const uint32_t* gpre, const uint32_t* tpre,
-                      uint64_t* pk, int32_t* pr, float* pv, int32_t* pj, hipStream_t s) {
+                      uint64_t* pk, int32_t* pr, float* pv, int32_t* pos_of, hipStream_t s) {
   const size_t lds = scatter_lds_bytes(pl.ndig, val != nullptr) + 16;
   hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)pl.ntiles), dim3(kScatThreads), lds, s, keys,
                      val, offset, nrows, pl.R, nshard, pl.npo_bits, pl.stride, pl.nho, pl.ndig, hv,
-                     base, gpre, tpre, pk, pr, pv, pj);
+                     base, gpre, tpre, pk, pr, pv, pos_of);
 }
 
-void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const int32_t* pj, const float* pv,
-                    int64_t nnz,
+void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const float* pv, int64_t nnz,
                     int nshard, const PartPlan& pl, const PartHeavy& hv, const int64_t* base,
                     const Lookback& lb,
                     uint64_t* uniq, int32_t* ucnt, int64_t* csc_off, int32_t* csc_row,
-                    float* csc_val, int32_t* lid, unsigned long long* up, unsigned int* arrive,
+                    float* csc_val, int32_t* plid, unsigned long long* up, unsigned int* arrive,
                     int64_t* owner_cnt, hipStream_t s, int64_t* tim) {
   auto kern = pv ? k_part_dedup<true> : k_part_dedup<false>;
-  hipLaunchKernelGGL(kern, dim3((unsigned)pl.ndig), dim3(kDedupThreads), 0, s, pk, pr, pj, pv, base,
+  hipLaunchKernelGGL(kern, dim3((unsigned)pl.ndig), dim3(kDedupThreads), 0, s, pk, pr, pv, base,
                      (int)pl.ntiles, pl.ndig, nshard, pl.npo_bits, pl.stride, pl.nho, hv, lb, nnz, uniq,
                      ucnt, csc_off,
-                     csc_row, csc_val, lid, up, arrive, owner_cnt, tim);
+                     csc_row, csc_val, plid, up, arrive, owner_cnt, tim);
+}
+
+void loc_part_lid(const int32_t* pos_of, const int32_t* plid, int64_t nnz, int32_t* lid,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(k_part_lid, dim3((unsigned)((nnz + 1023) / 1024)), dim3(256), 0, s, pos_of,
+                     plid, nnz, lid);
 }
 
 void loc_part_empty(int nshard, int64_t* owner_cnt, int64_t* csc_off, hipStream_t s) {

@@ -108,21 +108,24 @@ void loc_part_hist(const uint64_t* keys, const int64_t* offset, int64_t nrows, i
 int64_t loc_part_groups(const PartPlan& pl);
 void loc_part_offsets(const PartPlan& pl, uint32_t* hist, uint32_t* gsum, int64_t* base,
                       hipStream_t s);
-// pk/pr/pj [nnz] (key, row, CSR position; + pv [nnz] when val) in partition
+// pk/pr [nnz] (+ pv [nnz] when val) in partition order; pos_of [nnz] in CSR
 // order (gpre / tpre: gsum / hist after loc_part_offsets)
 void loc_part_scatter(const uint64_t* keys, const float* val, const int64_t* offset,
                       int64_t nrows, int nshard, const PartPlan& pl, const PartHeavy& hv,
                       const int64_t* base, const uint32_t* gpre, const uint32_t* tpre,
-                      uint64_t* pk, int32_t* pr, float* pv, int32_t* pj, hipStream_t s);
+                      uint64_t* pk, int32_t* pr, float* pv, int32_t* pos_of, hipStream_t s);
 // up [kPartMaxDigits] u64 and *arrive (0 between calls): a workspace of its
-// own; lb: a look-back workspace no concurrent kernel uses. lid [nnz]: the
-// local id of every non-zero in CSR order (written at pj).
-void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const int32_t* pj, const float* pv,
-                    int64_t nnz, int nshard, const PartPlan& pl, const PartHeavy& hv,
-                    const int64_t* base, const Lookback& lb,
+// own; lb: a look-back workspace no concurrent kernel uses. plid [nnz]:
+// local ids in partition order.
+void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const float* pv, int64_t nnz,
+                    int nshard, const PartPlan& pl, const PartHeavy& hv, const int64_t* base,
+                    const Lookback& lb,
                     uint64_t* uniq, int32_t* ucnt, int64_t* csc_off, int32_t* csc_row,
-                    float* csc_val, int32_t* lid, unsigned long long* up, unsigned int* arrive,
+                    float* csc_val, int32_t* plid, unsigned long long* up, unsigned int* arrive,
                     int64_t* owner_cnt, hipStream_t s, int64_t* tim = nullptr);
+// lid[j] = plid[pos_of[j]]
+void loc_part_lid(const int32_t* pos_of, const int32_t* plid, int64_t nnz, int32_t* lid,
+                  hipStream_t s);
 // nnz == 0: zero owner counts and csc_off[0]
 void loc_part_empty(int nshard, int64_t* owner_cnt, int64_t* csc_off, hipStream_t s);
 

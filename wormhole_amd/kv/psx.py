@@ -726,7 +726,7 @@ class Psx:
             nat.drop_job()
             self.requests = nat.requests
             g = self.lrn.kv.guard
-            g.grows = max(g.grows, nat.grows)
+            g.grows, g.vgrows = max(g.grows, nat.grows), max(g.vgrows, nat.vgrows)
 
     def train(self, keys, offset, val, label, data_pass, next_batch):
         nat = self._native() if self.cuda else None
@@ -864,6 +864,7 @@ class Psx:
             self.lrn.n_mb += self._nat.flush()
             g = self.lrn.kv.guard
             g.grows = max(g.grows, self._nat.grows)
+            g.vgrows = max(g.vgrows, self._nat.vgrows)
         if self.push is not None and self.push.gvc is not None:
             self._c3(self.push)
         if self.job is not None and self.job[2] is not None:

@@ -751,7 +751,7 @@ class TreeBuilder:
         their reference. With a feature-sharded exchange, hist holds this
         rank's feature slice only: the local best goes through
         :meth:`HistExchange.pick`."""
-        x = self.xchg
+        x = getattr(self, "xchg", None)
         if x is None:
             return self._find_splits_local(hist, totals, self.valid_mask, 0)
         S = hist.shape[0]
@@ -989,7 +989,7 @@ class TreeBuilder:
     def _reduce_hist(self, h):
         """Rank partials -> global histograms: allreduced (all features), or
         this rank's feature slice (:class:`HistExchange`)."""
-        if self.xchg is not None:
+        if getattr(self, "xchg", None) is not None:
             return self.xchg.reduce_scatter(h)
         self._allreduce_hist(h)
         return h
