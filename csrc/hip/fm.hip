@@ -22,6 +22,7 @@
 // and the gradient mirrors it: gw[U] + gvc[m] (same vidx numbering). Only the
 // m keys with an embedding move 256 bytes; the rest move 8 (pull) / 4 (push).
 #include "wh_common.h"
+#include <string>
 #include "wh_kernels.h"
 #include "wh_lookback.h"
 #include "wh_loss.h"
@@ -616,15 +617,29 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
                                                     float* __restrict__ gw_out,
                                                     float* __restrict__ gvc,
                                                     float* __restrict__ part_gw,
-                                                    float* __restrict__ part_gv) {
+                                                    float* __restrict__ part_gv, int xcd) {
   using S = Shape<G>;
   __shared__ int2 stage[kThreads / 64][64];
   int2* st = stage[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63, gl = lane & (G - 1), sub = lane / G;
-  const int64_t nch = *nchunk_p;
-  const int64_t nw = (int64_t)gridDim.x * (kThreads / 64);
-  const int64_t w0 =
+  const int64_t nch_all = *nchunk_p;
+  // XCD-aware split (xcd != 0, grid a multiple of 8): the chunk list is
+  // ordered by the first row a chunk touches, and blocks b, b + 8, ... share
+  // one XCD's L2 (round-robin dispatch), so group b % 8 takes the b % 8-th
+  // eighth of the list: an XCD's xv gathers then cover ~1/8 of the rows
+  // (3.2 MB of 25.6 MB at 100k rows) and stay in its 4 MB L2 instead of
+  // every XCD sweeping all rows.
+  int64_t lo = 0, nch = nch_all, nw = (int64_t)gridDim.x * (kThreads / 64);
+  int64_t w0 =
       __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6));
+  if (xcd && (gridDim.x & 7) == 0) {
+    const int grp = blockIdx.x & 7;
+    lo = nch_all * grp / 8;
+    nch = nch_all * (grp + 1) / 8;
+    nw = (int64_t)(gridDim.x >> 3) * (kThreads / 64);
+    w0 = lo + __builtin_amdgcn_readfirstlane((int)(((int64_t)(blockIdx.x >> 3) * kThreads +
+                                                    threadIdx.x) >> 6));
+  }
   auto get_meta = [&](int64_t c) {
     return c < nch ? meta[c] : make_int4(0, 0, 0, -1);
   };
@@ -989,11 +1004,18 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
                        off_s + nuniq, key_s, beg_s, csc_off, pgs, gw);
   if (!hdr) return;
   const int G = vstride / 4;
-  const int64_t vblk = std::min<int64_t>((v_cap(nuniq, nnz) + 3) / 4,
-                                         WH_RESIDENT(G, k_bwd_v, 2048));
+  int64_t vblk = std::min<int64_t>((v_cap(nuniq, nnz) + 3) / 4,
+                                   WH_RESIDENT(G, k_bwd_v, 2048));
+  // XCD-aware chunk split (k_bwd_v): a grid of whole groups of 8 blocks;
+  // WH_BWD_XCD=0 keeps the plain round-robin walk (A/B)
+  static const int xcd = [] {
+    const char* e = std::getenv("WH_BWD_XCD");
+    return e && std::string(e) == "0" ? 0 : 1;
+  }();
+  if (xcd && vblk >= 64) vblk -= vblk % 8;
   const dim3 grid((unsigned)vblk), block(kThreads);
   WH_DISPATCH_G(G, k_bwd_v, grid, block, 0, s, off_v + nuniq, meta_sorted, csc_row, csc_val,
-                dual, xv, vc, vstride, gw, gvc, pgv_w, pgv);
+                dual, xv, vc, vstride, gw, gvc, pgv_w, pgv, xcd);
   if (det_part)
     hipLaunchKernelGGL(k_bwd_reduce_v, dim3(grid_for(vcap * 64, kThreads)), dim3(kThreads), 0, s,
                        off_v + nuniq, meta_v, csc_off, pgv_w, pgv, vstride, gw, gvc);

@@ -16,4 +16,9 @@ for i in 1 2 3; do
   echo "rccl_native $(b --loopback 8 --loopback-rccl)"
   echo "rccl_python $(WH_PSX_NATIVE=0 b --loopback 8 --loopback-rccl)"
 done | tee $OUT/ab.txt
+bash tools/gpu/env_ab.sh r4e/xcd "WH_BWD_XCD=0" || exit $?
+$T 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bprof -o run -- python3 bench.py --steps 100 > $OUT/bprof.log 2>&1 || exit $?
+WH_BWD_XCD=0 $T 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bprof0 -o run -- python3 bench.py --steps 100 > $OUT/bprof0.log 2>&1 || exit $?
+$T 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $OUT/pmc_xcd -o run -- python3 bench.py --steps 10 --warmup 2 --prewarm 100 > $OUT/pmc_xcd.log 2>&1 || exit $?
+WH_BWD_XCD=0 $T 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $OUT/pmc_rr -o run -- python3 bench.py --steps 10 --warmup 2 --prewarm 100 > $OUT/pmc_rr.log 2>&1 || exit $?
 echo all done rc=$rc
