@@ -115,10 +115,10 @@ __device__ __forceinline__ int digit_of(uint64_t k, const unsigned long long* hk
   return part_digit(k, nshard, npo_bits, stride, npo_bits - log2_nho(nho));
 }
 
-// the tile's row range [r0, r1) and its non-zero range
-__device__ __forceinline__ void tile_rows(const int64_t* off, int64_t nrows, int R, int64_t& r0,
+// tile t's row range [r0, r1)
+__device__ __forceinline__ void tile_rows(int64_t t, int64_t nrows, int R, int64_t& r0,
                                           int64_t& r1) {
-  r0 = (int64_t)blockIdx.x * R;
+  r0 = t * R;
   r1 = r0 + R < nrows ? r0 + R : nrows;
 }
 
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(const uint64_t* __re
   heavy_build(hv, nshard, npo_bits, stride, nho, hk, hd);
   const bool hon = hv.nho > 0;
   int64_t r0, r1;
-  tile_rows(off, nrows, R, r0, r1);
+  tile_rows(blockIdx.x, nrows, R, r0, r1);
   const int64_t j0 = off[r0], j1 = off[r1];
   for (int64_t b = j0; b < j1; b += 4 * kPartThreads) {
     uint64_t k[4];
@@ -254,13 +254,17 @@ __global__ __launch_bounds__(kScatThreads, 4) void k_part_scatter(
   __shared__ int hd[kHeavySlots];
   heavy_build(hv, nshard, npo_bits, stride, nho, hk, hd);
   const bool hon = hv.nho > 0;
+  // neighbouring tiles write neighbouring runs of every partition (often the
+  // same 128-byte lines): an XCD takes a contiguous range of tiles so those
+  // partial-line writes merge in its L2
+  const int64_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
   int64_t r0, r1;
-  tile_rows(off, nrows, R, r0, r1);
+  tile_rows(tile, nrows, R, r0, r1);
   const int nr = (int)(r1 - r0);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < ndig; i += kScatThreads)
-    gbase[i] = (uint32_t)base[i] + gpre[(int64_t)(blockIdx.x / kColTB) * ndig + i] +
-               tpre[(int64_t)blockIdx.x * ndig + i];
+    gbase[i] = (uint32_t)base[i] + gpre[(tile / kColTB) * ndig + i] +
+               tpre[tile * ndig + i];
   for (int i = threadIdx.x; i <= nr; i += kScatThreads) so[i] = off[r0 + i];
   __syncthreads();
   const int64_t j0 = so[0], j1 = so[nr];
@@ -621,7 +625,9 @@ __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
 __global__ __launch_bounds__(256) void k_part_lid(const int32_t* __restrict__ pos_of,
                                                   const int32_t* __restrict__ plid, int64_t nnz,
                                                   int32_t* __restrict__ lid) {
-  const int64_t j0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  // contiguous block ranges per XCD: the runs of pos_of a tile reads in
+  // every partition sit next to its neighbour tiles' runs (same plid lines)
+  const int64_t j0 = (xcd_swizzle(blockIdx.x, gridDim.x) * 256 + threadIdx.x) * 4;
   if (j0 + 3 < nnz) {
     const int4 p = *reinterpret_cast<const int4*>(pos_of + j0);
     *reinterpret_cast<int4*>(lid + j0) = make_int4(plid[p.x], plid[p.y], plid[p.z], plid[p.w]);

@@ -30,6 +30,15 @@ __host__ __device__ __forceinline__ int owner_of(uint64_t key, int nshard) {
   return nshard <= 1 ? 0 : (int)(mix64b(key) % (uint64_t)nshard);
 }
 
+// XCD-aware block remap (bijective for any n): blocks b, b + 8, ... share an
+// XCD's L2 under round-robin dispatch, so group b % 8 gets a CONTIGUOUS
+// range of the logical blocks -- neighbouring tiles whose reads or partial
+// line writes overlap then meet in one L2 (MI355X: 8 XCDs, 4 MB L2 each)
+__device__ __forceinline__ int64_t xcd_swizzle(int64_t b, int64_t n) {
+  const int64_t g = b & 7, q = n >> 3, r = n & 7;
+  return (g < r ? g * (q + 1) : r * (q + 1) + (g - r) * q) + (b >> 3);
+}
+
 // counter-based uniform in [0,1): stateless, reproducible per (seed, a, b)
 __host__ __device__ __forceinline__ float uhash01(uint64_t seed, uint64_t a, uint64_t b = 0) {
   uint64_t h = mix64(seed ^ mix64(a * 0x9e3779b97f4a7c15ull + b));
