@@ -239,7 +239,13 @@ class PsxStep {
     Tensor r = torch::empty_like(send);
     std::vector<int64_t> none;
     Tensor s = send.contiguous();
-    auto w = pg_->alltoall_base(r, s, none, none);
+    // a blocking collective, as Python's all_to_all_single(async_op=False):
+    // RCCL then runs it on the CURRENT stream (cs) instead of its own stream
+    // plus two event hand-offs -- this tiny exchange sits on the path of the
+    // step's one host read
+    c10d::AllToAllOptions opts;
+    opts.asyncOp = false;
+    auto w = pg_->alltoall_base(r, s, none, none, opts);
     w->wait();
     return r;
   }

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(kScatThreads, 4) void k_part_scatter(
     const int64_t* __restrict__ off, int64_t nrows, int R, int nshard, int npo_bits, int stride,
     int nho, int ndig, PartHeavy hv, const int64_t* __restrict__ base,
     const uint32_t* __restrict__ gpre, const uint32_t* __restrict__ tpre, uint64_t* __restrict__ pk,
-    int32_t* __restrict__ pr, float* __restrict__ pv, int32_t* __restrict__ pos_of) {
+    int32_t* __restrict__ pr, float* __restrict__ pv, int32_t* __restrict__ pos_of, int swz) {
   extern __shared__ __align__(16) unsigned char lds[];
   uint32_t* gbase = reinterpret_cast<uint32_t*>(lds);   // next free position per digit
   uint32_t* cnt = gbase + ndig;                          // chunk counts -> chunk starts
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kScatThreads, 4) void k_part_scatter(
   // neighbouring tiles write neighbouring runs of every partition (often the
   // same 128-byte lines): an XCD takes a contiguous range of tiles so those
   // partial-line writes merge in its L2
-  const int64_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t tile = swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   int64_t r0, r1;
   tile_rows(tile, nrows, R, r0, r1);
   const int nr = (int)(r1 - r0);
@@ -624,10 +624,11 @@ __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
 // partly contiguous (a tile's non-zeros of one partition sit together).
 __global__ __launch_bounds__(256) void k_part_lid(const int32_t* __restrict__ pos_of,
                                                   const int32_t* __restrict__ plid, int64_t nnz,
-                                                  int32_t* __restrict__ lid) {
+                                                  int32_t* __restrict__ lid, int swz) {
   // contiguous block ranges per XCD: the runs of pos_of a tile reads in
   // every partition sit next to its neighbour tiles' runs (same plid lines)
-  const int64_t j0 = (xcd_swizzle(blockIdx.x, gridDim.x) * 256 + threadIdx.x) * 4;
+  const int64_t b = swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t j0 = (b * 256 + threadIdx.x) * 4;
   if (j0 + 3 < nnz) {
     const int4 p = *reinterpret_cast<const int4*>(pos_of + j0);
     *reinterpret_cast<int4*>(lid + j0) = make_int4(plid[p.x], plid[p.y], plid[p.z], plid[p.w]);
@@ -642,6 +643,17 @@ __global__ void k_part_empty(int nshard, int64_t* owner_cnt, int64_t* csc_off) {
 }
 
 }  // namespace
+
+// WH_LOC_XCD=0: the scatter and the lid gather take tiles in dispatch order
+// (A/B of the XCD-contiguous tile ranges)
+static int loc_swizzle() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("WH_LOC_XCD");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on;
+}
 
 PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, bool heavy) {
   PartPlan pl;
@@ -715,7 +727,7 @@ void loc_part_scatter(const uint64_t* keys, const float* val, const int64_t* off
   const size_t lds = scatter_lds_bytes(pl.ndig, val != nullptr) + 16;
   hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)pl.ntiles), dim3(kScatThreads), lds, s, keys,
                      val, offset, nrows, pl.R, nshard, pl.npo_bits, pl.stride, pl.nho, pl.ndig, hv,
-                     base, gpre, tpre, pk, pr, pv, pos_of);
+                     base, gpre, tpre, pk, pr, pv, pos_of, loc_swizzle());
 }
 
 void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const float* pv, int64_t nnz,
@@ -734,7 +746,7 @@ void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const float* pv, int6
 void loc_part_lid(const int32_t* pos_of, const int32_t* plid, int64_t nnz, int32_t* lid,
                   hipStream_t s) {
   hipLaunchKernelGGL(k_part_lid, dim3((unsigned)((nnz + 1023) / 1024)), dim3(256), 0, s, pos_of,
-                     plid, nnz, lid);
+                     plid, nnz, lid, loc_swizzle());
 }
 
 void loc_part_empty(int nshard, int64_t* owner_cnt, int64_t* csc_off, hipStream_t s) {
