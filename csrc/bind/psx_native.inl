@@ -99,11 +99,18 @@ class PsxStep {
                   const c10::optional<Tensor>& noffset, const c10::optional<Tensor>& nval,
                   int64_t ready) {
     c10::DeviceGuard g(keys.device());
+    // WH_STEP_TIMING=1: host us per phase, printed every 1000 calls: s0 job,
+    // s1 count read (the host WAIT), s2 tables + C2/C3 issue, s3 localize
+    // finish + next begin + C1, s4 reply (forward), s5 owner push, s6 open,
+    // s7 C0 of the next job, s8 backward
+    HostTimer ht(timing_.get());
     S_stream_ = c10::hip::getCurrentHIPStream(dev_);
     fwd_mb_ = 0;
     ensure_job(keys, offset, val);
+    ht.mark(0);
     std::vector<int64_t> send, recv;
     const bool empty = counts(send, recv);
+    ht.mark(1);
     if (empty) {
       finish_job();
       return py::make_tuple(false, 0, 0, 0);
@@ -113,10 +120,12 @@ class PsxStep {
     PsxStP st = new_step(send, recv, label, true, data_pass, prev.get());
     if (prev) c2(*prev);
     if (push_ && push_->gvc.defined()) c3(*push_);
+    ht.mark(2);
     set_loc(*st, finish_job(), offset, val);
     const bool early = nkeys.has_value() && nkeys->defined();
     if (early) begin(*nkeys, *noffset, nval, st, ready, true);
     c1(*st);
+    ht.mark(3);
     if (prev) {
       reply(*prev);
       if (tau_ == 0 && prev->train) {
@@ -124,17 +133,22 @@ class PsxStep {
         owner_push(*prev);
       }
     }
+    ht.mark(4);
     if (push_) {
       owner_push(*push_);
       push_.reset();
     }
+    ht.mark(5);
     open(*st, true);
     pull_ = st;
+    ht.mark(6);
     if (early) exchange_deferred();
+    ht.mark(7);
     if (tau_ == 1 && prev && prev->train) {
       grad(*prev, false);  // C3 goes out behind the next call's C2
       push_ = prev;
     }
+    ht.mark(8);
     ++step_;
     return py::make_tuple(true, fwd_mb_, last_u_, last_v_);
   }
@@ -648,6 +662,7 @@ class PsxStep {
   bool job_deferred_ = false;
   int64_t uhint_ = 0, step_ = 0, requests_ = 0, fwd_mb_ = 0, last_u_ = 0, last_v_ = 0;
   int64_t wire_[4] = {0, 0, 0, 0};
+  std::unique_ptr<HostSplit> timing_{host_split("psx native step")};
   // guard
   hipEvent_t gev_[2] = {};
   int gk_ = 0;

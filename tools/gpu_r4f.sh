@@ -14,4 +14,7 @@ for i in 1 2 3; do
   echo "lin_rccl_native $(b --loopback 8 --loopback-rccl --model linear)"
   echo "lin_rccl_python $(WH_PSX_NATIVE=0 b --loopback 8 --loopback-rccl --model linear)"
 done | tee $OUT/ab.txt
+WH_STEP_TIMING=1 $T 300 python bench.py --loopback 8 --model linear > $OUT/lin_timing.log 2>&1 || exit $?
+WH_STEP_TIMING=1 $T 300 python bench.py --loopback 8 > $OUT/dif_timing.log 2>&1 || exit $?
+grep "host us" $OUT/lin_timing.log $OUT/dif_timing.log | tail -4
 echo all done
