@@ -85,6 +85,7 @@ class PsxStep {
   }
 
   ~PsxStep() {
+    if (timing_) timing_->print();
     job_.reset();
     (void)hipDeviceSynchronize();
     for (auto& e : ring_) (void)hipEventDestroy(e);
@@ -260,7 +261,7 @@ class PsxStep {
     c10d::AllToAllOptions opts;
     opts.asyncOp = false;
     auto w = pg_->alltoall_base(r, s, none, none, opts);
-    w->wait();
+    if (w) w->wait();  // (a blocking collective may return no work handle)
     return r;
   }
 
@@ -686,6 +687,6 @@ Tensor c10d_a2a_rows(py::object pg, const Tensor& x, const std::vector<int64_t>&
   for (int64_t r : recv_rows) rs.push_back(r * width);
   for (int64_t r : send_rows) ss.push_back(r * width);
   auto w = g->alltoall_base(of, xf, rs, ss);
-  w->wait();
+  if (w) w->wait();
   return out;
 }
