@@ -1281,7 +1281,12 @@ AucSide* auc_side(c10::DeviceIndex d, bool create) {
   auto it = m.find(d);
   if (it != m.end()) return it->second;
   if (!create) return nullptr;
-  auto* a = new AucSide{c10::hip::getStreamFromPool(false, d), nullptr, nullptr};
+  // a stream of its own: the pool's round-robin streams are shared (RCCL's
+  // internal stream comes from the same pool), and AUC kernels queued on a
+  // collective's stream would wait for it
+  hipStream_t h = nullptr;
+  WH_HIP_CHECK_HOST(hipStreamCreateWithFlags(&h, hipStreamNonBlocking));
+  auto* a = new AucSide{c10::hip::getStreamFromExternal(h, d), nullptr, nullptr};
   WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->in, hipEventDisableTiming));
   WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->out, hipEventDisableTiming));
   m[d] = a;
@@ -2731,7 +2736,9 @@ class LinearStep {
                                     std::string(std::getenv("WH_LINEAR_STEP")) == "localize");
     dev_ = store->slots_.device().index();
     c10::DeviceGuard g(store->slots_.device());
-    ls_ = c10::hip::getStreamFromPool(false, dev_);
+    hipStream_t h = nullptr;  // (own stream, not the shared pool)
+    WH_HIP_CHECK_HOST(hipStreamCreateWithFlags(&h, hipStreamNonBlocking));
+    ls_ = c10::hip::getStreamFromExternal(h, dev_);
     WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_s_, hipEventDisableTiming));
     WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_ls_, hipEventDisableTiming));
   }

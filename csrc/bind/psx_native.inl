@@ -71,9 +71,15 @@ class PsxStep {
                 "PsxStep: the process group must have P ranks (or 1: loopback-rccl)");
     dev_ = store->slots_.device().index();
     c10::DeviceGuard g(store->slots_.device());
-    ls_ = c10::hip::getStreamFromPool(false, dev_);
-    cs_ = c10::hip::getStreamFromPool(false, dev_);
-    xs_ = c10::hip::getStreamFromPool(false, dev_);
+    // streams of our own (as Python's torch.cuda.Stream()): the pool's
+    // round-robin streams are shared with RCCL's internal stream and other
+    // users, and a localize queued behind a collective on a shared stream
+    // serialises the step
+    for (hipStream_t* h : {&ls_h_, &cs_h_, &xs_h_})
+      WH_HIP_CHECK_HOST(hipStreamCreateWithFlags(h, hipStreamNonBlocking));
+    ls_ = c10::hip::getStreamFromExternal(ls_h_, dev_);
+    cs_ = c10::hip::getStreamFromExternal(cs_h_, dev_);
+    xs_ = c10::hip::getStreamFromExternal(xs_h_, dev_);
     for (auto& e : ring_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : gev_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (pg_) wh::fm_set_cu_reserve((int)cu_reserve);
@@ -91,6 +97,8 @@ class PsxStep {
     for (auto& e : ring_) (void)hipEventDestroy(e);
     for (auto& e : gev_) (void)hipEventDestroy(e);
     for (auto& e : pin_ev_) (void)hipEventDestroy(e);
+    for (hipStream_t h : {ls_h_, cs_h_, xs_h_})
+      if (h) (void)hipStreamDestroy(h);
   }
 
   // One training minibatch (Psx.train). Returns (has_data, minibatches
@@ -651,6 +659,7 @@ class PsxStep {
   c10::hip::HIPStream ls_ = c10::hip::getDefaultHIPStream();
   c10::hip::HIPStream cs_ = c10::hip::getDefaultHIPStream();
   c10::hip::HIPStream xs_ = c10::hip::getDefaultHIPStream();
+  hipStream_t ls_h_ = nullptr, cs_h_ = nullptr, xs_h_ = nullptr;
   hipEvent_t ring_[kRing] = {};
   int ring_i_ = 0;
   Tensor pins_[kPins];
