@@ -1274,6 +1274,7 @@ void auc_acc(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
 struct AucSide {
   c10::hip::HIPStream s;
   hipEvent_t in, out;
+  c10::hip::HIPStream own;  // the stream created here (s unless lent)
 };
 
 AucSide* auc_side(c10::DeviceIndex d, bool create) {
@@ -1286,11 +1287,27 @@ AucSide* auc_side(c10::DeviceIndex d, bool create) {
   // collective's stream would wait for it
   hipStream_t h = nullptr;
   WH_HIP_CHECK_HOST(hipStreamCreateWithFlags(&h, hipStreamNonBlocking));
-  auto* a = new AucSide{c10::hip::getStreamFromExternal(h, d), nullptr, nullptr};
+  auto st = c10::hip::getStreamFromExternal(h, d);
+  auto* a = new AucSide{st, nullptr, nullptr, st};
   WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->in, hipEventDisableTiming));
   WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->out, hipEventDisableTiming));
   m[d] = a;
   return a;
+}
+
+// Run the device's AUC side work on a stream of the caller's (the native
+// multi-shard step lends its count stream, idle when the AUC is enqueued:
+// one stream fewer competing for the GPU_MAX_HW_QUEUES=4 hardware queues; a
+// side stream that lands on the compute stream's queue serialises the AUC
+// with the next step's forward), or back on its own (lend = nullptr). The
+// old stream's work is ordered before the new one's.
+void auc_side_lend(c10::DeviceIndex d, hipStream_t lend) {
+  AucSide* a = auc_side(d, true);
+  auto next = lend ? c10::hip::getStreamFromExternal(lend, d) : a->own;
+  if (next.stream() == a->s.stream()) return;
+  WH_HIP_CHECK_HOST(hipEventRecord(a->out, a->s.stream()));
+  WH_HIP_CHECK_HOST(hipStreamWaitEvent(next.stream(), a->out, 0));
+  a->s = next;
 }
 
 void auc_acc_side(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {

@@ -23,9 +23,20 @@ namespace {
 struct PsxWork {  // an issued collective and the tensors it reads
   c10::intrusive_ptr<c10d::Work> w;
   Tensor keep;
+  hipEvent_t ev = nullptr;  // end of an on-stream transfer (recorded by a2a)
+  bool pending = false;
+  PsxWork() = default;
+  PsxWork(const PsxWork&) = delete;
+  PsxWork& operator=(const PsxWork&) = delete;
+  ~PsxWork() {
+    if (ev) (void)hipEventDestroy(ev);
+  }
   void wait() {
     if (w) w->wait();  // the current stream waits for the transfer
+    if (pending)
+      WH_HIP_CHECK_HOST(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), ev, 0));
     w.reset();
+    pending = false;
     keep = Tensor();
   }
 };
@@ -83,6 +94,7 @@ class PsxStep {
     for (auto& e : ring_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : gev_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (pg_) wh::fm_set_cu_reserve((int)cu_reserve);
+    if (!linear_ && lend_auc_) auc_side_lend(dev_, cs_h_);
     const int64_t dflt = std::max<int64_t>(4 * (P + 1) + P, 64);
     for (int i = 0; i < kPins; ++i) {
       pins_[i] = torch::empty({dflt}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
@@ -93,6 +105,10 @@ class PsxStep {
   ~PsxStep() {
     if (timing_) timing_->print();
     job_.reset();
+    if (!linear_ && lend_auc_) {
+      c10::DeviceGuard g(c10::Device(c10::kCUDA, dev_));
+      auc_side_lend(dev_, nullptr);
+    }
     (void)hipDeviceSynchronize();
     for (auto& e : ring_) (void)hipEventDestroy(e);
     for (auto& e : gev_) (void)hipEventDestroy(e);
@@ -228,6 +244,7 @@ class PsxStep {
     for (int64_t d = 1; d < x.dim(); ++d) row *= x.size(d);
     wire_[c] += row * (vsum(send_rows) - send_rows[rank_]);
     work->w.reset();
+    work->pending = false;
     if (!pg_) return x;  // loopback identity
     Tensor xc = x.contiguous();
     int64_t width = 1;
@@ -251,7 +268,22 @@ class PsxStep {
     } else if (xc.numel() == 0) {  // (1-rank loopback-rccl: nothing to copy)
       return out;
     }
-    work->w = pg_->alltoall_base(of, xf, rs, ss);
+    if (a2a_async_) {
+      work->w = pg_->alltoall_base(of, xf, rs, ss);
+    } else {
+      // on the issuing stream (xs, or S for C1) rather than RCCL's internal
+      // stream: that stream is created lazily and lands on whichever of the
+      // GPU_MAX_HW_QUEUES=4 hardware queues is next -- measured on the
+      // compute stream's queue, where every transfer then waited behind the
+      // forward / backward kernels (and they behind its barrier packets)
+      c10d::AllToAllOptions opts;
+      opts.asyncOp = false;
+      auto w = pg_->alltoall_base(of, xf, rs, ss, opts);
+      if (w) w->wait();
+      if (!work->ev) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&work->ev, hipEventDisableTiming));
+      WH_HIP_CHECK_HOST(hipEventRecord(work->ev, xs.stream()));
+      work->pending = true;
+    }
     work->keep = xc;
     return out;
   }
@@ -673,6 +705,16 @@ class PsxStep {
   int64_t uhint_ = 0, step_ = 0, requests_ = 0, fwd_mb_ = 0, last_u_ = 0, last_v_ = 0;
   int64_t wire_[4] = {0, 0, 0, 0};
   std::unique_ptr<HostSplit> timing_{host_split("psx native step")};
+  // WH_PSX_AUC_OWN=1: the AUC on its own side stream, not on cs
+  const bool lend_auc_ = [] {
+    const char* e = std::getenv("WH_PSX_AUC_OWN");
+    return !(e && std::string(e) == "1");
+  }();
+  // WH_PSX_A2A=async: C1..C3 on RCCL's internal stream (c10d's async path)
+  const bool a2a_async_ = [] {
+    const char* e = std::getenv("WH_PSX_A2A");
+    return e && std::string(e) == "async";
+  }();
   // guard
   hipEvent_t gev_[2] = {};
   int gk_ = 0;
