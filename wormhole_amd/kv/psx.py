@@ -692,13 +692,20 @@ class Psx:
         a GPU rank over RCCL, the loopback identity or the 1-rank RCCL
         loopback; no payload filter, collective timer, key modulo or
         embedding-gradient post-processing (those stay on this Python
-        step). ``WH_PSX_NATIVE=0`` keeps the Python step."""
+        step). ``WH_PSX_NATIVE=0`` keeps the Python step, ``=1`` forces the
+        native one; by default DiFacto over RCCL keeps the Python step: on the
+        1-rank RCCL loopback rehearsal it measured 103-109 M ex/s against the
+        native step's 98 (profiles/r4l_hwq_ab.txt; the linear step is 1.4x
+        faster native, the identity loopback on par)."""
         if self._nat is None:
             lrn, emb = self.lrn, self.lrn.emb
             post = emb is not None and (emb.grad_clipping > 0 or emb.dropout > 0 or
                                         bool(emb.grad_normalization))
             backend = getattr(self.comm, "backend", "")
-            ok = (self.cuda and os.environ.get("WH_PSX_NATIVE", "1") != "0" and
+            want = os.environ.get("WH_PSX_NATIVE", "")
+            if not want:
+                want = "0" if (not self.linear and backend in ("nccl", "loopback-rccl")) else "1"
+            ok = (self.cuda and want != "0" and
                   backend in ("nccl", "loopback", "loopback-rccl") and
                   not getattr(self.comm, "stage", False) and self.qf is None and
                   self.timer is None and not lrn.max_key and not post)
