@@ -10,7 +10,9 @@
 
 #include <dirent.h>
 #include <regex.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cctype>
@@ -117,10 +119,26 @@ InputSplit::InputSplit(const std::string& path, int part, int nparts, bool recor
   int64_t e = std::min<int64_t>(size, nstep * (part + 1));
   begin_ = Align(b, size);
   end_ = Align(e, size);
+  if (recordio_ && end_ > begin_) {
+    // CRB parts are read through a mapping: a record is decoded straight
+    // from the page cache by whichever reader thread takes it (a stdio read
+    // per record under the readers' lock copied every byte once more, on
+    // one thread: ~20 M Criteo rows/s, below the text path)
+    const int64_t pg = (int64_t)sysconf(_SC_PAGESIZE);
+    map_off_ = begin_ / pg * pg;
+    map_len_ = (size_t)(end_ - map_off_);
+    void* m = mmap(nullptr, map_len_, PROT_READ, MAP_SHARED, fileno(fp_), map_off_);
+    if (m != MAP_FAILED) {
+      map_ = static_cast<const char*>(m);
+      madvise(m, map_len_, MADV_SEQUENTIAL);
+      madvise(m, map_len_, MADV_WILLNEED);
+    }
+  }
   BeforeFirst();
 }
 
 InputSplit::~InputSplit() {
+  if (map_) munmap(const_cast<char*>(map_), map_len_);
   if (fp_) std::fclose(fp_);
 }
 
@@ -199,9 +217,63 @@ bool InputSplit::NextChunk(std::string* out, size_t hint) {
   return !out->empty() || pos_ < end_;
 }
 
+bool InputSplit::NextRecordView(const char** data, size_t* size, std::string* spill) {
+  if (!recordio_) throw std::runtime_error("NextRecordView on a text split");
+  if (!map_) {
+    if (!NextRecord(spill)) return false;
+    *data = spill->data();
+    *size = spill->size();
+    return true;
+  }
+  spill->clear();
+  bool joined = false;
+  while (true) {
+    if (pos_ >= end_ || pos_ + 8 > end_) return false;
+    const char* h = map_ + (pos_ - map_off_);
+    uint32_t hdr[2];
+    std::memcpy(hdr, h, 8);
+    WH_CHECK(hdr[0] == kRecordIOMagic, "invalid recordio stream in " + path_);
+    const uint32_t cflag = hdr[1] >> 29, len = hdr[1] & ((1u << 29) - 1);
+    const uint32_t padded = (len + 3u) & ~3u;
+    if (pos_ + 8 + (int64_t)padded > end_)
+      throw std::runtime_error("truncated recordio record in " + path_);
+    const char* body = h + 8;
+    pos_ += 8 + padded;
+    if (cflag == 0) {
+      *data = body;
+      *size = len;
+      return true;
+    }
+    if (cflag == 1) {
+      spill->assign(body, len);
+      joined = true;
+      continue;
+    }
+    // 2 = middle, 3 = end: the writer split at an embedded magic word
+    WH_CHECK(joined, "recordio continuation without a start in " + path_);
+    const uint32_t m = kRecordIOMagic;
+    spill->append(reinterpret_cast<const char*>(&m), 4);
+    spill->append(body, len);
+    if (cflag == 3) {
+      *data = spill->data();
+      *size = spill->size();
+      return true;
+    }
+  }
+}
+
 bool InputSplit::NextRecord(std::string* out) {
   out->clear();
   if (!recordio_) throw std::runtime_error("NextRecord on a text split");
+  if (map_) {
+    std::string spill;
+    const char* p;
+    size_t n;
+    if (!NextRecordView(&p, &n, &spill)) return false;
+    if (p == spill.data()) out->swap(spill);
+    else out->assign(p, n);
+    return true;
+  }
   while (true) {
     if (pos_ >= end_) return false;
     uint32_t hdr[2];

@@ -28,6 +28,11 @@ class InputSplit {
   bool NextChunk(std::string* out, size_t hint = 4 << 20);
   // recordio: next (re-assembled) record
   bool NextRecord(std::string* out);
+  // recordio, zero-copy: the next record as a view into the part's memory
+  // mapping (valid while this split lives); a record the writer split at
+  // embedded magic words is re-assembled into *spill and the view points
+  // there. Callers serialise the calls; the views can be read concurrently.
+  bool NextRecordView(const char** data, size_t* size, std::string* spill);
   int64_t begin() const { return begin_; }
   int64_t end() const { return end_; }
   int64_t bytes_read() const { return pos_ - begin_; }
@@ -39,6 +44,11 @@ class InputSplit {
   std::FILE* fp_ = nullptr;
   int64_t begin_ = 0, end_ = 0, pos_ = 0;
   std::string carry_;
+  // recordio parts are memory-mapped (map_ = file bytes [map_off_,
+  // map_off_ + map_len_) covering [begin_, end_)); null: stdio reads
+  const char* map_ = nullptr;
+  int64_t map_off_ = 0;
+  size_t map_len_ = 0;
 };
 
 class RecordIOWriter {

@@ -96,7 +96,37 @@ int LZ4Decompress(const char* src, char* dst, int csize, int cap) {
   const unsigned char* const iend = ip + csize;
   char* op = dst;
   char* const oend = dst + cap;
+  // Fast path for the common short sequence (literal and match lengths both
+  // in the token, offset >= 8, far from either end): fixed-size copies and
+  // no bound checks beyond the margins; anything else takes the generic
+  // path, one sequence at a time. CRB index sections of hashed keys are ~one
+  // such sequence per 8-byte key, so the per-sequence overhead is the
+  // decoder's speed (the generic path alone ran at ~1.1 GB/s on them).
+  // Margins: 16 literal bytes + 2 offset bytes readable (so this is never
+  // the last sequence), and 16 + 18 bytes writable.
+  const unsigned char* const ifast = csize > 18 ? iend - 18 : ip;
+  char* const ofast = cap > 34 ? oend - 34 : dst;
   while (ip < iend) {
+    if (ip < ifast && op < ofast) {
+      const unsigned t = *ip;
+      const size_t lit = t >> 4, ml = t & 15;
+      if (lit != 15 && ml != 15) {
+        std::memcpy(op, ip + 1, 16);
+        const unsigned char* q = ip + 1 + lit;
+        const size_t off = (size_t)q[0] | ((size_t)q[1] << 8);
+        char* const o2 = op + lit;
+        if (off >= 8 && off <= (size_t)(o2 - dst)) {
+          const char* m = o2 - off;
+          std::memcpy(o2, m, 8);  // off >= 8: each 8-byte source chunk is final
+          std::memcpy(o2 + 8, m + 8, 8);
+          std::memcpy(o2 + 16, m + 16, 2);
+          op = o2 + ml + kMinMatch;
+          ip = q + 2;
+          continue;
+        }
+        // (short offset or a bad one: the generic path below redoes it)
+      }
+    }
     const unsigned token = *ip++;
     size_t lit = token >> 4;
     if (lit == 15) {

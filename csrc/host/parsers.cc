@@ -298,9 +298,14 @@ void ThreadedReader::Work() {
       std::string buf;
       int64_t seq;
       bool ok;
+      const bool crb = reader_.fmt() == "crb";
+      const char* rec = nullptr;
+      size_t rec_n = 0;
       {
         std::lock_guard<std::mutex> io(io_mu_);
-        ok = reader_.NextRaw(&buf);
+        // crb: only the record's header is read under the lock; the body
+        // is decoded from the mapping by this thread, in parallel
+        ok = crb ? reader_.NextRecordView(&rec, &rec_n, &buf) : reader_.NextRaw(&buf);
         std::lock_guard<std::mutex> lk(mu_);
         seq = next_read_;
         if (ok) {
@@ -314,7 +319,16 @@ void ThreadedReader::Work() {
         return;
       }
       RowBlock b;
-      BlockReader::ParseRaw(reader_.fmt(), buf, &b);
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!spare_.empty()) {
+          b = std::move(spare_.back());
+          spare_.pop_back();
+        }
+      }
+      b.clear();  // (keeps the recycled capacity)
+      if (crb) CRBDecode(rec, rec_n, &b);
+      else BlockReader::ParseRaw(reader_.fmt(), buf, &b);
       {
         std::lock_guard<std::mutex> lk(mu_);
         ready_.emplace(seq, std::move(b));
@@ -339,7 +353,8 @@ bool ThreadedReader::Next(RowBlock* out) {
     if (!err_.empty()) throw std::runtime_error(err_);
     auto it = ready_.find(next_out_);
     if (it == ready_.end()) return false;  // all chunks consumed
-    *out = std::move(it->second);
+    std::swap(*out, it->second);
+    if (it->second.index.capacity() && spare_.size() < window_) spare_.push_back(std::move(it->second));
     ready_.erase(it);
     ++next_out_;
     cv_.notify_all();

@@ -27,6 +27,11 @@ class BlockReader {
   bool Next(RowBlock* blk);
   // I/O only: the next raw chunk (text: whole lines; crb: one record)
   bool NextRaw(std::string* buf);
+  // crb: the next record as a view into the split's mapping (see
+  // InputSplit::NextRecordView)
+  bool NextRecordView(const char** data, size_t* size, std::string* spill) {
+    return split_->NextRecordView(data, size, spill);
+  }
   // CPU only: parse a raw chunk of format fmt
   static void ParseRaw(const std::string& fmt, const std::string& buf, RowBlock* blk);
   const std::string& fmt() const { return fmt_; }
@@ -46,6 +51,7 @@ class ThreadedReader {
   ThreadedReader(const std::string& path, int part, int nparts, const std::string& fmt,
                  int nthreads = 0, size_t depth = 4);
   ~ThreadedReader();
+  // the next block in read order; *out's previous buffers are recycled
   bool Next(RowBlock* out);
   static int DefaultThreads();
 
@@ -57,6 +63,11 @@ class ThreadedReader {
   std::condition_variable cv_;
   int64_t next_read_ = 0, next_out_ = 0, total_ = -1;  // total_: chunks once EOF is seen
   std::map<int64_t, RowBlock> ready_;
+  // blocks handed back by Next (the consumer's previous one): their buffers
+  // are reused by the decoders -- fresh multi-MB vectors per record were
+  // mmap / munmap pairs, and the munmaps' TLB shootdowns across the decoder
+  // threads made 8 threads slower than 2 until malloc's threshold adapted
+  std::vector<RowBlock> spare_;
   bool stop_ = false;
   std::string err_;
   std::vector<std::thread> th_;

@@ -307,7 +307,18 @@ class PyBlockIter {
       bool any_v = false, any_w = false;
       while (have < rows_) {
         if (!cur_ || cur_pos_ == (int64_t)cur_->size()) {
-          auto b = std::make_shared<RowBlock>();
+          // a block no piece holds any more goes back to the reader (its
+          // buffers are recycled by the decoders)
+          std::shared_ptr<RowBlock> b;
+          for (auto& q : pool_)
+            if (q.use_count() == 1 && q != cur_) {
+              b = q;
+              break;
+            }
+          if (!b) {
+            b = std::make_shared<RowBlock>();
+            if (pool_.size() < 8) pool_.push_back(b);
+          }
           if (!reader_.Next(b.get())) {
             cur_.reset();
             break;
@@ -389,6 +400,7 @@ class PyBlockIter {
   int ncopy_;
   std::shared_ptr<RowBlock> cur_;
   int64_t cur_pos_ = 0;
+  std::vector<std::shared_ptr<RowBlock>> pool_;
 };
 
 py::tuple localize_cpu(const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,

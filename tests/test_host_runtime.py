@@ -368,3 +368,25 @@ def test_parallel_parser_is_ordered(tmp_path, monkeypatch):
             assert same(u, v)
     for u, v in zip(outs[1][0], outs[3][0]):
         assert same(u, v)
+
+
+@pytest.mark.parametrize("period", [1, 2, 3, 5, 7, 8, 9, 12, 15, 16, 17, 24, 40])
+def test_lz4_roundtrip_repeats(host, period):
+    """Short-offset matches and the decoder's fast loop: periodic runs of
+    every offset class, and CRB-like index sections (8-byte hashed keys
+    drawn with repeats, one short sequence per key)."""
+    rng = np.random.default_rng(period)
+    unit = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+    runs = []
+    for i in range(60):
+        runs.append(unit * int(rng.integers(1, 40)))
+        runs.append(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes())
+    for d in (b"".join(runs), (unit * 5000)[:31337]):
+        c = host.lz4_compress(d)
+        assert host.lz4_decompress(c, len(d)) == d
+    keys = rng.integers(0, 2**63, 64 + period * 10, dtype=np.int64)
+    pick = np.minimum(rng.pareto(1.1, 50000) * 3, keys.size - 1).astype(np.int64)
+    d = keys[pick].tobytes()
+    c = host.lz4_compress(d)
+    assert len(c) < len(d)
+    assert host.lz4_decompress(c, len(d)) == d
