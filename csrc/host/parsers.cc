@@ -220,6 +220,73 @@ void CRBDecode(const char* data, size_t size, RowBlock* blk) {
   if (!section(blk->weight.data(), nrows * sizeof(float))) blk->weight.clear();
 }
 
+void CRBLocate(const char* data, size_t size, CRBRecord* r) {
+  if (data != r->spill.data()) {
+    r->view = data;
+  }
+  size_t cur = 0;
+  auto get_int = [&]() {
+    WH_CHECK(cur + 4 <= size, "truncated crb record");
+    int v;
+    std::memcpy(&v, data + cur, 4);
+    cur += 4;
+    return v;
+  };
+  WH_CHECK(get_int() == kCRBMagic, "wrong data format (not a CRB record)");
+  r->isz = get_int();
+  WH_CHECK(r->isz == 8 || r->isz == 4, "unsupported crb index width");
+  r->nrows = get_int();
+  WH_CHECK(r->nrows >= 0, "bad crb row count");
+  for (int s = 0; s < 5; ++s) {
+    r->csz[s] = get_int();
+    r->at[s] = cur;
+    if (r->csz[s] > 0) {
+      WH_CHECK(cur + r->csz[s] <= size, "truncated crb section");
+      cur += r->csz[s];
+    }
+  }
+  r->off.clear();
+}
+
+void CRBDecodeOffsets(CRBRecord* r) {
+  const int n = r->nrows;
+  std::vector<size_t> o(n + 1, 0);
+  if (r->csz[1] > 0) {
+    const int got = LZ4Decompress(r->base() + r->at[1], (char*)o.data(), r->csz[1],
+                                  (int)((n + 1) * sizeof(size_t)));
+    WH_CHECK(got == (int)((n + 1) * sizeof(size_t)), "crb section size mismatch");
+  }
+  r->off.resize(n + 1);
+  for (int i = 0; i <= n; ++i) r->off[i] = (int64_t)(o[i] - o[0]);
+}
+
+bool CRBDecodeRows(const CRBRecord& r, int sec, int64_t r0, int64_t r1, void* dst,
+                   std::vector<char>* tmp) {
+  if (r.csz[sec] <= 0) return false;
+  const bool per_nnz = sec == 2 || sec == 3;
+  const int64_t total = per_nnz ? r.nnz() : r.nrows;
+  const int64_t a = per_nnz ? r.off[r0] : r0, b = per_nnz ? r.off[r1] : r1;
+  const int esz = sec == 2 ? r.isz : 4;
+  const int bytes = (int)(total * esz);
+  const char* src = r.base() + r.at[sec];
+  if (a == 0 && b == total && !(sec == 2 && esz == 4)) {  // whole section, in place
+    WH_CHECK(LZ4Decompress(src, (char*)dst, r.csz[sec], bytes) == bytes,
+             "crb section size mismatch");
+    return true;
+  }
+  if (tmp->size() < (size_t)bytes + 64) tmp->resize((size_t)bytes + 64);
+  WH_CHECK(LZ4Decompress(src, tmp->data(), r.csz[sec], bytes) == bytes,
+           "crb section size mismatch");
+  if (sec == 2 && esz == 4) {
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(tmp->data());
+    uint64_t* d = static_cast<uint64_t*>(dst);
+    for (int64_t j = a; j < b; ++j) d[j - a] = s32[j];
+  } else {
+    std::memcpy(dst, tmp->data() + a * esz, (size_t)(b - a) * esz);
+  }
+  return true;
+}
+
 // --------------------------------------------------------------- parsing
 BlockReader::BlockReader(const std::string& path, int part, int nparts, const std::string& fmt)
     : fmt_(fmt) {

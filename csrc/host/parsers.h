@@ -20,6 +20,28 @@ void ParseAdfea(const char* p, const char* end, RowBlock* blk);
 std::string CRBEncode(const RowBlock& b);
 void CRBDecode(const char* data, size_t size, RowBlock* blk);
 
+// A CRB record with its sections located but not decoded, and its row
+// offsets decoded: the unit of the direct CRB reader (registry.cc
+// BlockIter), which decodes every section straight into its place in the
+// output block instead of into a RowBlock that is then copied.
+struct CRBRecord {
+  std::string spill;        // the bytes of a re-assembled record (else a view)
+  const char* view = nullptr;
+  size_t at[5] = {};        // label, offset, index, value, weight: byte offset
+  int csz[5] = {};          // compressed size (<= 0: absent)
+  int nrows = 0, isz = 8;
+  hvec<int64_t> off;        // nrows + 1 row offsets from 0 (CRBDecodeOffsets)
+  const char* base() const { return spill.empty() ? view : spill.data(); }
+  int64_t nnz() const { return off.back(); }
+};
+void CRBLocate(const char* data, size_t size, CRBRecord* r);
+void CRBDecodeOffsets(CRBRecord* r);
+// rows [r0, r1) of section sec (0 label, 2 index, 3 value, 4 weight) into
+// dst (index as uint64, the others float); false when the record has no
+// such section (dst untouched). tmp: scratch for partial ranges / widening.
+bool CRBDecodeRows(const CRBRecord& r, int sec, int64_t r0, int64_t r1, void* dst,
+                   std::vector<char>* tmp);
+
 // parse part k/n of a file chunk by chunk
 class BlockReader {
  public:

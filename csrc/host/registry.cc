@@ -5,6 +5,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -280,27 +281,171 @@ class PyMinibatchIter {
   bool pinned_;
 };
 
-// CSR blocks of `rows` rows straight from a ThreadedReader's decoded chunks
-// (CRB records or parsed text chunks, in file order) into (pinned) tensors,
-// for the device shuffle buffer (wormhole_amd/data/device_text.py). Each
-// chunk's row range is copied into its final slice by a pool of threads: ONE
-// copy per byte, in parallel. MinibatchIter assembled a RowBlock first and
-// then copied it into tensors, both on one thread -- the bound of CRB input
-// (two copies of ~330 MB per million Criteo rows).
+// CSR blocks of `rows` rows (file order) in (pinned) tensors, for the device
+// shuffle buffer (wormhole_amd/data/device_text.py): CRB records decoded
+// straight into the block (next_crb), other formats' parsed chunks copied
+// into it by a thread pool (next_blocks). MinibatchIter assembled a RowBlock
+// first and then copied it into tensors, both on one thread -- the round-2
+// bound of CRB input (two copies of ~330 MB per million Criteo rows).
 class PyBlockIter {
  public:
   PyBlockIter(const std::string& path, int part, int nparts, const std::string& fmt,
               int64_t rows, bool pinned, int nthreads)
-      : reader_(path, part, nparts, fmt, nthreads), rows_(std::max<int64_t>(rows, 1)),
-        pinned_(pinned), ncopy_(std::max(1, std::min(8, (int)std::thread::hardware_concurrency()))) {}
+      : rows_(std::max<int64_t>(rows, 1)), pinned_(pinned),
+        ncopy_(std::max(1, std::min(8, (int)std::thread::hardware_concurrency()))) {
+    if (fmt == "crb") {
+      split_.reset(new InputSplit(path, part, nparts, true));
+      ndec_ = nthreads > 0 ? nthreads : ThreadedReader::DefaultThreads();
+    } else {
+      reader_.reset(new ThreadedReader(path, part, nparts, fmt, nthreads));
+    }
+  }
 
-  py::object next() {
+  py::object next() { return split_ ? next_crb() : next_blocks(); }
+
+ private:
+  // pinned output tensors of a block (values / weights only when present)
+  struct Out {
+    Tensor k, o, l, v, w;
+  };
+  Out alloc(int64_t rows, int64_t nnz, bool any_v, bool any_w) {
+    auto opt = [&](torch::ScalarType dt) {
+      return torch::TensorOptions().dtype(dt).pinned_memory(pinned_);
+    };
+    Out out;
+    out.k = torch::empty({nnz}, opt(torch::kInt64));
+    out.o = torch::empty({rows + 1}, opt(torch::kInt64));
+    out.l = torch::empty({rows}, opt(torch::kFloat32));
+    if (any_v) out.v = torch::empty({nnz}, opt(torch::kFloat32));
+    if (any_w) out.w = torch::empty({rows}, opt(torch::kFloat32));
+    return out;
+  }
+  static py::object to_py(Out& out, bool binary) {
+    // every value 1: binary data (reference minibatch_iter.h:114-116)
+    if (binary) out.v = Tensor();
+    py::object val = out.v.defined() ? py::cast(out.v) : py::none();
+    py::object wt = out.w.defined() ? py::cast(out.w) : py::none();
+    return py::make_tuple(out.k, out.o, val, out.l, wt);
+  }
+  template <class F>
+  static void parallel(size_t n, int nthreads, F&& f) {
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+      for (size_t i = next++; i < n; i = next++) f(i);
+    };
+    const int nt = (int)std::min<size_t>((size_t)nthreads, n);
+    std::vector<std::thread> th;
+    std::exception_ptr err;
+    std::mutex em;
+    auto guarded = [&] {
+      try {
+        work();
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(em);
+        if (!err) err = std::current_exception();
+        next = n;
+      }
+    };
+    for (int t = 1; t < nt; ++t) th.emplace_back(guarded);
+    guarded();
+    for (auto& t : th) t.join();
+    if (err) std::rethrow_exception(err);
+  }
+
+  // CRB: records are located in the part's mapping, their row offsets
+  // decoded, and every section LZ4-decoded by a thread pool STRAIGHT into
+  // its slice of the (pinned) output block -- no RowBlock in between and no
+  // second copy (host memory traffic was the bound: ~1 GB per million
+  // Criteo rows through decode + copy, ~0.45 GB now). A record straddling
+  // two blocks is carried over (its sections decoded once per block, into
+  // scratch, for the rows each needs).
+  py::object next_crb() {
+    struct Piece {
+      std::shared_ptr<CRBRecord> r;
+      int64_t r0, r1, row_base, nnz_base;
+    };
+    std::vector<Piece> pieces;
+    Out out;
+    bool binary = false;
+    {
+      py::gil_scoped_release nogil;
+      int64_t have = 0;
+      std::vector<std::shared_ptr<CRBRecord>> fresh;
+      while (have < rows_) {
+        if (!carry_) {
+          auto r = std::make_shared<CRBRecord>();
+          const char* p;
+          size_t n;
+          if (!split_->NextRecordView(&p, &n, &r->spill)) break;
+          CRBLocate(p, n, r.get());
+          if (r->nrows == 0) continue;
+          carry_ = r;
+          carry_pos_ = 0;
+          fresh.push_back(r);
+        }
+        const int64_t take = std::min<int64_t>(rows_ - have, carry_->nrows - carry_pos_);
+        pieces.push_back({carry_, carry_pos_, carry_pos_ + take, have, 0});
+        carry_pos_ += take;
+        have += take;
+        if (carry_pos_ == carry_->nrows) carry_.reset();
+      }
+      if (pieces.empty()) {
+        py::gil_scoped_acquire g;
+        return py::none();
+      }
+      parallel(fresh.size(), ndec_, [&](size_t i) { CRBDecodeOffsets(fresh[i].get()); });
+      int64_t nnz = 0;
+      bool any_v = false, any_w = false;
+      for (auto& pc : pieces) {
+        pc.nnz_base = nnz;
+        nnz += pc.r->off[pc.r1] - pc.r->off[pc.r0];
+        any_v = any_v || pc.r->csz[3] > 0;
+        any_w = any_w || pc.r->csz[4] > 0;
+      }
+      out = alloc(have, nnz, any_v, any_w);
+      uint64_t* kp = reinterpret_cast<uint64_t*>(out.k.data_ptr());
+      int64_t* op = out.o.data_ptr<int64_t>();
+      float* lp = out.l.data_ptr<float>();
+      float* vp = any_v ? out.v.data_ptr<float>() : nullptr;
+      float* wp = any_w ? out.w.data_ptr<float>() : nullptr;
+      op[0] = 0;
+      std::atomic<bool> non_one{false};
+      parallel(pieces.size(), ndec_, [&](size_t i) {
+        thread_local std::vector<char> tmp;
+        const Piece& pc = pieces[i];
+        const CRBRecord& r = *pc.r;
+        const int64_t n = pc.r1 - pc.r0, s = r.off[pc.r0], e = r.off[pc.r1];
+        CRBDecodeRows(r, 2, pc.r0, pc.r1, kp + pc.nnz_base, &tmp);
+        if (!CRBDecodeRows(r, 0, pc.r0, pc.r1, lp + pc.row_base, &tmp))
+          std::fill(lp + pc.row_base, lp + pc.row_base + n, 0.f);
+        for (int64_t q = 0; q < n; ++q) op[pc.row_base + q + 1] = pc.nnz_base + (r.off[pc.r0 + q + 1] - s);
+        if (vp) {
+          float* v = vp + pc.nnz_base;
+          if (!CRBDecodeRows(r, 3, pc.r0, pc.r1, v, &tmp)) {
+            std::fill(v, v + (e - s), 1.f);
+          } else {
+            for (int64_t j = 0; j < e - s && !non_one.load(std::memory_order_relaxed); ++j)
+              if (v[j] != 1.f) non_one = true;
+          }
+        }
+        if (wp && !CRBDecodeRows(r, 4, pc.r0, pc.r1, wp + pc.row_base, &tmp))
+          std::fill(wp + pc.row_base, wp + pc.row_base + n, 1.f);
+      });
+      binary = vp && !non_one;
+    }
+    return to_py(out, binary);
+  }
+
+  // other formats: chunks parsed by a ThreadedReader into RowBlocks, whose
+  // row ranges a thread pool copies into their slices of the output
+  py::object next_blocks() {
     struct Piece {
       std::shared_ptr<RowBlock> b;
       int64_t r0, r1, row_base, nnz_base;
     };
     std::vector<Piece> pieces;
-    Tensor k, o, l, v, w;
+    Out out;
+    bool binary = false;
     {
       py::gil_scoped_release nogil;
       int64_t have = 0, nnz = 0;
@@ -308,10 +453,10 @@ class PyBlockIter {
       while (have < rows_) {
         if (!cur_ || cur_pos_ == (int64_t)cur_->size()) {
           // a block no piece holds any more goes back to the reader (its
-          // buffers are recycled by the decoders)
+          // buffers are recycled by the parsers)
           std::shared_ptr<RowBlock> b;
           for (auto& q : pool_)
-            if (q.use_count() == 1 && q != cur_) {
+            if (q.use_count() == 1) {
               b = q;
               break;
             }
@@ -319,7 +464,7 @@ class PyBlockIter {
             b = std::make_shared<RowBlock>();
             if (pool_.size() < 8) pool_.push_back(b);
           }
-          if (!reader_.Next(b.get())) {
+          if (!reader_->Next(b.get())) {
             cur_.reset();
             break;
           }
@@ -340,64 +485,50 @@ class PyBlockIter {
         py::gil_scoped_acquire g;
         return py::none();
       }
-      auto opt = [&](torch::ScalarType dt) {
-        return torch::TensorOptions().dtype(dt).pinned_memory(pinned_);
-      };
-      k = torch::empty({nnz}, opt(torch::kInt64));
-      o = torch::empty({have + 1}, opt(torch::kInt64));
-      l = torch::empty({have}, opt(torch::kFloat32));
-      if (any_v) v = torch::empty({nnz}, opt(torch::kFloat32));
-      if (any_w) w = torch::empty({have}, opt(torch::kFloat32));
-      uint64_t* kp = reinterpret_cast<uint64_t*>(k.data_ptr());
-      int64_t* op = o.data_ptr<int64_t>();
-      float* lp = l.data_ptr<float>();
-      float* vp = any_v ? v.data_ptr<float>() : nullptr;
-      float* wp = any_w ? w.data_ptr<float>() : nullptr;
+      out = alloc(have, nnz, any_v, any_w);
+      uint64_t* kp = reinterpret_cast<uint64_t*>(out.k.data_ptr());
+      int64_t* op = out.o.data_ptr<int64_t>();
+      float* lp = out.l.data_ptr<float>();
+      float* vp = any_v ? out.v.data_ptr<float>() : nullptr;
+      float* wp = any_w ? out.w.data_ptr<float>() : nullptr;
       op[0] = 0;
-      std::atomic<size_t> next{0};
       std::atomic<bool> non_one{false};
-      auto work = [&] {
-        for (size_t i = next++; i < pieces.size(); i = next++) {
-          const Piece& pc = pieces[i];
-          const RowBlock& b = *pc.b;
-          const int64_t s = b.offset[pc.r0], e = b.offset[pc.r1], n = pc.r1 - pc.r0;
-          std::memcpy(kp + pc.nnz_base, b.index.data() + s, (e - s) * sizeof(uint64_t));
-          std::memcpy(lp + pc.row_base, b.label.data() + pc.r0, n * sizeof(float));
-          for (int64_t r = 0; r < n; ++r)
-            op[pc.row_base + r + 1] = pc.nnz_base + (b.offset[pc.r0 + r + 1] - s);
-          if (vp) {
-            if (b.value.empty()) {
-              std::fill(vp + pc.nnz_base, vp + pc.nnz_base + (e - s), 1.f);
-            } else {
-              std::memcpy(vp + pc.nnz_base, b.value.data() + s, (e - s) * sizeof(float));
-              for (int64_t j = s; j < e && !non_one.load(std::memory_order_relaxed); ++j)
-                if (b.value[j] != 1.f) non_one = true;
-            }
-          }
-          if (wp) {
-            if (b.weight.empty()) std::fill(wp + pc.row_base, wp + pc.row_base + n, 1.f);
-            else std::memcpy(wp + pc.row_base, b.weight.data() + pc.r0, n * sizeof(float));
+      parallel(pieces.size(), ncopy_, [&](size_t i) {
+        const Piece& pc = pieces[i];
+        const RowBlock& b = *pc.b;
+        const int64_t s = b.offset[pc.r0], e = b.offset[pc.r1], n = pc.r1 - pc.r0;
+        std::memcpy(kp + pc.nnz_base, b.index.data() + s, (e - s) * sizeof(uint64_t));
+        std::memcpy(lp + pc.row_base, b.label.data() + pc.r0, n * sizeof(float));
+        for (int64_t r = 0; r < n; ++r)
+          op[pc.row_base + r + 1] = pc.nnz_base + (b.offset[pc.r0 + r + 1] - s);
+        if (vp) {
+          if (b.value.empty()) {
+            std::fill(vp + pc.nnz_base, vp + pc.nnz_base + (e - s), 1.f);
+          } else {
+            std::memcpy(vp + pc.nnz_base, b.value.data() + s, (e - s) * sizeof(float));
+            for (int64_t j = s; j < e && !non_one.load(std::memory_order_relaxed); ++j)
+              if (b.value[j] != 1.f) non_one = true;
           }
         }
-      };
-      const int nt = (int)std::min<size_t>((size_t)ncopy_, pieces.size());
-      std::vector<std::thread> th;
-      for (int t = 1; t < nt; ++t) th.emplace_back(work);
-      work();
-      for (auto& t : th) t.join();
-      // every value 1: binary data (reference minibatch_iter.h:114-116)
-      if (vp && !non_one) v = Tensor();
+        if (wp) {
+          if (b.weight.empty()) std::fill(wp + pc.row_base, wp + pc.row_base + n, 1.f);
+          else std::memcpy(wp + pc.row_base, b.weight.data() + pc.r0, n * sizeof(float));
+        }
+      });
+      binary = vp && !non_one;
     }
-    py::object val = v.defined() ? py::cast(v) : py::none();
-    py::object wt = w.defined() ? py::cast(w) : py::none();
-    return py::make_tuple(k, o, val, l, wt);
+    return to_py(out, binary);
   }
 
- private:
-  ThreadedReader reader_;
   int64_t rows_;
   bool pinned_;
-  int ncopy_;
+  int ncopy_, ndec_ = 1;
+  // CRB
+  std::unique_ptr<InputSplit> split_;
+  std::shared_ptr<CRBRecord> carry_;
+  int64_t carry_pos_ = 0;
+  // other formats
+  std::unique_ptr<ThreadedReader> reader_;
   std::shared_ptr<RowBlock> cur_;
   int64_t cur_pos_ = 0;
   std::vector<std::shared_ptr<RowBlock>> pool_;

@@ -208,9 +208,11 @@ def test_crb_file_split_via_minibatch_iter(host, tmp_path):
 @pytest.mark.parametrize("with_val", [False, True])
 @pytest.mark.parametrize("rows", [777, 2000, 100000])
 def test_block_iter_matches_minibatch_iter(host, tmp_path, with_val, rows):
-    """BlockIter (decoded chunks copied in parallel straight into the block
-    tensors) yields the same blocks as MinibatchIter without a shuffle buffer:
-    same rows in file order, same CSR, values dropped when all are 1."""
+    """BlockIter (CRB records decoded in parallel straight into the block
+    tensors; parsed text chunks copied into them) yields the same blocks as
+    MinibatchIter without a shuffle buffer: same rows in file order (records
+    straddling blocks split), same CSR, weights, values dropped when all are
+    1."""
     path = os.path.join(DATA, "agaricus.txt.train")
     keys, off, val, lab, _ = host.load_split(path, 0, 1, "libsvm")
     g = torch.Generator().manual_seed(3)
@@ -221,7 +223,8 @@ def test_block_iter_matches_minibatch_iter(host, tmp_path, with_val, rows):
         r1 = min(r0 + 1000, 6513)
         o = off[r0:r1 + 1] - off[r0]
         w.write(host.crb_encode(keys[off[r0]:off[r1]], o,
-                                v[off[r0]:off[r1]] if with_val else None, lab[r0:r1]))
+                                v[off[r0]:off[r1]] if with_val else None, lab[r0:r1],
+                                (lab[r0:r1] + 2.0) if with_val else None))
     w.close()
     for k in range(2):
         a = host.MinibatchIter(p, k, 2, "crb", rows)
