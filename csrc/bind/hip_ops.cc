@@ -20,6 +20,7 @@
 #include <cmath>
 #include <functional>
 #include <map>
+#include <mutex>
 #include <memory>
 #include <numeric>
 #include <tuple>
@@ -816,8 +817,15 @@ class KVStore {
     auto head = torch::empty({std::max<int64_t>(n, 1)}, keys.options().dtype(torch::kUInt8));
     // linear (vstride 0): the reply is w_out itself (returned in rbuf's place)
     auto rbuf = torch::empty({vstride_ > 0 ? rows_cap : 0, (int64_t)std::max(vstride_, 1)}, f32);
-    auto vcnt = torch::empty({P}, keys.options().dtype(torch::kInt64));
-    if (vstride_ == 0) vcnt.zero_();
+    // linear: no V rows, a cached all-zero vcnt (read only; no fill launch per open)
+    Tensor vcnt;
+    if (vstride_ == 0) {
+      if (!vcnt0_.defined() || vcnt0_.numel() != P || vcnt0_.device() != keys.device())
+        vcnt0_ = torch::zeros({P}, keys.options().dtype(torch::kInt64));
+      vcnt = vcnt0_;
+    } else {
+      vcnt = torch::empty({P}, keys.options().dtype(torch::kInt64));
+    }
     if (!vbase_.defined()) vbase_ = torch::empty({1}, vnext_.options());
     const bool ok = wh::ps_open(
         table(), rec ? nullptr : reinterpret_cast<const uint64_t*>(keys.data_ptr()),
@@ -963,7 +971,7 @@ class KVStore {
   int64_t cap() const { return cap_; }
   int64_t vcap() const { return vcap_; }
 
-  Tensor slots_, keys_, w_, z_, sq_, cnt_, vrow_, V_, VG_, vnext_, stats_, vbase_;
+  Tensor slots_, keys_, w_, z_, sq_, cnt_, vrow_, V_, VG_, vnext_, stats_, vbase_, vcnt0_;
   int64_t epoch_ = 0;  // ps_open chain-tag epoch (1..255)
   int64_t opens_ = 0;  // ps_open calls so far (tests: the epoch wrapped)
 
@@ -1271,6 +1279,21 @@ void auc_acc(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
 // stream first; auc_join makes the current stream wait for it): the Python
 // form of this (stream objects, wait_stream, a stream context) cost ~30 us
 // of host time per minibatch, which bounds small-minibatch training.
+// Streams of the native layer's own (not the c10 pool's round-robin streams,
+// one of which RCCL also takes for its internal stream): created once per
+// device and role and never destroyed -- the caching allocator records
+// events on every stream a block was used on when the block is freed, which
+// can be after the step object that used the stream is gone.
+enum OwnStream { kStreamLinearLs, kStreamPsxLs, kStreamPsxCs, kStreamPsxXs, kStreamAuc, kOwnStreams };
+hipStream_t own_stream(int dev, int role) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, hipStream_t> m;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& h = m[{dev, role}];
+  if (!h) WH_HIP_CHECK_HOST(hipStreamCreateWithFlags(&h, hipStreamNonBlocking));
+  return h;
+}
+
 struct AucSide {
   c10::hip::HIPStream s;
   hipEvent_t in, out;
@@ -1285,9 +1308,7 @@ AucSide* auc_side(c10::DeviceIndex d, bool create) {
   // a stream of its own: the pool's round-robin streams are shared (RCCL's
   // internal stream comes from the same pool), and AUC kernels queued on a
   // collective's stream would wait for it
-  hipStream_t h = nullptr;
-  WH_HIP_CHECK_HOST(hipStreamCreateWithFlags(&h, hipStreamNonBlocking));
-  auto st = c10::hip::getStreamFromExternal(h, d);
+  auto st = c10::hip::getStreamFromExternal(own_stream(d, kStreamAuc), d);
   auto* a = new AucSide{st, nullptr, nullptr, st};
   WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->in, hipEventDisableTiming));
   WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->out, hipEventDisableTiming));
@@ -2753,9 +2774,7 @@ class LinearStep {
                                     std::string(std::getenv("WH_LINEAR_STEP")) == "localize");
     dev_ = store->slots_.device().index();
     c10::DeviceGuard g(store->slots_.device());
-    hipStream_t h = nullptr;  // (own stream, not the shared pool)
-    WH_HIP_CHECK_HOST(hipStreamCreateWithFlags(&h, hipStreamNonBlocking));
-    ls_ = c10::hip::getStreamFromExternal(h, dev_);
+    ls_ = c10::hip::getStreamFromExternal(own_stream(dev_, kStreamLinearLs), dev_);
     WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_s_, hipEventDisableTiming));
     WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&ev_ls_, hipEventDisableTiming));
   }

@@ -86,15 +86,28 @@ class PsxStep {
     // round-robin streams are shared with RCCL's internal stream and other
     // users, and a localize queued behind a collective on a shared stream
     // serialises the step
-    for (hipStream_t* h : {&ls_h_, &cs_h_, &xs_h_})
-      WH_HIP_CHECK_HOST(hipStreamCreateWithFlags(h, hipStreamNonBlocking));
-    ls_ = c10::hip::getStreamFromExternal(ls_h_, dev_);
-    cs_ = c10::hip::getStreamFromExternal(cs_h_, dev_);
-    xs_ = c10::hip::getStreamFromExternal(xs_h_, dev_);
+    //
+    // One stream (WH_PSX_STREAMS=one, the linear step's default): every phase
+    // on the compute stream. At the linear step's 10 000 rows the step is
+    // bound by host API calls, and each cross-stream edge costs two of them
+    // (an event record and a wait, ~40 per step) for an overlap worth less.
+    one_ = [&] {
+      const char* e = std::getenv("WH_PSX_STREAMS");
+      const std::string v = e ? e : "";
+      return v == "one" || (v != "multi" && linear_);
+    }();
+    if (!one_) {
+      ls_h_ = own_stream(dev_, kStreamPsxLs);
+      cs_h_ = own_stream(dev_, kStreamPsxCs);
+      xs_h_ = own_stream(dev_, kStreamPsxXs);
+      ls_ = c10::hip::getStreamFromExternal(ls_h_, dev_);
+      cs_ = c10::hip::getStreamFromExternal(cs_h_, dev_);
+      xs_ = c10::hip::getStreamFromExternal(xs_h_, dev_);
+    }
     for (auto& e : ring_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : gev_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (pg_) wh::fm_set_cu_reserve((int)cu_reserve);
-    if (!linear_ && lend_auc_) auc_side_lend(dev_, cs_h_);
+    if (!linear_ && lend_auc_ && !one_) auc_side_lend(dev_, cs_h_);
     const int64_t dflt = std::max<int64_t>(4 * (P + 1) + P, 64);
     for (int i = 0; i < kPins; ++i) {
       pins_[i] = torch::empty({dflt}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
@@ -105,7 +118,7 @@ class PsxStep {
   ~PsxStep() {
     if (timing_) timing_->print();
     job_.reset();
-    if (!linear_ && lend_auc_) {
+    if (!linear_ && lend_auc_ && !one_) {
       c10::DeviceGuard g(c10::Device(c10::kCUDA, dev_));
       auc_side_lend(dev_, nullptr);
     }
@@ -113,8 +126,6 @@ class PsxStep {
     for (auto& e : ring_) (void)hipEventDestroy(e);
     for (auto& e : gev_) (void)hipEventDestroy(e);
     for (auto& e : pin_ev_) (void)hipEventDestroy(e);
-    for (hipStream_t h : {ls_h_, cs_h_, xs_h_})
-      if (h) (void)hipStreamDestroy(h);
   }
 
   // One training minibatch (Psx.train). Returns (has_data, minibatches
@@ -129,7 +140,7 @@ class PsxStep {
     // finish + next begin + C1, s4 reply (forward), s5 owner push, s6 open,
     // s7 C0 of the next job, s8 backward
     HostTimer ht(timing_.get());
-    S_stream_ = c10::hip::getCurrentHIPStream(dev_);
+    set_streams();
     fwd_mb_ = 0;
     ensure_job(keys, offset, val);
     ht.mark(0);
@@ -182,7 +193,7 @@ class PsxStep {
   // forwarded here.
   int64_t flush() {
     c10::DeviceGuard g(store_->slots_.device());
-    S_stream_ = c10::hip::getCurrentHIPStream(dev_);
+    set_streams();
     fwd_mb_ = 0;
     if (push_ && push_->gvc.defined()) c3(*push_);
     if (job_ && job_carried_) {  // the begun job carries the last pull's V counts
@@ -280,9 +291,11 @@ class PsxStep {
       opts.asyncOp = false;
       auto w = pg_->alltoall_base(of, xf, rs, ss, opts);
       if (w) w->wait();
-      if (!work->ev) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&work->ev, hipEventDisableTiming));
-      WH_HIP_CHECK_HOST(hipEventRecord(work->ev, xs.stream()));
-      work->pending = true;
+      if (!one_) {  // (one stream: the consumer is on it already)
+        if (!work->ev) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&work->ev, hipEventDisableTiming));
+        WH_HIP_CHECK_HOST(hipEventRecord(work->ev, xs.stream()));
+        work->pending = true;
+      }
     }
     work->keep = xc;
     return out;
@@ -312,6 +325,7 @@ class PsxStep {
     return e;
   }
   void wait_on(const c10::hip::HIPStream& waiter, const c10::hip::HIPStream& producer) {
+    if (waiter.stream() == producer.stream()) return;
     WH_HIP_CHECK_HOST(hipStreamWaitEvent(waiter.stream(), record(producer), 0));
   }
 
@@ -512,6 +526,19 @@ class PsxStep {
         c10::hip::HIPCachingAllocator::recordStream(x->storage().data_ptr(), S_stream_);
   }
 
+  // the compute stream of this call; one stream: every phase on it
+  void set_streams() {
+    S_stream_ = c10::hip::getCurrentHIPStream(dev_);
+    if (one_) ls_ = cs_ = xs_ = S_stream_;
+  }
+
+  // a minibatch's exact AUC into the learner's sum: on the AUC side stream,
+  // or in order on the compute stream (one stream)
+  void auc(PsxSt& st) {
+    if (one_) auc_acc(st.py, st.label, auc_sum_);
+    else auc_acc_side(st.py, st.label, auc_sum_);
+  }
+
   // ------------------------------------------------------------ phases
   void c1(PsxSt& st) {
     Tensor rec = linear_ ? st.uniq
@@ -534,7 +561,7 @@ class PsxStep {
     st.rbuf = o[4];
     st.vcnt = o[5];
     st.keys_o = Tensor();
-    st.ev_open = record(S_stream_);
+    st.ev_open = one_ ? nullptr : record(S_stream_);
     if (insert) guard_after(false);
   }
 
@@ -566,7 +593,7 @@ class PsxStep {
     st.py = fw[0];
     st.dual = fw[1];
     st.xv = fw[2];
-    if (!st.train) auc_acc_side(st.py, st.label, auc_sum_);
+    if (!st.train) auc(st);
     if (st.label.numel()) ++fwd_mb_;
     last_u_ = st.U;
     last_v_ = vsum(st.vrecv);
@@ -585,9 +612,9 @@ class PsxStep {
       ps_pack_gw(b[0], b[1], st.segS_w, st.segHS_w, st.vrecv_d);
       st.gvc = b[1];
     }
-    st.ev_grad = record(S_stream_);
+    st.ev_grad = one_ ? nullptr : record(S_stream_);
     if (issue) c3(st);
-    auc_acc_side(st.py, st.label, auc_sum_);
+    auc(st);
     st.rrecv = st.hdr = st.dual = st.xv = st.lid = Tensor();
     st.csc_off = st.csc_row = st.csc_val = Tensor();
   }
@@ -705,6 +732,7 @@ class PsxStep {
   int64_t uhint_ = 0, step_ = 0, requests_ = 0, fwd_mb_ = 0, last_u_ = 0, last_v_ = 0;
   int64_t wire_[4] = {0, 0, 0, 0};
   std::unique_ptr<HostSplit> timing_{host_split("psx native step")};
+  bool one_ = false;
   // WH_PSX_AUC_OWN=1: the AUC on its own side stream, not on cs
   const bool lend_auc_ = [] {
     const char* e = std::getenv("WH_PSX_AUC_OWN");
