@@ -1202,7 +1202,7 @@ Tensor ps_records(const Tensor& uniq, const c10::optional<Tensor>& ucnt) {
 // [4P], payload int64 [S+1+5P]; payload[S+1 : S+1+4P] is the exchange's
 // receive slot)
 std::vector<Tensor> ps_c0(const Tensor& owner_cnt, const c10::optional<Tensor>& vcnt, int64_t P,
-                          int64_t flag) {
+                          int64_t flag, bool loopback = false) {
   CHECK_IN(owner_cnt, torch::kInt64);
   const int S = (int)owner_cnt.numel() - 1;
   TORCH_CHECK(S >= 1 && S <= P, "ps_c0: owner counts must cover 1..P shards");
@@ -1216,7 +1216,7 @@ std::vector<Tensor> ps_c0(const Tensor& owner_cnt, const c10::optional<Tensor>& 
   auto send = torch::empty({4 * P}, owner_cnt.options());
   auto payload = torch::empty({S + 1 + 5 * P}, owner_cnt.options());
   TORCH_CHECK(wh::ps_c0(ptr<int64_t>(owner_cnt), vp, S, (int)P, flag, ptr<int64_t>(send),
-                        ptr<int64_t>(payload), cur_stream(owner_cnt)),
+                        ptr<int64_t>(payload), cur_stream(owner_cnt), loopback ? 1 : 0),
               "ps_c0: too many peers");
   return {send, payload};
 }
@@ -3187,7 +3187,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("ps_unpack", &ps_unpack);
   m.def("ps_pack_gw", &ps_pack_gw);
   m.def("ps_records", &ps_records);
-  m.def("ps_c0", &ps_c0);
+  m.def("ps_c0", &ps_c0, py::arg("owner_cnt"), py::arg("vcnt"), py::arg("P"), py::arg("flag"),
+        py::arg("loopback") = false);
   m.def("auc", &auc);
   m.def("quant_rows", &quant_rows);
   m.def("key_mod", &key_mod);

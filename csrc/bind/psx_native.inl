@@ -358,9 +358,10 @@ class PsxStep {
       c10::hip::HIPCachingAllocator::recordStream(owner_cnt.storage().data_ptr(), cs_);
       if (vc.defined()) c10::hip::HIPCachingAllocator::recordStream(vc.storage().data_ptr(), cs_);
       c10::hip::HIPStreamGuard sg(cs_);
-      auto c0 = ps_c0(owner_cnt, vc.defined() ? c10::optional<Tensor>(vc) : c10::nullopt, P_, flag);
-      Tensor recv = exchange_counts(c0[0]);
-      c0[1].narrow(0, S_ + 1, 4 * P_).copy_(recv);
+      // (loopback identity: the kernel fills the receive slot itself)
+      auto c0 = ps_c0(owner_cnt, vc.defined() ? c10::optional<Tensor>(vc) : c10::nullopt, P_, flag,
+                      !pg_);
+      if (pg_) c0[1].narrow(0, S_ + 1, 4 * P_).copy_(exchange_counts(c0[0]));
       return std::make_tuple(c0[1], cs_.stream(), (int64_t)4, P_);
     };
   }
@@ -456,8 +457,8 @@ class PsxStep {
     auto zero = torch::zeros({S_ + 1}, st.vcnt.options());
     wait_on(cs_, S_stream_);
     c10::hip::HIPStreamGuard sg(cs_);
-    auto c0 = ps_c0(zero, st.vcnt, P_, 1);
-    c0[1].narrow(0, S_ + 1, 4 * P_).copy_(exchange_counts(c0[0]));
+    auto c0 = ps_c0(zero, st.vcnt, P_, 1, !pg_);
+    if (pg_) c0[1].narrow(0, S_ + 1, 4 * P_).copy_(exchange_counts(c0[0]));
     Tensor v = c0[1].cpu();
     const int64_t* h = v.data_ptr<int64_t>();
     st.vrecv.assign(P_, 0);
@@ -562,7 +563,9 @@ class PsxStep {
     st.vcnt = o[5];
     st.keys_o = Tensor();
     st.ev_open = one_ ? nullptr : record(S_stream_);
-    if (insert) guard_after(false);
+    // the summary every gevery_ opens: in between, guard_before's estimate
+    // counts every key inserted since the last one (gsince_), an upper bound
+    if (insert && ++gskip_ >= gevery_) guard_after(false);
   }
 
   void c2(PsxSt& st) {
@@ -688,6 +691,7 @@ class PsxStep {
     grecent_[1] = n;
   }
   void guard_after(bool sync) {
+    gskip_ = 0;
     gk_ ^= 1;
     wait_on(cs_, S_stream_);
     {
@@ -743,7 +747,14 @@ class PsxStep {
     const char* e = std::getenv("WH_PSX_A2A");
     return e && std::string(e) == "async";
   }();
-  // guard
+  // guard (WH_GUARD_EVERY: opens per store summary; the linear step's
+  // default 4 -- a launch, an event and a host read less on 3 of 4 steps)
+  const int gevery_ = [this] {
+    const char* e = std::getenv("WH_GUARD_EVERY");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : (linear_ ? 4 : 1);
+  }();
+  int gskip_ = 0;
   hipEvent_t gev_[2] = {};
   int gk_ = 0;
   bool gpend_ = false;

@@ -379,14 +379,17 @@ __global__ __launch_bounds__(kThreads) void k_ps_records(const uint64_t* __restr
 __global__ __launch_bounds__(256) void k_ps_c0(const int64_t* __restrict__ owner_cnt,
                                                const int64_t* __restrict__ vcnt, int S, int P,
                                                int64_t flag, int64_t* __restrict__ send,
-                                               int64_t* __restrict__ payload) {
+                                               int64_t* __restrict__ payload, int loop) {
   for (int p = threadIdx.x; p <= S; p += blockDim.x) payload[p] = owner_cnt[p];
   for (int p = threadIdx.x; p < P; p += blockDim.x) {
     const int64_t v = vcnt ? vcnt[p] : 0;
-    send[4 * p] = p < S ? owner_cnt[p] : 0;
-    send[4 * p + 1] = owner_cnt[S];
-    send[4 * p + 2] = v;
-    send[4 * p + 3] = flag;
+    const int64_t m[4] = {p < S ? owner_cnt[p] : 0, owner_cnt[S], v, flag};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      send[4 * p + k] = m[k];
+      // loopback identity: what peer p would send this rank is what it sends
+      if (loop) payload[S + 1 + 4 * p + k] = m[k];
+    }
     payload[S + 1 + 4 * P + p] = v;
   }
 }
@@ -708,10 +711,10 @@ void ps_records(const uint64_t* uniq, const int32_t* ucnt, int64_t U, int32_t* r
 }
 
 bool ps_c0(const int64_t* owner_cnt, const int64_t* vcnt, int S, int P, int64_t flag,
-           int64_t* send, int64_t* payload, hipStream_t s) {
+           int64_t* send, int64_t* payload, hipStream_t s, int loop) {
   if (P < 1 || P > 4096 || S < 1 || S > P) return false;
   hipLaunchKernelGGL(k_ps_c0, dim3(1), dim3(256), 0, s, owner_cnt, vcnt, S, P, flag, send,
-                     payload);
+                     payload, loop);
   return true;
 }
 

@@ -258,8 +258,10 @@ bool ps_push(const KVTable& t, const int32_t* slot, const int64_t* vpos, const u
 void ps_records(const uint64_t* uniq, const int32_t* ucnt, int64_t U, int32_t* rec,
                 hipStream_t s);
 // C0 count exchange buffers: send[4P] and payload[S+1+5P] (see psx.hip)
+// loop: also fill the payload's receive slot with send (the loopback
+// identity exchange, no collective)
 bool ps_c0(const int64_t* owner_cnt, const int64_t* vcnt, int S, int P, int64_t flag,
-           int64_t* send, int64_t* payload, hipStream_t s);
+           int64_t* send, int64_t* payload, hipStream_t s, int loop = 0);
 // linear model (vstride 0) owner push over all P segments: chain heads apply
 // their key's gradients in peer order; SGD request counter starts at t0
 bool ps_push_linear(const KVTable& t, const int32_t* slot, const uint32_t* chain,
