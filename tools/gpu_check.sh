@@ -6,7 +6,7 @@ TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests -m gpu ${PYTEST_X--x} -q -rf --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc" >> $OUT/pytest.log
 tail -3 $OUT/pytest.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
