@@ -722,3 +722,19 @@ def test_kmeans_update_matches_torch(hip):
     got, ne = hip.kmeans_update(sums.to(DEV), C.to(DEV))
     assert int(ne) == int(empty.sum())
     assert torch.allclose(got.cpu(), exp, atol=1e-6, rtol=1e-6)
+
+
+def test_auc_acc_reused_range_stays_exact(hip):
+    """The accumulating AUC cuts its buckets from the previous call's
+    {min, max}: minibatches whose scores drift past that range (shifted,
+    rescaled, all equal, then back) still sum to the exact AUCs."""
+    g = torch.Generator().manual_seed(8)
+    acc = torch.zeros(1, dtype=torch.float64, device=DEV)
+    tot = 0.0
+    base = torch.randn(100000, generator=g)
+    for py in (base, base + 50.0, base * 1e-3, torch.full((60000,), 0.25), base, -base,
+               torch.round(base * 8) / 8):
+        lab = (torch.rand(py.numel(), generator=g) < 0.3).float()
+        tot += float(ref.auc(py, lab))
+        hip.auc_acc(py.to(DEV), lab.to(DEV), acc)
+        assert abs(float(acc) - tot) < 1e-8, (float(acc), tot)
