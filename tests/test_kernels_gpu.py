@@ -725,9 +725,10 @@ def test_kmeans_update_matches_torch(hip):
 
 
 def test_auc_acc_reused_range_stays_exact(hip):
-    """The accumulating AUC cuts its buckets from the previous call's
-    {min, max}: minibatches whose scores drift past that range (shifted,
-    rescaled, all equal, then back) still sum to the exact AUCs."""
+    """Accumulated AUCs over minibatches whose scores drift far apart
+    (shifted, rescaled, all equal, then back) sum to the exact AUCs: the
+    persistent bucket workspace carries nothing between calls but counts
+    it re-arms."""
     g = torch.Generator().manual_seed(8)
     acc = torch.zeros(1, dtype=torch.float64, device=DEV)
     tot = 0.0
