@@ -91,23 +91,28 @@ class PsxStep {
     // on the compute stream. At the linear step's 10 000 rows the step is
     // bound by host API calls, and each cross-stream edge costs two of them
     // (an event record and a wait, ~40 per step) for an overlap worth less.
-    one_ = [&] {
+    // Two streams (WH_PSX_STREAMS=two): the localize on its own stream, the
+    // counts and the exchange on the compute stream.
+    {
       const char* e = std::getenv("WH_PSX_STREAMS");
       const std::string v = e ? e : "";
-      return v == "one" || (v != "multi" && linear_);
-    }();
+      one_ = v == "one" || (v != "multi" && v != "two" && linear_);
+      sx_ = one_ || v == "two";
+    }
     if (!one_) {
       ls_h_ = own_stream(dev_, kStreamPsxLs);
+      ls_ = c10::hip::getStreamFromExternal(ls_h_, dev_);
+    }
+    if (!sx_) {
       cs_h_ = own_stream(dev_, kStreamPsxCs);
       xs_h_ = own_stream(dev_, kStreamPsxXs);
-      ls_ = c10::hip::getStreamFromExternal(ls_h_, dev_);
       cs_ = c10::hip::getStreamFromExternal(cs_h_, dev_);
       xs_ = c10::hip::getStreamFromExternal(xs_h_, dev_);
     }
     for (auto& e : ring_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : gev_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (pg_) wh::fm_set_cu_reserve((int)cu_reserve);
-    if (!linear_ && lend_auc_ && !one_) auc_side_lend(dev_, cs_h_);
+    if (!linear_ && lend_auc_ && !sx_) auc_side_lend(dev_, cs_h_);
     const int64_t dflt = std::max<int64_t>(4 * (P + 1) + P, 64);
     for (int i = 0; i < kPins; ++i) {
       pins_[i] = torch::empty({dflt}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
@@ -118,7 +123,7 @@ class PsxStep {
   ~PsxStep() {
     if (timing_) timing_->print();
     job_.reset();
-    if (!linear_ && lend_auc_ && !one_) {
+    if (!linear_ && lend_auc_ && !sx_) {
       c10::DeviceGuard g(c10::Device(c10::kCUDA, dev_));
       auc_side_lend(dev_, nullptr);
     }
@@ -291,7 +296,7 @@ class PsxStep {
       opts.asyncOp = false;
       auto w = pg_->alltoall_base(of, xf, rs, ss, opts);
       if (w) w->wait();
-      if (!one_) {  // (one stream: the consumer is on it already)
+      if (!sx_) {  // (exchange on the compute stream: the consumer is on it already)
         if (!work->ev) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&work->ev, hipEventDisableTiming));
         WH_HIP_CHECK_HOST(hipEventRecord(work->ev, xs.stream()));
         work->pending = true;
@@ -530,13 +535,14 @@ class PsxStep {
   // the compute stream of this call; one stream: every phase on it
   void set_streams() {
     S_stream_ = c10::hip::getCurrentHIPStream(dev_);
-    if (one_) ls_ = cs_ = xs_ = S_stream_;
+    if (one_) ls_ = S_stream_;
+    if (sx_) cs_ = xs_ = S_stream_;
   }
 
   // a minibatch's exact AUC into the learner's sum: on the AUC side stream,
   // or in order on the compute stream (one stream)
   void auc(PsxSt& st) {
-    if (one_) auc_acc(st.py, st.label, auc_sum_);
+    if (sx_) auc_acc(st.py, st.label, auc_sum_);
     else auc_acc_side(st.py, st.label, auc_sum_);
   }
 
@@ -562,7 +568,7 @@ class PsxStep {
     st.rbuf = o[4];
     st.vcnt = o[5];
     st.keys_o = Tensor();
-    st.ev_open = one_ ? nullptr : record(S_stream_);
+    st.ev_open = sx_ ? nullptr : record(S_stream_);
     // the summary every gevery_ opens: in between, guard_before's estimate
     // counts every key inserted since the last one (gsince_), an upper bound
     if (insert && ++gskip_ >= gevery_) guard_after(false);
@@ -615,7 +621,7 @@ class PsxStep {
       ps_pack_gw(b[0], b[1], st.segS_w, st.segHS_w, st.vrecv_d);
       st.gvc = b[1];
     }
-    st.ev_grad = one_ ? nullptr : record(S_stream_);
+    st.ev_grad = sx_ ? nullptr : record(S_stream_);
     if (issue) c3(st);
     auc(st);
     st.rrecv = st.hdr = st.dual = st.xv = st.lid = Tensor();
@@ -736,7 +742,7 @@ class PsxStep {
   int64_t uhint_ = 0, step_ = 0, requests_ = 0, fwd_mb_ = 0, last_u_ = 0, last_v_ = 0;
   int64_t wire_[4] = {0, 0, 0, 0};
   std::unique_ptr<HostSplit> timing_{host_split("psx native step")};
-  bool one_ = false;
+  bool one_ = false, sx_ = false;
   // WH_PSX_AUC_OWN=1: the AUC on its own side stream, not on cs
   const bool lend_auc_ = [] {
     const char* e = std::getenv("WH_PSX_AUC_OWN");
