@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Localize microbenchmark: one 100k-row Criteo-shaped minibatch (device
 synthetic) localized repeatedly with the previous unique count as the hint;
-prints mean ms per call (events) for the path picked by WH_LOCALIZE."""
+prints mean ms per call (events) for the path picked by WH_LOCALIZE.
+TEXT=<criteo text file>: four minibatches of its lines instead (parsed on
+the device), e.g. the files benchmarks/bench_e2e.py writes."""
 import json
 import os
 import sys
@@ -22,6 +24,18 @@ def main():
     dev = torch.device("cuda", 0)
     card = torch.tensor(CRITEO_TB_CARD, dtype=torch.int64, device=dev)
     batches = [hip.synth_criteo(n, 11, s, card) for s in range(4)]
+    if os.environ.get("TEXT"):  # Criteo text (e.g. bench_e2e.py's files), parsed on the device
+        raw = open(os.environ["TEXT"], "rb").read()
+        cut, pos = [0], 0
+        for _ in range(4):
+            for _ in range(n):
+                pos = raw.index(b"\n", pos) + 1
+            cut.append(pos)
+        batches = []
+        for a, b in zip(cut, cut[1:]):
+            t = torch.frombuffer(bytearray(raw[a:b]), dtype=torch.uint8).to(dev)
+            k, l, o = hip.parse_criteo(t, n, True)
+            batches.append((k, l, o))
     if os.environ.get("SKEW") == "0":  # uniform ids, same count of distinct ids
         g = torch.Generator(device=dev).manual_seed(5)
         batches = [(torch.randint(0, 600000, (k.numel(),), device=dev, generator=g) *

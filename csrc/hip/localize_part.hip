@@ -680,8 +680,15 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
     // owners by the hash, so 128 / nshard per owner covers the same ids as
     // 128 on one shard, and the digit count (hence the scatter's run length)
     // stays that of one shard
-    nho = 128;
-    while (nho > 1 && (int64_t)nho * nshard > kPartHeavyTotal) nho >>= 1;
+    // WH_LOC_HEAVY: heavy-id partitions over all owners (a power of two)
+    static int64_t htotal = -1;
+    if (htotal < 0) {
+      const char* e = getenv("WH_LOC_HEAVY");
+      htotal = e ? atoll(e) : kPartHeavyTotal;
+      if (htotal < 1 || htotal > kPartMaxHeavy) htotal = kPartHeavyTotal;
+    }
+    nho = (int)htotal;
+    while (nho > 1 && (int64_t)nho * nshard > htotal) nho >>= 1;
     while (nho > 1 && (int64_t)nho * nshard > kPartMaxHeavy) nho >>= 1;
     if ((int64_t)nho * nshard > kPartMaxHeavy) nho = 0;
   }
