@@ -673,6 +673,13 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
   int npo_bits = 0;
   while (((int64_t)nshard << (npo_bits + 1)) * target <= uest) ++npo_bits;
   while (((int64_t)nshard << npo_bits) * 3072 < uest) ++npo_bits;
+  // and enough partitions for the dedup's workgroups (one per partition) to
+  // fill the GPU: <= ~16K non-zeros each. A minibatch of few distinct ids
+  // (18.6K per 100K rows in bench_e2e.py's Criteo text) otherwise got 32
+  // partitions of ~120K non-zeros: 0.66 ms of dedup on 32 workgroups.
+  while (((int64_t)nshard << npo_bits) * 16384 < nnz &&
+         ((int64_t)nshard << (npo_bits + 1)) <= kPartMaxDigits / 2)
+    ++npo_bits;
   // heavy-id partitions per owner (a power of two, <= kPartMaxHeavy in all)
   int nho = 0;
   if (heavy) {
