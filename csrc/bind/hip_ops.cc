@@ -432,35 +432,45 @@ class LocalizeJob {
     }
     ws.part_inflight++;
     counted_ = true;
+    // the job's temporaries in ONE allocation (eight separate tensors were
+    // eight trips through the allocator and dispatcher per minibatch: host
+    // time is the bound of the multi-shard step at 10k rows); the stream-
+    // ordered allocator keeps it safe to drop at the end of this call
     const int64_t nh = (int64_t)plan_.ndig * plan_.ntiles;
-    auto hist = torch::empty({nh}, i32);
+    const int64_t ng = wh::loc_part_groups(plan_) * plan_.ndig;
+    int64_t at = 0;
+    auto carve = [&](int64_t bytes) {
+      const int64_t o = at;
+      at += (bytes + 255) / 256 * 256;
+      return o;
+    };
+    const int64_t o_hist = carve(nh * 4), o_gsum = carve(ng * 4),
+                  o_base = carve((plan_.ndig + 1) * 8), o_pk = carve(nnz * 8), o_pr = carve(nnz * 4),
+                  o_pv = carve(vp ? nnz * 4 : 0), o_pos = carve(nnz * 4), o_plid = carve(nnz * 4);
+    auto tmp = torch::empty({std::max<int64_t>(at, 256)}, keys_.options().dtype(torch::kUInt8));
+    char* tb = static_cast<char*>(tmp.data_ptr());
+    auto* hist = reinterpret_cast<uint32_t*>(tb + o_hist);
+    auto* gsum = reinterpret_cast<uint32_t*>(tb + o_gsum);
+    auto* base = reinterpret_cast<int64_t*>(tb + o_base);
+    auto* pk = reinterpret_cast<uint64_t*>(tb + o_pk);
+    auto* pr = reinterpret_cast<int32_t*>(tb + o_pr);
+    auto* pv = vp ? reinterpret_cast<float*>(tb + o_pv) : nullptr;
+    auto* pos_of = reinterpret_cast<int32_t*>(tb + o_pos);
+    auto* plid = reinterpret_cast<int32_t*>(tb + o_plid);
     const auto* kp = reinterpret_cast<const uint64_t*>(keys_.data_ptr());
-    wh::loc_part_hist(kp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv,
-                      reinterpret_cast<uint32_t*>(hist.data_ptr()), s);
-    auto gsum = torch::empty({wh::loc_part_groups(plan_) * plan_.ndig}, i32);
-    auto base = torch::empty({plan_.ndig + 1}, i64);
-    wh::loc_part_offsets(plan_, reinterpret_cast<uint32_t*>(hist.data_ptr()),
-                         reinterpret_cast<uint32_t*>(gsum.data_ptr()), ptr<int64_t>(base), s);
-    auto pk = torch::empty({nnz}, i64);
-    auto pr = torch::empty({nnz}, i32);
-    auto pv = torch::empty({vp ? nnz : 0}, keys_.options().dtype(torch::kFloat32));
-    auto pos_of = torch::empty({nnz}, i32);
-    wh::loc_part_scatter(kp, vp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv, ptr<int64_t>(base),
-                         reinterpret_cast<const uint32_t*>(gsum.data_ptr()),
-                         reinterpret_cast<const uint32_t*>(hist.data_ptr()),
-                         reinterpret_cast<uint64_t*>(pk.data_ptr()), ptr<int32_t>(pr),
-                         vp ? ptr<float>(pv) : nullptr, ptr<int32_t>(pos_of), s);
-    auto plid = torch::empty({nnz}, i32);
+    wh::loc_part_hist(kp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv, hist, s);
+    wh::loc_part_offsets(plan_, hist, gsum, base, s);
+    wh::loc_part_scatter(kp, vp, ptr<int64_t>(offset_), nrows, nsh, plan_, hv, base, gsum, hist, pk,
+                         pr, pv, pos_of, s);
     auto* pw = reinterpret_cast<unsigned long long*>(ws.part_ws.data_ptr());
-    wh::loc_part_dedup(reinterpret_cast<const uint64_t*>(pk.data_ptr()), ptr<int32_t>(pr),
-                       vp ? ptr<float>(pv) : nullptr, nnz, nsh, plan_, hv, ptr<int64_t>(base),
+    wh::loc_part_dedup(pk, pr, pv, nnz, nsh, plan_, hv, base,
                        wh::lookback_bind(ws.lb_loc.data_ptr()),
                        reinterpret_cast<uint64_t*>(uniq_.data_ptr()), ptr<int32_t>(ucnt_),
                        ptr<int64_t>(csc_off_), ptr<int32_t>(csc_row_),
-                       vp ? ptr<float>(csc_val_) : nullptr, ptr<int32_t>(plid), pw,
+                       vp ? ptr<float>(csc_val_) : nullptr, plid, pw,
                        reinterpret_cast<unsigned int*>(pw + wh::kPartMaxDigits),
                        ptr<int64_t>(owner_cnt), s, loc_timing() ? ptr<int64_t>(loc_timing_buf()) : nullptr);
-    wh::loc_part_lid(ptr<int32_t>(pos_of), ptr<int32_t>(plid), nnz, ptr<int32_t>(lid_), s);
+    wh::loc_part_lid(pos_of, plid, nnz, ptr<int32_t>(lid_), s);
     return owner_cnt;
   }
 
