@@ -214,6 +214,70 @@ __global__ __launch_bounds__(256) void k_nl_fill(const uint8_t* __restrict__ t, 
   }
 }
 
+// 16 bytes per thread (one 16-byte load; the byte before them by one more):
+// the same ends as k_nl_count / k_nl_fill with a sixteenth of the load
+// instructions -- those scanned a byte per lane and loaded every byte twice
+// (it and its predecessor). Needs a 16-byte aligned text.
+__device__ __forceinline__ uint32_t nl_ends16(const uint8_t* __restrict__ t, int64_t n, int64_t j0) {
+  uint8_t c[16];
+  if (j0 + 16 <= n) {
+    const uint4 v = *reinterpret_cast<const uint4*>(t + j0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c[k] = j0 + k < n ? t[j0 + k] : (uint8_t)0;
+  }
+  uint8_t prev = j0 > 0 && j0 - 1 < n ? t[j0 - 1] : (uint8_t)'\n';
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    // is_end: a newline after a non-newline byte (byte 0 never ends a line)
+    if (j0 + k < n && j0 + k > 0 && c[k] == '\n' && prev != '\n') m |= 1u << k;
+    prev = c[k];
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(256) void k_nl_count16(const uint8_t* __restrict__ t, int64_t n,
+                                                    int32_t* __restrict__ cnt) {
+  __shared__ int wc[4];
+  const int64_t j0 = (int64_t)blockIdx.x * kNlTile + threadIdx.x * 16;
+  int c = __popc(nl_ends16(t, n, j0));
+  c = (int)wave_sum((float)c);
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+__global__ __launch_bounds__(256) void k_nl_fill16(const uint8_t* __restrict__ t, int64_t n,
+                                                   const int64_t* __restrict__ off,
+                                                   int64_t* __restrict__ start) {
+  __shared__ int wc[4];
+  if (blockIdx.x == 0 && threadIdx.x == 0) start[0] = 0;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j0 = (int64_t)blockIdx.x * kNlTile + threadIdx.x * 16;
+  const uint32_t m = nl_ends16(t, n, j0);
+  const int c = __popc(m);
+  int x = c;  // wave inclusive scan of the per-thread counts
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wc[w] = x;
+  __syncthreads();
+  int64_t base = off[blockIdx.x] + x - c;
+  for (int q = 0; q < w; ++q) base += wc[q];
+  uint32_t mm = m;
+  while (mm) {
+    const int k = __ffs(mm) - 1;
+    mm &= mm - 1;
+    start[++base] = j0 + k + 1;
+  }
+}
+
 // ---- fields ---------------------------------------------------------------
 constexpr int kCriteoFields = 39;
 constexpr int kMaxLine = 1 << 16;
@@ -269,11 +333,27 @@ __global__ __launch_bounds__(256) void k_criteo_fields(const uint8_t* __restrict
   int my_start = lane == 0 ? 0 : -1;  // relative to b
   int ntabs = 0;
   const int len = (int)(e - b < kMaxLine ? e - b : kMaxLine);
+  // the line's first kStage bytes staged in LDS up front: all of a lane's
+  // byte loads in flight together (the window loop below then scans LDS;
+  // loading each 64-byte window inside it made every line a chain of ~5
+  // dependent global round trips)
+  {
+    const int lim = len < kStage ? len : kStage;
+    uint8_t pre[kStage / 64];
+#pragma unroll
+    for (int u = 0; u < kStage / 64; ++u) {
+      const int i = u * 64 + lane;
+      pre[u] = i < lim ? t[b + i] : (uint8_t)0;
+    }
+#pragma unroll
+    for (int u = 0; u < kStage / 64; ++u) my[u * 64 + lane] = pre[u];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
   int w0 = 0;
   for (; w0 < len && ntabs < nf; w0 += 64) {
     const int i = w0 + lane;
-    const uint8_t c = i < len ? t[b + i] : 0;
-    if (i < kStage) my[i] = c;
+    const uint8_t c = i < len ? (i < kStage ? my[i] : t[b + i]) : (uint8_t)0;
     const uint64_t m = __ballot(i < len && c == '\t');
     // the k-th tab of the line starts field k: lane k takes its position
     uint64_t mm = m;
@@ -521,10 +601,18 @@ int64_t text_lines(const uint8_t* text, int64_t nbytes, int32_t* tile_cnt, int64
                      int64_t* scan_tmp, int64_t* start, hipStream_t s) {
   const int64_t ntile = (nbytes + kNlTile - 1) / kNlTile;
   if (ntile <= 0) return 0;
-  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)ntile), dim3(256), 0, s, text, nbytes, tile_cnt);
+  const bool v16 = (reinterpret_cast<uintptr_t>(text) & 15) == 0;
+  if (v16)
+    hipLaunchKernelGGL(k_nl_count16, dim3((unsigned)ntile), dim3(256), 0, s, text, nbytes, tile_cnt);
+  else
+    hipLaunchKernelGGL(k_nl_count, dim3((unsigned)ntile), dim3(256), 0, s, text, nbytes, tile_cnt);
   scan_i32(tile_cnt, tile_off, ntile, scan_tmp, s);
-  hipLaunchKernelGGL(k_nl_fill, dim3((unsigned)ntile), dim3(256), 0, s, text, nbytes, tile_off,
-                     start);
+  if (v16)
+    hipLaunchKernelGGL(k_nl_fill16, dim3((unsigned)ntile), dim3(256), 0, s, text, nbytes, tile_off,
+                       start);
+  else
+    hipLaunchKernelGGL(k_nl_fill, dim3((unsigned)ntile), dim3(256), 0, s, text, nbytes, tile_off,
+                       start);
   return ntile;
 }
 
