@@ -569,22 +569,24 @@ __global__ __launch_bounds__(256) void k_libsvm_fill(
 }
 
 // rows sel[i] of a CSR block -> row i of a new CSR block (noff: its offsets);
-// one wave per row, the device half of the shuffle buffer
+// 16 lanes per row (a Criteo row is 39 keys: a whole wave per row left 25 of
+// its 64 lanes idle), the device half of the shuffle buffer
+constexpr int kGatherLanes = 16;
 __global__ __launch_bounds__(256) void k_csr_gather(
     const int64_t* __restrict__ off, const uint64_t* __restrict__ keys,
     const float* __restrict__ val, const float* __restrict__ label,
     const int64_t* __restrict__ sel, int64_t nsel, const int64_t* __restrict__ noff,
     uint64_t* __restrict__ okeys, float* __restrict__ oval, float* __restrict__ olabel) {
-  const int lane = threadIdx.x & 63;
-  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int sub = threadIdx.x & (kGatherLanes - 1);
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / kGatherLanes;
   if (i >= nsel) return;
   const int64_t r = sel[i];
   const int64_t a = off[r], c = off[r + 1] - a, o = noff[i];
-  for (int64_t j = lane; j < c; j += 64) {
+  for (int64_t j = sub; j < c; j += kGatherLanes) {
     okeys[o + j] = keys[a + j];
     if (val) oval[o + j] = val[a + j];
   }
-  if (lane == 0) olabel[i] = label[r];
+  if (sub == 0) olabel[i] = label[r];
 }
 
 }  // namespace
@@ -593,7 +595,9 @@ void csr_gather(const int64_t* off, const uint64_t* keys, const float* val, cons
                 const int64_t* sel, int64_t nsel, const int64_t* noff, uint64_t* okeys,
                 float* oval, float* olabel, hipStream_t s) {
   if (nsel <= 0) return;
-  hipLaunchKernelGGL(k_csr_gather, dim3((unsigned)((nsel + 3) / 4)), dim3(256), 0, s, off, keys,
+  const int64_t rows_per_block = 256 / kGatherLanes;
+  hipLaunchKernelGGL(k_csr_gather, dim3((unsigned)((nsel + rows_per_block - 1) / rows_per_block)),
+                     dim3(256), 0, s, off, keys,
                      val, label, sel, nsel, noff, okeys, oval, olabel);
 }
 
