@@ -739,3 +739,24 @@ def test_auc_acc_reused_range_stays_exact(hip):
         tot += float(ref.auc(py, lab))
         hip.auc_acc(py.to(DEV), lab.to(DEV), acc)
         assert abs(float(acc) - tot) < 1e-8, (float(acc), tot)
+
+
+@pytest.mark.parametrize("nshard", [1, 8])
+def test_localize_few_distinct_ids_many_partitions(hip, nshard):
+    """~2M non-zeros over 2000 power-law ids (the shape of bench_e2e.py's
+    Criteo text: few distinct ids, heavy duplication): the plan splits them
+    into many partitions of few ids (<= ~16K non-zeros each) and single-id
+    partitions for the hot ids elected by the previous call; every output
+    still matches the reference."""
+    keys, off, _, _ = _rand_batch(50000, 20, 2000, 11, False, skew=True)
+    k, o = keys.to(DEV), off.to(DEV)
+    hint = 0
+    for _ in range(3):  # the second and third calls use the elected hot ids
+        uniq, ucnt, owner_cnt, lid = hip.localize(k, o, None, nshard, hint)[:4]
+        hint = uniq.numel()
+        ru = torch.unique(keys)
+        assert torch.equal(torch.sort(uniq.cpu()).values, ru)
+        assert torch.equal(uniq[lid.long()].cpu(), keys)
+        assert torch.equal(ucnt.cpu().long(), torch.bincount(lid.long().cpu(), minlength=hint))
+        own = ref.owner_of(uniq.cpu(), nshard)
+        assert torch.equal(torch.bincount(own, minlength=nshard), owner_cnt)
