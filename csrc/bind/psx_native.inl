@@ -6,17 +6,21 @@
 // feature counts -> ZVPull(w, V) -> compute -> ZVPush(gw, gV)) and
 // learn/linear/async_sgd.h:240-301 (ZPull w -> gradient -> ZPush), with
 // max_concurrency minibatches in flight. A call of PsxStep::train enqueues
-// exactly what Psx.train does -- the same four collectives C0..C3, the same
-// streams (compute S, localize ls, count side cs, exchange xs), the same
-// event edges -- but from C++: the Python step spent ~300 us of host time
-// per call at the reference's minibatch of 10000 rows (~40 Python-level
-// operations and stream switches), more than the GPU work it launched.
+// what Psx.train does -- the same four collectives C0..C3 and phases -- but
+// from C++: the Python step spent ~300 us of host time per call at the
+// reference's minibatch of 10000 rows (~40 Python-level operations and
+// stream switches), more than the GPU work it launched. Streams
+// (WH_PSX_STREAMS): `multi` as the Python step (compute S, localize ls,
+// count side cs, exchange xs; DiFacto's default), `one` (everything on S;
+// linear's default: at 10k rows host API calls bound the step and each
+// cross-stream edge costs an event record and a wait), `two` (ls + S).
 //
 // Transport: the process group's all-to-all through c10d (RCCL over xGMI;
-// c10d::ProcessGroup::alltoall_base, its work's wait() orders the CURRENT
-// stream after the transfer, no host wait), a 1-rank RCCL group for the
-// loopback-rccl rehearsal, or the identity (P virtual shards in one
-// process, the --loopback bench).
+// c10d::ProcessGroup::alltoall_base as a blocking collective on the issuing
+// stream, so RCCL runs it there -- no host wait; WH_PSX_A2A=async uses
+// RCCL's internal stream), a 1-rank RCCL group for the loopback-rccl
+// rehearsal, or the identity (P virtual shards in one process, the
+// --loopback bench).
 
 namespace {
 
