@@ -1268,6 +1268,68 @@ Tensor vidx_renumber(const Tensor& hdr) {
   return pos.narrow(0, n, 1);
 }
 
+// WH_STEP_TIMING=1: host time per section of a native step, summed and
+// printed (mean us per call) at exit -- the launch-bound small-minibatch path
+// WH_STEP_TIMING=2: also the absolute CLOCK_MONOTONIC ns of every mark of
+// calls 200..219, printed at exit (to line up with a rocprofv3 kernel trace)
+struct HostSplit {
+  const char* name;
+  double us[10] = {};
+  int64_t calls = 0;
+  bool abs = false;
+  std::vector<std::array<int64_t, 11>> marks;
+  explicit HostSplit(const char* n) : name(n) {}
+  void print() const {
+    std::fprintf(stderr, "[%s host us/call over %lld]", name, (long long)calls);
+    for (int i = 0; i < 10; ++i)
+      if (us[i] > 0) std::fprintf(stderr, " s%d %.2f", i, us[i] / calls);
+    std::fprintf(stderr, "\n");
+    for (const auto& m : marks) {
+      std::fprintf(stderr, "[%s marks ns]", name);
+      for (int64_t v : m) std::fprintf(stderr, " %lld", (long long)v);
+      std::fprintf(stderr, "\n");
+    }
+  }
+};
+class HostTimer {
+ public:
+  explicit HostTimer(HostSplit* h) : h_(h) {
+    if (h_) {
+      t_ = std::chrono::steady_clock::now();
+      rec_ = h_->abs && h_->calls >= 200 && h_->calls < 220;
+      if (rec_) m_.fill(0), m_[0] = ns(t_);
+    }
+  }
+  void mark(int i) {
+    if (!h_) return;
+    const auto n = std::chrono::steady_clock::now();
+    h_->us[i] += std::chrono::duration<double, std::micro>(n - t_).count();
+    if (rec_ && i + 1 < 11) m_[i + 1] = ns(n);
+    t_ = n;
+  }
+  ~HostTimer() {
+    if (!h_) return;
+    if (rec_) h_->marks.push_back(m_);
+    if (++h_->calls % 1000 == 0) h_->print();
+  }
+
+ private:
+  static int64_t ns(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(t.time_since_epoch()).count();
+  }
+  HostSplit* h_;
+  std::chrono::steady_clock::time_point t_;
+  bool rec_ = false;
+  std::array<int64_t, 11> m_{};
+};
+static HostSplit* host_split(const char* name) {
+  const char* e = std::getenv("WH_STEP_TIMING");
+  if (!(e && (e[0] == '1' || e[0] == '2'))) return nullptr;
+  auto* h = new HostSplit(name);
+  h->abs = e[0] == '2';
+  return h;
+}
+
 // -------------------------------------------------------------- metrics
 // auc_sum[0] += exact AUC of (py, label) (sort-free bucketed rank sum)
 void auc_acc(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
@@ -2186,44 +2248,6 @@ class PinnedBuf {
 // A ring of pinned staging buffers for stream-ordered uploads: a slot is
 // rewritten only after the copy that last read it has run (its event), so
 // the host never has to drain the stream to reuse staging memory.
-// WH_STEP_TIMING=1: host time per section of a native step, summed and
-// printed (mean us per call) at exit -- the launch-bound small-minibatch path
-struct HostSplit {
-  const char* name;
-  double us[10] = {};
-  int64_t calls = 0;
-  explicit HostSplit(const char* n) : name(n) {}
-  void print() const {
-    std::fprintf(stderr, "[%s host us/call over %lld]", name, (long long)calls);
-    for (int i = 0; i < 10; ++i)
-      if (us[i] > 0) std::fprintf(stderr, " s%d %.2f", i, us[i] / calls);
-    std::fprintf(stderr, "\n");
-  }
-};
-class HostTimer {
- public:
-  explicit HostTimer(HostSplit* h) : h_(h) {
-    if (h_) t_ = std::chrono::steady_clock::now();
-  }
-  void mark(int i) {
-    if (!h_) return;
-    const auto n = std::chrono::steady_clock::now();
-    h_->us[i] += std::chrono::duration<double, std::micro>(n - t_).count();
-    t_ = n;
-  }
-  ~HostTimer() {
-    if (h_ && ++h_->calls % 1000 == 0) h_->print();
-  }
-
- private:
-  HostSplit* h_;
-  std::chrono::steady_clock::time_point t_;
-};
-static HostSplit* host_split(const char* name) {
-  const char* e = std::getenv("WH_STEP_TIMING");
-  return e && e[0] == '1' ? new HostSplit(name) : nullptr;
-}
-
 class PinnedRing {
  public:
   static constexpr int N = 4;

@@ -149,6 +149,7 @@ class PsxStep {
     // finish + next begin + C1, s4 reply (forward), s5 owner push, s6 open,
     // s7 C0 of the next job, s8 backward
     HostTimer ht(timing_.get());
+    ht_ = timing_ ? &ht : nullptr;
     set_streams();
     fwd_mb_ = 0;
     ensure_job(keys, offset, val);
@@ -193,7 +194,7 @@ class PsxStep {
       grad(*prev, false);  // C3 goes out behind the next call's C2
       push_ = prev;
     }
-    ht.mark(8);
+    ht_ = nullptr;
     ++step_;
     return py::make_tuple(true, fwd_mb_, last_u_, last_v_);
   }
@@ -546,7 +547,7 @@ class PsxStep {
   // a minibatch's exact AUC into the learner's sum: on the AUC side stream,
   // or in order on the compute stream (one stream)
   void auc(PsxSt& st) {
-    if (sx_) auc_acc(st.py, st.label, auc_sum_);
+    if (sx_ || auc_on_s_) auc_acc(st.py, st.label, auc_sum_);
     else auc_acc_side(st.py, st.label, auc_sum_);
   }
 
@@ -622,12 +623,14 @@ class PsxStep {
       st.gvc = b[0].reshape({-1});
     } else {
       auto b = fm_backward(st.csc_off, st.csc_row, cv, st.dual, st.xv, st.hdr, st.rrecv, vs_);
+      if (ht_) ht_->mark(8);
       ps_pack_gw(b[0], b[1], st.segS_w, st.segHS_w, st.vrecv_d);
       st.gvc = b[1];
     }
     st.ev_grad = sx_ ? nullptr : record(S_stream_);
     if (issue) c3(st);
     auc(st);
+    if (ht_) ht_->mark(9);
     st.rrecv = st.hdr = st.dual = st.xv = st.lid = Tensor();
     st.csc_off = st.csc_row = st.csc_val = Tensor();
   }
@@ -747,10 +750,17 @@ class PsxStep {
   int64_t wire_[4] = {0, 0, 0, 0};
   std::unique_ptr<HostSplit> timing_{host_split("psx native step")};
   bool one_ = false, sx_ = false;
-  // WH_PSX_AUC_OWN=1: the AUC on its own side stream, not on cs
+  // WH_PSX_AUC=s: the AUC in order on the compute stream (diagnosis A/B)
+  const bool auc_on_s_ = [] {
+    const char* e = std::getenv("WH_PSX_AUC");
+    return e && std::string(e) == "s";
+  }();
+  HostTimer* ht_ = nullptr;  // (WH_STEP_TIMING: the running call's marks, for grad's split)
+  // WH_PSX_AUC_LEND=1: the AUC side work on the count stream cs instead of
+  // its own stream (measured 115 vs 120-123 M ex/s at loopback 8: off)
   const bool lend_auc_ = [] {
-    const char* e = std::getenv("WH_PSX_AUC_OWN");
-    return !(e && std::string(e) == "1");
+    const char* e = std::getenv("WH_PSX_AUC_LEND");
+    return e && std::string(e) == "1";
   }();
   // WH_PSX_A2A=async: C1..C3 on RCCL's internal stream (c10d's async path)
   const bool a2a_async_ = [] {
