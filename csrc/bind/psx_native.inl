@@ -556,7 +556,11 @@ class PsxStep {
     Tensor rec = linear_ ? st.uniq
                          : ps_records(st.uniq, st.use_cnt ? c10::optional<Tensor>(st.ucnt)
                                                           : c10::nullopt);
-    st.keys_o = a2a(1, rec, st.send, st.recv, nullptr, &st.w_c1);
+    // on the exchange stream behind the records (RCCL copies the keys there
+    // while the compute stream goes on with the previous minibatch's forward;
+    // on the compute stream itself the forward queued behind the transfer)
+    hipEvent_t ready = (pg_ && !sx_) ? record(S_stream_) : nullptr;
+    st.keys_o = a2a(1, rec, st.send, st.recv, ready, &st.w_c1);
   }
 
   void open(PsxSt& st, bool insert) {
