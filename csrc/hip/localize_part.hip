@@ -677,7 +677,13 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
   // fill the GPU: <= ~16K non-zeros each. A minibatch of few distinct ids
   // (18.6K per 100K rows in bench_e2e.py's Criteo text) otherwise got 32
   // partitions of ~120K non-zeros: 0.66 ms of dedup on 32 workgroups.
-  while (((int64_t)nshard << npo_bits) * 16384 < nnz &&
+  static int64_t per_part = -1;  // WH_LOC_NNZ_PART: non-zeros per partition (target)
+  if (per_part < 0) {
+    const char* e = getenv("WH_LOC_NNZ_PART");
+    per_part = e ? atoll(e) : 16384;
+    if (per_part < 512) per_part = 16384;
+  }
+  while (((int64_t)nshard << npo_bits) * per_part < nnz &&
          ((int64_t)nshard << (npo_bits + 1)) <= kPartMaxDigits / 2)
     ++npo_bits;
   // heavy-id partitions per owner (a power of two, <= kPartMaxHeavy in all)
