@@ -293,6 +293,8 @@ class DeviceTextIter:
         e0 = torch.cuda.Event()
         e0.record(self.stream)
         e0.synchronize()
+        # (hoff stays a pinned tensor: a Python list of a shuffle buffer's
+        # million offsets took the producer tens of ms under the GIL)
         pk, pv, pl = _native.hip().csr_gather(keys, off, val, label, sel, noff, int(hoff[n]))
         ev = torch.cuda.Event()
         ev.record(self.stream)
@@ -319,8 +321,6 @@ class DeviceTextIter:
     def next(self):
         if not self.shuffled:
             return self._get()
-        dev = self.dev
-        main = torch.cuda.current_stream(dev)
         parts, need = [], self.mb
         while need > 0:
             if self.cur is None or self.cur[5] == self.cur[6]:
@@ -328,6 +328,7 @@ class DeviceTextIter:
                 if blk is None:
                     self.cur = None
                     break
+                main = torch.cuda.current_stream(self.dev)
                 main.wait_event(blk[6])
                 for x in blk[:4]:
                     if x is not None:
