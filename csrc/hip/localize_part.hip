@@ -686,6 +686,20 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
   while (((int64_t)nshard << npo_bits) * per_part < nnz &&
          ((int64_t)nshard << (npo_bits + 1)) <= kPartMaxDigits / 2)
     ++npo_bits;
+  // and never fewer than WH_LOC_MIN_PARTS (128) hashed partitions: the
+  // linear step's 10K-row minibatch (390K non-zeros, ~94K distinct ids over
+  // 8 owners) otherwise got 32, so 32 dedup workgroups (dedup 35 -> 30 us;
+  // linear loopback 8 51.9 -> 54.5 M ex/s on one box, inside the
+  // run-to-run spread on another; 256 measured no better)
+  static int64_t min_parts = -1;
+  if (min_parts < 0) {
+    const char* e = getenv("WH_LOC_MIN_PARTS");
+    min_parts = e ? atoll(e) : 128;
+    if (min_parts < 1) min_parts = 1;
+  }
+  while (((int64_t)nshard << npo_bits) < min_parts &&
+         ((int64_t)nshard << (npo_bits + 1)) <= kPartMaxDigits / 2)
+    ++npo_bits;
   // heavy-id partitions per owner (a power of two, <= kPartMaxHeavy in all)
   int nho = 0;
   if (heavy) {
