@@ -728,8 +728,19 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
   if (pl.ndig > kPartMaxDigits || uest > ((int64_t)nshard << npo_bits) * 3072) return pl;
   // tiles of R whole rows, ~4096 non-zeros each (8192 halves the histogram
   // but leaves too few workgroups: hist 28 -> 37 us, scatter 64 -> 80 us)
+  // A small minibatch takes smaller tiles, down to 1024 non-zeros, for at
+  // least WH_LOC_MIN_TILES (256) histogram / scatter workgroups: the linear
+  // step's 10K rows made 96 tiles of 4096.
+  static int64_t min_tiles = -1;
+  if (min_tiles < 0) {
+    const char* e = getenv("WH_LOC_MIN_TILES");
+    min_tiles = e ? atoll(e) : 256;
+    if (min_tiles < 1) min_tiles = 1;
+  }
+  int64_t tile_nnz = nnz / min_tiles;
+  tile_nnz = tile_nnz < 1024 ? 1024 : (tile_nnz > 4096 ? 4096 : tile_nnz);
   const int64_t avg = (nnz + nrows - 1) / nrows;
-  int64_t R = 4096 / (avg > 0 ? avg : 1);
+  int64_t R = tile_nnz / (avg > 0 ? avg : 1);
   R = R < 1 ? 1 : (R > kPartMaxRows ? kPartMaxRows : R);
   pl.R = (int)R;
   pl.ntiles = (nrows + R - 1) / R;
