@@ -56,7 +56,7 @@ def gen_ninja():
                  "-DTORCH_API_INCLUDE_EXTENSION_H" % (cxxflags, ROCM, tinc))
     hostflags = "%s %s -DTORCH_API_INCLUDE_EXTENSION_H -pthread" % (cxxflags, tinc)
     tlibs = "-L%s -Wl,-rpath,%s -lc10 -ltorch -ltorch_cpu -ltorch_python" % (tlib, tlib)
-    hiplibs = "%s -lc10_hip -ltorch_hip -lamdhip64" % tlibs
+    hiplibs = "%s -lc10_hip -ltorch_hip -lamdhip64 -lrccl" % tlibs
 
     lines = [
         "ninja_required_version = 1.3",

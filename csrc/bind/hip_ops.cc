@@ -1369,7 +1369,6 @@ hipStream_t own_stream(int dev, int role) {
 struct AucSide {
   c10::hip::HIPStream s;
   hipEvent_t in, out;
-  c10::hip::HIPStream own;  // the stream created here (s unless lent)
 };
 
 AucSide* auc_side(c10::DeviceIndex d, bool create) {
@@ -1381,26 +1380,11 @@ AucSide* auc_side(c10::DeviceIndex d, bool create) {
   // internal stream comes from the same pool), and AUC kernels queued on a
   // collective's stream would wait for it
   auto st = c10::hip::getStreamFromExternal(own_stream(d, kStreamAuc), d);
-  auto* a = new AucSide{st, nullptr, nullptr, st};
+  auto* a = new AucSide{st, nullptr, nullptr};
   WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->in, hipEventDisableTiming));
   WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&a->out, hipEventDisableTiming));
   m[d] = a;
   return a;
-}
-
-// Run the device's AUC side work on a stream of the caller's (the native
-// multi-shard step lends its count stream, idle when the AUC is enqueued:
-// one stream fewer competing for the GPU_MAX_HW_QUEUES=4 hardware queues; a
-// side stream that lands on the compute stream's queue serialises the AUC
-// with the next step's forward), or back on its own (lend = nullptr). The
-// old stream's work is ordered before the new one's.
-void auc_side_lend(c10::DeviceIndex d, hipStream_t lend) {
-  AucSide* a = auc_side(d, true);
-  auto next = lend ? c10::hip::getStreamFromExternal(lend, d) : a->own;
-  if (next.stream() == a->s.stream()) return;
-  WH_HIP_CHECK_HOST(hipEventRecord(a->out, a->s.stream()));
-  WH_HIP_CHECK_HOST(hipStreamWaitEvent(next.stream(), a->out, 0));
-  a->s = next;
 }
 
 void auc_acc_side(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
@@ -3152,6 +3136,7 @@ class LinearStep {
   int64_t hint_ = 0, grows_ = 0, pushes_ = 0;
 };
 
+#include "rccl_comm.h"
 #include "psx_native.inl"
 
 PYBIND11_MODULE(_hip, m) {
@@ -3182,12 +3167,25 @@ PYBIND11_MODULE(_hip, m) {
       .def_property_readonly("grows", &LinearStep::grows)
       .def_property_readonly("direct", [](const LinearStep& l) { return l.direct(); })
       .def_property("pushes", &LinearStep::pushes, &LinearStep::set_pushes);
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def(py::init<const std::string&, int64_t, int64_t, int64_t>(), py::arg("uid"),
+           py::arg("nranks"), py::arg("rank"), py::arg("device"))
+      .def_static("unique_id", &RcclComm::unique_id)
+      .def("close", &RcclComm::close)
+      .def("a2av", &RcclComm::a2av_t, py::arg("x"), py::arg("send_rows"), py::arg("recv_rows"))
+      .def("allreduce_sum", [](RcclComm& c, Tensor t) { c.allreduce_sum(t); })
+      .def_property_readonly("size", &RcclComm::size)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("device", &RcclComm::device);
+  m.attr("PSX_TX_IDENTITY") = (int)kTxIdentity;
+  m.attr("PSX_TX_RCCL") = (int)kTxRccl;
+  m.attr("PSX_TX_STAGED") = (int)kTxStaged;
   py::class_<PsxStep>(m, "PsxStep")
-      .def(py::init<KVStore*, int64_t, int64_t, int64_t, py::object, bool, std::vector<double>,
-                    std::vector<double>, int64_t, bool, int64_t, int64_t, Tensor, Tensor, int64_t,
-                    double, int64_t>(),
-           py::arg("store"), py::arg("P"), py::arg("S"), py::arg("rank"), py::arg("pg"),
-           py::arg("linear"), py::arg("lin_hp"), py::arg("hp"), py::arg("threshold"),
+      .def(py::init<KVStore*, int64_t, int64_t, int64_t, int64_t, py::object, py::object, bool,
+                    std::vector<double>, std::vector<double>, int64_t, bool, int64_t, int64_t,
+                    Tensor, Tensor, int64_t, double, int64_t>(),
+           py::arg("store"), py::arg("P"), py::arg("S"), py::arg("rank"), py::arg("tx"),
+           py::arg("pg"), py::arg("rccl"), py::arg("linear"), py::arg("lin_hp"), py::arg("hp"), py::arg("threshold"),
            py::arg("l1_shrk"), py::arg("seed"), py::arg("loss"), py::arg("met"),
            py::arg("auc_sum"), py::arg("tau"), py::arg("max_load"), py::arg("cu_reserve"),
            py::keep_alive<1, 2>())

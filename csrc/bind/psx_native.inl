@@ -1,6 +1,6 @@
 // Native driver of the pipelined multi-shard parameter-server step
-// (included by hip_ops.cc after LinearStep; the Python twin and the
-// reference of every phase is wormhole_amd/kv/psx.py Psx.train).
+// (included by hip_ops.cc after LinearStep; the Python twin, kept as the
+// test oracle, is wormhole_amd/kv/psx.py Psx.train).
 //
 // Reference per-minibatch flow: learn/difacto/async_sgd.h:372-424 (push the
 // feature counts -> ZVPull(w, V) -> compute -> ZVPush(gw, gV)) and
@@ -9,25 +9,30 @@
 // what Psx.train does -- the same four collectives C0..C3 and phases -- but
 // from C++: the Python step spent ~300 us of host time per call at the
 // reference's minibatch of 10000 rows (~40 Python-level operations and
-// stream switches), more than the GPU work it launched. Streams
-// (WH_PSX_STREAMS): `multi` as the Python step (compute S, localize ls,
-// count side cs, exchange xs; DiFacto's default), `one` (everything on S;
-// linear's default: at 10k rows host API calls bound the step and each
-// cross-stream edge costs an event record and a wait), `two` (ls + S).
+// stream switches), more than the GPU work it launched. Streams: DiFacto
+// runs the compute stream S, the localize stream ls, the count side stream
+// cs and the exchange stream xs; the linear step runs everything on S (at
+// 10 000 rows host API calls bound the step, and each cross-stream edge
+// costs an event record and a wait for an overlap worth less).
 //
-// Transport: the process group's all-to-all through c10d (RCCL over xGMI;
-// c10d::ProcessGroup::alltoall_base as a blocking collective on the issuing
-// stream, so RCCL runs it there -- no host wait; WH_PSX_A2A=async uses
-// RCCL's internal stream), a 1-rank RCCL group for the loopback-rccl
-// rehearsal, or the identity (P virtual shards in one process, the
-// --loopback bench).
+// Transport (kTx*):
+//   kTxRccl     our own RCCL communicator (csrc/bind/rccl_comm.h): every
+//               exchange is one grouped ncclSend / ncclRecv per peer on the
+//               issuing stream (a 1-rank communicator with P virtual peers
+//               in the one-GPU --loopback-rccl rehearsal);
+//   kTxStaged   a gloo process group with the ranks sharing one GPU (RCCL
+//               refuses two ranks on one device): device -> host, gloo
+//               all-to-all-v, host -> device, synchronously; the multi-
+//               process correctness rehearsal of the RCCL path;
+//   kTxIdentity P virtual shards in one process, no transfer (--loopback).
 
 namespace {
 
-struct PsxWork {  // an issued collective and the tensors it reads
-  c10::intrusive_ptr<c10d::Work> w;
+enum PsxTx { kTxIdentity = 0, kTxRccl = 1, kTxStaged = 2 };
+
+struct PsxWork {  // an issued exchange and the tensor it reads
   Tensor keep;
-  hipEvent_t ev = nullptr;  // end of an on-stream transfer (recorded by a2a)
+  hipEvent_t ev = nullptr;  // end of the transfer on the exchange stream
   bool pending = false;
   PsxWork() = default;
   PsxWork(const PsxWork&) = delete;
@@ -35,11 +40,9 @@ struct PsxWork {  // an issued collective and the tensors it reads
   ~PsxWork() {
     if (ev) (void)hipEventDestroy(ev);
   }
-  void wait() {
-    if (w) w->wait();  // the current stream waits for the transfer
+  void wait() {  // the current stream waits for the transfer
     if (pending)
       WH_HIP_CHECK_HOST(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), ev, 0));
-    w.reset();
     pending = false;
     keep = Tensor();
   }
@@ -61,48 +64,68 @@ using PsxStP = std::shared_ptr<PsxSt>;
 int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 int64_t vsum(const std::vector<int64_t>& v) { return std::accumulate(v.begin(), v.end(), (int64_t)0); }
 
+// kTxStaged's host all-to-all-v: row-wise alltoall_base over a (gloo)
+// process group, exposed for a multi-rank CPU test.
+Tensor c10d_rows(const c10::intrusive_ptr<c10d::ProcessGroup>& g, const Tensor& x,
+                 const std::vector<int64_t>& send_rows, const std::vector<int64_t>& recv_rows) {
+  Tensor xc = x.contiguous();
+  int64_t width = 1;
+  for (int64_t d = 1; d < xc.dim(); ++d) width *= xc.size(d);
+  std::vector<int64_t> shape(xc.sizes().begin(), xc.sizes().end());
+  shape[0] = vsum(recv_rows);
+  Tensor out = torch::empty(shape, xc.options());
+  Tensor of = out.view({-1}), xf = xc.view({-1});
+  std::vector<int64_t> rs, ss;
+  for (int64_t r : recv_rows) rs.push_back(r * width);
+  for (int64_t r : send_rows) ss.push_back(r * width);
+  auto w = g->alltoall_base(of, xf, rs, ss);
+  if (w) w->wait();
+  return out;
+}
+
 }  // namespace
 
 class PsxStep {
  public:
-  // pg: the process group (None: loopback identity over P virtual shards);
-  // lin_hp: (algo, alpha, beta, l1, l2) of the linear wire format's owner
-  // push; hp / threshold / l1_shrk / seed: DiFacto's (kv/psx.py reads the
-  // same from the learner); met / auc_sum: the learner's device progress
-  // accumulators.
-  PsxStep(KVStore* store, int64_t P, int64_t S, int64_t rank, py::object pg, bool linear,
-          std::vector<double> lin_hp, std::vector<double> hp, int64_t threshold, bool l1_shrk,
-          int64_t seed, int64_t loss, Tensor met, Tensor auc_sum, int64_t tau, double max_load,
-          int64_t cu_reserve)
+  // tx: the transport (PsxTx); pg: the gloo process group of kTxStaged;
+  // rccl: the communicator of kTxRccl (P ranks, or 1 for the loopback
+  // rehearsal); lin_hp: (algo, alpha, beta, l1, l2) of the linear wire
+  // format's owner push; hp / threshold / l1_shrk / seed: DiFacto's
+  // (kv/psx.py reads the same from the learner); met / auc_sum: the
+  // learner's device progress accumulators.
+  PsxStep(KVStore* store, int64_t P, int64_t S, int64_t rank, int64_t tx, py::object pg,
+          py::object rccl, bool linear, std::vector<double> lin_hp, std::vector<double> hp,
+          int64_t threshold, bool l1_shrk, int64_t seed, int64_t loss, Tensor met, Tensor auc_sum,
+          int64_t tau, double max_load, int64_t cu_reserve)
       : store_(store), P_(P), S_(S), rank_(rank), linear_(linear), lin_hp_(std::move(lin_hp)),
         hp_(std::move(hp)), threshold_(threshold), l1_shrk_(l1_shrk), seed_(seed), loss_(loss),
         met_(std::move(met)), auc_sum_(std::move(auc_sum)), tau_(tau), max_load_(max_load) {
     TORCH_CHECK(P >= 2 && S >= 1 && S <= P && rank >= 0 && rank < P, "PsxStep: bad P / S / rank");
     TORCH_CHECK(lin_hp_.size() == 5 && hp_.size() == 8, "PsxStep: hyper-parameter sizes");
+    TORCH_CHECK(tau >= 0 && tau <= 1, "PsxStep: tau must be 0 or 1");
     vs_ = store->vstride();
     TORCH_CHECK(linear_ == (vs_ == 0), "PsxStep: the linear wire format is the vstride-0 store");
-    if (!pg.is_none()) pg_ = pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
-    TORCH_CHECK(!pg_ || pg_->getSize() == P || pg_->getSize() == 1,
-                "PsxStep: the process group must have P ranks (or 1: loopback-rccl)");
+    TORCH_CHECK(tx >= kTxIdentity && tx <= kTxStaged, "PsxStep: unknown transport");
+    tx_ = (PsxTx)tx;
+    if (tx_ == kTxStaged) {
+      TORCH_CHECK(!pg.is_none(), "PsxStep: the staged transport needs a process group");
+      pg_ = pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
+      TORCH_CHECK(pg_->getSize() == P && pg_->getRank() == rank,
+                  "PsxStep: the process group must have P ranks");
+    } else if (tx_ == kTxRccl) {
+      TORCH_CHECK(!rccl.is_none(), "PsxStep: the RCCL transport needs a communicator");
+      rccl_ = rccl.cast<std::shared_ptr<RcclComm>>();
+      TORCH_CHECK((rccl_->size() == P && rccl_->rank() == rank) || rccl_->size() == 1,
+                  "PsxStep: the communicator must have P ranks (or 1: loopback rehearsal)");
+    }
     dev_ = store->slots_.device().index();
+    TORCH_CHECK(!rccl_ || rccl_->device() == dev_, "PsxStep: communicator on another device");
     c10::DeviceGuard g(store->slots_.device());
     // streams of our own (as Python's torch.cuda.Stream()): the pool's
-    // round-robin streams are shared with RCCL's internal stream and other
-    // users, and a localize queued behind a collective on a shared stream
-    // serialises the step
-    //
-    // One stream (WH_PSX_STREAMS=one, the linear step's default): every phase
-    // on the compute stream. At the linear step's 10 000 rows the step is
-    // bound by host API calls, and each cross-stream edge costs two of them
-    // (an event record and a wait, ~40 per step) for an overlap worth less.
-    // Two streams (WH_PSX_STREAMS=two): the localize on its own stream, the
-    // counts and the exchange on the compute stream.
-    {
-      const char* e = std::getenv("WH_PSX_STREAMS");
-      const std::string v = e ? e : "";
-      one_ = v == "one" || (v != "multi" && v != "two" && linear_);
-      sx_ = one_ || v == "two";
-    }
+    // round-robin streams are shared with other users, and a localize queued
+    // behind a collective on a shared stream serialises the step. The linear
+    // step keeps every phase on the compute stream (see the file comment).
+    one_ = sx_ = linear_;
     if (!one_) {
       ls_h_ = own_stream(dev_, kStreamPsxLs);
       ls_ = c10::hip::getStreamFromExternal(ls_h_, dev_);
@@ -115,8 +138,7 @@ class PsxStep {
     }
     for (auto& e : ring_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : gev_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (pg_) wh::fm_set_cu_reserve((int)cu_reserve);
-    if (!linear_ && lend_auc_ && !sx_) auc_side_lend(dev_, cs_h_);
+    if (tx_ == kTxRccl) wh::fm_set_cu_reserve((int)cu_reserve);
     const int64_t dflt = std::max<int64_t>(4 * (P + 1) + P, 64);
     for (int i = 0; i < kPins; ++i) {
       pins_[i] = torch::empty({dflt}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
@@ -127,10 +149,6 @@ class PsxStep {
   ~PsxStep() {
     if (timing_) timing_->print();
     job_.reset();
-    if (!linear_ && lend_auc_ && !sx_) {
-      c10::DeviceGuard g(c10::Device(c10::kCUDA, dev_));
-      auc_side_lend(dev_, nullptr);
-    }
     (void)hipDeviceSynchronize();
     for (auto& e : ring_) (void)hipEventDestroy(e);
     for (auto& e : gev_) (void)hipEventDestroy(e);
@@ -264,14 +282,17 @@ class PsxStep {
     int64_t row = x.element_size();
     for (int64_t d = 1; d < x.dim(); ++d) row *= x.size(d);
     wire_[c] += row * (vsum(send_rows) - send_rows[rank_]);
-    work->w.reset();
     work->pending = false;
-    if (!pg_) return x;  // loopback identity
+    work->keep = Tensor();
+    if (tx_ == kTxIdentity) return x;
     Tensor xc = x.contiguous();
-    int64_t width = 1;
-    for (int64_t d = 1; d < xc.dim(); ++d) width *= xc.size(d);
+    if (tx_ == kTxStaged) return staged_a2a(xc, send_rows, recv_rows);
     std::vector<int64_t> shape(xc.sizes().begin(), xc.sizes().end());
     shape[0] = vsum(recv_rows);
+    // issued from xs behind the producer's event only (the compute stream
+    // goes on with the work enqueued after the producer: C2 of minibatch
+    // i-1 overlaps the backward of i-2), or on S itself when no event is
+    // given (C1; the linear step's single stream)
     c10::hip::HIPStream xs = ready ? xs_ : S_stream_;
     if (ready) {
       WH_HIP_CHECK_HOST(hipStreamWaitEvent(xs_.stream(), ready, 0));
@@ -281,50 +302,37 @@ class PsxStep {
     Tensor out = torch::empty(shape, xc.options());
     if (ready)  // allocated on xs, read on S
       c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), S_stream_);
-    Tensor of = out.view({-1}), xf = xc.view({-1});
-    std::vector<int64_t> rs, ss;
-    if (pg_->getSize() > 1) {
-      for (int64_t r : recv_rows) rs.push_back(r * width);
-      for (int64_t r : send_rows) ss.push_back(r * width);
-    } else if (xc.numel() == 0) {  // (1-rank loopback-rccl: nothing to copy)
-      return out;
-    }
-    if (a2a_async_) {
-      work->w = pg_->alltoall_base(of, xf, rs, ss);
-    } else {
-      // on the issuing stream (xs, or S for C1) rather than RCCL's internal
-      // stream: that stream is created lazily and lands on whichever of the
-      // GPU_MAX_HW_QUEUES=4 hardware queues is next -- measured on the
-      // compute stream's queue, where every transfer then waited behind the
-      // forward / backward kernels (and they behind its barrier packets)
-      c10d::AllToAllOptions opts;
-      opts.asyncOp = false;
-      auto w = pg_->alltoall_base(of, xf, rs, ss, opts);
-      if (w) w->wait();
-      if (!sx_) {  // (exchange on the compute stream: the consumer is on it already)
-        if (!work->ev) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&work->ev, hipEventDisableTiming));
-        WH_HIP_CHECK_HOST(hipEventRecord(work->ev, xs.stream()));
-        work->pending = true;
-      }
+    rccl_->a2av(xc.data_ptr(), out.data_ptr(), row, send_rows, recv_rows, xs.stream());
+    if (xs.stream() != S_stream_.stream()) {
+      if (!work->ev) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&work->ev, hipEventDisableTiming));
+      WH_HIP_CHECK_HOST(hipEventRecord(work->ev, xs.stream()));
+      work->pending = true;
     }
     work->keep = xc;
     return out;
   }
 
+  // kTxStaged: the rows through host memory and the gloo group, in order on
+  // the current stream (blocking: the correctness rehearsal of the RCCL
+  // path with several ranks on one GPU)
+  Tensor staged_a2a(const Tensor& xc, const std::vector<int64_t>& send_rows,
+                    const std::vector<int64_t>& recv_rows) {
+    Tensor h = xc.to(torch::kCPU);  // (waits for the current stream's queue)
+    Tensor r = c10d_rows(pg_, h, send_rows, recv_rows);
+    return r.to(xc.device());
+  }
+
   // int64 [4P] per peer -> the peers' [4P], on the current stream
   Tensor exchange_counts(const Tensor& send) {
-    if (!pg_) return send.clone();
-    Tensor r = torch::empty_like(send);
-    std::vector<int64_t> none;
+    if (tx_ == kTxIdentity) return send.clone();
+    std::vector<int64_t> four(P_, 4);
     Tensor s = send.contiguous();
-    // a blocking collective, as Python's all_to_all_single(async_op=False):
-    // RCCL then runs it on the CURRENT stream (cs) instead of its own stream
-    // plus two event hand-offs -- this tiny exchange sits on the path of the
-    // step's one host read
-    c10d::AllToAllOptions opts;
-    opts.asyncOp = false;
-    auto w = pg_->alltoall_base(r, s, none, none, opts);
-    if (w) w->wait();  // (a blocking collective may return no work handle)
+    if (tx_ == kTxStaged) return staged_a2a(s, four, four);
+    // one 32-byte send / recv per peer on the current stream (cs): this tiny
+    // exchange sits on the path of the step's one host read
+    Tensor r = torch::empty_like(s);
+    rccl_->a2av(s.data_ptr(), r.data_ptr(), 4 * sizeof(int64_t), four, four,
+                c10::hip::getCurrentHIPStream(dev_).stream());
     return r;
   }
 
@@ -370,8 +378,8 @@ class PsxStep {
       c10::hip::HIPStreamGuard sg(cs_);
       // (loopback identity: the kernel fills the receive slot itself)
       auto c0 = ps_c0(owner_cnt, vc.defined() ? c10::optional<Tensor>(vc) : c10::nullopt, P_, flag,
-                      !pg_);
-      if (pg_) c0[1].narrow(0, S_ + 1, 4 * P_).copy_(exchange_counts(c0[0]));
+                      tx_ == kTxIdentity);
+      if (tx_ != kTxIdentity) c0[1].narrow(0, S_ + 1, 4 * P_).copy_(exchange_counts(c0[0]));
       return std::make_tuple(c0[1], cs_.stream(), (int64_t)4, P_);
     };
   }
@@ -467,8 +475,8 @@ class PsxStep {
     auto zero = torch::zeros({S_ + 1}, st.vcnt.options());
     wait_on(cs_, S_stream_);
     c10::hip::HIPStreamGuard sg(cs_);
-    auto c0 = ps_c0(zero, st.vcnt, P_, 1, !pg_);
-    if (pg_) c0[1].narrow(0, S_ + 1, 4 * P_).copy_(exchange_counts(c0[0]));
+    auto c0 = ps_c0(zero, st.vcnt, P_, 1, tx_ == kTxIdentity);
+    if (tx_ != kTxIdentity) c0[1].narrow(0, S_ + 1, 4 * P_).copy_(exchange_counts(c0[0]));
     Tensor v = c0[1].cpu();
     const int64_t* h = v.data_ptr<int64_t>();
     st.vrecv.assign(P_, 0);
@@ -547,7 +555,7 @@ class PsxStep {
   // a minibatch's exact AUC into the learner's sum: on the AUC side stream,
   // or in order on the compute stream (one stream)
   void auc(PsxSt& st) {
-    if (sx_ || auc_on_s_) auc_acc(st.py, st.label, auc_sum_);
+    if (sx_) auc_acc(st.py, st.label, auc_sum_);
     else auc_acc_side(st.py, st.label, auc_sum_);
   }
 
@@ -559,7 +567,7 @@ class PsxStep {
     // on the exchange stream behind the records (RCCL copies the keys there
     // while the compute stream goes on with the previous minibatch's forward;
     // on the compute stream itself the forward queued behind the transfer)
-    hipEvent_t ready = (pg_ && !sx_) ? record(S_stream_) : nullptr;
+    hipEvent_t ready = (tx_ == kTxRccl && !sx_) ? record(S_stream_) : nullptr;
     st.keys_o = a2a(1, rec, st.send, st.recv, ready, &st.w_c1);
   }
 
@@ -733,7 +741,9 @@ class PsxStep {
   int64_t tau_;
   double max_load_;
   int vs_ = 0;
-  c10::intrusive_ptr<c10d::ProcessGroup> pg_;
+  PsxTx tx_ = kTxIdentity;
+  c10::intrusive_ptr<c10d::ProcessGroup> pg_;  // kTxStaged
+  std::shared_ptr<RcclComm> rccl_;             // kTxRccl
   c10::DeviceIndex dev_ = 0;
   c10::hip::HIPStream S_stream_ = c10::hip::getDefaultHIPStream();
   c10::hip::HIPStream ls_ = c10::hip::getDefaultHIPStream();
@@ -754,30 +764,10 @@ class PsxStep {
   int64_t wire_[4] = {0, 0, 0, 0};
   std::unique_ptr<HostSplit> timing_{host_split("psx native step")};
   bool one_ = false, sx_ = false;
-  // WH_PSX_AUC=s: the AUC in order on the compute stream (diagnosis A/B)
-  const bool auc_on_s_ = [] {
-    const char* e = std::getenv("WH_PSX_AUC");
-    return e && std::string(e) == "s";
-  }();
   HostTimer* ht_ = nullptr;  // (WH_STEP_TIMING: the running call's marks, for grad's split)
-  // WH_PSX_AUC_LEND=1: the AUC side work on the count stream cs instead of
-  // its own stream (measured 115 vs 120-123 M ex/s at loopback 8: off)
-  const bool lend_auc_ = [] {
-    const char* e = std::getenv("WH_PSX_AUC_LEND");
-    return e && std::string(e) == "1";
-  }();
-  // WH_PSX_A2A=async: C1..C3 on RCCL's internal stream (c10d's async path)
-  const bool a2a_async_ = [] {
-    const char* e = std::getenv("WH_PSX_A2A");
-    return e && std::string(e) == "async";
-  }();
-  // guard (WH_GUARD_EVERY: opens per store summary; the linear step's
-  // default 4 -- a launch, an event and a host read less on 3 of 4 steps)
-  const int gevery_ = [this] {
-    const char* e = std::getenv("WH_GUARD_EVERY");
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : (linear_ ? 4 : 1);
-  }();
+  // guard: opens per store summary (the linear step: a launch, an event and
+  // a host read less on 3 of 4 steps)
+  const int gevery_ = linear_ ? 4 : 1;
   int gskip_ = 0;
   hipEvent_t gev_[2] = {};
   int gk_ = 0;
@@ -785,22 +775,7 @@ class PsxStep {
   int64_t gkeys_ = 0, gvused_ = 0, gsince_ = 0, grecent_[2] = {0, 0}, grows_ = 0, vgrows_ = 0;
 };
 
-// The c10d call path PsxStep uses (py::object -> ProcessGroup, row-wise
-// alltoall_base, work wait), exposed for a multi-rank CPU test over gloo.
 Tensor c10d_a2a_rows(py::object pg, const Tensor& x, const std::vector<int64_t>& send_rows,
                      const std::vector<int64_t>& recv_rows) {
-  auto g = pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
-  Tensor xc = x.contiguous();
-  int64_t width = 1;
-  for (int64_t d = 1; d < xc.dim(); ++d) width *= xc.size(d);
-  std::vector<int64_t> shape(xc.sizes().begin(), xc.sizes().end());
-  shape[0] = vsum(recv_rows);
-  Tensor out = torch::empty(shape, xc.options());
-  Tensor of = out.view({-1}), xf = xc.view({-1});
-  std::vector<int64_t> rs, ss;
-  for (int64_t r : recv_rows) rs.push_back(r * width);
-  for (int64_t r : send_rows) ss.push_back(r * width);
-  auto w = g->alltoall_base(of, xf, rs, ss);
-  if (w) w->wait();
-  return out;
+  return c10d_rows(pg.cast<c10::intrusive_ptr<c10d::ProcessGroup>>(), x, send_rows, recv_rows);
 }

@@ -234,37 +234,141 @@ def test_loopback_gpu_matches_cpu(max_conc):
     assert abs(pg[0] / pg[5] - pc[0] / pc[5]) < 1e-4
 
 
-def _rccl_loopback_main(rank, port, out_dir, max_conc):
+def _rccl_loopback_main(rank, port, out_dir, model, max_conc):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from wormhole_amd.parallel.comm import LoopbackComm
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     rc = LoopbackComm(4, dev, rccl=True)
     assert rc.backend == "loopback-rccl"
-    a, pa, _ = _run(rc, _conf(max_conc=max_conc), dev, steps=6, rows=2000)
-    b, pb, _ = _run(LoopbackComm(4, dev), _conf(max_conc=max_conc), dev, steps=6, rows=2000)
-    ma, mb = _model(a), _model(b)
-    assert ma.keys() == mb.keys()
-    for k, (w, c, v) in mb.items():
-        wa, ca, va = ma[k]
-        assert c == ca and (v is None) == (va is None), k
-        assert abs(w - wa) <= 1e-5 and (v is None or torch.allclose(v, va, atol=1e-5)), k
-    assert abs(pa[0] / pa[5] - pb[0] / pb[5]) < 1e-5
+    if model == "difacto":
+        a, pa, _ = _run(rc, _conf(max_conc=max_conc), dev, steps=6, rows=2000)
+        b, pb, _ = _run(LoopbackComm(4, dev), _conf(max_conc=max_conc), dev, steps=6, rows=2000)
+        assert a.psx._nat and b.psx._nat  # the native step, over RCCL and the identity
+        ma, mb = _model(a), _model(b)
+        assert ma.keys() == mb.keys()
+        for k, (w, c, v) in mb.items():
+            wa, ca, va = ma[k]
+            assert c == ca and (v is None) == (va is None), k
+            assert abs(w - wa) <= 1e-5 and (v is None or torch.allclose(v, va, atol=1e-5)), k
+        assert abs(pa[0] / pa[5] - pb[0] / pb[5]) < 1e-5
+    else:
+        a, pa, bt = _lin_run(rc, dev, 3, steps=6, rows=2000, max_conc=max_conc)
+        b, pb, _ = _lin_run(LoopbackComm(4, dev), dev, 3, max_conc=max_conc, batches=bt)
+        assert a.psx._nat and b.psx._nat
+        ma, mb = _lin_model(a), _lin_model(b)
+        assert ma.keys() == mb.keys() and len(ma) > 1000
+        for k, w in mb.items():
+            assert abs(w - ma[k]) <= 1e-5 * max(1.0, abs(w)), k
+        assert abs(pa[0] / pa[4] - pb[0] / pb[4]) < 1e-5
+    # the wire tally counts what crosses to the (virtual) peers
+    assert sum(a.psx._nat.wire()) > 0
     rc.finalize()
     with open(os.path.join(out_dir, "ok"), "w") as f:
         f.write("ok\n")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("max_conc", [1, 2])
-def test_loopback_rccl_transport(tmp_path, max_conc):
-    """The multi-shard step with every exchange issued as a real RCCL
-    all-to-all (1-rank group, async work handles on the process group's
-    stream) trains the same model as the identity loopback: the stream
-    ordering of C0-C3 against the compute and side streams holds under RCCL."""
-    mp.spawn(_rccl_loopback_main, args=(_free_port(), str(tmp_path), max_conc), nprocs=1,
-             join=True)
+@pytest.mark.parametrize("model,max_conc", [("difacto", 1), ("difacto", 2), ("linear", 1),
+                                            ("linear", 2)])
+def test_loopback_rccl_transport(tmp_path, model, max_conc):
+    """The native multi-shard step over its own RCCL communicator (1 rank,
+    every virtual peer's segment a grouped ncclSend / ncclRecv to self) trains
+    the same model as the identity loopback: the stream ordering of C0-C3
+    against the compute and side streams holds under RCCL."""
+    mp.spawn(_rccl_loopback_main, args=(_free_port(), str(tmp_path), model, max_conc),
+             nprocs=1, join=True)
     assert (tmp_path / "ok").read_text() == "ok\n"
+
+
+def _lockstep(lr, batches, cap=64):
+    """Every rank steps in lockstep: a rank past its own minibatches passes
+    empty ones (solver/ps.py run_pass), always with a look-ahead (the SAME
+    tensor objects the next call gets), until a call reports that no rank
+    had data."""
+    dev = batches[0][0].device if batches else lr.device
+    items = [(k, o, lab) for k, lab, o in batches]
+    items += [(torch.zeros(0, dtype=torch.int64, device=dev),
+               torch.zeros(1, dtype=torch.int64, device=dev),
+               torch.zeros(0, dtype=torch.float32, device=dev)) for _ in range(cap + 1)]
+    for i in range(cap):
+        k, o, lab = items[i]
+        nk, no, _ = items[i + 1]
+        lr.process(k, o, None, lab, 0, 0, next_batch=(nk, no, None))
+        if lr.last_empty:
+            break
+    else:
+        raise AssertionError("no empty step within %d calls" % cap)
+    lr.flush()
+    return lr.take_progress()
+
+
+def _staged_main(rank, world, port, out_dir, model, max_conc):
+    """One rank of a gloo-staged group on the shared GPU: the native step
+    (kTxStaged) and the Python step train on the same uneven data (rank r
+    has 6 - r minibatches of 300 + 100 r rows); this rank's shard must agree."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    from wormhole_amd.config.schema import LinearConfig
+    from wormhole_amd.data.synthetic import criteo_batch_cpu
+    from wormhole_amd.models.difacto import DifactoLearner
+    from wormhole_amd.models.linear import LinearLearner
+    from wormhole_amd.parallel.comm import Comm
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    comm = Comm(dev, backend="gloo")
+    assert comm.stage
+    mine = [[t.to(dev) for t in criteo_batch_cpu(300 + 100 * rank, 31 + rank, s, CARD)]
+            for s in range(6 - rank)]
+    res = {}
+    for native in ("0", "1"):
+        os.environ["WH_PSX_NATIVE"] = native
+        if model == "difacto":
+            lr = DifactoLearner(_conf(max_conc=max_conc), comm, dev, cap=1 << 14, vcap=1 << 12,
+                                seed=5)
+        else:
+            lr = LinearLearner(LinearConfig(algo=3, lambda_l1=0.1, lr_eta=0.1,
+                                            max_concurrency=max_conc), comm, dev, cap=1 << 14,
+                               seed=5)
+        prog = _lockstep(lr, mine)
+        assert bool(lr.psx._nat) == (native == "1")
+        res[native] = (_model(lr) if model == "difacto" else _lin_model(lr), prog)
+    (mp_, pp), (mn, pn) = res["0"], res["1"]
+    assert mp_.keys() == mn.keys() and len(mp_) > 100
+    if model == "difacto":
+        bad = sum(1 for k, (w, c, v) in mp_.items()
+                  if c != mn[k][1] or abs(w - mn[k][0]) > 1e-4 * max(1.0, abs(w)) or
+                  (v is None) != (mn[k][2] is None) or
+                  (v is not None and not torch.allclose(v, mn[k][2], atol=1e-4)))
+        nmb = pn[4]
+    else:
+        bad = sum(1 for k, w in mp_.items() if abs(w - mn[k]) > 1e-4 * max(1.0, abs(w)))
+        nmb = pn[3]
+    assert bad <= len(mp_) // 1000, bad
+    assert nmb == 6 - rank  # every minibatch of this rank forwarded exactly once
+    for a, c in zip(pn, pp):
+        assert abs(a - c) <= 1e-3 * max(1.0, abs(a)), (pn, pp)
+    comm.barrier()
+    with open(os.path.join(out_dir, "r%d" % rank), "w") as f:
+        f.write("ok\n")
+    comm.finalize()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,model,max_conc", [(2, "difacto", 2), (2, "difacto", 1),
+                                                  (2, "linear", 2), (3, "difacto", 2),
+                                                  (3, "linear", 1)])
+def test_native_step_multi_process_staged(tmp_path, world, model, max_conc):
+    """The native multi-shard step in 2 and 3 processes (ranks sharing the
+    GPU, transfers staged through gloo), uneven data per rank: every rank's
+    shard equals the one the Python step trains on the same data, and every
+    minibatch is forwarded once (learn/difacto/async_sgd.h:363-425 with W
+    workers and S = W servers)."""
+    mp.spawn(_staged_main, args=(world, _free_port(), str(tmp_path), model, max_conc),
+             nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / ("r%d" % r)).read_text() == "ok\n"
 
 
 @pytest.mark.gpu

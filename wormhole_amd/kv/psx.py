@@ -269,9 +269,9 @@ class Psx:
         # beta, l1, l2) -- the linear model's, or DiFacto's FTRL on w (algo 4)
         self.lin_hp = lrn.psx_linear_hp() if self.linear else None
         # the native driver of train() (csrc/bind/psx_native.inl PsxStep):
-        # decided at the first training call (apps set max_key after
-        # construction); False = this Python step
+        # decided at the first training call; False = this Python step
         self._nat = None
+        self._kmod_cache = None  # (keys, keys % max_key) of the last reduced tensor
 
     # ------------------------------------------------------------ wire stats
     def _tally(self, c, x, send_rows):
@@ -688,40 +688,55 @@ class Psx:
 
     # ------------------------------------------------------------ native
     def _native(self):
-        """The C++ driver of :meth:`train` when this configuration has one:
-        a GPU rank over RCCL, the loopback identity or the 1-rank RCCL
-        loopback; no payload filter, collective timer, key modulo or
-        embedding-gradient post-processing (those stay on this Python
-        step). ``WH_PSX_NATIVE=0`` keeps the Python step, ``=1`` forces the
-        native one; by default DiFacto over RCCL keeps the Python step: on the
-        1-rank RCCL loopback rehearsal it measured 103-109 M ex/s against the
-        native step's 98 (profiles/r4l_hwq_ab.txt; the linear step is 1.4x
-        faster native, the identity loopback on par)."""
+        """The C++ driver of :meth:`train` (csrc/bind/psx_native.inl
+        PsxStep) -- the default for every GPU configuration: RCCL ranks (its
+        own communicator, grouped send / recv per peer), gloo-staged ranks
+        sharing one GPU, the loopback identity and the 1-rank RCCL loopback.
+        The payload filter, the collective timer and the embedding-gradient
+        post-processing stay on this Python step, which is also the test
+        oracle (``WH_PSX_NATIVE=0`` selects it)."""
         if self._nat is None:
             lrn, emb = self.lrn, self.lrn.emb
             post = emb is not None and (emb.grad_clipping > 0 or emb.dropout > 0 or
                                         bool(emb.grad_normalization))
             backend = getattr(self.comm, "backend", "")
-            want = os.environ.get("WH_PSX_NATIVE", "")
-            if not want:
-                want = "0" if (not self.linear and backend in ("nccl", "loopback-rccl")) else "1"
-            ok = (self.cuda and want != "0" and
-                  backend in ("nccl", "loopback", "loopback-rccl") and
-                  not getattr(self.comm, "stage", False) and self.qf is None and
-                  self.timer is None and not lrn.max_key and not post)
+            staged = bool(getattr(self.comm, "stage", False))
+            hip = _native.hip()
+            tx = {"loopback": hip.PSX_TX_IDENTITY, "loopback-rccl": hip.PSX_TX_RCCL,
+                  "nccl": hip.PSX_TX_RCCL}.get(backend)
+            if staged and backend == "gloo":
+                tx = hip.PSX_TX_STAGED
+            ok = (self.cuda and os.environ.get("WH_PSX_NATIVE", "1") != "0" and tx is not None
+                  and self.qf is None and self.timer is None and not post)
             self._nat = False
             if ok:
-                pg = self.comm.pg if backend in ("nccl", "loopback-rccl") else None
-                self._nat = _native.hip().PsxStep(
+                self._nat = hip.PsxStep(
                     store=self.store, P=self.P, S=self.nshard,
-                    rank=int(getattr(self.comm, "rank", 0)), pg=pg, linear=self.linear,
+                    rank=int(getattr(self.comm, "rank", 0)), tx=tx,
+                    pg=self.comm.pg if tx == hip.PSX_TX_STAGED else None,
+                    rccl=self.comm.rccl() if tx == hip.PSX_TX_RCCL else None,
+                    linear=self.linear,
                     lin_hp=list(self.lin_hp) if self.linear else [0.0] * 5,
                     hp=list(lrn.hp), threshold=int(lrn.threshold), l1_shrk=bool(lrn.l1_shrk),
                     seed=int(lrn.seed), loss=int(lrn.loss), met=lrn.met, auc_sum=lrn.auc_sum,
                     tau=int(self.tau), max_load=float(lrn.kv.guard.max_load),
-                    cu_reserve=_CU_RESERVE if backend in ("nccl", "loopback-rccl") else 0)
+                    cu_reserve=_CU_RESERVE if tx == hip.PSX_TX_RCCL else 0)
                 self._nat.requests = self.requests
         return self._nat or None
+
+    def _kmod(self, keys):
+        """max_key (ps-lite's flag, learn/base/localizer.h:108-115): the
+        native step localizes the keys modulo max_key; the same input tensor
+        maps to the same reduced tensor (the begun localize of the next
+        minibatch is matched by identity)."""
+        if keys is None or not self.lrn.max_key:
+            return keys
+        c = self._kmod_cache
+        if c is not None and c[0] is keys:
+            return c[1]
+        k = ops.key_mod(keys, self.lrn.max_key)
+        self._kmod_cache = (keys, k)
+        return k
 
     def _native_drain(self):
         """Hand the pipeline back to the Python step (an evaluation or a
@@ -744,6 +759,11 @@ class Psx:
                 nk, no, nv = next_batch[:3]
                 if len(next_batch) > 3 and next_batch[3] is not None:
                     ready = next_batch[3].cuda_event
+            keys = self._kmod(keys)
+            if nk is not None and self.lrn.max_key:
+                if ready:  # the reduction reads the next keys on this stream
+                    torch.cuda.current_stream(self.dev).wait_event(next_batch[3])
+                nk = self._kmod(nk)
             has, nmb, u, v = nat.train(keys=keys, offset=offset, val=val, label=label,
                                        data_pass=int(data_pass), next_keys=nk, next_offset=no,
                                        next_val=nv, ready=ready)

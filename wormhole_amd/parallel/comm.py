@@ -25,6 +25,9 @@ _LOCAL_VARS = ("LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID",
                "SLURM_LOCALID")
 
 
+_RCCL_SEQ = 0  # native communicators made so far (the store key of each id)
+
+
 def env_rank():
     for v in _RANK_VARS:
         if v in os.environ:
@@ -94,6 +97,7 @@ class Comm:
         # staged through host memory around every transfer
         self.stage = backend == "gloo" and self.device.type == "cuda"
         self.pg = None
+        self._rccl = None  # the native exchange's own communicator (rccl())
         # ps-lite COMPRESSING filter (msg_compression): LZ4 per peer chunk on
         # HOST transfers (gloo between CPU ranks; not the staged multi-rank GPU
         # rehearsal, whose payloads are device rows staged per step). Device
@@ -111,6 +115,38 @@ class Comm:
             self.pg = dist.group.WORLD
             self.rank = dist.get_rank()
             self.size = dist.get_world_size()
+
+    # ------------------------------------------------------ native RCCL
+    def rccl(self):
+        """This group's own RCCL communicator (csrc/bind/rccl_comm.h
+        RcclComm: grouped ncclSend / ncclRecv per peer, driven from C++ by
+        the multi-shard step). Created on first use by every rank at the
+        same point: rank 0 makes the id and passes it through the c10d
+        store."""
+        if self._rccl is None:
+            from .. import _native
+            hip = _native.hip()
+            if self.backend != "nccl" or self.device.type != "cuda":
+                raise RuntimeError("Comm.rccl: needs the nccl backend on a GPU")
+            global _RCCL_SEQ
+            _RCCL_SEQ += 1
+            key = "wh_rccl_uid_%d" % _RCCL_SEQ
+            if self.size == 1:
+                uid = hip.RcclComm.unique_id()
+            else:
+                store = dist.distributed_c10d._get_default_store()
+                if self.rank == 0:
+                    uid = hip.RcclComm.unique_id()
+                    store.set(key, uid)
+                else:
+                    uid = store.get(key)
+            self._rccl = hip.RcclComm(bytes(uid), self.size, self.rank, self.device.index)
+        return self._rccl
+
+    def _close_rccl(self):
+        if self._rccl is not None:
+            self._rccl.close()
+            self._rccl = None
 
     # ----------------------------------------------------------- basics
     def barrier(self):
@@ -296,6 +332,7 @@ class Comm:
         return r
 
     def finalize(self):
+        self._close_rccl()
         if self.size > 1 and dist.is_initialized():
             # every rank is past its last collective before any tears the
             # group down (a gloo rank whose peer closed its sockets early
@@ -321,6 +358,7 @@ class LoopbackComm(Comm):
         self.backend = "loopback"
         self.stage = False
         self.pg = None
+        self._rccl = None
         self.compress = False
         # rccl=True: every exchange still moves this process's own bytes, but
         # through a real RCCL all-to-all on a 1-rank process group (async work
@@ -328,8 +366,8 @@ class LoopbackComm(Comm):
         # calls Comm makes over xGMI), so the RCCL stream semantics of the
         # multi-shard step are exercised on a one-GPU box, where RCCL refuses
         # two ranks on one device.
-        self.rccl = bool(rccl) and self.device.type == "cuda"
-        if self.rccl:
+        self.rccl_on = bool(rccl) and self.device.type == "cuda"
+        if self.rccl_on:
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29531")
@@ -338,6 +376,18 @@ class LoopbackComm(Comm):
             assert dist.get_world_size() == 1, "rccl loopback needs a 1-rank group"
             self.pg = dist.group.WORLD
             self.backend = "loopback-rccl"
+
+    def rccl(self):
+        """A 1-rank RCCL communicator: the native step sends each of the P
+        virtual peers' segments as its own send / recv pair to self, so a
+        P-peer exchange's host and launch costs are paid as over xGMI."""
+        if not self.rccl_on:
+            raise RuntimeError("LoopbackComm.rccl: built without rccl=True")
+        if self._rccl is None:
+            from .. import _native
+            hip = _native.hip()
+            self._rccl = hip.RcclComm(bytes(hip.RcclComm.unique_id()), 1, 0, self.device.index)
+        return self._rccl
 
     def _a2a(self, x, async_op):
         """Identity exchange through RCCL (1-rank all-to-all = self copy)."""
@@ -368,18 +418,18 @@ class LoopbackComm(Comm):
 
     def all_to_all_v(self, x, send_rows, recv_rows):
         assert list(send_rows) == list(recv_rows), "loopback exchange must be symmetric"
-        if self.rccl and x.is_cuda:
+        if self.rccl_on and x.is_cuda:
             return self._a2a(x, False)[0]
         return x
 
     def all_to_all_v_async(self, x, send_rows, recv_rows):
         assert list(send_rows) == list(recv_rows), "loopback exchange must be symmetric"
-        if self.rccl and x.is_cuda:
+        if self.rccl_on and x.is_cuda:
             return self._a2a(x, True)
         return x, _Done()
 
     def all_to_all_v_multi(self, items, async_op=False):
-        if self.rccl:
+        if self.rccl_on:
             outs, hs = [], []
             for x, s, r in items:
                 assert list(s) == list(r), "loopback exchange must be symmetric"
@@ -391,10 +441,11 @@ class LoopbackComm(Comm):
         return (outs, _Done()) if async_op else outs
 
     def exchange_counts_dev(self, send_dev):
-        if self.rccl and send_dev.is_cuda:
+        if self.rccl_on and send_dev.is_cuda:
             return self._a2a(send_dev, False)[0]
         return send_dev.clone()
 
     def finalize(self):
-        if self.rccl and dist.is_initialized():
+        self._close_rccl()
+        if self.rccl_on and dist.is_initialized():
             dist.destroy_process_group()
