@@ -84,6 +84,8 @@ def main():
     ap.add_argument("--max-concurrency", type=int, default=2,
                     help="minibatches in flight per worker (reference default 2): with >= 2 "
                          "the multi-shard step is pipelined one minibatch deep")
+    ap.add_argument("--host-profile", default=None,
+                    help="write a cProfile of the timed steps' host (Python) side to PATH.<rank>")
     ap.add_argument("--launch-timeout", type=int, default=3600,
                     help="self-launched multi-rank runs are killed after this many seconds")
     args = ap.parse_args()
@@ -139,10 +141,6 @@ def main():
     # minibatch's localize; the learner waits on its event just before the
     # next localize begins.
     gen = torch.cuda.Stream(device) if device.type == "cuda" else None
-    if device.type == "cuda" and os.environ.get("WH_COMPUTE_PRIO", "0") != "0":
-        # (experiment) the compute stream as a high-priority HIP stream: its
-        # kernels' workgroups dispatch ahead of the localize / AUC side streams
-        torch.cuda.set_stream(torch.cuda.Stream(device, priority=-1))
     main = torch.cuda.current_stream(device) if device.type == "cuda" else None
     if gen is not None:
         from wormhole_amd.utils import streams
@@ -181,7 +179,7 @@ def main():
     comm.barrier()
     sync()
     prof = None
-    if os.environ.get("WH_HOST_PROFILE"):  # host-side (Python) profile of the timed steps
+    if args.host_profile:  # host-side (Python) profile of the timed steps
         import cProfile
         prof = cProfile.Profile()
         prof.enable()
@@ -198,7 +196,7 @@ def main():
     if prof is not None:
         import pstats
         prof.disable()
-        with open(os.environ["WH_HOST_PROFILE"] + ".%d" % comm.rank, "w") as f:
+        with open(args.host_profile + ".%d" % comm.rank, "w") as f:
             pstats.Stats(prof, stream=f).sort_stats("tottime").print_stats(40)
             pstats.Stats(prof, stream=f).sort_stats("cumulative").print_stats(60)
     per_rank = [float(x) for x in comm.allgather_object(dt)] if comm.size > 1 and \

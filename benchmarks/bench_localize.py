@@ -13,6 +13,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from wormhole_amd import _native  # noqa: E402
+from wormhole_amd.utils import trace  # noqa: E402
 from wormhole_amd.data.synthetic import CRITEO_TB_CARD  # noqa: E402
 
 
@@ -52,11 +53,12 @@ def main():
         out = hip.localize(k, o, None, nshard, hint)
     e1.record()
     torch.cuda.synchronize()
-    print(json.dumps({"bench": "localize", "mode": os.environ.get("WH_LOCALIZE", "part"),
-                      "dbg": os.environ.get("WH_LOC_DBG", "0"), "rows": n, "nshard": nshard,
+    print(json.dumps({"bench": "localize",
+                      "mode": "hash" if os.environ.get("WH_DETERMINISTIC") == "1" else "part",
+                      "rows": n, "nshard": nshard,
                       "uniq": hint, "skew": os.environ.get("SKEW", "1"),
                       "ms_per_call": e0.elapsed_time(e1) / iters}))
-    if os.environ.get("WH_LOC_TIMING"):
+    if trace.timing_on("loc"):
         t = hip.loc_timing_read().view(-1, 4).cpu()
         t = t[t[:, 0] > 0]
         t0 = int(t[:, 0].min())

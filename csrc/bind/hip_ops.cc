@@ -19,6 +19,7 @@
 #include <chrono>
 #include <cmath>
 #include <functional>
+#include <deque>
 #include <map>
 #include <mutex>
 #include <memory>
@@ -170,11 +171,20 @@ bool deterministic() {
   return on == 1;
 }
 
-// WH_LOC_TIMING=1: the partitioned dedup stores per-partition phase
-// timestamps (100 MHz) into a device buffer (loc_timing_read) -- a profiling aid
+// WH_TIMING: comma-separated profiling aids (docs/build.md): step, step2,
+// loc, ingest, comm. True when `what` is one of the listed items.
+bool timing_on(const char* what) {
+  const char* e = std::getenv("WH_TIMING");
+  if (!e) return false;
+  const std::string v = std::string(",") + e + ",";
+  return v.find(std::string(",") + what + ",") != std::string::npos;
+}
+
+// WH_TIMING=loc: the partitioned dedup stores per-partition phase
+// timestamps (100 MHz) into a device buffer (loc_timing_read)
 bool loc_timing() {
   static int on = -1;
-  if (on < 0) on = std::getenv("WH_LOC_TIMING") != nullptr;
+  if (on < 0) on = timing_on("loc") ? 1 : 0;
   return on == 1;
 }
 Tensor& loc_timing_buf() {
@@ -252,14 +262,8 @@ class LocalizeJob {
     enqueue();
   }
 
-  static bool part_enabled() {
-    static int on = -1;
-    if (on < 0) {
-      const char* m = std::getenv("WH_LOCALIZE");
-      on = !(m && std::string(m) == "hash") && !deterministic();
-    }
-    return on == 1;
-  }
+  // the hash path is the deterministic one (WH_DETERMINISTIC=1)
+  static bool part_enabled() { return !deterministic(); }
 
   ~LocalizeJob() {
     if (event_) (void)hipEventDestroy(event_);
@@ -1268,10 +1272,11 @@ Tensor vidx_renumber(const Tensor& hdr) {
   return pos.narrow(0, n, 1);
 }
 
-// WH_STEP_TIMING=1: host time per section of a native step, summed and
-// printed (mean us per call) at exit -- the launch-bound small-minibatch path
-// WH_STEP_TIMING=2: also the absolute CLOCK_MONOTONIC ns of every mark of
-// calls 200..219, printed at exit (to line up with a rocprofv3 kernel trace)
+// WH_TIMING=step: host time per section of a native step, summed and
+// printed (mean us per call) every 1000 calls and at exit -- the launch-
+// bound small-minibatch path. WH_TIMING=step2: also the absolute
+// steady-clock ns of every mark of calls 200..219 (to line up with a
+// rocprofv3 kernel trace)
 struct HostSplit {
   const char* name;
   double us[10] = {};
@@ -1323,10 +1328,10 @@ class HostTimer {
   std::array<int64_t, 11> m_{};
 };
 static HostSplit* host_split(const char* name) {
-  const char* e = std::getenv("WH_STEP_TIMING");
-  if (!(e && (e[0] == '1' || e[0] == '2'))) return nullptr;
+  const bool abs = timing_on("step2");
+  if (!abs && !timing_on("step")) return nullptr;
   auto* h = new HostSplit(name);
-  h->abs = e[0] == '2';
+  h->abs = abs;
   return h;
 }
 
@@ -1688,30 +1693,6 @@ Tensor gbdt_partition(const Tensor& B, const Tensor& ridx, const Tensor& pos_nod
   c10::DeviceGuard g(B.device());
   auto s = cur_stream(B);
   const int64_t n = ridx.numel();
-  // WH_GBDT_PART=fused: flags + look-back scan in one pass. Opt-in: with the
-  // level loop host-bound it measured level with the 4-launch path (77.6 vs
-  // 79.1 trees/s over 3 x 60 trees), so the proven path stays the default.
-  static const bool fused = [] {
-    const char* e = std::getenv("WH_GBDT_PART");
-    return e && std::string(e) == "fused";
-  }();
-  if (fused) {  // one-pass flags + look-back scan, then the scatter
-    auto lscan32 = torch::empty({n + 1}, ridx.options());
-    if (wh::gbdt_partition_fused(ptr<uint8_t>(B), bc, B.size(0), (int)B.size(1),
-                                 ptr<int32_t>(ridx), n, ptr<int32_t>(pos_node),
-                                 ptr<int32_t>(node_feat), ptr<int32_t>(node_bin),
-                                 ptr<uint8_t>(node_defl), lookback(B.device()),
-                                 ptr<int32_t>(lscan32), s)) {
-      auto nl = lscan32.index_select(0, seg_end.to(torch::kInt64)) -
-                lscan32.index_select(0, seg_beg.to(torch::kInt64));
-      nleft_out.copy_(nl);
-      auto out = torch::empty_like(ridx);
-      wh::gbdt_scatter32(ptr<int32_t>(ridx), n, ptr<int32_t>(pos_node), ptr<int32_t>(node_feat),
-                         ptr<int32_t>(seg_beg), ptr<int32_t>(nleft_out), ptr<int32_t>(lscan32),
-                         ptr<int32_t>(out), s);
-      return out;
-    }
-  }
   auto left = torch::empty({n}, ridx.options());
   wh::gbdt_goleft(ptr<uint8_t>(B), bc, B.size(0), (int)B.size(1), ptr<int32_t>(ridx), n,
                   ptr<int32_t>(pos_node), ptr<int32_t>(node_feat), ptr<int32_t>(node_bin),
@@ -1780,7 +1761,7 @@ Tensor gbdt_qscale(const Tensor& m, double nglobal, int64_t R) {
 
 void gbdt_leaf_walk(const Tensor& B, const Tensor& feat, const Tensor& bin, const Tensor& defl,
                     const Tensor& left, const Tensor& right, const Tensor& val,
-                    const Tensor& margin) {
+                    const Tensor& margin, bool lds) {
   CHECK_IN(B, torch::kUInt8);
   CHECK_IN(feat, torch::kInt32);
   CHECK_IN(bin, torch::kInt32);
@@ -1798,7 +1779,7 @@ void gbdt_leaf_walk(const Tensor& B, const Tensor& feat, const Tensor& bin, cons
   TORCH_CHECK(nn <= INT32_MAX, "leaf_walk: too many nodes");
   wh::gbdt_leaf_walk(ptr<uint8_t>(B), B.size(0), (int)B.size(1), (int)nn, ptr<int32_t>(feat),
                      ptr<int32_t>(bin), ptr<uint8_t>(defl), ptr<int32_t>(left),
-                     ptr<int32_t>(right), ptr<float>(val), ptr<float>(margin), cur_stream(B));
+                     ptr<int32_t>(right), ptr<float>(val), ptr<float>(margin), cur_stream(B), lds);
 }
 
 void gbdt_predict(const Tensor& X, const Tensor& feat, const Tensor& thr, const Tensor& left,
@@ -1905,12 +1886,8 @@ Tensor kmeans_accum(const Tensor& X, const Tensor& assign, int64_t k) {
   const int f = (int)X.size(1);
   TORCH_CHECK(assign.numel() == n);
   auto sums = torch::zeros({k, f + 1}, X.options());
-  // counting-sort path unless WH_KMEANS_ACCUM=atomic (A/B) or k / f too large
-  static const bool atomic_only = [] {
-    const char* e = std::getenv("WH_KMEANS_ACCUM");
-    return e && std::string(e) == "atomic";
-  }();
-  if (!atomic_only && n > 0) {
+  // counting-sort path unless k / f are too large for it (then atomics)
+  if (n > 0) {
     auto scratch = torch::empty({wh::kmeans_accum_scratch(n, (int)k)},
                                 X.options().dtype(torch::kUInt8));
     if (wh::kmeans_accum_sorted(ptr<float>(X), n, f, (int)k, ptr<int32_t>(assign),
@@ -2782,14 +2759,13 @@ class LinearStep {
   };
   static constexpr int kSumm = 4;
   LinearStep(KVStore* store, int64_t algo, double alpha, double beta, double l1, double l2,
-             int64_t loss, double max_load)
+             int64_t loss, double max_load, bool direct)
       : store_(store), algo_(algo), alpha_(alpha), beta_(beta), l1_(l1), l2_(l2), loss_(loss),
         max_load_(max_load) {
     TORCH_CHECK(store->vstride() == 0, "LinearStep needs a linear store");
     // the localize-free step unless a bitwise-repeatable one is asked for
     // (its per-slot gradient sums are float atomics)
-    direct_ = !deterministic() && !(std::getenv("WH_LINEAR_STEP") &&
-                                    std::string(std::getenv("WH_LINEAR_STEP")) == "localize");
+    direct_ = direct && !deterministic();
     dev_ = store->slots_.device().index();
     c10::DeviceGuard g(store->slots_.device());
     ls_ = c10::hip::getStreamFromExternal(own_stream(dev_, kStreamLinearLs), dev_);
@@ -2805,14 +2781,6 @@ class LinearStep {
       if (m.ev) (void)hipEventDestroy(m.ev);
       if (m.h) (void)hipHostFree(m.h);
     }
-  }
-
-  // WH_LS_WAIT=1: the localize stream waits for S before every job (the
-  // conservative order of the Python path; A/B of the record-stream handoff)
-  static bool ls_waits_s() {
-    static int on = -1;
-    if (on < 0) on = std::getenv("WH_LS_WAIT") && std::string(std::getenv("WH_LS_WAIT")) == "1";
-    return on == 1;
   }
 
   // one minibatch; returns the predictions py [rows]. next_*: the next
@@ -2974,7 +2942,7 @@ class LinearStep {
       // workspace is S's until then) or when the next minibatch has no
       // producer event: it was then made on S (slices, offset rebasing, the
       // handover from a parse stream), possibly by work queued just now
-      if (s_job_ || ls_waits_s() || !ready) {
+      if (s_job_ || !ready) {
         WH_HIP_CHECK_HOST(hipEventRecord(ev_s_, S));
         WH_HIP_CHECK_HOST(hipStreamWaitEvent(ls_.stream(), ev_s_, 0));
         s_job_ = false;
@@ -3097,17 +3065,10 @@ class LinearStep {
   bool direct() const { return direct_; }
   // the localize-free step pays off while a minibatch is small (launch- and
   // latency-bound: the reference's 10000 rows: 71.0 vs 55.1 M ex/s); above
-  // WH_LINEAR_DIRECT_NNZ non-zeros (default 600k, ~15k Criteo rows; at 25k
-  // rows the localize path is ahead, 129 vs 109 M ex/s) the localize's global
-  // dedup does fewer table probes and atomics than per-tile dedup
-  bool use_direct(int64_t nnz) const {
-    static int64_t lim = -1;
-    if (lim < 0) {
-      const char* e = std::getenv("WH_LINEAR_DIRECT_NNZ");
-      lim = e ? std::atoll(e) : 600000;
-    }
-    return direct_ && nnz <= lim;
-  }
+  // 600k non-zeros (~15k Criteo rows; at 25k rows the localize path is
+  // ahead, 129 vs 109 M ex/s) the localize's global dedup does fewer table
+  // probes and atomics than per-tile dedup
+  bool use_direct(int64_t nnz) const { return direct_ && nnz <= 600000; }
   int64_t pushes() const { return pushes_; }
   void set_pushes(int64_t p) { pushes_ = p; }
 
@@ -3155,9 +3116,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("loc_retries", []() { return loc_retries(); },
         "localize jobs redone on the hash path after a partition overflow (count)");
   py::class_<LinearStep>(m, "LinearStep")
-      .def(py::init<KVStore*, int64_t, double, double, double, double, int64_t, double>(),
+      .def(py::init<KVStore*, int64_t, double, double, double, double, int64_t, double, bool>(),
            py::arg("store"), py::arg("algo"), py::arg("alpha"), py::arg("beta"), py::arg("l1"),
-           py::arg("l2"), py::arg("loss"), py::arg("max_load") = 0.7, py::keep_alive<1, 2>())
+           py::arg("l2"), py::arg("loss"), py::arg("max_load") = 0.7, py::arg("direct") = true,
+           py::keep_alive<1, 2>())
       .def("step", &LinearStep::step, py::arg("keys"), py::arg("offset"), py::arg("val"),
            py::arg("label"), py::arg("train"), py::arg("met"), py::arg("auc_sum"),
            py::arg("next_keys") = py::none(), py::arg("next_offset") = py::none(),
@@ -3251,7 +3213,10 @@ PYBIND11_MODULE(_hip, m) {
   m.def("owlqn_step", &owlqn_step);
   m.def("multi_dot", &multi_dot);
   m.def("gbdt_leaf_add", &gbdt_leaf_add);
-  m.def("gbdt_leaf_walk", &gbdt_leaf_walk);
+  m.def("gbdt_leaf_walk", &gbdt_leaf_walk, py::arg("B"), py::arg("feat"), py::arg("bin"),
+        py::arg("defl"), py::arg("left"), py::arg("right"), py::arg("val"), py::arg("margin"),
+        py::arg("lds") = true, "margins += the tree's leaf per row (lds: the LDS-resident walk "
+        "when the tree and row tile fit; else the global-memory walk)");
   m.def("gbdt_predict", &gbdt_predict);
   m.def("kmeans_pack_x", &kmeans_pack_x);
   m.def("kmeans_pack_c", &kmeans_pack_c);

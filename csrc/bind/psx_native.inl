@@ -56,7 +56,10 @@ struct PsxSt {  // one minibatch in flight (kv/psx.py _Step)
   Tensor tabs, segS_w, segHS_w, segS_o, segHS_o, vrecv_d;
   Tensor keys_o, slot, vpos, chain, head, rbuf, vcnt;
   Tensor rrecv, hdr, py, dual, xv, gpush, gvc;
+  // C2 / C3 wait for these only: the open's and the backward's ends on S
+  // (the step's own pair from PsxStep::sev_, recorded once each)
   hipEvent_t ev_open = nullptr, ev_grad = nullptr;
+  hipEvent_t own_open = nullptr, own_grad = nullptr;
   PsxWork w_c1, w_c2, w_c3;
 };
 using PsxStP = std::shared_ptr<PsxSt>;
@@ -102,7 +105,8 @@ class PsxStep {
         met_(std::move(met)), auc_sum_(std::move(auc_sum)), tau_(tau), max_load_(max_load) {
     TORCH_CHECK(P >= 2 && S >= 1 && S <= P && rank >= 0 && rank < P, "PsxStep: bad P / S / rank");
     TORCH_CHECK(lin_hp_.size() == 5 && hp_.size() == 8, "PsxStep: hyper-parameter sizes");
-    TORCH_CHECK(tau >= 0 && tau <= 1, "PsxStep: tau must be 0 or 1");
+    TORCH_CHECK(tau >= 0 && tau <= kMaxTau, "PsxStep: tau (max_concurrency - 1) must be 0..",
+                kMaxTau);
     vs_ = store->vstride();
     TORCH_CHECK(linear_ == (vs_ == 0), "PsxStep: the linear wire format is the vstride-0 store");
     TORCH_CHECK(tx >= kTxIdentity && tx <= kTxStaged, "PsxStep: unknown transport");
@@ -138,6 +142,8 @@ class PsxStep {
     }
     for (auto& e : ring_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : gev_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& p : sev_)
+      for (auto& e : p) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (tx_ == kTxRccl) wh::fm_set_cu_reserve((int)cu_reserve);
     const int64_t dflt = std::max<int64_t>(4 * (P + 1) + P, 64);
     for (int i = 0; i < kPins; ++i) {
@@ -152,6 +158,8 @@ class PsxStep {
     (void)hipDeviceSynchronize();
     for (auto& e : ring_) (void)hipEventDestroy(e);
     for (auto& e : gev_) (void)hipEventDestroy(e);
+    for (auto& p : sev_)
+      for (auto& e : p) (void)hipEventDestroy(e);
     for (auto& e : pin_ev_) (void)hipEventDestroy(e);
   }
 
@@ -162,7 +170,7 @@ class PsxStep {
                   const c10::optional<Tensor>& noffset, const c10::optional<Tensor>& nval,
                   int64_t ready) {
     c10::DeviceGuard g(keys.device());
-    // WH_STEP_TIMING=1: host us per phase, printed every 1000 calls: s0 job,
+    // WH_TIMING=step: host us per phase, printed every 1000 calls: s0 job,
     // s1 count read (the host WAIT), s2 tables + C2/C3 issue, s3 localize
     // finish + next begin + C1, s4 reply (forward), s5 owner push, s6 open,
     // s7 C0 of the next job, s8 backward
@@ -183,7 +191,8 @@ class PsxStep {
     if (prev && !prev->have_v) vcount_exchange(*prev);
     PsxStP st = new_step(send, recv, label, true, data_pass, prev.get());
     if (prev) c2(*prev);
-    if (push_ && push_->gvc.defined()) c3(*push_);
+    // the newest push (its backward ran at the end of the previous call)
+    if (!pushes_.empty() && pushes_.back()->gvc.defined()) c3(*pushes_.back());
     ht.mark(2);
     set_loc(*st, finish_job(), offset, val);
     const bool early = nkeys.has_value() && nkeys->defined();
@@ -198,9 +207,12 @@ class PsxStep {
       }
     }
     ht.mark(4);
-    if (push_) {
-      owner_push(*push_);
-      push_.reset();
+    // staleness tau: the pull of this minibatch sees every push up to tau
+    // minibatches back (each push lands tau - 1 calls after its transfer was
+    // issued, max_concurrency = tau + 1 minibatches in flight)
+    while (tau_ > 0 && (int64_t)pushes_.size() >= tau_) {
+      owner_push(*pushes_.front());
+      pushes_.pop_front();
     }
     ht.mark(5);
     open(*st, true);
@@ -208,9 +220,9 @@ class PsxStep {
     ht.mark(6);
     if (early) exchange_deferred();
     ht.mark(7);
-    if (tau_ == 1 && prev && prev->train) {
+    if (tau_ >= 1 && prev && prev->train) {
       grad(*prev, false);  // C3 goes out behind the next call's C2
-      push_ = prev;
+      pushes_.push_back(prev);
     }
     ht_ = nullptr;
     ++step_;
@@ -223,7 +235,7 @@ class PsxStep {
     c10::DeviceGuard g(store_->slots_.device());
     set_streams();
     fwd_mb_ = 0;
-    if (push_ && push_->gvc.defined()) c3(*push_);
+    if (!pushes_.empty() && pushes_.back()->gvc.defined()) c3(*pushes_.back());
     if (job_ && job_carried_) {  // the begun job carries the last pull's V counts
       std::vector<int64_t> a, b;
       counts(a, b);
@@ -236,10 +248,8 @@ class PsxStep {
       reply(*st);
       if (st->train) grad(*st, true);
     }
-    if (push_) {
-      owner_push(*push_);
-      push_.reset();
-    }
+    for (auto& p : pushes_) owner_push(*p);  // in minibatch order
+    pushes_.clear();
     if (st && st->train) owner_push(*st);
     pull_.reset();
     return fwd_mb_;
@@ -259,7 +269,7 @@ class PsxStep {
     }
   }
 
-  bool busy() const { return (bool)pull_ || (bool)push_ || (bool)job_; }
+  bool busy() const { return (bool)pull_ || !pushes_.empty() || (bool)job_; }
   std::vector<int64_t> wire() const { return {wire_[0], wire_[1], wire_[2], wire_[3]}; }
   void wire_reset() { wire_[0] = wire_[1] = wire_[2] = wire_[3] = 0; }
   int64_t grows() const { return grows_; }
@@ -331,7 +341,7 @@ class PsxStep {
     // one 32-byte send / recv per peer on the current stream (cs): this tiny
     // exchange sits on the path of the step's one host read
     Tensor r = torch::empty_like(s);
-    rccl_->a2av(s.data_ptr(), r.data_ptr(), 4 * sizeof(int64_t), four, four,
+    rccl_->a2av(s.data_ptr(), r.data_ptr(), sizeof(int64_t), four, four,
                 c10::hip::getCurrentHIPStream(dev_).stream());
     return r;
   }
@@ -498,6 +508,13 @@ class PsxStep {
     st->train = train;
     st->use_cnt = train && data_pass == 0 && !linear_;
     st->seed_step = step_;
+    // events of their own per step: at most tau + 2 steps are alive (the
+    // pull in flight, the tau pushes in flight and this one), so a pair is
+    // reused only kStepEv > kMaxTau + 2 steps later, long after its waits
+    // were enqueued
+    st->own_open = sev_[sev_i_][0];
+    st->own_grad = sev_[sev_i_][1];
+    sev_i_ = (sev_i_ + 1) % kStepEv;
     const int64_t vs = std::max<int64_t>(vs_, 1);
     st->Hw.assign(P_, 0);
     st->Ho.assign(P_, 0);
@@ -585,7 +602,8 @@ class PsxStep {
     st.rbuf = o[4];
     st.vcnt = o[5];
     st.keys_o = Tensor();
-    st.ev_open = sx_ ? nullptr : record(S_stream_);
+    if (!sx_) WH_HIP_CHECK_HOST(hipEventRecord(st.own_open, S_stream_.stream()));
+    st.ev_open = sx_ ? nullptr : st.own_open;
     // the summary every gevery_ opens: in between, guard_before's estimate
     // counts every key inserted since the last one (gsince_), an upper bound
     if (insert && ++gskip_ >= gevery_) guard_after(false);
@@ -639,7 +657,8 @@ class PsxStep {
       ps_pack_gw(b[0], b[1], st.segS_w, st.segHS_w, st.vrecv_d);
       st.gvc = b[1];
     }
-    st.ev_grad = sx_ ? nullptr : record(S_stream_);
+    if (!sx_) WH_HIP_CHECK_HOST(hipEventRecord(st.own_grad, S_stream_.stream()));
+    st.ev_grad = sx_ ? nullptr : st.own_grad;
     if (issue) c3(st);
     auc(st);
     if (ht_) ht_->mark(9);
@@ -696,7 +715,9 @@ class PsxStep {
       while ((double)need > 0.5 * (double)cap) cap *= 2;
       Tensor remap = store_->grow(cap);
       ++grows_;
-      for (PsxSt* st : {pull_.get(), push_.get()})
+      std::vector<PsxSt*> live{pull_.get()};
+      for (auto& p : pushes_) live.push_back(p.get());
+      for (PsxSt* st : live)
         if (st && st->slot.defined() && st->slot.numel()) {
           auto s64 = st->slot.to(torch::kInt64);
           st->slot = torch::where(s64 >= 0, remap.index_select(0, s64.clamp_min(0)), st->slot);
@@ -729,7 +750,8 @@ class PsxStep {
     if (sync) guard_read();
   }
 
-  static constexpr int kRing = 32, kPins = 8;
+  static constexpr int kMaxTau = 8;
+  static constexpr int kRing = 32, kPins = 8, kStepEv = kMaxTau + 4;
   KVStore* store_;
   int64_t P_, S_, rank_;
   bool linear_;
@@ -751,6 +773,8 @@ class PsxStep {
   c10::hip::HIPStream xs_ = c10::hip::getDefaultHIPStream();
   hipStream_t ls_h_ = nullptr, cs_h_ = nullptr, xs_h_ = nullptr;
   hipEvent_t ring_[kRing] = {};
+  hipEvent_t sev_[kStepEv][2] = {};
+  int sev_i_ = 0;
   int ring_i_ = 0;
   Tensor pins_[kPins];
   hipEvent_t pin_ev_[kPins] = {};
@@ -758,13 +782,14 @@ class PsxStep {
   int pin_i_ = 0;
   std::unique_ptr<LocalizeJob> job_;
   Tensor job_keys_;
-  PsxStP job_carried_, pull_, push_;
+  PsxStP job_carried_, pull_;
+  std::deque<PsxStP> pushes_;  // backward done, push not yet applied (oldest first)
   bool job_deferred_ = false;
   int64_t uhint_ = 0, step_ = 0, requests_ = 0, fwd_mb_ = 0, last_u_ = 0, last_v_ = 0;
   int64_t wire_[4] = {0, 0, 0, 0};
   std::unique_ptr<HostSplit> timing_{host_split("psx native step")};
   bool one_ = false, sx_ = false;
-  HostTimer* ht_ = nullptr;  // (WH_STEP_TIMING: the running call's marks, for grad's split)
+  HostTimer* ht_ = nullptr;  // (WH_TIMING=step: the running call's marks, for grad's split)
   // guard: opens per store summary (the linear step: a launch, an event and
   // a host read less on 3 of 4 steps)
   const int gevery_ = linear_ ? 4 : 1;

@@ -74,9 +74,10 @@ class RcclComm {
   // (send_rows[q] rows of row_bytes, segments in peer order) goes to q, and
   // q's segment for this rank lands at recv's q-th offset. The own segment
   // is a device copy. With a 1-rank communicator and P > 1 row counts (the
-  // loopback rehearsal) every segment is a send / recv pair to self and
-  // send_rows must equal recv_rows. Zero-row segments are skipped on both
-  // sides (the row counts are symmetric by construction).
+  // loopback rehearsal: virtual rank 0 of P) segment 0 is the own copy and
+  // every other segment a send / recv pair to self, the calls a real rank
+  // issues; send_rows must equal recv_rows. Zero-row segments are skipped
+  // on both sides (the row counts are symmetric by construction).
   void a2av(const void* send, void* recv, int64_t row_bytes, const std::vector<int64_t>& send_rows,
             const std::vector<int64_t>& recv_rows, hipStream_t s) {
     TORCH_CHECK(comm_ != nullptr, "RcclComm: closed");
@@ -90,7 +91,7 @@ class RcclComm {
     bool open = false;
     for (int q = 0; q < P; ++q) {
       const int64_t sb = send_rows[q] * row_bytes, rb = recv_rows[q] * row_bytes;
-      if (virt) {
+      if (virt && q > 0) {
         TORCH_CHECK(sb == rb, "RcclComm.a2av: loopback segments must be symmetric");
         if (sb > 0) {
           if (!open) WH_NCCL_CHECK(ncclGroupStart());
@@ -98,7 +99,7 @@ class RcclComm {
           WH_NCCL_CHECK(ncclSend(sp + so, (size_t)sb, ncclUint8, 0, comm_, s));
           WH_NCCL_CHECK(ncclRecv(rp + ro, (size_t)rb, ncclUint8, 0, comm_, s));
         }
-      } else if (q == rank_) {
+      } else if (q == rank_) {  // (virtual: rank_ == 0)
         TORCH_CHECK(sb == rb, "RcclComm.a2av: own segment sizes differ");
         if (sb > 0) WH_HIP_CHECK_HOST(hipMemcpyAsync(rp + ro, sp + so, (size_t)sb,
                                                      hipMemcpyDeviceToDevice, s));

@@ -617,29 +617,15 @@ __global__ __launch_bounds__(kThreads) void k_bwd_v(const int64_t* __restrict__ 
                                                     float* __restrict__ gw_out,
                                                     float* __restrict__ gvc,
                                                     float* __restrict__ part_gw,
-                                                    float* __restrict__ part_gv, int xcd) {
+                                                    float* __restrict__ part_gv) {
   using S = Shape<G>;
   __shared__ int2 stage[kThreads / 64][64];
   int2* st = stage[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63, gl = lane & (G - 1), sub = lane / G;
   const int64_t nch_all = *nchunk_p;
-  // XCD-aware split (xcd != 0, grid a multiple of 8): the chunk list is
-  // ordered by the first row a chunk touches, and blocks b, b + 8, ... share
-  // one XCD's L2 (round-robin dispatch), so group b % 8 takes the b % 8-th
-  // eighth of the list: an XCD's xv gathers then cover ~1/8 of the rows
-  // (3.2 MB of 25.6 MB at 100k rows) and stay in its 4 MB L2 instead of
-  // every XCD sweeping all rows.
-  int64_t lo = 0, nch = nch_all, nw = (int64_t)gridDim.x * (kThreads / 64);
-  int64_t w0 =
+  const int64_t nch = nch_all, nw = (int64_t)gridDim.x * (kThreads / 64);
+  const int64_t w0 =
       __builtin_amdgcn_readfirstlane((int)(((int64_t)blockIdx.x * kThreads + threadIdx.x) >> 6));
-  if (xcd && (gridDim.x & 7) == 0) {
-    const int grp = blockIdx.x & 7;
-    lo = nch_all * grp / 8;
-    nch = nch_all * (grp + 1) / 8;
-    nw = (int64_t)(gridDim.x >> 3) * (kThreads / 64);
-    w0 = lo + __builtin_amdgcn_readfirstlane((int)(((int64_t)(blockIdx.x >> 3) * kThreads +
-                                                    threadIdx.x) >> 6));
-  }
   auto get_meta = [&](int64_t c) {
     return c < nch ? meta[c] : make_int4(0, 0, 0, -1);
   };
@@ -874,19 +860,7 @@ static int resident_blocks(K kernel, int cap) {
   return n < cap ? n : cap;
 }
 
-// WH_FM_BLOCKS_PER_CU overrides the occupancy query (experiments)
-static int blocks_override(int cap) {
-  static int per_cu = [] {
-    const char* e = std::getenv("WH_FM_BLOCKS_PER_CU");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (per_cu <= 0) return 0;
-  return std::min(per_cu * device_cus(), cap);
-}
-
-#define WH_RESIDENT(G, KERNEL, CAP)                                              \
-  (blocks_override(CAP) > 0 ? blocks_override(CAP) : WH_RESIDENT_Q(G, KERNEL, CAP))
-#define WH_RESIDENT_Q(G, KERNEL, CAP)                                            \
+#define WH_RESIDENT(G, KERNEL, CAP)                                            \
   ((G) == 1 ? resident_blocks(KERNEL<1>, CAP) : (G) == 2 ? resident_blocks(KERNEL<2>, CAP) \
    : (G) == 4 ? resident_blocks(KERNEL<4>, CAP) : (G) == 8 ? resident_blocks(KERNEL<8>, CAP) \
    : (G) == 16 ? resident_blocks(KERNEL<16>, CAP) : (G) == 32 ? resident_blocks(KERNEL<32>, CAP) \
@@ -1006,19 +980,13 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
   const int G = vstride / 4;
   int64_t vblk = std::min<int64_t>((v_cap(nuniq, nnz) + 3) / 4,
                                    WH_RESIDENT(G, k_bwd_v, 2048));
-  // XCD-aware chunk split (k_bwd_v; WH_BWD_XCD=1, a grid of whole groups of
-  // 8 blocks): its L2 hit rate rises 44.5 -> 54.7 % and the kernel alone is
-  // 5 % faster, but the step lost 1.5 % on one MI355X (137.0 / 137.7 vs
-  // 139.1 / 139.4 M ex/s: the groups' uneven ends leave a tail beside the
-  // concurrent localize), so the plain round-robin walk is the default
-  static const int xcd = [] {
-    const char* e = std::getenv("WH_BWD_XCD");
-    return e && std::string(e) == "1" ? 1 : 0;
-  }();
-  if (xcd && vblk >= 64) vblk -= vblk % 8;
+  // (an XCD-aware split of the chunk list -- group b % 8 of the blocks on
+  // the b % 8-th eighth -- raised this kernel's L2 hit rate 44.5 -> 54.7 %
+  // but cost the step 1.5 %: the groups' uneven ends leave a tail beside the
+  // concurrent localize; measured round 4, removed)
   const dim3 grid((unsigned)vblk), block(kThreads);
   WH_DISPATCH_G(G, k_bwd_v, grid, block, 0, s, off_v + nuniq, meta_sorted, csc_row, csc_val,
-                dual, xv, vc, vstride, gw, gvc, pgv_w, pgv, xcd);
+                dual, xv, vc, vstride, gw, gvc, pgv_w, pgv);
   if (det_part)
     hipLaunchKernelGGL(k_bwd_reduce_v, dim3(grid_for(vcap * 64, kThreads)), dim3(kThreads), 0, s,
                        off_v + nuniq, meta_v, csc_off, pgv_w, pgv, vstride, gw, gvc);

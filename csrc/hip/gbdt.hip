@@ -299,70 +299,6 @@ __global__ void k_scatter(const int32_t* __restrict__ ridx, int64_t n,
   out[dst] = ridx[i];
 }
 
-// Partition flags and their exclusive scan in ONE pass (decoupled look-back,
-// wh_lookback.h): replaces goleft -> tile_sum -> scan_partials -> tile_scan
-// and the int32 flag array; lscan[i] = rows before i that go left, lscan[n] =
-// all of them. The scatter recovers row i's flag as lscan[i+1] - lscan[i].
-constexpr int kPartPer = 4;
-constexpr int kPartTile = 256 * kPartPer;
-
-__global__ __launch_bounds__(256) void k_goleft_scan(
-    const uint8_t* __restrict__ B, const uint8_t* __restrict__ Bc, int64_t nrows, int f,
-    const int32_t* __restrict__ ridx, int64_t n, const int32_t* __restrict__ pos_node,
-    const int32_t* __restrict__ node_feat, const int32_t* __restrict__ node_bin,
-    const uint8_t* __restrict__ node_defl, Lookback lb, int ntiles, int32_t* __restrict__ lscan) {
-  __shared__ uint32_t shs[16];
-  __shared__ int sht;
-  const int tile = lb_tile(lb, ntiles, &sht);
-  const int64_t i0 = (int64_t)tile * kPartTile + threadIdx.x * kPartPer;
-  int nd[kPartPer], rw[kPartPer];
-#pragma unroll
-  for (int r = 0; r < kPartPer; ++r) {
-    const bool ok = i0 + r < n;
-    nd[r] = ok ? pos_node[i0 + r] : -1;
-    rw[r] = ok ? ridx[i0 + r] : 0;
-  }
-  uint32_t l[kPartPer];
-#pragma unroll
-  for (int r = 0; r < kPartPer; ++r) {
-    const int feat = nd[r] >= 0 ? node_feat[nd[r]] : -1;
-    l[r] = 0;
-    if (feat >= 0) {
-      const int b = Bc ? Bc[(int64_t)feat * nrows + rw[r]] : B[(int64_t)rw[r] * f + feat];
-      l[r] = (b == kMissing) ? (uint32_t)node_defl[nd[r]] : (b <= node_bin[nd[r]] ? 1u : 0u);
-    }
-  }
-  uint32_t v[1] = {l[0] + l[1] + l[2] + l[3]}, ex[1], tot[1];
-  lb_block_scan<1>(lb, tile, v, ex, tot, shs);
-  uint32_t run = ex[0];
-#pragma unroll
-  for (int r = 0; r < kPartPer; ++r) {
-    if (i0 + r < n) lscan[i0 + r] = (int32_t)run;
-    run += l[r];
-  }
-  if (tile == ntiles - 1 && threadIdx.x == 255) lscan[n] = (int32_t)tot[0];
-}
-
-__global__ void k_scatter32(const int32_t* __restrict__ ridx, int64_t n,
-                            const int32_t* __restrict__ pos_node,
-                            const int32_t* __restrict__ node_feat,
-                            const int32_t* __restrict__ seg_beg, const int32_t* __restrict__ nleft,
-                            const int32_t* __restrict__ lscan, int32_t* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int nd = pos_node[i];
-  if (nd < 0 || node_feat[nd] < 0) {
-    out[i] = ridx[i];
-    return;
-  }
-  const int64_t b = seg_beg[nd];
-  const int32_t li = lscan[i];
-  const int64_t lbefore = li - lscan[b];
-  const bool left = lscan[i + 1] != li;
-  const int64_t dst = left ? b + lbefore : b + nleft[nd] + ((i - b) - lbefore);
-  out[dst] = ridx[i];
-}
-
 __global__ void k_leaf_add(const int32_t* __restrict__ ridx, int64_t n,
                            const int32_t* __restrict__ pos_node, const float* __restrict__ leaf,
                            float* __restrict__ margin) {
@@ -710,26 +646,6 @@ void gbdt_scatter(const int32_t* ridx, int64_t n, const int32_t* pos_node, const
                      node_feat, seg_beg, nleft, left, lscan, out);
 }
 
-bool gbdt_partition_fused(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f,
-                          const int32_t* ridx, int64_t n, const int32_t* pos_node,
-                          const int32_t* node_feat, const int32_t* node_bin,
-                          const uint8_t* node_defl, const Lookback& lb, int32_t* lscan,
-                          hipStream_t s) {
-  const int64_t ntiles = (n + kPartTile - 1) / kPartTile;
-  if (n <= 0 || ntiles > kLbMaxTiles || n >= (int64_t)INT32_MAX) return false;
-  hipLaunchKernelGGL(k_goleft_scan, dim3((unsigned)ntiles), dim3(256), 0, s, B, Bc, nrows, f,
-                     ridx, n, pos_node, node_feat, node_bin, node_defl, lb, (int)ntiles, lscan);
-  return true;
-}
-
-void gbdt_scatter32(const int32_t* ridx, int64_t n, const int32_t* pos_node,
-                    const int32_t* node_feat, const int32_t* seg_beg, const int32_t* nleft,
-                    const int32_t* lscan, int32_t* out, hipStream_t s) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_scatter32, dim3(grid_for(n, 256)), dim3(256), 0, s, ridx, n, pos_node,
-                     node_feat, seg_beg, nleft, lscan, out);
-}
-
 void gbdt_leaf_add(const int32_t* ridx, int64_t n, const int32_t* pos_node, const float* leaf,
                    float* margin, hipStream_t s) {
   if (n <= 0) return;
@@ -874,13 +790,13 @@ void gbdt_gpair(int64_t n, const float* margin, const float* label, const float*
 
 void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, int nn, const int32_t* feat, const int32_t* bin,
                     const uint8_t* defl, const int32_t* left, const int32_t* right,
-                    const float* val, float* margin, hipStream_t s) {
+                    const float* val, float* margin, hipStream_t s, bool lds) {
   if (n <= 0) return;
-  const size_t lds = (size_t)nn * 8 + (size_t)kWalkRows * f;
-  if (nn > 0 && nn <= 65535 && f <= kWalkMaxF && lds <= 48 * 1024 &&
-      (reinterpret_cast<uintptr_t>(B) & 3) == 0 && getenv("WH_GBDT_WALK") == nullptr) {
+  const size_t lbytes = (size_t)nn * 8 + (size_t)kWalkRows * f;
+  if (nn > 0 && nn <= 65535 && f <= kWalkMaxF && lbytes <= 48 * 1024 &&
+      (reinterpret_cast<uintptr_t>(B) & 3) == 0 && lds) {
     hipLaunchKernelGGL(k_leaf_walk_lds, dim3((unsigned)((n + kWalkRows - 1) / kWalkRows)),
-                       dim3(kWalkRows), lds, s, B, n, f, nn, feat, bin, defl, left, right, val,
+                       dim3(kWalkRows), lbytes, s, B, n, f, nn, feat, bin, defl, left, right, val,
                        margin);
     return;
   }

@@ -391,18 +391,11 @@ void kmeans_pack_x(const float* X, int64_t n, int f, float* Xp, hipStream_t s) {
 }
 
 // the block-tiled kernel handles F <= 128; wider rows use the streamed kernel.
-// NSUB = centroid subtiles of 32 per LDS chunk (WH_KMEANS_NSUB, default 2: measured
-// 32.8 vs 27.2 iter/s at 10M x 128, k=1000 -- two 32-wide subtiles keep
-// more waves resident per CU than four).
+// NSUB = centroid subtiles of 32 per LDS chunk: 2 (measured 32.8 vs 27.2
+// iter/s against 4 at 10M x 128, k=1000 -- two 32-wide subtiles keep more
+// waves resident per CU than four).
 static bool blocked(int f) { return kmeans_ks(f) <= 64; }
-static int nsub() {
-  static int v = 0;
-  if (v == 0) {
-    const char* e = getenv("WH_KMEANS_NSUB");
-    v = (e && atoi(e) == 4) ? 4 : 2;
-  }
-  return v;
-}
+static constexpr int nsub() { return 2; }
 
 int64_t kmeans_cp_elems(int k, int f) {
   const int ks = kmeans_ks(f);
@@ -460,8 +453,7 @@ void kmeans_assign(const float* Xp, int64_t n, int f, const float* Cp, int k, in
   if (blocked(f)) {
     const int ns = nsub(), nchunk = (k + 32 * ns - 1) / (32 * ns);
     const dim3 grid((unsigned)((ntiles + 3) / 4));
-    if (ns == 2) launch_blk<2>(ks, grid, s, Xp, n, Cp, nchunk, k, assign, score);
-    else launch_blk<4>(ks, grid, s, Xp, n, Cp, nchunk, k, assign, score);
+    launch_blk<nsub()>(ks, grid, s, Xp, n, Cp, nchunk, k, assign, score);
     return;
   }
   const int nchunk = (k + 31) / 32;
@@ -1097,8 +1089,7 @@ void kmeans_assign_x3(const void* Xp, const float* xnorm, const float* X, int64_
   if (n <= 0) return;
   const int ks = x3_ks(f);
   const int nchunk = (k + 32 * kX3Nsub - 1) / (32 * kX3Nsub);
-  // persistent grid: one workgroup per CU (128 KiB of LDS each), or one per
-  // row group with WH_X3_PERSIST=0
+  // persistent grid: one workgroup per CU (128 KiB of LDS each)
   const int64_t ngroups = ((n + 31) / 32 + kX3Waves - 1) / kX3Waves;
   static int ncu = [] {
     int dev = 0, v = 256;
@@ -1107,11 +1098,7 @@ void kmeans_assign_x3(const void* Xp, const float* xnorm, const float* X, int64_
       v = 256;
     return v;
   }();
-  static const bool persist = [] {
-    const char* e = std::getenv("WH_X3_PERSIST");
-    return !(e && e[0] == '0');
-  }();
-  const int64_t g = persist ? std::min<int64_t>(ngroups, ncu) : ngroups;
+  const int64_t g = std::min<int64_t>(ngroups, ncu);
   const dim3 grid((unsigned)g), block(kX3Threads);
   // eps: 3 * 2^-18 for the split + 2^-24 * (3 * 16 * ks) for the fp32 sums, x2 margin
   const float eps = 2.f * (3.f / 262144.f + (48.f * ks) / 16777216.f);

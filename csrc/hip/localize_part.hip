@@ -239,7 +239,7 @@ __global__ __launch_bounds__(kScatThreads, 4) void k_part_scatter(
     const int64_t* __restrict__ off, int64_t nrows, int R, int nshard, int npo_bits, int stride,
     int nho, int ndig, PartHeavy hv, const int64_t* __restrict__ base,
     const uint32_t* __restrict__ gpre, const uint32_t* __restrict__ tpre, uint64_t* __restrict__ pk,
-    int32_t* __restrict__ pr, float* __restrict__ pv, int32_t* __restrict__ pos_of, int swz) {
+    int32_t* __restrict__ pr, float* __restrict__ pv, int32_t* __restrict__ pos_of) {
   extern __shared__ __align__(16) unsigned char lds[];
   uint32_t* gbase = reinterpret_cast<uint32_t*>(lds);   // next free position per digit
   uint32_t* cnt = gbase + ndig;                          // chunk counts -> chunk starts
@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kScatThreads, 4) void k_part_scatter(
   // neighbouring tiles write neighbouring runs of every partition (often the
   // same 128-byte lines): an XCD takes a contiguous range of tiles so those
   // partial-line writes merge in its L2
-  const int64_t tile = swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
   int64_t r0, r1;
   tile_rows(tile, nrows, R, r0, r1);
   const int nr = (int)(r1 - r0);
@@ -624,10 +624,10 @@ __global__ __launch_bounds__(kDedupThreads, 8) void k_part_dedup(
 // partly contiguous (a tile's non-zeros of one partition sit together).
 __global__ __launch_bounds__(256) void k_part_lid(const int32_t* __restrict__ pos_of,
                                                   const int32_t* __restrict__ plid, int64_t nnz,
-                                                  int32_t* __restrict__ lid, int swz) {
+                                                  int32_t* __restrict__ lid) {
   // contiguous block ranges per XCD: the runs of pos_of a tile reads in
   // every partition sit next to its neighbour tiles' runs (same plid lines)
-  const int64_t b = swz ? xcd_swizzle(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t b = xcd_swizzle(blockIdx.x, gridDim.x);
   const int64_t j0 = (b * 256 + threadIdx.x) * 4;
   if (j0 + 3 < nnz) {
     const int4 p = *reinterpret_cast<const int4*>(pos_of + j0);
@@ -644,17 +644,6 @@ __global__ void k_part_empty(int nshard, int64_t* owner_cnt, int64_t* csc_off) {
 
 }  // namespace
 
-// WH_LOC_XCD=0: the scatter and the lid gather take tiles in dispatch order
-// (A/B of the XCD-contiguous tile ranges)
-static int loc_swizzle() {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = getenv("WH_LOC_XCD");
-    on = (e && e[0] == '0') ? 0 : 1;
-  }
-  return on;
-}
-
 PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, bool heavy) {
   PartPlan pl;
   pl.ok = false;
@@ -664,12 +653,7 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
   // scatter)
   // as few hashed partitions as fit: ~2K distinct ids each at the estimate
   // (<= 3K, i.e. LDS load <= 0.75 before the estimate's own 25% headroom)
-  static int64_t target = -1;  // WH_LOC_PART_IDS: tuning knob (distinct ids per partition)
-  if (target < 0) {
-    const char* e = getenv("WH_LOC_PART_IDS");
-    target = e ? atoll(e) : 2048;
-    if (target < 256 || target > 3072) target = 2048;
-  }
+  constexpr int64_t target = 2048;  // distinct ids per partition
   int npo_bits = 0;
   while (((int64_t)nshard << (npo_bits + 1)) * target <= uest) ++npo_bits;
   while (((int64_t)nshard << npo_bits) * 3072 < uest) ++npo_bits;
@@ -677,26 +661,16 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
   // fill the GPU: <= ~16K non-zeros each. A minibatch of few distinct ids
   // (18.6K per 100K rows in bench_e2e.py's Criteo text) otherwise got 32
   // partitions of ~120K non-zeros: 0.66 ms of dedup on 32 workgroups.
-  static int64_t per_part = -1;  // WH_LOC_NNZ_PART: non-zeros per partition (target)
-  if (per_part < 0) {
-    const char* e = getenv("WH_LOC_NNZ_PART");
-    per_part = e ? atoll(e) : 16384;
-    if (per_part < 512) per_part = 16384;
-  }
+  constexpr int64_t per_part = 16384;  // non-zeros per partition (target)
   while (((int64_t)nshard << npo_bits) * per_part < nnz &&
          ((int64_t)nshard << (npo_bits + 1)) <= kPartMaxDigits / 2)
     ++npo_bits;
-  // and never fewer than WH_LOC_MIN_PARTS (128) hashed partitions: the
+  // and never fewer than 128 hashed partitions: the
   // linear step's 10K-row minibatch (390K non-zeros, ~94K distinct ids over
   // 8 owners) otherwise got 32, so 32 dedup workgroups (dedup 35 -> 30 us;
   // linear loopback 8 51.9 -> 54.5 M ex/s on one box, inside the
   // run-to-run spread on another; 256 measured no better)
-  static int64_t min_parts = -1;
-  if (min_parts < 0) {
-    const char* e = getenv("WH_LOC_MIN_PARTS");
-    min_parts = e ? atoll(e) : 128;
-    if (min_parts < 1) min_parts = 1;
-  }
+  constexpr int64_t min_parts = 128;
   while (((int64_t)nshard << npo_bits) < min_parts &&
          ((int64_t)nshard << (npo_bits + 1)) <= kPartMaxDigits / 2)
     ++npo_bits;
@@ -707,13 +681,7 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
     // owners by the hash, so 128 / nshard per owner covers the same ids as
     // 128 on one shard, and the digit count (hence the scatter's run length)
     // stays that of one shard
-    // WH_LOC_HEAVY: heavy-id partitions over all owners (a power of two)
-    static int64_t htotal = -1;
-    if (htotal < 0) {
-      const char* e = getenv("WH_LOC_HEAVY");
-      htotal = e ? atoll(e) : kPartHeavyTotal;
-      if (htotal < 1 || htotal > kPartMaxHeavy) htotal = kPartHeavyTotal;
-    }
+    constexpr int64_t htotal = kPartHeavyTotal;
     nho = (int)htotal;
     while (nho > 1 && (int64_t)nho * nshard > htotal) nho >>= 1;
     while (nho > 1 && (int64_t)nho * nshard > kPartMaxHeavy) nho >>= 1;
@@ -729,14 +697,9 @@ PartPlan loc_part_plan(int64_t nnz, int64_t nrows, int nshard, int64_t uest, boo
   // tiles of R whole rows, ~4096 non-zeros each (8192 halves the histogram
   // but leaves too few workgroups: hist 28 -> 37 us, scatter 64 -> 80 us)
   // A small minibatch takes smaller tiles, down to 1024 non-zeros, for at
-  // least WH_LOC_MIN_TILES (256) histogram / scatter workgroups: the linear
-  // step's 10K rows made 96 tiles of 4096.
-  static int64_t min_tiles = -1;
-  if (min_tiles < 0) {
-    const char* e = getenv("WH_LOC_MIN_TILES");
-    min_tiles = e ? atoll(e) : 256;
-    if (min_tiles < 1) min_tiles = 1;
-  }
+  // least 256 histogram / scatter workgroups: the linear step's 10K rows
+  // made 96 tiles of 4096.
+  constexpr int64_t min_tiles = 256;
   int64_t tile_nnz = nnz / min_tiles;
   tile_nnz = tile_nnz < 1024 ? 1024 : (tile_nnz > 4096 ? 4096 : tile_nnz);
   const int64_t avg = (nnz + nrows - 1) / nrows;
@@ -772,7 +735,7 @@ void loc_part_scatter(const uint64_t* keys, const float* val, const int64_t* off
   const size_t lds = scatter_lds_bytes(pl.ndig, val != nullptr) + 16;
   hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)pl.ntiles), dim3(kScatThreads), lds, s, keys,
                      val, offset, nrows, pl.R, nshard, pl.npo_bits, pl.stride, pl.nho, pl.ndig, hv,
-                     base, gpre, tpre, pk, pr, pv, pos_of, loc_swizzle());
+                     base, gpre, tpre, pk, pr, pv, pos_of);
 }
 
 void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const float* pv, int64_t nnz,
@@ -791,7 +754,7 @@ void loc_part_dedup(const uint64_t* pk, const int32_t* pr, const float* pv, int6
 void loc_part_lid(const int32_t* pos_of, const int32_t* plid, int64_t nnz, int32_t* lid,
                   hipStream_t s) {
   hipLaunchKernelGGL(k_part_lid, dim3((unsigned)((nnz + 1023) / 1024)), dim3(256), 0, s, pos_of,
-                     plid, nnz, lid, loc_swizzle());
+                     plid, nnz, lid);
 }
 
 void loc_part_empty(int nshard, int64_t* owner_cnt, int64_t* csc_off, hipStream_t s) {

@@ -482,14 +482,6 @@ void gbdt_scatter(const int32_t* ridx, int64_t n, const int32_t* pos_node, const
                   const int64_t* lscan, int32_t* out, hipStream_t s);
 // partition flags + exclusive scan in one look-back pass: lscan int32 [n + 1]
 // (false when n needs more than kLbMaxTiles tiles: use goleft + scan_i32)
-bool gbdt_partition_fused(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f,
-                          const int32_t* ridx, int64_t n, const int32_t* pos_node,
-                          const int32_t* node_feat, const int32_t* node_bin,
-                          const uint8_t* node_defl, const Lookback& lb, int32_t* lscan,
-                          hipStream_t s);
-void gbdt_scatter32(const int32_t* ridx, int64_t n, const int32_t* pos_node,
-                    const int32_t* node_feat, const int32_t* seg_beg, const int32_t* nleft,
-                    const int32_t* lscan, int32_t* out, hipStream_t s);
 void gbdt_leaf_add(const int32_t* ridx, int64_t n, const int32_t* pos_node, const float* leaf,
                    float* margin, hipStream_t s);
 // best split per node over hist [S, F, nbin, 2] (double) and totals [S, 2]:
@@ -530,7 +522,7 @@ void gbdt_gpair(int64_t n, const float* margin, const float* label, const float*
                 bool logistic, float* gpair, double* scratch, double* stats, hipStream_t s);
 void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, int nn, const int32_t* feat, const int32_t* bin,
                     const uint8_t* defl, const int32_t* left, const int32_t* right,
-                    const float* val, float* margin, hipStream_t s);
+                    const float* val, float* margin, hipStream_t s, bool lds = true);
 void gbdt_predict(const float* X, int64_t n, int f, const int32_t* feat, const float* thr,
                   const int32_t* left, const int32_t* right, const uint8_t* defl,
                   const float* leaf, float* margin, hipStream_t s);

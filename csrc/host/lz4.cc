@@ -180,20 +180,15 @@ int LZ4Decompress(const char* src, char* dst, int csize, int cap) {
         m += 8;
       } while (op < mend);
     } else if (oend - mend >= 8) {
-      // short offset: replicate the period byte-wise once, then copy in
-      // 8-byte steps from a source at least 8 behind
+      // short offset (period off < 8): write the first 8 bytes byte-wise,
+      // then copy 8 bytes at a time from `step` behind -- the smallest
+      // multiple of the period that is >= 8, so source and destination never
+      // overlap and the source lies in bytes already written (op + 8 - step
+      // > op - off = m)
+      const size_t off = (size_t)(op - m);
       for (size_t i = 0; i < 8; ++i) op[i] = m[i];
-      char* q = op + 8;
-      const char* r = m + 8;
-      while (q < mend) {
-        if (q - r >= 8) {
-          std::memcpy(q, r, 8);
-          q += 8;
-          r += 8;
-        } else {
-          *q++ = *r++;
-        }
-      }
+      const size_t step = off * ((8 + off - 1) / off);
+      for (char* q = op + 8; q < mend; q += 8) std::memcpy(q, q - step, 8);
     } else {
       for (size_t i = 0; i < mlen; ++i) op[i] = m[i];  // overlapping (short offset)
     }

@@ -200,18 +200,21 @@ void CRBDecode(const char* data, size_t size, RowBlock* blk) {
   const int nrows = get_int();
   blk->label.resize(nrows);
   if (!section(blk->label.data(), nrows * sizeof(float))) blk->label.assign(nrows, 0.f);
-  std::vector<size_t> off(nrows + 1);
+  std::vector<size_t> off(nrows + 1, 0);
   section(off.data(), (nrows + 1) * sizeof(size_t));
   blk->offset.assign(off.begin(), off.end());
   const int64_t base = blk->offset[0];
   for (auto& o : blk->offset) o -= base;
   const int nnz = (int)blk->offset.back();
+  // (a record whose rows hold non-zeros must carry the index section)
   if (isz == 8) {
     blk->index.resize(nnz);
-    section(blk->index.data(), nnz * sizeof(uint64_t));
+    WH_CHECK(section(blk->index.data(), nnz * sizeof(uint64_t)) || nnz == 0,
+             "crb record has non-zeros but no index section");
   } else {
     std::vector<uint32_t> tmp(nnz);
-    section(tmp.data(), nnz * sizeof(uint32_t));
+    WH_CHECK(section(tmp.data(), nnz * sizeof(uint32_t)) || nnz == 0,
+             "crb record has non-zeros but no index section");
     blk->index.assign(tmp.begin(), tmp.end());
   }
   blk->value.resize(nnz);

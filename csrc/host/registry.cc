@@ -327,27 +327,29 @@ class PyBlockIter {
     py::object wt = out.w.defined() ? py::cast(out.w) : py::none();
     return py::make_tuple(out.k, out.o, val, out.l, wt);
   }
+  // f(i, w): item i on worker w (0 <= w < nthreads; worker 0 is the
+  // calling thread)
   template <class F>
   static void parallel(size_t n, int nthreads, F&& f) {
     std::atomic<size_t> next{0};
-    auto work = [&] {
-      for (size_t i = next++; i < n; i = next++) f(i);
+    auto work = [&](int w) {
+      for (size_t i = next++; i < n; i = next++) f(i, w);
     };
     const int nt = (int)std::min<size_t>((size_t)nthreads, n);
     std::vector<std::thread> th;
     std::exception_ptr err;
     std::mutex em;
-    auto guarded = [&] {
+    auto guarded = [&](int w) {
       try {
-        work();
+        work(w);
       } catch (...) {
         std::lock_guard<std::mutex> lk(em);
         if (!err) err = std::current_exception();
         next = n;
       }
     };
-    for (int t = 1; t < nt; ++t) th.emplace_back(guarded);
-    guarded();
+    for (int t = 1; t < nt; ++t) th.emplace_back(guarded, t);
+    guarded(0);
     for (auto& t : th) t.join();
     if (err) std::rethrow_exception(err);
   }
@@ -393,7 +395,7 @@ class PyBlockIter {
         py::gil_scoped_acquire g;
         return py::none();
       }
-      parallel(fresh.size(), ndec_, [&](size_t i) { CRBDecodeOffsets(fresh[i].get()); });
+      parallel(fresh.size(), ndec_, [&](size_t i, int) { CRBDecodeOffsets(fresh[i].get()); });
       int64_t nnz = 0;
       bool any_v = false, any_w = false;
       for (auto& pc : pieces) {
@@ -410,12 +412,18 @@ class PyBlockIter {
       float* wp = any_w ? out.w.data_ptr<float>() : nullptr;
       op[0] = 0;
       std::atomic<bool> non_one{false};
-      parallel(pieces.size(), ndec_, [&](size_t i) {
-        thread_local std::vector<char> tmp;
+      // per-worker LZ4 scratch kept across calls (the workers are new
+      // threads each call: a thread_local buffer was re-allocated per block)
+      if (scratch_.size() < (size_t)std::max(ndec_, 1)) scratch_.resize(std::max(ndec_, 1));
+      parallel(pieces.size(), ndec_, [&](size_t i, int w) {
+        std::vector<char>& tmp = scratch_[w];
         const Piece& pc = pieces[i];
         const CRBRecord& r = *pc.r;
         const int64_t n = pc.r1 - pc.r0, s = r.off[pc.r0], e = r.off[pc.r1];
-        CRBDecodeRows(r, 2, pc.r0, pc.r1, kp + pc.nnz_base, &tmp);
+        // rows with non-zeros need the index section (a record without one
+        // is corrupt: the keys would be left as whatever the block held)
+        if (!CRBDecodeRows(r, 2, pc.r0, pc.r1, kp + pc.nnz_base, &tmp))
+          WH_CHECK(e == s, "crb record has non-zeros but no index section");
         if (!CRBDecodeRows(r, 0, pc.r0, pc.r1, lp + pc.row_base, &tmp))
           std::fill(lp + pc.row_base, lp + pc.row_base + n, 0.f);
         for (int64_t q = 0; q < n; ++q) op[pc.row_base + q + 1] = pc.nnz_base + (r.off[pc.r0 + q + 1] - s);
@@ -493,7 +501,7 @@ class PyBlockIter {
       float* wp = any_w ? out.w.data_ptr<float>() : nullptr;
       op[0] = 0;
       std::atomic<bool> non_one{false};
-      parallel(pieces.size(), ncopy_, [&](size_t i) {
+      parallel(pieces.size(), ncopy_, [&](size_t i, int) {
         const Piece& pc = pieces[i];
         const RowBlock& b = *pc.b;
         const int64_t s = b.offset[pc.r0], e = b.offset[pc.r1], n = pc.r1 - pc.r0;
@@ -523,6 +531,7 @@ class PyBlockIter {
   int64_t rows_;
   bool pinned_;
   int ncopy_, ndec_ = 1;
+  std::vector<std::vector<char>> scratch_;  // next_crb's LZ4 scratch, one per decode worker
   // CRB
   std::unique_ptr<InputSplit> split_;
   std::shared_ptr<CRBRecord> carry_;

@@ -192,8 +192,8 @@ def test_gbdt_native_grower_matches_python_loop(gamma, colsample, hist, monkeypa
     (leaf values looked up before the BFS renumbering) and colsample.  The
     two loops cut rows into different chunks; both histogram precisions must
     give bit-identical sums for any chunking."""
-    monkeypatch.setenv("WH_GBDT_HIST", hist)
     from wormhole_amd.models import gbdt as G
+    monkeypatch.setattr(G, "HIST32", hist == "32")
     from wormhole_amd.parallel.bsp import BSP
     g = torch.Generator().manual_seed(2)
     n, f = 60000, 24
@@ -248,7 +248,7 @@ def test_gbdt_device_level_loop_matches_host_grower(gamma, colsample, depth, mon
     obj = G.Objective(p.objective)
     res = []
     for grower in ("dev", "host"):  # (the builder calls the device loop by default)
-        monkeypatch.setenv("WH_GBDT_GROWER", grower)
+        monkeypatch.setattr(G, "HOST_GROWER", grower == "host")
         margin = torch.zeros(n, device=dev)
         tb = G.TreeBuilder(p, bsp, dm, cuts, B)
         gen = torch.Generator().manual_seed(5)
@@ -369,7 +369,8 @@ def test_native_linear_lookahead_made_on_the_compute_stream(monkeypatch):
     from wormhole_amd.data.synthetic import criteo_batch
     from wormhole_amd.models.linear import LinearLearner
     from wormhole_amd.parallel.comm import Comm
-    monkeypatch.setenv("WH_LINEAR_STEP", "localize")
+    from wormhole_amd.models import linear as L
+    monkeypatch.setattr(L, "DIRECT_STEP", False)
     dev = torch.device("cuda", 0)
     card = [50, 400, 3000, 20, 7, 900, 100000]
     batches = [criteo_batch(3000, 5, s, dev, card) for s in range(8)]
@@ -414,11 +415,11 @@ def test_gbdt_leaf_walk_matches_raw_value_predict(f, walk, monkeypatch):
     pruned tree on the bins (k_leaf_walk); predicting the same (compacted)
     trees on the raw values must give the same margins (missing values,
     gamma pruning included). f = 13: the LDS walk's byte tail (rows not a
-    multiple of 4 bytes); WH_GBDT_WALK: the per-level gather kernel."""
+    multiple of 4 bytes); walk = "global": the global-memory walk kernel."""
     from wormhole_amd.models import gbdt as G
     from wormhole_amd.parallel.bsp import BSP
     if walk:
-        monkeypatch.setenv("WH_GBDT_WALK", walk)
+        monkeypatch.setattr(G, "LEAF_WALK_LDS", False)
     g = torch.Generator().manual_seed(4)
     n = 50000
     X = torch.randn(n, f, generator=g)

@@ -84,6 +84,23 @@ def test_lz4_roundtrip(host, n):
         assert len(host.lz4_compress(a)) < len(a)
 
 
+@pytest.mark.parametrize("period", [1, 2, 3, 5, 7])
+def test_lz4_short_offset_runs(host, period):
+    """Matches whose offset is shorter than 8 bytes (the decoder's period-
+    stepping copy): long periodic runs between literals, lengths that end
+    on and off the 8-byte step."""
+    rng = np.random.default_rng(period)
+    parts = []
+    for run in (9, 16, 17, 63, 64, 1000, 4099):
+        pat = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+        parts.append(rng.integers(0, 256, 11, dtype=np.uint8).tobytes())
+        parts.append((pat * (run // period + 1))[:run])
+    d = b"".join(parts) + b"tail-literals!"
+    c = host.lz4_compress(d)
+    assert len(c) < len(d)
+    assert host.lz4_decompress(c, len(d)) == d
+
+
 def test_lz4_decodes_reference_format(host):
     # hand-built LZ4 block: literal "abcd", match (offset 4, len 8), literals "xyz12"
     blk = bytes([0x44]) + b"abcd" + bytes([4, 0]) + bytes([0x50]) + b"xyz12"

@@ -255,3 +255,33 @@ def test_device_crb_blocks_match_host_records(tmp_path, shuf):
         assert sorted(rows) == sorted(rows_h) and rows != rows_h
     else:
         assert rows == rows_h
+
+
+def test_crb_truncated_record_is_an_error(tmp_path):
+    """A CRB part cut inside its last record (a partial copy, a writer that
+    died) is an error when read, not a silently shorter pass. (Parts are read
+    through a shared mapping: files must not change while being read.)"""
+    host = _native.host()
+    data = _criteo_text(1200, 4)
+    keys_h, off_h, _, lab_h, _ = host.parse_text(data, "criteo")
+    p = tmp_path / "t.crb"
+    w = host.RecordIOWriter(str(p))
+    for a in range(0, 1200, 400):
+        b = a + 400
+        w.write(host.crb_encode(keys_h[off_h[a]:off_h[b]], off_h[a:b + 1] - off_h[a], None,
+                                lab_h[a:b], None))
+    w.close()
+    full = p.read_bytes()
+    it = host.MinibatchIter(str(p), 0, 1, "crb", 300, 0, 1.0, 1, False)
+    n = 0
+    while True:
+        b = it.next()
+        if b is None:
+            break
+        n += int(b[3].numel())
+    assert n == 1200
+    p.write_bytes(full[:len(full) - 100])  # inside the third record
+    it = host.MinibatchIter(str(p), 0, 1, "crb", 300, 0, 1.0, 1, False)
+    with pytest.raises(Exception, match="truncated"):
+        while it.next() is not None:
+            pass

@@ -307,8 +307,12 @@ def _staged_main(rank, world, port, out_dir, model, max_conc):
     """One rank of a gloo-staged group on the shared GPU: the native step
     (kTxStaged) and the Python step train on the same uneven data (rank r
     has 6 - r minibatches of 300 + 100 r rows); this rank's shard must agree."""
+    # bitwise-repeatable kernels (ordered reductions of the hot keys'
+    # gradients): AdaGrad's first steps on an embedding row are ~eta * sign(g),
+    # so float-atomic rounding on a near-zero gradient would flip a row by
+    # 2 eta between ANY two runs, native or not
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world))
+                      WORLD_SIZE=str(world), WH_DETERMINISTIC="1")
     torch.set_num_threads(1)
     from wormhole_amd.config.schema import LinearConfig
     from wormhole_amd.data.synthetic import criteo_batch_cpu
@@ -337,15 +341,25 @@ def _staged_main(rank, world, port, out_dir, model, max_conc):
     (mp_, pp), (mn, pn) = res["0"], res["1"]
     assert mp_.keys() == mn.keys() and len(mp_) > 100
     if model == "difacto":
-        bad = sum(1 for k, (w, c, v) in mp_.items()
-                  if c != mn[k][1] or abs(w - mn[k][0]) > 1e-4 * max(1.0, abs(w)) or
-                  (v is None) != (mn[k][2] is None) or
-                  (v is not None and not torch.allclose(v, mn[k][2], atol=1e-4)))
+        kinds = {"count": 0, "w": 0, "has_v": 0, "v": 0}
+        ex = []
+        for k, (w, c, v) in mp_.items():
+            wn, cn, vn = mn[k]
+            kind = ("count" if c != cn else "has_v" if (v is None) != (vn is None) else
+                    "w" if abs(w - wn) > 1e-4 * max(1.0, abs(w)) else
+                    "v" if v is not None and not torch.allclose(v, vn, atol=1e-4) else None)
+            if kind:
+                kinds[kind] += 1
+                if len(ex) < 4:
+                    ex.append((k, kind, c, cn, w, wn))
+        bad = sum(kinds.values())
+        assert kinds["count"] == 0 and kinds["has_v"] == 0, (kinds, ex)
         nmb = pn[4]
     else:
         bad = sum(1 for k, w in mp_.items() if abs(w - mn[k]) > 1e-4 * max(1.0, abs(w)))
+        kinds, ex = {"w": bad}, []
         nmb = pn[3]
-    assert bad <= len(mp_) // 1000, bad
+    assert bad <= max(2, len(mp_) // 1000), (bad, len(mp_), kinds, ex)
     assert nmb == 6 - rank  # every minibatch of this rank forwarded exactly once
     for a, c in zip(pn, pp):
         assert abs(a - c) <= 1e-3 * max(1.0, abs(a)), (pn, pp)
@@ -620,3 +634,75 @@ def test_native_c10d_all_to_all_three_ranks():
     object cast to c10d::ProcessGroup, a row-wise uneven alltoall_base and
     its work's wait (here over gloo between 3 CPU ranks; RCCL on GPUs)."""
     mp.spawn(_c10d_main, args=(3, _free_port()), nprocs=3, join=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,max_conc", [("difacto", 3), ("difacto", 4), ("linear", 3),
+                                            ("linear", 4)])
+def test_native_deep_pipeline_bounded_drift(model, max_conc):
+    """max_concurrency = tau + 1 > 2 (learn/solver/minibatch_solver.h:284-322:
+    an arbitrary in-flight bound): the native step keeps tau pushes in flight,
+    so a minibatch's pull misses at most the tau previous pushes. Against the
+    strict order (max_concurrency 1): the same keys, feature counts and
+    embedding allocation (both are exact at the open), every minibatch
+    forwarded once, and the training loss within a small drift."""
+    from wormhole_amd.parallel.comm import LoopbackComm
+    dev = torch.device("cuda", 0)
+    if model == "difacto":
+        deep, pd, b = _run(LoopbackComm(4, dev), _conf(max_conc=max_conc), dev, steps=12,
+                           rows=2000)
+        strict, ps, _ = _run(LoopbackComm(4, dev), _conf(max_conc=1), dev, steps=12, rows=2000)
+        md, ms = _model(deep), _model(strict)
+        assert all(md[k][1] == c and (md[k][2] is None) == (v is None)
+                   for k, (w, c, v) in ms.items())
+        i_n, i_ex = 4, 5
+    else:
+        deep, pd, b = _lin_run(LoopbackComm(4, dev), dev, 3, steps=12, rows=2000,
+                               max_conc=max_conc)
+        strict, ps, _ = _lin_run(LoopbackComm(4, dev), dev, 3, max_conc=1, batches=b)
+        md, ms = _lin_model(deep), _lin_model(strict)
+        i_n, i_ex = 3, 4
+    assert deep.psx._nat and deep.psx.tau_max == max_conc - 1
+    assert md.keys() == ms.keys()
+    assert pd[i_n] == ps[i_n] == 12 and pd[i_ex] == ps[i_ex]
+    # (a drift that grows with the staleness: 12 minibatches, tau of them stale)
+    assert abs(pd[0] / pd[i_ex] - ps[0] / ps[i_ex]) < 0.02 * (max_conc - 1)
+    assert not deep.psx._nat.busy  # flushed: every push applied
+
+
+def test_max_concurrency_out_of_range_is_an_error():
+    from wormhole_amd.parallel.comm import LoopbackComm
+    with pytest.raises(ValueError, match="max_concurrency"):
+        _run(LoopbackComm(2, "cpu"), _conf(max_conc=10), "cpu", steps=1)
+    # the Python step pipelines one deep under any larger bound
+    lb, _, _ = _run(LoopbackComm(2, "cpu"), _conf(max_conc=4), "cpu", steps=3)
+    assert lb.psx.tau == 1 and lb.psx.tau_max == 3
+
+
+def _rccl_a2av_main(rank, out_dir):
+    from wormhole_amd import _native
+    hip = _native.hip()
+    torch.cuda.set_device(0)
+    c = hip.RcclComm(bytes(hip.RcclComm.unique_id()), 1, 0, 0)
+    assert c.size == 1 and c.rank == 0
+    g = torch.Generator().manual_seed(3)
+    for rows, width, dt in (([5, 0, 7, 1], 3, torch.float32), ([2, 2, 2, 2, 2, 2, 2, 2], 1,
+                                                               torch.int64),
+                            ([0, 0, 9], 16, torch.float32)):
+        n = sum(rows)
+        x = torch.randint(-1 << 20, 1 << 20, (n, width), generator=g).to(dt).cuda()
+        y = c.a2av(x, rows, rows)  # 1 rank, len(rows) virtual peers: the identity
+        torch.cuda.synchronize()
+        assert y.shape == x.shape and torch.equal(x, y), rows
+    c.close()
+    with open(os.path.join(out_dir, "ok"), "w") as f:
+        f.write("ok\n")
+
+
+@pytest.mark.gpu
+def test_rccl_comm_virtual_peers_identity(tmp_path):
+    """RcclComm.a2av on a 1-rank communicator with P virtual peers (segment 0
+    the own copy, the rest send / recv pairs to self): every row arrives
+    where it left, for uneven and empty segments and any row width."""
+    mp.spawn(_rccl_a2av_main, args=(str(tmp_path),), nprocs=1, join=True)
+    assert (tmp_path / "ok").read_text() == "ok\n"

@@ -11,9 +11,8 @@ CODE = ("import sys; sys.path.insert(0, %r)\n"
 app = sys.argv[1] if len(sys.argv) > 1 else "linear"
 conf = "learn/%s/guide/demo.conf" % app
 modes = [("cpu", {"WH_DEVICE": "cpu"}), ("gpu", {"WH_DEVICE": "auto"}),
-         ("gpu-localize", {"WH_DEVICE": "auto", "WH_LINEAR_STEP": "localize"}),
          ("gpu-hostparse", {"WH_DEVICE": "auto", "WH_DEVICE_PARSE": "0"}),
-         ("gpu-nolookahead", {"WH_DEVICE": "auto", "WH_PS_LOOKAHEAD": "0"})]
+         ("gpu-deterministic", {"WH_DEVICE": "auto", "WH_DETERMINISTIC": "1"})]
 work = "/tmp/demo_modes"
 os.makedirs(work, exist_ok=True)
 if not os.path.exists(os.path.join(work, "learn")):

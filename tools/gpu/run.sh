@@ -2,7 +2,7 @@
 # One GPU call, several bench.py configurations, each REPS times interleaved.
 # Usage: bash tools/gpu/run.sh TAG REPS "name|ENV=v ...|bench args" ...
 #   e.g. bash tools/gpu/run.sh base 2 "d1||" "lb8r||--loopback 8 --loopback-rccl" \
-#          "lin8|WH_STEP_TIMING=1|--model linear --loopback 8"
+#          "lin8|WH_TIMING=step|--model linear --loopback 8"
 # Logs go to gpurun_out/TAG/<name>.<i>.log; one summary line per run is
 # printed and appended to gpurun_out/TAG/summary.txt. The first failing run
 # ends the call (no retries).

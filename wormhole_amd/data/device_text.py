@@ -29,6 +29,7 @@ import os
 import torch
 
 from .. import _native
+from ..utils import trace
 
 def applies(fmt, path, device):
     """Device parsing is used for plain Criteo / libsvm files on a GPU worker,
@@ -135,11 +136,7 @@ class DeviceTextIter:
         # copied by a thread pool (host.BlockIter; one copy per byte)
         self.blocks = fmt == "crb"
         if self.blocks:
-            if os.environ.get("WH_CRB_BLOCKITER", "1") == "0":  # (A/B: the assembling iterator)
-                self.tb = host.MinibatchIter(path, part, nparts, fmt, int(mb * self.per_block), 0,
-                                             1.0, int(seed), True)
-            else:
-                self.tb = host.BlockIter(path, part, nparts, fmt, int(mb * self.per_block), True)
+            self.tb = host.BlockIter(path, part, nparts, fmt, int(mb * self.per_block), True)
         else:
             # several readers over line-aligned sub-ranges of the part, taken
             # round-robin in a fixed order (one reader thread copies ~7 GB/s
@@ -158,7 +155,6 @@ class DeviceTextIter:
             self.gen = torch.Generator(device=device)
             self.gen.manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
         self.stream = _producer_stream(device)
-        depth = int(os.environ.get("WH_TEXT_DEPTH", depth))
         self.q = queue.Queue(maxsize=max(1, depth))
         self.stop = False
         self.done = False
@@ -178,9 +174,9 @@ class DeviceTextIter:
         return False
 
     def _produce(self):
-        # WH_INGEST_TIMING=1: the producer's seconds waiting for the readers,
+        # WH_TIMING=ingest: the producer's seconds waiting for the readers,
         # working (copy / parse / shuffle), and blocked on a full queue
-        timing = os.environ.get("WH_INGEST_TIMING") == "1"
+        timing = trace.timing_on("ingest")
         self.t_read = self.t_work = self.t_put = 0.0
         try:
             import time

@@ -69,7 +69,7 @@ import numpy as np
 import torch
 
 from .. import _native, ops
-from ..utils import streams
+from ..utils import streams, trace
 
 TRAIN, VAL, PRED = 0, 1, 2
 # (Stream placements measured and dropped -- docs/performance.md "Measured
@@ -77,7 +77,7 @@ TRAIN, VAL, PRED = 0, 1, 2
 # localize on a side stream at the open instead of right after this one's
 # localize, C3 issued at the end of the backward instead of behind the next
 # call's C2, a training step's AUC right after its forward.)
-_COMM_TIMING = os.environ.get("WH_COMM_TIMING", "0") not in ("", "0")
+_COMM_TIMING = trace.timing_on("comm")
 # CUs the persistent FM kernels leave free for RCCL's channel workgroups when
 # the exchange runs over RCCL (csrc/hip/fm.hip fm_set_cu_reserve): C2 / C3
 # are issued while a forward / backward holds the machine, and must start
@@ -244,7 +244,17 @@ class Psx:
         if self.cuda and getattr(self.comm, "backend", "") in ("nccl", "loopback-rccl"):
             _native.hip().set_cu_reserve(_CU_RESERVE)
         self.pins = _PinRing(self.dev) if self.cuda else None
-        self.tau = 1 if int(getattr(lrn.conf, "max_concurrency", 2) or 2) >= 2 else 0
+        # staleness: max_concurrency - 1 minibatches may pull before a push
+        # of theirs lands (the reference's in-flight bound,
+        # learn/solver/minibatch_solver.h:284-322). The native step honours
+        # any depth up to 8; this Python step (the oracle, and the payload-
+        # filter configurations) pipelines at most one deep, which stays
+        # within the bound.
+        mc = int(getattr(lrn.conf, "max_concurrency", 2) or 2)
+        if mc < 1 or mc > 9:
+            raise ValueError("max_concurrency must be 1..9 (got %d)" % mc)
+        self.tau_max = mc - 1
+        self.tau = min(self.tau_max, 1)
         self.job = None     # (keys, LocalizeJob | finished tuple, carried step)
         self.pull = None    # opened, reply not yet exchanged
         self.push = None    # push in flight to the owners
@@ -258,7 +268,7 @@ class Psx:
         # bytes this rank sends to OTHER ranks per collective (C0..C3): what
         # crosses xGMI (own-segment rows stay in HBM)
         self.wire = [0, 0, 0, 0]
-        # WH_COMM_TIMING=1: per-collective (issue-ready -> landed) GPU times
+        # WH_TIMING=comm: per-collective (issue-ready -> landed) GPU times
         self.timer = _CollTimer(self.dev) if (self.cuda and _COMM_TIMING) else None
         fb = int(getattr(lrn.conf, "fixed_bytes", 0) or 0)
         if fb not in (0, 1, 2, 3):
@@ -352,7 +362,7 @@ class Psx:
 
     def wire_report(self, steps):
         """Per-step averages since :meth:`wire_reset`: bytes each collective
-        sent to peers (and, with WH_COMM_TIMING=1, its GPU time in ms)."""
+        sent to peers (and, with WH_TIMING=comm, its GPU time in ms)."""
         steps = max(int(steps), 1)
         wire = list(self.wire)
         if self._nat:
@@ -719,7 +729,7 @@ class Psx:
                     lin_hp=list(self.lin_hp) if self.linear else [0.0] * 5,
                     hp=list(lrn.hp), threshold=int(lrn.threshold), l1_shrk=bool(lrn.l1_shrk),
                     seed=int(lrn.seed), loss=int(lrn.loss), met=lrn.met, auc_sum=lrn.auc_sum,
-                    tau=int(self.tau), max_load=float(lrn.kv.guard.max_load),
+                    tau=int(self.tau_max), max_load=float(lrn.kv.guard.max_load),
                     cu_reserve=_CU_RESERVE if tx == hip.PSX_TX_RCCL else 0)
                 self._nat.requests = self.requests
         return self._nat or None

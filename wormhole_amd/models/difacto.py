@@ -11,7 +11,6 @@ learn/difacto/async_sgd.h:363-425), re-expressed on the GPU:
   ->  gradient clip / dropout / normalisation  ->  push  ->  owner applies
   FTRL on w and AdaGrad on V in one fused kernel.
 """
-import os
 
 import torch
 
@@ -76,7 +75,7 @@ class DifactoLearner:
         post = emb is not None and (emb.grad_clipping > 0 or emb.dropout > 0
                                     or bool(emb.grad_normalization))
         self.direct_pull = (self.device.type == "cuda" and comm.size == 1 and self.vstride > 0
-                            and not post and os.environ.get("WH_DIFACTO_PULL", "") != "copy")
+                            and not post)
         self.psx = None
         if comm.size > 1:
             from ..kv.psx import Psx

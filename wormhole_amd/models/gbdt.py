@@ -32,6 +32,11 @@ from ..utils.fs import open_uri  # noqa: E402
 RT_EPS = 1e-6
 MISSING_BIN = 255
 _HIST32_ROWS = 8192  # rows per int32 LDS pass of the GPU histogram
+# Alternate device paths, kept as the tests' cross-checks (process-wide, the
+# same on every rank):
+HIST32 = True  # int32 LDS histogram passes (False: int64 sums throughout)
+LEAF_WALK_LDS = True  # the LDS-resident tree walk when it fits (False: global walk)
+HOST_GROWER = False  # the per-level host grower instead of the device level loop
 
 
 # ------------------------------------------------------------------ params
@@ -675,7 +680,7 @@ class TreeBuilder:
         m = gpair_stats(gpair)[1] if self.dm.n else torch.zeros(2, device=self.device)
         m = m.float().contiguous()
         self.bsp.allreduce(m, op="max")
-        r32 = _HIST32_ROWS if os.environ.get("WH_GBDT_HIST", "32") != "64" else 0
+        r32 = _HIST32_ROWS if HIST32 else 0
         if m.is_cuda:  # one launch (csrc/hip/gbdt.hip k_qscale), same formula as below
             return _native.hip().gbdt_qscale(m, float(self._nglobal), r32)
         e = torch.floor(torch.log2(2.0 ** 61 / (self._nglobal * m.double().clamp_min(1e-30))))
@@ -849,9 +854,9 @@ class TreeBuilder:
             self._cut_lists = (self.cuts.values.tolist(), self.cuts.offsets.tolist())
         ar = self._allreduce_hist if self.bsp.world > 1 else None
         # the level loop on the device (one host read per tree) unless the
-        # per-level host grower is asked for; every rank takes the same one
-        # (WH_GBDT_GROWER is process-wide, set alike on every rank)
-        host = os.environ.get("WH_GBDT_GROWER", "") == "host" or p.max_depth > 10
+        # per-level host grower is asked for (HOST_GROWER, or trees deeper
+        # than the device loop's heap numbering)
+        host = HOST_GROWER or p.max_depth > 10
         kw = dict(B=self.B, Bc=self._Bc, ridx0=self._iota(n), gpair=gpair, qscale=self._qscale,
                   valid=self._valid_dev[1], nbin=self.nbin, fgroups=self.fgroups,
                   max_fcnt=self.max_fcnt, cut_vals=self._cut_lists[0],
@@ -1102,7 +1107,7 @@ class TreeBuilder:
             d = torch.from_numpy(h).to(self.device, non_blocking=True)
             _native.hip().gbdt_leaf_walk(
                 B, d[:nn], d[nn:2 * nn], d[4 * nn:5 * nn].to(torch.uint8), d[2 * nn:3 * nn],
-                d[3 * nn:4 * nn], d[5 * nn:].view(torch.float32), margin)
+                d[3 * nn:4 * nn], d[5 * nn:].view(torch.float32), margin, lds=LEAF_WALK_LDS)
         elif n and self.gpu:
             val = torch.zeros(len(tree.feat), dtype=torch.float32)
             for nd in leaf_segs:

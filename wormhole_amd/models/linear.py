@@ -15,6 +15,10 @@ from ..parallel.comm import LoopbackComm
 from ..utils import trace
 
 TRAIN, VAL, PRED = 0, 1, 2
+# one GPU, one shard: the localize-free native step (per-tile de-duplication,
+# csrc/bind/hip_ops.cc LinearStep) up to ~15k Criteo rows; False keeps the
+# localize path at every size (the tests' cross-check of the two)
+DIRECT_STEP = True
 
 
 class LinearLearner:
@@ -69,7 +73,7 @@ class LinearLearner:
             self._native = _native.hip().LinearStep(
                 store=self.store, algo=int(conf.algo), alpha=conf.lr_eta, beta=conf.lr_beta,
                 l1=conf.lambda_l1, l2=conf.lambda_l2, loss=int(conf.loss),
-                max_load=self.kv.guard.max_load)
+                max_load=self.kv.guard.max_load, direct=DIRECT_STEP)
 
     def _localize(self, keys, offset, val, next_batch):
         return localize_pipelined(self, keys, offset, val, next_batch)

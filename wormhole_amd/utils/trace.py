@@ -13,6 +13,9 @@
 * ``MetricsStream`` -- JSON-lines metrics for benchmark harnesses, enabled by
   ``WH_METRICS=<path>`` (one line per progress report: examples/s and the
   stage breakdown).
+* ``timing_on(what)`` -- the profiling aids listed in ``WH_TIMING``
+  (comma-separated: ``step``, ``step2``, ``loc``, ``ingest``, ``comm``;
+  docs/build.md).
 """
 import contextlib
 import ctypes
@@ -20,6 +23,12 @@ import json
 import os
 import threading
 import time
+
+def timing_on(what):
+    """True when ``what`` is listed in WH_TIMING (the C++ side reads the same
+    variable: csrc/bind/hip_ops.cc timing_on)."""
+    return what in os.environ.get("WH_TIMING", "").split(",")
+
 
 _lock = threading.Lock()
 _acc = {}
