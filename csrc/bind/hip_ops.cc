@@ -1976,11 +1976,18 @@ Tensor spmv_t(const Tensor& csc_off, const Tensor& csc_row, const c10::optional<
   CHECK_IN(csc_row, torch::kInt32);
   CHECK_IN(p, torch::kFloat32);
   c10::DeviceGuard g(p.device());
+  // the linear backward's chunked segmented sums (fm.hip k_chunk_plan /
+  // k_bwd_scalar): a column is cut into chunks of at most a wave's width
+  // and multi-chunk columns are summed across chunks, so a power-law head
+  // (one Criteo value in a third of all rows) costs what its chunk count
+  // costs -- one lane per column serialised such a column (298 ms per
+  // L-BFGS gradient pass at 4M Criteo rows)
   const int64_t ncol = csc_off.numel() - 1;
-  auto y = torch::empty({ncol}, p.options());
-  wh::spmv_t(ncol, ptr<int64_t>(csc_off), ptr<int32_t>(csc_row), optptr<float>(csc_val),
-             ptr<float>(p), ptr<float>(y), cur_stream(p));
-  return y;
+  auto wdummy = torch::empty({ncol}, p.options());  // (vstride 0: never read)
+  auto pl = fm_bwd_alloc(csc_off, csc_row.numel(), ncol, 0, 0);
+  fm_bwd_launch(pl, csc_off, csc_row, optptr<float>(csc_val), ptr<float>(p), nullptr, wdummy,
+                nullptr, 0, p.numel(), 0);
+  return pl[0];
 }
 
 

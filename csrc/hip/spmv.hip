@@ -2,8 +2,9 @@
 // SURVEY §2.5; reference learn/base/spmv.h:72-119 partitions rows / output
 // ranges over OpenMP threads).
 //   spmv   : y = X x           G lanes stride over one CSR row, group reduce
-//   spmv_t : y = X^T p         one lane per CSC column (segmented sum over the
-//                              column's occurrence list: no atomics)
+//   spmv_t : y = X^T p         runs on the linear backward's chunked
+//                              segmented sums (fm.hip; csrc/bind/hip_ops.cc
+//                              spmv_t): skew-robust over power-law columns
 // Columns are the dense local ids produced by `localize`, so the same
 // kernels serve L-BFGS (whole split resident in HBM) and minibatch apps.
 #include "wh_common.h"
@@ -33,23 +34,6 @@ __global__ __launch_bounds__(kThreads) void k_spmv(int64_t nrows, const int64_t*
   if (row < nrows && gl == 0) y[row] = acc;
 }
 
-__global__ __launch_bounds__(kThreads) void k_spmv_t(int64_t ncol, const int64_t* __restrict__ csc_off,
-                                                     const int32_t* __restrict__ csc_row,
-                                                     const float* __restrict__ csc_val,
-                                                     const float* __restrict__ p, float* __restrict__ y) {
-  const int64_t c = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (c >= ncol) return;
-  const int64_t b = csc_off[c], e = csc_off[c + 1];
-  float acc0 = 0.f, acc1 = 0.f;
-  int64_t j = b;
-  for (; j + 1 < e; j += 2) {
-    acc0 += p[csc_row[j]] * (csc_val ? csc_val[j] : 1.f);
-    acc1 += p[csc_row[j + 1]] * (csc_val ? csc_val[j + 1] : 1.f);
-  }
-  if (j < e) acc0 += p[csc_row[j]] * (csc_val ? csc_val[j] : 1.f);
-  y[c] = acc0 + acc1;
-}
-
 }  // namespace
 
 void spmv(int64_t nrows, const int64_t* off, const int32_t* col, const float* val, const float* x,
@@ -60,11 +44,5 @@ void spmv(int64_t nrows, const int64_t* off, const int32_t* col, const float* va
                      off, col, val, x, y);
 }
 
-void spmv_t(int64_t ncol, const int64_t* csc_off, const int32_t* csc_row, const float* csc_val,
-            const float* p, float* y, hipStream_t s) {
-  if (ncol <= 0) return;
-  hipLaunchKernelGGL(k_spmv_t, dim3(grid_for(ncol, kThreads)), dim3(kThreads), 0, s, ncol,
-                     csc_off, csc_row, csc_val, p, y);
-}
 
 }  // namespace wh

@@ -348,9 +348,6 @@ void fm_grad_scale(const int64_t* m, int64_t m_cap, float* gvc, int vstride, int
 // y = X x over CSR (col < 0 entries skipped); y = X^T p over the CSC of localize
 void spmv(int64_t nrows, const int64_t* off, const int32_t* col, const float* val, const float* x,
           float* y, hipStream_t s);
-void spmv_t(int64_t ncol, const int64_t* csc_off, const int32_t* csc_row, const float* csc_val,
-            const float* p, float* y, hipStream_t s);
-
 // ------------------------------------------------------------ metrics.hip
 // exact per-minibatch AUC (reference BinClassEval::AUC) from predictions
 // sorted ascending: area = sum over negatives of #positives ranked below.

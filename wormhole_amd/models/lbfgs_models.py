@@ -165,7 +165,7 @@ class LinearObjective:
         gu = ops.spmv_t(self.d.csc_off, self.d.csc_row, self.d.csc_val, g)
         valid, idx = self._feat()
         grad = torch.zeros_like(w)
-        grad.index_add_(0, idx[valid], gu[valid])
+        grad.index_copy_(0, idx[valid], gu[valid])  # (unique ids: a scatter, no atomics)
         grad[F] = g.sum()
         if self.bsp.rank == 0 and self.reg_L2 != 0.0:
             grad[:F] += self.reg_L2 * w[:F]
