@@ -190,6 +190,10 @@ class PsxStep {
     PsxStP prev = pull_;
     if (prev && !prev->have_v) vcount_exchange(*prev);
     PsxStP st = new_step(send, recv, label, true, data_pass, prev.get());
+    // (C2, C3 and C1 stay three RCCL launches: grouped into one, RCCL split
+    // the group's several operations per peer over serialised launches and
+    // C1, which the open waits for, landed only behind the big C2 / C3 --
+    // measured 74 vs 92 M ex/s on the loopback rehearsal)
     if (prev) c2(*prev);
     // the newest push (its backward ran at the end of the previous call)
     if (!pushes_.empty() && pushes_.back()->gvc.defined()) c3(*pushes_.back());
@@ -313,12 +317,12 @@ class PsxStep {
     if (ready)  // allocated on xs, read on S
       c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), S_stream_);
     rccl_->a2av(xc.data_ptr(), out.data_ptr(), row, send_rows, recv_rows, xs.stream());
+    work->keep = xc;
     if (xs.stream() != S_stream_.stream()) {
       if (!work->ev) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&work->ev, hipEventDisableTiming));
       WH_HIP_CHECK_HOST(hipEventRecord(work->ev, xs.stream()));
       work->pending = true;
     }
-    work->keep = xc;
     return out;
   }
 

@@ -13,9 +13,8 @@
 // The communicator is built with ncclCommInitRank from an id that rank 0
 // makes (unique_id()) and the Python side passes around through the c10d
 // store (wormhole_amd/parallel/comm.py Comm.rccl). A 1-rank communicator
-// stands in for P virtual peers in the one-GPU loopback rehearsal: each
-// virtual peer's segment is then its own send / recv pair to self, so the
-// host and kernel-launch cost of a P-peer group is paid as over xGMI.
+// stands in for P virtual peers in the one-GPU loopback rehearsal (the own
+// segment a device copy, the other P-1 one send / recv pair to self).
 #pragma once
 
 #include <rccl/rccl.h>
@@ -75,9 +74,12 @@ class RcclComm {
   // q's segment for this rank lands at recv's q-th offset. The own segment
   // is a device copy. With a 1-rank communicator and P > 1 row counts (the
   // loopback rehearsal: virtual rank 0 of P) segment 0 is the own copy and
-  // every other segment a send / recv pair to self, the calls a real rank
-  // issues; send_rows must equal recv_rows. Zero-row segments are skipped
-  // on both sides (the row counts are symmetric by construction).
+  // segments 1..P-1 -- contiguous on both sides -- ONE send / recv pair to
+  // self: RCCL serialises several operations to one peer over separate
+  // launches (21 pairs to self per step took 9 launches of ~29 us), which a
+  // real rank's one operation per peer does not pay; send_rows must equal
+  // recv_rows. Zero-row segments are skipped on both sides (the row counts
+  // are symmetric by construction).
   void a2av(const void* send, void* recv, int64_t row_bytes, const std::vector<int64_t>& send_rows,
             const std::vector<int64_t>& recv_rows, hipStream_t s) {
     TORCH_CHECK(comm_ != nullptr, "RcclComm: closed");
@@ -89,17 +91,25 @@ class RcclComm {
     char* rp = static_cast<char*>(recv);
     int64_t so = 0, ro = 0;
     bool open = false;
+    if (virt) {
+      int64_t own = send_rows[0] * row_bytes, rest = 0;
+      for (int q = 0; q < P; ++q) {
+        TORCH_CHECK(send_rows[q] == recv_rows[q],
+                    "RcclComm.a2av: loopback segments must be symmetric");
+        if (q > 0) rest += send_rows[q] * row_bytes;
+      }
+      if (own > 0) WH_HIP_CHECK_HOST(hipMemcpyAsync(rp, sp, (size_t)own, hipMemcpyDeviceToDevice, s));
+      if (rest > 0) {
+        WH_NCCL_CHECK(ncclGroupStart());
+        WH_NCCL_CHECK(ncclSend(sp + own, (size_t)rest, ncclUint8, 0, comm_, s));
+        WH_NCCL_CHECK(ncclRecv(rp + own, (size_t)rest, ncclUint8, 0, comm_, s));
+        WH_NCCL_CHECK(ncclGroupEnd());
+      }
+      return;
+    }
     for (int q = 0; q < P; ++q) {
       const int64_t sb = send_rows[q] * row_bytes, rb = recv_rows[q] * row_bytes;
-      if (virt && q > 0) {
-        TORCH_CHECK(sb == rb, "RcclComm.a2av: loopback segments must be symmetric");
-        if (sb > 0) {
-          if (!open) WH_NCCL_CHECK(ncclGroupStart());
-          open = true;
-          WH_NCCL_CHECK(ncclSend(sp + so, (size_t)sb, ncclUint8, 0, comm_, s));
-          WH_NCCL_CHECK(ncclRecv(rp + ro, (size_t)rb, ncclUint8, 0, comm_, s));
-        }
-      } else if (q == rank_) {  // (virtual: rank_ == 0)
+      if (q == rank_) {
         TORCH_CHECK(sb == rb, "RcclComm.a2av: own segment sizes differ");
         if (sb > 0) WH_HIP_CHECK_HOST(hipMemcpyAsync(rp + ro, sp + so, (size_t)sb,
                                                      hipMemcpyDeviceToDevice, s));

@@ -361,8 +361,12 @@ def _staged_main(rank, world, port, out_dir, model, max_conc):
         nmb = pn[3]
     assert bad <= max(2, len(mp_) // 1000), (bad, len(mp_), kinds, ex)
     assert nmb == 6 - rank  # every minibatch of this rank forwarded exactly once
-    for a, c in zip(pn, pp):
-        assert abs(a - c) <= 1e-3 * max(1.0, abs(a)), (pn, pp)
+    # (the per-minibatch AUC of an early model ranks near-tied predictions:
+    # 1e-6 differences in them move it by up to ~1 %)
+    i_auc = 1 if model == "difacto" else 2
+    for i, (a, c) in enumerate(zip(pn, pp)):
+        tol = 0.02 * nmb if i == i_auc else 1e-3 * max(1.0, abs(a))
+        assert abs(a - c) <= tol, (i, pn, pp)
     comm.barrier()
     with open(os.path.join(out_dir, "r%d" % rank), "w") as f:
         f.write("ok\n")
