@@ -83,6 +83,13 @@ class RcclComm {
   void a2av(const void* send, void* recv, int64_t row_bytes, const std::vector<int64_t>& send_rows,
             const std::vector<int64_t>& recv_rows, hipStream_t s) {
     TORCH_CHECK(comm_ != nullptr, "RcclComm: closed");
+    // the widest element the rows and both buffers allow: RCCL's copy loop
+    // moves elements of the given type (8-byte rows and 256-byte embedding
+    // rows as int64, 12-byte key records as int32)
+    const uintptr_t al = reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv) |
+                         (uintptr_t)row_bytes;
+    const int esz = (al & 7) == 0 ? 8 : (al & 3) == 0 ? 4 : 1;
+    const ncclDataType_t dt = esz == 8 ? ncclInt64 : esz == 4 ? ncclInt32 : ncclUint8;
     const int P = (int)send_rows.size();
     TORCH_CHECK((int)recv_rows.size() == P, "RcclComm.a2av: row vectors differ in length");
     const bool virt = world_ == 1 && P > 1;
@@ -101,8 +108,8 @@ class RcclComm {
       if (own > 0) WH_HIP_CHECK_HOST(hipMemcpyAsync(rp, sp, (size_t)own, hipMemcpyDeviceToDevice, s));
       if (rest > 0) {
         WH_NCCL_CHECK(ncclGroupStart());
-        WH_NCCL_CHECK(ncclSend(sp + own, (size_t)rest, ncclUint8, 0, comm_, s));
-        WH_NCCL_CHECK(ncclRecv(rp + own, (size_t)rest, ncclUint8, 0, comm_, s));
+        WH_NCCL_CHECK(ncclSend(sp + own, (size_t)(rest / esz), dt, 0, comm_, s));
+        WH_NCCL_CHECK(ncclRecv(rp + own, (size_t)(rest / esz), dt, 0, comm_, s));
         WH_NCCL_CHECK(ncclGroupEnd());
       }
       return;
@@ -118,8 +125,8 @@ class RcclComm {
           if (!open) WH_NCCL_CHECK(ncclGroupStart());
           open = true;
         }
-        if (sb > 0) WH_NCCL_CHECK(ncclSend(sp + so, (size_t)sb, ncclUint8, q, comm_, s));
-        if (rb > 0) WH_NCCL_CHECK(ncclRecv(rp + ro, (size_t)rb, ncclUint8, q, comm_, s));
+        if (sb > 0) WH_NCCL_CHECK(ncclSend(sp + so, (size_t)(sb / esz), dt, q, comm_, s));
+        if (rb > 0) WH_NCCL_CHECK(ncclRecv(rp + ro, (size_t)(rb / esz), dt, q, comm_, s));
       }
       so += sb;
       ro += rb;
