@@ -117,13 +117,29 @@ class PsxStep {
       TORCH_CHECK(pg_->getSize() == P && pg_->getRank() == rank,
                   "PsxStep: the process group must have P ranks");
     } else if (tx_ == kTxRccl) {
+      // (c0, c1, c23): RCCL runs every operation of ONE communicator in issue
+      // order, whatever stream it was issued on, so the count exchange C0 and
+      // the keys C1 -- both on the path to the next open -- get
+      // communicators of their own instead of queueing behind the big pull /
+      // push transfers C2 / C3 of earlier minibatches. One communicator for
+      // all three is accepted too (tests).
       TORCH_CHECK(!rccl.is_none(), "PsxStep: the RCCL transport needs a communicator");
-      rccl_ = rccl.cast<std::shared_ptr<RcclComm>>();
-      TORCH_CHECK((rccl_->size() == P && rccl_->rank() == rank) || rccl_->size() == 1,
-                  "PsxStep: the communicator must have P ranks (or 1: loopback rehearsal)");
+      if (py::isinstance<py::sequence>(rccl)) {
+        auto seq = rccl.cast<py::sequence>();
+        TORCH_CHECK(seq.size() == 3, "PsxStep: rccl = (c0, c1, c23) communicators");
+        rccl_c0_ = seq[0].cast<std::shared_ptr<RcclComm>>();
+        rccl_c1_ = seq[1].cast<std::shared_ptr<RcclComm>>();
+        rccl_ = seq[2].cast<std::shared_ptr<RcclComm>>();
+      } else {
+        rccl_ = rccl_c0_ = rccl_c1_ = rccl.cast<std::shared_ptr<RcclComm>>();
+      }
+      for (const auto& c : {rccl_c0_, rccl_c1_, rccl_})
+        TORCH_CHECK((c->size() == P && c->rank() == rank) || c->size() == 1,
+                    "PsxStep: the communicators must have P ranks (or 1: loopback rehearsal)");
     }
     dev_ = store->slots_.device().index();
-    TORCH_CHECK(!rccl_ || rccl_->device() == dev_, "PsxStep: communicator on another device");
+    for (const auto& c : {rccl_c0_, rccl_c1_, rccl_})
+      TORCH_CHECK(!c || c->device() == dev_, "PsxStep: communicator on another device");
     c10::DeviceGuard g(store->slots_.device());
     // streams of our own (as Python's torch.cuda.Stream()): the pool's
     // round-robin streams are shared with other users, and a localize queued
@@ -316,7 +332,8 @@ class PsxStep {
     Tensor out = torch::empty(shape, xc.options());
     if (ready)  // allocated on xs, read on S
       c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), S_stream_);
-    rccl_->a2av(xc.data_ptr(), out.data_ptr(), row, send_rows, recv_rows, xs.stream());
+    (c == 1 ? rccl_c1_ : rccl_)->a2av(xc.data_ptr(), out.data_ptr(), row, send_rows, recv_rows,
+                                      xs.stream());
     work->keep = xc;
     if (xs.stream() != S_stream_.stream()) {
       if (!work->ev) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&work->ev, hipEventDisableTiming));
@@ -345,7 +362,7 @@ class PsxStep {
     // one 32-byte send / recv per peer on the current stream (cs): this tiny
     // exchange sits on the path of the step's one host read
     Tensor r = torch::empty_like(s);
-    rccl_->a2av(s.data_ptr(), r.data_ptr(), sizeof(int64_t), four, four,
+    rccl_c0_->a2av(s.data_ptr(), r.data_ptr(), sizeof(int64_t), four, four,
                 c10::hip::getCurrentHIPStream(dev_).stream());
     return r;
   }
@@ -769,7 +786,7 @@ class PsxStep {
   int vs_ = 0;
   PsxTx tx_ = kTxIdentity;
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;  // kTxStaged
-  std::shared_ptr<RcclComm> rccl_;             // kTxRccl
+  std::shared_ptr<RcclComm> rccl_, rccl_c0_, rccl_c1_;  // kTxRccl: C2 / C3, C0, C1
   c10::DeviceIndex dev_ = 0;
   c10::hip::HIPStream S_stream_ = c10::hip::getDefaultHIPStream();
   c10::hip::HIPStream ls_ = c10::hip::getDefaultHIPStream();

@@ -724,7 +724,8 @@ class Psx:
                     store=self.store, P=self.P, S=self.nshard,
                     rank=int(getattr(self.comm, "rank", 0)), tx=tx,
                     pg=self.comm.pg if tx == hip.PSX_TX_STAGED else None,
-                    rccl=self.comm.rccl() if tx == hip.PSX_TX_RCCL else None,
+                    rccl=(self.comm.rccl("c0"), self.comm.rccl("c1"), self.comm.rccl("c23"))
+                    if tx == hip.PSX_TX_RCCL else None,
                     linear=self.linear,
                     lin_hp=list(self.lin_hp) if self.linear else [0.0] * 5,
                     hp=list(lrn.hp), threshold=int(lrn.threshold), l1_shrk=bool(lrn.l1_shrk),

@@ -117,20 +117,24 @@ class Comm:
             self.size = dist.get_world_size()
 
     # ------------------------------------------------------ native RCCL
-    def rccl(self):
-        """This group's own RCCL communicator (csrc/bind/rccl_comm.h
+    def rccl(self, tag="c23"):
+        """This group's own RCCL communicator ``tag`` (csrc/bind/rccl_comm.h
         RcclComm: grouped ncclSend / ncclRecv per peer, driven from C++ by
-        the multi-shard step). Created on first use by every rank at the
-        same point: rank 0 makes the id and passes it through the c10d
-        store."""
+        the multi-shard step, which keeps one per exchange class: RCCL runs a
+        communicator's operations in issue order). Created on first use by
+        every rank at the same point: rank 0 makes the id and passes it
+        through the c10d store."""
         if self._rccl is None:
+            self._rccl = {}
+        c = self._rccl.get(tag)
+        if c is None:
             from .. import _native
             hip = _native.hip()
             if self.backend != "nccl" or self.device.type != "cuda":
                 raise RuntimeError("Comm.rccl: needs the nccl backend on a GPU")
             global _RCCL_SEQ
             _RCCL_SEQ += 1
-            key = "wh_rccl_uid_%d" % _RCCL_SEQ
+            key = "wh_rccl_uid_%d_%s" % (_RCCL_SEQ, tag)
             if self.size == 1:
                 uid = hip.RcclComm.unique_id()
             else:
@@ -140,13 +144,14 @@ class Comm:
                     store.set(key, uid)
                 else:
                     uid = store.get(key)
-            self._rccl = hip.RcclComm(bytes(uid), self.size, self.rank, self.device.index)
-        return self._rccl
+            c = self._rccl[tag] = hip.RcclComm(bytes(uid), self.size, self.rank,
+                                               self.device.index)
+        return c
 
     def _close_rccl(self):
-        if self._rccl is not None:
-            self._rccl.close()
-            self._rccl = None
+        for c in (self._rccl or {}).values():
+            c.close()
+        self._rccl = None
 
     # ----------------------------------------------------------- basics
     def barrier(self):
@@ -377,17 +382,21 @@ class LoopbackComm(Comm):
             self.pg = dist.group.WORLD
             self.backend = "loopback-rccl"
 
-    def rccl(self):
-        """A 1-rank RCCL communicator: the native step sends each of the P
-        virtual peers' segments as its own send / recv pair to self, so a
-        P-peer exchange's host and launch costs are paid as over xGMI."""
+    def rccl(self, tag="c23"):
+        """A 1-rank RCCL communicator ``tag``: the native step moves the P-1
+        virtual peers' segments as one send / recv pair to self (the own
+        segment a device copy)."""
         if not self.rccl_on:
             raise RuntimeError("LoopbackComm.rccl: built without rccl=True")
         if self._rccl is None:
+            self._rccl = {}
+        c = self._rccl.get(tag)
+        if c is None:
             from .. import _native
             hip = _native.hip()
-            self._rccl = hip.RcclComm(bytes(hip.RcclComm.unique_id()), 1, 0, self.device.index)
-        return self._rccl
+            c = self._rccl[tag] = hip.RcclComm(bytes(hip.RcclComm.unique_id()), 1, 0,
+                                               self.device.index)
+        return c
 
     def _a2a(self, x, async_op):
         """Identity exchange through RCCL (1-rank all-to-all = self copy)."""
