@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Localize microbenchmark: one 100k-row Criteo-shaped minibatch (device
 synthetic) localized repeatedly with the previous unique count as the hint;
-prints mean ms per call (events) for the path picked by WH_LOCALIZE.
+prints mean ms per call (events) for the partitioned path (the hash path with WH_DETERMINISTIC=1).
 TEXT=<criteo text file>: four minibatches of its lines instead (parsed on
 the device), e.g. the files benchmarks/bench_e2e.py writes."""
 import json

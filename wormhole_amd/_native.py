@@ -15,7 +15,18 @@ _err = {}
 
 
 def _try(name):
+    # WH_AB_HIP=<path to another build's _hip.so>: load that one instead
+    # (same-box A/B of two kernel builds in one benchmark call; tools/gpu/ab.sh)
+    alt = os.environ.get("WH_AB_HIP") if name == "_hip" else None
     try:
+        if alt:
+            import importlib.util as ilu
+            import sys
+            spec = ilu.spec_from_file_location("wormhole_amd._hip", alt)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            sys.modules["wormhole_amd._hip"] = mod
+            return mod
         return importlib.import_module("wormhole_amd." + name)
     except ImportError as e:  # pragma: no cover - reported by require_*()
         _err[name] = e
