@@ -1597,12 +1597,16 @@ void gbdt_hist(const Tensor& B, int64_t nbin, const Tensor& ridx, const Tensor& 
 }
 
 // ------------------------------------------------------------------ lbfgs
-Tensor owlqn_dir(const Tensor& g, const Tensor& w, double l1) {
+Tensor owlqn_dir(const Tensor& g, const Tensor& w, double l1, const c10::optional<Tensor>& out) {
   CHECK_IN(g, torch::kFloat32);
   CHECK_IN(w, torch::kFloat32);
   TORCH_CHECK(g.numel() == w.numel());
   c10::DeviceGuard dg(g.device());
-  auto d = torch::empty_like(g);
+  Tensor d = out.has_value() ? *out : torch::empty_like(g);
+  if (out.has_value()) {
+    CHECK_IN(d, torch::kFloat32);
+    TORCH_CHECK(d.numel() == g.numel(), "owlqn_dir: out size");
+  }
   wh::owlqn_dir(ptr<float>(g), ptr<float>(w), g.numel(), (float)l1, ptr<float>(d), cur_stream(g));
   return d;
 }
@@ -1612,9 +1616,10 @@ Tensor owlqn_fix_dot(const Tensor& d, const Tensor& steep, bool fix) {
   CHECK_IN(steep, torch::kFloat32);
   TORCH_CHECK(d.numel() == steep.numel());
   c10::DeviceGuard dg(d.device());
-  auto v = torch::zeros({1}, d.options().dtype(torch::kFloat64));
-  wh::owlqn_fix_dot(ptr<float>(d), ptr<float>(steep), d.numel(), fix ? 1 : 0, ptr<double>(v),
-                    cur_stream(d));
+  auto part = torch::empty({wh::owlqn_part_doubles()}, d.options().dtype(torch::kFloat64));
+  auto v = torch::empty({1}, d.options().dtype(torch::kFloat64));
+  wh::owlqn_fix_dot(ptr<float>(d), ptr<float>(steep), d.numel(), fix ? 1 : 0, ptr<double>(part),
+                    ptr<double>(v), cur_stream(d));
   return v;
 }
 
@@ -1624,10 +1629,59 @@ std::vector<Tensor> owlqn_step(const Tensor& w, const Tensor& d, double alpha, b
   TORCH_CHECK(w.numel() == d.numel());
   c10::DeviceGuard dg(w.device());
   auto nw = torch::empty_like(w);
-  auto l1 = torch::zeros({1}, w.options().dtype(torch::kFloat64));
+  auto part = torch::empty({wh::owlqn_part_doubles()}, w.options().dtype(torch::kFloat64));
+  auto l1 = torch::empty({1}, w.options().dtype(torch::kFloat64));
   wh::owlqn_step(ptr<float>(w), ptr<float>(d), w.numel(), (float)alpha, fix ? 1 : 0,
-                 ptr<float>(nw), ptr<double>(l1), cur_stream(w));
+                 ptr<float>(nw), ptr<double>(part), ptr<double>(l1), cur_stream(w));
   return {nw, l1};
+}
+
+// <H[r], H[probe k]> for every row r of the history [R, n]: [R, K] fp64
+Tensor hist_dots(const Tensor& H, const std::vector<int64_t>& probes) {
+  CHECK_IN(H, torch::kFloat32);
+  TORCH_CHECK(H.dim() == 2, "hist_dots: H must be [R, n]");
+  const int R = (int)H.size(0), K = (int)probes.size();
+  std::vector<int32_t> pr(K);
+  for (int k = 0; k < K; ++k) {
+    TORCH_CHECK(probes[k] >= 0 && probes[k] < R, "hist_dots: probe row out of range");
+    pr[k] = (int32_t)probes[k];
+  }
+  c10::DeviceGuard dg(H.device());
+  auto part = torch::empty({wh::owlqn_part_doubles() * 4}, H.options().dtype(torch::kFloat64));
+  auto out = torch::empty({R, K}, H.options().dtype(torch::kFloat64));
+  TORCH_CHECK(wh::hist_dots(ptr<float>(H), R, H.size(1), H.size(1), pr.data(), K,
+                            ptr<double>(part), ptr<double>(out), cur_stream(H)),
+              "hist_dots: 1..4 probes, row length a multiple of 4");
+  return out;
+}
+
+// the direction slice d = sum coef[r] H[rows[r]] (fp32, list order), sign
+// fixed against H[steep_row]; returns (d, sum d * steep as fp64 [1])
+std::vector<Tensor> dir_fix_dot(const Tensor& H, const std::vector<int64_t>& rows,
+                                const std::vector<double>& coef, int64_t steep_row, bool fix,
+                                int64_t n) {
+  CHECK_IN(H, torch::kFloat32);
+  TORCH_CHECK(H.dim() == 2 && rows.size() == coef.size() && rows.size() <= 64,
+              "dir_fix_dot: <= 64 rows of H [R, n]");
+  const int R = (int)H.size(0);
+  std::vector<int32_t> r32(rows.size());
+  std::vector<float> c32(rows.size());
+  for (size_t i = 0; i < rows.size(); ++i) {
+    TORCH_CHECK(rows[i] >= 0 && rows[i] < R, "dir_fix_dot: row out of range");
+    r32[i] = (int32_t)rows[i];
+    c32[i] = (float)coef[i];
+  }
+  TORCH_CHECK(steep_row >= 0 && steep_row < R, "dir_fix_dot: steep row out of range");
+  if (n < 0) n = H.size(1);
+  TORCH_CHECK(n <= H.size(1), "dir_fix_dot: n exceeds the row length");
+  c10::DeviceGuard dg(H.device());
+  auto d = torch::empty({n}, H.options());
+  auto part = torch::empty({wh::owlqn_part_doubles()}, H.options().dtype(torch::kFloat64));
+  auto v = torch::empty({1}, H.options().dtype(torch::kFloat64));
+  wh::dir_fix_dot(ptr<float>(H), n, H.size(1), r32.data(), c32.data(), (int)rows.size(),
+                  (int)steep_row, fix ? 1 : 0, ptr<float>(d), ptr<double>(part), ptr<double>(v),
+                  cur_stream(H));
+  return {d, v};
 }
 
 Tensor multi_dot(const Tensor& H, const Tensor& ia, const Tensor& ib) {
@@ -1990,6 +2044,79 @@ Tensor spmv_t(const Tensor& csc_off, const Tensor& csc_row, const c10::optional<
   return pl[0];
 }
 
+
+// ------------------------------------------------------------------ glm
+// column-start bits of a CSC with nnz entries (glm.hip), as int64 words
+Tensor glm_heads(const Tensor& csc_off, int64_t nnz) {
+  CHECK_IN(csc_off, torch::kInt64);
+  c10::DeviceGuard g(csc_off.device());
+  const int64_t words = wh::glm_heads_words(nnz);
+  auto hb = torch::empty({words}, csc_off.options());
+  wh::glm_heads(ptr<int64_t>(csc_off), csc_off.numel() - 1,
+                reinterpret_cast<uint64_t*>(hb.data_ptr<int64_t>()), words, cur_stream(csc_off));
+  return hb;
+}
+
+// rows of a linear model: mode 0 -> (None, [loss, 0]); 1 -> (pred - label,
+// [loss, sum]); 2 -> (margin, None). bias: index of the bias weight in w (or -1)
+std::vector<c10::optional<Tensor>> glm_fwd(int64_t mode, const Tensor& offset, const Tensor& gcol,
+                                           const c10::optional<Tensor>& val, const Tensor& w,
+                                           int64_t bias, double base,
+                                           const c10::optional<Tensor>& label, int64_t loss) {
+  CHECK_IN(offset, torch::kInt64);
+  CHECK_IN(gcol, torch::kInt32);
+  CHECK_IN(w, torch::kFloat32);
+  TORCH_CHECK(mode >= 0 && mode <= 2, "glm_fwd: mode 0 / 1 / 2");
+  TORCH_CHECK(bias < w.numel(), "glm_fwd: bias index out of range");
+  const int64_t nrows = offset.numel() - 1;
+  if (mode != 2) {
+    TORCH_CHECK(label.has_value() && label->numel() == nrows, "glm_fwd: label [nrows] needed");
+    CHECK_IN((*label), torch::kFloat32);
+  }
+  if (val.has_value() && val->defined() && val->numel())
+    TORCH_CHECK(val->numel() == gcol.numel(), "glm_fwd: val must match gcol");
+  c10::DeviceGuard g(w.device());
+  c10::optional<Tensor> out, sums;
+  if (mode != 0) out = torch::empty({nrows}, w.options());
+  Tensor part;
+  if (mode != 2) {
+    sums = torch::empty({2}, w.options().dtype(torch::kFloat64));
+    part = torch::empty({std::max<int64_t>(2 * wh::glm_fwd_blocks(nrows), 2)},
+                        w.options().dtype(torch::kFloat64));
+  }
+  const float* vp = (val.has_value() && val->defined() && val->numel()) ? ptr<float>(*val) : nullptr;
+  wh::glm_fwd((int)mode, nrows, ptr<int64_t>(offset), ptr<int32_t>(gcol), vp, ptr<float>(w),
+              bias >= 0 ? ptr<float>(w) + bias : nullptr, (float)base,
+              mode != 2 ? ptr<float>(*label) : nullptr, (int)loss,
+              out.has_value() ? ptr<float>(*out) : nullptr,
+              mode != 2 ? ptr<double>(part) : nullptr,
+              sums.has_value() ? ptr<double>(*sums) : nullptr, cur_stream(w));
+  return {out, sums};
+}
+
+// grad[ucol[c]] (+)= sum over column c's CSC entries of g[row] (* val);
+// grad must be zero where the columns land
+void glm_xtg(const Tensor& crow, const c10::optional<Tensor>& cval, const Tensor& hb,
+             const Tensor& col0, const Tensor& ucol, const Tensor& g, Tensor& grad,
+             bool all_atomic) {
+  CHECK_IN(crow, torch::kInt32);
+  CHECK_IN(hb, torch::kInt64);
+  CHECK_IN(col0, torch::kInt32);
+  CHECK_IN(ucol, torch::kInt32);
+  CHECK_IN(g, torch::kFloat32);
+  CHECK_IN(grad, torch::kFloat32);
+  const int64_t nnz = crow.numel();
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(crow.data_ptr()) & 15) == 0,
+              "glm_xtg: CSC rows must be 16-byte aligned");
+  TORCH_CHECK(hb.numel() >= wh::glm_heads_words(nnz), "glm_xtg: short column-start bits");
+  TORCH_CHECK(col0.numel() >= wh::glm_xtg_waves(nnz), "glm_xtg: short per-wave columns");
+  const float* vp = (cval.has_value() && cval->defined() && cval->numel()) ? ptr<float>(*cval) : nullptr;
+  if (vp) TORCH_CHECK(cval->numel() == nnz, "glm_xtg: val must match rows");
+  c10::DeviceGuard dg(g.device());
+  wh::glm_xtg(nnz, ptr<int32_t>(crow), vp, reinterpret_cast<const uint64_t*>(ptr<int64_t>(hb)),
+              ptr<int32_t>(col0), ptr<int32_t>(ucol), ptr<float>(g), ptr<float>(grad),
+              all_atomic ? 1 : 0, cur_stream(g));
+}
 
 // ------------------------------------------------------------- gbdt (CSR)
 Tensor gbdt_bin_csr(const Tensor& fid, const c10::optional<Tensor>& val, int64_t ncol,
@@ -3215,10 +3342,19 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("seg_end"), py::arg("nleft"), py::arg("Bc") = py::none());
   m.def("gbdt_seg_fill", &gbdt_seg_fill);
   m.def("gbdt_split", &gbdt_split);
-  m.def("owlqn_dir", &owlqn_dir);
+  m.def("owlqn_dir", &owlqn_dir, py::arg("g"), py::arg("w"), py::arg("l1"),
+        py::arg("out") = py::none());
   m.def("owlqn_fix_dot", &owlqn_fix_dot);
   m.def("owlqn_step", &owlqn_step);
   m.def("multi_dot", &multi_dot);
+  m.def("hist_dots", &hist_dots, py::arg("H"), py::arg("probes"));
+  m.def("dir_fix_dot", &dir_fix_dot, py::arg("H"), py::arg("rows"), py::arg("coef"),
+        py::arg("steep_row"), py::arg("fix"), py::arg("n") = -1);
+  m.def("glm_heads", &glm_heads, py::arg("csc_off"), py::arg("nnz"));
+  m.def("glm_fwd", &glm_fwd, py::arg("mode"), py::arg("offset"), py::arg("gcol"), py::arg("val"),
+        py::arg("w"), py::arg("bias"), py::arg("base"), py::arg("label"), py::arg("loss"));
+  m.def("glm_xtg", &glm_xtg, py::arg("crow"), py::arg("cval"), py::arg("hb"), py::arg("col0"),
+        py::arg("ucol"), py::arg("g"), py::arg("grad"), py::arg("all_atomic") = false);
   m.def("gbdt_leaf_add", &gbdt_leaf_add);
   m.def("gbdt_leaf_walk", &gbdt_leaf_walk, py::arg("B"), py::arg("feat"), py::arg("bin"),
         py::arg("defl"), py::arg("left"), py::arg("right"), py::arg("val"), py::arg("margin"),

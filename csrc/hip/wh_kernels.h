@@ -415,14 +415,47 @@ bool kmeans_accum_sorted(const float* X, int64_t n, int f, int k, const int32_t*
 
 // -------------------------------------------------------------- lbfgs.hip
 void owlqn_dir(const float* g, const float* w, int64_t n, float l1, float* d, hipStream_t s);
-// vdot (fp64, accumulated) += sum d * steep after the optional sign fix
-void owlqn_fix_dot(float* d, const float* steep, int64_t n, int fix, double* vdot, hipStream_t s);
-// nw = fix(w + alpha d); l1sum (fp64, accumulated) += |nw|_1
+// fp64 scratch the reductions below need (doubles)
+int64_t owlqn_part_doubles();
+// *vdot = sum d * steep after the optional sign fix
+void owlqn_fix_dot(float* d, const float* steep, int64_t n, int fix, double* part, double* vdot,
+                   hipStream_t s);
+// nw = fix(w + alpha d); *l1sum = |nw|_1
 void owlqn_step(const float* w, const float* d, int64_t n, float alpha, int fix, float* nw,
-                double* l1sum, hipStream_t s);
+                double* part, double* l1sum, hipStream_t s);
+// out[r * K + k] = <H[r], H[probe[k]]> for r < R (row stride ld, K <= 4);
+// false when n / ld are not multiples of 4 or H is not 16-byte aligned
+bool hist_dots(const float* H, int R, int64_t n, int64_t ld, const int32_t* probe, int K,
+               double* part, double* out, hipStream_t s);
+// d = sum_r coef[r] H[rows[r]] (fp32, in list order), sign-fixed against
+// H[steep_row] when fix; *vdot = sum d * steep. false if nrow > 64
+bool dir_fix_dot(const float* H, int64_t n, int64_t ld, const int32_t* rows, const float* coef,
+                 int nrow, int steep_row, int fix, float* d, double* part, double* vdot,
+                 hipStream_t s);
 // out[p] (fp64, accumulated) += <H[ia[p]], H[ib[p]]>; false if R > 64 or np > 64
 bool multi_dot(const float* H, int R, int64_t n, const int32_t* ia, const int32_t* ib, int np,
                double* out, hipStream_t s);
+
+// --------------------------------------------------------------- glm.hip
+// out[v] = sum over nblk blocks of part[b * stride + v], v < nv (fixed
+// order; stride 0 = nv)
+void sum_parts(const double* part, int nblk, int nv, double* out, hipStream_t s, int stride = 0);
+// linear-model rows over the prepared split (glm.hip header): mode 0 sums[0]
+// = loss; 1 also out = pred - label and sums[1] = its sum; 2 out = margin.
+// part: glm_fwd_blocks(nrows) * 2 doubles
+int64_t glm_fwd_blocks(int64_t nrows);
+void glm_fwd(int mode, int64_t nrows, const int64_t* off, const int32_t* gcol, const float* val,
+             const float* w, const float* bias, float base, const float* label, int loss,
+             float* out, double* part, double* sums, hipStream_t s);
+// run-start bits of an entry stream (glm_heads_words(nnz) u64; run u starts
+// at off[u]) and X^T g into grad (zeroed by the caller) at the runs' global
+// indices ucol (all_atomic: several runs may share one index)
+int64_t glm_xtg_waves(int64_t nnz);
+int64_t glm_heads_words(int64_t nnz);
+void glm_heads(const int64_t* csc_off, int64_t U, uint64_t* hb, int64_t words, hipStream_t s);
+void glm_xtg(int64_t nnz, const int32_t* crow, const float* cval, const uint64_t* hb,
+             const int32_t* col0w, const int32_t* ucol, const float* g, float* grad,
+             int all_atomic, hipStream_t s);
 
 // -------------------------------------------------------------- gbdt.hip
 void gbdt_bin(const float* X, int64_t n, int f, const float* cuts, const int32_t* cut_off,

@@ -359,6 +359,96 @@ def test_difacto_learner_matches_cpu(hip):
     assert pg[6] == pc[6] and pg[7] == pc[7]
 
 
+def test_hist_dots_and_dir_fix_dot(hip):
+    """The solver's history kernels: every row against up to 4 probe rows
+    (exact fp64) and the direction build + sign fix + dot (fp32 in list
+    order, as the reference AddScale loop)."""
+    g = torch.Generator().manual_seed(5)
+    for R, n in [(21, 100_000), (3, 4096), (9, 40)]:
+        H = torch.randn(R, n, generator=g)
+        for probes in ([R - 1], [0, R - 1], [R - 1, 1, 2], [0, 1, 2, R - 1][: min(4, R)]):
+            out = hip.hist_dots(H.to(DEV), probes).cpu()
+            ref_ = H.double() @ H[probes].double().t()
+            assert out.shape == (R, len(probes))
+            assert torch.allclose(out, ref_, rtol=1e-10, atol=1e-9)
+        rows = list(range(R // 2, R)) + list(range(R // 2))
+        coef = [float(x) for x in torch.randn(R, generator=g)]
+        for fix in (False, True):
+            d, v = hip.dir_fix_dot(H.to(DEV), rows, coef, R - 1, fix)
+            acc = torch.zeros(n)
+            for r, c in zip(rows, coef):
+                acc = acc + H[r] * torch.tensor(c, dtype=torch.float32)
+            st = H[R - 1]
+            if fix:
+                acc = torch.where(acc * st <= 0, torch.zeros_like(acc), acc)
+            assert torch.allclose(d.cpu(), acc, rtol=1e-5, atol=1e-5)
+            rv = float((d.cpu() * st).double().sum())
+            assert abs(float(v) - rv) <= 1e-9 * max(1.0, abs(rv))
+
+
+def test_glm_xtg_plain_csc(hip):
+    """glm.hip's segmented X^T g over a plain CSC (run = column, stores for
+    columns inside a wave, atomics at wave cuts) against torch."""
+    keys, off, val, _ = _rand_batch(20000, 30, 3000, 17, with_val=True)
+    uniq, _c, _o, _lid, csc_off, csc_row, csc_val = [
+        t.to(DEV) if t is not None else None for t in
+        __import__("wormhole_amd.ops", fromlist=["localize"]).localize(
+            keys.to(DEV), off.to(DEV), val.to(DEV), 1)]
+    nnz = csc_row.numel()
+    g = torch.randn(off.numel() - 1, device=DEV)
+    hb = hip.glm_heads(csc_off, nnz)
+    waves = (nnz + 1023) // 1024
+    col0 = (torch.searchsorted(csc_off, torch.arange(waves, device=DEV) * 1024, right=True)
+            - 1).int()
+    U = csc_off.numel() - 1
+    ucol = torch.arange(U, device=DEV, dtype=torch.int32)
+    out = torch.zeros(U, device=DEV)
+    hip.glm_xtg(csc_row.contiguous(), csc_val, hb, col0, ucol, g, out)
+    key = torch.repeat_interleave(torch.arange(U, device=DEV), csc_off[1:] - csc_off[:-1])
+    ref_ = torch.zeros(U, dtype=torch.float64, device=DEV).index_add_(
+        0, key, (csc_val * g[csc_row.long()]).double())
+    assert torch.allclose(out.double(), ref_, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("with_val,loss", [(False, 1), (True, 1), (False, 0)])
+def test_glm_objective_matches_cpu(with_val, loss):
+    """L-BFGS linear objective on the GPU (glm.hip: fused margin + loss, the
+    segmented CSC X^T g with power-law columns spanning many 1024-entry
+    waves) against the torch path on the CPU."""
+    from wormhole_amd.models.lbfgs_models import LinearObjective, _SplitData
+    from wormhole_amd.parallel.bsp import BSP
+    g = torch.Generator().manual_seed(3 + loss)
+    nrows, F = 60_000, 50_000
+    lens = torch.randint(1, 40, (nrows,), generator=g)
+    off = torch.zeros(nrows + 1, dtype=torch.int64)
+    off[1:] = torch.cumsum(lens, 0)
+    nnz = int(off[-1])
+    u = torch.rand(nnz, generator=g)
+    keys = (torch.exp(u * np.log(F * 1.2)) - 1).long()  # some ids >= F (outside the model)
+    keys[:: 7] = 3  # one very heavy column
+    val = (torch.rand(nnz, generator=g) + 0.5) if with_val else None
+    label = (torch.rand(nrows, generator=g) < 0.3).float()
+    objs = []
+    for dev in (torch.device("cpu"), DEV):
+        d = _SplitData(keys, off, val, label, dev)
+        o = LinearObjective(BSP(torch.device("cpu")), d, dev)
+        o.set_param("objective", "logistic" if loss == 1 else "linear")
+        o.set_param("num_feature", str(F))
+        o.param.base_score = 0.1
+        objs.append(o)
+    w = torch.randn(F + 1, generator=g) * 0.05
+    lc = objs[0].eval(w)
+    lg = objs[1].eval(w.to(DEV))
+    assert abs(lg - lc) <= 1e-5 * abs(lc)
+    gc = objs[0].calc_grad(w)
+    gg = objs[1].calc_grad(w.to(DEV)).cpu()
+    scale = float(gc.abs().max())
+    assert torch.allclose(gg, gc, rtol=1e-4, atol=1e-5 * scale)
+    mc = objs[0].margin(w)
+    mg = objs[1].margin(w.to(DEV)).cpu()
+    assert torch.allclose(mg, mc, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("n,f,k", [(1000, 5, 7), (4096, 64, 33), (5000, 127, 100),
                                    (3000, 128, 1000), (777, 200, 40)])
 def test_kmeans_assign_accum(hip, n, f, k):
@@ -619,7 +709,7 @@ def test_owlqn_kernels(hip, l1):
     assert torch.equal(d.cpu(), ref_d)
     steep = torch.randn(n, generator=g)
     ref_fixed = sv.fix_dir_l1_sign(ref_d.clone(), steep)
-    ref_v = float((ref_fixed.double() * steep.double()).sum())
+    ref_v = float((ref_fixed * steep).double().sum())  # float products, fp64 sum (lbfgs.h Dot)
     v = hip.owlqn_fix_dot(d, steep.to(DEV), l1 != 0.0)
     assert torch.equal(d.cpu(), ref_fixed)
     assert abs(float(v) - ref_v) <= 1e-9 * max(1.0, abs(ref_v))

@@ -3,6 +3,11 @@
 * linear / logistic regression (reference learn/lbfgs-linear/{linear.h,lbfgs.cc})
 * factorization machine, order 2 (reference learn/lbfgs-fm/{fm.h,fm.cc})
 
+On the GPU the linear objective runs on csrc/hip/glm.hip over a plan of the
+split prepared once (:class:`_GLMPlan`): one fused pass for margin + loss
+(+ pred - label), one segmented CSC pass for X^T (pred - label) written
+straight into the global gradient.
+
 Each rank loads ``RowBlockIter(data, rank, world)`` (its byte-range split of
 the libsvm file) ONCE into HBM, localizes it once (unique feature ids + the
 per-feature CSC), and then every objective/gradient evaluation is one fused
@@ -98,6 +103,56 @@ class _SplitData:
         self.max_col = int(keys.max().item()) + 1 if keys.numel() else 0
 
 
+# rows per block of the X^T stream: the 2 MB of pred - label a block gathers
+# from stays in an XCD's 4 MB L2
+_XTG_ROW_BLOCK_SHIFT = 19
+
+
+class _GLMPlan:
+    """The split, prepared once for the glm.hip passes:
+
+    * ``gcol``: the CSR entries' global weight index (-1: id >= num_feature)
+    * the X^T stream: the valid entries ordered (row block, global id), rows
+      ascending inside, as runs of one (block, id) each -- ``crow`` /
+      ``cval`` per entry, the run-start bits ``hb``, the run of every
+      1024-entry wave's first entry ``col0`` and each run's global id
+      ``rucol`` (runs of one id in several blocks add atomically)."""
+
+    def __init__(self, d, F):
+        from .. import _native
+        self.hip = _native.hip()
+        self.F = F
+        dev = d.uniq.device
+        uniq = d.uniq
+        ucol = torch.where(uniq < F, uniq, torch.full_like(uniq, -1)).to(torch.int32)
+        lid = d.lid.long()
+        self.gcol = torch.where(lid >= 0, ucol[lid.clamp_min(0)],
+                                torch.full_like(d.lid, -1)).to(torch.int32).contiguous()
+        self.label = d.label.float().contiguous()
+        nrows = d.offset.numel() - 1
+        gid = self.gcol.long()
+        rows = torch.repeat_interleave(torch.arange(nrows, device=dev),
+                                       d.offset[1:] - d.offset[:-1], output_size=gid.numel())
+        keep = gid >= 0
+        rows, gid = rows[keep], gid[keep]
+        key = ((rows >> _XTG_ROW_BLOCK_SHIFT) << 31) | gid
+        key, perm = torch.sort(key, stable=True)
+        self.crow = rows[perm].to(torch.int32)
+        self.cval = d.val[keep][perm].contiguous() if d.val is not None else None
+        del rows, gid
+        nnz = key.numel()
+        starts = torch.ones(nnz, dtype=torch.bool, device=dev)
+        if nnz > 1:
+            starts[1:] = key[1:] != key[:-1]
+        run_off = torch.nonzero(starts).view(-1)
+        self.rucol = (key[run_off] & ((1 << 31) - 1)).to(torch.int32)
+        run_off = torch.cat([run_off, torch.tensor([nnz], device=dev, dtype=torch.int64)])
+        self.hb = self.hip.glm_heads(run_off, nnz)
+        waves = (nnz + 1023) // 1024
+        pos = torch.arange(waves, device=dev, dtype=torch.int64) * 1024
+        self.col0 = (torch.searchsorted(run_off, pos, right=True) - 1).to(torch.int32)
+
+
 class LinearObjective:
     def __init__(self, bsp, data, device):
         self.bsp = bsp
@@ -141,8 +196,23 @@ class LinearObjective:
         idx = torch.where(valid, self.d.uniq, torch.zeros_like(self.d.uniq))
         return valid, idx
 
+    def _plan(self):
+        F = self.param.num_feature
+        p = getattr(self, "_glm", None)
+        if p is None or p.F != F:
+            p = self._glm = _GLMPlan(self.d, F)
+        return p
+
+    def _glm_fwd(self, mode, w):
+        p = self._plan()
+        return p.hip.glm_fwd(mode, self.d.offset, p.gcol, self.d.val, w.contiguous(), p.F,
+                             float(self.param.base_score), p.label if mode != 2 else None,
+                             int(self.param.loss_type))
+
     def margin(self, w):
         F = self.param.num_feature
+        if w.is_cuda:
+            return self._glm_fwd(2, w)[0]
         valid, idx = self._feat()
         wu = torch.where(valid, w[idx], torch.zeros((), device=w.device))
         return ops.spmv(self.d.offset, self.d.lid, self.d.val, wu.contiguous()) + (
@@ -150,8 +220,11 @@ class LinearObjective:
 
     def eval(self, w):
         F = self.param.num_feature
-        val = float(margin_to_loss(self.param.loss_type, self.d.label, self.margin(w)).sum(
-            dtype=torch.float64))
+        if w.is_cuda:  # margin + loss in one pass (glm.hip k_glm_fwd)
+            val = float(self._glm_fwd(0, w)[1][0])
+        else:
+            val = float(margin_to_loss(self.param.loss_type, self.d.label, self.margin(w)).sum(
+                dtype=torch.float64))
         if self.bsp.rank == 0 and self.reg_L2 != 0.0:
             val += 0.5 * self.reg_L2 * float((w[:F].double() ** 2).sum())
         if math.isnan(val):
@@ -160,6 +233,15 @@ class LinearObjective:
 
     def calc_grad(self, w):
         F = self.param.num_feature
+        if w.is_cuda:  # pred - label, then X^T of it (glm.hip)
+            g, sums = self._glm_fwd(1, w)
+            p = self._plan()
+            grad = torch.zeros_like(w)
+            p.hip.glm_xtg(p.crow, p.cval, p.hb, p.col0, p.rucol, g, grad, True)
+            grad[F:F + 1].copy_(sums[1:2])
+            if self.bsp.rank == 0 and self.reg_L2 != 0.0:
+                grad[:F] += self.reg_L2 * w[:F]
+            return grad
         pred = margin_to_pred(self.param.loss_type, self.margin(w))
         g = (pred - self.d.label).contiguous()
         gu = ops.spmv_t(self.d.csc_off, self.d.csc_row, self.d.csc_val, g)

@@ -65,7 +65,7 @@ class LBFGSSolver:
         self.data[a, b] = v
 
     def H(self, i):
-        return self.hist[self._map(i)]
+        return self.hist[self._map(i), : self.nsub]
 
     # --------------------------------------------------------------- init
     def init(self):
@@ -86,7 +86,10 @@ class LBFGSSolver:
         self.nsub = self.re - self.rb
         m = self.size_memory
         dev = self.device
-        self.hist = torch.zeros(2 * m + 1, self.nsub, dtype=torch.float32, device=dev)
+        # rows padded to a multiple of 4 floats (16-byte rows for the
+        # history kernels); the padding stays zero
+        self.hist = torch.zeros(2 * m + 1, (self.nsub + 3) // 4 * 4, dtype=torch.float32,
+                                device=dev)
         if version == 0:
             self.num_iteration = 0
             self.offset = 0
@@ -202,20 +205,19 @@ class LBFGSSolver:
         gsub = grad[rb:re]
         if n != 0:
             y_last = self.H(m + n - 1)
-            y_last.copy_(gsub - y_last)  # y_{n-1} = g_new - g_old
-            self.H(2 * m).copy_(self.set_l1_dir(gsub, weight[rb:re]))
+            torch.sub(gsub, y_last, out=y_last)  # y_{n-1} = g_new - g_old
+            if gsub.is_cuda:  # written in place into the history row
+                _native.hip().owlqn_dir(gsub.contiguous(), weight[rb:re].contiguous(),
+                                        float(self.reg_L1), self.H(2 * m))
+            else:
+                self.H(2 * m).copy_(self.set_l1_dir(gsub, weight[rb:re]))
             idx = []
             for j in range(n):
                 idx += [(j, 2 * m), (j, n - 1), (j, m + n - 1)]
             for j in range(n):
                 idx += [(m + j, 2 * m), (m + j, m + n - 1)]
-            ia = torch.tensor([self._map(a) for a, _ in idx], device=self.device)
-            ib = torch.tensor([self._map(b) for _, b in idx], device=self.device)
             # all new partial dots in ONE batched reduction, then one allreduce
-            if self.hist.is_cuda:  # one pass over the history (k_multi_dot)
-                tmp = _native.hip().multi_dot(self.hist, ia.int(), ib.int())
-            else:
-                tmp = (self.hist[ia] * self.hist[ib]).sum(1, dtype=torch.float64)
+            tmp = self._history_dots(idx)
             self.bsp.allreduce(tmp)
             tmp = tmp.cpu()
             for k, (a, b) in enumerate(idx):
@@ -235,16 +237,21 @@ class LBFGSSolver:
                 vsum = sum(delta[k] * D(k, m + j) for k in range(2 * m + 1))
                 beta = vsum / D(j, m + j)
                 delta[j] += alpha[j] - beta
-            coef = torch.zeros(2 * m + 1, dtype=torch.float32)
-            for k in list(range(n)) + list(range(m, m + n)) + [2 * m]:
-                coef[self._map(k)] = delta[k]
-            dirsub = coef.to(self.device) @ self.hist  # skinny GEMV over the shard
             steep = self.H(2 * m)
-            if dirsub.is_cuda:  # sign fix + dot in one pass (k_owlqn_fix_dot)
-                dirsub = dirsub.contiguous()
-                vdot = -float(_native.hip().owlqn_fix_dot(dirsub, steep.contiguous(),
-                                                          self.reg_L1 != 0.0))
+            if self.hist.is_cuda:
+                # d = sum delta_k H_k in the reference's AddScale order (y rows,
+                # the steepest direction, s rows), sign fix + dot: ONE pass
+                # over the history (lbfgs.hip k_dir_fix_dot)
+                order = list(range(m, m + n)) + [2 * m] + list(range(n))
+                dirsub, v = _native.hip().dir_fix_dot(
+                    self.hist, [self._map(k) for k in order], [delta[k] for k in order],
+                    self._map(2 * m), self.reg_L1 != 0.0, self.nsub)
+                vdot = -float(v)
             else:
+                coef = torch.zeros(2 * m + 1, dtype=torch.float32)
+                for k in list(range(n)) + list(range(m, m + n)) + [2 * m]:
+                    coef[self._map(k)] = delta[k]
+                dirsub = coef.to(self.device) @ self.hist[:, : self.nsub]  # skinny GEMV
                 dirsub = self.fix_dir_l1_sign(dirsub, steep)
                 vdot = -float((dirsub * steep).sum(dtype=torch.float64))
             d = self._allgather_dir(dirsub)
@@ -260,9 +267,30 @@ class LBFGSSolver:
         self.H(m + n - 1).copy_(gsub)
         return d, vdot
 
+    def _history_dots(self, idx):
+        """fp64 <H_a, H_b> for the (a, b) index pairs of FindChangeDirection.
+        Every pair's b is one of three probe rows (the steepest direction and
+        the newest s / y), so on the GPU all rows are dotted with the probes
+        in one pass (lbfgs.hip k_hist_dots) and the pairs picked out."""
+        ia = [self._map(a) for a, _ in idx]
+        ib = [self._map(b) for _, b in idx]
+        if not self.hist.is_cuda:
+            a, b = torch.tensor(ia), torch.tensor(ib)
+            return (self.hist[a] * self.hist[b]).sum(1, dtype=torch.float64)
+        probes = sorted(set(ib))
+        if len(probes) <= 4:
+            out = _native.hip().hist_dots(self.hist, probes)
+            col = {p: k for k, p in enumerate(probes)}
+            sel = torch.tensor([a * len(probes) + col[b] for a, b in zip(ia, ib)],
+                               device=self.device)
+            return out.view(-1)[sel]
+        return _native.hip().multi_dot(self.hist[:, : self.nsub].contiguous(),
+                                       torch.tensor(ia, device=self.device).int(),
+                                       torch.tensor(ib, device=self.device).int())
+
     def _allgather_dir(self, dirsub):
         if self.bsp.world == 1:
-            return dirsub.clone()
+            return dirsub
         pad = torch.zeros(self.step, dtype=dirsub.dtype, device=dirsub.device)
         pad[: dirsub.numel()] = dirsub
         parts = self.bsp.comm.allgather(pad)
@@ -295,6 +323,6 @@ class LBFGSSolver:
                 self.new_objval = new_val
                 break
             alpha *= backoff
-        self.H(self.num_useful - 1).copy_(new_w[self.rb:self.re] - w[self.rb:self.re])
+        torch.sub(new_w[self.rb:self.re], w[self.rb:self.re], out=self.H(self.num_useful - 1))
         self.num_iteration += 1
         return new_w, it
