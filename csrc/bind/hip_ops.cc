@@ -2070,7 +2070,8 @@ std::vector<c10::optional<Tensor>> glm_fwd(int64_t mode, const Tensor& offset, c
   TORCH_CHECK(bias < w.numel(), "glm_fwd: bias index out of range");
   const int64_t nrows = offset.numel() - 1;
   if (mode != 2) {
-    TORCH_CHECK(label.has_value() && label->numel() == nrows, "glm_fwd: label [nrows] needed");
+    TORCH_CHECK(label.has_value() && label->defined() && label->numel() == nrows,
+                "glm_fwd: label [nrows] needed");
     CHECK_IN((*label), torch::kFloat32);
   }
   if (val.has_value() && val->defined() && val->numel())
@@ -2096,13 +2097,15 @@ std::vector<c10::optional<Tensor>> glm_fwd(int64_t mode, const Tensor& offset, c
 
 // grad[ucol[c]] (+)= sum over column c's CSC entries of g[row] (* val);
 // grad must be zero where the columns land
+// ucol: the runs' output indices, or an EMPTY tensor for the run index itself
 void glm_xtg(const Tensor& crow, const c10::optional<Tensor>& cval, const Tensor& hb,
              const Tensor& col0, const Tensor& ucol, const Tensor& g, Tensor& grad,
              bool all_atomic) {
   CHECK_IN(crow, torch::kInt32);
   CHECK_IN(hb, torch::kInt64);
   CHECK_IN(col0, torch::kInt32);
-  CHECK_IN(ucol, torch::kInt32);
+  const bool has_u = ucol.numel() > 0;
+  if (has_u) CHECK_IN(ucol, torch::kInt32);
   CHECK_IN(g, torch::kFloat32);
   CHECK_IN(grad, torch::kFloat32);
   const int64_t nnz = crow.numel();
@@ -2114,8 +2117,21 @@ void glm_xtg(const Tensor& crow, const c10::optional<Tensor>& cval, const Tensor
   if (vp) TORCH_CHECK(cval->numel() == nnz, "glm_xtg: val must match rows");
   c10::DeviceGuard dg(g.device());
   wh::glm_xtg(nnz, ptr<int32_t>(crow), vp, reinterpret_cast<const uint64_t*>(ptr<int64_t>(hb)),
-              ptr<int32_t>(col0), ptr<int32_t>(ucol), ptr<float>(g), ptr<float>(grad),
-              all_atomic ? 1 : 0, cur_stream(g));
+              ptr<int32_t>(col0), has_u ? ptr<int32_t>(ucol) : nullptr, ptr<float>(g),
+              ptr<float>(grad), all_atomic ? 1 : 0, cur_stream(g));
+}
+
+void glm_runs_reduce(const Tensor& coff, const Tensor& rlist, const Tensor& S, const Tensor& cgid,
+                     Tensor& grad) {
+  CHECK_IN(coff, torch::kInt64);
+  CHECK_IN(rlist, torch::kInt32);
+  CHECK_IN(S, torch::kFloat32);
+  CHECK_IN(cgid, torch::kInt32);
+  CHECK_IN(grad, torch::kFloat32);
+  TORCH_CHECK(cgid.numel() == coff.numel() - 1, "glm_runs_reduce: cgid / coff sizes");
+  c10::DeviceGuard dg(S.device());
+  wh::glm_runs_reduce(cgid.numel(), ptr<int64_t>(coff), ptr<int32_t>(rlist), ptr<float>(S),
+                      ptr<int32_t>(cgid), ptr<float>(grad), cur_stream(S));
 }
 
 // ------------------------------------------------------------- gbdt (CSR)
@@ -3355,6 +3371,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("w"), py::arg("bias"), py::arg("base"), py::arg("label"), py::arg("loss"));
   m.def("glm_xtg", &glm_xtg, py::arg("crow"), py::arg("cval"), py::arg("hb"), py::arg("col0"),
         py::arg("ucol"), py::arg("g"), py::arg("grad"), py::arg("all_atomic") = false);
+  m.def("glm_runs_reduce", &glm_runs_reduce, py::arg("coff"), py::arg("rlist"), py::arg("S"),
+        py::arg("cgid"), py::arg("grad"));
   m.def("gbdt_leaf_add", &gbdt_leaf_add);
   m.def("gbdt_leaf_walk", &gbdt_leaf_walk, py::arg("B"), py::arg("feat"), py::arg("bin"),
         py::arg("defl"), py::arg("left"), py::arg("right"), py::arg("val"), py::arg("margin"),

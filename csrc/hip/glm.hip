@@ -19,18 +19,22 @@
 //
 // X^T g (k_glm_xtg): a segmented sum over a stream of entries grouped in
 // RUNS (one output index per run), not one thread per column: each wave
-// takes 1024 consecutive entries (16 per lane, read as four int4 -- fully
-// coalesced), gathers g at their rows, sums the runs inside each lane
-// serially and joins runs that cross lanes with one segmented wave scan.
+// takes 1024 consecutive entries, gathers g at their rows (in wave order,
+// transposed through LDS to 16 consecutive entries per lane), sums the runs
+// inside each lane serially and joins runs that cross lanes with one
+// segmented wave scan.
 // Over a plain CSC (run = column) a column inside one wave is written with a
 // plain store and only the (at most two) runs cut by a wave boundary are
 // added atomically, so a heavy power-law column costs its entries, not a
 // serial loop of one thread (the per-column chunk walk before this ran at
 // ~0.3 TB/s on 156M entries). The L-BFGS plan streams the entries ROW-BLOCK
-// major instead (runs = (block of 2^19 rows, column), all added atomically):
-// the g slice a block gathers from (2 MB) stays in L2, where the plain CSC's
-// uniformly random row gathers fetched a 128-byte line per 4-byte value from
-// the 16 MB g (~1.8 ms per 156M entries, MALL-bound).
+// major instead (runs = (block of 2^19 rows, column)): the g slice a block
+// gathers from (2 MB) stays in L2, where the plain CSC's uniformly random row
+// gathers fetched a 128-byte line per 4-byte value from the 16 MB g (1.8 ms
+// per 156M entries, MALL-bound). The run sums land in stream order in S
+// (coalesced), and k_glm_runs_reduce adds each column's <= 8 runs into the
+// gradient (adding the runs atomically into the 64 MB gradient instead
+// re-fetched its lines once per block: 1.07 ms, 13M atomics).
 #include "wh_common.h"
 #include "wh_kernels.h"
 
@@ -140,7 +144,7 @@ __global__ __launch_bounds__(kT) void k_sum_parts(const double* __restrict__ par
 
 __device__ __forceinline__ void xtg_emit(const int32_t* ucol, int col, float v, bool atomic,
                                          float* grad) {
-  const int32_t gi = ucol[col];
+  const int32_t gi = ucol ? ucol[col] : col;
   if (gi < 0) return;
   if (atomic) atomicAdd(grad + gi, v);
   else grad[gi] = v;
@@ -157,31 +161,41 @@ __global__ __launch_bounds__(kT) void k_glm_xtg(int64_t nnz, const int32_t* __re
   const int64_t wv = ((int64_t)blockIdx.x * kT + threadIdx.x) >> 6;
   const int64_t wbase = wv * kXW;
   if (wbase >= nnz) return;  // (uniform per wave)
-  const int64_t p0 = wbase + (int64_t)lane * kXE;
   const bool full = wbase + kXW <= nnz;
-  int32_t r[kXE];
-  if (full) {
-    const int4* rp = reinterpret_cast<const int4*>(crow + p0);
+  // Gathers in WAVE order (instruction k reads entries wbase + 64 k + lane):
+  // a hot column's consecutive entries are rows a few apart, so the lanes of
+  // one gather share g's cache lines (each distinct line is one L2 request;
+  // lane-contiguous gathers put every lane on its own line). The values are
+  // then transposed through LDS to 16 consecutive entries per lane.
+  __shared__ float xs[kT / 64][kXW + kXW / 16];
+  float* xw = xs[threadIdx.x >> 6];
+  {
+    int32_t r[kXE];
 #pragma unroll
-    for (int q = 0; q < kXE / 4; ++q) {
-      const int4 v = rp[q];
-      r[4 * q] = v.x;
-      r[4 * q + 1] = v.y;
-      r[4 * q + 2] = v.z;
-      r[4 * q + 3] = v.w;
+    for (int k = 0; k < kXE; ++k) {
+      const int64_t p = wbase + k * 64 + lane;
+      r[k] = (full || p < nnz) ? crow[p] : -1;
     }
-  } else {
+    float v[kXE];
 #pragma unroll
-    for (int k = 0; k < kXE; ++k) r[k] = p0 + k < nnz ? crow[p0 + k] : -1;
+    for (int k = 0; k < kXE; ++k) v[k] = r[k] >= 0 ? g[r[k]] : 0.f;
+    if (cval) {
+#pragma unroll
+      for (int k = 0; k < kXE; ++k)
+        if (r[k] >= 0) v[k] *= cval[wbase + k * 64 + lane];
+    }
+#pragma unroll
+    for (int k = 0; k < kXE; ++k) {
+      const int i = k * 64 + lane;
+      xw[i + (i >> 4)] = v[k];  // (one pad word per 16: conflict-free reads below)
+    }
   }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   float x[kXE];
 #pragma unroll
-  for (int k = 0; k < kXE; ++k) x[k] = r[k] >= 0 ? g[r[k]] : 0.f;
-  if (cval) {
-#pragma unroll
-    for (int k = 0; k < kXE; ++k)
-      if (r[k] >= 0) x[k] *= cval[p0 + k];
-  }
+  for (int k = 0; k < kXE; ++k) x[k] = xw[lane * (kXE + 1) + k];
   // this lane's 16 column-start bits (entries past nnz carry none)
   const uint32_t bits =
       (uint32_t)(hb[(wbase >> 6) + (lane >> 2)] >> ((lane & 3) * kXE)) & 0xffffu;
@@ -254,6 +268,22 @@ __global__ __launch_bounds__(kT) void k_glm_heads(const int64_t* __restrict__ cs
   if (csc_off[u + 1] > p) atomicOr(hb + (p >> 6), 1ull << (p & 63));
 }
 
+// grad[cgid[c]] = sum of the run sums S over column c's runs (rlist
+// [coff[c], coff[c + 1]), in block order: deterministic)
+__global__ __launch_bounds__(kT) void k_glm_runs_reduce(int64_t ncol,
+                                                        const int64_t* __restrict__ coff,
+                                                        const int32_t* __restrict__ rlist,
+                                                        const float* __restrict__ S,
+                                                        const int32_t* __restrict__ cgid,
+                                                        float* __restrict__ grad) {
+  const int64_t c = (int64_t)blockIdx.x * kT + threadIdx.x;
+  if (c >= ncol) return;
+  const int64_t b = coff[c], e = coff[c + 1];
+  float v = 0.f;
+  for (int64_t k = b; k < e; ++k) v += S[rlist[k]];
+  grad[cgid[c]] = v;
+}
+
 }  // namespace
 
 void sum_parts(const double* part, int nblk, int nv, double* out, hipStream_t s, int stride) {
@@ -284,6 +314,13 @@ void glm_fwd(int mode, int64_t nrows, const int64_t* off, const int32_t* gcol, c
     hipLaunchKernelGGL(k_glm_fwd<2>, dim3(nb), dim3(kT), 0, s, nrows, off, gcol, val, w, bias,
                        base, label, loss, out, part);
   if (mode != 2) sum_parts(part, nb, 2, sums, s);
+}
+
+void glm_runs_reduce(int64_t ncol, const int64_t* coff, const int32_t* rlist, const float* S,
+                     const int32_t* cgid, float* grad, hipStream_t s) {
+  if (ncol > 0)
+    hipLaunchKernelGGL(k_glm_runs_reduce, dim3(grid_for(ncol, kT)), dim3(kT), 0, s, ncol, coff,
+                       rlist, S, cgid, grad);
 }
 
 int64_t glm_xtg_waves(int64_t nnz) { return (nnz + kXW - 1) / kXW; }

@@ -449,8 +449,12 @@ void glm_fwd(int mode, int64_t nrows, const int64_t* off, const int32_t* gcol, c
              float* out, double* part, double* sums, hipStream_t s);
 // run-start bits of an entry stream (glm_heads_words(nnz) u64; run u starts
 // at off[u]) and X^T g into grad (zeroed by the caller) at the runs' global
-// indices ucol (all_atomic: several runs may share one index)
+// indices ucol (null: the run index itself; all_atomic: several runs may
+// share one index)
 int64_t glm_xtg_waves(int64_t nnz);
+// grad[cgid[c]] = sum_k S[rlist[k]] over k in [coff[c], coff[c + 1])
+void glm_runs_reduce(int64_t ncol, const int64_t* coff, const int32_t* rlist, const float* S,
+                     const int32_t* cgid, float* grad, hipStream_t s);
 int64_t glm_heads_words(int64_t nnz);
 void glm_heads(const int64_t* csc_off, int64_t U, uint64_t* hb, int64_t words, hipStream_t s);
 void glm_xtg(int64_t nnz, const int32_t* crow, const float* cval, const uint64_t* hb,

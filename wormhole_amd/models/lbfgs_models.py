@@ -115,8 +115,9 @@ class _GLMPlan:
     * the X^T stream: the valid entries ordered (row block, global id), rows
       ascending inside, as runs of one (block, id) each -- ``crow`` /
       ``cval`` per entry, the run-start bits ``hb``, the run of every
-      1024-entry wave's first entry ``col0`` and each run's global id
-      ``rucol`` (runs of one id in several blocks add atomically)."""
+      1024-entry wave's first entry ``col0``; and per id (``cgid``) its runs
+      in block order (``rlist`` [``coff[c]``, ``coff[c + 1]``)), summed by
+      the reduce."""
 
     def __init__(self, d, F):
         from .. import _native
@@ -129,6 +130,7 @@ class _GLMPlan:
         self.gcol = torch.where(lid >= 0, ucol[lid.clamp_min(0)],
                                 torch.full_like(d.lid, -1)).to(torch.int32).contiguous()
         self.label = d.label.float().contiguous()
+        self.none_i32 = torch.empty(0, dtype=torch.int32, device=dev)
         nrows = d.offset.numel() - 1
         gid = self.gcol.long()
         rows = torch.repeat_interleave(torch.arange(nrows, device=dev),
@@ -145,7 +147,18 @@ class _GLMPlan:
         if nnz > 1:
             starts[1:] = key[1:] != key[:-1]
         run_off = torch.nonzero(starts).view(-1)
-        self.rucol = (key[run_off] & ((1 << 31) - 1)).to(torch.int32)
+        rgid = key[run_off] & ((1 << 31) - 1)
+        self.nruns = run_off.numel()
+        # each id's runs in block order: the reduce of the run sums
+        rk, rperm = torch.sort(rgid, stable=True)
+        cst = torch.ones(rk.numel(), dtype=torch.bool, device=dev)
+        if rk.numel() > 1:
+            cst[1:] = rk[1:] != rk[:-1]
+        cpos = torch.nonzero(cst).view(-1)
+        self.cgid = rk[cpos].to(torch.int32)
+        self.coff = torch.cat([cpos, torch.tensor([rk.numel()], device=dev, dtype=torch.int64)])
+        self.rlist = rperm.to(torch.int32)
+        del rk, rperm, rgid
         run_off = torch.cat([run_off, torch.tensor([nnz], device=dev, dtype=torch.int64)])
         self.hb = self.hip.glm_heads(run_off, nnz)
         waves = (nnz + 1023) // 1024
@@ -237,7 +250,9 @@ class LinearObjective:
             g, sums = self._glm_fwd(1, w)
             p = self._plan()
             grad = torch.zeros_like(w)
-            p.hip.glm_xtg(p.crow, p.cval, p.hb, p.col0, p.rucol, g, grad, True)
+            S = torch.zeros(p.nruns, dtype=torch.float32, device=w.device)
+            p.hip.glm_xtg(p.crow, p.cval, p.hb, p.col0, p.none_i32, g, S)
+            p.hip.glm_runs_reduce(p.coff, p.rlist, S, p.cgid, grad)
             grad[F:F + 1].copy_(sums[1:2])
             if self.bsp.rank == 0 and self.reg_L2 != 0.0:
                 grad[:F] += self.reg_L2 * w[:F]
