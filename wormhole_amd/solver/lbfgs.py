@@ -220,22 +220,27 @@ class LBFGSSolver:
             tmp = self._history_dots(idx)
             self.bsp.allreduce(tmp)
             tmp = tmp.cpu()
-            for k, (a, b) in enumerate(idx):
-                self._set_dotbuf(a, b, float(tmp[k]))
-            # two-loop recursion on the dot basis (vector-free)
+            pa, pb = zip(*(self._dot_idx(a, b) for a, b in idx))
+            self.data[list(pa), list(pb)] = tmp.to(self.data.dtype)
+            # two-loop recursion on the dot basis (vector-free), in plain
+            # floats over the logical dot matrix (0-d tensor arithmetic here
+            # cost milliseconds of host time per iteration)
+            R = 2 * m + 1
+            phys = self.data.tolist()
+            mp = [self._map(i) for i in range(R)]
+            D = [[phys[mp[min(i, j)]][mp[max(i, j)]] for j in range(R)] for i in range(R)]
             alpha = [0.0] * n
-            delta = [0.0] * (2 * m + 1)
+            delta = [0.0] * R
             delta[2 * m] = 1.0
-            D = self.dotbuf
             for j in range(n - 1, -1, -1):
-                vsum = sum(delta[k] * D(k, j) for k in range(2 * m + 1))
-                alpha[j] = vsum / D(j, m + j)
+                vsum = sum(delta[k] * D[k][j] for k in range(R))
+                alpha[j] = vsum / D[j][m + j]
                 delta[m + j] -= alpha[j]
-            scale = D(n - 1, m + n - 1) / D(m + n - 1, m + n - 1)
+            scale = D[n - 1][m + n - 1] / D[m + n - 1][m + n - 1]
             delta = [x * scale for x in delta]
             for j in range(n):
-                vsum = sum(delta[k] * D(k, m + j) for k in range(2 * m + 1))
-                beta = vsum / D(j, m + j)
+                vsum = sum(delta[k] * D[k][m + j] for k in range(R))
+                beta = vsum / D[j][m + j]
                 delta[j] += alpha[j] - beta
             steep = self.H(2 * m)
             if self.hist.is_cuda:
