@@ -802,10 +802,13 @@ class KVStore {
   // rows of the reply buffer to allocate (>= segHS[P] + n). Returns (slot,
   // vpos [n+1], chain [n] (int32 view of the chain links), head uint8 [n],
   // rbuf [rows_cap, vstride], vcnt [P]).
+  // chain_in: a chain buffer [>= n] the preceding push on this stream
+  // zeroed (ps_push prep_chain), with vbase snapshotted there too: the open
+  // then skips its own prep launch
   std::vector<Tensor> ps_open(const Tensor& keys, bool use_cnt, const Tensor& segS,
                               const Tensor& segHS, int64_t rows_cap, bool insert, bool chains,
                               const std::vector<double>& h, int64_t threshold, bool l1_shrk,
-                              int64_t seed) {
+                              int64_t seed, const c10::optional<Tensor>& chain_in = c10::nullopt) {
     CHECK_DEV(keys); CHECK_CONT(keys);
     CHECK_IN(segS, torch::kInt64);
     CHECK_IN(segHS, torch::kInt64);
@@ -827,7 +830,13 @@ class KVStore {
     auto slot = torch::empty({std::max<int64_t>(n, 1)}, i32);
     auto wout = torch::empty({std::max<int64_t>(n, 1)}, f32);
     auto vpos = torch::empty({n + 1}, keys.options().dtype(torch::kInt64));
-    auto chain = torch::empty({std::max<int64_t>(n, 1)}, i32);
+    const bool prepped = chain_in.has_value() && chain_in->defined() && chain_in->numel() > 0;
+    if (prepped) {
+      CHECK_IN((*chain_in), torch::kInt32);
+      TORCH_CHECK(chain_in->numel() >= std::max<int64_t>(n, 1), "ps_open: prepped chain too small");
+      TORCH_CHECK(vbase_.defined(), "ps_open: prepped without a push prep");
+    }
+    auto chain = prepped ? *chain_in : torch::empty({std::max<int64_t>(n, 1)}, i32);
     auto head = torch::empty({std::max<int64_t>(n, 1)}, keys.options().dtype(torch::kUInt8));
     // linear (vstride 0): the reply is w_out itself (returned in rbuf's place)
     auto rbuf = torch::empty({vstride_ > 0 ? rows_cap : 0, (int64_t)std::max(vstride_, 1)}, f32);
@@ -847,17 +856,34 @@ class KVStore {
         insert ? 1 : 0, chains ? 1 : 0, (uint32_t)epoch_, ptr<int32_t>(vbase_),
         ptr<int64_t>(segS), ptr<int64_t>(segHS), P, lookback(keys.device()), ptr<int32_t>(slot),
         ptr<float>(wout), ptr<int64_t>(vpos), reinterpret_cast<uint32_t*>(chain.data_ptr()),
-        reinterpret_cast<uint8_t*>(head.data_ptr()), ptr<float>(rbuf), ptr<int64_t>(vcnt), s);
+        reinterpret_cast<uint8_t*>(head.data_ptr()), ptr<float>(rbuf), ptr<int64_t>(vcnt), s,
+        prepped ? 1 : 0);
     TORCH_CHECK(ok, "ps_open: limits exceeded (P <= 256, n < 2^24)");
     return {slot.narrow(0, 0, n), vpos, chain.narrow(0, 0, n), head.narrow(0, 0, n),
             vstride_ > 0 ? rbuf : wout.narrow(0, 0, n), vcnt};
+  }
+
+  // the next open's prep folded into a push (see ps_open chain_in): zero
+  // prep_chain's first prep_n entries and snapshot vnext into vbase
+  wh::PsPrep push_prep(const c10::optional<Tensor>& prep_chain, int64_t prep_n) {
+    wh::PsPrep pr;
+    if (!(prep_chain.has_value() && prep_chain->defined() && prep_chain->numel() > 0)) return pr;
+    CHECK_IN((*prep_chain), torch::kInt32);
+    TORCH_CHECK(prep_n >= 0 && prep_n <= prep_chain->numel(), "push prep: chain too small");
+    if (!vbase_.defined()) vbase_ = torch::empty({1}, vnext_.options());
+    pr.chain = reinterpret_cast<uint32_t*>(prep_chain->data_ptr());
+    pr.n = prep_n;
+    pr.vbase = ptr<int32_t>(vbase_);
+    return pr;
   }
 
   // Linear owner push of a P-shard minibatch: g [n] = the gradients pushed
   // for this owner's received keys (segment order); t0 = SGD requests so far.
   void ps_push_linear(const Tensor& slot, const c10::optional<Tensor>& chain,
                       const c10::optional<Tensor>& head, const Tensor& segS, const Tensor& g,
-                      int64_t algo, double alpha, double beta, double l1, double l2, double t0) {
+                      int64_t algo, double alpha, double beta, double l1, double l2, double t0,
+                      const c10::optional<Tensor>& prep_chain = c10::nullopt,
+                      int64_t prep_n = 0) {
     CHECK_IN(slot, torch::kInt32);
     CHECK_IN(segS, torch::kInt64);
     CHECK_IN(g, torch::kFloat32);
@@ -876,7 +902,8 @@ class KVStore {
     c10::DeviceGuard dg(slot.device());
     wh::LinearHP h{(int)algo, (float)alpha, (float)beta, (float)l1, (float)l2, 0.f};
     TORCH_CHECK(wh::ps_push_linear(table(), ptr<int32_t>(slot), cp, hp, n, ptr<int64_t>(segS),
-                                   (int)segS.numel() - 1, ptr<float>(g), h, t0, cur_stream(slot)),
+                                   (int)segS.numel() - 1, ptr<float>(g), h, t0, cur_stream(slot),
+                                   push_prep(prep_chain, prep_n)),
                 "ps_push_linear: limits exceeded (P <= 256)");
   }
 
@@ -885,7 +912,8 @@ class KVStore {
   void ps_push(const Tensor& slot, const Tensor& vpos, const c10::optional<Tensor>& chain,
                const c10::optional<Tensor>& head, const Tensor& segS, const Tensor& segHS,
                const Tensor& gbuf, const std::vector<double>& h, int64_t threshold, bool l1_shrk,
-               int64_t seed) {
+               int64_t seed, const c10::optional<Tensor>& prep_chain = c10::nullopt,
+               int64_t prep_n = 0) {
     CHECK_IN(slot, torch::kInt32);
     CHECK_IN(vpos, torch::kInt64);
     CHECK_IN(segS, torch::kInt64);
@@ -907,7 +935,8 @@ class KVStore {
     c10::DeviceGuard g(slot.device());
     TORCH_CHECK(wh::ps_push(table(), ptr<int32_t>(slot), ptr<int64_t>(vpos), cp, hp, n,
                             ptr<int64_t>(segS), ptr<int64_t>(segHS), P, ptr<float>(gbuf),
-                            dhp(h, threshold, l1_shrk, seed), cur_stream(slot)),
+                            dhp(h, threshold, l1_shrk, seed), cur_stream(slot),
+                            push_prep(prep_chain, prep_n)),
                 "ps_push: limits exceeded");
   }
 
@@ -3433,13 +3462,16 @@ PYBIND11_MODULE(_hip, m) {
       .def("difacto_push", &KVStore::difacto_push)
       .def("ps_open", &KVStore::ps_open, py::arg("keys"), py::arg("use_cnt"), py::arg("segS"),
            py::arg("segHS"), py::arg("rows_cap"), py::arg("insert"), py::arg("chains"), py::arg("h"),
-           py::arg("threshold"), py::arg("l1_shrk"), py::arg("seed"))
+           py::arg("threshold"), py::arg("l1_shrk"), py::arg("seed"),
+           py::arg("chain_in") = py::none())
       .def("ps_push", &KVStore::ps_push, py::arg("slot"), py::arg("vpos"), py::arg("chain"),
            py::arg("head"), py::arg("segS"), py::arg("segHS"), py::arg("gbuf"), py::arg("h"),
-           py::arg("threshold"), py::arg("l1_shrk"), py::arg("seed"))
+           py::arg("threshold"), py::arg("l1_shrk"), py::arg("seed"),
+           py::arg("prep_chain") = py::none(), py::arg("prep_n") = 0)
       .def("ps_push_linear", &KVStore::ps_push_linear, py::arg("slot"), py::arg("chain"),
            py::arg("head"), py::arg("segS"), py::arg("g"), py::arg("algo"), py::arg("alpha"),
-           py::arg("beta"), py::arg("l1"), py::arg("l2"), py::arg("t0"))
+           py::arg("beta"), py::arg("l1"), py::arg("l2"), py::arg("t0"),
+           py::arg("prep_chain") = py::none(), py::arg("prep_n") = 0)
       .def("grow", &KVStore::grow)
       .def("grow_v", &KVStore::grow_v)
       .def("summary", &KVStore::summary)

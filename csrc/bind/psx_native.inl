@@ -206,6 +206,11 @@ class PsxStep {
     PsxStP prev = pull_;
     if (prev && !prev->have_v) vcount_exchange(*prev);
     PsxStP st = new_step(send, recv, label, true, data_pass, prev.get());
+    // the open's chain buffer, prepared by the last push before it
+    const int64_t n_open = vsum(recv);
+    Tensor prep = torch::empty({std::max<int64_t>(n_open, 1)},
+                               torch::TensorOptions().dtype(torch::kInt32).device(torch::kCUDA, dev_));
+    bool prepped = false;
     // (C2, C3 and C1 stay three RCCL launches: grouped into one, RCCL split
     // the group's several operations per peer over serialised launches and
     // C1, which the open waits for, landed only behind the big C2 / C3 --
@@ -223,7 +228,8 @@ class PsxStep {
       reply(*prev);
       if (tau_ == 0 && prev->train) {
         grad(*prev, true);
-        owner_push(*prev);
+        owner_push(*prev, prep, n_open);
+        prepped = true;
       }
     }
     ht.mark(4);
@@ -231,11 +237,14 @@ class PsxStep {
     // minibatches back (each push lands tau - 1 calls after its transfer was
     // issued, max_concurrency = tau + 1 minibatches in flight)
     while (tau_ > 0 && (int64_t)pushes_.size() >= tau_) {
-      owner_push(*pushes_.front());
+      const bool last = (int64_t)pushes_.size() - 1 < tau_;
+      if (last) owner_push(*pushes_.front(), prep, n_open);
+      else owner_push(*pushes_.front());
+      prepped = prepped || last;
       pushes_.pop_front();
     }
     ht.mark(5);
-    open(*st, true);
+    open(*st, true, prepped ? prep : Tensor());
     pull_ = st;
     ht.mark(6);
     if (early) exchange_deferred();
@@ -609,13 +618,14 @@ class PsxStep {
     st.keys_o = a2a(1, rec, st.send, st.recv, ready, &st.w_c1);
   }
 
-  void open(PsxSt& st, bool insert) {
+  void open(PsxSt& st, bool insert, const Tensor& prepped = Tensor()) {
     st.w_c1.wait();
     const int64_t n = vsum(st.recv);
     if (insert) guard_before(n);
     const int64_t rows = linear_ ? 0 : vsum(st.Ho) + n;
     auto o = store_->ps_open(st.keys_o, st.use_cnt, st.segS_o, st.segHS_o, rows, insert, st.train,
-                             hp_, threshold_, l1_shrk_, seed_);
+                             hp_, threshold_, l1_shrk_, seed_,
+                             prepped.defined() ? c10::optional<Tensor>(prepped) : c10::nullopt);
     st.slot = o[0];
     st.vpos = o[1];
     st.chain = o[2];
@@ -698,15 +708,20 @@ class PsxStep {
     st.gvc = Tensor();
   }
 
-  void owner_push(PsxSt& st) {
+  // prep (defined): the next open's chain buffer, zeroed by this push's
+  // kernel together with the V-row snapshot (the open's prep launch saved
+  // on the compute stream's chain); prep_n its used length
+  void owner_push(PsxSt& st, const Tensor& prep = Tensor(), int64_t prep_n = 0) {
     st.w_c3.wait();
+    const c10::optional<Tensor> pc = prep.defined() ? c10::optional<Tensor>(prep) : c10::nullopt;
     if (linear_) {
       store_->ps_push_linear(st.slot, st.chain, st.head, st.segS_o, st.gpush, (int64_t)lin_hp_[0],
-                             lin_hp_[1], lin_hp_[2], lin_hp_[3], lin_hp_[4], (double)requests_);
+                             lin_hp_[1], lin_hp_[2], lin_hp_[3], lin_hp_[4], (double)requests_, pc,
+                             prep_n);
       requests_ += P_;  // one request per worker (ps-lite SGD's t)
     } else {
       store_->ps_push(st.slot, st.vpos, st.chain, st.head, st.segS_o, st.segHS_o, st.gpush, hp_,
-                      threshold_, l1_shrk_, seed_);
+                      threshold_, l1_shrk_, seed_, pc, prep_n);
     }
     st.gpush = st.slot = st.vpos = st.chain = st.head = Tensor();
   }

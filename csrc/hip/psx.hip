@@ -78,6 +78,23 @@ __device__ __forceinline__ unsigned long long next_ct(unsigned long long cur, ui
   return ((unsigned long long)nt << 32) | (uint32_t)((uint32_t)cur + add);
 }
 
+// a segment's V-row prefix published by k_ps_open (tagged granule; a spin
+// past its bound sets *err like the look-back and yields 0)
+__device__ __forceinline__ uint32_t seg_granule(const unsigned long long* g,
+                                                unsigned long long tag, unsigned int* err) {
+  unsigned long long v = lb_load(g);
+  unsigned spins = 0;
+  while ((v & 0xffffffff00000000ull) != tag) {
+    if (++spins > (1u << 22)) {
+      atomicOr(err, 1u);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    v = lb_load(g);
+  }
+  return (uint32_t)v;
+}
+
 // ---------------------------------------------------------------- owner open
 // keys: u64 [n] (rec == null) or 12-byte records rec [n x 3] int32 {key lo,
 // key hi, count}. Writes slot[n], w_out[n], vpos[n+1], chain[n] (train) and
@@ -89,7 +106,7 @@ __global__ __launch_bounds__(kThreads) void k_ps_open(
     const int32_t* __restrict__ vbase_p, const int64_t* __restrict__ segS,
     const int64_t* __restrict__ segHS, int P, Lookback lb, int ntiles, int32_t* __restrict__ slot_out,
     float* __restrict__ w_out, int64_t* __restrict__ vpos, uint32_t* __restrict__ chain,
-    uint8_t* __restrict__ head, float* __restrict__ rbuf) {
+    uint8_t* __restrict__ head, float* __restrict__ rbuf, int64_t* __restrict__ vcnt) {
   __shared__ uint32_t shs[16];
   __shared__ int sht;
   __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1];
@@ -229,6 +246,55 @@ __global__ __launch_bounds__(kThreads) void k_ps_open(
     run += row[r] >= 0 ? 1u : 0u;
   }
   if (tile == ntiles - 1 && threadIdx.x == 0) vpos[n] = tot[0];
+  if (t.vstride > 0) {
+    // The headers {w, row inside the peer's V block} of this tile's keys, in
+    // this launch (a separate pack kernel after the open cost a launch on
+    // the step's critical chain): a header goes to float (HS_p + VS_p) *
+    // vstride + 2 (i - S_p), and VS_p = vpos[S_p] is known to the tile
+    // holding item S_p once its look-back is done. That tile publishes it as
+    // a tagged granule (look-back channel 1, status 3: earlier launches'
+    // granules never match); readers wait only on tiles that took their
+    // ticket earlier (resident or finished), as the look-back itself does.
+    __shared__ uint32_t sv[kPullTile];
+    unsigned long long* sg = lb.gran + (size_t)kLbMaxTiles;
+    const unsigned long long tag = (unsigned long long)((lb.epoch << 2) | 3u) << 32;
+    const int64_t t0 = (int64_t)tile * kPullTile;
+    {
+      uint32_t rr = ex[0];
+#pragma unroll
+      for (int r = 0; r < kPullPer; ++r) {
+        sv[threadIdx.x * kPullPer + r] = rr;
+        rr += row[r] >= 0 ? 1u : 0u;
+      }
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p <= P; p += blockDim.x) {
+      const int64_t sp = sS[p];
+      if (sp >= t0 && sp < t0 + kPullTile && sp < n)
+        lb_store(sg + p, tag | sv[sp - t0]);
+      else if (sp >= n && tile == ntiles - 1)
+        lb_store(sg + p, tag | tot[0]);
+    }
+    int cp = -1;
+    uint32_t cvs = 0;
+#pragma unroll
+    for (int r = 0; r < kPullPer; ++r) {
+      const int64_t i = i0 + r;
+      if (i >= n) break;
+      const int p = seg_of(sS, P, i);
+      if (p != cp) {
+        cp = p;
+        cvs = seg_granule(sg + p, tag, lb.err);
+      }
+      const int32_t j = row[r] >= 0 ? (int32_t)(sv[threadIdx.x * kPullPer + r] - cvs) : -1;
+      *reinterpret_cast<float2*>(rbuf + (sHS[p] + cvs) * t.vstride + 2 * (i - sS[p])) =
+          make_float2(w[r], __int_as_float(j));
+    }
+    if (tile == ntiles - 1)
+      for (int p = threadIdx.x; p < P; p += blockDim.x)
+        vcnt[p] = (int64_t)seg_granule(sg + p + 1, tag, lb.err) -
+                  (int64_t)seg_granule(sg + p, tag, lb.err);
+  }
   const long long ci = wave_sum_ll(created), cf = wave_sum_ll(failed), cv = wave_sum_ll(newv);
   if (lane == 0) {
     if (ci) atomicAdd(stat_ptr(t.stats, 4), (unsigned long long)ci);
@@ -471,12 +537,21 @@ __device__ __forceinline__ int64_t chain_next_after(const uint32_t* chain, int64
   return best;
 }
 
+// the next open's prep (PsPrep), folded into a push launch
+__device__ __forceinline__ void ps_prep_in(const PsPrep& pr, const int32_t* vnext) {
+  if (pr.vbase && blockIdx.x == 0 && threadIdx.x == 0) *pr.vbase = *vnext;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < pr.n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    pr.chain[i] = 0u;
+}
+
 template <int G>
 __global__ __launch_bounds__(kThreads) void k_ps_push(
     KVTable t, const int32_t* __restrict__ slot, const int64_t* __restrict__ vpos,
     const uint32_t* __restrict__ chain, const uint8_t* __restrict__ headf, int64_t n,
     const int64_t* __restrict__ segS, const int64_t* __restrict__ segHS, int P,
-    const float* __restrict__ gbuf, DifactoHP hp) {
+    const float* __restrict__ gbuf, DifactoHP hp, PsPrep prep) {
+  ps_prep_in(prep, t.vnext);  // (before any row of this push is allocated)
   __shared__ int64_t sS[kMaxSeg + 1], sHS[kMaxSeg + 1], sVS[kMaxSeg + 1];
   load_seg(segS, sS, P);
   load_seg(segHS, sHS, P);
@@ -642,7 +717,8 @@ __global__ __launch_bounds__(kThreads) void k_ps_push(
 __global__ __launch_bounds__(kThreads) void k_psl_push(
     KVTable t, const int32_t* __restrict__ slot, const uint32_t* __restrict__ chain,
     const uint8_t* __restrict__ headf, int64_t n, const int64_t* __restrict__ segS, int P,
-    const float* __restrict__ g, LinearHP hp, double t0) {
+    const float* __restrict__ g, LinearHP hp, double t0, PsPrep prep) {
+  ps_prep_in(prep, t.vnext);
   __shared__ int64_t sS[kMaxSeg + 1];
   load_seg(segS, sS, P);
   __syncthreads();
@@ -670,11 +746,11 @@ __global__ __launch_bounds__(kThreads) void k_psl_push(
 
 bool ps_push_linear(const KVTable& t, const int32_t* slot, const uint32_t* chain,
                     const uint8_t* head, int64_t n, const int64_t* segS, int P, const float* g,
-                    LinearHP hp, double t0, hipStream_t s) {
+                    LinearHP hp, double t0, hipStream_t s, PsPrep prep) {
   if (P < 1 || P > kMaxSeg || t.vstride != 0) return false;
-  if (n <= 0) return true;
-  hipLaunchKernelGGL(k_psl_push, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t, slot,
-                     chain, head, n, segS, P, g, hp, t0);
+  if (n <= 0 && prep.n <= 0 && !prep.vbase) return true;
+  hipLaunchKernelGGL(k_psl_push, dim3(grid_for(n > prep.n ? n : prep.n, kThreads)),
+                     dim3(kThreads), 0, s, t, slot, chain, head, n, segS, P, g, hp, t0, prep);
   return true;
 }
 
@@ -682,13 +758,14 @@ bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t
              DifactoHP hp, int insert, int chains, uint32_t epoch, int32_t* vbase,
              const int64_t* segS, const int64_t* segHS, int P, const Lookback& lb, int32_t* slot,
              float* w_out, int64_t* vpos, uint32_t* chain, uint8_t* head, float* rbuf,
-             int64_t* vcnt, hipStream_t s) {
+             int64_t* vcnt, hipStream_t s, int prepped) {
   const int64_t ntiles = (n + kPullTile - 1) / kPullTile;
   if (P < 1 || P > kMaxSeg || ntiles > kLbMaxTiles || n >= (1 << 24) || epoch < 1 ||
       epoch > 255)
     return false;
-  hipLaunchKernelGGL(k_ps_prep, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, chain,
-                     chains ? n : 0, t.vnext, vbase);
+  if (!prepped)
+    hipLaunchKernelGGL(k_ps_prep, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, chain,
+                       chains ? n : 0, t.vnext, vbase);
   if (epoch == 1) {  // a new epoch cycle: no tag of the previous cycle may survive
     hipLaunchKernelGGL(k_ps_sweep_tags, dim3(grid_for(t.cap, kThreads, 8192)), dim3(kThreads), 0,
                        s, t.sl, t.cap);
@@ -697,25 +774,27 @@ bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t
     const int G = lanes_per_key(t.vstride);
     WH_DISPATCH_G(G, k_ps_open, dim3((unsigned)ntiles), dim3(kThreads), 0, s, t, keys, rec, n, hp,
                   insert, use_cnt, chains, epoch, vbase, segS, segHS, P, lb, (int)ntiles, slot,
-                  w_out, vpos, chain, head, rbuf);
+                  w_out, vpos, chain, head, rbuf, vcnt);
   } else {
     WH_HIP_CHECK(hipMemsetAsync(vpos, 0, sizeof(int64_t), s));
+    // (no keys: only the per-peer V row counts, all zero)
+    if (t.vstride > 0)
+      hipLaunchKernelGGL(k_ps_pack_hdr, dim3(1), dim3(kThreads), 0, s, w_out, vpos, n,
+                         t.vstride, segS, segHS, P, rbuf, vcnt);
   }
-  // linear (vstride 0): the reply is w_out itself, one float per key
-  if (t.vstride > 0)
-    hipLaunchKernelGGL(k_ps_pack_hdr, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, w_out,
-                       vpos, n, t.vstride, segS, segHS, P, rbuf, vcnt);
+  // linear (vstride 0): the reply is w_out itself, one float per key; the
+  // headers of the embedding model are written by the open
   return true;
 }
 
 bool ps_push(const KVTable& t, const int32_t* slot, const int64_t* vpos, const uint32_t* chain,
              const uint8_t* head, int64_t n, const int64_t* segS, const int64_t* segHS, int P,
-             const float* gbuf, DifactoHP hp, hipStream_t s) {
+             const float* gbuf, DifactoHP hp, hipStream_t s, PsPrep prep) {
   if (P < 1 || P > kMaxSeg || t.vstride == 0) return false;
-  if (n <= 0) return true;
+  if (n <= 0 && prep.n <= 0 && !prep.vbase) return true;
   const int G = lanes_per_key(t.vstride);
-  WH_DISPATCH_G(G, k_ps_push, dim3(grid_for(n, kThreads)), dim3(kThreads), 0, s, t, slot, vpos,
-                chain, head, n, segS, segHS, P, gbuf, hp);
+  WH_DISPATCH_G(G, k_ps_push, dim3(grid_for(n > prep.n ? n : prep.n, kThreads)), dim3(kThreads),
+                0, s, t, slot, vpos, chain, head, n, segS, segHS, P, gbuf, hp, prep);
   return true;
 }
 

@@ -246,14 +246,22 @@ bool vidx_renumber_fused(float* hdr, int64_t n, const Lookback& lb, int64_t* cou
 // ps_unpack / ps_pack_gw: worker side (segments = keys sent per owner,
 //   vrecv[P] = V rows received per owner).
 // Each returns false when its limits are exceeded (P > 256, n >= 2^24).
+// PsPrep: the next open's preparation done by a push kernel that runs
+// right before it on the same stream (zero chain[n], *vbase = vnext at the
+// push's start); an open given prepped != 0 then skips its own prep launch.
+struct PsPrep {
+  uint32_t* chain = nullptr;
+  int64_t n = 0;
+  int32_t* vbase = nullptr;
+};
 bool ps_open(const KVTable& t, const uint64_t* keys, const int32_t* rec, int64_t n, int use_cnt,
              DifactoHP hp, int insert, int chains, uint32_t epoch, int32_t* vbase,
              const int64_t* segS, const int64_t* segHS, int P, const Lookback& lb, int32_t* slot,
              float* w_out, int64_t* vpos, uint32_t* chain, uint8_t* head, float* rbuf,
-             int64_t* vcnt, hipStream_t s);
+             int64_t* vcnt, hipStream_t s, int prepped = 0);
 bool ps_push(const KVTable& t, const int32_t* slot, const int64_t* vpos, const uint32_t* chain,
              const uint8_t* head, int64_t n, const int64_t* segS, const int64_t* segHS, int P,
-             const float* gbuf, DifactoHP hp, hipStream_t s);
+             const float* gbuf, DifactoHP hp, hipStream_t s, PsPrep prep = PsPrep());
 // worker: 12-byte {lo, hi, count} records of the key exchange (ucnt may be null)
 void ps_records(const uint64_t* uniq, const int32_t* ucnt, int64_t U, int32_t* rec,
                 hipStream_t s);
@@ -266,7 +274,7 @@ bool ps_c0(const int64_t* owner_cnt, const int64_t* vcnt, int S, int P, int64_t 
 // their key's gradients in peer order; SGD request counter starts at t0
 bool ps_push_linear(const KVTable& t, const int32_t* slot, const uint32_t* chain,
                     const uint8_t* head, int64_t n, const int64_t* segS, int P, const float* g,
-                    LinearHP hp, double t0, hipStream_t s);
+                    LinearHP hp, double t0, hipStream_t s, PsPrep prep = PsPrep());
 bool ps_unpack(const float* rbuf, int64_t U, int vstride, const int64_t* segS,
                const int64_t* segHS, const int64_t* vrecv, int P, float* hdr, int64_t* rows_total,
                hipStream_t s);
