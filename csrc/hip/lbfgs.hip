@@ -238,7 +238,7 @@ bool hist_dots(const float* H, int R, int64_t n, int64_t ld, const int32_t* prob
   if (K < 1 || K > 4 || R < 1 || (n & 3) || (ld & 3) ||
       (reinterpret_cast<uintptr_t>(H) & 15))
     return false;
-  constexpr int RM = 8;
+  constexpr int RM = 11;
   const int4 pr = make_int4(probe[0], K > 1 ? probe[1] : 0, K > 2 ? probe[2] : 0,
                             K > 3 ? probe[3] : 0);
   const unsigned nb = red_blocks(n / 4);

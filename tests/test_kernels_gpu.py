@@ -775,6 +775,47 @@ def test_ps_open_rejects_more_than_2_24_keys(hip):
     assert int((out[0] >= 0).sum()) == 100  # every key got a slot
 
 
+def test_ps_open_headers_uneven_segments(hip):
+    """The owner open writes each peer region's headers itself (segment
+    V-row prefixes published between tiles): empty leading / middle /
+    trailing segments and segments spanning several 1024-key tiles land at
+    (HS_p + VS_p) * vstride + 2 (i - S_p) with the row index inside the
+    peer's V block, and vcnt[p] counts each peer's rows."""
+    from wormhole_amd.kv import make_store
+    st = make_store(1 << 14, 1 << 13, 16, DEV)
+    sizes = [0, 700, 0, 1500, 3, 0, 2100, 0]
+    P, n = len(sizes), sum(sizes)
+    g = torch.Generator().manual_seed(9)
+    keys = torch.randperm(1 << 20, generator=g)[:n].long() * 2654435761 + 5
+    cnt = (torch.arange(n) % 3 == 0).to(torch.int32) * 5
+    rec = torch.cat([keys.view(torch.int32).view(n, 2), cnt[:, None]], 1).contiguous()  # {lo, hi, count}
+    vs = 16
+    S = [0]
+    for z in sizes:
+        S.append(S[-1] + z)
+    H = [0]
+    for z in sizes:
+        H.append(H[-1] + (2 * z + vs - 1) // vs)
+    segS = torch.tensor(S, dtype=torch.int64, device=DEV)
+    segHS = torch.tensor(H, dtype=torch.int64, device=DEV)
+    hp = [0.1, 1.0, 0.0, 0.0, 0.1, 1.0, 0.0, 0.01]
+    slot, vpos, chain, head, rbuf, vcnt = st.ps_open(rec.to(DEV), True, segS, segHS, H[-1] + n,
+                                                     True, True, hp, 2, False, 0)
+    assert rbuf.shape[1] == vs
+    vp = vpos.cpu().tolist()
+    assert vp[n] == sum(1 for i in range(n) if i % 3 == 0)  # count 5 > threshold 2
+    flat = rbuf.cpu().view(-1)
+    bits = flat.view(torch.int32)
+    for p in range(P):
+        VS = vp[S[p]]
+        assert int(vcnt[p]) == vp[S[p + 1]] - VS
+        base = (H[p] + VS) * vs
+        for i in range(S[p], S[p + 1]):
+            j = vp[i] - VS if vp[i + 1] > vp[i] else -1
+            assert float(flat[base + 2 * (i - S[p])]) == 0.0  # fresh keys: w = 0
+            assert int(bits[base + 2 * (i - S[p]) + 1]) == j, (p, i)
+
+
 def test_localize_hint_scales_with_minibatch_size(hip):
     """Uneven minibatches (CRB records cut parts into short and long blocks):
     a job begun with the previous, much smaller minibatch's unique count as
