@@ -719,13 +719,20 @@ class Psx:
             ok = (self.cuda and os.environ.get("WH_PSX_NATIVE", "1") != "0" and tx is not None
                   and self.qf is None and self.timer is None and not post)
             self._nat = False
+            rccl = None
+            if ok and tx == hip.PSX_TX_RCCL:
+                try:
+                    rccl = (self.comm.rccl("c0"), self.comm.rccl("c1"), self.comm.rccl("c23"))
+                except RuntimeError as e:  # (every rank fails alike: the Python step serves)
+                    print("[psx] own RCCL communicators unavailable (%s): the Python step "
+                          "exchanges over the c10d group" % str(e).splitlines()[0], flush=True)
+                    ok = False
             if ok:
                 self._nat = hip.PsxStep(
                     store=self.store, P=self.P, S=self.nshard,
                     rank=int(getattr(self.comm, "rank", 0)), tx=tx,
                     pg=self.comm.pg if tx == hip.PSX_TX_STAGED else None,
-                    rccl=(self.comm.rccl("c0"), self.comm.rccl("c1"), self.comm.rccl("c23"))
-                    if tx == hip.PSX_TX_RCCL else None,
+                    rccl=rccl,
                     linear=self.linear,
                     lin_hp=list(self.lin_hp) if self.linear else [0.0] * 5,
                     hp=list(lrn.hp), threshold=int(lrn.threshold), l1_shrk=bool(lrn.l1_shrk),
