@@ -181,10 +181,15 @@ __global__ __launch_bounds__(kThreads) void k_difacto_pull(KVTable t, const int3
   const int lane = threadIdx.x & 63;
   const int64_t i0 = (int64_t)tile * kPullTile + threadIdx.x * kPullPer;
   int32_t sl[kPullPer];
-  if (i0 + kPullPer <= n && (reinterpret_cast<uintptr_t>(slot) & 15) == 0) {
-    const int4 q = *reinterpret_cast<const int4*>(slot + i0);
-    sl[0] = q.x; sl[1] = q.y; sl[2] = q.z; sl[3] = q.w;
-  } else {
+  bool vec = false;
+  if constexpr (kPullPer == 4) {
+    if (i0 + kPullPer <= n && (reinterpret_cast<uintptr_t>(slot) & 15) == 0) {
+      const int4 q = *reinterpret_cast<const int4*>(slot + i0);
+      sl[0] = q.x; sl[1] = q.y; sl[2] = q.z; sl[3] = q.w;
+      vec = true;
+    }
+  }
+  if (!vec) {
 #pragma unroll
     for (int r = 0; r < kPullPer; ++r) sl[r] = i0 + r < n ? slot[i0 + r] : -1;
   }
