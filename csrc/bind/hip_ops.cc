@@ -2095,7 +2095,7 @@ std::vector<c10::optional<Tensor>> glm_fwd(int64_t mode, const Tensor& offset, c
   CHECK_IN(offset, torch::kInt64);
   CHECK_IN(gcol, torch::kInt32);
   CHECK_IN(w, torch::kFloat32);
-  TORCH_CHECK(mode >= 0 && mode <= 2, "glm_fwd: mode 0 / 1 / 2");
+  TORCH_CHECK(mode >= 0 && mode <= 3, "glm_fwd: mode 0 / 1 / 2 / 3");
   TORCH_CHECK(bias < w.numel(), "glm_fwd: bias index out of range");
   const int64_t nrows = offset.numel() - 1;
   if (mode != 2) {
@@ -2121,6 +2121,22 @@ std::vector<c10::optional<Tensor>> glm_fwd(int64_t mode, const Tensor& offset, c
               out.has_value() ? ptr<float>(*out) : nullptr,
               mode != 2 ? ptr<double>(part) : nullptr,
               sums.has_value() ? ptr<double>(*sums) : nullptr, cur_stream(w));
+  return {out, sums};
+}
+
+// (pred - label, [loss, sum]) from the margins glm_fwd mode 3 stored
+std::vector<Tensor> glm_grad_from_margin(const Tensor& margin, const Tensor& label, int64_t loss) {
+  CHECK_IN(margin, torch::kFloat32);
+  CHECK_IN(label, torch::kFloat32);
+  TORCH_CHECK(margin.numel() == label.numel(), "glm_grad_from_margin: sizes differ");
+  c10::DeviceGuard g(margin.device());
+  const int64_t n = margin.numel();
+  auto out = torch::empty({n}, margin.options());
+  auto sums = torch::empty({2}, margin.options().dtype(torch::kFloat64));
+  auto part = torch::empty({std::max<int64_t>(2 * wh::glm_fwd_blocks(n), 2)},
+                           margin.options().dtype(torch::kFloat64));
+  wh::glm_grad_from_margin(n, ptr<float>(margin), ptr<float>(label), (int)loss, ptr<float>(out),
+                           ptr<double>(part), ptr<double>(sums), cur_stream(margin));
   return {out, sums};
 }
 
@@ -3400,6 +3416,8 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("w"), py::arg("bias"), py::arg("base"), py::arg("label"), py::arg("loss"));
   m.def("glm_xtg", &glm_xtg, py::arg("crow"), py::arg("cval"), py::arg("hb"), py::arg("col0"),
         py::arg("ucol"), py::arg("g"), py::arg("grad"), py::arg("all_atomic") = false);
+  m.def("glm_grad_from_margin", &glm_grad_from_margin, py::arg("margin"), py::arg("label"),
+        py::arg("loss"));
   m.def("glm_runs_reduce", &glm_runs_reduce, py::arg("coff"), py::arg("rlist"), py::arg("S"),
         py::arg("cgid"), py::arg("grad"));
   m.def("gbdt_leaf_add", &gbdt_leaf_add);

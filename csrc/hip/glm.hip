@@ -53,7 +53,9 @@ __device__ __forceinline__ float logistic_loss(float y, float m) {
 }
 
 // MODE 0: loss partials; 1: g = pred - label into out + {loss, sum g}
-// partials; 2: margins into out
+// partials; 2: margins into out; 3: margins into out + loss partials (an
+// objective evaluation whose margins the next gradient at the same weights
+// reuses)
 template <int MODE>
 __global__ __launch_bounds__(kT) void k_glm_fwd(int64_t nrows, const int64_t* __restrict__ off,
                                                 const int32_t* __restrict__ gcol,
@@ -93,9 +95,8 @@ __global__ __launch_bounds__(kT) void k_glm_fwd(int64_t nrows, const int64_t* __
     }
     const float m = group_sum<kFwdG>(acc) + b0;
     if (gl == 0) {
-      if (MODE == 2) {
-        out[row] = m;
-      } else {
+      if (MODE == 2 || MODE == 3) out[row] = m;
+      if (MODE != 2) {
         const float y = label[row];
         float l;
         if (loss == 1) {
@@ -119,6 +120,46 @@ __global__ __launch_bounds__(kT) void k_glm_fwd(int64_t nrows, const int64_t* __
   sl = wave_sum_d(sl);
   sg = wave_sum_d(sg);
   if (lane == 0) {
+    sh[0][threadIdx.x >> 6] = sl;
+    sh[1][threadIdx.x >> 6] = sg;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double s = 0.0;
+    for (int i = 0; i < kT / 64; ++i) s += sh[threadIdx.x][i];
+    part[2 * (int64_t)blockIdx.x + threadIdx.x] = s;
+  }
+}
+
+// g = pred - label from stored margins + {loss, sum g} partials (the
+// gradient pass at weights whose margins an evaluation just computed)
+__global__ __launch_bounds__(kT) void k_glm_from_margin(int64_t nrows,
+                                                        const float* __restrict__ margin,
+                                                        const float* __restrict__ label, int loss,
+                                                        float* __restrict__ g_out,
+                                                        double* __restrict__ part) {
+  double sl = 0.0, sg = 0.0;
+  for (int64_t row = (int64_t)blockIdx.x * kT + threadIdx.x; row < nrows;
+       row += (int64_t)gridDim.x * kT) {
+    const float m = margin[row], y = label[row];
+    float l, p;
+    if (loss == 1) {
+      l = logistic_loss(y, m);
+      p = 1.f / (1.f + expf(-m));
+    } else {
+      const float d = m - y;
+      l = 0.5f * d * d;
+      p = m;
+    }
+    const float g = p - y;
+    g_out[row] = g;
+    sl += (double)l;
+    sg += (double)g;
+  }
+  __shared__ double sh[2][kT / 64];
+  sl = wave_sum_d(sl);
+  sg = wave_sum_d(sg);
+  if ((threadIdx.x & 63) == 0) {
     sh[0][threadIdx.x >> 6] = sl;
     sh[1][threadIdx.x >> 6] = sg;
   }
@@ -310,8 +351,11 @@ void glm_fwd(int mode, int64_t nrows, const int64_t* off, const int32_t* gcol, c
   else if (mode == 1)
     hipLaunchKernelGGL(k_glm_fwd<1>, dim3(nb), dim3(kT), 0, s, nrows, off, gcol, val, w, bias,
                        base, label, loss, out, part);
-  else
+  else if (mode == 2)
     hipLaunchKernelGGL(k_glm_fwd<2>, dim3(nb), dim3(kT), 0, s, nrows, off, gcol, val, w, bias,
+                       base, label, loss, out, part);
+  else
+    hipLaunchKernelGGL(k_glm_fwd<3>, dim3(nb), dim3(kT), 0, s, nrows, off, gcol, val, w, bias,
                        base, label, loss, out, part);
   if (mode != 2) sum_parts(part, nb, 2, sums, s);
 }
@@ -321,6 +365,18 @@ void glm_runs_reduce(int64_t ncol, const int64_t* coff, const int32_t* rlist, co
   if (ncol > 0)
     hipLaunchKernelGGL(k_glm_runs_reduce, dim3(grid_for(ncol, kT)), dim3(kT), 0, s, ncol, coff,
                        rlist, S, cgid, grad);
+}
+
+void glm_grad_from_margin(int64_t nrows, const float* margin, const float* label, int loss,
+                          float* g, double* part, double* sums, hipStream_t s) {
+  if (nrows <= 0) {
+    WH_HIP_CHECK(hipMemsetAsync(sums, 0, 2 * sizeof(double), s));
+    return;
+  }
+  const int nb = (int)glm_fwd_blocks(nrows);
+  hipLaunchKernelGGL(k_glm_from_margin, dim3(nb), dim3(kT), 0, s, nrows, margin, label, loss, g,
+                     part);
+  sum_parts(part, nb, 2, sums, s);
 }
 
 int64_t glm_xtg_waves(int64_t nnz) { return (nnz + kXW - 1) / kXW; }

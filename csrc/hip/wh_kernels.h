@@ -449,12 +449,16 @@ bool multi_dot(const float* H, int R, int64_t n, const int32_t* ia, const int32_
 // order; stride 0 = nv)
 void sum_parts(const double* part, int nblk, int nv, double* out, hipStream_t s, int stride = 0);
 // linear-model rows over the prepared split (glm.hip header): mode 0 sums[0]
-// = loss; 1 also out = pred - label and sums[1] = its sum; 2 out = margin.
+// = loss; 1 also out = pred - label and sums[1] = its sum; 2 out = margin;
+// 3 out = margin and sums[0] = loss.
 // part: glm_fwd_blocks(nrows) * 2 doubles
 int64_t glm_fwd_blocks(int64_t nrows);
 void glm_fwd(int mode, int64_t nrows, const int64_t* off, const int32_t* gcol, const float* val,
              const float* w, const float* bias, float base, const float* label, int loss,
              float* out, double* part, double* sums, hipStream_t s);
+// g = pred - label from margins (+ sums {loss, sum g}; part as glm_fwd)
+void glm_grad_from_margin(int64_t nrows, const float* margin, const float* label, int loss,
+                          float* g, double* part, double* sums, hipStream_t s);
 // run-start bits of an entry stream (glm_heads_words(nnz) u64; run u starts
 // at off[u]) and X^T g into grad (zeroed by the caller) at the runs' global
 // indices ucol (null: the run index itself; all_atomic: several runs may

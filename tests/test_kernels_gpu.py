@@ -437,13 +437,17 @@ def test_glm_objective_matches_cpu(with_val, loss):
         o.param.base_score = 0.1
         objs.append(o)
     w = torch.randn(F + 1, generator=g) * 0.05
+    wd = w.to(DEV)
     lc = objs[0].eval(w)
-    lg = objs[1].eval(w.to(DEV))
+    lg = objs[1].eval(wd)
     assert abs(lg - lc) <= 1e-5 * abs(lc)
     gc = objs[0].calc_grad(w)
-    gg = objs[1].calc_grad(w.to(DEV)).cpu()
     scale = float(gc.abs().max())
-    assert torch.allclose(gg, gc, rtol=1e-4, atol=1e-5 * scale)
+    # the gradient at the weights just evaluated reuses their margins; a
+    # second call recomputes them
+    for _ in range(2):
+        gg = objs[1].calc_grad(wd).cpu()
+        assert torch.allclose(gg, gc, rtol=1e-4, atol=1e-5 * scale)
     mc = objs[0].margin(w)
     mg = objs[1].margin(w.to(DEV)).cpu()
     assert torch.allclose(mg, mc, rtol=1e-5, atol=1e-5)

@@ -234,7 +234,11 @@ class LinearObjective:
     def eval(self, w):
         F = self.param.num_feature
         if w.is_cuda:  # margin + loss in one pass (glm.hip k_glm_fwd)
-            val = float(self._glm_fwd(0, w)[1][0])
+            m, sums = self._glm_fwd(3, w)
+            # the accepted point of a line search is the next gradient's: its
+            # margins are kept for calc_grad (one SpMV per iteration saved)
+            self._mcache = (w, w._version, self.param.num_feature, m)
+            val = float(sums[0])
         else:
             val = float(margin_to_loss(self.param.loss_type, self.d.label, self.margin(w)).sum(
                 dtype=torch.float64))
@@ -247,8 +251,13 @@ class LinearObjective:
     def calc_grad(self, w):
         F = self.param.num_feature
         if w.is_cuda:  # pred - label, then X^T of it (glm.hip)
-            g, sums = self._glm_fwd(1, w)
+            mc = getattr(self, "_mcache", None)
             p = self._plan()
+            if mc is not None and mc[0] is w and mc[1] == w._version and mc[2] == F:
+                g, sums = p.hip.glm_grad_from_margin(mc[3], p.label, int(self.param.loss_type))
+            else:
+                g, sums = self._glm_fwd(1, w)
+            self._mcache = None
             grad = torch.zeros_like(w)
             S = torch.zeros(p.nruns, dtype=torch.float32, device=w.device)
             p.hip.glm_xtg(p.crow, p.cval, p.hb, p.col0, p.none_i32, g, S)
@@ -346,7 +355,11 @@ class FMObjective(LinearObjective):
 
     def eval(self, w):
         F, k = self.param.num_feature, self.nfactor
-        val = float(margin_to_loss(self.param.loss_type, self.d.label, self.margin(w)).sum(
+        fw = self._forward(w)
+        # (kept for a gradient at the same weights: the accepted line-search
+        # point's forward is not run twice)
+        self._fcache = (w, w._version, F, fw)
+        val = float(margin_to_loss(self.param.loss_type, self.d.label, fw[0]).sum(
             dtype=torch.float64))
         if self.bsp.rank == 0:
             if self.reg_L2 != 0.0:
@@ -359,7 +372,12 @@ class FMObjective(LinearObjective):
 
     def calc_grad(self, w):
         F, k = self.param.num_feature, self.nfactor
-        margin, (hdr, vc), vs, xv = self._forward(w)
+        fc = getattr(self, "_fcache", None)
+        self._fcache = None
+        if fc is not None and fc[0] is w and fc[1] == w._version and fc[2] == F:
+            margin, (hdr, vc), vs, xv = fc[3]
+        else:
+            margin, (hdr, vc), vs, xv = self._forward(w)
         g = (margin_to_pred(self.param.loss_type, margin) - self.d.label).contiguous()
         gw, gvc = ops.fm_backward(self.d.csc_off, self.d.csc_row, self.d.csc_val, g, xv, hdr, vc,
                                   vs)
