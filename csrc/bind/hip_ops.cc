@@ -12,6 +12,7 @@
 #include <torch/csrc/distributed/c10d/Work.hpp>
 
 #include <algorithm>
+#include <map>
 #include <array>
 #include <cstdio>
 #include <cstdlib>
@@ -87,6 +88,11 @@ struct DevWs {
   // heavy-id hints, double-buffered by job parity: keys [2][kPartMaxHeavy]
   // u64, then counts [2][kPartMaxOwners] u32
   Tensor heavy_ws;
+  // the backward's scratch (chunk lists, bucket histograms, offsets) per
+  // stream, grow-only: reused in stream order by the next backward on the
+  // same stream (eight allocations per call were ~20 us of host time, the
+  // bound of the small-minibatch multi-shard step)
+  std::map<hipStream_t, std::vector<Tensor>> bwd_scratch;
   int heavy_parity = 0;
   int64_t heavy_layout = -1;  // nshard * 65536 + nho of the set the last job elected
   int part_inflight = 0;
@@ -1094,6 +1100,32 @@ static std::vector<Tensor> fm_bwd_alloc(const Tensor& csc_off, int64_t nnz, int6
           torch::empty({wh::scan_tmp_elems(U)}, i64), det};
 }
 
+// fm_bwd_alloc's layout with the scratch entries (2..9) taken from the
+// stream's grow-only workspace (only gw / gvc are fresh: they are outputs)
+static std::vector<Tensor> fm_bwd_alloc_ws(const Tensor& csc_off, int64_t nnz, int64_t U,
+                                           int64_t vc_rows, int64_t vstride) {
+  auto f32 = csc_off.options().dtype(torch::kFloat32);
+  auto i32 = csc_off.options().dtype(torch::kInt32);
+  auto i64 = csc_off.options().dtype(torch::kInt64);
+  const int64_t cap = wh::fm_bwd_chunks_bound(U, nnz);
+  const int64_t mb = vstride > 0 ? wh::fm_bwd_meta_bound(U, nnz) : 1;
+  const int64_t need[8] = {cap, cap, 2 * 4 * mb, wh::fm_bwd_bucket_scratch(),
+                           std::max<int64_t>(2 * U, 1), 2 * (U + 1), wh::scan_tmp_elems(U),
+                           deterministic() ? wh::fm_bwd_det_floats(U, nnz, (int)vstride) : 0};
+  const c10::TensorOptions opt[8] = {i32, i32, i32, i32, i64, i64, i64, f32};
+  auto& ws = dev_ws(csc_off.device()).bwd_scratch[cur_stream(csc_off)];
+  if (ws.size() != 8) ws.assign(8, Tensor());
+  std::vector<Tensor> pl(10);
+  pl[0] = torch::empty({U}, f32);
+  pl[1] = vstride > 0 ? torch::empty({vc_rows, vstride}, f32) : torch::empty({0}, f32);
+  for (int i = 0; i < 8; ++i) {
+    if (!ws[i].defined() || ws[i].numel() < need[i])
+      ws[i] = torch::empty({std::max<int64_t>(need[i] + need[i] / 4, 1)}, opt[i]);
+    pl[2 + i] = need[i] == 0 ? ws[i].narrow(0, 0, 0) : ws[i];
+  }
+  return pl;
+}
+
 static void fm_bwd_launch(const std::vector<Tensor>& pl, const Tensor& csc_off,
                           const Tensor& csc_row, const float* csc_val, const float* dual,
                           const float* xv, const Tensor& w_or_hdr, const float* vcp,
@@ -1136,7 +1168,7 @@ std::vector<Tensor> fm_backward(const Tensor& csc_off, const Tensor& csc_row,
     vrows = vc->numel() ? vc->size(0) : 0;
     vcp = vc->numel() ? ptr<float>(*vc) : nullptr;
   }
-  auto pl = fm_bwd_alloc(csc_off, csc_row.numel(), csc_off.numel() - 1, vrows, vstride);
+  auto pl = fm_bwd_alloc_ws(csc_off, csc_row.numel(), csc_off.numel() - 1, vrows, vstride);
   fm_bwd_launch(pl, csc_off, csc_row, optptr<float>(csc_val), ptr<float>(dual),
                 vstride > 0 ? optptr<float>(xv) : nullptr, w_or_hdr, vcp, vstride, dual.numel(), 0);
   return {pl[0], pl[1]};
