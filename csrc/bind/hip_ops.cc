@@ -414,12 +414,29 @@ class LocalizeJob {
     const int nsh = (int)nshard_;
     const float* vp = val_.defined() ? ptr<float>(val_) : nullptr;
     auto owner_cnt = torch::empty({nshard_ + 1}, i64);
-    uniq_ = torch::empty({nnz}, i64);
-    ucnt_ = torch::empty({nnz}, i32);
-    csc_off_ = torch::empty({nnz + 1}, i64);
-    csc_row_ = torch::empty({nnz}, i32);
-    csc_val_ = torch::empty({vp ? nnz : 0}, keys_.options().dtype(torch::kFloat32));
-    lid_ = torch::empty({nnz}, i32);
+    {
+      // the job's outputs carved from ONE allocation (six separate tensors
+      // were six trips through the allocator per minibatch; the views keep
+      // the block alive as long as any of them is in use)
+      int64_t at = 0;
+      auto carve = [&](int64_t bytes) {
+        const int64_t o = at;
+        at += (bytes + 255) / 256 * 256;
+        return o;
+      };
+      const int64_t o_u = carve(nnz * 8), o_c = carve(nnz * 4), o_o = carve((nnz + 1) * 8),
+                    o_r = carve(nnz * 4), o_v = carve(vp ? nnz * 4 : 0), o_l = carve(nnz * 4);
+      auto blk = torch::empty({std::max<int64_t>(at, 256)}, keys_.options().dtype(torch::kUInt8));
+      auto view = [&](int64_t o, int64_t n, torch::ScalarType dt, int64_t esz) {
+        return blk.narrow(0, o, n * esz).view(dt);
+      };
+      uniq_ = view(o_u, nnz, torch::kInt64, 8);
+      ucnt_ = view(o_c, nnz, torch::kInt32, 4);
+      csc_off_ = view(o_o, nnz + 1, torch::kInt64, 8);
+      csc_row_ = view(o_r, nnz, torch::kInt32, 4);
+      csc_val_ = view(o_v, vp ? nnz : 0, torch::kFloat32, 4);
+      lid_ = view(o_l, nnz, torch::kInt32, 4);
+    }
     // heavy-id hints: read the set the previous job elected, elect into the
     // other buffer; a job begun while another is in flight uses none
     wh::PartHeavy hv{};
@@ -833,17 +850,28 @@ class KVStore {
     auto s = cur_stream(keys);
     auto i32 = keys.options().dtype(torch::kInt32);
     auto f32 = keys.options().dtype(torch::kFloat32);
-    auto slot = torch::empty({std::max<int64_t>(n, 1)}, i32);
-    auto wout = torch::empty({std::max<int64_t>(n, 1)}, f32);
-    auto vpos = torch::empty({n + 1}, keys.options().dtype(torch::kInt64));
+    // the open's outputs from ONE allocation (see LocalizeJob::enqueue_part)
+    const int64_t n1 = std::max<int64_t>(n, 1);
+    int64_t at = 0;
+    auto carve = [&](int64_t bytes) {
+      const int64_t o = at;
+      at += (bytes + 255) / 256 * 256;
+      return o;
+    };
+    const int64_t o_s = carve(n1 * 4), o_w = carve(n1 * 4), o_p = carve((n + 1) * 8),
+                  o_h = carve(n1);
+    auto blk = torch::empty({at}, keys.options().dtype(torch::kUInt8));
+    auto slot = blk.narrow(0, o_s, n1 * 4).view(torch::kInt32);
+    auto wout = blk.narrow(0, o_w, n1 * 4).view(torch::kFloat32);
+    auto vpos = blk.narrow(0, o_p, (n + 1) * 8).view(torch::kInt64);
     const bool prepped = chain_in.has_value() && chain_in->defined() && chain_in->numel() > 0;
     if (prepped) {
       CHECK_IN((*chain_in), torch::kInt32);
       TORCH_CHECK(chain_in->numel() >= std::max<int64_t>(n, 1), "ps_open: prepped chain too small");
       TORCH_CHECK(vbase_.defined(), "ps_open: prepped without a push prep");
     }
-    auto chain = prepped ? *chain_in : torch::empty({std::max<int64_t>(n, 1)}, i32);
-    auto head = torch::empty({std::max<int64_t>(n, 1)}, keys.options().dtype(torch::kUInt8));
+    auto chain = prepped ? *chain_in : torch::empty({n1}, i32);
+    auto head = blk.narrow(0, o_h, n1);
     // linear (vstride 0): the reply is w_out itself (returned in rbuf's place)
     auto rbuf = torch::empty({vstride_ > 0 ? rows_cap : 0, (int64_t)std::max(vstride_, 1)}, f32);
     // linear: no V rows, a cached all-zero vcnt (read only; no fill launch per open)
