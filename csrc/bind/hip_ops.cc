@@ -1094,11 +1094,22 @@ std::vector<Tensor> fm_forward(const Tensor& offset, const Tensor& lid,
   }
   const float* vp = optptr<float>(val);
   c10::DeviceGuard g(offset.device());
-  auto f32 = offset.options().dtype(torch::kFloat32);
-  auto py = torch::empty({nrows}, f32);
-  auto dual = torch::empty({nrows}, f32);
-  auto xv = torch::empty({vstride > 0 ? nrows * vstride : 0}, f32);
-  auto part = torch::empty({wh::fm_fwd_partials()}, met.options());
+  // py, dual, xv and the metric partials from ONE allocation (the views keep
+  // it alive; four allocations were host time of the small-minibatch step)
+  int64_t at = 0;
+  auto carve = [&](int64_t bytes) {
+    const int64_t o = at;
+    at += (bytes + 255) / 256 * 256;
+    return o;
+  };
+  const int64_t nxv = vstride > 0 ? nrows * vstride : 0;
+  const int64_t o_py = carve(nrows * 4), o_du = carve(nrows * 4), o_xv = carve(nxv * 4),
+                o_pt = carve(wh::fm_fwd_partials() * 8);
+  auto blk = torch::empty({std::max<int64_t>(at, 256)}, offset.options().dtype(torch::kUInt8));
+  auto py = blk.narrow(0, o_py, nrows * 4).view(torch::kFloat32);
+  auto dual = blk.narrow(0, o_du, nrows * 4).view(torch::kFloat32);
+  auto xv = blk.narrow(0, o_xv, nxv * 4).view(torch::kFloat32);
+  auto part = blk.narrow(0, o_pt, wh::fm_fwd_partials() * 8).view(torch::kFloat64);
   // a 5th metric slot asks for the per-minibatch flipped accuracy (linear)
   const int lossf = (int)loss | (met.numel() >= 5 ? 256 : 0);
   wh::fm_forward(nrows, ptr<int64_t>(offset), ptr<int32_t>(lid), vp, ptr<float>(w_or_hdr), vcp,
