@@ -343,6 +343,16 @@ class Comm:
             # group down (a gloo rank whose peer closed its sockets early
             # could abort in a transport thread: seen under CPU overload)
             self.barrier()
+            if self.backend == "gloo":
+                # gloo's barrier work holds the group's earlier works (and
+                # so their tensors); the worker thread drops them just after
+                # the barrier completes, and a tensor freed there takes the
+                # GIL. Were the interpreter already finalising, that thread
+                # would be ended mid-unwind and abort the process: give it
+                # the GIL for a moment first (bin/_launch.py skips the
+                # teardown altogether for the apps)
+                import time
+                time.sleep(0.05)
             dist.destroy_process_group()
 
 
