@@ -10,10 +10,17 @@
 //   6  LDS atomics only, ds_add_u64 (fixed point), hashed bins
 //   7  production with int32 fixed point (ds_add_u32)
 //   8  production with int64 fixed point (ds_add_u64, 2x LDS)
+//   9  production, (g, h) packed into ONE ds_add_u64 per bin: qh * 2^32 + qg
+//      (int32 fixed point each; the sum's low word is exactly sum(qg) while
+//      |sum| < 2^31, the rest is sum(qh)) -- same LDS bytes as 7, half the
+//      atomics
+// 7p / 9p: 7 / 9 with a random permutation as the row index (the deep-level
+// worst case of the partitioned row order)
 // Build: hipcc -O3 --offload-arch=gfx950 -o /tmp/hb tools/microbench/hist_bench.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
@@ -29,7 +36,7 @@ template <int MODE>
 __global__ __launch_bounds__(1024) void k_hist(const uint8_t* B, const int* ridx, const float2* gp,
                                                int chunk, int n, float* out) {
   extern __shared__ float lds[];
-  const int nl2 = 2 * F * NBIN * (MODE >= 6 && MODE != 7 ? 2 : 1);
+  const int nl2 = 2 * F * NBIN * (MODE == 6 || MODE == 8 ? 2 : 1);
   for (int i = threadIdx.x; i < nl2; i += blockDim.x) lds[i] = 0.f;
   __syncthreads();
   const int rbeg = blockIdx.x * chunk, nrow = min(chunk, n - rbeg);
@@ -62,7 +69,11 @@ __global__ __launch_bounds__(1024) void k_hist(const uint8_t* B, const int* ridx
         if (MODE == 1) {
           acc ^= b + __float_as_uint(g[u].x);
         } else if (b != 255) {
-          if (MODE == 6 || MODE == 8) {
+          if (MODE == 9) {
+            unsigned long long* l64 = reinterpret_cast<unsigned long long*>(lds);
+            const long long qg = (int)(g[u].x * 1024), qh = (int)(g[u].y * 1024);
+            atomicAdd(&l64[fj * NBIN + b], (unsigned long long)(qh * 4294967296LL + qg));
+          } else if (MODE == 6 || MODE == 8) {
             unsigned long long* l64 = reinterpret_cast<unsigned long long*>(lds);
             atomicAdd(&l64[2 * (fj * NBIN + b)], (unsigned long long)(long long)(g[u].x * 1073741824.f));
             atomicAdd(&l64[2 * (fj * NBIN + b) + 1], (unsigned long long)(long long)(g[u].y * 1073741824.f));
@@ -88,7 +99,7 @@ __global__ __launch_bounds__(1024) void k_hist(const uint8_t* B, const int* ridx
 template <int MODE>
 float run(int threads, const uint8_t* B, const int* ridx, const float2* gp, int n, float* out) {
   const int nblk = 1024, chunk = (n + nblk - 1) / nblk;
-  const size_t lds = 2 * F * NBIN * 4 * (MODE >= 6 && MODE != 7 ? 2 : 1);
+  const size_t lds = 2 * F * NBIN * 4 * (MODE == 6 || MODE == 8 ? 2 : 1);
   CK(hipFuncSetAttribute((const void*)k_hist<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
@@ -134,5 +145,14 @@ int main() {
   printf("6 atomics only u64   %.3f ms\n", run<6>(1024, B, ridx, gp, n, out));
   printf("7 production u32     %.3f ms\n", run<7>(1024, B, ridx, gp, n, out));
   printf("8 production u64     %.3f ms\n", run<8>(1024, B, ridx, gp, n, out));
+  printf("9 production packed  %.3f ms\n", run<9>(1024, B, ridx, gp, n, out));
+  for (int i = n - 1; i > 0; --i) {  // Fisher-Yates with the LCG
+    s = s * 1664525u + 1013904223u;
+    const int j = (int)(((uint64_t)s * (uint64_t)(i + 1)) >> 32);
+    std::swap(hr[i], hr[j]);
+  }
+  CK(hipMemcpy(ridx, hr.data(), n * 4, hipMemcpyHostToDevice));
+  printf("7p u32, random ridx  %.3f ms\n", run<7>(1024, B, ridx, gp, n, out));
+  printf("9p packed, random    %.3f ms\n", run<9>(1024, B, ridx, gp, n, out));
   return 0;
 }
