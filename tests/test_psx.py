@@ -376,9 +376,10 @@ def _staged_main(rank, world, port, out_dir, model, max_conc):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,model,max_conc", [(2, "difacto", 2), (2, "difacto", 1),
                                                   (2, "linear", 2), (3, "difacto", 2),
-                                                  (3, "linear", 1)])
+                                                  (3, "linear", 1), (4, "difacto", 2),
+                                                  (5, "linear", 2)])
 def test_native_step_multi_process_staged(tmp_path, world, model, max_conc):
-    """The native multi-shard step in 2 and 3 processes (ranks sharing the
+    """The native multi-shard step in 2 to 5 processes (ranks sharing the
     GPU, transfers staged through gloo), uneven data per rank: every rank's
     shard equals the one the Python step trains on the same data, and every
     minibatch is forwarded once (learn/difacto/async_sgd.h:363-425 with W
