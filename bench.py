@@ -86,8 +86,11 @@ def main():
                          "the multi-shard step is pipelined one minibatch deep")
     ap.add_argument("--host-profile", default=None,
                     help="write a cProfile of the timed steps' host (Python) side to PATH.<rank>")
-    ap.add_argument("--launch-timeout", type=int, default=3600,
-                    help="self-launched multi-rank runs are killed after this many seconds")
+    ap.add_argument("--launch-timeout", type=int, default=540,
+                    help="self-launched multi-rank runs are killed after this many seconds "
+                         "(below the driver's 600 s bench limit, so a stuck run still ends "
+                         "with this launcher's message; the native step's own watchdog, "
+                         "WH_RCCL_TIMEOUT_S, ends a stalled exchange sooner)")
     args = ap.parse_args()
     if args.gpus > 1 and args.loopback <= 1 and not launch.launched():
         # no launcher around us: start the N ranks ourselves (before any GPU
@@ -112,7 +115,8 @@ def main():
         from wormhole_amd.parallel.comm import LoopbackComm
         comm = LoopbackComm(args.loopback, device, rccl=args.loopback_rccl)
     else:
-        comm = Comm(device)
+        # (c10d's own collectives time out well inside the driver's limit)
+        comm = Comm(device, timeout_s=int(os.environ.get("WH_RCCL_TIMEOUT_S", "120")) + 60)
         # the group is what --gpus says, on distinct devices
         launch.verify_world(comm, args.gpus if launch.launched() else 1,
                             same_gpu_ok=os.environ.get("WH_BENCH_SAME_GPU") == "1")
@@ -205,6 +209,10 @@ def main():
     comm.allreduce(t, "max")
     dt = float(t.item())
     wire = psx.wire_report(args.steps) if psx is not None else None
+    # sampled GPU time of each exchange class on the native RCCL step, per rank
+    nat = getattr(psx, "_nat", None) if psx is not None else None
+    xt = [round(v, 1) for v in nat.xtime()[:4]] if nat else None
+    xts = comm.allgather_object(xt) if comm.size > 1 and args.loopback <= 1 else [xt]
     prog = learner.take_progress()
     guard = learner.kv.guard
     guard.after_open()
@@ -250,6 +258,10 @@ def main():
             "rank_ms_per_step_min": 1000.0 * min(per_rank) / args.steps,
             "rank_ms_per_step_max": 1000.0 * max(per_rank) / args.steps,
             "wire_bytes_per_gpu_step": wire,
+            "exchange_gpu_us_per_rank": ({"C0": [x[0] for x in xts], "C1": [x[1] for x in xts],
+                                          "C2": [x[2] for x in xts], "C3": [x[3] for x in xts]}
+                                         if xts and xts[0] is not None else None),
+            "watchdog_deadline_s": nat.watchdog_deadline if nat else None,
             "localize_retries": (_native.hip().loc_retries() if device.type == "cuda" else 0),
         }), flush=True)
     comm.finalize()

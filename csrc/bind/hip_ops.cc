@@ -3426,11 +3426,17 @@ PYBIND11_MODULE(_hip, m) {
       .def("guard_sync", &PsxStep::guard_sync)
       .def("wire", &PsxStep::wire)
       .def("wire_reset", &PsxStep::wire_reset)
+      .def("xtime", &PsxStep::xtime,
+           "sampled GPU us per exchange C0..C3 and the sample counts (RCCL transport)")
+      .def_property_readonly("watchdog_deadline", &PsxStep::watchdog_deadline)
       .def_property_readonly("busy", &PsxStep::busy)
       .def_property_readonly("grows", &PsxStep::grows)
       .def_property_readonly("vgrows", &PsxStep::vgrows)
       .def_property("requests", &PsxStep::requests, &PsxStep::set_requests)
       .def_property("step", &PsxStep::step, &PsxStep::set_step);
+  m.def("a2a_plan", &a2a_plan_py, py::arg("rank"), py::arg("world"), py::arg("row_bytes"),
+        py::arg("send_rows"), py::arg("recv_rows"),
+        "one rank's per-peer all-to-all-v plan: (esz, (own_src, own_dst, own_bytes), sends, recvs)");
   m.def("c10d_a2a_rows", &c10d_a2a_rows, py::arg("pg"), py::arg("x"), py::arg("send_rows"),
         py::arg("recv_rows"));
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),

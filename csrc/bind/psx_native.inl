@@ -26,27 +26,197 @@
 //               process correctness rehearsal of the RCCL path;
 //   kTxIdentity P virtual shards in one process, no transfer (--loopback).
 
+#include <condition_variable>
+#include <thread>
+#include <unistd.h>
+
 namespace {
 
 enum PsxTx { kTxIdentity = 0, kTxRccl = 1, kTxStaged = 2 };
 
+struct PsxEv {  // a HIP event shared by an exchange and the watchdog's log
+  hipEvent_t e = nullptr;
+  explicit PsxEv(bool timing = false) {
+    WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&e, timing ? hipEventDefault : hipEventDisableTiming));
+  }
+  PsxEv(const PsxEv&) = delete;
+  PsxEv& operator=(const PsxEv&) = delete;
+  ~PsxEv() {
+    if (e) (void)hipEventDestroy(e);
+  }
+};
+using PsxEvP = std::shared_ptr<PsxEv>;
+
 struct PsxWork {  // an issued exchange and the tensor it reads
   Tensor keep;
-  hipEvent_t ev = nullptr;  // end of the transfer on the exchange stream
+  PsxEvP ev;  // end of the transfer on the exchange stream
   bool pending = false;
   PsxWork() = default;
   PsxWork(const PsxWork&) = delete;
   PsxWork& operator=(const PsxWork&) = delete;
-  ~PsxWork() {
-    if (ev) (void)hipEventDestroy(ev);
-  }
   void wait() {  // the current stream waits for the transfer
     if (pending)
-      WH_HIP_CHECK_HOST(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), ev, 0));
+      WH_HIP_CHECK_HOST(hipStreamWaitEvent(c10::hip::getCurrentHIPStream().stream(), ev->e, 0));
     pending = false;
     keep = Tensor();
   }
 };
+
+// ------------------------------------------------------------ watchdog
+// A multi-rank step that stops making progress -- a peer that never posts
+// its half of an exchange, a transport error, mismatched collectives --
+// would otherwise hang until an outer launcher kills the job, with no
+// record of what stalled. The watchdog thread watches the step's host side:
+// while a PsxStep call is running, the host must pass a phase mark (an
+// exchange issued, a host read returned) at least every `deadline` seconds,
+// and no RCCL communicator of the step may report an asynchronous error.
+// On a breach it prints the rank, the step, the phase the host is blocked
+// in and the recent exchanges -- class C0..C3, step, issuing stream, rows
+// per peer, and whether each has completed on the device -- then aborts the
+// communicators and ends the process with exit status 3 (a plain exit, no
+// re-exec). WH_RCCL_TIMEOUT_S sets the deadline (default 120 s).
+//
+// (ps-lite's van dies on a lost peer through its heartbeat timeout; c10d's
+// own watchdog covers the collectives issued through torch.distributed.)
+struct PsxXLog {
+  int cls = -1;
+  int64_t step = -1;
+  const char* stream = "";
+  std::vector<int64_t> send, recv;
+  PsxEvP ev;  // completion on the issuing stream (null: not tracked)
+};
+
+class PsxWatchdog {
+ public:
+  static constexpr int kExit = 3;
+  PsxWatchdog(int rank, double deadline_s, std::vector<std::shared_ptr<RcclComm>> comms)
+      : rank_(rank), deadline_(deadline_s), comms_(std::move(comms)) {
+    beat_ = now();
+    th_ = std::thread([this] { run(); });
+  }
+  PsxWatchdog(const PsxWatchdog&) = delete;
+  PsxWatchdog& operator=(const PsxWatchdog&) = delete;
+  ~PsxWatchdog() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    if (th_.joinable()) th_.join();
+  }
+  double deadline() const { return deadline_; }
+
+  // a PsxStep call begins / ends (the deadline applies in between only: the
+  // host may legitimately spend any time elsewhere, e.g. reading input)
+  void enter(const char* call, int64_t step) {
+    std::lock_guard<std::mutex> l(m_);
+    depth_++;
+    phase_ = call;
+    cls_ = -1;
+    step_ = step;
+    beat_ = now();
+  }
+  void leave() {
+    std::lock_guard<std::mutex> l(m_);
+    depth_ = std::max(0, depth_ - 1);
+    beat_ = now();
+  }
+  // the host passed a mark: `what` (of exchange class cls, -1 none)
+  void phase(const char* what, int cls, int64_t step) {
+    std::lock_guard<std::mutex> l(m_);
+    phase_ = what;
+    cls_ = cls;
+    step_ = step;
+    beat_ = now();
+  }
+  void log(PsxXLog&& x) {
+    std::lock_guard<std::mutex> l(m_);
+    ring_[ri_ % kLog] = std::move(x);
+    ++ri_;
+  }
+
+ private:
+  static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+  }
+  static std::string rows(const std::vector<int64_t>& v) {
+    std::string s = "[";
+    for (size_t i = 0; i < v.size(); ++i) s += (i ? "," : "") + std::to_string(v[i]);
+    return s + "]";
+  }
+  void run() {
+    std::unique_lock<std::mutex> l(m_);
+    while (!stop_) {
+      cv_.wait_for(l, std::chrono::milliseconds(200));
+      if (stop_ || depth_ == 0) continue;
+      std::string why;
+      for (size_t i = 0; i < comms_.size() && why.empty(); ++i) {
+        const std::string e = comms_[i] ? comms_[i]->async_error_str() : std::string();
+        if (!e.empty() && e.find("in progress") == std::string::npos)
+          why = "RCCL communicator " + std::to_string(i) + " reports an asynchronous error: " + e;
+      }
+      const double idle = now() - beat_;
+      if (why.empty() && idle > deadline_) {
+        char b[160];
+        std::snprintf(b, sizeof b, "no progress for %.1f s (deadline %.0f s, WH_RCCL_TIMEOUT_S)",
+                      idle, deadline_);
+        why = b;
+      }
+      if (!why.empty()) fail(why, idle);  // (holds the lock: the owner stays blocked)
+    }
+  }
+  [[noreturn]] void fail(const std::string& why, double idle) {
+    std::fprintf(stderr, "[psx watchdog] rank %d: %s\n", rank_, why.c_str());
+    std::fprintf(stderr,
+                 "[psx watchdog] rank %d: host blocked in '%s'%s%s of step %lld for %.1f s\n",
+                 rank_, phase_, cls_ >= 0 ? " of C" : "",
+                 cls_ >= 0 ? std::to_string(cls_).c_str() : "", (long long)step_, idle);
+    const int64_t n = std::min<int64_t>(ri_, kLog);
+    for (int64_t i = ri_ - n; i < ri_; ++i) {
+      const PsxXLog& x = ring_[i % kLog];
+      const char* st = "issued";
+      if (x.ev) st = hipEventQuery(x.ev->e) == hipSuccess ? "done" : "PENDING";
+      std::fprintf(stderr,
+                   "[psx watchdog] rank %d:   C%d of step %lld on %s: send rows %s recv rows %s "
+                   "-- %s\n",
+                   rank_, x.cls, (long long)x.step, x.stream, rows(x.send).c_str(),
+                   rows(x.recv).c_str(), st);
+    }
+    for (auto& c : comms_)
+      if (c) c->abort();
+    std::fprintf(stderr, "[psx watchdog] rank %d: communicators aborted, exiting with status %d\n",
+                 rank_, kExit);
+    std::fflush(stderr);
+    std::fflush(stdout);
+    ::_exit(kExit);
+  }
+
+  static constexpr int kLog = 16;
+  const int rank_;
+  const double deadline_;
+  std::vector<std::shared_ptr<RcclComm>> comms_;
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+  int depth_ = 0;
+  const char* phase_ = "";
+  int cls_ = -1;
+  int64_t step_ = 0;
+  double beat_ = 0;
+  PsxXLog ring_[kLog];
+  int64_t ri_ = 0;
+  std::thread th_;
+};
+
+// WH_FAULT=xstall:<rank>:<step>: that rank stops before its first exchange
+// of that step and never posts it (the peers' watchdogs must catch it)
+void parse_xstall(int64_t rank, int64_t* step) {
+  *step = -1;
+  const char* f = std::getenv("WH_FAULT");
+  long long r = -1, s = -1;
+  if (f && std::sscanf(f, "xstall:%lld:%lld", &r, &s) == 2 && r == rank) *step = s;
+}
 
 struct PsxSt {  // one minibatch in flight (kv/psx.py _Step)
   bool train = false, use_cnt = false, have_v = false;
@@ -166,9 +336,19 @@ class PsxStep {
       pins_[i] = torch::empty({dflt}, torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
       WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&pin_ev_[i], hipEventDisableTiming));
     }
+    parse_xstall(rank_, &fault_step_);
+    if (tx_ != kTxIdentity) {  // (the identity transport cannot stall on a peer)
+      const char* t = std::getenv("WH_RCCL_TIMEOUT_S");
+      const double dl = t && std::atof(t) > 0 ? std::atof(t) : 120.0;
+      std::vector<std::shared_ptr<RcclComm>> cs;
+      if (tx_ == kTxRccl) cs = {rccl_c0_, rccl_c1_, rccl_};
+      wd_ = std::make_unique<PsxWatchdog>((int)rank_, dl, cs);
+    }
+    xt_on_ = tx_ == kTxRccl;
   }
 
   ~PsxStep() {
+    wd_.reset();
     if (timing_) timing_->print();
     job_.reset();
     (void)hipDeviceSynchronize();
@@ -186,6 +366,7 @@ class PsxStep {
                   const c10::optional<Tensor>& noffset, const c10::optional<Tensor>& nval,
                   int64_t ready) {
     c10::DeviceGuard g(keys.device());
+    WdCall wc(wd_.get(), "train", step_);
     // WH_TIMING=step: host us per phase, printed every 1000 calls: s0 job,
     // s1 count read (the host WAIT), s2 tables + C2/C3 issue, s3 localize
     // finish + next begin + C1, s4 reply (forward), s5 owner push, s6 open,
@@ -262,6 +443,7 @@ class PsxStep {
   // forwarded here.
   int64_t flush() {
     c10::DeviceGuard g(store_->slots_.device());
+    WdCall wc(wd_.get(), "flush", step_);
     set_streams();
     fwd_mb_ = 0;
     if (!pushes_.empty() && pushes_.back()->gvc.defined()) c3(*pushes_.back());
@@ -287,6 +469,7 @@ class PsxStep {
   // drop a begun localize (before the Python step runs an evaluation /
   // read-only pull of its own: every rank does it at the same point)
   void drop_job() {
+    WdCall wc(wd_.get(), "drop_job", step_);
     if (job_) {
       if (job_deferred_) {
         c10::hip::HIPStreamGuard sg(ls_);
@@ -300,7 +483,24 @@ class PsxStep {
 
   bool busy() const { return (bool)pull_ || !pushes_.empty() || (bool)job_; }
   std::vector<int64_t> wire() const { return {wire_[0], wire_[1], wire_[2], wire_[3]}; }
-  void wire_reset() { wire_[0] = wire_[1] = wire_[2] = wire_[3] = 0; }
+  void wire_reset() {
+    wire_[0] = wire_[1] = wire_[2] = wire_[3] = 0;
+    xt_harvest(true);
+    for (int c = 0; c < 4; ++c) xt_us_[c] = 0, xt_n_[c] = 0;
+  }
+  // sampled GPU time per exchange class C0..C3 (RCCL transport; every
+  // kXtEvery-th step, events around the grouped send / recv on its stream;
+  // it includes the wait for the slowest peer): {mean us x4, samples x4}
+  std::vector<double> xtime() {
+    xt_harvest(true);
+    std::vector<double> o(8, 0.0);
+    for (int c = 0; c < 4; ++c) {
+      o[c] = xt_n_[c] ? xt_us_[c] / (double)xt_n_[c] : 0.0;
+      o[4 + c] = (double)xt_n_[c];
+    }
+    return o;
+  }
+  double watchdog_deadline() const { return wd_ ? wd_->deadline() : 0.0; }
   int64_t grows() const { return grows_; }
   int64_t vgrows() const { return vgrows_; }
   int64_t requests() const { return requests_; }
@@ -324,8 +524,15 @@ class PsxStep {
     work->pending = false;
     work->keep = Tensor();
     if (tx_ == kTxIdentity) return x;
+    fault(c);
     Tensor xc = x.contiguous();
-    if (tx_ == kTxStaged) return staged_a2a(xc, send_rows, recv_rows);
+    if (tx_ == kTxStaged) {
+      mark("staged exchange", c);
+      xlog(c, send_rows, recv_rows, "host (staged)", nullptr);
+      Tensor r = staged_a2a(xc, send_rows, recv_rows);
+      mark("staged exchange returned", c);
+      return r;
+    }
     std::vector<int64_t> shape(xc.sizes().begin(), xc.sizes().end());
     shape[0] = vsum(recv_rows);
     // issued from xs behind the producer's event only (the compute stream
@@ -341,38 +548,82 @@ class PsxStep {
     Tensor out = torch::empty(shape, xc.options());
     if (ready)  // allocated on xs, read on S
       c10::hip::HIPCachingAllocator::recordStream(out.storage().data_ptr(), S_stream_);
+    PsxEvP t0 = xt_begin(xs.stream());
     (c == 1 ? rccl_c1_ : rccl_)->a2av(xc.data_ptr(), out.data_ptr(), row, send_rows, recv_rows,
                                       xs.stream());
+    xt_end(c, std::move(t0), xs.stream());
     work->keep = xc;
     if (xs.stream() != S_stream_.stream()) {
-      if (!work->ev) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&work->ev, hipEventDisableTiming));
-      WH_HIP_CHECK_HOST(hipEventRecord(work->ev, xs.stream()));
+      if (!work->ev) work->ev = std::make_shared<PsxEv>();
+      WH_HIP_CHECK_HOST(hipEventRecord(work->ev->e, xs.stream()));
       work->pending = true;
     }
+    mark("exchange issued", c);
+    xlog(c, send_rows, recv_rows, xs.stream() == xs_.stream() && !sx_ ? "xs" : "S",
+         work->pending ? work->ev : nullptr);
     return out;
   }
 
   // kTxStaged: the rows through host memory and the gloo group, in order on
   // the current stream (blocking: the correctness rehearsal of the RCCL
   // path with several ranks on one GPU)
+  // It executes the same a2a_plan() as RcclComm::a2av (per-peer offsets,
+  // the own segment a local copy, zero-byte segments skipped) with one c10d
+  // send / recv per peer.
   Tensor staged_a2a(const Tensor& xc, const std::vector<int64_t>& send_rows,
                     const std::vector<int64_t>& recv_rows) {
-    Tensor h = xc.to(torch::kCPU);  // (waits for the current stream's queue)
-    Tensor r = c10d_rows(pg_, h, send_rows, recv_rows);
-    return r.to(xc.device());
+    Tensor h = xc.to(torch::kCPU).contiguous();  // (waits for the current stream's queue)
+    int64_t row = h.element_size();
+    for (int64_t d = 1; d < h.dim(); ++d) row *= h.size(d);
+    std::vector<int64_t> shape(h.sizes().begin(), h.sizes().end());
+    if (shape.empty()) shape.push_back(0);
+    shape[0] = vsum(recv_rows);
+    Tensor out = torch::empty(shape, h.options());
+    const A2aPlan pl = a2a_plan((int)rank_, (int)P_, row, send_rows, recv_rows);
+    Tensor hb = h.reshape({-1}).view(torch::kUInt8), ob = out.view({-1}).view(torch::kUInt8);
+    std::vector<c10::intrusive_ptr<c10d::Work>> ws;
+    for (const auto& g : pl.recvs) {
+      std::vector<Tensor> t{ob.narrow(0, g.off, g.bytes)};
+      ws.push_back(pg_->recv(t, g.peer, kStagedTag));
+    }
+    for (const auto& g : pl.sends) {
+      std::vector<Tensor> t{hb.narrow(0, g.off, g.bytes)};
+      ws.push_back(pg_->send(t, g.peer, kStagedTag));
+    }
+    if (pl.own_bytes > 0)
+      ob.narrow(0, pl.own_dst, pl.own_bytes).copy_(hb.narrow(0, pl.own_src, pl.own_bytes));
+    for (auto& w : ws)
+      if (w) w->wait();
+    return out.to(xc.device());
   }
 
   // int64 [4P] per peer -> the peers' [4P], on the current stream
   Tensor exchange_counts(const Tensor& send) {
     if (tx_ == kTxIdentity) return send.clone();
+    fault(0);
     std::vector<int64_t> four(P_, 4);
     Tensor s = send.contiguous();
-    if (tx_ == kTxStaged) return staged_a2a(s, four, four);
+    if (tx_ == kTxStaged) {
+      mark("staged exchange", 0);
+      xlog(0, four, four, "host (staged)", nullptr);
+      Tensor r = staged_a2a(s, four, four);
+      mark("staged exchange returned", 0);
+      return r;
+    }
     // one 32-byte send / recv per peer on the current stream (cs): this tiny
     // exchange sits on the path of the step's one host read
     Tensor r = torch::empty_like(s);
-    rccl_c0_->a2av(s.data_ptr(), r.data_ptr(), sizeof(int64_t), four, four,
-                c10::hip::getCurrentHIPStream(dev_).stream());
+    const hipStream_t cur = c10::hip::getCurrentHIPStream(dev_).stream();
+    PsxEvP t0 = xt_begin(cur);
+    rccl_c0_->a2av(s.data_ptr(), r.data_ptr(), sizeof(int64_t), four, four, cur);
+    xt_end(0, std::move(t0), cur);
+    PsxEvP ev;
+    if (wd_) {
+      ev = std::make_shared<PsxEv>();
+      WH_HIP_CHECK_HOST(hipEventRecord(ev->e, cur));
+    }
+    mark("exchange issued", 0);
+    xlog(0, four, four, cur == cs_h_ ? "cs" : "S", std::move(ev));
     return r;
   }
 
@@ -391,7 +642,10 @@ class PsxStep {
   Tensor put(const std::vector<int64_t>& a) {
     const int k = pin_i_;
     pin_i_ = (pin_i_ + 1) % kPins;
-    if (pin_used_[k]) WH_HIP_CHECK_HOST(hipEventSynchronize(pin_ev_[k]));
+    if (pin_used_[k]) {
+      mark("pinned table ring (host wait)", -1);
+      WH_HIP_CHECK_HOST(hipEventSynchronize(pin_ev_[k]));
+    }
     if ((int64_t)a.size() > pins_[k].numel())
       pins_[k] = torch::empty({2 * (int64_t)a.size()},
                               torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
@@ -404,6 +658,74 @@ class PsxStep {
     WH_HIP_CHECK_HOST(hipEventRecord(pin_ev_[k], S_stream_.stream()));
     pin_used_[k] = true;
     return d;
+  }
+
+  // ------------------------------------------------------------ watchdog
+  struct WdCall {  // a call the deadline applies to
+    PsxWatchdog* w;
+    WdCall(PsxWatchdog* w_, const char* c, int64_t s) : w(w_) {
+      if (w) w->enter(c, s);
+    }
+    ~WdCall() {
+      if (w) w->leave();
+    }
+  };
+  void mark(const char* what, int c) {
+    if (wd_) wd_->phase(what, c, step_);
+  }
+  void xlog(int c, const std::vector<int64_t>& s, const std::vector<int64_t>& r, const char* stream,
+            PsxEvP ev) {
+    if (!wd_) return;
+    PsxXLog x;
+    x.cls = c;
+    x.step = step_;
+    x.stream = stream;
+    x.send = s;
+    x.recv = r;
+    x.ev = std::move(ev);
+    wd_->log(std::move(x));
+  }
+  void fault(int c) {
+    if (fault_step_ < 0 || step_ != fault_step_) return;
+    fault_step_ = -1;
+    std::fprintf(stderr, "[psx] WH_FAULT: rank %lld stalls before C%d of step %lld\n",
+                 (long long)rank_, c, (long long)step_);
+    std::fflush(stderr);
+    mark("WH_FAULT stall", c);
+    std::this_thread::sleep_for(std::chrono::hours(1));
+  }
+
+  // sampled exchange timing (RCCL transport)
+  PsxEvP xt_begin(hipStream_t s) {
+    if (!xt_on_ || step_ % kXtEvery != 0) return nullptr;
+    auto e = std::make_shared<PsxEv>(true);
+    WH_HIP_CHECK_HOST(hipEventRecord(e->e, s));
+    return e;
+  }
+  void xt_end(int c, PsxEvP a, hipStream_t s) {
+    if (!a) return;
+    auto b = std::make_shared<PsxEv>(true);
+    WH_HIP_CHECK_HOST(hipEventRecord(b->e, s));
+    xt_pend_.push_back({c, std::move(a), std::move(b)});
+    if (xt_pend_.size() > 64) xt_harvest(false);
+  }
+  void xt_harvest(bool sync) {
+    std::vector<XtPend> keep;
+    for (auto& p : xt_pend_) {
+      if (sync) {
+        mark("exchange timing read (host wait)", p.cls);
+        WH_HIP_CHECK_HOST(hipEventSynchronize(p.b->e));
+      } else if (hipEventQuery(p.b->e) != hipSuccess) {
+        keep.push_back(std::move(p));
+        continue;
+      }
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, p.a->e, p.b->e) == hipSuccess) {
+        xt_us_[p.cls] += 1000.0 * ms;
+        xt_n_[p.cls] += 1;
+      }
+    }
+    xt_pend_.swap(keep);
   }
 
   // ------------------------------------------------------------ localize
@@ -470,7 +792,9 @@ class PsxStep {
   // rank has data
   bool counts(std::vector<int64_t>& send, std::vector<int64_t>& recv) {
     exchange_deferred();
+    mark("C0 count read (host wait)", 0);
     auto c = job_->counts();
+    mark("C0 counts read", 0);
     const int64_t* oc = c[0].data_ptr<int64_t>();
     const Tensor& tail = c[1];
     const int64_t* t = tail.data_ptr<int64_t>();
@@ -517,7 +841,9 @@ class PsxStep {
     c10::hip::HIPStreamGuard sg(cs_);
     auto c0 = ps_c0(zero, st.vcnt, P_, 1, tx_ == kTxIdentity);
     if (tx_ != kTxIdentity) c0[1].narrow(0, S_ + 1, 4 * P_).copy_(exchange_counts(c0[0]));
+    mark("C0 V-count read (host wait)", 0);
     Tensor v = c0[1].cpu();
+    mark("C0 V-counts read", 0);
     const int64_t* h = v.data_ptr<int64_t>();
     st.vrecv.assign(P_, 0);
     st.vown.assign(P_, 0);
@@ -734,6 +1060,7 @@ class PsxStep {
   // (summary slots 2 / 3 of the store: 0 / 1 belong to the Python guard)
   void guard_read() {
     if (!gpend_) return;
+    mark("store summary read (host wait)", -1);
     WH_HIP_CHECK_HOST(hipEventSynchronize(gev_[gk_]));
     gpend_ = false;
     auto h = store_->summary_read(2 + gk_);
@@ -788,6 +1115,11 @@ class PsxStep {
 
   static constexpr int kMaxTau = 8;
   static constexpr int kRing = 32, kPins = 8, kStepEv = kMaxTau + 4;
+  static constexpr int kStagedTag = 7, kXtEvery = 16;
+  struct XtPend {
+    int cls;
+    PsxEvP a, b;
+  };
   KVStore* store_;
   int64_t P_, S_, rank_;
   bool linear_;
@@ -826,6 +1158,12 @@ class PsxStep {
   std::unique_ptr<HostSplit> timing_{host_split("psx native step")};
   bool one_ = false, sx_ = false;
   HostTimer* ht_ = nullptr;  // (WH_TIMING=step: the running call's marks, for grad's split)
+  std::unique_ptr<PsxWatchdog> wd_;  // (transports with peers)
+  int64_t fault_step_ = -1;          // WH_FAULT=xstall
+  bool xt_on_ = false;
+  std::vector<XtPend> xt_pend_;
+  double xt_us_[4] = {0, 0, 0, 0};
+  int64_t xt_n_[4] = {0, 0, 0, 0};
   // guard: opens per store summary (the linear step: a launch, an event and
   // a host read less on 3 of 4 steps)
   const int gevery_ = linear_ ? 4 : 1;

@@ -721,12 +721,12 @@ class Psx:
             self._nat = False
             rccl = None
             if ok and tx == hip.PSX_TX_RCCL:
-                try:
-                    rccl = (self.comm.rccl("c0"), self.comm.rccl("c1"), self.comm.rccl("c23"))
-                except RuntimeError as e:  # (every rank fails alike: the Python step serves)
-                    print("[psx] own RCCL communicators unavailable (%s): the Python step "
-                          "exchanges over the c10d group" % str(e).splitlines()[0], flush=True)
-                    ok = False
+                ok = self._own_rccl()
+                if ok:
+                    rccl = ok
+            if not ok and self.cuda and self.tau_max > 1:
+                print("[psx] max_concurrency %d: the Python step keeps at most 2 minibatches in "
+                      "flight (staleness 1)" % (self.tau_max + 1), flush=True)
             if ok:
                 self._nat = hip.PsxStep(
                     store=self.store, P=self.P, S=self.nshard,
@@ -741,6 +741,35 @@ class Psx:
                     cu_reserve=_CU_RESERVE if tx == hip.PSX_TX_RCCL else 0)
                 self._nat.requests = self.requests
         return self._nat or None
+
+    def _own_rccl(self):
+        """The native step's own communicators: (c0, c1, c23) -- C0 and C1 on
+        the path to the next open get their own, RCCL running one
+        communicator's operations in issue order -- or one shared by all
+        four exchanges with ``WH_PSX_RCCL_COMMS=1``. Creating them is
+        collective; the ranks then agree on the outcome (a failure on one
+        rank alone would leave it on the Python step's c10d collectives and
+        its peers on the native ones, a deadlock), and the communicators
+        made are closed again if any rank failed. Returns the communicators,
+        or False (every rank then takes the Python step)."""
+        one = os.environ.get("WH_PSX_RCCL_COMMS", "3") == "1"
+        made, err = [], None
+        try:
+            for tag in (("c23",) if one else ("c0", "c1", "c23")):
+                made.append(self.comm.rccl(tag))
+        except RuntimeError as e:
+            err = str(e).splitlines()[0]
+        good = err is None
+        if getattr(self.comm, "size", 1) > 1 and getattr(self.comm, "pg", None) is not None:
+            flag = torch.tensor([1 if good else 0], dtype=torch.int64, device=self.dev)
+            self.comm.allreduce(flag, "min")
+            good = bool(int(flag.item()))
+        if not good:
+            self.comm._close_rccl()
+            print("[psx] own RCCL communicators unavailable (%s): the Python step exchanges "
+                  "over the c10d group" % (err or "failed on another rank"), flush=True)
+            return False
+        return made[0] if one else tuple(made)
 
     def _kmod(self, keys):
         """max_key (ps-lite's flag, learn/base/localizer.h:108-115): the

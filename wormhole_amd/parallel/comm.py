@@ -48,6 +48,21 @@ def env_local_rank():
     return 0
 
 
+def same_gpu_rccl(rank):
+    """Let several RCCL ranks share one GPU (a rehearsal of the multi-GPU
+    data plane on a one-GPU box). RCCL refuses two ranks of one host on the
+    same device; with a host id of its own per rank (``NCCL_HOSTID``, which
+    RCCL hashes in place of the host name) every rank looks like a node of
+    its own, and the ranks talk through RCCL's network transport over the
+    loopback interface (sockets, host-staged) instead of xGMI peer access.
+    The transfers are slow, but every RCCL call of the multi-rank path --
+    grouped per-peer ncclSend / ncclRecv on the step's three communicators,
+    c10d's collectives -- runs for real. Must run before the first RCCL
+    call of the process."""
+    os.environ["NCCL_HOSTID"] = "wh-same-gpu-rank-%d" % int(rank)
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+
+
 class _Done:
     def wait(self):
         pass
@@ -104,6 +119,8 @@ class Comm:
         # transfers over RCCL/xGMI stay raw (docs/linear.md msg_compression).
         self.compress = False
         if self.size > 1 and init:
+            if backend == "nccl" and os.environ.get("WH_BENCH_SAME_GPU") == "1":
+                same_gpu_rccl(self.rank)
             if not dist.is_initialized():
                 os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
                 os.environ.setdefault("MASTER_PORT", "29500")

@@ -45,7 +45,7 @@ def self_launch(script, argv, nproc, device="cuda", timeout_s=3600):
     return its exit code (never hangs past ``timeout_s``: the whole process
     group is killed and 124 returned). Rank 0's stdout (the JSON line)
     passes straight through."""
-    if device == "cuda":
+    if device == "cuda" and os.environ.get("WH_BENCH_SAME_GPU") != "1":
         n = visible_gpus()
         if n < nproc:
             sys.stderr.write(
