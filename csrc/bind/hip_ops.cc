@@ -3411,11 +3411,14 @@ PYBIND11_MODULE(_hip, m) {
   py::class_<PsxStep>(m, "PsxStep")
       .def(py::init<KVStore*, int64_t, int64_t, int64_t, int64_t, py::object, py::object, bool,
                     std::vector<double>, std::vector<double>, int64_t, bool, int64_t, int64_t,
-                    Tensor, Tensor, int64_t, double, int64_t>(),
+                    Tensor, Tensor, int64_t, double, int64_t, std::vector<int64_t>,
+                    std::vector<double>>(),
            py::arg("store"), py::arg("P"), py::arg("S"), py::arg("rank"), py::arg("tx"),
            py::arg("pg"), py::arg("rccl"), py::arg("linear"), py::arg("lin_hp"), py::arg("hp"), py::arg("threshold"),
            py::arg("l1_shrk"), py::arg("seed"), py::arg("loss"), py::arg("met"),
            py::arg("auc_sum"), py::arg("tau"), py::arg("max_load"), py::arg("cu_reserve"),
+           py::arg("filt") = std::vector<int64_t>{0, 0},
+           py::arg("post") = std::vector<double>{0.0, 0.0, 0.0, 0.0},
            py::keep_alive<1, 2>())
       .def("train", &PsxStep::train, py::arg("keys"), py::arg("offset"), py::arg("val"),
            py::arg("label"), py::arg("data_pass"), py::arg("next_keys") = py::none(),

@@ -183,10 +183,19 @@ class PsxWatchdog {
                    rank_, x.cls, (long long)x.step, x.stream, rows(x.send).c_str(),
                    rows(x.recv).c_str(), st);
     }
-    for (auto& c : comms_)
-      if (c) c->abort();
-    std::fprintf(stderr, "[psx watchdog] rank %d: communicators aborted, exiting with status %d\n",
-                 rank_, kExit);
+    // (ncclCommAbort can itself wait on a stuck proxy or kernel: it gets a
+    // thread of its own and a few seconds; the exit does not wait longer)
+    auto fin = std::make_shared<std::atomic<bool>>(false);
+    auto comms = comms_;
+    std::thread([comms, fin] {
+      for (auto& c : comms)
+        if (c) c->abort();
+      fin->store(true);
+    }).detach();
+    for (int i = 0; i < 100 && !fin->load(); ++i)
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    std::fprintf(stderr, "[psx watchdog] rank %d: communicators %s, exiting with status %d\n",
+                 rank_, fin->load() ? "aborted" : "abort still pending after 5 s", kExit);
     std::fflush(stderr);
     std::fflush(stdout);
     ::_exit(kExit);
@@ -225,7 +234,11 @@ struct PsxSt {  // one minibatch in flight (kv/psx.py _Step)
   Tensor label, uniq, ucnt, lid, offset, val, csc_off, csc_row, csc_val;
   Tensor tabs, segS_w, segHS_w, segS_o, segHS_o, vrecv_d;
   Tensor keys_o, slot, vpos, chain, head, rbuf, vcnt;
-  Tensor rrecv, hdr, py, dual, xv, gpush, gvc;
+  Tensor rrecv, hdr, rows, py, dual, xv, gpush, gvc;
+  // fixed_bytes filter: the receiving side's region table (device) and float
+  // extent of C2 / C3's wire rows (q2_desc / q3_desc undefined: exact floats)
+  Tensor q2_desc, q3_desc;
+  int64_t q2_ext = 0, q3_ext = 0;
   // C2 / C3 wait for these only: the open's and the backward's ends on S
   // (the step's own pair from PsxStep::sev_, recorded once each)
   hipEvent_t ev_open = nullptr, ev_grad = nullptr;
@@ -269,12 +282,26 @@ class PsxStep {
   PsxStep(KVStore* store, int64_t P, int64_t S, int64_t rank, int64_t tx, py::object pg,
           py::object rccl, bool linear, std::vector<double> lin_hp, std::vector<double> hp,
           int64_t threshold, bool l1_shrk, int64_t seed, int64_t loss, Tensor met, Tensor auc_sum,
-          int64_t tau, double max_load, int64_t cu_reserve)
+          int64_t tau, double max_load, int64_t cu_reserve, std::vector<int64_t> filt,
+          std::vector<double> post)
       : store_(store), P_(P), S_(S), rank_(rank), linear_(linear), lin_hp_(std::move(lin_hp)),
         hp_(std::move(hp)), threshold_(threshold), l1_shrk_(l1_shrk), seed_(seed), loss_(loss),
         met_(std::move(met)), auc_sum_(std::move(auc_sum)), tau_(tau), max_load_(max_load) {
     TORCH_CHECK(P >= 2 && S >= 1 && S <= P && rank >= 0 && rank < P, "PsxStep: bad P / S / rank");
     TORCH_CHECK(lin_hp_.size() == 5 && hp_.size() == 8, "PsxStep: hyper-parameter sizes");
+    // filt = (fixed_bytes, filter seed): ps-lite's FIXING_FLOAT filter on the
+    // exchanged floats (kv/psx.py _QFilter); post = (grad_clipping, dropout,
+    // grad_normalization, dim): the embedding-gradient post-processing
+    TORCH_CHECK(filt.size() == 2 && post.size() == 4, "PsxStep: filt = (nb, seed), post = "
+                "(clip, dropout, normalize, dim)");
+    qnb_ = (int)filt[0];
+    qseed_ = filt[1];
+    TORCH_CHECK(qnb_ >= 0 && qnb_ <= 3, "PsxStep: fixed_bytes must be 0..3");
+    clip_ = post[0];
+    dropout_ = post[1];
+    gnorm_ = post[2] != 0.0;
+    pdim_ = (int64_t)post[3];
+    post_on_ = !linear && (clip_ > 0 || dropout_ > 0 || gnorm_);
     TORCH_CHECK(tau >= 0 && tau <= kMaxTau, "PsxStep: tau (max_concurrency - 1) must be 0..",
                 kMaxTau);
     vs_ = store->vstride();
@@ -345,6 +372,11 @@ class PsxStep {
       wd_ = std::make_unique<PsxWatchdog>((int)rank_, dl, cs);
     }
     xt_on_ = tx_ == kTxRccl;
+    if (timing_on("comm")) xt_every_ = 1;  // WH_TIMING=comm: every exchange timed
+    if (qnb_) {
+      qW_ = linear_ ? 64 : std::max(vs_, 1);
+      qR_ = (4 + qW_ * qnb_ + 3) / 4 * 4;  // ops/ref.py quant_record_bytes
+    }
   }
 
   ~PsxStep() {
@@ -489,7 +521,7 @@ class PsxStep {
     for (int c = 0; c < 4; ++c) xt_us_[c] = 0, xt_n_[c] = 0;
   }
   // sampled GPU time per exchange class C0..C3 (RCCL transport; every
-  // kXtEvery-th step, events around the grouped send / recv on its stream;
+  // 16th step, every step with WH_TIMING=comm; events around the grouped send / recv on its stream;
   // it includes the wait for the slowest peer): {mean us x4, samples x4}
   std::vector<double> xtime() {
     xt_harvest(true);
@@ -697,7 +729,7 @@ class PsxStep {
 
   // sampled exchange timing (RCCL transport)
   PsxEvP xt_begin(hipStream_t s) {
-    if (!xt_on_ || step_ % kXtEvery != 0) return nullptr;
+    if (!xt_on_ || step_ % xt_every_ != 0) return nullptr;
     auto e = std::make_shared<PsxEv>(true);
     WH_HIP_CHECK_HOST(hipEventRecord(e->e, s));
     return e;
@@ -934,9 +966,9 @@ class PsxStep {
 
   // ------------------------------------------------------------ phases
   void c1(PsxSt& st) {
-    Tensor rec = linear_ ? st.uniq
-                         : ps_records(st.uniq, st.use_cnt ? c10::optional<Tensor>(st.ucnt)
-                                                          : c10::nullopt);
+    c10::optional<Tensor> cnt;
+    if (st.use_cnt) cnt = qnb_ ? st.ucnt.clamp_max(255) : st.ucnt;  // TRUNCATE_FLOAT(1)
+    Tensor rec = linear_ ? st.uniq : ps_records(st.uniq, cnt);
     // on the exchange stream behind the records (RCCL copies the keys there
     // while the compute stream goes on with the previous minibatch's forward;
     // on the compute stream itself the forward queued behind the transfer)
@@ -973,13 +1005,84 @@ class PsxStep {
       recv_rows[p] = linear_ ? st.send[p] : st.Hw[p] + st.vrecv[p];
     }
     Tensor x = st.rbuf.narrow(0, 0, vsum(send_rows));
-    st.rrecv = a2a(2, x, send_rows, recv_rows, st.ev_open, &st.w_c2);
+    hipEvent_t ready = st.ev_open;
+    if (qnb_ && !linear_) {  // (linear pulls travel exact)
+      x = qpack(x, st.recv, st.send, st.vown, st.vrecv, st.Ho, st.Hw, send_rows, recv_rows,
+                &st.q2_desc, &st.q2_ext);
+      ready = sx_ ? nullptr : record(S_stream_);
+    }
+    st.rrecv = a2a(2, x, send_rows, recv_rows, ready, &st.w_c2);
     st.ev_open = nullptr;
     st.rbuf = Tensor();
   }
 
+  // fixed_bytes: the float regions x (this side: n keys, v embedding rows, H
+  // header rows per peer) -> uint8 wire rows, on S (kv/psx.py Psx._qpack);
+  // rows out / in per peer replace send_rows / recv_rows, and the receiving
+  // side's table and float extent are kept for qunpack
+  struct QLayout {
+    std::vector<int64_t> desc, rows;
+    int64_t ext = 0;
+  };
+  QLayout qlayout(const std::vector<int64_t>& n, const std::vector<int64_t>& v,
+                  const std::vector<int64_t>& H) const {
+    QLayout L;
+    L.desc.assign(6 * P_, 0);
+    int64_t sf = 0, sq = 0;
+    for (int64_t p = 0; p < P_; ++p) {
+      int64_t a, vf, nf, ha, nr, ext;
+      if (linear_) {
+        a = 0, vf = 0, nf = n[p], ha = 0;
+        nr = cdiv64(n[p], qW_);
+        ext = n[p];
+      } else {
+        a = 2 * n[p], vf = H[p] * vs_, nf = v[p] * vs_;
+        ha = cdiv64(4 * a, qR_);
+        nr = v[p];
+        ext = (H[p] + v[p]) * vs_;
+      }
+      const int64_t d[6] = {sf, a, vf, nf, sq, ha};
+      for (int k = 0; k < 6; ++k) L.desc[6 * p + k] = d[k];
+      L.rows.push_back(ha + nr);
+      sf += ext;
+      sq += ha + nr;
+    }
+    L.ext = sf;
+    return L;
+  }
+  Tensor qpack(const Tensor& x, const std::vector<int64_t>& ns, const std::vector<int64_t>& nr,
+               const std::vector<int64_t>& vs, const std::vector<int64_t>& vr,
+               const std::vector<int64_t>& Hs, const std::vector<int64_t>& Hr,
+               std::vector<int64_t>& send_rows, std::vector<int64_t>& recv_rows, Tensor* rdesc,
+               int64_t* rext) {
+    const QLayout ls = qlayout(ns, vs, Hs), lr = qlayout(nr, vr, Hr);
+    TORCH_CHECK(ls.ext == x.numel(), "psx filter: region layout ", ls.ext, " floats vs buffer ",
+                x.numel());
+    std::vector<int64_t> both(ls.desc);
+    both.insert(both.end(), lr.desc.begin(), lr.desc.end());
+    Tensor t = put(both);
+    ++qcalls_;
+    c10::hip::HIPStreamGuard sg(S_stream_);
+    Tensor q = ps_qpack(x.contiguous().view({-1}), t.narrow(0, 0, 6 * P_).view({P_, 6}),
+                        vsum(ls.rows), qW_, qnb_, qseed_ + (qcalls_ << 20));
+    send_rows = ls.rows;
+    recv_rows = lr.rows;
+    *rdesc = t.narrow(0, 6 * P_, 6 * P_).view({P_, 6});
+    *rext = lr.ext;
+    return q;
+  }
+  Tensor qunpack(const Tensor& q, Tensor& desc, int64_t ext) {
+    const int64_t vs = linear_ ? 1 : vs_;
+    Tensor out = linear_ ? torch::empty({ext}, q.options().dtype(torch::kFloat32))
+                         : torch::empty({ext / vs, vs}, q.options().dtype(torch::kFloat32));
+    ps_qunpack(q, desc, qW_, qnb_, out);
+    desc = Tensor();
+    return out;
+  }
+
   void reply(PsxSt& st) {
     st.w_c2.wait();
+    if (st.q2_desc.defined()) st.rrecv = qunpack(st.rrecv, st.q2_desc, st.q2_ext);
     const c10::optional<Tensor> val =
         st.val.defined() ? c10::optional<Tensor>(st.val) : c10::nullopt;
     std::vector<Tensor> fw;
@@ -989,6 +1092,7 @@ class PsxStep {
     } else {
       auto u = ps_unpack(st.rrecv, st.U, st.segS_w, st.segHS_w, st.vrecv_d);
       st.hdr = u[0];
+      st.rows = u[1];
       fw = fm_forward(st.offset, st.lid, val, st.hdr, st.rrecv, vs_, st.label, loss_, met_);
     }
     st.py = fw[0];
@@ -1011,6 +1115,7 @@ class PsxStep {
     } else {
       auto b = fm_backward(st.csc_off, st.csc_row, cv, st.dual, st.xv, st.hdr, st.rrecv, vs_);
       if (ht_) ht_->mark(8);
+      if (post_on_) grad_post(st, b[1]);
       ps_pack_gw(b[0], b[1], st.segS_w, st.segHS_w, st.vrecv_d);
       st.gvc = b[1];
     }
@@ -1019,8 +1124,22 @@ class PsxStep {
     if (issue) c3(st);
     auc(st);
     if (ht_) ht_->mark(9);
-    st.rrecv = st.hdr = st.dual = st.xv = st.lid = Tensor();
+    st.rrecv = st.hdr = st.rows = st.dual = st.xv = st.lid = Tensor();
     st.csc_off = st.csc_row = st.csc_val = Tensor();
+  }
+
+  // clipping / dropout / normalization of the embedding gradient rows
+  // (kv/psx.py Psx._grad; learn/difacto/loss.h:145-155); the normalization
+  // runs over the V rows only (the header rows zeroed first)
+  void grad_post(PsxSt& st, const Tensor& gvc) {
+    if (gnorm_) {
+      int64_t base = 0;
+      for (int64_t q = 0; q < P_; ++q) {
+        if (st.Hw[q] > 0) gvc.narrow(0, base, st.Hw[q]).zero_();
+        base += st.Hw[q] + st.vrecv[q];
+      }
+    }
+    fm_grad_post(gvc, st.rows, pdim_, clip_, dropout_, seed_ + 7919 * st.seed_step + 1, gnorm_);
   }
 
   void c3(PsxSt& st) {
@@ -1029,7 +1148,14 @@ class PsxStep {
       send_rows[p] = linear_ ? st.send[p] : st.Hw[p] + st.vrecv[p];
       recv_rows[p] = linear_ ? st.recv[p] : st.Ho[p] + st.vown[p];
     }
-    st.gpush = a2a(3, st.gvc, send_rows, recv_rows, st.ev_grad, &st.w_c3);
+    Tensor x = st.gvc;
+    hipEvent_t ready = st.ev_grad;
+    if (qnb_) {
+      x = qpack(x, st.send, st.recv, st.vrecv, st.vown, st.Hw, st.Ho, send_rows, recv_rows,
+                &st.q3_desc, &st.q3_ext);
+      ready = sx_ ? nullptr : record(S_stream_);
+    }
+    st.gpush = a2a(3, x, send_rows, recv_rows, ready, &st.w_c3);
     st.ev_grad = nullptr;
     st.gvc = Tensor();
   }
@@ -1039,6 +1165,7 @@ class PsxStep {
   // on the compute stream's chain); prep_n its used length
   void owner_push(PsxSt& st, const Tensor& prep = Tensor(), int64_t prep_n = 0) {
     st.w_c3.wait();
+    if (st.q3_desc.defined()) st.gpush = qunpack(st.gpush, st.q3_desc, st.q3_ext);
     const c10::optional<Tensor> pc = prep.defined() ? c10::optional<Tensor>(prep) : c10::nullopt;
     if (linear_) {
       store_->ps_push_linear(st.slot, st.chain, st.head, st.segS_o, st.gpush, (int64_t)lin_hp_[0],
@@ -1115,7 +1242,7 @@ class PsxStep {
 
   static constexpr int kMaxTau = 8;
   static constexpr int kRing = 32, kPins = 8, kStepEv = kMaxTau + 4;
-  static constexpr int kStagedTag = 7, kXtEvery = 16;
+  static constexpr int kStagedTag = 7;
   struct XtPend {
     int cls;
     PsxEvP a, b;
@@ -1161,7 +1288,16 @@ class PsxStep {
   std::unique_ptr<PsxWatchdog> wd_;  // (transports with peers)
   int64_t fault_step_ = -1;          // WH_FAULT=xstall
   bool xt_on_ = false;
+  int64_t xt_every_ = 16;
   std::vector<XtPend> xt_pend_;
+  // fixed_bytes filter (qnb_ > 0): bytes per float, seed, floats and bytes
+  // per wire record; the seed sequence follows kv/psx.py _QFilter.next_seed
+  int qnb_ = 0, qW_ = 0, qR_ = 0;
+  int64_t qseed_ = 0, qcalls_ = 0;
+  // embedding-gradient post-processing (learn/difacto/loss.h:131-155)
+  double clip_ = 0, dropout_ = 0;
+  bool gnorm_ = false, post_on_ = false;
+  int64_t pdim_ = 0;
   double xt_us_[4] = {0, 0, 0, 0};
   int64_t xt_n_[4] = {0, 0, 0, 0};
   // guard: opens per store summary (the linear step: a launch, an event and

@@ -19,11 +19,20 @@ import torch.multiprocessing as mp
 CARD = [50, 400, 3000, 20, 7, 900]
 
 
-def _conf(max_conc=2, l1_shrk=False, dim=8, thr=3):
+def _conf(max_conc=2, l1_shrk=False, dim=8, thr=3, opts=""):
+    """opts: "fb<n>" the fixed_bytes filter, "clip" / "drop" / "norm" the
+    embedding-gradient post-processing (learn/difacto/loss.h:145-155)."""
     from wormhole_amd.config.schema import DifactoConfig, Embedding
     emb = Embedding(dim=dim, threshold=thr)
+    if "clip" in opts:
+        emb.grad_clipping = 0.05
+    if "drop" in opts:
+        emb.dropout = 0.1
+    if "norm" in opts:
+        emb.grad_normalization = True
+    fb = int(opts[opts.index("fb") + 2]) if "fb" in opts else 0
     return DifactoConfig(embedding=[emb], lambda_l1=0.01, l1_shrk=l1_shrk,
-                         max_concurrency=max_conc)
+                         max_concurrency=max_conc, fixed_bytes=fb)
 
 
 def _run(comm, conf, device, steps=6, rows=300, seed=17, nxt=True, nshard=None):
@@ -303,7 +312,7 @@ def _lockstep(lr, batches, cap=64):
     return lr.take_progress()
 
 
-def _staged_main(rank, world, port, out_dir, model, max_conc):
+def _staged_main(rank, world, port, out_dir, model, max_conc, opts=""):
     """One rank of a gloo-staged group on the shared GPU: the native step
     (kTxStaged) and the Python step train on the same uneven data (rank r
     has 6 - r minibatches of 300 + 100 r rows); this rank's shard must agree."""
@@ -325,12 +334,13 @@ def _staged_main(rank, world, port, out_dir, model, max_conc):
     for native in ("0", "1"):
         os.environ["WH_PSX_NATIVE"] = native
         if model == "difacto":
-            lr = DifactoLearner(_conf(max_conc=max_conc), comm, dev, cap=1 << 14, vcap=1 << 12,
-                                seed=5)
+            lr = DifactoLearner(_conf(max_conc=max_conc, opts=opts), comm, dev, cap=1 << 14,
+                                vcap=1 << 12, seed=5)
         else:
+            fb = int(opts[opts.index("fb") + 2]) if "fb" in opts else 0
             lr = LinearLearner(LinearConfig(algo=3, lambda_l1=0.1, lr_eta=0.1,
-                                            max_concurrency=max_conc), comm, dev, cap=1 << 14,
-                               seed=5)
+                                            max_concurrency=max_conc, fixed_bytes=fb), comm, dev,
+                               cap=1 << 14, seed=5)
         prog = _lockstep(lr, mine)
         assert bool(lr.psx._nat) == (native == "1")
         res[native] = (_model(lr) if model == "difacto" else _lin_model(lr), prog)
@@ -374,17 +384,17 @@ def _staged_main(rank, world, port, out_dir, model, max_conc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,model,max_conc", [(2, "difacto", 2), (2, "difacto", 1),
-                                                  (2, "linear", 2), (3, "difacto", 2),
-                                                  (3, "linear", 1), (4, "difacto", 2),
-                                                  (5, "linear", 2)])
-def test_native_step_multi_process_staged(tmp_path, world, model, max_conc):
+@pytest.mark.parametrize("world,model,max_conc,opts", [
+    (2, "difacto", 2, ""), (2, "difacto", 1, ""), (2, "linear", 2, ""), (3, "difacto", 2, ""),
+    (3, "linear", 1, ""), (4, "difacto", 2, ""), (5, "linear", 2, ""),
+    (2, "difacto", 2, "fb1clip"), (3, "difacto", 1, "fb2dropnorm"), (2, "linear", 2, "fb1")])
+def test_native_step_multi_process_staged(tmp_path, world, model, max_conc, opts):
     """The native multi-shard step in 2 to 5 processes (ranks sharing the
     GPU, transfers staged through gloo), uneven data per rank: every rank's
     shard equals the one the Python step trains on the same data, and every
     minibatch is forwarded once (learn/difacto/async_sgd.h:363-425 with W
     workers and S = W servers)."""
-    mp.spawn(_staged_main, args=(world, _free_port(), str(tmp_path), model, max_conc),
+    mp.spawn(_staged_main, args=(world, _free_port(), str(tmp_path), model, max_conc, opts),
              nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / ("r%d" % r)).read_text() == "ok\n"
@@ -584,24 +594,29 @@ def test_linear_loopback_gpu_matches_cpu(algo, max_conc):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,max_conc", [("difacto", 2), ("difacto", 1), ("linear", 2),
-                                            ("linear", 1)])
-def test_native_step_matches_python_step(model, max_conc, monkeypatch):
+@pytest.mark.parametrize("model,max_conc,opts", [
+    ("difacto", 2, ""), ("difacto", 1, ""), ("linear", 2, ""), ("linear", 1, ""),
+    ("difacto", 2, "fb1"), ("difacto", 1, "fb3clipdrop"), ("difacto", 2, "clipnorm"),
+    ("linear", 2, "fb2")])
+def test_native_step_matches_python_step(model, max_conc, opts, monkeypatch):
     """The C++ driver of the multi-shard step (csrc/bind/psx_native.inl
     PsxStep) trains the same model as the Python step it ports (kv/psx.py
-    Psx.train, WH_PSX_NATIVE=0), pipelined and strict, on 4 loopback shards."""
+    Psx.train, WH_PSX_NATIVE=0), pipelined and strict, on 4 loopback shards;
+    with the fixed_bytes filter (the same stochastic-rounding seeds in the
+    same order) and the embedding-gradient post-processing too."""
     from wormhole_amd.parallel.comm import LoopbackComm
     dev = torch.device("cuda", 0)
     runs = {}
     for native in ("1", "0"):
         monkeypatch.setenv("WH_PSX_NATIVE", native)
         if model == "difacto":
-            lr, prog, b = _run(LoopbackComm(4, dev), _conf(max_conc=max_conc), dev, steps=8,
-                               rows=3000)
+            lr, prog, b = _run(LoopbackComm(4, dev), _conf(max_conc=max_conc, opts=opts), dev,
+                               steps=8, rows=3000)
             runs[native] = (_model(lr), prog, bool(lr.psx._nat))
         else:
+            fb = int(opts[opts.index("fb") + 2]) if "fb" in opts else 0
             lr, prog, b = _lin_run(LoopbackComm(4, dev), dev, 3, steps=8, rows=3000,
-                                   max_conc=max_conc)
+                                   max_conc=max_conc, fixed_bytes=fb)
             runs[native] = (_lin_model(lr), prog, bool(lr.psx._nat))
     (mn, pn, isn), (mp_, pp, isp) = runs["1"], runs["0"]
     assert isn and not isp

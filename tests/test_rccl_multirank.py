@@ -122,7 +122,7 @@ def _a2av_main(rank, world, port, out_dir):
                      (3, torch.uint8)][trial % 4]
         rows = [[rng.choice([0, 1, 5, 300]) for _ in range(world)] for _ in range(world)]
         if trial == 5:
-            rows[rank] = [0] * world
+            rows[1] = [0] * world  # (every rank agrees: rank 1 sends nothing)
         mine = rows[rank]
         x = torch.cat([torch.full((mine[q], width), 10 * rank + q, dtype=dt)
                        for q in range(world)]).to(dev)
@@ -211,7 +211,7 @@ def _rccl_step_main(rank, world, port, out_dir, model, max_conc, comms):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,model,max_conc,comms", [(2, "difacto", 2, 3), (3, "difacto", 2, 3),
-                                                        (2, "linear", 2, 3), (3, "difacto", 3, 1),
+                                                        (2, "linear", 2, 3), (3, "difacto", 2, 1),
                                                         (2, "difacto", 1, 3)])
 def test_native_step_multi_rank_rccl_same_gpu(tmp_path, world, model, max_conc, comms):
     mp.spawn(_rccl_step_main, args=(world, _free_port(), str(tmp_path), model, max_conc, comms),
@@ -268,5 +268,5 @@ def test_watchdog_ends_a_stalled_exchange(tmp_path, backend):
     assert "[psx watchdog] rank 0: no progress" in errs[0], errs[0]
     assert "of step 3" in errs[0] and "C" in errs[0]
     assert "WH_FAULT: rank 1 stalls" in errs[1] and "[psx watchdog] rank 1" in errs[1], errs[1]
-    assert "communicators aborted, exiting with status 3" in errs[0]
+    assert "exiting with status 3" in errs[0] and "exiting with status 3" in errs[1]
     assert not any((tmp_path / ("returned%d" % r)).exists() for r in range(2))

@@ -372,6 +372,11 @@ class Psx:
         if self.timer is not None:
             for c, ms in self.timer.report().items():
                 out["c%d_ms" % c] = ms / steps
+        elif self._nat and _COMM_TIMING:  # (the native step's per-exchange GPU time)
+            xt = self._nat.xtime()
+            for c in range(4):
+                if xt[4 + c]:
+                    out["c%d_ms" % c] = xt[c] / 1000.0 * xt[4 + c] / steps
         return out
 
     # ------------------------------------------------------------ streams
@@ -702,9 +707,9 @@ class Psx:
         PsxStep) -- the default for every GPU configuration: RCCL ranks (its
         own communicator, grouped send / recv per peer), gloo-staged ranks
         sharing one GPU, the loopback identity and the 1-rank RCCL loopback.
-        The payload filter, the collective timer and the embedding-gradient
-        post-processing stay on this Python step, which is also the test
-        oracle (``WH_PSX_NATIVE=0`` selects it)."""
+        It covers the payload filter (fixed_bytes), the embedding-gradient
+        post-processing and the exchange timing too; this Python step is the
+        test oracle (``WH_PSX_NATIVE=0`` selects it) and the CPU path."""
         if self._nat is None:
             lrn, emb = self.lrn, self.lrn.emb
             post = emb is not None and (emb.grad_clipping > 0 or emb.dropout > 0 or
@@ -716,8 +721,7 @@ class Psx:
                   "nccl": hip.PSX_TX_RCCL}.get(backend)
             if staged and backend == "gloo":
                 tx = hip.PSX_TX_STAGED
-            ok = (self.cuda and os.environ.get("WH_PSX_NATIVE", "1") != "0" and tx is not None
-                  and self.qf is None and self.timer is None and not post)
+            ok = self.cuda and os.environ.get("WH_PSX_NATIVE", "1") != "0" and tx is not None
             self._nat = False
             rccl = None
             if ok and tx == hip.PSX_TX_RCCL:
@@ -738,8 +742,14 @@ class Psx:
                     hp=list(lrn.hp), threshold=int(lrn.threshold), l1_shrk=bool(lrn.l1_shrk),
                     seed=int(lrn.seed), loss=int(lrn.loss), met=lrn.met, auc_sum=lrn.auc_sum,
                     tau=int(self.tau_max), max_load=float(lrn.kv.guard.max_load),
-                    cu_reserve=_CU_RESERVE if tx == hip.PSX_TX_RCCL else 0)
+                    cu_reserve=_CU_RESERVE if tx == hip.PSX_TX_RCCL else 0,
+                    filt=[self.qf.nb, self.qf.seed] if self.qf is not None else [0, 0],
+                    post=[float(emb.grad_clipping), float(emb.dropout),
+                          1.0 if emb.grad_normalization else 0.0, float(lrn.dim)]
+                    if post else [0.0, 0.0, 0.0, 0.0])
                 self._nat.requests = self.requests
+                self._nat.step = self.lrn.step
+                self.timer = None  # (the native step times its own exchanges)
         return self._nat or None
 
     def _own_rccl(self):
@@ -807,6 +817,8 @@ class Psx:
                 if len(next_batch) > 3 and next_batch[3] is not None:
                     ready = next_batch[3].cuda_event
             keys = self._kmod(keys)
+            if nat.step != self.lrn.step:  # (an evaluation pass counted steps in between)
+                nat.step = self.lrn.step
             if nk is not None and self.lrn.max_key:
                 if ready:  # the reduction reads the next keys on this stream
                     torch.cuda.current_stream(self.dev).wait_event(next_batch[3])
