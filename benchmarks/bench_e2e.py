@@ -59,6 +59,67 @@ def criteo_text(nrows, seed):
     return buf.tobytes()
 
 
+def _run_job(cmd, work, vper):
+    """One run of the job; the training pass(es) run from the first
+    "Training: iter = 0" line to the "Validating" / "Hit max" line that
+    follows the last pass, and their examples are the last progress-table
+    row of each pass (the table restarts every pass)."""
+    t1 = time.time()
+    proc = subprocess.Popen(cmd, cwd=work, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                            text=True, bufsize=1)
+    lines, stamps = [], []
+    for line in proc.stdout:
+        lines.append(line)
+        stamps.append(time.time())
+    err = proc.stderr.read()
+    rc = proc.wait()
+    wall = time.time() - t1
+    out = "".join(lines)
+    if rc != 0:
+        sys.stderr.write(out[-3000:] + err[-3000:])
+        raise SystemExit(rc)
+    is_row = [bool(re.match(r"^\s*[\d.]+\s+[\d.e+]+\s+[\d.e+]+", l)) for l in lines]
+    t_start = t_end = v_start = v_end = None
+    ttl, vttl, last_row, phase = 0.0, 0.0, None, None
+    for i, l in enumerate(lines):
+        if l.startswith("Training: iter") or l.startswith("Validating") or l.startswith("Hit max"):
+            if last_row is not None:
+                if phase == "train":
+                    ttl += last_row
+                elif phase == "val":
+                    vttl += last_row
+            last_row = None
+        if l.startswith("Training: iter"):
+            phase = "train"
+            if t_start is None:
+                t_start = stamps[i]
+        elif l.startswith("Validating"):
+            if t_end is None:
+                t_end = stamps[i]
+            if v_start is None:
+                v_start = stamps[i]
+            phase = "val"
+        elif l.startswith("Hit max"):
+            if t_end is None:
+                t_end = stamps[i]
+            if v_start is not None and v_end is None:
+                v_end = stamps[i]
+            phase = None
+        elif is_row[i] and phase is not None:
+            last_row = float(l.split()[1])
+    if last_row is not None and phase == "train":
+        ttl += last_row
+    sec = (t_end or time.time()) - t_start
+    print(out[-1500:], file=sys.stderr)
+    for l in err.splitlines():  # the workers' per-pass stage summaries
+        if "minibatches" in l or "[ingest]" in l:
+            print(l, file=sys.stderr)
+    return {"value": ttl / sec if sec > 0 else None, "examples": ttl, "train_sec": sec,
+            "job_wall_sec": wall,
+            "val_examples_per_s": (vttl / (v_end - v_start)) if (vper and v_start and v_end)
+            else None, "val_examples": vttl if vper else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=2_000_000)
@@ -72,10 +133,18 @@ def main():
                          "validation pass (the reference log's 0.93 M ex/s)")
     ap.add_argument("--rand-shuffle", type=int, default=10,
                     help="shuffle buffer in minibatches (the reference default is 10)")
+    ap.add_argument("--passes", type=int, default=1,
+                    help="data passes (max_data_pass): a timed region of several seconds "
+                         "over files that fit the box")
+    ap.add_argument("--repeat", type=int, default=1,
+                    help="run the job this many times over the same files and report the "
+                         "median and the spread")
     ap.add_argument("--dir", default=None)
     ap.add_argument("--reuse", action="store_true",
                     help="keep the data files already in --dir (A/B runs over the same files)")
     args = ap.parse_args()
+    if args.passes > 1 and args.val_rows:
+        raise SystemExit("--passes > 1 with --val-rows is not supported (validation per pass)")
     work = args.dir or tempfile.mkdtemp(prefix="wh_e2e_")
     os.makedirs(work, exist_ok=True)
     t0 = time.time()
@@ -101,9 +170,9 @@ def main():
     pattern = os.path.join(work, "train-part_.*\\.%s" % ("crb" if args.format == "crb" else "txt"))
     conf = os.path.join(work, "job.conf")
     with open(conf, "w") as f:
-        f.write('train_data = "%s"\ndata_format = "%s"\nminibatch = %d\nmax_data_pass = 1\n'
+        f.write('train_data = "%s"\ndata_format = "%s"\nminibatch = %d\nmax_data_pass = %d\n'
                 "print_sec = 1\nrand_shuffle = %d\n" % (pattern, args.format, args.minibatch,
-                                                   args.rand_shuffle))
+                                                   args.passes, args.rand_shuffle))
         if vper:
             f.write('val_data = "%s"\n' % os.path.join(work, "val-part_.*\\.txt"))
         if args.model == "linear":
@@ -114,54 +183,21 @@ def main():
     binp = os.path.join(ROOT, "bin", "%s.dmlc" % args.model)
     cmd = [sys.executable, os.path.join(ROOT, "tracker", "dmlc_local.py"), "-n", str(args.n),
            "-s", str(args.n), binp, conf]
-    # the scheduler's stdout is timestamped as it streams: the training pass
-    # runs from "Training: iter = 0" to the next "Validating"/"Hit max" line
-    t1 = time.time()
-    proc = subprocess.Popen(cmd, cwd=work, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                            text=True, bufsize=1)
-    lines, t_start, t_end, v_start, v_end = [], None, None, None, None
-    for line in proc.stdout:
-        now = time.time()
-        lines.append(line)
-        if t_start is None and line.startswith("Training: iter = 0"):
-            t_start = now
-        elif t_start is not None and t_end is None and (
-                line.startswith("Validating") or line.startswith("Hit max")):
-            t_end = now
-        if v_start is None and line.startswith("Validating"):
-            v_start = now
-        elif v_start is not None and v_end is None and line.startswith("Hit max"):
-            v_end = now
-    err = proc.stderr.read()
-    rc = proc.wait()
-    wall = time.time() - t1
-    out = "".join(lines)
-    if rc != 0:
-        sys.stderr.write(out[-3000:] + err[-3000:])
-        raise SystemExit(rc)
-    rows = [l for l in lines if re.match(r"^\s*[\d.]+\s+[\d.e+]+\s+[\d.e+]+", l)]
-    if vper:  # the last table row is the validation pass's; the training rows precede it
-        vi = [i for i, l in enumerate(lines) if l.startswith("Validating")][0]
-        trows = [l for l in rows if lines.index(l) < vi]
-        vrows = [l for l in rows if lines.index(l) > vi]
-        ttl = float(trows[-1].split()[1])
-        vttl = float(vrows[-1].split()[1]) if vrows else 0.0
-    else:
-        ttl = float(rows[-1].split()[1])
-        vttl = 0.0
-    sec = (t_end or time.time()) - t_start
-    print(out[-1500:], file=sys.stderr)
-    for l in err.splitlines():  # the workers' per-pass stage summaries
-        if "minibatches" in l or "[ingest]" in l:
-            print(l, file=sys.stderr)
+    runs = [_run_job(cmd, work, vper) for _ in range(max(1, args.repeat))]
+    vals = sorted(r["value"] for r in runs if r["value"])
+    med = vals[len(vals) // 2] if vals else None
+    r = runs[-1]
     print(json.dumps({
         "metric": "end-to-end examples/sec from %s files, %s.dmlc, %d worker(s)" % (
             args.format, args.model, args.n),
-        "value": ttl / sec if sec > 0 else None, "unit": "examples/s",
-        "examples": ttl, "train_sec": sec, "job_wall_sec": wall, "datagen_sec": gen_s,
+        "value": med, "unit": "examples/s",
+        "runs": [round(x["value"] / 1e6, 2) if x["value"] else None for x in runs],
+        "runs_unit": "M examples/s", "spread_min": vals[0] if vals else None,
+        "spread_max": vals[-1] if vals else None,
+        "examples": r["examples"], "train_sec": r["train_sec"], "job_wall_sec": r["job_wall_sec"],
+        "datagen_sec": gen_s, "passes": args.passes,
         "reference_linear_published": 1.85e6,
-        "val_examples_per_s": (vttl / (v_end - v_start)) if (vper and v_start and v_end) else None,
-        "val_examples": vttl if vper else None,
+        "val_examples_per_s": r["val_examples_per_s"], "val_examples": r["val_examples"],
         "reference_linear_val_published": 0.93e6,
         "config": {"rows": args.rows, "files": args.files, "minibatch": args.minibatch,
                    "val_rows": args.val_rows,

@@ -87,14 +87,19 @@ def main():
         return inner(w)
     obj.eval = counted
     solver.init()
+    # the objective after every iteration (pins the trajectory: a change to
+    # the solver or the kernels that moves the iterates shows here)
+    traj = [float(solver.old_objval)]
     for _ in range(args.warmup):
         solver.update_one_iter()
+        traj.append(float(solver.old_objval))
     sync()
     bsp.barrier()
     e0, it0 = evals[0], solver.num_iteration
     t1 = time.perf_counter()
     for _ in range(args.iters):
         solver.update_one_iter()
+        traj.append(float(solver.old_objval))  # (a host float the solver already holds)
     sync()
     bsp.barrier()
     dt = time.perf_counter() - t1
@@ -121,7 +126,7 @@ def main():
             "reg_L1": args.reg_l1, "iters": n_it, "ms_per_iter": 1000.0 * dt / n_it,
             "objective_evals_per_iter": (evals[0] - e0) / n_it,
             "ms_objective_pass": 1000.0 * t_eval, "ms_gradient_pass": 1000.0 * t_grad,
-            "objval": float(solver.old_objval), "load_s": t_load,
+            "objval": float(solver.old_objval), "objval_per_iter": traj, "load_s": t_load,
             "data": "synthetic Criteo-1TB-shaped (13 int + 26 cat fields, power law), "
                     "keys hashed into num_feature columns; device-resident CSR",
         }), flush=True)

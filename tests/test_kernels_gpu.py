@@ -453,6 +453,45 @@ def test_glm_objective_matches_cpu(with_val, loss):
     assert torch.allclose(mg, mc, rtol=1e-5, atol=1e-5)
 
 
+def test_owlqn_trajectory_matches_cpu():
+    """Ten OWL-QN iterations (learn/solver/lbfgs.h:168-196: gradient, the
+    two-loop direction with the L1 sign fixes, the backtracking line search)
+    on Criteo-shaped data hashed into 2^18 columns: the GPU path (glm.hip
+    objective / gradient, lbfgs.hip history dots and direction) follows the
+    CPU path's objective iteration by iteration and ends at the same
+    weights."""
+    from wormhole_amd.data.synthetic import CRITEO_TB_CARD, criteo_batch_cpu
+    from wormhole_amd.models.lbfgs_models import LinearObjective, _SplitData
+    from wormhole_amd.parallel.bsp import BSP
+    from wormhole_amd.solver.lbfgs import LBFGSSolver
+    F = 1 << 18
+    keys, label, off = criteo_batch_cpu(100_000, 4242, 0, CRITEO_TB_CARD)
+    keys = torch.remainder(keys, F)
+    runs = []
+    for dev in (torch.device("cpu"), DEV):
+        bsp = BSP(torch.device("cpu"))
+        obj = LinearObjective(bsp, _SplitData(keys, off, None, label, dev), dev)
+        obj.set_param("objective", "logistic")
+        obj.set_param("num_feature", str(F))
+        sol = LBFGSSolver(bsp, obj)
+        sol.silent = True
+        for k, v in (("reg_L1", 1.0), ("size_memory", 10), ("lbfgs_stop_tol", 0.0),
+                     ("min_lbfgs_iter", 1 << 30), ("max_lbfgs_iter", 10)):
+            sol.set_param(k, str(v))
+        sol.init()
+        traj = [float(sol.old_objval)]
+        for _ in range(10):
+            sol.update_one_iter()
+            traj.append(float(sol.old_objval))
+        runs.append((traj, sol.weight.detach().cpu()))
+    (tc, wc), (tg, wg) = runs
+    assert tc[-1] < 0.95 * tc[0]  # it trains
+    for i, (a, b) in enumerate(zip(tc, tg)):
+        assert abs(a - b) <= 1e-5 * abs(a), (i, tc, tg)
+    assert (wc != 0).sum() > 100
+    assert torch.allclose(wg, wc, rtol=1e-3, atol=1e-4 * float(wc.abs().max()))
+
+
 @pytest.mark.parametrize("n,f,k", [(1000, 5, 7), (4096, 64, 33), (5000, 127, 100),
                                    (3000, 128, 1000), (777, 200, 40)])
 def test_kmeans_assign_accum(hip, n, f, k):
