@@ -2807,7 +2807,7 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                         const Tensor& root_tot, std::vector<float> cut_vals,
                         std::vector<int64_t> cut_off, double eta, double alpha, double lambda,
                         double mcw, int64_t max_depth, double rt_eps, py::object allreduce,
-                        py::object reduce_scatter, py::object pick, int64_t f_lo) {
+                        py::object reduce_scatter, py::object pick, int64_t f_lo, bool walk) {
   // Multi-rank: either every level's built histograms are allreduced (all
   // features on every rank), or -- reduce_scatter / pick given
   // (models/gbdt.py HistExchange) -- each rank receives the global sums of
@@ -2926,10 +2926,16 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                        pfeat + 3 * S, pdefl + S, pdefl + 2 * S,
                        last ? nullptr : ptr<double>(tot_next), last ? nullptr : ptr<int32_t>(nleft), s);
     if (last) break;
+    // walk: the caller adds the leaf values by walking the tree over each
+    // row's bins (models/gbdt.py _finish), so the level whose children are
+    // the max-depth leaves needs neither their rows partitioned nor their
+    // histograms (never split): only the children's totals (from the split
+    // search, above) and the node table (~9 % of a depth-8 tree)
+    const bool leaves_next = walk && d + 1 == D;
     // partition of the split slots' rows on the device segment table
     auto sbeg = seg_cur.view({S, 2}).select(1, 0).contiguous();
-    auto ridx_new = torch::empty_like(ridx);
-    if (n > 0)
+    auto ridx_new = leaves_next ? ridx : torch::empty_like(ridx);
+    if (n > 0 && !leaves_next)
       TORCH_CHECK(wh::gbdt_partition_cursor(ptr<uint8_t>(B), ptr<uint8_t>(Bc), B.size(0), F,
                                             ptr<int32_t>(ridx), n, ptr<int32_t>(sbeg), d_iota, S,
                                             pfeat, pfeat + S, pdefl, pfeat + 2 * S, pfeat + 3 * S,
@@ -2951,6 +2957,12 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                                       ptr<int32_t>(sp), ptr<int32_t>(sp) + 4 * S, ptr<int32_t>(tasks),
                                       ptr<int32_t>(sp) + 5 * S, ptr<int32_t>(red), s),
                 "gbdt_grow_dev: too many slots");
+    if (leaves_next) {  // (leaf segments: left child empty -- unused by the walk)
+      tot_cur = tot_next;
+      seg_cur = seg_next;
+      alive_cur = alive_next;
+      continue;
+    }
     auto hs = torch::empty({S, F, nbin, 2}, f64);
     auto part = torch::empty({std::max<int64_t>(ub, 1) * pstride}, gpair.options().dtype(torch::kInt64));
     wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
@@ -3528,7 +3540,7 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("root_tot"), py::arg("cut_vals"), py::arg("cut_off"), py::arg("eta"), py::arg("alpha"),
         py::arg("reg_lambda"), py::arg("min_child_weight"), py::arg("max_depth"), py::arg("rt_eps"),
         py::arg("allreduce"), py::arg("reduce_scatter") = py::none(), py::arg("pick") = py::none(),
-        py::arg("f_lo") = 0);
+        py::arg("f_lo") = 0, py::arg("walk") = false);
   m.def("gbdt_gpair", &gbdt_gpair);
   m.def("gbdt_qscale", &gbdt_qscale);
   // the ingest ops block on one small device read each: the GIL is released

@@ -870,7 +870,8 @@ class TreeBuilder:
             out = _native.hip().gbdt_grow_dev(
                 root_tot=tot.contiguous(), **kw,
                 reduce_scatter=x.reduce_scatter if x is not None else None,
-                pick=x.pick if x is not None else None, f_lo=x.lo if x is not None else 0)
+                pick=x.pick if x is not None else None, f_lo=x.lo if x is not None else 0,
+                walk=self._walks(n))
         (feat, bin_, cond, defl, left, right, parent, gain, cover, bw, leaf, segs, ridx) = out
         tree = RegTree()
         tree.feat, tree.bin, tree.cond, tree.defl = list(feat), list(bin_), list(cond), list(defl)
@@ -1084,6 +1085,14 @@ class TreeBuilder:
                     tree.leaf[i] = self.p.eta * tree.base_weight[i]
                     changed = True
 
+    def _walks(self, n):
+        """True when :meth:`_finish` adds the leaf values by walking each
+        row's bins (the dense GPU matrix): the grower may then skip the last
+        level's partition and histograms."""
+        B = getattr(self, "B", None)
+        return bool(n and self.gpu and B is not None and B.dim() == 2 and B.shape[0] == n
+                    and B.dtype == torch.uint8 and not getattr(self.dm, "sparse", False))
+
     def _finish(self, tree, ridx, margin, n, leaf_segs):
         """Prune, then add the leaf values to the training margins from the
         final (pre-prune) leaf segments, then renumber: a pruned-away
@@ -1091,8 +1100,7 @@ class TreeBuilder:
         after pruning, looked up BEFORE the BFS renumbering changes ids."""
         self._prune_mark(tree)
         B = getattr(self, "B", None)
-        if (n and self.gpu and B is not None and B.dim() == 2 and B.shape[0] == n
-                and B.dtype == torch.uint8 and not getattr(self.dm, "sparse", False)):
+        if self._walks(n):
             # walk the pruned tree per row on its bins (a pruned-away
             # subtree's rows stop at its collapsed root, whose leaf value
             # _prune_mark set): coalesced, instead of a scatter by ridx
