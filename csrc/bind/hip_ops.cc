@@ -3377,6 +3377,7 @@ class LinearStep {
 
 #include "rccl_comm.h"
 #include "psx_native.inl"
+#include "difacto_step.inl"
 
 PYBIND11_MODULE(_hip, m) {
   m.doc() = "wormhole_amd gfx950 HIP kernels";
@@ -3452,6 +3453,22 @@ PYBIND11_MODULE(_hip, m) {
   m.def("a2a_plan", &a2a_plan_py, py::arg("rank"), py::arg("world"), py::arg("row_bytes"),
         py::arg("send_rows"), py::arg("recv_rows"),
         "one rank's per-peer all-to-all-v plan: (esz, (own_src, own_dst, own_bytes), sends, recvs)");
+  py::class_<DifactoStep>(m, "DifactoStep")
+      .def(py::init<KVStore*, std::vector<double>, int64_t, bool, int64_t, int64_t,
+                    std::vector<double>, double, bool>(),
+           py::arg("store"), py::arg("hp"), py::arg("threshold"), py::arg("l1_shrk"),
+           py::arg("seed"), py::arg("loss"), py::arg("post"), py::arg("max_load"),
+           py::arg("direct"), py::keep_alive<1, 2>())
+      .def("step", &DifactoStep::step, py::arg("keys"), py::arg("offset"), py::arg("val"),
+           py::arg("label"), py::arg("train"), py::arg("data_pass"), py::arg("met"),
+           py::arg("auc_sum"), py::arg("step"), py::arg("next_keys") = py::none(),
+           py::arg("next_offset") = py::none(), py::arg("next_val") = py::none(),
+           py::arg("ready") = 0)
+      .def("reset", &DifactoStep::reset)
+      .def("guard_sync", &DifactoStep::guard_sync)
+      .def_property_readonly("direct", &DifactoStep::direct)
+      .def_property_readonly("grows", &DifactoStep::grows)
+      .def_property_readonly("vgrows", &DifactoStep::vgrows);
   m.def("c10d_a2a_rows", &c10d_a2a_rows, py::arg("pg"), py::arg("x"), py::arg("send_rows"),
         py::arg("recv_rows"));
   m.def("localize", &localize, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(),

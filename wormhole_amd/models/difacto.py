@@ -12,6 +12,8 @@ learn/difacto/async_sgd.h:363-425), re-expressed on the GPU:
   FTRL on w and AdaGrad on V in one fused kernel.
 """
 
+import os
+
 import torch
 
 from .. import ops
@@ -80,6 +82,20 @@ class DifactoLearner:
         if comm.size > 1:
             from ..kv.psx import Psx
             self.psx = Psx(self)
+        # one shard on the GPU: the whole minibatch in one native call
+        # (csrc/bind/difacto_step.inl; WH_DIFACTO_NATIVE=0 keeps this
+        # module's op-by-op step, the test oracle)
+        self._nat = None
+        if (self.psx is None and self.device.type == "cuda" and self.vstride > 0
+                and os.environ.get("WH_DIFACTO_NATIVE", "1") != "0"):
+            from .. import _native
+            e = emb
+            self._nat = _native.hip().DifactoStep(
+                store=self.store, hp=[float(x) for x in self.hp], threshold=self.threshold,
+                l1_shrk=self.l1_shrk, seed=int(seed), loss=int(self.loss),
+                post=[float(e.grad_clipping), float(e.dropout),
+                      1.0 if e.grad_normalization else 0.0, float(self.dim)],
+                max_load=float(self.kv.guard.max_load), direct=self.direct_pull)
 
     def psx_linear_hp(self):
         """Embedding-free model on the multi-shard step's linear wire format:
@@ -101,6 +117,22 @@ class DifactoLearner:
             self.last_empty = self.psx.last_empty
             return py if wtype == PRED else None
         self.last_empty = offset.numel() <= 1 and self.comm.size == 1
+        if self._nat is not None and not self.max_key:
+            nk = no = nv = None
+            ready = 0
+            if next_batch is not None:
+                nk, no, nv = next_batch[:3]
+                if len(next_batch) > 3 and next_batch[3] is not None:
+                    ready = next_batch[3].cuda_event
+            py, u, m = self._nat.step(keys=keys, offset=offset, val=val, label=label,
+                                      train=train, data_pass=int(data_pass), met=self.met,
+                                      auc_sum=self.auc_sum, step=self.step, next_keys=nk,
+                                      next_offset=no, next_val=nv, ready=ready)
+            self.last_sizes = (u, m)
+            if label.numel():
+                self.n_mb += 1
+            self.step += 1
+            return py if wtype == PRED else None
         with trace.span("localize"):
             loc = localize_current(self, keys, offset, val)
         uniq, ucnt, owner_cnt, lid, csc_off, csc_row, csc_val = loc[:7]
@@ -149,6 +181,9 @@ class DifactoLearner:
         model: progress counters, save, end of pass, end of a timed run)."""
         if self.psx is not None:
             self.psx.flush()
+        if self._nat is not None:  # (its guard's growth counts, for the reports)
+            g = self.kv.guard
+            g.grows, g.vgrows = max(g.grows, self._nat.grows), max(g.vgrows, self._nat.vgrows)
         self.kv.flush()
 
     def take_progress(self):
