@@ -763,7 +763,19 @@ __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast
 constexpr int kX3Waves = 8;
 constexpr int kX3Threads = 64 * kX3Waves;
 
-template <int KS, int NSUB, int SLOTS>
+//
+// PIPE: each chunk's MFMAs in two halves of NSUB / 2 subtiles, the top-2
+// epilogue of one half issued between the other half's MFMAs (the previous
+// chunk's second half under this chunk's first, this chunk's first under
+// its second). Without it every chunk ends in a dependent epilogue: the
+// VALU waits for the MFMA chain to drain, and the two waves of a SIMD --
+// released together by the chunk barrier -- drain and rank at the same
+// time, idling the matrix pipe (the MFMAs alone take 2.9 of the kernel's
+// 8.0 ms at 10M x 128, k = 1000: profiles/round6_kmeans.txt). The B
+// operands of the next k-step are loaded before the current one's MFMAs.
+// Same accumulators (the pending half is carried across the chunk
+// boundary), same result.
+template <int KS, int NSUB, int SLOTS, bool PIPE>
 __global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __restrict__ Xp,
                                                              const float* __restrict__ xnorm,
                                                              int64_t n,
@@ -830,12 +842,12 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __rest
   int i1[16];
   // (padded centroid columns >= k start their accumulators at -1e30, so no
   // per-score bounds test is needed; 5 VALU per score)
-  auto top2 = [&](const f32x16 (&sc)[NSUB], int cbase) {
+  auto top2 = [&](const f32x16 (&sc)[NSUB], int cbase, int j0 = 0, int j1 = NSUB) {
     const int col0 = cbase + (lane & 31);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
 #pragma unroll
-      for (int j = 0; j < NSUB; ++j) {
+      for (int j = j0; j < j1; ++j) {
         const float v = sc[j][r];
         const bool nb = v > b1[r];
         b2[r] = fmaxf(b2[r], fminf(b1[r], v));
@@ -844,6 +856,61 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __rest
       }
     }
   };
+  // MFMAs of subtiles [j0, j1) of chunk c with the ranking of the OTHER
+  // half (columns from rbase) between them, in program order (sched_barrier
+  // fences: left alone the compiler hoists the whole VALU block after the
+  // MFMAs); the B operands double-buffered in registers one k-step ahead
+  auto mfma_rank = [&](f32x16 (&acc)[NSUB], const uint4* cur, int c, int j0, int rbase) {
+    constexpr int HN = NSUB / 2;
+    const int o0 = j0 == 0 ? HN : 0;  // the other half's subtiles [o0, o0 + HN)
+    constexpr int NU = 16 * HN;       // its score updates, spread over the groups
+    constexpr int PER_G = (NU + 3 * KS - 1) / (3 * KS);
+    const int col0 = rbase + (lane & 31);
+    auto rank_upd = [&](int u) {
+      if (u >= NU) return;
+      const int r = u / HN, j = o0 + u % HN;
+      const float v = acc[j][r];
+      const bool nb = v > b1[r];
+      b2[r] = fmaxf(b2[r], fminf(b1[r], v));
+      i1[r] = nb ? col0 + 32 * j : i1[r];
+      b1[r] = fmaxf(b1[r], v);
+    };
+#pragma unroll
+    for (int jj = 0; jj < HN; ++jj) {
+      const float init = c * CH + 32 * (j0 + jj) + (lane & 31) < k ? 0.f : -1e30f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j0 + jj][r] = init;
+    }
+    bf16x8 bh[2][HN], bl[2][HN];
+    auto load_b = [&](int s, int buf) {
+#pragma unroll
+      for (int jj = 0; jj < HN; ++jj) {
+        bh[buf][jj] = as_bf16x8(cur[((s * NSUB + j0 + jj) * 2) * 64 + lane]);
+        bl[buf][jj] = as_bf16x8(cur[((s * NSUB + j0 + jj) * 2 + 1) * 64 + lane]);
+      }
+    };
+    load_b(0, 0);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (s + 1 < KS) load_b(s + 1, (s + 1) & 1);
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+#pragma unroll
+        for (int jj = 0; jj < HN; ++jj)
+          acc[j0 + jj] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              g == 2 ? al[s] : ah[s], g == 1 ? bl[s & 1][jj] : bh[s & 1][jj], acc[j0 + jj], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < PER_G; ++t) rank_upd((s * 3 + g) * PER_G + t);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  f32x16 acc[NSUB];
+#pragma unroll
+  for (int j = 0; j < NSUB; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = -INFINITY;
   int64_t q = 0;
   for (; grp < ngroups; grp += gridDim.x) {
     const int64_t tile = grp * kX3Waves + wid;
@@ -879,7 +946,20 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __rest
 #else
       const uint4* cur = lds + (q % SLOTS) * CF;
 #endif
-      f32x16 acc[NSUB];
+      if constexpr (PIPE) {
+        constexpr int H = NSUB / 2;
+        mfma_rank(acc, cur, c, 0, (c > 0 ? c - 1 : 0) * CH);  // + the previous chunk's 2nd half
+        mfma_rank(acc, cur, c, H, c * CH);                    // + this chunk's first half
+        if (c == nchunk - 1 && grp + gridDim.x < ngroups) load_a(grp + gridDim.x, ah, al);
+        if (c == nchunk - 1) {  // the group's last half, then -inf for the next group
+          top2(acc, c * CH, H, NSUB);
+#pragma unroll
+          for (int j = H; j < NSUB; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[j][r] = -INFINITY;
+        }
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < NSUB; ++j) {
         const float init = c * CH + 32 * j + (lane & 31) < k ? 0.f : -1e30f;
@@ -908,7 +988,13 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __rest
       // after the group's last MFMAs the A registers are free: the next
       // group's fragments (L2 hits) load under the epilogue
       if (c == nchunk - 1 && grp + gridDim.x < ngroups) load_a(grp + gridDim.x, ah, al);
-#if !defined(WH_X3_VARIANT) || WH_X3_VARIANT != 1
+#if defined(WH_X3_VARIANT) && WH_X3_VARIANT == 3
+      // (microbench: a 1-VALU epilogue that keeps every accumulator live)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int j = 0; j < NSUB; ++j) b1[r] = fmaxf(b1[r], acc[j][r]);
+#elif !defined(WH_X3_VARIANT) || WH_X3_VARIANT != 1
       top2(acc, c * CH);
 #else
       if (acc[0][0] == 12345.f) b1[0] = 1.f;  // (microbench: no epilogue)
@@ -936,7 +1022,11 @@ __global__ __launch_bounds__(kX3Threads, 1) void k_assign_x3(const uint4* __rest
           if (row < n) {
             assign[row] = kk == 0x7fffffff ? 0 : kk;
             if (score) score[row] = v1;
+#if defined(WH_X3_VARIANT)
+            if (false) {  // (timing microbench: its scores are not the real ones)
+#else
             if (!(v1 - v2 >= 2.f * eps * xnorm[row])) {  // a near-tie: exact re-score
+#endif
               const int qq = atomicAdd(amb, 1);
               amb[1 + qq] = (int32_t)row;
             }
@@ -1049,6 +1139,17 @@ __global__ __launch_bounds__(256) void k_refine_rows(const float* __restrict__ X
 constexpr int kX3Nsub = WH_X3_NSUB;
 constexpr int kX3Slots = kX3Nsub == 4 ? 2 : 3;  // LDS ring: SLOTS x (KS * NSUB * 2 KiB)
 
+// the pipelined epilogue (PIPE) always; the unpipelined kernel only in the
+// timing microbench builds (-DWH_X3_VARIANT=0..3, tools/variant_so.sh:
+// 1 no epilogue, 2 no C DMA, 3 a one-VALU epilogue)
+bool x3_pipe() {
+#if defined(WH_X3_VARIANT)
+  return false;
+#else
+  return true;
+#endif
+}
+
 int x3_ks(int f) {  // k-steps of 16 features, padded to the template widths
   const int ks = (f + 15) / 16;
   return ks <= 2 ? 2 : ks <= 4 ? 4 : 8;
@@ -1107,16 +1208,28 @@ void kmeans_assign_x3(const void* Xp, const float* xnorm, const float* X, int64_
   const uint4* cp = static_cast<const uint4*>(Cp);
   switch (ks) {
     case 2:
-      hipLaunchKernelGGL((k_assign_x3<2, kX3Nsub, kX3Slots>), grid, block, 0, s, xp, xnorm, n, cp, nchunk, k,
-                         eps, assign, score, amb);
+      if (x3_pipe())
+        hipLaunchKernelGGL((k_assign_x3<2, kX3Nsub, kX3Slots, true>), grid, block, 0, s, xp, xnorm, n,
+                           cp, nchunk, k, eps, assign, score, amb);
+      else
+        hipLaunchKernelGGL((k_assign_x3<2, kX3Nsub, kX3Slots, false>), grid, block, 0, s, xp, xnorm,
+                           n, cp, nchunk, k, eps, assign, score, amb);
       break;
     case 4:
-      hipLaunchKernelGGL((k_assign_x3<4, kX3Nsub, kX3Slots>), grid, block, 0, s, xp, xnorm, n, cp, nchunk, k,
-                         eps, assign, score, amb);
+      if (x3_pipe())
+        hipLaunchKernelGGL((k_assign_x3<4, kX3Nsub, kX3Slots, true>), grid, block, 0, s, xp, xnorm, n,
+                           cp, nchunk, k, eps, assign, score, amb);
+      else
+        hipLaunchKernelGGL((k_assign_x3<4, kX3Nsub, kX3Slots, false>), grid, block, 0, s, xp, xnorm,
+                           n, cp, nchunk, k, eps, assign, score, amb);
       break;
     default:
-      hipLaunchKernelGGL((k_assign_x3<8, kX3Nsub, kX3Slots>), grid, block, 0, s, xp, xnorm, n, cp, nchunk, k,
-                         eps, assign, score, amb);
+      if (x3_pipe())
+        hipLaunchKernelGGL((k_assign_x3<8, kX3Nsub, kX3Slots, true>), grid, block, 0, s, xp, xnorm, n,
+                           cp, nchunk, k, eps, assign, score, amb);
+      else
+        hipLaunchKernelGGL((k_assign_x3<8, kX3Nsub, kX3Slots, false>), grid, block, 0, s, xp, xnorm,
+                           n, cp, nchunk, k, eps, assign, score, amb);
       break;
   }
   hipLaunchKernelGGL(k_transpose_c, dim3(grid_for((int64_t)k * f, 256)), dim3(256), 0, s, C, k, f,

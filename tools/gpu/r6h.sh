@@ -10,3 +10,8 @@ done
 unset WH_AB_HIP
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/gbdtprof -o run -- python3 $GRAFT_REPO_ROOT/benchmarks/bench_gbdt.py --trees 20 > $O/gbdtprof.log 2>&1 || { tail -20 $O/gbdtprof.log; exit 1; }
 echo "== gbdt"; head -14 $(find $O/gbdtprof -name "*kernel_stats.csv") | cut -d, -f1-5
+for v in "p1|" "lb8|--loopback 8"; do
+  IFS='|' read -r n a <<< "$v"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/dif_$n -o run -- python3 $GRAFT_REPO_ROOT/bench.py --steps 100 --warmup 10 --prewarm 300 $a > $O/dif_$n.log 2>&1 || { tail -20 $O/dif_$n.log; exit 1; }
+  echo "== difacto $n"; head -30 $(find $O/dif_$n -name "*kernel_stats.csv") | cut -d, -f1-5
+done
