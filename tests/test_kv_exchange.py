@@ -286,7 +286,7 @@ def test_fixed_bytes_loopback_gpu_matches_cpu():
     cg.fixed_bytes = cc.fixed_bytes = 3
     g, pg, _ = _run(LoopbackComm(4, dev), cg, dev, steps=6, rows=2000)
     c, pc, _ = _run(LoopbackComm(4, "cpu"), cc, "cpu", steps=6, rows=2000)
-    assert g.psx.qf is not None and g.psx.wire[2] > 0
+    assert g.psx.qf is not None and g.psx.wire_report(1)["c2"] > 0  # (native or Python tally)
     mg, mc = _model(g), _model(c)
     assert mg.keys() == mc.keys()
     bad = sum(1 for k, (w, n, v) in mc.items() if abs(w - mg[k][0]) > 1e-3 * max(1.0, abs(w)))
