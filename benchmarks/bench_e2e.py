@@ -79,37 +79,31 @@ def _run_job(cmd, work, vper):
         sys.stderr.write(out[-3000:] + err[-3000:])
         raise SystemExit(rc)
     is_row = [bool(re.match(r"^\s*[\d.]+\s+[\d.e+]+\s+[\d.e+]+", l)) for l in lines]
-    t_start = t_end = v_start = v_end = None
-    ttl, vttl, last_row, phase = 0.0, 0.0, None, None
+    # each pass: from its "Training: iter = k" line to the next stage line
+    # ("Validating" -- printed after every pass, with or without val_data --
+    # or "Hit max"); the examples are its table's last row
+    sec, ttl, vttl, v_start, v_end = 0.0, 0.0, 0.0, None, None
+    last_row, phase, p_start = None, None, None
     for i, l in enumerate(lines):
-        if l.startswith("Training: iter") or l.startswith("Validating") or l.startswith("Hit max"):
-            if last_row is not None:
-                if phase == "train":
-                    ttl += last_row
-                elif phase == "val":
-                    vttl += last_row
+        stage = l.startswith(("Training: iter", "Validating", "Hit max"))
+        if stage:
+            if phase == "train":
+                sec += stamps[i] - p_start
+                ttl += last_row or 0.0
+            elif phase == "val":
+                vttl += last_row or 0.0
+                if vper:
+                    v_end = stamps[i]
             last_row = None
+            phase = None
         if l.startswith("Training: iter"):
-            phase = "train"
-            if t_start is None:
-                t_start = stamps[i]
+            phase, p_start = "train", stamps[i]
         elif l.startswith("Validating"):
-            if t_end is None:
-                t_end = stamps[i]
+            phase = "val"
             if v_start is None:
                 v_start = stamps[i]
-            phase = "val"
-        elif l.startswith("Hit max"):
-            if t_end is None:
-                t_end = stamps[i]
-            if v_start is not None and v_end is None:
-                v_end = stamps[i]
-            phase = None
         elif is_row[i] and phase is not None:
             last_row = float(l.split()[1])
-    if last_row is not None and phase == "train":
-        ttl += last_row
-    sec = (t_end or time.time()) - t_start
     print(out[-1500:], file=sys.stderr)
     for l in err.splitlines():  # the workers' per-pass stage summaries
         if "minibatches" in l or "[ingest]" in l:
