@@ -81,7 +81,7 @@ def gen_ninja():
         "  command = $hipcc --offload-arch=%s -shared -fPIC $in -o $out %s" % (ARCH, hiplibs),
         "  description = LINK $out",
         "rule link_host",
-        "  command = $cxx -shared -fPIC -pthread $in -o $out %s" % tlibs,
+        "  command = $cxx -shared -fPIC -pthread $in -o $out %s -lssl -lcrypto" % tlibs,
         "  description = LINK $out",
         "rule tool",
         "  command = $cxx -O3 -std=c++17 -Wall -Wno-sign-compare -pthread -I%s/csrc -MD -MF $out.d -c $in -o $out" % ROOT,
@@ -89,7 +89,7 @@ def gen_ninja():
         "  deps = gcc",
         "  description = CXX(tool) $in",
         "rule link_tool",
-        "  command = $cxx -pthread $in -o $out",
+        "  command = $cxx -pthread $in -o $out -lssl -lcrypto",
         "  description = LINK $out",
     ]
     hip_objs = []
@@ -108,7 +108,7 @@ def gen_ninja():
         host_objs.append(obj)
     # standalone native tools (no torch): bin/native/{convert,text2crb}
     core = []
-    for name in ("parsers", "io", "lz4", "cityhash"):
+    for name in ("parsers", "io", "remote_fs", "json", "lz4", "cityhash"):
         obj = os.path.join(BUILD, "tool", name + ".o")
         lines.append("build %s: tool %s" % (obj, os.path.join(ROOT, "csrc/host/%s.cc" % name)))
         core.append(obj)
@@ -122,7 +122,7 @@ def gen_ninja():
                                                     " ".join(core)))
     # host runtime self-test (no torch): bin/native/host_selftest
     st = []
-    for name in ("workload_pool", "conf_parser", "van", "json"):
+    for name in ("workload_pool", "conf_parser", "van"):
         obj = os.path.join(BUILD, "tool", name + ".o")
         lines.append("build %s: tool %s" % (obj, os.path.join(ROOT, "csrc/host/%s.cc" % name)))
         st.append(obj)
@@ -139,7 +139,7 @@ def gen_ninja():
 
 
 SELFTEST_SRCS = ("csrc/tests/host_selftest.cc", "csrc/host/parsers.cc", "csrc/host/io.cc",
-                 "csrc/host/lz4.cc", "csrc/host/cityhash.cc", "csrc/host/workload_pool.cc",
+                 "csrc/host/remote_fs.cc", "csrc/host/lz4.cc", "csrc/host/cityhash.cc", "csrc/host/workload_pool.cc",
                  "csrc/host/conf_parser.cc", "csrc/host/van.cc", "csrc/host/json.cc")
 
 
@@ -156,7 +156,7 @@ def build_sanitized(kind, jobs=None):
         subprocess.run(["g++"] + flags + ["-c", os.path.join(ROOT, src), "-o", obj], check=True)
         objs.append(obj)
     exe = os.path.join(out_dir, "host_selftest")
-    subprocess.run(["g++"] + flags + objs + ["-o", exe], check=True)
+    subprocess.run(["g++"] + flags + objs + ["-o", exe, "-lssl", "-lcrypto"], check=True)
     return exe
 
 

@@ -8,6 +8,8 @@
 //     3-bit continuation flag, 4-byte alignment)
 #include "io.h"
 
+#include "remote_fs.h"
+
 #include <dirent.h>
 #include <regex.h>
 #include <sys/mman.h>
@@ -52,6 +54,11 @@ std::string strip_scheme(const std::string& p) { return ResolvePath(p); }
 }  // namespace
 
 std::vector<std::string> ListDirectory(const std::string& dir_in) {
+  if (IsRemote(dir_in)) {  // WebHDFS / S3 (csrc/host/remote_fs.cc)
+    std::vector<std::string> out;
+    for (const auto& e : RemoteList(dir_in)) out.push_back(e.uri);
+    return out;
+  }
   const std::string dir = strip_scheme(dir_in);
   std::vector<std::string> out;
   struct stat st;
@@ -77,8 +84,10 @@ std::vector<std::string> ListDirectory(const std::string& dir_in) {
 }
 
 std::vector<std::string> MatchFile(const std::string& pattern_in) {
-  const std::string pattern = strip_scheme(pattern_in);
-  const size_t pos = pattern.find_last_of("/\\");
+  const std::string pattern = IsRemote(pattern_in) ? pattern_in : strip_scheme(pattern_in);
+  // directory = up to the last '/' (not '\\': a backslash escapes the regex,
+  // e.g. "part-[0-9]\\.txt")
+  const size_t pos = pattern.find_last_of('/');
   std::string path = "./";
   if (pos != std::string::npos) path = pattern.substr(0, pos);
   std::string file = pos == std::string::npos ? pattern : pattern.substr(pos + 1);
@@ -102,6 +111,7 @@ std::vector<std::string> MatchFile(const std::string& pattern_in) {
 }
 
 int64_t FileSize(const std::string& path) {
+  if (IsRemote(path)) return RemoteSize(path);
   struct stat st;
   if (stat(strip_scheme(path).c_str(), &st) != 0) return -1;
   return (int64_t)st.st_size;
@@ -109,17 +119,29 @@ int64_t FileSize(const std::string& path) {
 
 // ------------------------------------------------------------------ split
 InputSplit::InputSplit(const std::string& path, int part, int nparts, bool recordio)
-    : path_(strip_scheme(path)), recordio_(recordio) {
-  fp_ = std::fopen(path_.c_str(), "rb");
-  if (!fp_) throw std::runtime_error("cannot open " + path_);
-  const int64_t size = FileSize(path_);
+    : path_(IsRemote(path) ? path : strip_scheme(path)), recordio_(recordio) {
+  if (IsRemote(path_)) {
+    remote_ = std::make_unique<RemoteReader>(path_);
+  } else {
+    fp_ = std::fopen(path_.c_str(), "rb");
+    if (!fp_) throw std::runtime_error("cannot open " + path_);
+  }
+  const int64_t size = remote_ ? remote_->size() : FileSize(path_);
   WH_CHECK(nparts >= 1 && part >= 0 && part < nparts, "bad part index");
   const int64_t nstep = (size + nparts - 1) / nparts;
   int64_t b = std::min<int64_t>(size, nstep * part);
   int64_t e = std::min<int64_t>(size, nstep * (part + 1));
   begin_ = Align(b, size);
   end_ = Align(e, size);
-  if (recordio_ && end_ > begin_) {
+  if (recordio_ && end_ > begin_ && remote_) {
+    // a remote CRB part is fetched whole (one ranged read) and decoded from
+    // memory like a mapping
+    own_ = RemoteRead(path_, begin_, end_ - begin_);
+    WH_CHECK((int64_t)own_.size() == end_ - begin_, "short read of " + path_);
+    map_off_ = begin_;
+    map_len_ = own_.size();
+    map_ = own_.data();
+  } else if (recordio_ && end_ > begin_) {
     // CRB parts are read through a mapping: a record is decoded straight
     // from the page cache by whichever reader thread takes it (a stdio read
     // per record under the readers' lock copied every byte once more, on
@@ -138,7 +160,7 @@ InputSplit::InputSplit(const std::string& path, int part, int nparts, bool recor
 }
 
 InputSplit::~InputSplit() {
-  if (map_) munmap(const_cast<char*>(map_), map_len_);
+  if (map_ && own_.empty()) munmap(const_cast<char*>(map_), map_len_);
   if (fp_) std::fclose(fp_);
 }
 
@@ -147,14 +169,14 @@ int64_t InputSplit::Align(int64_t pos, int64_t size) {
   if (pos >= size) return size;
   if (!recordio_) {
     // a line belongs to the part holding its first byte
-    std::fseek(fp_, pos - 1, SEEK_SET);
+    src_seek(pos - 1);
     int c;
     int64_t p = pos - 1;
-    while ((c = std::fgetc(fp_)) != EOF) {
+    while ((c = src_getc()) != EOF) {
       ++p;
       if (c == '\n' || c == '\r') {
         // swallow a "\r\n" pair
-        int c2 = std::fgetc(fp_);
+        int c2 = src_getc();
         if (c2 != EOF && (c2 == '\n' || c2 == '\r') && c2 != c) ++p;
         return p;
       }
@@ -168,9 +190,9 @@ int64_t InputSplit::Align(int64_t pos, int64_t size) {
   constexpr int64_t kBlock = 1 << 20;
   std::vector<uint32_t> w(kBlock / 4 + 2);
   while (p + 8 <= size) {
-    std::fseek(fp_, p, SEEK_SET);
+    src_seek(p);
     const int64_t want = std::min<int64_t>(kBlock + 8, size - p) / 4;
-    const size_t got = std::fread(w.data(), 4, (size_t)want, fp_);
+    const size_t got = src_read(w.data(), 4 * (size_t)want) / 4;
     if (got < 2) break;
     for (size_t i = 0; i + 1 < got; ++i) {
       if (w[i] == kRecordIOMagic) {
@@ -183,8 +205,17 @@ int64_t InputSplit::Align(int64_t pos, int64_t size) {
   return size;
 }
 
+void InputSplit::src_seek(int64_t off) {
+  if (remote_) remote_->Seek(off);
+  else std::fseek(fp_, off, SEEK_SET);
+}
+int InputSplit::src_getc() { return remote_ ? remote_->GetC() : std::fgetc(fp_); }
+size_t InputSplit::src_read(void* buf, size_t n) {
+  return remote_ ? remote_->Read(static_cast<char*>(buf), n) : std::fread(buf, 1, n, fp_);
+}
+
 void InputSplit::BeforeFirst() {
-  std::fseek(fp_, begin_, SEEK_SET);
+  src_seek(begin_);
   pos_ = begin_;
   carry_.clear();
 }
@@ -199,7 +230,7 @@ bool InputSplit::NextChunk(std::string* out, size_t hint) {
   if (want > 0) {
     const size_t old = buf.size();
     buf.resize(old + want);
-    const size_t got = std::fread(&buf[old], 1, want, fp_);
+    const size_t got = src_read(&buf[old], want);
     buf.resize(old + got);
     pos_ += got;
   }
@@ -277,12 +308,12 @@ bool InputSplit::NextRecord(std::string* out) {
   while (true) {
     if (pos_ >= end_) return false;
     uint32_t hdr[2];
-    if (std::fread(hdr, 4, 2, fp_) != 2) return false;
+    if (src_read(hdr, 8) != 8) return false;
     WH_CHECK(hdr[0] == kRecordIOMagic, "invalid recordio stream in " + path_);
     const uint32_t cflag = hdr[1] >> 29, len = hdr[1] & ((1u << 29) - 1);
     const uint32_t padded = (len + 3u) & ~3u;
     std::string data(padded, '\0');
-    if (padded && std::fread(&data[0], 1, padded, fp_) != padded)
+    if (padded && src_read(&data[0], padded) != padded)
       throw std::runtime_error("truncated recordio record in " + path_);
     pos_ += 8 + padded;
     data.resize(len);
@@ -304,14 +335,31 @@ bool InputSplit::NextRecord(std::string* out) {
 
 // --------------------------------------------------------------- recordio
 RecordIOWriter::RecordIOWriter(const std::string& path_in) {
+  if (IsRemote(path_in)) {  // buffered, uploaded whole at Close()
+    remote_ = path_in;
+    fp_ = open_memstream(&mem_, &mem_len_);
+    if (!fp_) throw std::runtime_error("cannot buffer " + path_in);
+    return;
+  }
   const std::string path = ResolvePath(path_in);
   fp_ = std::fopen(path.c_str(), "wb");
   if (!fp_) throw std::runtime_error("cannot open " + path + " for writing");
 }
-RecordIOWriter::~RecordIOWriter() { Close(); }
+RecordIOWriter::~RecordIOWriter() {
+  try {
+    Close();
+  } catch (...) {
+  }
+}
 void RecordIOWriter::Close() {
   if (fp_) std::fclose(fp_);
   fp_ = nullptr;
+  if (mem_) {
+    const std::string data(mem_, mem_len_);
+    std::free(mem_);
+    mem_ = nullptr;
+    RemoteWrite(remote_, data);
+  }
 }
 
 void RecordIOWriter::WriteRecord(const char* buf, size_t size) {

@@ -1,5 +1,6 @@
 #pragma once
 #include <cstdio>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -11,7 +12,9 @@ namespace host {
 constexpr uint32_t kRecordIOMagic = 0xced7230a;
 
 // URI -> local path (file://, plain paths; other schemes through the mount
-// named by WH_FS_MOUNT_<SCHEME>; throws when none is configured)
+// named by WH_FS_MOUNT_<SCHEME>; throws when none is configured). hdfs://,
+// viewfs:// and s3:// without a mount are read and written natively
+// (remote_fs.h) by the functions and classes below.
 std::string ResolvePath(const std::string& uri);
 std::vector<std::string> ListDirectory(const std::string& dir);
 std::vector<std::string> MatchFile(const std::string& pattern);
@@ -19,6 +22,8 @@ int64_t FileSize(const std::string& path);
 
 // Part `part` of `nparts` of one file, snapped to line (text) or record
 // (RecordIO) boundaries so every record belongs to exactly one part.
+class RemoteReader;
+
 class InputSplit {
  public:
   InputSplit(const std::string& path, int part, int nparts, bool recordio);
@@ -39,9 +44,14 @@ class InputSplit {
 
  private:
   int64_t Align(int64_t pos, int64_t size);
+  void src_seek(int64_t off);
+  int src_getc();
+  size_t src_read(void* buf, size_t n);
   std::string path_;
   bool recordio_;
-  std::FILE* fp_ = nullptr;
+  std::FILE* fp_ = nullptr;                // local file
+  std::unique_ptr<RemoteReader> remote_;  // or a remote one
+  std::string own_;                        // a remote recordio part, fetched whole
   int64_t begin_ = 0, end_ = 0, pos_ = 0;
   std::string carry_;
   // recordio parts are memory-mapped (map_ = file bytes [map_off_,
@@ -63,6 +73,9 @@ class RecordIOWriter {
  private:
   std::FILE* fp_ = nullptr;
   size_t bytes_ = 0;
+  std::string remote_;  // a remote target: records buffered in mem_
+  char* mem_ = nullptr;
+  size_t mem_len_ = 0;
 };
 
 }  // namespace host

@@ -12,6 +12,7 @@
 
 #include "common.h"
 #include "io.h"
+#include "remote_fs.h"
 #include "localizer.h"
 #include "parsers.h"
 #include "scheduler.h"
@@ -113,7 +114,7 @@ class PyTextBatches {
     InputSplit split(path, part, nparts, false);
     begin_ = split.begin();
     end_ = split.end();
-    path_ = ResolvePath(path);
+    path_ = IsRemote(path) ? path : ResolvePath(path);
     th_ = std::thread([this] { Run(); });
   }
   ~PyTextBatches() {
@@ -160,9 +161,18 @@ class PyTextBatches {
   // partial line after a cut is copied into the next buffer
   void Run() {
     try {
-      std::FILE* fp = std::fopen(path_.c_str(), "rb");
-      if (!fp) throw std::runtime_error("cannot open " + path_);
-      std::fseek(fp, begin_, SEEK_SET);
+      // a local file through stdio, a remote one (WebHDFS / S3) through
+      // ranged reads with a read-ahead window
+      std::unique_ptr<RemoteReader> rr;
+      std::FILE* fp = nullptr;
+      if (IsRemote(path_)) {
+        rr = std::make_unique<RemoteReader>(path_, 16 << 20);
+        rr->Seek(begin_);
+      } else {
+        fp = std::fopen(path_.c_str(), "rb");
+        if (!fp) throw std::runtime_error("cannot open " + path_);
+        std::fseek(fp, begin_, SEEK_SET);
+      }
       int64_t left = end_ - begin_;
       int64_t cap = 4 << 20;
       Tensor cur = Alloc(cap);
@@ -216,12 +226,13 @@ class PyTextBatches {
           b = static_cast<char*>(cur.data_ptr());
         }
         const int64_t want = std::min<int64_t>(left, cap - 1 - have);
-        const int64_t got = (int64_t)std::fread(b + have, 1, (size_t)want, fp);
+        const int64_t got = rr ? (int64_t)rr->Read(b + have, (size_t)want)
+                               : (int64_t)std::fread(b + have, 1, (size_t)want, fp);
         have += got;
         left -= got;
         if (got == 0 || left <= 0) eof = true;
       }
-      std::fclose(fp);
+      if (fp) std::fclose(fp);
     } catch (const std::exception& e) {
       std::lock_guard<std::mutex> lk(mu_);
       err_ = e.what();
@@ -669,23 +680,64 @@ void register_all(py::module& m) {
       o += n;
     }
   });
-  m.def("match_file", &MatchFile);
+  // (the file-system calls release the GIL: a remote URI is network I/O)
+  m.def("match_file", &MatchFile, py::call_guard<py::gil_scoped_release>());
   m.def("resolve_path", &ResolvePath);
-  m.def("list_directory", &ListDirectory);
-  m.def("file_size", &FileSize);
+  m.def("list_directory", &ListDirectory, py::call_guard<py::gil_scoped_release>());
+  m.def("file_size", &FileSize, py::call_guard<py::gil_scoped_release>());
+  // native WebHDFS / S3 (remote_fs.h): the Python side's model and
+  // prediction files go through these (wormhole_amd/utils/fs.py)
+  m.def("is_remote", &IsRemote);
+  m.def("remote_list", [](const std::string& uri) {
+    py::list out;
+    std::vector<RemoteEntry> es;
+    {
+      py::gil_scoped_release nogil;
+      es = RemoteList(uri);
+    }
+    for (const auto& e : es) out.append(py::make_tuple(e.uri, e.size));
+    return out;
+  });
+  m.def("remote_size", [](const std::string& uri) {
+    py::gil_scoped_release nogil;
+    return RemoteSize(uri);
+  });
+  m.def("remote_read", [](const std::string& uri, int64_t off, int64_t len) {
+    std::string d;
+    {
+      py::gil_scoped_release nogil;
+      d = RemoteRead(uri, off, len);
+    }
+    return py::bytes(d);
+  }, py::arg("uri"), py::arg("off") = 0, py::arg("len") = (int64_t)1 << 62);
+  m.def("remote_write", [](const std::string& uri, const std::string& data) {
+    py::gil_scoped_release nogil;
+    RemoteWrite(uri, data);
+  });
+  m.def("sigv4_authorization", &SigV4Authorization, py::arg("method"), py::arg("host"),
+        py::arg("path"), py::arg("query"), py::arg("amz_date"), py::arg("payload_sha256"),
+        py::arg("region"), py::arg("key_id"), py::arg("secret"), py::arg("token") = "");
   m.def("load_split", &load_split, py::arg("path"), py::arg("part") = 0, py::arg("nparts") = 1,
         py::arg("fmt") = "libsvm");
   m.def("read_text_split", [](const std::string& path, int part, int nparts) {
-    InputSplit s(path, part, nparts, false);
     std::string chunk, all;
-    while (s.NextChunk(&chunk)) all += chunk;
+    {
+      py::gil_scoped_release nogil;
+      InputSplit s(path, part, nparts, false);
+      while (s.NextChunk(&chunk)) all += chunk;
+    }
     return py::bytes(all);
   });
   m.def("read_recordio", [](const std::string& path, int part, int nparts) {
-    InputSplit s(path, part, nparts, true);
-    std::string rec;
+    std::vector<std::string> recs;
+    {
+      py::gil_scoped_release nogil;
+      InputSplit s(path, part, nparts, true);
+      std::string rec;
+      while (s.NextRecord(&rec)) recs.push_back(rec);
+    }
     py::list out;
-    while (s.NextRecord(&rec)) out.append(py::bytes(rec));
+    for (const auto& r : recs) out.append(py::bytes(r));
     return out;
   });
   m.def("crb_encode", [](const Tensor& keys, const Tensor& offset, const c10::optional<Tensor>& val,
@@ -720,23 +772,26 @@ void register_all(py::module& m) {
         std::string s = b;
         w.WriteRecord(s);
       })
-      .def("close", &RecordIOWriter::Close)
+      .def("close", &RecordIOWriter::Close, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("bytes_written", &RecordIOWriter::bytes_written);
 
   py::class_<PyTextBatches>(m, "TextBatches")
-      .def(py::init<const std::string&, int, int, int64_t, bool, int64_t>(), py::arg("path"),
+      .def(py::init<const std::string&, int, int, int64_t, bool, int64_t>(),
+           py::call_guard<py::gil_scoped_release>(), py::arg("path"),
            py::arg("part"), py::arg("nparts"), py::arg("minibatch"), py::arg("pinned") = true,
            py::arg("depth") = 3)
       .def("next", &PyTextBatches::next);
   py::class_<PyMinibatchIter>(m, "MinibatchIter")
       .def(py::init<const std::string&, int, int, const std::string&, int64_t, int64_t, double,
                     int64_t, bool>(),
+           py::call_guard<py::gil_scoped_release>(),
            py::arg("path"), py::arg("part"), py::arg("nparts"), py::arg("fmt"),
            py::arg("minibatch"), py::arg("shuffle_buf") = 0, py::arg("neg_sampling") = 1.0,
            py::arg("seed") = 0, py::arg("pinned") = false)
       .def("next", &PyMinibatchIter::next);
   py::class_<PyBlockIter>(m, "BlockIter")
       .def(py::init<const std::string&, int, int, const std::string&, int64_t, bool, int>(),
+           py::call_guard<py::gil_scoped_release>(),
            py::arg("path"), py::arg("part"), py::arg("nparts"), py::arg("fmt"), py::arg("rows"),
            py::arg("pinned") = true, py::arg("nthreads") = 0)
       .def("next", &PyBlockIter::next);

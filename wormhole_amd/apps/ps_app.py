@@ -37,12 +37,10 @@ def latest_checkpoint(model_out, nshard):
     """Newest iteration k whose periodic save completed on every shard (each
     worker seals its shard with ``<model_out>_iter-<k>_part-<r>.ok`` once
     the shard and its resume state are written), or -1."""
-    import glob
     import re
-    from ..utils.fs import resolve
-    base = resolve(model_out)
+    from ..utils import fs
     seen = {}
-    for f in glob.glob(glob.escape(base) + "_iter-*_part-*.ok"):
+    for f in fs.glob(str(model_out) + "_iter-*_part-*.ok"):
         m = re.match(r".*_iter-(\d+)_part-(\d+)\.ok$", f)
         if m:
             seen.setdefault(int(m.group(1)), set()).add(int(m.group(2)))

@@ -142,9 +142,8 @@ def write_state(snap, path):
 
 def load_state(store, path):
     """Restore the full optimizer state saved next to a shard (if any)."""
-    import os
-    from ..utils.fs import resolve
-    if not os.path.exists(resolve(path + ".state")):
+    from ..utils import fs
+    if not fs.exists(path + ".state"):
         return 0
     rec = np.frombuffer(open_uri(path + ".state", "rb").read(), dtype=_STATE)
     kt = torch.from_numpy(rec["k"].view(np.int64).copy())

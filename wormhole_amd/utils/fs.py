@@ -3,19 +3,76 @@
 doc/common/input.rst:53-115: local paths, ``file://``, ``hdfs://``,
 ``viewfs://``, ``s3://``, ``azure://``).
 
-Local paths and ``file://`` are opened directly. A remote scheme is served
-through a local mount of that filesystem (an HDFS FUSE / NFS gateway mount,
-mountpoint-s3 / s3fs, blobfuse ...) named by ``WH_FS_MOUNT_<SCHEME>``:
+Local paths and ``file://`` are opened directly. ``hdfs://`` / ``viewfs://``
+(WebHDFS) and ``s3://`` (S3 REST, SigV4) are read and written natively by
+the host runtime (csrc/host/remote_fs.h: addressing and credentials there);
+:func:`open_uri`, :func:`exists` and :func:`glob` take them. Any remote
+scheme can instead be served through a local mount of that filesystem (an
+HDFS FUSE / NFS gateway mount, mountpoint-s3 / s3fs, blobfuse ...) named by
+``WH_FS_MOUNT_<SCHEME>``, which then takes precedence:
 
     WH_FS_MOUNT_HDFS=/mnt/hdfs   hdfs://nn:9000/user/a/part-0 -> /mnt/hdfs/user/a/part-0
     WH_FS_MOUNT_S3=/mnt/s3       s3://bucket/key             -> /mnt/s3/bucket/key
 
 (HDFS / viewfs drop the name-node authority, object stores keep the bucket /
 container.) The native runtime resolves URIs the same way
-(csrc/host/io.cc ResolvePath). A scheme without a mount is an error that
-names the variable to set, never a silent local fallback.
+(csrc/host/io.cc ResolvePath). :func:`resolve` maps a URI to a LOCAL path:
+for another scheme without a mount it is an error that names the variable
+to set, never a silent local fallback.
 """
+import fnmatch
+import io
 import os
+
+_NATIVE = {"hdfs", "viewfs", "s3", "s3a", "s3n"}  # served by csrc/host/remote_fs.cc
+
+
+def is_remote(path):
+    """A URI the host runtime reads and writes over the network (a native
+    scheme with no ``WH_FS_MOUNT_<SCHEME>`` configured)."""
+    p = str(path)
+    if "://" not in p:
+        return False
+    scheme = p.split("://", 1)[0].lower()
+    return scheme in _NATIVE and not os.environ.get("WH_FS_MOUNT_" + scheme.upper())
+
+
+def _host():
+    from .. import _native
+    return _native.host()
+
+
+class _RemoteWriter(io.BytesIO):
+    """Buffers a file written to a remote URI and uploads it whole on close."""
+
+    def __init__(self, uri, initial=b""):
+        super().__init__(initial)
+        self.seek(0, io.SEEK_END)
+        self._uri = uri
+        self._sent = False
+
+    def close(self):
+        if not self._sent and not self.closed:
+            self._sent = True
+            _host().remote_write(self._uri, self.getvalue())
+        super().close()
+
+
+def exists(path):
+    if is_remote(path):
+        return _host().remote_size(str(path)) >= 0
+    return os.path.exists(resolve(path))
+
+
+def glob(pattern):
+    """Files matching a shell pattern in their last path component (the
+    directory part is literal), local or remote."""
+    p = str(pattern)
+    if is_remote(p):
+        d, name = p.rsplit("/", 1)
+        return [u for u, _ in _host().remote_list(d) if fnmatch.fnmatchcase(u.rsplit("/", 1)[1], name)]
+    import glob as _g
+    return sorted(_g.glob(resolve(p)))
 
 _DROP_AUTHORITY = {"hdfs", "viewfs"}
 
@@ -40,7 +97,20 @@ def resolve(path):
 
 
 def open_uri(path, mode="r", **kw):
-    """open() on a resolved URI; parent directories are created for writes."""
+    """open() on a resolved URI; parent directories are created for writes.
+    A remote URI is read whole when opened, or written whole when closed."""
+    if is_remote(path):
+        uri = str(path)
+        text = "b" not in mode
+        if any(c in mode for c in "wax"):
+            init = _host().remote_read(uri) if ("a" in mode and exists(uri)) else b""
+            raw = _RemoteWriter(uri, init)
+        else:
+            raw = io.BytesIO(_host().remote_read(uri))
+        if text:
+            return io.TextIOWrapper(raw, encoding=kw.get("encoding") or "utf-8",
+                                    newline=kw.get("newline"))
+        return raw
     p = resolve(path)
     if any(c in mode for c in "wax"):
         d = os.path.dirname(p)
