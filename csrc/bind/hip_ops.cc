@@ -102,6 +102,32 @@ struct DevWs {
   // parts into short and long blocks; an unscaled hint under-sized the plan,
   // every partition overflowed LDS and the job fell back to the hash path)
   int64_t last_nnz = 0, last_u = -1;
+  // pinned count buffers + events of the localize jobs' one host read,
+  // reused (a pinned allocation, an event create and destroy per job were
+  // host time of the launch-bound small-minibatch step)
+  struct PinnedRead {
+    int64_t* host = nullptr;
+    int64_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool busy = false;
+  };
+  std::vector<std::unique_ptr<PinnedRead>> reads;
+  PinnedRead* acquire_read(int64_t n) {
+    for (auto& r : reads)
+      if (!r->busy && r->cap >= n) {
+        r->busy = true;
+        return r.get();
+      }
+    auto r = std::make_unique<PinnedRead>();
+    r->cap = std::max<int64_t>(n, 64);
+    void* p = nullptr;
+    WH_HIP_CHECK_HOST(hipHostMalloc(&p, r->cap * sizeof(int64_t), hipHostMallocDefault));
+    r->host = static_cast<int64_t*>(p);
+    WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+    r->busy = true;
+    reads.push_back(std::move(r));
+    return reads.back().get();
+  }
   bool loc_dirty[2] = {false, false};
   bool loc_busy[2] = {false, false};
   int loc_next = 0;
@@ -272,7 +298,10 @@ class LocalizeJob {
   static bool part_enabled() { return !deterministic(); }
 
   ~LocalizeJob() {
-    if (event_) (void)hipEventDestroy(event_);
+    if (rd_) {  // abandoned before its read: the copy may still be in flight
+      (void)hipEventSynchronize(rd_->ev);
+      rd_->busy = false;
+    }
     if (counted_) dev_ws(keys_.device()).part_inflight--;
     if (tab_ >= 0 && !done_) {
       DevWs& ws = dev_ws(keys_.device());
@@ -301,8 +330,8 @@ class LocalizeJob {
     c10::DeviceGuard g(keys_.device());
     DevWs& ws = dev_ws(keys_.device());
     while (true) {
-      WH_HIP_CHECK_HOST(hipEventSynchronize(event_));
-      const int64_t* h = host_.data_ptr<int64_t>();
+      WH_HIP_CHECK_HOST(hipEventSynchronize(rd_->ev));
+      const int64_t* h = rd_->host;
       const bool own = h[nshard_] != 0;
       bool over = own;
       for (int64_t q = 1; q < nrecv_; q += stride_) over |= h[nshard_ + 1 + q] != 0;
@@ -325,7 +354,7 @@ class LocalizeJob {
       tsize_ = safe_;
       enqueue();
     }
-    const int64_t* h = host_.data_ptr<int64_t>();
+    const int64_t* h = rd_->host;
     owner_cnt_h_ = torch::empty({nshard_}, torch::kInt64);
     for (int64_t p = 0; p < nshard_; ++p) owner_cnt_h_.data_ptr<int64_t>()[p] = h[p];
     // everything after the owner counts (the peers' values and any extra)
@@ -333,6 +362,8 @@ class LocalizeJob {
     recv_h_ = torch::empty({nrecv_ ? ntail : 0}, torch::kInt64);
     for (int64_t q = 0; q < recv_h_.numel(); ++q)
       recv_h_.data_ptr<int64_t>()[q] = h[nshard_ + 1 + q];
+    rd_->busy = false;  // read and copied out: back to the pool
+    rd_ = nullptr;
     return {owner_cnt_h_, recv_h_};
   }
 
@@ -588,15 +619,17 @@ class LocalizeJob {
       }
     }
     dev_counts_ = both.contiguous();
-    if (!host_.defined() || host_.numel() < dev_counts_.numel())
-      host_ = torch::empty({dev_counts_.numel()},
-                           torch::TensorOptions().dtype(torch::kInt64).pinned_memory(true));
+    DevWs& ws = dev_ws(keys_.device());
+    if (rd_ && rd_->cap < dev_counts_.numel()) {  // (a retry: the last copy was waited for)
+      rd_->busy = false;
+      rd_ = nullptr;
+    }
+    if (!rd_) rd_ = ws.acquire_read(dev_counts_.numel());
     // an async copy into pinned memory + an event: nothing blocks here
-    WH_HIP_CHECK_HOST(hipMemcpyAsync(host_.data_ptr(), dev_counts_.data_ptr(),
+    WH_HIP_CHECK_HOST(hipMemcpyAsync(rd_->host, dev_counts_.data_ptr(),
                                      dev_counts_.numel() * sizeof(int64_t),
                                      hipMemcpyDeviceToHost, cs));
-    if (!event_) WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&event_, hipEventDisableTiming));
-    WH_HIP_CHECK_HOST(hipEventRecord(event_, cs));
+    WH_HIP_CHECK_HOST(hipEventRecord(rd_->ev, cs));
   }
 
   Tensor keys_, offset_, val_;
@@ -607,12 +640,12 @@ class LocalizeJob {
   Tensor owner_cnt_;
   int tab_ = -1;
   bool done_ = false;
-  Tensor tkeys_, slot_of_, blkoff_, dev_counts_, host_, owner_cnt_h_, recv_h_;
+  Tensor tkeys_, slot_of_, blkoff_, dev_counts_, owner_cnt_h_, recv_h_;
   Tensor uniq_, ucnt_, csc_off_, csc_row_, csc_val_, lid_;  // partitioned path outputs
   wh::PartPlan plan_{};
   bool part_ = false;
   bool counted_ = false;  // in DevWs::part_inflight
-  hipEvent_t event_ = nullptr;
+  DevWs::PinnedRead* rd_ = nullptr;  // the count read's pinned buffer + event
 };
 
 std::vector<Tensor> localize(const Tensor& keys, const Tensor& offset,
@@ -1436,6 +1469,7 @@ static HostSplit* host_split(const char* name) {
 }
 
 // -------------------------------------------------------------- metrics
+void auc_after_side(c10::DeviceIndex d, hipStream_t s);
 // auc_sum[0] += exact AUC of (py, label) (sort-free bucketed rank sum)
 void auc_acc(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
   CHECK_IN(py, torch::kFloat32);
@@ -1444,6 +1478,7 @@ void auc_acc(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
   TORCH_CHECK(py.numel() == label.numel(), "auc: py/label size mismatch");
   TORCH_CHECK(py.numel() < (int64_t)1 << 30, "auc: at most 2^30 examples per call");
   c10::DeviceGuard g(py.device());
+  auc_after_side(py.device().index(), cur_stream(py));  // (the workspace is shared)
   const int64_t n = py.numel();
   const int64_t wsb = wh::auc_ws_bytes(n);
   Tensor scratch;
@@ -1474,6 +1509,7 @@ hipStream_t own_stream(int dev, int role) {
 struct AucSide {
   c10::hip::HIPStream s;
   hipEvent_t in, out;
+  bool dirty = false;  // AUC work queued on the side stream since the last join
 };
 
 AucSide* auc_side(c10::DeviceIndex d, bool create) {
@@ -1492,14 +1528,29 @@ AucSide* auc_side(c10::DeviceIndex d, bool create) {
   return a;
 }
 
+// the stream s waits for the side stream's queued AUC work, if any
+void auc_after_side(c10::DeviceIndex d, hipStream_t s) {
+  AucSide* a = auc_side(d, false);
+  if (!a || !a->dirty) return;
+  WH_HIP_CHECK_HOST(hipEventRecord(a->out, a->s.stream()));
+  WH_HIP_CHECK_HOST(hipStreamWaitEvent(s, a->out, 0));
+  a->dirty = false;
+}
+
 void auc_acc_side(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
   CHECK_IN(py, torch::kFloat32);
   CHECK_IN(label, torch::kFloat32);
   CHECK_IN(auc_sum, torch::kFloat64);
   TORCH_CHECK(py.numel() == label.numel(), "auc: py/label size mismatch");
   TORCH_CHECK(py.numel() < (int64_t)1 << 30, "auc: at most 2^30 examples per call");
+  // a small minibatch's AUC is ONE launch of a few microseconds (the
+  // pairwise k_auc_small): it runs in order on the current stream, without
+  // the side stream's event pair (~4 us of host time in a launch-bound
+  // 1000-row step)
+  if (py.numel() <= 4096) return auc_acc(py, label, auc_sum);
   c10::DeviceGuard g(py.device());
   AucSide* a = auc_side(py.device().index(), true);
+  a->dirty = true;
   WH_HIP_CHECK_HOST(hipEventRecord(a->in, cur_stream(py)));
   WH_HIP_CHECK_HOST(hipStreamWaitEvent(a->s.stream(), a->in, 0));
   c10::hip::HIPCachingAllocator::recordStream(py.storage().data_ptr(), a->s);
@@ -1515,11 +1566,8 @@ void auc_acc_side(const Tensor& py, const Tensor& label, const Tensor& auc_sum) 
 
 void auc_join(const Tensor& auc_sum) {
   if (!auc_sum.is_cuda()) return;
-  AucSide* a = auc_side(auc_sum.device().index(), false);
-  if (!a) return;
   c10::DeviceGuard g(auc_sum.device());
-  WH_HIP_CHECK_HOST(hipEventRecord(a->out, a->s.stream()));
-  WH_HIP_CHECK_HOST(hipStreamWaitEvent(cur_stream(auc_sum), a->out, 0));
+  auc_after_side(auc_sum.device().index(), cur_stream(auc_sum));
 }
 
 Tensor auc(const Tensor& py, const Tensor& label) {

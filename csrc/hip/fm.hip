@@ -939,8 +939,12 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
   const int64_t ntiles = (nuniq + kPlanTile - 1) / kPlanTile;
   const int64_t vcap = v_cap(nuniq, nnz);
   // V chunks ordered by first-row bucket (meta_v[cap..2cap) receives the
-  // list); deterministic mode keeps the key-major list (partials by index)
-  int4* meta_sorted = (det_part || !hdr) ? meta_v : meta_v + vcap;
+  // list); deterministic mode keeps the key-major list (partials by index),
+  // and so does a minibatch whose xv rows fit in L2 many times over (the
+  // bucketing buys locality there is no need for: three launches of host
+  // time in a launch-bound small step)
+  const bool bucket = hdr && !det_part && nrows * (int64_t)vstride * 4 > ((int64_t)2 << 20);
+  int4* meta_sorted = bucket ? meta_v + vcap : meta_v;
   if (phase != 2) {
   if (lb && ntiles <= kLbMaxTiles) {  // one launch
     hipLaunchKernelGGL(k_chunk_plan, dim3((unsigned)ntiles), dim3(kThreads), 0, s, nuniq, csc_off,
@@ -954,7 +958,7 @@ void fm_backward(int64_t nuniq, int64_t nnz, int64_t nrows, const int64_t* csc_o
     hipLaunchKernelGGL(k_chunk_fill, dim3(grid_for(nuniq, kThreads)), dim3(kThreads), 0, s,
                        nuniq, csc_off, off_s, off_v, hdr, vstride, key_s, beg_s, meta_v, gw, gvc);
   }
-  if (hdr && !det_part) {
+  if (bucket) {
     const int shift = bucket_shift(std::max<int64_t>(nrows, 1));
     hipLaunchKernelGGL(k_vchunk_hist, dim3(kBucketBlocks), dim3(kThreads), 0, s, off_v + nuniq,
                        meta_v, csc_row, shift, bucket_hist);
