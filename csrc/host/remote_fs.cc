@@ -1,6 +1,7 @@
 // WebHDFS and S3 over HTTP/1.1 (see remote_fs.h).
 #include "remote_fs.h"
 
+#include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -9,6 +10,8 @@
 #include <openssl/hmac.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
+#include <pthread.h>
+#include <signal.h>
 #include <sys/socket.h>
 #include <sys/time.h>
 #include <unistd.h>
@@ -113,18 +116,52 @@ Url parse_url(const std::string& u) {
   return r;
 }
 
+// One client context per CA source: the system store, or the file named by
+// SSL_CERT_FILE (OpenSSL's own variable, read when a context is made -- a
+// context per value, so a process that changes it gets the new trust set).
+// Peers are verified: chain and host name (or IP address).
 SSL_CTX* tls_ctx() {
-  static std::once_flag once;
-  static SSL_CTX* ctx = nullptr;
-  std::call_once(once, [] {
-    ctx = SSL_CTX_new(TLS_client_method());
-    if (!ctx) return;
-    SSL_CTX_set_default_verify_paths(ctx);
-    SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
-  });
+  static std::mutex mu;
+  static std::map<std::string, SSL_CTX*> ctxs;
+  const char* cf = std::getenv("SSL_CERT_FILE");
+  const std::string key = cf ? cf : "";
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = ctxs.find(key);
+  if (it != ctxs.end()) return it->second;
+  SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
   if (!ctx) throw std::runtime_error("TLS: cannot create a client context");
+  SSL_CTX_set_default_verify_paths(ctx);
+  SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+  ctxs[key] = ctx;
   return ctx;
 }
+
+bool is_ip_literal(const std::string& h) {
+  unsigned char b[16];
+  return inet_pton(AF_INET, h.c_str(), b) == 1 || inet_pton(AF_INET6, h.c_str(), b) == 1;
+}
+
+// SSL_write on a socket the peer closed raises SIGPIPE (OpenSSL's send has
+// no MSG_NOSIGNAL): blocked on this thread for the write, and a pending one
+// consumed, so a dropped connection is an error return, not a dead process
+struct NoSigpipe {
+  sigset_t old{}, pipe{};
+  NoSigpipe() {
+    sigemptyset(&pipe);
+    sigaddset(&pipe, SIGPIPE);
+    pthread_sigmask(SIG_BLOCK, &pipe, &old);
+  }
+  ~NoSigpipe() {
+    sigset_t pend;
+    sigpending(&pend);
+    if (sigismember(&pend, SIGPIPE) && !sigismember(&old, SIGPIPE)) {
+      timespec zero{0, 0};
+      while (sigtimedwait(&pipe, nullptr, &zero) > 0) {
+      }
+    }
+    pthread_sigmask(SIG_SETMASK, &old, nullptr);
+  }
+};
 
 class Conn {
  public:
@@ -152,8 +189,13 @@ class Conn {
     if (u.tls) {
       ssl_ = SSL_new(tls_ctx());
       SSL_set_fd(ssl_, fd_);
-      SSL_set_tlsext_host_name(ssl_, u.host.c_str());
-      SSL_set1_host(ssl_, u.host.c_str());
+      if (is_ip_literal(u.host)) {  // an address: checked against the IP SANs, no SNI
+        X509_VERIFY_PARAM_set1_ip_asc(SSL_get0_param(ssl_), u.host.c_str());
+      } else {
+        SSL_set_tlsext_host_name(ssl_, u.host.c_str());
+        SSL_set1_host(ssl_, u.host.c_str());
+      }
+      NoSigpipe np;
       if (SSL_connect(ssl_) != 1) {
         char buf[256];
         ERR_error_string_n(ERR_get_error(), buf, sizeof buf);
@@ -168,6 +210,7 @@ class Conn {
     if (fd_ >= 0) close(fd_);
   }
   void write_all(const std::string& s) {
+    NoSigpipe np;
     size_t off = 0;
     while (off < s.size()) {
       const int n = ssl_ ? SSL_write(ssl_, s.data() + off, (int)std::min<size_t>(s.size() - off, 1 << 20))

@@ -7,7 +7,8 @@ the native remote file systems (csrc/host/remote_fs.cc) are tested against.
     ... WH_WEBHDFS_PORT=srv.port, WH_S3_ENDPOINT=srv.url ...
     srv.stop()
 
-WebHDFS: /webhdfs/v1/<path>?op=LISTSTATUS|GETFILESTATUS|OPEN|CREATE (OPEN and
+With certfile / keyfile the endpoint is HTTPS (tests point SSL_CERT_FILE at
+the certificate). WebHDFS: /webhdfs/v1/<path>?op=LISTSTATUS|GETFILESTATUS|OPEN|CREATE (OPEN and
 CREATE answer 307 to /datanode/<path>, like a name node). S3: path-style
 /<bucket>/<key> under <root>/<bucket>; listings paginate 2 keys at a time.
 """
@@ -15,6 +16,7 @@ import hashlib
 import hmac
 import json
 import os
+import ssl
 import threading
 import urllib.parse
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
@@ -111,8 +113,8 @@ class _Handler(BaseHTTPRequestHandler):
                                 "length": 0 if os.path.isdir(f) else os.path.getsize(f)})
             return self._send(200, json.dumps({"FileStatuses": {"FileStatus": ent}}).encode())
         if op in ("OPEN", "CREATE"):
-            loc = "http://127.0.0.1:%d/datanode%s?%s" % (self.server.server_port, _enc(path, "/"),
-                                                         urllib.parse.urlencode(q))
+            loc = "%s/datanode%s?%s" % (self.server.base_url, _enc(path, "/"),
+                                        urllib.parse.urlencode(q))
             return self._send(307, b"", {"Location": loc})
         return self._send(400, b"unsupported op")
 
@@ -208,8 +210,16 @@ class _Handler(BaseHTTPRequestHandler):
 
 
 class MockRemote:
-    def __init__(self, root, access_key="", secret_key="", region="us-east-1", hdfs_user=""):
+    """certfile / keyfile: serve HTTPS (the URLs then name `host`, which the
+    certificate must carry)."""
+
+    def __init__(self, root, access_key="", secret_key="", region="us-east-1", hdfs_user="",
+                 certfile=None, keyfile=None, host="127.0.0.1"):
         self.httpd = ThreadingHTTPServer(("127.0.0.1", 0), _Handler)
+        if certfile:
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(certfile, keyfile)
+            self.httpd.socket = ctx.wrap_socket(self.httpd.socket, server_side=True)
         self.httpd.daemon_threads = True
         self.httpd.root = os.path.abspath(root)
         self.httpd.access_key, self.httpd.secret_key = access_key, secret_key
@@ -218,7 +228,8 @@ class MockRemote:
         self.httpd.log = []
         self.httpd.denied = 0
         self.port = self.httpd.server_address[1]
-        self.url = "http://127.0.0.1:%d" % self.port
+        self.url = "%s://%s:%d" % ("https" if certfile else "http", host, self.port)
+        self.httpd.base_url = self.url
         self.th = threading.Thread(target=self.httpd.serve_forever, daemon=True)
 
     @property
@@ -241,6 +252,8 @@ class MockRemote:
         """The environment a client of this server needs."""
         e = {"WH_WEBHDFS_PORT": str(self.port), "WH_S3_ENDPOINT": self.url,
              "AWS_REGION": self.httpd.region}
+        if self.url.startswith("https"):
+            e["WH_WEBHDFS_URL"] = self.url
         if creds and self.httpd.secret_key:
             e.update(AWS_ACCESS_KEY_ID=self.httpd.access_key,
                      AWS_SECRET_ACCESS_KEY=self.httpd.secret_key)

@@ -9,10 +9,12 @@ request's Signature V4 with an implementation of its own):
   whole-object writes, missing objects;
 * InputSplit parts of text and RecordIO (CRB) files read remotely equal the
   local parts, byte for byte;
+* HTTPS endpoints: the server's certificate is verified (chain and name);
 * a one-worker (so deterministic) linear job trains from ``s3://`` data and saves its model to
   ``s3://`` (and ``hdfs://``): the same model as the same job on local files.
 """
 import os
+import shutil
 import subprocess
 import sys
 
@@ -174,3 +176,48 @@ def test_linear_job_trains_from_and_saves_to_remote(remote, tmp_path):
         assert got == ref, conf
         assert path.with_name(path.name + ".ok").exists()
     assert srv.denied == 0
+
+
+def _cert(d, name, san):
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-days", "1",
+                    "-keyout", str(d / (name + ".key")), "-out", str(d / (name + ".pem")),
+                    "-subj", "/CN=" + name, "-addext", "subjectAltName=" + san],
+                   check=True, capture_output=True)
+    return str(d / (name + ".pem")), str(d / (name + ".key"))
+
+
+@pytest.mark.skipif(shutil.which("openssl") is None, reason="needs the openssl CLI")
+def test_https_endpoints_verify_the_server(tmp_path, monkeypatch):
+    root = tmp_path / "remote"
+    (root / "bkt" / "d").mkdir(parents=True)
+    (root / "nn" / "d").mkdir(parents=True)
+    (root / "bkt" / "d" / "a.txt").write_bytes(b"x" * 5000 + b"\n")
+    (root / "nn" / "d" / "a.txt").write_bytes(b"y" * 3000 + b"\n")
+    cert, key = _cert(tmp_path, "localhost", "DNS:localhost")
+    other, _ = _cert(tmp_path, "other", "DNS:localhost")
+    srv = MockRemote(str(root), access_key="AK", secret_key="SK", certfile=cert, keyfile=key,
+                     host="localhost").start()
+    try:
+        for k, v in srv.env().items():
+            monkeypatch.setenv(k, v)
+        monkeypatch.setenv("SSL_CERT_FILE", cert)
+        host = _native.host()
+        assert host.remote_read("s3://bkt/d/a.txt", 10, 5) == b"xxxxx"
+        assert host.remote_read("hdfs://nn:8020/nn/d/a.txt") == b"y" * 3000 + b"\n"
+        host.remote_write("s3://bkt/d/b.bin", b"\x01" * 70000)
+        assert host.remote_size("s3://bkt/d/b.bin") == 70000
+        assert [u.rsplit("/", 1)[1] for u, _ in host.remote_list("s3://bkt/d")] == ["a.txt", "b.bin"]
+        assert host.read_text_split("s3://bkt/d/a.txt", 0, 1) == host.read_text_split(
+            str(root / "bkt" / "d" / "a.txt"), 0, 1)
+        # a certificate the client does not trust
+        monkeypatch.setenv("SSL_CERT_FILE", other)
+        with pytest.raises(RuntimeError, match="TLS handshake"):
+            host.remote_read("s3://bkt/d/a.txt")
+        # a trusted certificate for another name (the URL names the address)
+        monkeypatch.setenv("SSL_CERT_FILE", cert)
+        monkeypatch.setenv("WH_S3_ENDPOINT", "https://127.0.0.1:%d" % srv.port)
+        with pytest.raises(RuntimeError, match="TLS handshake"):
+            host.remote_read("s3://bkt/d/a.txt")
+        assert srv.denied == 0
+    finally:
+        srv.stop()
