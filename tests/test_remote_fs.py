@@ -221,3 +221,49 @@ def test_https_endpoints_verify_the_server(tmp_path, monkeypatch):
         assert srv.denied == 0
     finally:
         srv.stop()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["criteo", "crb"])
+def test_device_reader_from_remote_equals_local(remote, fmt):
+    """The GPU worker's reader (data/device_text.py: host reader threads cut
+    the part, the device parses / batches) over s3:// and hdfs:// URIs gives
+    the same minibatches, in the same order, as over the local file."""
+    import torch
+    from test_ingest import _criteo_text
+    from wormhole_amd.data.device_text import DeviceTextIter
+    srv, root = remote
+    host = _native.host()
+    dev = torch.device("cuda")
+    data = _criteo_text(4000, 11)
+    name = "c.txt" if fmt == "criteo" else "c.crb"
+    for sub in ("data", "bkt/train"):
+        local = root / sub / name
+        if fmt == "criteo":
+            local.write_bytes(data)
+        else:
+            keys_h, off_h, _, lab_h, _ = host.parse_text(data, "criteo")
+            w = host.RecordIOWriter(str(local))
+            for a in range(0, 4000, 900):
+                b = min(a + 900, 4000)
+                w.write(host.crb_encode(keys_h[off_h[a]:off_h[b]], off_h[a:b + 1] - off_h[a],
+                                        None, lab_h[a:b], None))
+            w.close()
+
+    def rows(uri, part, nparts):
+        it = DeviceTextIter(host, uri, part, nparts, fmt, 300, 0, 1.0, 7, dev)
+        out = []
+        while True:
+            b = it.next()
+            if b is None:
+                return out
+            keys, off, _, lab = [x.cpu() if x is not None else None for x in b.to_main(dev)]
+            out += [tuple(keys[off[i]:off[i + 1]].tolist()) + (float(lab[i]),)
+                    for i in range(lab.numel())]
+
+    for base, sub in (("hdfs://127.0.0.1:8020/data", "data"), ("s3://bkt/train", "bkt/train")):
+        for part, nparts in ((0, 1), (1, 3)):
+            want = rows(str(root / sub / name), part, nparts)
+            assert len(want) > 0
+            assert rows(base + "/" + name, part, nparts) == want
+    assert srv.denied == 0
