@@ -503,6 +503,84 @@ __global__ __launch_bounds__(kPcThreads) void k_part_cursor(
   };
   const int sg0 = seg_of(p0);
   const int sgl = seg_of(min(p0 + kPcTile, n) - 1);
+#if !defined(WH_PC_OLD)
+  if (sg0 == sgl) {
+    // Stable split of a tile inside ONE segment (every tile above the deep
+    // levels): thread t owns the 16 consecutive positions p0 + 16 t + u, and a
+    // block scan of the per-thread left counts ranks each row in position
+    // order, so a child receives each block's rows in the order they had --
+    // ascending row ids, as the level-0 identity order is. The next level's
+    // feature-byte gathers (Bc, one byte of feature-major bins per row) then
+    // walk each block's rows upwards through shared cache lines instead of
+    // jumping at random (the LDS-atomic ranks of the general path scramble
+    // a block's rows). The histograms are exact sums: trees are unchanged.
+    __shared__ int32_t s_base[2];
+    __shared__ uint32_t s_wl[kPcThreads / 64];
+    const int nd = tn[sg0];
+    const int feat = nd >= 0 ? node_feat[nd] : -1;
+    const int64_t ib = p0 + (int64_t)threadIdx.x * kPcPer;
+    int32_t rw[kPcPer];
+    if (ib + kPcPer <= n && (reinterpret_cast<uintptr_t>(ridx) & 15) == 0) {
+      const int4* r4 = reinterpret_cast<const int4*>(ridx + ib);
+#pragma unroll
+      for (int v = 0; v < kPcPer / 4; ++v) {
+        const int4 x = r4[v];
+        rw[4 * v] = x.x; rw[4 * v + 1] = x.y; rw[4 * v + 2] = x.z; rw[4 * v + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kPcPer; ++u) rw[u] = ib + u < n ? ridx[ib + u] : 0;
+    }
+    const int nv = (int)max((int64_t)0, min((int64_t)kPcPer, n - ib));  // valid positions
+    if (feat < 0) {  // finished leaf / unsplit node: the rows stay put
+      for (int u = 0; u < nv; ++u) out[ib + u] = rw[u];
+      return;
+    }
+    const int bin = node_bin[nd], defl = (int)node_defl[nd];
+    int bv[kPcPer];
+#pragma unroll
+    for (int u = 0; u < kPcPer; ++u)  // every gather in flight before the first is used
+      bv[u] = u < nv ? (Bc ? Bc[(int64_t)feat * nrows + rw[u]] : B[(int64_t)rw[u] * f + feat]) : 0;
+    uint32_t lm = 0;  // left flags of the thread's positions
+#pragma unroll
+    for (int u = 0; u < kPcPer; ++u) {
+      const int l = bv[u] == kMissing ? defl : (bv[u] <= bin ? 1 : 0);
+      lm |= (u < nv && l) ? 1u << u : 0u;
+    }
+    const uint32_t nl = (uint32_t)__popc(lm);
+    uint32_t inc = nl;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_wl[wid] = inc;
+    __syncthreads();
+    uint32_t lbefore = inc - nl, ltot = 0;
+#pragma unroll
+    for (int w = 0; w < kPcThreads / 64; ++w) {
+      if (w < wid) lbefore += s_wl[w];
+      ltot += s_wl[w];
+    }
+    const int64_t vtot = min((int64_t)kPcTile, n - p0);
+    if (threadIdx.x == 0) {
+      const int rtot = (int)(vtot - ltot);
+      s_base[0] = ltot ? atomicAdd(&lcur[nd], (int)ltot) : 0;
+      s_base[1] = rtot ? atomicSub(&rcur[nd], rtot) - rtot : 0;
+    }
+    __syncthreads();
+    int lo = s_base[0] + (int)lbefore;
+    int ro = s_base[1] + (int)(min((int64_t)threadIdx.x * kPcPer, vtot) - lbefore);
+#pragma unroll
+    for (int u = 0; u < kPcPer; ++u) {
+      if (u >= nv) continue;
+      if ((lm >> u) & 1u) out[lo++] = rw[u];
+      else out[ro++] = rw[u];
+    }
+    return;
+  }
+#endif
   // the tile's segments' split rules, read once per block into LDS
   for (int l = threadIdx.x; l < min(sgl - sg0 + 1, kPcMaxLocal); l += kPcThreads) {
     const int nd = tn[sg0 + l];
