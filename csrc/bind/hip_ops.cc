@@ -2772,7 +2772,7 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
     auto ridx_new = torch::empty_like(ridx);
     nleft_dev = torch::empty({nnode}, i32);
     if (!wh::gbdt_partition_cursor(ptr<uint8_t>(B), ptr<uint8_t>(Bc), B.size(0), F,
-                                   ptr<int32_t>(ridx), n, d_tb, d_tn, nt, d_feat, d_bin, d_defl,
+                                   ptr<int32_t>(ridx), n, d_tb, 1, d_tn, nt, d_feat, d_bin, d_defl,
                                    d_lc, d_rc, d_sb, nnode, ptr<int32_t>(nleft_dev),
                                    ptr<int32_t>(ridx_new), s)) {
       // position -> node map, flags, scan, per-node left counts, stable scatter
@@ -2901,34 +2901,53 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
   };
   const int D = (int)max_depth, NN = (2 << D) - 1, Smax = 1 << D, REC = wh::gbdt_node_rec();
   const int64_t pstride = wh::gbdt_hist_pstride((int)max_fcnt, (int)nbin);
-  // one small upload: root totals, root segment, feature groups, slot iota
+  // one small upload: root segment, feature groups, slot iota, then the root
+  // histogram's task list -- the same for every tree of a model, so kept
+  // per (device, rows, depth, groups) instead of uploaded per tree
   std::vector<int32_t> hw;
   hw.reserve(3 + 2 * G + Smax);
   hw.push_back(0), hw.push_back((int32_t)n), hw.push_back(1);
   for (auto& fg : fgroups) hw.push_back((int32_t)fg.first), hw.push_back((int32_t)fg.second);
   for (int i = 0; i < Smax; ++i) hw.push_back(i);
-  auto hdev = torch::from_blob(hw.data(), {(int64_t)hw.size()}, torch::kInt32).to(B.device());
+  const int64_t nch_root = std::max<int64_t>(1, (n + chunk - 1) / chunk);
+  std::vector<int32_t> root_tasks;
+  {
+    std::vector<int32_t> red;
+    for (int64_t c = 0; c < nch_root; ++c)
+      for (auto& fg : fgroups)
+        root_tasks.insert(root_tasks.end(), {0, (int)fg.first, (int)fg.second, (int)c, chunk});
+    for (int gi = 0; gi < G; ++gi)
+      red.insert(red.end(), {0, (int)fgroups[gi].first, (int)fgroups[gi].second, gi, (int)nch_root, G});
+    root_tasks.insert(root_tasks.end(), red.begin(), red.end());
+  }
+  // (never destroyed: device tensors must not be freed by static teardown)
+  static auto& upload_cache = *new std::map<std::vector<int32_t>, std::pair<Tensor, Tensor>>();
+  std::vector<int32_t> ukey = hw;
+  ukey.push_back((int32_t)B.device().index());
+  ukey.push_back(D);
+  auto uit = upload_cache.find(ukey);
+  if (uit == upload_cache.end()) {
+    if (upload_cache.size() > 16) upload_cache.clear();
+    auto a = torch::from_blob(hw.data(), {(int64_t)hw.size()}, torch::kInt32).to(B.device());
+    auto b = torch::from_blob(root_tasks.data(), {(int64_t)root_tasks.size()}, torch::kInt32)
+                 .to(B.device());
+    uit = upload_cache.emplace(ukey, std::make_pair(a, b)).first;
+  }
+  auto hdev = uit->second.first;
   const int32_t* d_root_seg = ptr<int32_t>(hdev);
   const int32_t* d_fg = d_root_seg + 3;
   const int32_t* d_iota = d_fg + 2 * G;
   Tensor tot_cur = root_tot;
   Tensor seg_cur = hdev.narrow(0, 0, 2);
-  Tensor alive_cur = torch::ones({1}, u8);
+  Tensor alive_cur = hdev.narrow(0, 2, 1).view(torch::kUInt8).narrow(0, 0, 1);  // (= 1: the root)
   auto nodes = torch::empty({NN, REC}, f64);  // every depth's apply writes all its slots' records
   const uint8_t* vp = reinterpret_cast<const uint8_t*>(valid.data_ptr());
   Tensor ridx = ridx0;
   // root histogram: the host's task list over [0, n)
   Tensor H_front;
   {
-    const int64_t nch = std::max<int64_t>(1, (n + chunk - 1) / chunk);
-    std::vector<int32_t> tasks, red;
-    for (int64_t c = 0; c < nch; ++c)
-      for (auto& fg : fgroups) tasks.insert(tasks.end(), {0, (int)fg.first, (int)fg.second, (int)c, chunk});
-    for (int gi = 0; gi < G; ++gi)
-      red.insert(red.end(), {0, (int)fgroups[gi].first, (int)fgroups[gi].second, gi, (int)nch, G});
-    tasks.insert(tasks.end(), red.begin(), red.end());
-    auto d = torch::from_blob(tasks.data(), {(int64_t)tasks.size()}, torch::kInt32).to(B.device());
-    const int64_t nt = nch * G;
+    const Tensor& d = uit->second.second;
+    const int64_t nt = nch_root * G;
     H_front = torch::empty({1, F, nbin, 2}, f64);
     auto part = torch::empty({nt * pstride}, gpair.options().dtype(torch::kInt64));
     wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
@@ -2962,7 +2981,6 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                     "gbdt_grow_dev: pick returned a bad candidate table");
       }
     }
-    auto nleft = last ? Tensor() : torch::empty({S}, i32);  // zeroed by the apply kernel
     auto pi = torch::empty({4 * S}, i32);  // pfeat | pbin | lcur | rcur
     auto pb = torch::empty({3 * S}, u8);   // pdefl | split | build_left
     Tensor tot_next = last ? Tensor() : torch::empty({2 * S, 2}, f64);
@@ -2972,7 +2990,7 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
                        ptr<int32_t>(seg_cur), ptr<uint8_t>(alive_cur), eta, alpha, lambda, mcw,
                        rt_eps, ptr<double>(nodes), pfeat, pfeat + S, pdefl, pfeat + 2 * S,
                        pfeat + 3 * S, pdefl + S, pdefl + 2 * S,
-                       last ? nullptr : ptr<double>(tot_next), last ? nullptr : ptr<int32_t>(nleft), s);
+                       last ? nullptr : ptr<double>(tot_next), nullptr, s);
     if (last) break;
     // walk: the caller adds the leaf values by walking the tree over each
     // row's bins (models/gbdt.py _finish), so the level whose children are
@@ -2980,15 +2998,15 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
     // histograms (never split): only the children's totals (from the split
     // search, above) and the node table (~9 % of a depth-8 tree)
     const bool leaves_next = walk && d + 1 == D;
-    // partition of the split slots' rows on the device segment table
-    auto sbeg = seg_cur.view({S, 2}).select(1, 0).contiguous();
+    // partition of the split slots' rows on the device segment table (the
+    // segment begins read in place from seg_cur's {begin, end} pairs; the
+    // children read the left cursors: no copy, no count kernel)
     auto ridx_new = leaves_next ? ridx : torch::empty_like(ridx);
     if (n > 0 && !leaves_next)
       TORCH_CHECK(wh::gbdt_partition_cursor(ptr<uint8_t>(B), ptr<uint8_t>(Bc), B.size(0), F,
-                                            ptr<int32_t>(ridx), n, ptr<int32_t>(sbeg), d_iota, S,
-                                            pfeat, pfeat + S, pdefl, pfeat + 2 * S, pfeat + 3 * S,
-                                            ptr<int32_t>(sbeg), S, ptr<int32_t>(nleft),
-                                            ptr<int32_t>(ridx_new), s),
+                                            ptr<int32_t>(ridx), n, ptr<int32_t>(seg_cur), 2, d_iota,
+                                            S, pfeat, pfeat + S, pdefl, pfeat + 2 * S, pfeat + 3 * S,
+                                            nullptr, S, nullptr, ptr<int32_t>(ridx_new), s),
                   "gbdt_grow_dev: partition refused the segment table");
     ridx = ridx_new;
     // next level's segments, the built children, their histogram tasks
@@ -3000,7 +3018,7 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
     auto tasks = torch::empty({std::max<int64_t>(ub, 1) * 5}, i32);
     auto red = torch::empty({(int64_t)S * G * 6}, i32);
     TORCH_CHECK(wh::gbdt_dev_children(S, ptr<int32_t>(seg_cur), pdefl + S, pdefl + 2 * S,
-                                      ptr<int32_t>(nleft), d_fg, G, chunk, ptr<int32_t>(seg_next),
+                                      pfeat + 2 * S, d_fg, G, chunk, ptr<int32_t>(seg_next),
                                       ptr<uint8_t>(alive_next), ptr<int32_t>(dseg),
                                       ptr<int32_t>(sp), ptr<int32_t>(sp) + 4 * S, ptr<int32_t>(tasks),
                                       ptr<int32_t>(sp) + 5 * S, ptr<int32_t>(red), s),
@@ -3011,17 +3029,26 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
       alive_cur = alive_next;
       continue;
     }
-    auto hs = torch::empty({S, F, nbin, 2}, f64);
     auto part = torch::empty({std::max<int64_t>(ub, 1) * pstride}, gpair.options().dtype(torch::kInt64));
-    wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
-                  ptr<float>(qscale), ptr<int32_t>(tasks), (int)std::max<int64_t>(ub, 1),
-                  ptr<int32_t>(red), S * G, (int)max_fcnt, dw, ptr<int64_t>(part),
-                  ptr<double>(hs), s, ptr<int32_t>(dseg), chunk, ptr<int32_t>(sp) + 5 * S,
-                  qscale.numel() == 3);
-    hs = reduce_hist(hs);
     auto H_next = torch::empty({2 * S, Fl, nbin, 2}, f64);
-    wh::gbdt_sibling(ptr<double>(H_front), ptr<double>(hs), ptr<int32_t>(sp),
-                     ptr<int32_t>(sp) + 4 * S, S, per, ptr<double>(H_next), s);
+    if (!reduce) {  // one rank: the reduce writes both children (no hs, no sibling launch)
+      wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
+                    ptr<float>(qscale), ptr<int32_t>(tasks), (int)std::max<int64_t>(ub, 1),
+                    ptr<int32_t>(red), S * G, (int)max_fcnt, dw, ptr<int64_t>(part),
+                    ptr<double>(H_next), s, ptr<int32_t>(dseg), chunk, ptr<int32_t>(sp) + 5 * S,
+                    qscale.numel() == 3, ptr<double>(H_front), ptr<int32_t>(sp),
+                    ptr<int32_t>(sp) + 4 * S);
+    } else {
+      auto hs = torch::empty({S, F, nbin, 2}, f64);
+      wh::gbdt_hist(ptr<uint8_t>(B), F, (int)nbin, ptr<int32_t>(ridx), ptr<float>(gpair),
+                    ptr<float>(qscale), ptr<int32_t>(tasks), (int)std::max<int64_t>(ub, 1),
+                    ptr<int32_t>(red), S * G, (int)max_fcnt, dw, ptr<int64_t>(part),
+                    ptr<double>(hs), s, ptr<int32_t>(dseg), chunk, ptr<int32_t>(sp) + 5 * S,
+                    qscale.numel() == 3);
+      hs = reduce_hist(hs);
+      wh::gbdt_sibling(ptr<double>(H_front), ptr<double>(hs), ptr<int32_t>(sp),
+                       ptr<int32_t>(sp) + 4 * S, S, per, ptr<double>(H_next), s);
+    }
     H_front = H_next;
     tot_cur = tot_next;
     seg_cur = seg_next;

@@ -219,7 +219,8 @@ constexpr int kRedE = 64, kRedK = 16;
 __global__ __launch_bounds__(kRedE * kRedK) void k_hist_reduce(
     const long long* __restrict__ part, int64_t pstride, const HistReduce* __restrict__ red, int f,
     int nbin, const float* __restrict__ qscale, double* __restrict__ hist,
-    const int32_t* __restrict__ dseg, int chunk) {
+    const int32_t* __restrict__ dseg, int chunk, const double* __restrict__ sib_hf,
+    const int32_t* __restrict__ sib_sp, const int32_t* __restrict__ sib_par) {
   __shared__ unsigned long long acc_s[kRedK][kRedE];
   HistReduce rd = red[blockIdx.y];
   if (dseg) {  // only the chunks that cover the slot's device segment wrote
@@ -240,8 +241,17 @@ __global__ __launch_bounds__(kRedE * kRedK) void k_hist_reduce(
   if (kj == 0 && e < nl2) {
 #pragma unroll
     for (int k = 1; k < kRedK; ++k) acc += acc_s[k][ei];
-    hist[((int64_t)rd.node * f + rd.fbeg) * nbin * 2 + e] =
-        (double)(long long)acc / (double)qscale[e & 1];
+    const double v = (double)(long long)acc / (double)qscale[e & 1];
+    if (sib_hf) {  // fused sibling step: both children of split rd.node
+      const int64_t per = (int64_t)f * nbin * 2, ge = (int64_t)rd.fbeg * nbin * 2 + e;
+      const int k = rd.node;
+      const double other = sib_hf[(int64_t)sib_par[k] * per + ge] - v;
+      const bool bl = sib_sp[4 * k + 3] != 0;
+      hist[(int64_t)(2 * k) * per + ge] = bl ? v : other;
+      hist[(int64_t)(2 * k + 1) * per + ge] = bl ? other : v;
+    } else {
+      hist[((int64_t)rd.node * f + rd.fbeg) * nbin * 2 + e] = v;
+    }
   }
 }
 
@@ -410,7 +420,8 @@ int64_t gbdt_hist_pstride(int max_fcnt, int nbin) { return ((int64_t)2 * max_fcn
 void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const float* gpair,
                const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
                int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s,
-               const int32_t* dseg, int chunk, const int32_t* ntask_dev, bool w32) {
+               const int32_t* dseg, int chunk, const int32_t* ntask_dev, bool w32,
+               const double* sib_hf, const int32_t* sib_sp, const int32_t* sib_par) {
   if (ntask <= 0) return;
   static bool attr = false;
   if (!attr) {  // dynamic LDS above 64 KB must be opted into per kernel
@@ -432,7 +443,7 @@ void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const flo
   if (nred > 0)
     hipLaunchKernelGGL(k_hist_reduce, dim3((unsigned)((2 * max_fcnt * nbin + kRedE - 1) / kRedE), nred),
                        dim3(kRedE * kRedK), 0, s, pt, ps, reinterpret_cast<const HistReduce*>(red), f, nbin,
-                       qscale, hist, ntask_dev ? nullptr : dseg, chunk);
+                       qscale, hist, ntask_dev ? nullptr : dseg, chunk, sib_hf, sib_sp, sib_par);
 }
 
 // Level bookkeeping on the device (the host tree grower, csrc/bind/gbdt_grow.cc):
@@ -480,7 +491,7 @@ constexpr int kPcMaxTiles = 2048, kPcMaxLocal = 512;
 
 __global__ __launch_bounds__(kPcThreads) void k_part_cursor(
     const uint8_t* __restrict__ B, const uint8_t* __restrict__ Bc, int64_t nrows, int f,
-    const int32_t* __restrict__ ridx, int64_t n, const int32_t* __restrict__ tb,
+    const int32_t* __restrict__ ridx, int64_t n, const int32_t* __restrict__ tb, int tbs,
     const int32_t* __restrict__ tn, int nt, const int32_t* __restrict__ node_feat,
     const int32_t* __restrict__ node_bin, const uint8_t* __restrict__ node_defl,
     int32_t* __restrict__ lcur, int32_t* __restrict__ rcur, int32_t* __restrict__ out) {
@@ -488,7 +499,7 @@ __global__ __launch_bounds__(kPcThreads) void k_part_cursor(
   __shared__ uint32_t cnt[2][kPcMaxLocal];
   __shared__ int32_t base[2][kPcMaxLocal];
   __shared__ int32_t s_feat[kPcMaxLocal], s_bin[kPcMaxLocal], s_defl[kPcMaxLocal];
-  for (int i = threadIdx.x; i < nt; i += kPcThreads) s_tb[i] = tb[i];
+  for (int i = threadIdx.x; i < nt; i += kPcThreads) s_tb[i] = tb[(int64_t)i * tbs];
   for (int i = threadIdx.x; i < kPcMaxLocal; i += kPcThreads) cnt[0][i] = cnt[1][i] = 0;
   __syncthreads();
   const int64_t p0 = (int64_t)blockIdx.x * kPcTile;
@@ -570,6 +581,7 @@ __global__ __launch_bounds__(kPcThreads) void k_part_cursor(
       s_base[1] = rtot ? atomicSub(&rcur[nd], rtot) - rtot : 0;
     }
     __syncthreads();
+#if defined(WH_PC_DIRECT)
     int lo = s_base[0] + (int)lbefore;
     int ro = s_base[1] + (int)(min((int64_t)threadIdx.x * kPcPer, vtot) - lbefore);
 #pragma unroll
@@ -578,6 +590,24 @@ __global__ __launch_bounds__(kPcThreads) void k_part_cursor(
       if ((lm >> u) & 1u) out[lo++] = rw[u];
       else out[ro++] = rw[u];
     }
+#else
+    // staged through LDS in child order (left rows, then right rows), then
+    // stored as two contiguous runs: every store instruction writes whole
+    // lines (the per-thread runs of the direct stores were ~8 rows each)
+    __shared__ int32_t s_rows[kPcTile];
+    int lo = (int)lbefore;
+    int ro = (int)ltot + (int)(min((int64_t)threadIdx.x * kPcPer, vtot) - lbefore);
+#pragma unroll
+    for (int u = 0; u < kPcPer; ++u) {
+      if (u >= nv) continue;
+      if ((lm >> u) & 1u) s_rows[lo++] = rw[u];
+      else s_rows[ro++] = rw[u];
+    }
+    __syncthreads();
+    const int bl = s_base[0], br = s_base[1] - (int)ltot;
+    for (int i = threadIdx.x; i < (int)vtot; i += kPcThreads)
+      out[(i < (int)ltot ? bl : br) + i] = s_rows[i];
+#endif
     return;
   }
 #endif
@@ -673,17 +703,18 @@ __global__ void k_nleft(const int32_t* __restrict__ lcur, const int32_t* __restr
 }
 
 bool gbdt_partition_cursor(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f,
-                           const int32_t* ridx, int64_t n, const int32_t* tb, const int32_t* tn,
-                           int nt, const int32_t* node_feat, const int32_t* node_bin,
-                           const uint8_t* node_defl, int32_t* lcur, int32_t* rcur,
-                           const int32_t* seg_beg, int nnode, int32_t* nleft, int32_t* out,
-                           hipStream_t s) {
+                           const int32_t* ridx, int64_t n, const int32_t* tb, int tbs,
+                           const int32_t* tn, int nt, const int32_t* node_feat,
+                           const int32_t* node_bin, const uint8_t* node_defl, int32_t* lcur,
+                           int32_t* rcur, const int32_t* seg_beg, int nnode, int32_t* nleft,
+                           int32_t* out, hipStream_t s) {
   if (nt > kPcMaxTiles || n <= 0) return false;
   hipLaunchKernelGGL(k_part_cursor, dim3((unsigned)((n + kPcTile - 1) / kPcTile)),
-                     dim3(kPcThreads), 0, s, B, Bc, nrows, f, ridx, n, tb, tn, nt, node_feat,
+                     dim3(kPcThreads), 0, s, B, Bc, nrows, f, ridx, n, tb, tbs, tn, nt, node_feat,
                      node_bin, node_defl, lcur, rcur, out);
-  hipLaunchKernelGGL(k_nleft, dim3((nnode + 255) / 256), dim3(256), 0, s, lcur, seg_beg, nnode,
-                     nleft);
+  if (nleft)  // (the device grower reads the left cursors themselves)
+    hipLaunchKernelGGL(k_nleft, dim3((nnode + 255) / 256), dim3(256), 0, s, lcur, seg_beg, nnode,
+                       nleft);
   return true;
 }
 
@@ -962,7 +993,7 @@ __global__ __launch_bounds__(256) void k_gd_apply(
 // groups (offsets by a block scan), its count, and the reduce entries.
 __global__ __launch_bounds__(1024) void k_gd_children(
     int S, const int32_t* __restrict__ seg, const uint8_t* __restrict__ split,
-    const uint8_t* __restrict__ build_left, const int32_t* __restrict__ nleft,
+    const uint8_t* __restrict__ build_left, const int32_t* __restrict__ lcur,
     const int32_t* __restrict__ fg, int G, int chunk, int32_t* __restrict__ seg_next,
     uint8_t* __restrict__ alive_next, int32_t* __restrict__ dseg, int32_t* __restrict__ sp,
     int32_t* __restrict__ par, HistTask* __restrict__ tasks, int32_t* __restrict__ ntask,
@@ -975,7 +1006,7 @@ __global__ __launch_bounds__(1024) void k_gd_children(
     b = seg[2 * sl];
     e = seg[2 * sl + 1];
     s_ = split[sl] != 0;
-    m = s_ ? b + nleft[sl] : e;
+    m = s_ ? lcur[sl] : e;  // the left cursor after the partition (= b when none ran)
     seg_next[4 * sl] = b;
     seg_next[4 * sl + 1] = m;
     seg_next[4 * sl + 2] = m;
@@ -1060,12 +1091,12 @@ void gbdt_dev_apply(int S, int node0, bool last, const double* so, const double*
 }
 
 bool gbdt_dev_children(int S, const int32_t* seg, const uint8_t* split, const uint8_t* build_left,
-                       const int32_t* nleft, const int32_t* fg, int G, int chunk,
+                       const int32_t* lcur, const int32_t* fg, int G, int chunk,
                        int32_t* seg_next, uint8_t* alive_next, int32_t* dseg, int32_t* sp,
                        int32_t* par, int32_t* tasks, int32_t* ntask, int32_t* red,
                        hipStream_t s) {
   if (S > 1024) return false;
-  hipLaunchKernelGGL(k_gd_children, dim3(1), dim3(1024), 0, s, S, seg, split, build_left, nleft,
+  hipLaunchKernelGGL(k_gd_children, dim3(1), dim3(1024), 0, s, S, seg, split, build_left, lcur,
                      fg, G, chunk, seg_next, alive_next, dseg, sp, par,
                      reinterpret_cast<HistTask*>(tasks), ntask, reinterpret_cast<HistReduce*>(red));
   return true;

@@ -483,7 +483,12 @@ void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const flo
                const float* qscale, const int32_t* tasks, int ntask, const int32_t* red, int nred,
                int max_fcnt, bool dword_rows, int64_t* part, double* hist, hipStream_t s,
                const int32_t* dseg = nullptr, int chunk = 0,
-               const int32_t* ntask_dev = nullptr, bool w32 = false);
+               const int32_t* ntask_dev = nullptr, bool w32 = false,
+               const double* sib_hf = nullptr, const int32_t* sib_sp = nullptr,
+               const int32_t* sib_par = nullptr);
+// sib_hf (optional): the reduce also does gbdt_sibling's work -- hist is then
+// the NEXT level's [2 x slots] histograms (built child from the sums, the
+// other one as parent sib_hf[sib_par[k]] - built; sib_sp as gbdt_sibling's sp)
 // w32: qscale holds {2^eg, 2^eh, R} and the blocks sum <= R rows at a time in
 // int32 (see k_hist)
 // ntask_dev (optional): the task count of a device-built list (ntask is then
@@ -495,8 +500,10 @@ void gbdt_dev_apply(int S, int node0, bool last, const double* so, const double*
                     double lambda, double mcw, double rt_eps, double* nodes, int32_t* pfeat,
                     int32_t* pbin, uint8_t* pdefl, int32_t* lcur, int32_t* rcur, uint8_t* split,
                     uint8_t* build_left, double* tot_next, int32_t* nleft, hipStream_t s);
+// lcur: the split slots' left cursors after the partition (their left
+// children end there; = the segment begin when no partition ran)
 bool gbdt_dev_children(int S, const int32_t* seg, const uint8_t* split, const uint8_t* build_left,
-                       const int32_t* nleft, const int32_t* fg, int G, int chunk,
+                       const int32_t* lcur, const int32_t* fg, int G, int chunk,
                        int32_t* seg_next, uint8_t* alive_next, int32_t* dseg, int32_t* sp,
                        int32_t* par, int32_t* tasks, int32_t* ntask, int32_t* red,
                        hipStream_t s);
@@ -506,14 +513,15 @@ bool gbdt_dev_children(int S, const int32_t* seg, const uint8_t* split, const ui
 void gbdt_child_segs(const int32_t* sp, int nsplit, const int32_t* nleft, int32_t* dseg,
                      hipStream_t s);
 // one-pass (order-free) partition by per-node cursors: lcur = seg_beg, rcur =
-// seg_end of the split nodes on entry; nleft [nnode] out. false: too many
-// segments for the LDS table (use goleft + scan + scatter)
+// seg_end of the split nodes on entry; nleft [nnode] out (optional). tb:
+// segment begins, tbs ints apart. false: too many segments for the LDS table
+// (use goleft + scan + scatter)
 bool gbdt_partition_cursor(const uint8_t* B, const uint8_t* Bc, int64_t nrows, int f,
-                           const int32_t* ridx, int64_t n, const int32_t* tb, const int32_t* tn,
-                           int nt, const int32_t* node_feat, const int32_t* node_bin,
-                           const uint8_t* node_defl, int32_t* lcur, int32_t* rcur,
-                           const int32_t* seg_beg, int nnode, int32_t* nleft, int32_t* out,
-                           hipStream_t s);
+                           const int32_t* ridx, int64_t n, const int32_t* tb, int tbs,
+                           const int32_t* tn, int nt, const int32_t* node_feat,
+                           const int32_t* node_bin, const uint8_t* node_defl, int32_t* lcur,
+                           int32_t* rcur, const int32_t* seg_beg, int nnode, int32_t* nleft,
+                           int32_t* out, hipStream_t s);
 void gbdt_sibling(const double* hf, const double* hs, const int32_t* sp, const int32_t* par,
                   int nsplit, int64_t per, double* out, hipStream_t s);
 // position -> node id over sorted segments tiling [0, n)
