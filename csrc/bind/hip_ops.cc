@@ -2849,13 +2849,79 @@ py::tuple gbdt_grow(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, cons
 // GPU per depth-8 tree of 11M rows). Every max_depth level is enqueued; the
 // levels below a tree's last split find no live node and do no row work but
 // the partition's pass.
+// A device grower's heap node table (host copy, float64 [2^(D+1) - 1, REC])
+// -> the tree lists, renumbered breadth-first: (feat, bin, cond, defl, left,
+// right, parent, gain, cover, base weight, leaf, [(leaf id, begin, end)])
+py::tuple gbdt_tree_from_nodes(const Tensor& hn, const std::vector<float>& cut_vals,
+                               const std::vector<int64_t>& cut_off) {
+  const int REC = wh::gbdt_node_rec();
+  TORCH_CHECK(!hn.is_cuda() && hn.scalar_type() == torch::kFloat64 && hn.is_contiguous() &&
+                  hn.dim() == 2 && hn.size(1) == REC,
+              "gbdt_tree_from_nodes: a host float64 node table");
+  const int NN = (int)hn.size(0);
+  const double* r = hn.data_ptr<double>();
+  std::vector<int> id_of(NN, -1), order;
+  for (int h = 0; h < NN; ++h)
+    if (r[(int64_t)h * REC] != 0.0) {
+      id_of[h] = (int)order.size();
+      order.push_back(h);
+    }
+  const size_t M = order.size();
+  std::vector<int> feat(M), bin(M), defl(M), left(M, -1), right(M, -1), parent(M, -1);
+  std::vector<double> gain(M), cover(M), bw(M), leaf(M);
+  std::vector<float> cond(M, 0.f);
+  py::list segs;
+  for (size_t i = 0; i < M; ++i) {
+    const int h = order[i];
+    const double* q = r + (int64_t)h * REC;
+    feat[i] = (int)q[1], bin[i] = (int)q[2], defl[i] = (int)q[3];
+    gain[i] = q[4], cover[i] = q[5], bw[i] = q[6], leaf[i] = q[7];
+    if (feat[i] >= 0) {
+      TORCH_CHECK(2 * h + 2 < NN, "gbdt_tree_from_nodes: a split at the last depth");
+      left[i] = id_of[2 * h + 1], right[i] = id_of[2 * h + 2];
+      TORCH_CHECK(left[i] >= 0 && right[i] >= 0, "gbdt_tree_from_nodes: a split node lost a child");
+      parent[left[i]] = (int)i, parent[right[i]] = (int)i;
+      cond[i] = cut_vals[cut_off[feat[i]] + bin[i]];
+    } else {
+      segs.append(py::make_tuple((int)i, (int)q[8], (int)q[9]));
+    }
+  }
+  return py::make_tuple(feat, bin, cond, defl, left, right, parent, gain, cover, bw, leaf, segs);
+}
+
+// margin += the leaf value each row reaches in a device grower's heap node
+// table (device float64 [NN, REC]): the table becomes the walk's compact
+// arrays on the device (one small kernel), then the usual row walk
+void gbdt_walk_heap(const Tensor& B, const Tensor& nodes, const Tensor& margin, bool lds) {
+  CHECK_IN(B, torch::kUInt8);
+  CHECK_IN(nodes, torch::kFloat64);
+  CHECK_IN(margin, torch::kFloat32);
+  const int REC = wh::gbdt_node_rec();
+  TORCH_CHECK(nodes.dim() == 2 && nodes.size(1) == REC && nodes.size(0) > 0 &&
+                  nodes.size(0) <= 65535,
+              "gbdt_walk_heap: a heap node table");
+  TORCH_CHECK(B.dim() == 2 && margin.numel() == B.size(0), "gbdt_walk_heap: B must be [n, f]");
+  c10::DeviceGuard g(B.device());
+  const int64_t NN = nodes.size(0);
+  auto buf = torch::empty({6 * NN}, B.options().dtype(torch::kInt32));
+  int32_t* b = ptr<int32_t>(buf);
+  int32_t *feat = b, *bin = b + NN, *left = b + 2 * NN, *right = b + 3 * NN;
+  float* leaf = reinterpret_cast<float*>(b + 4 * NN);
+  uint8_t* defl = reinterpret_cast<uint8_t*>(b + 5 * NN);
+  auto s = cur_stream(B);
+  wh::gbdt_heap_tree(ptr<double>(nodes), (int)NN, feat, bin, defl, left, right, leaf, s);
+  wh::gbdt_leaf_walk(ptr<uint8_t>(B), B.size(0), (int)B.size(1), (int)NN, feat, bin, defl, left,
+                     right, leaf, ptr<float>(margin), s, lds);
+}
+
 py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, const Tensor& gpair,
                         const Tensor& qscale, const Tensor& valid, int64_t nbin,
                         std::vector<std::pair<int64_t, int64_t>> fgroups, int64_t max_fcnt,
                         const Tensor& root_tot, std::vector<float> cut_vals,
                         std::vector<int64_t> cut_off, double eta, double alpha, double lambda,
                         double mcw, int64_t max_depth, double rt_eps, py::object allreduce,
-                        py::object reduce_scatter, py::object pick, int64_t f_lo, bool walk) {
+                        py::object reduce_scatter, py::object pick, int64_t f_lo, bool walk,
+                        bool defer) {
   // Multi-rank: either every level's built histograms are allreduced (all
   // features on every rank), or -- reduce_scatter / pick given
   // (models/gbdt.py HistExchange) -- each rank receives the global sums of
@@ -3055,35 +3121,13 @@ py::tuple gbdt_grow_dev(const Tensor& B, const Tensor& Bc, const Tensor& ridx0, 
     alive_cur = alive_next;
   }
   // the finished tree: ONE host read, renumbered breadth-first (the host
-  // grower's creation order)
-  auto hn = nodes.cpu();
-  const double* r = hn.data_ptr<double>();
-  std::vector<int> id_of(NN, -1), order;
-  for (int h = 0; h < NN; ++h)
-    if (r[(int64_t)h * REC] != 0.0) {
-      id_of[h] = (int)order.size();
-      order.push_back(h);
-    }
-  const size_t M = order.size();
-  std::vector<int> feat(M), bin(M), defl(M), left(M, -1), right(M, -1), parent(M, -1);
-  std::vector<double> gain(M), cover(M), bw(M), leaf(M);
-  std::vector<float> cond(M, 0.f);
-  py::list segs;
-  for (size_t i = 0; i < M; ++i) {
-    const int h = order[i];
-    const double* q = r + (int64_t)h * REC;
-    feat[i] = (int)q[1], bin[i] = (int)q[2], defl[i] = (int)q[3];
-    gain[i] = q[4], cover[i] = q[5], bw[i] = q[6], leaf[i] = q[7];
-    if (feat[i] >= 0) {
-      left[i] = id_of[2 * h + 1], right[i] = id_of[2 * h + 2];
-      TORCH_CHECK(left[i] >= 0 && right[i] >= 0, "gbdt_grow_dev: a split node lost a child");
-      parent[left[i]] = (int)i, parent[right[i]] = (int)i;
-      cond[i] = cut_vals[cut_off[feat[i]] + bin[i]];
-    } else {
-      segs.append(py::make_tuple((int)i, (int)q[8], (int)q[9]));
-    }
-  }
-  return py::make_tuple(feat, bin, cond, defl, left, right, parent, gain, cover, bw, leaf, segs,
+  // grower's creation order) -- or, defer: the device node table itself, for
+  // a heap walk on the device (gbdt_walk_heap) and a host read one tree later
+  // (gbdt_tree_from_nodes), so the host's tree bookkeeping overlaps the next
+  // tree instead of idling the GPU between trees
+  if (defer) return py::make_tuple(nodes, ridx);
+  py::tuple t = gbdt_tree_from_nodes(nodes.cpu(), cut_vals, cut_off);
+  return py::make_tuple(t[0], t[1], t[2], t[3], t[4], t[5], t[6], t[7], t[8], t[9], t[10], t[11],
                         ridx);
 }
 
@@ -3632,7 +3676,10 @@ PYBIND11_MODULE(_hip, m) {
         py::arg("root_tot"), py::arg("cut_vals"), py::arg("cut_off"), py::arg("eta"), py::arg("alpha"),
         py::arg("reg_lambda"), py::arg("min_child_weight"), py::arg("max_depth"), py::arg("rt_eps"),
         py::arg("allreduce"), py::arg("reduce_scatter") = py::none(), py::arg("pick") = py::none(),
-        py::arg("f_lo") = 0, py::arg("walk") = false);
+        py::arg("f_lo") = 0, py::arg("walk") = false, py::arg("defer") = false);
+  m.def("gbdt_tree_from_nodes", &gbdt_tree_from_nodes);
+  m.def("gbdt_walk_heap", &gbdt_walk_heap, py::arg("B"), py::arg("nodes"), py::arg("margin"),
+        py::arg("lds") = true);
   m.def("gbdt_gpair", &gbdt_gpair);
   m.def("gbdt_qscale", &gbdt_qscale);
   // the ingest ops block on one small device read each: the GIL is released

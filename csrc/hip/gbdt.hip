@@ -936,6 +936,30 @@ namespace {
 // defl, gain, cover, base weight, leaf, begin, end}.
 constexpr int kNodeRec = 10;
 
+// heap node records -> the row walk's arrays: node h splits on feat / bin
+// (children 2h + 1, 2h + 2) when alive and split, else is a leaf of value
+// rec[7] (dead nodes are never reached)
+__global__ __launch_bounds__(256) void k_heap_tree(const double* __restrict__ nodes, int nn,
+                                                   int32_t* __restrict__ feat,
+                                                   int32_t* __restrict__ bin,
+                                                   uint8_t* __restrict__ defl,
+                                                   int32_t* __restrict__ left,
+                                                   int32_t* __restrict__ right,
+                                                   float* __restrict__ leaf) {
+  for (int h = blockIdx.x * blockDim.x + threadIdx.x; h < nn; h += gridDim.x * blockDim.x) {
+    const double* q = nodes + (int64_t)h * kNodeRec;
+    const bool split = q[0] != 0.0 && q[1] >= 0.0 && 2 * h + 2 < nn;
+    feat[h] = split ? (int32_t)q[1] : -1;
+    bin[h] = split ? (int32_t)q[2] : 0;
+    defl[h] = split ? (uint8_t)q[3] : 0;
+    left[h] = split ? 2 * h + 1 : -1;
+    right[h] = split ? 2 * h + 2 : -1;
+    leaf[h] = (float)q[7];
+  }
+}
+
+
+
 // One block: for slot s of depth d (S slots), decide its split from the
 // split search's result, record the node, and set up the partition and the
 // next level's totals (the host grower's level bookkeeping).
@@ -1077,6 +1101,13 @@ __global__ __launch_bounds__(1024) void k_gd_children(
 }
 
 }  // namespace
+
+void gbdt_heap_tree(const double* nodes, int nn, int32_t* feat, int32_t* bin, uint8_t* defl,
+                    int32_t* left, int32_t* right, float* leaf, hipStream_t s) {
+  if (nn <= 0) return;
+  hipLaunchKernelGGL(k_heap_tree, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, s, nodes, nn,
+                     feat, bin, defl, left, right, leaf);
+}
 
 int gbdt_node_rec() { return kNodeRec; }
 

@@ -495,6 +495,9 @@ void gbdt_hist(const uint8_t* B, int f, int nbin, const int32_t* ridx, const flo
 // its upper bound; the reduce entries carry exact task counts)
 // ---- the level loop on the device (gbdt_grow_dev in csrc/bind/hip_ops.cc)
 int gbdt_node_rec();
+// heap node records [nn x gbdt_node_rec()] -> the leaf walk's tree arrays
+void gbdt_heap_tree(const double* nodes, int nn, int32_t* feat, int32_t* bin, uint8_t* defl,
+                    int32_t* left, int32_t* right, float* leaf, hipStream_t s);
 void gbdt_dev_apply(int S, int node0, bool last, const double* so, const double* tot,
                     const int32_t* seg, const uint8_t* alive, double eta, double alpha,
                     double lambda, double mcw, double rt_eps, double* nodes, int32_t* pfeat,

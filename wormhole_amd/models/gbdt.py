@@ -36,6 +36,7 @@ _HIST32_ROWS = 8192  # rows per int32 LDS pass of the GPU histogram
 # same on every rank):
 HIST32 = True  # int32 LDS histogram passes (False: int64 sums throughout)
 LEAF_WALK_LDS = True  # the LDS-resident tree walk when it fits (False: global walk)
+DEFER_TREES = True  # device trees: host lists one tree later (False: read every tree at once)
 HOST_GROWER = False  # the per-level host grower instead of the device level loop
 
 
@@ -554,6 +555,48 @@ class RegTree:
         return "\n".join(out) + "\n"
 
 
+
+class _DeviceTree(RegTree):
+    """A tree grown by the device level loop whose host lists are built on
+    first use (models/gbdt.py TreeBuilder._build_native, defer): the node
+    table is copied to pinned host memory right away, behind the tree's
+    kernels, and renumbered breadth-first (``gbdt_tree_from_nodes``) when an
+    attribute is first read -- by the builder one tree later, or by whoever
+    reads the model first. Until then it holds no lists."""
+
+    def __init__(self, nodes, cut_lists):  # noqa: D401 (no RegTree lists yet)
+        host = torch.empty(nodes.shape, dtype=nodes.dtype, pin_memory=True)
+        host.copy_(nodes, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.__dict__["_pend"] = (host, ev, cut_lists, nodes)
+
+    def materialize(self):
+        pend = self.__dict__.pop("_pend", None)
+        if pend is None:
+            return self
+        host, ev, (cut_vals, cut_off), _ = pend
+        ev.synchronize()
+        RegTree.__init__(self)
+        (feat, bin_, cond, defl, left, right, parent, gain, cover, bw, leaf,
+         _segs) = _native.hip().gbdt_tree_from_nodes(host, cut_vals, cut_off)
+        self.feat, self.bin, self.cond, self.defl = list(feat), list(bin_), list(cond), list(defl)
+        self.left, self.right, self.parent = list(left), list(right), list(parent)
+        self.gain, self.cover, self.base_weight = list(gain), list(cover), list(bw)
+        self.leaf = list(leaf)
+        TreeBuilder._compact(self)
+        return self
+
+    def __getattr__(self, name):  # only for attributes not set yet
+        if name.startswith("__") or "_pend" not in self.__dict__:
+            raise AttributeError(name)
+        self.materialize()
+        return object.__getattribute__(self, name)
+
+    def __getstate__(self):
+        self.materialize()
+        return self.__dict__
+
 def _fmt(x):
     return "%g" % x
 
@@ -863,6 +906,11 @@ class TreeBuilder:
                   cut_off=self._cut_lists[1], eta=float(p.eta), alpha=float(p.alpha),
                   reg_lambda=float(p.reg_lambda), min_child_weight=float(p.min_child_weight),
                   max_depth=int(p.max_depth), rt_eps=RT_EPS, allreduce=ar)
+        # deferred: the tree stays a device node table, the margins are
+        # walked from it on the device, and its host lists are built one tree
+        # later (no GPU idle between trees); needs the row walk and no
+        # pruning (gamma <= 0: every accepted split has gain > RT_EPS)
+        defer = not host and self._walks(n) and p.gamma <= 0 and DEFER_TREES
         if host:  # (the per-level host grower allreduces whole histograms)
             out = _native.hip().gbdt_grow(root_tot=tot.cpu().tolist(), **kw)
         else:  # root totals as a device tensor: no host wait
@@ -871,7 +919,15 @@ class TreeBuilder:
                 root_tot=tot.contiguous(), **kw,
                 reduce_scatter=x.reduce_scatter if x is not None else None,
                 pick=x.pick if x is not None else None, f_lo=x.lo if x is not None else 0,
-                walk=self._walks(n))
+                walk=self._walks(n), defer=defer)
+        if defer:
+            nodes = out[0]
+            _native.hip().gbdt_walk_heap(self.B, nodes, margin, lds=LEAF_WALK_LDS)
+            tree = _DeviceTree(nodes, self._cut_lists)
+            prev, self._pending = getattr(self, "_pending", None), tree
+            if prev is not None:
+                prev.materialize()  # (its copy finished during this tree's levels)
+            return tree
         (feat, bin_, cond, defl, left, right, parent, gain, cover, bw, leaf, segs, ridx) = out
         tree = RegTree()
         tree.feat, tree.bin, tree.cond, tree.defl = list(feat), list(bin_), list(cond), list(defl)
