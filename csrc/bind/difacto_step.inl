@@ -183,7 +183,7 @@ class DifactoStep {
   // 2 / 3 of the store (0 / 1 belong to the Python guard).
   void guard_read() {
     if (!gpend_) return;
-    WH_HIP_CHECK_HOST(hipEventSynchronize(gev_[gk_]));
+    wait_event(gev_[gk_]);
     gpend_ = false;
     auto h = store_->summary_read(2 + gk_);
     gkeys_ = h[0];

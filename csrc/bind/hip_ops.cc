@@ -57,6 +57,25 @@ T* ptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
                 __FILE__, ":", __LINE__);                                       \
   } while (0)
 
+// The host's wait for a step's one device read (the localize counts, the
+// store guard's summary): polled for up to 2 ms before a blocking wait. The
+// step's next launches go out the moment the read lands instead of after a
+// sleeping wait's wake-up (A/B on one box: headline 142.8-143.4 vs
+// 140.9-143.5 M, loopback 8 123.8 / 125.7 vs 123.2 / 125.1 M; within noise
+// elsewhere: profiles/round6_small_minibatch_host.txt).
+inline void wait_event(hipEvent_t e) {
+#if !defined(WH_BLOCKING_WAIT)
+  const auto t0 = std::chrono::steady_clock::now();
+  while (true) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) return;
+    WH_HIP_CHECK_HOST(r == hipErrorNotReady ? hipSuccess : r);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+  }
+#endif
+  WH_HIP_CHECK_HOST(hipEventSynchronize(e));
+}
+
 template <typename T>
 const T* optptr(const c10::optional<Tensor>& t) {
   return (t.has_value() && t->defined() && t->numel() > 0) ? reinterpret_cast<const T*>(t->data_ptr())
@@ -330,7 +349,7 @@ class LocalizeJob {
     c10::DeviceGuard g(keys_.device());
     DevWs& ws = dev_ws(keys_.device());
     while (true) {
-      WH_HIP_CHECK_HOST(hipEventSynchronize(rd_->ev));
+      wait_event(rd_->ev);
       const int64_t* h = rd_->host;
       const bool own = h[nshard_] != 0;
       bool over = own;

@@ -1188,7 +1188,7 @@ class PsxStep {
   void guard_read() {
     if (!gpend_) return;
     mark("store summary read (host wait)", -1);
-    WH_HIP_CHECK_HOST(hipEventSynchronize(gev_[gk_]));
+    wait_event(gev_[gk_]);
     gpend_ = false;
     auto h = store_->summary_read(2 + gk_);
     gkeys_ = h[0];
