@@ -334,11 +334,26 @@ bool InputSplit::NextRecord(std::string* out) {
 }
 
 // --------------------------------------------------------------- recordio
+namespace {
+// a FILE* whose writes stream into a RemoteWriter (its parts upload as they fill)
+ssize_t remote_cookie_write(void* c, const char* buf, size_t n) {
+  try {
+    static_cast<RemoteWriter*>(c)->Write(buf, n);
+    return (ssize_t)n;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "remote write: %s\n", e.what());
+    return -1;
+  }
+}
+}  // namespace
+
 RecordIOWriter::RecordIOWriter(const std::string& path_in) {
-  if (IsRemote(path_in)) {  // buffered, uploaded whole at Close()
-    remote_ = path_in;
-    fp_ = open_memstream(&mem_, &mem_len_);
-    if (!fp_) throw std::runtime_error("cannot buffer " + path_in);
+  if (IsRemote(path_in)) {
+    remote_ = std::make_unique<RemoteWriter>(path_in);
+    cookie_io_functions_t io{};
+    io.write = remote_cookie_write;
+    fp_ = fopencookie(remote_.get(), "w", io);
+    if (!fp_) throw std::runtime_error("cannot stream to " + path_in);
     return;
   }
   const std::string path = ResolvePath(path_in);
@@ -352,13 +367,12 @@ RecordIOWriter::~RecordIOWriter() {
   }
 }
 void RecordIOWriter::Close() {
-  if (fp_) std::fclose(fp_);
+  const bool failed = fp_ && std::fclose(fp_) != 0;
   fp_ = nullptr;
-  if (mem_) {
-    const std::string data(mem_, mem_len_);
-    std::free(mem_);
-    mem_ = nullptr;
-    RemoteWrite(remote_, data);
+  if (remote_) {
+    std::unique_ptr<RemoteWriter> w = std::move(remote_);
+    if (failed) throw std::runtime_error("remote RecordIO write failed");
+    w->Close();
   }
 }
 

@@ -73,9 +73,8 @@ class RecordIOWriter {
  private:
   std::FILE* fp_ = nullptr;
   size_t bytes_ = 0;
-  std::string remote_;  // a remote target: records buffered in mem_
-  char* mem_ = nullptr;
-  size_t mem_len_ = 0;
+  // a remote target: the FILE streams into it (fopencookie), one part at a time
+  std::unique_ptr<class RemoteWriter> remote_;
 };
 
 }  // namespace host

@@ -714,6 +714,26 @@ void register_all(py::module& m) {
     py::gil_scoped_release nogil;
     RemoteWrite(uri, data);
   });
+  // streaming remote writes (S3 multipart / WebHDFS append), one part held;
+  // dropped unclosed, its destructor aborts the upload over the network:
+  // without the GIL (a Python thread -- a test's in-process server -- may be
+  // the one that has to answer)
+  struct NoGilDelete {
+    void operator()(RemoteWriter* w) const {
+      py::gil_scoped_release nogil;
+      delete w;
+    }
+  };
+  py::class_<RemoteWriter, std::unique_ptr<RemoteWriter, NoGilDelete>>(m, "RemoteWriter")
+      .def(py::init<const std::string&, int64_t>(), py::arg("uri"), py::arg("part_bytes") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("write", [](RemoteWriter& w, py::bytes b) {
+        std::string d = b;
+        py::gil_scoped_release nogil;
+        w.Write(d.data(), d.size());
+      })
+      .def("close", &RemoteWriter::Close, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("parts", &RemoteWriter::parts);
   m.def("sigv4_authorization", &SigV4Authorization, py::arg("method"), py::arg("host"),
         py::arg("path"), py::arg("query"), py::arg("amz_date"), py::arg("payload_sha256"),
         py::arg("region"), py::arg("key_id"), py::arg("secret"), py::arg("token") = "");

@@ -592,22 +592,101 @@ std::string RemoteRead(const std::string& uri, int64_t off, int64_t len) {
 }
 
 void RemoteWrite(const std::string& uri, const std::string& data) {
+  RemoteWriter w(uri);
+  w.Write(data.data(), data.size());
+  w.Close();
+}
+
+namespace {
+// WebHDFS CREATE (PUT) / APPEND (POST): the name node answers 307 with the
+// data node that takes the bytes
+void hdfs_put(const std::string& uri, const std::string& op, const std::string& data) {
   const Parsed p = parse_uri(uri);
-  if (is_hdfs(p.scheme)) {
-    // CREATE: the name node answers 307 with the data node to PUT to
-    Resp r = request("PUT", hdfs_url(p, "CREATE") + "&overwrite=true", {}, "", false);
-    std::string loc = r.header("location");
-    if (r.status == 307 && !loc.empty()) {
-      r = request("PUT", loc, {{"Content-Type", "application/octet-stream"}}, data);
-    } else if (r.status == 201 || r.status == 200) {
-      return;  // (a gateway that stored the empty file and wants no data is not expected)
-    }
-    if (r.status != 201 && r.status != 200) http_fail("write", uri, r);
-    return;
+  const bool create = op == "CREATE";
+  const std::string method = create ? "PUT" : "POST";
+  Resp r = request(method, hdfs_url(p, op) + (create ? "&overwrite=true" : ""), {}, "", false);
+  const std::string loc = r.header("location");
+  if (r.status == 307 && !loc.empty())
+    r = request(method, loc, {{"Content-Type", "application/octet-stream"}}, data);
+  if (r.status != 201 && r.status != 200) http_fail(create ? "write" : "append", uri, r);
+}
+}  // namespace
+
+RemoteWriter::RemoteWriter(const std::string& uri, int64_t part_bytes)
+    : uri_(uri), part_(part_bytes > 0 ? part_bytes : (int64_t)64 << 20) {
+  const Parsed p = parse_uri(uri);
+  hdfs_ = is_hdfs(p.scheme);
+  if (!hdfs_ && !is_s3(p.scheme)) throw std::runtime_error("not a remote URI: " + uri);
+}
+
+RemoteWriter::~RemoteWriter() {
+  if (closed_ || hdfs_ || upload_id_.empty()) return;
+  try {  // dropped unclosed: do not leave the parts billed in the bucket
+    const S3Target t = s3_of(parse_uri(uri_));
+    s3_request("DELETE", t, t.key, {{"uploadId", upload_id_}}, {}, "");
+  } catch (...) {
   }
-  const S3Target t = s3_of(p);
-  Resp r = s3_request("PUT", t, t.key, {}, {{"Content-Type", "application/octet-stream"}}, data);
-  if (r.status != 200 && r.status != 201) http_fail("write", uri, r);
+}
+
+void RemoteWriter::Write(const char* p, size_t n) {
+  if (closed_) throw std::runtime_error("write after close: " + uri_);
+  buf_.append(p, n);
+  while ((int64_t)buf_.size() >= part_) Part(false);
+}
+
+// uploads the first min(part, buffered) bytes (all of them when last)
+void RemoteWriter::Part(bool last) {
+  const size_t n = last ? buf_.size() : (size_t)std::min<int64_t>(part_, (int64_t)buf_.size());
+  const std::string data = buf_.substr(0, n);
+  if (hdfs_) {
+    if (!created_) hdfs_put(uri_, "CREATE", data);
+    else if (!data.empty()) hdfs_put(uri_, "APPEND", data);
+    created_ = true;
+  } else {
+    const S3Target t = s3_of(parse_uri(uri_));
+    if (upload_id_.empty()) {
+      if (last) {  // the whole object fits one part: a plain PUT
+        Resp r = s3_request("PUT", t, t.key, {}, {{"Content-Type", "application/octet-stream"}}, data);
+        if (r.status != 200 && r.status != 201) http_fail("write", uri_, r);
+        buf_.clear();
+        ++nparts_;
+        return;
+      }
+      Resp r = s3_request("POST", t, t.key, {{"uploads", ""}},
+                          {{"Content-Type", "application/octet-stream"}}, "");
+      if (r.status != 200) http_fail("create multipart upload", uri_, r);
+      upload_id_ = xml_tag(r.body, "UploadId", 0, r.body.size());
+      if (upload_id_.empty()) http_fail("create multipart upload (no UploadId)", uri_, r);
+    }
+    if (!data.empty() || etags_.empty()) {
+      const std::string num = std::to_string(etags_.size() + 1);
+      Resp r = s3_request("PUT", t, t.key, {{"partNumber", num}, {"uploadId", upload_id_}}, {}, data);
+      if (r.status != 200) http_fail("upload part " + num, uri_, r);
+      const std::string etag = r.header("etag");
+      if (etag.empty()) http_fail("upload part " + num + " (no ETag)", uri_, r);
+      etags_.push_back(etag);
+    }
+    if (last) {
+      std::string x = "<CompleteMultipartUpload>";
+      for (size_t i = 0; i < etags_.size(); ++i)
+        x += "<Part><PartNumber>" + std::to_string(i + 1) + "</PartNumber><ETag>" + etags_[i] +
+             "</ETag></Part>";
+      x += "</CompleteMultipartUpload>";
+      Resp r = s3_request("POST", t, t.key, {{"uploadId", upload_id_}},
+                          {{"Content-Type", "application/xml"}}, x);
+      // (S3 can answer 200 and still report an error in the body)
+      if (r.status != 200 || r.body.find("<Error>") != std::string::npos)
+        http_fail("complete multipart upload", uri_, r);
+    }
+  }
+  ++nparts_;
+  buf_.erase(0, n);
+}
+
+void RemoteWriter::Close() {
+  if (closed_) return;
+  Part(true);
+  closed_ = true;
 }
 
 RemoteReader::RemoteReader(const std::string& uri, int64_t window) : uri_(uri), win_(window) {

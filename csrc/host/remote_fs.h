@@ -41,8 +41,31 @@ std::vector<RemoteEntry> RemoteList(const std::string& dir_uri);
 int64_t RemoteSize(const std::string& uri);
 // Bytes [off, off + len) (fewer at the end of the object).
 std::string RemoteRead(const std::string& uri, int64_t off, int64_t len);
-// Create / overwrite the object with `data`.
+// Create / overwrite the object with `data` (a RemoteWriter).
 void RemoteWrite(const std::string& uri, const std::string& data);
+
+// Streaming writes of one remote object, memory bounded by one part: S3
+// multipart upload (CreateMultipartUpload / UploadPart / Complete, aborted
+// if the writer is dropped unclosed; an object smaller than one part is a
+// single PUT), WebHDFS CREATE with the first part then APPEND per part.
+// part_bytes: 0 = 64 MiB (S3 wants parts of >= 5 MiB but the last).
+class RemoteWriter {
+ public:
+  explicit RemoteWriter(const std::string& uri, int64_t part_bytes = 0);
+  ~RemoteWriter();
+  RemoteWriter(const RemoteWriter&) = delete;
+  RemoteWriter& operator=(const RemoteWriter&) = delete;
+  void Write(const char* p, size_t n);
+  void Close();  // uploads what is left and finishes the object
+  int64_t parts() const { return nparts_; }
+
+ private:
+  void Part(bool last);
+  std::string uri_, buf_, upload_id_;
+  std::vector<std::string> etags_;
+  int64_t part_ = 0, nparts_ = 0;
+  bool hdfs_ = false, created_ = false, closed_ = false;
+};
 
 // Sequential reads of one remote object through a read-ahead window.
 class RemoteReader {

@@ -8,14 +8,17 @@ the native remote file systems (csrc/host/remote_fs.cc) are tested against.
     srv.stop()
 
 With certfile / keyfile the endpoint is HTTPS (tests point SSL_CERT_FILE at
-the certificate). WebHDFS: /webhdfs/v1/<path>?op=LISTSTATUS|GETFILESTATUS|OPEN|CREATE (OPEN and
-CREATE answer 307 to /datanode/<path>, like a name node). S3: path-style
-/<bucket>/<key> under <root>/<bucket>; listings paginate 2 keys at a time.
+the certificate). WebHDFS: /webhdfs/v1/<path>?op=LISTSTATUS|GETFILESTATUS|OPEN|CREATE|APPEND
+(OPEN, CREATE and APPEND answer 307 to /datanode/<path>, like a name node).
+S3: path-style /<bucket>/<key> under <root>/<bucket>; listings paginate 2 keys
+at a time; multipart uploads (create, upload part with ETags, complete with
+the part list checked, abort).
 """
 import hashlib
 import hmac
 import json
 import os
+import re
 import ssl
 import threading
 import urllib.parse
@@ -86,7 +89,7 @@ class _Handler(BaseHTTPRequestHandler):
             return self._datanode(path[len("/datanode"):], q)
         return self._s3(u, path, q)
 
-    do_GET = do_PUT = do_HEAD = lambda self: self._route()
+    do_GET = do_PUT = do_HEAD = do_POST = do_DELETE = lambda self: self._route()
 
     # ------------------------------------------------------------ WebHDFS
     def _webhdfs(self, path, q):
@@ -112,7 +115,7 @@ class _Handler(BaseHTTPRequestHandler):
                     ent.append({"pathSuffix": n, "type": "DIRECTORY" if os.path.isdir(f) else "FILE",
                                 "length": 0 if os.path.isdir(f) else os.path.getsize(f)})
             return self._send(200, json.dumps({"FileStatuses": {"FileStatus": ent}}).encode())
-        if op in ("OPEN", "CREATE"):
+        if op in ("OPEN", "CREATE", "APPEND"):
             loc = "%s/datanode%s?%s" % (self.server.base_url, _enc(path, "/"),
                                         urllib.parse.urlencode(q))
             return self._send(307, b"", {"Location": loc})
@@ -120,6 +123,12 @@ class _Handler(BaseHTTPRequestHandler):
 
     def _datanode(self, path, q):
         local = self._local(path)
+        if self.command == "POST" and q.get("op") == "APPEND":
+            if not os.path.isfile(local):
+                return self._send(404)
+            with open(local, "ab") as f:
+                f.write(self._body())
+            return self._send(200)
         if self.command == "PUT":
             os.makedirs(os.path.dirname(local), exist_ok=True)
             with open(local, "wb") as f:
@@ -144,7 +153,7 @@ class _Handler(BaseHTTPRequestHandler):
                      self.headers.get("x-amz-content-sha256", ""), self.server.region,
                      self.server.access_key, self.server.secret_key)
         body_ok = True
-        if self.command == "PUT":
+        if self.command in ("PUT", "POST"):
             body_ok = hashlib.sha256(self._peek_body()).hexdigest() == \
                 self.headers.get("x-amz-content-sha256")
         return hmac.compare_digest(auth, want) and body_ok
@@ -184,6 +193,40 @@ class _Handler(BaseHTTPRequestHandler):
             xml += "</ListBucketResult>"
             return self._send(200, xml.encode(), {"Content-Type": "application/xml"})
         local = os.path.join(broot, key)
+        ups = self.server.uploads
+        if self.command == "POST" and "uploads" in q:  # CreateMultipartUpload
+            uid = "up%d" % len(self.server.upload_ids)
+            self.server.upload_ids.append(uid)
+            ups[uid] = (key, {})
+            return self._send(200, ("<InitiateMultipartUploadResult><UploadId>%s</UploadId>"
+                                    "</InitiateMultipartUploadResult>" % uid).encode())
+        if "uploadId" in q:
+            uid = q["uploadId"]
+            if uid not in ups or ups[uid][0] != key:
+                return self._send(404, b"<Error><Code>NoSuchUpload</Code></Error>")
+            parts = ups[uid][1]
+            if self.command == "PUT":  # UploadPart
+                data = self._peek_body()
+                etag = '"%s"' % hashlib.md5(data).hexdigest()
+                parts[int(q["partNumber"])] = (etag, data)
+                return self._send(200, b"", {"ETag": etag})
+            if self.command == "DELETE":  # AbortMultipartUpload
+                del ups[uid]
+                self.server.aborted += 1
+                return self._send(204)
+            if self.command == "POST":  # CompleteMultipartUpload
+                body = self._peek_body().decode()
+                listed = re.findall(r"<Part><PartNumber>(\d+)</PartNumber><ETag>(.*?)</ETag></Part>", body)
+                nums = [int(n) for n, _ in listed]
+                if not listed or nums != sorted(nums) or any(parts.get(int(n), ("",))[0] != e
+                                                             for n, e in listed):
+                    return self._send(400, b"<Error><Code>InvalidPart</Code></Error>")
+                os.makedirs(os.path.dirname(local), exist_ok=True)
+                with open(local, "wb") as f:
+                    for n, _ in listed:
+                        f.write(parts[int(n)][1])
+                del ups[uid]
+                return self._send(200, b"<CompleteMultipartUploadResult></CompleteMultipartUploadResult>")
         if self.command == "PUT":
             os.makedirs(os.path.dirname(local), exist_ok=True)
             with open(local, "wb") as f:
@@ -227,6 +270,7 @@ class MockRemote:
         self.httpd.hdfs_user = hdfs_user
         self.httpd.log = []
         self.httpd.denied = 0
+        self.httpd.uploads, self.httpd.upload_ids, self.httpd.aborted = {}, [], 0
         self.port = self.httpd.server_address[1]
         self.url = "%s://%s:%d" % ("https" if certfile else "http", host, self.port)
         self.httpd.base_url = self.url
@@ -239,6 +283,14 @@ class MockRemote:
     @property
     def denied(self):
         return self.httpd.denied
+
+    @property
+    def aborted(self):
+        return self.httpd.aborted
+
+    @property
+    def open_uploads(self):
+        return len(self.httpd.uploads)
 
     def start(self):
         self.th.start()

@@ -7,6 +7,8 @@ request's Signature V4 with an implementation of its own):
 * SigV4 matches AWS's published example and the independent version;
 * listings (WebHDFS; S3 with pagination), MatchFile, sizes, ranged reads,
   whole-object writes, missing objects;
+* streaming writes: S3 multipart upload (aborted when dropped unclosed),
+  WebHDFS CREATE + APPEND, one part of memory;
 * InputSplit parts of text and RecordIO (CRB) files read remotely equal the
   local parts, byte for byte;
 * HTTPS endpoints: the server's certificate is verified (chain and name);
@@ -91,6 +93,52 @@ def test_listing_match_size_read_write(remote):
     assert srv.denied == 0
     # the S3 listing paginated (2 keys a page: 5 files + a sub-prefix)
     assert sum(1 for m, p, c in srv.log if "list-type=2" in p) >= 3 * 2
+
+
+@pytest.mark.parametrize("base", ["hdfs://127.0.0.1:8020/data", "s3://bkt/train"])
+def test_streaming_writer_parts(remote, base):
+    srv, root = remote
+    host = _native.host()
+    data = bytes((i * 131 + 7) % 256 for i in range(10_517))
+    w = host.RemoteWriter(base + "/big.bin", 1000)
+    at = 0
+    for n in (1, 999, 1000, 2500, 17, 6000):  # odd write sizes across part boundaries
+        w.write(data[at:at + n])
+        at += n
+    assert at == len(data)
+    w.close()
+    assert w.parts == 11  # 10 full parts + the 517-byte tail
+    assert host.remote_read(base + "/big.bin") == data
+    if base.startswith("s3"):
+        ops = [(m, p.split("?", 1)[1] if "?" in p else "") for m, p, c in srv.log if "big.bin" in p]
+        assert ops[0] == ("POST", "uploads="), ops
+        assert [m for m, q in ops if "uploadId=" in q and "partNumber=" not in q] == ["POST"], ops
+        assert sum(1 for m, q in ops if m == "PUT" and "partNumber=" in q) == 11
+        assert srv.open_uploads == 0
+    else:
+        ops = [p for m, p, c in srv.log if "big.bin" in p and "/webhdfs/" in p]
+        assert sum("op=CREATE" in p for p in ops) == 1 and sum("op=APPEND" in p for p in ops) == 10
+    # smaller than a part: one plain write
+    w = host.RemoteWriter(base + "/small.bin", 1000)
+    w.write(b"tiny")
+    w.close()
+    assert w.parts == 1 and host.remote_read(base + "/small.bin") == b"tiny"
+    if base.startswith("s3"):
+        assert not any("uploads" in p for m, p, c in srv.log if "small.bin" in p)
+        # a writer dropped unclosed aborts its upload: no object, no parts left
+        w = host.RemoteWriter(base + "/dropped.bin", 1000)
+        w.write(data[:3000])
+        del w
+        import gc
+        gc.collect()
+        assert srv.aborted == 1 and srv.open_uploads == 0
+        assert host.remote_size(base + "/dropped.bin") == -1
+    # the Python file object streams too (text, through the native writer)
+    with fs.open_uri(base + "/t.txt", "w") as f:
+        for i in range(3000):
+            f.write("line %d\n" % i)
+    assert fs.open_uri(base + "/t.txt").read() == "".join("line %d\n" % i for i in range(3000))
+    assert srv.denied == 0
 
 
 def test_wrong_credentials_are_refused(remote, monkeypatch):

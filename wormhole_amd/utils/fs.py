@@ -42,20 +42,32 @@ def _host():
     return _native.host()
 
 
-class _RemoteWriter(io.BytesIO):
-    """Buffers a file written to a remote URI and uploads it whole on close."""
+class _RemoteWriter(io.RawIOBase):
+    """A binary file streamed to a remote URI through the native
+    ``RemoteWriter`` (S3 multipart upload / WebHDFS append): memory is one
+    part, whatever the file's size. ``initial`` (append mode: the object's
+    current bytes) is written first."""
 
-    def __init__(self, uri, initial=b""):
-        super().__init__(initial)
-        self.seek(0, io.SEEK_END)
-        self._uri = uri
-        self._sent = False
+    def __init__(self, uri, initial=b"", part_bytes=0):
+        super().__init__()
+        self._w = _host().RemoteWriter(str(uri), part_bytes)
+        if initial:
+            self._w.write(bytes(initial))
+
+    def writable(self):
+        return True
+
+    def write(self, b):
+        b = bytes(b)
+        self._w.write(b)
+        return len(b)
 
     def close(self):
-        if not self._sent and not self.closed:
-            self._sent = True
-            _host().remote_write(self._uri, self.getvalue())
-        super().close()
+        if not self.closed:
+            try:
+                self._w.close()
+            finally:
+                super().close()
 
 
 def exists(path):
@@ -104,7 +116,7 @@ def open_uri(path, mode="r", **kw):
         text = "b" not in mode
         if any(c in mode for c in "wax"):
             init = _host().remote_read(uri) if ("a" in mode and exists(uri)) else b""
-            raw = _RemoteWriter(uri, init)
+            raw = io.BufferedWriter(_RemoteWriter(uri, init), 1 << 20)
         else:
             raw = io.BytesIO(_host().remote_read(uri))
         if text:
