@@ -189,12 +189,12 @@ def test_python_open_uri_exists_glob(remote):
         assert [u.rsplit("/", 1)[1] for u in fs.glob(base + "/model/m.*")] == ["m.bin", "m.txt"]
 
 
-def _job(work, conf, env_extra):
+def _job(work, conf, env_extra, args=()):
     env = dict(os.environ)
     env["WH_DEVICE"] = "cpu"
     env.update(env_extra)
     return subprocess.run([sys.executable, TRACKER, "-n", "1", "-s", "1",
-                           os.path.join(ROOT, "bin", "linear.dmlc"), conf],
+                           os.path.join(ROOT, "bin", "linear.dmlc"), conf] + list(args),
                           cwd=work, env=env, capture_output=True, text=True, timeout=300)
 
 
@@ -223,6 +223,22 @@ def test_linear_job_trains_from_and_saves_to_remote(remote, tmp_path):
         assert len(got) > 50 * 12
         assert got == ref, conf
         assert path.with_name(path.name + ".ok").exists()
+    # prediction from a remote model over remote data, written remotely: the
+    # same lines as the local prediction
+    pl = _job(work, "local.conf", dict(srv.env()), ["model_in=%s/model_local" % work,
+                                                    "val_data=%s/part-.*" % (root / "data"),
+                                                    "predict_out=%s/pl_" % work])
+    assert pl.returncode == 0, pl.stderr[-3000:]
+    ps = _job(work, "s3.conf", dict(srv.env()), ["model_in=s3://bkt/model/lin",
+                                                 "val_data=s3://bkt/train/part-.*",
+                                                 "predict_out=s3://bkt/pred/p_"])
+    assert ps.returncode == 0, ps.stderr[-3000:]
+    local_pred = sorted(p for p in work.iterdir() if p.name.startswith("pl_"))
+    remote_pred = sorted((root / "bkt" / "pred").iterdir())
+    assert len(local_pred) == len(remote_pred) > 0
+    for a, b in zip(local_pred, remote_pred):
+        assert a.name.replace("pl_", "p_") == b.name and a.read_text() == b.read_text()
+    assert sum(len(a.read_text().splitlines()) for a in local_pred) > 500
     assert srv.denied == 0
 
 

@@ -37,7 +37,7 @@ def save_linear(store, path):
 
 
 def load_linear(store, path):
-    raw = np.fromfile(path, dtype=[("k", "<u8"), ("w", "<f4")])
+    raw = np.frombuffer(open_uri(path, "rb").read(), dtype=[("k", "<u8"), ("w", "<f4")])
     keys = torch.from_numpy(raw["k"].view(np.int64).copy())
     w = torch.from_numpy(raw["w"].copy())
     _put(store, keys, {"w": w})
