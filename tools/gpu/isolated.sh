@@ -20,7 +20,10 @@ for f in glob.glob(out + "/ser/**/*kernel_trace.csv", recursive=True):
         n = x["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:60]
         agg[n][0] += 1
         agg[n][1] += (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3
-steps = max(c for c, _ in agg.values())
+# steps = the most common call count (a kernel launched twice per step, e.g.
+# the copies, must not set it)
+from collections import Counter
+steps = Counter(c for c, _ in agg.values()).most_common(1)[0][0]
 with open(out + "/isolated.txt", "w") as fo:
     tot = 0.0
     for n, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
