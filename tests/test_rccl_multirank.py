@@ -145,7 +145,7 @@ def _a2av_main(rank, world, port, out_dir):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_rccl_comm_a2av_multi_rank_same_gpu(tmp_path, world):
     """RcclComm.a2av's per-peer branch with real peers: uneven, empty and
     one-sided segments, 1- to 256-byte rows, a misaligned view."""
@@ -212,7 +212,8 @@ def _rccl_step_main(rank, world, port, out_dir, model, max_conc, comms):
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,model,max_conc,comms", [(2, "difacto", 2, 3), (3, "difacto", 2, 3),
                                                         (2, "linear", 2, 3), (3, "difacto", 2, 1),
-                                                        (2, "difacto", 1, 3)])
+                                                        (2, "difacto", 1, 3), (4, "difacto", 2, 3),
+                                                        (4, "linear", 2, 1)])
 def test_native_step_multi_rank_rccl_same_gpu(tmp_path, world, model, max_conc, comms):
     mp.spawn(_rccl_step_main, args=(world, _free_port(), str(tmp_path), model, max_conc, comms),
              nprocs=world, join=True)
