@@ -714,6 +714,24 @@ void register_all(py::module& m) {
     py::gil_scoped_release nogil;
     RemoteWrite(uri, data);
   });
+  // (tests) a whole object read sequentially through a RemoteReader of the
+  // given window in `chunk`-byte reads: (bytes, windows from the read-ahead)
+  m.def("remote_read_stream", [](const std::string& uri, int64_t window, int64_t chunk) {
+    std::string out;
+    int64_t pre = 0;
+    {
+      py::gil_scoped_release nogil;
+      RemoteReader r(uri, window);
+      std::string buf((size_t)std::max<int64_t>(chunk, 1), '\0');
+      while (true) {
+        const size_t n = r.Read(&buf[0], buf.size());
+        if (n == 0) break;
+        out.append(buf.data(), n);
+      }
+      pre = r.prefetched();
+    }
+    return py::make_tuple(py::bytes(out), pre);
+  });
   // streaming remote writes (S3 multipart / WebHDFS append), one part held;
   // dropped unclosed, its destructor aborts the upload over the network:
   // without the GIL (a Python thread -- a test's in-process server -- may be

@@ -694,10 +694,40 @@ RemoteReader::RemoteReader(const std::string& uri, int64_t window) : uri_(uri), 
   if (size_ < 0) throw std::runtime_error("cannot open " + uri);
 }
 
+RemoteReader::~RemoteReader() {
+  if (next_.valid()) {
+    try {
+      next_.get();
+    } catch (...) {
+    }
+  }
+}
+
 void RemoteReader::Fill() {
   if (pos_ >= buf_off_ && pos_ < buf_off_ + (int64_t)buf_.size()) return;
+  // a read that continues the last window is sequential
+  const bool seq = !buf_.empty() && pos_ == buf_off_ + (int64_t)buf_.size();
+  if (next_.valid() && next_off_ == pos_) {
+    buf_ = next_.get();  // (a failed read-ahead rethrows here)
+    ++prefetched_;
+  } else {
+    if (next_.valid()) {  // the read-ahead was for another place: drop it
+      try {
+        next_.get();
+      } catch (...) {
+      }
+    }
+    buf_ = pos_ < size_ ? RemoteRead(uri_, pos_, std::min(win_, size_ - pos_)) : std::string();
+  }
   buf_off_ = pos_;
-  buf_ = pos_ < size_ ? RemoteRead(uri_, pos_, std::min(win_, size_ - pos_)) : std::string();
+  sequential_ = seq;
+  const int64_t nx = buf_off_ + (int64_t)buf_.size();
+  if (sequential_ && !buf_.empty() && nx < size_) {
+    next_off_ = nx;
+    const std::string uri = uri_;
+    const int64_t len = std::min(win_, size_ - nx);
+    next_ = std::async(std::launch::async, [uri, nx, len] { return RemoteRead(uri, nx, len); });
+  }
 }
 
 size_t RemoteReader::Read(char* buf, size_t n) {

@@ -21,6 +21,7 @@
 //       AWS_SESSION_TOKEN) when set, anonymous otherwise
 #pragma once
 #include <cstdint>
+#include <future>
 #include <string>
 #include <vector>
 
@@ -67,15 +68,19 @@ class RemoteWriter {
   bool hdfs_ = false, created_ = false, closed_ = false;
 };
 
-// Sequential reads of one remote object through a read-ahead window.
+// Sequential reads of one remote object through a read-ahead window; once
+// two windows were read back to back, the next one is fetched in the
+// background while the current one is consumed (a seek elsewhere drops it).
 class RemoteReader {
  public:
   explicit RemoteReader(const std::string& uri, int64_t window = 8 << 20);
+  ~RemoteReader();
   int64_t size() const { return size_; }
   void Seek(int64_t off) { pos_ = off; }
   int64_t tell() const { return pos_; }
   size_t Read(char* buf, size_t n);
   int GetC();  // EOF (-1) at the end
+  int64_t prefetched() const { return prefetched_; }  // windows taken from the read-ahead
 
  private:
   void Fill();
@@ -83,6 +88,9 @@ class RemoteReader {
   int64_t size_ = 0, pos_ = 0, win_;
   std::string buf_;
   int64_t buf_off_ = 0;
+  std::future<std::string> next_;  // the read-ahead window at next_off_
+  int64_t next_off_ = -1, prefetched_ = 0;
+  bool sequential_ = false;
 };
 
 // (tests) SigV4 of a request: returns the Authorization header value for

@@ -141,6 +141,21 @@ def test_streaming_writer_parts(remote, base):
     assert srv.denied == 0
 
 
+@pytest.mark.parametrize("base", ["hdfs://127.0.0.1:8020/data", "s3://bkt/train"])
+def test_reader_read_ahead(remote, base):
+    """Sequential reads take their windows from the background read-ahead
+    (after the first two); the bytes are the object's."""
+    srv, root = remote
+    host = _native.host()
+    data = bytes((i * 7 + 3) % 256 for i in range(100_000))
+    host.remote_write(base + "/ra.bin", data)
+    got, pre = host.remote_read_stream(base + "/ra.bin", 4096, 1000)
+    assert got == data
+    assert pre >= 100_000 // 4096 - 2
+    got, _ = host.remote_read_stream(base + "/ra.bin", 4096, 70_000)  # reads spanning windows
+    assert got == data
+
+
 def test_wrong_credentials_are_refused(remote, monkeypatch):
     srv, _ = remote
     monkeypatch.setenv("AWS_SECRET_ACCESS_KEY", "wrong")
