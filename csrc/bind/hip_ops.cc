@@ -1429,13 +1429,34 @@ Tensor vidx_renumber(const Tensor& hdr) {
 // bound small-minibatch path. WH_TIMING=step2: also the absolute
 // steady-clock ns of every mark of calls 200..219 (to line up with a
 // rocprofv3 kernel trace)
+// every live split, so that a process leaving through os._exit (the bin/
+// launchers) can still print them: timing_flush()
+struct HostSplit;
+std::mutex& split_mu() {
+  static std::mutex m;
+  return m;
+}
+std::vector<HostSplit*>& live_splits() {
+  static auto* v = new std::vector<HostSplit*>();
+  return *v;
+}
 struct HostSplit {
   const char* name;
   double us[10] = {};
   int64_t calls = 0;
   bool abs = false;
   std::vector<std::array<int64_t, 11>> marks;
-  explicit HostSplit(const char* n) : name(n) {}
+  explicit HostSplit(const char* n) : name(n) {
+    std::lock_guard<std::mutex> lk(split_mu());
+    live_splits().push_back(this);
+  }
+  ~HostSplit() {
+    std::lock_guard<std::mutex> lk(split_mu());
+    auto& v = live_splits();
+    v.erase(std::remove(v.begin(), v.end(), this), v.end());
+  }
+  HostSplit(const HostSplit&) = delete;
+  HostSplit& operator=(const HostSplit&) = delete;
   void print() const {
     std::fprintf(stderr, "[%s host us/call over %lld]", name, (long long)calls);
     for (int i = 0; i < 10; ++i)
@@ -1479,6 +1500,15 @@ class HostTimer {
   bool rec_ = false;
   std::array<int64_t, 11> m_{};
 };
+// print every live split now (a short run's summary: the splits print every
+// 1000 calls and at their step's destruction, which os._exit skips)
+void timing_flush() {
+  std::lock_guard<std::mutex> lk(split_mu());
+  for (const HostSplit* h : live_splits())
+    if (h->calls > 0) h->print();
+  std::fflush(stderr);
+}
+
 static HostSplit* host_split(const char* name) {
   const bool abs = timing_on("step2");
   if (!abs && !timing_on("step")) return nullptr;
@@ -3637,6 +3667,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("auc_acc", &auc_acc);
   m.def("auc_acc_side", &auc_acc_side);
   m.def("auc_join", &auc_join);
+  m.def("timing_flush", &timing_flush);
   m.def("auc_sorted", &auc_sorted);
   m.def("synth_criteo", &synth_criteo);
   m.def("gather_rows", &gather_rows);
