@@ -364,29 +364,36 @@ __global__ __launch_bounds__(kWalkRows) void k_leaf_walk_lds(
                                            (uint32_t)(defl[j] != 0) << 24);
     tree[j] = make_uint2(w0, ((uint32_t)left[j] & 0xffffu) | ((uint32_t)right[j] << 16));
   }
-  const int64_t i0 = (int64_t)blockIdx.x * kWalkRows;
-  const int nr = (int)min<int64_t>(kWalkRows, n - i0);
-  const int nbytes = nr * f;
-  const uint8_t* src = B + i0 * f;  // 4-aligned: i0 * f is a multiple of 4 (kWalkRows % 4 == 0)
-  const int nw = nbytes >> 2;
-  for (int k = threadIdx.x; k < nw; k += blockDim.x)
-    reinterpret_cast<uint32_t*>(rows)[k] = reinterpret_cast<const uint32_t*>(src)[k];
-  for (int k = 4 * nw + threadIdx.x; k < nbytes; k += blockDim.x) rows[k] = src[k];
-  __syncthreads();
-  if ((int)threadIdx.x >= nr) return;
-  const uint8_t* row = rows + threadIdx.x * f;
-  int nd = 0;
-  for (int d = 0; d < 64; ++d) {
-    const uint2 t = tree[nd];
-    const uint32_t ft = t.x & 0xffffu;
-    if (ft == 0xffffu) break;
-    const int b = row[ft];
-    const bool l = b == kMissing ? (t.x >> 24) != 0 : b <= (int)((t.x >> 16) & 255u);
-    const int nx = (int)(l ? (t.y & 0xffffu) : (t.y >> 16));
-    if (nx >= nn) break;  // (a malformed child id cannot read past the tree)
-    nd = nx;
+  // persistent over row tiles: the tree is packed into LDS ONCE per block
+  // (one block per 256-row tile re-read the whole node table from L2 per
+  // tile: 511 nodes x 17 B for every 256 rows, more bytes than the rows)
+  for (int64_t tile = blockIdx.x; tile * kWalkRows < n; tile += gridDim.x) {
+    const int64_t i0 = tile * kWalkRows;
+    const int nr = (int)min<int64_t>(kWalkRows, n - i0);
+    const int nbytes = nr * f;
+    const uint8_t* src = B + i0 * f;  // 4-aligned: i0 * f is a multiple of 4 (kWalkRows % 4 == 0)
+    const int nw = nbytes >> 2;
+    __syncthreads();  // (the tree on the first tile; the previous tile's rows after)
+    for (int k = threadIdx.x; k < nw; k += blockDim.x)
+      reinterpret_cast<uint32_t*>(rows)[k] = reinterpret_cast<const uint32_t*>(src)[k];
+    for (int k = 4 * nw + threadIdx.x; k < nbytes; k += blockDim.x) rows[k] = src[k];
+    __syncthreads();
+    if ((int)threadIdx.x < nr) {
+      const uint8_t* row = rows + threadIdx.x * f;
+      int nd = 0;
+      for (int d = 0; d < 64; ++d) {
+        const uint2 t = tree[nd];
+        const uint32_t ft = t.x & 0xffffu;
+        if (ft == 0xffffu) break;
+        const int b = row[ft];
+        const bool l = b == kMissing ? (t.x >> 24) != 0 : b <= (int)((t.x >> 16) & 255u);
+        const int nx = (int)(l ? (t.y & 0xffffu) : (t.y >> 16));
+        if (nx >= nn) break;  // (a malformed child id cannot read past the tree)
+        nd = nx;
+      }
+      margin[i0 + threadIdx.x] += val[nd];
+    }
   }
-  margin[i0 + threadIdx.x] += val[nd];
 }
 
 __global__ void k_predict(const float* __restrict__ X, int64_t n, int f,
@@ -904,9 +911,17 @@ void gbdt_leaf_walk(const uint8_t* B, int64_t n, int f, int nn, const int32_t* f
   const size_t lbytes = (size_t)nn * 8 + (size_t)kWalkRows * f;
   if (nn > 0 && nn <= 65535 && f <= kWalkMaxF && lbytes <= 48 * 1024 &&
       (reinterpret_cast<uintptr_t>(B) & 3) == 0 && lds) {
-    hipLaunchKernelGGL(k_leaf_walk_lds, dim3((unsigned)((n + kWalkRows - 1) / kWalkRows)),
-                       dim3(kWalkRows), lbytes, s, B, n, f, nn, feat, bin, defl, left, right, val,
-                       margin);
+    // persistent: ~8 blocks per CU, each walking many tiles
+    const int64_t tiles = (n + kWalkRows - 1) / kWalkRows;
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0;
+      WH_HIP_CHECK(hipGetDevice(&dev));
+      WH_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)8 * std::max(cus, 1));
+    hipLaunchKernelGGL(k_leaf_walk_lds, dim3(grid), dim3(kWalkRows), lbytes, s, B, n, f, nn, feat,
+                       bin, defl, left, right, val, margin);
     return;
   }
   hipLaunchKernelGGL(k_leaf_walk, dim3(grid_for(n, 256)), dim3(256), 0, s, B, n, f, feat, bin, defl,
