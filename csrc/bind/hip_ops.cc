@@ -23,6 +23,8 @@
 #include <deque>
 #include <map>
 #include <mutex>
+#include <condition_variable>
+#include <thread>
 #include <memory>
 #include <numeric>
 #include <tuple>
@@ -30,6 +32,7 @@
 #include <vector>
 
 #include "hip/wh_kernels.h"
+#include "host/auc_host.h"
 
 namespace {
 
@@ -1586,6 +1589,168 @@ void auc_after_side(c10::DeviceIndex d, hipStream_t s) {
   a->dirty = false;
 }
 
+// Optionally (WH_AUC_HOST_THREADS=N > 0), a large training minibatch's AUC
+// on N host threads: the side stream copies (py, label) into pinned memory
+// and a worker computes the exact AUC (csrc/host/auc_host.h: the device
+// chain's definition) once the copy's event completes, so the GPU runs no
+// AUC kernels. Each job remembers the auc_sum it belongs to; auc_join
+// (auc_sum) waits for that tensor's jobs and adds their AUCs, folded in
+// submission order (a deterministic sum). Off by default: on the headline
+// step (100k rows) it measured level with the device chain (140.0 / 141.9 M
+// vs 140.7 / 139.5 M, profiles/round6_p1_isolated.txt), although dropping
+// the AUC altogether gains 3-5 % -- the side stream's event pair, the two
+// copies and the join remain.
+class HostAuc {
+ public:
+  // the pool new jobs go to (nullptr: the device chain)
+  static HostAuc* get() {
+    init();
+    return on() ? pool() : nullptr;
+  }
+  // the pool pending jobs are in (also after enable(0))
+  static HostAuc* any() {
+    init();
+    return pool();
+  }
+  static void enable(int nt) {
+    init();
+    if (nt > 0 && !pool()) pool() = new HostAuc(nt);
+    on() = nt > 0;
+  }
+
+  void submit(const float* py, const float* lab, int64_t n, hipStream_t s, const void* target) {
+    Job* j = nullptr;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      // back-pressure: the host falls this far behind only if its threads are starved
+      space_cv_.wait(lk, [&] { return outstanding_ < kMaxOutstanding; });
+      ++outstanding_;
+      for (size_t k = 0; k < free_.size(); ++k)
+        if (free_[k]->cap >= n) {
+          j = free_[k];
+          free_.erase(free_.begin() + k);
+          break;
+        }
+    }
+    if (!j) {
+      j = new Job();
+      WH_HIP_CHECK_HOST(hipEventCreateWithFlags(&j->ev, hipEventDisableTiming));
+    }
+    if (j->cap < n) {
+      if (j->buf) WH_HIP_CHECK_HOST(hipHostFree(j->buf));
+      j->cap = std::max<int64_t>(n, 1 << 17);
+      WH_HIP_CHECK_HOST(hipHostMalloc(reinterpret_cast<void**>(&j->buf), 2 * j->cap * sizeof(float),
+                                      hipHostMallocDefault));
+    }
+    j->n = n;
+    j->target = target;
+    j->done = false;
+    WH_HIP_CHECK_HOST(hipMemcpyAsync(j->buf, py, n * sizeof(float), hipMemcpyDeviceToHost, s));
+    WH_HIP_CHECK_HOST(hipMemcpyAsync(j->buf + j->cap, lab, n * sizeof(float), hipMemcpyDeviceToHost, s));
+    WH_HIP_CHECK_HOST(hipEventRecord(j->ev, s));
+    std::lock_guard<std::mutex> lk(mu_);
+    j->seq = next_seq_++;
+    pending_.push_back(j);
+    queue_.push_back(j);
+    work_cv_.notify_one();
+  }
+
+  bool has(const void* target) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (acc_.count(target)) return true;
+    for (Job* j : pending_)
+      if (j->target == target) return true;
+    return false;
+  }
+
+  // wait for target's jobs; their AUCs summed in submission order
+  double join(const void* target) {
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] {
+      for (Job* j : pending_)
+        if (j->target == target) return false;
+      return true;
+    });
+    auto it = acc_.find(target);
+    if (it == acc_.end()) return 0;
+    const double sum = it->second;
+    acc_.erase(it);
+    return sum;
+  }
+
+ private:
+  struct Job {
+    hipEvent_t ev = nullptr;
+    float* buf = nullptr;  // [cap] scores, then [cap] labels
+    int64_t cap = 0, n = 0;
+    const void* target = nullptr;
+    uint64_t seq = 0;
+    double result = 0;
+    bool done = false;
+  };
+  static constexpr int kMaxOutstanding = 64;
+  static HostAuc*& pool() {
+    static HostAuc* p = nullptr;  // never destroyed: os._exit ends the process
+    return p;
+  }
+  static bool& on() {
+    static bool b = false;
+    return b;
+  }
+  static void init() {
+    static const bool once = [] {
+      const char* e = std::getenv("WH_AUC_HOST_THREADS");
+      const int nt = e ? std::atoi(e) : 0;
+      if (nt > 0) pool() = new HostAuc(nt);
+      on() = nt > 0;
+      return true;
+    }();
+    (void)once;
+  }
+
+  explicit HostAuc(int nt) {
+    for (int t = 0; t < nt; ++t) std::thread([this] { run(); }).detach();
+  }
+
+  void run() {
+    std::vector<uint64_t> ws;
+    for (;;) {
+      Job* j;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        work_cv_.wait(lk, [&] { return !queue_.empty(); });
+        j = queue_.front();
+        queue_.pop_front();
+      }
+      WH_HIP_CHECK_HOST(hipEventSynchronize(j->ev));
+      const double r = wh::auc_exact_host(j->buf, j->buf + j->cap, j->n, ws);
+      std::lock_guard<std::mutex> lk(mu_);
+      j->result = r;
+      j->done = true;
+      // fold finished jobs into their target's sum in submission order (a
+      // deterministic sum) and recycle them, so jobs never wait for a join
+      while (!pending_.empty() && pending_.front()->done) {
+        Job* f = pending_.front();
+        pending_.pop_front();
+        acc_[f->target] += f->result;
+        free_.push_back(f);
+        --outstanding_;
+      }
+      done_cv_.notify_all();
+      space_cv_.notify_all();
+    }
+  }
+
+  std::mutex mu_;
+  std::condition_variable work_cv_, done_cv_, space_cv_;
+  std::deque<Job*> queue_;
+  std::deque<Job*> pending_;  // submitted, not yet folded (submission order)
+  std::map<const void*, double> acc_;  // folded AUC sums per target
+  std::vector<Job*> free_;
+  uint64_t next_seq_ = 0;
+  int outstanding_ = 0;
+};
+
 void auc_acc_side(const Tensor& py, const Tensor& label, const Tensor& auc_sum) {
   CHECK_IN(py, torch::kFloat32);
   CHECK_IN(label, torch::kFloat32);
@@ -1599,11 +1764,15 @@ void auc_acc_side(const Tensor& py, const Tensor& label, const Tensor& auc_sum) 
   if (py.numel() <= 4096) return auc_acc(py, label, auc_sum);
   c10::DeviceGuard g(py.device());
   AucSide* a = auc_side(py.device().index(), true);
-  a->dirty = true;
   WH_HIP_CHECK_HOST(hipEventRecord(a->in, cur_stream(py)));
   WH_HIP_CHECK_HOST(hipStreamWaitEvent(a->s.stream(), a->in, 0));
   c10::hip::HIPCachingAllocator::recordStream(py.storage().data_ptr(), a->s);
   c10::hip::HIPCachingAllocator::recordStream(label.storage().data_ptr(), a->s);
+  if (HostAuc* h = HostAuc::get()) {  // (the copies touch no shared workspace: not dirty)
+    h->submit(ptr<float>(py), ptr<float>(label), py.numel(), a->s.stream(), auc_sum.data_ptr());
+    return;
+  }
+  a->dirty = true;
   c10::hip::HIPStreamGuard sg(a->s);  // the scratch is the side stream's
   const int64_t n = py.numel();
   const int64_t wsb = wh::auc_ws_bytes(n);
@@ -1617,6 +1786,11 @@ void auc_join(const Tensor& auc_sum) {
   if (!auc_sum.is_cuda()) return;
   c10::DeviceGuard g(auc_sum.device());
   auc_after_side(auc_sum.device().index(), cur_stream(auc_sum));
+  HostAuc* h = HostAuc::any();
+  if (h && h->has(auc_sum.data_ptr())) {
+    const double s = h->join(auc_sum.data_ptr());
+    auc_sum.add_(s);
+  }
 }
 
 Tensor auc(const Tensor& py, const Tensor& label) {
@@ -3667,6 +3841,8 @@ PYBIND11_MODULE(_hip, m) {
   m.def("auc_acc", &auc_acc);
   m.def("auc_acc_side", &auc_acc_side);
   m.def("auc_join", &auc_join);
+  m.def("auc_host_threads", [](int n) { HostAuc::enable(n); },
+        "large training minibatches' AUC on n host threads (0: the device chain)");
   m.def("timing_flush", &timing_flush);
   m.def("auc_sorted", &auc_sorted);
   m.def("synth_criteo", &synth_criteo);

@@ -10,6 +10,7 @@
 #include <mutex>
 #include <thread>
 
+#include "auc_host.h"
 #include "common.h"
 #include "io.h"
 #include "remote_fs.h"
@@ -598,6 +599,17 @@ void register_all(py::module& m) {
                                 val ? c10::optional<Tensor>(val->cpu()) : c10::nullopt,
                                 label.cpu(), c10::nullopt));
   }, py::arg("keys"), py::arg("offset"), py::arg("val") = py::none(), py::arg("label"));
+  // the host AUC of csrc/host/auc_host.h (the device layer can run it on
+  // worker threads for large training minibatches: WH_AUC_HOST_THREADS)
+  m.def("auc_exact", [](torch::Tensor py, torch::Tensor label) {
+    TORCH_CHECK(!py.is_cuda() && py.scalar_type() == torch::kFloat32 &&
+                    label.scalar_type() == torch::kFloat32 && py.numel() == label.numel(),
+                "auc_exact: float32 CPU tensors of one size");
+    auto p = py.contiguous();
+    auto l = label.contiguous();
+    std::vector<uint64_t> ws;
+    return wh::auc_exact_host(p.data_ptr<float>(), l.data_ptr<float>(), p.numel(), ws);
+  });
   m.def("cityhash64", [](py::bytes b) {
     std::string s = b;
     return CityHash64(s.data(), s.size());

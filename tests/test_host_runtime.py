@@ -72,6 +72,27 @@ def test_cityhash64_known_values(host):
     assert host.cityhash64(b"68fd1e64") == host.cityhash64(b"68fd1e64")
 
 
+@pytest.mark.parametrize("kind", ["rand", "ties", "const", "wide", "tiny", "nonfinite", "negzero"])
+def test_host_auc_matches_oracle(host, kind):
+    """The host AUC (csrc/host/auc_host.h: bucketed fast path, radix path for
+    non-finite scores) equals the plain-PyTorch oracle bit for bit: ties
+    broken by index, -0 == +0, one class -> 1."""
+    g = torch.Generator().manual_seed(len(kind))
+    for n in (1, 2, 7, 999, 20000, 100000):
+        py = {"rand": lambda: torch.sigmoid(torch.randn(n, generator=g) * 3),
+              "ties": lambda: torch.randint(0, 5, (n,), generator=g).float() / 4,
+              "const": lambda: torch.full((n,), 0.5),
+              "wide": lambda: torch.randn(n, generator=g) * 1e4,
+              "tiny": lambda: torch.rand(n, generator=g) * 1e-30,
+              "nonfinite": lambda: torch.where(torch.rand(n, generator=g) < 0.02,
+                                               torch.tensor(float("nan")), torch.randn(n, generator=g)),
+              "negzero": lambda: torch.where(torch.rand(n, generator=g) < 0.5, torch.tensor(-0.0),
+                                             torch.rand(n, generator=g))}[kind]()
+        for p in (0.0, 0.3, 1.0):
+            lab = (torch.rand(n, generator=g) < p).float()
+            assert host.auc_exact(py, lab) == float(ref.auc(py, lab)), (n, p)
+
+
 @pytest.mark.parametrize("n", [0, 1, 13, 100, 65536 + 7, 300000])
 def test_lz4_roundtrip(host, n):
     rng = np.random.default_rng(n)

@@ -915,6 +915,47 @@ def test_auc_acc_reused_range_stays_exact(hip):
         assert abs(float(acc) - tot) < 1e-8, (float(acc), tot)
 
 
+def test_auc_side_host_threads_match_exact(hip):
+    """auc_acc_side on large minibatches (the host-thread AUC: pinned copy on
+    the side stream, exact AUC on a worker) interleaved over two sums, one
+    small minibatch (the on-stream device path) among them: auc_join adds
+    each sum's own AUCs, and freeing the inputs before the copy ran does
+    not change them (the side stream holds them in the caching allocator)."""
+    hip.auc_host_threads(2)
+    try:
+        _auc_side_checks(hip)
+    finally:
+        hip.auc_host_threads(0)
+    _auc_side_checks(hip)  # and the device chain on the side stream
+
+
+def _auc_side_checks(hip):
+    g = torch.Generator().manual_seed(9)
+    a = torch.zeros(1, dtype=torch.float64, device=DEV)
+    b = torch.zeros(1, dtype=torch.float64, device=DEV)
+    ta = tb = 0.0
+    base = torch.randn(100000, generator=g)
+    for k, py in enumerate((base, torch.sigmoid(base * 3), base[:3000], torch.full((50000,), 0.5),
+                            torch.round(base * 4) / 4, -base, base * 1e-4)):
+        lab = (torch.rand(py.numel(), generator=g) < 0.35).float()
+        r = float(ref.auc(py, lab))
+        pyd, labd = py.to(DEV), lab.to(DEV)
+        if k % 2:
+            tb += r
+            hip.auc_acc_side(pyd, labd, b)
+        else:
+            ta += r
+            hip.auc_acc_side(pyd, labd, a)
+        del pyd, labd  # freed while the copy may still be queued: the allocator
+        torch.empty(100000, device=DEV).fill_(7.0)  # must not hand them out before it
+    hip.auc_join(a)
+    hip.auc_join(b)
+    assert abs(float(a) - ta) < 1e-9, (float(a), ta)
+    assert abs(float(b) - tb) < 1e-9, (float(b), tb)
+    hip.auc_join(a)  # nothing pending: unchanged
+    assert abs(float(a) - ta) < 1e-9
+
+
 @pytest.mark.parametrize("nshard", [1, 8])
 def test_localize_few_distinct_ids_many_partitions(hip, nshard):
     """~2M non-zeros over 2000 power-law ids (the shape of bench_e2e.py's
