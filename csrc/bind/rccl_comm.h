@@ -42,9 +42,9 @@ struct A2aPlan {
     int peer;
     int64_t off, bytes;  // offset into this rank's send (or recv) buffer
   };
-  // element size of the transfer: a function of row_bytes alone, so every
-  // rank picks the same one (8-byte records as int64, 12-byte key records
-  // as int32, anything else as bytes)
+  // the rows' natural element size, a function of row_bytes alone (reported
+  // to the tests); a2av itself moves ncclUint8, so its datatype never
+  // depends on this rank's buffer alignment
   int esz = 1;
   int64_t own_src = 0, own_dst = 0, own_bytes = 0;  // the own segment: a local copy
   std::vector<Seg> sends, recvs;                     // peer order, zero-byte segments left out
@@ -176,13 +176,10 @@ class RcclComm {
     const A2aPlan pl = a2a_plan(rank_, world_, row_bytes, send_rows, recv_rows);
     const char* sp = static_cast<const char*>(send);
     char* rp = static_cast<char*>(recv);
-    // (every segment offset is a multiple of row_bytes, so of esz; a buffer
-    // start that is not -- a view at an odd offset -- moves as bytes. RCCL
-    // matches a send to its receive by byte count, so the peer's choice of
-    // element type does not have to agree with this one)
-    const uintptr_t base = reinterpret_cast<uintptr_t>(send) | reinterpret_cast<uintptr_t>(recv);
-    const int esz = (base % (uintptr_t)pl.esz) == 0 ? pl.esz : 1;
-    const ncclDataType_t dt = esz == 8 ? ncclInt64 : esz == 4 ? ncclInt32 : ncclUint8;
+    // bytes on the wire (ncclUint8): the element type of a send must match
+    // its receive on the peer, and a type picked from this rank's own buffer
+    // alignment is not something the peer can know -- point-to-point RCCL
+    // moves bytes either way, so nothing is lost
     if (pl.own_bytes > 0)
       WH_HIP_CHECK_HOST(hipMemcpyAsync(rp + pl.own_dst, sp + pl.own_src, (size_t)pl.own_bytes,
                                        hipMemcpyDeviceToDevice, s));
@@ -196,10 +193,10 @@ class RcclComm {
       const int pr = j < pl.recvs.size() ? pl.recvs[j].peer : 1 << 30;
       if (ps <= pr) {
         const auto& g = pl.sends[i++];
-        WH_NCCL_CHECK(ncclSend(sp + g.off, (size_t)(g.bytes / esz), dt, g.peer, comm_, s));
+        WH_NCCL_CHECK(ncclSend(sp + g.off, (size_t)g.bytes, ncclUint8, g.peer, comm_, s));
       } else {
         const auto& g = pl.recvs[j++];
-        WH_NCCL_CHECK(ncclRecv(rp + g.off, (size_t)(g.bytes / esz), dt, g.peer, comm_, s));
+        WH_NCCL_CHECK(ncclRecv(rp + g.off, (size_t)g.bytes, ncclUint8, g.peer, comm_, s));
       }
     }
     WH_NCCL_CHECK(ncclGroupEnd());
