@@ -15,6 +15,7 @@
 #include <thread>
 #include <vector>
 
+#include "host/auc_host.h"
 #include "host/common.h"
 #include "host/io.h"
 #include "host/json.h"
@@ -268,7 +269,39 @@ static void test_van() {
   server.Close();
 }
 
+// the host AUC against an O(n^2) count of the same definition (key order:
+// score bits, then index)
+static void test_auc() {
+  std::mt19937 rng(5);
+  std::vector<uint64_t> ws;
+  for (int n : {1, 2, 3, 17, 400, 3000}) {
+    for (int kind = 0; kind < 3; ++kind) {
+      std::vector<float> p(n), l(n);
+      for (int i = 0; i < n; ++i) {
+        p[i] = kind == 0 ? (float)(rng() % 1000) / 999.f
+                         : kind == 1 ? (float)(rng() % 4) * (rng() % 2 ? -1.f : 1.f) : 0.5f;
+        l[i] = (rng() % 3) == 0 ? 1.f : 0.f;
+      }
+      uint64_t tot = 0, tp = 0;
+      for (int i = 0; i < n; ++i) tp += l[i] > 0.f;
+      for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) {
+          if (!(l[i] > 0.f) || l[j] > 0.f) continue;
+          const uint32_t a = wh::auc_ord_bits(p[i]), b = wh::auc_ord_bits(p[j]);
+          tot += a < b || (a == b && i < j);
+        }
+      double want = 1.0;
+      if (tp != 0 && tp != (uint64_t)n) {
+        const double r = (double)tot / ((double)tp * (double)(n - tp));
+        want = r < 0.5 ? 1 - r : r;
+      }
+      EXPECT(wh::auc_exact_host(p.data(), l.data(), n, ws) == want);
+    }
+  }
+}
+
 int main() {
+  test_auc();
   test_lz4();
   test_crb();
   test_parsers();
