@@ -28,7 +28,11 @@ import os
 import sys
 import time
 
-import torch
+# (before torch: the HIP runtime reads it when it initialises; see
+# wormhole_amd/__init__.py)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
+import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
